@@ -1,0 +1,118 @@
+#!/usr/bin/env python3
+"""Headline benchmark: ResNet-18 Tiny-ImageNet training throughput (images/sec, whole node).
+
+Model: `create_resnet18_tiny_imagenet` (reference include/nn/example_models.hpp:306), random
+init, synthetic 64x64 RGB inputs + random labels of that shape, bf16 compute with fp32 master
+weights, Adam, softmax cross-entropy. Data parallel over RCCL, one process per GPU:
+
+  python bench.py --gpus 1 --steps 50 --warmup 10
+  python -m torch.distributed.run --nnodes=1 --nproc-per-node 8 --master-addr 127.0.0.1 \
+      --master-port 29500 bench.py --gpus 8 --steps 50 --warmup 10
+
+Weak scaling: every rank trains --batch images per step (global batch = batch x gpus).
+Exactly K steps are timed between a barrier + device synchronisation on both sides; the
+slowest rank's time is reported. Every timed step runs the full forward, loss, backward,
+gradient all-reduce and optimizer update.
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+import torch
+import torch.distributed as dist
+
+sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+
+METRIC = "images/sec (whole node) ResNet-18 Tiny-ImageNet training at 1/2/4/8 MI355X"
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=30)
+    ap.add_argument("--warmup", type=int, default=8)
+    ap.add_argument("--batch", type=int, default=int(os.environ.get("DCNN_BENCH_BATCH", "256")))
+    ap.add_argument("--model", default="resnet18_tiny_imagenet")
+    ap.add_argument("--graph", type=int, default=int(os.environ.get("DCNN_BENCH_GRAPH", "1")),
+                    help="capture the per-step compute in a hipGraph (1) or run eagerly (0)")
+    ap.add_argument("--bucket-mb", type=float, default=32.0)
+    ap.add_argument("--profile", action="store_true", help="print per-layer device times")
+    ap.add_argument("--device", default="cuda")
+    a = ap.parse_args()
+
+    from dcnn_amd.parallel.dp import DataParallel, init_distributed
+    from dcnn_amd.models import INPUT_SHAPES, NUM_CLASSES, create_model
+    from dcnn_amd.nn import Adam, LossFactory
+    from dcnn_amd.runtime.step import TrainStep
+
+    rank, world, local = init_distributed("nccl" if a.device == "cuda" else "gloo")
+    if a.gpus != world and world > 1:
+        raise SystemExit(f"--gpus {a.gpus} but WORLD_SIZE={world}")
+    dev = torch.device("cuda", local) if a.device == "cuda" else torch.device("cpu")
+    if dev.type == "cuda":
+        torch.cuda.set_device(dev)
+
+    model = create_model(a.model)
+    model.set_seed(1234)
+    model.set_device(f"GPU:{local}" if dev.type == "cuda" else "CPU")
+    model.initialize()
+    model.set_first_layer_input_grad(False)
+    dp = DataParallel(model, bucket_mb=a.bucket_mb)
+    opt = Adam(1e-3)
+    opt.attach(model)
+    loss_fn = LossFactory.create("softmax_crossentropy")
+
+    C, H, W = INPUT_SHAPES[a.model]
+    ncls = NUM_CLASSES[a.model]
+    g = torch.Generator(device="cpu").manual_seed(100 + rank)
+    nbuf = 4
+    xs = [torch.randn(a.batch, C, H, W, generator=g).to(dev) for _ in range(nbuf)]
+    ys = [torch.randint(0, ncls, (a.batch,), generator=g).to(dev) for _ in range(nbuf)]
+
+    step = TrainStep(dp, loss_fn, opt, use_graph=bool(a.graph) and dev.type == "cuda")
+
+    def sync():
+        if dev.type == "cuda":
+            torch.cuda.synchronize(dev)
+        if world > 1:
+            dist.barrier()
+
+    for i in range(a.warmup):
+        step(xs[i % nbuf], ys[i % nbuf])
+    sync()
+    t0 = time.perf_counter()
+    for i in range(a.steps):
+        step(xs[i % nbuf], ys[i % nbuf])
+    sync()
+    t1 = time.perf_counter()
+    elapsed = torch.tensor([t1 - t0], dtype=torch.float64, device=dev)
+    if world > 1:
+        dist.all_reduce(elapsed, op=dist.ReduceOp.MAX)
+    el = float(elapsed.item())
+    loss_val = float(step.last_loss.item()) if step.last_loss is not None else float("nan")
+    ms = el / a.steps * 1e3
+    imgs = a.batch * world * a.steps / el
+    if a.profile and rank == 0:
+        model.enable_profiling(True)
+        step.use_graph = False
+        for i in range(3):
+            step(xs[0], ys[0])
+        model.print_profiling_summary()
+    if rank == 0:
+        print(json.dumps({
+            "metric": METRIC, "value": round(imgs, 2), "unit": "images/sec", "n_gpus": world, "steps": a.steps,
+            "warmup": a.warmup, "ms_per_step": round(ms, 4), "higher_is_better": True, "scaling": "weak",
+            "vs_baseline": None, "dtype": "bf16", "data": "synthetic (random 64x64 RGB + random labels, random init)",
+            "config": {"model": a.model, "global_batch": a.batch * world, "per_gpu_batch": a.batch, "seq_len": None,
+                       "image_size": [C, H, W], "parallelism": f"dp{world}", "optimizer": "adam",
+                       "hipgraph": bool(step.use_graph), "final_loss": round(loss_val, 4)},
+        }), flush=True)
+    if world > 1:
+        dist.barrier()
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,78 @@
+#!/usr/bin/env python3
+"""Per-shape microbenchmark of the implicit-GEMM conv kernels (fwd / dgrad / wgrad) on the
+ResNet-18-tiny layer shapes. Reports device time per call and achieved TFLOP/s.
+
+  python benchmarks/conv_bench.py --batch 256 [--only fwd|dgrad|wgrad] [--iters 20]
+"""
+import argparse
+import os
+import sys
+
+import torch
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+# (name, Ci, H, W, Co, k, s, p)
+SHAPES = [
+    ("stem", 3, 64, 64, 32, 3, 1, 1),
+    ("l1.b1c1", 32, 32, 32, 64, 3, 1, 1),
+    ("l1.c", 64, 32, 32, 64, 3, 1, 1),
+    ("l1.proj", 32, 32, 32, 64, 1, 1, 0),
+    ("l2.b1c1", 64, 32, 32, 128, 3, 2, 1),
+    ("l2.c", 128, 16, 16, 128, 3, 1, 1),
+    ("l2.proj", 64, 32, 32, 128, 1, 2, 0),
+    ("l3.b1c1", 128, 16, 16, 256, 3, 2, 1),
+    ("l3.c", 256, 8, 8, 256, 3, 1, 1),
+    ("l3.proj", 128, 16, 16, 256, 1, 2, 0),
+    ("l4.b1c1", 256, 8, 8, 512, 3, 2, 1),
+    ("l4.c", 512, 4, 4, 512, 3, 1, 1),
+    ("l4.proj", 256, 8, 8, 512, 1, 2, 0),
+]
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--batch", type=int, default=256)
+    ap.add_argument("--iters", type=int, default=20)
+    ap.add_argument("--only", default="")
+    a = ap.parse_args()
+    from dcnn_amd.ops import hip
+    CL = torch.channels_last
+    N = a.batch
+    tot = {"fwd": 0.0, "dgrad": 0.0, "wgrad": 0.0}
+    print(f"{'shape':<10}{'op':<7}{'us':>9}{'TFLOP/s':>9}")
+    for (nm, Ci, H, W, Co, k, s, p) in SHAPES:
+        x = torch.randn(N, Ci, H, W, device="cuda").bfloat16().contiguous(memory_format=CL)
+        w = (torch.randn(Co, Ci, k, k, device="cuda") * 0.05).bfloat16().contiguous(memory_format=CL)
+        OH, OW = (H + 2 * p - k) // s + 1, (W + 2 * p - k) // s + 1
+        dy = torch.randn(N, Co, OH, OW, device="cuda").bfloat16().contiguous(memory_format=CL)
+        gw = torch.zeros(Co, Ci, k, k, device="cuda").contiguous(memory_format=CL)
+        wt = hip.conv_weight_t(w)
+        flops = 2.0 * N * OH * OW * Co * Ci * k * k
+        ops = {
+            "fwd": lambda: hip.conv2d_fwd(x, w, None, (s, s), (p, p), stats=True),
+            "dgrad": lambda: hip.conv2d_dgrad(dy, wt, x.shape, (s, s), (p, p)),
+            "wgrad": lambda: hip.conv2d_wgrad(dy, x, w.shape, (s, s), (p, p), gw, None),
+        }
+        for op, fn in ops.items():
+            if a.only and op != a.only:
+                continue
+            if op == "dgrad" and nm == "stem":
+                continue
+            for _ in range(3):
+                fn()
+            torch.cuda.synchronize()
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record()
+            for _ in range(a.iters):
+                fn()
+            e1.record()
+            torch.cuda.synchronize()
+            us = e0.elapsed_time(e1) * 1000 / a.iters
+            tot[op] += us
+            print(f"{nm:<10}{op:<7}{us:9.1f}{flops / us / 1e6:9.1f}")
+    print("totals (us, one pass over the shapes):", {k: round(v, 1) for k, v in tot.items()})
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,63 @@
+// Launcher API of the dcnn_amd HIP kernel library (shared by the .hip TUs and the bindings).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+typedef __bf16 bf16;
+
+namespace dcnn {
+struct NtArgs {
+  const bf16* A; const bf16* B; void* C;
+  int M, N, K; int lda, ldb, ldc; int mode;
+  int nb, sh, sw, cs, gh, gw; int kh, kw, strh, strw, padh, padw;
+  const float* bias; const bf16* residual; float* stats; int out_f32; int relu;
+};
+struct TnArgs {
+  const bf16* dY; const bf16* X; float* slab; float* bias_slab;
+  int M, N, P; int mode; int nb, sh, sw, cs, gh, gw; int kh, kw, strh, strw, padh, padw; int ldx; int k_per_split;
+};
+struct PoolGeom { int N, H, W, C, OH, OW, ph, pw, sh, sw, padh, padw; };
+
+void gemm_nt(const NtArgs& a, hipStream_t s);
+int gemm_nt_stat_rows(int M, int N);
+void gemm_tn(TnArgs a, int splits, hipStream_t s);
+int gemm_tn_splits(int M, int N, int P);
+void splitk_reduce(const float* slab, float* out, long n, int splits, int accumulate, hipStream_t s);
+
+int bn_partial_rows(long R, int C);
+void bn_partial(int dtype, const void* x, const void* dy, const void* yout, void* dy_out, const float* mean,
+                const float* istd, long R, int C, float* slab, int mode, hipStream_t s);
+void bn_slab_reduce(const float* slab, int rows, int C, float* sums, hipStream_t s);
+void bn_apply(int dtype, const void* x, void* y, long R, int C, const float* sums, float count, const float* gamma,
+              const float* beta, float eps, const void* residual, int relu, float* save_mean, float* save_istd,
+              float* run_mean, float* run_var, float momentum, int use_running, hipStream_t s);
+void bn_bwd_apply(int dtype, const void* dy, const void* yout, const void* x, void* dx, long R, int C, const float* mean,
+                  const float* istd, const float* gamma, const float* sums, float count, float* dgamma, float* dbeta,
+                  int eval_mode, hipStream_t s);
+void gn_fwd(int dtype, const void* x, void* y, int N, int HW, int C, int G, const float* gamma, const float* beta,
+            float eps, float* save_mean, float* save_istd, hipStream_t s);
+void gn_bwd(int dtype, const void* dy, const void* x, void* dx, int N, int HW, int C, int G, const float* gamma,
+            const float* mean, const float* istd, float* dgamma, float* dbeta, hipStream_t s);
+
+void maxpool_fwd(int dt, const void* x, void* y, uint8_t* idx, PoolGeom g, hipStream_t s);
+void maxpool_bwd(int dt, const void* dy, const uint8_t* idx, void* dx, PoolGeom g, hipStream_t s);
+void avgpool_fwd(int dt, const void* x, void* y, PoolGeom g, hipStream_t s);
+void avgpool_bwd(int dt, const void* dy, void* dx, PoolGeom g, hipStream_t s);
+void act_fwd(int dt, const void* x, void* y, long n, int type, float a, hipStream_t s);
+void act_bwd(int dt, const void* x, const void* dy, void* dx, long n, int type, float a, hipStream_t s);
+void softmax_rows(int dt, const void* x, void* y, long rows, int C, hipStream_t s);
+void softmax_rows_bwd(int dt, const void* y, const void* dy, void* dx, long rows, int C, hipStream_t s);
+void dropout(int dt, const void* x, void* y, long n, float p, uint64_t seed, hipStream_t s);
+void nchw_to_nhwc(int dt, const float* x, void* y, int N, int C, int HW, hipStream_t s);
+void conv_weight_transpose(int src_dt, const void* w, bf16* wt, int Co, int T_, int Ci, hipStream_t s);
+void cast_f32_bf16(const float* x, bf16* y, long n, hipStream_t s);
+void im2col(const float* x, float* col, int N, int C, int H, int W, int KH, int KW, int SH, int SW, int PH, int PW,
+            int OH, int OW, hipStream_t s);
+void col2im(const float* col, float* x, int N, int C, int H, int W, int KH, int KW, int SH, int SW, int PH, int PW,
+            int OH, int OW, hipStream_t s);
+void loss_fused(int dt, const void* pred, const float* target, const int64_t* labels, void* grad, float* loss_out,
+                int* correct, int N, int C, int type, float param, hipStream_t s);
+void adam_step(float* p, const float* g, float* m, float* v, bf16* shadow, long n, float lr, float b1, float b2,
+               float eps, float bc1, float bc2, float wd, int decoupled, const float* hyper, hipStream_t s);
+void sgd_step(float* p, const float* g, float* vel, bf16* shadow, long n, float lr, float mom, const float* hyper,
+              hipStream_t s);
+}  // namespace dcnn

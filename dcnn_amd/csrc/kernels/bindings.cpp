@@ -1,0 +1,149 @@
+// pybind11 entry points of the HIP kernel library. Arguments are raw device pointers
+// (uintptr_t, from torch.Tensor.data_ptr()) and the hipStream_t of the caller's current
+// stream, so launches land on whatever stream PyTorch-ROCm is using (including a stream
+// under hipGraph capture). No torch headers, no hipify: plain HIP + pybind11.
+#include <pybind11/pybind11.h>
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace py = pybind11;
+#include "api.h"
+
+
+using namespace dcnn;
+template <typename T>
+static inline T P(uintptr_t x) { return reinterpret_cast<T>(x); }
+static inline hipStream_t S(uintptr_t x) { return reinterpret_cast<hipStream_t>(x); }
+
+PYBIND11_MODULE(_kernels, m) {
+  m.doc() = "dcnn_amd HIP/CDNA4 (gfx950) kernel library";
+  m.attr("arch") = "gfx950";
+
+  m.def("gemm_nt",
+        [](uintptr_t A, uintptr_t B, uintptr_t C, int M, int N, int K, int lda, int ldb, int ldc, int mode, int nb,
+           int sh, int sw, int cs, int gh, int gw, int kh, int kw, int strh, int strw, int padh, int padw,
+           uintptr_t bias, uintptr_t residual, uintptr_t stats, int out_f32, int relu, uintptr_t stream) {
+          NtArgs a{P<const bf16*>(A), P<const bf16*>(B), P<void*>(C), M, N, K, lda, ldb, ldc, mode, nb, sh, sw, cs, gh,
+                   gw, kh, kw, strh, strw, padh, padw, P<const float*>(bias), P<const bf16*>(residual),
+                   P<float*>(stats), out_f32, relu};
+          gemm_nt(a, S(stream));
+        });
+  m.def("gemm_nt_stat_rows", &gemm_nt_stat_rows);
+  m.def("gemm_tn",
+        [](uintptr_t dY, uintptr_t X, uintptr_t slab, uintptr_t bias_slab, int M, int N, int Pn, int mode, int nb,
+           int sh, int sw, int cs, int gh, int gw, int kh, int kw, int strh, int strw, int padh, int padw, int ldx,
+           int splits, uintptr_t stream) {
+          TnArgs a{P<const bf16*>(dY), P<const bf16*>(X), P<float*>(slab), P<float*>(bias_slab), M, N, Pn, mode, nb, sh,
+                   sw, cs, gh, gw, kh, kw, strh, strw, padh, padw, ldx, 0};
+          gemm_tn(a, splits, S(stream));
+        });
+  m.def("gemm_tn_splits", &gemm_tn_splits);
+  m.def("splitk_reduce", [](uintptr_t slab, uintptr_t out, long n, int splits, int acc, uintptr_t st) {
+    splitk_reduce(P<const float*>(slab), P<float*>(out), n, splits, acc, S(st));
+  });
+
+  m.def("bn_partial_rows", &bn_partial_rows);
+  m.def("bn_partial", [](int dt, uintptr_t x, uintptr_t dy, uintptr_t yout, uintptr_t dy_out, uintptr_t mean,
+                         uintptr_t istd, long R, int C, uintptr_t slab, int mode, uintptr_t st) {
+    bn_partial(dt, P<const void*>(x), P<const void*>(dy), P<const void*>(yout), P<void*>(dy_out),
+               P<const float*>(mean), P<const float*>(istd), R, C, P<float*>(slab), mode, S(st));
+  });
+  m.def("bn_slab_reduce", [](uintptr_t slab, int rows, int C, uintptr_t sums, uintptr_t st) {
+    bn_slab_reduce(P<const float*>(slab), rows, C, P<float*>(sums), S(st));
+  });
+  m.def("bn_apply", [](int dt, uintptr_t x, uintptr_t y, long R, int C, uintptr_t sums, float count, uintptr_t gamma,
+                       uintptr_t beta, float eps, uintptr_t residual, int relu, uintptr_t save_mean,
+                       uintptr_t save_istd, uintptr_t run_mean, uintptr_t run_var, float momentum, int use_running,
+                       uintptr_t st) {
+    bn_apply(dt, P<const void*>(x), P<void*>(y), R, C, P<const float*>(sums), count, P<const float*>(gamma),
+             P<const float*>(beta), eps, P<const void*>(residual), relu, P<float*>(save_mean), P<float*>(save_istd),
+             P<float*>(run_mean), P<float*>(run_var), momentum, use_running, S(st));
+  });
+  m.def("bn_bwd_apply", [](int dt, uintptr_t dy, uintptr_t yout, uintptr_t x, uintptr_t dx, long R, int C,
+                           uintptr_t mean, uintptr_t istd, uintptr_t gamma, uintptr_t sums, float count,
+                           uintptr_t dgamma, uintptr_t dbeta, int eval_mode, uintptr_t st) {
+    bn_bwd_apply(dt, P<const void*>(dy), P<const void*>(yout), P<const void*>(x), P<void*>(dx), R, C,
+                 P<const float*>(mean), P<const float*>(istd), P<const float*>(gamma), P<const float*>(sums), count,
+                 P<float*>(dgamma), P<float*>(dbeta), eval_mode, S(st));
+  });
+  m.def("gn_fwd", [](int dt, uintptr_t x, uintptr_t y, int N, int HW, int C, int G, uintptr_t gamma, uintptr_t beta,
+                     float eps, uintptr_t sm, uintptr_t si, uintptr_t st) {
+    gn_fwd(dt, P<const void*>(x), P<void*>(y), N, HW, C, G, P<const float*>(gamma), P<const float*>(beta), eps,
+           P<float*>(sm), P<float*>(si), S(st));
+  });
+  m.def("gn_bwd", [](int dt, uintptr_t dy, uintptr_t x, uintptr_t dx, int N, int HW, int C, int G, uintptr_t gamma,
+                     uintptr_t mean, uintptr_t istd, uintptr_t dg, uintptr_t db, uintptr_t st) {
+    gn_bwd(dt, P<const void*>(dy), P<const void*>(x), P<void*>(dx), N, HW, C, G, P<const float*>(gamma),
+           P<const float*>(mean), P<const float*>(istd), P<float*>(dg), P<float*>(db), S(st));
+  });
+
+  auto geom = [](int N, int H, int W, int C, int OH, int OW, int ph, int pw, int sh, int sw, int padh, int padw) {
+    return PoolGeom{N, H, W, C, OH, OW, ph, pw, sh, sw, padh, padw};
+  };
+  m.def("maxpool_fwd", [geom](int dt, uintptr_t x, uintptr_t y, uintptr_t idx, int N, int H, int W, int C, int OH,
+                              int OW, int ph, int pw, int sh, int sw, int padh, int padw, uintptr_t st) {
+    maxpool_fwd(dt, P<const void*>(x), P<void*>(y), P<uint8_t*>(idx), geom(N, H, W, C, OH, OW, ph, pw, sh, sw, padh, padw),
+                S(st));
+  });
+  m.def("maxpool_bwd", [geom](int dt, uintptr_t dy, uintptr_t idx, uintptr_t dx, int N, int H, int W, int C, int OH,
+                              int OW, int ph, int pw, int sh, int sw, int padh, int padw, uintptr_t st) {
+    maxpool_bwd(dt, P<const void*>(dy), P<const uint8_t*>(idx), P<void*>(dx),
+                geom(N, H, W, C, OH, OW, ph, pw, sh, sw, padh, padw), S(st));
+  });
+  m.def("avgpool_fwd", [geom](int dt, uintptr_t x, uintptr_t y, int N, int H, int W, int C, int OH, int OW, int ph,
+                              int pw, int sh, int sw, int padh, int padw, uintptr_t st) {
+    avgpool_fwd(dt, P<const void*>(x), P<void*>(y), geom(N, H, W, C, OH, OW, ph, pw, sh, sw, padh, padw), S(st));
+  });
+  m.def("avgpool_bwd", [geom](int dt, uintptr_t dy, uintptr_t dx, int N, int H, int W, int C, int OH, int OW, int ph,
+                              int pw, int sh, int sw, int padh, int padw, uintptr_t st) {
+    avgpool_bwd(dt, P<const void*>(dy), P<void*>(dx), geom(N, H, W, C, OH, OW, ph, pw, sh, sw, padh, padw), S(st));
+  });
+  m.def("act_fwd", [](int dt, uintptr_t x, uintptr_t y, long n, int type, float a, uintptr_t st) {
+    act_fwd(dt, P<const void*>(x), P<void*>(y), n, type, a, S(st));
+  });
+  m.def("act_bwd", [](int dt, uintptr_t x, uintptr_t dy, uintptr_t dx, long n, int type, float a, uintptr_t st) {
+    act_bwd(dt, P<const void*>(x), P<const void*>(dy), P<void*>(dx), n, type, a, S(st));
+  });
+  m.def("softmax_rows", [](int dt, uintptr_t x, uintptr_t y, long rows, int C, uintptr_t st) {
+    softmax_rows(dt, P<const void*>(x), P<void*>(y), rows, C, S(st));
+  });
+  m.def("softmax_rows_bwd", [](int dt, uintptr_t y, uintptr_t dy, uintptr_t dx, long rows, int C, uintptr_t st) {
+    softmax_rows_bwd(dt, P<const void*>(y), P<const void*>(dy), P<void*>(dx), rows, C, S(st));
+  });
+  m.def("dropout", [](int dt, uintptr_t x, uintptr_t y, long n, float p, uint64_t seed, uintptr_t st) {
+    dropout(dt, P<const void*>(x), P<void*>(y), n, p, seed, S(st));
+  });
+  m.def("nchw_to_nhwc", [](int dt, uintptr_t x, uintptr_t y, int N, int C, int HW, uintptr_t st) {
+    nchw_to_nhwc(dt, P<const float*>(x), P<void*>(y), N, C, HW, S(st));
+  });
+  m.def("conv_weight_transpose", [](int dt, uintptr_t w, uintptr_t wt, int Co, int T_, int Ci, uintptr_t st) {
+    conv_weight_transpose(dt, P<const void*>(w), P<bf16*>(wt), Co, T_, Ci, S(st));
+  });
+  m.def("cast_f32_bf16", [](uintptr_t x, uintptr_t y, long n, uintptr_t st) {
+    cast_f32_bf16(P<const float*>(x), P<bf16*>(y), n, S(st));
+  });
+  m.def("im2col", [](uintptr_t x, uintptr_t col, int N, int C, int H, int W, int KH, int KW, int SH, int SW, int PH,
+                     int PW, int OH, int OW, uintptr_t st) {
+    im2col(P<const float*>(x), P<float*>(col), N, C, H, W, KH, KW, SH, SW, PH, PW, OH, OW, S(st));
+  });
+  m.def("col2im", [](uintptr_t col, uintptr_t x, int N, int C, int H, int W, int KH, int KW, int SH, int SW, int PH,
+                     int PW, int OH, int OW, uintptr_t st) {
+    col2im(P<const float*>(col), P<float*>(x), N, C, H, W, KH, KW, SH, SW, PH, PW, OH, OW, S(st));
+  });
+  m.def("loss_fused", [](int dt, uintptr_t pred, uintptr_t target, uintptr_t labels, uintptr_t grad, uintptr_t loss,
+                         uintptr_t correct, int N, int C, int type, float param, uintptr_t st) {
+    loss_fused(dt, P<const void*>(pred), P<const float*>(target), P<const int64_t*>(labels), P<void*>(grad),
+               P<float*>(loss), P<int*>(correct), N, C, type, param, S(st));
+  });
+  m.def("adam_step", [](uintptr_t p, uintptr_t g, uintptr_t mm, uintptr_t v, uintptr_t shadow, long n, float lr,
+                        float b1, float b2, float eps, float bc1, float bc2, float wd, int dec, uintptr_t hyper,
+                        uintptr_t st) {
+    adam_step(P<float*>(p), P<const float*>(g), P<float*>(mm), P<float*>(v), P<bf16*>(shadow), n, lr, b1, b2, eps, bc1,
+              bc2, wd, dec, P<const float*>(hyper), S(st));
+  });
+  m.def("sgd_step", [](uintptr_t p, uintptr_t g, uintptr_t vel, uintptr_t shadow, long n, float lr, float mom,
+                       uintptr_t hyper, uintptr_t st) {
+    sgd_step(P<float*>(p), P<const float*>(g), P<float*>(vel), P<bf16*>(shadow), n, lr, mom, P<const float*>(hyper),
+             S(st));
+  });
+}

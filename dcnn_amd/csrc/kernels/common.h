@@ -1,0 +1,113 @@
+// Shared CDNA4 (gfx950) device helpers for the dcnn_amd kernel library.
+// Wave64 everywhere: reductions use 64-lane shuffles (reference defect G16 hard-coded 32).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+#include <stdexcept>
+#include <string>
+
+#ifndef DCNN_BF16_DEFINED
+#define DCNN_BF16_DEFINED
+#endif
+typedef __bf16 bf16;
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+typedef float f32x16 __attribute__((ext_vector_type(16)));
+
+#define DCNN_HIP_CHECK(expr)                                                                   \
+  do {                                                                                         \
+    hipError_t _e = (expr);                                                                    \
+    if (_e != hipSuccess)                                                                      \
+      throw std::runtime_error(std::string("HIP error ") + hipGetErrorString(_e) + " at " +   \
+                               __FILE__ + ":" + std::to_string(__LINE__));                     \
+  } while (0)
+
+#define DCNN_LAUNCH_CHECK() DCNN_HIP_CHECK(hipGetLastError())
+
+namespace dcnn {
+
+constexpr int kWave = 64;
+
+__device__ __forceinline__ float to_f(float x) { return x; }
+__device__ __forceinline__ float to_f(bf16 x) { return (float)x; }
+template <typename T> __device__ __forceinline__ T from_f(float x);
+template <> __device__ __forceinline__ float from_f<float>(float x) { return x; }
+template <> __device__ __forceinline__ bf16 from_f<bf16>(float x) { return (bf16)x; }
+
+__device__ __forceinline__ float wave_sum(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+__device__ __forceinline__ float wave_max(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v = fmaxf(v, __shfl_xor(v, o, 64));
+  return v;
+}
+
+// Block-wide sum for blockDim.x <= 1024 (wave64). `sh` needs >= 16 floats.
+__device__ __forceinline__ float block_sum(float v, float* sh) {
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6, nw = (blockDim.x + 63) >> 6;
+  v = wave_sum(v);
+  __syncthreads();
+  if (lane == 0) sh[wid] = v;
+  __syncthreads();
+  float r = 0.f;
+  for (int i = 0; i < nw; ++i) r += sh[i];
+  return r;
+}
+
+// 8 x bf16 <-> 8 x f32 through one 16-byte access.
+struct alignas(16) Pack8 {
+  uint4 u;
+};
+__device__ __forceinline__ void unpack8(const uint4& u, float* f) {
+  const bf16* b = reinterpret_cast<const bf16*>(&u);
+#pragma unroll
+  for (int i = 0; i < 8; ++i) f[i] = (float)b[i];
+}
+__device__ __forceinline__ uint4 pack8(const float* f) {
+  uint4 u;
+  bf16* b = reinterpret_cast<bf16*>(&u);
+#pragma unroll
+  for (int i = 0; i < 8; ++i) b[i] = (bf16)f[i];
+  return u;
+}
+
+// Philox-4x32-10 counter RNG (stateless: dropout masks are regenerated in backward).
+struct Philox {
+  __device__ __forceinline__ static uint4 gen(uint64_t seed, uint64_t ctr) {
+    uint32_t k0 = (uint32_t)seed, k1 = (uint32_t)(seed >> 32);
+    uint32_t c0 = (uint32_t)ctr, c1 = (uint32_t)(ctr >> 32), c2 = 0x6a09e667u, c3 = 0xbb67ae85u;
+#pragma unroll
+    for (int r = 0; r < 10; ++r) {
+      uint64_t p0 = (uint64_t)0xD2511F53u * c0;
+      uint64_t p1 = (uint64_t)0xCD9E8D57u * c2;
+      uint32_t n0 = (uint32_t)(p1 >> 32) ^ c1 ^ k0;
+      uint32_t n1 = (uint32_t)p1;
+      uint32_t n2 = (uint32_t)(p0 >> 32) ^ c3 ^ k1;
+      uint32_t n3 = (uint32_t)p0;
+      c0 = n0;
+      c1 = n1;
+      c2 = n2;
+      c3 = n3;
+      k0 += 0x9E3779B9u;
+      k1 += 0xBB67AE85u;
+    }
+    return make_uint4(c0, c1, c2, c3);
+  }
+  __device__ __forceinline__ static float u01(uint32_t x) {
+    return ((x >> 8) + 0.5f) * (1.0f / 16777216.0f);
+  }
+};
+
+inline int ceil_div(long a, long b) { return (int)((a + b - 1) / b); }
+inline int grid_for(long n, int block, int cap = 2048 * 4) {
+  long g = (n + block - 1) / block;
+  if (g > cap) g = cap;
+  if (g < 1) g = 1;
+  return (int)g;
+}
+
+}  // namespace dcnn

@@ -1,0 +1,472 @@
+// BatchNorm / GroupNorm on NHWC activations (bf16 or fp32 I/O, fp32 statistics).
+//
+// Reference: src/nn/layers_impl/cuda/batchnorm_ops.cu:17-375 (K20-K24) launches ONE block per
+// channel for the statistics (64 blocks on 256 CUs) and stores x_hat. Here:
+//   * statistics are split reductions: partial (sum, sumsq) per row-chunk into a slab (or
+//     produced for free by the preceding conv's epilogue), then a channel-parallel reduce;
+//   * apply = one vectorised pass computing scale/shift per channel in LDS, optionally fusing
+//     the residual add and ReLU of a ResNet block; x_hat is never stored (recomputed from x);
+//   * backward fuses the ReLU mask into the reduction and the apply, and ACCUMULATES
+//     dgamma/dbeta (intended semantics; reference defect G4 overwrote on GPU).
+// Semantics kept: biased variance for normalisation, unbiased for the running variance,
+// running = (1-m)*running + m*batch (batchnorm_ops.cu:141-153).
+#include "common.h"
+#include "api.h"
+
+namespace dcnn {
+
+template <typename T, int V>
+struct VecIO;
+template <>
+struct VecIO<bf16, 8> {
+  __device__ static __forceinline__ void load(const bf16* p, float* f) {
+    unpack8(*reinterpret_cast<const uint4*>(p), f);
+  }
+  __device__ static __forceinline__ void store(bf16* p, const float* f) {
+    *reinterpret_cast<uint4*>(p) = pack8(f);
+  }
+};
+template <>
+struct VecIO<float, 8> {
+  __device__ static __forceinline__ void load(const float* p, float* f) {
+    const float4 a = reinterpret_cast<const float4*>(p)[0], b = reinterpret_cast<const float4*>(p)[1];
+    f[0] = a.x; f[1] = a.y; f[2] = a.z; f[3] = a.w; f[4] = b.x; f[5] = b.y; f[6] = b.z; f[7] = b.w;
+  }
+  __device__ static __forceinline__ void store(float* p, const float* f) {
+    reinterpret_cast<float4*>(p)[0] = make_float4(f[0], f[1], f[2], f[3]);
+    reinterpret_cast<float4*>(p)[1] = make_float4(f[4], f[5], f[6], f[7]);
+  }
+};
+template <typename T>
+struct VecIO1 {
+  __device__ static __forceinline__ void load(const T* p, float* f) { f[0] = to_f(p[0]); }
+  __device__ static __forceinline__ void store(T* p, const float* f) { p[0] = from_f<T>(f[0]); }
+};
+
+template <typename T, int V>
+__device__ __forceinline__ void vload(const T* p, float* f) {
+  if constexpr (V == 8) VecIO<T, 8>::load(p, f); else VecIO1<T>::load(p, f);
+}
+template <typename T, int V>
+__device__ __forceinline__ void vstore(T* p, const float* f) {
+  if constexpr (V == 8) VecIO<T, 8>::store(p, f); else VecIO1<T>::store(p, f);
+}
+
+// ---------------------------------------------------------------------------------------
+// partial statistics: slab[block][2][C] over rows [block*rpb, (block+1)*rpb)
+// mode 0: (sum x, sum x^2)
+// mode 1 (backward): (sum dy', sum dy' * xhat) with dy' = dy * (yout > 0 if yout)
+//                    optionally storing dy' (needed by a residual branch)
+// ---------------------------------------------------------------------------------------
+template <typename T, int V>
+__global__ void __launch_bounds__(256) bn_partial_kernel(const T* __restrict__ x, const T* __restrict__ dy,
+                                                         const T* __restrict__ yout, T* __restrict__ dy_out,
+                                                         const float* __restrict__ mean,
+                                                         const float* __restrict__ istd, long R, int C,
+                                                         int rpb, float* __restrict__ slab, int mode) {
+  extern __shared__ __attribute__((aligned(16))) float sh[];
+  const int groups = C / V;                       // channel vectors
+  const int tpr = groups < 256 ? groups : 256;    // threads per row
+  const int rows_conc = 256 / tpr;                // rows processed concurrently
+  const int g0 = threadIdx.x % tpr, rsub = threadIdx.x / tpr;
+  const long r0 = (long)blockIdx.x * rpb, r1 = min(R, r0 + rpb);
+  for (int gbase = 0; gbase < groups; gbase += tpr) {
+    const int g = gbase + g0;
+    float s[V], q[V];
+#pragma unroll
+    for (int v = 0; v < V; ++v) s[v] = q[v] = 0.f;
+    float mu[V], is[V];
+    if (mode == 1 && g < groups && rsub < rows_conc) {
+#pragma unroll
+      for (int v = 0; v < V; ++v) { mu[v] = mean[g * V + v]; is[v] = istd[g * V + v]; }
+    }
+    if (g < groups && rsub < rows_conc) {
+      for (long r = r0 + rsub; r < r1; r += rows_conc) {
+        const long o = r * C + (long)g * V;
+        float xv[V];
+        vload<T, V>(x + o, xv);
+        if (mode == 0) {
+#pragma unroll
+          for (int v = 0; v < V; ++v) { s[v] += xv[v]; q[v] += xv[v] * xv[v]; }
+        } else {
+          float d[V];
+          vload<T, V>(dy + o, d);
+          if (yout) {
+            float yo[V];
+            vload<T, V>(yout + o, yo);
+#pragma unroll
+            for (int v = 0; v < V; ++v) d[v] = yo[v] > 0.f ? d[v] : 0.f;
+            if (dy_out) vstore<T, V>(dy_out + o, d);
+          }
+#pragma unroll
+          for (int v = 0; v < V; ++v) {
+            s[v] += d[v];
+            q[v] += d[v] * (xv[v] - mu[v]) * is[v];
+          }
+        }
+      }
+    }
+    // reduce over rsub through LDS: sh[rows_conc][2][tpr*V]
+    __syncthreads();
+    if (g < groups && rsub < rows_conc) {
+#pragma unroll
+      for (int v = 0; v < V; ++v) {
+        sh[(rsub * 2 + 0) * tpr * V + g0 * V + v] = s[v];
+        sh[(rsub * 2 + 1) * tpr * V + g0 * V + v] = q[v];
+      }
+    }
+    __syncthreads();
+    const int width = tpr * V;
+    for (int c = threadIdx.x; c < 2 * width; c += 256) {
+      const int which = c / width, cc = c % width;
+      const int ch = gbase * V + cc;
+      if (ch < C) {
+        float acc = 0.f;
+        for (int k = 0; k < rows_conc; ++k) acc += sh[(k * 2 + which) * width + cc];
+        slab[((long)blockIdx.x * 2 + which) * C + ch] = acc;
+      }
+    }
+  }
+}
+
+// sums[2][C] += sum over slab rows (atomic; sums zeroed by the caller)
+__global__ void __launch_bounds__(256) bn_slab_reduce_kernel(const float* __restrict__ slab, int rows, int C,
+                                                             int rows_per_block, float* __restrict__ sums) {
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int c = blockIdx.x * 64 + lane;
+  const int rb = blockIdx.y * rows_per_block, re = min(rows, rb + rows_per_block);
+  __shared__ float red[4][2][64];
+  float s = 0.f, q = 0.f;
+  if (c < C) {
+    for (int r = rb + w; r < re; r += 4) {
+      s += slab[((long)r * 2 + 0) * C + c];
+      q += slab[((long)r * 2 + 1) * C + c];
+    }
+  }
+  red[w][0][lane] = s;
+  red[w][1][lane] = q;
+  __syncthreads();
+  if (w == 0 && c < C) {
+    s = red[0][0][lane] + red[1][0][lane] + red[2][0][lane] + red[3][0][lane];
+    q = red[0][1][lane] + red[1][1][lane] + red[2][1][lane] + red[3][1][lane];
+    atomicAdd(&sums[c], s);
+    atomicAdd(&sums[C + c], q);
+  }
+}
+
+// y = x*scale + shift (+ residual) (ReLU); scale/shift from batch sums or running stats.
+template <typename T, int V>
+__global__ void __launch_bounds__(256) bn_apply_kernel(const T* __restrict__ x, T* __restrict__ y, long R, int C,
+                                                       const float* __restrict__ sums, float count,
+                                                       const float* __restrict__ gamma,
+                                                       const float* __restrict__ beta, float eps,
+                                                       const T* __restrict__ residual, int relu,
+                                                       float* __restrict__ save_mean, float* __restrict__ save_istd,
+                                                       float* __restrict__ run_mean, float* __restrict__ run_var,
+                                                       float momentum, int use_running) {
+  extern __shared__ __attribute__((aligned(16))) float sh[];
+  float* scale = sh;
+  float* shift = sh + C;
+  for (int c = threadIdx.x; c < C; c += blockDim.x) {
+    float mean, istd;
+    if (use_running) {
+      mean = run_mean[c];
+      istd = rsqrtf(run_var[c] + eps);
+    } else {
+      mean = sums[c] / count;
+      const float var = fmaxf(sums[C + c] / count - mean * mean, 0.f);
+      istd = rsqrtf(var + eps);
+      if (blockIdx.x == 0) {
+        if (save_mean) { save_mean[c] = mean; save_istd[c] = istd; }
+        if (run_mean) {
+          const float unbiased = count > 1.f ? var * count / (count - 1.f) : var;
+          run_mean[c] = (1.f - momentum) * run_mean[c] + momentum * mean;
+          run_var[c] = (1.f - momentum) * run_var[c] + momentum * unbiased;
+        }
+      }
+    }
+    const float g = gamma ? gamma[c] : 1.f, b = beta ? beta[c] : 0.f;
+    scale[c] = g * istd;
+    shift[c] = b - mean * g * istd;
+  }
+  __syncthreads();
+  const long nv = R * C / V;
+  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < nv; i += (long)gridDim.x * blockDim.x) {
+    const long o = i * V;
+    const int c0 = (int)(o % C);
+    float xv[V];
+    vload<T, V>(x + o, xv);
+    float r[V];
+    if (residual) vload<T, V>(residual + o, r);
+#pragma unroll
+    for (int v = 0; v < V; ++v) {
+      float t = xv[v] * scale[c0 + v] + shift[c0 + v];
+      if (residual) t += r[v];
+      if (relu) t = fmaxf(t, 0.f);
+      xv[v] = t;
+    }
+    vstore<T, V>(y + o, xv);
+  }
+}
+
+// dx = gamma*istd*(dy' - sum_dy/M - xhat*sum_dyxhat/M); block 0 accumulates dgamma/dbeta.
+template <typename T, int V>
+__global__ void __launch_bounds__(256) bn_bwd_apply_kernel(const T* __restrict__ dy, const T* __restrict__ yout,
+                                                           const T* __restrict__ x, T* __restrict__ dx, long R,
+                                                           int C, const float* __restrict__ mean,
+                                                           const float* __restrict__ istd,
+                                                           const float* __restrict__ gamma,
+                                                           const float* __restrict__ sums, float count,
+                                                           float* __restrict__ dgamma, float* __restrict__ dbeta,
+                                                           int eval_mode) {
+  extern __shared__ __attribute__((aligned(16))) float sh[];
+  float* ca = sh;          // gamma*istd
+  float* cb = sh + C;      // mean(dy')
+  float* cc = sh + 2 * C;  // mean(dy' xhat)
+  float* cm = sh + 3 * C;  // mean
+  float* ci = sh + 4 * C;  // istd
+  for (int c = threadIdx.x; c < C; c += blockDim.x) {
+    const float g = gamma ? gamma[c] : 1.f;
+    ca[c] = g * istd[c];
+    cb[c] = eval_mode ? 0.f : sums[c] / count;
+    cc[c] = eval_mode ? 0.f : sums[C + c] / count;
+    cm[c] = mean[c];
+    ci[c] = istd[c];
+    if (blockIdx.x == 0 && sums) {
+      if (dgamma) dgamma[c] += sums[C + c];
+      if (dbeta) dbeta[c] += sums[c];
+    }
+  }
+  __syncthreads();
+  const long nv = R * C / V;
+  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < nv; i += (long)gridDim.x * blockDim.x) {
+    const long o = i * V;
+    const int c0 = (int)(o % C);
+    float d[V], xv[V];
+    vload<T, V>(dy + o, d);
+    vload<T, V>(x + o, xv);
+    if (yout) {
+      float yo[V];
+      vload<T, V>(yout + o, yo);
+#pragma unroll
+      for (int v = 0; v < V; ++v) d[v] = yo[v] > 0.f ? d[v] : 0.f;
+    }
+#pragma unroll
+    for (int v = 0; v < V; ++v) {
+      const int c = c0 + v;
+      const float xh = (xv[v] - cm[c]) * ci[c];
+      d[v] = ca[c] * (d[v] - cb[c] - xh * cc[c]);
+    }
+    vstore<T, V>(dx + o, d);
+  }
+}
+
+// ---------------------------------------------------------------------------------------
+// GroupNorm (NHWC): one workgroup per (image, group)
+// ---------------------------------------------------------------------------------------
+template <typename T>
+__global__ void __launch_bounds__(256) gn_fwd_kernel(const T* __restrict__ x, T* __restrict__ y, int HW, int C,
+                                                     int G, const float* __restrict__ gamma,
+                                                     const float* __restrict__ beta, float eps,
+                                                     float* __restrict__ save_mean, float* __restrict__ save_istd) {
+  __shared__ float sh[16];
+  const int n = blockIdx.x / G, g = blockIdx.x % G, Cg = C / G;
+  const long base = (long)n * HW * C + (long)g * Cg;
+  const long cnt = (long)HW * Cg;
+  float s = 0.f;
+  for (long i = threadIdx.x; i < cnt; i += blockDim.x) s += to_f(x[base + (i / Cg) * C + (i % Cg)]);
+  const float mean = block_sum(s, sh) / (float)cnt;
+  float q = 0.f;
+  for (long i = threadIdx.x; i < cnt; i += blockDim.x) {
+    const float d = to_f(x[base + (i / Cg) * C + (i % Cg)]) - mean;
+    q += d * d;
+  }
+  __syncthreads();
+  const float var = block_sum(q, sh) / (float)cnt;
+  const float is = rsqrtf(var + eps);
+  if (threadIdx.x == 0) { save_mean[blockIdx.x] = mean; save_istd[blockIdx.x] = is; }
+  for (long i = threadIdx.x; i < cnt; i += blockDim.x) {
+    const int c = g * Cg + (int)(i % Cg);
+    const long o = base + (i / Cg) * C + (i % Cg);
+    const float gm = gamma ? gamma[c] : 1.f, bt = beta ? beta[c] : 0.f;
+    y[o] = from_f<T>((to_f(x[o]) - mean) * is * gm + bt);
+  }
+}
+
+template <typename T>
+__global__ void __launch_bounds__(256) gn_bwd_kernel(const T* __restrict__ dy, const T* __restrict__ x,
+                                                     T* __restrict__ dx, int HW, int C, int G,
+                                                     const float* __restrict__ gamma,
+                                                     const float* __restrict__ mean, const float* __restrict__ istd,
+                                                     float* __restrict__ dgamma, float* __restrict__ dbeta) {
+  __shared__ float sh[16];
+  const int n = blockIdx.x / G, g = blockIdx.x % G, Cg = C / G;
+  const long base = (long)n * HW * C + (long)g * Cg;
+  const long cnt = (long)HW * Cg;
+  const float mu = mean[blockIdx.x], is = istd[blockIdx.x];
+  float s1 = 0.f, s2 = 0.f;
+  for (long i = threadIdx.x; i < cnt; i += blockDim.x) {
+    const int c = g * Cg + (int)(i % Cg);
+    const long o = base + (i / Cg) * C + (i % Cg);
+    const float gm = gamma ? gamma[c] : 1.f;
+    const float d = to_f(dy[o]) * gm, xh = (to_f(x[o]) - mu) * is;
+    s1 += d;
+    s2 += d * xh;
+  }
+  const float m1 = block_sum(s1, sh) / (float)cnt;
+  __syncthreads();
+  const float m2 = block_sum(s2, sh) / (float)cnt;
+  for (long i = threadIdx.x; i < cnt; i += blockDim.x) {
+    const int c = g * Cg + (int)(i % Cg);
+    const long o = base + (i / Cg) * C + (i % Cg);
+    const float gm = gamma ? gamma[c] : 1.f;
+    const float d = to_f(dy[o]) * gm, xh = (to_f(x[o]) - mu) * is;
+    dx[o] = from_f<T>(is * (d - m1 - xh * m2));
+  }
+  // per-channel dgamma/dbeta partial for this image: thread per channel of the group
+  for (int cl = threadIdx.x; cl < Cg; cl += blockDim.x) {
+    const int c = g * Cg + cl;
+    float a = 0.f, b = 0.f;
+    for (int p = 0; p < HW; ++p) {
+      const long o = base + (long)p * C + cl;
+      const float d = to_f(dy[o]);
+      a += d * (to_f(x[o]) - mu) * is;
+      b += d;
+    }
+    if (dgamma) atomicAdd(&dgamma[c], a);
+    if (dbeta) atomicAdd(&dbeta[c], b);
+  }
+}
+
+// ---------------------------------------------------------------------------------------
+// launchers
+// ---------------------------------------------------------------------------------------
+static int bn_rows_per_block(long R, int C) {
+  // ~ (256 CUs x 2) workgroups, each a multiple of the concurrent rows
+  long rpb = (R + 511) / 512;
+  if (rpb < 16) rpb = 16;
+  return (int)rpb;
+}
+
+int bn_partial_rows(long R, int C) {
+  const int rpb = bn_rows_per_block(R, C);
+  return (int)((R + rpb - 1) / rpb);
+}
+
+template <typename T>
+static void bn_partial_t(const T* x, const T* dy, const T* yout, T* dy_out, const float* mean,
+                         const float* istd, long R, int C, float* slab, int mode, hipStream_t s) {
+  const int rpb = bn_rows_per_block(R, C);
+  const int blocks = (int)((R + rpb - 1) / rpb);
+  if (C % 8 == 0) {
+    const int groups = C / 8, tpr = groups < 256 ? groups : 256, rc = 256 / tpr;
+    const size_t shm = (size_t)rc * 2 * tpr * 8 * sizeof(float);
+    hipLaunchKernelGGL((bn_partial_kernel<T, 8>), dim3(blocks), dim3(256), shm, s, x, dy, yout, dy_out, mean,
+                       istd, R, C, rpb, slab, mode);
+  } else {
+    const int tpr = C < 256 ? C : 256, rc = 256 / tpr;
+    const size_t shm = (size_t)rc * 2 * tpr * sizeof(float);
+    hipLaunchKernelGGL((bn_partial_kernel<T, 1>), dim3(blocks), dim3(256), shm, s, x, dy, yout, dy_out, mean,
+                       istd, R, C, rpb, slab, mode);
+  }
+  DCNN_LAUNCH_CHECK();
+}
+
+void bn_partial(int dtype, const void* x, const void* dy, const void* yout, void* dy_out, const float* mean,
+                const float* istd, long R, int C, float* slab, int mode, hipStream_t s) {
+  if (dtype == 0)
+    bn_partial_t<float>((const float*)x, (const float*)dy, (const float*)yout, (float*)dy_out, mean, istd, R, C,
+                        slab, mode, s);
+  else
+    bn_partial_t<bf16>((const bf16*)x, (const bf16*)dy, (const bf16*)yout, (bf16*)dy_out, mean, istd, R, C, slab,
+                       mode, s);
+}
+
+void bn_slab_reduce(const float* slab, int rows, int C, float* sums, hipStream_t s) {
+  DCNN_HIP_CHECK(hipMemsetAsync(sums, 0, sizeof(float) * 2 * C, s));
+  const int rpb = 64;
+  dim3 grid((C + 63) / 64, (rows + rpb - 1) / rpb);
+  hipLaunchKernelGGL(bn_slab_reduce_kernel, grid, dim3(256), 0, s, slab, rows, C, rpb, sums);
+  DCNN_LAUNCH_CHECK();
+}
+
+template <typename T>
+static void bn_apply_t(const T* x, T* y, long R, int C, const float* sums, float count, const float* gamma,
+                       const float* beta, float eps, const T* residual, int relu, float* save_mean,
+                       float* save_istd, float* run_mean, float* run_var, float momentum, int use_running,
+                       hipStream_t s) {
+  const size_t shm = 2 * C * sizeof(float);
+  if (C % 8 == 0) {
+    const int g = grid_for(R * C / 8, 256, 2048);
+    hipLaunchKernelGGL((bn_apply_kernel<T, 8>), dim3(g), dim3(256), shm, s, x, y, R, C, sums, count, gamma, beta,
+                       eps, residual, relu, save_mean, save_istd, run_mean, run_var, momentum, use_running);
+  } else {
+    const int g = grid_for(R * C, 256, 2048);
+    hipLaunchKernelGGL((bn_apply_kernel<T, 1>), dim3(g), dim3(256), shm, s, x, y, R, C, sums, count, gamma, beta,
+                       eps, residual, relu, save_mean, save_istd, run_mean, run_var, momentum, use_running);
+  }
+  DCNN_LAUNCH_CHECK();
+}
+
+void bn_apply(int dtype, const void* x, void* y, long R, int C, const float* sums, float count,
+              const float* gamma, const float* beta, float eps, const void* residual, int relu, float* save_mean,
+              float* save_istd, float* run_mean, float* run_var, float momentum, int use_running, hipStream_t s) {
+  if (dtype == 0)
+    bn_apply_t<float>((const float*)x, (float*)y, R, C, sums, count, gamma, beta, eps, (const float*)residual, relu,
+                      save_mean, save_istd, run_mean, run_var, momentum, use_running, s);
+  else
+    bn_apply_t<bf16>((const bf16*)x, (bf16*)y, R, C, sums, count, gamma, beta, eps, (const bf16*)residual, relu,
+                     save_mean, save_istd, run_mean, run_var, momentum, use_running, s);
+}
+
+template <typename T>
+static void bn_bwd_apply_t(const T* dy, const T* yout, const T* x, T* dx, long R, int C, const float* mean,
+                           const float* istd, const float* gamma, const float* sums, float count, float* dgamma,
+                           float* dbeta, int eval_mode, hipStream_t s) {
+  const size_t shm = 5 * C * sizeof(float);
+  if (C % 8 == 0) {
+    const int g = grid_for(R * C / 8, 256, 2048);
+    hipLaunchKernelGGL((bn_bwd_apply_kernel<T, 8>), dim3(g), dim3(256), shm, s, dy, yout, x, dx, R, C, mean, istd,
+                       gamma, sums, count, dgamma, dbeta, eval_mode);
+  } else {
+    const int g = grid_for(R * C, 256, 2048);
+    hipLaunchKernelGGL((bn_bwd_apply_kernel<T, 1>), dim3(g), dim3(256), shm, s, dy, yout, x, dx, R, C, mean, istd,
+                       gamma, sums, count, dgamma, dbeta, eval_mode);
+  }
+  DCNN_LAUNCH_CHECK();
+}
+
+void bn_bwd_apply(int dtype, const void* dy, const void* yout, const void* x, void* dx, long R, int C,
+                  const float* mean, const float* istd, const float* gamma, const float* sums, float count,
+                  float* dgamma, float* dbeta, int eval_mode, hipStream_t s) {
+  if (dtype == 0)
+    bn_bwd_apply_t<float>((const float*)dy, (const float*)yout, (const float*)x, (float*)dx, R, C, mean, istd, gamma,
+                          sums, count, dgamma, dbeta, eval_mode, s);
+  else
+    bn_bwd_apply_t<bf16>((const bf16*)dy, (const bf16*)yout, (const bf16*)x, (bf16*)dx, R, C, mean, istd, gamma,
+                         sums, count, dgamma, dbeta, eval_mode, s);
+}
+
+void gn_fwd(int dtype, const void* x, void* y, int N, int HW, int C, int G, const float* gamma, const float* beta,
+            float eps, float* save_mean, float* save_istd, hipStream_t s) {
+  if (dtype == 0)
+    hipLaunchKernelGGL(gn_fwd_kernel<float>, dim3(N * G), dim3(256), 0, s, (const float*)x, (float*)y, HW, C, G,
+                       gamma, beta, eps, save_mean, save_istd);
+  else
+    hipLaunchKernelGGL(gn_fwd_kernel<bf16>, dim3(N * G), dim3(256), 0, s, (const bf16*)x, (bf16*)y, HW, C, G, gamma,
+                       beta, eps, save_mean, save_istd);
+  DCNN_LAUNCH_CHECK();
+}
+
+void gn_bwd(int dtype, const void* dy, const void* x, void* dx, int N, int HW, int C, int G, const float* gamma,
+            const float* mean, const float* istd, float* dgamma, float* dbeta, hipStream_t s) {
+  if (dtype == 0)
+    hipLaunchKernelGGL(gn_bwd_kernel<float>, dim3(N * G), dim3(256), 0, s, (const float*)dy, (const float*)x,
+                       (float*)dx, HW, C, G, gamma, mean, istd, dgamma, dbeta);
+  else
+    hipLaunchKernelGGL(gn_bwd_kernel<bf16>, dim3(N * G), dim3(256), 0, s, (const bf16*)dy, (const bf16*)x,
+                       (bf16*)dx, HW, C, G, gamma, mean, istd, dgamma, dbeta);
+  DCNN_LAUNCH_CHECK();
+}
+
+}  // namespace dcnn

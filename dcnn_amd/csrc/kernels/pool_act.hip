@@ -1,0 +1,427 @@
+// Pooling, activations, dropout, layout conversion and misc tensor kernels (NHWC, wave64).
+//
+// Reference kernels replaced: K29-K32 (src/nn/layers_impl/cuda/{maxpool,avgpool}_ops.cu: size_t
+// argmax + atomicAdd scatter backward), K33 dropout (stored mask), K34-K36 activations,
+// K12/K13 im2col/col2im (src/tensor/cuda/tensor_kernels.cu), K7/K8 transposes.
+// Here: max-pool keeps a 1-byte window-local argmax and both pools use a GATHER backward
+// (no atomics, deterministic, works for overlapping windows); dropout regenerates its
+// Philox mask in backward (no mask tensor); activations are one templated elementwise kernel.
+#include "common.h"
+#include "api.h"
+
+namespace dcnn {
+
+template <typename T>
+__device__ __forceinline__ float ld(const T* p, long i) { return to_f(p[i]); }
+
+// ----------------------------------- pooling ---------------------------------------------
+
+
+template <typename T>
+__global__ void maxpool_fwd_kernel(const T* __restrict__ x, T* __restrict__ y, uint8_t* __restrict__ idx, PoolGeom g) {
+  const long total = (long)g.N * g.OH * g.OW * g.C;
+  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < total; i += (long)gridDim.x * blockDim.x) {
+    const int c = (int)(i % g.C);
+    long t = i / g.C;
+    const int ox = (int)(t % g.OW);
+    t /= g.OW;
+    const int oy = (int)(t % g.OH);
+    const int n = (int)(t / g.OH);
+    float best = -INFINITY;
+    int bi = 0;
+    for (int ky = 0; ky < g.ph; ++ky) {
+      const int iy = oy * g.sh - g.padh + ky;
+      if (iy < 0 || iy >= g.H) continue;
+      for (int kx = 0; kx < g.pw; ++kx) {
+        const int ix = ox * g.sw - g.padw + kx;
+        if (ix < 0 || ix >= g.W) continue;
+        const float v = ld(x, (((long)n * g.H + iy) * g.W + ix) * g.C + c);
+        if (v > best) { best = v; bi = ky * g.pw + kx; }
+      }
+    }
+    y[i] = from_f<T>(best);
+    idx[i] = (uint8_t)bi;
+  }
+}
+
+template <typename T>
+__global__ void maxpool_bwd_kernel(const T* __restrict__ dy, const uint8_t* __restrict__ idx, T* __restrict__ dx,
+                                   PoolGeom g) {
+  const long total = (long)g.N * g.H * g.W * g.C;
+  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < total; i += (long)gridDim.x * blockDim.x) {
+    const int c = (int)(i % g.C);
+    long t = i / g.C;
+    const int ix = (int)(t % g.W);
+    t /= g.W;
+    const int iy = (int)(t % g.H);
+    const int n = (int)(t / g.H);
+    // windows containing (iy, ix): oy*sh - padh <= iy <= oy*sh - padh + ph - 1
+    const int oy0 = max(0, (iy + g.padh - g.ph + g.sh) / g.sh), oy1 = min(g.OH - 1, (iy + g.padh) / g.sh);
+    const int ox0 = max(0, (ix + g.padw - g.pw + g.sw) / g.sw), ox1 = min(g.OW - 1, (ix + g.padw) / g.sw);
+    float acc = 0.f;
+    for (int oy = oy0; oy <= oy1; ++oy) {
+      const int ky = iy - (oy * g.sh - g.padh);
+      if (ky < 0 || ky >= g.ph) continue;
+      for (int ox = ox0; ox <= ox1; ++ox) {
+        const int kx = ix - (ox * g.sw - g.padw);
+        if (kx < 0 || kx >= g.pw) continue;
+        const long o = (((long)n * g.OH + oy) * g.OW + ox) * g.C + c;
+        if (idx[o] == ky * g.pw + kx) acc += ld(dy, o);
+      }
+    }
+    dx[i] = from_f<T>(acc);
+  }
+}
+
+template <typename T>
+__global__ void avgpool_fwd_kernel(const T* __restrict__ x, T* __restrict__ y, PoolGeom g) {
+  const long total = (long)g.N * g.OH * g.OW * g.C;
+  const float inv = 1.f / (float)(g.ph * g.pw);  // count_include_pad semantics (avgpool_ops.cu:53)
+  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < total; i += (long)gridDim.x * blockDim.x) {
+    const int c = (int)(i % g.C);
+    long t = i / g.C;
+    const int ox = (int)(t % g.OW);
+    t /= g.OW;
+    const int oy = (int)(t % g.OH);
+    const int n = (int)(t / g.OH);
+    float s = 0.f;
+    for (int ky = 0; ky < g.ph; ++ky) {
+      const int iy = oy * g.sh - g.padh + ky;
+      if (iy < 0 || iy >= g.H) continue;
+      for (int kx = 0; kx < g.pw; ++kx) {
+        const int ix = ox * g.sw - g.padw + kx;
+        if (ix < 0 || ix >= g.W) continue;
+        s += ld(x, (((long)n * g.H + iy) * g.W + ix) * g.C + c);
+      }
+    }
+    y[i] = from_f<T>(s * inv);
+  }
+}
+
+template <typename T>
+__global__ void avgpool_bwd_kernel(const T* __restrict__ dy, T* __restrict__ dx, PoolGeom g) {
+  const long total = (long)g.N * g.H * g.W * g.C;
+  const float inv = 1.f / (float)(g.ph * g.pw);
+  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < total; i += (long)gridDim.x * blockDim.x) {
+    const int c = (int)(i % g.C);
+    long t = i / g.C;
+    const int ix = (int)(t % g.W);
+    t /= g.W;
+    const int iy = (int)(t % g.H);
+    const int n = (int)(t / g.H);
+    const int oy0 = max(0, (iy + g.padh - g.ph + g.sh) / g.sh), oy1 = min(g.OH - 1, (iy + g.padh) / g.sh);
+    const int ox0 = max(0, (ix + g.padw - g.pw + g.sw) / g.sw), ox1 = min(g.OW - 1, (ix + g.padw) / g.sw);
+    float acc = 0.f;
+    for (int oy = oy0; oy <= oy1; ++oy) {
+      const int ky = iy - (oy * g.sh - g.padh);
+      if (ky < 0 || ky >= g.ph) continue;
+      for (int ox = ox0; ox <= ox1; ++ox) {
+        const int kx = ix - (ox * g.sw - g.padw);
+        if (kx < 0 || kx >= g.pw) continue;
+        acc += ld(dy, (((long)n * g.OH + oy) * g.OW + ox) * g.C + c);
+      }
+    }
+    dx[i] = from_f<T>(acc * inv);
+  }
+}
+
+// Global average pool (window == whole image, stride irrelevant): one wave per (n, 64 channels)
+template <typename T>
+__global__ void global_avgpool_fwd_kernel(const T* __restrict__ x, T* __restrict__ y, int N, int HW, int C) {
+  const long total = (long)N * C;
+  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < total; i += (long)gridDim.x * blockDim.x) {
+    const int c = (int)(i % C);
+    const int n = (int)(i / C);
+    float s = 0.f;
+    for (int p = 0; p < HW; ++p) s += ld(x, ((long)n * HW + p) * C + c);
+    y[i] = from_f<T>(s / (float)HW);
+  }
+}
+
+template <typename T>
+__global__ void global_avgpool_bwd_kernel(const T* __restrict__ dy, T* __restrict__ dx, int N, int HW, int C) {
+  const long total = (long)N * HW * C;
+  const float inv = 1.f / (float)HW;
+  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < total; i += (long)gridDim.x * blockDim.x) {
+    const int c = (int)(i % C);
+    const int n = (int)(i / ((long)HW * C));
+    dx[i] = from_f<T>(ld(dy, (long)n * C + c) * inv);
+  }
+}
+
+// ----------------------------------- activations -----------------------------------------
+enum Act { kRelu = 0, kLeaky = 1, kElu = 2, kSigmoid = 3, kTanh = 4, kLinear = 5 };
+
+__device__ __forceinline__ float act_f(int t, float x, float a) {
+  switch (t) {
+    case kRelu: return fmaxf(x, 0.f);
+    case kLeaky: return x > 0.f ? x : a * x;
+    case kElu: return x > 0.f ? x : a * (__expf(x) - 1.f);
+    case kSigmoid: return 1.f / (1.f + __expf(-x));
+    case kTanh: return tanhf(x);
+    default: return x;
+  }
+}
+__device__ __forceinline__ float act_df(int t, float x, float a) {
+  switch (t) {
+    case kRelu: return x > 0.f ? 1.f : 0.f;
+    case kLeaky: return x > 0.f ? 1.f : a;
+    case kElu: return x > 0.f ? 1.f : a * __expf(x);
+    case kSigmoid: { const float s = 1.f / (1.f + __expf(-x)); return s * (1.f - s); }
+    case kTanh: { const float t2 = tanhf(x); return 1.f - t2 * t2; }
+    default: return 1.f;
+  }
+}
+
+template <typename T>
+__global__ void act_fwd_kernel(const T* __restrict__ x, T* __restrict__ y, long n, int type, float alpha) {
+  const long n8 = n / 8;
+  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < n8; i += (long)gridDim.x * blockDim.x) {
+    float f[8];
+#pragma unroll
+    for (int v = 0; v < 8; ++v) f[v] = act_f(type, ld(x, i * 8 + v), alpha);
+#pragma unroll
+    for (int v = 0; v < 8; ++v) y[i * 8 + v] = from_f<T>(f[v]);
+  }
+  for (long i = n8 * 8 + blockIdx.x * (long)blockDim.x + threadIdx.x; i < n; i += (long)gridDim.x * blockDim.x)
+    y[i] = from_f<T>(act_f(type, ld(x, i), alpha));
+}
+
+template <typename T>
+__global__ void act_bwd_kernel(const T* __restrict__ x, const T* __restrict__ dy, T* __restrict__ dx, long n, int type,
+                               float alpha) {
+  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < n; i += (long)gridDim.x * blockDim.x)
+    dx[i] = from_f<T>(ld(dy, i) * act_df(type, ld(x, i), alpha));
+}
+
+// softmax over the innermost dim (channels in NHWC): one wave per row
+template <typename T>
+__global__ void softmax_rows_kernel(const T* __restrict__ x, T* __restrict__ y, long rows, int C) {
+  const int lane = threadIdx.x & 63;
+  const long row = (blockIdx.x * (long)blockDim.x + threadIdx.x) >> 6;
+  if (row >= rows) return;
+  const T* xr = x + row * C;
+  float m = -INFINITY;
+  for (int c = lane; c < C; c += 64) m = fmaxf(m, ld(xr, c));
+  m = wave_max(m);
+  float s = 0.f;
+  for (int c = lane; c < C; c += 64) s += __expf(ld(xr, c) - m);
+  s = wave_sum(s);
+  const float inv = 1.f / s;
+  for (int c = lane; c < C; c += 64) y[row * C + c] = from_f<T>(__expf(ld(xr, c) - m) * inv);
+}
+
+template <typename T>
+__global__ void softmax_rows_bwd_kernel(const T* __restrict__ y, const T* __restrict__ dy, T* __restrict__ dx,
+                                        long rows, int C) {
+  const int lane = threadIdx.x & 63;
+  const long row = (blockIdx.x * (long)blockDim.x + threadIdx.x) >> 6;
+  if (row >= rows) return;
+  float d = 0.f;
+  for (int c = lane; c < C; c += 64) d += ld(y, row * C + c) * ld(dy, row * C + c);
+  d = wave_sum(d);
+  for (int c = lane; c < C; c += 64) {
+    const long o = row * C + c;
+    dx[o] = from_f<T>(ld(y, o) * (ld(dy, o) - d));
+  }
+}
+
+// ------------------------------------- dropout -------------------------------------------
+template <typename T>
+__global__ void dropout_kernel(const T* __restrict__ x, T* __restrict__ y, long n, float p, uint64_t seed) {
+  const float scale = 1.f / (1.f - p);
+  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < (n + 3) / 4; i += (long)gridDim.x * blockDim.x) {
+    const uint4 r = Philox::gen(seed, (uint64_t)i);
+    const uint32_t rr[4] = {r.x, r.y, r.z, r.w};
+#pragma unroll
+    for (int v = 0; v < 4; ++v) {
+      const long o = i * 4 + v;
+      if (o < n) y[o] = from_f<T>(Philox::u01(rr[v]) >= p ? ld(x, o) * scale : 0.f);
+    }
+  }
+}
+
+// -------------------------------- layout / conversion ------------------------------------
+// x NCHW (float) -> y NHWC (T)
+template <typename T>
+__global__ void nchw_to_nhwc_kernel(const float* __restrict__ x, T* __restrict__ y, int N, int C, int HW) {
+  const long total = (long)N * C * HW;
+  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < total; i += (long)gridDim.x * blockDim.x) {
+    const int c = (int)(i % C);
+    const long t = i / C;
+    const int p = (int)(t % HW);
+    const int n = (int)(t / HW);
+    y[i] = from_f<T>(x[((long)n * C + c) * HW + p]);
+  }
+}
+
+// W[co][t][ci] -> Wt[ci][t][co]   (dgrad operand), source fp32 or bf16, dest bf16
+template <typename S>
+__global__ void conv_weight_transpose_kernel(const S* __restrict__ w, bf16* __restrict__ wt, int Co, int T_, int Ci) {
+  const long total = (long)Co * T_ * Ci;
+  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < total; i += (long)gridDim.x * blockDim.x) {
+    // i indexes the destination
+    const int co = (int)(i % Co);
+    long r = i / Co;
+    const int t = (int)(r % T_);
+    const int ci = (int)(r / T_);
+    wt[i] = (bf16)to_f(w[((long)co * T_ + t) * Ci + ci]);
+  }
+}
+
+__global__ void cast_f32_bf16_kernel(const float* __restrict__ x, bf16* __restrict__ y, long n) {
+  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < n; i += (long)gridDim.x * blockDim.x)
+    y[i] = (bf16)x[i];
+}
+
+// ------------------------------ im2col / col2im (NCHW, fp32) -----------------------------
+// col[(c,kh,kw)][n*OH*OW + oh*OW + ow]   (the reference's column layout, tensor_kernels.cu:18)
+__global__ void im2col_kernel(const float* __restrict__ x, float* __restrict__ col, int N, int C, int H, int W,
+                              int KH, int KW, int SH, int SW, int PH, int PW, int OH, int OW) {
+  const long cols = (long)N * OH * OW;
+  const long total = (long)C * KH * KW * cols;
+  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < total; i += (long)gridDim.x * blockDim.x) {
+    const long j = i % cols;
+    const int r = (int)(i / cols);
+    const int kw = r % KW, kh = (r / KW) % KH, c = r / (KW * KH);
+    const int ow = (int)(j % OW), oh = (int)((j / OW) % OH), n = (int)(j / ((long)OW * OH));
+    const int iy = oh * SH - PH + kh, ix = ow * SW - PW + kw;
+    col[i] = (iy >= 0 && iy < H && ix >= 0 && ix < W) ? x[(((long)n * C + c) * H + iy) * W + ix] : 0.f;
+  }
+}
+
+__global__ void col2im_kernel(const float* __restrict__ col, float* __restrict__ x, int N, int C, int H, int W,
+                              int KH, int KW, int SH, int SW, int PH, int PW, int OH, int OW) {
+  const long total = (long)N * C * H * W;
+  const long cols = (long)N * OH * OW;
+  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < total; i += (long)gridDim.x * blockDim.x) {
+    const int ix = (int)(i % W), iy = (int)((i / W) % H), c = (int)((i / ((long)W * H)) % C);
+    const int n = (int)(i / ((long)W * H * C));
+    float acc = 0.f;
+    for (int kh = 0; kh < KH; ++kh) {
+      const int ty = iy + PH - kh;
+      if (ty < 0 || ty % SH) continue;
+      const int oh = ty / SH;
+      if (oh >= OH) continue;
+      for (int kw = 0; kw < KW; ++kw) {
+        const int tx = ix + PW - kw;
+        if (tx < 0 || tx % SW) continue;
+        const int ow = tx / SW;
+        if (ow >= OW) continue;
+        acc += col[((long)(c * KH + kh) * KW + kw) * cols + ((long)n * OH + oh) * OW + ow];
+      }
+    }
+    x[i] = acc;
+  }
+}
+
+// ------------------------------------- launchers -----------------------------------------
+#define DCNN_DT(dtype, FN, ...) \
+  if (dtype == 0) FN<float>(__VA_ARGS__); else FN<bf16>(__VA_ARGS__)
+
+template <typename T>
+static void maxpool_fwd_t(const void* x, void* y, uint8_t* idx, PoolGeom g, hipStream_t s) {
+  const long total = (long)g.N * g.OH * g.OW * g.C;
+  hipLaunchKernelGGL(maxpool_fwd_kernel<T>, dim3(grid_for(total, 256)), dim3(256), 0, s, (const T*)x, (T*)y, idx, g);
+  DCNN_LAUNCH_CHECK();
+}
+template <typename T>
+static void maxpool_bwd_t(const void* dy, const uint8_t* idx, void* dx, PoolGeom g, hipStream_t s) {
+  const long total = (long)g.N * g.H * g.W * g.C;
+  hipLaunchKernelGGL(maxpool_bwd_kernel<T>, dim3(grid_for(total, 256)), dim3(256), 0, s, (const T*)dy, idx, (T*)dx, g);
+  DCNN_LAUNCH_CHECK();
+}
+template <typename T>
+static void avgpool_fwd_t(const void* x, void* y, PoolGeom g, hipStream_t s) {
+  if (g.OH == 1 && g.OW == 1 && g.ph == g.H && g.pw == g.W && g.padh == 0 && g.padw == 0) {
+    const long total = (long)g.N * g.C;
+    hipLaunchKernelGGL(global_avgpool_fwd_kernel<T>, dim3(grid_for(total, 256)), dim3(256), 0, s, (const T*)x, (T*)y,
+                       g.N, g.H * g.W, g.C);
+  } else {
+    const long total = (long)g.N * g.OH * g.OW * g.C;
+    hipLaunchKernelGGL(avgpool_fwd_kernel<T>, dim3(grid_for(total, 256)), dim3(256), 0, s, (const T*)x, (T*)y, g);
+  }
+  DCNN_LAUNCH_CHECK();
+}
+template <typename T>
+static void avgpool_bwd_t(const void* dy, void* dx, PoolGeom g, hipStream_t s) {
+  const long total = (long)g.N * g.H * g.W * g.C;
+  if (g.OH == 1 && g.OW == 1 && g.ph == g.H && g.pw == g.W && g.padh == 0 && g.padw == 0)
+    hipLaunchKernelGGL(global_avgpool_bwd_kernel<T>, dim3(grid_for(total, 256)), dim3(256), 0, s, (const T*)dy, (T*)dx,
+                       g.N, g.H * g.W, g.C);
+  else
+    hipLaunchKernelGGL(avgpool_bwd_kernel<T>, dim3(grid_for(total, 256)), dim3(256), 0, s, (const T*)dy, (T*)dx, g);
+  DCNN_LAUNCH_CHECK();
+}
+
+void maxpool_fwd(int dt, const void* x, void* y, uint8_t* idx, PoolGeom g, hipStream_t s) { DCNN_DT(dt, maxpool_fwd_t, x, y, idx, g, s); }
+void maxpool_bwd(int dt, const void* dy, const uint8_t* idx, void* dx, PoolGeom g, hipStream_t s) { DCNN_DT(dt, maxpool_bwd_t, dy, idx, dx, g, s); }
+void avgpool_fwd(int dt, const void* x, void* y, PoolGeom g, hipStream_t s) { DCNN_DT(dt, avgpool_fwd_t, x, y, g, s); }
+void avgpool_bwd(int dt, const void* dy, void* dx, PoolGeom g, hipStream_t s) { DCNN_DT(dt, avgpool_bwd_t, dy, dx, g, s); }
+
+template <typename T>
+static void act_fwd_t(const void* x, void* y, long n, int type, float a, hipStream_t s) {
+  hipLaunchKernelGGL(act_fwd_kernel<T>, dim3(grid_for(n / 8 + 1, 256)), dim3(256), 0, s, (const T*)x, (T*)y, n, type, a);
+  DCNN_LAUNCH_CHECK();
+}
+template <typename T>
+static void act_bwd_t(const void* x, const void* dy, void* dx, long n, int type, float a, hipStream_t s) {
+  hipLaunchKernelGGL(act_bwd_kernel<T>, dim3(grid_for(n, 256)), dim3(256), 0, s, (const T*)x, (const T*)dy, (T*)dx, n,
+                     type, a);
+  DCNN_LAUNCH_CHECK();
+}
+template <typename T>
+static void softmax_t(const void* x, void* y, long rows, int C, hipStream_t s) {
+  hipLaunchKernelGGL(softmax_rows_kernel<T>, dim3((rows * 64 + 255) / 256), dim3(256), 0, s, (const T*)x, (T*)y, rows, C);
+  DCNN_LAUNCH_CHECK();
+}
+template <typename T>
+static void softmax_bwd_t(const void* y, const void* dy, void* dx, long rows, int C, hipStream_t s) {
+  hipLaunchKernelGGL(softmax_rows_bwd_kernel<T>, dim3((rows * 64 + 255) / 256), dim3(256), 0, s, (const T*)y,
+                     (const T*)dy, (T*)dx, rows, C);
+  DCNN_LAUNCH_CHECK();
+}
+template <typename T>
+static void dropout_t(const void* x, void* y, long n, float p, uint64_t seed, hipStream_t s) {
+  hipLaunchKernelGGL(dropout_kernel<T>, dim3(grid_for((n + 3) / 4, 256)), dim3(256), 0, s, (const T*)x, (T*)y, n, p, seed);
+  DCNN_LAUNCH_CHECK();
+}
+template <typename T>
+static void nchw_to_nhwc_t(const float* x, void* y, int N, int C, int HW, hipStream_t s) {
+  hipLaunchKernelGGL(nchw_to_nhwc_kernel<T>, dim3(grid_for((long)N * C * HW, 256)), dim3(256), 0, s, x, (T*)y, N, C, HW);
+  DCNN_LAUNCH_CHECK();
+}
+template <typename T>
+static void wt_t(const void* w, bf16* wt, int Co, int T_, int Ci, hipStream_t s) {
+  hipLaunchKernelGGL(conv_weight_transpose_kernel<T>, dim3(grid_for((long)Co * T_ * Ci, 256)), dim3(256), 0, s,
+                     (const T*)w, wt, Co, T_, Ci);
+  DCNN_LAUNCH_CHECK();
+}
+
+void act_fwd(int dt, const void* x, void* y, long n, int type, float a, hipStream_t s) { DCNN_DT(dt, act_fwd_t, x, y, n, type, a, s); }
+void act_bwd(int dt, const void* x, const void* dy, void* dx, long n, int type, float a, hipStream_t s) { DCNN_DT(dt, act_bwd_t, x, dy, dx, n, type, a, s); }
+void softmax_rows(int dt, const void* x, void* y, long rows, int C, hipStream_t s) { DCNN_DT(dt, softmax_t, x, y, rows, C, s); }
+void softmax_rows_bwd(int dt, const void* y, const void* dy, void* dx, long rows, int C, hipStream_t s) { DCNN_DT(dt, softmax_bwd_t, y, dy, dx, rows, C, s); }
+void dropout(int dt, const void* x, void* y, long n, float p, uint64_t seed, hipStream_t s) { DCNN_DT(dt, dropout_t, x, y, n, p, seed, s); }
+void nchw_to_nhwc(int dt, const float* x, void* y, int N, int C, int HW, hipStream_t s) { DCNN_DT(dt, nchw_to_nhwc_t, x, y, N, C, HW, s); }
+void conv_weight_transpose(int src_dt, const void* w, bf16* wt, int Co, int T_, int Ci, hipStream_t s) { DCNN_DT(src_dt, wt_t, w, wt, Co, T_, Ci, s); }
+void cast_f32_bf16(const float* x, bf16* y, long n, hipStream_t s) {
+  hipLaunchKernelGGL(cast_f32_bf16_kernel, dim3(grid_for(n, 256)), dim3(256), 0, s, x, y, n);
+  DCNN_LAUNCH_CHECK();
+}
+void im2col(const float* x, float* col, int N, int C, int H, int W, int KH, int KW, int SH, int SW, int PH, int PW,
+            int OH, int OW, hipStream_t s) {
+  const long total = (long)C * KH * KW * N * OH * OW;
+  hipLaunchKernelGGL(im2col_kernel, dim3(grid_for(total, 256)), dim3(256), 0, s, x, col, N, C, H, W, KH, KW, SH, SW, PH,
+                     PW, OH, OW);
+  DCNN_LAUNCH_CHECK();
+}
+void col2im(const float* col, float* x, int N, int C, int H, int W, int KH, int KW, int SH, int SW, int PH, int PW,
+            int OH, int OW, hipStream_t s) {
+  const long total = (long)N * C * H * W;
+  hipLaunchKernelGGL(col2im_kernel, dim3(grid_for(total, 256)), dim3(256), 0, s, col, x, N, C, H, W, KH, KW, SH, SW, PH,
+                     PW, OH, OW);
+  DCNN_LAUNCH_CHECK();
+}
+
+}  // namespace dcnn

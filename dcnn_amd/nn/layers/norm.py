@@ -1,0 +1,265 @@
+"""BatchNorm and GroupNorm layers.
+
+Reference: `include/nn/layers_impl/batchnorm_layer.tpp:27-369`,
+`include/nn/layers_impl/groupnorm_layer.tpp:21-321`. GPU path: split-reduction statistics
+(or the preceding conv's epilogue partials), one fused apply pass (+ReLU, +residual add of a
+ResNet block), fused ReLU-masked backward; x_hat is recomputed rather than stored.
+dgamma/dbeta ACCUMULATE on both devices (reference defect G4).
+"""
+from __future__ import annotations
+
+from typing import Optional
+
+import torch
+
+from ..params import ParamSpec
+from .base import LayerConfig, ParameterizedLayer
+
+
+class BatchNorm(ParameterizedLayer):
+    type_name = "batchnorm"
+
+    def __init__(self, num_features: int, epsilon: float = 1e-5, momentum: float = 0.1, affine: bool = True,
+                 name: str = "batchnorm"):
+        super().__init__(name)
+        self.num_features = int(num_features)
+        self.epsilon = float(epsilon)
+        self.momentum = float(momentum)
+        self.affine = bool(affine)
+        self.running_mean = torch.zeros(self.num_features)
+        self.running_var = torch.ones(self.num_features)
+        # GPU fusion flags (set by the Sequential/ResidualBlock planner)
+        self.fuse_relu = False          # apply ReLU in the same pass (next Activation is passthrough)
+        self.emit_masked_grad = False   # backward also returns dy*(y>0) for a residual branch
+        self._last_masked = {}
+
+    def param_specs(self):
+        if not self.affine:
+            return []
+        return [ParamSpec("gamma", (self.num_features, 1, 1, 1)), ParamSpec("beta", (self.num_features, 1, 1, 1))]
+
+    def init_values(self, gen):
+        if not self.affine:
+            return []
+        return [torch.ones((self.num_features, 1, 1, 1)), torch.zeros((self.num_features, 1, 1, 1))]
+
+    def has_parameters(self):
+        return self.affine
+
+    def initialize(self):
+        super().initialize()
+        self._move_buffers(self.device)
+
+    def _move_buffers(self, device):
+        td = device.torch_device
+        self.running_mean = self.running_mean.to(td)
+        self.running_var = self.running_var.to(td)
+
+    def _gamma(self):
+        return self._params[0].view(-1) if self.affine else None
+
+    def _beta(self):
+        return self._params[1].view(-1) if self.affine else None
+
+    def forward(self, x, mb_id=0, residual: Optional[torch.Tensor] = None, relu: Optional[bool] = None):
+        """``residual``/``relu`` are used by a ResidualBlock to fuse ``act(bn(x) + shortcut)``."""
+        x = self._to_layer_device(x)
+        if x.shape[1] != self.num_features:
+            raise ValueError(f"BatchNorm '{self.name}': {x.shape[1]} channels, expected {self.num_features}")
+        do_relu = self.fuse_relu if relu is None else relu
+        if x.is_cuda:
+            from ...ops import hip
+            xa = hip.to_act(x, self.compute_dtype)
+            C = self.num_features
+            if self.training:
+                sums = hip.bn_stats(xa, getattr(x, "_bn_partial", None))
+                count = xa.numel() // C
+                mean = torch.empty(C, dtype=torch.float32, device=xa.device)
+                istd = torch.empty_like(mean)
+                y = hip.bn_apply(xa, sums, count, self._gamma(), self._beta(), self.epsilon, residual=residual,
+                                 relu=do_relu, save=(mean, istd), running=(self.running_mean, self.running_var),
+                                 momentum=self.momentum)
+            else:
+                y = hip.bn_apply(xa, None, 1, self._gamma(), self._beta(), self.epsilon, residual=residual,
+                                 relu=do_relu, running=(self.running_mean, self.running_var), use_running=True)
+                mean = self.running_mean
+                istd = torch.rsqrt(self.running_var + self.epsilon)
+            self._cache[mb_id] = (xa, y if do_relu else None, mean, istd, self.training)
+            return y
+        # ---- CPU reference path
+        C = self.num_features
+        if self.training:
+            mean = x.mean((0, 2, 3))
+            var = x.var((0, 2, 3), unbiased=False)
+            n = x.numel() // C
+            unbiased = var * n / max(n - 1, 1)
+            with torch.no_grad():
+                self.running_mean.mul_(1 - self.momentum).add_(self.momentum * mean)
+                self.running_var.mul_(1 - self.momentum).add_(self.momentum * unbiased)
+        else:
+            mean, var = self.running_mean, self.running_var
+        istd = torch.rsqrt(var + self.epsilon)
+        xhat = (x - mean.view(1, -1, 1, 1)) * istd.view(1, -1, 1, 1)
+        y = xhat * self._gamma().view(1, -1, 1, 1) + self._beta().view(1, -1, 1, 1) if self.affine else xhat
+        if residual is not None:
+            y = y + residual
+        if do_relu:
+            y = torch.relu(y)
+        self._cache[mb_id] = (x, y if do_relu else None, mean, istd, self.training)
+        return y
+
+    def backward(self, grad, mb_id=0):
+        ent = self._cache.pop(mb_id, None)
+        if ent is None:
+            raise RuntimeError(f"BatchNorm '{self.name}': no cached data for micro-batch {mb_id}")
+        x, yout, mean, istd, was_training = ent
+        grad = grad.to(x.device)
+        dg = self._grads[0].view(-1) if self.affine else None
+        db = self._grads[1].view(-1) if self.affine else None
+        if x.is_cuda:
+            from ...ops import hip
+            g = hip.to_act(grad, self.compute_dtype)
+            dx, dmask = hip.bn_backward(g, x, yout, mean, istd, self._gamma(), dg, db,
+                                        want_masked=self.emit_masked_grad, eval_mode=not was_training)
+            if self.emit_masked_grad:
+                self._last_masked[mb_id] = dmask if dmask is not None else g
+            return dx
+        d = grad * (yout > 0) if yout is not None else grad
+        if self.emit_masked_grad:
+            self._last_masked[mb_id] = d
+        m = istd.view(1, -1, 1, 1)
+        xhat = (x - mean.view(1, -1, 1, 1)) * m
+        gamma = self._gamma().view(1, -1, 1, 1) if self.affine else 1.0
+        sdy = d.sum((0, 2, 3))
+        sdyx = (d * xhat).sum((0, 2, 3))
+        if self.affine:
+            dg.add_(sdyx)
+            db.add_(sdy)
+        if not was_training:
+            return d * gamma * m
+        M = x.numel() // self.num_features
+        return gamma * m * (d - sdy.view(1, -1, 1, 1) / M - xhat * sdyx.view(1, -1, 1, 1) / M)
+
+    def pop_masked_grad(self, mb_id=0):
+        return self._last_masked.pop(mb_id)
+
+    def forward_flops(self, s):
+        n = 1
+        for d in s:
+            n *= d
+        return 6 * n  # stats (2) + normalize (2) + affine (2)
+
+    def backward_flops(self, s):
+        n = 1
+        for d in s:
+            n *= d
+        return 9 * n
+
+    def get_config(self):
+        return LayerConfig(self.name, dict(num_features=self.num_features, epsilon=self.epsilon,
+                                           momentum=self.momentum, affine=self.affine), self.type_name)
+
+    @staticmethod
+    def from_config(cfg):
+        p = cfg.parameters
+        return BatchNorm(p["num_features"], p.get("epsilon", 1e-5), p.get("momentum", 0.1), p.get("affine", True),
+                         cfg.name or "batchnorm")
+
+    def state_buffers(self):
+        return {"running_mean": self.running_mean, "running_var": self.running_var}
+
+
+class GroupNorm(ParameterizedLayer):
+    type_name = "groupnorm"
+
+    def __init__(self, num_groups: int, num_channels: int, epsilon: float = 1e-5, affine: bool = True,
+                 name: str = "groupnorm"):
+        super().__init__(name)
+        self.num_groups = int(num_groups)
+        self.num_channels = int(num_channels)
+        if self.num_channels % self.num_groups:
+            raise ValueError("num_channels must be divisible by num_groups")
+        self.epsilon = float(epsilon)
+        self.affine = bool(affine)
+
+    def param_specs(self):
+        if not self.affine:
+            return []
+        return [ParamSpec("gamma", (self.num_channels, 1, 1, 1)), ParamSpec("beta", (self.num_channels, 1, 1, 1))]
+
+    def init_values(self, gen):
+        if not self.affine:
+            return []
+        return [torch.ones((self.num_channels, 1, 1, 1)), torch.zeros((self.num_channels, 1, 1, 1))]
+
+    def has_parameters(self):
+        return self.affine
+
+    def forward(self, x, mb_id=0):
+        x = self._to_layer_device(x)
+        G = self.num_groups
+        gamma = self._params[0].view(-1) if self.affine else None
+        beta = self._params[1].view(-1) if self.affine else None
+        if x.is_cuda:
+            from ...ops import hip
+            xa = hip.to_act(x, self.compute_dtype)
+            y, mean, istd = hip.gn_fwd(xa, G, gamma, beta, self.epsilon)
+            self._cache[mb_id] = (xa, mean, istd)
+            return y
+        N, C, H, W = x.shape
+        xg = x.reshape(N, G, -1)
+        mean = xg.mean(-1)
+        var = xg.var(-1, unbiased=False)
+        istd = torch.rsqrt(var + self.epsilon)
+        xhat = ((xg - mean.unsqueeze(-1)) * istd.unsqueeze(-1)).reshape(N, C, H, W)
+        y = xhat * gamma.view(1, -1, 1, 1) + beta.view(1, -1, 1, 1) if self.affine else xhat
+        self._cache[mb_id] = (x, mean.reshape(-1), istd.reshape(-1))
+        return y
+
+    def backward(self, grad, mb_id=0):
+        ent = self._cache.pop(mb_id, None)
+        if ent is None:
+            raise RuntimeError(f"GroupNorm '{self.name}': no cached data for micro-batch {mb_id}")
+        x, mean, istd = ent
+        G = self.num_groups
+        gamma = self._params[0].view(-1) if self.affine else None
+        dg = self._grads[0].view(-1) if self.affine else None
+        db = self._grads[1].view(-1) if self.affine else None
+        if x.is_cuda:
+            from ...ops import hip
+            g = hip.to_act(grad.to(x.device), self.compute_dtype)
+            return hip.gn_bwd(g, x, G, gamma, mean, istd, dg, db)
+        N, C, H, W = x.shape
+        xg = x.reshape(N, G, -1)
+        xhat = ((xg - mean.view(N, G, 1)) * istd.view(N, G, 1)).reshape(N, C, H, W)
+        if self.affine:
+            dg.add_((grad * xhat).sum((0, 2, 3)))
+            db.add_(grad.sum((0, 2, 3)))
+        d = grad * gamma.view(1, -1, 1, 1) if self.affine else grad
+        dgp = d.reshape(N, G, -1)
+        xh = xhat.reshape(N, G, -1)
+        m1 = dgp.mean(-1, keepdim=True)
+        m2 = (dgp * xh).mean(-1, keepdim=True)
+        return (istd.view(N, G, 1) * (dgp - m1 - xh * m2)).reshape(N, C, H, W)
+
+    def forward_flops(self, s):
+        n = 1
+        for d in s:
+            n *= d
+        return 6 * n
+
+    def backward_flops(self, s):
+        n = 1
+        for d in s:
+            n *= d
+        return 9 * n
+
+    def get_config(self):
+        return LayerConfig(self.name, dict(num_groups=self.num_groups, num_channels=self.num_channels,
+                                           epsilon=self.epsilon, affine=self.affine), self.type_name)
+
+    @staticmethod
+    def from_config(cfg):
+        p = cfg.parameters
+        return GroupNorm(int(p["num_groups"]), p["num_channels"], p.get("epsilon", 1e-5), p.get("affine", True),
+                         cfg.name or "groupnorm")

@@ -1,0 +1,240 @@
+"""ResidualBlock: ``out = act(F(x) + S(x))`` (reference `include/nn/blocks_impl/residual_block.hpp:30-476`).
+
+GPU path fuses the tail of the block: the last BatchNorm of F applies ``+ S(x)`` and the ReLU
+in the same pass (no pre-activation tensor, no separate add/ReLU kernels), its backward emits
+the ReLU-masked gradient once for both branches, and the branch sum ``dF + dS`` is fused into
+the epilogue of the first conv's dgrad GEMM.
+"""
+from __future__ import annotations
+
+import json
+from typing import List, Optional
+
+import torch
+
+from ..activations import ActivationFactory
+from .base import LayerConfig, Layer
+from .conv import Conv2D
+from .misc import Activation
+from .norm import BatchNorm
+
+
+def plan_fusion(layers: List[Layer], on_gpu: bool) -> None:
+    """Mark cross-layer fusions for the GPU path (no-op on CPU: pure reference semantics)."""
+    for l in layers:
+        if isinstance(l, Conv2D):
+            l.emit_bn_stats = False
+        if isinstance(l, BatchNorm):
+            l.fuse_relu = False
+            l.emit_masked_grad = False
+        if isinstance(l, Activation):
+            l.passthrough = False
+    if not on_gpu:
+        return
+    for a, b in zip(layers[:-1], layers[1:]):
+        if isinstance(a, Conv2D) and isinstance(b, BatchNorm):
+            a.emit_bn_stats = True
+        if isinstance(a, BatchNorm) and isinstance(b, Activation) and b.activation_name == "relu":
+            a.fuse_relu = True
+            b.passthrough = True
+
+
+class ResidualBlock(Layer):
+    type_name = "residual_block"
+
+    def __init__(self, main_path: List[Layer], shortcut_path: Optional[List[Layer]] = None,
+                 activation: str = "relu", name: str = "residual_block"):
+        super().__init__(name)
+        self.main_path = list(main_path)
+        self.shortcut_path = list(shortcut_path or [])
+        self.activation_type = activation
+        self.act = ActivationFactory.create(activation)
+        self._fused = False
+
+    # structure -------------------------------------------------------------------------
+    def sublayers(self) -> List[Layer]:
+        return self.main_path + self.shortcut_path
+
+    def get_main_path(self):
+        return self.main_path
+
+    def get_shortcut_path(self):
+        return self.shortcut_path
+
+    def has_parameters(self):
+        return any(l.has_parameters() for l in self.sublayers())
+
+    def parameters(self):
+        return [p for l in self.sublayers() for p in l.parameters()]
+
+    def gradients(self):
+        return [g for l in self.sublayers() for g in l.gradients()]
+
+    def set_training(self, training):
+        super().set_training(training)
+        for l in self.sublayers():
+            l.set_training(training)
+
+    def set_device(self, device):
+        super().set_device(device)
+        for l in self.sublayers():
+            l.set_device(device)
+        self._plan()
+
+    def set_compute_dtype(self, dtype):
+        super().set_compute_dtype(dtype)
+        for l in self.sublayers():
+            l.set_compute_dtype(dtype)
+
+    def set_seed(self, seed):
+        super().set_seed(seed)
+        for i, l in enumerate(self.sublayers()):
+            l.set_seed(seed + 1 + i)
+
+    def initialize(self):
+        for l in self.sublayers():
+            l.initialize()
+        self._plan()
+        self.initialized = True
+
+    def _plan(self):
+        on_gpu = self.device.is_gpu()
+        plan_fusion(self.main_path, on_gpu)
+        plan_fusion(self.shortcut_path, on_gpu)
+        act_ok = self.activation_type in ("relu", "none", "linear")
+        self._fused = on_gpu and bool(self.main_path) and isinstance(self.main_path[-1], BatchNorm) and act_ok
+        if self._fused:
+            self.main_path[-1].emit_masked_grad = True
+        for l in self.sublayers():
+            l.needs_input_grad = True
+        if self.main_path:
+            self.main_path[0].needs_input_grad = self.needs_input_grad
+        if self.shortcut_path:
+            self.shortcut_path[0].needs_input_grad = self.needs_input_grad
+
+    def clear_cache(self, mb_id=None):
+        super().clear_cache(mb_id)
+        for l in self.sublayers():
+            l.clear_cache(mb_id)
+
+    # compute ---------------------------------------------------------------------------
+    def forward(self, x, mb_id=0):
+        x = self._to_layer_device(x)
+        if self._fused:
+            from ...ops import hip
+            xa = hip.to_act(x, self.compute_dtype)
+            s = xa
+            for l in self.shortcut_path:
+                s = l.forward(s, mb_id)
+            h = xa
+            for l in self.main_path[:-1]:
+                h = l.forward(h, mb_id)
+            out = self.main_path[-1].forward(h, mb_id, residual=hip.to_act(s, self.compute_dtype),
+                                             relu=self.activation_type == "relu")
+            self._cache[mb_id] = ("fused", None)
+            return out
+        h = x
+        for l in self.main_path:
+            h = l.forward(h, mb_id)
+        s = x
+        for l in self.shortcut_path:
+            s = l.forward(s, mb_id)
+        pre = h + s
+        out = self.act.apply(pre) if self.act is not None else pre
+        self._cache[mb_id] = ("plain", (pre, out))
+        return out
+
+    def backward(self, grad, mb_id=0):
+        kind, ent = self._cache.pop(mb_id)
+        if kind == "fused":
+            last = self.main_path[-1]
+            g = last.backward(grad, mb_id)
+            d_pre = last.pop_masked_grad(mb_id)
+            d_s = d_pre
+            for l in reversed(self.shortcut_path):
+                d_s = l.backward(d_s, mb_id)
+            for l in reversed(self.main_path[1:-1]):
+                g = l.backward(g, mb_id)
+            first = self.main_path[0]
+            if not self.needs_input_grad:
+                first.backward(g, mb_id) if len(self.main_path) > 1 else None
+                return None
+            if len(self.main_path) == 1:
+                return g + d_s
+            if isinstance(first, Conv2D):
+                return first.backward(g, mb_id, add_to=d_s)
+            return first.backward(g, mb_id) + d_s
+        pre, out = ent
+        g = self.act.gradient(pre, out, grad) if self.act is not None else grad
+        d_main = g
+        for l in reversed(self.main_path):
+            d_main = l.backward(d_main, mb_id)
+        d_s = g
+        for l in reversed(self.shortcut_path):
+            d_s = l.backward(d_s, mb_id)
+        if not self.needs_input_grad:
+            return None
+        return d_main + d_s
+
+    # shapes / cost -----------------------------------------------------------------------
+    def compute_output_shape(self, s):
+        for l in self.main_path:
+            s = l.compute_output_shape(s)
+        return s
+
+    def _flops(self, s, fwd):
+        total = 0
+        cur = list(s)
+        for l in self.main_path:
+            total += l.forward_flops(cur) if fwd else l.backward_flops(cur)
+            cur = l.compute_output_shape(cur)
+        cur2 = list(s)
+        for l in self.shortcut_path:
+            total += l.forward_flops(cur2) if fwd else l.backward_flops(cur2)
+            cur2 = l.compute_output_shape(cur2)
+        n = 1
+        for d in cur:
+            n *= d
+        return total + 2 * n
+
+    def forward_flops(self, s):
+        return self._flops(s, True)
+
+    def backward_flops(self, s):
+        return self._flops(s, False)
+
+    def cached_memory_bytes(self):
+        return super().cached_memory_bytes() + sum(l.cached_memory_bytes() for l in self.sublayers())
+
+    # config ------------------------------------------------------------------------------
+    @staticmethod
+    def _dump_path(path):
+        arr = []
+        for l in path:
+            c = l.get_config()
+            arr.append({"type": l.type(), "name": c.name, "parameters": c.parameters})
+        return json.dumps(arr)
+
+    def get_config(self):
+        return LayerConfig(self.name, dict(activation=self.activation_type,
+                                           has_projection=bool(self.shortcut_path),
+                                           main_path=self._dump_path(self.main_path),
+                                           shortcut_path=self._dump_path(self.shortcut_path)), self.type_name)
+
+    @staticmethod
+    def from_config(cfg):
+        from . import create_layer
+        p = cfg.parameters
+        main = [create_layer(d["type"], LayerConfig(d.get("name", ""), d.get("parameters", {}), d["type"]))
+                for d in json.loads(p.get("main_path", "[]"))]
+        short = []
+        if p.get("has_projection", False):
+            short = [create_layer(d["type"], LayerConfig(d.get("name", ""), d.get("parameters", {}), d["type"]))
+                     for d in json.loads(p.get("shortcut_path", "[]"))]
+        return ResidualBlock(main, short, p.get("activation", "relu"), cfg.name or "residual_block")
+
+    def clone(self):
+        c = ResidualBlock([l.clone() for l in self.main_path], [l.clone() for l in self.shortcut_path],
+                          self.activation_type, self.name)
+        c.training = self.training
+        return c

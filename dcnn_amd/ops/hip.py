@@ -1,0 +1,390 @@
+"""Torch-tensor front end of the HIP/CDNA4 kernel library (GPU path of every layer).
+
+Activations are NHWC in memory (torch ``channels_last``) so the channel dimension is the
+contiguous GEMM-K dimension of the implicit-GEMM convolution; the logical shape stays NCHW
+(the reference API/checkpoint layout). Conv weights are ``channels_last`` too, i.e. physical
+``[Cout][KH][KW][Cin]`` — the K-contiguous B operand of the MFMA GEMM. All launches go to
+PyTorch's current HIP stream and allocate workspaces from its caching allocator, so a whole
+training step can be captured into a hipGraph.
+"""
+from __future__ import annotations
+
+import torch
+
+from ._ext import dt_code, kernels, ptr, stream_ptr
+
+CL = torch.channels_last
+F32 = torch.float32
+BF16 = torch.bfloat16
+
+# gather modes of gemm_nt
+PLAIN, CONV_FWD, CONV_DGRAD = 0, 1, 2
+
+
+def _check_act(x: torch.Tensor, what: str):
+    if not x.is_cuda:
+        raise ValueError(f"{what}: expected a GPU tensor")
+    if x.dim() == 4 and not x.is_contiguous(memory_format=CL):
+        raise ValueError(f"{what}: expected channels_last (NHWC) memory layout")
+
+
+def to_act(x: torch.Tensor, dtype: torch.dtype) -> torch.Tensor:
+    """Bring a (N,C,H,W) tensor into the GPU activation format: NHWC memory, compute dtype."""
+    if x.dim() == 4 and x.dtype == dtype and x.is_contiguous(memory_format=CL):
+        return x
+    if x.dim() == 4 and x.dtype == F32 and x.is_contiguous():
+        # fused NCHW fp32 -> NHWC (bf16|fp32) conversion kernel (network input path)
+        N, C, H, W = x.shape
+        y = torch.empty((N, C, H, W), dtype=dtype, device=x.device, memory_format=CL)
+        kernels().nchw_to_nhwc(dt_code(dtype), x.data_ptr(), y.data_ptr(), N, C, H * W, stream_ptr())
+        return y
+    return x.to(dtype=dtype).contiguous(memory_format=CL)
+
+
+def conv_out_hw(H, W, kh, kw, sh, sw, ph, pw):
+    return (H + 2 * ph - kh) // sh + 1, (W + 2 * pw - kw) // sw + 1
+
+
+# ------------------------------------------------------------------------------ conv / dense
+def conv2d_fwd(x, w, bias, stride, pad, *, stats=False, residual=None, relu=False, out_fp32=False):
+    """y = conv(x, w) + bias  [+ residual] [ReLU]; optional BN partial statistics slab.
+
+    x: (N,Ci,H,W) bf16 channels_last; w: (Co,Ci,KH,KW) bf16 channels_last.
+    Returns (y, (slab, rows) | None).
+    """
+    _check_act(x, "conv2d_fwd.x")
+    K = kernels()
+    N, Ci, H, W = x.shape
+    Co, Ci2, KH, KW = w.shape
+    assert Ci == Ci2, f"conv2d: input channels {Ci} != weight {Ci2}"
+    assert x.dtype == BF16 and w.dtype == BF16 and w.is_contiguous(memory_format=CL)
+    sh, sw = stride
+    ph, pw = pad
+    OH, OW = conv_out_hw(H, W, KH, KW, sh, sw, ph, pw)
+    y = torch.empty((N, Co, OH, OW), dtype=F32 if out_fp32 else BF16, device=x.device, memory_format=CL)
+    M = N * OH * OW
+    slab = None
+    rows = 0
+    if stats:
+        rows = K.gemm_nt_stat_rows(M, Co)
+        slab = torch.empty((rows, 2, Co), dtype=F32, device=x.device)
+    if residual is not None:
+        assert residual.shape == y.shape and residual.is_contiguous(memory_format=CL) and residual.dtype == BF16
+    K.gemm_nt(x.data_ptr(), w.data_ptr(), y.data_ptr(), M, Co, KH * KW * Ci, 0, KH * KW * Ci, Co, CONV_FWD,
+              N, H, W, Ci, OH, OW, KH, KW, sh, sw, ph, pw, ptr(bias), ptr(residual), ptr(slab),
+              int(out_fp32), int(relu), stream_ptr())
+    return y, ((slab, rows) if stats else None)
+
+
+def conv_weight_t(w, out=None):
+    """(Co,Ci,KH,KW) channels_last weight -> bf16 [Ci][KH][KW][Co] dgrad operand."""
+    Co, Ci, KH, KW = w.shape
+    if out is None:
+        out = torch.empty((Ci, KH, KW, Co), dtype=BF16, device=w.device)
+    kernels().conv_weight_transpose(dt_code(w.dtype), w.data_ptr(), out.data_ptr(), Co, KH * KW, Ci, stream_ptr())
+    return out
+
+
+def conv2d_dgrad(dy, wt, x_shape, stride, pad, *, residual=None):
+    """dx = conv_transpose(dy, w) [+ residual];  wt = conv_weight_t(w)."""
+    _check_act(dy, "conv2d_dgrad.dy")
+    N, Ci, H, W = x_shape
+    _, OH, OW_, Co = dy.shape[0], dy.shape[2], dy.shape[3], dy.shape[1]
+    Ci2, KH, KW, Co2 = wt.shape
+    assert Ci == Ci2 and Co == Co2
+    dx = torch.empty((N, Ci, H, W), dtype=BF16, device=dy.device, memory_format=CL)
+    if residual is not None:
+        assert residual.shape == dx.shape and residual.is_contiguous(memory_format=CL)
+    M = N * H * W
+    Kd = KH * KW * Co
+    kernels().gemm_nt(dy.data_ptr(), wt.data_ptr(), dx.data_ptr(), M, Ci, Kd, 0, Kd, Ci, CONV_DGRAD,
+                      N, OH, OW_, Co, H, W, KH, KW, stride[0], stride[1], pad[0], pad[1],
+                      0, ptr(residual), 0, 0, 0, stream_ptr())
+    return dx
+
+
+def conv2d_wgrad(dy, x, w_shape, stride, pad, grad_w, grad_b=None):
+    """grad_w (+)= dW, grad_b (+)= sum(dy): split-K MFMA GEMM + fp32 slab reduce (beta = 1)."""
+    K = kernels()
+    N, Ci, H, W = x.shape
+    Co, _, KH, KW = w_shape
+    OH, OW = dy.shape[2], dy.shape[3]
+    P = N * OH * OW
+    Ng = KH * KW * Ci
+    splits = K.gemm_tn_splits(Co, Ng, P)
+    slab = torch.empty((splits, Co, Ng), dtype=F32, device=x.device)
+    bslab = torch.empty((splits, Co), dtype=F32, device=x.device) if grad_b is not None else None
+    st = stream_ptr()
+    K.gemm_tn(dy.data_ptr(), x.data_ptr(), slab.data_ptr(), ptr(bslab), Co, Ng, P, CONV_FWD,
+              N, H, W, Ci, OH, OW, KH, KW, stride[0], stride[1], pad[0], pad[1], 0, splits, st)
+    assert grad_w.is_contiguous(memory_format=CL) or KH * KW == 1 or Ci == 1
+    K.splitk_reduce(slab.data_ptr(), grad_w.data_ptr(), Co * Ng, splits, 1, st)
+    if grad_b is not None:
+        K.splitk_reduce(bslab.data_ptr(), grad_b.data_ptr(), Co, splits, 1, st)
+
+
+def dense_fwd(x2d, w2d, bias):
+    """y[N,Out] = x[N,In] . w[Out,In]^T + b   (bf16 in/out, fp32 accumulate)."""
+    N, In = x2d.shape
+    Out = w2d.shape[0]
+    y = torch.empty((N, Out), dtype=BF16, device=x2d.device)
+    kernels().gemm_nt(x2d.data_ptr(), w2d.data_ptr(), y.data_ptr(), N, Out, In, In, In, Out, PLAIN,
+                      0, 0, 0, 0, 1, 1, 1, 1, 1, 1, 0, 0, ptr(bias), 0, 0, 0, 0, stream_ptr())
+    return y
+
+
+def dense_dgrad(dy2d, wt2d):
+    """dx[N,In] = dy[N,Out] . w[Out,In]   with wt2d = w^T stored [In][Out]."""
+    N, Out = dy2d.shape
+    In = wt2d.shape[0]
+    dx = torch.empty((N, In), dtype=BF16, device=dy2d.device)
+    kernels().gemm_nt(dy2d.data_ptr(), wt2d.data_ptr(), dx.data_ptr(), N, In, Out, Out, Out, In, PLAIN,
+                      0, 0, 0, 0, 1, 1, 1, 1, 1, 1, 0, 0, 0, 0, 0, 0, 0, stream_ptr())
+    return dx
+
+
+def dense_wgrad(dy2d, x2d, grad_w, grad_b=None):
+    K = kernels()
+    N, Out = dy2d.shape
+    In = x2d.shape[1]
+    splits = K.gemm_tn_splits(Out, In, N)
+    slab = torch.empty((splits, Out, In), dtype=F32, device=x2d.device)
+    bslab = torch.empty((splits, Out), dtype=F32, device=x2d.device) if grad_b is not None else None
+    st = stream_ptr()
+    K.gemm_tn(dy2d.data_ptr(), x2d.data_ptr(), slab.data_ptr(), ptr(bslab), Out, In, N, PLAIN,
+              0, 0, 0, 0, 1, 1, 1, 1, 1, 1, 0, 0, In, splits, st)
+    K.splitk_reduce(slab.data_ptr(), grad_w.data_ptr(), Out * In, splits, 1, st)
+    if grad_b is not None:
+        K.splitk_reduce(bslab.data_ptr(), grad_b.data_ptr(), Out, splits, 1, st)
+
+
+# ------------------------------------------------------------------------------ batch norm
+def _rc(x):
+    N, C, H, W = x.shape
+    return N * H * W, C
+
+
+def bn_stats(x, partial=None):
+    """Per-channel (sum, sumsq) of x (NHWC). Uses the conv-epilogue partial slab if given."""
+    K = kernels()
+    R, C = _rc(x)
+    st = stream_ptr()
+    if partial is None:
+        rows = K.bn_partial_rows(R, C)
+        slab = torch.empty((rows, 2, C), dtype=F32, device=x.device)
+        K.bn_partial(dt_code(x.dtype), x.data_ptr(), 0, 0, 0, 0, 0, R, C, slab.data_ptr(), 0, st)
+    else:
+        slab, rows = partial
+    sums = torch.empty((2 * C,), dtype=F32, device=x.device)
+    K.bn_slab_reduce(slab.data_ptr(), rows, C, sums.data_ptr(), st)
+    return sums
+
+
+def bn_apply(x, sums, count, gamma, beta, eps, *, residual=None, relu=False, save=None, running=None,
+             momentum=0.1, use_running=False):
+    R, C = _rc(x)
+    y = torch.empty_like(x, memory_format=CL)
+    sm, si = save if save is not None else (None, None)
+    rm, rv = running if running is not None else (None, None)
+    kernels().bn_apply(dt_code(x.dtype), x.data_ptr(), y.data_ptr(), R, C, ptr(sums), float(count), ptr(gamma),
+                       ptr(beta), float(eps), ptr(residual), int(relu), ptr(sm), ptr(si), ptr(rm), ptr(rv),
+                       float(momentum), int(use_running), stream_ptr())
+    return y
+
+
+def bn_backward(dy, x, yout, mean, istd, gamma, dgamma, dbeta, *, want_masked=False, eval_mode=False):
+    """Returns (dx, masked_dy|None). yout given => ReLU was fused: dy' = dy * (yout > 0)."""
+    K = kernels()
+    R, C = _rc(x)
+    st = stream_ptr()
+    dt = dt_code(x.dtype)
+    dmask = torch.empty_like(dy, memory_format=CL) if (want_masked and yout is not None) else None
+    sums = None
+    if not eval_mode:
+        rows = K.bn_partial_rows(R, C)
+        slab = torch.empty((rows, 2, C), dtype=F32, device=x.device)
+        K.bn_partial(dt, x.data_ptr(), dy.data_ptr(), ptr(yout), ptr(dmask), mean.data_ptr(), istd.data_ptr(), R, C,
+                     slab.data_ptr(), 1, st)
+        sums = torch.empty((2 * C,), dtype=F32, device=x.device)
+        K.bn_slab_reduce(slab.data_ptr(), rows, C, sums.data_ptr(), st)
+    elif want_masked and yout is not None:
+        dmask = dy * (yout > 0)
+    dx = torch.empty_like(x, memory_format=CL)
+    src = dmask if dmask is not None else dy
+    K.bn_bwd_apply(dt, src.data_ptr(), 0 if dmask is not None else ptr(yout), x.data_ptr(), dx.data_ptr(), R, C,
+                   mean.data_ptr(), istd.data_ptr(), ptr(gamma), ptr(sums), float(R), ptr(dgamma), ptr(dbeta),
+                   int(eval_mode), st)
+    if eval_mode and (dgamma is not None or dbeta is not None):
+        # frozen-statistics backward still accumulates the affine gradients
+        xf = x.float()
+        d = (src if dmask is None else dmask).float()
+        if yout is not None and dmask is None:
+            d = d * (yout > 0)
+        xhat = (xf - mean.view(1, -1, 1, 1)) * istd.view(1, -1, 1, 1)
+        if dgamma is not None:
+            dgamma += (d * xhat).sum((0, 2, 3))
+        if dbeta is not None:
+            dbeta += d.sum((0, 2, 3))
+    return dx, dmask
+
+
+def gn_fwd(x, groups, gamma, beta, eps):
+    N, C, H, W = x.shape
+    y = torch.empty_like(x, memory_format=CL)
+    mean = torch.empty((N * groups,), dtype=F32, device=x.device)
+    istd = torch.empty_like(mean)
+    kernels().gn_fwd(dt_code(x.dtype), x.data_ptr(), y.data_ptr(), N, H * W, C, groups, ptr(gamma), ptr(beta),
+                     float(eps), mean.data_ptr(), istd.data_ptr(), stream_ptr())
+    return y, mean, istd
+
+
+def gn_bwd(dy, x, groups, gamma, mean, istd, dgamma, dbeta):
+    N, C, H, W = x.shape
+    dx = torch.empty_like(x, memory_format=CL)
+    kernels().gn_bwd(dt_code(x.dtype), dy.data_ptr(), x.data_ptr(), dx.data_ptr(), N, H * W, C, groups, ptr(gamma),
+                     mean.data_ptr(), istd.data_ptr(), ptr(dgamma), ptr(dbeta), stream_ptr())
+    return dx
+
+
+# ------------------------------------------------------------------------------ pooling
+def pool_out_hw(H, W, ph, pw, sh, sw, pdh, pdw):
+    return (H + 2 * pdh - ph) // sh + 1, (W + 2 * pdw - pw) // sw + 1
+
+
+def maxpool_fwd(x, ph, pw, sh, sw, pdh, pdw):
+    _check_act(x, "maxpool")
+    N, C, H, W = x.shape
+    OH, OW = pool_out_hw(H, W, ph, pw, sh, sw, pdh, pdw)
+    y = torch.empty((N, C, OH, OW), dtype=x.dtype, device=x.device, memory_format=CL)
+    idx = torch.empty((N, OH, OW, C), dtype=torch.uint8, device=x.device)
+    assert ph * pw <= 256
+    kernels().maxpool_fwd(dt_code(x.dtype), x.data_ptr(), y.data_ptr(), idx.data_ptr(), N, H, W, C, OH, OW, ph, pw,
+                          sh, sw, pdh, pdw, stream_ptr())
+    return y, idx
+
+
+def maxpool_bwd(dy, idx, x_shape, ph, pw, sh, sw, pdh, pdw):
+    N, C, H, W = x_shape
+    OH, OW = dy.shape[2], dy.shape[3]
+    dx = torch.empty((N, C, H, W), dtype=dy.dtype, device=dy.device, memory_format=CL)
+    kernels().maxpool_bwd(dt_code(dy.dtype), dy.data_ptr(), idx.data_ptr(), dx.data_ptr(), N, H, W, C, OH, OW, ph, pw,
+                          sh, sw, pdh, pdw, stream_ptr())
+    return dx
+
+
+def avgpool_fwd(x, ph, pw, sh, sw, pdh, pdw):
+    _check_act(x, "avgpool")
+    N, C, H, W = x.shape
+    OH, OW = pool_out_hw(H, W, ph, pw, sh, sw, pdh, pdw)
+    y = torch.empty((N, C, OH, OW), dtype=x.dtype, device=x.device, memory_format=CL)
+    kernels().avgpool_fwd(dt_code(x.dtype), x.data_ptr(), y.data_ptr(), N, H, W, C, OH, OW, ph, pw, sh, sw, pdh, pdw,
+                          stream_ptr())
+    return y
+
+
+def avgpool_bwd(dy, x_shape, ph, pw, sh, sw, pdh, pdw):
+    N, C, H, W = x_shape
+    OH, OW = dy.shape[2], dy.shape[3]
+    dy = dy.contiguous(memory_format=CL)
+    dx = torch.empty((N, C, H, W), dtype=dy.dtype, device=dy.device, memory_format=CL)
+    kernels().avgpool_bwd(dt_code(dy.dtype), dy.data_ptr(), dx.data_ptr(), N, H, W, C, OH, OW, ph, pw, sh, sw, pdh,
+                          pdw, stream_ptr())
+    return dx
+
+
+# ------------------------------------------------------------------------------ activations
+ACT_CODES = {"relu": 0, "leaky_relu": 1, "elu": 2, "sigmoid": 3, "tanh": 4, "linear": 5}
+
+
+def act_fwd(x, kind, alpha=0.01):
+    y = torch.empty_like(x)
+    kernels().act_fwd(dt_code(x.dtype), x.data_ptr(), y.data_ptr(), x.numel(), ACT_CODES[kind], float(alpha),
+                      stream_ptr())
+    return y
+
+
+def act_bwd(x, dy, kind, alpha=0.01):
+    dy = dy.contiguous(memory_format=CL) if x.dim() == 4 and x.is_contiguous(memory_format=CL) else dy.contiguous()
+    dx = torch.empty_like(x)
+    kernels().act_bwd(dt_code(x.dtype), x.data_ptr(), dy.data_ptr(), dx.data_ptr(), x.numel(), ACT_CODES[kind],
+                      float(alpha), stream_ptr())
+    return dx
+
+
+def softmax_channels(x):
+    """softmax over dim 1 of an NCHW-logical / NHWC-physical tensor (channel innermost)."""
+    N, C = x.shape[0], x.shape[1]
+    rows = x.numel() // C
+    y = torch.empty_like(x)
+    kernels().softmax_rows(dt_code(x.dtype), x.data_ptr(), y.data_ptr(), rows, C, stream_ptr())
+    return y
+
+
+def softmax_channels_bwd(y, dy):
+    C = y.shape[1]
+    rows = y.numel() // C
+    dy = dy.contiguous(memory_format=CL) if y.dim() == 4 else dy.contiguous()
+    dx = torch.empty_like(y)
+    kernels().softmax_rows_bwd(dt_code(y.dtype), y.data_ptr(), dy.data_ptr(), dx.data_ptr(), rows, C, stream_ptr())
+    return dx
+
+
+def dropout(x, p, seed):
+    y = torch.empty_like(x)
+    kernels().dropout(dt_code(x.dtype), x.data_ptr(), y.data_ptr(), x.numel(), float(p), int(seed) & ((1 << 64) - 1),
+                      stream_ptr())
+    return y
+
+
+# ------------------------------------------------------------------------------ loss / optim
+LOSS_CODES = {"crossentropy": 0, "softmax_crossentropy": 1, "logsoftmax_crossentropy": 2, "mse": 3, "mae": 4,
+              "huber": 5}
+
+
+def loss_fused(pred2d, target2d=None, labels=None, kind="softmax_crossentropy", param=1e-15, want_grad=True):
+    """Returns (loss[1] f32 device, grad|None, correct[1] int32 device). No host sync."""
+    N, C = pred2d.shape
+    pred2d = pred2d.contiguous()
+    grad = torch.empty_like(pred2d) if want_grad else None
+    loss = torch.empty((1,), dtype=F32, device=pred2d.device)
+    correct = torch.empty((1,), dtype=torch.int32, device=pred2d.device)
+    tgt = None
+    if target2d is not None:
+        tgt = target2d.reshape(N, C).to(F32).contiguous()
+    lab = labels.to(torch.int64).contiguous() if labels is not None else None
+    kernels().loss_fused(dt_code(pred2d.dtype), pred2d.data_ptr(), ptr(tgt), ptr(lab), ptr(grad), loss.data_ptr(),
+                         correct.data_ptr(), N, C, LOSS_CODES[kind], float(param), stream_ptr())
+    return loss, grad, correct
+
+
+def adam_step(p, g, m, v, shadow, lr, b1, b2, eps, bc1, bc2, wd, decoupled, hyper=None):
+    kernels().adam_step(p.data_ptr(), g.data_ptr(), m.data_ptr(), v.data_ptr(), ptr(shadow), p.numel(), float(lr),
+                        float(b1), float(b2), float(eps), float(bc1), float(bc2), float(wd), int(decoupled),
+                        ptr(hyper), stream_ptr())
+
+
+def sgd_step(p, g, vel, shadow, lr, momentum, hyper=None):
+    kernels().sgd_step(p.data_ptr(), g.data_ptr(), ptr(vel), ptr(shadow), p.numel(), float(lr), float(momentum),
+                       ptr(hyper), stream_ptr())
+
+
+def cast_bf16(src, dst):
+    kernels().cast_f32_bf16(src.data_ptr(), dst.data_ptr(), src.numel(), stream_ptr())
+
+
+def im2col(x, kh, kw, sh, sw, ph, pw):
+    N, C, H, W = x.shape
+    OH, OW = conv_out_hw(H, W, kh, kw, sh, sw, ph, pw)
+    x = x.contiguous().float()
+    col = torch.empty((C * kh * kw, N * OH * OW), dtype=F32, device=x.device)
+    kernels().im2col(x.data_ptr(), col.data_ptr(), N, C, H, W, kh, kw, sh, sw, ph, pw, OH, OW, stream_ptr())
+    return col
+
+
+def col2im(col, x_shape, kh, kw, sh, sw, ph, pw):
+    N, C, H, W = x_shape
+    OH, OW = conv_out_hw(H, W, kh, kw, sh, sw, ph, pw)
+    x = torch.empty((N, C, H, W), dtype=F32, device=col.device)
+    kernels().col2im(col.contiguous().data_ptr(), x.data_ptr(), N, C, H, W, kh, kw, sh, sw, ph, pw, OH, OW,
+                     stream_ptr())
+    return x

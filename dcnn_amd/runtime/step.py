@@ -1,0 +1,138 @@
+"""One training step, optionally captured as hipGraphs.
+
+Instead of a tracing compiler the whole per-step launch sequence (input layout conversion,
+~150 HIP kernels of forward/backward, fused loss, fused optimizer) is captured once with
+``torch.cuda.graph`` and replayed, removing host launch overhead.
+
+Data-parallel runs are captured in *segments* split at the gradient-bucket fire points of
+:class:`~dcnn_amd.parallel.dp.DataParallel`: between two segment replays the host enqueues
+the asynchronous RCCL all-reduce of the bucket just completed, so communication still
+overlaps the remaining backward segments while no collective is ever captured into a graph.
+The optimizer's step scalars are uploaded to device memory before each replay
+(``Optimizer.prepare_step``), so replays use the current learning rate / bias corrections.
+"""
+from __future__ import annotations
+
+from typing import List, Optional
+
+import torch
+import torch.distributed as dist
+
+
+class TrainStep:
+    def __init__(self, dp, loss_fn, optimizer, use_graph: bool = False):
+        from ..parallel.dp import DataParallel
+        if not isinstance(dp, DataParallel):
+            dp = DataParallel(dp, broadcast=False)
+        self.dp = dp
+        self.model = dp.model
+        self.loss_fn = loss_fn
+        self.opt = optimizer
+        self.use_graph = use_graph
+        self.graphs: Optional[List[torch.cuda.CUDAGraph]] = None
+        self.last_loss = None
+        self.last_correct = None
+        self._static_x = self._static_y = None
+
+    # ------------------------------------------------------------------ eager
+    def eager(self, x, y):
+        self.opt.clear_gradients()
+        out = self.dp.forward(x)
+        loss, grad, correct = self.loss_fn.loss_and_grad(out, y)
+        self.dp.backward(grad)
+        self.opt.update()
+        self.last_loss, self.last_correct = loss, correct
+        return loss
+
+    # ------------------------------------------------------------------ graph
+    def _segments(self):
+        """Backward layer ranges [hi..lo] ending at each bucket fire point (descending)."""
+        L = len(self.model.layers)
+        fires = sorted(self.dp.fire.keys(), reverse=True) if self.dp.world > 1 else []
+        segs = []
+        hi = L - 1
+        for f in fires:
+            segs.append((hi, f))
+            hi = f - 1
+        if hi >= 0:
+            segs.append((hi, 0))
+        return segs, fires
+
+    def _run_bwd(self, cur, hi, lo):
+        layers = self.model.layers
+        for i in range(hi, lo - 1, -1):
+            cur = layers[i].backward(cur, 0)
+        return cur
+
+    def _capture(self, x, y):
+        self._static_x = x.clone()
+        self._static_y = y.clone()
+        # warm up on a side stream (allocator pools, lazy init) as torch.cuda.graph requires
+        s = torch.cuda.Stream()
+        s.wait_stream(torch.cuda.current_stream())
+        with torch.cuda.stream(s):
+            for _ in range(2):
+                self.eager(self._static_x, self._static_y)
+        torch.cuda.current_stream().wait_stream(s)
+        torch.cuda.synchronize()
+        segs, fires = self._segments()
+        self._segs, self._fires = segs, fires
+        self.graphs = []
+        pool = None
+        fused_opt = hasattr(self.opt, "fused") and self.opt.fused()
+        if not fused_opt:
+            raise RuntimeError("graph capture needs the fused flat-buffer optimizer on the GPU")
+        self.opt.prepare_step()  # upload scalars used during capture (replays re-upload)
+        if hasattr(self.opt, "t"):
+            self.opt.t -= 1  # the capture itself is not a training step
+        world = self.dp.world
+        for k, (hi, lo) in enumerate(segs):
+            g = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(g, pool=pool):
+                if k == 0:
+                    self.opt.clear_gradients()
+                    out = self.dp.forward(self._static_x)
+                    loss, grad, correct = self.loss_fn.loss_and_grad(out, self._static_y)
+                    self._g_loss, self._g_correct = loss, correct
+                    cur = grad * (1.0 / world) if world > 1 else grad
+                else:
+                    cur = self._carry
+                cur = self._run_bwd(cur, hi, lo)
+                self._carry = cur
+                if world == 1 and k == len(segs) - 1:
+                    self.opt.launch_step()
+            if pool is None:
+                pool = g.pool()
+            self.graphs.append(g)
+        if world > 1:
+            g = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(g, pool=pool):
+                self.opt.launch_step()
+            self.graphs.append(g)
+        torch.cuda.synchronize()
+
+    def replay(self, x, y):
+        self._static_x.copy_(x, non_blocking=True)
+        self._static_y.copy_(y, non_blocking=True)
+        self.opt.prepare_step()
+        world = self.dp.world
+        flat = self.model.arena.grad
+        works = []
+        for k, (hi, lo) in enumerate(self._segs):
+            self.graphs[k].replay()
+            if world > 1 and k < len(self._fires):
+                a, b = self.dp.fire[self._fires[k]]
+                works.append(dist.all_reduce(flat[a:b], op=dist.ReduceOp.SUM, group=self.dp.pg, async_op=True))
+        if world > 1:
+            for w in works:
+                w.wait()
+            self.graphs[-1].replay()
+        self.last_loss, self.last_correct = self._g_loss, self._g_correct
+        return self.last_loss
+
+    def __call__(self, x, y):
+        if not self.use_graph:
+            return self.eager(x, y)
+        if self.graphs is None:
+            self._capture(x, y)
+        return self.replay(x, y)

@@ -1,0 +1,248 @@
+"""Numerics of every HIP kernel against a plain PyTorch fp32 reference of the same op
+(reference test strategy: `unit_tests/cuda_*_test.cpp`, `layer_device_agnosticity_test.cpp`).
+"""
+import math
+
+import pytest
+import torch
+import torch.nn.functional as F
+
+pytestmark = pytest.mark.gpu
+
+CL = torch.channels_last
+
+
+def rel_err(a, b):
+    a = a.float().cpu()
+    b = b.float().cpu()
+    return ((a - b).norm() / (b.norm() + 1e-12)).item()
+
+
+def bf(x):
+    return x.to(torch.bfloat16).float()
+
+
+@pytest.fixture(scope="module")
+def hip():
+    from dcnn_amd.ops import hip as h
+    from dcnn_amd.ops._ext import kernels
+    assert kernels().arch == "gfx950"
+    return h
+
+
+CONV_CASES = [
+    # N, Ci, H, W, Co, k, s, p
+    (2, 32, 16, 16, 64, 3, 1, 1),
+    (2, 64, 16, 16, 64, 3, 1, 1),
+    (2, 64, 16, 16, 128, 3, 2, 1),
+    (2, 64, 8, 8, 128, 1, 2, 0),
+    (2, 3, 16, 16, 32, 3, 1, 1),
+    (4, 512, 4, 4, 512, 3, 1, 1),
+    (2, 128, 9, 9, 64, 3, 1, 1),
+    (3, 64, 7, 5, 96, 3, 1, 1),
+    (2, 256, 8, 8, 256, 1, 1, 0),
+]
+
+
+@pytest.mark.parametrize("case", CONV_CASES)
+def test_conv_fwd_dgrad_wgrad(hip, case):
+    N, Ci, H, W, Co, k, s, p = case
+    torch.manual_seed(0)
+    x = torch.randn(N, Ci, H, W)
+    w = torch.randn(Co, Ci, k, k) / math.sqrt(Ci * k * k)
+    b = torch.randn(Co)
+    xb, wb = bf(x), bf(w)
+    y_ref = F.conv2d(xb, wb, b, s, p)
+    xg = x.cuda().to(torch.bfloat16).contiguous(memory_format=CL)
+    wg = w.cuda().to(torch.bfloat16).contiguous(memory_format=CL)
+    y, partial = hip.conv2d_fwd(xg, wg, b.cuda(), (s, s), (p, p), stats=True)
+    assert y.shape == y_ref.shape
+    assert rel_err(y, y_ref) < 1e-2, rel_err(y, y_ref)
+    # BN statistics from the epilogue
+    sums = hip.bn_stats(y, partial)
+    yf = y.float()
+    assert rel_err(sums[:Co], yf.sum((0, 2, 3))) < 1e-3
+    assert rel_err(sums[Co:], (yf * yf).sum((0, 2, 3))) < 1e-3
+    # dgrad
+    dy = torch.randn_like(y_ref)
+    dyb = bf(dy)
+    dx_ref = torch.nn.grad.conv2d_input(x.shape, wb, dyb, s, p)
+    dyg = dy.cuda().to(torch.bfloat16).contiguous(memory_format=CL)
+    wt = hip.conv_weight_t(wg)
+    dx = hip.conv2d_dgrad(dyg, wt, x.shape, (s, s), (p, p))
+    assert rel_err(dx, dx_ref) < 1e-2, rel_err(dx, dx_ref)
+    # dgrad + fused residual
+    r = torch.randn_like(x).cuda().to(torch.bfloat16).contiguous(memory_format=CL)
+    dx2 = hip.conv2d_dgrad(dyg, wt, x.shape, (s, s), (p, p), residual=r)
+    assert rel_err(dx2, dx_ref + r.float().cpu()) < 1e-2
+    # wgrad (accumulates into existing gradient) + bias grad
+    gw = torch.ones(Co, Ci, k, k, device="cuda").contiguous(memory_format=CL)
+    gb = torch.ones(Co, device="cuda")
+    hip.conv2d_wgrad(dyg, xg, w.shape, (s, s), (p, p), gw, gb)
+    dw_ref = torch.nn.grad.conv2d_weight(xb, w.shape, dyb, s, p) + 1
+    assert rel_err(gw, dw_ref) < 1e-2, rel_err(gw, dw_ref)
+    assert rel_err(gb, dyb.sum((0, 2, 3)) + 1) < 1e-2
+
+
+@pytest.mark.parametrize("shape", [(128, 512, 200), (64, 256, 10), (16, 192, 10), (256, 1024, 200)])
+def test_dense(hip, shape):
+    N, In, Out = shape
+    torch.manual_seed(1)
+    x, w, b = torch.randn(N, In), torch.randn(Out, In) / math.sqrt(In), torch.randn(Out)
+    y = hip.dense_fwd(x.cuda().bfloat16(), w.cuda().bfloat16(), b.cuda())
+    assert rel_err(y, bf(x) @ bf(w).t() + b) < 1e-2
+    dy = torch.randn(N, Out)
+    wt = hip.conv_weight_t(w.cuda().bfloat16().view(Out, In, 1, 1)).view(In, Out)
+    dx = hip.dense_dgrad(dy.cuda().bfloat16(), wt)
+    assert rel_err(dx, bf(dy) @ bf(w)) < 1e-2
+    gw = torch.zeros(Out, In, device="cuda")
+    gb = torch.zeros(Out, device="cuda")
+    hip.dense_wgrad(dy.cuda().bfloat16(), x.cuda().bfloat16(), gw, gb)
+    assert rel_err(gw, bf(dy).t() @ bf(x)) < 1e-2
+    assert rel_err(gb, bf(dy).sum(0)) < 1e-2
+
+
+@pytest.mark.parametrize("C", [32, 64, 512, 12])
+@pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float32])
+def test_batchnorm_fused(hip, C, dtype):
+    torch.manual_seed(2)
+    N, H, W = 4, 8, 8
+    x = torch.randn(N, C, H, W) * 2 + 0.5
+    g, bt = torch.rand(C) + 0.5, torch.randn(C)
+    r = torch.randn(N, C, H, W)
+    xg = x.cuda().to(dtype).contiguous(memory_format=CL)
+    rg = r.cuda().to(dtype).contiguous(memory_format=CL)
+    sums = hip.bn_stats(xg)
+    mean = torch.empty(C, device="cuda")
+    istd = torch.empty(C, device="cuda")
+    rm, rv = torch.zeros(C, device="cuda"), torch.ones(C, device="cuda")
+    y = hip.bn_apply(xg, sums, N * H * W, g.cuda(), bt.cuda(), 1e-5, residual=rg, relu=True, save=(mean, istd),
+                     running=(rm, rv), momentum=0.1)
+    xf = xg.float().cpu()
+    mu = xf.mean((0, 2, 3))
+    var = xf.var((0, 2, 3), unbiased=False)
+    ref = torch.relu((xf - mu.view(1, -1, 1, 1)) / torch.sqrt(var.view(1, -1, 1, 1) + 1e-5) * g.view(1, -1, 1, 1)
+                     + bt.view(1, -1, 1, 1) + rg.float().cpu())
+    tol = 2e-2 if dtype == torch.bfloat16 else 1e-4
+    assert rel_err(y, ref) < tol
+    assert rel_err(rm, 0.1 * mu) < 1e-3
+    n = N * H * W
+    assert rel_err(rv, 0.9 + 0.1 * var * n / (n - 1)) < 1e-3
+    # backward with fused relu mask, accumulate dgamma/dbeta
+    dy = torch.randn(N, C, H, W)
+    dyg = dy.cuda().to(dtype).contiguous(memory_format=CL)
+    dg, db = torch.ones(C, device="cuda"), torch.ones(C, device="cuda")
+    dx, dmask = hip.bn_backward(dyg, xg, y, mean, istd, g.cuda(), dg, db, want_masked=True)
+    xr = xf.clone().requires_grad_(True)
+    gr = g.clone().requires_grad_(True)
+    br = bt.clone().requires_grad_(True)
+    out = torch.relu(F.batch_norm(xr, None, None, gr, br, True, 0.0, 1e-5) + rg.float().cpu())
+    out.backward(dyg.float().cpu())
+    assert rel_err(dx, xr.grad) < (3e-2 if dtype == torch.bfloat16 else 1e-3)
+    assert rel_err(dg - 1, gr.grad) < 2e-2
+    assert rel_err(db - 1, br.grad) < 2e-2
+    assert rel_err(dmask, dyg.float().cpu() * (y.float().cpu() > 0)) < 1e-6
+
+
+def test_pools_and_act(hip):
+    torch.manual_seed(3)
+    x = torch.randn(2, 32, 16, 16)
+    xg = x.cuda().bfloat16().contiguous(memory_format=CL)
+    xb = bf(x)
+    for (ph, pw, sh, sw, pdh, pdw) in [(2, 2, 2, 2, 0, 0), (3, 3, 2, 2, 1, 1), (3, 3, 3, 3, 0, 0)]:
+        y, idx = hip.maxpool_fwd(xg, ph, pw, sh, sw, pdh, pdw)
+        yr, ir = F.max_pool2d(xb.requires_grad_(True), (ph, pw), (sh, sw), (pdh, pdw), return_indices=True)
+        assert rel_err(y, yr) < 1e-6
+        dy = torch.randn_like(yr)
+        dx = hip.maxpool_bwd(dy.cuda().bfloat16().contiguous(memory_format=CL), idx, x.shape, ph, pw, sh, sw, pdh, pdw)
+        xb.grad = None
+        yr.backward(bf(dy))
+        assert rel_err(dx, xb.grad) < 1e-2
+        xb = bf(x)
+        a = hip.avgpool_fwd(xg, ph, pw, sh, sw, pdh, pdw)
+        ar = F.avg_pool2d(bf(x), (ph, pw), (sh, sw), (pdh, pdw), count_include_pad=True)
+        assert rel_err(a, ar) < 1e-2
+    # global average pool (4x4 -> 1x1) fwd/bwd
+    x4 = torch.randn(3, 64, 4, 4)
+    x4g = x4.cuda().bfloat16().contiguous(memory_format=CL)
+    a = hip.avgpool_fwd(x4g, 4, 4, 1, 1, 0, 0)
+    assert rel_err(a, bf(x4).mean((2, 3), keepdim=True)) < 1e-2
+    d = hip.avgpool_bwd(torch.ones(3, 64, 1, 1, device="cuda", dtype=torch.bfloat16), x4.shape, 4, 4, 1, 1, 0, 0)
+    assert torch.allclose(d.float(), torch.full_like(d.float(), 1 / 16))
+    for kind in ["relu", "leaky_relu", "elu", "sigmoid", "tanh"]:
+        from dcnn_amd.nn.activations import ActivationFactory
+        fn = ActivationFactory.create(kind)
+        xf = torch.randn(1000)
+        yg = fn.apply(xf.cuda())
+        assert rel_err(yg, fn.apply(xf)) < 1e-5
+        gg = fn.gradient(xf.cuda(), yg, torch.ones(1000, device="cuda"))
+        assert rel_err(gg, fn.gradient(xf, fn.apply(xf), torch.ones(1000))) < 1e-5
+    s = hip.softmax_channels(xg)
+    assert rel_err(s, torch.softmax(bf(x), 1)) < 1e-2
+
+
+@pytest.mark.parametrize("kind", ["softmax_crossentropy", "logsoftmax_crossentropy", "crossentropy", "mse", "mae",
+                                  "huber"])
+def test_loss_fused(kind):
+    from dcnn_amd.nn.loss import LossFactory
+    torch.manual_seed(4)
+    L = LossFactory.create(kind)
+    p = torch.randn(64, 200, 1, 1)
+    if kind == "crossentropy":
+        p = torch.softmax(p, 1)
+    lab = torch.randint(0, 200, (64,))
+    t = F.one_hot(lab, 200).float().view(64, 200, 1, 1)
+    lc, gc, cc = L.loss_and_grad(p, t)
+    lg, gg, cg = L.loss_and_grad(p.cuda(), t.cuda())
+    assert abs(lg.item() - lc.item()) < 1e-4 * max(1, abs(lc.item()))
+    assert rel_err(gg, gc) < 1e-4
+    assert cg.item() == cc.item()
+    lg2, gg2, cg2 = L.loss_and_grad(p.cuda(), lab.cuda())
+    assert abs(lg2.item() - lc.item()) < 1e-4 * max(1, abs(lc.item()))
+
+
+def test_adam_sgd_flat():
+    from dcnn_amd.nn.params import ParamArena, ParamSpec
+    from dcnn_amd.nn.optimizers import SGD, Adam
+    for make in [lambda: Adam(1e-2, weight_decay=0.01), lambda: Adam(1e-2, weight_decay=0.01, decouple_weight_decay=True),
+                 lambda: SGD(0.1, 0.9), lambda: SGD(0.1)]:
+        res = []
+        for dev in ["cpu", "cuda"]:
+            torch.manual_seed(5)
+            specs = [ParamSpec("a", (7, 3, 3, 3), True), ParamSpec("b", (7, 1, 1, 1))]
+            ar = ParamArena(specs, torch.device(dev), torch.bfloat16 if dev == "cuda" else None)
+            ar.param(0).copy_(torch.randn(7, 3, 3, 3))
+            ar.param(1).copy_(torch.randn(7, 1, 1, 1))
+            ar.sync_shadow(force=True)
+            opt = make()
+            opt.attach([ar.param(0), ar.param(1)], [ar.grad_view(0), ar.grad_view(1)], ar)
+            assert opt.arena is not None
+            for it in range(3):
+                ar.grad_view(0).copy_(torch.randn(7, 3, 3, 3))
+                ar.grad_view(1).copy_(torch.randn(7, 1, 1, 1))
+                opt.update()
+            res.append((ar.param(0).cpu().clone(), ar))
+        assert rel_err(res[1][0], res[0][0]) < 1e-5
+        ar = res[1][1]
+        assert rel_err(ar.shadow_view(0).float(), ar.param(0)) < 1e-2
+
+
+def test_im2col_col2im(hip):
+    x = torch.randn(2, 3, 7, 7)
+    col = hip.im2col(x.cuda(), 3, 3, 2, 2, 1, 1)
+    ref = F.unfold(x, 3, padding=1, stride=2)  # [N, C*9, L]
+    ref = ref.permute(1, 0, 2).reshape(27, -1)
+    assert rel_err(col, ref) < 1e-6
+    back = hip.col2im(col, x.shape, 3, 3, 2, 2, 1, 1)
+    ref2 = F.fold(F.unfold(x, 3, padding=1, stride=2), (7, 7), 3, padding=1, stride=2)
+    assert rel_err(back, ref2) < 1e-6
+
+
+def test_dropout_regenerates_mask(hip):
+    x = torch.ones(10000, device="cuda")
+    y = hip.dropout(x, 0.3, 1234)
+    keep = (y > 0).float().mean().item()
+    assert abs(keep - 0.7) < 0.03
+    assert torch.allclose(y[y > 0], torch.full_like(y[y > 0], 1 / 0.7))
+    g = hip.dropout(torch.ones(10000, device="cuda"), 0.3, 1234)
+    assert torch.equal(g > 0, y > 0)

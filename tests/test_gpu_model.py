@@ -1,0 +1,124 @@
+"""Model-level GPU tests: GPU(bf16, fused) vs CPU(fp32 reference) forward/backward, hipGraph
+replay == eager, and training makes progress (reference: layer_device_agnosticity_test.cpp)."""
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+
+def rel(a, b):
+    a, b = a.float().cpu(), b.float().cpu()
+    return ((a - b).norm() / (b.norm() + 1e-12)).item()
+
+
+def bf16_emulate(model):
+    """Round params and every conv/dense/BN input+output (fwd and bwd) to bf16 on the CPU, so
+    the reference sees the same quantisation points as the GPU kernels."""
+    from dcnn_amd.nn.layers import BatchNorm, Conv2D, Dense, ResidualBlock
+    with torch.no_grad():
+        for p in model.parameters():
+            p.copy_(p.bfloat16().float())
+
+    def r(t):
+        return None if t is None else t.bfloat16().float()
+
+    def wrap(l):
+        f, b = l.forward, l.backward
+        l.forward = lambda x, mb=0, **kw: r(f(r(x), mb, **{k: (r(v) if torch.is_tensor(v) else v) for k, v in kw.items()}))
+        l.backward = lambda g, mb=0, **kw: r(b(r(g), mb, **{k: (r(v) if torch.is_tensor(v) else v) for k, v in kw.items()}))
+
+    def walk(ls):
+        for l in ls:
+            if isinstance(l, ResidualBlock):
+                walk(l.sublayers())
+            elif isinstance(l, (Conv2D, Dense, BatchNorm)):
+                wrap(l)
+    walk(model.layers)
+    return model
+
+
+@pytest.mark.parametrize("name,fwd_tol", [("resnet18_tiny_imagenet", 0.02), ("mnist_cnn", 0.02),
+                                          ("cifar10_cnn_v1", 0.02), ("resnet50_tiny_imagenet", 0.08)])
+def test_gpu_vs_cpu_model(name, fwd_tol):
+    from dcnn_amd.models import INPUT_SHAPES, NUM_CLASSES, create_model
+    from dcnn_amd.nn import LossFactory
+    torch.manual_seed(0)
+    C, H, W = INPUT_SHAPES[name]
+    B = 16
+    x = torch.randn(B, C, H, W)
+    y = torch.randint(0, NUM_CLASSES[name], (B,))
+    cpu = create_model(name)
+    cpu.set_seed(3)
+    cpu.initialize()
+    gpu = create_model(name)
+    gpu.set_seed(3)
+    gpu.set_device("GPU:0")
+    gpu.initialize()
+    for a, b in zip(cpu.parameters(), gpu.parameters()):
+        assert torch.equal(a, b.cpu())
+    bf16_emulate(cpu)
+    lf = LossFactory.create("softmax_crossentropy")
+    oc = cpu.forward(x)
+    og = gpu.forward(x.cuda())
+    assert rel(og, oc) < fwd_tol, rel(og, oc)
+    _, gc, _ = lf.loss_and_grad(oc, y)
+    _, gg, _ = lf.loss_and_grad(og, y.cuda())
+    cpu.backward(gc)
+    gpu.backward(gg)
+    errs = [rel(b, a) for a, b in zip(cpu.gradients(), gpu.gradients()) if a.norm() > 1e-6]
+    errs.sort()
+    assert errs[len(errs) // 2] < 0.05, errs
+    assert errs[int(len(errs) * 0.9)] < 0.2, errs
+
+
+def _make(seed=5):
+    from dcnn_amd.models import create_model
+    from dcnn_amd.nn import Adam, LossFactory
+    m = create_model("resnet18_tiny_imagenet")
+    m.set_seed(seed)
+    m.set_device("GPU:0")
+    m.initialize()
+    m.set_first_layer_input_grad(False)
+    opt = Adam(1e-3)
+    opt.attach(m)
+    return m, opt, LossFactory.create("softmax_crossentropy")
+
+
+def test_graph_replay_matches_eager():
+    """Graph capture runs 2 eager warm-up steps on the first batch before its first replay; the
+    eager run replays the same step sequence so both trajectories must agree."""
+    from dcnn_amd.runtime.step import TrainStep
+    torch.manual_seed(1)
+    xs = [torch.randn(32, 3, 64, 64, device="cuda") for _ in range(2)]
+    ys = [torch.randint(0, 200, (32,), device="cuda") for _ in range(2)]
+    order = [0, 1, 0, 1, 0, 1]
+    m, opt, lf = _make()
+    st = TrainStep(m, lf, opt, use_graph=False)
+    eager = []
+    for i in [0, 0] + order:
+        st(xs[i], ys[i])
+        eager.append(float(st.last_loss.item()))
+    m2, opt2, lf2 = _make()
+    st2 = TrainStep(m2, lf2, opt2, use_graph=True)
+    graph = []
+    for i in order:
+        st2(xs[i], ys[i])
+        graph.append(float(st2.last_loss.item()))
+    assert st2.graphs is not None and opt2.t == opt.t
+    for a, b in zip(eager[2:], graph):
+        assert abs(a - b) < 0.05 * abs(a) + 0.05, (eager, graph)
+    assert rel(m2.arena.data, m.arena.data) < 0.02
+
+
+def test_training_decreases_loss():
+    from dcnn_amd.runtime.step import TrainStep
+    torch.manual_seed(2)
+    x = torch.randn(64, 3, 64, 64, device="cuda")
+    y = torch.randint(0, 200, (64,), device="cuda")
+    m, opt, lf = _make(7)
+    st = TrainStep(m, lf, opt, use_graph=False)
+    first = float(st(x, y).item())
+    for _ in range(15):
+        st(x, y)
+    last = float(st.last_loss.item())
+    assert last < first * 0.5, (first, last)
