@@ -15,9 +15,29 @@ struct TnArgs {
   const bf16* dY; const bf16* X; float* slab; float* bias_slab;
   int M, N, P; int mode; int nb, sh, sw, cs, gh, gw; int kh, kw, strh, strw, padh, padw; int ldx; int k_per_split;
 };
+struct G2Args {
+  const bf16* A; const bf16* B; bf16* C;
+  unsigned a_bytes, b_bytes;
+  int M, N, Cs, H, W, GH, GW, SY, SX, ntaps;
+  int tap_dy[64], tap_dx[64], tap_srcoff[64], tap_b[64];
+  int ldb, ldc;
+  int OH, OW, OSY, OSX, ORY, ORX;
+  const float* bias; const bf16* residual; float* stats; int relu;
+};
+struct T2Args {
+  const bf16* dY; const bf16* X; float* slab; float* bias_slab;
+  unsigned a_bytes, b_bytes;
+  int M, N, P, ldy, Cs, H, W, GH, GW, SY, SX, ntaps;
+  int tap_dy[64], tap_dx[64];
+  int k_per_split;
+};
 struct PoolGeom { int N, H, W, C, OH, OW, ph, pw, sh, sw, padh, padw; };
 
 void gemm_nt(const NtArgs& a, hipStream_t s);
+void gemm_g2(const G2Args& a, hipStream_t s);
+int gemm_g2_stat_rows(int M, int N);
+void gemm_t2(T2Args a, int splits, hipStream_t s);
+int gemm_t2_splits(int M, int N, int P);
 int gemm_nt_stat_rows(int M, int N);
 void gemm_tn(TnArgs a, int splits, hipStream_t s);
 int gemm_tn_splits(int M, int N, int P);
@@ -48,6 +68,7 @@ void softmax_rows(int dt, const void* x, void* y, long rows, int C, hipStream_t 
 void softmax_rows_bwd(int dt, const void* y, const void* dy, void* dx, long rows, int C, hipStream_t s);
 void dropout(int dt, const void* x, void* y, long n, float p, uint64_t seed, hipStream_t s);
 void nchw_to_nhwc(int dt, const float* x, void* y, int N, int C, int HW, hipStream_t s);
+void nchw_to_nhwc_pad(int dt, const float* x, void* y, int N, int C, int Cp, int HW, hipStream_t s);
 void conv_weight_transpose(int src_dt, const void* w, bf16* wt, int Co, int T_, int Ci, hipStream_t s);
 void cast_f32_bf16(const float* x, bf16* y, long n, hipStream_t s);
 void im2col(const float* x, float* col, int N, int C, int H, int W, int KH, int KW, int SH, int SW, int PH, int PW,

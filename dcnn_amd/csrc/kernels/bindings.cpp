@@ -3,6 +3,9 @@
 // stream, so launches land on whatever stream PyTorch-ROCm is using (including a stream
 // under hipGraph capture). No torch headers, no hipify: plain HIP + pybind11.
 #include <pybind11/pybind11.h>
+#include <pybind11/stl.h>
+#include <array>
+#include <vector>
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
@@ -29,6 +32,39 @@ PYBIND11_MODULE(_kernels, m) {
           gemm_nt(a, S(stream));
         });
   m.def("gemm_nt_stat_rows", &gemm_nt_stat_rows);
+  m.def("gemm_g2",
+        [](uintptr_t A, uintptr_t B, uintptr_t C, unsigned a_bytes, unsigned b_bytes, int M, int N, int Cs, int H,
+           int W, int GH, int GW, int SY, int SX, std::vector<std::array<int, 4>> taps, int ldb, int ldc, int OH,
+           int OW, int OSY, int OSX, int ORY, int ORX, uintptr_t bias, uintptr_t residual, uintptr_t stats, int relu,
+           uintptr_t stream) {
+          G2Args a{};
+          a.A = P<const bf16*>(A); a.B = P<const bf16*>(B); a.C = P<bf16*>(C);
+          a.a_bytes = a_bytes; a.b_bytes = b_bytes;
+          a.M = M; a.N = N; a.Cs = Cs; a.H = H; a.W = W; a.GH = GH; a.GW = GW; a.SY = SY; a.SX = SX;
+          if (taps.size() > 64) throw std::runtime_error("gemm_g2: more than 64 taps");
+          a.ntaps = (int)taps.size();
+          for (size_t i = 0; i < taps.size(); ++i) {
+            a.tap_dy[i] = taps[i][0]; a.tap_dx[i] = taps[i][1]; a.tap_srcoff[i] = taps[i][2]; a.tap_b[i] = taps[i][3];
+          }
+          a.ldb = ldb; a.ldc = ldc; a.OH = OH; a.OW = OW; a.OSY = OSY; a.OSX = OSX; a.ORY = ORY; a.ORX = ORX;
+          a.bias = P<const float*>(bias); a.residual = P<const bf16*>(residual); a.stats = P<float*>(stats); a.relu = relu;
+          gemm_g2(a, S(stream));
+        });
+  m.def("gemm_g2_stat_rows", &gemm_g2_stat_rows);
+  m.def("gemm_t2",
+        [](uintptr_t dY, uintptr_t X, uintptr_t slab, uintptr_t bias_slab, unsigned a_bytes, unsigned b_bytes, int M,
+           int N, int Pn, int ldy, int Cs, int H, int W, int GH, int GW, int SY, int SX,
+           std::vector<std::array<int, 2>> taps, int splits, uintptr_t stream) {
+          T2Args a{};
+          a.dY = P<const bf16*>(dY); a.X = P<const bf16*>(X); a.slab = P<float*>(slab); a.bias_slab = P<float*>(bias_slab);
+          a.a_bytes = a_bytes; a.b_bytes = b_bytes; a.M = M; a.N = N; a.P = Pn; a.ldy = ldy; a.Cs = Cs;
+          a.H = H; a.W = W; a.GH = GH; a.GW = GW; a.SY = SY; a.SX = SX;
+          if (taps.size() > 64) throw std::runtime_error("gemm_t2: more than 64 taps");
+          a.ntaps = (int)taps.size();
+          for (size_t i = 0; i < taps.size(); ++i) { a.tap_dy[i] = taps[i][0]; a.tap_dx[i] = taps[i][1]; }
+          gemm_t2(a, splits, S(stream));
+        });
+  m.def("gemm_t2_splits", &gemm_t2_splits);
   m.def("gemm_tn",
         [](uintptr_t dY, uintptr_t X, uintptr_t slab, uintptr_t bias_slab, int M, int N, int Pn, int mode, int nb,
            int sh, int sw, int cs, int gh, int gw, int kh, int kw, int strh, int strw, int padh, int padw, int ldx,
@@ -115,6 +151,9 @@ PYBIND11_MODULE(_kernels, m) {
   });
   m.def("nchw_to_nhwc", [](int dt, uintptr_t x, uintptr_t y, int N, int C, int HW, uintptr_t st) {
     nchw_to_nhwc(dt, P<const float*>(x), P<void*>(y), N, C, HW, S(st));
+  });
+  m.def("nchw_to_nhwc_pad", [](int dt, uintptr_t x, uintptr_t y, int N, int C, int Cp, int HW, uintptr_t st) {
+    nchw_to_nhwc_pad(dt, P<const float*>(x), P<void*>(y), N, C, Cp, HW, S(st));
   });
   m.def("conv_weight_transpose", [](int dt, uintptr_t w, uintptr_t wt, int Co, int T_, int Ci, uintptr_t st) {
     conv_weight_transpose(dt, P<const void*>(w), P<bf16*>(wt), Co, T_, Ci, S(st));

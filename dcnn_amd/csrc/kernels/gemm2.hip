@@ -1,0 +1,525 @@
+// Implicit-GEMM convolution v2 for CDNA4 (gfx950): direct-to-LDS gather + MFMA 16x16x32 bf16.
+//
+// One generic "gathered NT GEMM" covers conv forward, conv dgrad (phase-decomposed for strided
+// convs so no MFMA work is spent on structurally-zero taps) and dense layers:
+//
+//   C[m][n] = sum_{t < ntaps, c < Cs} Src[img(m), gy(m)*SY + dy[t], gx(m)*SX + dx[t], c] * B[n][tapB[t] + c]
+//
+// * Src is an NHWC bf16 tensor; every 16-byte chunk of a tile row is fetched with
+//   `buffer_load_dwordx4 ... lds` straight into LDS (no VGPR staging, no ds_write). Padding /
+//   out-of-image taps are handled by the buffer descriptor's range check: an invalid chunk gets an
+//   out-of-range offset and the hardware writes zeros.
+// * Per GEMM row the validity of every tap is precomputed once into a 64-bit mask, so the K loop
+//   costs ~3 VALU per 16-byte chunk (mask test, select, add).
+// * LDS tiles are XOR-swizzled through the *source* address (glds writes lane-linear), read with
+//   conflict-free ds_read_b128; 2-stage pipeline: tile k+1 in flight while tile k is multiplied.
+// * Epilogue: bias added in registers, tile staged through LDS as bf16, then 16-byte coalesced
+//   stores with fused residual add, ReLU and per-channel (sum, sum^2) BatchNorm partials; the
+//   output row mapping supports the strided scatter of a dgrad phase.
+//
+// The weight-gradient kernel (tn2) uses the same loader on both operands (pixels = K) and
+// ds_read_b64_tr_b16 transposed fragment reads; split-K partials go to an fp32 slab.
+#include "common.h"
+#include "api.h"
+
+namespace dcnn {
+
+typedef __attribute__((address_space(3))) void lds_void;
+
+__device__ __forceinline__ int xcd_remap2(int bid, int nwg) {
+  const int xcd = bid & 7, q = nwg >> 3, r = nwg & 7;
+  const int base = xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q;
+  return base + (bid >> 3);
+}
+
+__device__ __forceinline__ void glds16(__amdgpu_buffer_rsrc_t rsrc, char* lds, unsigned voff) {
+  __builtin_amdgcn_raw_ptr_buffer_load_lds(rsrc, (lds_void*)lds, 16, voff, 0, 0, 0);
+}
+
+constexpr unsigned kOOB = 0x80000000u;  // any offset >= num_records reads zeros
+
+// ---------------------------------------------------------------------------------------------
+// gathered NT GEMM
+// ---------------------------------------------------------------------------------------------
+template <int BM, int BN, int BK, bool UNI>
+struct G2 {
+  static constexpr int CPR = BK / 8;                 // 16-B chunks per LDS row
+  static constexpr int RPI = 64 / CPR;               // rows covered by one wave-instruction (1 KiB)
+  static constexpr int RPB = 256 / (BK * 2);         // rows per 256-B bank row
+  static constexpr int A_INS = BM / RPI / 4;         // glds instructions per wave for A
+  static constexpr int B_INS = BN / RPI / 4;
+  static constexpr int TM = BM / 32, TN = BN / 32;   // 16x16 subtiles per wave (2x2 waves)
+  static constexpr int STAGE = (BM + BN) * BK * 2;
+  static constexpr int EPI_PITCH = BN * 2 + 16;      // bf16 staging row pitch (bytes)
+  static constexpr int LDS = (2 * STAGE > BM * EPI_PITCH) ? 2 * STAGE : BM * EPI_PITCH;
+  __device__ static __forceinline__ int swz(int row) { return (row / RPB) % CPR; }
+  __device__ static __forceinline__ int off(int row, int ch) { return row * (BK * 2) + ((ch ^ swz(row)) << 4); }
+};
+
+template <int BM, int BN, int BK, bool UNI>
+__global__ void __launch_bounds__(256, 2) gemm_g2_kernel(G2Args p) {
+  using T = G2<BM, BN, BK, UNI>;
+  __shared__ __attribute__((aligned(16))) char smem[T::LDS];
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int wm = wid >> 1, wn = wid & 1;
+  const int tiles_n = (p.N + BN - 1) / BN;
+  const int lt = xcd_remap2(blockIdx.x, gridDim.x);
+  const int tm = lt / tiles_n, tn = lt % tiles_n;
+  const int m0 = tm * BM, n0 = tn * BN;
+
+  const __amdgpu_buffer_rsrc_t rsA = __builtin_amdgcn_make_buffer_rsrc((void*)p.A, (short)0, p.a_bytes, 0x00020000);
+  const __amdgpu_buffer_rsrc_t rsB = __builtin_amdgcn_make_buffer_rsrc((void*)p.B, (short)0, p.b_bytes, 0x00020000);
+
+  // ---- per-lane A rows: pixel base offset + tap-validity mask (fixed over the K loop) ----
+  const int ch = lane % T::CPR;           // this lane's physical chunk slot within a row
+  unsigned a_base[T::A_INS];
+  uint64_t a_mask[T::A_INS];
+  int a_lch[T::A_INS];                    // logical chunk fetched by this lane (source-side swizzle)
+#pragma unroll
+  for (int i = 0; i < T::A_INS; ++i) {
+    const int row = (wid * T::A_INS + i) * T::RPI + lane / T::CPR;
+    a_lch[i] = ch ^ T::swz(row);
+    const int m = m0 + row;
+    uint64_t mask = 0;
+    unsigned base = 0;
+    if (m < p.M) {
+      const int ghw = p.GH * p.GW;
+      const int img = m / ghw, rem = m - img * ghw;
+      const int gy = rem / p.GW, gx = rem - gy * p.GW;
+      const int y0 = gy * p.SY, x0 = gx * p.SX;
+      base = (unsigned)((((long)img * p.H + y0) * p.W + x0) * p.Cs * 2);
+      for (int t = 0; t < p.ntaps; ++t) {
+        const int sy = y0 + p.tap_dy[t], sx = x0 + p.tap_dx[t];
+        if (sy >= 0 && sy < p.H && sx >= 0 && sx < p.W) mask |= (1ull << t);
+      }
+    }
+    a_base[i] = base;
+    a_mask[i] = mask;
+  }
+  unsigned b_base[T::B_INS];
+  bool b_ok[T::B_INS];
+  int b_lch[T::B_INS];
+#pragma unroll
+  for (int i = 0; i < T::B_INS; ++i) {
+    const int row = (wid * T::B_INS + i) * T::RPI + lane / T::CPR;
+    b_lch[i] = ch ^ T::swz(row);
+    const int n = n0 + row;
+    b_ok[i] = n < p.N;
+    b_base[i] = (unsigned)((long)n * p.ldb * 2);
+  }
+
+  auto stage = [&](int buf, int k0) {
+    char* As = smem + buf * T::STAGE;
+    char* Bs = As + BM * BK * 2;
+    // tap / channel of this K-step (uniform when Cs % BK == 0)
+    int tU = 0, cU = 0;
+    if constexpr (UNI) { tU = k0 / p.Cs; cU = k0 - tU * p.Cs; }
+#pragma unroll
+    for (int i = 0; i < T::A_INS; ++i) {
+      int t, c;
+      if constexpr (UNI) { t = tU; c = cU + a_lch[i] * 8; }
+      else { const int k = k0 + a_lch[i] * 8; t = k / p.Cs; c = k - t * p.Cs; }
+      const bool ok = t < p.ntaps && c < p.Cs && ((a_mask[i] >> t) & 1ull);
+      const unsigned voff = ok ? a_base[i] + (unsigned)(p.tap_srcoff[t] * 2 + c * 2) : kOOB;
+      glds16(rsA, As + (wid * T::A_INS + i) * 1024, voff);
+    }
+#pragma unroll
+    for (int i = 0; i < T::B_INS; ++i) {
+      int t, c;
+      if constexpr (UNI) { t = tU; c = cU + b_lch[i] * 8; }
+      else { const int k = k0 + b_lch[i] * 8; t = k / p.Cs; c = k - t * p.Cs; }
+      const bool ok = b_ok[i] && t < p.ntaps && c < p.Cs;
+      const unsigned voff = ok ? b_base[i] + (unsigned)((p.tap_b[t] + c) * 2) : kOOB;
+      glds16(rsB, Bs + (wid * T::B_INS + i) * 1024, voff);
+    }
+  };
+
+  f32x4 acc[T::TM][T::TN];
+#pragma unroll
+  for (int i = 0; i < T::TM; ++i)
+#pragma unroll
+    for (int j = 0; j < T::TN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  const int K = p.ntaps * p.Cs;
+  const int nk = (K + BK - 1) / BK;
+  stage(0, 0);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  int cur = 0;
+  for (int kt = 0; kt < nk; ++kt) {
+    if (kt + 1 < nk) stage(cur ^ 1, (kt + 1) * BK);
+    const char* As = smem + cur * T::STAGE;
+    const char* Bs = As + BM * BK * 2;
+#pragma unroll
+    for (int kk = 0; kk < BK / 32; ++kk) {
+      const int c = kk * 4 + (lane >> 4);
+      bf16x8 a[T::TM], b[T::TN];
+#pragma unroll
+      for (int i = 0; i < T::TM; ++i)
+        a[i] = *reinterpret_cast<const bf16x8*>(As + T::off(wm * (BM / 2) + i * 16 + (lane & 15), c));
+#pragma unroll
+      for (int j = 0; j < T::TN; ++j)
+        b[j] = *reinterpret_cast<const bf16x8*>(Bs + T::off(wn * (BN / 2) + j * 16 + (lane & 15), c));
+      __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+      for (int i = 0; i < T::TM; ++i)
+#pragma unroll
+        for (int j = 0; j < T::TN; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[i], b[j], acc[i][j], 0, 0, 0);
+      __builtin_amdgcn_s_setprio(0);
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    cur ^= 1;
+  }
+
+  // ---- epilogue 1: acc (+bias) -> bf16 LDS tile [BM][BN] ----
+#pragma unroll
+  for (int j = 0; j < T::TN; ++j) {
+    const int col = wn * (BN / 2) + j * 16 + (lane & 15);
+    const float bv = (p.bias && n0 + col < p.N) ? p.bias[n0 + col] : 0.f;
+#pragma unroll
+    for (int i = 0; i < T::TM; ++i)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int row = wm * (BM / 2) + i * 16 + (lane >> 4) * 4 + r;
+        *reinterpret_cast<bf16*>(smem + row * T::EPI_PITCH + col * 2) = (bf16)(acc[i][j][r] + bv);
+      }
+  }
+  __syncthreads();
+  // ---- epilogue 2: 16-byte rows -> global (+residual, ReLU, BN partial stats) ----
+  constexpr int CG = BN / 8;           // column groups of 8
+  constexpr int RSTEP = 256 / CG;      // rows handled concurrently
+  const int cg = tid % CG, r0 = tid / CG;
+  const int ncol = n0 + cg * 8;
+  const bool col_ok = ncol < p.N;      // N % 8 == 0 for this kernel
+  float s[8], q[8];
+#pragma unroll
+  for (int v = 0; v < 8; ++v) s[v] = q[v] = 0.f;
+  const int ghw = p.GH * p.GW;
+  for (int row = r0; row < BM; row += RSTEP) {
+    const int m = m0 + row;
+    if (m >= p.M || !col_ok) continue;
+    const int img = m / ghw, rem = m - img * ghw;
+    const int gy = rem / p.GW, gx = rem - gy * p.GW;
+    const long orow = ((long)img * p.OH + gy * p.OSY + p.ORY) * p.OW + gx * p.OSX + p.ORX;
+    float f[8];
+    unpack8(*reinterpret_cast<const uint4*>(smem + row * T::EPI_PITCH + cg * 16), f);
+    if (p.residual) {
+      float rr[8];
+      unpack8(*reinterpret_cast<const uint4*>(p.residual + orow * p.ldc + ncol), rr);
+#pragma unroll
+      for (int v = 0; v < 8; ++v) f[v] += rr[v];
+    }
+    if (p.relu) {
+#pragma unroll
+      for (int v = 0; v < 8; ++v) f[v] = fmaxf(f[v], 0.f);
+    }
+    const uint4 o = pack8(f);
+    *reinterpret_cast<uint4*>(reinterpret_cast<bf16*>(p.C) + orow * p.ldc + ncol) = o;
+    if (p.stats) {
+      float g[8];
+      unpack8(o, g);
+#pragma unroll
+      for (int v = 0; v < 8; ++v) { s[v] += g[v]; q[v] += g[v] * g[v]; }
+    }
+  }
+  if (p.stats) {
+    __syncthreads();
+    float* red = reinterpret_cast<float*>(smem);  // [RSTEP][2][BN]
+#pragma unroll
+    for (int v = 0; v < 8; ++v) {
+      red[(r0 * 2 + 0) * BN + cg * 8 + v] = s[v];
+      red[(r0 * 2 + 1) * BN + cg * 8 + v] = q[v];
+    }
+    __syncthreads();
+    for (int c = tid; c < 2 * BN; c += 256) {
+      const int which = c / BN, cc = c % BN;
+      if (n0 + cc < p.N) {
+        float a = 0.f;
+        for (int k = 0; k < RSTEP; ++k) a += red[(k * 2 + which) * BN + cc];
+        p.stats[((long)tm * 2 + which) * p.N + n0 + cc] = a;
+      }
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------------------------
+// gathered TN GEMM (weight gradient): dW[m][n] = sum_p dY[p][m] * Xcol[p][n],  n = (tap, c)
+// ---------------------------------------------------------------------------------------------
+template <int BM, int BN>
+struct T2 {
+  static constexpr int BK = 64;                       // pixels per K-step
+  static constexpr int ACH = BM / 8, BCH = BN / 8;    // 16-B chunks per LDS row
+  static constexpr int A_RPI = 64 / ACH, B_RPI = 64 / BCH;
+  static constexpr int A_INS = BK / A_RPI / 4, B_INS = BK / B_RPI / 4;
+  static constexpr int TM = BM / 32, TN = BN / 32;
+  static constexpr int STAGE = BK * (BM + BN) * 2;
+};
+
+template <int RCH>
+__device__ __forceinline__ int tr_swz(int row) {
+  if constexpr (RCH >= 16) return ((row & 3) | (((row >> 3) & 1) << 2)) << 1;
+  else if constexpr (RCH == 8) return (((row >> 1) & 1) | (((row >> 3) & 1) << 1)) << 1;
+  else return 0;
+}
+
+template <int BM, int BN>
+__global__ void __launch_bounds__(256, 2) gemm_t2_kernel(T2Args p) {
+  using T = T2<BM, BN>;
+  constexpr int BK = T::BK;
+  __shared__ __attribute__((aligned(16))) char smem[2 * T::STAGE];
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int wm = wid >> 1, wn = wid & 1;
+  const int tiles_m = (p.M + BM - 1) / BM, tiles_n = (p.N + BN - 1) / BN;
+  const int tiles = tiles_m * tiles_n;
+  const int lt = xcd_remap2(blockIdx.x, gridDim.x);
+  const int split = lt / tiles, tt = lt % tiles;
+  const int tm = tt / tiles_n, tn = tt % tiles_n;
+  const int m0 = tm * BM, n0 = tn * BN;
+  const int kbeg = split * p.k_per_split;
+  const int kend = min(p.P, kbeg + p.k_per_split);
+
+  const __amdgpu_buffer_rsrc_t rsA = __builtin_amdgcn_make_buffer_rsrc((void*)p.dY, (short)0, p.a_bytes, 0x00020000);
+  const __amdgpu_buffer_rsrc_t rsB = __builtin_amdgcn_make_buffer_rsrc((void*)p.X, (short)0, p.b_bytes, 0x00020000);
+
+  // A lanes: fixed column chunk (m), rows = pixels
+  int a_row[T::A_INS];
+  unsigned a_col[T::A_INS];
+#pragma unroll
+  for (int i = 0; i < T::A_INS; ++i) {
+    const int row = (wid * T::A_INS + i) * T::A_RPI + lane / T::ACH;
+    const int slot = lane % T::ACH;
+    const int lch = slot ^ tr_swz<T::ACH>(row);
+    a_row[i] = row;
+    const int m = m0 + lch * 8;
+    a_col[i] = m < p.M ? (unsigned)(m * 2) : kOOB;
+  }
+  // B lanes: fixed column chunk -> (tap dy/dx, channel) fixed over the K loop
+  int b_row[T::B_INS], b_dy[T::B_INS], b_dx[T::B_INS];
+  unsigned b_coff[T::B_INS];
+  bool b_ok[T::B_INS];
+#pragma unroll
+  for (int i = 0; i < T::B_INS; ++i) {
+    const int row = (wid * T::B_INS + i) * T::B_RPI + lane / T::BCH;
+    const int slot = lane % T::BCH;
+    const int lch = slot ^ tr_swz<T::BCH>(row);
+    b_row[i] = row;
+    const int n = n0 + lch * 8;
+    const int t = n / p.Cs, c = n - t * p.Cs;
+    b_ok[i] = n < p.N && t < p.ntaps;
+    b_dy[i] = b_ok[i] ? p.tap_dy[t] : 0;
+    b_dx[i] = b_ok[i] ? p.tap_dx[t] : 0;
+    b_coff[i] = (unsigned)(c * 2);
+  }
+  const int ghw = p.GH * p.GW;
+  const float inv_ghw = 1.f / (float)ghw, inv_gw = 1.f / (float)p.GW;
+
+  auto stage = [&](int buf, int k0) {
+    char* As = smem + buf * T::STAGE;
+    char* Bs = As + BK * BM * 2;
+#pragma unroll
+    for (int i = 0; i < T::A_INS; ++i) {
+      const int pix = k0 + a_row[i];
+      const unsigned voff = (pix < kend && a_col[i] != kOOB) ? (unsigned)(pix * p.ldy * 2) + a_col[i] : kOOB;
+      glds16(rsA, As + (wid * T::A_INS + i) * 1024, voff);
+    }
+#pragma unroll
+    for (int i = 0; i < T::B_INS; ++i) {
+      const int pix = k0 + b_row[i];
+      // pix -> (img, gy, gx) with a float reciprocal + exact integer correction
+      int img = (int)((float)pix * inv_ghw);
+      int rem = pix - img * ghw;
+      if (rem < 0) { img--; rem += ghw; } else if (rem >= ghw) { img++; rem -= ghw; }
+      int gy = (int)((float)rem * inv_gw);
+      int gx = rem - gy * p.GW;
+      if (gx < 0) { gy--; gx += p.GW; } else if (gx >= p.GW) { gy++; gx -= p.GW; }
+      const int sy = gy * p.SY + b_dy[i], sx = gx * p.SX + b_dx[i];
+      const bool ok = b_ok[i] && pix < kend && sy >= 0 && sy < p.H && sx >= 0 && sx < p.W;
+      const unsigned voff = ok ? (unsigned)((((long)img * p.H + sy) * p.W + sx) * p.Cs * 2) + b_coff[i] : kOOB;
+      glds16(rsB, Bs + (wid * T::B_INS + i) * 1024, voff);
+    }
+  };
+  auto tr_read = [&](const char* base, int rowbytes, int krow, int col0, auto rch) -> bf16x4 {
+    constexpr int RCH = decltype(rch)::value;
+    const int i = lane & 15, q = i >> 2, pp = i & 3;
+    const int row = krow + q;
+    const int col = col0 + 4 * pp;
+    const int chn = col >> 3, within = (col & 7) * 2;
+    const char* addr = base + row * rowbytes + ((chn ^ tr_swz<RCH>(row)) << 4) + within;
+    return __builtin_amdgcn_ds_read_tr16_b64_v4bf16((__attribute__((address_space(3))) bf16x4*)(const_cast<char*>(addr)));
+  };
+
+  f32x4 acc[T::TM][T::TN];
+#pragma unroll
+  for (int i = 0; i < T::TM; ++i)
+#pragma unroll
+    for (int j = 0; j < T::TN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  const bool do_bias = p.bias_slab != nullptr && tn == 0;
+  float bias_acc = 0.f;
+
+  const int nk = kend > kbeg ? (kend - kbeg + BK - 1) / BK : 0;
+  if (nk > 0) stage(0, kbeg);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  int cur = 0;
+  for (int kt = 0; kt < nk; ++kt) {
+    if (kt + 1 < nk) stage(cur ^ 1, kbeg + (kt + 1) * BK);
+    const char* As = smem + cur * T::STAGE;
+    const char* Bs = As + BK * BM * 2;
+    if (do_bias) {
+      constexpr int RS = 256 / BM;
+      const int col = tid % BM, rr = tid / BM;
+      const int chn = col >> 3, w = (col & 7) * 2;
+      for (int r = rr; r < BK; r += RS)
+        bias_acc += (float)*reinterpret_cast<const bf16*>(As + r * BM * 2 + ((chn ^ tr_swz<T::ACH>(r)) << 4) + w);
+    }
+#pragma unroll
+    for (int kk = 0; kk < BK / 32; ++kk) {
+      const int krow = kk * 32 + 8 * (lane >> 4);
+      bf16x8 a[T::TM], b[T::TN];
+#pragma unroll
+      for (int i = 0; i < T::TM; ++i) {
+        const bf16x4 lo = tr_read(As, BM * 2, krow, wm * (BM / 2) + i * 16, std::integral_constant<int, T::ACH>{});
+        const bf16x4 hi = tr_read(As, BM * 2, krow + 4, wm * (BM / 2) + i * 16, std::integral_constant<int, T::ACH>{});
+        a[i] = bf16x8{lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+      }
+#pragma unroll
+      for (int j = 0; j < T::TN; ++j) {
+        const bf16x4 lo = tr_read(Bs, BN * 2, krow, wn * (BN / 2) + j * 16, std::integral_constant<int, T::BCH>{});
+        const bf16x4 hi = tr_read(Bs, BN * 2, krow + 4, wn * (BN / 2) + j * 16, std::integral_constant<int, T::BCH>{});
+        b[j] = bf16x8{lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+      }
+      __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+      for (int i = 0; i < T::TM; ++i)
+#pragma unroll
+        for (int j = 0; j < T::TN; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[i], b[j], acc[i][j], 0, 0, 0);
+      __builtin_amdgcn_s_setprio(0);
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    cur ^= 1;
+  }
+
+  float* out = p.slab + (long)split * p.M * p.N;
+#pragma unroll
+  for (int i = 0; i < T::TM; ++i)
+#pragma unroll
+    for (int j = 0; j < T::TN; ++j) {
+      const int n = n0 + wn * (BN / 2) + j * 16 + (lane & 15);
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int m = m0 + wm * (BM / 2) + i * 16 + (lane >> 4) * 4 + r;
+        if (m < p.M && n < p.N) out[(long)m * p.N + n] = acc[i][j][r];
+      }
+    }
+  if (do_bias) {
+    float* red = reinterpret_cast<float*>(smem);
+    constexpr int RS = 256 / BM;
+    __syncthreads();
+    red[tid] = bias_acc;
+    __syncthreads();
+    if (tid < BM) {
+      float s = 0.f;
+      for (int k = 0; k < RS; ++k) s += red[tid + k * BM];
+      if (m0 + tid < p.M) p.bias_slab[(long)split * p.M + m0 + tid] = s;
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------------------------
+// launchers
+// ---------------------------------------------------------------------------------------------
+template <int BM, int BN, int BK, bool UNI>
+static void launch_g2(const G2Args& a, hipStream_t s) {
+  const int tiles = ((a.M + BM - 1) / BM) * ((a.N + BN - 1) / BN);
+  hipLaunchKernelGGL((gemm_g2_kernel<BM, BN, BK, UNI>), dim3(tiles), dim3(256), 0, s, a);
+  DCNN_LAUNCH_CHECK();
+}
+
+// Tile choice: the largest tile that still gives >= ~2 workgroups per CU.
+void g2_tile(int M, int N, int* bm, int* bn) {
+  auto tiles = [&](int m, int n) { return (long)((M + m - 1) / m) * ((N + n - 1) / n); };
+  if (N >= 128 && tiles(128, 128) >= 480) { *bm = 128; *bn = 128; return; }
+  if (tiles(128, 64) >= 480 || N < 128) {
+    *bm = tiles(128, 64) >= 400 ? 128 : 64;
+    *bn = 64;
+    return;
+  }
+  if (tiles(64, 128) >= 400) { *bm = 64; *bn = 128; return; }
+  *bm = 64;
+  *bn = 64;
+}
+
+int gemm_g2_stat_rows(int M, int N) {
+  int bm, bn;
+  g2_tile(M, N, &bm, &bn);
+  return (M + bm - 1) / bm;
+}
+
+void gemm_g2(const G2Args& a, hipStream_t s) {
+  if (a.N % 8 != 0 || a.Cs % 8 != 0 || a.ldb % 8 != 0 || a.ldc % 8 != 0 || a.ntaps > 64 || a.ntaps < 1)
+    throw std::runtime_error("gemm_g2: unsupported shape (needs N, Cs, ldb, ldc multiples of 8, 1..64 taps)");
+  int bm, bn;
+  g2_tile(a.M, a.N, &bm, &bn);
+  const int bk = (a.Cs % 64 == 0) ? 64 : 32;
+  const bool uni = a.Cs % bk == 0;
+#define DCNN_G2(BM, BN, BK, U) if (bm == BM && bn == BN && bk == BK && uni == U) return launch_g2<BM, BN, BK, U>(a, s)
+  DCNN_G2(128, 128, 64, true);
+  DCNN_G2(128, 64, 64, true);
+  DCNN_G2(64, 128, 64, true);
+  DCNN_G2(64, 64, 64, true);
+  DCNN_G2(128, 128, 32, true);
+  DCNN_G2(128, 64, 32, true);
+  DCNN_G2(64, 128, 32, true);
+  DCNN_G2(64, 64, 32, true);
+  DCNN_G2(128, 128, 32, false);
+  DCNN_G2(128, 64, 32, false);
+  DCNN_G2(64, 128, 32, false);
+  DCNN_G2(64, 64, 32, false);
+#undef DCNN_G2
+  throw std::runtime_error("gemm_g2: no variant");
+}
+
+template <int BM, int BN>
+static void launch_t2(T2Args a, int splits, hipStream_t s) {
+  const int tiles = ((a.M + BM - 1) / BM) * ((a.N + BN - 1) / BN);
+  hipLaunchKernelGGL((gemm_t2_kernel<BM, BN>), dim3(tiles * splits), dim3(256), 0, s, a);
+  DCNN_LAUNCH_CHECK();
+}
+
+void t2_tile(int M, int N, int* bm, int* bn) {
+  *bm = M >= 128 ? 128 : 64;
+  *bn = N >= 128 ? 128 : 64;
+}
+
+int gemm_t2_splits(int M, int N, int P) {
+  int bm, bn;
+  t2_tile(M, N, &bm, &bn);
+  const long tiles = (long)((M + bm - 1) / bm) * ((N + bn - 1) / bn);
+  long splits = (512 + tiles - 1) / tiles;
+  const long max_by_k = P / (64 * 4) > 0 ? P / (64 * 4) : 1;
+  if (splits > max_by_k) splits = max_by_k;
+  const long max_by_mem = (48l << 20) / (4l * M * N) > 0 ? (48l << 20) / (4l * M * N) : 1;
+  if (splits > max_by_mem) splits = max_by_mem;
+  if (splits < 1) splits = 1;
+  if (splits > 256) splits = 256;
+  return (int)splits;
+}
+
+void gemm_t2(T2Args a, int splits, hipStream_t s) {
+  if (a.M % 8 != 0 || a.N % 8 != 0 || a.Cs % 8 != 0 || a.ldy % 8 != 0 || a.ntaps > 64)
+    throw std::runtime_error("gemm_t2: unsupported shape");
+  int bm, bn;
+  t2_tile(a.M, a.N, &bm, &bn);
+  const int per = (a.P + splits - 1) / splits;
+  a.k_per_split = ((per + 63) / 64) * 64;
+  if (bm == 128 && bn == 128) return launch_t2<128, 128>(a, splits, s);
+  if (bm == 128 && bn == 64) return launch_t2<128, 64>(a, splits, s);
+  if (bm == 64 && bn == 128) return launch_t2<64, 128>(a, splits, s);
+  return launch_t2<64, 64>(a, splits, s);
+}
+
+}  // namespace dcnn

@@ -255,6 +255,19 @@ __global__ void nchw_to_nhwc_kernel(const float* __restrict__ x, T* __restrict__
   }
 }
 
+// x NCHW (float, C channels) -> y NHWC (T, Cp >= C channels, zero padded)
+template <typename T>
+__global__ void nchw_to_nhwc_pad_kernel(const float* __restrict__ x, T* __restrict__ y, int N, int C, int Cp, int HW) {
+  const long total = (long)N * Cp * HW;
+  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < total; i += (long)gridDim.x * blockDim.x) {
+    const int c = (int)(i % Cp);
+    const long t = i / Cp;
+    const int p = (int)(t % HW);
+    const int n = (int)(t / HW);
+    y[i] = from_f<T>(c < C ? x[((long)n * C + c) * HW + p] : 0.f);
+  }
+}
+
 // W[co][t][ci] -> Wt[ci][t][co]   (dgrad operand), source fp32 or bf16, dest bf16
 template <typename S>
 __global__ void conv_weight_transpose_kernel(const S* __restrict__ w, bf16* __restrict__ wt, int Co, int T_, int Ci) {
@@ -392,6 +405,12 @@ static void nchw_to_nhwc_t(const float* x, void* y, int N, int C, int HW, hipStr
   DCNN_LAUNCH_CHECK();
 }
 template <typename T>
+static void nchw_to_nhwc_pad_t(const float* x, void* y, int N, int C, int Cp, int HW, hipStream_t s) {
+  hipLaunchKernelGGL(nchw_to_nhwc_pad_kernel<T>, dim3(grid_for((long)N * Cp * HW, 256)), dim3(256), 0, s, x, (T*)y, N, C,
+                     Cp, HW);
+  DCNN_LAUNCH_CHECK();
+}
+template <typename T>
 static void wt_t(const void* w, bf16* wt, int Co, int T_, int Ci, hipStream_t s) {
   hipLaunchKernelGGL(conv_weight_transpose_kernel<T>, dim3(grid_for((long)Co * T_ * Ci, 256)), dim3(256), 0, s,
                      (const T*)w, wt, Co, T_, Ci);
@@ -404,6 +423,7 @@ void softmax_rows(int dt, const void* x, void* y, long rows, int C, hipStream_t 
 void softmax_rows_bwd(int dt, const void* y, const void* dy, void* dx, long rows, int C, hipStream_t s) { DCNN_DT(dt, softmax_bwd_t, y, dy, dx, rows, C, s); }
 void dropout(int dt, const void* x, void* y, long n, float p, uint64_t seed, hipStream_t s) { DCNN_DT(dt, dropout_t, x, y, n, p, seed, s); }
 void nchw_to_nhwc(int dt, const float* x, void* y, int N, int C, int HW, hipStream_t s) { DCNN_DT(dt, nchw_to_nhwc_t, x, y, N, C, HW, s); }
+void nchw_to_nhwc_pad(int dt, const float* x, void* y, int N, int C, int Cp, int HW, hipStream_t s) { DCNN_DT(dt, nchw_to_nhwc_pad_t, x, y, N, C, Cp, HW, s); }
 void conv_weight_transpose(int src_dt, const void* w, bf16* wt, int Co, int T_, int Ci, hipStream_t s) { DCNN_DT(src_dt, wt_t, w, wt, Co, T_, Ci, s); }
 void cast_f32_bf16(const float* x, bf16* y, long n, hipStream_t s) {
   hipLaunchKernelGGL(cast_f32_bf16_kernel, dim3(grid_for(n, 256)), dim3(256), 0, s, x, y, n);

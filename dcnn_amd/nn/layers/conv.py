@@ -66,12 +66,18 @@ class Conv2D(ParameterizedLayer):
             raise ValueError(f"Conv2D '{self.name}': input has {x.shape[1]} channels, expected {self.in_channels}")
         if x.is_cuda:
             from ...ops import hip
-            xa = hip.to_act(x, self.compute_dtype)
-            y, partial = hip.conv2d_fwd(xa, self.weight_operand(0), self._bias_vec(), (self.stride_h, self.stride_w),
+            if self.in_channels < 8:
+                # RGB stem: zero-pad channels to 8 so every 16-byte chunk is one tap (vector path)
+                xa = hip.to_act_padded(x, 8)
+                w = hip.pad_weight_channels(self.weight_operand(0), 8)
+            else:
+                xa = hip.to_act(x, self.compute_dtype)
+                w = self.weight_operand(0)
+            y, partial = hip.conv2d_fwd(xa, w, self._bias_vec(), (self.stride_h, self.stride_w),
                                         (self.pad_h, self.pad_w), stats=self.emit_bn_stats and self.training)
             if partial is not None:
                 y._bn_partial = partial
-            self._cache[mb_id] = xa
+            self._cache[mb_id] = (xa, tuple(x.shape))
             return y
         y = F.conv2d(x, self.weights, self._bias_vec(), (self.stride_h, self.stride_w), (self.pad_h, self.pad_w))
         self._cache[mb_id] = x
@@ -81,6 +87,10 @@ class Conv2D(ParameterizedLayer):
         x = self._cache.pop(mb_id, None)
         if x is None:
             raise RuntimeError(f"Conv2D '{self.name}': no cached input for micro-batch {mb_id}")
+        if isinstance(x, tuple):
+            x, x_shape = x
+        else:
+            x_shape = tuple(x.shape)
         grad = grad.to(x.device)
         if x.is_cuda:
             from ...ops import hip
@@ -91,7 +101,7 @@ class Conv2D(ParameterizedLayer):
                 return None
             wt = hip.conv_weight_t(self.weight_operand(0))
             res = hip.to_act(add_to, self.compute_dtype) if add_to is not None else None
-            return hip.conv2d_dgrad(g, wt, x.shape, (self.stride_h, self.stride_w), (self.pad_h, self.pad_w),
+            return hip.conv2d_dgrad(g, wt, x_shape, (self.stride_h, self.stride_w), (self.pad_h, self.pad_w),
                                     residual=res)
         st, pd = (self.stride_h, self.stride_w), (self.pad_h, self.pad_w)
         self._grads[0].add_(torch.nn.grad.conv2d_weight(x, self.weights.shape, grad, st, pd))

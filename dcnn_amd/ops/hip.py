@@ -46,34 +46,85 @@ def conv_out_hw(H, W, kh, kw, sh, sw, ph, pw):
 
 
 # ------------------------------------------------------------------------------ conv / dense
+def _nbytes(t):
+    return t.numel() * t.element_size()
+
+
+def _fwd_taps(C, W, KH, KW, ph, pw):
+    """Tap list of a forward conv: (dy, dx, src element offset, B-row element offset)."""
+    taps = []
+    for ky in range(KH):
+        for kx in range(KW):
+            dy, dx = ky - ph, kx - pw
+            taps.append((dy, dx, (dy * W + dx) * C, (ky * KW + kx) * C))
+    return taps
+
+
+def _g2_ok(Cs, N):
+    return Cs % 8 == 0 and N % 8 == 0
+
+
 def conv2d_fwd(x, w, bias, stride, pad, *, stats=False, residual=None, relu=False, out_fp32=False):
     """y = conv(x, w) + bias  [+ residual] [ReLU]; optional BN partial statistics slab.
 
-    x: (N,Ci,H,W) bf16 channels_last; w: (Co,Ci,KH,KW) bf16 channels_last.
+    x: (N,Ci,H,W) bf16 channels_last; w: (Co,Ci,KH,KW) bf16 channels_last (or a padded
+    [Co][KH][KW][Cp] operand when Ci was padded to Cp, see ``pad_input_channels``).
     Returns (y, (slab, rows) | None).
     """
     _check_act(x, "conv2d_fwd.x")
     K = kernels()
     N, Ci, H, W = x.shape
-    Co, Ci2, KH, KW = w.shape
-    assert Ci == Ci2, f"conv2d: input channels {Ci} != weight {Ci2}"
-    assert x.dtype == BF16 and w.dtype == BF16 and w.is_contiguous(memory_format=CL)
+    if w.dim() == 4 and w.shape[1] == Ci:
+        Co, _, KH, KW = w.shape
+        assert w.is_contiguous(memory_format=CL)
+    else:  # padded operand [Co][KH][KW][Ci]
+        Co, KH, KW, Cp = w.shape
+        assert Cp == Ci and w.is_contiguous()
+    assert x.dtype == BF16 and w.dtype == BF16
     sh, sw = stride
     ph, pw = pad
     OH, OW = conv_out_hw(H, W, KH, KW, sh, sw, ph, pw)
-    y = torch.empty((N, Co, OH, OW), dtype=F32 if out_fp32 else BF16, device=x.device, memory_format=CL)
     M = N * OH * OW
-    slab = None
-    rows = 0
+    if residual is not None:
+        assert tuple(residual.shape) == (N, Co, OH, OW) and residual.is_contiguous(memory_format=CL)
+    if _g2_ok(Ci, Co) and not out_fp32:
+        y = torch.empty((N, Co, OH, OW), dtype=BF16, device=x.device, memory_format=CL)
+        slab, rows = None, 0
+        if stats:
+            rows = K.gemm_g2_stat_rows(M, Co)
+            slab = torch.empty((rows, 2, Co), dtype=F32, device=x.device)
+        K.gemm_g2(x.data_ptr(), w.data_ptr(), y.data_ptr(), _nbytes(x), _nbytes(w), M, Co, Ci, H, W, OH, OW, sh, sw,
+                  _fwd_taps(Ci, W, KH, KW, ph, pw), KH * KW * Ci, Co, OH, OW, 1, 1, 0, 0, ptr(bias), ptr(residual),
+                  ptr(slab), int(relu), stream_ptr())
+        return y, ((slab, rows) if stats else None)
+    # generic fallback (odd channel counts): v1 kernels
+    y = torch.empty((N, Co, OH, OW), dtype=F32 if out_fp32 else BF16, device=x.device, memory_format=CL)
+    slab, rows = None, 0
     if stats:
         rows = K.gemm_nt_stat_rows(M, Co)
         slab = torch.empty((rows, 2, Co), dtype=F32, device=x.device)
-    if residual is not None:
-        assert residual.shape == y.shape and residual.is_contiguous(memory_format=CL) and residual.dtype == BF16
     K.gemm_nt(x.data_ptr(), w.data_ptr(), y.data_ptr(), M, Co, KH * KW * Ci, 0, KH * KW * Ci, Co, CONV_FWD,
               N, H, W, Ci, OH, OW, KH, KW, sh, sw, ph, pw, ptr(bias), ptr(residual), ptr(slab),
               int(out_fp32), int(relu), stream_ptr())
     return y, ((slab, rows) if stats else None)
+
+
+def to_act_padded(x, cp):
+    """(N,C,H,W) -> NHWC bf16 with channels zero-padded to cp (RGB stem: 3 -> 8) so the stem
+    conv runs on the vectorised MFMA path. One HIP pass from an NCHW fp32 input."""
+    N, C, H, W = x.shape
+    y = torch.empty((N, cp, H, W), dtype=BF16, device=x.device, memory_format=CL)
+    src = x if (x.dtype == F32 and x.is_contiguous()) else x.float().contiguous()
+    kernels().nchw_to_nhwc_pad(dt_code(BF16), src.data_ptr(), y.data_ptr(), N, C, cp, H * W, stream_ptr())
+    return y
+
+
+def pad_weight_channels(w, cp):
+    """(Co,Ci,KH,KW) -> bf16 [Co][KH][KW][cp] operand, zero-padded input channels."""
+    Co, Ci, KH, KW = w.shape
+    out = torch.zeros((Co, KH, KW, cp), dtype=BF16, device=w.device)
+    out[..., :Ci] = w.permute(0, 2, 3, 1).to(BF16)
+    return out
 
 
 def conv_weight_t(w, out=None):
@@ -86,35 +137,92 @@ def conv_weight_t(w, out=None):
 
 
 def conv2d_dgrad(dy, wt, x_shape, stride, pad, *, residual=None):
-    """dx = conv_transpose(dy, w) [+ residual];  wt = conv_weight_t(w)."""
+    """dx = conv_transpose(dy, w) [+ residual];  wt = conv_weight_t(w).
+
+    Strided convs are phase-decomposed: input pixels are split into stride^2 parity classes,
+    each a dense GEMM over only the kernel taps that reach it (no MFMA work on zero taps).
+    """
     _check_act(dy, "conv2d_dgrad.dy")
+    K = kernels()
     N, Ci, H, W = x_shape
-    _, OH, OW_, Co = dy.shape[0], dy.shape[2], dy.shape[3], dy.shape[1]
+    Co, OH, OW = dy.shape[1], dy.shape[2], dy.shape[3]
     Ci2, KH, KW, Co2 = wt.shape
     assert Ci == Ci2 and Co == Co2
-    dx = torch.empty((N, Ci, H, W), dtype=BF16, device=dy.device, memory_format=CL)
     if residual is not None:
-        assert residual.shape == dx.shape and residual.is_contiguous(memory_format=CL)
-    M = N * H * W
-    Kd = KH * KW * Co
-    kernels().gemm_nt(dy.data_ptr(), wt.data_ptr(), dx.data_ptr(), M, Ci, Kd, 0, Kd, Ci, CONV_DGRAD,
-                      N, OH, OW_, Co, H, W, KH, KW, stride[0], stride[1], pad[0], pad[1],
-                      0, ptr(residual), 0, 0, 0, stream_ptr())
+        assert tuple(residual.shape) == (N, Ci, H, W) and residual.is_contiguous(memory_format=CL)
+    sh, sw = stride
+    ph, pw = pad
+    if not _g2_ok(Co, Ci):
+        dx = torch.empty((N, Ci, H, W), dtype=BF16, device=dy.device, memory_format=CL)
+        Kd = KH * KW * Co
+        K.gemm_nt(dy.data_ptr(), wt.data_ptr(), dx.data_ptr(), N * H * W, Ci, Kd, 0, Kd, Ci, CONV_DGRAD,
+                  N, OH, OW, Co, H, W, KH, KW, sh, sw, ph, pw, 0, ptr(residual), 0, 0, 0, stream_ptr())
+        return dx
+    classes = []
+    empty_class = False
+    for ry in range(sh):
+        for rx in range(sw):
+            GH, GW = (H - ry + sh - 1) // sh, (W - rx + sw - 1) // sw
+            if GH <= 0 or GW <= 0:
+                continue
+            taps = []
+            for ky in range(KH):
+                if (ry + ph - ky) % sh:
+                    continue
+                dyo = (ry + ph - ky) // sh
+                for kx in range(KW):
+                    if (rx + pw - kx) % sw:
+                        continue
+                    dxo = (rx + pw - kx) // sw
+                    taps.append((dyo, dxo, (dyo * OW + dxo) * Co, (ky * KW + kx) * Co))
+            if taps:
+                classes.append((ry, rx, GH, GW, taps))
+            else:
+                empty_class = True
+    if empty_class:
+        dx = residual.clone() if residual is not None else torch.empty(
+            (N, Ci, H, W), dtype=BF16, device=dy.device, memory_format=CL).zero_()
+    else:
+        dx = torch.empty((N, Ci, H, W), dtype=BF16, device=dy.device, memory_format=CL)
+    st = stream_ptr()
+    for ry, rx, GH, GW, taps in classes:
+        K.gemm_g2(dy.data_ptr(), wt.data_ptr(), dx.data_ptr(), _nbytes(dy), _nbytes(wt), N * GH * GW, Ci, Co, OH, OW,
+                  GH, GW, 1, 1, taps, KH * KW * Co, Ci, H, W, sh, sw, ry, rx, 0, ptr(residual), 0, 0, st)
     return dx
 
 
 def conv2d_wgrad(dy, x, w_shape, stride, pad, grad_w, grad_b=None):
-    """grad_w (+)= dW, grad_b (+)= sum(dy): split-K MFMA GEMM + fp32 slab reduce (beta = 1)."""
+    """grad_w (+)= dW, grad_b (+)= sum(dy): split-K MFMA GEMM + fp32 slab reduce (beta = 1).
+
+    ``x`` may carry zero-padded channels (RGB stem); the padded columns are dropped on reduce.
+    """
     K = kernels()
-    N, Ci, H, W = x.shape
-    Co, _, KH, KW = w_shape
+    N, Cx, H, W = x.shape
+    Co, Ci, KH, KW = w_shape
     OH, OW = dy.shape[2], dy.shape[3]
     P = N * OH * OW
+    st = stream_ptr()
+    if _g2_ok(Cx, Co) and P < (1 << 24):
+        Ng = KH * KW * Cx
+        splits = K.gemm_t2_splits(Co, Ng, P)
+        slab = torch.empty((splits, Co, Ng), dtype=F32, device=x.device)
+        bslab = torch.empty((splits, Co), dtype=F32, device=x.device) if grad_b is not None else None
+        taps = [(ky - pad[0], kx - pad[1]) for ky in range(KH) for kx in range(KW)]
+        K.gemm_t2(dy.data_ptr(), x.data_ptr(), slab.data_ptr(), ptr(bslab), _nbytes(dy), _nbytes(x), Co, Ng, P, Co, Cx,
+                  H, W, OH, OW, stride[0], stride[1], taps, splits, st)
+        if Cx == Ci:
+            K.splitk_reduce(slab.data_ptr(), grad_w.data_ptr(), Co * Ng, splits, 1, st)
+        else:
+            tmp = torch.empty((Co, KH, KW, Cx), dtype=F32, device=x.device)
+            K.splitk_reduce(slab.data_ptr(), tmp.data_ptr(), Co * Ng, splits, 0, st)
+            grad_w.add_(tmp[..., :Ci].permute(0, 3, 1, 2))
+        if grad_b is not None:
+            K.splitk_reduce(bslab.data_ptr(), grad_b.data_ptr(), Co, splits, 1, st)
+        return
     Ng = KH * KW * Ci
     splits = K.gemm_tn_splits(Co, Ng, P)
     slab = torch.empty((splits, Co, Ng), dtype=F32, device=x.device)
     bslab = torch.empty((splits, Co), dtype=F32, device=x.device) if grad_b is not None else None
-    st = stream_ptr()
     K.gemm_tn(dy.data_ptr(), x.data_ptr(), slab.data_ptr(), ptr(bslab), Co, Ng, P, CONV_FWD,
               N, H, W, Ci, OH, OW, KH, KW, stride[0], stride[1], pad[0], pad[1], 0, splits, st)
     assert grad_w.is_contiguous(memory_format=CL) or KH * KW == 1 or Ci == 1
@@ -128,6 +236,10 @@ def dense_fwd(x2d, w2d, bias):
     N, In = x2d.shape
     Out = w2d.shape[0]
     y = torch.empty((N, Out), dtype=BF16, device=x2d.device)
+    if _g2_ok(In, Out):
+        kernels().gemm_g2(x2d.data_ptr(), w2d.data_ptr(), y.data_ptr(), _nbytes(x2d), _nbytes(w2d), N, Out, In, 1, 1,
+                          1, 1, 1, 1, [(0, 0, 0, 0)], In, Out, 1, 1, 1, 1, 0, 0, ptr(bias), 0, 0, 0, stream_ptr())
+        return y
     kernels().gemm_nt(x2d.data_ptr(), w2d.data_ptr(), y.data_ptr(), N, Out, In, In, In, Out, PLAIN,
                       0, 0, 0, 0, 1, 1, 1, 1, 1, 1, 0, 0, ptr(bias), 0, 0, 0, 0, stream_ptr())
     return y
@@ -138,6 +250,10 @@ def dense_dgrad(dy2d, wt2d):
     N, Out = dy2d.shape
     In = wt2d.shape[0]
     dx = torch.empty((N, In), dtype=BF16, device=dy2d.device)
+    if _g2_ok(Out, In):
+        kernels().gemm_g2(dy2d.data_ptr(), wt2d.data_ptr(), dx.data_ptr(), _nbytes(dy2d), _nbytes(wt2d), N, In, Out, 1,
+                          1, 1, 1, 1, 1, [(0, 0, 0, 0)], Out, In, 1, 1, 1, 1, 0, 0, 0, 0, 0, 0, stream_ptr())
+        return dx
     kernels().gemm_nt(dy2d.data_ptr(), wt2d.data_ptr(), dx.data_ptr(), N, In, Out, Out, Out, In, PLAIN,
                       0, 0, 0, 0, 1, 1, 1, 1, 1, 1, 0, 0, 0, 0, 0, 0, 0, stream_ptr())
     return dx
@@ -147,12 +263,19 @@ def dense_wgrad(dy2d, x2d, grad_w, grad_b=None):
     K = kernels()
     N, Out = dy2d.shape
     In = x2d.shape[1]
-    splits = K.gemm_tn_splits(Out, In, N)
-    slab = torch.empty((splits, Out, In), dtype=F32, device=x2d.device)
-    bslab = torch.empty((splits, Out), dtype=F32, device=x2d.device) if grad_b is not None else None
     st = stream_ptr()
-    K.gemm_tn(dy2d.data_ptr(), x2d.data_ptr(), slab.data_ptr(), ptr(bslab), Out, In, N, PLAIN,
-              0, 0, 0, 0, 1, 1, 1, 1, 1, 1, 0, 0, In, splits, st)
+    if _g2_ok(In, Out):
+        splits = K.gemm_t2_splits(Out, In, N)
+        slab = torch.empty((splits, Out, In), dtype=F32, device=x2d.device)
+        bslab = torch.empty((splits, Out), dtype=F32, device=x2d.device) if grad_b is not None else None
+        K.gemm_t2(dy2d.data_ptr(), x2d.data_ptr(), slab.data_ptr(), ptr(bslab), _nbytes(dy2d), _nbytes(x2d), Out, In,
+                  N, Out, In, 1, 1, 1, 1, 1, 1, [(0, 0)], splits, st)
+    else:
+        splits = K.gemm_tn_splits(Out, In, N)
+        slab = torch.empty((splits, Out, In), dtype=F32, device=x2d.device)
+        bslab = torch.empty((splits, Out), dtype=F32, device=x2d.device) if grad_b is not None else None
+        K.gemm_tn(dy2d.data_ptr(), x2d.data_ptr(), slab.data_ptr(), ptr(bslab), Out, In, N, PLAIN,
+                  0, 0, 0, 0, 1, 1, 1, 1, 1, 1, 0, 0, In, splits, st)
     K.splitk_reduce(slab.data_ptr(), grad_w.data_ptr(), Out * In, splits, 1, st)
     if grad_b is not None:
         K.splitk_reduce(bslab.data_ptr(), grad_b.data_ptr(), Out, splits, 1, st)

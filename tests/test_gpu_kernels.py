@@ -84,6 +84,24 @@ def test_conv_fwd_dgrad_wgrad(hip, case):
     assert rel_err(gb, dyb.sum((0, 2, 3)) + 1) < 1e-2
 
 
+def test_padded_rgb_stem(hip):
+    """RGB stem runs on the vector path with channels zero-padded 3 -> 8."""
+    torch.manual_seed(9)
+    N, H, W, Co = 4, 20, 20, 32
+    x = torch.randn(N, 3, H, W)
+    w = torch.randn(Co, 3, 3, 3) / 5
+    xp = hip.to_act_padded(x.cuda(), 8)
+    assert xp.shape == (N, 8, H, W) and xp.is_contiguous(memory_format=CL)
+    assert torch.equal(xp[:, 3:].float().cpu(), torch.zeros(N, 5, H, W))
+    wp = hip.pad_weight_channels(w.cuda().bfloat16().contiguous(memory_format=CL), 8)
+    y, _ = hip.conv2d_fwd(xp, wp, None, (1, 1), (1, 1))
+    assert rel_err(y, F.conv2d(bf(x), bf(w), None, 1, 1)) < 1e-2
+    dy = torch.randn(N, Co, H, W)
+    gw = torch.zeros(Co, 3, 3, 3, device="cuda").contiguous(memory_format=CL)
+    hip.conv2d_wgrad(dy.cuda().bfloat16().contiguous(memory_format=CL), xp, w.shape, (1, 1), (1, 1), gw)
+    assert rel_err(gw, torch.nn.grad.conv2d_weight(bf(x), w.shape, bf(dy), 1, 1)) < 1e-2
+
+
 @pytest.mark.parametrize("shape", [(128, 512, 200), (64, 256, 10), (16, 192, 10), (256, 1024, 200)])
 def test_dense(hip, shape):
     N, In, Out = shape
