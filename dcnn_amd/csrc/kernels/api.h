@@ -23,6 +23,7 @@ struct G2Args {
   int ldb, ldc;
   int OH, OW, OSY, OSX, ORY, ORX;
   const float* bias; const bf16* residual; float* stats; int relu;
+  float* zero_ptr; int zero_n;  // zeroed by workgroup 0 (BN sums consumed by the next kernel)
 };
 struct T2Args {
   const bf16* dY; const bf16* X; float* slab; float* bias_slab;
@@ -45,7 +46,7 @@ void splitk_reduce(const float* slab, float* out, long n, int splits, int accumu
 
 int bn_partial_rows(long R, int C);
 void bn_partial(int dtype, const void* x, const void* dy, const void* yout, void* dy_out, const float* mean,
-                const float* istd, long R, int C, float* slab, int mode, hipStream_t s);
+                const float* istd, long R, int C, float* slab, int mode, float* zero_sums, hipStream_t s);
 void bn_slab_reduce(const float* slab, int rows, int C, float* sums, hipStream_t s);
 void bn_apply(int dtype, const void* x, void* y, long R, int C, const float* sums, float count, const float* gamma,
               const float* beta, float eps, const void* residual, int relu, float* save_mean, float* save_istd,
@@ -71,6 +72,7 @@ void nchw_to_nhwc(int dt, const float* x, void* y, int N, int C, int HW, hipStre
 void nchw_to_nhwc_pad(int dt, const float* x, void* y, int N, int C, int Cp, int HW, hipStream_t s);
 void conv_weight_transpose(int src_dt, const void* w, bf16* wt, int Co, int T_, int Ci, hipStream_t s);
 void cast_f32_bf16(const float* x, bf16* y, long n, hipStream_t s);
+void multi_weight_transpose(const int64_t* table, int n, long max_numel, hipStream_t s);
 void im2col(const float* x, float* col, int N, int C, int H, int W, int KH, int KW, int SH, int SW, int PH, int PW,
             int OH, int OW, hipStream_t s);
 void col2im(const float* col, float* x, int N, int C, int H, int W, int KH, int KW, int SH, int SW, int PH, int PW,

@@ -36,7 +36,7 @@ PYBIND11_MODULE(_kernels, m) {
         [](uintptr_t A, uintptr_t B, uintptr_t C, unsigned a_bytes, unsigned b_bytes, int M, int N, int Cs, int H,
            int W, int GH, int GW, int SY, int SX, std::vector<std::array<int, 4>> taps, int ldb, int ldc, int OH,
            int OW, int OSY, int OSX, int ORY, int ORX, uintptr_t bias, uintptr_t residual, uintptr_t stats, int relu,
-           uintptr_t stream) {
+           uintptr_t zero_ptr, int zero_n, uintptr_t stream) {
           G2Args a{};
           a.A = P<const bf16*>(A); a.B = P<const bf16*>(B); a.C = P<bf16*>(C);
           a.a_bytes = a_bytes; a.b_bytes = b_bytes;
@@ -48,6 +48,7 @@ PYBIND11_MODULE(_kernels, m) {
           }
           a.ldb = ldb; a.ldc = ldc; a.OH = OH; a.OW = OW; a.OSY = OSY; a.OSX = OSX; a.ORY = ORY; a.ORX = ORX;
           a.bias = P<const float*>(bias); a.residual = P<const bf16*>(residual); a.stats = P<float*>(stats); a.relu = relu;
+          a.zero_ptr = P<float*>(zero_ptr); a.zero_n = zero_n;
           gemm_g2(a, S(stream));
         });
   m.def("gemm_g2_stat_rows", &gemm_g2_stat_rows);
@@ -80,9 +81,9 @@ PYBIND11_MODULE(_kernels, m) {
 
   m.def("bn_partial_rows", &bn_partial_rows);
   m.def("bn_partial", [](int dt, uintptr_t x, uintptr_t dy, uintptr_t yout, uintptr_t dy_out, uintptr_t mean,
-                         uintptr_t istd, long R, int C, uintptr_t slab, int mode, uintptr_t st) {
+                         uintptr_t istd, long R, int C, uintptr_t slab, int mode, uintptr_t zero_sums, uintptr_t st) {
     bn_partial(dt, P<const void*>(x), P<const void*>(dy), P<const void*>(yout), P<void*>(dy_out),
-               P<const float*>(mean), P<const float*>(istd), R, C, P<float*>(slab), mode, S(st));
+               P<const float*>(mean), P<const float*>(istd), R, C, P<float*>(slab), mode, P<float*>(zero_sums), S(st));
   });
   m.def("bn_slab_reduce", [](uintptr_t slab, int rows, int C, uintptr_t sums, uintptr_t st) {
     bn_slab_reduce(P<const float*>(slab), rows, C, P<float*>(sums), S(st));
@@ -158,7 +159,10 @@ PYBIND11_MODULE(_kernels, m) {
   m.def("conv_weight_transpose", [](int dt, uintptr_t w, uintptr_t wt, int Co, int T_, int Ci, uintptr_t st) {
     conv_weight_transpose(dt, P<const void*>(w), P<bf16*>(wt), Co, T_, Ci, S(st));
   });
-  m.def("cast_f32_bf16", [](uintptr_t x, uintptr_t y, long n, uintptr_t st) {
+  m.def("multi_weight_transpose", [](uintptr_t table, int n, long max_numel, uintptr_t st) {
+    multi_weight_transpose(P<const int64_t*>(table), n, max_numel, S(st));
+  });
+  m.def("cast_f32_bf16",[](uintptr_t x, uintptr_t y, long n, uintptr_t st) {
     cast_f32_bf16(P<const float*>(x), P<bf16*>(y), n, S(st));
   });
   m.def("im2col", [](uintptr_t x, uintptr_t col, int N, int C, int H, int W, int KH, int KW, int SH, int SW, int PH,

@@ -5,6 +5,7 @@
 #include <stdint.h>
 #include <stdexcept>
 #include <string>
+#include <type_traits>
 
 #ifndef DCNN_BF16_DEFINED
 #define DCNN_BF16_DEFINED

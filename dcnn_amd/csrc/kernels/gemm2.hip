@@ -69,6 +69,8 @@ __global__ void __launch_bounds__(256, 2) gemm_g2_kernel(G2Args p) {
 
   const __amdgpu_buffer_rsrc_t rsA = __builtin_amdgcn_make_buffer_rsrc((void*)p.A, (short)0, p.a_bytes, 0x00020000);
   const __amdgpu_buffer_rsrc_t rsB = __builtin_amdgcn_make_buffer_rsrc((void*)p.B, (short)0, p.b_bytes, 0x00020000);
+  if (p.zero_ptr && blockIdx.x == 0)
+    for (int i = tid; i < p.zero_n; i += 256) p.zero_ptr[i] = 0.f;
 
   // ---- per-lane A rows: pixel base offset + tap-validity mask (fixed over the K loop) ----
   const int ch = lane % T::CPR;           // this lane's physical chunk slot within a row

@@ -496,21 +496,32 @@ __global__ void __launch_bounds__(256, 2) gemm_tn_kernel(TnArgs p) {
 }
 
 // out[i] (+)= sum_s slab[s][i]   (float4 when aligned)
+// out[i] (+)= sum_s slab[s][i]. 2-D grid: blockIdx.y picks a group of splits so the reduce has
+// enough workgroups to fill the chip even when the output (a weight gradient) is tiny; groups
+// combine with float atomics (accumulate semantics, the gradient buffer is zeroed per step).
 __global__ void splitk_reduce_kernel(const float* __restrict__ slab, float* __restrict__ out, long n,
-                                     int splits, int accumulate) {
+                                     int splits, int per_group, int atomic) {
   const long n4 = n / 4;
+  const int s0 = blockIdx.y * per_group, s1 = min(splits, s0 + per_group);
   for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < n4; i += (long)gridDim.x * blockDim.x) {
-    float4 s = accumulate ? reinterpret_cast<float4*>(out)[i] : make_float4(0, 0, 0, 0);
-    for (int k = 0; k < splits; ++k) {
+    float4 s = make_float4(0, 0, 0, 0);
+    for (int k = s0; k < s1; ++k) {
       const float4 v = reinterpret_cast<const float4*>(slab + (long)k * n)[i];
       s.x += v.x; s.y += v.y; s.z += v.z; s.w += v.w;
     }
-    reinterpret_cast<float4*>(out)[i] = s;
+    float* o = out + i * 4;
+    if (atomic) {
+      atomicAdd(o + 0, s.x); atomicAdd(o + 1, s.y); atomicAdd(o + 2, s.z); atomicAdd(o + 3, s.w);
+    } else {
+      float4 c = reinterpret_cast<float4*>(out)[i];
+      c.x += s.x; c.y += s.y; c.z += s.z; c.w += s.w;
+      reinterpret_cast<float4*>(out)[i] = c;
+    }
   }
   for (long i = n4 * 4 + blockIdx.x * (long)blockDim.x + threadIdx.x; i < n; i += (long)gridDim.x * blockDim.x) {
-    float s = accumulate ? out[i] : 0.f;
-    for (int k = 0; k < splits; ++k) s += slab[(long)k * n + i];
-    out[i] = s;
+    float s = 0.f;
+    for (int k = s0; k < s1; ++k) s += slab[(long)k * n + i];
+    if (atomic) atomicAdd(out + i, s); else out[i] += s;
   }
 }
 
@@ -606,8 +617,17 @@ void gemm_tn(TnArgs a, int splits, hipStream_t s) {
 }
 
 void splitk_reduce(const float* slab, float* out, long n, int splits, int accumulate, hipStream_t s) {
-  hipLaunchKernelGGL(splitk_reduce_kernel, dim3(grid_for(n / 4 + 1, 256, 4096)), dim3(256), 0, s, slab, out,
-                     n, splits, accumulate);
+  if (!accumulate) DCNN_HIP_CHECK(hipMemsetAsync(out, 0, sizeof(float) * n, s));
+  const long n4 = n / 4 + 1;
+  const int gx = grid_for(n4, 256, 4096);
+  long want = (131072 + n4 - 1) / n4;  // aim for >= 512 workgroups in total
+  long groups = (splits + 3) / 4;
+  if (groups > want) groups = want;
+  if (groups < 1) groups = 1;
+  const int per = (int)((splits + groups - 1) / groups);
+  groups = (splits + per - 1) / per;
+  hipLaunchKernelGGL(splitk_reduce_kernel, dim3(gx, (unsigned)groups), dim3(256), 0, s, slab, out, n, splits, per,
+                     groups > 1 ? 1 : 0);
   DCNN_LAUNCH_CHECK();
 }
 

@@ -63,8 +63,11 @@ __global__ void __launch_bounds__(256) bn_partial_kernel(const T* __restrict__ x
                                                          const T* __restrict__ yout, T* __restrict__ dy_out,
                                                          const float* __restrict__ mean,
                                                          const float* __restrict__ istd, long R, int C,
-                                                         int rpb, float* __restrict__ slab, int mode) {
+                                                         int rpb, float* __restrict__ slab, int mode,
+                                                         float* __restrict__ zero_sums) {
   extern __shared__ __attribute__((aligned(16))) float sh[];
+  if (zero_sums && blockIdx.x == 0)
+    for (int i = threadIdx.x; i < 2 * C; i += blockDim.x) zero_sums[i] = 0.f;
   const int groups = C / V;                       // channel vectors
   const int tpr = groups < 256 ? groups : 256;    // threads per row
   const int rows_conc = 256 / tpr;                // rows processed concurrently
@@ -355,35 +358,35 @@ int bn_partial_rows(long R, int C) {
 
 template <typename T>
 static void bn_partial_t(const T* x, const T* dy, const T* yout, T* dy_out, const float* mean,
-                         const float* istd, long R, int C, float* slab, int mode, hipStream_t s) {
+                         const float* istd, long R, int C, float* slab, int mode, float* zs, hipStream_t s) {
   const int rpb = bn_rows_per_block(R, C);
   const int blocks = (int)((R + rpb - 1) / rpb);
   if (C % 8 == 0) {
     const int groups = C / 8, tpr = groups < 256 ? groups : 256, rc = 256 / tpr;
     const size_t shm = (size_t)rc * 2 * tpr * 8 * sizeof(float);
     hipLaunchKernelGGL((bn_partial_kernel<T, 8>), dim3(blocks), dim3(256), shm, s, x, dy, yout, dy_out, mean,
-                       istd, R, C, rpb, slab, mode);
+                       istd, R, C, rpb, slab, mode, zs);
   } else {
     const int tpr = C < 256 ? C : 256, rc = 256 / tpr;
     const size_t shm = (size_t)rc * 2 * tpr * sizeof(float);
     hipLaunchKernelGGL((bn_partial_kernel<T, 1>), dim3(blocks), dim3(256), shm, s, x, dy, yout, dy_out, mean,
-                       istd, R, C, rpb, slab, mode);
+                       istd, R, C, rpb, slab, mode, zs);
   }
   DCNN_LAUNCH_CHECK();
 }
 
 void bn_partial(int dtype, const void* x, const void* dy, const void* yout, void* dy_out, const float* mean,
-                const float* istd, long R, int C, float* slab, int mode, hipStream_t s) {
+                const float* istd, long R, int C, float* slab, int mode, float* zero_sums, hipStream_t s) {
   if (dtype == 0)
     bn_partial_t<float>((const float*)x, (const float*)dy, (const float*)yout, (float*)dy_out, mean, istd, R, C,
-                        slab, mode, s);
+                        slab, mode, zero_sums, s);
   else
     bn_partial_t<bf16>((const bf16*)x, (const bf16*)dy, (const bf16*)yout, (bf16*)dy_out, mean, istd, R, C, slab,
-                       mode, s);
+                       mode, zero_sums, s);
 }
 
+// `sums` must have been zeroed by the producer of `slab` (workgroup 0 of gemm_g2 / bn_partial)
 void bn_slab_reduce(const float* slab, int rows, int C, float* sums, hipStream_t s) {
-  DCNN_HIP_CHECK(hipMemsetAsync(sums, 0, sizeof(float) * 2 * C, s));
   const int rpb = 64;
   dim3 grid((C + 63) / 64, (rows + rpb - 1) / rpb);
   hipLaunchKernelGGL(bn_slab_reduce_kernel, grid, dim3(256), 0, s, slab, rows, C, rpb, sums);

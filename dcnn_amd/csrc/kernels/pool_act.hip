@@ -73,6 +73,66 @@ __global__ void maxpool_bwd_kernel(const T* __restrict__ dy, const uint8_t* __re
   }
 }
 
+// Non-overlapping windows (stride == pool, no padding), bf16, 8 channels per thread:
+// one 16-B load per window tap, one 8-B argmax store; the backward is a pure gather.
+__global__ void maxpool_fwd_nov8_kernel(const bf16* __restrict__ x, bf16* __restrict__ y, uint8_t* __restrict__ idx,
+                                        PoolGeom g) {
+  const int CV = g.C / 8;
+  const long total = (long)g.N * g.OH * g.OW * CV;
+  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < total; i += (long)gridDim.x * blockDim.x) {
+    const int cv = (int)(i % CV);
+    long t = i / CV;
+    const int ox = (int)(t % g.OW);
+    t /= g.OW;
+    const int oy = (int)(t % g.OH);
+    const int n = (int)(t / g.OH);
+    float best[8], v[8];
+    uint8_t bi[8];
+#pragma unroll
+    for (int e = 0; e < 8; ++e) { best[e] = -INFINITY; bi[e] = 0; }
+    for (int ky = 0; ky < g.ph; ++ky)
+      for (int kx = 0; kx < g.pw; ++kx) {
+        const int iy = oy * g.ph + ky, ix = ox * g.pw + kx;
+        unpack8(*reinterpret_cast<const uint4*>(x + (((long)n * g.H + iy) * g.W + ix) * g.C + cv * 8), v);
+#pragma unroll
+        for (int e = 0; e < 8; ++e)
+          if (v[e] > best[e]) { best[e] = v[e]; bi[e] = (uint8_t)(ky * g.pw + kx); }
+      }
+    *reinterpret_cast<uint4*>(y + i * 8) = pack8(best);
+    *reinterpret_cast<uint2*>(idx + i * 8) = *reinterpret_cast<uint2*>(bi);
+  }
+}
+
+__global__ void maxpool_bwd_nov8_kernel(const bf16* __restrict__ dy, const uint8_t* __restrict__ idx,
+                                        bf16* __restrict__ dx, PoolGeom g) {
+  const int CV = g.C / 8;
+  const long total = (long)g.N * g.H * g.W * CV;
+  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < total; i += (long)gridDim.x * blockDim.x) {
+    const int cv = (int)(i % CV);
+    long t = i / CV;
+    const int ix = (int)(t % g.W);
+    t /= g.W;
+    const int iy = (int)(t % g.H);
+    const int n = (int)(t / g.H);
+    const int oy = iy / g.ph, ox = ix / g.pw;
+    float out[8];
+    if (oy < g.OH && ox < g.OW) {
+      const long o = (((long)n * g.OH + oy) * g.OW + ox) * g.C + cv * 8;
+      const int local = (iy - oy * g.ph) * g.pw + (ix - ox * g.pw);
+      float d[8];
+      unpack8(*reinterpret_cast<const uint4*>(dy + o), d);
+      const uint2 ib = *reinterpret_cast<const uint2*>(idx + o);
+      const uint8_t* b = reinterpret_cast<const uint8_t*>(&ib);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) out[e] = b[e] == local ? d[e] : 0.f;
+    } else {
+#pragma unroll
+      for (int e = 0; e < 8; ++e) out[e] = 0.f;
+    }
+    *reinterpret_cast<uint4*>(dx + i * 8) = pack8(out);
+  }
+}
+
 template <typename T>
 __global__ void avgpool_fwd_kernel(const T* __restrict__ x, T* __restrict__ y, PoolGeom g) {
   const long total = (long)g.N * g.OH * g.OW * g.C;
@@ -282,6 +342,30 @@ __global__ void conv_weight_transpose_kernel(const S* __restrict__ w, bf16* __re
   }
 }
 
+// All dgrad weight operands of a model in ONE launch: table rows are
+// {src ptr, dst ptr, Co, taps, Ci}; blockIdx.y selects the tensor.
+__global__ void multi_weight_transpose_kernel(const int64_t* __restrict__ table) {
+  const int64_t* e = table + blockIdx.y * 5;
+  const bf16* w = reinterpret_cast<const bf16*>(e[0]);
+  bf16* wt = reinterpret_cast<bf16*>(e[1]);
+  const int Co = (int)e[2], T_ = (int)e[3], Ci = (int)e[4];
+  const long total = (long)Co * T_ * Ci;
+  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < total; i += (long)gridDim.x * blockDim.x) {
+    const int co = (int)(i % Co);
+    const long r = i / Co;
+    const int t = (int)(r % T_);
+    const int ci = (int)(r / T_);
+    wt[i] = w[((long)co * T_ + t) * Ci + ci];
+  }
+}
+
+void multi_weight_transpose(const int64_t* table, int n, long max_numel, hipStream_t s) {
+  if (n <= 0) return;
+  const int gx = grid_for(max_numel, 256, 1024);
+  hipLaunchKernelGGL(multi_weight_transpose_kernel, dim3(gx, n), dim3(256), 0, s, table);
+  DCNN_LAUNCH_CHECK();
+}
+
 __global__ void cast_f32_bf16_kernel(const float* __restrict__ x, bf16* __restrict__ y, long n) {
   for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < n; i += (long)gridDim.x * blockDim.x)
     y[i] = (bf16)x[i];
@@ -332,14 +416,36 @@ __global__ void col2im_kernel(const float* __restrict__ col, float* __restrict__
 #define DCNN_DT(dtype, FN, ...) \
   if (dtype == 0) FN<float>(__VA_ARGS__); else FN<bf16>(__VA_ARGS__)
 
+static bool pool_nov8(const PoolGeom& g) {
+  return g.C % 8 == 0 && g.sh == g.ph && g.sw == g.pw && g.padh == 0 && g.padw == 0;
+}
+
 template <typename T>
 static void maxpool_fwd_t(const void* x, void* y, uint8_t* idx, PoolGeom g, hipStream_t s) {
+  if constexpr (std::is_same<T, bf16>::value) {
+    if (pool_nov8(g)) {
+      const long total = (long)g.N * g.OH * g.OW * g.C / 8;
+      hipLaunchKernelGGL(maxpool_fwd_nov8_kernel, dim3(grid_for(total, 256)), dim3(256), 0, s, (const bf16*)x, (bf16*)y,
+                         idx, g);
+      DCNN_LAUNCH_CHECK();
+      return;
+    }
+  }
   const long total = (long)g.N * g.OH * g.OW * g.C;
   hipLaunchKernelGGL(maxpool_fwd_kernel<T>, dim3(grid_for(total, 256)), dim3(256), 0, s, (const T*)x, (T*)y, idx, g);
   DCNN_LAUNCH_CHECK();
 }
 template <typename T>
 static void maxpool_bwd_t(const void* dy, const uint8_t* idx, void* dx, PoolGeom g, hipStream_t s) {
+  if constexpr (std::is_same<T, bf16>::value) {
+    if (pool_nov8(g)) {
+      const long total = (long)g.N * g.H * g.W * g.C / 8;
+      hipLaunchKernelGGL(maxpool_bwd_nov8_kernel, dim3(grid_for(total, 256)), dim3(256), 0, s, (const bf16*)dy, idx,
+                         (bf16*)dx, g);
+      DCNN_LAUNCH_CHECK();
+      return;
+    }
+  }
   const long total = (long)g.N * g.H * g.W * g.C;
   hipLaunchKernelGGL(maxpool_bwd_kernel<T>, dim3(grid_for(total, 256)), dim3(256), 0, s, (const T*)dy, idx, (T*)dx, g);
   DCNN_LAUNCH_CHECK();

@@ -99,7 +99,10 @@ class Conv2D(ParameterizedLayer):
                              self._grads[0], self._grads[1].view(-1) if self.use_bias else None)
             if not self.needs_input_grad:
                 return None
-            wt = hip.conv_weight_t(self.weight_operand(0))
+            if getattr(self, "_wt_valid", False):
+                wt = self._wt_buf  # refreshed by the model's batched WeightTransposer this step
+            else:
+                wt = hip.conv_weight_t(self.weight_operand(0))
             res = hip.to_act(add_to, self.compute_dtype) if add_to is not None else None
             return hip.conv2d_dgrad(g, wt, x_shape, (self.stride_h, self.stride_w), (self.pad_h, self.pad_w),
                                     residual=res)

@@ -210,6 +210,21 @@ class Sequential:
             self.layers[0].needs_input_grad = self.first_layer_input_grad
             if isinstance(self.layers[0], ResidualBlock):
                 self.layers[0]._plan()
+        self._transposer = None
+        if on_gpu and self.initialized and self.compute_dtype == torch.bfloat16:
+            from ..ops.hip import WeightTransposer
+            convs = [l for l in _all_layers(self.layers) if isinstance(l, Conv2D)]
+            if convs:
+                self._transposer = WeightTransposer(convs)
+
+    def prepare_backward(self) -> None:
+        """Per-step setup of the backward pass: all dgrad weight operands in one launch."""
+        if getattr(self, "_transposer", None) is not None:
+            self._transposer.run()
+
+    def finish_backward(self) -> None:
+        if getattr(self, "_transposer", None) is not None:
+            self._transposer.invalidate()
 
     def set_first_layer_input_grad(self, need: bool) -> None:
         """Skip the (unused) input gradient of the first layer (reference G9 wasted it)."""
@@ -347,6 +362,7 @@ class Sequential:
             raise RuntimeError("Cannot backward through empty sequential model")
         g_dev = grad.device
         cur = grad.to(self.device.torch_device) if grad.device != self.device.torch_device else grad
+        self.prepare_backward()
         for i in range(len(self.layers) - 1, -1, -1):
             l = self.layers[i]
             t0 = self._prof_begin()
@@ -355,6 +371,7 @@ class Sequential:
             except Exception as e:
                 raise RuntimeError(f"Error in backward pass of layer {i} ({l.type()}): {e}") from e
             self._prof_end(l.name or l.type(), t0, self.backward_times_us)
+        self.finish_backward()
         if cur is not None and return_on_input_device and cur.device != g_dev:
             cur = cur.to(g_dev).float().contiguous()
         return cur

@@ -89,14 +89,15 @@ def conv2d_fwd(x, w, bias, stride, pad, *, stats=False, residual=None, relu=Fals
         assert tuple(residual.shape) == (N, Co, OH, OW) and residual.is_contiguous(memory_format=CL)
     if _g2_ok(Ci, Co) and not out_fp32:
         y = torch.empty((N, Co, OH, OW), dtype=BF16, device=x.device, memory_format=CL)
-        slab, rows = None, 0
+        slab, rows, sums = None, 0, None
         if stats:
             rows = K.gemm_g2_stat_rows(M, Co)
             slab = torch.empty((rows, 2, Co), dtype=F32, device=x.device)
+            sums = torch.empty((2 * Co,), dtype=F32, device=x.device)  # zeroed in-kernel
         K.gemm_g2(x.data_ptr(), w.data_ptr(), y.data_ptr(), _nbytes(x), _nbytes(w), M, Co, Ci, H, W, OH, OW, sh, sw,
                   _fwd_taps(Ci, W, KH, KW, ph, pw), KH * KW * Ci, Co, OH, OW, 1, 1, 0, 0, ptr(bias), ptr(residual),
-                  ptr(slab), int(relu), stream_ptr())
-        return y, ((slab, rows) if stats else None)
+                  ptr(slab), int(relu), ptr(sums), 2 * Co if stats else 0, stream_ptr())
+        return y, ((slab, rows, sums) if stats else None)
     # generic fallback (odd channel counts): v1 kernels
     y = torch.empty((N, Co, OH, OW), dtype=F32 if out_fp32 else BF16, device=x.device, memory_format=CL)
     slab, rows = None, 0
@@ -106,7 +107,8 @@ def conv2d_fwd(x, w, bias, stride, pad, *, stats=False, residual=None, relu=Fals
     K.gemm_nt(x.data_ptr(), w.data_ptr(), y.data_ptr(), M, Co, KH * KW * Ci, 0, KH * KW * Ci, Co, CONV_FWD,
               N, H, W, Ci, OH, OW, KH, KW, sh, sw, ph, pw, ptr(bias), ptr(residual), ptr(slab),
               int(out_fp32), int(relu), stream_ptr())
-    return y, ((slab, rows) if stats else None)
+    sums = torch.zeros((2 * Co,), dtype=F32, device=x.device) if stats else None
+    return y, ((slab, rows, sums) if stats else None)
 
 
 def to_act_padded(x, cp):
@@ -187,7 +189,7 @@ def conv2d_dgrad(dy, wt, x_shape, stride, pad, *, residual=None):
     st = stream_ptr()
     for ry, rx, GH, GW, taps in classes:
         K.gemm_g2(dy.data_ptr(), wt.data_ptr(), dx.data_ptr(), _nbytes(dy), _nbytes(wt), N * GH * GW, Ci, Co, OH, OW,
-                  GH, GW, 1, 1, taps, KH * KW * Co, Ci, H, W, sh, sw, ry, rx, 0, ptr(residual), 0, 0, st)
+                  GH, GW, 1, 1, taps, KH * KW * Co, Ci, H, W, sh, sw, ry, rx, 0, ptr(residual), 0, 0, 0, 0, st)
     return dx
 
 
@@ -238,7 +240,8 @@ def dense_fwd(x2d, w2d, bias):
     y = torch.empty((N, Out), dtype=BF16, device=x2d.device)
     if _g2_ok(In, Out):
         kernels().gemm_g2(x2d.data_ptr(), w2d.data_ptr(), y.data_ptr(), _nbytes(x2d), _nbytes(w2d), N, Out, In, 1, 1,
-                          1, 1, 1, 1, [(0, 0, 0, 0)], In, Out, 1, 1, 1, 1, 0, 0, ptr(bias), 0, 0, 0, stream_ptr())
+                          1, 1, 1, 1, [(0, 0, 0, 0)], In, Out, 1, 1, 1, 1, 0, 0, ptr(bias), 0, 0, 0, 0, 0,
+                          stream_ptr())
         return y
     kernels().gemm_nt(x2d.data_ptr(), w2d.data_ptr(), y.data_ptr(), N, Out, In, In, In, Out, PLAIN,
                       0, 0, 0, 0, 1, 1, 1, 1, 1, 1, 0, 0, ptr(bias), 0, 0, 0, 0, stream_ptr())
@@ -252,7 +255,8 @@ def dense_dgrad(dy2d, wt2d):
     dx = torch.empty((N, In), dtype=BF16, device=dy2d.device)
     if _g2_ok(Out, In):
         kernels().gemm_g2(dy2d.data_ptr(), wt2d.data_ptr(), dx.data_ptr(), _nbytes(dy2d), _nbytes(wt2d), N, In, Out, 1,
-                          1, 1, 1, 1, 1, [(0, 0, 0, 0)], Out, In, 1, 1, 1, 1, 0, 0, 0, 0, 0, 0, stream_ptr())
+                          1, 1, 1, 1, 1, [(0, 0, 0, 0)], Out, In, 1, 1, 1, 1, 0, 0, 0, 0, 0, 0, 0, 0,
+                          stream_ptr())
         return dx
     kernels().gemm_nt(dy2d.data_ptr(), wt2d.data_ptr(), dx.data_ptr(), N, In, Out, Out, Out, In, PLAIN,
                       0, 0, 0, 0, 1, 1, 1, 1, 1, 1, 0, 0, 0, 0, 0, 0, 0, stream_ptr())
@@ -295,10 +299,10 @@ def bn_stats(x, partial=None):
     if partial is None:
         rows = K.bn_partial_rows(R, C)
         slab = torch.empty((rows, 2, C), dtype=F32, device=x.device)
-        K.bn_partial(dt_code(x.dtype), x.data_ptr(), 0, 0, 0, 0, 0, R, C, slab.data_ptr(), 0, st)
+        sums = torch.empty((2 * C,), dtype=F32, device=x.device)
+        K.bn_partial(dt_code(x.dtype), x.data_ptr(), 0, 0, 0, 0, 0, R, C, slab.data_ptr(), 0, sums.data_ptr(), st)
     else:
-        slab, rows = partial
-    sums = torch.empty((2 * C,), dtype=F32, device=x.device)
+        slab, rows, sums = partial
     K.bn_slab_reduce(slab.data_ptr(), rows, C, sums.data_ptr(), st)
     return sums
 
@@ -326,9 +330,9 @@ def bn_backward(dy, x, yout, mean, istd, gamma, dgamma, dbeta, *, want_masked=Fa
     if not eval_mode:
         rows = K.bn_partial_rows(R, C)
         slab = torch.empty((rows, 2, C), dtype=F32, device=x.device)
-        K.bn_partial(dt, x.data_ptr(), dy.data_ptr(), ptr(yout), ptr(dmask), mean.data_ptr(), istd.data_ptr(), R, C,
-                     slab.data_ptr(), 1, st)
         sums = torch.empty((2 * C,), dtype=F32, device=x.device)
+        K.bn_partial(dt, x.data_ptr(), dy.data_ptr(), ptr(yout), ptr(dmask), mean.data_ptr(), istd.data_ptr(), R, C,
+                     slab.data_ptr(), 1, sums.data_ptr(), st)
         K.bn_slab_reduce(slab.data_ptr(), rows, C, sums.data_ptr(), st)
     elif want_masked and yout is not None:
         dmask = dy * (yout > 0)
@@ -493,6 +497,34 @@ def sgd_step(p, g, vel, shadow, lr, momentum, hyper=None):
 
 def cast_bf16(src, dst):
     kernels().cast_f32_bf16(src.data_ptr(), dst.data_ptr(), src.numel(), stream_ptr())
+
+
+class WeightTransposer:
+    """Regenerates every conv's dgrad operand ([Ci][KH][KW][Co] bf16) from the bf16 shadow
+    weights in ONE kernel launch per step (instead of one launch per conv)."""
+
+    def __init__(self, convs):
+        self.convs = [c for c in convs if c.in_channels % 8 == 0 and c.out_channels % 8 == 0]
+        rows = []
+        self.max_numel = 0
+        for c in self.convs:
+            w = c.weight_operand(0)
+            Co, Ci, KH, KW = w.shape
+            c._wt_buf = torch.empty((Ci, KH, KW, Co), dtype=BF16, device=w.device)
+            rows.append([w.data_ptr(), c._wt_buf.data_ptr(), Co, KH * KW, Ci])
+            self.max_numel = max(self.max_numel, w.numel())
+        self.table = torch.tensor(rows, dtype=torch.int64).to(self.convs[0]._wt_buf.device) if rows else None
+
+    def run(self):
+        if self.table is None:
+            return
+        kernels().multi_weight_transpose(self.table.data_ptr(), len(self.convs), self.max_numel, stream_ptr())
+        for c in self.convs:
+            c._wt_valid = True
+
+    def invalidate(self):
+        for c in self.convs:
+            c._wt_valid = False
 
 
 def im2col(x, kh, kw, sh, sw, ph, pw):

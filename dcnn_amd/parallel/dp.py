@@ -117,6 +117,7 @@ class DataParallel:
         m = self.model
         cur = grad
         flat = m.arena.grad
+        m.prepare_backward()
         for i in range(len(m.layers) - 1, -1, -1):
             t0 = m._prof_begin()
             cur = m.layers[i].backward(cur, mb_id)
@@ -124,6 +125,7 @@ class DataParallel:
             if self.world > 1 and i in self.fire:
                 lo, hi = self.fire[i]
                 self._works.append(dist.all_reduce(flat[lo:hi], op=dist.ReduceOp.SUM, group=self.pg, async_op=True))
+        m.finish_backward()
         if sync:
             self.finish()
         return cur

@@ -95,10 +95,13 @@ class TrainStep:
                     loss, grad, correct = self.loss_fn.loss_and_grad(out, self._static_y)
                     self._g_loss, self._g_correct = loss, correct
                     cur = grad * (1.0 / world) if world > 1 else grad
+                    self.model.prepare_backward()
                 else:
                     cur = self._carry
                 cur = self._run_bwd(cur, hi, lo)
                 self._carry = cur
+                if k == len(segs) - 1:
+                    self.model.finish_backward()
                 if world == 1 and k == len(segs) - 1:
                     self.opt.launch_step()
             if pool is None:
