@@ -44,13 +44,17 @@ def main():
     for (nm, Ci, H, W, Co, k, s, p) in SHAPES:
         x = torch.randn(N, Ci, H, W, device="cuda").bfloat16().contiguous(memory_format=CL)
         w = (torch.randn(Co, Ci, k, k, device="cuda") * 0.05).bfloat16().contiguous(memory_format=CL)
+        wf = w
+        if Ci < 8:  # the RGB stem runs channel-padded to 8 (as Conv2D does)
+            x = hip.to_act_padded(x.float().contiguous(), 8)
+            wf = hip.pad_weight_channels(w, 8)
         OH, OW = (H + 2 * p - k) // s + 1, (W + 2 * p - k) // s + 1
         dy = torch.randn(N, Co, OH, OW, device="cuda").bfloat16().contiguous(memory_format=CL)
         gw = torch.zeros(Co, Ci, k, k, device="cuda").contiguous(memory_format=CL)
         wt = hip.conv_weight_t(w)
         flops = 2.0 * N * OH * OW * Co * Ci * k * k
         ops = {
-            "fwd": lambda: hip.conv2d_fwd(x, w, None, (s, s), (p, p), stats=True),
+            "fwd": lambda: hip.conv2d_fwd(x, wf, None, (s, s), (p, p), stats=True),
             "dgrad": lambda: hip.conv2d_dgrad(dy, wt, x.shape, (s, s), (p, p)),
             "wgrad": lambda: hip.conv2d_wgrad(dy, x, w.shape, (s, s), (p, p), gw, None),
         }

@@ -266,7 +266,7 @@ __device__ __forceinline__ int tr_swz(int row) {
   else return 0;
 }
 
-template <int BM, int BN>
+template <int BM, int BN, bool FAST>
 __global__ void __launch_bounds__(256, 2) gemm_t2_kernel(T2Args p) {
   using T = T2<BM, BN>;
   constexpr int BK = T::BK;
@@ -316,6 +316,20 @@ __global__ void __launch_bounds__(256, 2) gemm_t2_kernel(T2Args p) {
   }
   const int ghw = p.GH * p.GW;
   const float inv_ghw = 1.f / (float)ghw, inv_gw = 1.f / (float)p.GW;
+  // FAST pixel decomposition constants (see stage())
+  int f_dimg[T::B_INS], f_dgy[T::B_INS];
+  unsigned f_xoff[T::B_INS];
+  bool f_xok[T::B_INS];
+#pragma unroll
+  for (int i = 0; i < T::B_INS; ++i) {
+    const int r = b_row[i];
+    int gx;
+    if (ghw % 64 == 0) { f_dimg[i] = 0; f_dgy[i] = r / p.GW; gx = r % p.GW; }
+    else { f_dimg[i] = r / ghw; const int rem = r % ghw; f_dgy[i] = rem / p.GW; gx = rem % p.GW; }
+    const int sx = gx * p.SX + b_dx[i];
+    f_xok[i] = b_ok[i] && sx >= 0 && sx < p.W;
+    f_xoff[i] = (unsigned)(sx * p.Cs * 2) + b_coff[i];
+  }
 
   auto stage = [&](int buf, int k0) {
     char* As = smem + buf * T::STAGE;
@@ -325,6 +339,22 @@ __global__ void __launch_bounds__(256, 2) gemm_t2_kernel(T2Args p) {
       const int pix = k0 + a_row[i];
       const unsigned voff = (pix < kend && a_col[i] != kOOB) ? (unsigned)(pix * p.ldy * 2) + a_col[i] : kOOB;
       glds16(rsA, As + (wid * T::A_INS + i) * 1024, voff);
+    }
+    if constexpr (FAST) {
+      // the 64 pixels of a K-step start at a multiple of 64 and tile whole image rows (or whole
+      // images): per-lane (image, row, col) offsets are constants, only a scalar base moves
+      const int img0 = k0 / ghw;
+      const int gy0 = (k0 - img0 * ghw) / p.GW;
+#pragma unroll
+      for (int i = 0; i < T::B_INS; ++i) {
+        const int pix = k0 + b_row[i];
+        const int img = img0 + f_dimg[i];
+        const int sy = (gy0 + f_dgy[i]) * p.SY + b_dy[i];
+        const bool ok = f_xok[i] && pix < kend && sy >= 0 && sy < p.H;
+        const unsigned voff = ok ? (unsigned)((((long)img * p.H + sy) * p.W) * p.Cs * 2) + f_xoff[i] : kOOB;
+        glds16(rsB, Bs + (wid * T::B_INS + i) * 1024, voff);
+      }
+      return;
     }
 #pragma unroll
     for (int i = 0; i < T::B_INS; ++i) {
@@ -485,10 +515,10 @@ void gemm_g2(const G2Args& a, hipStream_t s) {
   throw std::runtime_error("gemm_g2: no variant");
 }
 
-template <int BM, int BN>
+template <int BM, int BN, bool FAST>
 static void launch_t2(T2Args a, int splits, hipStream_t s) {
   const int tiles = ((a.M + BM - 1) / BM) * ((a.N + BN - 1) / BN);
-  hipLaunchKernelGGL((gemm_t2_kernel<BM, BN>), dim3(tiles * splits), dim3(256), 0, s, a);
+  hipLaunchKernelGGL((gemm_t2_kernel<BM, BN, FAST>), dim3(tiles * splits), dim3(256), 0, s, a);
   DCNN_LAUNCH_CHECK();
 }
 
@@ -518,10 +548,16 @@ void gemm_t2(T2Args a, int splits, hipStream_t s) {
   t2_tile(a.M, a.N, &bm, &bn);
   const int per = (a.P + splits - 1) / splits;
   a.k_per_split = ((per + 63) / 64) * 64;
-  if (bm == 128 && bn == 128) return launch_t2<128, 128>(a, splits, s);
-  if (bm == 128 && bn == 64) return launch_t2<128, 64>(a, splits, s);
-  if (bm == 64 && bn == 128) return launch_t2<64, 128>(a, splits, s);
-  return launch_t2<64, 64>(a, splits, s);
+  const int ghw = a.GH * a.GW;
+  const bool fast = (ghw % 64 == 0 && 64 % a.GW == 0) || (64 % ghw == 0);
+#define DCNN_T2(BM, BN) \
+  if (bm == BM && bn == BN) return fast ? launch_t2<BM, BN, true>(a, splits, s) : launch_t2<BM, BN, false>(a, splits, s)
+  DCNN_T2(128, 128);
+  DCNN_T2(128, 64);
+  DCNN_T2(64, 128);
+  DCNN_T2(64, 64);
+#undef DCNN_T2
+  throw std::runtime_error("gemm_t2: no variant");
 }
 
 }  // namespace dcnn
