@@ -1,0 +1,57 @@
+#!/usr/bin/env python3
+"""Summarise a rocprofv3 kernel trace (rocpd SQLite ``*_results.db`` or ``*_kernel_stats.csv``)
+into a markdown table suitable for ``profiles/``.
+
+Per-step times are normalised by the number of optimizer-kernel dispatches (one per
+training step), so eager warmup steps and graph replays are all counted.
+
+  python tools/prof_summary.py gpurun_out/prof6/run_results.db > profiles/resnet18_b256.md
+"""
+import csv
+import re
+import sqlite3
+import sys
+from collections import defaultdict
+
+
+def _short(name: str) -> str:
+    name = re.sub(r"^void ", "", name)
+    name = re.sub(r"\(.*\)$", "", name)
+    return name[:90]
+
+
+def load(path):
+    rows = defaultdict(lambda: [0, 0.0])
+    if path.endswith(".db"):
+        c = sqlite3.connect(path)
+        for name, dur in c.execute("select name, duration from kernels"):
+            r = rows[_short(name)]
+            r[0] += 1
+            r[1] += dur / 1e3  # ns -> us
+    else:
+        with open(path) as f:
+            for d in csv.DictReader(f):
+                r = rows[_short(d["Name"])]
+                r[0] += int(d["Calls"])
+                r[1] += float(d["TotalDurationNs"]) / 1e3
+    return rows
+
+
+def main():
+    path = sys.argv[1]
+    rows = load(path)
+    steps = sum(v[0] for k, v in rows.items() if "adam_kernel" in k or "sgd_kernel" in k) or 1
+    total = sum(v[1] for v in rows.values())
+    print(f"# Kernel summary: `{path}`\n")
+    print(f"optimizer dispatches (= training steps traced): {steps}; total GPU kernel time {total / 1e3:.2f} ms; "
+          f"**{total / steps / 1e3:.3f} ms kernel time per step**\n")
+    print("| kernel | calls | calls/step | total ms | us/step | % |")
+    print("|---|---:|---:|---:|---:|---:|")
+    for k, (n, us) in sorted(rows.items(), key=lambda kv: -kv[1][1]):
+        if us / total < 0.002:
+            continue
+        print(f"| `{k}` | {n} | {n / steps:.1f} | {us / 1e3:.2f} | {us / steps:.1f} | {100 * us / total:.1f} |")
+
+
+if __name__ == "__main__":
+    main()
