@@ -122,7 +122,7 @@ def build_native(force=False, verbose=False, max_workers=None):
     target = PKG / f"{name}{EXT_SUFFIX}"
     if force or not target.exists() or any(o.stat().st_mtime > target.stat().st_mtime for o in objs):
         link_flags = [f"-fsanitize={san}"] if san else []
-        _run([cxx, "-shared", "-fPIC", "-pthread", *link_flags, *map(str, objs), "-o", str(target)],
+        _run([cxx, "-shared", "-fPIC", "-pthread", *link_flags, *map(str, objs), "-o", str(target), "-lz", "-ldl"],
              verbose)
     return target
 

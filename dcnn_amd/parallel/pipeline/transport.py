@@ -1,0 +1,156 @@
+"""Pipeline data plane: how FORWARD_JOB / BACKWARD_JOB tensors move between stages.
+
+* ``MessageTransport`` — tensors inline in the control message (host copy; TCP between
+  machines or processes without RCCL).  The reference's only mode
+  (include/pipeline/binary_serializer.hpp:27-35).
+* ``LocalTransport`` — peers in the same process (in-process coordinator, or coordinator +
+  stage 0 sharing a rank): the tensor object is handed over through a process-wide mailbox,
+  the message carries only metadata; a device change is one ``.to()`` (xGMI peer copy
+  between GPUs).
+* ``P2PTransport`` — one process per GPU under ``torch.distributed``: metadata rides the
+  control plane, bytes go device-to-device with ``isend``/``irecv`` (RCCL over xGMI with the
+  "nccl" backend, gloo on CPU).  Forward activations and backward gradients use *separate*
+  process groups (separate RCCL communicators and streams), so a stage that interleaves
+  forward and backward micro-batches can never head-of-line block a peer; the coordinator's
+  traffic gets its own pair of groups as well.  Peers living in the same rank fall back to
+  the local mailbox.
+"""
+from __future__ import annotations
+
+import threading
+from collections import deque
+from typing import Dict, Optional
+
+import torch
+import torch.distributed as dist
+
+from . import messages as M
+
+
+class _Mailbox:
+    def __init__(self):
+        self._d: Dict = {}
+        self._cv = threading.Condition()
+
+    def put(self, key, t):
+        with self._cv:
+            self._d.setdefault(key, deque()).append(t)
+            self._cv.notify_all()
+
+    def take(self, key, timeout=60.0):
+        with self._cv:
+            ok = self._cv.wait_for(lambda: bool(self._d.get(key)), timeout)
+            if not ok:
+                raise TimeoutError(f"local mailbox: no tensor for {key}")
+            q = self._d[key]
+            t = q.popleft()
+            if not q:
+                del self._d[key]
+            return t
+
+
+MAILBOX = _Mailbox()
+
+
+class Transport:
+    """send(comm, recipient, command, mb_id, tensor) / recv(msg, device)."""
+
+    def send(self, comm, recipient: str, command: int, mb_id: int, t: Optional[torch.Tensor]) -> None:
+        raise NotImplementedError
+
+    def recv(self, msg, device) -> Optional[torch.Tensor]:
+        raise NotImplementedError
+
+    def flush(self) -> None:
+        pass
+
+
+class MessageTransport(Transport):
+    def __init__(self, codec: str = "none", legacy: bool = False):
+        self.codec = codec
+        self.legacy = legacy
+
+    def send(self, comm, recipient, command, mb_id, t):
+        comm.send(M.job_message(recipient, command, mb_id, t, self.codec, self.legacy))
+
+    def recv(self, msg, device):
+        return M.message_tensor(msg, device)
+
+
+class LocalTransport(Transport):
+    """Tensor objects through the process mailbox; key = (recipient comm id, command, mb)."""
+
+    def __init__(self, my_id: str, resolve=None):
+        self.my_id = my_id
+        self.resolve = resolve or (lambda name: name)
+
+    def send(self, comm, recipient, command, mb_id, t):
+        target = self.resolve(recipient)
+        if t is not None:
+            MAILBOX.put((target, int(command), int(mb_id)), t)
+        comm.send(M.meta_message(recipient, command, mb_id, t))
+
+    def recv(self, msg, device):
+        if not M.has_tensor(msg):
+            return None
+        t = MAILBOX.take((self.my_id, int(msg.command), int(msg.mb_id)))
+        return t.to(device) if device is not None and t.device != torch.device(device) else t
+
+
+class P2PTransport(Transport):
+    """torch.distributed point-to-point data plane (RCCL on GPU, gloo on CPU)."""
+
+    def __init__(self, my_id: str, ranks: Dict[str, int], groups: Dict[str, object], resolve=None):
+        self.my_id = my_id
+        self.ranks = dict(ranks)          # logical name / comm id -> rank
+        self.groups = groups              # {"fwd", "bwd", "cfwd", "cbwd"}
+        self.rank = dist.get_rank()
+        self.local = LocalTransport(my_id, resolve)
+        self._pending = deque()
+
+    def _group(self, command, peer_name):
+        coord = "coordinator" in (peer_name, self.my_id)
+        if int(command) == M.CommandType.FORWARD_JOB:
+            return self.groups["cfwd" if coord else "fwd"]
+        return self.groups["cbwd" if coord else "bwd"]
+
+    def _prune(self):
+        while self._pending and self._pending[0][0].is_completed():
+            self._pending.popleft()
+
+    def send(self, comm, recipient, command, mb_id, t):
+        dst = self.ranks[recipient]
+        if dst == self.rank:
+            self.local.send(comm, recipient, command, mb_id, t)
+            return
+        if t is not None:
+            phys, _ = M._physical(t.detach())
+            if not phys.is_contiguous():
+                phys = phys.contiguous()
+            w = dist.isend(phys, dst, group=self._group(command, recipient))
+            self._pending.append((w, phys))
+            self._prune()
+        comm.send(M.meta_message(recipient, command, mb_id, t))
+
+    def recv(self, msg, device):
+        if not M.has_tensor(msg):
+            return None
+        src_name = msg.sender
+        src = self.ranks.get(src_name)
+        if src is None or src == self.rank:
+            return self.local.recv(msg, device)
+        dev = torch.device(device) if device is not None else torch.device("cpu")
+        phys, logical = M.alloc_for(msg, dev)
+        dist.irecv(phys, src, group=self._group(msg.command, src_name)).wait()
+        return logical
+
+    def flush(self):
+        while self._pending:
+            w, _ = self._pending.popleft()
+            w.wait()
+
+
+def make_groups(backend: Optional[str] = None) -> Dict[str, object]:
+    """Create the four P2P process groups (all ranks must call this in the same order)."""
+    world = list(range(dist.get_world_size()))
+    return {k: dist.new_group(world, backend=backend) for k in ("fwd", "bwd", "cfwd", "cbwd")}

@@ -1,0 +1,170 @@
+"""Pipeline parallelism: partitioners, in-process coordinator parity with single-process
+micro-batched training, control commands, and the multi-process TCP + gloo-P2P path."""
+import json
+import os
+import subprocess
+import sys
+
+import pytest
+import torch
+
+from dcnn_amd.models import zoo
+from dcnn_amd.nn.loss import LossFactory
+from dcnn_amd.nn.optimizers import SGD, Adam
+from dcnn_amd.nn.sequential import Partition
+from dcnn_amd.parallel.pipeline import (FlopPartitioner, InProcessCoordinator, NaivePartitioner, StageConfig,
+                                        Endpoint, balanced_split)
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def test_naive_partitioner_matches_reference_rule():
+    m = zoo.create_model("resnet18_tiny_imagenet")
+    L = len(m.layers)
+    parts = NaivePartitioner().get_partitions(m, 3)
+    base, rem = divmod(L, 3)
+    sizes = [p.end_layer - p.start_layer for p in parts]
+    assert sizes == [base + (1 if i < rem else 0) for i in range(3)]
+    assert parts[0].start_layer == 0 and parts[-1].end_layer == L
+
+
+def test_balanced_split_is_optimal():
+    costs = [5, 1, 1, 1, 8, 2, 2]
+    parts = balanced_split(costs, 3)
+    sums = [sum(costs[p.start_layer:p.end_layer]) for p in parts]
+    assert max(sums) == 8
+    assert [(p.start_layer, p.end_layer) for p in parts][-1][1] == len(costs)
+
+
+def test_flop_partitioner_balances_better_than_naive():
+    m = zoo.create_model("resnet50_tiny_imagenet")
+    shape = [32, 3, 64, 64]
+    f = [a + b for a, b in zip(m.forward_complexity(shape), m.backward_complexity(shape))]
+
+    def worst(parts):
+        return max(sum(f[p.start_layer:p.end_layer]) for p in parts)
+
+    flop = FlopPartitioner(shape).get_partitions(m, 4)
+    naive = NaivePartitioner().get_partitions(m, 4)
+    assert worst(flop) <= worst(naive)
+
+
+def test_stage_config_json_roundtrip():
+    c = StageConfig("stage_1", 1, 2, {"name": "m", "layers": []}, {"type": "adam", "parameters": {}},
+                    next_stage_endpoint=Endpoint.network("127.0.0.1", 9000),
+                    coordinator_endpoint=Endpoint.in_process("coord"), ranks={"coordinator": 0})
+    d = StageConfig.from_json(c.dumps())
+    assert d.next_stage_endpoint.get("port") == 9000
+    assert d.coordinator_endpoint.communication_type == "in_process"
+    assert d.prev_stage_endpoint is None and d.ranks == {"coordinator": 0}
+
+
+def _reference_microbatched(model, x, y, m, opt, lossname="softmax_crossentropy", scale=True):
+    lf = LossFactory.create(lossname)
+    if not opt.params:
+        opt.attach(model)
+    n = x.shape[0] // m
+    tot = 0.0
+    for i in range(m):
+        out = model.forward(x[i * n:(i + 1) * n], i)
+        l, g, _ = lf.loss_and_grad(out, y[i * n:(i + 1) * n])
+        tot += float(l)
+        model.backward(g / m if scale else g, i)
+    opt.update()
+    opt.clear_gradients()
+    return tot / m
+
+
+@pytest.mark.parametrize("schedule", ["sync", "semi_async"])
+@pytest.mark.parametrize("transport", ["local", "message"])
+def test_inprocess_pipeline_matches_single_process(schedule, transport):
+    torch.manual_seed(0)
+    model = zoo.create_model("resnet9_cifar10")
+    model.set_seed(3)
+    model.initialize()
+    ref = model.clone()
+    ref.initialize()
+    ref.load_parameters([p.clone() for p in model.parameters()])
+    x = torch.randn(8, 3, 32, 32)
+    y = torch.randint(0, 10, (8,))
+    coord = InProcessCoordinator(model, Adam(1e-3), "softmax_crossentropy", num_stages=3, num_microbatches=4,
+                                 transport=transport)
+    try:
+        coord.initialize()
+        coord.deploy_stages()
+        coord.send_parameters(model)
+        coord.start()
+        losses = [coord.train_step(x, y, schedule) for _ in range(2)]
+        ref_opt = Adam(1e-3)
+        ref_losses = [_reference_microbatched(ref, x, y, 4, ref_opt) for _ in range(2)]
+        assert losses == pytest.approx(ref_losses, rel=1e-5)
+        got = coord.gather_model()
+        for a, b in zip(got.parameters(), ref.parameters()):
+            torch.testing.assert_close(a, b, rtol=1e-5, atol=1e-6)
+    finally:
+        coord.stop()
+
+
+def test_inprocess_control_commands(tmp_path):
+    model = zoo.create_model("mnist_cnn")
+    coord = InProcessCoordinator(model, SGD(0.05), "softmax_crossentropy", num_stages=2, num_microbatches=2,
+                                 partitioner=FlopPartitioner([2, 1, 28, 28]))
+    try:
+        coord.initialize()
+        coord.deploy_stages()
+        coord.start()
+        x, y = torch.randn(4, 1, 28, 28), torch.randint(0, 10, (4,))
+        coord.train_step(x, y)
+        assert coord.health_check() == {"stage_0": True, "stage_1": True}
+        st = coord.status()
+        assert [s["counts"]["forward"] for s in st] == [2, 2]
+        assert [s["counts"]["update"] for s in st] == [1, 1]
+        loads = coord.load_reports()
+        assert set(loads) == {"stage_0", "stage_1"} and all(v[0] > 0 for v in loads.values())
+        coord.barrier()
+        loss, correct = coord.evaluate_batch(x, y)
+        assert loss > 0 and 0 <= correct <= 4
+        # learning-rate change reaches every stage
+        coord.set_learning_rate(0.01)
+        coord.train_step(x, y)
+        assert all(s.optimizer.get_learning_rate() == pytest.approx(0.01) for s in coord.stages)
+        # checkpoint gathered at the coordinator round-trips through the reference format
+        path = str(tmp_path / "pipe_ckpt")
+        coord.save_checkpoint(path)
+        from dcnn_amd.nn.sequential import Sequential
+        re = Sequential.from_file(path)
+        for a, b in zip(re.parameters(), coord.model.parameters()):
+            torch.testing.assert_close(a, b)
+        coord.clear_profiling_data()
+    finally:
+        coord.stop()
+
+
+def test_stage_error_is_reported():
+    from dcnn_amd.parallel.pipeline import PipelineError
+    model = zoo.create_model("mnist_cnn")
+    coord = InProcessCoordinator(model, SGD(0.05), "softmax_crossentropy", num_stages=2, num_microbatches=1)
+    try:
+        coord.initialize()
+        coord.deploy_stages()
+        with pytest.raises(PipelineError):
+            coord.train_step(torch.randn(2, 3, 5, 5), torch.randint(0, 10, (2,)))  # wrong input shape
+    finally:
+        coord.stop()
+
+
+@pytest.mark.parametrize("transport,schedule", [("p2p", "semi_async"), ("message", "sync")])
+def test_multiprocess_pipeline_gloo(transport, schedule):
+    """3 processes (coordinator co-located with stage 0) over TCP control + gloo P2P data."""
+    port = 29800 + (0 if transport == "p2p" else 40)
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "3",
+           "--master-addr", "127.0.0.1", "--master-port", str(port - 100),
+           "-m", "dcnn_amd.parallel.pipeline.launch", "--model", "mnist_cnn", "--batch", "8",
+           "--microbatches", "4", "--steps", "2", "--warmup", "1", "--cpu", "--base-port", str(port),
+           "--transport", transport, "--schedule", schedule]
+    env = dict(os.environ, PYTHONPATH=ROOT, OMP_NUM_THREADS="1")
+    r = subprocess.run(cmd, cwd=ROOT, env=env, capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-3000:]
+    line = [l for l in r.stdout.splitlines() if l.startswith("{") and "pipeline" in l][-1]
+    d = json.loads(line)
+    assert d["stages"] == 3 and d["value"] > 0 and d["loss"] == d["loss"]
