@@ -30,7 +30,11 @@ double cpu_utilization_total(int sample_ms);
 long process_rss_kb();
 std::vector<std::pair<std::string, double>> thermal_zones();
 
-// affinity.cpp
+// jpeg.cpp — baseline Huffman JPEG -> interleaved RGB8
+bool decode_jpeg(const unsigned char* data, size_t n, std::vector<unsigned char>& rgb, int& w, int& h,
+                 std::string* err);
+
+// affinity (hwinfo.cpp)
 int set_thread_affinity(const std::vector<int>& cpus);
 std::vector<int> get_thread_affinity();
 
