@@ -40,6 +40,8 @@ def main():
     ap.add_argument("--bucket-mb", type=float, default=32.0)
     ap.add_argument("--profile", action="store_true", help="print per-layer device times")
     ap.add_argument("--device", default="cuda")
+    ap.add_argument("--dtype", default="bf16", choices=["bf16", "fp32"],
+                    help="compute dtype (fp32: the MFMA f32 path, e.g. the ResNet-9 CIFAR-10 fp32 config)")
     a = ap.parse_args()
 
     from dcnn_amd.parallel.dp import DataParallel, init_distributed
@@ -57,6 +59,8 @@ def main():
     model = create_model(a.model)
     model.set_seed(1234)
     model.set_device(f"GPU:{local}" if dev.type == "cuda" else "CPU")
+    if a.dtype == "fp32" and dev.type == "cuda":
+        model.set_compute_dtype(torch.float32)
     model.initialize()
     model.set_first_layer_input_grad(False)
     dp = DataParallel(model, bucket_mb=a.bucket_mb)
@@ -104,7 +108,7 @@ def main():
         print(json.dumps({
             "metric": METRIC, "value": round(imgs, 2), "unit": "images/sec", "n_gpus": world, "steps": a.steps,
             "warmup": a.warmup, "ms_per_step": round(ms, 4), "higher_is_better": True, "scaling": "weak",
-            "vs_baseline": None, "dtype": "bf16", "data": "synthetic (random 64x64 RGB + random labels, random init)",
+            "vs_baseline": None, "dtype": a.dtype if dev.type == "cuda" else "fp32", "data": "synthetic (random 64x64 RGB + random labels, random init)",
             "config": {"model": a.model, "global_batch": a.batch * world, "per_gpu_batch": a.batch, "seq_len": None,
                        "image_size": [C, H, W], "parallelism": f"dp{world}", "optimizer": "adam",
                        "hipgraph": bool(step.use_graph), "final_loss": round(loss_val, 4)},

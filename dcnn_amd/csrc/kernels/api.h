@@ -40,6 +40,12 @@ int gemm_g2_stat_rows(int M, int N);
 void gemm_t2(T2Args a, int splits, hipStream_t s);
 int gemm_t2_splits(int M, int N, int P);
 int gemm_nt_stat_rows(int M, int N);
+// fp32 path (gemm_f32.hip): same argument structs, fp32 operand/result pointers
+void gemm_g2f(const G2Args& a, hipStream_t s);
+int gemm_g2f_stat_rows(int M, int N);
+void gemm_t2f(T2Args a, int splits, hipStream_t s);
+int gemm_t2f_splits(int M, int N, int P);
+void conv_weight_transpose_f32(const float* w, float* wt, int Co, int T_, int Ci, hipStream_t s);
 void gemm_tn(TnArgs a, int splits, hipStream_t s);
 int gemm_tn_splits(int M, int N, int P);
 void splitk_reduce(const float* slab, float* out, long n, int splits, int accumulate, hipStream_t s);

@@ -32,6 +32,42 @@ PYBIND11_MODULE(_kernels, m) {
           gemm_nt(a, S(stream));
         });
   m.def("gemm_nt_stat_rows", &gemm_nt_stat_rows);
+  m.def("gemm_g2f",
+        [](uintptr_t A, uintptr_t B, uintptr_t C, unsigned a_bytes, unsigned b_bytes, int M, int N, int Cs, int H,
+           int W, int GH, int GW, int SY, int SX, std::vector<std::array<int, 4>> taps, int ldb, int ldc, int OH,
+           int OW, int OSY, int OSX, int ORY, int ORX, uintptr_t bias, uintptr_t residual, uintptr_t stats, int relu,
+           uintptr_t zero_ptr, int zero_n, uintptr_t stream) {
+          G2Args a{};  // fp32 operands (pointers reinterpreted by the kernel)
+          a.A = P<const bf16*>(A); a.B = P<const bf16*>(B); a.C = P<bf16*>(C);
+          a.a_bytes = a_bytes; a.b_bytes = b_bytes;
+          a.M = M; a.N = N; a.Cs = Cs; a.H = H; a.W = W; a.GH = GH; a.GW = GW; a.SY = SY; a.SX = SX;
+          if (taps.size() > 64) throw std::runtime_error("gemm_g2f: more than 64 taps");
+          a.ntaps = (int)taps.size();
+          for (size_t i = 0; i < taps.size(); ++i) {
+            a.tap_dy[i] = taps[i][0]; a.tap_dx[i] = taps[i][1]; a.tap_srcoff[i] = taps[i][2]; a.tap_b[i] = taps[i][3];
+          }
+          a.ldb = ldb; a.ldc = ldc; a.OH = OH; a.OW = OW; a.OSY = OSY; a.OSX = OSX; a.ORY = ORY; a.ORX = ORX;
+          a.bias = P<const float*>(bias); a.residual = P<const bf16*>(residual); a.stats = P<float*>(stats); a.relu = relu;
+          a.zero_ptr = P<float*>(zero_ptr); a.zero_n = zero_n;
+          gemm_g2f(a, S(stream));
+        });
+  m.def("gemm_g2f_stat_rows", &gemm_g2f_stat_rows);
+  m.def("gemm_t2f",
+        [](uintptr_t dY, uintptr_t X, uintptr_t slab, uintptr_t bias_slab, int M, int N, int Pn, int ldy, int Cs,
+           int H, int W, int GH, int GW, int SY, int SX, std::vector<std::array<int, 2>> taps, int splits,
+           uintptr_t stream) {
+          T2Args a{};
+          a.dY = P<const bf16*>(dY); a.X = P<const bf16*>(X); a.slab = P<float*>(slab); a.bias_slab = P<float*>(bias_slab);
+          a.M = M; a.N = N; a.P = Pn; a.ldy = ldy; a.Cs = Cs; a.H = H; a.W = W; a.GH = GH; a.GW = GW; a.SY = SY; a.SX = SX;
+          if (taps.size() > 64) throw std::runtime_error("gemm_t2f: more than 64 taps");
+          a.ntaps = (int)taps.size();
+          for (size_t i = 0; i < taps.size(); ++i) { a.tap_dy[i] = taps[i][0]; a.tap_dx[i] = taps[i][1]; }
+          gemm_t2f(a, splits, S(stream));
+        });
+  m.def("gemm_t2f_splits", &gemm_t2f_splits);
+  m.def("conv_weight_transpose_f32", [](uintptr_t w, uintptr_t wt, int Co, int T_, int Ci, uintptr_t st) {
+    conv_weight_transpose_f32(P<const float*>(w), P<float*>(wt), Co, T_, Ci, S(st));
+  });
   m.def("gemm_g2",
         [](uintptr_t A, uintptr_t B, uintptr_t C, unsigned a_bytes, unsigned b_bytes, int M, int N, int Cs, int H,
            int W, int GH, int GW, int SY, int SX, std::vector<std::array<int, 4>> taps, int ldb, int ldc, int OH,

@@ -1,0 +1,329 @@
+// fp32 implicit-GEMM convolution / dense kernels on CDNA4 MFMA (v_mfma_f32_16x16x4_f32).
+//
+// The fp32 compute path (the reference's only precision; BASELINE config "CIFAR-10 ResNet-9
+// fp32") uses the same gathered-GEMM formulation and host-side tap tables as the bf16 v2
+// kernels (gemm2.hip) — conv forward, phase-decomposed dgrad and dense share one NT kernel,
+// weight gradients one split-K TN kernel — with fp32 operands end to end:
+//
+// * 64x64 output tile, 256 threads (2x2 waves, 32x32 per wave = 2x2 MFMA 16x16 subtiles),
+//   BK = 16 reduction elements per stage; global float4 loads are register-staged one stage
+//   ahead (loads of tile k+1 overlap the MFMAs of tile k).
+// * Each lane reads one float4 of A and of B per 16-wide K block from LDS and issues four
+//   16x16x4 MFMAs (k permuted consistently between operands, so the sum is unchanged).
+// * Padding / out-of-image taps are zero-filled from a per-row tap-validity mask.
+// * Epilogue: bias, residual add, ReLU and per-channel BatchNorm (sum, sum^2) partials, with
+//   the strided output-row scatter of a dgrad phase.
+#include "common.h"
+#include "api.h"
+
+namespace dcnn {
+
+namespace {
+constexpr int FBM = 64, FBN = 64, FBK = 16, FPITCH = FBK + 4;  // LDS row pitch (floats): conflict-free b128 reads
+
+__device__ __forceinline__ int xcd_remap_f(int bid, int nwg) {
+  const int xcd = bid & 7, q = nwg >> 3, r = nwg & 7;
+  const int base = xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q;
+  return base + (bid >> 3);
+}
+
+__device__ __forceinline__ f32x4 mfma4(const float4& a, const float4& b, f32x4 c) {
+  c = __builtin_amdgcn_mfma_f32_16x16x4f32(a.x, b.x, c, 0, 0, 0);
+  c = __builtin_amdgcn_mfma_f32_16x16x4f32(a.y, b.y, c, 0, 0, 0);
+  c = __builtin_amdgcn_mfma_f32_16x16x4f32(a.z, b.z, c, 0, 0, 0);
+  c = __builtin_amdgcn_mfma_f32_16x16x4f32(a.w, b.w, c, 0, 0, 0);
+  return c;
+}
+}  // namespace
+
+// C[m][n] = sum_{t, c} Src[pix(m) + tap t][c] * B[n][tap_b[t] + c]   (G2Args semantics, fp32)
+__global__ void __launch_bounds__(256, 2) gemm_g2f_kernel(G2Args p) {
+  __shared__ __attribute__((aligned(16))) float As[2][FBM * FPITCH];
+  __shared__ __attribute__((aligned(16))) float Bs[2][FBN * FPITCH];
+  __shared__ float red[2][FBN];
+  const float* A = reinterpret_cast<const float*>(p.A);
+  const float* B = reinterpret_cast<const float*>(p.B);
+  float* C = reinterpret_cast<float*>(p.C);
+  const float* R = reinterpret_cast<const float*>(p.residual);
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int wm = wid >> 1, wn = wid & 1;
+  const int tiles_n = (p.N + FBN - 1) / FBN;
+  const int lt = xcd_remap_f(blockIdx.x, gridDim.x);
+  const int tm = lt / tiles_n, tn = lt % tiles_n;
+  const int m0 = tm * FBM, n0 = tn * FBN;
+  if (p.zero_ptr && blockIdx.x == 0)
+    for (int i = tid; i < p.zero_n; i += 256) p.zero_ptr[i] = 0.f;
+
+  // this thread loads row lr, float4 chunk lc (4 chunks of 4 floats = BK 16)
+  const int lr = tid >> 2, lc = tid & 3;
+  long a_base = 0;
+  uint64_t a_mask = 0;
+  {
+    const int m = m0 + lr;
+    if (m < p.M) {
+      const int ghw = p.GH * p.GW;
+      const int img = m / ghw, rem = m - img * ghw;
+      const int gy = rem / p.GW, gx = rem - gy * p.GW;
+      const int y0 = gy * p.SY, x0 = gx * p.SX;
+      a_base = (((long)img * p.H + y0) * p.W + x0) * p.Cs;
+      for (int t = 0; t < p.ntaps; ++t) {
+        const int sy = y0 + p.tap_dy[t], sx = x0 + p.tap_dx[t];
+        if (sy >= 0 && sy < p.H && sx >= 0 && sx < p.W) a_mask |= (1ull << t);
+      }
+    }
+  }
+  const int bn_row = n0 + lr;
+  const bool b_ok = bn_row < p.N;
+  const long b_base = (long)bn_row * p.ldb;
+  const bool vec = (p.Cs & 3) == 0;
+
+  auto load = [&](int k0, float4& ra, float4& rb) {
+    float va[4], vb[4];
+#pragma unroll
+    for (int e = 0; e < 4; ++e) { va[e] = 0.f; vb[e] = 0.f; }
+    const int k = k0 + lc * 4;
+    if (vec) {  // the 4 elements share one tap
+      const int t = k / p.Cs, c = k - t * p.Cs;
+      if (t < p.ntaps) {
+        if ((a_mask >> t) & 1ull) {
+          const float4 v = *reinterpret_cast<const float4*>(A + a_base + p.tap_srcoff[t] + c);
+          va[0] = v.x; va[1] = v.y; va[2] = v.z; va[3] = v.w;
+        }
+        if (b_ok) {
+          const float4 v = *reinterpret_cast<const float4*>(B + b_base + p.tap_b[t] + c);
+          vb[0] = v.x; vb[1] = v.y; vb[2] = v.z; vb[3] = v.w;
+        }
+      }
+    } else {
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const int kk = k + e, t = kk / p.Cs, c = kk - t * p.Cs;
+        if (t < p.ntaps) {
+          if ((a_mask >> t) & 1ull) va[e] = A[a_base + p.tap_srcoff[t] + c];
+          if (b_ok) vb[e] = B[b_base + p.tap_b[t] + c];
+        }
+      }
+    }
+    ra = make_float4(va[0], va[1], va[2], va[3]);
+    rb = make_float4(vb[0], vb[1], vb[2], vb[3]);
+  };
+
+  f32x4 acc[2][2];
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int j = 0; j < 2; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  const int K = p.ntaps * p.Cs;
+  const int nk = (K + FBK - 1) / FBK;
+  float4 ra, rb;
+  load(0, ra, rb);
+  int cur = 0;
+  for (int kt = 0; kt < nk; ++kt) {
+    *reinterpret_cast<float4*>(&As[cur][lr * FPITCH + lc * 4]) = ra;
+    *reinterpret_cast<float4*>(&Bs[cur][lr * FPITCH + lc * 4]) = rb;
+    __syncthreads();
+    if (kt + 1 < nk) load((kt + 1) * FBK, ra, rb);
+    const int g = lane >> 4;
+    float4 a[2], b[2];
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+      a[i] = *reinterpret_cast<const float4*>(&As[cur][(wm * 32 + i * 16 + (lane & 15)) * FPITCH + g * 4]);
+#pragma unroll
+    for (int j = 0; j < 2; ++j)
+      b[j] = *reinterpret_cast<const float4*>(&Bs[cur][(wn * 32 + j * 16 + (lane & 15)) * FPITCH + g * 4]);
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+      for (int j = 0; j < 2; ++j) acc[i][j] = mfma4(a[i], b[j], acc[i][j]);
+    cur ^= 1;
+  }
+
+  // ---- epilogue straight from the accumulators: lane owns column (lane&15) of each subtile ----
+  if (p.stats && tid < 2 * FBN) (&red[0][0])[tid] = 0.f;
+  if (p.stats) __syncthreads();
+  const int ghw = p.GH * p.GW;
+#pragma unroll
+  for (int j = 0; j < 2; ++j) {
+    const int col = n0 + wn * 32 + j * 16 + (lane & 15);
+    const bool cok = col < p.N;
+    const float bv = (p.bias && cok) ? p.bias[col] : 0.f;
+    float s = 0.f, q = 0.f;
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int m = m0 + wm * 32 + i * 16 + (lane >> 4) * 4 + r;
+        if (m >= p.M || !cok) continue;
+        const int img = m / ghw, rem = m - img * ghw;
+        const int gy = rem / p.GW, gx = rem - gy * p.GW;
+        const long orow = ((long)img * p.OH + gy * p.OSY + p.ORY) * p.OW + gx * p.OSX + p.ORX;
+        float v = acc[i][j][r] + bv;
+        if (R) v += R[orow * p.ldc + col];
+        if (p.relu) v = fmaxf(v, 0.f);
+        C[orow * p.ldc + col] = v;
+        s += v;
+        q += v * v;
+      }
+    if (p.stats && cok) {
+      atomicAdd(&red[0][wn * 32 + j * 16 + (lane & 15)], s);
+      atomicAdd(&red[1][wn * 32 + j * 16 + (lane & 15)], q);
+    }
+  }
+  if (p.stats) {
+    __syncthreads();
+    if (tid < 2 * FBN) {
+      const int which = tid / FBN, cc = tid % FBN;
+      if (n0 + cc < p.N) p.stats[((long)tm * 2 + which) * p.N + n0 + cc] = red[which][cc];
+    }
+  }
+}
+
+// dW[m][n] (+ bias grad) = sum_p dY[p][m] * X[gather(p, tap(n))][c(n)] over this split's pixels
+__global__ void __launch_bounds__(256, 2) gemm_t2f_kernel(T2Args p) {
+  __shared__ __attribute__((aligned(16))) float As[FBM * FPITCH];  // [m][k]
+  __shared__ __attribute__((aligned(16))) float Bs[FBN * FPITCH];  // [n][k]
+  const float* dY = reinterpret_cast<const float*>(p.dY);
+  const float* X = reinterpret_cast<const float*>(p.X);
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int wm = wid >> 1, wn = wid & 1;
+  const int tiles_m = (p.M + FBM - 1) / FBM, tiles_n = (p.N + FBN - 1) / FBN;
+  const int tiles = tiles_m * tiles_n;
+  const int lt = xcd_remap_f(blockIdx.x, gridDim.x);
+  const int split = lt / tiles, tt = lt % tiles;
+  const int tm = tt / tiles_n, tn = tt % tiles_n;
+  const int m0 = tm * FBM, n0 = tn * FBN;
+  const long pbeg = (long)split * p.k_per_split;
+  const long pend = pbeg + p.k_per_split < p.P ? pbeg + p.k_per_split : p.P;
+
+  // loader: pixel row lk (0..15), 4 consecutive columns starting at 4*lq (0..15)
+  const int lk = tid >> 4, lq = tid & 15;
+  const int am = m0 + lq * 4;        // dY columns
+  const int bn = n0 + lq * 4;        // (tap, c) columns
+  const bool vecA = (p.ldy & 3) == 0 && am + 3 < p.M;
+  const bool vecB = (p.Cs & 3) == 0 && bn + 3 < p.N;
+  float bias_acc = 0.f;
+
+  f32x4 acc[2][2];
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int j = 0; j < 2; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  const int ghw = p.GH * p.GW;
+  for (long k0 = pbeg; k0 < pend; k0 += FBK) {
+    const long pix = k0 + lk;
+    float va[4] = {0.f, 0.f, 0.f, 0.f}, vb[4] = {0.f, 0.f, 0.f, 0.f};
+    if (pix < pend) {
+      if (vecA) {
+        const float4 v = *reinterpret_cast<const float4*>(dY + pix * p.ldy + am);
+        va[0] = v.x; va[1] = v.y; va[2] = v.z; va[3] = v.w;
+      } else {
+#pragma unroll
+        for (int e = 0; e < 4; ++e)
+          if (am + e < p.M) va[e] = dY[pix * p.ldy + am + e];
+      }
+      const int img = (int)(pix / ghw), rem = (int)(pix - (long)img * ghw);
+      const int gy = rem / p.GW, gx = rem - gy * p.GW;
+      const int y0 = gy * p.SY, x0 = gx * p.SX;
+      if (vecB) {
+        const int t = bn / p.Cs, c = bn - t * p.Cs;
+        const int sy = y0 + p.tap_dy[t], sx = x0 + p.tap_dx[t];
+        if (sy >= 0 && sy < p.H && sx >= 0 && sx < p.W) {
+          const float4 v = *reinterpret_cast<const float4*>(X + (((long)img * p.H + sy) * p.W + sx) * p.Cs + c);
+          vb[0] = v.x; vb[1] = v.y; vb[2] = v.z; vb[3] = v.w;
+        }
+      } else {
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const int n = bn + e;
+          if (n >= p.N) continue;
+          const int t = n / p.Cs, c = n - t * p.Cs;
+          const int sy = y0 + p.tap_dy[t], sx = x0 + p.tap_dx[t];
+          if (sy >= 0 && sy < p.H && sx >= 0 && sx < p.W) vb[e] = X[(((long)img * p.H + sy) * p.W + sx) * p.Cs + c];
+        }
+      }
+    }
+    __syncthreads();  // previous tile fully consumed
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      As[(lq * 4 + e) * FPITCH + lk] = va[e];
+      Bs[(lq * 4 + e) * FPITCH + lk] = vb[e];
+    }
+    __syncthreads();
+    if (p.bias_slab && tn == 0 && tid < FBM) {
+#pragma unroll
+      for (int k = 0; k < FBK; ++k) bias_acc += As[tid * FPITCH + k];
+    }
+    const int g = lane >> 4;
+    float4 a[2], b[2];
+#pragma unroll
+    for (int i = 0; i < 2; ++i) a[i] = *reinterpret_cast<const float4*>(&As[(wm * 32 + i * 16 + (lane & 15)) * FPITCH + g * 4]);
+#pragma unroll
+    for (int j = 0; j < 2; ++j) b[j] = *reinterpret_cast<const float4*>(&Bs[(wn * 32 + j * 16 + (lane & 15)) * FPITCH + g * 4]);
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+      for (int j = 0; j < 2; ++j) acc[i][j] = mfma4(a[i], b[j], acc[i][j]);
+  }
+  float* out = p.slab + (long)split * p.M * p.N;
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      const int col = n0 + wn * 32 + j * 16 + (lane & 15);
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int row = m0 + wm * 32 + i * 16 + (lane >> 4) * 4 + r;
+        if (row < p.M && col < p.N) out[(long)row * p.N + col] = acc[i][j][r];
+      }
+    }
+  if (p.bias_slab && tn == 0 && tid < FBM && m0 + tid < p.M) p.bias_slab[(long)split * p.M + m0 + tid] = bias_acc;
+}
+
+void gemm_g2f(const G2Args& a, hipStream_t s) {
+  if (a.ntaps > 64) throw std::runtime_error("gemm_g2f: at most 64 taps");
+  const int tiles = ((a.M + FBM - 1) / FBM) * ((a.N + FBN - 1) / FBN);
+  hipLaunchKernelGGL(gemm_g2f_kernel, dim3(tiles), dim3(256), 0, s, a);
+}
+
+int gemm_g2f_stat_rows(int M, int N) { return (M + FBM - 1) / FBM; }
+
+int gemm_t2f_splits(int M, int N, int P) {
+  const int tiles = ((M + FBM - 1) / FBM) * ((N + FBN - 1) / FBN);
+  int splits = (1024 + tiles - 1) / tiles;
+  const long max_by_k = (P + 255) / 256;             // at least 256 pixels per split
+  if (splits > max_by_k) splits = (int)max_by_k;
+  const long slab_cap = (96l << 20) / (4l * M * N);  // <= 96 MB of fp32 partials
+  if (splits > slab_cap) splits = (int)(slab_cap > 0 ? slab_cap : 1);
+  if (splits > 256) splits = 256;
+  return splits < 1 ? 1 : splits;
+}
+
+void gemm_t2f(T2Args a, int splits, hipStream_t s) {
+  if (a.ntaps > 64) throw std::runtime_error("gemm_t2f: at most 64 taps");
+  const long per = (a.P + splits - 1) / splits;
+  a.k_per_split = (int)(((per + FBK - 1) / FBK) * FBK);
+  const int tiles = ((a.M + FBM - 1) / FBM) * ((a.N + FBN - 1) / FBN);
+  hipLaunchKernelGGL(gemm_t2f_kernel, dim3(tiles * splits), dim3(256), 0, s, a);
+}
+
+// [Co][T][Ci] fp32 -> [Ci][T][Co] fp32 (dgrad B operand of the fp32 path)
+__global__ void conv_weight_transpose_f32_kernel(const float* __restrict__ w, float* __restrict__ wt, int Co, int T,
+                                                 int Ci) {
+  const long n = (long)Co * T * Ci;
+  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < n; i += (long)gridDim.x * blockDim.x) {
+    const int co = (int)(i % Co);
+    const long r = i / Co;
+    const int t = (int)(r % T), ci = (int)(r / T);
+    wt[i] = w[((long)co * T + t) * Ci + ci];
+  }
+}
+
+void conv_weight_transpose_f32(const float* w, float* wt, int Co, int T, int Ci, hipStream_t s) {
+  const long n = (long)Co * T * Ci;
+  const int blocks = (int)((n + 255) / 256 < 4096 ? (n + 255) / 256 : 4096);
+  hipLaunchKernelGGL(conv_weight_transpose_f32_kernel, dim3(blocks > 0 ? blocks : 1), dim3(256), 0, s, w, wt, Co, T, Ci);
+}
+
+}  // namespace dcnn

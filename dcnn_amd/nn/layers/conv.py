@@ -66,7 +66,7 @@ class Conv2D(ParameterizedLayer):
             raise ValueError(f"Conv2D '{self.name}': input has {x.shape[1]} channels, expected {self.in_channels}")
         if x.is_cuda:
             from ...ops import hip
-            if self.in_channels < 8:
+            if self.in_channels < 8 and self.compute_dtype == torch.bfloat16:
                 # RGB stem: zero-pad channels to 8 so every 16-byte chunk is one tap (vector path)
                 xa = hip.to_act_padded(x, 8)
                 w = hip.pad_weight_channels(self.weight_operand(0), 8)
@@ -102,7 +102,7 @@ class Conv2D(ParameterizedLayer):
             if getattr(self, "_wt_valid", False):
                 wt = self._wt_buf  # refreshed by the model's batched WeightTransposer this step
             else:
-                wt = hip.conv_weight_t(self.weight_operand(0))
+                wt = hip.conv_weight_t(self.weight_operand(0), dtype=self.compute_dtype)
             res = hip.to_act(add_to, self.compute_dtype) if add_to is not None else None
             return hip.conv2d_dgrad(g, wt, x_shape, (self.stride_h, self.stride_w), (self.pad_h, self.pad_w),
                                     residual=res)
@@ -228,7 +228,8 @@ class Dense(ParameterizedLayer):
             if not self.needs_input_grad:
                 return None
             w = self.weight_operand(0)
-            wt = hip.conv_weight_t(w.view(self.output_features, self.input_features, 1, 1)).view(
+            wt = hip.conv_weight_t(w.view(self.output_features, self.input_features, 1, 1),
+                                   dtype=self.compute_dtype).view(
                 self.input_features, self.output_features)
             dx = hip.dense_dgrad(g2, wt)
         else:

@@ -92,6 +92,7 @@ class Sequential:
         self.training = True
         self.device: Device = get_cpu()
         self.compute_dtype = torch.float32
+        self.dtype_pref: Optional[torch.dtype] = None  # None: bf16 on GPU, fp32 on CPU
         self.arena: Optional[ParamArena] = None
         self.initialized = False
         self.enable_profiling_ = False
@@ -168,9 +169,9 @@ class Sequential:
             vals = [p.detach().to("cpu").clone() for p in self.parameters()]
             bufs = self._collect_buffers()
         self.device = dev
-        if self.compute_dtype == torch.float32 and dev.is_gpu():
-            self.compute_dtype = torch.bfloat16
-        if not dev.is_gpu():
+        if dev.is_gpu():
+            self.compute_dtype = self.dtype_pref or torch.bfloat16
+        else:
             self.compute_dtype = torch.float32
         for l in _all_layers(self.layers):
             l.device = dev
@@ -189,6 +190,7 @@ class Sequential:
             raise ValueError("CPU path computes in float32 (reference semantics)")
         if dtype not in (torch.float32, torch.bfloat16):
             raise ValueError("compute dtype must be float32 or bfloat16")
+        self.dtype_pref = dtype
         self.compute_dtype = dtype
         for l in _all_layers(self.layers):
             l.set_compute_dtype(dtype)

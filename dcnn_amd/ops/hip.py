@@ -80,13 +80,24 @@ def conv2d_fwd(x, w, bias, stride, pad, *, stats=False, residual=None, relu=Fals
     else:  # padded operand [Co][KH][KW][Ci]
         Co, KH, KW, Cp = w.shape
         assert Cp == Ci and w.is_contiguous()
-    assert x.dtype == BF16 and w.dtype == BF16
+    assert x.dtype == w.dtype and x.dtype in (BF16, F32)
     sh, sw = stride
     ph, pw = pad
     OH, OW = conv_out_hw(H, W, KH, KW, sh, sw, ph, pw)
     M = N * OH * OW
     if residual is not None:
         assert tuple(residual.shape) == (N, Co, OH, OW) and residual.is_contiguous(memory_format=CL)
+    if x.dtype == F32:  # fp32 compute path: MFMA f32 16x16x4 gathered GEMM
+        y = torch.empty((N, Co, OH, OW), dtype=F32, device=x.device, memory_format=CL)
+        slab, rows, sums = None, 0, None
+        if stats:
+            rows = K.gemm_g2f_stat_rows(M, Co)
+            slab = torch.empty((rows, 2, Co), dtype=F32, device=x.device)
+            sums = torch.empty((2 * Co,), dtype=F32, device=x.device)  # zeroed in-kernel
+        K.gemm_g2f(x.data_ptr(), w.data_ptr(), y.data_ptr(), _nbytes(x), _nbytes(w), M, Co, Ci, H, W, OH, OW, sh, sw,
+                   _fwd_taps(Ci, W, KH, KW, ph, pw), KH * KW * Ci, Co, OH, OW, 1, 1, 0, 0, ptr(bias), ptr(residual),
+                   ptr(slab), int(relu), ptr(sums), 2 * Co if stats else 0, stream_ptr())
+        return y, ((slab, rows, sums) if stats else None)
     if _g2_ok(Ci, Co) and not out_fp32:
         y = torch.empty((N, Co, OH, OW), dtype=BF16, device=x.device, memory_format=CL)
         slab, rows, sums = None, 0, None
@@ -129,9 +140,17 @@ def pad_weight_channels(w, cp):
     return out
 
 
-def conv_weight_t(w, out=None):
-    """(Co,Ci,KH,KW) channels_last weight -> bf16 [Ci][KH][KW][Co] dgrad operand."""
+def conv_weight_t(w, out=None, dtype=BF16):
+    """(Co,Ci,KH,KW) channels_last weight -> [Ci][KH][KW][Co] dgrad operand (bf16, or fp32 for
+    the fp32 compute path)."""
     Co, Ci, KH, KW = w.shape
+    if dtype == F32:
+        src = w if (w.dtype == F32 and (w.is_contiguous(memory_format=CL) or KH * KW == 1 or Ci == 1)) \
+            else w.float().contiguous(memory_format=CL)
+        if out is None:
+            out = torch.empty((Ci, KH, KW, Co), dtype=F32, device=w.device)
+        kernels().conv_weight_transpose_f32(src.data_ptr(), out.data_ptr(), Co, KH * KW, Ci, stream_ptr())
+        return out
     if out is None:
         out = torch.empty((Ci, KH, KW, Co), dtype=BF16, device=w.device)
     kernels().conv_weight_transpose(dt_code(w.dtype), w.data_ptr(), out.data_ptr(), Co, KH * KW, Ci, stream_ptr())
@@ -154,7 +173,10 @@ def conv2d_dgrad(dy, wt, x_shape, stride, pad, *, residual=None):
         assert tuple(residual.shape) == (N, Ci, H, W) and residual.is_contiguous(memory_format=CL)
     sh, sw = stride
     ph, pw = pad
-    if not _g2_ok(Co, Ci):
+    f32 = dy.dtype == F32
+    if f32:
+        assert wt.dtype == F32, "fp32 dgrad needs an fp32 transposed weight (conv_weight_t(..., dtype=F32))"
+    if not f32 and not _g2_ok(Co, Ci):
         dx = torch.empty((N, Ci, H, W), dtype=BF16, device=dy.device, memory_format=CL)
         Kd = KH * KW * Co
         K.gemm_nt(dy.data_ptr(), wt.data_ptr(), dx.data_ptr(), N * H * W, Ci, Kd, 0, Kd, Ci, CONV_DGRAD,
@@ -181,15 +203,17 @@ def conv2d_dgrad(dy, wt, x_shape, stride, pad, *, residual=None):
                 classes.append((ry, rx, GH, GW, taps))
             else:
                 empty_class = True
+    odt = F32 if f32 else BF16
     if empty_class:
         dx = residual.clone() if residual is not None else torch.empty(
-            (N, Ci, H, W), dtype=BF16, device=dy.device, memory_format=CL).zero_()
+            (N, Ci, H, W), dtype=odt, device=dy.device, memory_format=CL).zero_()
     else:
-        dx = torch.empty((N, Ci, H, W), dtype=BF16, device=dy.device, memory_format=CL)
+        dx = torch.empty((N, Ci, H, W), dtype=odt, device=dy.device, memory_format=CL)
     st = stream_ptr()
+    g2 = K.gemm_g2f if f32 else K.gemm_g2
     for ry, rx, GH, GW, taps in classes:
-        K.gemm_g2(dy.data_ptr(), wt.data_ptr(), dx.data_ptr(), _nbytes(dy), _nbytes(wt), N * GH * GW, Ci, Co, OH, OW,
-                  GH, GW, 1, 1, taps, KH * KW * Co, Ci, H, W, sh, sw, ry, rx, 0, ptr(residual), 0, 0, 0, 0, st)
+        g2(dy.data_ptr(), wt.data_ptr(), dx.data_ptr(), _nbytes(dy), _nbytes(wt), N * GH * GW, Ci, Co, OH, OW,
+           GH, GW, 1, 1, taps, KH * KW * Co, Ci, H, W, sh, sw, ry, rx, 0, ptr(residual), 0, 0, 0, 0, st)
     return dx
 
 
@@ -204,6 +228,20 @@ def conv2d_wgrad(dy, x, w_shape, stride, pad, grad_w, grad_b=None):
     OH, OW = dy.shape[2], dy.shape[3]
     P = N * OH * OW
     st = stream_ptr()
+    if dy.dtype == F32:
+        assert x.dtype == F32 and Cx == Ci
+        Ng = KH * KW * Ci
+        splits = K.gemm_t2f_splits(Co, Ng, P)
+        slab = torch.empty((splits, Co, Ng), dtype=F32, device=x.device)
+        bslab = torch.empty((splits, Co), dtype=F32, device=x.device) if grad_b is not None else None
+        taps = [(ky - pad[0], kx - pad[1]) for ky in range(KH) for kx in range(KW)]
+        K.gemm_t2f(dy.data_ptr(), x.data_ptr(), slab.data_ptr(), ptr(bslab), Co, Ng, P, Co, Ci, H, W, OH, OW,
+                   stride[0], stride[1], taps, splits, st)
+        assert grad_w.is_contiguous(memory_format=CL) or KH * KW == 1 or Ci == 1
+        K.splitk_reduce(slab.data_ptr(), grad_w.data_ptr(), Co * Ng, splits, 1, st)
+        if grad_b is not None:
+            K.splitk_reduce(bslab.data_ptr(), grad_b.data_ptr(), Co, splits, 1, st)
+        return
     if _g2_ok(Cx, Co) and P < (1 << 24):
         Ng = KH * KW * Cx
         splits = K.gemm_t2_splits(Co, Ng, P)
@@ -237,6 +275,12 @@ def dense_fwd(x2d, w2d, bias):
     """y[N,Out] = x[N,In] . w[Out,In]^T + b   (bf16 in/out, fp32 accumulate)."""
     N, In = x2d.shape
     Out = w2d.shape[0]
+    if x2d.dtype == F32:
+        y = torch.empty((N, Out), dtype=F32, device=x2d.device)
+        kernels().gemm_g2f(x2d.data_ptr(), w2d.data_ptr(), y.data_ptr(), _nbytes(x2d), _nbytes(w2d), N, Out, In, 1, 1,
+                           1, 1, 1, 1, [(0, 0, 0, 0)], In, Out, 1, 1, 1, 1, 0, 0, ptr(bias), 0, 0, 0, 0, 0,
+                           stream_ptr())
+        return y
     y = torch.empty((N, Out), dtype=BF16, device=x2d.device)
     if _g2_ok(In, Out):
         kernels().gemm_g2(x2d.data_ptr(), w2d.data_ptr(), y.data_ptr(), _nbytes(x2d), _nbytes(w2d), N, Out, In, 1, 1,
@@ -252,6 +296,12 @@ def dense_dgrad(dy2d, wt2d):
     """dx[N,In] = dy[N,Out] . w[Out,In]   with wt2d = w^T stored [In][Out]."""
     N, Out = dy2d.shape
     In = wt2d.shape[0]
+    if dy2d.dtype == F32:
+        dx = torch.empty((N, In), dtype=F32, device=dy2d.device)
+        kernels().gemm_g2f(dy2d.data_ptr(), wt2d.data_ptr(), dx.data_ptr(), _nbytes(dy2d), _nbytes(wt2d), N, In, Out,
+                           1, 1, 1, 1, 1, 1, [(0, 0, 0, 0)], Out, In, 1, 1, 1, 1, 0, 0, 0, 0, 0, 0, 0, 0,
+                           stream_ptr())
+        return dx
     dx = torch.empty((N, In), dtype=BF16, device=dy2d.device)
     if _g2_ok(Out, In):
         kernels().gemm_g2(dy2d.data_ptr(), wt2d.data_ptr(), dx.data_ptr(), _nbytes(dy2d), _nbytes(wt2d), N, In, Out, 1,
@@ -268,7 +318,13 @@ def dense_wgrad(dy2d, x2d, grad_w, grad_b=None):
     N, Out = dy2d.shape
     In = x2d.shape[1]
     st = stream_ptr()
-    if _g2_ok(In, Out):
+    if dy2d.dtype == F32:
+        splits = K.gemm_t2f_splits(Out, In, N)
+        slab = torch.empty((splits, Out, In), dtype=F32, device=x2d.device)
+        bslab = torch.empty((splits, Out), dtype=F32, device=x2d.device) if grad_b is not None else None
+        K.gemm_t2f(dy2d.data_ptr(), x2d.data_ptr(), slab.data_ptr(), ptr(bslab), Out, In, N, Out, In, 1, 1, 1, 1,
+                   1, 1, [(0, 0)], splits, st)
+    elif _g2_ok(In, Out):
         splits = K.gemm_t2_splits(Out, In, N)
         slab = torch.empty((splits, Out, In), dtype=F32, device=x2d.device)
         bslab = torch.empty((splits, Out), dtype=F32, device=x2d.device) if grad_b is not None else None

@@ -264,3 +264,54 @@ def test_dropout_regenerates_mask(hip):
     assert torch.allclose(y[y > 0], torch.full_like(y[y > 0], 1 / 0.7))
     g = hip.dropout(torch.ones(10000, device="cuda"), 0.3, 1234)
     assert torch.equal(g > 0, y > 0)
+
+
+# ------------------------------------------------------------------ fp32 compute path (MFMA f32)
+F32_CASES = CONV_CASES + [(2, 3, 32, 32, 64, 3, 1, 1), (2, 6, 9, 9, 10, 3, 2, 1), (1, 5, 7, 7, 7, 1, 1, 0)]
+
+
+@pytest.mark.parametrize("case", F32_CASES)
+def test_conv_fp32_fwd_dgrad_wgrad(hip, case):
+    N, Ci, H, W, Co, k, s, p = case
+    torch.manual_seed(1)
+    x = torch.randn(N, Ci, H, W)
+    w = torch.randn(Co, Ci, k, k) / math.sqrt(Ci * k * k)
+    b = torch.randn(Co)
+    xg = x.cuda().contiguous(memory_format=CL)
+    wg = w.cuda().contiguous(memory_format=CL)
+    r = torch.randn(F.conv2d(x, w, None, s, p).shape)
+    y, partial = hip.conv2d_fwd(xg, wg, b.cuda(), (s, s), (p, p), stats=True,
+                                residual=r.cuda().contiguous(memory_format=CL), relu=True)
+    y_ref = torch.relu(F.conv2d(x, w, b, s, p) + r)
+    assert y.dtype == torch.float32
+    assert rel_err(y, y_ref) < 1e-5, rel_err(y, y_ref)
+    sums = hip.bn_stats(y, partial)
+    assert rel_err(sums[:Co], y_ref.sum((0, 2, 3))) < 1e-5
+    assert rel_err(sums[Co:], (y_ref * y_ref).sum((0, 2, 3))) < 1e-5
+    dy = torch.randn_like(y_ref)
+    dyg = dy.cuda().contiguous(memory_format=CL)
+    wt = hip.conv_weight_t(wg, dtype=torch.float32)
+    dx = hip.conv2d_dgrad(dyg, wt, x.shape, (s, s), (p, p))
+    dx_ref = torch.nn.grad.conv2d_input(x.shape, w, dy, s, p)
+    assert dx.dtype == torch.float32 and rel_err(dx, dx_ref) < 1e-5, rel_err(dx, dx_ref)
+    gw = torch.ones(Co, Ci, k, k, device="cuda").contiguous(memory_format=CL)
+    gb = torch.ones(Co, device="cuda")
+    hip.conv2d_wgrad(dyg, xg, w.shape, (s, s), (p, p), gw, gb)
+    gw_ref = torch.nn.grad.conv2d_weight(x, w.shape, dy, s, p) + 1
+    assert rel_err(gw, gw_ref) < 1e-5, rel_err(gw, gw_ref)
+    assert rel_err(gb, dy.sum((0, 2, 3)) + 1) < 1e-5
+
+
+@pytest.mark.parametrize("shape", [(8, 512, 200), (5, 27, 10), (64, 256, 128)])
+def test_dense_fp32(hip, shape):
+    N, In, Out = shape
+    torch.manual_seed(2)
+    x, w, b = torch.randn(N, In), torch.randn(Out, In) / math.sqrt(In), torch.randn(Out)
+    y = hip.dense_fwd(x.cuda(), w.cuda(), b.cuda())
+    assert rel_err(y, x @ w.t() + b) < 1e-5
+    dy = torch.randn(N, Out)
+    wt = hip.conv_weight_t(w.cuda().view(Out, In, 1, 1), dtype=torch.float32).view(In, Out)
+    assert rel_err(hip.dense_dgrad(dy.cuda(), wt), dy @ w) < 1e-5
+    gw, gb = torch.zeros(Out, In, device="cuda"), torch.zeros(Out, device="cuda")
+    hip.dense_wgrad(dy.cuda(), x.cuda(), gw, gb)
+    assert rel_err(gw, dy.t() @ x) < 1e-5 and rel_err(gb, dy.sum(0)) < 1e-5
