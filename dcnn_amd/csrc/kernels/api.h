@@ -40,6 +40,14 @@ int gemm_g2_stat_rows(int M, int N);
 void gemm_t2(T2Args a, int splits, hipStream_t s);
 int gemm_t2_splits(int M, int N, int P);
 int gemm_nt_stat_rows(int M, int N);
+// generic tensor ops (ops.hip)
+void elementwise(int mode, int op, const float* a, const float* b, float* c, long n, float s0, float s1, hipStream_t s);
+void reduce(int op, const float* a, const float* b, long n, float* workspace, float* out, hipStream_t s);
+void fill_random(float* out, long n, uint64_t seed, float a, float b, int normal, hipStream_t s);
+void transpose_batched(const float* in, float* out, int batch, int rows, int cols, hipStream_t s);
+void nchw_cnhw(const float* in, float* out, int N, int C, int HW, int to_cnhw, hipStream_t s);
+void pad_crop(const float* in, float* out, int NC, int H, int W, int OH, int OW, int top, int left, float value,
+              hipStream_t s);
 // fp32 path (gemm_f32.hip): same argument structs, fp32 operand/result pointers
 void gemm_g2f(const G2Args& a, hipStream_t s);
 int gemm_g2f_stat_rows(int M, int N);

@@ -32,6 +32,26 @@ PYBIND11_MODULE(_kernels, m) {
           gemm_nt(a, S(stream));
         });
   m.def("gemm_nt_stat_rows", &gemm_nt_stat_rows);
+  m.def("elementwise", [](int mode, int op, uintptr_t a, uintptr_t b, uintptr_t c, long n, float s0, float s1,
+                          uintptr_t st) {
+    elementwise(mode, op, P<const float*>(a), P<const float*>(b), P<float*>(c), n, s0, s1, S(st));
+  });
+  m.def("reduce", [](int op, uintptr_t a, uintptr_t b, long n, uintptr_t ws, uintptr_t out, uintptr_t st) {
+    reduce(op, P<const float*>(a), P<const float*>(b), n, P<float*>(ws), P<float*>(out), S(st));
+  });
+  m.def("fill_random", [](uintptr_t out, long n, uint64_t seed, float a, float b, int normal, uintptr_t st) {
+    fill_random(P<float*>(out), n, seed, a, b, normal, S(st));
+  });
+  m.def("transpose_batched", [](uintptr_t in, uintptr_t out, int batch, int rows, int cols, uintptr_t st) {
+    transpose_batched(P<const float*>(in), P<float*>(out), batch, rows, cols, S(st));
+  });
+  m.def("nchw_cnhw", [](uintptr_t in, uintptr_t out, int N, int C, int HW, int to_cnhw, uintptr_t st) {
+    nchw_cnhw(P<const float*>(in), P<float*>(out), N, C, HW, to_cnhw, S(st));
+  });
+  m.def("pad_crop", [](uintptr_t in, uintptr_t out, int NC, int H, int W, int OH, int OW, int top, int left,
+                       float value, uintptr_t st) {
+    pad_crop(P<const float*>(in), P<float*>(out), NC, H, W, OH, OW, top, left, value, S(st));
+  });
   m.def("gemm_g2f",
         [](uintptr_t A, uintptr_t B, uintptr_t C, unsigned a_bytes, unsigned b_bytes, int M, int N, int Cs, int H,
            int W, int GH, int GW, int SY, int SX, std::vector<std::array<int, 4>> taps, int ldb, int ldc, int OH,

@@ -291,6 +291,13 @@ std::string decompress(const std::string& in, Codec codec, size_t hint) {
 }
 
 // ------------------------------------------------------------------ queue
+// Deadlines on system_clock: libstdc++ then waits with pthread_cond_timedwait, which
+// ThreadSanitizer intercepts (its steady_clock path, pthread_cond_clockwait, is invisible to
+// the GCC 11 TSan runtime and produces false double-lock reports).
+static std::chrono::system_clock::time_point deadline_ms(int ms) {
+  return std::chrono::system_clock::now() + std::chrono::milliseconds(ms);
+}
+
 void MessageQueue::push(Message&& m) {
   const uint16_t c = m.command < CMD_COUNT ? m.command : CMD_START;
   {
@@ -306,7 +313,7 @@ bool MessageQueue::pop(Message& out, int timeout_ms) {
   auto ready = [&] { return total_ > 0 || closed_; };
   if (timeout_ms < 0)
     cv_.wait(lk, ready);
-  else if (!cv_.wait_for(lk, std::chrono::milliseconds(timeout_ms), ready))
+  else if (!cv_.wait_until(lk, deadline_ms(timeout_ms), ready))
     return false;
   if (total_ == 0) return false;
   for (int c = 0; c < CMD_COUNT; ++c) {
@@ -326,7 +333,7 @@ bool MessageQueue::pop_command(uint16_t cmd, Message& out, int timeout_ms) {
   auto ready = [&] { return !q_[cmd].empty() || closed_; };
   if (timeout_ms < 0)
     cv_.wait(lk, ready);
-  else if (!cv_.wait_for(lk, std::chrono::milliseconds(timeout_ms), ready))
+  else if (!cv_.wait_until(lk, deadline_ms(timeout_ms), ready))
     return false;
   if (q_[cmd].empty()) return false;
   out = std::move(q_[cmd].front());
@@ -592,7 +599,7 @@ bool TcpCommunicator::wait_for_peer(const std::string& name, int timeout_ms) {
     if (a != alias_.end()) n = a->second;
     return conns_.count(n) > 0;
   };
-  return cv_.wait_for(lk, std::chrono::milliseconds(timeout_ms), have);
+  return cv_.wait_until(lk, deadline_ms(timeout_ms), have);
 }
 
 void TcpCommunicator::write_frame(Conn& c, const Message& m) {
