@@ -41,7 +41,7 @@ constexpr unsigned kOOB = 0x80000000u;  // any offset >= num_records reads zeros
 // ---------------------------------------------------------------------------------------------
 // gathered NT GEMM
 // ---------------------------------------------------------------------------------------------
-template <int BM, int BN, int BK, bool UNI>
+template <int BM, int BN, int BK, bool UNI, int NST>
 struct G2 {
   static constexpr int CPR = BK / 8;                 // 16-B chunks per LDS row
   static constexpr int RPI = 64 / CPR;               // rows covered by one wave-instruction (1 KiB)
@@ -51,14 +51,15 @@ struct G2 {
   static constexpr int TM = BM / 32, TN = BN / 32;   // 16x16 subtiles per wave (2x2 waves)
   static constexpr int STAGE = (BM + BN) * BK * 2;
   static constexpr int EPI_PITCH = BN * 2 + 16;      // bf16 staging row pitch (bytes)
-  static constexpr int LDS = (2 * STAGE > BM * EPI_PITCH) ? 2 * STAGE : BM * EPI_PITCH;
+  static constexpr int LDS = (NST * STAGE > BM * EPI_PITCH) ? NST * STAGE : BM * EPI_PITCH;
+  static constexpr int INS = A_INS + B_INS;          // glds instructions per wave per stage
   __device__ static __forceinline__ int swz(int row) { return (row / RPB) % CPR; }
   __device__ static __forceinline__ int off(int row, int ch) { return row * (BK * 2) + ((ch ^ swz(row)) << 4); }
 };
 
-template <int BM, int BN, int BK, bool UNI>
+template <int BM, int BN, int BK, bool UNI, int NST>
 __global__ void __launch_bounds__(256, 2) gemm_g2_kernel(G2Args p) {
-  using T = G2<BM, BN, BK, UNI>;
+  using T = G2<BM, BN, BK, UNI, NST>;
   __shared__ __attribute__((aligned(16))) char smem[T::LDS];
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const int wm = wid >> 1, wn = wid & 1;
@@ -69,8 +70,10 @@ __global__ void __launch_bounds__(256, 2) gemm_g2_kernel(G2Args p) {
 
   const __amdgpu_buffer_rsrc_t rsA = __builtin_amdgcn_make_buffer_rsrc((void*)p.A, (short)0, p.a_bytes, 0x00020000);
   const __amdgpu_buffer_rsrc_t rsB = __builtin_amdgcn_make_buffer_rsrc((void*)p.B, (short)0, p.b_bytes, 0x00020000);
-  if (p.zero_ptr && blockIdx.x == 0)
+  if (p.zero_ptr && blockIdx.x == 0) {
     for (int i = tid; i < p.zero_n; i += 256) p.zero_ptr[i] = 0.f;
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // keep the glds counting below exact
+  }
 
   // ---- per-lane A rows: pixel base offset + tap-validity mask (fixed over the K loop) ----
   const int ch = lane % T::CPR;           // this lane's physical chunk slot within a row
@@ -144,13 +147,8 @@ __global__ void __launch_bounds__(256, 2) gemm_g2_kernel(G2Args p) {
 
   const int K = p.ntaps * p.Cs;
   const int nk = (K + BK - 1) / BK;
-  stage(0, 0);
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __syncthreads();
-  int cur = 0;
-  for (int kt = 0; kt < nk; ++kt) {
-    if (kt + 1 < nk) stage(cur ^ 1, (kt + 1) * BK);
-    const char* As = smem + cur * T::STAGE;
+  auto compute = [&](int buf) {
+    const char* As = smem + buf * T::STAGE;
     const char* Bs = As + BM * BK * 2;
 #pragma unroll
     for (int kk = 0; kk < BK / 32; ++kk) {
@@ -170,9 +168,43 @@ __global__ void __launch_bounds__(256, 2) gemm_g2_kernel(G2Args p) {
           acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[i], b[j], acc[i][j], 0, 0, 0);
       __builtin_amdgcn_s_setprio(0);
     }
+  };
+  if constexpr (NST == 2) {
+    stage(0, 0);
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
-    cur ^= 1;
+    int cur = 0;
+    for (int kt = 0; kt < nk; ++kt) {
+      if (kt + 1 < nk) stage(cur ^ 1, (kt + 1) * BK);
+      compute(cur);
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __syncthreads();
+      cur ^= 1;
+    }
+  } else {
+    // 3-buffer ring: tile k+2 is issued while tile k is multiplied, so every load has two
+    // MFMA phases to land. Only counted vmcnt waits (the newest stage stays in flight across
+    // the barrier) and raw s_barrier, which unlike __syncthreads() does not drain the
+    // outstanding LDS-DMA.
+    stage(0, 0);
+    if (nk > 1) {
+      stage(1, BK);
+      asm volatile("s_waitcnt vmcnt(%0)" ::"n"(T::INS) : "memory");
+    } else {
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+    __builtin_amdgcn_s_barrier();
+    int cur = 0;
+    for (int kt = 0; kt < nk; ++kt) {
+      const bool more = kt + 2 < nk;
+      if (more) stage(cur == 0 ? 2 : cur - 1, (kt + 2) * BK);
+      compute(cur);
+      if (more) asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)" ::"n"(T::INS) : "memory");
+      else asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+      __builtin_amdgcn_s_barrier();
+      asm volatile("" ::: "memory");
+      cur = cur == 2 ? 0 : cur + 1;
+    }
   }
 
   // ---- epilogue 1: acc (+bias) -> bf16 LDS tile [BM][BN] ----
@@ -464,10 +496,21 @@ __global__ void __launch_bounds__(256, 2) gemm_t2_kernel(T2Args p) {
 // ---------------------------------------------------------------------------------------------
 // launchers
 // ---------------------------------------------------------------------------------------------
+static int g2_stages() {
+  static int st = [] {
+    const char* e = getenv("DCNN_G2_STAGES");
+    return (e && atoi(e) == 3) ? 3 : 2;  // 3-stage ring: opt-in (measured slower on the ResNet shapes)
+  }();
+  return st;
+}
+
 template <int BM, int BN, int BK, bool UNI>
 static void launch_g2(const G2Args& a, hipStream_t s) {
   const int tiles = ((a.M + BM - 1) / BM) * ((a.N + BN - 1) / BN);
-  hipLaunchKernelGGL((gemm_g2_kernel<BM, BN, BK, UNI>), dim3(tiles), dim3(256), 0, s, a);
+  if (g2_stages() == 3)
+    hipLaunchKernelGGL((gemm_g2_kernel<BM, BN, BK, UNI, 3>), dim3(tiles), dim3(256), 0, s, a);
+  else
+    hipLaunchKernelGGL((gemm_g2_kernel<BM, BN, BK, UNI, 2>), dim3(tiles), dim3(256), 0, s, a);
   DCNN_LAUNCH_CHECK();
 }
 
