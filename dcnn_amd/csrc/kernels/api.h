@@ -23,7 +23,7 @@ struct G2Args {
   int ldb, ldc;
   int OH, OW, OSY, OSX, ORY, ORX;
   const float* bias; const bf16* residual; float* stats; int relu;
-  float* stats_out; int unused;  // stats: sharded workspace (common.h stats_finalize); stats_out: final [2][N] sums
+  float* zero_ptr; int zero_n;  // zeroed by workgroup 0 (BN sums consumed by the next kernel)
 };
 struct T2Args {
   const bf16* dY; const bf16* X; float* slab; float* bias_slab;

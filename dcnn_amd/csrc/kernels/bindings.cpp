@@ -68,7 +68,7 @@ PYBIND11_MODULE(_kernels, m) {
           }
           a.ldb = ldb; a.ldc = ldc; a.OH = OH; a.OW = OW; a.OSY = OSY; a.OSX = OSX; a.ORY = ORY; a.ORX = ORX;
           a.bias = P<const float*>(bias); a.residual = P<const bf16*>(residual); a.stats = P<float*>(stats); a.relu = relu;
-          a.stats_out = P<float*>(zero_ptr); a.unused = zero_n;
+          a.zero_ptr = P<float*>(zero_ptr); a.zero_n = zero_n;
           gemm_g2f(a, S(stream));
         });
   m.def("gemm_g2f_stat_rows", &gemm_g2f_stat_rows);
@@ -104,7 +104,7 @@ PYBIND11_MODULE(_kernels, m) {
           }
           a.ldb = ldb; a.ldc = ldc; a.OH = OH; a.OW = OW; a.OSY = OSY; a.OSX = OSX; a.ORY = ORY; a.ORX = ORX;
           a.bias = P<const float*>(bias); a.residual = P<const bf16*>(residual); a.stats = P<float*>(stats); a.relu = relu;
-          a.stats_out = P<float*>(zero_ptr); a.unused = zero_n;
+          a.zero_ptr = P<float*>(zero_ptr); a.zero_n = zero_n;
           gemm_g2(a, S(stream));
         });
   m.def("gemm_g2_stat_rows", &gemm_g2_stat_rows);

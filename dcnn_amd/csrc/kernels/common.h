@@ -59,47 +59,6 @@ __device__ __forceinline__ float block_sum(float v, float* sh) {
   return r;
 }
 
-// ---- in-launch BatchNorm statistics reduction ---------------------------------------------
-// A statistics workspace is float[kStatShards][n2] followed by one int arrival counter; it is
-// all-zero between launches (allocated zeroed, re-zeroed by the finaliser). Producer blocks
-// atomically add their partial (sum, sum^2) rows into shard (blockIdx.x % kStatShards), then
-// call stats_finalize: the last block to arrive folds the shards into out[n2], zeroes the
-// shards and resets the counter — no separate reduce launch and no memset node per layer.
-// Publication follows the agent-scope release / acquire hand-off (counted vmcnt drains, fence
-// before the ticket, atomic loads in the reducer).
-constexpr int kStatShards = 8;
-
-__device__ __forceinline__ void stats_finalize(float* ws, float* out, int n2, int* flag_lds) {
-  int* counter = reinterpret_cast<int*>(ws + kStatShards * n2);
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __syncthreads();
-  if (threadIdx.x == 0) {
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    const int nb = gridDim.x * gridDim.y * gridDim.z;
-    *flag_lds = __hip_atomic_fetch_add(counter, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == nb - 1;
-  }
-  __syncthreads();
-  if (*flag_lds) {
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-    // Float atomics execute at the memory side, not in L2, so a plain (or sc1) load could hit a
-    // stale copy of the shard line left in this XCD's L2 by an earlier kernel; an atomic
-    // exchange also executes at the memory side: it reads the final value and re-zeroes it.
-    for (int i = threadIdx.x; i < n2; i += blockDim.x) {
-      float s = 0.f;
-#pragma unroll
-      for (int k = 0; k < kStatShards; ++k)
-        s += __hip_atomic_exchange(ws + k * n2 + i, 0.f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      out[i] = s;
-    }
-    if (threadIdx.x == 0) __hip_atomic_exchange(counter, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  }
-}
-
-__device__ __forceinline__ float* stat_shard(float* ws, int n2) {
-  return ws + (long)(blockIdx.x % kStatShards) * n2;
-}
-
 // 8 x bf16 <-> 8 x f32 through one 16-byte access.
 struct alignas(16) Pack8 {
   uint4 u;

@@ -70,6 +70,10 @@ __global__ void __launch_bounds__(256, 2) gemm_g2_kernel(G2Args p) {
 
   const __amdgpu_buffer_rsrc_t rsA = __builtin_amdgcn_make_buffer_rsrc((void*)p.A, (short)0, p.a_bytes, 0x00020000);
   const __amdgpu_buffer_rsrc_t rsB = __builtin_amdgcn_make_buffer_rsrc((void*)p.B, (short)0, p.b_bytes, 0x00020000);
+  if (p.zero_ptr && blockIdx.x == 0) {
+    for (int i = tid; i < p.zero_n; i += 256) p.zero_ptr[i] = 0.f;
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // keep the glds counting below exact
+  }
 
   // ---- per-lane A rows: pixel base offset + tap-validity mask (fixed over the K loop) ----
   const int ch = lane % T::CPR;           // this lane's physical chunk slot within a row
@@ -268,10 +272,9 @@ __global__ void __launch_bounds__(256, 2) gemm_g2_kernel(G2Args p) {
       if (n0 + cc < p.N) {
         float a = 0.f;
         for (int k = 0; k < RSTEP; ++k) a += red[(k * 2 + which) * BN + cc];
-        atomicAdd(stat_shard(p.stats, 2 * p.N) + which * p.N + n0 + cc, a);
+        p.stats[((long)tm * 2 + which) * p.N + n0 + cc] = a;
       }
     }
-    stats_finalize(p.stats, p.stats_out, 2 * p.N, reinterpret_cast<int*>(smem + T::LDS - 16));
   }
 }
 

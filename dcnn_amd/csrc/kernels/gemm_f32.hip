@@ -41,7 +41,6 @@ __global__ void __launch_bounds__(256, 2) gemm_g2f_kernel(G2Args p) {
   __shared__ __attribute__((aligned(16))) float As[2][FBM * FPITCH];
   __shared__ __attribute__((aligned(16))) float Bs[2][FBN * FPITCH];
   __shared__ float red[2][FBN];
-  __shared__ int flag;
   const float* A = reinterpret_cast<const float*>(p.A);
   const float* B = reinterpret_cast<const float*>(p.B);
   float* C = reinterpret_cast<float*>(p.C);
@@ -52,6 +51,8 @@ __global__ void __launch_bounds__(256, 2) gemm_g2f_kernel(G2Args p) {
   const int lt = xcd_remap_f(blockIdx.x, gridDim.x);
   const int tm = lt / tiles_n, tn = lt % tiles_n;
   const int m0 = tm * FBM, n0 = tn * FBN;
+  if (p.zero_ptr && blockIdx.x == 0)
+    for (int i = tid; i < p.zero_n; i += 256) p.zero_ptr[i] = 0.f;
 
   // this thread loads row lr, float4 chunk lc (4 chunks of 4 floats = BK 16)
   const int lr = tid >> 2, lc = tid & 3;
@@ -173,9 +174,8 @@ __global__ void __launch_bounds__(256, 2) gemm_g2f_kernel(G2Args p) {
     __syncthreads();
     if (tid < 2 * FBN) {
       const int which = tid / FBN, cc = tid % FBN;
-      if (n0 + cc < p.N) atomicAdd(stat_shard(p.stats, 2 * p.N) + which * p.N + n0 + cc, red[which][cc]);
+      if (n0 + cc < p.N) p.stats[((long)tm * 2 + which) * p.N + n0 + cc] = red[which][cc];
     }
-    stats_finalize(p.stats, p.stats_out, 2 * p.N, &flag);
   }
 }
 

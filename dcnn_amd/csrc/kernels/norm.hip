@@ -63,12 +63,12 @@ __global__ void __launch_bounds__(256) bn_partial_kernel(const T* __restrict__ x
                                                          const T* __restrict__ yout, T* __restrict__ dy_out,
                                                          const float* __restrict__ mean,
                                                          const float* __restrict__ istd, long R, int C,
-                                                         int rpb, float* __restrict__ ws, int mode,
-                                                         float* __restrict__ sums_out) {
+                                                         int rpb, float* __restrict__ slab, int mode,
+                                                         float* __restrict__ zero_sums) {
   extern __shared__ __attribute__((aligned(16))) float sh[];
-  __shared__ int flag;
-  float* shard = stat_shard(ws, 2 * C);
-  const int groups = C / V;                     // channel vectors
+  if (zero_sums && blockIdx.x == 0)
+    for (int i = threadIdx.x; i < 2 * C; i += blockDim.x) zero_sums[i] = 0.f;
+  const int groups = C / V;                       // channel vectors
   const int tpr = groups < 256 ? groups : 256;    // threads per row
   const int rows_conc = 256 / tpr;                // rows processed concurrently
   const int g0 = threadIdx.x % tpr, rsub = threadIdx.x / tpr;
@@ -126,11 +126,10 @@ __global__ void __launch_bounds__(256) bn_partial_kernel(const T* __restrict__ x
       if (ch < C) {
         float acc = 0.f;
         for (int k = 0; k < rows_conc; ++k) acc += sh[(k * 2 + which) * width + cc];
-        atomicAdd(shard + which * C + ch, acc);
+        slab[((long)blockIdx.x * 2 + which) * C + ch] = acc;
       }
     }
   }
-  stats_finalize(ws, sums_out, 2 * C, &flag);
 }
 
 // sums[2][C] += sum over slab rows (atomic; sums zeroed by the caller)

@@ -87,24 +87,39 @@ def conv2d_fwd(x, w, bias, stride, pad, *, stats=False, residual=None, relu=Fals
     M = N * OH * OW
     if residual is not None:
         assert tuple(residual.shape) == (N, Co, OH, OW) and residual.is_contiguous(memory_format=CL)
-    fast = x.dtype == F32 or (_g2_ok(Ci, Co) and not out_fp32)
-    if fast:
-        # fp32: MFMA f32 16x16x4 kernel; bf16: direct-to-LDS MFMA 16x16x32 kernel. With stats,
-        # the epilogue reduces per-channel (sum, sum^2) in-launch into `sums`.
-        y = torch.empty((N, Co, OH, OW), dtype=x.dtype, device=x.device, memory_format=CL)
-        ws = stats_workspace(Co, x.device) if stats else None
-        sums = torch.empty((2 * Co,), dtype=F32, device=x.device) if stats else None
-        g2 = K.gemm_g2f if x.dtype == F32 else K.gemm_g2
-        g2(x.data_ptr(), w.data_ptr(), y.data_ptr(), _nbytes(x), _nbytes(w), M, Co, Ci, H, W, OH, OW, sh, sw,
-           _fwd_taps(Ci, W, KH, KW, ph, pw), KH * KW * Ci, Co, OH, OW, 1, 1, 0, 0, ptr(bias), ptr(residual),
-           ptr(ws), int(relu), ptr(sums), 0, stream_ptr())
-        return y, sums
-    # generic fallback (odd channel counts): v1 kernels; the BatchNorm computes its own statistics
+    if x.dtype == F32:  # fp32 compute path: MFMA f32 16x16x4 gathered GEMM
+        y = torch.empty((N, Co, OH, OW), dtype=F32, device=x.device, memory_format=CL)
+        slab, rows, sums = None, 0, None
+        if stats:
+            rows = K.gemm_g2f_stat_rows(M, Co)
+            slab = torch.empty((rows, 2, Co), dtype=F32, device=x.device)
+            sums = torch.empty((2 * Co,), dtype=F32, device=x.device)  # zeroed in-kernel
+        K.gemm_g2f(x.data_ptr(), w.data_ptr(), y.data_ptr(), _nbytes(x), _nbytes(w), M, Co, Ci, H, W, OH, OW, sh, sw,
+                   _fwd_taps(Ci, W, KH, KW, ph, pw), KH * KW * Ci, Co, OH, OW, 1, 1, 0, 0, ptr(bias), ptr(residual),
+                   ptr(slab), int(relu), ptr(sums), 2 * Co if stats else 0, stream_ptr())
+        return y, ((slab, rows, sums) if stats else None)
+    if _g2_ok(Ci, Co) and not out_fp32:
+        y = torch.empty((N, Co, OH, OW), dtype=BF16, device=x.device, memory_format=CL)
+        slab, rows, sums = None, 0, None
+        if stats:
+            rows = K.gemm_g2_stat_rows(M, Co)
+            slab = torch.empty((rows, 2, Co), dtype=F32, device=x.device)
+            sums = torch.empty((2 * Co,), dtype=F32, device=x.device)  # zeroed in-kernel
+        K.gemm_g2(x.data_ptr(), w.data_ptr(), y.data_ptr(), _nbytes(x), _nbytes(w), M, Co, Ci, H, W, OH, OW, sh, sw,
+                  _fwd_taps(Ci, W, KH, KW, ph, pw), KH * KW * Ci, Co, OH, OW, 1, 1, 0, 0, ptr(bias), ptr(residual),
+                  ptr(slab), int(relu), ptr(sums), 2 * Co if stats else 0, stream_ptr())
+        return y, ((slab, rows, sums) if stats else None)
+    # generic fallback (odd channel counts): v1 kernels
     y = torch.empty((N, Co, OH, OW), dtype=F32 if out_fp32 else BF16, device=x.device, memory_format=CL)
+    slab, rows = None, 0
+    if stats:
+        rows = K.gemm_nt_stat_rows(M, Co)
+        slab = torch.empty((rows, 2, Co), dtype=F32, device=x.device)
     K.gemm_nt(x.data_ptr(), w.data_ptr(), y.data_ptr(), M, Co, KH * KW * Ci, 0, KH * KW * Ci, Co, CONV_FWD,
-              N, H, W, Ci, OH, OW, KH, KW, sh, sw, ph, pw, ptr(bias), ptr(residual), 0,
+              N, H, W, Ci, OH, OW, KH, KW, sh, sw, ph, pw, ptr(bias), ptr(residual), ptr(slab),
               int(out_fp32), int(relu), stream_ptr())
-    return y, None
+    sums = torch.zeros((2 * Co,), dtype=F32, device=x.device) if stats else None
+    return y, ((slab, rows, sums) if stats else None)
 
 
 def to_act_padded(x, cp):
@@ -332,31 +347,19 @@ def _rc(x):
     return N * H * W, C
 
 
-_STAT_SHARDS = 8
-_stat_ws = {}
-
-
-def stats_workspace(C, device):
-    """Persistent zeroed [8 shards][2C] + counter workspace of the in-launch BatchNorm statistics
-    reduction (common.h ``stats_finalize``): kernels leave it zeroed, so it is allocated once per
-    (device, C) and reused by every layer/step — producer launches on one stream are ordered."""
-    key = (str(device), C, torch.cuda.current_stream(device).cuda_stream)
-    ws = _stat_ws.get(key)
-    if ws is None:
-        ws = torch.zeros(_STAT_SHARDS * 2 * C + 1, dtype=F32, device=device)
-        _stat_ws[key] = ws
-    return ws
-
-
 def bn_stats(x, partial=None):
-    """Per-channel (sum, sumsq) of x (NHWC); ``partial`` = sums already produced by the conv epilogue."""
-    if partial is not None:
-        return partial
+    """Per-channel (sum, sumsq) of x (NHWC). Uses the conv-epilogue partial slab if given."""
     K = kernels()
     R, C = _rc(x)
-    sums = torch.empty((2 * C,), dtype=F32, device=x.device)
-    K.bn_partial(dt_code(x.dtype), x.data_ptr(), 0, 0, 0, 0, 0, R, C, stats_workspace(C, x.device).data_ptr(), 0,
-                 sums.data_ptr(), stream_ptr())
+    st = stream_ptr()
+    if partial is None:
+        rows = K.bn_partial_rows(R, C)
+        slab = torch.empty((rows, 2, C), dtype=F32, device=x.device)
+        sums = torch.empty((2 * C,), dtype=F32, device=x.device)
+        K.bn_partial(dt_code(x.dtype), x.data_ptr(), 0, 0, 0, 0, 0, R, C, slab.data_ptr(), 0, sums.data_ptr(), st)
+    else:
+        slab, rows, sums = partial
+    K.bn_slab_reduce(slab.data_ptr(), rows, C, sums.data_ptr(), st)
     return sums
 
 
@@ -381,9 +384,12 @@ def bn_backward(dy, x, yout, mean, istd, gamma, dgamma, dbeta, *, want_masked=Fa
     dmask = torch.empty_like(dy, memory_format=CL) if (want_masked and yout is not None) else None
     sums = None
     if not eval_mode:
+        rows = K.bn_partial_rows(R, C)
+        slab = torch.empty((rows, 2, C), dtype=F32, device=x.device)
         sums = torch.empty((2 * C,), dtype=F32, device=x.device)
         K.bn_partial(dt, x.data_ptr(), dy.data_ptr(), ptr(yout), ptr(dmask), mean.data_ptr(), istd.data_ptr(), R, C,
-                     stats_workspace(C, x.device).data_ptr(), 1, sums.data_ptr(), st)
+                     slab.data_ptr(), 1, sums.data_ptr(), st)
+        K.bn_slab_reduce(slab.data_ptr(), rows, C, sums.data_ptr(), st)
     elif want_masked and yout is not None:
         dmask = dy * (yout > 0)
     dx = torch.empty_like(x, memory_format=CL)
