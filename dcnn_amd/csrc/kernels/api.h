@@ -33,6 +33,19 @@ struct T2Args {
   int k_per_split;
 };
 struct PoolGeom { int N, H, W, C, OH, OW, ph, pw, sh, sw, padh, padw; };
+// halo-tiled stride-1 direct conv (hconv.hip): out[NB][H][W][N] = sum_t in[y+dy_t][x+dx_t][:] . B[n][tap_b_t + :]
+struct HConvArgs {
+  const bf16* A; const bf16* B; bf16* C;
+  unsigned a_bytes, b_bytes;
+  int NB, H, W, Cs, N, ldb, ntaps;
+  int tap_dy[9], tap_dx[9], tap_b[9];
+  int TH, TW, IMG, HPR;  // filled by the launcher (HPR: halo rows padded to 32)
+  const float* bias; const bf16* residual; float* stats; int relu;
+  float* zero_ptr; int zero_n;  // zeroed by workgroup 0 (BN sums accumulated by the next kernel)
+};
+void hconv(HConvArgs a, hipStream_t s);
+bool hconv_supported(int NB, int H, int W, int Cs, int N, int ntaps);
+int hconv_stat_rows(int NB, int H, int W, int N);
 
 void gemm_nt(const NtArgs& a, hipStream_t s);
 void gemm_g2(const G2Args& a, hipStream_t s);

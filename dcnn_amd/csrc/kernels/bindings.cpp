@@ -52,6 +52,23 @@ PYBIND11_MODULE(_kernels, m) {
                        float value, uintptr_t st) {
     pad_crop(P<const float*>(in), P<float*>(out), NC, H, W, OH, OW, top, left, value, S(st));
   });
+  m.def("hconv",
+        [](uintptr_t A, uintptr_t B, uintptr_t C, unsigned a_bytes, unsigned b_bytes, int NB, int H, int W, int Cs,
+           int N, int ldb, std::vector<std::array<int, 3>> taps, uintptr_t bias, uintptr_t residual, uintptr_t stats,
+           int relu, uintptr_t zero_ptr, int zero_n, uintptr_t stream) {
+          HConvArgs a{};
+          a.zero_ptr = P<float*>(zero_ptr); a.zero_n = zero_n;
+          a.A = P<const bf16*>(A); a.B = P<const bf16*>(B); a.C = P<bf16*>(C);
+          a.a_bytes = a_bytes; a.b_bytes = b_bytes;
+          a.NB = NB; a.H = H; a.W = W; a.Cs = Cs; a.N = N; a.ldb = ldb;
+          if (taps.size() > 9 || taps.empty()) throw std::runtime_error("hconv: 1..9 taps");
+          a.ntaps = (int)taps.size();
+          for (size_t i = 0; i < taps.size(); ++i) { a.tap_dy[i] = taps[i][0]; a.tap_dx[i] = taps[i][1]; a.tap_b[i] = taps[i][2]; }
+          a.bias = P<const float*>(bias); a.residual = P<const bf16*>(residual); a.stats = P<float*>(stats); a.relu = relu;
+          hconv(a, S(stream));
+        });
+  m.def("hconv_supported", &hconv_supported);
+  m.def("hconv_stat_rows", &hconv_stat_rows);
   m.def("gemm_g2f",
         [](uintptr_t A, uintptr_t B, uintptr_t C, unsigned a_bytes, unsigned b_bytes, int M, int N, int Cs, int H,
            int W, int GH, int GW, int SY, int SX, std::vector<std::array<int, 4>> taps, int ldb, int ldc, int OH,

@@ -9,6 +9,8 @@ training step can be captured into a hipGraph.
 """
 from __future__ import annotations
 
+import os
+
 import torch
 
 from ._ext import dt_code, kernels, ptr, stream_ptr
@@ -64,6 +66,21 @@ def _g2_ok(Cs, N):
     return Cs % 8 == 0 and N % 8 == 0
 
 
+_HCONV = os.environ.get("DCNN_HCONV", "1") != "0"
+
+
+def _hconv_ok(N, OH, OW, H, W, sh, sw, Cs, Co, taps, wop):
+    """Halo-tiled direct conv applies to stride-1 'same' convs with a 1-pixel reach (3x3/pad 1
+    forward and its dgrad) on 64-multiple channel counts."""
+    if not _HCONV or (sh, sw) != (1, 1) or (OH, OW) != (H, W) or len(taps) > 9:
+        return False
+    if any(abs(t[0]) > 1 or abs(t[1]) > 1 for t in taps):
+        return False
+    if len(taps) == 1:  # 1x1: the plain GEMM is already read-once
+        return False
+    return bool(kernels().hconv_supported(N, H, W, Cs, Co, len(taps)))
+
+
 def conv2d_fwd(x, w, bias, stride, pad, *, stats=False, residual=None, relu=False, out_fp32=False):
     """y = conv(x, w) + bias  [+ residual] [ReLU]; optional BN partial statistics slab.
 
@@ -97,6 +114,18 @@ def conv2d_fwd(x, w, bias, stride, pad, *, stats=False, residual=None, relu=Fals
         K.gemm_g2f(x.data_ptr(), w.data_ptr(), y.data_ptr(), _nbytes(x), _nbytes(w), M, Co, Ci, H, W, OH, OW, sh, sw,
                    _fwd_taps(Ci, W, KH, KW, ph, pw), KH * KW * Ci, Co, OH, OW, 1, 1, 0, 0, ptr(bias), ptr(residual),
                    ptr(slab), int(relu), ptr(sums), 2 * Co if stats else 0, stream_ptr())
+        return y, ((slab, rows, sums) if stats else None)
+    taps = _fwd_taps(Ci, W, KH, KW, ph, pw)
+    if not out_fp32 and _hconv_ok(N, OH, OW, H, W, sh, sw, Ci, Co, taps, w):
+        y = torch.empty((N, Co, OH, OW), dtype=BF16, device=x.device, memory_format=CL)
+        slab, rows, sums = None, 0, None
+        if stats:
+            rows = K.hconv_stat_rows(N, H, W, Co)
+            slab = torch.empty((rows, 2, Co), dtype=F32, device=x.device)
+            sums = torch.empty((2 * Co,), dtype=F32, device=x.device)  # zeroed in-kernel
+        K.hconv(x.data_ptr(), w.data_ptr(), y.data_ptr(), _nbytes(x), _nbytes(w), N, H, W, Ci, Co, KH * KW * Ci,
+                [(t[0], t[1], t[3]) for t in taps], ptr(bias), ptr(residual), ptr(slab), int(relu), ptr(sums),
+                2 * Co if stats else 0, stream_ptr())
         return y, ((slab, rows, sums) if stats else None)
     if _g2_ok(Ci, Co) and not out_fp32:
         y = torch.empty((N, Co, OH, OW), dtype=BF16, device=x.device, memory_format=CL)
@@ -211,6 +240,11 @@ def conv2d_dgrad(dy, wt, x_shape, stride, pad, *, residual=None):
         dx = torch.empty((N, Ci, H, W), dtype=odt, device=dy.device, memory_format=CL)
     st = stream_ptr()
     g2 = K.gemm_g2f if f32 else K.gemm_g2
+    if not f32 and len(classes) == 1 and not empty_class and \
+            _hconv_ok(N, H, W, OH, OW, sh, sw, Co, Ci, classes[0][4], wt):
+        K.hconv(dy.data_ptr(), wt.data_ptr(), dx.data_ptr(), _nbytes(dy), _nbytes(wt), N, OH, OW, Co, Ci, KH * KW * Co,
+                [(t[0], t[1], t[3]) for t in classes[0][4]], 0, ptr(residual), 0, 0, 0, 0, st)
+        return dx
     for ry, rx, GH, GW, taps in classes:
         g2(dy.data_ptr(), wt.data_ptr(), dx.data_ptr(), _nbytes(dy), _nbytes(wt), N * GH * GW, Ci, Co, OH, OW,
            GH, GW, 1, 1, taps, KH * KW * Co, Ci, H, W, sh, sw, ry, rx, 0, ptr(residual), 0, 0, 0, 0, st)
