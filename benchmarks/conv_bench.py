@@ -35,13 +35,17 @@ def main():
     ap.add_argument("--batch", type=int, default=256)
     ap.add_argument("--iters", type=int, default=20)
     ap.add_argument("--only", default="")
+    ap.add_argument("--shapes", default="", help="comma-separated shape names (default: all)")
     a = ap.parse_args()
     from dcnn_amd.ops import hip
     CL = torch.channels_last
     N = a.batch
     tot = {"fwd": 0.0, "dgrad": 0.0, "wgrad": 0.0}
     print(f"{'shape':<10}{'op':<7}{'us':>9}{'TFLOP/s':>9}")
+    keep = set(a.shapes.split(",")) if a.shapes else None
     for (nm, Ci, H, W, Co, k, s, p) in SHAPES:
+        if keep is not None and nm not in keep:
+            continue
         x = torch.randn(N, Ci, H, W, device="cuda").bfloat16().contiguous(memory_format=CL)
         w = (torch.randn(Co, Ci, k, k, device="cuda") * 0.05).bfloat16().contiguous(memory_format=CL)
         wf = w

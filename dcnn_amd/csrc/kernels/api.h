@@ -46,6 +46,17 @@ struct HConvArgs {
 void hconv(HConvArgs a, hipStream_t s);
 bool hconv_supported(int NB, int H, int W, int Cs, int N, int ntaps);
 int hconv_stat_rows(int NB, int H, int W, int N);
+// halo-tiled stride-1 weight gradient (hwgrad.hip): slab[split][Co][t*Cs + c] = partial dW
+struct HWArgs {
+  const bf16* dY; const bf16* X; float* slab; float* bias_slab;  // bias_slab[split][Co] (optional)
+  unsigned dy_bytes, x_bytes;
+  int NB, H, W, Cs, Co, ntaps;
+  int tap_dy[9], tap_dx[9];
+  int TH, TW, IMG, HPR, tiles_per_split, dbg;  // filled by the launcher
+};
+void hwgrad(HWArgs a, int splits, hipStream_t s);
+bool hwgrad_supported(int NB, int H, int W, int Cs, int Co, int ntaps);
+int hwgrad_splits(int NB, int H, int W, int Cs, int Co);
 
 void gemm_nt(const NtArgs& a, hipStream_t s);
 void gemm_g2(const G2Args& a, hipStream_t s);

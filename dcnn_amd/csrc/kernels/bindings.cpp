@@ -69,6 +69,21 @@ PYBIND11_MODULE(_kernels, m) {
         });
   m.def("hconv_supported", &hconv_supported);
   m.def("hconv_stat_rows", &hconv_stat_rows);
+  m.def("hwgrad",
+        [](uintptr_t dY, uintptr_t X, uintptr_t slab, uintptr_t bias_slab, unsigned dy_bytes, unsigned x_bytes, int NB,
+           int H, int W, int Cs, int Co, std::vector<std::array<int, 2>> taps, int splits, uintptr_t stream) {
+          HWArgs a{};
+          a.dY = P<const bf16*>(dY); a.X = P<const bf16*>(X); a.slab = P<float*>(slab);
+          a.bias_slab = P<float*>(bias_slab);
+          a.dy_bytes = dy_bytes; a.x_bytes = x_bytes;
+          a.NB = NB; a.H = H; a.W = W; a.Cs = Cs; a.Co = Co;
+          if (taps.size() > 9 || taps.empty()) throw std::runtime_error("hwgrad: 1..9 taps");
+          a.ntaps = (int)taps.size();
+          for (size_t i = 0; i < taps.size(); ++i) { a.tap_dy[i] = taps[i][0]; a.tap_dx[i] = taps[i][1]; }
+          hwgrad(a, splits, S(stream));
+        });
+  m.def("hwgrad_supported", &hwgrad_supported);
+  m.def("hwgrad_splits", &hwgrad_splits);
   m.def("gemm_g2f",
         [](uintptr_t A, uintptr_t B, uintptr_t C, unsigned a_bytes, unsigned b_bytes, int M, int N, int Cs, int H,
            int W, int GH, int GW, int SY, int SX, std::vector<std::array<int, 4>> taps, int ldb, int ldc, int OH,

@@ -47,6 +47,31 @@ __device__ __forceinline__ float wave_max(float v) {
   return v;
 }
 
+// ---- opaque 16-byte direct-to-LDS loads ------------------------------------------------------
+// The compiler's wait-count pass cannot tell which LDS bytes a builtin LDS-DMA load writes, so it
+// puts `s_waitcnt vmcnt(0)` in front of every later ds_read_b64_tr_b16 — which serialises a
+// double-buffered loop (the prefetch of tile k+1 must land before tile k is read). Issued from
+// inline asm the DMA is invisible to that pass; the kernels order it themselves with an explicit
+// `s_waitcnt vmcnt(0)` + barrier before the buffer is read.
+typedef int i32x4 __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ i32x4 raw_rsrc(const void* base, unsigned bytes) {
+  const uint64_t a = (uint64_t)base;
+  i32x4 r;
+  r[0] = (int)(uint32_t)a;
+  r[1] = (int)((a >> 32) & 0xffff);  // stride 0
+  r[2] = (int)bytes;                 // num_records: offsets >= bytes read zeros
+  r[3] = 0x00020000;
+  return r;
+}
+__device__ __forceinline__ void glds16_opaque(i32x4 rsrc, const char* lds, unsigned voff) {
+  const unsigned m0 = __builtin_amdgcn_readfirstlane(
+      (unsigned)(uintptr_t)((const __attribute__((address_space(3))) char*)lds));
+  asm volatile("s_mov_b32 m0, %0\n\ts_nop 0\n\tbuffer_load_dwordx4 %1, %2, 0 offen lds"
+               :
+               : "s"(m0), "v"(voff), "s"(rsrc)
+               : "memory", "m0");
+}
+
 // Block-wide sum for blockDim.x <= 1024 (wave64). `sh` needs >= 16 floats.
 __device__ __forceinline__ float block_sum(float v, float* sh) {
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6, nw = (blockDim.x + 63) >> 6;

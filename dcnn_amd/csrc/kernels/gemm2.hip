@@ -314,8 +314,9 @@ __global__ void __launch_bounds__(256, 2) gemm_t2_kernel(T2Args p) {
   const int kbeg = split * p.k_per_split;
   const int kend = min(p.P, kbeg + p.k_per_split);
 
-  const __amdgpu_buffer_rsrc_t rsA = __builtin_amdgcn_make_buffer_rsrc((void*)p.dY, (short)0, p.a_bytes, 0x00020000);
-  const __amdgpu_buffer_rsrc_t rsB = __builtin_amdgcn_make_buffer_rsrc((void*)p.X, (short)0, p.b_bytes, 0x00020000);
+  // opaque LDS DMA (common.h): keeps the next K-step's loads in flight across the tr reads
+  const i32x4 rsA = raw_rsrc(p.dY, p.a_bytes);
+  const i32x4 rsB = raw_rsrc(p.X, p.b_bytes);
 
   // A lanes: fixed column chunk (m), rows = pixels
   int a_row[T::A_INS];
@@ -370,7 +371,7 @@ __global__ void __launch_bounds__(256, 2) gemm_t2_kernel(T2Args p) {
     for (int i = 0; i < T::A_INS; ++i) {
       const int pix = k0 + a_row[i];
       const unsigned voff = (pix < kend && a_col[i] != kOOB) ? (unsigned)(pix * p.ldy * 2) + a_col[i] : kOOB;
-      glds16(rsA, As + (wid * T::A_INS + i) * 1024, voff);
+      glds16_opaque(rsA, As + (wid * T::A_INS + i) * 1024, voff);
     }
     if constexpr (FAST) {
       // the 64 pixels of a K-step start at a multiple of 64 and tile whole image rows (or whole
@@ -384,7 +385,7 @@ __global__ void __launch_bounds__(256, 2) gemm_t2_kernel(T2Args p) {
         const int sy = (gy0 + f_dgy[i]) * p.SY + b_dy[i];
         const bool ok = f_xok[i] && pix < kend && sy >= 0 && sy < p.H;
         const unsigned voff = ok ? (unsigned)((((long)img * p.H + sy) * p.W) * p.Cs * 2) + f_xoff[i] : kOOB;
-        glds16(rsB, Bs + (wid * T::B_INS + i) * 1024, voff);
+        glds16_opaque(rsB, Bs + (wid * T::B_INS + i) * 1024, voff);
       }
       return;
     }
@@ -401,7 +402,7 @@ __global__ void __launch_bounds__(256, 2) gemm_t2_kernel(T2Args p) {
       const int sy = gy * p.SY + b_dy[i], sx = gx * p.SX + b_dx[i];
       const bool ok = b_ok[i] && pix < kend && sy >= 0 && sy < p.H && sx >= 0 && sx < p.W;
       const unsigned voff = ok ? (unsigned)((((long)img * p.H + sy) * p.W + sx) * p.Cs * 2) + b_coff[i] : kOOB;
-      glds16(rsB, Bs + (wid * T::B_INS + i) * 1024, voff);
+      glds16_opaque(rsB, Bs + (wid * T::B_INS + i) * 1024, voff);
     }
   };
   auto tr_read = [&](const char* base, int rowbytes, int krow, int col0, auto rch) -> bf16x4 {

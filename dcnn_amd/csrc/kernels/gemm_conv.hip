@@ -504,8 +504,17 @@ __global__ void splitk_reduce_kernel(const float* __restrict__ slab, float* __re
   const long n4 = n / 4;
   const int s0 = blockIdx.y * per_group, s1 = min(splits, s0 + per_group);
   for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < n4; i += (long)gridDim.x * blockDim.x) {
+    // 8 independent 16-byte loads in flight per lane: the slab stream is latency-bound otherwise
     float4 s = make_float4(0, 0, 0, 0);
-    for (int k = s0; k < s1; ++k) {
+    int k = s0;
+    for (; k + 8 <= s1; k += 8) {
+      float4 v[8];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) v[u] = reinterpret_cast<const float4*>(slab + (long)(k + u) * n)[i];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) { s.x += v[u].x; s.y += v[u].y; s.z += v[u].z; s.w += v[u].w; }
+    }
+    for (; k < s1; ++k) {
       const float4 v = reinterpret_cast<const float4*>(slab + (long)k * n)[i];
       s.x += v.x; s.y += v.y; s.z += v.z; s.w += v.w;
     }

@@ -1,0 +1,307 @@
+// Halo-tiled weight gradient for stride-1 convolutions with a 1-pixel reach (3x3 pad 1) on
+// CDNA4 MFMA 16x16x32 bf16 — the wgrad counterpart of hconv.hip.
+//
+//   dW[co][t][ci] = sum_p dY[p][co] * X[p + off_t][ci]
+//
+// The gathered TN GEMM (gemm2.hip, gemm_t2) streams one (dY, X-gather) pair per tap column
+// block, i.e. the input is re-read 9x through L2 (~64 flop/byte). Here a workgroup owns a
+// 64(co) x 9(taps) x 64(ci) block of dW and a run of spatial pixel tiles (IMG x TH x TW = 128
+// pixels). Per tile it stages the dY tile [128 px][64 co] and the X halo
+// [(TH+2)(TW+2) px][64 ci] into LDS once (16-byte direct-to-LDS loads, zero-filled padding),
+// then all 9 taps read their B fragments from the same halo at a per-tap row offset; the dY
+// (A) fragments are read once per 32-pixel k-step and reused by the 9 taps (~240 flop/byte).
+// Fragments are pixel-major in LDS and read with ds_read_b64_tr_b16 (transposing LDS reads).
+//
+// Wave w (of 4) owns the 16 input channels w*16..+15 of every tap: acc[4 co subtiles][9 taps].
+// Workgroups of one split (same pixel tiles) are adjacent in the XCD-remapped order, so the
+// dY/X tiles they share stay in one XCD's L2. Split-K partials go to an fp32 slab
+// [split][Co][9*Cs] (same layout as gemm_t2) reduced by splitk_reduce.
+#include "common.h"
+#include "api.h"
+
+namespace dcnn {
+
+namespace {
+constexpr unsigned kOOBw = 0x80000000u;
+constexpr int PT = 128;  // pixels per spatial tile (GEMM K per tile)
+
+__device__ __forceinline__ void glds16w(i32x4 rsrc, char* lds, unsigned voff) { glds16_opaque(rsrc, lds, voff); }
+
+__device__ __forceinline__ int xcd_remap_w(int bid, int nwg) {
+  const int xcd = bid & 7, q = nwg >> 3, r = nwg & 7;
+  const int base = xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q;
+  return base + (bid >> 3);
+}
+
+// 128-byte rows (64 bf16), 16-byte chunk XOR pattern tuned for 4-row transposed reads
+__device__ __forceinline__ int wswz(int row) { return (((row >> 1) & 1) | (((row >> 3) & 1) << 1)) << 1; }
+
+// transposed fragment read: this lane gets rows krow..krow+3 (pixels) of column col0 + (lane & 15)
+__device__ __forceinline__ bf16x4 tr4(const char* base, int row, int col) {
+  const int chn = col >> 3, within = (col & 7) * 2;
+  const char* addr = base + row * 128 + ((chn ^ wswz(row)) << 4) + within;
+  return __builtin_amdgcn_ds_read_tr16_b64_v4bf16((__attribute__((address_space(3))) bf16x4*)(const_cast<char*>(addr)));
+}
+}  // namespace
+
+// compile-time tile geometry (TW x TH pixels x IMG images = 128): every per-lane index in the
+// prologue folds to shifts / constant multiplies — with one wave per SIMD nothing hides a long
+// integer-division prologue
+template <int TW, int TH, int IMG>
+struct HWGeo {
+  static constexpr int HW2 = TW + 2, HPI = (TH + 2) * HW2, HP = IMG * HPI;
+  static constexpr int HNI = (HP + 31) / 32;  // halo glds per wave per tile
+  static constexpr int HPR = HNI * 32;        // halo rows in LDS
+  static constexpr int TPX = TH * TW;
+  static constexpr int STAGE = PT * 128 + HPR * 128;
+  static constexpr int EPI_TAPS = (2 * STAGE) / (64 * 68 * 4);  // taps staged per epilogue pass
+  static_assert(TPX * IMG == PT, "tile must hold 128 pixels");
+};
+
+template <int TW, int TH, int IMG>
+__global__ void __launch_bounds__(256, 1) hwgrad_kernel(HWArgs p) {
+  using G = HWGeo<TW, TH, IMG>;
+  constexpr int HNI = G::HNI, HW2 = G::HW2, HPI = G::HPI, HP = G::HP, TPX = G::TPX, STAGE = G::STAGE;
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int co_tiles = p.Co / 64, ci_chunks = p.Cs / 64;
+  const int per_split = co_tiles * ci_chunks;
+  const int lt = xcd_remap_w(blockIdx.x, gridDim.x);
+  const int split = lt / per_split, rem = lt - split * per_split;
+  const int co0 = (rem / ci_chunks) * 64, c0 = (rem % ci_chunks) * 64;
+
+  const int tx_tiles = p.W / TW, ty_tiles = p.H / TH, tpi = tx_tiles * ty_tiles;
+  const int total_tiles = (p.NB / IMG) * tpi;
+  const int tbeg = split * p.tiles_per_split;
+  const int tend = min(total_tiles, tbeg + p.tiles_per_split);
+
+  // DCNN_HWGRAD_DBG (timing experiments only, results are wrong when set): bit 1 = no slab
+  // stores, bit 2 = no global loads (zero-record descriptors), bit 16 = no pixel tiles
+  const i32x4 rsY = raw_rsrc(p.dY, (p.dbg & 2) ? 0u : p.dy_bytes);
+  const i32x4 rsX = raw_rsrc(p.X, (p.dbg & 2) ? 0u : p.x_bytes);
+
+  // ---- dY loader: 4 glds per lane, rows (pixels) fixed relative to the tile origin ----
+  const int slot = lane & 7;
+  unsigned y_rel[4], y_col[4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int row = (wid * 4 + i) * 8 + (lane >> 3);
+    const int im = row / TPX, r2 = row - im * TPX;
+    y_rel[i] = (unsigned)((im * p.H + r2 / TW) * p.W + r2 % TW);
+    y_col[i] = (unsigned)((co0 + ((slot ^ wswz(row)) * 8)) * 2);
+  }
+  // ---- halo loader: row (im, hy, hx) of each lane fixed; only the validity test and a
+  //      uniform base move with the tile (6 VALU per 16-byte load) ----
+  int h_rel[HNI], h_hy[HNI], h_hx[HNI];
+#pragma unroll
+  for (int j = 0; j < HNI; ++j) {
+    const int row = (wid * HNI + j) * 8 + (lane >> 3);
+    const int im = row / HPI, r2 = row - im * HPI;
+    const int hy = r2 / HW2 - 1, hx = r2 % HW2 - 1;
+    const bool real = row < HP;
+    h_hy[j] = real ? hy : -(1 << 20);  // padding rows of the buffer: never valid
+    h_hx[j] = hx;
+    h_rel[j] = ((im * p.H + hy) * p.W + hx) * p.Cs * 2 + (c0 + ((slot ^ wswz(row)) * 8)) * 2;
+  }
+  auto load_tile = [&](int buf, int tile) {
+    char* Ys = smem + buf * STAGE;
+    char* Hs = Ys + PT * 128;
+    const int ig = tile / tpi, tr = tile - ig * tpi;
+    const int y0 = (tr / tx_tiles) * TH, x0 = (tr % tx_tiles) * TW;
+    const int g0 = (ig * IMG * p.H + y0) * p.W + x0;  // tile origin pixel
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+      glds16w(rsY, Ys + (wid * 4 + i) * 1024, (unsigned)(g0 + y_rel[i]) * (unsigned)(p.Co * 2) + y_col[i]);
+    const int gx = g0 * p.Cs * 2;
+#pragma unroll
+    for (int j = 0; j < HNI; ++j) {
+      const bool ok = (unsigned)(y0 + h_hy[j]) < (unsigned)p.H && (unsigned)(x0 + h_hx[j]) < (unsigned)p.W;
+      glds16w(rsX, Hs + (wid * HNI + j) * 1024, ok ? (unsigned)(gx + h_rel[j]) : kOOBw);
+    }
+  };
+
+  // ---- per-lane halo row of tap (0,0) for each of the 8 (k-step, half) pixel quads ----
+  int hrow[8];
+#pragma unroll
+  for (int s = 0; s < 8; ++s) {
+    const int px = (s >> 1) * 32 + 8 * (lane >> 4) + (s & 1) * 4 + ((lane & 15) >> 2);
+    const int im = px / TPX, r2 = px - im * TPX;
+    hrow[s] = im * HPI + (r2 / TW + 1) * HW2 + (r2 % TW + 1);
+  }
+  int toff[9];
+#pragma unroll
+  for (int t = 0; t < 9; ++t) toff[t] = p.tap_dy[t] * HW2 + p.tap_dx[t];
+
+  f32x4 acc[4][9];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int t = 0; t < 9; ++t) acc[i][t] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  const int bcol = wid * 16 + 4 * (lane & 3);  // B column (input channel) this lane reads
+  const bool do_bias = p.bias_slab != nullptr && c0 == 0;
+  float bias_acc = 0.f;
+  const int nt = (p.dbg & 16) ? 0 : tend - tbeg;
+  if (nt > 0) load_tile(0, tbeg);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  int cur = 0;
+  for (int it = 0; it < nt; ++it) {
+    if (it + 1 < nt) load_tile(cur ^ 1, tbeg + it + 1);
+    const char* Ys = smem + cur * STAGE;
+    const char* Hs = Ys + PT * 128;
+    // software pipeline over the 4 k-steps: the fragments of step kk+1 are read while the 36
+    // MFMAs of step kk run (one wave per SIMD: nothing else hides the LDS latency)
+    bf16x8 a[2][4], b[2][9];
+    auto read_step = [&](int kk, bf16x8* av, bf16x8* bv) {
+      const int krow = kk * 32 + 8 * (lane >> 4) + ((lane & 15) >> 2);
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int col = i * 16 + 4 * (lane & 3);
+        const bf16x4 lo = tr4(Ys, krow, col), hi = tr4(Ys, krow + 4, col);
+        av[i] = bf16x8{lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+      }
+#pragma unroll
+      for (int t = 0; t < 9; ++t) {
+        const bf16x4 lo = tr4(Hs, hrow[kk * 2] + toff[t], bcol), hi = tr4(Hs, hrow[kk * 2 + 1] + toff[t], bcol);
+        bv[t] = bf16x8{lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+      }
+    };
+    read_step(0, a[0], b[0]);
+#pragma unroll
+    for (int kk = 0; kk < 4; ++kk) {
+      const int c = kk & 1;
+      __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0): step kk's fragments have landed
+      if (kk + 1 < 4) read_step(kk + 1, a[c ^ 1], b[c ^ 1]);
+#pragma unroll
+      for (int t = 0; t < 9; ++t)
+#pragma unroll
+        for (int i = 0; i < 4; ++i) acc[i][t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[c][i], b[c][t], acc[i][t], 0, 0, 0);
+      if (kk + 1 < 4) {
+        // interleave: the 26 fragment reads of step kk+1 (and their address VALU) issue in the
+        // shadow of step kk's MFMAs instead of in front of them (in-order issue, 1 wave/SIMD)
+#pragma unroll
+        for (int g = 0; g < 26; ++g) {
+          __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);  // MFMA
+          __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);  // DS read
+          __builtin_amdgcn_sched_group_barrier(0x002, 2, 0);  // VALU
+        }
+        __builtin_amdgcn_sched_group_barrier(0x008, 10, 0);
+      }
+    }
+    if (do_bias) {  // bias gradient: column sums of the staged dY tile (first ci chunk only)
+      const int col = tid & 63, chn = col >> 3, w = (col & 7) * 2;
+      for (int r = tid >> 6; r < PT; r += 4)
+        bias_acc += (float)*reinterpret_cast<const bf16*>(Ys + r * 128 + ((chn ^ wswz(r)) << 4) + w);
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    cur ^= 1;
+  }
+
+  // ---- slab[split][co][t*Cs + ci]: taps staged through LDS (pitch 68 floats) so every lane
+  //      stores 16 contiguous bytes and each 16-lane group a whole 256-byte row segment ----
+  const long Ng = 9l * p.Cs;
+  float* out = p.slab + (long)split * p.Co * Ng;
+  float* stg = reinterpret_cast<float*>(smem);
+  constexpr int ET = G::EPI_TAPS;
+#pragma unroll
+  for (int t0 = 0; t0 < 9; t0 += ET) {
+    __syncthreads();
+#pragma unroll
+    for (int u = 0; u < ET; ++u) {
+      if (t0 + u < 9) {
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+#pragma unroll
+          for (int r = 0; r < 4; ++r)
+            stg[(u * 64 + i * 16 + (lane >> 4) * 4 + r) * 68 + wid * 16 + (lane & 15)] = acc[i][t0 + u][r];
+      }
+    }
+    __syncthreads();
+    const int nrows = (9 - t0 < ET ? 9 - t0 : ET) * 64;
+    for (int q = tid; q < nrows * 16; q += 256) {
+      const int row = q >> 4, c4 = (q & 15) * 4;
+      const int u = row >> 6, co = co0 + (row & 63);
+      const float4 v = *reinterpret_cast<const float4*>(stg + row * 68 + c4);
+      if (!(p.dbg & 1)) *reinterpret_cast<float4*>(out + (long)co * Ng + (t0 + u) * p.Cs + c0 + c4) = v;
+    }
+  }
+  if (do_bias) {
+    __syncthreads();
+    stg[tid] = bias_acc;
+    __syncthreads();
+    if (tid < 64) p.bias_slab[(long)split * p.Co + co0 + tid] = stg[tid] + stg[tid + 64] + stg[tid + 128] + stg[tid + 192];
+  }
+}
+
+// ---------------------------------------------------------------------------------------------
+// host side
+// ---------------------------------------------------------------------------------------------
+// supported tile geometries (TW, TH, IMG): W multiple of 16 and H of 8; 8x8; 4x4 maps
+static bool hw_geometry(int H, int W, int* TH, int* TW, int* IMG) {
+  if (W % 16 == 0 && H % 8 == 0) { *TW = 16; *TH = 8; *IMG = 1; return true; }
+  if (W == 8 && H == 8) { *TW = 8; *TH = 8; *IMG = 2; return true; }
+  if (W == 4 && H == 4) { *TW = 4; *TH = 4; *IMG = 8; return true; }
+  return false;
+}
+
+bool hwgrad_supported(int NB, int H, int W, int Cs, int Co, int ntaps) {
+  int th, tw, img;
+  if (Cs % 64 || Co % 64 || ntaps != 9) return false;  // 3x3 (all 9 taps unrolled)
+  if (!hw_geometry(H, W, &th, &tw, &img) || NB % img) return false;
+  // 32-bit buffer offsets
+  return (long)NB * H * W * (Cs > Co ? Cs : Co) * 2 < (1l << 31);
+}
+
+static int hw_target_blocks() {
+  static const int v = [] {
+    const char* e = getenv("DCNN_HWGRAD_BLOCKS");
+    const int x = e ? atoi(e) : 0;
+    return x > 0 ? x : 256;
+  }();
+  return v;
+}
+
+// number of split-K partial slabs (the caller sizes the slab [splits][Co][ntaps*Cs])
+int hwgrad_splits(int NB, int H, int W, int Cs, int Co) {
+  int th, tw, img;
+  if (!hw_geometry(H, W, &th, &tw, &img)) return 1;
+  const int total = (NB / img) * (H / th) * (W / tw);
+  const int per_split = (Co / 64) * (Cs / 64);
+  int want = (hw_target_blocks() + per_split - 1) / per_split;
+  if (want < 1) want = 1;
+  if (want > total) want = total;
+  const int tps = (total + want - 1) / want;
+  return (total + tps - 1) / tps;
+}
+
+void hwgrad(HWArgs a, int splits, hipStream_t s) {
+  if (!hwgrad_supported(a.NB, a.H, a.W, a.Cs, a.Co, a.ntaps)) throw std::runtime_error("hwgrad: unsupported shape");
+  for (int t = 0; t < a.ntaps; ++t)
+    if (a.tap_dy[t] < -1 || a.tap_dy[t] > 1 || a.tap_dx[t] < -1 || a.tap_dx[t] > 1)
+      throw std::runtime_error("hwgrad: taps must reach at most 1 pixel");
+  if (splits != hwgrad_splits(a.NB, a.H, a.W, a.Cs, a.Co)) throw std::runtime_error("hwgrad: split count mismatch");
+  hw_geometry(a.H, a.W, &a.TH, &a.TW, &a.IMG);
+  const int total = (a.NB / a.IMG) * (a.H / a.TH) * (a.W / a.TW);
+  a.tiles_per_split = (total + splits - 1) / splits;
+  static const int dbg = [] { const char* e = getenv("DCNN_HWGRAD_DBG"); return e ? atoi(e) : 0; }();
+  a.dbg = dbg;  // timing experiments only (results are wrong when set)
+  const int grid = splits * (a.Co / 64) * (a.Cs / 64);
+#define DCNN_HW(TW_, TH_, IMG_)                                                                         \
+  if (a.TW == TW_ && a.TH == TH_ && a.IMG == IMG_) {                                                    \
+    auto k = hwgrad_kernel<TW_, TH_, IMG_>;                                                             \
+    const int lds = 2 * HWGeo<TW_, TH_, IMG_>::STAGE;                                                   \
+    DCNN_HIP_CHECK(hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, lds)); \
+    hipLaunchKernelGGL(k, dim3(grid), dim3(256), lds, s, a);                                            \
+    DCNN_LAUNCH_CHECK();                                                                                \
+    return;                                                                                             \
+  }
+  DCNN_HW(16, 8, 1)
+  DCNN_HW(8, 8, 2)
+  DCNN_HW(4, 4, 8)
+#undef DCNN_HW
+  throw std::runtime_error("hwgrad: no kernel for this geometry");
+}
+
+}  // namespace dcnn

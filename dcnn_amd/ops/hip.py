@@ -67,6 +67,7 @@ def _g2_ok(Cs, N):
 
 
 _HCONV = os.environ.get("DCNN_HCONV", "1") != "0"
+_HWGRAD = os.environ.get("DCNN_HWGRAD", "1") != "0"
 
 
 def _hconv_ok(N, OH, OW, H, W, sh, sw, Cs, Co, taps, wop):
@@ -272,6 +273,21 @@ def conv2d_wgrad(dy, x, w_shape, stride, pad, grad_w, grad_b=None):
         K.gemm_t2f(dy.data_ptr(), x.data_ptr(), slab.data_ptr(), ptr(bslab), Co, Ng, P, Co, Ci, H, W, OH, OW,
                    stride[0], stride[1], taps, splits, st)
         assert grad_w.is_contiguous(memory_format=CL) or KH * KW == 1 or Ci == 1
+        K.splitk_reduce(slab.data_ptr(), grad_w.data_ptr(), Co * Ng, splits, 1, st)
+        if grad_b is not None:
+            K.splitk_reduce(bslab.data_ptr(), grad_b.data_ptr(), Co, splits, 1, st)
+        return
+    taps = [(ky - pad[0], kx - pad[1]) for ky in range(KH) for kx in range(KW)]
+    if (Cx == Ci and _HWGRAD and tuple(stride) == (1, 1) and (OH, OW) == (H, W)
+            and 1 < len(taps) <= 9 and all(abs(a) <= 1 and abs(b) <= 1 for a, b in taps)
+            and K.hwgrad_supported(N, H, W, Ci, Co, len(taps))):
+        # halo-tiled wgrad: X read ~1.4x instead of once per tap
+        Ng = KH * KW * Ci
+        splits = K.hwgrad_splits(N, H, W, Ci, Co)
+        slab = torch.empty((splits, Co, Ng), dtype=F32, device=x.device)
+        bslab = torch.empty((splits, Co), dtype=F32, device=x.device) if grad_b is not None else None
+        K.hwgrad(dy.data_ptr(), x.data_ptr(), slab.data_ptr(), ptr(bslab), _nbytes(dy), _nbytes(x), N, H, W, Ci, Co,
+                 taps, splits, st)
         K.splitk_reduce(slab.data_ptr(), grad_w.data_ptr(), Co * Ng, splits, 1, st)
         if grad_b is not None:
             K.splitk_reduce(bslab.data_ptr(), grad_b.data_ptr(), Co, splits, 1, st)

@@ -84,6 +84,28 @@ def test_conv_fwd_dgrad_wgrad(hip, case):
     assert rel_err(gb, dyb.sum((0, 2, 3)) + 1) < 1e-2
 
 
+@pytest.mark.parametrize("case", [
+    # N, Ci, H, W, Co: halo-tiled wgrad geometries (TW=16 / 8 / 4, several images per tile)
+    (4, 64, 32, 32, 64), (6, 128, 16, 16, 64), (4, 64, 16, 16, 192), (8, 256, 8, 8, 128), (16, 128, 4, 4, 256),
+    (3, 64, 16, 48, 64),
+])
+def test_halo_wgrad(hip, case):
+    from dcnn_amd.ops._ext import kernels
+    N, Ci, H, W, Co = case
+    assert kernels().hwgrad_supported(N, H, W, Ci, Co, 9)
+    torch.manual_seed(1)
+    x = torch.randn(N, Ci, H, W)
+    dy = torch.randn(N, Co, H, W)
+    xg = x.cuda().to(torch.bfloat16).contiguous(memory_format=CL)
+    dyg = dy.cuda().to(torch.bfloat16).contiguous(memory_format=CL)
+    gw = torch.full((Co, Ci, 3, 3), 0.5, device="cuda").contiguous(memory_format=CL)
+    gb = torch.ones(Co, device="cuda")
+    hip.conv2d_wgrad(dyg, xg, (Co, Ci, 3, 3), (1, 1), (1, 1), gw, gb)
+    dw_ref = torch.nn.grad.conv2d_weight(bf(x), (Co, Ci, 3, 3), bf(dy), 1, 1) + 0.5
+    assert rel_err(gw, dw_ref) < 1e-3, rel_err(gw, dw_ref)
+    assert rel_err(gb, bf(dy).sum((0, 2, 3)) + 1) < 1e-4
+
+
 def test_padded_rgb_stem(hip):
     """RGB stem runs on the vector path with channels zero-padded 3 -> 8."""
     torch.manual_seed(9)
