@@ -37,7 +37,7 @@ def main():
     ap.add_argument("--model", default="resnet18_tiny_imagenet")
     ap.add_argument("--graph", type=int, default=int(os.environ.get("DCNN_BENCH_GRAPH", "1")),
                     help="capture the per-step compute in a hipGraph (1) or run eagerly (0)")
-    ap.add_argument("--bucket-mb", type=float, default=32.0)
+    ap.add_argument("--bucket-mb", type=float, default=4.0)
     ap.add_argument("--profile", action="store_true", help="print per-layer device times")
     ap.add_argument("--device", default="cuda")
     ap.add_argument("--dtype", default="bf16", choices=["bf16", "fp32"],

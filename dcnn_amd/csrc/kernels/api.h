@@ -81,6 +81,9 @@ void conv_weight_transpose_f32(const float* w, float* wt, int Co, int T_, int Ci
 void gemm_tn(TnArgs a, int splits, hipStream_t s);
 int gemm_tn_splits(int M, int N, int P);
 void splitk_reduce(const float* slab, float* out, long n, int splits, int accumulate, hipStream_t s);
+// weight + bias slabs in one launch (nb = 0: bias segment absent)
+void splitk_reduce2(const float* slab, float* out, long n, const float* bslab, float* bout, long nb, int splits,
+                    int accumulate, hipStream_t s);
 
 int bn_partial_rows(long R, int C);
 void bn_partial(int dtype, const void* x, const void* dy, const void* yout, void* dy_out, const float* mean,

@@ -166,6 +166,11 @@ PYBIND11_MODULE(_kernels, m) {
   m.def("splitk_reduce", [](uintptr_t slab, uintptr_t out, long n, int splits, int acc, uintptr_t st) {
     splitk_reduce(P<const float*>(slab), P<float*>(out), n, splits, acc, S(st));
   });
+  m.def("splitk_reduce2", [](uintptr_t slab, uintptr_t out, long n, uintptr_t bslab, uintptr_t bout, long nb,
+                             int splits, int acc, uintptr_t st) {
+    splitk_reduce2(P<const float*>(slab), P<float*>(out), n, P<const float*>(bslab), P<float*>(bout), nb, splits, acc,
+                   S(st));
+  });
 
   m.def("bn_partial_rows", &bn_partial_rows);
   m.def("bn_partial", [](int dt, uintptr_t x, uintptr_t dy, uintptr_t yout, uintptr_t dy_out, uintptr_t mean,

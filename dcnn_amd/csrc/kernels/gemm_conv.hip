@@ -495,15 +495,22 @@ __global__ void __launch_bounds__(256, 2) gemm_tn_kernel(TnArgs p) {
   }
 }
 
-// out[i] (+)= sum_s slab[s][i]   (float4 when aligned)
 // out[i] (+)= sum_s slab[s][i]. 2-D grid: blockIdx.y picks a group of splits so the reduce has
 // enough workgroups to fill the chip even when the output (a weight gradient) is tiny; groups
 // combine with float atomics (accumulate semantics, the gradient buffer is zeroed per step).
-__global__ void splitk_reduce_kernel(const float* __restrict__ slab, float* __restrict__ out, long n,
-                                     int splits, int per_group, int atomic) {
-  const long n4 = n / 4;
-  const int s0 = blockIdx.y * per_group, s1 = min(splits, s0 + per_group);
-  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < n4; i += (long)gridDim.x * blockDim.x) {
+// One launch reduces up to two slabs (a weight gradient and its bias gradient): blocks
+// [0, gxa) take segment a, the rest segment b — one kernel boundary per layer instead of two.
+struct SplitkSeg {
+  const float* slab;
+  float* out;
+  long n;
+};
+
+__device__ __forceinline__ void splitk_segment(const SplitkSeg g, long bid, long nblk, int s0, int s1, int atomic) {
+  const long n = g.n, n4 = n / 4;
+  const float* __restrict__ slab = g.slab;
+  float* __restrict__ out = g.out;
+  for (long i = bid * blockDim.x + threadIdx.x; i < n4; i += nblk * blockDim.x) {
     // 8 independent 16-byte loads in flight per lane: the slab stream is latency-bound otherwise
     float4 s = make_float4(0, 0, 0, 0);
     int k = s0;
@@ -527,11 +534,19 @@ __global__ void splitk_reduce_kernel(const float* __restrict__ slab, float* __re
       reinterpret_cast<float4*>(out)[i] = c;
     }
   }
-  for (long i = n4 * 4 + blockIdx.x * (long)blockDim.x + threadIdx.x; i < n; i += (long)gridDim.x * blockDim.x) {
+  for (long i = n4 * 4 + bid * blockDim.x + threadIdx.x; i < n; i += nblk * blockDim.x) {
     float s = 0.f;
     for (int k = s0; k < s1; ++k) s += slab[(long)k * n + i];
     if (atomic) atomicAdd(out + i, s); else out[i] += s;
   }
+}
+
+__global__ void splitk_reduce_kernel(SplitkSeg a, SplitkSeg b, int gxa, int splits, int per_group, int atomic) {
+  const int s0 = blockIdx.y * per_group, s1 = min(splits, s0 + per_group);
+  if ((int)blockIdx.x < gxa)
+    splitk_segment(a, blockIdx.x, gxa, s0, s1, atomic);
+  else
+    splitk_segment(b, blockIdx.x - gxa, gridDim.x - gxa, s0, s1, atomic);
 }
 
 // ----------------------------------------------------------------------------------------
@@ -625,19 +640,29 @@ void gemm_tn(TnArgs a, int splits, hipStream_t s) {
   throw std::runtime_error("gemm_tn: no kernel variant");
 }
 
-void splitk_reduce(const float* slab, float* out, long n, int splits, int accumulate, hipStream_t s) {
-  if (!accumulate) DCNN_HIP_CHECK(hipMemsetAsync(out, 0, sizeof(float) * n, s));
+void splitk_reduce2(const float* slab, float* out, long n, const float* bslab, float* bout, long nb, int splits,
+                    int accumulate, hipStream_t s) {
+  if (!accumulate) {
+    DCNN_HIP_CHECK(hipMemsetAsync(out, 0, sizeof(float) * n, s));
+    if (nb > 0) DCNN_HIP_CHECK(hipMemsetAsync(bout, 0, sizeof(float) * nb, s));
+  }
   const long n4 = n / 4 + 1;
-  const int gx = grid_for(n4, 256, 4096);
+  const int gxa = grid_for(n4, 256, 4096);
+  const int gxb = nb > 0 ? grid_for(nb / 4 + 1, 256, 64) : 0;
   long want = (131072 + n4 - 1) / n4;  // aim for >= 512 workgroups in total
   long groups = (splits + 3) / 4;
   if (groups > want) groups = want;
   if (groups < 1) groups = 1;
   const int per = (int)((splits + groups - 1) / groups);
   groups = (splits + per - 1) / per;
-  hipLaunchKernelGGL(splitk_reduce_kernel, dim3(gx, (unsigned)groups), dim3(256), 0, s, slab, out, n, splits, per,
-                     groups > 1 ? 1 : 0);
+  const SplitkSeg a{slab, out, n}, b{bslab, bout, nb > 0 ? nb : 0};
+  hipLaunchKernelGGL(splitk_reduce_kernel, dim3(gxa + gxb, (unsigned)groups), dim3(256), 0, s, a, b, gxa, splits,
+                     per, groups > 1 ? 1 : 0);
   DCNN_LAUNCH_CHECK();
+}
+
+void splitk_reduce(const float* slab, float* out, long n, int splits, int accumulate, hipStream_t s) {
+  splitk_reduce2(slab, out, n, nullptr, nullptr, 0, splits, accumulate, s);
 }
 
 }  // namespace dcnn

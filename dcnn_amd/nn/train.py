@@ -49,7 +49,7 @@ class TrainingConfig:
     device_type: str = "CPU"
     num_microbatches: int = 2
     use_graph: bool = True          # hipGraph-captured step on the GPU
-    bucket_mb: float = 32.0         # DP all-reduce bucket size
+    bucket_mb: float = 4.0          # DP all-reduce bucket size (small trailing bucket = little exposed comm)
     snapshot_dir: str = "model_snapshots"
     max_batches_per_epoch: int = 0  # 0 = full epoch
 

@@ -252,6 +252,14 @@ def conv2d_dgrad(dy, wt, x_shape, stride, pad, *, residual=None):
     return dx
 
 
+def _reduce_wb(K, slab, grad_w, n, bslab, grad_b, nb, splits, st):
+    """grad_w += sum over splits of slab, grad_b += sum of bslab — one launch for both."""
+    if grad_b is None:
+        K.splitk_reduce(slab.data_ptr(), grad_w.data_ptr(), n, splits, 1, st)
+    else:
+        K.splitk_reduce2(slab.data_ptr(), grad_w.data_ptr(), n, bslab.data_ptr(), grad_b.data_ptr(), nb, splits, 1, st)
+
+
 def conv2d_wgrad(dy, x, w_shape, stride, pad, grad_w, grad_b=None):
     """grad_w (+)= dW, grad_b (+)= sum(dy): split-K MFMA GEMM + fp32 slab reduce (beta = 1).
 
@@ -273,9 +281,7 @@ def conv2d_wgrad(dy, x, w_shape, stride, pad, grad_w, grad_b=None):
         K.gemm_t2f(dy.data_ptr(), x.data_ptr(), slab.data_ptr(), ptr(bslab), Co, Ng, P, Co, Ci, H, W, OH, OW,
                    stride[0], stride[1], taps, splits, st)
         assert grad_w.is_contiguous(memory_format=CL) or KH * KW == 1 or Ci == 1
-        K.splitk_reduce(slab.data_ptr(), grad_w.data_ptr(), Co * Ng, splits, 1, st)
-        if grad_b is not None:
-            K.splitk_reduce(bslab.data_ptr(), grad_b.data_ptr(), Co, splits, 1, st)
+        _reduce_wb(K, slab, grad_w, Co * Ng, bslab, grad_b, Co, splits, st)
         return
     taps = [(ky - pad[0], kx - pad[1]) for ky in range(KH) for kx in range(KW)]
     if (Cx == Ci and _HWGRAD and tuple(stride) == (1, 1) and (OH, OW) == (H, W)
@@ -288,9 +294,7 @@ def conv2d_wgrad(dy, x, w_shape, stride, pad, grad_w, grad_b=None):
         bslab = torch.empty((splits, Co), dtype=F32, device=x.device) if grad_b is not None else None
         K.hwgrad(dy.data_ptr(), x.data_ptr(), slab.data_ptr(), ptr(bslab), _nbytes(dy), _nbytes(x), N, H, W, Ci, Co,
                  taps, splits, st)
-        K.splitk_reduce(slab.data_ptr(), grad_w.data_ptr(), Co * Ng, splits, 1, st)
-        if grad_b is not None:
-            K.splitk_reduce(bslab.data_ptr(), grad_b.data_ptr(), Co, splits, 1, st)
+        _reduce_wb(K, slab, grad_w, Co * Ng, bslab, grad_b, Co, splits, st)
         return
     if _g2_ok(Cx, Co) and P < (1 << 24):
         Ng = KH * KW * Cx
@@ -316,9 +320,7 @@ def conv2d_wgrad(dy, x, w_shape, stride, pad, grad_w, grad_b=None):
     K.gemm_tn(dy.data_ptr(), x.data_ptr(), slab.data_ptr(), ptr(bslab), Co, Ng, P, CONV_FWD,
               N, H, W, Ci, OH, OW, KH, KW, stride[0], stride[1], pad[0], pad[1], 0, splits, st)
     assert grad_w.is_contiguous(memory_format=CL) or KH * KW == 1 or Ci == 1
-    K.splitk_reduce(slab.data_ptr(), grad_w.data_ptr(), Co * Ng, splits, 1, st)
-    if grad_b is not None:
-        K.splitk_reduce(bslab.data_ptr(), grad_b.data_ptr(), Co, splits, 1, st)
+    _reduce_wb(K, slab, grad_w, Co * Ng, bslab, grad_b, Co, splits, st)
 
 
 def dense_fwd(x2d, w2d, bias):
@@ -386,9 +388,7 @@ def dense_wgrad(dy2d, x2d, grad_w, grad_b=None):
         bslab = torch.empty((splits, Out), dtype=F32, device=x2d.device) if grad_b is not None else None
         K.gemm_tn(dy2d.data_ptr(), x2d.data_ptr(), slab.data_ptr(), ptr(bslab), Out, In, N, PLAIN,
                   0, 0, 0, 0, 1, 1, 1, 1, 1, 1, 0, 0, In, splits, st)
-    K.splitk_reduce(slab.data_ptr(), grad_w.data_ptr(), Out * In, splits, 1, st)
-    if grad_b is not None:
-        K.splitk_reduce(bslab.data_ptr(), grad_b.data_ptr(), Out, splits, 1, st)
+    _reduce_wb(K, slab, grad_w, Out * In, bslab, grad_b, Out, splits, st)
 
 
 # ------------------------------------------------------------------------------ batch norm

@@ -4,8 +4,10 @@ One process per GPU (`torch.distributed`, backend "nccl" = RCCL on ROCm, "gloo" 
 Gradients live in the model's flat fp32 arena; they are all-reduced in *buckets* that are
 contiguous slices of that buffer, launched asynchronously from inside the backward pass as
 soon as the layers covering a bucket have finished (last layers first), so RCCL traffic over
-xGMI overlaps the remaining backward compute. Buckets default to ~32 MB: large enough to run
-near the per-link xGMI bandwidth, few enough that the launch cost is negligible.
+xGMI overlaps the remaining backward compute. Buckets default to ~4 MB (built from the last
+layer backwards, so ResNet-18-tiny gets 19 / 15 / 4.7 / 4.9 / 1.5 MB buckets): the only
+all-reduce that cannot overlap compute is the trailing one after the stem's backward, so it
+should be small, while every bucket stays large enough to run near per-link xGMI bandwidth.
 
 The 1/world factor of the gradient average is folded into the incoming loss gradient (every
 gradient is linear in it), so the all-reduce is a plain SUM and no extra pass over the
@@ -39,7 +41,7 @@ def init_distributed(backend: Optional[str] = None) -> Tuple[int, int, int]:
 
 
 class DataParallel:
-    def __init__(self, model: Sequential, process_group=None, bucket_mb: float = 32.0, broadcast: bool = True):
+    def __init__(self, model: Sequential, process_group=None, bucket_mb: float = 4.0, broadcast: bool = True):
         if not model.initialized:
             model.initialize()
         self.model = model
