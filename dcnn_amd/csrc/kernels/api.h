@@ -5,6 +5,14 @@
 typedef __bf16 bf16;
 
 namespace dcnn {
+// Backward-BatchNorm fusion into a dgrad epilogue. The GEMM output is the gradient arriving at
+// a BatchNorm(+ReLU) layer: the epilogue masks it with that layer's ReLU output (y > 0, when y
+// is set), stores the masked gradient dy', and writes per-tile (sum dy', sum dy' * xhat) rows
+// into `stats`, xhat = (x - mean) * istd — the statistics the BN backward needs, without a
+// separate pass over dy, x and y. Inactive when x == nullptr.
+struct BnbArgs {
+  const bf16* y; const bf16* x; const float* mean; const float* istd;
+};
 struct NtArgs {
   const bf16* A; const bf16* B; void* C;
   int M, N, K; int lda, ldb, ldc; int mode;
@@ -24,6 +32,7 @@ struct G2Args {
   int OH, OW, OSY, OSX, ORY, ORX;
   const float* bias; const bf16* residual; float* stats; int relu;
   float* zero_ptr; int zero_n;  // zeroed by workgroup 0 (BN sums consumed by the next kernel)
+  BnbArgs bnb;
 };
 struct T2Args {
   const bf16* dY; const bf16* X; float* slab; float* bias_slab;
@@ -42,6 +51,7 @@ struct HConvArgs {
   int TH, TW, IMG, HPR;  // filled by the launcher (HPR: halo rows padded to 32)
   const float* bias; const bf16* residual; float* stats; int relu;
   float* zero_ptr; int zero_n;  // zeroed by workgroup 0 (BN sums accumulated by the next kernel)
+  BnbArgs bnb;
 };
 void hconv(HConvArgs a, hipStream_t s);
 bool hconv_supported(int NB, int H, int W, int Cs, int N, int ntaps);

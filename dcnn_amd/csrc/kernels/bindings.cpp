@@ -55,8 +55,9 @@ PYBIND11_MODULE(_kernels, m) {
   m.def("hconv",
         [](uintptr_t A, uintptr_t B, uintptr_t C, unsigned a_bytes, unsigned b_bytes, int NB, int H, int W, int Cs,
            int N, int ldb, std::vector<std::array<int, 3>> taps, uintptr_t bias, uintptr_t residual, uintptr_t stats,
-           int relu, uintptr_t zero_ptr, int zero_n, uintptr_t stream) {
+           int relu, uintptr_t zero_ptr, int zero_n, std::array<uintptr_t, 4> bnb, uintptr_t stream) {
           HConvArgs a{};
+          a.bnb = BnbArgs{P<const bf16*>(bnb[0]), P<const bf16*>(bnb[1]), P<const float*>(bnb[2]), P<const float*>(bnb[3])};
           a.zero_ptr = P<float*>(zero_ptr); a.zero_n = zero_n;
           a.A = P<const bf16*>(A); a.B = P<const bf16*>(B); a.C = P<bf16*>(C);
           a.a_bytes = a_bytes; a.b_bytes = b_bytes;
@@ -88,8 +89,9 @@ PYBIND11_MODULE(_kernels, m) {
         [](uintptr_t A, uintptr_t B, uintptr_t C, unsigned a_bytes, unsigned b_bytes, int M, int N, int Cs, int H,
            int W, int GH, int GW, int SY, int SX, std::vector<std::array<int, 4>> taps, int ldb, int ldc, int OH,
            int OW, int OSY, int OSX, int ORY, int ORX, uintptr_t bias, uintptr_t residual, uintptr_t stats, int relu,
-           uintptr_t zero_ptr, int zero_n, uintptr_t stream) {
+           uintptr_t zero_ptr, int zero_n, std::array<uintptr_t, 4> bnb, uintptr_t stream) {
           G2Args a{};  // fp32 operands (pointers reinterpreted by the kernel)
+          if (bnb[1]) throw std::runtime_error("gemm_g2f: backward-BN epilogue fusion is bf16-only");
           a.A = P<const bf16*>(A); a.B = P<const bf16*>(B); a.C = P<bf16*>(C);
           a.a_bytes = a_bytes; a.b_bytes = b_bytes;
           a.M = M; a.N = N; a.Cs = Cs; a.H = H; a.W = W; a.GH = GH; a.GW = GW; a.SY = SY; a.SX = SX;
@@ -124,8 +126,9 @@ PYBIND11_MODULE(_kernels, m) {
         [](uintptr_t A, uintptr_t B, uintptr_t C, unsigned a_bytes, unsigned b_bytes, int M, int N, int Cs, int H,
            int W, int GH, int GW, int SY, int SX, std::vector<std::array<int, 4>> taps, int ldb, int ldc, int OH,
            int OW, int OSY, int OSX, int ORY, int ORX, uintptr_t bias, uintptr_t residual, uintptr_t stats, int relu,
-           uintptr_t zero_ptr, int zero_n, uintptr_t stream) {
+           uintptr_t zero_ptr, int zero_n, std::array<uintptr_t, 4> bnb, uintptr_t stream) {
           G2Args a{};
+          a.bnb = BnbArgs{P<const bf16*>(bnb[0]), P<const bf16*>(bnb[1]), P<const float*>(bnb[2]), P<const float*>(bnb[3])};
           a.A = P<const bf16*>(A); a.B = P<const bf16*>(B); a.C = P<bf16*>(C);
           a.a_bytes = a_bytes; a.b_bytes = b_bytes;
           a.M = M; a.N = N; a.Cs = Cs; a.H = H; a.W = W; a.GH = GH; a.GW = GW; a.SY = SY; a.SX = SX;

@@ -227,9 +227,14 @@ __global__ void __launch_bounds__(256, 2) gemm_g2_kernel(G2Args p) {
   const int cg = tid % CG, r0 = tid / CG;
   const int ncol = n0 + cg * 8;
   const bool col_ok = ncol < p.N;      // N % 8 == 0 for this kernel
-  float s[8], q[8];
+  float s[8], q[8], mu[8], is[8];
 #pragma unroll
-  for (int v = 0; v < 8; ++v) s[v] = q[v] = 0.f;
+  for (int v = 0; v < 8; ++v) s[v] = q[v] = mu[v] = is[v] = 0.f;
+  const bool bnb = p.bnb.x != nullptr;  // backward-BN fusion (api.h BnbArgs)
+  if (bnb && col_ok) {
+#pragma unroll
+    for (int v = 0; v < 8; ++v) { mu[v] = p.bnb.mean[ncol + v]; is[v] = p.bnb.istd[ncol + v]; }
+  }
   const int ghw = p.GH * p.GW;
   for (int row = r0; row < BM; row += RSTEP) {
     const int m = m0 + row;
@@ -249,13 +254,26 @@ __global__ void __launch_bounds__(256, 2) gemm_g2_kernel(G2Args p) {
 #pragma unroll
       for (int v = 0; v < 8; ++v) f[v] = fmaxf(f[v], 0.f);
     }
+    if (bnb && p.bnb.y) {
+      float yo[8];
+      unpack8(*reinterpret_cast<const uint4*>(p.bnb.y + orow * p.ldc + ncol), yo);
+#pragma unroll
+      for (int v = 0; v < 8; ++v) f[v] = yo[v] > 0.f ? f[v] : 0.f;
+    }
     const uint4 o = pack8(f);
     *reinterpret_cast<uint4*>(reinterpret_cast<bf16*>(p.C) + orow * p.ldc + ncol) = o;
     if (p.stats) {
       float g[8];
       unpack8(o, g);
+      if (bnb) {
+        float xv[8];
+        unpack8(*reinterpret_cast<const uint4*>(p.bnb.x + orow * p.ldc + ncol), xv);
 #pragma unroll
-      for (int v = 0; v < 8; ++v) { s[v] += g[v]; q[v] += g[v] * g[v]; }
+        for (int v = 0; v < 8; ++v) { s[v] += g[v]; q[v] += g[v] * (xv[v] - mu[v]) * is[v]; }
+      } else {
+#pragma unroll
+        for (int v = 0; v < 8; ++v) { s[v] += g[v]; q[v] += g[v] * g[v]; }
+      }
     }
   }
   if (p.stats) {

@@ -43,6 +43,25 @@ class LayerConfig(dict):
         return self["parameters"].get(key, default)
 
 
+def run_backward(layers, i: int, grad, mb_id: int = 0):
+    """``layers[i].backward(grad, mb_id)`` inside a layer chain, with the backward-BN fusion
+    request of the layer that will consume its output (the nearest non-passthrough layer below
+    it, see ``Layer.bwd_bn_spec``) attached for the duration of the call."""
+    l = layers[i]
+    req = None
+    if l.needs_input_grad:
+        j = i - 1
+        while j >= 0 and layers[j].passthrough:
+            j -= 1
+        if j >= 0:
+            req = layers[j].bwd_bn_spec(mb_id)
+    l._bnb_request = req
+    try:
+        return l.backward(grad, mb_id)
+    finally:
+        l._bnb_request = None
+
+
 class Layer:
     type_name = "layer"
 
@@ -123,6 +142,18 @@ class Layer:
 
     def backward(self, grad: torch.Tensor, mb_id: int = 0) -> Optional[torch.Tensor]:
         raise NotImplementedError
+
+    # ---------------------------------------------------------------- backward fusion hooks
+    # A container asks the layer that will RECEIVE a gradient for a fusion request
+    # (``bwd_bn_spec``) and hands it to the layer that PRODUCES that gradient via
+    # ``_bnb_request`` for the duration of its backward call (see ``run_backward``).
+    _bnb_request = None
+    passthrough = False
+
+    def bwd_bn_spec(self, mb_id: int = 0):
+        """``ops.hip.BnbRequest`` when this layer's backward starts with a BatchNorm whose ReLU mask
+        and statistics the gradient's producer may fuse into its epilogue; None otherwise."""
+        return None
 
     def _on_gpu(self) -> bool:
         return self.device.is_gpu()

@@ -105,7 +105,7 @@ class Conv2D(ParameterizedLayer):
                 wt = hip.conv_weight_t(self.weight_operand(0), dtype=self.compute_dtype)
             res = hip.to_act(add_to, self.compute_dtype) if add_to is not None else None
             return hip.conv2d_dgrad(g, wt, x_shape, (self.stride_h, self.stride_w), (self.pad_h, self.pad_w),
-                                    residual=res)
+                                    residual=res, bnb=self._bnb_request)
         st, pd = (self.stride_h, self.stride_w), (self.pad_h, self.pad_w)
         self._grads[0].add_(torch.nn.grad.conv2d_weight(x, self.weights.shape, grad, st, pd))
         if self.use_bias:

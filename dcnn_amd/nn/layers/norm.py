@@ -118,9 +118,12 @@ class BatchNorm(ParameterizedLayer):
         db = self._grads[1].view(-1) if self.affine else None
         if x.is_cuda:
             from ...ops import hip
+            pre = getattr(grad, "_bnb", None)
+            fused = pre[1:] if (pre is not None and pre[0] is self) else None
             g = hip.to_act(grad, self.compute_dtype)
             dx, dmask = hip.bn_backward(g, x, yout, mean, istd, self._gamma(), dg, db,
-                                        want_masked=self.emit_masked_grad, eval_mode=not was_training)
+                                        want_masked=self.emit_masked_grad, eval_mode=not was_training,
+                                        fused=fused)
             if self.emit_masked_grad:
                 self._last_masked[mb_id] = dmask if dmask is not None else g
             return dx
@@ -139,6 +142,16 @@ class BatchNorm(ParameterizedLayer):
             return d * gamma * m
         M = x.numel() // self.num_features
         return gamma * m * (d - sdy.view(1, -1, 1, 1) / M - xhat * sdyx.view(1, -1, 1, 1) / M)
+
+    def bwd_bn_spec(self, mb_id=0):
+        ent = self._cache.get(mb_id)
+        if ent is None:
+            return None
+        x, yout, mean, istd, was_training = ent
+        if not (was_training and x.is_cuda and x.dtype == torch.bfloat16 and x.is_contiguous(memory_format=torch.channels_last)):
+            return None
+        from ...ops.hip import BnbRequest
+        return BnbRequest(self, yout, x, mean, istd)
 
     def pop_masked_grad(self, mb_id=0):
         return self._last_masked.pop(mb_id)

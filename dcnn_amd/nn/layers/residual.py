@@ -13,7 +13,7 @@ from typing import List, Optional
 import torch
 
 from ..activations import ActivationFactory
-from .base import LayerConfig, Layer
+from .base import LayerConfig, Layer, run_backward
 from .conv import Conv2D
 from .misc import Activation
 from .norm import BatchNorm
@@ -153,8 +153,10 @@ class ResidualBlock(Layer):
             d_s = d_pre
             for l in reversed(self.shortcut_path):
                 d_s = l.backward(d_s, mb_id)
-            for l in reversed(self.main_path[1:-1]):
-                g = l.backward(g, mb_id)
+            for k in range(len(self.main_path) - 2, 0, -1):
+                # the BN below (after its passthrough ReLU) gets its mask + statistics fused into
+                # this layer's dgrad epilogue
+                g = run_backward(self.main_path, k, g, mb_id)
             first = self.main_path[0]
             if not self.needs_input_grad:
                 first.backward(g, mb_id) if len(self.main_path) > 1 else None
@@ -162,7 +164,13 @@ class ResidualBlock(Layer):
             if len(self.main_path) == 1:
                 return g + d_s
             if isinstance(first, Conv2D):
-                return first.backward(g, mb_id, add_to=d_s)
+                # the block's input gradient dF + dS is consumed by the previous block's tail BN:
+                # forward the outer container's fusion request to the conv that produces it
+                first._bnb_request = self._bnb_request
+                try:
+                    return first.backward(g, mb_id, add_to=d_s)
+                finally:
+                    first._bnb_request = None
             return first.backward(g, mb_id) + d_s
         pre, out = ent
         g = self.act.gradient(pre, out, grad) if self.act is not None else grad
@@ -175,6 +183,12 @@ class ResidualBlock(Layer):
         if not self.needs_input_grad:
             return None
         return d_main + d_s
+
+    def bwd_bn_spec(self, mb_id=0):
+        ent = self._cache.get(mb_id)
+        if not self._fused or ent is None or ent[0] != "fused":
+            return None
+        return self.main_path[-1].bwd_bn_spec(mb_id)
 
     # shapes / cost -----------------------------------------------------------------------
     def compute_output_shape(self, s):

@@ -31,6 +31,7 @@ from ..device import Device, DeviceType, get_cpu, get_device
 from .layers import (Activation, AvgPool2D, BatchNorm, Conv2D, Dense, Dropout, Flatten, GroupNorm, Layer,
                      LayerBuilder, LayerConfig, LayerFactory, MaxPool2D, ParameterizedLayer, ResidualBlock,
                      create_layer, plan_fusion)
+from .layers.base import run_backward
 from .params import ParamArena
 
 
@@ -369,7 +370,7 @@ class Sequential:
             l = self.layers[i]
             t0 = self._prof_begin()
             try:
-                cur = l.backward(cur, mb_id)
+                cur = run_backward(self.layers, i, cur, mb_id)
             except Exception as e:
                 raise RuntimeError(f"Error in backward pass of layer {i} ({l.type()}): {e}") from e
             self._prof_end(l.name or l.type(), t0, self.backward_times_us)

@@ -19,6 +19,9 @@ CL = torch.channels_last
 F32 = torch.float32
 BF16 = torch.bfloat16
 
+# backward-BN epilogue fusion operands (api.h BnbArgs): (y, x, mean, istd) pointers, 0 = off
+_NOBNB = (0, 0, 0, 0)
+
 # gather modes of gemm_nt
 PLAIN, CONV_FWD, CONV_DGRAD = 0, 1, 2
 
@@ -114,7 +117,7 @@ def conv2d_fwd(x, w, bias, stride, pad, *, stats=False, residual=None, relu=Fals
             sums = torch.empty((2 * Co,), dtype=F32, device=x.device)  # zeroed in-kernel
         K.gemm_g2f(x.data_ptr(), w.data_ptr(), y.data_ptr(), _nbytes(x), _nbytes(w), M, Co, Ci, H, W, OH, OW, sh, sw,
                    _fwd_taps(Ci, W, KH, KW, ph, pw), KH * KW * Ci, Co, OH, OW, 1, 1, 0, 0, ptr(bias), ptr(residual),
-                   ptr(slab), int(relu), ptr(sums), 2 * Co if stats else 0, stream_ptr())
+                   ptr(slab), int(relu), ptr(sums), 2 * Co if stats else 0, _NOBNB, stream_ptr())
         return y, ((slab, rows, sums) if stats else None)
     taps = _fwd_taps(Ci, W, KH, KW, ph, pw)
     if not out_fp32 and _hconv_ok(N, OH, OW, H, W, sh, sw, Ci, Co, taps, w):
@@ -126,7 +129,7 @@ def conv2d_fwd(x, w, bias, stride, pad, *, stats=False, residual=None, relu=Fals
             sums = torch.empty((2 * Co,), dtype=F32, device=x.device)  # zeroed in-kernel
         K.hconv(x.data_ptr(), w.data_ptr(), y.data_ptr(), _nbytes(x), _nbytes(w), N, H, W, Ci, Co, KH * KW * Ci,
                 [(t[0], t[1], t[3]) for t in taps], ptr(bias), ptr(residual), ptr(slab), int(relu), ptr(sums),
-                2 * Co if stats else 0, stream_ptr())
+                2 * Co if stats else 0, _NOBNB, stream_ptr())
         return y, ((slab, rows, sums) if stats else None)
     if _g2_ok(Ci, Co) and not out_fp32:
         y = torch.empty((N, Co, OH, OW), dtype=BF16, device=x.device, memory_format=CL)
@@ -137,7 +140,7 @@ def conv2d_fwd(x, w, bias, stride, pad, *, stats=False, residual=None, relu=Fals
             sums = torch.empty((2 * Co,), dtype=F32, device=x.device)  # zeroed in-kernel
         K.gemm_g2(x.data_ptr(), w.data_ptr(), y.data_ptr(), _nbytes(x), _nbytes(w), M, Co, Ci, H, W, OH, OW, sh, sw,
                   _fwd_taps(Ci, W, KH, KW, ph, pw), KH * KW * Ci, Co, OH, OW, 1, 1, 0, 0, ptr(bias), ptr(residual),
-                  ptr(slab), int(relu), ptr(sums), 2 * Co if stats else 0, stream_ptr())
+                  ptr(slab), int(relu), ptr(sums), 2 * Co if stats else 0, _NOBNB, stream_ptr())
         return y, ((slab, rows, sums) if stats else None)
     # generic fallback (odd channel counts): v1 kernels
     y = torch.empty((N, Co, OH, OW), dtype=F32 if out_fp32 else BF16, device=x.device, memory_format=CL)
@@ -187,11 +190,33 @@ def conv_weight_t(w, out=None, dtype=BF16):
     return out
 
 
-def conv2d_dgrad(dy, wt, x_shape, stride, pad, *, residual=None):
+class BnbRequest:
+    """Backward-BatchNorm fusion request handed to a gradient producer (api.h ``BnbArgs``).
+
+    ``bn`` is the consuming BatchNorm layer; ``y`` its (ReLU) output used as the mask (None: no
+    ReLU was fused), ``x`` its input, ``mean``/``istd`` its saved batch statistics. A producer
+    that honours the request returns dy' = dy * (y > 0) with ``dy'._bnb = (bn, slab, rows, sums)``
+    attached: per-tile (sum dy', sum dy' * xhat) rows and the zeroed [2][C] sums to reduce into.
+    """
+    __slots__ = ("bn", "y", "x", "mean", "istd")
+
+    def __init__(self, bn, y, x, mean, istd):
+        self.bn, self.y, self.x, self.mean, self.istd = bn, y, x, mean, istd
+
+    def args(self):
+        return (ptr(self.y), self.x.data_ptr(), self.mean.data_ptr(), self.istd.data_ptr())
+
+
+_BNB = os.environ.get("DCNN_BNB_FUSE", "1") != "0"
+
+
+def conv2d_dgrad(dy, wt, x_shape, stride, pad, *, residual=None, bnb=None):
     """dx = conv_transpose(dy, w) [+ residual];  wt = conv_weight_t(w).
 
     Strided convs are phase-decomposed: input pixels are split into stride^2 parity classes,
     each a dense GEMM over only the kernel taps that reach it (no MFMA work on zero taps).
+    ``bnb`` (a :class:`BnbRequest`): fuse the consuming BatchNorm's ReLU mask and backward
+    statistics into the epilogue (honoured on the bf16 MFMA paths; see ``dx._bnb``).
     """
     _check_act(dy, "conv2d_dgrad.dy")
     K = kernels()
@@ -241,14 +266,36 @@ def conv2d_dgrad(dy, wt, x_shape, stride, pad, *, residual=None):
         dx = torch.empty((N, Ci, H, W), dtype=odt, device=dy.device, memory_format=CL)
     st = stream_ptr()
     g2 = K.gemm_g2f if f32 else K.gemm_g2
+    fuse = (bnb is not None and _BNB and not f32 and not empty_class and bnb.x.dtype == BF16
+            and tuple(bnb.x.shape) == (N, Ci, H, W))
     if not f32 and len(classes) == 1 and not empty_class and \
             _hconv_ok(N, H, W, OH, OW, sh, sw, Co, Ci, classes[0][4], wt):
+        slab = sums = None
+        rows = 0
+        if fuse:
+            rows = K.hconv_stat_rows(N, H, W, Ci)
+            slab = torch.empty((rows, 2, Ci), dtype=F32, device=dy.device)
+            sums = torch.empty((2 * Ci,), dtype=F32, device=dy.device)  # zeroed in-kernel
         K.hconv(dy.data_ptr(), wt.data_ptr(), dx.data_ptr(), _nbytes(dy), _nbytes(wt), N, OH, OW, Co, Ci, KH * KW * Co,
-                [(t[0], t[1], t[3]) for t in classes[0][4]], 0, ptr(residual), 0, 0, 0, 0, st)
+                [(t[0], t[1], t[3]) for t in classes[0][4]], 0, ptr(residual), ptr(slab), 0, ptr(sums),
+                2 * Ci if fuse else 0, bnb.args() if fuse else _NOBNB, st)
+        if fuse:
+            dx._bnb = (bnb.bn, slab, rows, sums)
         return dx
-    for ry, rx, GH, GW, taps in classes:
+    crow = [K.gemm_g2_stat_rows(N * GH * GW, Ci) if fuse else 0 for _, _, GH, GW, _ in classes]
+    rows = sum(crow)
+    slab = torch.empty((rows, 2, Ci), dtype=F32, device=dy.device) if fuse else None
+    sums = torch.empty((2 * Ci,), dtype=F32, device=dy.device) if fuse else None
+    r0 = 0
+    for k, (ry, rx, GH, GW, taps) in enumerate(classes):
+        sp = slab.data_ptr() + r0 * 2 * Ci * 4 if fuse else 0
+        zp = ptr(sums) if (fuse and k == 0) else 0
         g2(dy.data_ptr(), wt.data_ptr(), dx.data_ptr(), _nbytes(dy), _nbytes(wt), N * GH * GW, Ci, Co, OH, OW,
-           GH, GW, 1, 1, taps, KH * KW * Co, Ci, H, W, sh, sw, ry, rx, 0, ptr(residual), 0, 0, 0, 0, st)
+           GH, GW, 1, 1, taps, KH * KW * Co, Ci, H, W, sh, sw, ry, rx, 0, ptr(residual), sp, 0, zp,
+           2 * Ci if zp else 0, bnb.args() if fuse else _NOBNB, st)
+        r0 += crow[k]
+    if fuse:
+        dx._bnb = (bnb.bn, slab, rows, sums)
     return dx
 
 
@@ -330,13 +377,13 @@ def dense_fwd(x2d, w2d, bias):
     if x2d.dtype == F32:
         y = torch.empty((N, Out), dtype=F32, device=x2d.device)
         kernels().gemm_g2f(x2d.data_ptr(), w2d.data_ptr(), y.data_ptr(), _nbytes(x2d), _nbytes(w2d), N, Out, In, 1, 1,
-                           1, 1, 1, 1, [(0, 0, 0, 0)], In, Out, 1, 1, 1, 1, 0, 0, ptr(bias), 0, 0, 0, 0, 0,
+                           1, 1, 1, 1, [(0, 0, 0, 0)], In, Out, 1, 1, 1, 1, 0, 0, ptr(bias), 0, 0, 0, 0, 0, _NOBNB,
                            stream_ptr())
         return y
     y = torch.empty((N, Out), dtype=BF16, device=x2d.device)
     if _g2_ok(In, Out):
         kernels().gemm_g2(x2d.data_ptr(), w2d.data_ptr(), y.data_ptr(), _nbytes(x2d), _nbytes(w2d), N, Out, In, 1, 1,
-                          1, 1, 1, 1, [(0, 0, 0, 0)], In, Out, 1, 1, 1, 1, 0, 0, ptr(bias), 0, 0, 0, 0, 0,
+                          1, 1, 1, 1, [(0, 0, 0, 0)], In, Out, 1, 1, 1, 1, 0, 0, ptr(bias), 0, 0, 0, 0, 0, _NOBNB,
                           stream_ptr())
         return y
     kernels().gemm_nt(x2d.data_ptr(), w2d.data_ptr(), y.data_ptr(), N, Out, In, In, In, Out, PLAIN,
@@ -351,13 +398,13 @@ def dense_dgrad(dy2d, wt2d):
     if dy2d.dtype == F32:
         dx = torch.empty((N, In), dtype=F32, device=dy2d.device)
         kernels().gemm_g2f(dy2d.data_ptr(), wt2d.data_ptr(), dx.data_ptr(), _nbytes(dy2d), _nbytes(wt2d), N, In, Out,
-                           1, 1, 1, 1, 1, 1, [(0, 0, 0, 0)], Out, In, 1, 1, 1, 1, 0, 0, 0, 0, 0, 0, 0, 0,
+                           1, 1, 1, 1, 1, 1, [(0, 0, 0, 0)], Out, In, 1, 1, 1, 1, 0, 0, 0, 0, 0, 0, 0, 0, _NOBNB,
                            stream_ptr())
         return dx
     dx = torch.empty((N, In), dtype=BF16, device=dy2d.device)
     if _g2_ok(Out, In):
         kernels().gemm_g2(dy2d.data_ptr(), wt2d.data_ptr(), dx.data_ptr(), _nbytes(dy2d), _nbytes(wt2d), N, In, Out, 1,
-                          1, 1, 1, 1, 1, [(0, 0, 0, 0)], Out, In, 1, 1, 1, 1, 0, 0, 0, 0, 0, 0, 0, 0,
+                          1, 1, 1, 1, 1, [(0, 0, 0, 0)], Out, In, 1, 1, 1, 1, 0, 0, 0, 0, 0, 0, 0, 0, _NOBNB,
                           stream_ptr())
         return dx
     kernels().gemm_nt(dy2d.data_ptr(), wt2d.data_ptr(), dx.data_ptr(), N, In, Out, Out, Out, In, PLAIN,
@@ -425,12 +472,24 @@ def bn_apply(x, sums, count, gamma, beta, eps, *, residual=None, relu=False, sav
     return y
 
 
-def bn_backward(dy, x, yout, mean, istd, gamma, dgamma, dbeta, *, want_masked=False, eval_mode=False):
-    """Returns (dx, masked_dy|None). yout given => ReLU was fused: dy' = dy * (yout > 0)."""
+def bn_backward(dy, x, yout, mean, istd, gamma, dgamma, dbeta, *, want_masked=False, eval_mode=False, fused=None):
+    """Returns (dx, masked_dy|None). yout given => ReLU was fused: dy' = dy * (yout > 0).
+
+    ``fused`` = (slab, rows, sums) when the producer of ``dy`` already applied the ReLU mask and
+    wrote the backward statistics in its epilogue (:class:`BnbRequest`): only the slab reduce
+    and the apply pass remain.
+    """
     K = kernels()
     R, C = _rc(x)
     st = stream_ptr()
     dt = dt_code(x.dtype)
+    if fused is not None and not eval_mode:
+        slab, rows, sums = fused
+        K.bn_slab_reduce(slab.data_ptr(), rows, C, sums.data_ptr(), st)
+        dx = torch.empty_like(x, memory_format=CL)
+        K.bn_bwd_apply(dt, dy.data_ptr(), 0, x.data_ptr(), dx.data_ptr(), R, C, mean.data_ptr(), istd.data_ptr(),
+                       ptr(gamma), sums.data_ptr(), float(R), ptr(dgamma), ptr(dbeta), 0, st)
+        return dx, (dy if want_masked else None)
     dmask = torch.empty_like(dy, memory_format=CL) if (want_masked and yout is not None) else None
     sums = None
     if not eval_mode:

@@ -20,6 +20,7 @@ from typing import List, Optional, Tuple
 import torch
 import torch.distributed as dist
 
+from ..nn.layers.base import run_backward
 from ..nn.sequential import Sequential, _leaf_param_layers
 
 
@@ -122,7 +123,7 @@ class DataParallel:
         m.prepare_backward()
         for i in range(len(m.layers) - 1, -1, -1):
             t0 = m._prof_begin()
-            cur = m.layers[i].backward(cur, mb_id)
+            cur = run_backward(m.layers, i, cur, mb_id)
             m._prof_end(m.layers[i].name or m.layers[i].type(), t0, m.backward_times_us)
             if self.world > 1 and i in self.fire:
                 lo, hi = self.fire[i]

@@ -59,9 +59,10 @@ class TrainStep:
         return segs, fires
 
     def _run_bwd(self, cur, hi, lo):
+        from ..nn.layers.base import run_backward
         layers = self.model.layers
         for i in range(hi, lo - 1, -1):
-            cur = layers[i].backward(cur, 0)
+            cur = run_backward(layers, i, cur, 0)
         return cur
 
     def _capture(self, x, y):

@@ -184,6 +184,49 @@ def test_batchnorm_fused(hip, C, dtype):
     assert rel_err(dmask, dyg.float().cpu() * (y.float().cpu() > 0)) < 1e-6
 
 
+@pytest.mark.parametrize("case", [
+    # N, C (BN channels = dgrad output), H, W, Co (dgrad input channels), stride, relu, residual
+    (4, 64, 16, 16, 64, 1, True, False),     # hconv dgrad, ReLU mask
+    (4, 64, 16, 16, 64, 1, True, True),      # + fused branch sum (ResNet block input gradient)
+    (4, 64, 16, 16, 128, 2, True, True),     # strided: 4 phase-class g2 launches into one slab
+    (2, 128, 8, 8, 64, 1, False, False),     # BN without a ReLU
+    (8, 512, 4, 4, 512, 1, True, False),     # 4x4 layer-4 geometry
+])
+def test_dgrad_bwd_bn_fusion(hip, case):
+    """conv dgrad with the consuming BatchNorm's ReLU mask + backward statistics in the epilogue
+    (ops.hip.BnbRequest) == dgrad followed by the standalone BN backward."""
+    N, C, H, W, Co, s, relu, resid = case
+    torch.manual_seed(5)
+    OH, OW = (H + 2 - 3) // s + 1, (W + 2 - 3) // s + 1
+    xb = (torch.randn(N, C, H, W) * 1.5 + 0.3).cuda().bfloat16().contiguous(memory_format=CL)
+    g, bt = (torch.rand(C) + 0.5).cuda(), torch.randn(C).cuda()
+    sums = hip.bn_stats(xb)
+    mean, istd = torch.empty(C, device="cuda"), torch.empty(C, device="cuda")
+    y = hip.bn_apply(xb, sums, N * H * W, g, bt, 1e-5, relu=relu, save=(mean, istd))
+    yout = y if relu else None
+    w = (torch.randn(Co, C, 3, 3) / math.sqrt(9 * C)).cuda().bfloat16().contiguous(memory_format=CL)
+    wt = hip.conv_weight_t(w)
+    dy = torch.randn(N, Co, OH, OW).cuda().bfloat16().contiguous(memory_format=CL)
+    r = torch.randn(N, C, H, W).cuda().bfloat16().contiguous(memory_format=CL) if resid else None
+    # unfused reference path
+    d_ref = hip.conv2d_dgrad(dy, wt, (N, C, H, W), (s, s), (1, 1), residual=r)
+    dg0, db0 = torch.zeros(C, device="cuda"), torch.zeros(C, device="cuda")
+    dx0, m0 = hip.bn_backward(d_ref, xb, yout, mean, istd, g, dg0, db0, want_masked=True)
+    # fused
+    req = hip.BnbRequest("bn", yout, xb, mean, istd)
+    d = hip.conv2d_dgrad(dy, wt, (N, C, H, W), (s, s), (1, 1), residual=r, bnb=req)
+    assert getattr(d, "_bnb", None) is not None and d._bnb[0] == "bn"
+    masked = d_ref.float() * (y.float() > 0) if relu else d_ref.float()
+    assert rel_err(d, masked) < 1e-6
+    dg1, db1 = torch.zeros(C, device="cuda"), torch.zeros(C, device="cuda")
+    dx1, m1 = hip.bn_backward(d, xb, yout, mean, istd, g, dg1, db1, want_masked=True, fused=d._bnb[1:])
+    assert rel_err(dx1, dx0) < 1e-2, rel_err(dx1, dx0)
+    assert rel_err(dg1, dg0) < 1e-3, rel_err(dg1, dg0)
+    assert rel_err(db1, db0) < 1e-3, rel_err(db1, db0)
+    if relu:
+        assert rel_err(m1, m0) < 1e-6
+
+
 def test_pools_and_act(hip):
     torch.manual_seed(3)
     x = torch.randn(2, 32, 16, 16)
