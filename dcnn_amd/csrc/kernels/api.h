@@ -112,6 +112,11 @@ void gn_bwd(int dtype, const void* dy, const void* x, void* dx, int N, int HW, i
 
 void maxpool_fwd(int dt, const void* x, void* y, uint8_t* idx, PoolGeom g, hipStream_t s);
 void maxpool_bwd(int dt, const void* dy, const uint8_t* idx, void* dx, PoolGeom g, hipStream_t s);
+// max-pool backward fused with the producing BatchNorm+ReLU's backward statistics (stem)
+bool maxpool_bwd_bnb_supported(PoolGeom g);
+int maxpool_bwd_bnb_rows(PoolGeom g);
+void maxpool_bwd_bnb(const bf16* dy, const uint8_t* idx, const bf16* ypool, const bf16* x, const float* mean,
+                     const float* istd, bf16* dx, PoolGeom g, float* slab, float* zero_sums, hipStream_t s);
 void avgpool_fwd(int dt, const void* x, void* y, PoolGeom g, hipStream_t s);
 void avgpool_bwd(int dt, const void* dy, void* dx, PoolGeom g, hipStream_t s);
 void act_fwd(int dt, const void* x, void* y, long n, int type, float a, hipStream_t s);

@@ -223,6 +223,22 @@ PYBIND11_MODULE(_kernels, m) {
     maxpool_bwd(dt, P<const void*>(dy), P<const uint8_t*>(idx), P<void*>(dx),
                 geom(N, H, W, C, OH, OW, ph, pw, sh, sw, padh, padw), S(st));
   });
+  m.def("maxpool_bwd_bnb_supported", [geom](int N, int H, int W, int C, int OH, int OW, int ph, int pw, int sh, int sw,
+                                            int padh, int padw) {
+    return maxpool_bwd_bnb_supported(geom(N, H, W, C, OH, OW, ph, pw, sh, sw, padh, padw));
+  });
+  m.def("maxpool_bwd_bnb_rows", [geom](int N, int H, int W, int C, int OH, int OW, int ph, int pw, int sh, int sw,
+                                       int padh, int padw) {
+    return maxpool_bwd_bnb_rows(geom(N, H, W, C, OH, OW, ph, pw, sh, sw, padh, padw));
+  });
+  m.def("maxpool_bwd_bnb", [geom](uintptr_t dy, uintptr_t idx, uintptr_t ypool, uintptr_t x, uintptr_t mean,
+                                  uintptr_t istd, uintptr_t dx, int N, int H, int W, int C, int OH, int OW, int ph,
+                                  int pw, int sh, int sw, int padh, int padw, uintptr_t slab, uintptr_t zero_sums,
+                                  uintptr_t st) {
+    maxpool_bwd_bnb(P<const bf16*>(dy), P<const uint8_t*>(idx), P<const bf16*>(ypool), P<const bf16*>(x),
+                    P<const float*>(mean), P<const float*>(istd), P<bf16*>(dx),
+                    geom(N, H, W, C, OH, OW, ph, pw, sh, sw, padh, padw), P<float*>(slab), P<float*>(zero_sums), S(st));
+  });
   m.def("avgpool_fwd", [geom](int dt, uintptr_t x, uintptr_t y, int N, int H, int W, int C, int OH, int OW, int ph,
                               int pw, int sh, int sw, int padh, int padw, uintptr_t st) {
     avgpool_fwd(dt, P<const void*>(x), P<void*>(y), geom(N, H, W, C, OH, OW, ph, pw, sh, sw, padh, padw), S(st));

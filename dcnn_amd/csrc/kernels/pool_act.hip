@@ -133,6 +133,76 @@ __global__ void maxpool_bwd_nov8_kernel(const bf16* __restrict__ dy, const uint8
   }
 }
 
+// The same gather fused with the backward statistics of the BatchNorm(+ReLU) whose output the
+// pool consumed (the ResNet stem: conv -> BN -> ReLU -> maxpool). dy' = dy at the window's argmax
+// where the pooled value (= that ReLU output) is > 0, else 0; per block (sum dy', sum dy' * xhat)
+// rows go to slab[block][2][C] (xhat from the BN input x). Saves the full-resolution pass over dy
+// and the ReLU output that a separate bn_partial would make. Requires C / 8 to divide 256 and the
+// grid-stride to be a multiple of C / 8 (fixed channel group per thread).
+__global__ void __launch_bounds__(256) maxpool_bwd_bnb_kernel(const bf16* __restrict__ dy,
+                                                              const uint8_t* __restrict__ idx,
+                                                              const bf16* __restrict__ ypool,
+                                                              const bf16* __restrict__ x,
+                                                              const float* __restrict__ mean,
+                                                              const float* __restrict__ istd, bf16* __restrict__ dx,
+                                                              PoolGeom g, float* __restrict__ slab,
+                                                              float* __restrict__ zero_sums) {
+  __shared__ float red[256 * 16];
+  if (zero_sums && blockIdx.x == 0)  // the [2][C] sums bn_slab_reduce accumulates into
+    for (int j = threadIdx.x; j < 2 * g.C; j += blockDim.x) zero_sums[j] = 0.f;
+  const int CV = g.C / 8;
+  const long total = (long)g.N * g.H * g.W * CV;
+  const int cv = threadIdx.x % CV;  // fixed: blockDim and the grid stride are multiples of CV
+  float mu[8], is[8], s[8], q[8];
+#pragma unroll
+  for (int e = 0; e < 8; ++e) {
+    mu[e] = mean[cv * 8 + e];
+    is[e] = istd[cv * 8 + e];
+    s[e] = q[e] = 0.f;
+  }
+  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < total; i += (long)gridDim.x * blockDim.x) {
+    long t = i / CV;
+    const int ix = (int)(t % g.W);
+    t /= g.W;
+    const int iy = (int)(t % g.H);
+    const int n = (int)(t / g.H);
+    const int oy = iy / g.ph, ox = ix / g.pw;
+    float out[8];
+    if (oy < g.OH && ox < g.OW) {
+      const long o = (((long)n * g.OH + oy) * g.OW + ox) * g.C + cv * 8;
+      const int local = (iy - oy * g.ph) * g.pw + (ix - ox * g.pw);
+      float d[8], yp[8], xv[8];
+      unpack8(*reinterpret_cast<const uint4*>(dy + o), d);
+      unpack8(*reinterpret_cast<const uint4*>(ypool + o), yp);
+      unpack8(*reinterpret_cast<const uint4*>(x + i * 8), xv);
+      const uint2 ib = *reinterpret_cast<const uint2*>(idx + o);
+      const uint8_t* b = reinterpret_cast<const uint8_t*>(&ib);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        out[e] = (b[e] == local && yp[e] > 0.f) ? d[e] : 0.f;
+        s[e] += out[e];
+        q[e] += out[e] * (xv[e] - mu[e]) * is[e];
+      }
+    } else {
+#pragma unroll
+      for (int e = 0; e < 8; ++e) out[e] = 0.f;
+    }
+    *reinterpret_cast<uint4*>(dx + i * 8) = pack8(out);
+  }
+#pragma unroll
+  for (int e = 0; e < 8; ++e) {
+    red[threadIdx.x * 16 + e] = s[e];
+    red[threadIdx.x * 16 + 8 + e] = q[e];
+  }
+  __syncthreads();
+  for (int j = threadIdx.x; j < 2 * g.C; j += blockDim.x) {
+    const int which = j / g.C, c = j % g.C, grp = c / 8, e = c % 8;
+    float a = 0.f;
+    for (int tt = grp; tt < (int)blockDim.x; tt += CV) a += red[tt * 16 + which * 8 + e];
+    slab[((long)blockIdx.x * 2 + which) * g.C + c] = a;
+  }
+}
+
 template <typename T>
 __global__ void avgpool_fwd_kernel(const T* __restrict__ x, T* __restrict__ y, PoolGeom g) {
   const long total = (long)g.N * g.OH * g.OW * g.C;
@@ -470,6 +540,23 @@ static void avgpool_bwd_t(const void* dy, void* dx, PoolGeom g, hipStream_t s) {
                        g.N, g.H * g.W, g.C);
   else
     hipLaunchKernelGGL(avgpool_bwd_kernel<T>, dim3(grid_for(total, 256)), dim3(256), 0, s, (const T*)dy, (T*)dx, g);
+  DCNN_LAUNCH_CHECK();
+}
+
+static int bnb_pool_blocks(const PoolGeom& g) {
+  const long total = (long)g.N * g.H * g.W * g.C / 8;
+  return grid_for(total, 256, 1024);
+}
+
+bool maxpool_bwd_bnb_supported(PoolGeom g) { return pool_nov8(g) && 256 % (g.C / 8) == 0; }
+
+int maxpool_bwd_bnb_rows(PoolGeom g) { return bnb_pool_blocks(g); }
+
+void maxpool_bwd_bnb(const bf16* dy, const uint8_t* idx, const bf16* ypool, const bf16* x, const float* mean,
+                     const float* istd, bf16* dx, PoolGeom g, float* slab, float* zero_sums, hipStream_t s) {
+  if (!maxpool_bwd_bnb_supported(g)) throw std::runtime_error("maxpool_bwd_bnb: unsupported geometry");
+  hipLaunchKernelGGL(maxpool_bwd_bnb_kernel, dim3(bnb_pool_blocks(g)), dim3(256), 0, s, dy, idx, ypool, x, mean, istd,
+                     dx, g, slab, zero_sums);
   DCNN_LAUNCH_CHECK();
 }
 

@@ -69,7 +69,8 @@ class Conv2D(ParameterizedLayer):
             if self.in_channels < 8 and self.compute_dtype == torch.bfloat16:
                 # RGB stem: zero-pad channels to 8 so every 16-byte chunk is one tap (vector path)
                 xa = hip.to_act_padded(x, 8)
-                w = hip.pad_weight_channels(self.weight_operand(0), 8)
+                w = hip.pad_weight_channels(self.weight_operand(0), 8, out=getattr(self, "_wpad", None))
+                self._wpad = w  # padding channels stay zero: later steps copy only the real ones
             else:
                 xa = hip.to_act(x, self.compute_dtype)
                 w = self.weight_operand(0)

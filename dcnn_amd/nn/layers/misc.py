@@ -56,19 +56,21 @@ class MaxPool2D(_Pool):
             from ...ops import hip
             xa = hip.to_act(x, self.compute_dtype)
             y, idx = hip.maxpool_fwd(xa, *self._geom())
-            self._cache[mb_id] = (idx, tuple(xa.shape))
+            # the output is kept (it is the next layer's cached input anyway): its sign is the
+            # ReLU mask when the producing BatchNorm's backward statistics are fused in backward
+            self._cache[mb_id] = (idx, tuple(xa.shape), y)
             return y
         y, idx = F.max_pool2d(x, (self.pool_h, self.pool_w), (self.stride_h, self.stride_w),
                               (self.pad_h, self.pad_w), return_indices=True)
-        self._cache[mb_id] = (idx, tuple(x.shape))
+        self._cache[mb_id] = (idx, tuple(x.shape), None)
         return y
 
     def backward(self, grad, mb_id=0):
-        idx, shape = self._cache.pop(mb_id)
+        idx, shape, y = self._cache.pop(mb_id)
         if idx.is_cuda:
             from ...ops import hip
             g = hip.to_act(grad.to(idx.device), self.compute_dtype)
-            return hip.maxpool_bwd(g, idx, shape, *self._geom())
+            return hip.maxpool_bwd(g, idx, shape, *self._geom(), ypool=y, bnb=self._bnb_request)
         return torch.ops.aten.max_pool2d_with_indices_backward(
             grad, torch.empty(shape), [self.pool_h, self.pool_w], [self.stride_h, self.stride_w],
             [self.pad_h, self.pad_w], [1, 1], False, idx)

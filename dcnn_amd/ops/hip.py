@@ -165,10 +165,12 @@ def to_act_padded(x, cp):
     return y
 
 
-def pad_weight_channels(w, cp):
-    """(Co,Ci,KH,KW) -> bf16 [Co][KH][KW][cp] operand, zero-padded input channels."""
+def pad_weight_channels(w, cp, out=None):
+    """(Co,Ci,KH,KW) -> bf16 [Co][KH][KW][cp] operand, zero-padded input channels. ``out``: a
+    previous result to refresh in place (one copy of the real channels, padding already zero)."""
     Co, Ci, KH, KW = w.shape
-    out = torch.zeros((Co, KH, KW, cp), dtype=BF16, device=w.device)
+    if out is None or tuple(out.shape) != (Co, KH, KW, cp) or out.device != w.device:
+        out = torch.zeros((Co, KH, KW, cp), dtype=BF16, device=w.device)
     out[..., :Ci] = w.permute(0, 2, 3, 1).to(BF16)
     return out
 
@@ -555,12 +557,27 @@ def maxpool_fwd(x, ph, pw, sh, sw, pdh, pdw):
     return y, idx
 
 
-def maxpool_bwd(dy, idx, x_shape, ph, pw, sh, sw, pdh, pdw):
+def maxpool_bwd(dy, idx, x_shape, ph, pw, sh, sw, pdh, pdw, *, ypool=None, bnb=None):
+    """Gather-form max-pool backward. With ``bnb`` (the BatchNorm+ReLU that produced the pool's
+    input, see :class:`BnbRequest`) and the pool output ``ypool``, the ReLU mask (pooled value > 0)
+    and that BatchNorm's backward statistics are fused in (``dx._bnb`` attached)."""
     N, C, H, W = x_shape
     OH, OW = dy.shape[2], dy.shape[3]
+    K = kernels()
     dx = torch.empty((N, C, H, W), dtype=dy.dtype, device=dy.device, memory_format=CL)
-    kernels().maxpool_bwd(dt_code(dy.dtype), dy.data_ptr(), idx.data_ptr(), dx.data_ptr(), N, H, W, C, OH, OW, ph, pw,
-                          sh, sw, pdh, pdw, stream_ptr())
+    g = (N, H, W, C, OH, OW, ph, pw, sh, sw, pdh, pdw)
+    # the kernel masks with (pooled value > 0): only valid when a ReLU sits between BN and pool
+    if (bnb is not None and _BNB and bnb.y is not None and ypool is not None and dy.dtype == BF16 and bnb.x.dtype == BF16
+            and tuple(bnb.x.shape) == (N, C, H, W) and bnb.x.is_contiguous(memory_format=CL)
+            and K.maxpool_bwd_bnb_supported(*g)):
+        rows = K.maxpool_bwd_bnb_rows(*g)
+        slab = torch.empty((rows, 2, C), dtype=F32, device=dy.device)
+        sums = torch.empty((2 * C,), dtype=F32, device=dy.device)  # zeroed in-kernel
+        K.maxpool_bwd_bnb(dy.data_ptr(), idx.data_ptr(), ypool.data_ptr(), bnb.x.data_ptr(), bnb.mean.data_ptr(),
+                          bnb.istd.data_ptr(), dx.data_ptr(), *g, slab.data_ptr(), sums.data_ptr(), stream_ptr())
+        dx._bnb = (bnb.bn, slab, rows, sums)
+        return dx
+    K.maxpool_bwd(dt_code(dy.dtype), dy.data_ptr(), idx.data_ptr(), dx.data_ptr(), *g, stream_ptr())
     return dx
 
 

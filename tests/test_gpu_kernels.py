@@ -227,6 +227,32 @@ def test_dgrad_bwd_bn_fusion(hip, case):
         assert rel_err(m1, m0) < 1e-6
 
 
+@pytest.mark.parametrize("C", [32, 64, 8])
+def test_maxpool_bwd_bn_fusion(hip, C):
+    """Stem pattern conv -> BN -> ReLU -> maxpool 2x2: the pool backward fused with the BN's ReLU
+    mask (pooled value > 0) and backward statistics == pool backward + standalone BN backward."""
+    torch.manual_seed(6)
+    N, H, W = 4, 16, 16
+    xb = (torch.randn(N, C, H, W) * 1.3 + 0.2).cuda().bfloat16().contiguous(memory_format=CL)
+    g, bt = (torch.rand(C) + 0.5).cuda(), torch.randn(C).cuda()
+    sums = hip.bn_stats(xb)
+    mean, istd = torch.empty(C, device="cuda"), torch.empty(C, device="cuda")
+    y = hip.bn_apply(xb, sums, N * H * W, g, bt, 1e-3, relu=True, save=(mean, istd))
+    yp, idx = hip.maxpool_fwd(y, 2, 2, 2, 2, 0, 0)
+    dyp = torch.randn(N, C, H // 2, W // 2).cuda().bfloat16().contiguous(memory_format=CL)
+    d_ref = hip.maxpool_bwd(dyp, idx, (N, C, H, W), 2, 2, 2, 2, 0, 0)
+    dg0, db0 = torch.zeros(C, device="cuda"), torch.zeros(C, device="cuda")
+    dx0, _ = hip.bn_backward(d_ref, xb, y, mean, istd, g, dg0, db0)
+    req = hip.BnbRequest("bn", y, xb, mean, istd)
+    d = hip.maxpool_bwd(dyp, idx, (N, C, H, W), 2, 2, 2, 2, 0, 0, ypool=yp, bnb=req)
+    assert getattr(d, "_bnb", None) is not None
+    assert rel_err(d, d_ref.float() * (y.float() > 0)) < 1e-6
+    dg1, db1 = torch.zeros(C, device="cuda"), torch.zeros(C, device="cuda")
+    dx1, _ = hip.bn_backward(d, xb, y, mean, istd, g, dg1, db1, fused=d._bnb[1:])
+    assert rel_err(dx1, dx0) < 1e-2, rel_err(dx1, dx0)
+    assert rel_err(dg1, dg0) < 1e-3 and rel_err(db1, db0) < 1e-3
+
+
 def test_pools_and_act(hip):
     torch.manual_seed(3)
     x = torch.randn(2, 32, 16, 16)
