@@ -128,7 +128,7 @@ void nchw_to_nhwc(int dt, const float* x, void* y, int N, int C, int HW, hipStre
 void nchw_to_nhwc_pad(int dt, const float* x, void* y, int N, int C, int Cp, int HW, hipStream_t s);
 void conv_weight_transpose(int src_dt, const void* w, bf16* wt, int Co, int T_, int Ci, hipStream_t s);
 void cast_f32_bf16(const float* x, bf16* y, long n, hipStream_t s);
-void multi_weight_transpose(const int64_t* table, int n, long max_numel, hipStream_t s);
+void multi_weight_transpose(const int64_t* table, int n, long max_tiles, hipStream_t s);
 void im2col(const float* x, float* col, int N, int C, int H, int W, int KH, int KW, int SH, int SW, int PH, int PW,
             int OH, int OW, hipStream_t s);
 void col2im(const float* col, float* x, int N, int C, int H, int W, int KH, int KW, int SH, int SW, int PH, int PW,

@@ -271,8 +271,8 @@ PYBIND11_MODULE(_kernels, m) {
   m.def("conv_weight_transpose", [](int dt, uintptr_t w, uintptr_t wt, int Co, int T_, int Ci, uintptr_t st) {
     conv_weight_transpose(dt, P<const void*>(w), P<bf16*>(wt), Co, T_, Ci, S(st));
   });
-  m.def("multi_weight_transpose", [](uintptr_t table, int n, long max_numel, uintptr_t st) {
-    multi_weight_transpose(P<const int64_t*>(table), n, max_numel, S(st));
+  m.def("multi_weight_transpose", [](uintptr_t table, int n, long max_tiles, uintptr_t st) {
+    multi_weight_transpose(P<const int64_t*>(table), n, max_tiles, S(st));
   });
   m.def("cast_f32_bf16",[](uintptr_t x, uintptr_t y, long n, uintptr_t st) {
     cast_f32_bf16(P<const float*>(x), P<bf16*>(y), n, S(st));

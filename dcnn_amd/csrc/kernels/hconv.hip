@@ -11,7 +11,12 @@
 // resident) weight slice is streamed per tap.
 //
 //   K loop: for each 64-channel chunk c: halo(c) [prefetched one chunk ahead]
-//             for each tap t: B(c, t) [prefetched one step ahead], MFMA over 64 channels
+//             for each tap t: B(c, t) [ring of NBS LDS stages, NBS - 1 steps ahead, counted
+//                                      vmcnt waits], MFMA over 64 channels
+//
+// A step is only TM x TN x 2 MFMAs per wave (8 for the 64x64 tiles of the 4x4 layers), far
+// shorter than an L2 round trip, so a one-step-ahead weight prefetch leaves the loop latency
+// bound; the deeper ring keeps two steps in flight.
 //
 // The epilogue is the gemm2 one (bias, residual, ReLU, BatchNorm partial statistics, 16-byte
 // stores through an LDS-staged bf16 tile), with the spatial-tile -> NHWC row mapping.
@@ -20,14 +25,25 @@
 
 namespace dcnn {
 
-typedef __attribute__((address_space(3))) void lds_void_h;
-
 namespace {
 constexpr unsigned kOOBh = 0x80000000u;
 
-__device__ __forceinline__ void glds16h(__amdgpu_buffer_rsrc_t rsrc, char* lds, unsigned voff) {
-  __builtin_amdgcn_raw_ptr_buffer_load_lds(rsrc, (lds_void_h*)lds, 16, voff, 0, 0, 0);
+// opaque to the compiler's wait-count pass: the manual vmcnt waits of the B ring below are the
+// only synchronisation of these LDS writes (a visible LDS DMA would be drained before every
+// ds_read, defeating the ring)
+__device__ __forceinline__ void glds16h(i32x4 rsrc, char* lds, unsigned voff) { glds16_opaque(rsrc, lds, voff); }
+
+// wait until at most m * U of this lane's direct-to-LDS loads are outstanding (m in 0..2)
+template <int U>
+__device__ __forceinline__ void vm_wait_groups(int m) {
+  if (m <= 0)
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  else if (m == 1)
+    asm volatile("s_waitcnt vmcnt(%0)" ::"n"(U) : "memory");
+  else
+    asm volatile("s_waitcnt vmcnt(%0)" ::"n"(2 * U) : "memory");
 }
+__device__ __forceinline__ void lds_barrier() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
 
 __device__ __forceinline__ int xcd_remap_h(int bid, int nwg) {
   const int xcd = bid & 7, q = nwg >> 3, r = nwg & 7;
@@ -40,24 +56,25 @@ __device__ __forceinline__ int hoff(int row, int ch) { return row * 128 + ((ch ^
 }  // namespace
 
 // TPS taps per K step (one barrier per step), NHB halo buffers (1 when there is a single
-// 64-channel chunk: nothing to prefetch)
-template <int BM, int BN, int TPS, int NHB>
+// 64-channel chunk: nothing to prefetch), NBS weight stages (NBS - 1 steps in flight)
+template <int BM, int BN, int TPS, int NHB, int NBS>
 struct HC {
   static constexpr int TM = BM / 32, TN = BN / 32;      // 16x16 subtiles per wave (2x2 waves)
   static constexpr int BTAP = BN * 128;                  // bytes of one tap's weight slice
   static constexpr int BST = TPS * BTAP;                 // bytes per weight stage
   static constexpr int B_INS = BN / 32;                  // glds per wave per tap slice
   static constexpr int EPI_PITCH = BN * 2 + 16;
-  // dynamic LDS: NHB halo buffers of HALO = 128 * (halo rows padded to 32) bytes, then 2 weight stages
+  // dynamic LDS: NHB halo buffers of HALO = 128 * (halo rows padded to 32) bytes, then NBS weight stages
   static int lds_bytes(int halo) {
-    const int main = NHB * halo + 2 * BST, epi = BM * EPI_PITCH;
+    const int main = NHB * halo + NBS * BST, epi = BM * EPI_PITCH;
     return main > epi ? main : epi;
   }
 };
 
-template <int BM, int BN, int TPS, int NHB>
+template <int BM, int BN, int TPS, int NHB, int NBS>
 __global__ void __launch_bounds__(256, 1) hconv_kernel(HConvArgs p) {
-  using T = HC<BM, BN, TPS, NHB>;
+  using T = HC<BM, BN, TPS, NHB, NBS>;
+  static_assert(NBS >= 2 && NBS <= 4 && (NBS == 2 || TPS == 1), "deep weight ring needs 1 tap per step");
   extern __shared__ __attribute__((aligned(16))) char smem[];
   struct { int HALO; } T_rt{p.HPR * 128};
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
@@ -77,8 +94,8 @@ __global__ void __launch_bounds__(256, 1) hconv_kernel(HConvArgs p) {
   if (p.zero_ptr && blockIdx.x == 0)
     for (int i = tid; i < p.zero_n; i += 256) p.zero_ptr[i] = 0.f;
 
-  const __amdgpu_buffer_rsrc_t rsA = __builtin_amdgcn_make_buffer_rsrc((void*)p.A, (short)0, p.a_bytes, 0x00020000);
-  const __amdgpu_buffer_rsrc_t rsB = __builtin_amdgcn_make_buffer_rsrc((void*)p.B, (short)0, p.b_bytes, 0x00020000);
+  const i32x4 rsA = raw_rsrc(p.A, p.a_bytes);
+  const i32x4 rsB = raw_rsrc(p.B, p.b_bytes);
 
   // ---- halo loader: per-lane pixel base offsets for its rows (fixed across chunks) ----
   const int hch = lane & 7;                               // physical chunk slot
@@ -152,18 +169,33 @@ __global__ void __launch_bounds__(256, 1) hconv_kernel(HConvArgs p) {
   const int nchunk = p.Cs / 64;
   const int spc = (p.ntaps + TPS - 1) / TPS;  // K steps per channel chunk
   const int nsteps = nchunk * spc;
+  // step j's weights live in stage j % NBS; step k + NBS - 1 is issued at the top of step k into
+  // the stage step k - 1 consumed. The halo of chunk c + 1 is issued at the first step of chunk
+  // c, >= NBS steps before it is read (host: spc >= NBS), so it is always older than the weight
+  // stage being waited for and the per-step wait counts only weight loads (a halo issued later
+  // in the window only makes the wait conservative).
+  constexpr int BU = TPS * T::B_INS;  // weight loads per lane per step
+  auto step_ct = [&](int j, int* cj, int* tj) { *cj = j / spc; *tj = (j - *cj * spc) * TPS; };
   load_halo(0, 0);
-  load_b(0, 0, 0);
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __syncthreads();
+#pragma unroll
+  for (int j = 0; j < NBS - 1; ++j) {
+    if (j < nsteps) {
+      int cj, tj;
+      step_ct(j, &cj, &tj);
+      load_b(j, cj * 64, tj);
+    }
+  }
+  vm_wait_groups<BU>(min(NBS - 2, nsteps - 1));
+  lds_barrier();
   int bcur = 0;
   for (int k = 0; k < nsteps; ++k) {
     const int c = k / spc, t0 = (k - c * spc) * TPS;
-    if (k + 1 < nsteps) {
-      const int c1 = (k + 1) / spc, t1 = (k + 1 - c1 * spc) * TPS;
-      load_b(bcur ^ 1, c1 * 64, t1);
-      if (NHB == 2 && t0 == 0 && c + 1 < nchunk) load_halo((c + 1) & 1, (c + 1) * 64);
+    if (k + NBS - 1 < nsteps) {
+      int cj, tj;
+      step_ct(k + NBS - 1, &cj, &tj);
+      load_b(bcur == 0 ? NBS - 1 : bcur - 1, cj * 64, tj);
     }
+    if (NHB == 2 && t0 == 0 && c + 1 < nchunk) load_halo((c + 1) & 1, (c + 1) * 64);
     const char* Hs = smem + (NHB == 2 ? (c & 1) : 0) * T_rt.HALO;
 #pragma unroll
     for (int u = 0; u < TPS; ++u) {
@@ -189,9 +221,10 @@ __global__ void __launch_bounds__(256, 1) hconv_kernel(HConvArgs p) {
         __builtin_amdgcn_s_setprio(0);
       }
     }
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
-    bcur ^= 1;
+    // step k + 1's weights (and halo) landed for this lane, then for the whole workgroup
+    vm_wait_groups<BU>(min(NBS - 2, nsteps - 2 - k));
+    lds_barrier();
+    bcur = bcur == NBS - 1 ? 0 : bcur + 1;
   }
 
   // ---- epilogue 1: acc (+bias) -> bf16 LDS tile [BM][BN] ----
@@ -334,17 +367,35 @@ static void launch_hconv(HConvArgs a, hipStream_t s) {
     const char* e = getenv("DCNN_HCONV_TPS");
     return (e && atoi(e) == 3) ? 3 : 1;  // 3 taps/step: fewer barriers but 1 workgroup/CU (slower)
   }();
-#define DCNN_HC(TPS, NHB)                                                                              \
+  static const int bstages = [] {
+    const char* e = getenv("DCNN_HCONV_BSTAGES");
+    const int v = e ? atoi(e) : 3;
+    return v < 2 ? 2 : (v > 4 ? 4 : v);
+  }();
+  // deep weight ring: one tap per step, every halo prefetch >= NBS steps ahead of its use, and
+  // only where the extra stage keeps the workgroups per CU (LDS-bound occupancy: losing one
+  // costs more than the deeper prefetch gains, measured 63.4k vs 65.0k img/s on ResNet-18)
+  auto wg_per_cu = [&](int nb) {
+    const int main = (multi ? 2 : 1) * a.HPR * 128 + nb * BN * 128, epi = BM * (BN * 2 + 16);
+    return 163840 / (main > epi ? main : epi);
+  };
+  int nbs = (tps == 1 && a.ntaps >= bstages) ? bstages : 2;
+  while (nbs > 2 && wg_per_cu(nbs) < wg_per_cu(2)) --nbs;
+#define DCNN_HC(TPS, NHB, NBS)                                                                         \
   {                                                                                                    \
-    auto k = hconv_kernel<BM, BN, TPS, NHB>;                                                           \
-    const int lds = HC<BM, BN, TPS, NHB>::lds_bytes(a.HPR * 128);                                      \
+    auto k = hconv_kernel<BM, BN, TPS, NHB, NBS>;                                                      \
+    const int lds = HC<BM, BN, TPS, NHB, NBS>::lds_bytes(a.HPR * 128);                                 \
     DCNN_HIP_CHECK(hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, lds)); \
     hipLaunchKernelGGL(k, dim3(grid), dim3(256), lds, s, a);                                           \
   }
   if (tps == 3) {
-    if (multi) DCNN_HC(3, 2) else DCNN_HC(3, 1)
+    if (multi) DCNN_HC(3, 2, 2) else DCNN_HC(3, 1, 2)
+  } else if (nbs == 4) {
+    if (multi) DCNN_HC(1, 2, 4) else DCNN_HC(1, 1, 4)
+  } else if (nbs == 3) {
+    if (multi) DCNN_HC(1, 2, 3) else DCNN_HC(1, 1, 3)
   } else {
-    if (multi) DCNN_HC(1, 2) else DCNN_HC(1, 1)
+    if (multi) DCNN_HC(1, 2, 2) else DCNN_HC(1, 1, 2)
   }
 #undef DCNN_HC
   DCNN_LAUNCH_CHECK();

@@ -7,7 +7,8 @@
 // block, i.e. the input is re-read 9x through L2 (~64 flop/byte). Here a workgroup owns a
 // 64(co) x 9(taps) x 64(ci) block of dW and a run of spatial pixel tiles (IMG x TH x TW = 128
 // pixels). Per tile it stages the dY tile [128 px][64 co] and the X halo
-// [(TH+2)(TW+2) px][64 ci] into LDS once (16-byte direct-to-LDS loads, zero-filled padding),
+// [(TH+2)(TW+2) px][64 ci] into LDS once (16-byte direct-to-LDS loads, zero-filled padding,
+// a 3-stage ring so two tiles are in flight while one is consumed),
 // then all 9 taps read their B fragments from the same halo at a per-tap row offset; the dY
 // (A) fragments are read once per 32-pixel k-step and reused by the 9 taps (~240 flop/byte).
 // Fragments are pixel-major in LDS and read with ds_read_b64_tr_b16 (transposing LDS reads).
@@ -58,10 +59,14 @@ struct HWGeo {
   static_assert(TPX * IMG == PT, "tile must hold 128 pixels");
 };
 
-template <int TW, int TH, int IMG>
+// NS = LDS stages of the (dY, halo) tile ring: NS - 1 tiles are in flight while one is consumed
+// (3 stages: 120-156 KB of LDS, still one workgroup per CU as with 2)
+template <int TW, int TH, int IMG, int NS>
 __global__ void __launch_bounds__(256, 1) hwgrad_kernel(HWArgs p) {
   using G = HWGeo<TW, TH, IMG>;
   constexpr int HNI = G::HNI, HW2 = G::HW2, HPI = G::HPI, HP = G::HP, TPX = G::TPX, STAGE = G::STAGE;
+  constexpr int INS = 4 + HNI;  // direct-to-LDS loads per lane per tile (the vmcnt unit)
+  static_assert(NS == 2 || NS == 3, "2 or 3 stages");
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const int co_tiles = p.Co / 64, ci_chunks = p.Cs / 64;
@@ -142,12 +147,18 @@ __global__ void __launch_bounds__(256, 1) hwgrad_kernel(HWArgs p) {
   const bool do_bias = p.bias_slab != nullptr && c0 == 0;
   float bias_acc = 0.f;
   const int nt = (p.dbg & 16) ? 0 : tend - tbeg;
+  // tile it lives in stage it % NS; tile it + NS - 1 is issued at the top of iteration it into
+  // the stage iteration it - 1 consumed (the barrier closing it - 1 retired every read of it)
   if (nt > 0) load_tile(0, tbeg);
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  if (NS == 3 && nt > 1) load_tile(1, tbeg + 1);
+  if (NS == 3 && nt > 1)
+    asm volatile("s_waitcnt vmcnt(%0)" ::"n"(INS) : "memory");  // tile 0 landed, tile 1 may fly
+  else
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
   int cur = 0;
   for (int it = 0; it < nt; ++it) {
-    if (it + 1 < nt) load_tile(cur ^ 1, tbeg + it + 1);
+    if (it + NS - 1 < nt) load_tile(cur == 0 ? NS - 1 : cur - 1, tbeg + it + NS - 1);
     const char* Ys = smem + cur * STAGE;
     const char* Hs = Ys + PT * 128;
     // software pipeline over the 4 k-steps: the fragments of step kk+1 are read while the 36
@@ -194,9 +205,13 @@ __global__ void __launch_bounds__(256, 1) hwgrad_kernel(HWArgs p) {
       for (int r = tid >> 6; r < PT; r += 4)
         bias_acc += (float)*reinterpret_cast<const bf16*>(Ys + r * 128 + ((chn ^ wswz(r)) << 4) + w);
     }
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
-    cur ^= 1;
+    // tile it + 1 must have landed (this lane's loads, then the barrier for everyone's); with 3
+    // stages the loads of tile it + 2, issued after it, may stay in flight
+    if (NS == 3 && it + 2 < nt)
+      asm volatile("s_waitcnt vmcnt(%0)\n\ts_waitcnt lgkmcnt(0)\n\ts_barrier" ::"n"(INS) : "memory");
+    else
+      asm volatile("s_waitcnt vmcnt(0)\n\ts_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+    cur = cur == NS - 1 ? 0 : cur + 1;
   }
 
   // ---- slab[split][co][t*Cs + ci]: taps staged through LDS (pitch 68 floats) so every lane
@@ -288,18 +303,25 @@ void hwgrad(HWArgs a, int splits, hipStream_t s) {
   static const int dbg = [] { const char* e = getenv("DCNN_HWGRAD_DBG"); return e ? atoi(e) : 0; }();
   a.dbg = dbg;  // timing experiments only (results are wrong when set)
   const int grid = splits * (a.Co / 64) * (a.Cs / 64);
-#define DCNN_HW(TW_, TH_, IMG_)                                                                         \
-  if (a.TW == TW_ && a.TH == TH_ && a.IMG == IMG_) {                                                    \
-    auto k = hwgrad_kernel<TW_, TH_, IMG_>;                                                             \
-    const int lds = 2 * HWGeo<TW_, TH_, IMG_>::STAGE;                                                   \
+  static const int stages = [] {
+    const char* e = getenv("DCNN_HWGRAD_STAGES");
+    return (e && atoi(e) == 2) ? 2 : 3;
+  }();
+#define DCNN_HW(TW_, TH_, IMG_, NS_)                                                                    \
+  if (a.TW == TW_ && a.TH == TH_ && a.IMG == IMG_ && stages == NS_) {                                   \
+    auto k = hwgrad_kernel<TW_, TH_, IMG_, NS_>;                                                        \
+    const int lds = NS_ * HWGeo<TW_, TH_, IMG_>::STAGE;                                                 \
     DCNN_HIP_CHECK(hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, lds)); \
     hipLaunchKernelGGL(k, dim3(grid), dim3(256), lds, s, a);                                            \
     DCNN_LAUNCH_CHECK();                                                                                \
     return;                                                                                             \
   }
-  DCNN_HW(16, 8, 1)
-  DCNN_HW(8, 8, 2)
-  DCNN_HW(4, 4, 8)
+  DCNN_HW(16, 8, 1, 3)
+  DCNN_HW(8, 8, 2, 3)
+  DCNN_HW(4, 4, 8, 3)
+  DCNN_HW(16, 8, 1, 2)
+  DCNN_HW(8, 8, 2, 2)
+  DCNN_HW(4, 4, 8, 2)
 #undef DCNN_HW
   throw std::runtime_error("hwgrad: no kernel for this geometry");
 }

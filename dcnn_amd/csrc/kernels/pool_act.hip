@@ -414,25 +414,45 @@ __global__ void conv_weight_transpose_kernel(const S* __restrict__ w, bf16* __re
 
 // All dgrad weight operands of a model in ONE launch: table rows are
 // {src ptr, dst ptr, Co, taps, Ci}; blockIdx.y selects the tensor.
-__global__ void multi_weight_transpose_kernel(const int64_t* __restrict__ table) {
+// [Co][T][Ci] -> [Ci][T][Co] for every conv of a model in one launch (blockIdx.y = conv). Each
+// workgroup moves one 64(co) x 64(ci) tile of one tap through LDS: 16-byte coalesced loads along
+// ci, 16-byte coalesced stores along co (Ci, Co multiples of 8, 256-byte aligned arena views).
+__global__ void __launch_bounds__(256) multi_weight_transpose_kernel(const int64_t* __restrict__ table) {
   const int64_t* e = table + blockIdx.y * 5;
   const bf16* w = reinterpret_cast<const bf16*>(e[0]);
   bf16* wt = reinterpret_cast<bf16*>(e[1]);
   const int Co = (int)e[2], T_ = (int)e[3], Ci = (int)e[4];
-  const long total = (long)Co * T_ * Ci;
-  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < total; i += (long)gridDim.x * blockDim.x) {
-    const int co = (int)(i % Co);
-    const long r = i / Co;
-    const int t = (int)(r % T_);
-    const int ci = (int)(r / T_);
-    wt[i] = w[((long)co * T_ + t) * Ci + ci];
+  const int tco = (Co + 63) / 64, tci = (Ci + 63) / 64;
+  int b = blockIdx.x;
+  if (b >= T_ * tco * tci) return;  // this conv has fewer tiles than the largest one
+  const int t = b % T_;
+  b /= T_;
+  const int ic = b % tci, oc = b / tci;
+  __shared__ bf16 tile[64][72];  // row pitch 144 B keeps the 16-byte row chunks aligned
+  for (int k = threadIdx.x; k < 64 * 8; k += 256) {
+    const int r = k >> 3, c8 = (k & 7) * 8;
+    const int co = oc * 64 + r, ci = ic * 64 + c8;
+    uint4 v = make_uint4(0, 0, 0, 0);
+    if (co < Co && ci < Ci) v = *reinterpret_cast<const uint4*>(w + ((long)co * T_ + t) * Ci + ci);
+    *reinterpret_cast<uint4*>(&tile[r][c8]) = v;
+  }
+  __syncthreads();
+  for (int k = threadIdx.x; k < 64 * 8; k += 256) {
+    const int r = k >> 3, c8 = (k & 7) * 8;  // r: ci within the tile, c8: first of 8 co
+    const int ci = ic * 64 + r, co = oc * 64 + c8;
+    if (ci < Ci && co < Co) {
+      uint4 v;
+      bf16* o = reinterpret_cast<bf16*>(&v);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) o[j] = tile[c8 + j][r];
+      *reinterpret_cast<uint4*>(wt + ((long)ci * T_ + t) * Co + co) = v;
+    }
   }
 }
 
-void multi_weight_transpose(const int64_t* table, int n, long max_numel, hipStream_t s) {
+void multi_weight_transpose(const int64_t* table, int n, long max_tiles, hipStream_t s) {
   if (n <= 0) return;
-  const int gx = grid_for(max_numel, 256, 1024);
-  hipLaunchKernelGGL(multi_weight_transpose_kernel, dim3(gx, n), dim3(256), 0, s, table);
+  hipLaunchKernelGGL(multi_weight_transpose_kernel, dim3((unsigned)max_tiles, n), dim3(256), 0, s, table);
   DCNN_LAUNCH_CHECK();
 }
 

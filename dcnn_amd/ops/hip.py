@@ -210,6 +210,7 @@ class BnbRequest:
 
 
 _BNB = os.environ.get("DCNN_BNB_FUSE", "1") != "0"
+_BNB_POOL = os.environ.get("DCNN_BNB_POOL", "1") != "0"  # the stem max-pool part of the fusion
 
 
 def conv2d_dgrad(dy, wt, x_shape, stride, pad, *, residual=None, bnb=None):
@@ -567,7 +568,7 @@ def maxpool_bwd(dy, idx, x_shape, ph, pw, sh, sw, pdh, pdw, *, ypool=None, bnb=N
     dx = torch.empty((N, C, H, W), dtype=dy.dtype, device=dy.device, memory_format=CL)
     g = (N, H, W, C, OH, OW, ph, pw, sh, sw, pdh, pdw)
     # the kernel masks with (pooled value > 0): only valid when a ReLU sits between BN and pool
-    if (bnb is not None and _BNB and bnb.y is not None and ypool is not None and dy.dtype == BF16 and bnb.x.dtype == BF16
+    if (bnb is not None and _BNB and _BNB_POOL and bnb.y is not None and ypool is not None and dy.dtype == BF16 and bnb.x.dtype == BF16
             and tuple(bnb.x.shape) == (N, C, H, W) and bnb.x.is_contiguous(memory_format=CL)
             and K.maxpool_bwd_bnb_supported(*g)):
         rows = K.maxpool_bwd_bnb_rows(*g)
@@ -688,19 +689,19 @@ class WeightTransposer:
     def __init__(self, convs):
         self.convs = [c for c in convs if c.in_channels % 8 == 0 and c.out_channels % 8 == 0]
         rows = []
-        self.max_numel = 0
+        self.max_tiles = 0  # 64x64 (co, ci) tiles per tap: the launch's x extent
         for c in self.convs:
             w = c.weight_operand(0)
             Co, Ci, KH, KW = w.shape
             c._wt_buf = torch.empty((Ci, KH, KW, Co), dtype=BF16, device=w.device)
             rows.append([w.data_ptr(), c._wt_buf.data_ptr(), Co, KH * KW, Ci])
-            self.max_numel = max(self.max_numel, w.numel())
+            self.max_tiles = max(self.max_tiles, KH * KW * ((Co + 63) // 64) * ((Ci + 63) // 64))
         self.table = torch.tensor(rows, dtype=torch.int64).to(self.convs[0]._wt_buf.device) if rows else None
 
     def run(self):
         if self.table is None:
             return
-        kernels().multi_weight_transpose(self.table.data_ptr(), len(self.convs), self.max_numel, stream_ptr())
+        kernels().multi_weight_transpose(self.table.data_ptr(), len(self.convs), self.max_tiles, stream_ptr())
         for c in self.convs:
             c._wt_valid = True
 

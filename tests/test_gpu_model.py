@@ -157,8 +157,8 @@ def test_bwd_bn_fusion_matches_unfused(name, monkeypatch):
 
     monkeypatch.setattr(hip, "kernels", lambda: Spy())
     res = {}
-    for fuse in (False, "again", True):
-        monkeypatch.setattr(hip, "_BNB", fuse is True)
+    for fuse in (False, "again", True, "fused again"):
+        monkeypatch.setattr(hip, "_BNB", fuse is True or fuse == "fused again")
         m = create_model(name)
         m.set_seed(11)
         m.set_device("GPU:0")
@@ -169,15 +169,17 @@ def test_bwd_bn_fusion_matches_unfused(name, monkeypatch):
         m.backward(g)
         torch.cuda.synchronize()
         res[fuse] = ([t.float().cpu().clone() for t in m.gradients()], calls["n"])
-    (g0, n0), (g1, n1), (g2, _) = res[False], res[True], res["again"]
+    (g0, n0), (g1, n1), (g2, _), (g3, _) = res[False], res[True], res["again"], res["fused again"]
     assert n1 < n0, (n0, n1)
-    # float-atomic summation order makes two UNFUSED runs differ already (BN statistics, amplified
-    # through ~20 BatchNorms at batch 16): the fused run must stay within that noise floor. The
+    # float-atomic summation order makes two runs of the SAME path differ already (BN statistics,
+    # amplified through ~20 BatchNorms at batch 16; typically ~20%, occasionally two runs happen
+    # to agree): the fused run must stay within the larger of the two same-path noise floors. The
     # exact per-kernel equivalence is test_gpu_kernels.py::test_dgrad_bwd_bn_fusion.
     scale = max(a.norm().item() for a in g0)
-    for j, (a, b, c) in enumerate(zip(g0, g1, g2)):
+    for j, (a, b, c, d) in enumerate(zip(g0, g1, g2, g3)):
         den = max(a.norm().item(), 0.05 * scale)
-        e, noise = (a - b).norm().item() / den, (a - c).norm().item() / den
+        e = (a - b).norm().item() / den
+        noise = max((a - c).norm().item(), (b - d).norm().item()) / den
         assert e < 2.5 * noise + 0.02, (j, e, noise)
 
 

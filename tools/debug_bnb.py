@@ -22,8 +22,8 @@ def main():
     lf = LossFactory.create("softmax_crossentropy")
     res = {}
     names = []
-    for fuse in ("off", "off2", "on"):
-        hip._BNB = fuse == "on"
+    for fuse in ("off", "off2", "on", "on2"):
+        hip._BNB = fuse.startswith("on")
         m = create_model(name)
         m.set_seed(11)
         m.set_device("GPU:0")
@@ -38,11 +38,11 @@ def main():
                 for s in l.param_specs():
                     names.append(f"{l.name}.{s.name}")
     for j in range(len(res["off"]) - 1, -1, -1):
-        a, b, c = res["off"][j], res["on"][j], res["off2"][j]
-        e = (a - b).norm().item() / max(a.norm().item(), 1e-12)
-        e0 = (a - c).norm().item() / max(a.norm().item(), 1e-12)
+        a, b, c, d = res["off"][j], res["on"][j], res["off2"][j], res["on2"][j]
+        n = max(a.norm().item(), 1e-12)
+        e, e0, e1 = (a - b).norm().item() / n, (a - c).norm().item() / n, (b - d).norm().item() / n
         print(f"{j:3d} {names[j] if j < len(names) else '?':40s} |g|={a.norm().item():10.4e} "
-              f"fused-vs-unfused={e:.3e} unfused-vs-unfused={e0:.3e}")
+              f"fused-vs-unfused={e:.3e} unfused-vs-unfused={e0:.3e} fused-vs-fused={e1:.3e}")
 
 
 if __name__ == "__main__":
