@@ -132,20 +132,26 @@ __global__ void __launch_bounds__(256) bn_partial_kernel(const T* __restrict__ x
   }
 }
 
-// sums[2][C] += sum over slab rows (atomic; sums zeroed by the caller)
+// sums[2][C] += sum over slab rows (atomic; sums zeroed by the caller). Lane = channel, wave w
+// of the block sums rows [rb + w*RW, rb + (w+1)*RW) with all 2*RW loads issued before the first
+// add: the slab is tiny (L2/MALL resident) and the kernel is pure load latency otherwise
+template <int RW>
 __global__ void __launch_bounds__(256) bn_slab_reduce_kernel(const float* __restrict__ slab, int rows, int C,
-                                                             int rows_per_block, float* __restrict__ sums) {
+                                                             float* __restrict__ sums) {
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   const int c = blockIdx.x * 64 + lane;
-  const int rb = blockIdx.y * rows_per_block, re = min(rows, rb + rows_per_block);
+  const int r0 = (blockIdx.y * 4 + w) * RW;
   __shared__ float red[4][2][64];
-  float s = 0.f, q = 0.f;
-  if (c < C) {
-    for (int r = rb + w; r < re; r += 4) {
-      s += slab[((long)r * 2 + 0) * C + c];
-      q += slab[((long)r * 2 + 1) * C + c];
-    }
+  float vs[RW], vq[RW];
+#pragma unroll
+  for (int j = 0; j < RW; ++j) {
+    const bool ok = c < C && r0 + j < rows;
+    vs[j] = ok ? slab[((long)(r0 + j) * 2 + 0) * C + c] : 0.f;
+    vq[j] = ok ? slab[((long)(r0 + j) * 2 + 1) * C + c] : 0.f;
   }
+  float s = 0.f, q = 0.f;
+#pragma unroll
+  for (int j = 0; j < RW; ++j) { s += vs[j]; q += vq[j]; }
   red[w][0][lane] = s;
   red[w][1][lane] = q;
   __syncthreads();
@@ -387,9 +393,15 @@ void bn_partial(int dtype, const void* x, const void* dy, const void* yout, void
 
 // `sums` must have been zeroed by the producer of `slab` (workgroup 0 of gemm_g2 / bn_partial)
 void bn_slab_reduce(const float* slab, int rows, int C, float* sums, hipStream_t s) {
-  const int rpb = 64;
-  dim3 grid((C + 63) / 64, (rows + rpb - 1) / rpb);
-  hipLaunchKernelGGL(bn_slab_reduce_kernel, grid, dim3(256), 0, s, slab, rows, C, rpb, sums);
+  // 8 rows per wave (32 per block) unless that leaves > ~1024 blocks (each adds 2x64 atomics)
+  const long cg = (C + 63) / 64;
+  if (cg * ((rows + 31) / 32) <= 1024) {
+    hipLaunchKernelGGL(bn_slab_reduce_kernel<8>, dim3((unsigned)cg, (rows + 31) / 32), dim3(256), 0, s, slab, rows, C,
+                       sums);
+  } else {
+    hipLaunchKernelGGL(bn_slab_reduce_kernel<32>, dim3((unsigned)cg, (rows + 127) / 128), dim3(256), 0, s, slab,
+                       rows, C, sums);
+  }
   DCNN_LAUNCH_CHECK();
 }
 
