@@ -128,6 +128,18 @@ void nchw_to_nhwc(int dt, const float* x, void* y, int N, int C, int HW, hipStre
 void nchw_to_nhwc_pad(int dt, const float* x, void* y, int N, int C, int Cp, int HW, hipStream_t s);
 void conv_weight_transpose(int src_dt, const void* w, bf16* wt, int Co, int T_, int Ci, hipStream_t s);
 void cast_f32_bf16(const float* x, bf16* y, long n, hipStream_t s);
+// RGB stem conv (stem.hip): 3x3 s1 p1 from fp32 NCHW input, Ci <= 4, Co in {16,32,48,64}
+struct StemArgs {
+  const float* x; const void* w; int w_bf16; long ws[4];  // weight [Co][Ci][3][3] element strides
+  const float* bias; bf16* y; float* slab; float* zero_ptr; int zero_n;  // fwd
+  const bf16* dy; float* bias_slab; long gs[4]; long n_slab;             // wgrad (gs: grad strides)
+  int halo_bytes; int N, Ci, H, W, Co, TH;
+};
+bool stem_supported(int N, int Ci, int H, int W, int Co);
+int stem_tiles_host(int N, int H, int W);
+int stem_wgrad_blocks(int N, int H, int W);
+void stem_fwd(StemArgs a, hipStream_t s);
+void stem_wgrad(StemArgs a, int blocks, hipStream_t s);
 void multi_weight_transpose(const int64_t* table, int n, long max_tiles, hipStream_t s);
 void im2col(const float* x, float* col, int N, int C, int H, int W, int KH, int KW, int SH, int SW, int PH, int PW,
             int OH, int OW, hipStream_t s);

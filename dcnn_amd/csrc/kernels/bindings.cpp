@@ -271,6 +271,30 @@ PYBIND11_MODULE(_kernels, m) {
   m.def("conv_weight_transpose", [](int dt, uintptr_t w, uintptr_t wt, int Co, int T_, int Ci, uintptr_t st) {
     conv_weight_transpose(dt, P<const void*>(w), P<bf16*>(wt), Co, T_, Ci, S(st));
   });
+  m.def("stem_supported", &stem_supported);
+  m.def("stem_tiles", &stem_tiles_host);
+  m.def("stem_wgrad_blocks", &stem_wgrad_blocks);
+  m.def("stem_fwd", [](uintptr_t x, uintptr_t w, int w_bf16, std::array<long, 4> ws, uintptr_t bias, uintptr_t y,
+                       uintptr_t slab, uintptr_t zero_ptr, int zero_n, int N, int Ci, int H, int W, int Co,
+                       uintptr_t st) {
+    StemArgs a{};
+    a.x = P<const float*>(x); a.w = P<const void*>(w); a.w_bf16 = w_bf16;
+    for (int i = 0; i < 4; ++i) a.ws[i] = ws[i];
+    a.bias = P<const float*>(bias); a.y = P<bf16*>(y); a.slab = P<float*>(slab);
+    a.zero_ptr = P<float*>(zero_ptr); a.zero_n = zero_n;
+    a.N = N; a.Ci = Ci; a.H = H; a.W = W; a.Co = Co;
+    stem_fwd(a, S(st));
+  });
+  m.def("stem_wgrad", [](uintptr_t x, uintptr_t dy, uintptr_t slab, uintptr_t bias_slab, std::array<long, 4> gs,
+                         int N, int Ci, int H, int W, int Co, int blocks, uintptr_t st) {
+    StemArgs a{};
+    a.x = P<const float*>(x); a.dy = P<const bf16*>(dy); a.slab = P<float*>(slab);
+    a.bias_slab = P<float*>(bias_slab);
+    for (int i = 0; i < 4; ++i) a.gs[i] = gs[i];
+    a.n_slab = (long)Co * Ci * 9;
+    a.N = N; a.Ci = Ci; a.H = H; a.W = W; a.Co = Co;
+    stem_wgrad(a, blocks, S(st));
+  });
   m.def("multi_weight_transpose", [](uintptr_t table, int n, long max_tiles, uintptr_t st) {
     multi_weight_transpose(P<const int64_t*>(table), n, max_tiles, S(st));
   });

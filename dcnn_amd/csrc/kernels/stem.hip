@@ -1,0 +1,267 @@
+// RGB stem convolution (3x3, stride 1, pad 1, Ci <= 4, Co = 16..64) straight from the
+// network's fp32 NCHW input, forward and weight gradient, on CDNA4 MFMA 16x16x32 bf16.
+//
+// The generic implicit GEMM (gemm2.hip) needs the input as NHWC bf16 with >= 8 channels, so the
+// stem used to pay a layout/pad pass (nchw_to_nhwc_pad) and then ran a K = 72 GEMM whose
+// 16-byte gathers carry 3 useful channels of 8 (~25 TFLOP/s, 7x over its memory floor). Here a
+// workgroup owns a band of TH full image rows (TH * W = 512 output pixels) and stages its halo
+// [(TH+2)][(W+2)][4 ch] once in LDS as bf16, converting from fp32 NCHW on the way in. The GEMM
+// K axis is ordered (tap, channel-of-4): the 16x16x32 A fragment of a lane is two adjacent taps
+// of one pixel = two 8-byte LDS reads, so K = 9 x 4 = 36 is two MFMA k-steps (taps 0-7, tap 8).
+//
+//   fwd:   y[p][co] = sum_k im2col(x)[p][k] * w[co][k]  (+ bias), bf16 NHWC, BN partial stats
+//   wgrad: dW[co][k] = sum_p dY[p][co] * im2col(x)[p][k] ; column k = 36 of the B operand is
+//          all ones, so the same MFMAs also produce the bias gradient sum_p dY[p][co].
+//          Per-workgroup partials go to an fp32 slab reduced by splitk_reduce2.
+#include "common.h"
+#include "api.h"
+
+namespace dcnn {
+
+namespace {
+constexpr int SPX = 512;          // output pixels per tile (TH * W)
+constexpr int HALO_MAX = 6 * 130 * 4;  // bf16 elements of the forward halo (W <= 128)
+
+__device__ __forceinline__ int stem_tiles(const StemArgs& p) { return p.N * (p.H / p.TH); }
+
+// halo [(TH+2)][(W+2)][4] bf16 (8 bytes per pixel) of tile `tile` from fp32 NCHW, zero padded
+__device__ __forceinline__ void stage_halo(const StemArgs& p, int tile, bf16* hs) {
+  const int tpi = p.H / p.TH, n = tile / tpi, y0 = (tile - n * tpi) * p.TH;
+  const int HW2 = p.W + 2, rows = p.TH + 2, per_c = rows * HW2;
+  for (int i = threadIdx.x; i < 4 * per_c; i += blockDim.x) {
+    const int c = i / per_c, r = i - c * per_c, hy = r / HW2, hx = r - hy * HW2;
+    const int y = y0 + hy - 1, x = hx - 1;
+    float v = 0.f;
+    if (c < p.Ci && (unsigned)y < (unsigned)p.H && (unsigned)x < (unsigned)p.W)
+      v = p.x[(((long)n * p.Ci + c) * p.H + y) * p.W + x];
+    hs[r * 4 + c] = (bf16)v;
+  }
+}
+
+__device__ __forceinline__ float wval(const StemArgs& p, int co, int tap, int ch) {
+  if (ch >= p.Ci || tap > 8) return 0.f;
+  const long o = co * p.ws[0] + ch * p.ws[1] + (tap / 3) * p.ws[2] + (tap % 3) * p.ws[3];
+  return p.w_bf16 ? (float)reinterpret_cast<const bf16*>(p.w)[o] : reinterpret_cast<const float*>(p.w)[o];
+}
+
+__device__ __forceinline__ bf16x8 cat44(bf16x4 lo, bf16x4 hi) {
+  return bf16x8{lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+}
+}  // namespace
+
+// ---------------------------------------------------------------------------------------------
+// forward: one tile per workgroup, wave w takes 16-pixel groups w, w+4, ...
+// ---------------------------------------------------------------------------------------------
+template <int NCB>
+__global__ void __launch_bounds__(256) stem_fwd_kernel(StemArgs p) {
+  constexpr int CO = NCB * 16;
+  __shared__ __attribute__((aligned(16))) bf16 halo[HALO_MAX];
+  __shared__ __attribute__((aligned(16))) bf16 stg[4][16 * CO];
+  __shared__ float red[4][2][CO];
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6, kg = lane >> 4, col = lane & 15;
+  const int tile = blockIdx.x;
+  if (p.zero_ptr && tile == 0)
+    for (int i = threadIdx.x; i < p.zero_n; i += 256) p.zero_ptr[i] = 0.f;
+  stage_halo(p, tile, halo);
+
+  // B fragments (weights), k-step 0: taps 2kg, 2kg+1; k-step 1: tap 8 in lane group 0
+  bf16x8 b0[NCB], b1[NCB];
+  float bias[NCB];
+#pragma unroll
+  for (int cb = 0; cb < NCB; ++cb) {
+    const int co = cb * 16 + col;
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      b0[cb][e] = (bf16)wval(p, co, 2 * kg + (e >> 2), e & 3);
+      b1[cb][e] = (bf16)(kg == 0 ? wval(p, co, 8, e & 3) * (e < 4) : 0.f);
+    }
+    bias[cb] = p.bias ? p.bias[co] : 0.f;
+  }
+  __syncthreads();
+
+  const int HW2 = p.W + 2;
+  const int tpi = p.H / p.TH, n = tile / tpi, y0 = (tile - n * tpi) * p.TH;
+  // per-lane tap offsets (in halo pixels) of the A fragment: taps 2kg, 2kg+1 and tap 8
+  const int t0 = 2 * kg, t1 = 2 * kg + 1;
+  const int o0 = (t0 / 3) * HW2 + t0 % 3, o1 = (t1 / 3) * HW2 + t1 % 3, o8 = 2 * HW2 + 2;
+  float s[NCB], q[NCB];
+#pragma unroll
+  for (int cb = 0; cb < NCB; ++cb) s[cb] = q[cb] = 0.f;
+  const bf16x4 z4 = bf16x4{(bf16)0.f, (bf16)0.f, (bf16)0.f, (bf16)0.f};
+  for (int g = wid; g < SPX / 16; g += 4) {
+    const int px = g * 16 + col, py = px / p.W, pxx = px - py * p.W;
+    const int hp = py * HW2 + pxx;  // halo pixel of tap (0, 0)
+    const bf16x4* h4 = reinterpret_cast<const bf16x4*>(halo);
+    const bf16x8 a0 = cat44(h4[hp + o0], h4[hp + o1]);
+    const bf16x8 a1 = cat44(kg == 0 ? h4[hp + o8] : z4, z4);
+#pragma unroll
+    for (int cb = 0; cb < NCB; ++cb) {
+      f32x4 acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a0, b0[cb], f32x4{0.f, 0.f, 0.f, 0.f}, 0, 0, 0);
+      acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a1, b1[cb], acc, 0, 0, 0);
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const bf16 v = (bf16)(acc[r] + bias[cb]);
+        const float f = (float)v;
+        s[cb] += f;
+        q[cb] += f * f;
+        stg[wid][(kg * 4 + r) * CO + cb * 16 + col] = v;
+      }
+    }
+    // the 16 pixels of a group are contiguous in NHWC: 16 * CO * 2 bytes, 16 per lane
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_wave_barrier();
+    const long obase = (((long)n * p.H + y0) * p.W + g * 16) * CO;
+    for (int c = lane; c < 2 * CO; c += 64)
+      reinterpret_cast<uint4*>(p.y + obase)[c] = reinterpret_cast<const uint4*>(stg[wid])[c];
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_wave_barrier();
+  }
+  if (!p.slab) return;
+  // channel sums: lane groups (kg) via cross-lane adds, then the 4 waves through LDS
+#pragma unroll
+  for (int cb = 0; cb < NCB; ++cb) {
+    s[cb] += __shfl_xor(s[cb], 16);
+    s[cb] += __shfl_xor(s[cb], 32);
+    q[cb] += __shfl_xor(q[cb], 16);
+    q[cb] += __shfl_xor(q[cb], 32);
+    if (kg == 0) { red[wid][0][cb * 16 + col] = s[cb]; red[wid][1][cb * 16 + col] = q[cb]; }
+  }
+  __syncthreads();
+  for (int i = threadIdx.x; i < 2 * CO; i += 256) {
+    const int which = i / CO, c = i - which * CO;
+    p.slab[((long)tile * 2 + which) * CO + c] = red[0][which][c] + red[1][which][c] + red[2][which][c] + red[3][which][c];
+  }
+}
+
+// ---------------------------------------------------------------------------------------------
+// weight gradient: workgroup b accumulates tiles b, b + grid, ...; each tile's 16 k-steps of 32
+// pixels are split over the 4 waves. D[co][k] with k = tap*4 + ch (k < 36), k = 36: ones.
+// ---------------------------------------------------------------------------------------------
+template <int NCB>
+__global__ void __launch_bounds__(256) stem_wgrad_kernel(StemArgs p) {
+  constexpr int CO = NCB * 16;
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  bf16* halo = reinterpret_cast<bf16*>(smem);                     // [(TH+2)(W+2)][4]
+  bf16* dys = reinterpret_cast<bf16*>(smem + p.halo_bytes);       // [512][CO]
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6, kg = lane >> 4, col = lane & 15;
+  const int HW2 = p.W + 2;
+  const int ntile = stem_tiles(p);
+  f32x4 acc[NCB][3];
+#pragma unroll
+  for (int cb = 0; cb < NCB; ++cb)
+#pragma unroll
+    for (int nb = 0; nb < 3; ++nb) acc[cb][nb] = f32x4{0.f, 0.f, 0.f, 0.f};
+  // B column of this lane in each of the 3 n-blocks: k = nb*16 + col -> (tap, ch); k = 36: ones
+  int koff[3];
+  bool kval[3], kone[3];
+#pragma unroll
+  for (int nb = 0; nb < 3; ++nb) {
+    const int k = nb * 16 + col, tap = k >> 2, ch = k & 3;
+    kval[nb] = k < 36 && ch < p.Ci;
+    kone[nb] = k == 36;
+    koff[nb] = ((tap < 9 ? (tap / 3) * HW2 + tap % 3 : 0) * 4) + ch;
+  }
+  for (int tile = blockIdx.x; tile < ntile; tile += gridDim.x) {
+    __syncthreads();  // previous tile's fragments consumed
+    stage_halo(p, tile, halo);
+    const int tpi = p.H / p.TH, n = tile / tpi, y0 = (tile - n * tpi) * p.TH;
+    const uint4* src = reinterpret_cast<const uint4*>(p.dy + (((long)n * p.H + y0) * p.W) * CO);
+    for (int i = threadIdx.x; i < SPX * CO / 8; i += 256) reinterpret_cast<uint4*>(dys)[i] = src[i];
+    __syncthreads();
+    for (int ks = wid; ks < SPX / 32; ks += 4) {
+      // this lane's 8 pixels (GEMM k) of the step: ks*32 + kg*8 .. +7, all in one image row
+      const int p0 = ks * 32 + kg * 8, py = p0 / p.W, px0 = p0 - py * p.W;
+      bf16x8 a[NCB], b[3];
+#pragma unroll
+      for (int cb = 0; cb < NCB; ++cb)
+#pragma unroll
+        for (int e = 0; e < 8; ++e) a[cb][e] = dys[(p0 + e) * CO + cb * 16 + col];
+      const int hb = (py * HW2 + px0) * 4;
+#pragma unroll
+      for (int nb = 0; nb < 3; ++nb)
+#pragma unroll
+        for (int e = 0; e < 8; ++e)
+          b[nb][e] = kval[nb] ? halo[hb + e * 4 + koff[nb]] : (bf16)(kone[nb] ? 1.f : 0.f);
+#pragma unroll
+      for (int cb = 0; cb < NCB; ++cb)
+#pragma unroll
+        for (int nb = 0; nb < 3; ++nb) acc[cb][nb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[cb], b[nb], acc[cb][nb], 0, 0, 0);
+    }
+  }
+  // 4 waves -> one partial: D rows (co) = 4*kg + r of block cb, column k = nb*16 + col
+  __syncthreads();
+  float* red = reinterpret_cast<float*>(smem);  // [4][CO][48]
+#pragma unroll
+  for (int cb = 0; cb < NCB; ++cb)
+#pragma unroll
+    for (int nb = 0; nb < 3; ++nb)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) red[(wid * CO + cb * 16 + kg * 4 + r) * 48 + nb * 16 + col] = acc[cb][nb][r];
+  __syncthreads();
+  float* out = p.slab + (long)blockIdx.x * p.n_slab;
+  for (int i = threadIdx.x; i < CO * 37; i += 256) {
+    const int co = i / 37, k = i - co * 37, tap = k >> 2, ch = k & 3;
+    const float v = red[(0 * CO + co) * 48 + k] + red[(1 * CO + co) * 48 + k] + red[(2 * CO + co) * 48 + k] +
+                    red[(3 * CO + co) * 48 + k];
+    if (k == 36) {
+      if (p.bias_slab) p.bias_slab[(long)blockIdx.x * CO + co] = v;
+    } else if (ch < p.Ci) {
+      out[co * p.gs[0] + ch * p.gs[1] + (tap / 3) * p.gs[2] + (tap % 3) * p.gs[3]] = v;
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------------------------
+// host side
+// ---------------------------------------------------------------------------------------------
+bool stem_supported(int N, int Ci, int H, int W, int Co) {
+  if (Ci < 1 || Ci > 4 || Co % 16 || Co > 64 || W % 16 || SPX % W) return false;
+  const int th = SPX / W;
+  if (H % th || (th + 2) * (W + 2) * 4 > HALO_MAX) return false;
+  return N > 0 && (long)N * Ci * H * W < (1l << 31);
+}
+
+int stem_tiles_host(int N, int H, int W) { return N * (H / (SPX / W)); }
+
+int stem_wgrad_blocks(int N, int H, int W) {
+  const int t = stem_tiles_host(N, H, W);
+  return t < 1024 ? t : 1024;
+}
+
+void stem_fwd(StemArgs a, hipStream_t s) {
+  if (!stem_supported(a.N, a.Ci, a.H, a.W, a.Co)) throw std::runtime_error("stem_fwd: unsupported shape");
+  a.TH = SPX / a.W;
+  const int grid = stem_tiles_host(a.N, a.H, a.W);
+  switch (a.Co / 16) {
+    case 1: hipLaunchKernelGGL(stem_fwd_kernel<1>, dim3(grid), dim3(256), 0, s, a); break;
+    case 2: hipLaunchKernelGGL(stem_fwd_kernel<2>, dim3(grid), dim3(256), 0, s, a); break;
+    case 3: hipLaunchKernelGGL(stem_fwd_kernel<3>, dim3(grid), dim3(256), 0, s, a); break;
+    default: hipLaunchKernelGGL(stem_fwd_kernel<4>, dim3(grid), dim3(256), 0, s, a); break;
+  }
+  DCNN_LAUNCH_CHECK();
+}
+
+void stem_wgrad(StemArgs a, int blocks, hipStream_t s) {
+  if (!stem_supported(a.N, a.Ci, a.H, a.W, a.Co)) throw std::runtime_error("stem_wgrad: unsupported shape");
+  if (blocks != stem_wgrad_blocks(a.N, a.H, a.W)) throw std::runtime_error("stem_wgrad: block count mismatch");
+  a.TH = SPX / a.W;
+  a.halo_bytes = (((a.TH + 2) * (a.W + 2) * 8) + 15) / 16 * 16;
+  const int main = a.halo_bytes + SPX * a.Co * 2, epi = 4 * a.Co * 48 * 4;
+  const int lds = main > epi ? main : epi;
+#define DCNN_SW(C)                                                                                        \
+  {                                                                                                       \
+    auto k = stem_wgrad_kernel<C>;                                                                        \
+    DCNN_HIP_CHECK(hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, lds)); \
+    hipLaunchKernelGGL(k, dim3(blocks), dim3(256), lds, s, a);                                            \
+  }
+  switch (a.Co / 16) {
+    case 1: DCNN_SW(1) break;
+    case 2: DCNN_SW(2) break;
+    case 3: DCNN_SW(3) break;
+    default: DCNN_SW(4) break;
+  }
+#undef DCNN_SW
+  DCNN_LAUNCH_CHECK();
+}
+
+}  // namespace dcnn

@@ -66,6 +66,16 @@ class Conv2D(ParameterizedLayer):
             raise ValueError(f"Conv2D '{self.name}': input has {x.shape[1]} channels, expected {self.in_channels}")
         if x.is_cuda:
             from ...ops import hip
+            st, pd = (self.stride_h, self.stride_w), (self.pad_h, self.pad_w)
+            if (self.compute_dtype == torch.bfloat16 and not self.needs_input_grad
+                    and hip.stem_ok(x, self.weights.shape, st, pd)):
+                # RGB stem straight from the fp32 NCHW input (stem.hip): no layout/pad pass
+                y, partial = hip.stem_conv_fwd(x, self.weight_operand(0), self._bias_vec(),
+                                               stats=self.emit_bn_stats and self.training)
+                if partial is not None:
+                    y._bn_partial = partial
+                self._cache[mb_id] = (x, tuple(x.shape), "stem")
+                return y
             if self.in_channels < 8 and self.compute_dtype == torch.bfloat16:
                 # RGB stem: zero-pad channels to 8 so every 16-byte chunk is one tap (vector path)
                 xa = hip.to_act_padded(x, 8)
@@ -88,14 +98,18 @@ class Conv2D(ParameterizedLayer):
         x = self._cache.pop(mb_id, None)
         if x is None:
             raise RuntimeError(f"Conv2D '{self.name}': no cached input for micro-batch {mb_id}")
+        stem = isinstance(x, tuple) and len(x) == 3
         if isinstance(x, tuple):
-            x, x_shape = x
+            x, x_shape = x[0], x[1]
         else:
             x_shape = tuple(x.shape)
         grad = grad.to(x.device)
         if x.is_cuda:
             from ...ops import hip
             g = hip.to_act(grad, self.compute_dtype)
+            if stem:  # forward ran stem.hip (never with an input gradient)
+                hip.stem_conv_wgrad(g, x, self._grads[0], self._grads[1].view(-1) if self.use_bias else None)
+                return None
             hip.conv2d_wgrad(g, x, self.weights.shape, (self.stride_h, self.stride_w), (self.pad_h, self.pad_w),
                              self._grads[0], self._grads[1].view(-1) if self.use_bias else None)
             if not self.needs_input_grad:

@@ -155,6 +155,57 @@ def conv2d_fwd(x, w, bias, stride, pad, *, stats=False, residual=None, relu=Fals
     return y, ((slab, rows, sums) if stats else None)
 
 
+_STEM = os.environ.get("DCNN_STEM", "1") != "0"
+
+
+def stem_ok(x, w_shape, stride, pad):
+    """The RGB stem kernels (stem.hip) take this conv: fp32 NCHW input, 3x3 s1 p1, Ci <= 4."""
+    if not _STEM or x.dtype != F32 or not x.is_contiguous() or x.dim() != 4:
+        return False
+    Co, Ci, KH, KW = w_shape
+    N, C, H, W = x.shape
+    return ((KH, KW) == (3, 3) and tuple(stride) == (1, 1) and tuple(pad) == (1, 1) and C == Ci
+            and kernels().stem_supported(N, Ci, H, W, Co))
+
+
+def stem_conv_fwd(x, w, bias=None, stats=False):
+    """3x3/s1/p1 conv of the fp32 NCHW network input (Ci <= 4) -> bf16 NHWC, optionally with the
+    BatchNorm partial statistics (same ``(slab, rows, sums)`` contract as :func:`conv2d_fwd`).
+    ``w``: (Co, Ci, 3, 3) fp32 or bf16, any strides. One pass: no layout/pad kernel."""
+    N, Ci, H, W = x.shape
+    Co = w.shape[0]
+    K = kernels()
+    y = torch.empty((N, Co, H, W), dtype=BF16, device=x.device, memory_format=CL)
+    slab = sums = None
+    rows = 0
+    if stats:
+        rows = K.stem_tiles(N, H, W)
+        slab = torch.empty((rows, 2, Co), dtype=F32, device=x.device)
+        sums = torch.empty((2 * Co,), dtype=F32, device=x.device)  # zeroed in-kernel
+    assert w.dtype in (F32, BF16) and tuple(w.shape) == (Co, Ci, 3, 3)
+    K.stem_fwd(x.data_ptr(), w.data_ptr(), int(w.dtype == BF16), list(w.stride()), ptr(bias), y.data_ptr(),
+               ptr(slab), ptr(sums), 2 * Co if stats else 0, N, Ci, H, W, Co, stream_ptr())
+    return y, ((slab, rows, sums) if stats else None)
+
+
+def stem_conv_wgrad(dy, x, grad_w, grad_b=None):
+    """grad_w += dW, grad_b += sum(dy) of :func:`stem_conv_fwd` (dy: bf16 NHWC)."""
+    N, Ci, H, W = x.shape
+    Co = dy.shape[1]
+    K = kernels()
+    dy = dy.contiguous(memory_format=CL)
+    assert dy.dtype == BF16 and tuple(dy.shape) == (N, Co, H, W)
+    assert grad_w.is_contiguous() or grad_w.is_contiguous(memory_format=CL), "dense fp32 weight gradient"
+    blocks = K.stem_wgrad_blocks(N, H, W)
+    n = Co * Ci * 9
+    slab = torch.empty((blocks, n), dtype=F32, device=x.device)
+    bslab = torch.empty((blocks, Co), dtype=F32, device=x.device) if grad_b is not None else None
+    st = stream_ptr()
+    K.stem_wgrad(x.data_ptr(), dy.data_ptr(), slab.data_ptr(), ptr(bslab), list(grad_w.stride()), N, Ci, H, W, Co,
+                 blocks, st)
+    _reduce_wb(K, slab, grad_w, n, bslab, grad_b, Co, blocks, st)
+
+
 def to_act_padded(x, cp):
     """(N,C,H,W) -> NHWC bf16 with channels zero-padded to cp (RGB stem: 3 -> 8) so the stem
     conv runs on the vectorised MFMA path. One HIP pass from an NCHW fp32 input."""

@@ -124,6 +124,45 @@ def test_padded_rgb_stem(hip):
     assert rel_err(gw, torch.nn.grad.conv2d_weight(bf(x), w.shape, bf(dy), 1, 1)) < 1e-2
 
 
+@pytest.mark.parametrize("case", [
+    # N, Ci, H, W, Co, bias, weight dtype/layout
+    (4, 3, 64, 64, 32, False, "bf16_cl"), (3, 3, 32, 32, 64, True, "f32"), (2, 1, 32, 16, 16, True, "f32_cl"),
+    (2, 4, 16, 128, 48, False, "bf16"),
+])
+def test_stem_conv(hip, case):
+    """stem.hip: 3x3/s1/p1 conv straight from fp32 NCHW (fwd + BN statistics, wgrad + bias grad)
+    against the fp32 reference on the bf16-rounded operands."""
+    N, Ci, H, W, Co, use_b, wfmt = case
+    torch.manual_seed(11)
+    x = torch.randn(N, Ci, H, W)
+    w = torch.randn(Co, Ci, 3, 3) / math.sqrt(Ci * 9)
+    b = torch.randn(Co) if use_b else None
+    xg = x.cuda()
+    assert hip.stem_ok(xg, w.shape, (1, 1), (1, 1))
+    wg = w.cuda().to(torch.bfloat16 if wfmt.startswith("bf16") else torch.float32)
+    if wfmt.endswith("_cl"):
+        wg = wg.contiguous(memory_format=CL)
+    y, partial = hip.stem_conv_fwd(xg, wg, b.cuda() if use_b else None, stats=True)
+    y_ref = F.conv2d(bf(x), bf(w), b, 1, 1)
+    assert y.shape == y_ref.shape and y.is_contiguous(memory_format=CL)
+    assert rel_err(y, y_ref) < 1e-2, rel_err(y, y_ref)
+    sums = hip.bn_stats(y, partial)
+    yf = y.float()
+    assert rel_err(sums[:Co], yf.sum((0, 2, 3))) < 1e-3
+    assert rel_err(sums[Co:], (yf * yf).sum((0, 2, 3))) < 1e-3
+    dy = torch.randn(N, Co, H, W)
+    dyg = dy.cuda().to(torch.bfloat16).contiguous(memory_format=CL)
+    gw = torch.full((Co, Ci, 3, 3), 0.25, device="cuda")
+    if wfmt.endswith("_cl"):
+        gw = gw.contiguous(memory_format=CL)
+    gb = torch.ones(Co, device="cuda") if use_b else None
+    hip.stem_conv_wgrad(dyg, xg, gw, gb)
+    dw_ref = torch.nn.grad.conv2d_weight(bf(x), w.shape, bf(dy), 1, 1) + 0.25
+    assert rel_err(gw, dw_ref) < 1e-2, rel_err(gw, dw_ref)
+    if use_b:
+        assert rel_err(gb, bf(dy).sum((0, 2, 3)) + 1) < 1e-2
+
+
 @pytest.mark.parametrize("shape", [(128, 512, 200), (64, 256, 10), (16, 192, 10), (256, 1024, 200)])
 def test_dense(hip, shape):
     N, In, Out = shape
