@@ -227,6 +227,19 @@ PYBIND11_MODULE(_kernels, m) {
                                             int padh, int padw) {
     return maxpool_bwd_bnb_supported(geom(N, H, W, C, OH, OW, ph, pw, sh, sw, padh, padw));
   });
+  m.def("bn_relu_maxpool_supported", [geom](int N, int H, int W, int C, int OH, int OW, int ph, int pw, int sh, int sw,
+                                            int padh, int padw) {
+    return bn_relu_maxpool_supported(geom(N, H, W, C, OH, OW, ph, pw, sh, sw, padh, padw));
+  });
+  m.def("bn_relu_maxpool", [geom](uintptr_t x, uintptr_t y, uintptr_t idx, int N, int H, int W, int C, int OH, int OW,
+                                  int ph, int pw, int sh, int sw, int padh, int padw, uintptr_t sums, float count,
+                                  uintptr_t gamma, uintptr_t beta, float eps, uintptr_t save_mean, uintptr_t save_istd,
+                                  uintptr_t run_mean, uintptr_t run_var, float momentum, uintptr_t st) {
+    bn_relu_maxpool(P<const bf16*>(x), P<bf16*>(y), P<uint8_t*>(idx), geom(N, H, W, C, OH, OW, ph, pw, sh, sw, padh, padw),
+                    P<const float*>(sums), count, P<const float*>(gamma), P<const float*>(beta), eps,
+                    P<float*>(save_mean), P<float*>(save_istd), P<float*>(run_mean), P<float*>(run_var), momentum,
+                    S(st));
+  });
   m.def("maxpool_bwd_bnb_rows", [geom](int N, int H, int W, int C, int OH, int OW, int ph, int pw, int sh, int sw,
                                        int padh, int padw) {
     return maxpool_bwd_bnb_rows(geom(N, H, W, C, OH, OW, ph, pw, sh, sw, padh, padw));

@@ -218,6 +218,68 @@ __global__ void __launch_bounds__(256) bn_apply_kernel(const T* __restrict__ x, 
   }
 }
 
+// Training-mode BatchNorm + ReLU + non-overlapping max-pool in one pass (the ResNet stem):
+// y[n][oy][ox][c] = max over the window of relu(x * scale + shift), rounded to bf16 BEFORE the
+// comparison exactly as bn_apply + maxpool_fwd would, idx = window position of the max. The
+// full-resolution BN output is never written: the backward (maxpool_bwd_bnb) masks with the
+// pooled value and recomputes xhat from x.
+__global__ void __launch_bounds__(256) bn_relu_maxpool_kernel(const bf16* __restrict__ x, bf16* __restrict__ y,
+                                                              uint8_t* __restrict__ idx, PoolGeom g,
+                                                              const float* __restrict__ sums, float count,
+                                                              const float* __restrict__ gamma,
+                                                              const float* __restrict__ beta, float eps,
+                                                              float* __restrict__ save_mean,
+                                                              float* __restrict__ save_istd,
+                                                              float* __restrict__ run_mean,
+                                                              float* __restrict__ run_var, float momentum) {
+  extern __shared__ __attribute__((aligned(16))) float sh[];
+  float* scale = sh;
+  float* shift = sh + g.C;
+  for (int c = threadIdx.x; c < g.C; c += blockDim.x) {
+    const float mean = sums[c] / count;
+    const float var = fmaxf(sums[g.C + c] / count - mean * mean, 0.f);
+    const float istd = rsqrtf(var + eps);
+    if (blockIdx.x == 0) {
+      if (save_mean) { save_mean[c] = mean; save_istd[c] = istd; }
+      if (run_mean) {
+        const float unbiased = count > 1.f ? var * count / (count - 1.f) : var;
+        run_mean[c] = (1.f - momentum) * run_mean[c] + momentum * mean;
+        run_var[c] = (1.f - momentum) * run_var[c] + momentum * unbiased;
+      }
+    }
+    const float gm = gamma ? gamma[c] : 1.f, b = beta ? beta[c] : 0.f;
+    scale[c] = gm * istd;
+    shift[c] = b - mean * gm * istd;
+  }
+  __syncthreads();
+  const int CV = g.C / 8;
+  const long total = (long)g.N * g.OH * g.OW * CV;
+  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < total; i += (long)gridDim.x * blockDim.x) {
+    const int cv = (int)(i % CV);
+    long t = i / CV;
+    const int ox = (int)(t % g.OW);
+    t /= g.OW;
+    const int oy = (int)(t % g.OH);
+    const int n = (int)(t / g.OH);
+    float sc[8], sf[8], best[8], v[8];
+    uint8_t bi[8];
+#pragma unroll
+    for (int e = 0; e < 8; ++e) { sc[e] = scale[cv * 8 + e]; sf[e] = shift[cv * 8 + e]; best[e] = -INFINITY; bi[e] = 0; }
+    for (int ky = 0; ky < g.ph; ++ky)
+      for (int kx = 0; kx < g.pw; ++kx) {
+        const int iy = oy * g.ph + ky, ix = ox * g.pw + kx;
+        unpack8(*reinterpret_cast<const uint4*>(x + (((long)n * g.H + iy) * g.W + ix) * g.C + cv * 8), v);
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+          const float r = (float)(bf16)fmaxf(v[e] * sc[e] + sf[e], 0.f);
+          if (r > best[e]) { best[e] = r; bi[e] = (uint8_t)(ky * g.pw + kx); }
+        }
+      }
+    *reinterpret_cast<uint4*>(y + i * 8) = pack8(best);
+    *reinterpret_cast<uint2*>(idx + i * 8) = *reinterpret_cast<uint2*>(bi);
+  }
+}
+
 // dx = gamma*istd*(dy' - sum_dy/M - xhat*sum_dyxhat/M); block 0 accumulates dgamma/dbeta.
 template <typename T, int V>
 __global__ void __launch_bounds__(256) bn_bwd_apply_kernel(const T* __restrict__ dy, const T* __restrict__ yout,
@@ -402,6 +464,21 @@ void bn_slab_reduce(const float* slab, int rows, int C, float* sums, hipStream_t
     hipLaunchKernelGGL(bn_slab_reduce_kernel<32>, dim3((unsigned)cg, (rows + 127) / 128), dim3(256), 0, s, slab,
                        rows, C, sums);
   }
+  DCNN_LAUNCH_CHECK();
+}
+
+bool bn_relu_maxpool_supported(PoolGeom g) {
+  return g.C % 8 == 0 && g.ph == g.sh && g.pw == g.sw && g.padh == 0 && g.padw == 0 && g.ph * g.pw <= 255 &&
+         g.OH == g.H / g.ph && g.OW == g.W / g.pw;
+}
+
+void bn_relu_maxpool(const bf16* x, bf16* y, uint8_t* idx, PoolGeom g, const float* sums, float count,
+                     const float* gamma, const float* beta, float eps, float* save_mean, float* save_istd,
+                     float* run_mean, float* run_var, float momentum, hipStream_t s) {
+  if (!bn_relu_maxpool_supported(g)) throw std::runtime_error("bn_relu_maxpool: unsupported geometry");
+  const long total = (long)g.N * g.OH * g.OW * g.C / 8;
+  hipLaunchKernelGGL(bn_relu_maxpool_kernel, dim3(grid_for(total, 256, 2048)), dim3(256), 2 * g.C * sizeof(float), s,
+                     x, y, idx, g, sums, count, gamma, beta, eps, save_mean, save_istd, run_mean, run_var, momentum);
   DCNN_LAUNCH_CHECK();
 }
 

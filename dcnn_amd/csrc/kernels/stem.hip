@@ -24,17 +24,41 @@ constexpr int HALO_MAX = 6 * 130 * 4;  // bf16 elements of the forward halo (W <
 
 __device__ __forceinline__ int stem_tiles(const StemArgs& p) { return p.N * (p.H / p.TH); }
 
-// halo [(TH+2)][(W+2)][4] bf16 (8 bytes per pixel) of tile `tile` from fp32 NCHW, zero padded
+// halo [(TH+2)][(W+2)][4] bf16 (8 bytes per pixel) of tile `tile` from fp32 NCHW, zero padded.
+// Tiles span whole rows, so the left/right halo columns are always padding: the interior is
+// read with 16-byte loads (4 pixels of one channel row, all of a thread's loads issued before
+// its first LDS store), and the padding columns / channels >= Ci are zero-filled. The three
+// sets are disjoint: no ordering between them is needed.
 __device__ __forceinline__ void stage_halo(const StemArgs& p, int tile, bf16* hs) {
+  constexpr int J = 3;  // interior float4 per thread: Ci * (TH+2) * W/4 <= 768 (stem_supported)
   const int tpi = p.H / p.TH, n = tile / tpi, y0 = (tile - n * tpi) * p.TH;
-  const int HW2 = p.W + 2, rows = p.TH + 2, per_c = rows * HW2;
-  for (int i = threadIdx.x; i < 4 * per_c; i += blockDim.x) {
-    const int c = i / per_c, r = i - c * per_c, hy = r / HW2, hx = r - hy * HW2;
-    const int y = y0 + hy - 1, x = hx - 1;
-    float v = 0.f;
-    if (c < p.Ci && (unsigned)y < (unsigned)p.H && (unsigned)x < (unsigned)p.W)
-      v = p.x[(((long)n * p.Ci + c) * p.H + y) * p.W + x];
-    hs[r * 4 + c] = (bf16)v;
+  const int HW2 = p.W + 2, rows = p.TH + 2, w4 = p.W >> 2, per_c = rows * w4, total = p.Ci * per_c;
+  float4 v[J];
+#pragma unroll
+  for (int j = 0; j < J; ++j) {
+    const int i = threadIdx.x + j * 256;
+    const int c = i / per_c, r = i - c * per_c, hy = r / w4, x4 = r - hy * w4;
+    const int y = y0 + hy - 1;
+    v[j] = make_float4(0.f, 0.f, 0.f, 0.f);
+    if (i < total && (unsigned)y < (unsigned)p.H)
+      v[j] = *reinterpret_cast<const float4*>(p.x + (((long)n * p.Ci + c) * p.H + y) * p.W + x4 * 4);
+  }
+  for (int i = threadIdx.x; i < (4 - p.Ci) * rows * HW2; i += 256) {  // channels >= Ci
+    const int c = p.Ci + i / (rows * HW2), r = i % (rows * HW2);
+    hs[r * 4 + c] = (bf16)0.f;
+  }
+  for (int i = threadIdx.x; i < p.Ci * rows * 2; i += 256) {  // left / right padding columns
+    const int c = i / (rows * 2), r = i % (rows * 2), hy = r >> 1;
+    hs[(hy * HW2 + (r & 1) * (HW2 - 1)) * 4 + c] = (bf16)0.f;
+  }
+#pragma unroll
+  for (int j = 0; j < J; ++j) {
+    const int i = threadIdx.x + j * 256;
+    const int c = i / per_c, r = i - c * per_c, hy = r / w4, x4 = r - hy * w4;
+    if (i < total) {
+      bf16* d = hs + (hy * HW2 + 1 + x4 * 4) * 4 + c;
+      d[0] = (bf16)v[j].x; d[4] = (bf16)v[j].y; d[8] = (bf16)v[j].z; d[12] = (bf16)v[j].w;
+    }
   }
 }
 
@@ -53,7 +77,8 @@ __device__ __forceinline__ bf16x8 cat44(bf16x4 lo, bf16x4 hi) {
 // forward: one tile per workgroup, wave w takes 16-pixel groups w, w+4, ...
 // ---------------------------------------------------------------------------------------------
 template <int NCB>
-__global__ void __launch_bounds__(256) stem_fwd_kernel(StemArgs p) {
+// <= 64 VGPRs for Co <= 32: 8 workgroups per CU, a ResNet stem's whole grid resident at once
+__global__ void __launch_bounds__(256, NCB <= 2 ? 8 : 4) stem_fwd_kernel(StemArgs p) {
   constexpr int CO = NCB * 16;
   __shared__ __attribute__((aligned(16))) bf16 halo[HALO_MAX];
   __shared__ __attribute__((aligned(16))) bf16 stg[4][16 * CO];
@@ -138,7 +163,7 @@ __global__ void __launch_bounds__(256) stem_fwd_kernel(StemArgs p) {
 // pixels are split over the 4 waves. D[co][k] with k = tap*4 + ch (k < 36), k = 36: ones.
 // ---------------------------------------------------------------------------------------------
 template <int NCB>
-__global__ void __launch_bounds__(256) stem_wgrad_kernel(StemArgs p) {
+__global__ void __launch_bounds__(256, NCB <= 2 ? 4 : 2) stem_wgrad_kernel(StemArgs p) {
   constexpr int CO = NCB * 16;
   extern __shared__ __attribute__((aligned(16))) char smem[];
   bf16* halo = reinterpret_cast<bf16*>(smem);                     // [(TH+2)(W+2)][4]
@@ -146,6 +171,7 @@ __global__ void __launch_bounds__(256) stem_wgrad_kernel(StemArgs p) {
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6, kg = lane >> 4, col = lane & 15;
   const int HW2 = p.W + 2;
   const int ntile = stem_tiles(p);
+  const i32x4 rs_dy = raw_rsrc(p.dy, (unsigned)((long)p.N * p.H * p.W * CO * 2));
   f32x4 acc[NCB][3];
 #pragma unroll
   for (int cb = 0; cb < NCB; ++cb)
@@ -163,10 +189,16 @@ __global__ void __launch_bounds__(256) stem_wgrad_kernel(StemArgs p) {
   }
   for (int tile = blockIdx.x; tile < ntile; tile += gridDim.x) {
     __syncthreads();  // previous tile's fragments consumed
-    stage_halo(p, tile, halo);
     const int tpi = p.H / p.TH, n = tile / tpi, y0 = (tile - n * tpi) * p.TH;
-    const uint4* src = reinterpret_cast<const uint4*>(p.dy + (((long)n * p.H + y0) * p.W) * CO);
-    for (int i = threadIdx.x; i < SPX * CO / 8; i += 256) reinterpret_cast<uint4*>(dys)[i] = src[i];
+    // the dY tile is contiguous in NHWC: 16-byte direct-to-LDS loads, 1 KB per wave instruction
+    const unsigned src = (unsigned)((((long)n * p.H + y0) * p.W) * CO * 2);
+#pragma unroll
+    for (int j = 0; j < SPX * CO * 2 / 1024 / 4; ++j) {
+      const int blk = wid * (SPX * CO * 2 / 1024 / 4) + j;
+      glds16_opaque(rs_dy, reinterpret_cast<char*>(dys) + blk * 1024, src + blk * 1024 + lane * 16);
+    }
+    stage_halo(p, tile, halo);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
     for (int ks = wid; ks < SPX / 32; ks += 4) {
       // this lane's 8 pixels (GEMM k) of the step: ks*32 + kg*8 .. +7, all in one image row
@@ -217,7 +249,7 @@ __global__ void __launch_bounds__(256) stem_wgrad_kernel(StemArgs p) {
 bool stem_supported(int N, int Ci, int H, int W, int Co) {
   if (Ci < 1 || Ci > 4 || Co % 16 || Co > 64 || W % 16 || SPX % W) return false;
   const int th = SPX / W;
-  if (H % th || (th + 2) * (W + 2) * 4 > HALO_MAX) return false;
+  if (H % th || (th + 2) * (W + 2) * 4 > HALO_MAX || Ci * (th + 2) * (W / 4) > 3 * 256) return false;
   return N > 0 && (long)N * Ci * H * W < (1l << 31);
 }
 

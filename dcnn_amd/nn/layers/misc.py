@@ -52,6 +52,8 @@ class MaxPool2D(_Pool):
 
     def forward(self, x, mb_id=0):
         x = self._to_layer_device(x)
+        if getattr(x, "_prepooled_by", None) is self:
+            return x  # the preceding BatchNorm+ReLU already pooled and filled this layer's cache
         if x.is_cuda:
             from ...ops import hip
             xa = hip.to_act(x, self.compute_dtype)

@@ -16,6 +16,10 @@ from ..params import ParamSpec
 from .base import LayerConfig, ParameterizedLayer
 
 
+# BatchNorm cache marker: the forward fused ReLU + max-pool (see BatchNorm.forward)
+_POOLED = object()
+
+
 class BatchNorm(ParameterizedLayer):
     type_name = "batchnorm"
 
@@ -71,6 +75,23 @@ class BatchNorm(ParameterizedLayer):
             from ...ops import hip
             xa = hip.to_act(x, self.compute_dtype)
             C = self.num_features
+            pool = self.fuse_pool
+            if (self.training and pool is not None and do_relu and residual is None
+                    and hip.bn_relu_maxpool_ok(xa, *pool._geom())):
+                # BatchNorm + ReLU + max-pool in one pass: the full-resolution output is never
+                # stored; the pool layer finds its cache filled and passes the result through
+                sums = hip.bn_stats(xa, getattr(x, "_bn_partial", None))
+                mean = torch.empty(C, dtype=torch.float32, device=xa.device)
+                istd = torch.empty_like(mean)
+                y, idx = hip.bn_relu_maxpool(xa, sums, xa.numel() // C, self._gamma(), self._beta(), self.epsilon,
+                                             pool._geom(), save=(mean, istd),
+                                             running=(self.running_mean, self.running_var), momentum=self.momentum)
+                pool._cache[mb_id] = (idx, tuple(xa.shape), y)
+                y._prepooled_by = pool
+                # backward: the pool's fused backward masks with the pooled value (y > 0) and
+                # hands this layer its statistics; there is no full-resolution ReLU output
+                self._cache[mb_id] = (xa, _POOLED, mean, istd, True)
+                return y
             if self.training:
                 sums = hip.bn_stats(xa, getattr(x, "_bn_partial", None))
                 count = xa.numel() // C
@@ -120,6 +141,11 @@ class BatchNorm(ParameterizedLayer):
             from ...ops import hip
             pre = getattr(grad, "_bnb", None)
             fused = pre[1:] if (pre is not None and pre[0] is self) else None
+            if yout is _POOLED:
+                if fused is None:
+                    raise RuntimeError(f"BatchNorm '{self.name}': forward fused the max-pool, so the backward "
+                                       "needs the fused max-pool backward statistics")
+                yout = None
             g = hip.to_act(grad, self.compute_dtype)
             dx, dmask = hip.bn_backward(g, x, yout, mean, istd, self._gamma(), dg, db,
                                         want_masked=self.emit_masked_grad, eval_mode=not was_training,
@@ -151,6 +177,8 @@ class BatchNorm(ParameterizedLayer):
         if not (was_training and x.is_cuda and x.dtype == torch.bfloat16 and x.is_contiguous(memory_format=torch.channels_last)):
             return None
         from ...ops.hip import BnbRequest
+        if yout is _POOLED:  # only the max-pool's fused backward can honour this request
+            return BnbRequest(self, None, x, mean, istd, pooled=True)
         return BnbRequest(self, yout, x, mean, istd)
 
     def pop_masked_grad(self, mb_id=0):

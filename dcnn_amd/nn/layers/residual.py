@@ -15,7 +15,7 @@ import torch
 from ..activations import ActivationFactory
 from .base import LayerConfig, Layer, run_backward
 from .conv import Conv2D
-from .misc import Activation
+from .misc import Activation, MaxPool2D
 from .norm import BatchNorm
 
 
@@ -26,6 +26,7 @@ def plan_fusion(layers: List[Layer], on_gpu: bool) -> None:
             l.emit_bn_stats = False
         if isinstance(l, BatchNorm):
             l.fuse_relu = False
+            l.fuse_pool = None
             l.emit_masked_grad = False
         if isinstance(l, Activation):
             l.passthrough = False
@@ -37,6 +38,11 @@ def plan_fusion(layers: List[Layer], on_gpu: bool) -> None:
         if isinstance(a, BatchNorm) and isinstance(b, Activation) and b.activation_name == "relu":
             a.fuse_relu = True
             b.passthrough = True
+    for a, b, c in zip(layers[:-2], layers[1:-1], layers[2:]):
+        # BatchNorm + ReLU + max-pool (ResNet stem): the pool is computed by the BatchNorm's
+        # forward when the shapes allow it at run time (BatchNorm.forward / MaxPool2D.forward)
+        if isinstance(a, BatchNorm) and a.fuse_relu and b.passthrough and isinstance(c, MaxPool2D):
+            a.fuse_pool = c
 
 
 class ResidualBlock(Layer):

@@ -251,10 +251,12 @@ class BnbRequest:
     that honours the request returns dy' = dy * (y > 0) with ``dy'._bnb = (bn, slab, rows, sums)``
     attached: per-tile (sum dy', sum dy' * xhat) rows and the zeroed [2][C] sums to reduce into.
     """
-    __slots__ = ("bn", "y", "x", "mean", "istd")
+    __slots__ = ("bn", "y", "x", "mean", "istd", "pooled")
 
-    def __init__(self, bn, y, x, mean, istd):
-        self.bn, self.y, self.x, self.mean, self.istd = bn, y, x, mean, istd
+    def __init__(self, bn, y, x, mean, istd, pooled=False):
+        # pooled: the BatchNorm's forward fused ReLU + max-pool (no full-resolution y; only the
+        # max-pool backward, masking with the pooled value, can honour the request)
+        self.bn, self.y, self.x, self.mean, self.istd, self.pooled = bn, y, x, mean, istd, pooled
 
     def args(self):
         return (ptr(self.y), self.x.data_ptr(), self.mean.data_ptr(), self.istd.data_ptr())
@@ -320,7 +322,7 @@ def conv2d_dgrad(dy, wt, x_shape, stride, pad, *, residual=None, bnb=None):
         dx = torch.empty((N, Ci, H, W), dtype=odt, device=dy.device, memory_format=CL)
     st = stream_ptr()
     g2 = K.gemm_g2f if f32 else K.gemm_g2
-    fuse = (bnb is not None and _BNB and not f32 and not empty_class and bnb.x.dtype == BF16
+    fuse = (bnb is not None and _BNB and not bnb.pooled and not f32 and not empty_class and bnb.x.dtype == BF16
             and tuple(bnb.x.shape) == (N, Ci, H, W))
     if not f32 and len(classes) == 1 and not empty_class and \
             _hconv_ok(N, H, W, OH, OW, sh, sw, Co, Ci, classes[0][4], wt):
@@ -526,6 +528,34 @@ def bn_apply(x, sums, count, gamma, beta, eps, *, residual=None, relu=False, sav
     return y
 
 
+def bn_relu_maxpool_ok(x, ph, pw, sh, sw, pdh, pdw):
+    """Can :func:`bn_relu_maxpool` take this BatchNorm+ReLU+max-pool? Its backward relies on the
+    fused max-pool backward (:func:`maxpool_bwd` with ``bnb``), so both must be available."""
+    if not (_BNB and _BNB_POOL) or x.dtype != BF16 or not x.is_contiguous(memory_format=CL):
+        return False
+    N, C, H, W = x.shape
+    OH, OW = pool_out_hw(H, W, ph, pw, sh, sw, pdh, pdw)
+    g = (N, H, W, C, OH, OW, ph, pw, sh, sw, pdh, pdw)
+    K = kernels()
+    return K.bn_relu_maxpool_supported(*g) and K.maxpool_bwd_bnb_supported(*g)
+
+
+def bn_relu_maxpool(x, sums, count, gamma, beta, eps, pool, *, save, running, momentum=0.1):
+    """Training BatchNorm (batch statistics ``sums``) + ReLU + max-pool ``pool`` = (ph, pw, sh, sw,
+    pdh, pdw) in one pass: returns the pooled output and the window argmax (max-pool layout)."""
+    N, C, H, W = x.shape
+    ph, pw, sh, sw, pdh, pdw = pool
+    OH, OW = pool_out_hw(H, W, ph, pw, sh, sw, pdh, pdw)
+    y = torch.empty((N, C, OH, OW), dtype=BF16, device=x.device, memory_format=CL)
+    idx = torch.empty((N, OH, OW, C), dtype=torch.uint8, device=x.device)
+    sm, si = save
+    rm, rv = running
+    kernels().bn_relu_maxpool(x.data_ptr(), y.data_ptr(), idx.data_ptr(), N, H, W, C, OH, OW, ph, pw, sh, sw, pdh, pdw,
+                              sums.data_ptr(), float(count), ptr(gamma), ptr(beta), float(eps), sm.data_ptr(),
+                              si.data_ptr(), ptr(rm), ptr(rv), float(momentum), stream_ptr())
+    return y, idx
+
+
 def bn_backward(dy, x, yout, mean, istd, gamma, dgamma, dbeta, *, want_masked=False, eval_mode=False, fused=None):
     """Returns (dx, masked_dy|None). yout given => ReLU was fused: dy' = dy * (yout > 0).
 
@@ -619,7 +649,7 @@ def maxpool_bwd(dy, idx, x_shape, ph, pw, sh, sw, pdh, pdw, *, ypool=None, bnb=N
     dx = torch.empty((N, C, H, W), dtype=dy.dtype, device=dy.device, memory_format=CL)
     g = (N, H, W, C, OH, OW, ph, pw, sh, sw, pdh, pdw)
     # the kernel masks with (pooled value > 0): only valid when a ReLU sits between BN and pool
-    if (bnb is not None and _BNB and _BNB_POOL and bnb.y is not None and ypool is not None and dy.dtype == BF16 and bnb.x.dtype == BF16
+    if (bnb is not None and _BNB and _BNB_POOL and (bnb.y is not None or bnb.pooled) and ypool is not None and dy.dtype == BF16 and bnb.x.dtype == BF16
             and tuple(bnb.x.shape) == (N, C, H, W) and bnb.x.is_contiguous(memory_format=CL)
             and K.maxpool_bwd_bnb_supported(*g)):
         rows = K.maxpool_bwd_bnb_rows(*g)

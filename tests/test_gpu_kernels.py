@@ -163,6 +163,31 @@ def test_stem_conv(hip, case):
         assert rel_err(gb, bf(dy).sum((0, 2, 3)) + 1) < 1e-2
 
 
+@pytest.mark.parametrize("C", [32, 64, 8])
+def test_bn_relu_maxpool(hip, C):
+    """Fused training BatchNorm + ReLU + 2x2 max-pool == bn_apply(relu) then maxpool_fwd, bit for
+    bit (pooled values, argmax, saved statistics, running statistics)."""
+    torch.manual_seed(5)
+    N, H, W = 4, 16, 12
+    x = (torch.randn(N, C, H, W) * 2 + 0.5).cuda().bfloat16().contiguous(memory_format=CL)
+    assert hip.bn_relu_maxpool_ok(x, 2, 2, 2, 2, 0, 0)
+    gamma, beta = torch.rand(C, device="cuda") + 0.5, torch.randn(C, device="cuda")
+    sums = hip.bn_stats(x, None)
+    cnt = x.numel() // C
+    m1, i1, m2, i2 = (torch.empty(C, device="cuda") for _ in range(4))
+    r1 = (torch.zeros(C, device="cuda"), torch.ones(C, device="cuda"))
+    r2 = (torch.zeros(C, device="cuda"), torch.ones(C, device="cuda"))
+    yfull = hip.bn_apply(x, sums, cnt, gamma, beta, 1e-3, relu=True, save=(m1, i1), running=r1, momentum=0.1)
+    y_ref, idx_ref = hip.maxpool_fwd(yfull, 2, 2, 2, 2, 0, 0)
+    y, idx = hip.bn_relu_maxpool(x, sums, cnt, gamma, beta, 1e-3, (2, 2, 2, 2, 0, 0), save=(m2, i2), running=r2,
+                                 momentum=0.1)
+    torch.cuda.synchronize()
+    assert torch.equal(y.cpu(), y_ref.cpu())
+    assert torch.equal(idx.cpu(), idx_ref.cpu())
+    for a, b in [(m1, m2), (i1, i2), (r1[0], r2[0]), (r1[1], r2[1])]:
+        assert torch.equal(a.cpu(), b.cpu())
+
+
 @pytest.mark.parametrize("shape", [(128, 512, 200), (64, 256, 10), (16, 192, 10), (256, 1024, 200)])
 def test_dense(hip, shape):
     N, In, Out = shape
