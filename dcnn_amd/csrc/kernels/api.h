@@ -95,6 +95,12 @@ void splitk_reduce(const float* slab, float* out, long n, int splits, int accumu
 void splitk_reduce2(const float* slab, float* out, long n, const float* bslab, float* bout, long nb, int splits,
                     int accumulate, hipStream_t s);
 
+// many split-K slab reductions in one launch (grad += sum over splits), kernel-argument table
+constexpr int kMaxRed = 48;
+struct RedEnt { const float* slab; float* out; long n; int splits, unit0, chunks, groups, vec, pad_; };
+struct MultiRed { int count; RedEnt e[kMaxRed]; };
+void multi_splitk_reduce(MultiRed t, hipStream_t s);
+
 int bn_partial_rows(long R, int C);
 void bn_partial(int dtype, const void* x, const void* dy, const void* yout, void* dy_out, const float* mean,
                 const float* istd, long R, int C, float* slab, int mode, float* zero_sums, hipStream_t s);

@@ -4,6 +4,7 @@
 // under hipGraph capture). No torch headers, no hipify: plain HIP + pybind11.
 #include <pybind11/pybind11.h>
 #include <pybind11/stl.h>
+#include <algorithm>
 #include <array>
 #include <vector>
 #include <hip/hip_runtime.h>
@@ -284,6 +285,20 @@ PYBIND11_MODULE(_kernels, m) {
   m.def("conv_weight_transpose", [](int dt, uintptr_t w, uintptr_t wt, int Co, int T_, int Ci, uintptr_t st) {
     conv_weight_transpose(dt, P<const void*>(w), P<bf16*>(wt), Co, T_, Ci, S(st));
   });
+  m.def("multi_splitk_reduce", [](std::vector<std::array<int64_t, 4>> ents, uintptr_t st) {
+    // entries: (slab ptr, out ptr, n, splits); launched in batches of kMaxRed
+    for (size_t b = 0; b < ents.size(); b += kMaxRed) {
+      MultiRed t{};
+      t.count = (int)std::min(ents.size() - b, (size_t)kMaxRed);
+      for (int k = 0; k < t.count; ++k) {
+        const auto& e = ents[b + k];
+        t.e[k].slab = P<const float*>((uintptr_t)e[0]); t.e[k].out = P<float*>((uintptr_t)e[1]);
+        t.e[k].n = e[2]; t.e[k].splits = (int)e[3];
+      }
+      multi_splitk_reduce(t, S(st));
+    }
+  });
+  m.def("multi_red_max", []() { return kMaxRed; });
   m.def("stem_supported", &stem_supported);
   m.def("stem_tiles", &stem_tiles_host);
   m.def("stem_wgrad_blocks", &stem_wgrad_blocks);

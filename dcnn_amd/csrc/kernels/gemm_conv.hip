@@ -549,6 +549,83 @@ __global__ void splitk_reduce_kernel(SplitkSeg a, SplitkSeg b, int gxa, int spli
     splitk_segment(b, blockIdx.x - gxa, gridDim.x - gxa, s0, s1, atomic);
 }
 
+// Deferred split-K reduction: the fp32 slabs of many weight gradients summed into their
+// gradients in ONE launch (api.h MultiRed). A work unit is (entry, chunk of 256 floats, group of
+// 32 splits); each wave of the unit sums 8 splits with all 8 loads in flight, the 4 waves meet
+// in LDS, and wave 0 adds into the gradient (atomically when the entry has several groups).
+__global__ void __launch_bounds__(256) multi_splitk_reduce_kernel(MultiRed t) {
+  int k = 0;
+  while (k + 1 < t.count && (int)blockIdx.x >= t.e[k + 1].unit0) ++k;
+  const float* slab = t.e[k].slab;
+  float* out = t.e[k].out;
+  const long n = t.e[k].n;
+  const int splits = t.e[k].splits, chunks = t.e[k].chunks, groups = t.e[k].groups, vec = t.e[k].vec;
+  const int local = blockIdx.x - t.e[k].unit0, chunk = local % chunks, grp = local / chunks;
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int s0 = grp * 32 + w * 8;
+  __shared__ float4 red[3][64];
+  float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
+  if (vec) {  // n % 4 == 0: lane owns 4 consecutive floats
+    const long i4 = (long)chunk * 64 + lane;
+    const bool ok = i4 * 4 < n;
+    float4 v[8];
+#pragma unroll
+    for (int u = 0; u < 8; ++u)
+      v[u] = (ok && s0 + u < splits) ? reinterpret_cast<const float4*>(slab + (long)(s0 + u) * n)[i4]
+                                     : make_float4(0.f, 0.f, 0.f, 0.f);
+#pragma unroll
+    for (int u = 0; u < 8; ++u) { acc.x += v[u].x; acc.y += v[u].y; acc.z += v[u].z; acc.w += v[u].w; }
+  } else {  // one float per lane
+    const long i = (long)chunk * 64 + lane;
+    const bool ok = i < n;
+    float v[8];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) v[u] = (ok && s0 + u < splits) ? slab[(long)(s0 + u) * n + i] : 0.f;
+#pragma unroll
+    for (int u = 0; u < 8; ++u) acc.x += v[u];
+  }
+  if (w > 0) red[w - 1][lane] = acc;
+  __syncthreads();
+  if (w > 0) return;
+#pragma unroll
+  for (int j = 0; j < 3; ++j) {
+    acc.x += red[j][lane].x; acc.y += red[j][lane].y; acc.z += red[j][lane].z; acc.w += red[j][lane].w;
+  }
+  if (vec) {
+    const long i4 = (long)chunk * 64 + lane;
+    if (i4 * 4 >= n) return;
+    float* o = out + i4 * 4;
+    if (groups > 1) {
+      atomicAdd(o + 0, acc.x); atomicAdd(o + 1, acc.y); atomicAdd(o + 2, acc.z); atomicAdd(o + 3, acc.w);
+    } else {
+      float4 c = reinterpret_cast<float4*>(out)[i4];
+      c.x += acc.x; c.y += acc.y; c.z += acc.z; c.w += acc.w;
+      reinterpret_cast<float4*>(out)[i4] = c;
+    }
+  } else {
+    const long i = (long)chunk * 64 + lane;
+    if (i >= n) return;
+    if (groups > 1) atomicAdd(out + i, acc.x); else out[i] += acc.x;
+  }
+}
+
+void multi_splitk_reduce(MultiRed t, hipStream_t s) {
+  if (t.count <= 0) return;
+  if (t.count > kMaxRed) throw std::runtime_error("multi_splitk_reduce: too many entries");
+  int units = 0;
+  for (int k = 0; k < t.count; ++k) {
+    RedEnt& e = t.e[k];
+    e.vec = (e.n % 4 == 0 && ((uintptr_t)e.slab % 16) == 0 && ((uintptr_t)e.out % 16) == 0) ? 1 : 0;
+    const long per = e.vec ? 256 : 64;
+    e.chunks = (int)((e.n + per - 1) / per);
+    e.groups = (e.splits + 31) / 32;
+    e.unit0 = units;
+    units += e.chunks * e.groups;
+  }
+  hipLaunchKernelGGL(multi_splitk_reduce_kernel, dim3(units), dim3(256), 0, s, t);
+  DCNN_LAUNCH_CHECK();
+}
+
 // ----------------------------------------------------------------------------------------
 // launchers
 // ----------------------------------------------------------------------------------------

@@ -221,13 +221,27 @@ class Sequential:
                 self._transposer = WeightTransposer(convs)
 
     def prepare_backward(self) -> None:
-        """Per-step setup of the backward pass: all dgrad weight operands in one launch."""
+        """Per-step setup of the backward pass: all dgrad weight operands in one launch, and the
+        split-K weight-gradient reductions queued for one batched launch (ops.hip.grad_reducer)."""
         if getattr(self, "_transposer", None) is not None:
             self._transposer.run()
+        if self.device.is_gpu():
+            from ..ops.hip import grad_reducer
+            grad_reducer.begin()
+
+    def flush_gradients(self) -> None:
+        """Complete every queued weight-gradient reduction (before a gradient is consumed
+        mid-backward, e.g. a data-parallel bucket all-reduce)."""
+        if self.device.is_gpu():
+            from ..ops.hip import grad_reducer
+            grad_reducer.flush()
 
     def finish_backward(self) -> None:
         if getattr(self, "_transposer", None) is not None:
             self._transposer.invalidate()
+        if self.device.is_gpu():
+            from ..ops.hip import grad_reducer
+            grad_reducer.end()
 
     def set_first_layer_input_grad(self, need: bool) -> None:
         """Skip the (unused) input gradient of the first layer (reference G9 wasted it)."""

@@ -355,8 +355,53 @@ def conv2d_dgrad(dy, wt, x_shape, stride, pad, *, residual=None, bnb=None):
     return dx
 
 
+class _DeferredReduce:
+    """Split-K weight-gradient reductions queued during a model backward and launched together
+    (``multi_splitk_reduce``: one kernel for the whole queue instead of one per layer, ~26 for
+    ResNet-18). The slabs stay referenced until the flush; with 288 GB of HBM per GPU holding
+    every layer's slab for one backward (< 2 GB for ResNet-18 at batch 256) is the cheap side of
+    the trade. Active between ``begin()`` / ``end()`` (Sequential.prepare_backward /
+    finish_backward); gradient consumers inside that window (the data-parallel bucket
+    all-reduce) call ``flush()`` first. Outside it every reduction runs immediately."""
+
+    def __init__(self):
+        self.active = False
+        self.pending = []  # (slab, out, n, splits) — tensors kept alive until the launch
+
+    def begin(self):
+        self.active = _DEFER_REDUCE
+
+    def add(self, slab, out, n, splits):
+        self.pending.append((slab, out, int(n), int(splits)))
+
+    def flush(self):
+        if self.pending:
+            kernels().multi_splitk_reduce([(t[0].data_ptr(), t[1].data_ptr(), t[2], t[3]) for t in self.pending],
+                                          stream_ptr())
+            self.pending.clear()
+
+    def end(self):
+        self.flush()
+        self.active = False
+
+
+_DEFER_REDUCE = os.environ.get("DCNN_DEFER_REDUCE", "1") != "0"
+grad_reducer = _DeferredReduce()
+
+
+def _dense(t):
+    """A gradient tensor whose storage is exactly its numel() elements (any dim order)."""
+    return t.is_contiguous() or t.is_contiguous(memory_format=CL)
+
+
 def _reduce_wb(K, slab, grad_w, n, bslab, grad_b, nb, splits, st):
-    """grad_w += sum over splits of slab, grad_b += sum of bslab — one launch for both."""
+    """grad_w += sum over splits of slab, grad_b += sum of bslab — one launch for both (or
+    queued on :data:`grad_reducer` inside a model backward)."""
+    if grad_reducer.active and _dense(grad_w) and (grad_b is None or grad_b.is_contiguous()):
+        grad_reducer.add(slab, grad_w, n, splits)
+        if grad_b is not None:
+            grad_reducer.add(bslab, grad_b, nb, splits)
+        return
     if grad_b is None:
         K.splitk_reduce(slab.data_ptr(), grad_w.data_ptr(), n, splits, 1, st)
     else:
@@ -408,11 +453,11 @@ def conv2d_wgrad(dy, x, w_shape, stride, pad, grad_w, grad_b=None):
         K.gemm_t2(dy.data_ptr(), x.data_ptr(), slab.data_ptr(), ptr(bslab), _nbytes(dy), _nbytes(x), Co, Ng, P, Co, Cx,
                   H, W, OH, OW, stride[0], stride[1], taps, splits, st)
         if Cx == Ci:
-            K.splitk_reduce(slab.data_ptr(), grad_w.data_ptr(), Co * Ng, splits, 1, st)
-        else:
-            tmp = torch.empty((Co, KH, KW, Cx), dtype=F32, device=x.device)
-            K.splitk_reduce(slab.data_ptr(), tmp.data_ptr(), Co * Ng, splits, 0, st)
-            grad_w.add_(tmp[..., :Ci].permute(0, 3, 1, 2))
+            _reduce_wb(K, slab, grad_w, Co * Ng, bslab, grad_b, Co, splits, st)
+            return
+        tmp = torch.empty((Co, KH, KW, Cx), dtype=F32, device=x.device)
+        K.splitk_reduce(slab.data_ptr(), tmp.data_ptr(), Co * Ng, splits, 0, st)
+        grad_w.add_(tmp[..., :Ci].permute(0, 3, 1, 2))
         if grad_b is not None:
             K.splitk_reduce(bslab.data_ptr(), grad_b.data_ptr(), Co, splits, 1, st)
         return

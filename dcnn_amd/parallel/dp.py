@@ -127,6 +127,7 @@ class DataParallel:
             m._prof_end(m.layers[i].name or m.layers[i].type(), t0, m.backward_times_us)
             if self.world > 1 and i in self.fire:
                 lo, hi = self.fire[i]
+                m.flush_gradients()  # queued split-K reductions of this bucket's layers
                 self._works.append(dist.all_reduce(flat[lo:hi], op=dist.ReduceOp.SUM, group=self.pg, async_op=True))
         m.finish_backward()
         if sync:

@@ -100,6 +100,7 @@ class TrainStep:
                 else:
                     cur = self._carry
                 cur = self._run_bwd(cur, hi, lo)
+                self.model.flush_gradients()  # the bucket all-reduced after this segment is complete
                 self._carry = cur
                 if k == len(segs) - 1:
                     self.model.finish_backward()

@@ -163,6 +163,51 @@ def test_stem_conv(hip, case):
         assert rel_err(gb, bf(dy).sum((0, 2, 3)) + 1) < 1e-2
 
 
+def test_multi_splitk_reduce(hip):
+    """Batched split-K reduction (grad += sum over splits) over entries of every kind: float4 and
+    scalar rows, 1 / several / > 32 splits (atomic groups), more entries than one launch holds."""
+    from dcnn_amd.ops._ext import kernels
+    torch.manual_seed(3)
+    K = kernels()
+    shapes = [(1, 64), (5, 1000), (40, 36864), (100, 12), (33, 4608), (7, 3)] * 9  # 54 > one launch
+    slabs = [torch.randn(s, n, device="cuda") for s, n in shapes]
+    outs = [torch.randn(n, device="cuda") for _, n in shapes]
+    refs = [o.cpu() + sl.cpu().sum(0) for o, sl in zip(outs, slabs)]
+    K.multi_splitk_reduce([(sl.data_ptr(), o.data_ptr(), o.numel(), sl.shape[0]) for sl, o in zip(slabs, outs)],
+                          hip.stream_ptr())
+    torch.cuda.synchronize()
+    for o, r in zip(outs, refs):
+        assert rel_err(o, r) < 1e-5
+
+
+def test_deferred_reduce_in_model_backward(hip):
+    """Inside a model backward the wgrad reductions are queued and flushed by finish_backward:
+    gradients read afterwards equal the per-layer immediate reduction (same model, same batch,
+    conv layers run one by one outside any backward window)."""
+    from dcnn_amd.models import create_model
+    torch.manual_seed(8)
+    m = create_model("mnist_cnn")
+    m.set_seed(2)
+    m.set_device("GPU:0")
+    m.initialize()
+    x = torch.randn(8, 1, 28, 28, device="cuda")
+    out = m.forward(x, return_on_input_device=False)
+    g = torch.randn_like(out.float())
+    m.backward(g)
+    assert not hip.grad_reducer.pending and not hip.grad_reducer.active
+    deferred = [t.float().cpu().clone() for t in m.gradients()]
+    m.clear_gradients()
+    prev = hip._DEFER_REDUCE
+    hip._DEFER_REDUCE = False
+    try:
+        m.forward(x, return_on_input_device=False)
+        m.backward(g)
+    finally:
+        hip._DEFER_REDUCE = prev
+    for a, b in zip(deferred, m.gradients()):
+        assert rel_err(b, a) < 2e-2, rel_err(b, a)
+
+
 @pytest.mark.parametrize("C", [32, 64, 8])
 def test_bn_relu_maxpool(hip, C):
     """Fused training BatchNorm + ReLU + 2x2 max-pool == bn_apply(relu) then maxpool_fwd, bit for
