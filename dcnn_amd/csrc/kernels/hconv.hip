@@ -203,23 +203,27 @@ __global__ void __launch_bounds__(256, 1) hconv_kernel(HConvArgs p) {
       if (TPS > 1 && t >= p.ntaps) break;
       const char* Bs = smem + NHB * T_rt.HALO + bcur * T::BST + u * T::BTAP;
       const int toff = p.tap_dy[t] * HW2 + p.tap_dx[t];
+      // both k-halves' fragments are read up front: the second half's LDS latency hides behind
+      // the first half's MFMAs instead of sitting between them
+      bf16x8 a[2][T::TM], b[2][T::TN];
 #pragma unroll
       for (int kk = 0; kk < 2; ++kk) {
         const int ch = kk * 4 + (lane >> 4);
-        bf16x8 a[T::TM], b[T::TN];
 #pragma unroll
-        for (int i = 0; i < T::TM; ++i) a[i] = *reinterpret_cast<const bf16x8*>(Hs + hoff(arow0[i] + toff, ch));
+        for (int i = 0; i < T::TM; ++i) a[kk][i] = *reinterpret_cast<const bf16x8*>(Hs + hoff(arow0[i] + toff, ch));
 #pragma unroll
         for (int j = 0; j < T::TN; ++j)
-          b[j] = *reinterpret_cast<const bf16x8*>(Bs + hoff(wn * (BN / 2) + j * 16 + (lane & 15), ch));
-        __builtin_amdgcn_s_setprio(1);
+          b[kk][j] = *reinterpret_cast<const bf16x8*>(Bs + hoff(wn * (BN / 2) + j * 16 + (lane & 15), ch));
+      }
+      __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+      for (int kk = 0; kk < 2; ++kk)
 #pragma unroll
         for (int i = 0; i < T::TM; ++i)
 #pragma unroll
           for (int j = 0; j < T::TN; ++j)
-            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[i], b[j], acc[i][j], 0, 0, 0);
-        __builtin_amdgcn_s_setprio(0);
-      }
+            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[kk][i], b[kk][j], acc[i][j], 0, 0, 0);
+      __builtin_amdgcn_s_setprio(0);
     }
     // step k + 1's weights (and halo) landed for this lane, then for the whole workgroup
     vm_wait_groups<BU>(min(NBS - 2, nsteps - 2 - k));

@@ -84,6 +84,23 @@ def test_conv_fwd_dgrad_wgrad(hip, case):
     assert rel_err(gb, dyb.sum((0, 2, 3)) + 1) < 1e-2
 
 
+def test_hconv_layer4_shape(hip):
+    """Full ResNet layer-4 shape (4x4 maps, 512 channels, batch 256: 512 workgroups, 72 K steps
+    each through the weight ring) of the halo conv, forward and dgrad, vs the fp32 reference."""
+    N, C, H, W = 256, 512, 4, 4
+    torch.manual_seed(4)
+    x = torch.randn(N, C, H, W)
+    w = torch.randn(C, C, 3, 3) / math.sqrt(C * 9)
+    xg = x.cuda().to(torch.bfloat16).contiguous(memory_format=CL)
+    wg = w.cuda().to(torch.bfloat16).contiguous(memory_format=CL)
+    y, _ = hip.conv2d_fwd(xg, wg, None, (1, 1), (1, 1))
+    assert rel_err(y, F.conv2d(bf(x), bf(w), None, 1, 1)) < 1e-2
+    dy = torch.randn(N, C, H, W)
+    dx = hip.conv2d_dgrad(dy.cuda().to(torch.bfloat16).contiguous(memory_format=CL), hip.conv_weight_t(wg), x.shape,
+                          (1, 1), (1, 1))
+    assert rel_err(dx, torch.nn.grad.conv2d_input(x.shape, bf(w), bf(dy), 1, 1)) < 1e-2
+
+
 @pytest.mark.parametrize("case", [
     # N, Ci, H, W, Co: halo-tiled wgrad geometries (TW=16 / 8 / 4, several images per tile)
     (4, 64, 32, 32, 64), (6, 128, 16, 16, 64), (4, 64, 16, 16, 192), (8, 256, 8, 8, 128), (16, 128, 4, 4, 256),
