@@ -10,6 +10,7 @@ training step can be captured into a hipGraph.
 from __future__ import annotations
 
 import os
+import threading
 
 import torch
 
@@ -386,7 +387,24 @@ class _DeferredReduce:
 
 
 _DEFER_REDUCE = os.environ.get("DCNN_DEFER_REDUCE", "1") != "0"
-grad_reducer = _DeferredReduce()
+_tls = threading.local()
+
+
+class _ThreadReducer:
+    """``grad_reducer``: the calling thread's :class:`_DeferredReduce` (a pipeline stage's
+    backward on its own thread and stream must not flush another stage's queue)."""
+
+    def _get(self):
+        r = getattr(_tls, "reducer", None)
+        if r is None:
+            r = _tls.reducer = _DeferredReduce()
+        return r
+
+    def __getattr__(self, k):
+        return getattr(self._get(), k)
+
+
+grad_reducer = _ThreadReducer()
 
 
 def _dense(t):
