@@ -71,6 +71,100 @@ struct HC {
   }
 };
 
+// Shared epilogue of the halo convs: acc (+bias) -> bf16 tile staged in LDS `smem` (>= BM x
+// EPI_PITCH bytes) -> NHWC rows (+residual, ReLU, backward-BN mask) and the tile's BatchNorm
+// statistics row `tm`. Contains block barriers: every thread of the workgroup must call it.
+template <int BM, int BN>
+__device__ __forceinline__ void hc_epilogue(const HConvArgs& p, f32x4 (&acc)[BM / 32][BN / 32], char* smem, int n0,
+                                            int tm, int img0, int y0, int x0) {
+  using T = HC<BM, BN, 1, 1, 2>;
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int wm = wid >> 1, wn = wid & 1;
+  // ---- epilogue 1: acc (+bias) -> bf16 LDS tile [BM][BN] ----
+#pragma unroll
+  for (int j = 0; j < T::TN; ++j) {
+    const int col = wn * (BN / 2) + j * 16 + (lane & 15);
+    const float bv = p.bias ? p.bias[n0 + col] : 0.f;
+#pragma unroll
+    for (int i = 0; i < T::TM; ++i)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int row = wm * (BM / 2) + i * 16 + (lane >> 4) * 4 + r;
+        *reinterpret_cast<bf16*>(smem + row * T::EPI_PITCH + col * 2) = (bf16)(acc[i][j][r] + bv);
+      }
+  }
+  __syncthreads();
+  // ---- epilogue 2: 16-byte rows -> NHWC global (+residual, ReLU, BN partial stats) ----
+  constexpr int CG = BN / 8;
+  constexpr int RSTEP = 256 / CG;
+  const int cg = tid % CG, r0 = tid / CG;
+  const int ncol = n0 + cg * 8;
+  float s[8], q[8], mu[8], is[8];
+#pragma unroll
+  for (int v = 0; v < 8; ++v) s[v] = q[v] = mu[v] = is[v] = 0.f;
+  const bool bnb = p.bnb.x != nullptr;  // backward-BN fusion (api.h BnbArgs)
+  if (bnb && true) {
+#pragma unroll
+    for (int v = 0; v < 8; ++v) { mu[v] = p.bnb.mean[ncol + v]; is[v] = p.bnb.istd[ncol + v]; }
+  }
+  const int tpx = p.TH * p.TW;
+  for (int row = r0; row < BM; row += RSTEP) {
+    const int im = row / tpx, r2 = row - im * tpx;
+    const int n = img0 + im;
+    if (n >= p.NB) continue;
+    const long orow = ((long)n * p.H + y0 + r2 / p.TW) * p.W + x0 + r2 % p.TW;
+    float f[8];
+    unpack8(*reinterpret_cast<const uint4*>(smem + row * T::EPI_PITCH + cg * 16), f);
+    if (p.residual) {
+      float rr[8];
+      unpack8(*reinterpret_cast<const uint4*>(p.residual + orow * p.N + ncol), rr);
+#pragma unroll
+      for (int v = 0; v < 8; ++v) f[v] += rr[v];
+    }
+    if (p.relu) {
+#pragma unroll
+      for (int v = 0; v < 8; ++v) f[v] = fmaxf(f[v], 0.f);
+    }
+    if (bnb && p.bnb.y) {
+      float yo[8];
+      unpack8(*reinterpret_cast<const uint4*>(p.bnb.y + orow * p.N + ncol), yo);
+#pragma unroll
+      for (int v = 0; v < 8; ++v) f[v] = yo[v] > 0.f ? f[v] : 0.f;
+    }
+    const uint4 o = pack8(f);
+    *reinterpret_cast<uint4*>(p.C + orow * p.N + ncol) = o;
+    if (p.stats) {
+      float g[8];
+      unpack8(o, g);
+      if (bnb) {
+        float xv[8];
+        unpack8(*reinterpret_cast<const uint4*>(p.bnb.x + orow * p.N + ncol), xv);
+#pragma unroll
+        for (int v = 0; v < 8; ++v) { s[v] += g[v]; q[v] += g[v] * (xv[v] - mu[v]) * is[v]; }
+      } else {
+#pragma unroll
+        for (int v = 0; v < 8; ++v) { s[v] += g[v]; q[v] += g[v] * g[v]; }
+      }
+    }
+  }
+  if (p.stats) {
+    __syncthreads();
+    float* red = reinterpret_cast<float*>(smem);  // [RSTEP][2][BN]
+#pragma unroll
+    for (int v = 0; v < 8; ++v) {
+      red[(r0 * 2 + 0) * BN + cg * 8 + v] = s[v];
+      red[(r0 * 2 + 1) * BN + cg * 8 + v] = q[v];
+    }
+    __syncthreads();
+    for (int cc = tid; cc < 2 * BN; cc += 256) {
+      const int which = cc / BN, c2 = cc % BN;
+      float a = 0.f;
+      for (int k = 0; k < RSTEP; ++k) a += red[(k * 2 + which) * BN + c2];
+      p.stats[((long)tm * 2 + which) * p.N + n0 + c2] = a;
+    }
+  }
+}
+
 template <int BM, int BN, int TPS, int NHB, int NBS>
 __global__ void __launch_bounds__(256, 1) hconv_kernel(HConvArgs p) {
   using T = HC<BM, BN, TPS, NHB, NBS>;
@@ -231,89 +325,7 @@ __global__ void __launch_bounds__(256, 1) hconv_kernel(HConvArgs p) {
     bcur = bcur == NBS - 1 ? 0 : bcur + 1;
   }
 
-  // ---- epilogue 1: acc (+bias) -> bf16 LDS tile [BM][BN] ----
-#pragma unroll
-  for (int j = 0; j < T::TN; ++j) {
-    const int col = wn * (BN / 2) + j * 16 + (lane & 15);
-    const float bv = p.bias ? p.bias[n0 + col] : 0.f;
-#pragma unroll
-    for (int i = 0; i < T::TM; ++i)
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const int row = wm * (BM / 2) + i * 16 + (lane >> 4) * 4 + r;
-        *reinterpret_cast<bf16*>(smem + row * T::EPI_PITCH + col * 2) = (bf16)(acc[i][j][r] + bv);
-      }
-  }
-  __syncthreads();
-  // ---- epilogue 2: 16-byte rows -> NHWC global (+residual, ReLU, BN partial stats) ----
-  constexpr int CG = BN / 8;
-  constexpr int RSTEP = 256 / CG;
-  const int cg = tid % CG, r0 = tid / CG;
-  const int ncol = n0 + cg * 8;
-  float s[8], q[8], mu[8], is[8];
-#pragma unroll
-  for (int v = 0; v < 8; ++v) s[v] = q[v] = mu[v] = is[v] = 0.f;
-  const bool bnb = p.bnb.x != nullptr;  // backward-BN fusion (api.h BnbArgs)
-  if (bnb && true) {
-#pragma unroll
-    for (int v = 0; v < 8; ++v) { mu[v] = p.bnb.mean[ncol + v]; is[v] = p.bnb.istd[ncol + v]; }
-  }
-  const int tpx = p.TH * p.TW;
-  for (int row = r0; row < BM; row += RSTEP) {
-    const int im = row / tpx, r2 = row - im * tpx;
-    const int n = img0 + im;
-    if (n >= p.NB) continue;
-    const long orow = ((long)n * p.H + y0 + r2 / p.TW) * p.W + x0 + r2 % p.TW;
-    float f[8];
-    unpack8(*reinterpret_cast<const uint4*>(smem + row * T::EPI_PITCH + cg * 16), f);
-    if (p.residual) {
-      float rr[8];
-      unpack8(*reinterpret_cast<const uint4*>(p.residual + orow * p.N + ncol), rr);
-#pragma unroll
-      for (int v = 0; v < 8; ++v) f[v] += rr[v];
-    }
-    if (p.relu) {
-#pragma unroll
-      for (int v = 0; v < 8; ++v) f[v] = fmaxf(f[v], 0.f);
-    }
-    if (bnb && p.bnb.y) {
-      float yo[8];
-      unpack8(*reinterpret_cast<const uint4*>(p.bnb.y + orow * p.N + ncol), yo);
-#pragma unroll
-      for (int v = 0; v < 8; ++v) f[v] = yo[v] > 0.f ? f[v] : 0.f;
-    }
-    const uint4 o = pack8(f);
-    *reinterpret_cast<uint4*>(p.C + orow * p.N + ncol) = o;
-    if (p.stats) {
-      float g[8];
-      unpack8(o, g);
-      if (bnb) {
-        float xv[8];
-        unpack8(*reinterpret_cast<const uint4*>(p.bnb.x + orow * p.N + ncol), xv);
-#pragma unroll
-        for (int v = 0; v < 8; ++v) { s[v] += g[v]; q[v] += g[v] * (xv[v] - mu[v]) * is[v]; }
-      } else {
-#pragma unroll
-        for (int v = 0; v < 8; ++v) { s[v] += g[v]; q[v] += g[v] * g[v]; }
-      }
-    }
-  }
-  if (p.stats) {
-    __syncthreads();
-    float* red = reinterpret_cast<float*>(smem);  // [RSTEP][2][BN]
-#pragma unroll
-    for (int v = 0; v < 8; ++v) {
-      red[(r0 * 2 + 0) * BN + cg * 8 + v] = s[v];
-      red[(r0 * 2 + 1) * BN + cg * 8 + v] = q[v];
-    }
-    __syncthreads();
-    for (int cc = tid; cc < 2 * BN; cc += 256) {
-      const int which = cc / BN, c2 = cc % BN;
-      float a = 0.f;
-      for (int k = 0; k < RSTEP; ++k) a += red[(k * 2 + which) * BN + c2];
-      p.stats[((long)tm * 2 + which) * p.N + n0 + c2] = a;
-    }
-  }
+  hc_epilogue<BM, BN>(p, acc, smem, n0, tm, img0, y0, x0);
 }
 
 // ---------------------------------------------------------------------------------------------
