@@ -106,9 +106,10 @@ def main():
         model.print_profiling_summary()
     if rank == 0:
         print(json.dumps({
-            "metric": METRIC, "value": round(imgs, 2), "unit": "images/sec", "n_gpus": world, "steps": a.steps,
+            "metric": METRIC if a.model == "resnet18_tiny_imagenet" else f"images/sec (whole node) {a.model} training",
+            "value": round(imgs, 2), "unit": "images/sec", "n_gpus": world, "steps": a.steps,
             "warmup": a.warmup, "ms_per_step": round(ms, 4), "higher_is_better": True, "scaling": "weak",
-            "vs_baseline": None, "dtype": a.dtype if dev.type == "cuda" else "fp32", "data": "synthetic (random 64x64 RGB + random labels, random init)",
+            "vs_baseline": None, "dtype": a.dtype if dev.type == "cuda" else "fp32", "data": f"synthetic (random {H}x{W}x{C} inputs + random labels, random init)",
             "config": {"model": a.model, "global_batch": a.batch * world, "per_gpu_batch": a.batch, "seq_len": None,
                        "image_size": [C, H, W], "parallelism": f"dp{world}", "optimizer": "adam",
                        "hipgraph": bool(step.use_graph), "final_loss": round(loss_val, 4)},
