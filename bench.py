@@ -38,6 +38,8 @@ def main():
     ap.add_argument("--graph", type=int, default=int(os.environ.get("DCNN_BENCH_GRAPH", "1")),
                     help="capture the per-step compute in a hipGraph (1) or run eagerly (0)")
     ap.add_argument("--bucket-mb", type=float, default=4.0)
+    ap.add_argument("--pg", action="store_true",
+                    help="create the RCCL process group even at world size 1 (segmented DP step on one GPU)")
     ap.add_argument("--profile", action="store_true", help="print per-layer device times")
     ap.add_argument("--device", default="cuda")
     ap.add_argument("--dtype", default="bf16", choices=["bf16", "fp32"],
@@ -50,6 +52,14 @@ def main():
     from dcnn_amd.runtime.step import TrainStep
 
     rank, world, local = init_distributed("nccl" if a.device == "cuda" else "gloo")
+    if a.pg and not dist.is_initialized():
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        os.environ.setdefault("MASTER_PORT", "29533")
+        if a.device == "cuda":
+            torch.cuda.set_device(0)
+            dist.init_process_group("nccl", rank=0, world_size=1, device_id=torch.device("cuda", 0))
+        else:
+            dist.init_process_group("gloo", rank=0, world_size=1)
     if a.gpus != world and world > 1:
         raise SystemExit(f"--gpus {a.gpus} but WORLD_SIZE={world}")
     dev = torch.device("cuda", local) if a.device == "cuda" else torch.device("cpu")
@@ -114,7 +124,7 @@ def main():
                        "image_size": [C, H, W], "parallelism": f"dp{world}", "optimizer": "adam",
                        "hipgraph": bool(step.use_graph), "final_loss": round(loss_val, 4)},
         }), flush=True)
-    if world > 1:
+    if dist.is_initialized():
         dist.barrier()
         dist.destroy_process_group()
 

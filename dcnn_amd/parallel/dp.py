@@ -49,6 +49,10 @@ class DataParallel:
         self.pg = process_group
         self.world = dist.get_world_size(process_group) if dist.is_initialized() else 1
         self.rank = dist.get_rank(process_group) if dist.is_initialized() else 0
+        # bucketed all-reduce runs whenever a process group exists (also at world size 1, which
+        # exercises the RCCL + segmented-graph path on a single GPU); plain single-process
+        # training has no group and skips it
+        self.active = dist.is_initialized()
         self.bucket_bytes = int(bucket_mb * 2**20)
         self._works: List = []
         self._build_buckets()
@@ -125,7 +129,7 @@ class DataParallel:
             t0 = m._prof_begin()
             cur = run_backward(m.layers, i, cur, mb_id)
             m._prof_end(m.layers[i].name or m.layers[i].type(), t0, m.backward_times_us)
-            if self.world > 1 and i in self.fire:
+            if self.active and i in self.fire:
                 lo, hi = self.fire[i]
                 m.flush_gradients()  # queued split-K reductions of this bucket's layers
                 self._works.append(dist.all_reduce(flat[lo:hi], op=dist.ReduceOp.SUM, group=self.pg, async_op=True))

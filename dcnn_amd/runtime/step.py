@@ -48,7 +48,7 @@ class TrainStep:
     def _segments(self):
         """Backward layer ranges [hi..lo] ending at each bucket fire point (descending)."""
         L = len(self.model.layers)
-        fires = sorted(self.dp.fire.keys(), reverse=True) if self.dp.world > 1 else []
+        fires = sorted(self.dp.fire.keys(), reverse=True) if self.dp.active else []
         segs = []
         hi = L - 1
         for f in fires:
@@ -65,9 +65,24 @@ class TrainStep:
             cur = run_backward(layers, i, cur, 0)
         return cur
 
+    def _training_state(self):
+        """Tensors a step mutates: fp32 master weights, optimizer moments, BN running stats."""
+        from ..parallel.dp import _bn_buffers
+        ts = [self.model.arena.data]
+        for name in ("m", "v", "velocity"):
+            ts += list(getattr(self.opt, name, None) or [])
+        for l in self.model.layers:
+            ts += _bn_buffers(l)
+        return ts
+
     def _capture(self, x, y):
         self._static_x = x.clone()
         self._static_y = y.clone()
+        # the warm-up steps below must not train: snapshot the state and restore it afterwards,
+        # so the first replay is the first update (as in eager mode)
+        state = self._training_state()
+        saved = [t.detach().clone() for t in state]
+        saved_t = getattr(self.opt, "t", None)
         # warm up on a side stream (allocator pools, lazy init) as torch.cuda.graph requires
         s = torch.cuda.Stream()
         s.wait_stream(torch.cuda.current_stream())
@@ -75,6 +90,14 @@ class TrainStep:
             for _ in range(2):
                 self.eager(self._static_x, self._static_y)
         torch.cuda.current_stream().wait_stream(s)
+        torch.cuda.synchronize()
+        with torch.no_grad():
+            for t, c in zip(state, saved):
+                t.copy_(c)
+        del saved
+        if saved_t is not None:
+            self.opt.t = saved_t
+        self.model.arena.sync_shadow(force=True)
         torch.cuda.synchronize()
         segs, fires = self._segments()
         self._segs, self._fires = segs, fires
@@ -87,6 +110,7 @@ class TrainStep:
         if hasattr(self.opt, "t"):
             self.opt.t -= 1  # the capture itself is not a training step
         world = self.dp.world
+        active = self.dp.active
         for k, (hi, lo) in enumerate(segs):
             g = torch.cuda.CUDAGraph()
             with torch.cuda.graph(g, pool=pool):
@@ -104,12 +128,12 @@ class TrainStep:
                 self._carry = cur
                 if k == len(segs) - 1:
                     self.model.finish_backward()
-                if world == 1 and k == len(segs) - 1:
+                if not active and k == len(segs) - 1:
                     self.opt.launch_step()
             if pool is None:
                 pool = g.pool()
             self.graphs.append(g)
-        if world > 1:
+        if active:
             g = torch.cuda.CUDAGraph()
             with torch.cuda.graph(g, pool=pool):
                 self.opt.launch_step()
@@ -120,15 +144,15 @@ class TrainStep:
         self._static_x.copy_(x, non_blocking=True)
         self._static_y.copy_(y, non_blocking=True)
         self.opt.prepare_step()
-        world = self.dp.world
+        active = self.dp.active
         flat = self.model.arena.grad
         works = []
         for k, (hi, lo) in enumerate(self._segs):
             self.graphs[k].replay()
-            if world > 1 and k < len(self._fires):
+            if active and k < len(self._fires):
                 a, b = self.dp.fire[self._fires[k]]
                 works.append(dist.all_reduce(flat[a:b], op=dist.ReduceOp.SUM, group=self.dp.pg, async_op=True))
-        if world > 1:
+        if active:
             for w in works:
                 w.wait()
             self.graphs[-1].replay()
