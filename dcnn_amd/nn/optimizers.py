@@ -93,15 +93,32 @@ class Optimizer:
     def get_learning_rate(self) -> float:
         return self.learning_rate
 
+    _HYPER_SLOTS = 8
+
     def _device_hyper(self, vals):
-        """Device copy of step scalars (read by the kernel; graph-replay safe)."""
+        """Device copy of step scalars (read by the kernel; graph-replay safe).
+
+        Uploaded from a ring of pinned host slots with an asynchronous copy: a pageable copy
+        would be staged synchronously and stall the host until the stream drains, so the next
+        step's graph launches could not run ahead of the GPU. A slot is rewritten only after the
+        event of its previous copy has completed (eight steps earlier, in practice never waits).
+        """
         dev = self._flat_p.device
         if self._hyper is None:
             self._hyper = torch.zeros(4, dtype=torch.float32, device=dev)
-        # pageable source: the copy is staged synchronously, so a later host write can never
-        # race an in-flight copy of a previous step
-        host = torch.tensor(list(vals) + [0.0] * (4 - len(vals)), dtype=torch.float32)
-        self._hyper.copy_(host)
+            self._hyper_host = torch.zeros(self._HYPER_SLOTS, 4, dtype=torch.float32).pin_memory()
+            self._hyper_ev = [None] * self._HYPER_SLOTS
+            self._hyper_i = 0
+        k = self._hyper_i
+        self._hyper_i = (k + 1) % self._HYPER_SLOTS
+        if self._hyper_ev[k] is not None:
+            self._hyper_ev[k].synchronize()
+        slot = self._hyper_host[k]
+        slot.copy_(torch.tensor(list(vals) + [0.0] * (4 - len(vals)), dtype=torch.float32))
+        self._hyper.copy_(slot, non_blocking=True)
+        ev = torch.cuda.Event()
+        ev.record()
+        self._hyper_ev[k] = ev
         return self._hyper
 
     def state_dict(self) -> dict:

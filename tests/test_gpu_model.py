@@ -106,8 +106,8 @@ def _make(seed=5):
 
 
 def test_graph_replay_matches_eager():
-    """Graph capture runs 2 eager warm-up steps on the first batch before its first replay; the
-    eager run replays the same step sequence so both trajectories must agree."""
+    """Graph capture's eager warm-up steps are rolled back (weights, optimizer moments and step,
+    BN running statistics), so the graph trajectory equals the eager one step for step."""
     from dcnn_amd.runtime.step import TrainStep
     torch.manual_seed(1)
     xs = [torch.randn(32, 3, 64, 64, device="cuda") for _ in range(2)]
@@ -116,7 +116,7 @@ def test_graph_replay_matches_eager():
     m, opt, lf = _make()
     st = TrainStep(m, lf, opt, use_graph=False)
     eager = []
-    for i in [0, 0] + order:
+    for i in order:
         st(xs[i], ys[i])
         eager.append(float(st.last_loss.item()))
     m2, opt2, lf2 = _make()
@@ -126,7 +126,8 @@ def test_graph_replay_matches_eager():
         st2(xs[i], ys[i])
         graph.append(float(st2.last_loss.item()))
     assert st2.graphs is not None and opt2.t == opt.t
-    for a, b in zip(eager[2:], graph):
+    assert abs(eager[0] - graph[0]) < 1e-2 * abs(eager[0]), (eager, graph)
+    for a, b in zip(eager, graph):
         assert abs(a - b) < 0.15 * abs(a) + 0.1, (eager, graph)
     # Adam's normalised update turns order-dependent float-atomic rounding (BN statistics) into
     # lr-sized parameter differences, so compare trajectories loosely
