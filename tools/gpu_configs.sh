@@ -17,3 +17,6 @@ run python benchmarks/pipeline_bench.py --stages 1 --schedule sync --steps 10 --
 run python benchmarks/pipeline_bench.py --stages 4 --schedule sync --steps 10 --warmup 3 || exit $?
 run python benchmarks/pipeline_bench.py --stages 4 --schedule semi_async --steps 10 --warmup 3 || exit $?
 run python benchmarks/pipeline_bench.py --stages 8 --schedule semi_async --steps 10 --warmup 3 || exit $?
+run python bench.py --batch 512 --steps 20 --warmup 5 || exit $?
+run python bench.py --batch 1024 --steps 20 --warmup 5 || exit $?
+run python bench.py --pg --steps 30 --warmup 5 || exit $?
