@@ -104,7 +104,10 @@ void multi_splitk_reduce(MultiRed t, hipStream_t s);
 int bn_partial_rows(long R, int C);
 void bn_partial(int dtype, const void* x, const void* dy, const void* yout, void* dy_out, const float* mean,
                 const float* istd, long R, int C, float* slab, int mode, float* zero_sums, hipStream_t s);
-void bn_slab_reduce(const float* slab, int rows, int C, float* sums, hipStream_t s);
+// deterministic slab reduce: mode 0 Welford triples [rows][3][C] -> (mean, var); mode 1 sums [rows][2][C]
+int bn_stat_parts(int rows);
+void bn_stat_reduce(int mode, const float* slab, int rows, int C, float* out, float* part, unsigned* ticket,
+                    hipStream_t s);
 void bn_apply(int dtype, const void* x, void* y, long R, int C, const float* sums, float count, const float* gamma,
               const float* beta, float eps, const void* residual, int relu, float* save_mean, float* save_istd,
               float* run_mean, float* run_var, float momentum, int use_running, hipStream_t s);
@@ -119,7 +122,7 @@ void bn_relu_maxpool(const bf16* x, bf16* y, uint8_t* idx, PoolGeom g, const flo
 void gn_fwd(int dtype, const void* x, void* y, int N, int HW, int C, int G, const float* gamma, const float* beta,
             float eps, float* save_mean, float* save_istd, hipStream_t s);
 void gn_bwd(int dtype, const void* dy, const void* x, void* dx, int N, int HW, int C, int G, const float* gamma,
-            const float* mean, const float* istd, float* dgamma, float* dbeta, hipStream_t s);
+            const float* mean, const float* istd, float* dgamma, float* dbeta, float* aff, hipStream_t s);
 
 void maxpool_fwd(int dt, const void* x, void* y, uint8_t* idx, PoolGeom g, hipStream_t s);
 void maxpool_bwd(int dt, const void* dy, const uint8_t* idx, void* dx, PoolGeom g, hipStream_t s);
@@ -134,7 +137,8 @@ void act_fwd(int dt, const void* x, void* y, long n, int type, float a, hipStrea
 void act_bwd(int dt, const void* x, const void* dy, void* dx, long n, int type, float a, hipStream_t s);
 void softmax_rows(int dt, const void* x, void* y, long rows, int C, hipStream_t s);
 void softmax_rows_bwd(int dt, const void* y, const void* dy, void* dx, long rows, int C, hipStream_t s);
-void dropout(int dt, const void* x, void* y, long n, float p, uint64_t seed, hipStream_t s);
+void dropout(int dt, const void* x, void* y, long n, float p, uint64_t seed, const uint64_t* ctr, hipStream_t s);
+void counter_bump(uint64_t* ctr, uint64_t* slot, hipStream_t s);
 void nchw_to_nhwc(int dt, const float* x, void* y, int N, int C, int HW, hipStream_t s);
 void nchw_to_nhwc_pad(int dt, const float* x, void* y, int N, int C, int Cp, int HW, hipStream_t s);
 void conv_weight_transpose(int src_dt, const void* w, bf16* wt, int Co, int T_, int Ci, hipStream_t s);

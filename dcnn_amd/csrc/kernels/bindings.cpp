@@ -182,8 +182,10 @@ PYBIND11_MODULE(_kernels, m) {
     bn_partial(dt, P<const void*>(x), P<const void*>(dy), P<const void*>(yout), P<void*>(dy_out),
                P<const float*>(mean), P<const float*>(istd), R, C, P<float*>(slab), mode, P<float*>(zero_sums), S(st));
   });
-  m.def("bn_slab_reduce", [](uintptr_t slab, int rows, int C, uintptr_t sums, uintptr_t st) {
-    bn_slab_reduce(P<const float*>(slab), rows, C, P<float*>(sums), S(st));
+  m.def("bn_stat_parts", &bn_stat_parts);
+  m.def("bn_stat_reduce", [](int mode, uintptr_t slab, int rows, int C, uintptr_t out, uintptr_t part, uintptr_t ticket,
+                             uintptr_t st) {
+    bn_stat_reduce(mode, P<const float*>(slab), rows, C, P<float*>(out), P<float*>(part), P<unsigned*>(ticket), S(st));
   });
   m.def("bn_apply", [](int dt, uintptr_t x, uintptr_t y, long R, int C, uintptr_t sums, float count, uintptr_t gamma,
                        uintptr_t beta, float eps, uintptr_t residual, int relu, uintptr_t save_mean,
@@ -206,9 +208,9 @@ PYBIND11_MODULE(_kernels, m) {
            P<float*>(sm), P<float*>(si), S(st));
   });
   m.def("gn_bwd", [](int dt, uintptr_t dy, uintptr_t x, uintptr_t dx, int N, int HW, int C, int G, uintptr_t gamma,
-                     uintptr_t mean, uintptr_t istd, uintptr_t dg, uintptr_t db, uintptr_t st) {
+                     uintptr_t mean, uintptr_t istd, uintptr_t dg, uintptr_t db, uintptr_t aff, uintptr_t st) {
     gn_bwd(dt, P<const void*>(dy), P<const void*>(x), P<void*>(dx), N, HW, C, G, P<const float*>(gamma),
-           P<const float*>(mean), P<const float*>(istd), P<float*>(dg), P<float*>(db), S(st));
+           P<const float*>(mean), P<const float*>(istd), P<float*>(dg), P<float*>(db), P<float*>(aff), S(st));
   });
 
   auto geom = [](int N, int H, int W, int C, int OH, int OW, int ph, int pw, int sh, int sw, int padh, int padw) {
@@ -273,8 +275,11 @@ PYBIND11_MODULE(_kernels, m) {
   m.def("softmax_rows_bwd", [](int dt, uintptr_t y, uintptr_t dy, uintptr_t dx, long rows, int C, uintptr_t st) {
     softmax_rows_bwd(dt, P<const void*>(y), P<const void*>(dy), P<void*>(dx), rows, C, S(st));
   });
-  m.def("dropout", [](int dt, uintptr_t x, uintptr_t y, long n, float p, uint64_t seed, uintptr_t st) {
-    dropout(dt, P<const void*>(x), P<void*>(y), n, p, seed, S(st));
+  m.def("dropout", [](int dt, uintptr_t x, uintptr_t y, long n, float p, uint64_t seed, uintptr_t ctr, uintptr_t st) {
+    dropout(dt, P<const void*>(x), P<void*>(y), n, p, seed, P<const uint64_t*>(ctr), S(st));
+  });
+  m.def("counter_bump", [](uintptr_t ctr, uintptr_t slot, uintptr_t st) {
+    counter_bump(P<uint64_t*>(ctr), P<uint64_t*>(slot), S(st));
   });
   m.def("nchw_to_nhwc", [](int dt, uintptr_t x, uintptr_t y, int N, int C, int HW, uintptr_t st) {
     nchw_to_nhwc(dt, P<const float*>(x), P<void*>(y), N, C, HW, S(st));

@@ -84,6 +84,33 @@ __device__ __forceinline__ float block_sum(float v, float* sh) {
   return r;
 }
 
+// ---- BatchNorm statistics partials (deterministic, cancellation-free) ----------------------
+// Every producer of forward BatchNorm statistics writes, per tile and channel, the triple
+// (count, mean, M2 = sum (x - mean)^2) into a slab [tiles][3][C]. Within a tile the sums are
+// taken about a pivot (a value of the tile itself), so E[x^2] - mean^2 cancellation never
+// happens; tiles are combined with Chan's pairwise update in a fixed order (bn_stat_reduce).
+struct Welford {
+  float n, mean, m2;
+};
+__device__ __forceinline__ Welford welford_merge(Welford a, Welford b) {
+  const float n = a.n + b.n;
+  if (b.n <= 0.f) return a;
+  if (a.n <= 0.f) return b;
+  const float d = b.mean - a.mean, f = b.n / n;
+  return Welford{n, a.mean + d * f, a.m2 + b.m2 + d * d * a.n * f};
+}
+// tile triple from pivot-shifted sums: s1 = sum (x - p), s2 = sum (x - p)^2 over n values
+__device__ __forceinline__ Welford welford_from_shifted(float n, float p, float s1, float s2) {
+  if (n <= 0.f) return Welford{0.f, 0.f, 0.f};
+  const float d = s1 / n;
+  return Welford{n, p + d, fmaxf(s2 - s1 * d, 0.f)};
+}
+__device__ __forceinline__ void store_welford(float* slab, long tile, int C, int c, Welford w) {
+  slab[(tile * 3 + 0) * C + c] = w.n;
+  slab[(tile * 3 + 1) * C + c] = w.mean;
+  slab[(tile * 3 + 2) * C + c] = w.m2;
+}
+
 // 8 x bf16 <-> 8 x f32 through one 16-byte access.
 struct alignas(16) Pack8 {
   uint4 u;

@@ -227,13 +227,19 @@ __global__ void __launch_bounds__(256, 2) gemm_g2_kernel(G2Args p) {
   const int cg = tid % CG, r0 = tid / CG;
   const int ncol = n0 + cg * 8;
   const bool col_ok = ncol < p.N;      // N % 8 == 0 for this kernel
-  float s[8], q[8], mu[8], is[8];
+  float s[8], q[8], mu[8], is[8], pv[8];
 #pragma unroll
-  for (int v = 0; v < 8; ++v) s[v] = q[v] = mu[v] = is[v] = 0.f;
+  for (int v = 0; v < 8; ++v) s[v] = q[v] = mu[v] = is[v] = pv[v] = 0.f;
   const bool bnb = p.bnb.x != nullptr;  // backward-BN fusion (api.h BnbArgs)
   if (bnb && col_ok) {
 #pragma unroll
     for (int v = 0; v < 8; ++v) { mu[v] = p.bnb.mean[ncol + v]; is[v] = p.bnb.istd[ncol + v]; }
+  }
+  // forward statistics about a pivot (tile row 0, always a valid row): (count, mean, M2) triples
+  float piv_col = 0.f;
+  if (p.stats && !bnb) {
+    unpack8(*reinterpret_cast<const uint4*>(smem + cg * 16), pv);
+    if (tid < BN) piv_col = (float)*reinterpret_cast<const bf16*>(smem + tid * 2);
   }
   const int ghw = p.GH * p.GW;
   for (int row = r0; row < BM; row += RSTEP) {
@@ -272,7 +278,7 @@ __global__ void __launch_bounds__(256, 2) gemm_g2_kernel(G2Args p) {
         for (int v = 0; v < 8; ++v) { s[v] += g[v]; q[v] += g[v] * (xv[v] - mu[v]) * is[v]; }
       } else {
 #pragma unroll
-        for (int v = 0; v < 8; ++v) { s[v] += g[v]; q[v] += g[v] * g[v]; }
+        for (int v = 0; v < 8; ++v) { const float d = g[v] - pv[v]; s[v] += d; q[v] += d * d; }
       }
     }
   }
@@ -285,13 +291,20 @@ __global__ void __launch_bounds__(256, 2) gemm_g2_kernel(G2Args p) {
       red[(r0 * 2 + 1) * BN + cg * 8 + v] = q[v];
     }
     __syncthreads();
-    for (int c = tid; c < 2 * BN; c += 256) {
-      const int which = c / BN, cc = c % BN;
-      if (n0 + cc < p.N) {
-        float a = 0.f;
-        for (int k = 0; k < RSTEP; ++k) a += red[(k * 2 + which) * BN + cc];
-        p.stats[((long)tm * 2 + which) * p.N + n0 + cc] = a;
+    if (bnb) {  // backward: plain sums [tiles][2][N]
+      for (int c = tid; c < 2 * BN; c += 256) {
+        const int which = c / BN, cc = c % BN;
+        if (n0 + cc < p.N) {
+          float a = 0.f;
+          for (int k = 0; k < RSTEP; ++k) a += red[(k * 2 + which) * BN + cc];
+          p.stats[((long)tm * 2 + which) * p.N + n0 + cc] = a;
+        }
       }
+    } else if (tid < BN && n0 + tid < p.N) {  // forward: Welford triple [tiles][3][N]
+      float a = 0.f, b = 0.f;
+      for (int k = 0; k < RSTEP; ++k) { a += red[(k * 2 + 0) * BN + tid]; b += red[(k * 2 + 1) * BN + tid]; }
+      const float cnt = (float)min(BM, p.M - m0);
+      store_welford(p.stats, tm, p.N, n0 + tid, welford_from_shifted(cnt, piv_col, a, b));
     }
   }
 }

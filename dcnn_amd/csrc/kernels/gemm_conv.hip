@@ -222,14 +222,17 @@ __global__ void __launch_bounds__(256, 2) gemm_nt_kernel(NtArgs p) {
   }
 
   // ---- epilogue ----
-  float csum[T::TN], csq[T::TN];
+  // BatchNorm statistics about a per-(M-wave, column) pivot, merged with Chan's update (no
+  // cancellation, fixed order)
+  float csum[T::TN], csq[T::TN], ccnt[T::TN], cpiv[T::TN];
 #pragma unroll
-  for (int j = 0; j < T::TN; ++j) csum[j] = csq[j] = 0.f;
+  for (int j = 0; j < T::TN; ++j) csum[j] = csq[j] = ccnt[j] = 0.f;
 #pragma unroll
   for (int j = 0; j < T::TN; ++j) {
     const int n = n0 + wn * (BN / 2) + j * 16 + (lane & 15);
     const bool nok = n < p.N;
     const float bv = (p.bias && nok) ? p.bias[n] : 0.f;
+    cpiv[j] = __shfl(p.out_f32 ? acc[0][j][0] + bv : (float)(bf16)(acc[0][j][0] + bv), lane & 15, 64);
 #pragma unroll
     for (int i = 0; i < T::TM; ++i) {
 #pragma unroll
@@ -247,8 +250,10 @@ __global__ void __launch_bounds__(256, 2) gemm_nt_kernel(NtArgs p) {
             reinterpret_cast<bf16*>(p.C)[o] = h;
             v = (float)h;  // statistics of the stored values
           }
-          csum[j] += v;
-          csq[j] += v * v;
+          const float d = v - cpiv[j];
+          csum[j] += d;
+          csq[j] += d * d;
+          ccnt[j] += 1.f;
         }
       }
     }
@@ -258,23 +263,28 @@ __global__ void __launch_bounds__(256, 2) gemm_nt_kernel(NtArgs p) {
     float* red = reinterpret_cast<float*>(smem);  // reuse LDS (loop finished, barrier passed)
 #pragma unroll
     for (int j = 0; j < T::TN; ++j) {
-      float s = csum[j], q = csq[j];
+      float s = csum[j], q = csq[j], c = ccnt[j];
       s += __shfl_xor(s, 16, 64);
       s += __shfl_xor(s, 32, 64);
       q += __shfl_xor(q, 16, 64);
       q += __shfl_xor(q, 32, 64);
+      c += __shfl_xor(c, 16, 64);
+      c += __shfl_xor(c, 32, 64);
       if (lane < 16) {
         const int col = wn * (BN / 2) + j * 16 + lane;
-        red[(wm * 2 + 0) * BN + col] = s;
-        red[(wm * 2 + 1) * BN + col] = q;
+        red[(wm * 4 + 0) * BN + col] = s;
+        red[(wm * 4 + 1) * BN + col] = q;
+        red[(wm * 4 + 2) * BN + col] = cpiv[j];
+        red[(wm * 4 + 3) * BN + col] = c;
       }
     }
     __syncthreads();
     for (int c = tid; c < BN; c += 256) {
       const int n = n0 + c;
       if (n < p.N) {
-        p.stats[((long)tm * 2 + 0) * p.N + n] = red[0 * BN + c] + red[2 * BN + c];
-        p.stats[((long)tm * 2 + 1) * p.N + n] = red[1 * BN + c] + red[3 * BN + c];
+        Welford t = welford_from_shifted(red[3 * BN + c], red[2 * BN + c], red[0 * BN + c], red[1 * BN + c]);
+        t = welford_merge(t, welford_from_shifted(red[7 * BN + c], red[6 * BN + c], red[4 * BN + c], red[5 * BN + c]));
+        store_welford(p.stats, tm, p.N, n, t);
       }
     }
   }
@@ -506,83 +516,87 @@ struct SplitkSeg {
   long n;
 };
 
-__device__ __forceinline__ void splitk_segment(const SplitkSeg g, long bid, long nblk, int s0, int s1, int atomic) {
+__device__ __forceinline__ void splitk_segment(const SplitkSeg g, long bid, long nblk, int splits, int accumulate) {
   const long n = g.n, n4 = n / 4;
   const float* __restrict__ slab = g.slab;
   float* __restrict__ out = g.out;
   for (long i = bid * blockDim.x + threadIdx.x; i < n4; i += nblk * blockDim.x) {
     // 8 independent 16-byte loads in flight per lane: the slab stream is latency-bound otherwise
     float4 s = make_float4(0, 0, 0, 0);
-    int k = s0;
-    for (; k + 8 <= s1; k += 8) {
+    int k = 0;
+    for (; k + 8 <= splits; k += 8) {
       float4 v[8];
 #pragma unroll
       for (int u = 0; u < 8; ++u) v[u] = reinterpret_cast<const float4*>(slab + (long)(k + u) * n)[i];
 #pragma unroll
       for (int u = 0; u < 8; ++u) { s.x += v[u].x; s.y += v[u].y; s.z += v[u].z; s.w += v[u].w; }
     }
-    for (; k < s1; ++k) {
+    for (; k < splits; ++k) {
       const float4 v = reinterpret_cast<const float4*>(slab + (long)k * n)[i];
       s.x += v.x; s.y += v.y; s.z += v.z; s.w += v.w;
     }
-    float* o = out + i * 4;
-    if (atomic) {
-      atomicAdd(o + 0, s.x); atomicAdd(o + 1, s.y); atomicAdd(o + 2, s.z); atomicAdd(o + 3, s.w);
-    } else {
+    if (accumulate) {
       float4 c = reinterpret_cast<float4*>(out)[i];
       c.x += s.x; c.y += s.y; c.z += s.z; c.w += s.w;
       reinterpret_cast<float4*>(out)[i] = c;
+    } else {
+      reinterpret_cast<float4*>(out)[i] = s;
     }
   }
   for (long i = n4 * 4 + bid * blockDim.x + threadIdx.x; i < n; i += nblk * blockDim.x) {
     float s = 0.f;
-    for (int k = s0; k < s1; ++k) s += slab[(long)k * n + i];
-    if (atomic) atomicAdd(out + i, s); else out[i] += s;
+    for (int k = 0; k < splits; ++k) s += slab[(long)k * n + i];
+    out[i] = accumulate ? out[i] + s : s;
   }
 }
 
-__global__ void splitk_reduce_kernel(SplitkSeg a, SplitkSeg b, int gxa, int splits, int per_group, int atomic) {
-  const int s0 = blockIdx.y * per_group, s1 = min(splits, s0 + per_group);
+// Split-K combine: every output element is summed by ONE thread over the splits in index order
+// (deterministic, no float atomics); up to two slabs (a weight gradient and its bias gradient)
+// per launch: blocks [0, gxa) take segment a, the rest segment b.
+__global__ void splitk_reduce_kernel(SplitkSeg a, SplitkSeg b, int gxa, int splits, int accumulate) {
   if ((int)blockIdx.x < gxa)
-    splitk_segment(a, blockIdx.x, gxa, s0, s1, atomic);
+    splitk_segment(a, blockIdx.x, gxa, splits, accumulate);
   else
-    splitk_segment(b, blockIdx.x - gxa, gridDim.x - gxa, s0, s1, atomic);
+    splitk_segment(b, blockIdx.x - gxa, gridDim.x - gxa, splits, accumulate);
 }
 
 // Deferred split-K reduction: the fp32 slabs of many weight gradients summed into their
-// gradients in ONE launch (api.h MultiRed). A work unit is (entry, chunk of 256 floats, group of
-// 32 splits); each wave of the unit sums 8 splits with all 8 loads in flight, the 4 waves meet
-// in LDS, and wave 0 adds into the gradient (atomically when the entry has several groups).
+// gradients in ONE launch (api.h MultiRed). A work unit is (entry, chunk of 256 floats); wave w
+// sums splits {32g + 8w .. 32g + 8w + 7} for every group g in order, all 8 loads of a group in
+// flight, the 4 waves meet in LDS in wave order and wave 0 adds into the gradient. Fixed
+// summation order throughout: bit-reproducible, no atomics.
 __global__ void __launch_bounds__(256) multi_splitk_reduce_kernel(MultiRed t) {
   int k = 0;
   while (k + 1 < t.count && (int)blockIdx.x >= t.e[k + 1].unit0) ++k;
   const float* slab = t.e[k].slab;
   float* out = t.e[k].out;
   const long n = t.e[k].n;
-  const int splits = t.e[k].splits, chunks = t.e[k].chunks, groups = t.e[k].groups, vec = t.e[k].vec;
-  const int local = blockIdx.x - t.e[k].unit0, chunk = local % chunks, grp = local / chunks;
+  const int splits = t.e[k].splits, groups = t.e[k].groups, vec = t.e[k].vec;
+  const int chunk = blockIdx.x - t.e[k].unit0;
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-  const int s0 = grp * 32 + w * 8;
   __shared__ float4 red[3][64];
   float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
-  if (vec) {  // n % 4 == 0: lane owns 4 consecutive floats
-    const long i4 = (long)chunk * 64 + lane;
-    const bool ok = i4 * 4 < n;
-    float4 v[8];
+  for (int g = 0; g < groups; ++g) {
+    const int s0 = g * 32 + w * 8;
+    if (vec) {  // n % 4 == 0: lane owns 4 consecutive floats
+      const long i4 = (long)chunk * 64 + lane;
+      const bool ok = i4 * 4 < n;
+      float4 v[8];
 #pragma unroll
-    for (int u = 0; u < 8; ++u)
-      v[u] = (ok && s0 + u < splits) ? reinterpret_cast<const float4*>(slab + (long)(s0 + u) * n)[i4]
-                                     : make_float4(0.f, 0.f, 0.f, 0.f);
+      for (int u = 0; u < 8; ++u)
+        v[u] = (ok && s0 + u < splits) ? reinterpret_cast<const float4*>(slab + (long)(s0 + u) * n)[i4]
+                                       : make_float4(0.f, 0.f, 0.f, 0.f);
 #pragma unroll
-    for (int u = 0; u < 8; ++u) { acc.x += v[u].x; acc.y += v[u].y; acc.z += v[u].z; acc.w += v[u].w; }
-  } else {  // one float per lane
-    const long i = (long)chunk * 64 + lane;
-    const bool ok = i < n;
-    float v[8];
+      for (int u = 0; u < 8; ++u) { acc.x += v[u].x; acc.y += v[u].y; acc.z += v[u].z; acc.w += v[u].w; }
+    } else {  // one float per lane
+      const long i = (long)chunk * 64 + lane;
+      const bool ok = i < n;
+      float v[8];
 #pragma unroll
-    for (int u = 0; u < 8; ++u) v[u] = (ok && s0 + u < splits) ? slab[(long)(s0 + u) * n + i] : 0.f;
+      for (int u = 0; u < 8; ++u) v[u] = (ok && s0 + u < splits) ? slab[(long)(s0 + u) * n + i] : 0.f;
 #pragma unroll
-    for (int u = 0; u < 8; ++u) acc.x += v[u];
+      for (int u = 0; u < 8; ++u) acc.x += v[u];
+    }
   }
   if (w > 0) red[w - 1][lane] = acc;
   __syncthreads();
@@ -594,18 +608,13 @@ __global__ void __launch_bounds__(256) multi_splitk_reduce_kernel(MultiRed t) {
   if (vec) {
     const long i4 = (long)chunk * 64 + lane;
     if (i4 * 4 >= n) return;
-    float* o = out + i4 * 4;
-    if (groups > 1) {
-      atomicAdd(o + 0, acc.x); atomicAdd(o + 1, acc.y); atomicAdd(o + 2, acc.z); atomicAdd(o + 3, acc.w);
-    } else {
-      float4 c = reinterpret_cast<float4*>(out)[i4];
-      c.x += acc.x; c.y += acc.y; c.z += acc.z; c.w += acc.w;
-      reinterpret_cast<float4*>(out)[i4] = c;
-    }
+    float4 c = reinterpret_cast<float4*>(out)[i4];
+    c.x += acc.x; c.y += acc.y; c.z += acc.z; c.w += acc.w;
+    reinterpret_cast<float4*>(out)[i4] = c;
   } else {
     const long i = (long)chunk * 64 + lane;
     if (i >= n) return;
-    if (groups > 1) atomicAdd(out + i, acc.x); else out[i] += acc.x;
+    out[i] += acc.x;
   }
 }
 
@@ -620,7 +629,7 @@ void multi_splitk_reduce(MultiRed t, hipStream_t s) {
     e.chunks = (int)((e.n + per - 1) / per);
     e.groups = (e.splits + 31) / 32;
     e.unit0 = units;
-    units += e.chunks * e.groups;
+    units += e.chunks;
   }
   hipLaunchKernelGGL(multi_splitk_reduce_kernel, dim3(units), dim3(256), 0, s, t);
   DCNN_LAUNCH_CHECK();
@@ -719,22 +728,11 @@ void gemm_tn(TnArgs a, int splits, hipStream_t s) {
 
 void splitk_reduce2(const float* slab, float* out, long n, const float* bslab, float* bout, long nb, int splits,
                     int accumulate, hipStream_t s) {
-  if (!accumulate) {
-    DCNN_HIP_CHECK(hipMemsetAsync(out, 0, sizeof(float) * n, s));
-    if (nb > 0) DCNN_HIP_CHECK(hipMemsetAsync(bout, 0, sizeof(float) * nb, s));
-  }
   const long n4 = n / 4 + 1;
   const int gxa = grid_for(n4, 256, 4096);
   const int gxb = nb > 0 ? grid_for(nb / 4 + 1, 256, 64) : 0;
-  long want = (131072 + n4 - 1) / n4;  // aim for >= 512 workgroups in total
-  long groups = (splits + 3) / 4;
-  if (groups > want) groups = want;
-  if (groups < 1) groups = 1;
-  const int per = (int)((splits + groups - 1) / groups);
-  groups = (splits + per - 1) / per;
   const SplitkSeg a{slab, out, n}, b{bslab, bout, nb > 0 ? nb : 0};
-  hipLaunchKernelGGL(splitk_reduce_kernel, dim3(gxa + gxb, (unsigned)groups), dim3(256), 0, s, a, b, gxa, splits,
-                     per, groups > 1 ? 1 : 0);
+  hipLaunchKernelGGL(splitk_reduce_kernel, dim3(gxa + gxb), dim3(256), 0, s, a, b, gxa, splits, accumulate);
   DCNN_LAUNCH_CHECK();
 }
 

@@ -40,7 +40,7 @@ __device__ __forceinline__ f32x4 mfma4(const float4& a, const float4& b, f32x4 c
 __global__ void __launch_bounds__(256, 2) gemm_g2f_kernel(G2Args p) {
   __shared__ __attribute__((aligned(16))) float As[2][FBM * FPITCH];
   __shared__ __attribute__((aligned(16))) float Bs[2][FBN * FPITCH];
-  __shared__ float red[2][FBN];
+  __shared__ float red[2][4][FBN];  // per M-wave: shifted (sum, sum^2), pivot, count
   const float* A = reinterpret_cast<const float*>(p.A);
   const float* B = reinterpret_cast<const float*>(p.B);
   float* C = reinterpret_cast<float*>(p.C);
@@ -140,15 +140,17 @@ __global__ void __launch_bounds__(256, 2) gemm_g2f_kernel(G2Args p) {
   }
 
   // ---- epilogue straight from the accumulators: lane owns column (lane&15) of each subtile ----
-  if (p.stats && tid < 2 * FBN) (&red[0][0])[tid] = 0.f;
-  if (p.stats) __syncthreads();
+  // Forward BatchNorm statistics: per (M-wave, column) the values are summed about a pivot (the
+  // wave's first row of the column), reduced over the lane groups by a fixed butterfly, and the
+  // two M-waves are merged with Chan's update into a (count, mean, M2) triple. No atomics.
   const int ghw = p.GH * p.GW;
 #pragma unroll
   for (int j = 0; j < 2; ++j) {
     const int col = n0 + wn * 32 + j * 16 + (lane & 15);
     const bool cok = col < p.N;
     const float bv = (p.bias && cok) ? p.bias[col] : 0.f;
-    float s = 0.f, q = 0.f;
+    const float piv = __shfl(acc[0][j][0] + bv, lane & 15, 64);
+    float s = 0.f, q = 0.f, n = 0.f;
 #pragma unroll
     for (int i = 0; i < 2; ++i)
 #pragma unroll
@@ -162,19 +164,33 @@ __global__ void __launch_bounds__(256, 2) gemm_g2f_kernel(G2Args p) {
         if (R) v += R[orow * p.ldc + col];
         if (p.relu) v = fmaxf(v, 0.f);
         C[orow * p.ldc + col] = v;
-        s += v;
-        q += v * v;
+        const float d = v - piv;
+        s += d;
+        q += d * d;
+        n += 1.f;
       }
-    if (p.stats && cok) {
-      atomicAdd(&red[0][wn * 32 + j * 16 + (lane & 15)], s);
-      atomicAdd(&red[1][wn * 32 + j * 16 + (lane & 15)], q);
+    if (p.stats) {
+      s += __shfl_xor(s, 16, 64);
+      s += __shfl_xor(s, 32, 64);
+      q += __shfl_xor(q, 16, 64);
+      q += __shfl_xor(q, 32, 64);
+      n += __shfl_xor(n, 16, 64);
+      n += __shfl_xor(n, 32, 64);
+      if (lane < 16) {
+        const int c = wn * 32 + j * 16 + lane;
+        red[wm][0][c] = s;
+        red[wm][1][c] = q;
+        red[wm][2][c] = piv;
+        red[wm][3][c] = n;
+      }
     }
   }
   if (p.stats) {
     __syncthreads();
-    if (tid < 2 * FBN) {
-      const int which = tid / FBN, cc = tid % FBN;
-      if (n0 + cc < p.N) p.stats[((long)tm * 2 + which) * p.N + n0 + cc] = red[which][cc];
+    if (tid < FBN && n0 + tid < p.N) {
+      Welford t = welford_from_shifted(red[0][3][tid], red[0][2][tid], red[0][0][tid], red[0][1][tid]);
+      t = welford_merge(t, welford_from_shifted(red[1][3][tid], red[1][2][tid], red[1][0][tid], red[1][1][tid]));
+      store_welford(p.stats, tm, p.N, n0 + tid, t);
     }
   }
 }

@@ -99,13 +99,20 @@ __device__ __forceinline__ void hc_epilogue(const HConvArgs& p, f32x4 (&acc)[BM 
   constexpr int RSTEP = 256 / CG;
   const int cg = tid % CG, r0 = tid / CG;
   const int ncol = n0 + cg * 8;
-  float s[8], q[8], mu[8], is[8];
+  float s[8], q[8], mu[8], is[8], pv[8];
 #pragma unroll
-  for (int v = 0; v < 8; ++v) s[v] = q[v] = mu[v] = is[v] = 0.f;
+  for (int v = 0; v < 8; ++v) s[v] = q[v] = mu[v] = is[v] = pv[v] = 0.f;
   const bool bnb = p.bnb.x != nullptr;  // backward-BN fusion (api.h BnbArgs)
   if (bnb && true) {
 #pragma unroll
     for (int v = 0; v < 8; ++v) { mu[v] = p.bnb.mean[ncol + v]; is[v] = p.bnb.istd[ncol + v]; }
+  }
+  // forward statistics are summed about a pivot (tile row 0 of the column, a value of the tile
+  // itself) and leave as a (count, mean, M2) triple: no E[x^2] - mean^2 cancellation
+  float piv_col = 0.f;
+  if (p.stats && !bnb) {
+    unpack8(*reinterpret_cast<const uint4*>(smem + cg * 16), pv);
+    if (tid < BN) piv_col = (float)*reinterpret_cast<const bf16*>(smem + tid * 2);
   }
   const int tpx = p.TH * p.TW;
   for (int row = r0; row < BM; row += RSTEP) {
@@ -143,7 +150,7 @@ __device__ __forceinline__ void hc_epilogue(const HConvArgs& p, f32x4 (&acc)[BM 
         for (int v = 0; v < 8; ++v) { s[v] += g[v]; q[v] += g[v] * (xv[v] - mu[v]) * is[v]; }
       } else {
 #pragma unroll
-        for (int v = 0; v < 8; ++v) { s[v] += g[v]; q[v] += g[v] * g[v]; }
+        for (int v = 0; v < 8; ++v) { const float d = g[v] - pv[v]; s[v] += d; q[v] += d * d; }
       }
     }
   }
@@ -156,11 +163,18 @@ __device__ __forceinline__ void hc_epilogue(const HConvArgs& p, f32x4 (&acc)[BM 
       red[(r0 * 2 + 1) * BN + cg * 8 + v] = q[v];
     }
     __syncthreads();
-    for (int cc = tid; cc < 2 * BN; cc += 256) {
-      const int which = cc / BN, c2 = cc % BN;
-      float a = 0.f;
-      for (int k = 0; k < RSTEP; ++k) a += red[(k * 2 + which) * BN + c2];
-      p.stats[((long)tm * 2 + which) * p.N + n0 + c2] = a;
+    if (bnb) {  // backward: plain sums [tiles][2][N]
+      for (int cc = tid; cc < 2 * BN; cc += 256) {
+        const int which = cc / BN, c2 = cc % BN;
+        float a = 0.f;
+        for (int k = 0; k < RSTEP; ++k) a += red[(k * 2 + which) * BN + c2];
+        p.stats[((long)tm * 2 + which) * p.N + n0 + c2] = a;
+      }
+    } else if (tid < BN) {  // forward: Welford triple [tiles][3][N], fixed summation order
+      float a = 0.f, b = 0.f;
+      for (int k = 0; k < RSTEP; ++k) { a += red[(k * 2 + 0) * BN + tid]; b += red[(k * 2 + 1) * BN + tid]; }
+      const float cnt = (float)(min(p.IMG, p.NB - img0) * tpx);
+      store_welford(p.stats, tm, p.N, n0 + tid, welford_from_shifted(cnt, piv_col, a, b));
     }
   }
 }

@@ -15,13 +15,16 @@ namespace dcnn {
 
 enum LossType { kCE = 0, kSoftmaxCE = 1, kLogSoftmaxCE = 2, kMSE = 3, kMAE = 4, kHuber = 5 };
 
+// One workgroup of 16 waves; wave w takes rows w, w + 16, ... (a batch is <= a few thousand
+// rows of <= a few thousand classes: microseconds of work). Per-wave loss / correct partials meet
+// in LDS and are summed in wave order: the loss is bit-reproducible (no float atomics) and no
+// memset of the outputs is needed.
+constexpr int kLossWaves = 16;
+
 template <typename T>
-__global__ void loss_kernel(const T* __restrict__ pred, const float* __restrict__ target,
-                            const int64_t* __restrict__ labels, T* __restrict__ grad, float* __restrict__ loss_out,
-                            int* __restrict__ correct, int N, int C, int type, float param) {
-  const int lane = threadIdx.x & 63;
-  const int row = (blockIdx.x * blockDim.x + threadIdx.x) >> 6;
-  if (row >= N) return;
+__device__ __forceinline__ void loss_row(const T* __restrict__ pred, const float* __restrict__ target,
+                                         const int64_t* __restrict__ labels, T* __restrict__ grad, int row, int N,
+                                         int C, int type, float param, int lane, float* lsum_out, int* hit) {
   const T* p = pred + (long)row * C;
   auto tgt = [&](int c) -> float {
     if (labels) return (int64_t)c == labels[row] ? 1.f : 0.f;
@@ -54,26 +57,24 @@ __global__ void loss_kernel(const T* __restrict__ pred, const float* __restrict_
     for (int c = lane; c < C; c += 64) if (tgt(c) > 0.5f && c < hot) hot = c;
 #pragma unroll
     for (int o = 32; o > 0; o >>= 1) hot = min(hot, __shfl_xor(hot, o, 64));
-    if (lane == 0 && hot < C) lsum = lse - to_f(p[hot]);
+    if (hot < C) lsum = (lse - to_f(p[hot])) * invN;
     if (grad) {
       const float inv_s = 1.f / s;
       for (int c = lane; c < C; c += 64)
         grad[(long)row * C + c] = from_f<T>((__expf(to_f(p[c]) - pm) * inv_s - tgt(c)) * invN);
     }
-    if (lane == 0) atomicAdd(loss_out, lsum * invN);
   } else if (type == kCE) {
     int hot = 0x7fffffff;
     for (int c = lane; c < C; c += 64) if (tgt(c) > 0.5f && c < hot) hot = c;
 #pragma unroll
     for (int o = 32; o > 0; o >>= 1) hot = min(hot, __shfl_xor(hot, o, 64));
-    if (lane == 0 && hot < C) {
+    if (hot < C) {
       const float v = fminf(fmaxf(to_f(p[hot]), param), 1.f - param);
-      lsum = -__logf(v);
+      lsum = -__logf(v) * invN;
     }
     if (grad)
       for (int c = lane; c < C; c += 64)
         grad[(long)row * C + c] = from_f<T>((to_f(p[c]) - tgt(c)) * invN);
-    if (lane == 0) atomicAdd(loss_out, lsum * invN);
   } else {
     for (int c = lane; c < C; c += 64) {
       const float d = to_f(p[c]) - tgt(c), ad = fabsf(d);
@@ -87,23 +88,45 @@ __global__ void loss_kernel(const T* __restrict__ pred, const float* __restrict_
       lsum += l;
       if (grad) grad[(long)row * C + c] = from_f<T>(g);
     }
-    lsum = wave_sum(lsum);
-    if (lane == 0) atomicAdd(loss_out, lsum * invNC);
+    lsum = wave_sum(lsum) * invNC;
   }
-  if (lane == 0 && correct && pi == ti) atomicAdd(correct, 1);
+  *lsum_out += lsum;
+  *hit += (pi == ti) ? 1 : 0;
+}
+
+template <typename T>
+__global__ void __launch_bounds__(kLossWaves * 64) loss_kernel(const T* __restrict__ pred,
+                                                              const float* __restrict__ target,
+                                                              const int64_t* __restrict__ labels,
+                                                              T* __restrict__ grad, float* __restrict__ loss_out,
+                                                              int* __restrict__ correct, int N, int C, int type,
+                                                              float param) {
+  __shared__ float wl[kLossWaves];
+  __shared__ int wc[kLossWaves];
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  float lsum = 0.f;
+  int hits = 0;
+  for (int row = w; row < N; row += kLossWaves)
+    loss_row<T>(pred, target, labels, grad, row, N, C, type, param, lane, &lsum, &hits);
+  if (lane == 0) { wl[w] = lsum; wc[w] = hits; }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    float l = 0.f;
+    int h = 0;
+    for (int k = 0; k < kLossWaves; ++k) { l += wl[k]; h += wc[k]; }
+    *loss_out = l;
+    if (correct) *correct = h;
+  }
 }
 
 void loss_fused(int dt, const void* pred, const float* target, const int64_t* labels, void* grad, float* loss_out,
                 int* correct, int N, int C, int type, float param, hipStream_t s) {
-  DCNN_HIP_CHECK(hipMemsetAsync(loss_out, 0, sizeof(float), s));
-  if (correct) DCNN_HIP_CHECK(hipMemsetAsync(correct, 0, sizeof(int), s));
-  const dim3 grid((N * 64 + 255) / 256);
   if (dt == 0)
-    hipLaunchKernelGGL(loss_kernel<float>, grid, dim3(256), 0, s, (const float*)pred, target, labels, (float*)grad,
-                       loss_out, correct, N, C, type, param);
+    hipLaunchKernelGGL(loss_kernel<float>, dim3(1), dim3(kLossWaves * 64), 0, s, (const float*)pred, target, labels,
+                       (float*)grad, loss_out, correct, N, C, type, param);
   else
-    hipLaunchKernelGGL(loss_kernel<bf16>, grid, dim3(256), 0, s, (const bf16*)pred, target, labels, (bf16*)grad,
-                       loss_out, correct, N, C, type, param);
+    hipLaunchKernelGGL(loss_kernel<bf16>, dim3(1), dim3(kLossWaves * 64), 0, s, (const bf16*)pred, target, labels,
+                       (bf16*)grad, loss_out, correct, N, C, type, param);
   DCNN_LAUNCH_CHECK();
 }
 

@@ -53,10 +53,12 @@ __device__ __forceinline__ void vstore(T* p, const float* f) {
 }
 
 // ---------------------------------------------------------------------------------------
-// partial statistics: slab[block][2][C] over rows [block*rpb, (block+1)*rpb)
-// mode 0: (sum x, sum x^2)
-// mode 1 (backward): (sum dy', sum dy' * xhat) with dy' = dy * (yout > 0 if yout)
-//                    optionally storing dy' (needed by a residual branch)
+// partial statistics over rows [block*rpb, (block+1)*rpb)
+// mode 0: slab[block][3][C] = (count, mean, M2) of x — sums taken about a per-block pivot (the
+//         block's first row), merged later with Chan's update: no E[x^2] - mean^2 cancellation
+// mode 1 (backward): slab[block][2][C] = (sum dy', sum dy' * xhat) with dy' = dy * (yout > 0 if
+//         yout), optionally storing dy' (needed by a residual branch)
+// All cross-thread sums run in a fixed order: the result is bit-reproducible.
 // ---------------------------------------------------------------------------------------
 template <typename T, int V>
 __global__ void __launch_bounds__(256) bn_partial_kernel(const T* __restrict__ x, const T* __restrict__ dy,
@@ -75,14 +77,15 @@ __global__ void __launch_bounds__(256) bn_partial_kernel(const T* __restrict__ x
   const long r0 = (long)blockIdx.x * rpb, r1 = min(R, r0 + rpb);
   for (int gbase = 0; gbase < groups; gbase += tpr) {
     const int g = gbase + g0;
-    float s[V], q[V];
+    float s[V], q[V], pv[V];
 #pragma unroll
-    for (int v = 0; v < V; ++v) s[v] = q[v] = 0.f;
+    for (int v = 0; v < V; ++v) s[v] = q[v] = pv[v] = 0.f;
     float mu[V], is[V];
     if (mode == 1 && g < groups && rsub < rows_conc) {
 #pragma unroll
       for (int v = 0; v < V; ++v) { mu[v] = mean[g * V + v]; is[v] = istd[g * V + v]; }
     }
+    if (mode == 0 && g < groups && rsub < rows_conc) vload<T, V>(x + r0 * C + (long)g * V, pv);  // pivot row
     if (g < groups && rsub < rows_conc) {
       for (long r = r0 + rsub; r < r1; r += rows_conc) {
         const long o = r * C + (long)g * V;
@@ -90,7 +93,7 @@ __global__ void __launch_bounds__(256) bn_partial_kernel(const T* __restrict__ x
         vload<T, V>(x + o, xv);
         if (mode == 0) {
 #pragma unroll
-          for (int v = 0; v < V; ++v) { s[v] += xv[v]; q[v] += xv[v] * xv[v]; }
+          for (int v = 0; v < V; ++v) { const float d = xv[v] - pv[v]; s[v] += d; q[v] += d * d; }
         } else {
           float d[V];
           vload<T, V>(dy + o, d);
@@ -109,57 +112,140 @@ __global__ void __launch_bounds__(256) bn_partial_kernel(const T* __restrict__ x
         }
       }
     }
-    // reduce over rsub through LDS: sh[rows_conc][2][tpr*V]
+    // reduce over rsub through LDS in a fixed order: sh[rows_conc][2][tpr*V] (+ pivots)
     __syncthreads();
+    const int width = tpr * V;
     if (g < groups && rsub < rows_conc) {
 #pragma unroll
       for (int v = 0; v < V; ++v) {
-        sh[(rsub * 2 + 0) * tpr * V + g0 * V + v] = s[v];
-        sh[(rsub * 2 + 1) * tpr * V + g0 * V + v] = q[v];
+        sh[(rsub * 2 + 0) * width + g0 * V + v] = s[v];
+        sh[(rsub * 2 + 1) * width + g0 * V + v] = q[v];
+        if (rsub == 0) sh[rows_conc * 2 * width + g0 * V + v] = pv[v];
       }
     }
     __syncthreads();
-    const int width = tpr * V;
-    for (int c = threadIdx.x; c < 2 * width; c += 256) {
-      const int which = c / width, cc = c % width;
-      const int ch = gbase * V + cc;
+    const float cnt = (float)(r1 - r0);
+    for (int c = threadIdx.x; c < width; c += 256) {
+      const int ch = gbase * V + c;
       if (ch < C) {
-        float acc = 0.f;
-        for (int k = 0; k < rows_conc; ++k) acc += sh[(k * 2 + which) * width + cc];
-        slab[((long)blockIdx.x * 2 + which) * C + ch] = acc;
+        float a = 0.f, b = 0.f;
+        for (int k = 0; k < rows_conc; ++k) { a += sh[(k * 2 + 0) * width + c]; b += sh[(k * 2 + 1) * width + c]; }
+        if (mode == 0) {
+          store_welford(slab, blockIdx.x, C, ch, welford_from_shifted(cnt, sh[rows_conc * 2 * width + c], a, b));
+        } else {
+          slab[((long)blockIdx.x * 2 + 0) * C + ch] = a;
+          slab[((long)blockIdx.x * 2 + 1) * C + ch] = b;
+        }
       }
     }
+    __syncthreads();
   }
 }
 
-// sums[2][C] += sum over slab rows (atomic; sums zeroed by the caller). Lane = channel, wave w
-// of the block sums rows [rb + w*RW, rb + (w+1)*RW) with all 2*RW loads issued before the first
-// add: the slab is tiny (L2/MALL resident) and the kernel is pure load latency otherwise
-template <int RW>
-__global__ void __launch_bounds__(256) bn_slab_reduce_kernel(const float* __restrict__ slab, int rows, int C,
-                                                             float* __restrict__ sums) {
+// ---------------------------------------------------------------------------------------
+// Deterministic statistics reduce: slab rows -> stats[2][C]
+//   MODE 0: rows are (count, mean, M2) triples -> stats = (mean, biased variance)
+//   MODE 1: rows are (sum a, sum b) pairs      -> stats = (sum a, sum b)
+// Grid (C/64, ny): lane = channel, each block merges up to 256 rows (each wave up to 4 chunks of
+// 16, all loads of a chunk in flight) in row order. With ny > 1 the blocks publish their partials
+// (agent release) and take a ticket; the last block of a channel column merges the ny partials
+// in block order (agent acquire). Every merge order is fixed: the result does not depend on timing.
+// ---------------------------------------------------------------------------------------
+template <int MODE>
+struct StatAcc {
+  float a, b, c;  // MODE 0: (n, mean, M2); MODE 1: (sum a, sum b, -)
+  __device__ __forceinline__ static StatAcc zero() { return StatAcc{0.f, 0.f, 0.f}; }
+  __device__ __forceinline__ StatAcc merge(const StatAcc& o) const {
+    if constexpr (MODE == 0) {
+      const Welford w = welford_merge(Welford{a, b, c}, Welford{o.a, o.b, o.c});
+      return StatAcc{w.n, w.mean, w.m2};
+    } else {
+      return StatAcc{a + o.a, b + o.b, 0.f};
+    }
+  }
+};
+constexpr int kStatRW = 16, kStatChunks = 4, kStatRowsPerBlock = 4 * kStatRW * kStatChunks;
+
+template <int MODE>
+__device__ __forceinline__ StatAcc<MODE> stat_rows(const float* __restrict__ src, int r0, int r1, int C, int c) {
+  constexpr int NV = MODE == 0 ? 3 : 2;
+  StatAcc<MODE> acc = StatAcc<MODE>::zero();
+  for (int rb = r0; rb < r1; rb += kStatRW) {
+    float v[kStatRW][NV];
+#pragma unroll
+    for (int j = 0; j < kStatRW; ++j)
+#pragma unroll
+      for (int k = 0; k < NV; ++k) v[j][k] = (rb + j < r1) ? src[((long)(rb + j) * NV + k) * C + c] : 0.f;
+#pragma unroll
+    for (int j = 0; j < kStatRW; ++j) acc = acc.merge(StatAcc<MODE>{v[j][0], v[j][1], v[j][NV - 1]});
+  }
+  return acc;
+}
+
+template <int MODE>
+__global__ void __launch_bounds__(256) bn_stat_reduce_kernel(const float* __restrict__ slab, int rows, int C,
+                                                             float* __restrict__ part, unsigned* __restrict__ ticket,
+                                                             float* __restrict__ out) {
+  __shared__ StatAcc<MODE> red[4][64];
+  __shared__ int last;
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   const int c = blockIdx.x * 64 + lane;
-  const int r0 = (blockIdx.y * 4 + w) * RW;
-  __shared__ float red[4][2][64];
-  float vs[RW], vq[RW];
-#pragma unroll
-  for (int j = 0; j < RW; ++j) {
-    const bool ok = c < C && r0 + j < rows;
-    vs[j] = ok ? slab[((long)(r0 + j) * 2 + 0) * C + c] : 0.f;
-    vq[j] = ok ? slab[((long)(r0 + j) * 2 + 1) * C + c] : 0.f;
-  }
-  float s = 0.f, q = 0.f;
-#pragma unroll
-  for (int j = 0; j < RW; ++j) { s += vs[j]; q += vq[j]; }
-  red[w][0][lane] = s;
-  red[w][1][lane] = q;
+  const bool cok = c < C;
+  const int ny = gridDim.y, by = blockIdx.y;
+  auto finish = [&](StatAcc<MODE> t) {
+    if constexpr (MODE == 0) {
+      out[c] = t.b;
+      out[C + c] = t.a > 0.f ? t.c / t.a : 0.f;
+    } else {
+      out[c] = t.a;
+      out[C + c] = t.b;
+    }
+  };
+  // ---- level 1: this block's rows, wave w takes a contiguous quarter ----
+  const int b0 = by * kStatRowsPerBlock, b1 = min(rows, b0 + kStatRowsPerBlock);
+  const int q = (b1 - b0 + 3) / 4;
+  const int w0 = min(b1, b0 + w * q), w1 = min(b1, w0 + q);
+  red[w][lane] = cok ? stat_rows<MODE>(slab, w0, w1, C, c) : StatAcc<MODE>::zero();
   __syncthreads();
-  if (w == 0 && c < C) {
-    s = red[0][0][lane] + red[1][0][lane] + red[2][0][lane] + red[3][0][lane];
-    q = red[0][1][lane] + red[1][1][lane] + red[2][1][lane] + red[3][1][lane];
-    atomicAdd(&sums[c], s);
-    atomicAdd(&sums[C + c], q);
+  if (ny == 1) {
+    if (w == 0 && cok) finish(red[0][lane].merge(red[1][lane]).merge(red[2][lane]).merge(red[3][lane]));
+    return;
+  }
+  if (w == 0) {
+    if (cok) {
+      const StatAcc<MODE> t = red[0][lane].merge(red[1][lane]).merge(red[2][lane]).merge(red[3][lane]);
+      part[((long)by * 3 + 0) * C + c] = t.a;
+      part[((long)by * 3 + 1) * C + c] = t.b;
+      part[((long)by * 3 + 2) * C + c] = t.c;
+    }
+    // publish: this wave's stores drained, agent-scope release, then the ticket
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    if (lane == 0) {
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      const unsigned old = __hip_atomic_fetch_add(&ticket[blockIdx.x], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      last = old == (unsigned)(ny - 1);
+      if (last) {
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      }
+    }
+  }
+  __syncthreads();
+  if (!last) return;
+  // ---- level 2 (last block of this channel column): partials in block order ----
+  const int pq = (ny + 3) / 4, p0 = min(ny, w * pq), p1 = min(ny, p0 + pq);
+  StatAcc<MODE> t = StatAcc<MODE>::zero();
+  if (cok)
+    for (int k = p0; k < p1; ++k)
+      t = t.merge(StatAcc<MODE>{part[((long)k * 3 + 0) * C + c], part[((long)k * 3 + 1) * C + c],
+                                part[((long)k * 3 + 2) * C + c]});
+  __syncthreads();
+  red[w][lane] = t;
+  __syncthreads();
+  if (w == 0) {
+    if (cok) finish(red[0][lane].merge(red[1][lane]).merge(red[2][lane]).merge(red[3][lane]));
+    if (lane == 0) ticket[blockIdx.x] = 0u;  // ready for the next reduce on this stream
   }
 }
 
@@ -182,8 +268,8 @@ __global__ void __launch_bounds__(256) bn_apply_kernel(const T* __restrict__ x, 
       mean = run_mean[c];
       istd = rsqrtf(run_var[c] + eps);
     } else {
-      mean = sums[c] / count;
-      const float var = fmaxf(sums[C + c] / count - mean * mean, 0.f);
+      mean = sums[c];  // stats from bn_stat_reduce: (mean, biased variance)
+      const float var = sums[C + c];
       istd = rsqrtf(var + eps);
       if (blockIdx.x == 0) {
         if (save_mean) { save_mean[c] = mean; save_istd[c] = istd; }
@@ -236,8 +322,7 @@ __global__ void __launch_bounds__(256) bn_relu_maxpool_kernel(const bf16* __rest
   float* scale = sh;
   float* shift = sh + g.C;
   for (int c = threadIdx.x; c < g.C; c += blockDim.x) {
-    const float mean = sums[c] / count;
-    const float var = fmaxf(sums[g.C + c] / count - mean * mean, 0.f);
+    const float mean = sums[c], var = sums[g.C + c];  // (mean, biased variance)
     const float istd = rsqrtf(var + eps);
     if (blockIdx.x == 0) {
       if (save_mean) { save_mean[c] = mean; save_istd[c] = istd; }
@@ -369,7 +454,7 @@ __global__ void __launch_bounds__(256) gn_bwd_kernel(const T* __restrict__ dy, c
                                                      T* __restrict__ dx, int HW, int C, int G,
                                                      const float* __restrict__ gamma,
                                                      const float* __restrict__ mean, const float* __restrict__ istd,
-                                                     float* __restrict__ dgamma, float* __restrict__ dbeta) {
+                                                     float* __restrict__ aff) {
   __shared__ float sh[16];
   const int n = blockIdx.x / G, g = blockIdx.x % G, Cg = C / G;
   const long base = (long)n * HW * C + (long)g * Cg;
@@ -394,7 +479,8 @@ __global__ void __launch_bounds__(256) gn_bwd_kernel(const T* __restrict__ dy, c
     const float d = to_f(dy[o]) * gm, xh = (to_f(x[o]) - mu) * is;
     dx[o] = from_f<T>(is * (d - m1 - xh * m2));
   }
-  // per-channel dgamma/dbeta partial for this image: thread per channel of the group
+  // per-channel dgamma/dbeta partial of this image -> aff[n][2][C] (summed over images in a fixed
+  // order by gn_affine_reduce_kernel: no float atomics)
   for (int cl = threadIdx.x; cl < Cg; cl += blockDim.x) {
     const int c = g * Cg + cl;
     float a = 0.f, b = 0.f;
@@ -404,9 +490,19 @@ __global__ void __launch_bounds__(256) gn_bwd_kernel(const T* __restrict__ dy, c
       a += d * (to_f(x[o]) - mu) * is;
       b += d;
     }
-    if (dgamma) atomicAdd(&dgamma[c], a);
-    if (dbeta) atomicAdd(&dbeta[c], b);
+    aff[((long)n * 2 + 0) * C + c] = a;
+    aff[((long)n * 2 + 1) * C + c] = b;
   }
+}
+
+__global__ void gn_affine_reduce_kernel(const float* __restrict__ aff, int N, int C, float* __restrict__ dgamma,
+                                        float* __restrict__ dbeta) {
+  const int c = blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= C) return;
+  float a = 0.f, b = 0.f;
+  for (int n = 0; n < N; ++n) { a += aff[((long)n * 2 + 0) * C + c]; b += aff[((long)n * 2 + 1) * C + c]; }
+  if (dgamma) dgamma[c] += a;
+  if (dbeta) dbeta[c] += b;
 }
 
 // ---------------------------------------------------------------------------------------
@@ -431,12 +527,12 @@ static void bn_partial_t(const T* x, const T* dy, const T* yout, T* dy_out, cons
   const int blocks = (int)((R + rpb - 1) / rpb);
   if (C % 8 == 0) {
     const int groups = C / 8, tpr = groups < 256 ? groups : 256, rc = 256 / tpr;
-    const size_t shm = (size_t)rc * 2 * tpr * 8 * sizeof(float);
+    const size_t shm = ((size_t)rc * 2 + 1) * tpr * 8 * sizeof(float);
     hipLaunchKernelGGL((bn_partial_kernel<T, 8>), dim3(blocks), dim3(256), shm, s, x, dy, yout, dy_out, mean,
                        istd, R, C, rpb, slab, mode, zs);
   } else {
     const int tpr = C < 256 ? C : 256, rc = 256 / tpr;
-    const size_t shm = (size_t)rc * 2 * tpr * sizeof(float);
+    const size_t shm = ((size_t)rc * 2 + 1) * tpr * sizeof(float);
     hipLaunchKernelGGL((bn_partial_kernel<T, 1>), dim3(blocks), dim3(256), shm, s, x, dy, yout, dy_out, mean,
                        istd, R, C, rpb, slab, mode, zs);
   }
@@ -453,17 +549,20 @@ void bn_partial(int dtype, const void* x, const void* dy, const void* yout, void
                        mode, zero_sums, s);
 }
 
-// `sums` must have been zeroed by the producer of `slab` (workgroup 0 of gemm_g2 / bn_partial)
-void bn_slab_reduce(const float* slab, int rows, int C, float* sums, hipStream_t s) {
-  // 8 rows per wave (32 per block) unless that leaves > ~1024 blocks (each adds 2x64 atomics)
-  const long cg = (C + 63) / 64;
-  if (cg * ((rows + 31) / 32) <= 1024) {
-    hipLaunchKernelGGL(bn_slab_reduce_kernel<8>, dim3((unsigned)cg, (rows + 31) / 32), dim3(256), 0, s, slab, rows, C,
-                       sums);
-  } else {
-    hipLaunchKernelGGL(bn_slab_reduce_kernel<32>, dim3((unsigned)cg, (rows + 127) / 128), dim3(256), 0, s, slab,
-                       rows, C, sums);
-  }
+int bn_stat_parts(int rows) { return (rows + kStatRowsPerBlock - 1) / kStatRowsPerBlock; }
+
+// mode 0: slab [rows][3][C] Welford triples -> out = (mean, var); mode 1: slab [rows][2][C] sums.
+// part: bn_stat_parts(rows) x 3 x C floats (unused when that is 1); ticket: ceil(C/64) zeroed
+// words, left zeroed again (one ticket array per stream).
+void bn_stat_reduce(int mode, const float* slab, int rows, int C, float* out, float* part, unsigned* ticket,
+                    hipStream_t s) {
+  const int ny = bn_stat_parts(rows);
+  if (ny > 1 && (!part || !ticket)) throw std::runtime_error("bn_stat_reduce: workspace required");
+  const dim3 grid((unsigned)((C + 63) / 64), (unsigned)ny);
+  if (mode == 0)
+    hipLaunchKernelGGL(bn_stat_reduce_kernel<0>, grid, dim3(256), 0, s, slab, rows, C, part, ticket, out);
+  else
+    hipLaunchKernelGGL(bn_stat_reduce_kernel<1>, grid, dim3(256), 0, s, slab, rows, C, part, ticket, out);
   DCNN_LAUNCH_CHECK();
 }
 
@@ -551,14 +650,18 @@ void gn_fwd(int dtype, const void* x, void* y, int N, int HW, int C, int G, cons
 }
 
 void gn_bwd(int dtype, const void* dy, const void* x, void* dx, int N, int HW, int C, int G, const float* gamma,
-            const float* mean, const float* istd, float* dgamma, float* dbeta, hipStream_t s) {
+            const float* mean, const float* istd, float* dgamma, float* dbeta, float* aff, hipStream_t s) {
   if (dtype == 0)
     hipLaunchKernelGGL(gn_bwd_kernel<float>, dim3(N * G), dim3(256), 0, s, (const float*)dy, (const float*)x,
-                       (float*)dx, HW, C, G, gamma, mean, istd, dgamma, dbeta);
+                       (float*)dx, HW, C, G, gamma, mean, istd, aff);
   else
     hipLaunchKernelGGL(gn_bwd_kernel<bf16>, dim3(N * G), dim3(256), 0, s, (const bf16*)dy, (const bf16*)x,
-                       (bf16*)dx, HW, C, G, gamma, mean, istd, dgamma, dbeta);
+                       (bf16*)dx, HW, C, G, gamma, mean, istd, aff);
   DCNN_LAUNCH_CHECK();
+  if (dgamma || dbeta) {
+    hipLaunchKernelGGL(gn_affine_reduce_kernel, dim3((C + 255) / 256), dim3(256), 0, s, aff, N, C, dgamma, dbeta);
+    DCNN_LAUNCH_CHECK();
+  }
 }
 
 }  // namespace dcnn

@@ -358,8 +358,12 @@ __global__ void softmax_rows_bwd_kernel(const T* __restrict__ y, const T* __rest
 
 // ------------------------------------- dropout -------------------------------------------
 template <typename T>
-__global__ void dropout_kernel(const T* __restrict__ x, T* __restrict__ y, long n, float p, uint64_t seed) {
+__global__ void dropout_kernel(const T* __restrict__ x, T* __restrict__ y, long n, float p, uint64_t seed,
+                               const uint64_t* __restrict__ ctr) {
   const float scale = 1.f / (1.f - p);
+  // device-side draw counter: a hipGraph replay captures `seed` as a constant, the counter slot is
+  // rewritten by counter_bump before every replayed forward, so each replay draws a new mask
+  if (ctr) seed += ctr[0] * 0x9E3779B97F4A7C15ull;
   for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < (n + 3) / 4; i += (long)gridDim.x * blockDim.x) {
     const uint4 r = Philox::gen(seed, (uint64_t)i);
     const uint32_t rr[4] = {r.x, r.y, r.z, r.w};
@@ -368,6 +372,15 @@ __global__ void dropout_kernel(const T* __restrict__ x, T* __restrict__ y, long 
       const long o = i * 4 + v;
       if (o < n) y[o] = from_f<T>(Philox::u01(rr[v]) >= p ? ld(x, o) * scale : 0.f);
     }
+  }
+}
+
+// slot = ++ctr (one thread): per-forward draw index for dropout, advanced inside the graph
+__global__ void counter_bump_kernel(uint64_t* ctr, uint64_t* slot) {
+  if (threadIdx.x == 0 && blockIdx.x == 0) {
+    const uint64_t v = ctr[0] + 1;
+    ctr[0] = v;
+    slot[0] = v;
   }
 }
 
@@ -608,8 +621,9 @@ static void softmax_bwd_t(const void* y, const void* dy, void* dx, long rows, in
   DCNN_LAUNCH_CHECK();
 }
 template <typename T>
-static void dropout_t(const void* x, void* y, long n, float p, uint64_t seed, hipStream_t s) {
-  hipLaunchKernelGGL(dropout_kernel<T>, dim3(grid_for((n + 3) / 4, 256)), dim3(256), 0, s, (const T*)x, (T*)y, n, p, seed);
+static void dropout_t(const void* x, void* y, long n, float p, uint64_t seed, const uint64_t* ctr, hipStream_t s) {
+  hipLaunchKernelGGL(dropout_kernel<T>, dim3(grid_for((n + 3) / 4, 256)), dim3(256), 0, s, (const T*)x, (T*)y, n, p, seed,
+                     ctr);
   DCNN_LAUNCH_CHECK();
 }
 template <typename T>
@@ -634,7 +648,13 @@ void act_fwd(int dt, const void* x, void* y, long n, int type, float a, hipStrea
 void act_bwd(int dt, const void* x, const void* dy, void* dx, long n, int type, float a, hipStream_t s) { DCNN_DT(dt, act_bwd_t, x, dy, dx, n, type, a, s); }
 void softmax_rows(int dt, const void* x, void* y, long rows, int C, hipStream_t s) { DCNN_DT(dt, softmax_t, x, y, rows, C, s); }
 void softmax_rows_bwd(int dt, const void* y, const void* dy, void* dx, long rows, int C, hipStream_t s) { DCNN_DT(dt, softmax_bwd_t, y, dy, dx, rows, C, s); }
-void dropout(int dt, const void* x, void* y, long n, float p, uint64_t seed, hipStream_t s) { DCNN_DT(dt, dropout_t, x, y, n, p, seed, s); }
+void dropout(int dt, const void* x, void* y, long n, float p, uint64_t seed, const uint64_t* ctr, hipStream_t s) {
+  DCNN_DT(dt, dropout_t, x, y, n, p, seed, ctr, s);
+}
+void counter_bump(uint64_t* ctr, uint64_t* slot, hipStream_t s) {
+  hipLaunchKernelGGL(counter_bump_kernel, dim3(1), dim3(64), 0, s, ctr, slot);
+  DCNN_LAUNCH_CHECK();
+}
 void nchw_to_nhwc(int dt, const float* x, void* y, int N, int C, int HW, hipStream_t s) { DCNN_DT(dt, nchw_to_nhwc_t, x, y, N, C, HW, s); }
 void nchw_to_nhwc_pad(int dt, const float* x, void* y, int N, int C, int Cp, int HW, hipStream_t s) { DCNN_DT(dt, nchw_to_nhwc_pad_t, x, y, N, C, Cp, HW, s); }
 void conv_weight_transpose(int src_dt, const void* w, bf16* wt, int Co, int T_, int Ci, hipStream_t s) { DCNN_DT(src_dt, wt_t, w, wt, Co, T_, Ci, s); }

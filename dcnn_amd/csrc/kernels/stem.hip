@@ -82,7 +82,7 @@ __global__ void __launch_bounds__(256, NCB <= 2 ? 8 : 4) stem_fwd_kernel(StemArg
   constexpr int CO = NCB * 16;
   __shared__ __attribute__((aligned(16))) bf16 halo[HALO_MAX];
   __shared__ __attribute__((aligned(16))) bf16 stg[4][16 * CO];
-  __shared__ float red[4][2][CO];
+  __shared__ float red[4][3][CO];  // per wave: pivot-shifted (sum, sum^2) and the pivot
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6, kg = lane >> 4, col = lane & 15;
   const int tile = blockIdx.x;
   if (p.zero_ptr && tile == 0)
@@ -109,9 +109,12 @@ __global__ void __launch_bounds__(256, NCB <= 2 ? 8 : 4) stem_fwd_kernel(StemArg
   // per-lane tap offsets (in halo pixels) of the A fragment: taps 2kg, 2kg+1 and tap 8
   const int t0 = 2 * kg, t1 = 2 * kg + 1;
   const int o0 = (t0 / 3) * HW2 + t0 % 3, o1 = (t1 / 3) * HW2 + t1 % 3, o8 = 2 * HW2 + 2;
-  float s[NCB], q[NCB];
+  // statistics are summed about a per-wave pivot (the wave's first output row of each channel)
+  // and merged over the 4 waves with Chan's update: (count, mean, M2) triples, fixed order
+  float s[NCB], q[NCB], piv[NCB];
 #pragma unroll
-  for (int cb = 0; cb < NCB; ++cb) s[cb] = q[cb] = 0.f;
+  for (int cb = 0; cb < NCB; ++cb) s[cb] = q[cb] = piv[cb] = 0.f;
+  bool first = true;
   const bf16x4 z4 = bf16x4{(bf16)0.f, (bf16)0.f, (bf16)0.f, (bf16)0.f};
   for (int g = wid; g < SPX / 16; g += 4) {
     const int px = g * 16 + col, py = px / p.W, pxx = px - py * p.W;
@@ -123,15 +126,17 @@ __global__ void __launch_bounds__(256, NCB <= 2 ? 8 : 4) stem_fwd_kernel(StemArg
     for (int cb = 0; cb < NCB; ++cb) {
       f32x4 acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a0, b0[cb], f32x4{0.f, 0.f, 0.f, 0.f}, 0, 0, 0);
       acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a1, b1[cb], acc, 0, 0, 0);
+      if (first) piv[cb] = __shfl((float)(bf16)(acc[0] + bias[cb]), col, 64);  // row 0 of this column
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
         const bf16 v = (bf16)(acc[r] + bias[cb]);
-        const float f = (float)v;
+        const float f = (float)v - piv[cb];
         s[cb] += f;
         q[cb] += f * f;
         stg[wid][(kg * 4 + r) * CO + cb * 16 + col] = v;
       }
     }
+    first = false;
     // the 16 pixels of a group are contiguous in NHWC: 16 * CO * 2 bytes, 16 per lane
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     __builtin_amdgcn_wave_barrier();
@@ -149,12 +154,21 @@ __global__ void __launch_bounds__(256, NCB <= 2 ? 8 : 4) stem_fwd_kernel(StemArg
     s[cb] += __shfl_xor(s[cb], 32);
     q[cb] += __shfl_xor(q[cb], 16);
     q[cb] += __shfl_xor(q[cb], 32);
-    if (kg == 0) { red[wid][0][cb * 16 + col] = s[cb]; red[wid][1][cb * 16 + col] = q[cb]; }
+    if (kg == 0) {
+      red[wid][0][cb * 16 + col] = s[cb];
+      red[wid][1][cb * 16 + col] = q[cb];
+      red[wid][2][cb * 16 + col] = piv[cb];
+    }
   }
   __syncthreads();
-  for (int i = threadIdx.x; i < 2 * CO; i += 256) {
-    const int which = i / CO, c = i - which * CO;
-    p.slab[((long)tile * 2 + which) * CO + c] = red[0][which][c] + red[1][which][c] + red[2][which][c] + red[3][which][c];
+  for (int c = threadIdx.x; c < CO; c += 256) {
+    Welford t{0.f, 0.f, 0.f};
+#pragma unroll
+    for (int w = 0; w < 4; ++w) {
+      const int ng = w < SPX / 16 ? (SPX / 16 - 1 - w) / 4 + 1 : 0;  // groups this wave ran
+      t = welford_merge(t, welford_from_shifted((float)(ng * 16), red[w][2][c], red[w][0][c], red[w][1][c]));
+    }
+    store_welford(p.slab, tile, CO, c, t);
   }
 }
 

@@ -128,6 +128,8 @@ class Dropout(StatelessLayer):
             raise ValueError("dropout_rate must be in [0, 1)")
         self.dropout_rate = float(dropout_rate)
         self._counter = 0
+        self._dev_ctr = None   # GPU: device draw counter, advanced in-stream (hipGraph replays too)
+        self._slots = {}       # mb_id -> 1-element device tensor holding that forward's draw index
 
     def _next_seed(self):
         self._counter += 1
@@ -143,8 +145,17 @@ class Dropout(StatelessLayer):
         if x.is_cuda:
             from ...ops import hip
             xa = hip.to_act(x, self.compute_dtype) if x.dim() == 4 else x.to(self.compute_dtype).contiguous()
-            self._cache[mb_id] = seed   # mask regenerated from the Philox seed in backward
-            return hip.dropout(xa, self.dropout_rate, seed)
+            # the host seed is a constant of a captured graph: the per-forward draw index is
+            # bumped on the device so every replay (and every micro-batch) gets a fresh mask
+            if self._dev_ctr is None or self._dev_ctr.device != xa.device:
+                self._dev_ctr = torch.zeros(1, dtype=torch.int64, device=xa.device)
+                self._slots = {}
+            slot = self._slots.get(mb_id)
+            if slot is None:
+                slot = self._slots[mb_id] = torch.zeros(1, dtype=torch.int64, device=xa.device)
+            hip.counter_bump(self._dev_ctr, slot)
+            self._cache[mb_id] = (seed, slot)   # mask regenerated from Philox(seed, slot) in backward
+            return hip.dropout(xa, self.dropout_rate, seed, slot)
         gen = torch.Generator().manual_seed(seed)
         mask = (torch.rand(x.shape, generator=gen) >= self.dropout_rate).to(x.dtype) / (1 - self.dropout_rate)
         self._cache[mb_id] = mask
@@ -154,10 +165,10 @@ class Dropout(StatelessLayer):
         ent = self._cache.pop(mb_id, None)
         if ent is None:
             return grad
-        if isinstance(ent, int):
+        if isinstance(ent, tuple):
             from ...ops import hip
             g = hip.to_act(grad, self.compute_dtype) if grad.dim() == 4 else grad.to(self.compute_dtype).contiguous()
-            return hip.dropout(g, self.dropout_rate, ent)
+            return hip.dropout(g, self.dropout_rate, ent[0], ent[1])
         return grad * ent
 
     def forward_flops(self, s):

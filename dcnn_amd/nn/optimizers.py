@@ -115,9 +115,13 @@ class Optimizer:
             self._hyper_ev[k].synchronize()
         slot = self._hyper_host[k]
         slot.copy_(torch.tensor(list(vals) + [0.0] * (4 - len(vals)), dtype=torch.float32))
-        self._hyper.copy_(slot, non_blocking=True)
+        # the copy and the event that guards the pinned slot go on the SAME stream: the current
+        # stream of the arena's device (a pipeline stage thread may have another device current)
+        s = torch.cuda.current_stream(dev)
+        with torch.cuda.stream(s):
+            self._hyper.copy_(slot, non_blocking=True)
         ev = torch.cuda.Event()
-        ev.record()
+        ev.record(s)
         self._hyper_ev[k] = ev
         return self._hyper
 

@@ -114,7 +114,7 @@ def conv2d_fwd(x, w, bias, stride, pad, *, stats=False, residual=None, relu=Fals
         slab, rows, sums = None, 0, None
         if stats:
             rows = K.gemm_g2f_stat_rows(M, Co)
-            slab = torch.empty((rows, 2, Co), dtype=F32, device=x.device)
+            slab = torch.empty((rows, 3, Co), dtype=F32, device=x.device)
             sums = torch.empty((2 * Co,), dtype=F32, device=x.device)  # zeroed in-kernel
         K.gemm_g2f(x.data_ptr(), w.data_ptr(), y.data_ptr(), _nbytes(x), _nbytes(w), M, Co, Ci, H, W, OH, OW, sh, sw,
                    _fwd_taps(Ci, W, KH, KW, ph, pw), KH * KW * Ci, Co, OH, OW, 1, 1, 0, 0, ptr(bias), ptr(residual),
@@ -126,7 +126,7 @@ def conv2d_fwd(x, w, bias, stride, pad, *, stats=False, residual=None, relu=Fals
         slab, rows, sums = None, 0, None
         if stats:
             rows = K.hconv_stat_rows(N, H, W, Co)
-            slab = torch.empty((rows, 2, Co), dtype=F32, device=x.device)
+            slab = torch.empty((rows, 3, Co), dtype=F32, device=x.device)
             sums = torch.empty((2 * Co,), dtype=F32, device=x.device)  # zeroed in-kernel
         K.hconv(x.data_ptr(), w.data_ptr(), y.data_ptr(), _nbytes(x), _nbytes(w), N, H, W, Ci, Co, KH * KW * Ci,
                 [(t[0], t[1], t[3]) for t in taps], ptr(bias), ptr(residual), ptr(slab), int(relu), ptr(sums),
@@ -137,7 +137,7 @@ def conv2d_fwd(x, w, bias, stride, pad, *, stats=False, residual=None, relu=Fals
         slab, rows, sums = None, 0, None
         if stats:
             rows = K.gemm_g2_stat_rows(M, Co)
-            slab = torch.empty((rows, 2, Co), dtype=F32, device=x.device)
+            slab = torch.empty((rows, 3, Co), dtype=F32, device=x.device)
             sums = torch.empty((2 * Co,), dtype=F32, device=x.device)  # zeroed in-kernel
         K.gemm_g2(x.data_ptr(), w.data_ptr(), y.data_ptr(), _nbytes(x), _nbytes(w), M, Co, Ci, H, W, OH, OW, sh, sw,
                   _fwd_taps(Ci, W, KH, KW, ph, pw), KH * KW * Ci, Co, OH, OW, 1, 1, 0, 0, ptr(bias), ptr(residual),
@@ -148,11 +148,11 @@ def conv2d_fwd(x, w, bias, stride, pad, *, stats=False, residual=None, relu=Fals
     slab, rows = None, 0
     if stats:
         rows = K.gemm_nt_stat_rows(M, Co)
-        slab = torch.empty((rows, 2, Co), dtype=F32, device=x.device)
+        slab = torch.empty((rows, 3, Co), dtype=F32, device=x.device)
     K.gemm_nt(x.data_ptr(), w.data_ptr(), y.data_ptr(), M, Co, KH * KW * Ci, 0, KH * KW * Ci, Co, CONV_FWD,
               N, H, W, Ci, OH, OW, KH, KW, sh, sw, ph, pw, ptr(bias), ptr(residual), ptr(slab),
               int(out_fp32), int(relu), stream_ptr())
-    sums = torch.zeros((2 * Co,), dtype=F32, device=x.device) if stats else None
+    sums = torch.empty((2 * Co,), dtype=F32, device=x.device) if stats else None
     return y, ((slab, rows, sums) if stats else None)
 
 
@@ -181,7 +181,7 @@ def stem_conv_fwd(x, w, bias=None, stats=False):
     rows = 0
     if stats:
         rows = K.stem_tiles(N, H, W)
-        slab = torch.empty((rows, 2, Co), dtype=F32, device=x.device)
+        slab = torch.empty((rows, 3, Co), dtype=F32, device=x.device)
         sums = torch.empty((2 * Co,), dtype=F32, device=x.device)  # zeroed in-kernel
     assert w.dtype in (F32, BF16) and tuple(w.shape) == (Co, Ci, 3, 3)
     K.stem_fwd(x.data_ptr(), w.data_ptr(), int(w.dtype == BF16), list(w.stride()), ptr(bias), y.data_ptr(),
@@ -563,20 +563,47 @@ def _rc(x):
     return N * H * W, C
 
 
+_tickets = {}
+
+
+def _ticket(device, C):
+    """Per-(stream, device) ticket words of bn_stat_reduce (zeroed once; every reduce leaves
+    them zeroed again, and reduces on one stream never overlap)."""
+    key = (stream_ptr(), device.index)
+    t = _tickets.get(key)
+    need = (C + 63) // 64
+    if t is None or t.numel() < need:
+        t = torch.zeros(max(need, 64), dtype=torch.int32, device=device)
+        _tickets[key] = t
+    return t
+
+
+def stat_reduce(mode, slab, rows, C, out):
+    """Deterministic slab reduce (norm.hip bn_stat_reduce): mode 0 = Welford (count, mean, M2)
+    tile triples -> out = (mean, biased var); mode 1 = (sum a, sum b) rows -> out = sums."""
+    K = kernels()
+    ny = K.bn_stat_parts(rows)
+    part = torch.empty((ny, 3, C), dtype=F32, device=slab.device) if ny > 1 else None
+    K.bn_stat_reduce(mode, slab.data_ptr(), rows, C, out.data_ptr(), ptr(part),
+                     _ticket(slab.device, C).data_ptr() if ny > 1 else 0, stream_ptr())
+    return out
+
+
 def bn_stats(x, partial=None):
-    """Per-channel (sum, sumsq) of x (NHWC). Uses the conv-epilogue partial slab if given."""
+    """Per-channel (mean, biased variance) of x (NHWC), as one [2][C] fp32 tensor. Uses the
+    producing conv's epilogue Welford slab if given, else a bn_partial pass; the reduction is
+    deterministic and cancellation-free (Chan merges of pivot-shifted tile statistics)."""
     K = kernels()
     R, C = _rc(x)
     st = stream_ptr()
     if partial is None:
         rows = K.bn_partial_rows(R, C)
-        slab = torch.empty((rows, 2, C), dtype=F32, device=x.device)
+        slab = torch.empty((rows, 3, C), dtype=F32, device=x.device)
         sums = torch.empty((2 * C,), dtype=F32, device=x.device)
-        K.bn_partial(dt_code(x.dtype), x.data_ptr(), 0, 0, 0, 0, 0, R, C, slab.data_ptr(), 0, sums.data_ptr(), st)
+        K.bn_partial(dt_code(x.dtype), x.data_ptr(), 0, 0, 0, 0, 0, R, C, slab.data_ptr(), 0, 0, st)
     else:
         slab, rows, sums = partial
-    K.bn_slab_reduce(slab.data_ptr(), rows, C, sums.data_ptr(), st)
-    return sums
+    return stat_reduce(0, slab, rows, C, sums)
 
 
 def bn_apply(x, sums, count, gamma, beta, eps, *, residual=None, relu=False, save=None, running=None,
@@ -632,7 +659,7 @@ def bn_backward(dy, x, yout, mean, istd, gamma, dgamma, dbeta, *, want_masked=Fa
     dt = dt_code(x.dtype)
     if fused is not None and not eval_mode:
         slab, rows, sums = fused
-        K.bn_slab_reduce(slab.data_ptr(), rows, C, sums.data_ptr(), st)
+        stat_reduce(1, slab, rows, C, sums)
         dx = torch.empty_like(x, memory_format=CL)
         K.bn_bwd_apply(dt, dy.data_ptr(), 0, x.data_ptr(), dx.data_ptr(), R, C, mean.data_ptr(), istd.data_ptr(),
                        ptr(gamma), sums.data_ptr(), float(R), ptr(dgamma), ptr(dbeta), 0, st)
@@ -644,8 +671,8 @@ def bn_backward(dy, x, yout, mean, istd, gamma, dgamma, dbeta, *, want_masked=Fa
         slab = torch.empty((rows, 2, C), dtype=F32, device=x.device)
         sums = torch.empty((2 * C,), dtype=F32, device=x.device)
         K.bn_partial(dt, x.data_ptr(), dy.data_ptr(), ptr(yout), ptr(dmask), mean.data_ptr(), istd.data_ptr(), R, C,
-                     slab.data_ptr(), 1, sums.data_ptr(), st)
-        K.bn_slab_reduce(slab.data_ptr(), rows, C, sums.data_ptr(), st)
+                     slab.data_ptr(), 1, 0, st)
+        stat_reduce(1, slab, rows, C, sums)
     elif want_masked and yout is not None:
         dmask = dy * (yout > 0)
     dx = torch.empty_like(x, memory_format=CL)
@@ -680,8 +707,9 @@ def gn_fwd(x, groups, gamma, beta, eps):
 def gn_bwd(dy, x, groups, gamma, mean, istd, dgamma, dbeta):
     N, C, H, W = x.shape
     dx = torch.empty_like(x, memory_format=CL)
+    aff = torch.empty((N, 2, C), dtype=F32, device=x.device)  # per-image affine partials
     kernels().gn_bwd(dt_code(x.dtype), dy.data_ptr(), x.data_ptr(), dx.data_ptr(), N, H * W, C, groups, ptr(gamma),
-                     mean.data_ptr(), istd.data_ptr(), ptr(dgamma), ptr(dbeta), stream_ptr())
+                     mean.data_ptr(), istd.data_ptr(), ptr(dgamma), ptr(dbeta), aff.data_ptr(), stream_ptr())
     return dx
 
 
@@ -783,11 +811,18 @@ def softmax_channels_bwd(y, dy):
     return dx
 
 
-def dropout(x, p, seed):
+def dropout(x, p, seed, slot=None):
+    """Inverted dropout with a Philox mask of (seed, *slot). ``slot``: a 1-element int64 device
+    tensor written by :func:`counter_bump` (graph-replay safe: the draw index lives on the device)."""
     y = torch.empty_like(x)
     kernels().dropout(dt_code(x.dtype), x.data_ptr(), y.data_ptr(), x.numel(), float(p), int(seed) & ((1 << 64) - 1),
-                      stream_ptr())
+                      ptr(slot), stream_ptr())
     return y
+
+
+def counter_bump(ctr, slot):
+    """slot = ++ctr on the device (both 1-element int64 tensors)."""
+    kernels().counter_bump(ctr.data_ptr(), slot.data_ptr(), stream_ptr())
 
 
 # ------------------------------------------------------------------------------ loss / optim

@@ -114,3 +114,62 @@ def test_gpu_dp_rccl_world1_graph_segments(tmp_path):
         assert abs(r["losses"][0] - e["losses"][0]) < 1e-5 * abs(e["losses"][0]), (r["losses"], e["losses"])
         for lr_, le in zip(r["losses"], e["losses"]):
             assert abs(lr_ - le) < 3e-2 * max(1.0, abs(le)), (r["losses"], e["losses"])
+
+
+def _bnfree_model(seed):
+    from dcnn_amd.nn import SequentialBuilder
+    m = (SequentialBuilder("dp_exact").input([3, 16, 16])
+         .conv2d(16, 3, 3, 1, 1, 1, 1).activation("relu").maxpool2d(2, 2, 2, 2)
+         .conv2d(32, 3, 3, 1, 1, 1, 1).activation("relu").flatten().dense(10).build())
+    m.set_seed(seed)
+    m.set_device("GPU:0")
+    m.set_compute_dtype(torch.float32)
+    m.initialize()
+    m.set_first_layer_input_grad(False)
+    return m
+
+
+def _exact_worker(rank, world, port, out, use_graph):
+    """fp32 + SGD, BN-free: each rank trains its half of the batch; after the bucket all-reduce
+    the gradient and the updated parameters must equal a single process on the whole batch."""
+    import torch.distributed as dist
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    torch.cuda.set_device(0)
+    if world > 1:
+        dist.init_process_group("gloo", rank=rank, world_size=world)
+    from dcnn_amd.nn import SGD, LossFactory
+    from dcnn_amd.parallel.dp import DataParallel
+    from dcnn_amd.runtime.step import TrainStep
+    m = _bnfree_model(3)
+    dp = DataParallel(m, bucket_mb=0.004)  # ~1 KB buckets: several fire points inside backward
+    opt = SGD(0.1)
+    opt.attach(m)
+    st = TrainStep(dp, LossFactory.create("softmax_crossentropy"), opt, use_graph=use_graph)
+    g = torch.Generator().manual_seed(21)
+    x = torch.randn(16, 3, 16, 16, generator=g)
+    y = torch.randint(0, 10, (16,), generator=g)
+    per = 16 // world
+    xs, ys = x[rank * per:(rank + 1) * per].cuda(), y[rank * per:(rank + 1) * per].cuda()
+    p0 = m.arena.data.cpu().clone()
+    st(xs, ys)
+    torch.cuda.synchronize()
+    torch.save({"g": m.arena.grad.cpu(), "p": m.arena.data.cpu(), "p0": p0, "buckets": len(dp.buckets)},
+               os.path.join(out, f"w{world}r{rank}g{int(use_graph)}.pt"))
+    if world > 1:
+        dist.barrier()
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("use_graph", [False, True])
+def test_gpu_dp_two_ranks_equal_single_process(tmp_path, use_graph):
+    mp.spawn(_exact_worker, args=(2, _port(), str(tmp_path), use_graph), nprocs=2, join=True)
+    mp.spawn(_exact_worker, args=(1, _port(), str(tmp_path), use_graph), nprocs=1, join=True)
+    r0 = torch.load(tmp_path / f"w2r0g{int(use_graph)}.pt", weights_only=True)
+    r1 = torch.load(tmp_path / f"w2r1g{int(use_graph)}.pt", weights_only=True)
+    ref = torch.load(tmp_path / f"w1r0g{int(use_graph)}.pt", weights_only=True)
+    assert r0["buckets"] > 2
+    assert torch.equal(r0["p0"], ref["p0"])
+    assert torch.equal(r0["g"], r1["g"]) and torch.equal(r0["p"], r1["p"])
+    # averaged half-batch gradients == whole-batch gradient (fp32; summation order differs)
+    torch.testing.assert_close(r0["g"], ref["g"], rtol=1e-5, atol=1e-6)
+    torch.testing.assert_close(r0["p"], ref["p"], rtol=1e-5, atol=1e-6)

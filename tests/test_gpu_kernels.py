@@ -59,10 +59,10 @@ def test_conv_fwd_dgrad_wgrad(hip, case):
     assert y.shape == y_ref.shape
     assert rel_err(y, y_ref) < 1e-2, rel_err(y, y_ref)
     # BN statistics from the epilogue
-    sums = hip.bn_stats(y, partial)
-    yf = y.float()
-    assert rel_err(sums[:Co], yf.sum((0, 2, 3))) < 1e-3
-    assert rel_err(sums[Co:], (yf * yf).sum((0, 2, 3))) < 1e-3
+    stats = hip.bn_stats(y, partial)  # (mean, biased variance)
+    yf = y.float().double()
+    assert rel_err(stats[:Co], yf.mean((0, 2, 3))) < 1e-4
+    assert rel_err(stats[Co:], yf.var((0, 2, 3), unbiased=False)) < 1e-4
     # dgrad
     dy = torch.randn_like(y_ref)
     dyb = bf(dy)
@@ -163,10 +163,10 @@ def test_stem_conv(hip, case):
     y_ref = F.conv2d(bf(x), bf(w), b, 1, 1)
     assert y.shape == y_ref.shape and y.is_contiguous(memory_format=CL)
     assert rel_err(y, y_ref) < 1e-2, rel_err(y, y_ref)
-    sums = hip.bn_stats(y, partial)
-    yf = y.float()
-    assert rel_err(sums[:Co], yf.sum((0, 2, 3))) < 1e-3
-    assert rel_err(sums[Co:], (yf * yf).sum((0, 2, 3))) < 1e-3
+    stats = hip.bn_stats(y, partial)  # (mean, biased variance)
+    yf = y.float().double()
+    assert rel_err(stats[:Co], yf.mean((0, 2, 3))) < 1e-4
+    assert rel_err(stats[Co:], yf.var((0, 2, 3), unbiased=False)) < 1e-4
     dy = torch.randn(N, Co, H, W)
     dyg = dy.cuda().to(torch.bfloat16).contiguous(memory_format=CL)
     gw = torch.full((Co, Ci, 3, 3), 0.25, device="cuda")
@@ -502,9 +502,9 @@ def test_conv_fp32_fwd_dgrad_wgrad(hip, case):
     y_ref = torch.relu(F.conv2d(x, w, b, s, p) + r)
     assert y.dtype == torch.float32
     assert rel_err(y, y_ref) < 1e-5, rel_err(y, y_ref)
-    sums = hip.bn_stats(y, partial)
-    assert rel_err(sums[:Co], y_ref.sum((0, 2, 3))) < 1e-5
-    assert rel_err(sums[Co:], (y_ref * y_ref).sum((0, 2, 3))) < 1e-5
+    stats = hip.bn_stats(y, partial)  # (mean, biased variance)
+    assert rel_err(stats[:Co], y_ref.double().mean((0, 2, 3))) < 1e-5
+    assert rel_err(stats[Co:], y_ref.double().var((0, 2, 3), unbiased=False)) < 1e-5
     dy = torch.randn_like(y_ref)
     dyg = dy.cuda().contiguous(memory_format=CL)
     wt = hip.conv_weight_t(wg, dtype=torch.float32)
@@ -532,3 +532,63 @@ def test_dense_fp32(hip, shape):
     gw, gb = torch.zeros(Out, In, device="cuda"), torch.zeros(Out, device="cuda")
     hip.dense_wgrad(dy.cuda(), x.cuda(), gw, gb)
     assert rel_err(gw, dy.t() @ x) < 1e-5 and rel_err(gb, dy.sum(0)) < 1e-5
+
+
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+def test_bn_stats_large_mean_matches_fp64(dtype):
+    """mean 1e3, std 1: E[x^2] - mean^2 in fp32 would lose every digit of the variance; the
+    pivot-shifted tile statistics + Chan merges match the fp64 variance to 1e-3 (16384 rows:
+    the two-level ticketed reduce runs)."""
+    torch.manual_seed(11)
+    N, C, H, W = 64, 64, 16, 16
+    x = (1e3 + torch.randn(N, C, H, W)).cuda().to(dtype).contiguous(memory_format=CL)
+    assert hip.kernels().bn_stat_parts(hip.kernels().bn_partial_rows(N * H * W, C)) > 1
+    st = hip.bn_stats(x)
+    xd = x.double()
+    assert rel_err(st[:C], xd.mean((0, 2, 3))) < 1e-6
+    var = xd.var((0, 2, 3), unbiased=False)
+    assert ((st[C:].double().cpu() - var.cpu()).abs() / var.cpu()).max() < 1e-3
+
+
+@pytest.mark.parametrize("shape", [(8, 64, 32, 32, 64), (16, 64, 8, 8, 128), (8, 24, 12, 12, 40), (8, 3, 12, 12, 20)])
+def test_conv_epilogue_stats_large_mean_and_deterministic(shape):
+    """Conv-epilogue BatchNorm statistics (hconv / gemm_g2 / v1 paths) with a 1e3 bias: variance
+    matches fp64 of the stored output to 1e-3, and two runs are bit-identical."""
+    N, Ci, H, W, Co = shape
+    torch.manual_seed(12)
+    x = torch.randn(N, Ci, H, W).cuda().bfloat16().contiguous(memory_format=CL)
+    w = (torch.randn(Co, Ci, 3, 3) / math.sqrt(9 * Ci)).cuda().bfloat16().contiguous(memory_format=CL)
+    b = torch.full((Co,), 1e3, device="cuda")
+    outs = []
+    for _ in range(2):
+        y, partial = hip.conv2d_fwd(x, w, b, (1, 1), (1, 1), stats=True)
+        outs.append((y, hip.bn_stats(y, partial).clone()))
+    (y, st), (y2, st2) = outs
+    assert torch.equal(y, y2) and torch.equal(st, st2)
+    yd = y.double()
+    var = yd.var((0, 2, 3), unbiased=False).cpu()
+    assert rel_err(st[:Co], yd.mean((0, 2, 3))) < 1e-6
+    assert ((st[Co:].double().cpu() - var).abs() / var).max() < 1e-3
+
+
+def test_stat_reduce_many_rows_deterministic():
+    """bn_stat_reduce with several hundred slab rows in both modes: equals an fp64 reference and
+    is bit-identical across runs (ticketed last-block merge in fixed order)."""
+    torch.manual_seed(13)
+    rows, C = 1000, 200
+    n = torch.randint(1, 50, (rows, 1)).float().expand(rows, C)
+    mean = torch.randn(rows, C) * 3 + 7
+    m2 = torch.rand(rows, C) * n
+    slab = torch.stack([n, mean, m2], 1).contiguous().cuda()
+    out = [hip.stat_reduce(0, slab, rows, C, torch.empty(2 * C, device="cuda")).clone() for _ in range(2)]
+    assert torch.equal(out[0], out[1])
+    nd, md, m2d = n.double(), mean.double(), m2.double()
+    tot = nd.sum(0)
+    mu = (nd * md).sum(0) / tot
+    var = (m2d.sum(0) + (nd * (md - mu) ** 2).sum(0)) / tot
+    assert rel_err(out[0][:C], mu) < 1e-6 and rel_err(out[0][C:], var) < 1e-5
+    slab1 = torch.randn(rows, 2, C).cuda()
+    s1 = [hip.stat_reduce(1, slab1, rows, C, torch.empty(2 * C, device="cuda")).clone() for _ in range(2)]
+    assert torch.equal(s1[0], s1[1])
+    ref = slab1.double().sum(0).reshape(-1).cpu()
+    assert (s1[0].double().cpu() - ref).abs().max() < 1e-4

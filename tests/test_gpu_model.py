@@ -126,12 +126,77 @@ def test_graph_replay_matches_eager():
         st2(xs[i], ys[i])
         graph.append(float(st2.last_loss.item()))
     assert st2.graphs is not None and opt2.t == opt.t
-    assert abs(eager[0] - graph[0]) < 1e-2 * abs(eager[0]), (eager, graph)
-    for a, b in zip(eager, graph):
-        assert abs(a - b) < 0.15 * abs(a) + 0.1, (eager, graph)
-    # Adam's normalised update turns order-dependent float-atomic rounding (BN statistics) into
-    # lr-sized parameter differences, so compare trajectories loosely
-    assert rel(m2.arena.data, m.arena.data) < 0.2
+    # deterministic kernels (no float atomics on the training path): bit-identical trajectories
+    assert eager == graph, (eager, graph)
+    assert torch.equal(m2.arena.data, m.arena.data)
+
+
+def test_graph_replay_matches_eager_fp32_sgd():
+    """Same check on the fp32 compute path with SGD + momentum (every state tensor restored)."""
+    from dcnn_amd.models import create_model
+    from dcnn_amd.nn import SGD, LossFactory
+    from dcnn_amd.runtime.step import TrainStep
+    torch.manual_seed(3)
+    xs = [torch.randn(16, 3, 32, 32, device="cuda") for _ in range(2)]
+    ys = [torch.randint(0, 10, (16,), device="cuda") for _ in range(2)]
+    runs = []
+    for use_graph in (False, True):
+        m = create_model("resnet9_cifar10")
+        m.set_seed(9)
+        m.set_device("GPU:0")
+        m.set_compute_dtype(torch.float32)
+        m.initialize()
+        m.set_first_layer_input_grad(False)
+        opt = SGD(0.02, 0.9)
+        opt.attach(m)
+        st = TrainStep(m, LossFactory.create("softmax_crossentropy"), opt, use_graph=use_graph)
+        losses = []
+        for i in [0, 1, 0, 1, 0]:
+            st(xs[i], ys[i])
+            losses.append(float(st.last_loss.item()))
+        runs.append((losses, m.arena.data.cpu().clone(), [b.cpu().clone() for b in _bn_bufs(m)]))
+    (le, pe, be), (lg, pg, bg) = runs
+    for a, b in zip(le, lg):
+        assert abs(a - b) <= 1e-4 * abs(a), (le, lg)
+    torch.testing.assert_close(pg, pe, rtol=1e-4, atol=1e-6)
+    for a, b in zip(be, bg):
+        torch.testing.assert_close(b, a, rtol=1e-4, atol=1e-6)
+
+
+def _bn_bufs(m):
+    from dcnn_amd.parallel.dp import _bn_buffers
+    out = []
+    for l in m.layers:
+        out += _bn_buffers(l)
+    return out
+
+
+def test_dropout_mask_changes_between_graph_replays():
+    """The dropout seed is a constant of the captured graph; the per-forward draw index lives on
+    the device and is bumped inside the graph, so two replays on the same input with lr = 0 give
+    different losses (different masks), and forward/backward of one replay share one mask."""
+    from dcnn_amd.nn import SGD, LossFactory, SequentialBuilder
+    from dcnn_amd.nn.layers import Dropout
+    from dcnn_amd.runtime.step import TrainStep
+    m = (SequentialBuilder("drop").input([64, 1, 1]).flatten().dense(64).activation("relu").dropout(0.5)
+         .dense(10).build())
+    m.set_seed(1)
+    m.set_device("GPU:0")
+    m.initialize()
+    m.set_first_layer_input_grad(False)
+    opt = SGD(0.0)
+    opt.attach(m)
+    st = TrainStep(m, LossFactory.create("softmax_crossentropy"), opt, use_graph=True)
+    x = torch.randn(32, 64, 1, 1, device="cuda")
+    y = torch.randint(0, 10, (32,), device="cuda")
+    losses = []
+    for _ in range(4):
+        st(x, y)
+        losses.append(float(st.last_loss.item()))
+    assert st.graphs is not None
+    assert len(set(losses)) == len(losses), losses
+    drop = [l for l in m.layers if isinstance(l, Dropout)][0]
+    assert int(drop._dev_ctr.item()) >= 4
 
 
 @pytest.mark.parametrize("name", ["resnet18_tiny_imagenet", "resnet50_tiny_imagenet"])
@@ -175,16 +240,18 @@ def test_bwd_bn_fusion_matches_unfused(name, monkeypatch):
         res[fuse] = ([t.float().cpu().clone() for t in m.gradients()], calls["n"])
     (g0, n0), (g1, n1), (g2, _), (g3, _) = res[False], res[True], res["again"], res["fused again"]
     assert n1 < n0, (n0, n1)
-    # float-atomic summation order makes two runs of the SAME path differ already (BN statistics,
-    # amplified through ~20 BatchNorms at batch 16; typically ~20%, occasionally two runs happen
-    # to agree): the fused run must stay within the larger of the two same-path noise floors. The
-    # exact per-kernel equivalence is test_gpu_kernels.py::test_dgrad_bwd_bn_fusion.
+    # deterministic reductions: repeating a path is bit-exact
+    for a, c in zip(g0, g2):
+        assert torch.equal(a, c)
+    for b, d in zip(g1, g3):
+        assert torch.equal(b, d)
+    # fused vs unfused differ only by bf16 rounding points (the fused path masks/rounds the
+    # gradient in the dgrad epilogue), amplified through the BatchNorm chain at batch 16
     scale = max(a.norm().item() for a in g0)
-    for j, (a, b, c, d) in enumerate(zip(g0, g1, g2, g3)):
+    for j, (a, b) in enumerate(zip(g0, g1)):
         den = max(a.norm().item(), 0.05 * scale)
         e = (a - b).norm().item() / den
-        noise = max((a - c).norm().item(), (b - d).norm().item()) / den
-        assert e < 2.5 * noise + 0.02, (j, e, noise)
+        assert e < 1e-2, (j, e)
 
 
 def test_training_decreases_loss():
