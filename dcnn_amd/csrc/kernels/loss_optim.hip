@@ -15,12 +15,10 @@ namespace dcnn {
 
 enum LossType { kCE = 0, kSoftmaxCE = 1, kLogSoftmaxCE = 2, kMSE = 3, kMAE = 4, kHuber = 5 };
 
-// One workgroup of 16 waves; wave w takes rows w, w + 16, ... (a batch is <= a few thousand
-// rows of <= a few thousand classes: microseconds of work). Per-wave loss / correct partials meet
-// in LDS and are summed in wave order: the loss is bit-reproducible (no float atomics) and no
-// memset of the outputs is needed.
-constexpr int kLossWaves = 16;
-
+// One wave per sample row (4 rows per workgroup). Each row's loss and hit are written to a
+// workspace; the workgroups then take a ticket and the last one sums the N row values in a
+// fixed pairwise order (agent release / acquire around the ticket): the loss is bit-reproducible
+// with no float atomics and no memset of the outputs.
 template <typename T>
 __device__ __forceinline__ void loss_row(const T* __restrict__ pred, const float* __restrict__ target,
                                          const int64_t* __restrict__ labels, T* __restrict__ grad, int row, int N,
@@ -95,38 +93,76 @@ __device__ __forceinline__ void loss_row(const T* __restrict__ pred, const float
 }
 
 template <typename T>
-__global__ void __launch_bounds__(kLossWaves * 64) loss_kernel(const T* __restrict__ pred,
-                                                              const float* __restrict__ target,
-                                                              const int64_t* __restrict__ labels,
-                                                              T* __restrict__ grad, float* __restrict__ loss_out,
-                                                              int* __restrict__ correct, int N, int C, int type,
-                                                              float param) {
-  __shared__ float wl[kLossWaves];
-  __shared__ int wc[kLossWaves];
+__global__ void __launch_bounds__(256) loss_kernel(const T* __restrict__ pred, const float* __restrict__ target,
+                                                   const int64_t* __restrict__ labels, T* __restrict__ grad,
+                                                   float* __restrict__ loss_out, int* __restrict__ correct, int N,
+                                                   int C, int type, float param, float* __restrict__ rowv,
+                                                   unsigned* __restrict__ ticket) {
+  __shared__ float sl[256];
+  __shared__ int sc[256];
+  __shared__ int last;
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int row = blockIdx.x * 4 + w;
   float lsum = 0.f;
   int hits = 0;
-  for (int row = w; row < N; row += kLossWaves)
-    loss_row<T>(pred, target, labels, grad, row, N, C, type, param, lane, &lsum, &hits);
-  if (lane == 0) { wl[w] = lsum; wc[w] = hits; }
+  if (row < N) loss_row<T>(pred, target, labels, grad, row, N, C, type, param, lane, &lsum, &hits);
+  if (gridDim.x == 1) {
+    if (lane == 0) { sl[w] = lsum; sc[w] = hits; }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      *loss_out = (sl[0] + sl[1]) + (sl[2] + sl[3]);
+      if (correct) *correct = sc[0] + sc[1] + sc[2] + sc[3];
+    }
+    return;
+  }
+  if (lane == 0 && row < N) {
+    rowv[row] = lsum;
+    reinterpret_cast<int*>(rowv + N)[row] = hits;
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
   if (threadIdx.x == 0) {
-    float l = 0.f;
-    int h = 0;
-    for (int k = 0; k < kLossWaves; ++k) { l += wl[k]; h += wc[k]; }
-    *loss_out = l;
-    if (correct) *correct = h;
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    const unsigned old = __hip_atomic_fetch_add(ticket, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    last = old == gridDim.x - 1;
+    if (last) {
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+  }
+  __syncthreads();
+  if (!last) return;
+  // last workgroup: thread t sums rows t, t + 256, ... in order, then a fixed LDS tree
+  float l = 0.f;
+  int h = 0;
+  for (int r = threadIdx.x; r < N; r += 256) { l += rowv[r]; h += reinterpret_cast<const int*>(rowv + N)[r]; }
+  sl[threadIdx.x] = l;
+  sc[threadIdx.x] = h;
+  __syncthreads();
+  for (int o = 128; o > 0; o >>= 1) {
+    if (threadIdx.x < o) { sl[threadIdx.x] += sl[threadIdx.x + o]; sc[threadIdx.x] += sc[threadIdx.x + o]; }
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) {
+    *loss_out = sl[0];
+    if (correct) *correct = sc[0];
+    *ticket = 0u;  // ready for the next loss on this stream
   }
 }
 
+int loss_workspace_floats(int N) { return 2 * N; }
+
 void loss_fused(int dt, const void* pred, const float* target, const int64_t* labels, void* grad, float* loss_out,
-                int* correct, int N, int C, int type, float param, hipStream_t s) {
+                int* correct, int N, int C, int type, float param, float* ws, unsigned* ticket, hipStream_t s) {
+  const int blocks = (N + 3) / 4;
+  if (blocks > 1 && (!ws || !ticket)) throw std::runtime_error("loss_fused: workspace required");
   if (dt == 0)
-    hipLaunchKernelGGL(loss_kernel<float>, dim3(1), dim3(kLossWaves * 64), 0, s, (const float*)pred, target, labels,
-                       (float*)grad, loss_out, correct, N, C, type, param);
+    hipLaunchKernelGGL(loss_kernel<float>, dim3(blocks), dim3(256), 0, s, (const float*)pred, target, labels,
+                       (float*)grad, loss_out, correct, N, C, type, param, ws, ticket);
   else
-    hipLaunchKernelGGL(loss_kernel<bf16>, dim3(1), dim3(kLossWaves * 64), 0, s, (const bf16*)pred, target, labels,
-                       (bf16*)grad, loss_out, correct, N, C, type, param);
+    hipLaunchKernelGGL(loss_kernel<bf16>, dim3(blocks), dim3(256), 0, s, (const bf16*)pred, target, labels,
+                       (bf16*)grad, loss_out, correct, N, C, type, param, ws, ticket);
   DCNN_LAUNCH_CHECK();
 }
 

@@ -146,8 +146,8 @@ __global__ void __launch_bounds__(256) bn_partial_kernel(const T* __restrict__ x
 // Deterministic statistics reduce: slab rows -> stats[2][C]
 //   MODE 0: rows are (count, mean, M2) triples -> stats = (mean, biased variance)
 //   MODE 1: rows are (sum a, sum b) pairs      -> stats = (sum a, sum b)
-// Grid (C/64, ny): lane = channel, each block merges up to 256 rows (each wave up to 4 chunks of
-// 16, all loads of a chunk in flight) in row order. With ny > 1 the blocks publish their partials
+// Grid (C/64, ny): lane = channel, each block merges 64 rows (each wave 16, all loads in flight,
+// pairwise tree) in row order. With ny > 1 the blocks publish their partials
 // (agent release) and take a ticket; the last block of a channel column merges the ny partials
 // in block order (agent acquire). Every merge order is fixed: the result does not depend on timing.
 // ---------------------------------------------------------------------------------------
@@ -164,28 +164,33 @@ struct StatAcc {
     }
   }
 };
-constexpr int kStatRW = 16, kStatChunks = 4, kStatRowsPerBlock = 4 * kStatRW * kStatChunks;
+constexpr int kStatRW = 16, kStatRowsPerBlock = 4 * kStatRW;
 
-template <int MODE>
-__device__ __forceinline__ StatAcc<MODE> stat_rows(const float* __restrict__ src, int r0, int r1, int C, int c) {
+// Merge up to kStatRW rows [r0, r1) of channel c: every load in flight at once, then a pairwise
+// tree (log2 16 = 4 dependent merge levels instead of a 16-long chain). Fixed order.
+template <int MODE, int NR>
+__device__ __forceinline__ StatAcc<MODE> stat_tree(const float* __restrict__ src, long stride_row, int r0, int r1,
+                                                   int C, int c) {
   constexpr int NV = MODE == 0 ? 3 : 2;
-  StatAcc<MODE> acc = StatAcc<MODE>::zero();
-  for (int rb = r0; rb < r1; rb += kStatRW) {
-    float v[kStatRW][NV];
+  StatAcc<MODE> v[NR];
 #pragma unroll
-    for (int j = 0; j < kStatRW; ++j)
-#pragma unroll
-      for (int k = 0; k < NV; ++k) v[j][k] = (rb + j < r1) ? src[((long)(rb + j) * NV + k) * C + c] : 0.f;
-#pragma unroll
-    for (int j = 0; j < kStatRW; ++j) acc = acc.merge(StatAcc<MODE>{v[j][0], v[j][1], v[j][NV - 1]});
+  for (int j = 0; j < NR; ++j) {
+    const bool ok = r0 + j < r1;
+    const float* q = src + (long)(r0 + j) * stride_row + c;
+    v[j] = ok ? StatAcc<MODE>{q[0], q[C], NV == 3 ? q[(NV - 1) * C] : 0.f} : StatAcc<MODE>::zero();
   }
-  return acc;
+#pragma unroll
+  for (int w = 1; w < NR; w *= 2)
+#pragma unroll
+    for (int j = 0; j + w < NR; j += 2 * w) v[j] = v[j].merge(v[j + w]);
+  return v[0];
 }
 
 template <int MODE>
 __global__ void __launch_bounds__(256) bn_stat_reduce_kernel(const float* __restrict__ slab, int rows, int C,
                                                              float* __restrict__ part, unsigned* __restrict__ ticket,
                                                              float* __restrict__ out) {
+  constexpr int NV = MODE == 0 ? 3 : 2;
   __shared__ StatAcc<MODE> red[4][64];
   __shared__ int last;
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
@@ -201,19 +206,18 @@ __global__ void __launch_bounds__(256) bn_stat_reduce_kernel(const float* __rest
       out[C + c] = t.b;
     }
   };
-  // ---- level 1: this block's rows, wave w takes a contiguous quarter ----
-  const int b0 = by * kStatRowsPerBlock, b1 = min(rows, b0 + kStatRowsPerBlock);
-  const int q = (b1 - b0 + 3) / 4;
-  const int w0 = min(b1, b0 + w * q), w1 = min(b1, w0 + q);
-  red[w][lane] = cok ? stat_rows<MODE>(slab, w0, w1, C, c) : StatAcc<MODE>::zero();
+  // ---- level 1: wave w merges rows [b0 + 16w, b0 + 16w + 16) of this block ----
+  const int w0 = by * kStatRowsPerBlock + w * kStatRW;
+  red[w][lane] = cok ? stat_tree<MODE, kStatRW>(slab, (long)NV * C, w0, min(rows, w0 + kStatRW), C, c)
+                     : StatAcc<MODE>::zero();
   __syncthreads();
   if (ny == 1) {
-    if (w == 0 && cok) finish(red[0][lane].merge(red[1][lane]).merge(red[2][lane]).merge(red[3][lane]));
+    if (w == 0 && cok) finish(red[0][lane].merge(red[1][lane]).merge(red[2][lane].merge(red[3][lane])));
     return;
   }
   if (w == 0) {
     if (cok) {
-      const StatAcc<MODE> t = red[0][lane].merge(red[1][lane]).merge(red[2][lane]).merge(red[3][lane]);
+      const StatAcc<MODE> t = red[0][lane].merge(red[1][lane]).merge(red[2][lane].merge(red[3][lane]));
       part[((long)by * 3 + 0) * C + c] = t.a;
       part[((long)by * 3 + 1) * C + c] = t.b;
       part[((long)by * 3 + 2) * C + c] = t.c;
@@ -233,18 +237,16 @@ __global__ void __launch_bounds__(256) bn_stat_reduce_kernel(const float* __rest
   }
   __syncthreads();
   if (!last) return;
-  // ---- level 2 (last block of this channel column): partials in block order ----
-  const int pq = (ny + 3) / 4, p0 = min(ny, w * pq), p1 = min(ny, p0 + pq);
+  // ---- level 2 (last block of this channel column): wave w merges partials [16w, 16w + 16) ----
   StatAcc<MODE> t = StatAcc<MODE>::zero();
   if (cok)
-    for (int k = p0; k < p1; ++k)
-      t = t.merge(StatAcc<MODE>{part[((long)k * 3 + 0) * C + c], part[((long)k * 3 + 1) * C + c],
-                                part[((long)k * 3 + 2) * C + c]});
+    for (int k0 = w * kStatRW; k0 < ny; k0 += 4 * kStatRW)
+      t = t.merge(stat_tree<MODE, kStatRW>(part, 3L * C, k0, min(ny, k0 + kStatRW), C, c));
   __syncthreads();
   red[w][lane] = t;
   __syncthreads();
   if (w == 0) {
-    if (cok) finish(red[0][lane].merge(red[1][lane]).merge(red[2][lane]).merge(red[3][lane]));
+    if (cok) finish(red[0][lane].merge(red[1][lane]).merge(red[2][lane].merge(red[3][lane])));
     if (lane == 0) ticket[blockIdx.x] = 0u;  // ready for the next reduce on this stream
   }
 }

@@ -566,10 +566,11 @@ def _rc(x):
 _tickets = {}
 
 
-def _ticket(device, C):
-    """Per-(stream, device) ticket words of bn_stat_reduce (zeroed once; every reduce leaves
-    them zeroed again, and reduces on one stream never overlap)."""
-    key = (stream_ptr(), device.index)
+def _ticket(device, C, slot="stat"):
+    """Per-(stream, device, user) ticket words of the ticketed reductions (bn_stat_reduce, the
+    loss): zeroed once, every launch leaves them zeroed again, and launches on one stream never
+    overlap."""
+    key = (stream_ptr(), device.index, slot)
     t = _tickets.get(key)
     need = (C + 63) // 64
     if t is None or t.numel() < need:
@@ -841,8 +842,11 @@ def loss_fused(pred2d, target2d=None, labels=None, kind="softmax_crossentropy", 
     if target2d is not None:
         tgt = target2d.reshape(N, C).to(F32).contiguous()
     lab = labels.to(torch.int64).contiguous() if labels is not None else None
-    kernels().loss_fused(dt_code(pred2d.dtype), pred2d.data_ptr(), ptr(tgt), ptr(lab), ptr(grad), loss.data_ptr(),
-                         correct.data_ptr(), N, C, LOSS_CODES[kind], float(param), stream_ptr())
+    K = kernels()
+    ws = torch.empty((K.loss_workspace_floats(N),), dtype=F32, device=pred2d.device) if N > 4 else None
+    tk = _ticket(pred2d.device, 0, slot="loss") if N > 4 else None
+    K.loss_fused(dt_code(pred2d.dtype), pred2d.data_ptr(), ptr(tgt), ptr(lab), ptr(grad), loss.data_ptr(),
+                 correct.data_ptr(), N, C, LOSS_CODES[kind], float(param), ptr(ws), ptr(tk), stream_ptr())
     return loss, grad, correct
 
 

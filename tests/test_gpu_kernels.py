@@ -535,7 +535,7 @@ def test_dense_fp32(hip, shape):
 
 
 @pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
-def test_bn_stats_large_mean_matches_fp64(dtype):
+def test_bn_stats_large_mean_matches_fp64(hip, dtype):
     """mean 1e3, std 1: E[x^2] - mean^2 in fp32 would lose every digit of the variance; the
     pivot-shifted tile statistics + Chan merges match the fp64 variance to 1e-3 (16384 rows:
     the two-level ticketed reduce runs)."""
@@ -551,7 +551,7 @@ def test_bn_stats_large_mean_matches_fp64(dtype):
 
 
 @pytest.mark.parametrize("shape", [(8, 64, 32, 32, 64), (16, 64, 8, 8, 128), (8, 24, 12, 12, 40), (8, 3, 12, 12, 20)])
-def test_conv_epilogue_stats_large_mean_and_deterministic(shape):
+def test_conv_epilogue_stats_large_mean_and_deterministic(hip, shape):
     """Conv-epilogue BatchNorm statistics (hconv / gemm_g2 / v1 paths) with a 1e3 bias: variance
     matches fp64 of the stored output to 1e-3, and two runs are bit-identical."""
     N, Ci, H, W, Co = shape
@@ -571,7 +571,7 @@ def test_conv_epilogue_stats_large_mean_and_deterministic(shape):
     assert ((st[Co:].double().cpu() - var).abs() / var).max() < 1e-3
 
 
-def test_stat_reduce_many_rows_deterministic():
+def test_stat_reduce_many_rows_deterministic(hip):
     """bn_stat_reduce with several hundred slab rows in both modes: equals an fp64 reference and
     is bit-identical across runs (ticketed last-block merge in fixed order)."""
     torch.manual_seed(13)
