@@ -146,8 +146,8 @@ __global__ void __launch_bounds__(256) bn_partial_kernel(const T* __restrict__ x
 // Deterministic statistics reduce: slab rows -> stats[2][C]
 //   MODE 0: rows are (count, mean, M2) triples -> stats = (mean, biased variance)
 //   MODE 1: rows are (sum a, sum b) pairs      -> stats = (sum a, sum b)
-// Grid (C/64, ny): lane = channel, each block merges 64 rows (each wave 16, all loads in flight,
-// pairwise tree) in row order. With ny > 1 the blocks publish their partials
+// Grid (C/64, ny): lane = channel, each 1024-thread block merges 256 rows (each of its 16 waves
+// 16 rows, all loads in flight, pairwise trees in registers and then across the waves in LDS). With ny > 1 the blocks publish their partials
 // (agent release) and take a ticket; the last block of a channel column merges the ny partials
 // in block order (agent acquire). Every merge order is fixed: the result does not depend on timing.
 // ---------------------------------------------------------------------------------------
@@ -164,7 +164,7 @@ struct StatAcc {
     }
   }
 };
-constexpr int kStatRW = 16, kStatRowsPerBlock = 4 * kStatRW;
+constexpr int kStatRW = 16, kStatWaves = 16, kStatRowsPerBlock = kStatWaves * kStatRW;
 
 // Merge up to kStatRW rows [r0, r1) of channel c: every load in flight at once, then a pairwise
 // tree (log2 16 = 4 dependent merge levels instead of a 16-long chain). Fixed order.
@@ -186,12 +186,23 @@ __device__ __forceinline__ StatAcc<MODE> stat_tree(const float* __restrict__ src
   return v[0];
 }
 
+// the 16 waves' results in LDS merged by a fixed pairwise tree; result in red[0][lane]
 template <int MODE>
-__global__ void __launch_bounds__(256) bn_stat_reduce_kernel(const float* __restrict__ slab, int rows, int C,
-                                                             float* __restrict__ part, unsigned* __restrict__ ticket,
-                                                             float* __restrict__ out) {
+__device__ __forceinline__ void stat_tree_lds(StatAcc<MODE> (*red)[64], int w, int lane) {
+#pragma unroll
+  for (int o = kStatWaves / 2; o > 0; o >>= 1) {
+    __syncthreads();
+    if (w < o) red[w][lane] = red[w][lane].merge(red[w + o][lane]);
+  }
+  __syncthreads();
+}
+
+template <int MODE>
+__global__ void __launch_bounds__(1024) bn_stat_reduce_kernel(const float* __restrict__ slab, int rows, int C,
+                                                              float* __restrict__ part, unsigned* __restrict__ ticket,
+                                                              float* __restrict__ out) {
   constexpr int NV = MODE == 0 ? 3 : 2;
-  __shared__ StatAcc<MODE> red[4][64];
+  __shared__ StatAcc<MODE> red[kStatWaves][64];
   __shared__ int last;
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   const int c = blockIdx.x * 64 + lane;
@@ -210,14 +221,14 @@ __global__ void __launch_bounds__(256) bn_stat_reduce_kernel(const float* __rest
   const int w0 = by * kStatRowsPerBlock + w * kStatRW;
   red[w][lane] = cok ? stat_tree<MODE, kStatRW>(slab, (long)NV * C, w0, min(rows, w0 + kStatRW), C, c)
                      : StatAcc<MODE>::zero();
-  __syncthreads();
+  stat_tree_lds<MODE>(red, w, lane);
   if (ny == 1) {
-    if (w == 0 && cok) finish(red[0][lane].merge(red[1][lane]).merge(red[2][lane].merge(red[3][lane])));
+    if (w == 0 && cok) finish(red[0][lane]);
     return;
   }
   if (w == 0) {
     if (cok) {
-      const StatAcc<MODE> t = red[0][lane].merge(red[1][lane]).merge(red[2][lane].merge(red[3][lane]));
+      const StatAcc<MODE> t = red[0][lane];
       part[((long)by * 3 + 0) * C + c] = t.a;
       part[((long)by * 3 + 1) * C + c] = t.b;
       part[((long)by * 3 + 2) * C + c] = t.c;
@@ -240,13 +251,12 @@ __global__ void __launch_bounds__(256) bn_stat_reduce_kernel(const float* __rest
   // ---- level 2 (last block of this channel column): wave w merges partials [16w, 16w + 16) ----
   StatAcc<MODE> t = StatAcc<MODE>::zero();
   if (cok)
-    for (int k0 = w * kStatRW; k0 < ny; k0 += 4 * kStatRW)
+    for (int k0 = w * kStatRW; k0 < ny; k0 += kStatRowsPerBlock)
       t = t.merge(stat_tree<MODE, kStatRW>(part, 3L * C, k0, min(ny, k0 + kStatRW), C, c));
-  __syncthreads();
   red[w][lane] = t;
-  __syncthreads();
+  stat_tree_lds<MODE>(red, w, lane);
   if (w == 0) {
-    if (cok) finish(red[0][lane].merge(red[1][lane]).merge(red[2][lane].merge(red[3][lane])));
+    if (cok) finish(red[0][lane]);
     if (lane == 0) ticket[blockIdx.x] = 0u;  // ready for the next reduce on this stream
   }
 }
@@ -562,9 +572,9 @@ void bn_stat_reduce(int mode, const float* slab, int rows, int C, float* out, fl
   if (ny > 1 && (!part || !ticket)) throw std::runtime_error("bn_stat_reduce: workspace required");
   const dim3 grid((unsigned)((C + 63) / 64), (unsigned)ny);
   if (mode == 0)
-    hipLaunchKernelGGL(bn_stat_reduce_kernel<0>, grid, dim3(256), 0, s, slab, rows, C, part, ticket, out);
+    hipLaunchKernelGGL(bn_stat_reduce_kernel<0>, grid, dim3(64 * kStatWaves), 0, s, slab, rows, C, part, ticket, out);
   else
-    hipLaunchKernelGGL(bn_stat_reduce_kernel<1>, grid, dim3(256), 0, s, slab, rows, C, part, ticket, out);
+    hipLaunchKernelGGL(bn_stat_reduce_kernel<1>, grid, dim3(64 * kStatWaves), 0, s, slab, rows, C, part, ticket, out);
   DCNN_LAUNCH_CHECK();
 }
 
