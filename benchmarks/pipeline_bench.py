@@ -38,6 +38,8 @@ def main(argv=None):
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--partitioner", default="flops", choices=["flops", "naive"])
     ap.add_argument("--cpu", action="store_true")
+    ap.add_argument("--no-graph", action="store_true", help="eager stages (no per-micro-batch hipGraphs)")
+    ap.add_argument("--profiling", action="store_true", help="per-layer HIP-event timings on eager steps")
     a = ap.parse_args(argv)
 
     from dcnn_amd.models import zoo
@@ -53,7 +55,8 @@ def main(argv=None):
     coord = InProcessCoordinator(model, Adam(1e-3), "softmax_crossentropy", num_stages=a.stages,
                                  num_microbatches=a.microbatches,
                                  partitioner=create_partitioner(a.partitioner, [a.batch // a.microbatches] + in_shape),
-                                 device=devs[0], stage_devices=devs, seed=1234)
+                                 device=devs[0], stage_devices=devs, seed=1234,
+                                 use_graph=use_gpu and not a.no_graph, profiling=a.profiling)
     dev = torch.device("cuda", 0) if use_gpu else torch.device("cpu")
     try:
         coord.initialize()
@@ -81,7 +84,7 @@ def main(argv=None):
         dt = time.perf_counter() - t0
         res = {"metric": f"pipeline images/sec {a.model}", "value": round(a.batch * a.steps / dt, 1),
                "unit": "images/sec", "stages": a.stages, "gpus": max(ngpu, 0), "stage_devices": devs,
-               "schedule": a.schedule, "microbatches": a.microbatches, "batch": a.batch,
+               "schedule": a.schedule, "hipgraph": use_gpu and not a.no_graph, "microbatches": a.microbatches, "batch": a.batch,
                "ms_per_step": round(dt / a.steps * 1e3, 3), "steps": a.steps, "warmup": a.warmup,
                "dtype": "bf16" if use_gpu else "fp32", "data": "synthetic", "coordinator": "in_process",
                "partitions": [(p.start_layer, p.end_layer) for p in coord.partitions],

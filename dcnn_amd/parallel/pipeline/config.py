@@ -51,6 +51,7 @@ class StageConfig:
     first_layer_input_grad: bool = False     # stage 0 does not return dL/dinput (reference G9)
     ranks: Optional[Dict[str, int]] = None   # torch.distributed ranks: {"prev": r, "next": r, "coordinator": r}
     profiling: bool = True
+    use_graph: bool = False                  # GPU: replay per-micro-batch hipGraphs after the first step
 
     def to_json(self) -> dict:
         d = dict(self.__dict__)

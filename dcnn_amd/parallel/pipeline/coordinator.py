@@ -49,7 +49,7 @@ class Coordinator:
                  partitioner: Optional[Partitioner] = None, input_shape: Optional[Sequence[int]] = None,
                  device: str = "CPU", stage_devices: Optional[Sequence[str]] = None, transport: str = "message",
                  codec: str = "none", grad_scale: str = "mean", seed: Optional[int] = None,
-                 timeout_s: float = 120.0):
+                 timeout_s: float = 120.0, use_graph: Optional[bool] = None, profiling: bool = True):
         self.model = model
         self.optimizer_config = optimizer.get_config() if hasattr(optimizer, "get_config") else dict(optimizer)
         self.loss: Loss = LossFactory.create(loss) if isinstance(loss, str) else loss
@@ -64,6 +64,8 @@ class Coordinator:
         self.grad_scale = grad_scale
         self.seed = seed
         self.timeout_s = timeout_s
+        self.use_graph = use_graph        # None: hipGraph replay on every GPU stage
+        self.profiling = bool(profiling)  # per-layer timings (eager steps) for balance_load
         self.stage_names = [f"stage_{i}" for i in range(self.num_stages)]
         self.partitions: List[Partition] = []
         self.stage_configs: List[StageConfig] = []
@@ -93,7 +95,9 @@ class Coordinator:
                 stage_id=self.stage_names[i], stage_index=i, num_stages=self.num_stages,
                 model_config=self.model.get_config(part), optimizer_config=dict(self.optimizer_config),
                 device=self.stage_devices[i], transport=self.transport_kind, codec=self.codec,
-                seed=None if self.seed is None else self.seed + i))
+                seed=None if self.seed is None else self.seed + i, profiling=self.profiling,
+                use_graph=(self.stage_devices[i].upper().startswith("GPU") if self.use_graph is None
+                           else bool(self.use_graph))))
         self._init_topology()
 
     def _init_topology(self) -> None:
@@ -168,10 +172,23 @@ class Coordinator:
         return self.transport.recv(msg, self.device)
 
     def _loss_grad(self, out, y, mb):
-        loss, grad, correct = self.loss.loss_and_grad(out, y.to(out.device))
+        loss, grad, correct = self.loss.loss_and_grad(out, y.to(out.device, non_blocking=True))
         if self.grad_scale == "mean" and self.num_microbatches > 1:
-            grad = grad * (1.0 / self.num_microbatches)
+            grad = grad.mul_(1.0 / self.num_microbatches)
         return loss, grad.to(out.dtype), correct
+
+    def _finish(self, losses, corrects) -> float:
+        """ONE host sync per step: the micro-batch losses / correct counts stay on the device
+        until every backward has been issued."""
+        m = max(len(losses), 1)
+        if not losses:
+            self.last_correct = 0
+            return 0.0
+        tot = torch.stack([l.reshape(()).float() for l in losses]).sum()
+        cor = torch.stack([c.reshape(()).to(torch.int64) for c in corrects]).sum()
+        both = torch.stack([tot.double(), cor.double()]).cpu()
+        self.last_correct = int(both[1])
+        return float(both[0]) / m
 
     # ------------------------------------------------------------------ schedules
     def split(self, x: torch.Tensor, y: torch.Tensor):
@@ -194,21 +211,20 @@ class Coordinator:
         outs = {}
         for msg in self.join(C.FORWARD_JOB, m):
             outs[int(msg.mb_id)] = self._output(msg)
-        total, correct = 0.0, 0
+        losses, corrects = [], []
         for i in range(m):
             loss, grad, c = self._loss_grad(outs[i], ys[i], i)
-            total += float(loss)
-            correct += int(c)
+            losses.append(loss)
+            corrects.append(c)
             self.backward(grad, i)
         self.join(C.BACKWARD_JOB, m)
-        self.last_correct = correct
-        return total / max(m, 1)
+        return self._finish(losses, corrects)
 
     def async_process_batch(self, xs: Sequence[torch.Tensor], ys: Sequence[torch.Tensor]) -> float:
         m = len(xs)
         for i in range(m):
             self.forward(xs[i], i)
-        total, correct, done = 0.0, 0, 0
+        losses, corrects, done = [], [], 0
         deadline = time.time() + self.timeout_s
         while done < m:
             self._check_errors()
@@ -221,12 +237,11 @@ class Coordinator:
             out = self._output(msg)
             loss, grad, c = self._loss_grad(out, ys[mb], mb)
             self.backward(grad, mb)
-            total += float(loss)
-            correct += int(c)
+            losses.append(loss)
+            corrects.append(c)
             done += 1
         self.join(C.BACKWARD_JOB, m)
-        self.last_correct = correct
-        return total / max(m, 1)
+        return self._finish(losses, corrects)
 
     def train_step(self, x: torch.Tensor, y: torch.Tensor, schedule: str = "semi_async") -> float:
         xs, ys = self.split(x, y)
@@ -240,13 +255,14 @@ class Coordinator:
         xs, ys = self.split(x, y)
         for i, xi in enumerate(xs):
             self.forward(xi, i)
-        total, correct = 0.0, 0
+        losses, corrects = [], []
         for msg in self.join(C.FORWARD_JOB, len(xs)):
             out = self._output(msg)
             loss, _, c = self.loss.loss_and_grad(out, ys[int(msg.mb_id)].to(out.device), want_grad=False)
-            total += float(loss)
-            correct += int(c)
-        return total / len(xs), correct
+            losses.append(loss)
+            corrects.append(c)
+        mean = self._finish(losses, corrects)
+        return mean, self.last_correct
 
     def update_parameters(self) -> None:
         """UPDATE_PARAMETERS broadcast; a pending learning-rate change rides along as JSON."""

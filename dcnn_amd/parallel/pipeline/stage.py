@@ -10,7 +10,11 @@ purpose:
 * handler failures are reported to the coordinator (ERROR_REPORT / JOB_FAILURE with the
   traceback) instead of killing the stage;
 * stage 0 does not ship the unused input gradient back (SURVEY G9) unless asked to;
-* activations stay in the stage's compute dtype (bf16 on MI355X) end to end.
+* activations stay in the stage's compute dtype (bf16 on MI355X) end to end;
+* a GPU stage runs on its own HIP stream (stages sharing a GPU overlap instead of serialising
+  on the null stream) with its device current on the stage thread, and from its second training
+  step on replays per-micro-batch hipGraphs (``graphs.StageGraphs``) instead of launching every
+  layer op from Python.
 """
 from __future__ import annotations
 
@@ -28,6 +32,7 @@ from ...nn.sequential import Sequential, _all_layers
 from ...nn.layers import BatchNorm
 from . import messages as M
 from .config import StageConfig
+from .graphs import StageGraphs
 from .transport import LocalTransport, MessageTransport, P2PTransport
 
 C = M.CommandType
@@ -78,6 +83,9 @@ class PipelineStage:
         self.fwd_ms = []
         self.bwd_ms = []
         self.last_error: Optional[str] = None
+        self.stream: Optional[torch.cuda.Stream] = None
+        self.graphs: Optional[StageGraphs] = None
+        self.steps_done = 0
 
     # ------------------------------------------------------------------ loop
     def run(self, poll_ms: int = 200) -> None:
@@ -118,6 +126,13 @@ class PipelineStage:
 
     # ------------------------------------------------------------------ dispatch
     def process_message(self, msg) -> None:
+        if self.stream is not None:
+            with torch.cuda.device(self.stream.device), torch.cuda.stream(self.stream):
+                self._process(msg)
+        else:
+            self._process(msg)
+
+    def _process(self, msg) -> None:
         cmd = msg.command
         try:
             if cmd == C.FORWARD_JOB:
@@ -132,6 +147,7 @@ class PipelineStage:
                 self.optimizer.update()
                 self.optimizer.clear_gradients()
                 self.counts["update"] += 1
+                self.steps_done += 1
                 self._reply(C.PARAMETERS_UPDATED)
             elif cmd == C.TRAIN_MODE:
                 self.model.set_training(True)
@@ -195,6 +211,13 @@ class PipelineStage:
         dev = cfg.device
         if dev.upper().startswith("GPU") and not torch.cuda.is_available():
             raise RuntimeError(f"{self.id}: GPU requested but no GPU is visible")
+        self.stream = None
+        self.graphs = None
+        self.steps_done = 0
+        if dev.upper().startswith("GPU"):
+            idx = int(dev.split(":")[1]) if ":" in dev else 0
+            self.stream = torch.cuda.Stream(device=idx)
+            torch.cuda.set_device(idx)
         model.set_device(dev)
         if cfg.compute_dtype not in ("auto", "", None):
             model.set_compute_dtype(getattr(torch, cfg.compute_dtype))
@@ -204,6 +227,11 @@ class PipelineStage:
         self.model = model
         self.optimizer = OptimizerFactory.create_from_config(cfg.optimizer_config)
         self.optimizer.attach(model)
+        if self.stream is not None:
+            # initialisation ran on this thread's default stream; order the stage stream after it
+            self.stream.wait_stream(torch.cuda.current_stream(self.stream.device))
+            if cfg.use_graph:
+                self.graphs = StageGraphs(model, self.stream)
         if hasattr(self.comm, "set_id"):  # network worker: adopt the stage name before dialing peers
             self.comm.set_id(cfg.stage_id)
             self.id = cfg.stage_id
@@ -256,7 +284,12 @@ class PipelineStage:
         mb = int(msg.mb_id)
         t0 = time.perf_counter()
         x = self.transport.recv(msg, self._device())
-        out = self.model.forward(x, mb, return_on_input_device=False)
+        if self._graph_ok():
+            out = self.graphs.forward(x, mb)
+        else:
+            if self.graphs is not None:
+                self.graphs.forget_forward(mb)
+            out = self.model.forward(x, mb, return_on_input_device=False)
         last = self.cfg.stage_index == self.cfg.num_stages - 1
         self.transport.send(self.comm, "coordinator" if last else "next_stage", C.FORWARD_JOB, mb, out)
         self.counts["forward"] += 1
@@ -266,7 +299,10 @@ class PipelineStage:
         mb = int(msg.mb_id)
         t0 = time.perf_counter()
         g = self.transport.recv(msg, self._device())
-        gin = self.model.backward(g, mb, return_on_input_device=False)
+        if self.graphs is not None and self.graphs.can_backward(mb):
+            gin = self.graphs.backward(g, mb)
+        else:
+            gin = self.model.backward(g, mb, return_on_input_device=False)
         first = self.cfg.stage_index == 0
         if first and not self.cfg.first_layer_input_grad:
             gin = None
@@ -274,9 +310,16 @@ class PipelineStage:
         self.counts["backward"] += 1
         self.bwd_ms.append((time.perf_counter() - t0) * 1e3)
 
+    def _graph_ok(self) -> bool:
+        """Replay graphs once one eager training step has run (allocations settled, per-layer
+        profile recorded) and only for training forwards."""
+        return self.graphs is not None and self.steps_done >= 1 and self.model.training
+
     def status(self) -> dict:
         m = self.model
         d = {"id": self.id, "counts": dict(self.counts), "pid": os.getpid()}
+        if self.graphs is not None:
+            d["graphs"] = {"captures": self.graphs.captures, "replays": self.graphs.replays}
         if m is not None:
             d.update(device=str(m.device.torch_device), layers=[l.name for l in m.layers],
                      num_parameters=m.num_parameters(),

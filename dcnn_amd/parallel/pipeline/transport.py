@@ -6,14 +6,18 @@
 * ``LocalTransport`` — peers in the same process (in-process coordinator, or coordinator +
   stage 0 sharing a rank): the tensor object is handed over through a process-wide mailbox,
   the message carries only metadata; a device change is one ``.to()`` (xGMI peer copy
-  between GPUs).
+  between GPUs). Every stage computes on its own stream, so a GPU tensor travels with an
+  event recorded on the producer's stream: the consumer's stream waits on it (no host sync)
+  and the tensor is marked as used by the consumer stream for the caching allocator.
 * ``P2PTransport`` — one process per GPU under ``torch.distributed``: metadata rides the
   control plane, bytes go device-to-device with ``isend``/``irecv`` (RCCL over xGMI with the
   "nccl" backend, gloo on CPU).  Forward activations and backward gradients use *separate*
   process groups (separate RCCL communicators and streams), so a stage that interleaves
   forward and backward micro-batches can never head-of-line block a peer; the coordinator's
   traffic gets its own pair of groups as well.  Peers living in the same rank fall back to
-  the local mailbox.
+  the local mailbox. With RCCL, ``Work.wait()`` on a receive makes the *current stream* wait for
+  the communicator's stream — the host thread does not block — so a stage posts its receive
+  and immediately enqueues the micro-batch's compute behind it.
 """
 from __future__ import annotations
 
@@ -52,6 +56,30 @@ class _Mailbox:
 MAILBOX = _Mailbox()
 
 
+def _stamp(t: Optional[torch.Tensor]):
+    """Mailbox entry: the tensor and, for a GPU tensor, an event on the producer's stream."""
+    if t is not None and t.is_cuda:
+        ev = torch.cuda.Event()
+        ev.record(torch.cuda.current_stream(t.device))
+        return t, ev
+    return t, None
+
+
+def _claim(entry, device) -> torch.Tensor:
+    """Order the consumer's stream(s) after the producer and move to ``device`` if needed."""
+    t, ev = entry
+    dev = torch.device(device) if device is not None else t.device
+    if ev is not None:
+        s = torch.cuda.current_stream(t.device)
+        s.wait_event(ev)
+        t.record_stream(s)
+        if dev.type == "cuda" and dev != t.device:
+            torch.cuda.current_stream(dev).wait_event(ev)
+    if dev != t.device:
+        t = t.to(dev, non_blocking=True)
+    return t
+
+
 class Transport:
     """send(comm, recipient, command, mb_id, tensor) / recv(msg, device)."""
 
@@ -87,14 +115,13 @@ class LocalTransport(Transport):
     def send(self, comm, recipient, command, mb_id, t):
         target = self.resolve(recipient)
         if t is not None:
-            MAILBOX.put((target, int(command), int(mb_id)), t)
+            MAILBOX.put((target, int(command), int(mb_id)), _stamp(t))
         comm.send(M.meta_message(recipient, command, mb_id, t))
 
     def recv(self, msg, device):
         if not M.has_tensor(msg):
             return None
-        t = MAILBOX.take((self.my_id, int(msg.command), int(msg.mb_id)))
-        return t.to(device) if device is not None and t.device != torch.device(device) else t
+        return _claim(MAILBOX.take((self.my_id, int(msg.command), int(msg.mb_id))), device)
 
 
 class P2PTransport(Transport):
