@@ -38,6 +38,8 @@ def main():
     ap.add_argument("--graph", type=int, default=int(os.environ.get("DCNN_BENCH_GRAPH", "1")),
                     help="capture the per-step compute in a hipGraph (1) or run eagerly (0)")
     ap.add_argument("--bucket-mb", type=float, default=4.0)
+    ap.add_argument("--grad-dtype", default="fp32", choices=["fp32", "bf16"],
+                    help="gradient all-reduce wire format (bf16: all_to_all shards + fp32 sum + all_gather)")
     ap.add_argument("--pg", action="store_true",
                     help="create the RCCL process group even at world size 1 (segmented DP step on one GPU)")
     ap.add_argument("--profile", action="store_true", help="print per-layer device times")
@@ -73,7 +75,7 @@ def main():
         model.set_compute_dtype(torch.float32)
     model.initialize()
     model.set_first_layer_input_grad(False)
-    dp = DataParallel(model, bucket_mb=a.bucket_mb)
+    dp = DataParallel(model, bucket_mb=a.bucket_mb, grad_dtype=a.grad_dtype)
     opt = Adam(1e-3)
     opt.attach(model)
     loss_fn = LossFactory.create("softmax_crossentropy")
@@ -117,6 +119,7 @@ def main():
             "vs_baseline": None, "dtype": a.dtype if dev.type == "cuda" else "fp32", "data": f"synthetic (random {H}x{W}x{C} inputs + random labels, random init)",
             "config": {"model": a.model, "global_batch": a.batch * world, "per_gpu_batch": a.batch, "seq_len": None,
                        "image_size": [C, H, W], "parallelism": f"dp{world}", "optimizer": "adam",
+                       "grad_allreduce": a.grad_dtype if world > 1 else None,
                        "hipgraph": timed_with_graph, "final_loss": round(loss_val, 4)},
         }), flush=True)
     if a.profile and rank == 0:

@@ -360,4 +360,13 @@ PYBIND11_MODULE(_kernels, m) {
     sgd_step(P<float*>(p), P<const float*>(g), P<float*>(vel), P<bf16*>(shadow), n, lr, mom, P<const float*>(hyper),
              S(st));
   });
+  m.def("grad_pack_bf16", [](uintptr_t g, uintptr_t out, long n, float scale, uintptr_t st) {
+    grad_pack_bf16(P<const float*>(g), P<bf16*>(out), n, scale, S(st));
+  });
+  m.def("grad_sum_chunks_bf16", [](uintptr_t src, int w, long ld, long n, uintptr_t dst, uintptr_t st) {
+    grad_sum_chunks_bf16(P<const bf16*>(src), w, ld, n, P<bf16*>(dst), S(st));
+  });
+  m.def("grad_unpack_bf16", [](uintptr_t in, uintptr_t g, long n, uintptr_t st) {
+    grad_unpack_bf16(P<const bf16*>(in), P<float*>(g), n, S(st));
+  });
 }

@@ -1,0 +1,93 @@
+// Gradient wire-format kernels for the data-parallel bf16 all-reduce (parallel/dp.py).
+//
+// A bf16 ring all-reduce would round the running sum to bf16 at every one of its world-1 hops.
+// Instead a bucket goes out as bf16 shards (all_to_all), each rank sums the world copies of its
+// shard in fp32 in a fixed rank order (deterministic), rounds once to bf16, and the reduced
+// shards are all-gathered and expanded back into the fp32 gradient arena. Same wire bytes as a
+// bf16 ring all-reduce (2 (w-1)/w * n * 2 B per rank), half of the fp32 one, one rounding.
+// All three passes are HBM-bound streams: 16-byte vector loads/stores, grid-stride.
+#include "api.h"
+#include "common.h"
+
+namespace dcnn {
+
+namespace {
+
+// 8 fp32 -> 8 bf16 (x scale)
+__global__ void grad_pack_kernel(const float* __restrict__ g, bf16* __restrict__ out, long n, float scale) {
+  const long n8 = n / 8;
+  const long stride = (long)gridDim.x * blockDim.x;
+  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < n8; i += stride) {
+    const f32x4 a = *reinterpret_cast<const f32x4*>(g + i * 8);
+    const f32x4 b = *reinterpret_cast<const f32x4*>(g + i * 8 + 4);
+    bf16x8 o;
+    for (int k = 0; k < 4; ++k) {
+      o[k] = (bf16)(a[k] * scale);
+      o[k + 4] = (bf16)(b[k] * scale);
+    }
+    *reinterpret_cast<bf16x8*>(out + i * 8) = o;
+  }
+  for (long i = n8 * 8 + blockIdx.x * (long)blockDim.x + threadIdx.x; i < n; i += stride) out[i] = (bf16)(g[i] * scale);
+}
+
+// dst[i] = bf16( sum_{r=0..w-1} src[r*ld + i] )   (fp32 accumulation in rank order)
+__global__ void grad_sum_chunks_kernel(const bf16* __restrict__ src, int w, long ld, long n, bf16* __restrict__ dst) {
+  const long n8 = n / 8;
+  const long stride = (long)gridDim.x * blockDim.x;
+  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < n8; i += stride) {
+    float acc[8];
+    for (int k = 0; k < 8; ++k) acc[k] = 0.f;
+    for (int r = 0; r < w; ++r) {
+      const bf16x8 v = *reinterpret_cast<const bf16x8*>(src + r * ld + i * 8);
+      for (int k = 0; k < 8; ++k) acc[k] += (float)v[k];
+    }
+    bf16x8 o;
+    for (int k = 0; k < 8; ++k) o[k] = (bf16)acc[k];
+    *reinterpret_cast<bf16x8*>(dst + i * 8) = o;
+  }
+  for (long i = n8 * 8 + blockIdx.x * (long)blockDim.x + threadIdx.x; i < n; i += stride) {
+    float acc = 0.f;
+    for (int r = 0; r < w; ++r) acc += (float)src[r * ld + i];
+    dst[i] = (bf16)acc;
+  }
+}
+
+__global__ void grad_unpack_kernel(const bf16* __restrict__ in, float* __restrict__ g, long n) {
+  const long n8 = n / 8;
+  const long stride = (long)gridDim.x * blockDim.x;
+  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < n8; i += stride) {
+    const bf16x8 v = *reinterpret_cast<const bf16x8*>(in + i * 8);
+    f32x4 a, b;
+    for (int k = 0; k < 4; ++k) {
+      a[k] = (float)v[k];
+      b[k] = (float)v[k + 4];
+    }
+    *reinterpret_cast<f32x4*>(g + i * 8) = a;
+    *reinterpret_cast<f32x4*>(g + i * 8 + 4) = b;
+  }
+  for (long i = n8 * 8 + blockIdx.x * (long)blockDim.x + threadIdx.x; i < n; i += stride) g[i] = (float)in[i];
+}
+
+inline int stream_grid(long n) { return grid_for((n + 7) / 8, 256); }
+
+}  // namespace
+
+void grad_pack_bf16(const float* g, bf16* out, long n, float scale, hipStream_t s) {
+  if (n <= 0) return;
+  hipLaunchKernelGGL(grad_pack_kernel, dim3(stream_grid(n)), dim3(256), 0, s, g, out, n, scale);
+  DCNN_LAUNCH_CHECK();
+}
+
+void grad_sum_chunks_bf16(const bf16* src, int w, long ld, long n, bf16* dst, hipStream_t s) {
+  if (n <= 0) return;
+  hipLaunchKernelGGL(grad_sum_chunks_kernel, dim3(stream_grid(n)), dim3(256), 0, s, src, w, ld, n, dst);
+  DCNN_LAUNCH_CHECK();
+}
+
+void grad_unpack_bf16(const bf16* in, float* g, long n, hipStream_t s) {
+  if (n <= 0) return;
+  hipLaunchKernelGGL(grad_unpack_kernel, dim3(stream_grid(n)), dim3(256), 0, s, in, g, n);
+  DCNN_LAUNCH_CHECK();
+}
+
+}  // namespace dcnn

@@ -12,6 +12,18 @@ should be small, while every bucket stays large enough to run near per-link xGMI
 The 1/world factor of the gradient average is folded into the incoming loss gradient (every
 gradient is linear in it), so the all-reduce is a plain SUM and no extra pass over the
 45 MB gradient buffer is needed.
+
+``grad_dtype="bf16"`` halves the wire bytes: a bucket is packed to bf16, exchanged as shards
+(``all_to_all``), each rank sums the world copies of its shard in fp32 in rank order
+(``comm.hip``, deterministic, one rounding instead of one per ring hop), and the reduced shards
+are all-gathered and expanded back into the fp32 arena. On the GPU that pipeline runs on a side
+stream forked from the compute stream at the bucket's fire point, so backward compute keeps
+running while it waits on RCCL.
+
+Every collective is issued from the stream it depends on, with no host synchronisation, so the
+whole step — forward, backward, bucket collectives and optimizer — can be captured as ONE
+hipGraph (``runtime/step.py``): RCCL kernels are stream-capturable, and the NCCL process
+group forks its internal stream from the capturing stream and joins it back on ``wait()``.
 """
 from __future__ import annotations
 
@@ -42,7 +54,8 @@ def init_distributed(backend: Optional[str] = None) -> Tuple[int, int, int]:
 
 
 class DataParallel:
-    def __init__(self, model: Sequential, process_group=None, bucket_mb: float = 4.0, broadcast: bool = True):
+    def __init__(self, model: Sequential, process_group=None, bucket_mb: float = 4.0, broadcast: bool = True,
+                 grad_dtype: str = "fp32"):
         if not model.initialized:
             model.initialize()
         self.model = model
@@ -54,7 +67,13 @@ class DataParallel:
         # training has no group and skips it
         self.active = dist.is_initialized()
         self.bucket_bytes = int(bucket_mb * 2**20)
+        if grad_dtype not in ("fp32", "bf16"):
+            raise ValueError("grad_dtype must be 'fp32' or 'bf16'")
+        self.grad_dtype = grad_dtype
         self._works: List = []
+        self._pending_unpack: List = []
+        self._wire = {}          # (lo, hi) -> persistent bf16 wire buffers of that bucket
+        self._comm_stream = None
         self._build_buckets()
         if broadcast and self.world > 1:
             self.broadcast_parameters()
@@ -130,24 +149,84 @@ class DataParallel:
             cur = run_backward(m.layers, i, cur, mb_id)
             m._prof_end(m.layers[i].name or m.layers[i].type(), t0, m.backward_times_us)
             if self.active and i in self.fire:
-                lo, hi = self.fire[i]
                 m.flush_gradients()  # queued split-K reductions of this bucket's layers
-                self._works.append(dist.all_reduce(flat[lo:hi], op=dist.ReduceOp.SUM, group=self.pg, async_op=True))
+                self.reduce_bucket(*self.fire[i])
         m.finish_backward()
         if sync:
             self.finish()
         return cur
 
+    # ---------------------------------------------------------------- bucket collectives
+    def reduce_bucket(self, lo: int, hi: int) -> None:
+        """Start the SUM all-reduce of ``arena.grad[lo:hi]`` (completed by :meth:`finish`)."""
+        flat = self.model.arena.grad
+        if self.grad_dtype == "fp32" or self.world == 1:
+            self._works.append(dist.all_reduce(flat[lo:hi], op=dist.ReduceOp.SUM, group=self.pg, async_op=True))
+            return
+        if flat.is_cuda:
+            self._reduce_bf16_gpu(lo, hi)
+        else:
+            self._reduce_bf16_cpu(lo, hi)
+
+    def _wire_bufs(self, lo, hi, device):
+        key = (lo, hi)
+        b = self._wire.get(key)
+        if b is None:
+            n = hi - lo
+            w = self.world
+            shard = -(-n // (w * 64)) * 64   # 64-element shards keep every chunk 128-byte aligned
+            z = lambda k: torch.zeros(k, dtype=torch.bfloat16, device=device)
+            b = self._wire[key] = (n, shard, z(w * shard), z(w * shard), z(shard), z(w * shard))
+        return b
+
+    def _reduce_bf16_gpu(self, lo, hi):
+        from ..ops._ext import kernels, stream_ptr
+        K = kernels()
+        flat = self.model.arena.grad
+        n, shard, packed, recv, red, gathered = self._wire_bufs(lo, hi, flat.device)
+        main = torch.cuda.current_stream(flat.device)
+        if self._comm_stream is None:
+            self._comm_stream = torch.cuda.Stream(device=flat.device)
+        cs = self._comm_stream
+        cs.wait_stream(main)  # fork: the bucket's gradients are complete on the compute stream
+        with torch.cuda.stream(cs):
+            st = stream_ptr(flat.device)
+            K.grad_pack_bf16(flat[lo:hi].data_ptr(), packed.data_ptr(), n, 1.0, st)
+            dist.all_to_all_single(recv, packed, group=self.pg, async_op=True).wait()
+            K.grad_sum_chunks_bf16(recv.data_ptr(), self.world, shard, shard, red.data_ptr(), st)
+            dist.all_gather_into_tensor(gathered, red, group=self.pg, async_op=True).wait()
+            K.grad_unpack_bf16(gathered.data_ptr(), flat[lo:hi].data_ptr(), n, st)
+        self._pending_unpack.append(cs)
+
+    def _reduce_bf16_cpu(self, lo, hi):
+        """Same wire format over gloo (bf16 payloads moved as int32 bit-pattern pairs)."""
+        flat = self.model.arena.grad
+        n, shard, packed, recv, red, gathered = self._wire_bufs(lo, hi, flat.device)
+        packed[:n].copy_(flat[lo:hi].to(torch.bfloat16))
+        dist.all_to_all_single(recv.view(torch.int32), packed.view(torch.int32), group=self.pg)
+        acc = torch.zeros(shard, dtype=torch.float32)
+        for r in range(self.world):   # fixed rank order, fp32 accumulation
+            acc += recv[r * shard:(r + 1) * shard].float()
+        red.copy_(acc.to(torch.bfloat16))
+        dist.all_gather_into_tensor(gathered.view(torch.int32), red.view(torch.int32), group=self.pg)
+        flat[lo:hi].copy_(gathered[:n].float())
+
     def finish(self):
         for w in self._works:
             w.wait()
         self._works.clear()
+        if self._pending_unpack:
+            main = torch.cuda.current_stream(self.model.arena.grad.device)
+            for cs in self._pending_unpack:
+                main.wait_stream(cs)  # join the side-stream bf16 pipelines
+            self._pending_unpack.clear()
 
     def allreduce_gradients(self):
         """Non-overlapped fallback: one SUM all-reduce per bucket after backward."""
         if self.world > 1:
             for lo, hi in self.buckets:
-                dist.all_reduce(self.model.arena.grad[lo:hi], group=self.pg)
+                self.reduce_bucket(lo, hi)
+            self.finish()
 
     def sync_batchnorm_buffers(self):
         """Average BN running statistics across replicas (before eval / checkpoint)."""

@@ -4,15 +4,19 @@ Instead of a tracing compiler the whole per-step launch sequence (input layout c
 ~150 HIP kernels of forward/backward, fused loss, fused optimizer) is captured once with
 ``torch.cuda.graph`` and replayed, removing host launch overhead.
 
-Data-parallel runs are captured in *segments* split at the gradient-bucket fire points of
-:class:`~dcnn_amd.parallel.dp.DataParallel`: between two segment replays the host enqueues
-the asynchronous RCCL all-reduce of the bucket just completed, so communication still
-overlaps the remaining backward segments while no collective is ever captured into a graph.
+Data-parallel steps are captured WHOLE: the bucket collectives that
+:class:`~dcnn_amd.parallel.dp.DataParallel` fires from inside the backward pass are RCCL
+kernels on the process group's internal stream, forked from the capturing stream at each fire
+point and joined back before the optimizer, so one replay runs forward, backward, every
+overlapped all-reduce and the update with no host involvement. ``DCNN_DP_CAPTURE=0`` selects
+the older *segmented* capture instead: one graph per backward segment between fire points, the
+host enqueuing each bucket's asynchronous all-reduce between two segment replays.
 The optimizer's step scalars are uploaded to device memory before each replay
 (``Optimizer.prepare_step``), so replays use the current learning rate / bias corrections.
 """
 from __future__ import annotations
 
+import os
 from typing import List, Optional
 
 import torch
@@ -30,6 +34,8 @@ class TrainStep:
         self.opt = optimizer
         self.use_graph = use_graph
         self.graphs: Optional[List[torch.cuda.CUDAGraph]] = None
+        self.capture_collectives = os.environ.get("DCNN_DP_CAPTURE", "1") != "0"
+        self._whole = False
         self.last_loss = None
         self.last_correct = None
         self._static_x = self._static_y = None
@@ -99,13 +105,29 @@ class TrainStep:
             self.opt.t = saved_t
         self.model.arena.sync_shadow(force=True)
         torch.cuda.synchronize()
+        fused_opt = hasattr(self.opt, "fused") and self.opt.fused()
+        if not fused_opt:
+            raise RuntimeError("graph capture needs the fused flat-buffer optimizer on the GPU")
+        if self.dp.active and self.capture_collectives and dist.get_backend(self.dp.pg) == "nccl":
+            # (gloo moves CUDA tensors through the host: not capturable, keeps the segments)
+            t0 = getattr(self.opt, "t", None)
+            try:
+                self._capture_whole()
+                return
+            except Exception as e:  # e.g. a collective library build without capture support
+                import warnings
+                warnings.warn(f"capturing the bucket collectives into the step graph failed ({e}); "
+                              "falling back to the segmented capture")
+                self.dp._works.clear()
+                self.dp._pending_unpack.clear()
+                if t0 is not None:
+                    self.opt.t = t0
+                self.graphs, self._whole = None, False
+                torch.cuda.synchronize()
         segs, fires = self._segments()
         self._segs, self._fires = segs, fires
         self.graphs = []
         pool = None
-        fused_opt = hasattr(self.opt, "fused") and self.opt.fused()
-        if not fused_opt:
-            raise RuntimeError("graph capture needs the fused flat-buffer optimizer on the GPU")
         self.opt.prepare_step()  # upload scalars used during capture (replays re-upload)
         if hasattr(self.opt, "t"):
             self.opt.t -= 1  # the capture itself is not a training step
@@ -140,10 +162,37 @@ class TrainStep:
             self.graphs.append(g)
         torch.cuda.synchronize()
 
+    def _capture_whole(self):
+        """ONE graph: forward, loss, backward with the bucket collectives it fires, optimizer."""
+        self.opt.prepare_step()
+        if hasattr(self.opt, "t"):
+            self.opt.t -= 1
+        m = self.model
+        prof = m.enable_profiling_
+        m.enable_profiling_ = False
+        g = torch.cuda.CUDAGraph()
+        try:
+            with torch.cuda.graph(g, capture_error_mode="thread_local"):
+                self.opt.clear_gradients()
+                out = self.dp.forward(self._static_x)
+                loss, grad, correct = self.loss_fn.loss_and_grad(out, self._static_y)
+                self._g_loss, self._g_correct = loss, correct
+                self.dp.backward(grad, sync=True)
+                self.opt.launch_step()
+        finally:
+            m.enable_profiling_ = prof
+        self.graphs = [g]
+        self._whole = True
+        torch.cuda.synchronize()
+
     def replay(self, x, y):
         self._static_x.copy_(x, non_blocking=True)
         self._static_y.copy_(y, non_blocking=True)
         self.opt.prepare_step()
+        if self._whole:
+            self.graphs[0].replay()
+            self.last_loss, self.last_correct = self._g_loss, self._g_correct
+            return self.last_loss
         active = self.dp.active
         flat = self.model.arena.grad
         works = []

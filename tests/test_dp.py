@@ -95,3 +95,44 @@ def test_bench_under_torchrun_cpu():
     d = lines[0]
     assert d["n_gpus"] == 2 and d["config"]["global_batch"] == 8 and d["value"] > 0
     assert d["config"]["parallelism"] == "dp2"
+
+
+def _bf16_worker(rank, world, port, out_dir, grad_dtype):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    torch.set_num_threads(1)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    from dcnn_amd.models import zoo
+    from dcnn_amd.nn import SGD, LossFactory
+    from dcnn_amd.parallel.dp import DataParallel
+    model = zoo.create_model("mnist_cnn")
+    model.set_seed(5)
+    model.initialize()
+    dp = DataParallel(model, bucket_mb=0.05, grad_dtype=grad_dtype)
+    lf = LossFactory.create("softmax_crossentropy")
+    g = torch.Generator().manual_seed(3 + rank)
+    x = torch.randn(8, 1, 28, 28, generator=g)
+    y = torch.randint(0, 10, (8,), generator=g)
+    model.clear_gradients()
+    out = dp.forward(x)
+    _, grad, _ = lf.loss_and_grad(out, y)
+    dp.backward(grad)
+    torch.save({"g": model.arena.grad.clone(), "nb": len(dp.buckets)}, os.path.join(out_dir, f"{grad_dtype}{rank}.pt"))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_dp_bf16_gradient_allreduce_matches_fp32(tmp_path):
+    """bf16 wire format (all_to_all shards, fp32 rank-order sum, all_gather): every rank ends
+    with the same gradient, equal to the fp32 all-reduce up to one bf16 rounding of the sum
+    (plus the bf16 rounding of each rank's contribution)."""
+    for dt in ("fp32", "bf16"):
+        mp.spawn(_bf16_worker, args=(3, _free_port(), str(tmp_path), dt), nprocs=3, join=True)
+    f = [torch.load(tmp_path / f"fp32{r}.pt", weights_only=True)["g"] for r in range(3)]
+    b = [torch.load(tmp_path / f"bf16{r}.pt", weights_only=True) for r in range(3)]
+    assert b[0]["nb"] > 1
+    for r in range(1, 3):
+        assert torch.equal(b[0]["g"], b[r]["g"])
+    ref = f[0]
+    err = (b[0]["g"] - ref).abs()
+    assert float(err.max()) <= 2 * 2 ** -8 * float(ref.abs().max()) + 1e-12
+    assert float((b[0]["g"] - ref).norm()) <= 2 ** -7 * float(ref.norm())

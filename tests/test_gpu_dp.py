@@ -58,11 +58,12 @@ def test_gpu_dp_two_ranks_shared_gpu(tmp_path, use_graph):
     assert r0["losses"][-1] < r0["losses"][0]
 
 
-def _rccl_worker(rank, port, out, with_pg, use_graph):
+def _rccl_worker(rank, port, out, with_pg, use_graph, whole=True):
     """World size 1 over the real RCCL backend: graph capture/replay must coexist with the
-    process group's watchdog, and the bucket all-reduces run between segment replays."""
+    process group's watchdog; the bucket all-reduces are captured inside the step graph
+    (``whole``) or run between segment replays (DCNN_DP_CAPTURE=0)."""
     import torch.distributed as dist
-    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), DCNN_DP_CAPTURE="1" if whole else "0")
     torch.cuda.set_device(0)
     if with_pg:
         dist.init_process_group("nccl", rank=0, world_size=1, device_id=torch.device("cuda", 0))
@@ -90,23 +91,29 @@ def _rccl_worker(rank, port, out, with_pg, use_graph):
     losses += [float(st(x, y)) for _ in range(3)]
     torch.cuda.synchronize()
     big = [(o, s.shape) for o, s in zip(m.arena.offsets, m.arena.specs) if torch.Size(s.shape).numel() >= 4096]
-    torch.save({"g": grad, "losses": losses, "segs": len(st._segs) if use_graph else 0,
-                "big": [(o, torch.Size(sh).numel()) for o, sh in big]},
-               os.path.join(out, f"pg{int(with_pg)}g{int(use_graph)}.pt"))
+    torch.save({"g": grad, "losses": losses, "segs": len(getattr(st, "_segs", [])) if use_graph else 0,
+                "whole": st._whole, "big": [(o, torch.Size(sh).numel()) for o, sh in big]},
+               os.path.join(out, f"pg{int(with_pg)}g{int(use_graph)}w{int(whole)}.pt"))
     if with_pg:
         dist.destroy_process_group()
 
 
 def test_gpu_dp_rccl_world1_graph_segments(tmp_path):
-    """Segmented-graph step with an RCCL group == unsegmented graph step == eager step; the
-    graph warm-up must not train (first-step losses agree with eager)."""
-    for with_pg, use_graph in ((True, True), (False, True), (False, False)):
-        mp.spawn(_rccl_worker, args=(_port(), str(tmp_path), with_pg, use_graph), nprocs=1, join=True)
-    a = torch.load(tmp_path / "pg1g1.pt", weights_only=True)
-    b = torch.load(tmp_path / "pg0g1.pt", weights_only=True)
-    e = torch.load(tmp_path / "pg0g0.pt", weights_only=True)
+    """RCCL group, collectives captured in the step graph == segmented graph step == graph step
+    without a group == eager step; the graph warm-up must not train (first-step losses agree
+    with eager). The deterministic kernels make the three graph variants bit-identical."""
+    for with_pg, use_graph, whole in ((True, True, True), (True, True, False), (False, True, True),
+                                      (False, False, True)):
+        mp.spawn(_rccl_worker, args=(_port(), str(tmp_path), with_pg, use_graph, whole), nprocs=1, join=True)
+    w = torch.load(tmp_path / "pg1g1w1.pt", weights_only=True)
+    a = torch.load(tmp_path / "pg1g1w0.pt", weights_only=True)
+    b = torch.load(tmp_path / "pg0g1w1.pt", weights_only=True)
+    e = torch.load(tmp_path / "pg0g0w1.pt", weights_only=True)
+    assert w["whole"] and not a["whole"]
     assert a["segs"] > 1 and b["segs"] == 1
-    for r in (a, b):
+    assert w["losses"] == a["losses"] == b["losses"], (w["losses"], a["losses"], b["losses"])
+    assert torch.equal(w["g"], a["g"]) and torch.equal(w["g"], b["g"])
+    for r in (w, a, b):
         # weight gradients (biases ahead of a BatchNorm have ~zero true gradient: skipped)
         for o, n in e["big"]:
             ge, gr = e["g"][o:o + n], r["g"][o:o + n]
@@ -173,3 +180,24 @@ def test_gpu_dp_two_ranks_equal_single_process(tmp_path, use_graph):
     # averaged half-batch gradients == whole-batch gradient (fp32; summation order differs)
     torch.testing.assert_close(r0["g"], ref["g"], rtol=1e-5, atol=1e-6)
     torch.testing.assert_close(r0["p"], ref["p"], rtol=1e-5, atol=1e-6)
+
+
+def test_gpu_bf16_grad_wire_kernels():
+    """comm.hip: pack (fp32 -> bf16), fixed-order fp32 sum of the rank chunks, unpack."""
+    from dcnn_amd.ops._ext import kernels, stream_ptr
+    K = kernels()
+    w, n, shard = 4, 1000, 1024
+    g = torch.randn(n, device="cuda")
+    packed = torch.zeros(shard, dtype=torch.bfloat16, device="cuda")
+    K.grad_pack_bf16(g.data_ptr(), packed.data_ptr(), n, 1.0, stream_ptr())
+    assert torch.equal(packed[:n], g.to(torch.bfloat16))
+    src = torch.randn(w, shard, device="cuda").to(torch.bfloat16)
+    red = torch.empty(shard - 3, dtype=torch.bfloat16, device="cuda")
+    K.grad_sum_chunks_bf16(src.data_ptr(), w, shard, shard - 3, red.data_ptr(), stream_ptr())
+    ref = src.float()[0].clone()
+    for r in range(1, w):
+        ref += src.float()[r]
+    assert torch.equal(red, ref[:shard - 3].to(torch.bfloat16))
+    out = torch.empty(n, device="cuda")
+    K.grad_unpack_bf16(packed.data_ptr(), out.data_ptr(), n, stream_ptr())
+    assert torch.equal(out, packed[:n].float())
