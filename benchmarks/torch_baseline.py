@@ -5,7 +5,11 @@ create_resnet18_tiny_imagenet) run with stock PyTorch-ROCm (MIOpen/hipBLASLt ker
 same MI355X, synthetic data, Adam, cross-entropy. Modes: fp32 NCHW (the script's default) and
 bf16 autocast + channels_last (PyTorch's best eager configuration).
 
+``--model resnet9_cifar10`` runs the same comparison for the CIFAR-10 ResNet-9 BASELINE config
+(the layer stack of create_resnet9_cifar10, reference examples/cifar10_resnet9.cpp:20-79).
+
   python benchmarks/torch_baseline.py --batch 256 --steps 20 --warmup 5 --mode bf16
+  python benchmarks/torch_baseline.py --model resnet9_cifar10 --batch 128 --mode fp32
 """
 import argparse
 import json
@@ -47,22 +51,56 @@ class ResNet18Tiny(nn.Module):
         return self.fc(torch.flatten(self.pool(self.blocks(self.stem(x))), 1))
 
 
+class ResBlock(nn.Module):
+    """Basic residual block with identity shortcut (cin == cout, stride 1)."""
+
+    def __init__(self, c):
+        super().__init__()
+        self.c1, self.b1 = nn.Conv2d(c, c, 3, 1, 1), nn.BatchNorm2d(c)
+        self.c2, self.b2 = nn.Conv2d(c, c, 3, 1, 1), nn.BatchNorm2d(c)
+
+    def forward(self, x):
+        h = torch.relu(self.b1(self.c1(x)))
+        return torch.relu(self.b2(self.c2(h)) + x)
+
+
+def _cbr(cin, cout):
+    return [nn.Conv2d(cin, cout, 3, 1, 1), nn.BatchNorm2d(cout), nn.ReLU()]
+
+
+class ResNet9Cifar(nn.Module):
+    def __init__(self, ncls=10):
+        super().__init__()
+        self.body = nn.Sequential(*_cbr(3, 64), *_cbr(64, 128), nn.MaxPool2d(2, 2), ResBlock(128), ResBlock(128),
+                                  *_cbr(128, 256), nn.MaxPool2d(2, 2), ResBlock(256), ResBlock(256),
+                                  *_cbr(256, 512), nn.MaxPool2d(2, 2), ResBlock(512), nn.AvgPool2d(4, 1))
+        self.fc = nn.Linear(512, ncls)
+
+    def forward(self, x):
+        return self.fc(torch.flatten(self.body(x), 1))
+
+
+MODELS = {"resnet18_tiny_imagenet": (ResNet18Tiny, (3, 64, 64), 200), "resnet9_cifar10": (ResNet9Cifar, (3, 32, 32), 10)}
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--batch", type=int, default=256)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--mode", choices=["fp32", "bf16"], default="bf16")
+    ap.add_argument("--model", choices=sorted(MODELS), default="resnet18_tiny_imagenet")
     a = ap.parse_args()
     torch.backends.cudnn.benchmark = True
     dev = torch.device("cuda")
-    m = ResNet18Tiny().to(dev)
+    cls, shape, ncls = MODELS[a.model]
+    m = cls().to(dev)
     mf = torch.channels_last if a.mode == "bf16" else torch.contiguous_format
     m = m.to(memory_format=mf)
     opt = torch.optim.Adam(m.parameters(), 1e-3)
     lossf = nn.CrossEntropyLoss()
-    xs = [torch.randn(a.batch, 3, 64, 64, device=dev).to(memory_format=mf) for _ in range(4)]
-    ys = [torch.randint(0, 200, (a.batch,), device=dev) for _ in range(4)]
+    xs = [torch.randn(a.batch, *shape, device=dev).to(memory_format=mf) for _ in range(4)]
+    ys = [torch.randint(0, ncls, (a.batch,), device=dev) for _ in range(4)]
 
     def step(i):
         opt.zero_grad(set_to_none=True)
@@ -80,7 +118,7 @@ def main():
         loss = step(i)
     torch.cuda.synchronize()
     el = time.perf_counter() - t0
-    print(json.dumps({"framework": "pytorch-rocm " + torch.__version__, "mode": a.mode, "batch": a.batch,
+    print(json.dumps({"framework": "pytorch-rocm " + torch.__version__, "model": a.model, "mode": a.mode, "batch": a.batch,
                       "images_per_sec": round(a.batch * a.steps / el, 1), "ms_per_step": round(el / a.steps * 1e3, 3),
                       "loss": round(float(loss), 4)}))
 

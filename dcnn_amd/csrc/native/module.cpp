@@ -9,6 +9,7 @@ using namespace dcnn_native;
 
 void bind_comm(py::module_& m);   // comm.cpp
 void bind_data(py::module_& m);   // data.cpp
+void bind_cpu(py::module_& m);    // cpu_bind.cpp
 
 PYBIND11_MODULE(_native, m) {
   m.doc() = "dcnn_amd host runtime (C++)";
@@ -43,4 +44,5 @@ PYBIND11_MODULE(_native, m) {
   m.def("get_thread_affinity", &get_thread_affinity);
   bind_comm(m);
   bind_data(m);
+  bind_cpu(m);
 }

@@ -2,8 +2,9 @@
 `include/nn/activations_impl/*`): relu, leaky_relu(0.01), elu(1.0), sigmoid, tanh,
 softmax (over the channel dim per spatial location), linear; "none" -> None.
 
-Each function has a CPU (ATen) and a GPU (HIP kernel) implementation of
-``apply(x)`` and ``gradient(x, y, grad)`` (x = input, y = output).
+Each function has a CPU (native C++ backend, csrc/native/cpu_ops.cpp) and a GPU (HIP kernel)
+implementation of ``apply(x)`` and ``gradient(x, y, grad)`` (x = input, y = output); the ATen
+formulas kept in ``_cpu`` / ``_cpu_grad`` are the test oracle.
 """
 from __future__ import annotations
 
@@ -25,13 +26,15 @@ class ActivationFunction:
         if x.is_cuda:
             from ..ops import hip
             return hip.act_fwd(x, self.name_str, self.alpha)
-        return self._cpu(x)
+        from ..ops import cpu
+        return cpu.act_fwd(x, self.name_str, self.alpha)
 
     def gradient(self, x: torch.Tensor, y: torch.Tensor, grad: torch.Tensor) -> torch.Tensor:
         if x.is_cuda:
             from ..ops import hip
             return hip.act_bwd(x, grad, self.name_str, self.alpha)
-        return self._cpu_grad(x, y, grad)
+        from ..ops import cpu
+        return cpu.act_bwd(x, grad.to(x.dtype), self.name_str, self.alpha)
 
     def _cpu(self, x):
         return x.clone()
@@ -116,13 +119,15 @@ class Softmax(ActivationFunction):
         if x.is_cuda:
             from ..ops import hip
             return hip.softmax_channels(x)
-        return torch.softmax(x, dim=1)
+        from ..ops import cpu
+        return cpu.softmax_channels(x)
 
     def gradient(self, x, y, grad):
         if x.is_cuda:
             from ..ops import hip
             return hip.softmax_channels_bwd(y, grad)
-        return y * (grad - (grad * y).sum(1, keepdim=True))
+        from ..ops import cpu
+        return cpu.softmax_channels_bwd(y, grad.to(y.dtype))
 
 
 class ActivationFactory:

@@ -6,7 +6,8 @@ per-micro-batch caches keyed by ``mb_id`` (so one layer object can hold several 
 micro-batches of a pipeline schedule). Two execution paths are chosen per call from the
 tensor's device:
 
-* CPU: the reference semantics in fp32 NCHW, written with ATen CPU ops (the oracle path).
+* CPU: the reference semantics in NCHW, fp32 (or fp64), on the native C++ backend
+  (``ops/cpu.py`` over csrc/native/cpu_ops.cpp + the blocked GEMM); ATen is only the test oracle.
 * GPU (MI355X): the HIP/CDNA4 kernel library, NHWC (channels_last) activations in the
   model's compute dtype (bf16 by default, fp32 accumulation / master weights).
 """
@@ -163,8 +164,8 @@ class Layer:
         td = self.device.torch_device
         if x.device != td:
             x = x.to(td, non_blocking=True)
-        if not self._on_gpu() and x.dtype != torch.float32:
-            x = x.float()
+        if not self._on_gpu() and x.dtype != self.compute_dtype:
+            x = x.to(self.compute_dtype)
         return x
 
     # ---------------------------------------------------------------- params
@@ -253,11 +254,14 @@ class ParameterizedLayer(Layer):
     def shadow_dtype(self) -> Optional[torch.dtype]:
         return torch.bfloat16 if (self._on_gpu() and self.compute_dtype == torch.bfloat16) else None
 
+    def master_dtype(self) -> torch.dtype:
+        return torch.float64 if (not self._on_gpu() and self.compute_dtype == torch.float64) else torch.float32
+
     def initialize(self) -> None:
         if self.initialized and self.arena is not None:
             return
         specs = self.param_specs()
-        arena = ParamArena(specs, self.device.torch_device, self.shadow_dtype())
+        arena = ParamArena(specs, self.device.torch_device, self.shadow_dtype(), self.master_dtype())
         vals = self.init_values(self.make_generator())
         for i, v in enumerate(vals):
             arena.param(i).copy_(v)
@@ -278,7 +282,7 @@ class ParameterizedLayer(Layer):
             self.initialized = False
             self.arena = None
             specs = self.param_specs()
-            arena = ParamArena(specs, new.torch_device, self.shadow_dtype())
+            arena = ParamArena(specs, new.torch_device, self.shadow_dtype(), self.master_dtype())
             for i, v in enumerate(old_vals):
                 arena.param(i).copy_(v)
             arena.sync_shadow(force=True)

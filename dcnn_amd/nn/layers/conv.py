@@ -3,7 +3,8 @@
 Reference: `include/nn/layers_impl/conv2d_layer.tpp` (im2col -> cuBLAS -> CNHW->NCHW -> bias,
 cuDNN variant) and `include/nn/layers_impl/dense_layer.tpp`. GPU path here: implicit-GEMM on
 MFMA (no im2col buffer, no layout transposes, bias/residual/BN-statistics fused into the
-epilogue, split-K wgrad accumulating into the fp32 master gradient).
+epilogue, split-K wgrad accumulating into the fp32 master gradient). CPU path: the native
+backend's per-sample im2col + blocked GEMM (``ops/cpu.py``), float32 or float64.
 """
 from __future__ import annotations
 
@@ -90,7 +91,8 @@ class Conv2D(ParameterizedLayer):
                 y._bn_partial = partial
             self._cache[mb_id] = (xa, tuple(x.shape))
             return y
-        y = F.conv2d(x, self.weights, self._bias_vec(), (self.stride_h, self.stride_w), (self.pad_h, self.pad_w))
+        from ...ops import cpu
+        y = cpu.conv2d_fwd(x, self.weights, self._bias_vec(), (self.stride_h, self.stride_w), (self.pad_h, self.pad_w))
         self._cache[mb_id] = x
         return y
 
@@ -121,15 +123,12 @@ class Conv2D(ParameterizedLayer):
             res = hip.to_act(add_to, self.compute_dtype) if add_to is not None else None
             return hip.conv2d_dgrad(g, wt, x_shape, (self.stride_h, self.stride_w), (self.pad_h, self.pad_w),
                                     residual=res, bnb=self._bnb_request)
+        from ...ops import cpu
         st, pd = (self.stride_h, self.stride_w), (self.pad_h, self.pad_w)
-        self._grads[0].add_(torch.nn.grad.conv2d_weight(x, self.weights.shape, grad, st, pd))
-        if self.use_bias:
-            self._grads[1].add_(grad.sum((0, 2, 3)).view(-1, 1, 1, 1))
-        if not self.needs_input_grad:
-            return None
-        dx = torch.nn.grad.conv2d_input(x.shape, self.weights, grad, st, pd)
-        if add_to is not None:
-            dx = dx + add_to.to(dx.dtype)
+        dx = cpu.conv2d_bwd(x, self.weights, grad.to(x.dtype), st, pd, self._grads[0],
+                            self._grads[1].view(-1) if self.use_bias else None, need_dx=self.needs_input_grad)
+        if dx is not None and add_to is not None:
+            cpu.elementwise(0, 0, dx, add_to.to(dx.dtype), out=dx)
         return dx
 
     # shapes / cost ----------------------------------------------------------------------
@@ -224,8 +223,9 @@ class Dense(ParameterizedLayer):
             b = self._params[1].view(-1) if self.use_bias else None
             y = hip.dense_fwd(x2, w, b)
         else:
-            y = F.linear(x2, self.weights.view(self.output_features, self.input_features),
-                         self._params[1].view(-1) if self.use_bias else None)
+            from ...ops import cpu
+            y = cpu.dense_fwd(x2, self.weights.view(self.output_features, self.input_features),
+                              self._params[1].view(-1) if self.use_bias else None)
         self._cache[mb_id] = (x2, tuple(x.shape))
         return y.view(n, self.output_features, 1, 1)
 
@@ -248,13 +248,12 @@ class Dense(ParameterizedLayer):
                 self.input_features, self.output_features)
             dx = hip.dense_dgrad(g2, wt)
         else:
+            from ...ops import cpu
             w = self.weights.view(self.output_features, self.input_features)
-            self._grads[0].add_((g2.t() @ x2).view_as(self._grads[0]))
-            if self.use_bias:
-                self._grads[1].add_(g2.sum(0).view(-1, 1, 1, 1))
-            if not self.needs_input_grad:
+            dx = cpu.dense_bwd(x2, w, g2.to(x2.dtype), self._grads[0].view(self.output_features, self.input_features),
+                               self._grads[1].view(-1) if self.use_bias else None, need_dx=self.needs_input_grad)
+            if dx is None:
                 return None
-            dx = g2 @ w
         if len(in_shape) == 4 and (in_shape[2] != 1 or in_shape[3] != 1):
             dx = dx.view(in_shape)
             if dx.is_cuda:

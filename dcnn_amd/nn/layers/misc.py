@@ -62,8 +62,9 @@ class MaxPool2D(_Pool):
             # ReLU mask when the producing BatchNorm's backward statistics are fused in backward
             self._cache[mb_id] = (idx, tuple(xa.shape), y)
             return y
-        y, idx = F.max_pool2d(x, (self.pool_h, self.pool_w), (self.stride_h, self.stride_w),
-                              (self.pad_h, self.pad_w), return_indices=True)
+        from ...ops import cpu
+        y, idx = cpu.maxpool_fwd(x, (self.pool_h, self.pool_w), (self.stride_h, self.stride_w),
+                                 (self.pad_h, self.pad_w))
         self._cache[mb_id] = (idx, tuple(x.shape), None)
         return y
 
@@ -73,9 +74,8 @@ class MaxPool2D(_Pool):
             from ...ops import hip
             g = hip.to_act(grad.to(idx.device), self.compute_dtype)
             return hip.maxpool_bwd(g, idx, shape, *self._geom(), ypool=y, bnb=self._bnb_request)
-        return torch.ops.aten.max_pool2d_with_indices_backward(
-            grad, torch.empty(shape), [self.pool_h, self.pool_w], [self.stride_h, self.stride_w],
-            [self.pad_h, self.pad_w], [1, 1], False, idx)
+        from ...ops import cpu
+        return cpu.maxpool_bwd(grad.to(self.compute_dtype), idx, shape)
 
     @staticmethod
     def from_config(cfg):
@@ -98,9 +98,10 @@ class AvgPool2D(_Pool):
             y = hip.avgpool_fwd(xa, *self._geom())
             self._cache[mb_id] = tuple(xa.shape)
             return y
+        from ...ops import cpu
         self._cache[mb_id] = tuple(x.shape)
-        return F.avg_pool2d(x, (self.pool_h, self.pool_w), (self.stride_h, self.stride_w), (self.pad_h, self.pad_w),
-                            count_include_pad=True)
+        return cpu.avgpool_fwd(x, (self.pool_h, self.pool_w), (self.stride_h, self.stride_w),
+                               (self.pad_h, self.pad_w))
 
     def backward(self, grad, mb_id=0):
         shape = self._cache.pop(mb_id)
@@ -108,9 +109,9 @@ class AvgPool2D(_Pool):
             from ...ops import hip
             g = hip.to_act(grad.to(self.device.torch_device), self.compute_dtype)
             return hip.avgpool_bwd(g, shape, *self._geom())
-        return torch.ops.aten.avg_pool2d_backward(grad, torch.empty(shape), [self.pool_h, self.pool_w],
-                                                  [self.stride_h, self.stride_w], [self.pad_h, self.pad_w], False,
-                                                  True, None)
+        from ...ops import cpu
+        return cpu.avgpool_bwd(grad.to(self.compute_dtype), shape, (self.pool_h, self.pool_w),
+                               (self.stride_h, self.stride_w), (self.pad_h, self.pad_w))
 
     @staticmethod
     def from_config(cfg):
@@ -156,10 +157,12 @@ class Dropout(StatelessLayer):
             hip.counter_bump(self._dev_ctr, slot)
             self._cache[mb_id] = (seed, slot)   # mask regenerated from Philox(seed, slot) in backward
             return hip.dropout(xa, self.dropout_rate, seed, slot)
-        gen = torch.Generator().manual_seed(seed)
-        mask = (torch.rand(x.shape, generator=gen) >= self.dropout_rate).to(x.dtype) / (1 - self.dropout_rate)
+        from ...ops import cpu
+        u = cpu.fill_random(torch.empty(x.shape, dtype=x.dtype), 0.0, 1.0, seed, False)  # Philox, as on the GPU
+        mask = cpu.elementwise(1, 7, u, s0=self.dropout_rate)             # u > p
+        cpu.elementwise(1, 2, mask, out=mask, s0=1.0 / (1 - self.dropout_rate))
         self._cache[mb_id] = mask
-        return x * mask
+        return cpu.elementwise(0, 2, x, mask)
 
     def backward(self, grad, mb_id=0):
         ent = self._cache.pop(mb_id, None)
@@ -169,7 +172,8 @@ class Dropout(StatelessLayer):
             from ...ops import hip
             g = hip.to_act(grad, self.compute_dtype) if grad.dim() == 4 else grad.to(self.compute_dtype).contiguous()
             return hip.dropout(g, self.dropout_rate, ent[0], ent[1])
-        return grad * ent
+        from ...ops import cpu
+        return cpu.elementwise(0, 2, grad.to(ent.dtype), ent)
 
     def forward_flops(self, s):
         n = 1

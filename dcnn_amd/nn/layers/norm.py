@@ -3,7 +3,9 @@
 Reference: `include/nn/layers_impl/batchnorm_layer.tpp:27-369`,
 `include/nn/layers_impl/groupnorm_layer.tpp:21-321`. GPU path: split-reduction statistics
 (or the preceding conv's epilogue partials), one fused apply pass (+ReLU, +residual add of a
-ResNet block), fused ReLU-masked backward; x_hat is recomputed rather than stored.
+ResNet block), fused ReLU-masked backward; x_hat is recomputed rather than stored. CPU path:
+the native backend (two-pass statistics in double, fused affine/residual/ReLU, one pass per
+channel for the backward).
 dgamma/dbeta ACCUMULATE on both devices (reference defect G4).
 """
 from __future__ import annotations
@@ -107,25 +109,15 @@ class BatchNorm(ParameterizedLayer):
                 istd = torch.rsqrt(self.running_var + self.epsilon)
             self._cache[mb_id] = (xa, y if do_relu else None, mean, istd, self.training)
             return y
-        # ---- CPU reference path
-        C = self.num_features
-        if self.training:
-            mean = x.mean((0, 2, 3))
-            var = x.var((0, 2, 3), unbiased=False)
-            n = x.numel() // C
-            unbiased = var * n / max(n - 1, 1)
-            with torch.no_grad():
-                self.running_mean.mul_(1 - self.momentum).add_(self.momentum * mean)
-                self.running_var.mul_(1 - self.momentum).add_(self.momentum * unbiased)
-        else:
-            mean, var = self.running_mean, self.running_var
-        istd = torch.rsqrt(var + self.epsilon)
-        xhat = (x - mean.view(1, -1, 1, 1)) * istd.view(1, -1, 1, 1)
-        y = xhat * self._gamma().view(1, -1, 1, 1) + self._beta().view(1, -1, 1, 1) if self.affine else xhat
-        if residual is not None:
-            y = y + residual
-        if do_relu:
-            y = torch.relu(y)
+        # ---- CPU: native backend (two-pass per-channel statistics, fused affine/residual/ReLU)
+        from ...ops import cpu
+        if self.running_mean.dtype != x.dtype:
+            self.running_mean = self.running_mean.to(x.dtype)
+            self.running_var = self.running_var.to(x.dtype)
+        res = residual.to(x.dtype) if residual is not None else None
+        y, mean, istd = cpu.batchnorm_fwd(x, self._gamma(), self._beta(), self.epsilon, self.training,
+                                          self.running_mean, self.running_var, self.momentum, relu=do_relu,
+                                          residual=res)
         self._cache[mb_id] = (x, y if do_relu else None, mean, istd, self.training)
         return y
 
@@ -153,21 +145,12 @@ class BatchNorm(ParameterizedLayer):
             if self.emit_masked_grad:
                 self._last_masked[mb_id] = dmask if dmask is not None else g
             return dx
-        d = grad * (yout > 0) if yout is not None else grad
+        from ...ops import cpu
+        dx, masked = cpu.batchnorm_bwd(x, grad.to(x.dtype), yout, mean, istd, self._gamma(), dg, db,
+                                       training=was_training, want_masked=self.emit_masked_grad)
         if self.emit_masked_grad:
-            self._last_masked[mb_id] = d
-        m = istd.view(1, -1, 1, 1)
-        xhat = (x - mean.view(1, -1, 1, 1)) * m
-        gamma = self._gamma().view(1, -1, 1, 1) if self.affine else 1.0
-        sdy = d.sum((0, 2, 3))
-        sdyx = (d * xhat).sum((0, 2, 3))
-        if self.affine:
-            dg.add_(sdyx)
-            db.add_(sdy)
-        if not was_training:
-            return d * gamma * m
-        M = x.numel() // self.num_features
-        return gamma * m * (d - sdy.view(1, -1, 1, 1) / M - xhat * sdyx.view(1, -1, 1, 1) / M)
+            self._last_masked[mb_id] = masked
+        return dx
 
     def bwd_bn_spec(self, mb_id=0):
         ent = self._cache.get(mb_id)
@@ -247,14 +230,9 @@ class GroupNorm(ParameterizedLayer):
             y, mean, istd = hip.gn_fwd(xa, G, gamma, beta, self.epsilon)
             self._cache[mb_id] = (xa, mean, istd)
             return y
-        N, C, H, W = x.shape
-        xg = x.reshape(N, G, -1)
-        mean = xg.mean(-1)
-        var = xg.var(-1, unbiased=False)
-        istd = torch.rsqrt(var + self.epsilon)
-        xhat = ((xg - mean.unsqueeze(-1)) * istd.unsqueeze(-1)).reshape(N, C, H, W)
-        y = xhat * gamma.view(1, -1, 1, 1) + beta.view(1, -1, 1, 1) if self.affine else xhat
-        self._cache[mb_id] = (x, mean.reshape(-1), istd.reshape(-1))
+        from ...ops import cpu
+        y, mean, istd = cpu.groupnorm_fwd(x, G, gamma, beta, self.epsilon)
+        self._cache[mb_id] = (x, mean, istd)
         return y
 
     def backward(self, grad, mb_id=0):
@@ -270,18 +248,8 @@ class GroupNorm(ParameterizedLayer):
             from ...ops import hip
             g = hip.to_act(grad.to(x.device), self.compute_dtype)
             return hip.gn_bwd(g, x, G, gamma, mean, istd, dg, db)
-        N, C, H, W = x.shape
-        xg = x.reshape(N, G, -1)
-        xhat = ((xg - mean.view(N, G, 1)) * istd.view(N, G, 1)).reshape(N, C, H, W)
-        if self.affine:
-            dg.add_((grad * xhat).sum((0, 2, 3)))
-            db.add_(grad.sum((0, 2, 3)))
-        d = grad * gamma.view(1, -1, 1, 1) if self.affine else grad
-        dgp = d.reshape(N, G, -1)
-        xh = xhat.reshape(N, G, -1)
-        m1 = dgp.mean(-1, keepdim=True)
-        m2 = (dgp * xh).mean(-1, keepdim=True)
-        return (istd.view(N, G, 1) * (dgp - m1 - xh * m2)).reshape(N, C, H, W)
+        from ...ops import cpu
+        return cpu.groupnorm_bwd(x, grad.to(x.dtype), G, gamma, mean, istd, dg, db)
 
     def forward_flops(self, s):
         n = 1

@@ -5,8 +5,10 @@ accepted. Loss = batch mean; gradient scaled by 1/N of the tensor given (1/(N*C)
 regression losses) exactly as `src/nn/loss_impl/cpu/loss_ops.cpp`.
 
 GPU: ``loss_and_grad`` is ONE fused HIP kernel (loss + gradient + correct count, device
-scalars, no host sync — graph-capturable). ``compute_loss`` keeps the reference's host-scalar
-API (it synchronises, like the reference's D2H copy).
+scalars, no host sync — graph-capturable); CPU: the same fused pass in the native backend
+(``ops/cpu.py``). The ATen formulas in ``_cpu_loss`` / ``_cpu_grad`` are the test oracle.
+``compute_loss`` keeps the reference's host-scalar API (it synchronises, like the reference's
+D2H copy).
 """
 from __future__ import annotations
 
@@ -66,14 +68,12 @@ class Loss:
             t2, lab = self._targets(p2, target)
             loss, grad, correct = hip.loss_fused(p2, t2, lab, self.kind, self.param, want_grad)
             return loss, (grad.view(pred.shape) if grad is not None else None), correct
+        from ..ops import cpu
         t2, lab = self._targets(p2, target)
-        if lab is not None:
-            t2 = torch.nn.functional.one_hot(lab, p2.shape[1]).to(p2.dtype)
-        p2 = p2.float()
-        loss = self._cpu_loss(p2, t2)
-        grad = self._cpu_grad(p2, t2).view(pred.shape) if want_grad else None
-        correct = (p2.argmax(1) == t2.argmax(1)).sum().to(torch.int32).view(1)
-        return loss.view(1), grad, correct
+        if p2.dtype not in (torch.float32, torch.float64):
+            p2 = p2.float()
+        loss, grad, correct = cpu.loss_fused(p2, t2, lab, self.kind, self.param, want_grad)
+        return loss, (grad.view(pred.shape) if grad is not None else None), correct
 
     # ---- reference API
     def compute_loss(self, pred, target) -> float:

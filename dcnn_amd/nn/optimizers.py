@@ -4,7 +4,8 @@
 of one :class:`ParamArena` (the normal case: a Sequential or a pipeline stage), the update is
 ONE fused kernel over the flat buffer which also refreshes the bf16 shadow weights; the
 step-dependent scalars (lr, bias corrections) are read from a tiny device tensor so a
-hipGraph-captured training step replays correctly.
+hipGraph-captured training step replays correctly. A CPU arena is updated by the native
+backend's flat-buffer loops (``ops/cpu.py``), in the arena's dtype (float32 or float64).
 """
 from __future__ import annotations
 
@@ -165,7 +166,8 @@ class SGD(Optimizer):
                 self.prepare_step()
                 self.launch_step()
                 return
-            self._sgd_torch(p, g, self.velocity[0] if self.momentum > 0 else None)
+            from ..ops import cpu
+            cpu.sgd_step(p, g, self.velocity[0] if self.momentum > 0 else None, self.learning_rate, self.momentum)
             self.arena.sync_shadow()
             return
         for i, (p, g) in enumerate(zip(self.params, self.grads)):
@@ -243,6 +245,12 @@ class Adam(Optimizer):
         self.t += 1
         bc1 = 1.0 - self.beta1 ** self.t
         bc2 = 1.0 - self.beta2 ** self.t
+        if self.arena is not None and not self._flat_p.is_cuda:
+            from ..ops import cpu   # native flat-buffer step (CPU arena, float32 or float64)
+            cpu.adam_step(self._flat_p, self._flat_g, self.m[0], self.v[0], self.learning_rate, self.beta1,
+                          self.beta2, self.epsilon, bc1, bc2, self.weight_decay, self.decouple_weight_decay)
+            self.arena.sync_shadow()
+            return
         pairs = [(self._flat_p, self._flat_g)] if self.arena is not None else list(zip(self.params, self.grads))
         with torch.no_grad():
             for i, (p, g) in enumerate(pairs):

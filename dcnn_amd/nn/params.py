@@ -38,8 +38,10 @@ def _strides(shape, channels_last):
 
 
 class ParamArena:
-    def __init__(self, specs: List[ParamSpec], device: torch.device, shadow_dtype: Optional[torch.dtype] = None):
+    def __init__(self, specs: List[ParamSpec], device: torch.device, shadow_dtype: Optional[torch.dtype] = None,
+                 dtype: torch.dtype = torch.float32):
         self.device = torch.device(device)
+        self.dtype = dtype
         self.specs = list(specs)
         self.offsets = []
         off = 0
@@ -50,8 +52,8 @@ class ParamArena:
                 n *= d
             off += (n + ALIGN - 1) // ALIGN * ALIGN
         self.numel = max(off, ALIGN)
-        self.data = torch.zeros(self.numel, dtype=torch.float32, device=self.device)
-        self.grad = torch.zeros(self.numel, dtype=torch.float32, device=self.device)
+        self.data = torch.zeros(self.numel, dtype=dtype, device=self.device)
+        self.grad = torch.zeros(self.numel, dtype=dtype, device=self.device)
         self.shadow = (torch.zeros(self.numel, dtype=shadow_dtype, device=self.device)
                        if shadow_dtype is not None else None)
         self._synced_version = -1
@@ -59,7 +61,8 @@ class ParamArena:
 
     def _view(self, buf, i):
         s = self.specs[i]
-        return torch.as_strided(buf, s.shape, _strides(s.shape, s.channels_last), self.offsets[i])
+        cl = s.channels_last and self.device.type == "cuda"
+        return torch.as_strided(buf, s.shape, _strides(s.shape, cl), self.offsets[i])
 
     def param(self, i):
         return self._view(self.data, i)

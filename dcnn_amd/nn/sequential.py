@@ -171,9 +171,10 @@ class Sequential:
             bufs = self._collect_buffers()
         self.device = dev
         if dev.is_gpu():
-            self.compute_dtype = self.dtype_pref or torch.bfloat16
+            pref = self.dtype_pref if self.dtype_pref in (torch.float32, torch.bfloat16) else None
+            self.compute_dtype = pref or torch.bfloat16
         else:
-            self.compute_dtype = torch.float32
+            self.compute_dtype = torch.float64 if self.dtype_pref == torch.float64 else torch.float32
         for l in _all_layers(self.layers):
             l.device = dev
             l.set_compute_dtype(self.compute_dtype)
@@ -187,10 +188,11 @@ class Sequential:
         self._plan()
 
     def set_compute_dtype(self, dtype: torch.dtype) -> None:
-        if not self.device.is_gpu() and dtype != torch.float32:
-            raise ValueError("CPU path computes in float32 (reference semantics)")
-        if dtype not in (torch.float32, torch.bfloat16):
-            raise ValueError("compute dtype must be float32 or bfloat16")
+        """GPU: bfloat16 (default) or float32. CPU: float32 (default) or float64 — the native
+        backend's double-precision path (reference dkernels.cpp / dgemm.cpp)."""
+        ok = (torch.float32, torch.bfloat16) if self.device.is_gpu() else (torch.float32, torch.float64)
+        if dtype not in ok:
+            raise ValueError(f"compute dtype on {'GPU' if self.device.is_gpu() else 'CPU'} must be one of {ok}")
         self.dtype_pref = dtype
         self.compute_dtype = dtype
         for l in _all_layers(self.layers):
@@ -257,7 +259,8 @@ class Sequential:
                 specs.append(s)
                 owners.append(l)
         shadow = torch.bfloat16 if (self.device.is_gpu() and self.compute_dtype == torch.bfloat16) else None
-        self.arena = ParamArena(specs, self.device.torch_device, shadow)
+        adt = torch.float64 if self.compute_dtype == torch.float64 else torch.float32
+        self.arena = ParamArena(specs, self.device.torch_device, shadow, adt)
         idx = 0
         for l in leaves:
             n = len(l.param_specs())

@@ -1,10 +1,12 @@
 """Device-agnostic generic ops (reference include/ops/ops.hpp:17-944).
 
 Every op takes torch tensors and dispatches on their device: GPU tensors run the HIP kernels
-of ``csrc/kernels/ops.hip`` (fp32; anything else raises — no silent fallback), CPU tensors use
-PyTorch's CPU kernels (the CPU backend).  Reductions return a 1-element *device* tensor
+of ``csrc/kernels/ops.hip`` (fp32; anything else raises — no silent fallback), CPU tensors run
+the native C++ backend (``ops/cpu.py``, float32 and float64 — the reference's skernels.cpp /
+dkernels.cpp pair) with the same op codes. Reductions return a 1-element *device* tensor
 (the reference blocks and copies to the host on every call); call ``float()`` to
-synchronise.
+synchronise. The CPU random fills use the GPU's Philox-4x32-10 stream: the same seed gives the
+same numbers on either device.
 """
 from __future__ import annotations
 
@@ -12,6 +14,7 @@ from typing import Optional
 
 import torch
 
+from . import cpu as _cpu
 from ._ext import kernels, stream_ptr
 
 _B = {"add": 0, "sub": 1, "mul": 2, "div": 3, "min": 4, "max": 5, "equal": 6, "greater": 7}
@@ -48,8 +51,7 @@ def _binary(name, torch_fn):
     def f(a: torch.Tensor, b: torch.Tensor, out: Optional[torch.Tensor] = None) -> torch.Tensor:
         if _gpu(a, b, out):
             return _ew(0, _B[name], a, b, out)
-        r = torch_fn(a, b).to(a.dtype)
-        return out.copy_(r) if out is not None else r
+        return _cpu.elementwise(0, _B[name], a, b, out)
     f.__name__ = name
     return f
 
@@ -68,8 +70,7 @@ def _scalar(name, torch_fn):
     def f(a: torch.Tensor, s: float, out: Optional[torch.Tensor] = None) -> torch.Tensor:
         if _gpu(a, out):
             return _ew(1, _B[name], a, None, out, s)
-        r = torch_fn(a, s).to(a.dtype)
-        return out.copy_(r) if out is not None else r
+        return _cpu.elementwise(1, _B[name], a, None, out, s)
     f.__name__ = name + "_scalar"
     return f
 
@@ -85,8 +86,7 @@ def _unary(name, torch_fn):
     def f(a: torch.Tensor, out: Optional[torch.Tensor] = None) -> torch.Tensor:
         if _gpu(a, out):
             return _ew(2, _U[name], a, None, out)
-        r = torch_fn(a)
-        return out.copy_(r) if out is not None else r
+        return _cpu.elementwise(2, _U[name], a, None, out)
     f.__name__ = name
     return f
 
@@ -103,24 +103,21 @@ copy = _unary("copy", torch.clone)
 def clamp(a, lo, hi, out=None):
     if _gpu(a, out):
         return _ew(2, CLAMP, a, None, out, lo, hi)
-    r = torch.clamp(a, lo, hi)
-    return out.copy_(r) if out is not None else r
+    return _cpu.elementwise(2, CLAMP, a, None, out, lo, hi)
 
 
 def sub_mul_scalar(a, sub_v, mul_v, out=None):
     """(a - sub_v) * mul_v"""
     if _gpu(a, out):
         return _ew(2, SUB_MUL, a, None, out, sub_v, mul_v)
-    r = (a - sub_v) * mul_v
-    return out.copy_(r) if out is not None else r
+    return _cpu.elementwise(2, SUB_MUL, a, None, out, sub_v, mul_v)
 
 
 def mul_add_scalar(a, mul_v, add_v, out=None):
     """a * mul_v + add_v"""
     if _gpu(a, out):
         return _ew(2, MUL_ADD, a, None, out, mul_v, add_v)
-    r = a * mul_v + add_v
-    return out.copy_(r) if out is not None else r
+    return _cpu.elementwise(2, MUL_ADD, a, None, out, mul_v, add_v)
 
 
 def _ternary(name, torch_fn):
@@ -130,7 +127,7 @@ def _ternary(name, torch_fn):
             kernels().elementwise(3, _T[name], a.data_ptr(), b.data_ptr(), c.data_ptr(), a.numel(), 0.0, 0.0,
                                   stream_ptr())
             return c
-        return c.copy_(torch_fn(a, b, c))
+        return _cpu.ternary(_T[name], a, b, c)
     f.__name__ = name
     return f
 
@@ -145,7 +142,7 @@ def axpy(alpha: float, x: torch.Tensor, y: torch.Tensor) -> torch.Tensor:
     if _gpu(x, y):
         kernels().elementwise(4, 0, x.data_ptr(), 0, y.data_ptr(), x.numel(), float(alpha), 0.0, stream_ptr())
         return y
-    return y.add_(x, alpha=alpha)
+    return _cpu.axpy(alpha, x, y)
 
 
 def set_scalar(a: torch.Tensor, v: float) -> torch.Tensor:
@@ -164,13 +161,7 @@ def _reduce(op, a, b=None):
         kernels().reduce(op, a.data_ptr(), 0 if b is None else b.data_ptr(), a.numel(), ws.data_ptr(), out.data_ptr(),
                          stream_ptr())
         return out
-    if op == 0:
-        return a.sum().view(1)
-    if op == 1:
-        return (a * b).sum().view(1)
-    if op == 2:
-        return (a * a).sum().view(1)
-    return ((a - b) ** 2).sum().view(1)
+    return _cpu.reduce(op, a, b)
 
 
 def sum(a):  # noqa: A001
@@ -195,8 +186,7 @@ def fill_random_uniform(a: torch.Tensor, low: float = 0.0, high: float = 1.0, se
         kernels().fill_random(a.data_ptr(), a.numel(), int(seed) & ((1 << 64) - 1), float(low), float(high), 0,
                               stream_ptr())
         return a
-    g = torch.Generator().manual_seed(int(seed))
-    return a.uniform_(low, high, generator=g)
+    return _cpu.fill_random(a, low, high, seed, False)
 
 
 def fill_random_normal(a: torch.Tensor, mean: float = 0.0, std: float = 1.0, seed: int = 0) -> torch.Tensor:
@@ -204,8 +194,7 @@ def fill_random_normal(a: torch.Tensor, mean: float = 0.0, std: float = 1.0, see
         kernels().fill_random(a.data_ptr(), a.numel(), int(seed) & ((1 << 64) - 1), float(mean), float(std), 1,
                               stream_ptr())
         return a
-    g = torch.Generator().manual_seed(int(seed))
-    return a.normal_(mean, std, generator=g)
+    return _cpu.fill_random(a, mean, std, seed, True)
 
 
 # ---- layout
@@ -215,8 +204,7 @@ def transpose_2d(a: torch.Tensor, rows: int, cols: int, batch: int = 1) -> torch
         out = torch.empty(batch * rows * cols, dtype=a.dtype, device=a.device)
         kernels().transpose_batched(a.data_ptr(), out.data_ptr(), batch, rows, cols, stream_ptr())
         return out.view(batch, cols, rows) if batch > 1 else out.view(cols, rows)
-    r = a.reshape(batch, rows, cols).transpose(1, 2).contiguous()
-    return r if batch > 1 else r.view(cols, rows)
+    return _cpu.transpose_2d(a, rows, cols, batch)
 
 
 def nchw_to_cnhw(a: torch.Tensor) -> torch.Tensor:
@@ -225,7 +213,7 @@ def nchw_to_cnhw(a: torch.Tensor) -> torch.Tensor:
         out = torch.empty((C, N, H, W), dtype=a.dtype, device=a.device)
         kernels().nchw_cnhw(a.data_ptr(), out.data_ptr(), N, C, H * W, 1, stream_ptr())
         return out
-    return a.permute(1, 0, 2, 3).contiguous()
+    return _cpu.swap01(a)
 
 
 def cnhw_to_nchw(a: torch.Tensor) -> torch.Tensor:
@@ -234,4 +222,4 @@ def cnhw_to_nchw(a: torch.Tensor) -> torch.Tensor:
         out = torch.empty((N, C, H, W), dtype=a.dtype, device=a.device)
         kernels().nchw_cnhw(a.data_ptr(), out.data_ptr(), N, C, H * W, 0, stream_ptr())
         return out
-    return a.permute(1, 0, 2, 3).contiguous()
+    return _cpu.swap01(a)

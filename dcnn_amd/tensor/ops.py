@@ -1,13 +1,14 @@
 """Tensor ops (reference include/tensor/tensor_ops.hpp:14-255, CPU tensor_ops.hpp and CUDA
 tensor_ops.cpp / tensor_kernels.cu): im2col / col2im, pad / unpad / crop, batch & channel
-slicing, micro-batch split, channel softmax — NCHW fp32, GPU tensors on HIP kernels, CPU
-tensors on PyTorch CPU kernels."""
+slicing, micro-batch split, channel softmax — NCHW, GPU tensors (fp32) on HIP kernels, CPU
+tensors (fp32 / fp64) on the native C++ backend (``ops/cpu.py``)."""
 from __future__ import annotations
 
 from typing import List
 
 import torch
 
+from ..ops import cpu as _cpu
 from ..ops._ext import kernels, stream_ptr
 
 
@@ -24,19 +25,14 @@ def im2col(x: torch.Tensor, kh: int, kw: int, sh: int = 1, sw: int = 1, ph: int 
     if _gpu(x):
         from ..ops import hip
         return hip.im2col(x.contiguous(), kh, kw, sh, sw, ph, pw)
-    N, C, H, W = x.shape
-    cols = torch.nn.functional.unfold(x, (kh, kw), padding=(ph, pw), stride=(sh, sw))  # [N, C*kh*kw, L]
-    return cols.permute(1, 0, 2).reshape(C * kh * kw, -1).contiguous()
+    return _cpu.im2col(x, kh, kw, sh, sw, ph, pw)
 
 
 def col2im(col: torch.Tensor, x_shape, kh: int, kw: int, sh: int = 1, sw: int = 1, ph: int = 0, pw: int = 0):
     if _gpu(col):
         from ..ops import hip
         return hip.col2im(col, x_shape, kh, kw, sh, sw, ph, pw)
-    N, C, H, W = x_shape
-    K = C * kh * kw
-    c = col.reshape(K, N, -1).permute(1, 0, 2)
-    return torch.nn.functional.fold(c, (H, W), (kh, kw), padding=(ph, pw), stride=(sh, sw))
+    return _cpu.col2im(col, x_shape, kh, kw, sh, sw, ph, pw)
 
 
 def _pad_crop(x, OH, OW, top, left, value=0.0):
@@ -52,14 +48,14 @@ def pad(x: torch.Tensor, pad_h: int, pad_w: int, value: float = 0.0) -> torch.Te
     N, C, H, W = x.shape
     if _gpu(x):
         return _pad_crop(x, H + 2 * pad_h, W + 2 * pad_w, pad_h, pad_w, value)
-    return torch.nn.functional.pad(x, (pad_w, pad_w, pad_h, pad_h), value=value)
+    return _cpu.pad2d(x, pad_h, pad_w, value)
 
 
 def unpad(x: torch.Tensor, pad_h: int, pad_w: int) -> torch.Tensor:
     N, C, H, W = x.shape
     if _gpu(x):
         return _pad_crop(x, H - 2 * pad_h, W - 2 * pad_w, -pad_h, -pad_w)
-    return x[:, :, pad_h:H - pad_h, pad_w:W - pad_w].contiguous()
+    return _cpu.crop2d(x, pad_h, pad_w, H - 2 * pad_h, W - 2 * pad_w)
 
 
 def crop(x: torch.Tensor, start_h: int, start_w: int, end_h: int, end_w: int) -> torch.Tensor:
@@ -69,7 +65,7 @@ def crop(x: torch.Tensor, start_h: int, start_w: int, end_h: int, end_w: int) ->
         raise ValueError("Invalid crop dimensions")
     if _gpu(x):
         return _pad_crop(x, end_h - start_h + 1, end_w - start_w + 1, -start_h, -start_w)
-    return x[:, :, start_h:end_h + 1, start_w:end_w + 1].contiguous()
+    return _cpu.crop2d(x, start_h, start_w, end_h - start_h + 1, end_w - start_w + 1)
 
 
 def slice_batch(x: torch.Tensor, start: int, end: int) -> torch.Tensor:
@@ -105,4 +101,4 @@ def apply_softmax(x: torch.Tensor) -> torch.Tensor:
         N, C, H, W = x.shape
         y = hip.softmax_channels(x.contiguous(memory_format=torch.channels_last))
         return x.copy_(y)
-    return x.copy_(torch.softmax(x, dim=1))
+    return x.copy_(_cpu.softmax_channels(x))
