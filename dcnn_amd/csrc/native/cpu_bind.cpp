@@ -41,6 +41,7 @@ void bind_cpu(py::module_& parent) {
   m.def("set_num_threads", &set_num_threads);
   m.def("get_num_threads", &get_num_threads);
   m.def("gemm_uses_avx2", &gemm_uses_avx2);
+  m.def("gemm_uses_avx512", &gemm_uses_avx512);
   m.def("gemm", [](int dt, bool ta, bool tb, long M, long N, long K, double alpha, uintptr_t A, long lda, uintptr_t B,
                    long ldb, double beta, uintptr_t C, long ldc) {
     DT_DISPATCH(dt, gemm(ta, tb, M, N, K, (T)alpha, P<const T>(A), lda, P<const T>(B), ldb, (T)beta, P<T>(C), ldc));

@@ -5,19 +5,23 @@
 // (include/utils/mkl_utils.hpp:18-143). Here one GotoBLAS-style driver covers every transpose
 // combination: op(A) is packed into MR-row panels and op(B) into NR-column panels (the transpose is
 // absorbed by the packing), an MR x NR register-blocked micro-kernel runs over a KC-deep panel pair,
-// and (row block, column-panel group) tasks run on the native thread pool. The micro-kernel is
-// picked at run time: AVX2+FMA (6x16 float / 6x8 double, 12 ymm accumulators) when the CPU has it,
-// a portable scalar kernel otherwise — no -march flags, so the .so runs on any x86-64 host.
-// Every output element is owned by one task and K is always walked in the same order: results
-// are bit-identical across runs and thread counts.
-#include "cpu_kernels.h"
-
+// and (row block, column-panel group) tasks run on the native thread pool. The micro-kernel family
+// is picked at run time from the CPU's features — AVX-512 (6x32 float / 6x16 double, 12 zmm
+// accumulators), AVX2+FMA (6x16 / 6x8, 12 ymm accumulators) or portable scalar — with no -march
+// flags, so the .so runs on any x86-64 host.
+//
+// Shapes with a small output and a long reduction (a convolution's weight gradient: Co x K outputs
+// summed over N*OH*OW) are split along K into a FIXED number of slices (independent of the thread
+// count), each reduced into its own partial, and the partials are summed in slice order. Every output
+// element is owned by one task and K is always walked in the same order: results are bit-identical
+// across runs and thread counts.
 #include <immintrin.h>
 
 #include <algorithm>
 #include <cstring>
 #include <vector>
 
+#include "cpu_kernels.h"
 #include "threadpool.h"
 
 namespace dcnn_native {
@@ -25,32 +29,160 @@ namespace cpu {
 
 namespace {
 
-template <typename T>
-struct Blk;
-template <>
-struct Blk<float> {
-  static constexpr int MR = 6, NR = 16, MC = 144, KC = 256, NC = 3072;
-};
-template <>
-struct Blk<double> {
-  static constexpr int MR = 6, NR = 8, MC = 96, KC = 256, NC = 1536;
-};
-
 bool has_avx2_fma() {
   static const bool ok = __builtin_cpu_supports("avx2") && __builtin_cpu_supports("fma");
   return ok;
 }
+bool has_avx512() {
+  static const bool ok = __builtin_cpu_supports("avx512f");
+  return ok;
+}
 
-// element (i, k) of op(A), (k, j) of op(B)
-template <typename T>
-inline T a_at(const T* A, long lda, bool ta, long i, long k) { return ta ? A[k * lda + i] : A[i * lda + k]; }
-template <typename T>
-inline T b_at(const T* B, long ldb, bool tb, long k, long j) { return tb ? B[j * ldb + k] : B[k * ldb + j]; }
+// ---- micro-kernels: Ctile[rows][cols] (ldc) += alpha * sum_k Ap[k][0:MR] x Bp[k][0:NR] ----
+template <typename T, int MR, int NR>
+void micro_scalar(long kc, const T* Ap, const T* Bp, T* C, long ldc, T alpha, int rows, int cols) {
+  T acc[MR][NR] = {};
+  for (long k = 0; k < kc; ++k) {
+    const T* a = Ap + k * MR;
+    const T* b = Bp + k * NR;
+    for (int r = 0; r < MR; ++r)
+      for (int c = 0; c < NR; ++c) acc[r][c] += a[r] * b[c];
+  }
+  for (int r = 0; r < rows; ++r)
+    for (int c = 0; c < cols; ++c) C[r * ldc + c] += alpha * acc[r][c];
+}
+
+template <typename T, int MR, int NR>
+inline void store_tile(const T (&t)[MR][NR], T* C, long ldc, int rows, int cols) {
+  for (int r = 0; r < rows; ++r) {
+    T* cr = C + r * ldc;
+    for (int c = 0; c < cols; ++c) cr[c] += t[r][c];
+  }
+}
+
+// AVX2: 6 x 16 float (two ymm per row)
+__attribute__((target("avx2,fma"))) void micro_avx2_f(long kc, const float* Ap, const float* Bp, float* C, long ldc,
+                                                      float alpha, int rows, int cols) {
+  __m256 c[6][2];
+  for (int r = 0; r < 6; ++r) c[r][0] = c[r][1] = _mm256_setzero_ps();
+  for (long k = 0; k < kc; ++k) {
+    const __m256 b0 = _mm256_loadu_ps(Bp + k * 16), b1 = _mm256_loadu_ps(Bp + k * 16 + 8);
+    const float* a = Ap + k * 6;
+#pragma GCC unroll 6
+    for (int r = 0; r < 6; ++r) {
+      const __m256 av = _mm256_broadcast_ss(a + r);
+      c[r][0] = _mm256_fmadd_ps(av, b0, c[r][0]);
+      c[r][1] = _mm256_fmadd_ps(av, b1, c[r][1]);
+    }
+  }
+  const __m256 al = _mm256_set1_ps(alpha);
+  if (rows == 6 && cols == 16) {
+    for (int r = 0; r < 6; ++r) {
+      float* cr = C + r * ldc;
+      _mm256_storeu_ps(cr, _mm256_fmadd_ps(al, c[r][0], _mm256_loadu_ps(cr)));
+      _mm256_storeu_ps(cr + 8, _mm256_fmadd_ps(al, c[r][1], _mm256_loadu_ps(cr + 8)));
+    }
+    return;
+  }
+  alignas(32) float t[6][16];
+  for (int r = 0; r < 6; ++r) {
+    _mm256_store_ps(t[r], _mm256_mul_ps(al, c[r][0]));
+    _mm256_store_ps(t[r] + 8, _mm256_mul_ps(al, c[r][1]));
+  }
+  store_tile<float, 6, 16>(t, C, ldc, rows, cols);
+}
+
+// AVX2: 6 x 8 double
+__attribute__((target("avx2,fma"))) void micro_avx2_d(long kc, const double* Ap, const double* Bp, double* C, long ldc,
+                                                      double alpha, int rows, int cols) {
+  __m256d c[6][2];
+  for (int r = 0; r < 6; ++r) c[r][0] = c[r][1] = _mm256_setzero_pd();
+  for (long k = 0; k < kc; ++k) {
+    const __m256d b0 = _mm256_loadu_pd(Bp + k * 8), b1 = _mm256_loadu_pd(Bp + k * 8 + 4);
+    const double* a = Ap + k * 6;
+#pragma GCC unroll 6
+    for (int r = 0; r < 6; ++r) {
+      const __m256d av = _mm256_broadcast_sd(a + r);
+      c[r][0] = _mm256_fmadd_pd(av, b0, c[r][0]);
+      c[r][1] = _mm256_fmadd_pd(av, b1, c[r][1]);
+    }
+  }
+  alignas(32) double t[6][8];
+  const __m256d al = _mm256_set1_pd(alpha);
+  for (int r = 0; r < 6; ++r) {
+    _mm256_store_pd(t[r], _mm256_mul_pd(al, c[r][0]));
+    _mm256_store_pd(t[r] + 4, _mm256_mul_pd(al, c[r][1]));
+  }
+  store_tile<double, 6, 8>(t, C, ldc, rows, cols);
+}
+
+// AVX-512: 6 x 32 float (two zmm per row)
+__attribute__((target("avx512f"))) void micro_avx512_f(long kc, const float* Ap, const float* Bp, float* C, long ldc,
+                                                       float alpha, int rows, int cols) {
+  __m512 c[6][2];
+  for (int r = 0; r < 6; ++r) c[r][0] = c[r][1] = _mm512_setzero_ps();
+  for (long k = 0; k < kc; ++k) {
+    const __m512 b0 = _mm512_loadu_ps(Bp + k * 32), b1 = _mm512_loadu_ps(Bp + k * 32 + 16);
+    const float* a = Ap + k * 6;
+#pragma GCC unroll 6
+    for (int r = 0; r < 6; ++r) {
+      const __m512 av = _mm512_set1_ps(a[r]);
+      c[r][0] = _mm512_fmadd_ps(av, b0, c[r][0]);
+      c[r][1] = _mm512_fmadd_ps(av, b1, c[r][1]);
+    }
+  }
+  const __m512 al = _mm512_set1_ps(alpha);
+  if (rows == 6 && cols == 32) {
+    for (int r = 0; r < 6; ++r) {
+      float* cr = C + r * ldc;
+      _mm512_storeu_ps(cr, _mm512_fmadd_ps(al, c[r][0], _mm512_loadu_ps(cr)));
+      _mm512_storeu_ps(cr + 16, _mm512_fmadd_ps(al, c[r][1], _mm512_loadu_ps(cr + 16)));
+    }
+    return;
+  }
+  alignas(64) float t[6][32];
+  for (int r = 0; r < 6; ++r) {
+    _mm512_store_ps(t[r], _mm512_mul_ps(al, c[r][0]));
+    _mm512_store_ps(t[r] + 16, _mm512_mul_ps(al, c[r][1]));
+  }
+  store_tile<float, 6, 32>(t, C, ldc, rows, cols);
+}
+
+// AVX-512: 6 x 16 double
+__attribute__((target("avx512f"))) void micro_avx512_d(long kc, const double* Ap, const double* Bp, double* C,
+                                                       long ldc, double alpha, int rows, int cols) {
+  __m512d c[6][2];
+  for (int r = 0; r < 6; ++r) c[r][0] = c[r][1] = _mm512_setzero_pd();
+  for (long k = 0; k < kc; ++k) {
+    const __m512d b0 = _mm512_loadu_pd(Bp + k * 16), b1 = _mm512_loadu_pd(Bp + k * 16 + 8);
+    const double* a = Ap + k * 6;
+#pragma GCC unroll 6
+    for (int r = 0; r < 6; ++r) {
+      const __m512d av = _mm512_set1_pd(a[r]);
+      c[r][0] = _mm512_fmadd_pd(av, b0, c[r][0]);
+      c[r][1] = _mm512_fmadd_pd(av, b1, c[r][1]);
+    }
+  }
+  alignas(64) double t[6][16];
+  const __m512d al = _mm512_set1_pd(alpha);
+  for (int r = 0; r < 6; ++r) {
+    _mm512_store_pd(t[r], _mm512_mul_pd(al, c[r][0]));
+    _mm512_store_pd(t[r] + 8, _mm512_mul_pd(al, c[r][1]));
+  }
+  store_tile<double, 6, 16>(t, C, ldc, rows, cols);
+}
+
+// ---- kernel families: blocking + micro-kernel ----
+template <typename T, int MR_, int NR_, int MC_, int KC_, int NC_>
+struct Family {
+  static constexpr int MR = MR_, NR = NR_, MC = MC_, KC = KC_, NC = NC_;
+  using Micro = void (*)(long, const T*, const T*, T*, long, T, int, int);
+  Micro micro;
+};
 
 // pack op(A)[i0:i0+mc, k0:k0+kc] into MR-row panels: dst[p][k][r], zero-padded rows
-template <typename T>
+template <typename T, int MR>
 void pack_a(const T* A, long lda, bool ta, long i0, long mc, long k0, long kc, T* dst) {
-  constexpr int MR = Blk<T>::MR;
   for (long p = 0; p < mc; p += MR) {
     const int rows = (int)std::min<long>(MR, mc - p);
     T* d = dst + p * kc;
@@ -69,10 +201,9 @@ void pack_a(const T* A, long lda, bool ta, long i0, long mc, long k0, long kc, T
   }
 }
 
-// pack op(B)[k0:k0+kc, j0:j0+nc] into NR-column panels: dst[q][k][c], zero-padded columns
-template <typename T>
+// pack op(B)[k0:k0+kc, j:j+cols] into one NR-column panel: d[k][c], zero-padded columns
+template <typename T, int NR>
 void pack_b_panel(const T* B, long ldb, bool tb, long k0, long kc, long j, int cols, T* d) {
-  constexpr int NR = Blk<T>::NR;
   if (!tb) {
     for (long k = 0; k < kc; ++k) {
       const T* src = B + (k0 + k) * ldb + j;
@@ -80,100 +211,13 @@ void pack_b_panel(const T* B, long ldb, bool tb, long k0, long kc, long j, int c
       for (int c = cols; c < NR; ++c) d[k * NR + c] = T(0);
     }
   } else {
-    for (long k = 0; k < kc; ++k) {
-      for (int c = 0; c < cols; ++c) d[k * NR + c] = B[(j + c) * ldb + k0 + k];
+    for (int c = 0; c < cols; ++c) {
+      const T* src = B + (j + c) * ldb + k0;
+      for (long k = 0; k < kc; ++k) d[k * NR + c] = src[k];
+    }
+    for (long k = 0; k < kc; ++k)
       for (int c = cols; c < NR; ++c) d[k * NR + c] = T(0);
-    }
   }
-}
-
-// ---- micro-kernels: Ctile[MR][NR] (ldc) += alpha * sum_k Ap[k][:] x Bp[k][:] ----
-template <typename T>
-void micro_scalar(long kc, const T* Ap, const T* Bp, T* C, long ldc, T alpha, int rows, int cols) {
-  constexpr int MR = Blk<T>::MR, NR = Blk<T>::NR;
-  T acc[MR][NR] = {};
-  for (long k = 0; k < kc; ++k) {
-    const T* a = Ap + k * MR;
-    const T* b = Bp + k * NR;
-    for (int r = 0; r < MR; ++r)
-      for (int c = 0; c < NR; ++c) acc[r][c] += a[r] * b[c];
-  }
-  for (int r = 0; r < rows; ++r)
-    for (int c = 0; c < cols; ++c) C[r * ldc + c] += alpha * acc[r][c];
-}
-
-__attribute__((target("avx2,fma"))) void micro_avx2(long kc, const float* Ap, const float* Bp, float* C, long ldc,
-                                                    float alpha, int rows, int cols) {
-  __m256 c00 = _mm256_setzero_ps(), c01 = _mm256_setzero_ps(), c10 = _mm256_setzero_ps(), c11 = _mm256_setzero_ps();
-  __m256 c20 = _mm256_setzero_ps(), c21 = _mm256_setzero_ps(), c30 = _mm256_setzero_ps(), c31 = _mm256_setzero_ps();
-  __m256 c40 = _mm256_setzero_ps(), c41 = _mm256_setzero_ps(), c50 = _mm256_setzero_ps(), c51 = _mm256_setzero_ps();
-  for (long k = 0; k < kc; ++k) {
-    const __m256 b0 = _mm256_loadu_ps(Bp + k * 16), b1 = _mm256_loadu_ps(Bp + k * 16 + 8);
-    const float* a = Ap + k * 6;
-    __m256 a0 = _mm256_broadcast_ss(a + 0);
-    c00 = _mm256_fmadd_ps(a0, b0, c00); c01 = _mm256_fmadd_ps(a0, b1, c01);
-    a0 = _mm256_broadcast_ss(a + 1);
-    c10 = _mm256_fmadd_ps(a0, b0, c10); c11 = _mm256_fmadd_ps(a0, b1, c11);
-    a0 = _mm256_broadcast_ss(a + 2);
-    c20 = _mm256_fmadd_ps(a0, b0, c20); c21 = _mm256_fmadd_ps(a0, b1, c21);
-    a0 = _mm256_broadcast_ss(a + 3);
-    c30 = _mm256_fmadd_ps(a0, b0, c30); c31 = _mm256_fmadd_ps(a0, b1, c31);
-    a0 = _mm256_broadcast_ss(a + 4);
-    c40 = _mm256_fmadd_ps(a0, b0, c40); c41 = _mm256_fmadd_ps(a0, b1, c41);
-    a0 = _mm256_broadcast_ss(a + 5);
-    c50 = _mm256_fmadd_ps(a0, b0, c50); c51 = _mm256_fmadd_ps(a0, b1, c51);
-  }
-  alignas(32) float t[6][16];
-  const __m256 al = _mm256_set1_ps(alpha);
-  _mm256_store_ps(t[0], _mm256_mul_ps(al, c00)); _mm256_store_ps(t[0] + 8, _mm256_mul_ps(al, c01));
-  _mm256_store_ps(t[1], _mm256_mul_ps(al, c10)); _mm256_store_ps(t[1] + 8, _mm256_mul_ps(al, c11));
-  _mm256_store_ps(t[2], _mm256_mul_ps(al, c20)); _mm256_store_ps(t[2] + 8, _mm256_mul_ps(al, c21));
-  _mm256_store_ps(t[3], _mm256_mul_ps(al, c30)); _mm256_store_ps(t[3] + 8, _mm256_mul_ps(al, c31));
-  _mm256_store_ps(t[4], _mm256_mul_ps(al, c40)); _mm256_store_ps(t[4] + 8, _mm256_mul_ps(al, c41));
-  _mm256_store_ps(t[5], _mm256_mul_ps(al, c50)); _mm256_store_ps(t[5] + 8, _mm256_mul_ps(al, c51));
-  if (cols == 16) {
-    for (int r = 0; r < rows; ++r) {
-      float* cr = C + r * ldc;
-      _mm256_storeu_ps(cr, _mm256_add_ps(_mm256_loadu_ps(cr), _mm256_load_ps(t[r])));
-      _mm256_storeu_ps(cr + 8, _mm256_add_ps(_mm256_loadu_ps(cr + 8), _mm256_load_ps(t[r] + 8)));
-    }
-  } else {
-    for (int r = 0; r < rows; ++r)
-      for (int c = 0; c < cols; ++c) C[r * ldc + c] += t[r][c];
-  }
-}
-
-__attribute__((target("avx2,fma"))) void micro_avx2(long kc, const double* Ap, const double* Bp, double* C, long ldc,
-                                                    double alpha, int rows, int cols) {
-  __m256d c00 = _mm256_setzero_pd(), c01 = _mm256_setzero_pd(), c10 = _mm256_setzero_pd(), c11 = _mm256_setzero_pd();
-  __m256d c20 = _mm256_setzero_pd(), c21 = _mm256_setzero_pd(), c30 = _mm256_setzero_pd(), c31 = _mm256_setzero_pd();
-  __m256d c40 = _mm256_setzero_pd(), c41 = _mm256_setzero_pd(), c50 = _mm256_setzero_pd(), c51 = _mm256_setzero_pd();
-  for (long k = 0; k < kc; ++k) {
-    const __m256d b0 = _mm256_loadu_pd(Bp + k * 8), b1 = _mm256_loadu_pd(Bp + k * 8 + 4);
-    const double* a = Ap + k * 6;
-    __m256d a0 = _mm256_broadcast_sd(a + 0);
-    c00 = _mm256_fmadd_pd(a0, b0, c00); c01 = _mm256_fmadd_pd(a0, b1, c01);
-    a0 = _mm256_broadcast_sd(a + 1);
-    c10 = _mm256_fmadd_pd(a0, b0, c10); c11 = _mm256_fmadd_pd(a0, b1, c11);
-    a0 = _mm256_broadcast_sd(a + 2);
-    c20 = _mm256_fmadd_pd(a0, b0, c20); c21 = _mm256_fmadd_pd(a0, b1, c21);
-    a0 = _mm256_broadcast_sd(a + 3);
-    c30 = _mm256_fmadd_pd(a0, b0, c30); c31 = _mm256_fmadd_pd(a0, b1, c31);
-    a0 = _mm256_broadcast_sd(a + 4);
-    c40 = _mm256_fmadd_pd(a0, b0, c40); c41 = _mm256_fmadd_pd(a0, b1, c41);
-    a0 = _mm256_broadcast_sd(a + 5);
-    c50 = _mm256_fmadd_pd(a0, b0, c50); c51 = _mm256_fmadd_pd(a0, b1, c51);
-  }
-  alignas(32) double t[6][8];
-  const __m256d al = _mm256_set1_pd(alpha);
-  _mm256_store_pd(t[0], _mm256_mul_pd(al, c00)); _mm256_store_pd(t[0] + 4, _mm256_mul_pd(al, c01));
-  _mm256_store_pd(t[1], _mm256_mul_pd(al, c10)); _mm256_store_pd(t[1] + 4, _mm256_mul_pd(al, c11));
-  _mm256_store_pd(t[2], _mm256_mul_pd(al, c20)); _mm256_store_pd(t[2] + 4, _mm256_mul_pd(al, c21));
-  _mm256_store_pd(t[3], _mm256_mul_pd(al, c30)); _mm256_store_pd(t[3] + 4, _mm256_mul_pd(al, c31));
-  _mm256_store_pd(t[4], _mm256_mul_pd(al, c40)); _mm256_store_pd(t[4] + 4, _mm256_mul_pd(al, c41));
-  _mm256_store_pd(t[5], _mm256_mul_pd(al, c50)); _mm256_store_pd(t[5] + 4, _mm256_mul_pd(al, c51));
-  for (int r = 0; r < rows; ++r)
-    for (int c = 0; c < cols; ++c) C[r * ldc + c] += t[r][c];
 }
 
 template <typename T>
@@ -190,65 +234,116 @@ void scale_c(T* C, long M, long N, long ldc, T beta) {
   });
 }
 
-template <typename T>
-void gemm_impl(bool ta, bool tb, long M, long N, long K, T alpha, const T* A, long lda, const T* B, long ldb, T beta,
-               T* C, long ldc) {
-  using Bk = Blk<T>;
-  constexpr int MR = Bk::MR, NR = Bk::NR;
-  scale_c(C, M, N, ldc, beta);
-  if (M <= 0 || N <= 0 || K <= 0 || alpha == T(0)) return;
-  const bool avx = has_avx2_fma();
-  std::vector<T> bpack;
-  for (long jc = 0; jc < N; jc += Bk::NC) {
-    const long nc = std::min<long>(Bk::NC, N - jc);
+// C += alpha * op(A) op(B) over k in [k0, k1). `serial` runs everything on the calling thread.
+template <typename T, typename F>
+void gemm_accumulate(const F& fam, bool ta, bool tb, long M, long N, long k0, long k1, T alpha, const T* A, long lda,
+                     const T* B, long ldb, T* C, long ldc, bool serial) {
+  constexpr int MR = F::MR, NR = F::NR, MC = F::MC, KC = F::KC, NC = F::NC;
+  std::vector<T> bpack, apack;
+  for (long jc = 0; jc < N; jc += NC) {
+    const long nc = std::min<long>(NC, N - jc);
     const long npan = (nc + NR - 1) / NR;
-    for (long pc = 0; pc < K; pc += Bk::KC) {
-      const long kc = std::min<long>(Bk::KC, K - pc);
+    for (long pc = k0; pc < k1; pc += KC) {
+      const long kc = std::min<long>(KC, k1 - pc);
       bpack.resize((size_t)npan * NR * kc);
+      const long mblocks = (M + MC - 1) / MC;
+      const long arows = mblocks * MC;
+      apack.resize((size_t)((arows + MR - 1) / MR) * MR * kc);
       T* bp = bpack.data();
-      parallel_for(0, npan, std::max(1L, 4096 / kc), [&](long lo, long hi) {
-        for (long q = lo; q < hi; ++q)
-          pack_b_panel(B, ldb, tb, pc, kc, jc + q * NR, (int)std::min<long>(NR, nc - q * NR), bp + q * kc * NR);
-      });
-      // tasks: (row block of MC) x (group of column panels); more groups when rows are few
-      const long mblocks = (M + Bk::MC - 1) / Bk::MC;
-      const long want = (long)get_num_threads() * 2;
+      T* ap = apack.data();
+      // pack every B panel and every A row block once (one parallel region)
+      auto pack = [&](long t) {
+        if (t < npan) {
+          pack_b_panel<T, NR>(B, ldb, tb, pc, kc, jc + t * NR, (int)std::min<long>(NR, nc - t * NR), bp + t * kc * NR);
+        } else {
+          const long ib = t - npan, i0 = ib * MC;
+          pack_a<T, MR>(A, lda, ta, i0, std::min<long>(MC, M - i0), pc, kc, ap + i0 * kc);
+        }
+      };
+      if (serial) {
+        for (long t = 0; t < npan + mblocks; ++t) pack(t);
+      } else {
+        ThreadPool::instance().run(npan + mblocks, pack);
+      }
+      // tasks: (row block) x (group of column panels); more groups when row blocks are few
+      const long want = serial ? 1 : (long)get_num_threads() * 2;
       const long groups = std::max(1L, std::min(npan, (want + mblocks - 1) / mblocks));
-      ThreadPool::instance().run(mblocks * groups, [&](long task) {
+      auto compute = [&](long task) {
         const long ib = task / groups, g = task % groups;
-        const long i0 = ib * Bk::MC, mc = std::min<long>(Bk::MC, M - i0);
+        const long i0 = ib * MC, mc = std::min<long>(MC, M - i0);
         const long q0 = g * npan / groups, q1 = (g + 1) * npan / groups;
-        thread_local std::vector<T> apack;
-        apack.resize((size_t)((mc + MR - 1) / MR) * MR * kc);
-        pack_a(A, lda, ta, i0, mc, pc, kc, apack.data());
+        const T* aps = ap + i0 * kc;
         for (long q = q0; q < q1; ++q) {
           const int cols = (int)std::min<long>(NR, nc - q * NR);
           const T* bq = bp + q * kc * NR;
           for (long p = 0; p < mc; p += MR) {
             const int rows = (int)std::min<long>(MR, mc - p);
-            T* ct = C + (i0 + p) * ldc + jc + q * NR;
-            if (avx)
-              micro_avx2(kc, apack.data() + p * kc, bq, ct, ldc, alpha, rows, cols);
-            else
-              micro_scalar<T>(kc, apack.data() + p * kc, bq, ct, ldc, alpha, rows, cols);
+            fam.micro(kc, aps + p * kc, bq, C + (i0 + p) * ldc + jc + q * NR, ldc, alpha, rows, cols);
           }
         }
-      });
+      };
+      if (serial) {
+        for (long t = 0; t < mblocks * groups; ++t) compute(t);
+      } else {
+        ThreadPool::instance().run(mblocks * groups, compute);
+      }
     }
   }
 }
+
+template <typename T, typename F>
+void gemm_impl(const F& fam, bool ta, bool tb, long M, long N, long K, T alpha, const T* A, long lda, const T* B,
+               long ldb, T beta, T* C, long ldc) {
+  scale_c(C, M, N, ldc, beta);
+  if (M <= 0 || N <= 0 || K <= 0 || alpha == T(0)) return;
+  // small output, long reduction: fixed K slices into private partials, summed in slice order
+  const long slices = std::min<long>(16, K / (4L * F::KC));
+  if (slices >= 2 && M * N <= 96L * 1024) {  // (inside a parallel region the slices run serially)
+    std::vector<T> part((size_t)slices * M * N, T(0));
+    ThreadPool::instance().run(slices, [&](long s) {
+      const long k0 = s * K / slices, k1 = (s + 1) * K / slices;
+      gemm_accumulate(fam, ta, tb, M, N, k0, k1, alpha, A, lda, B, ldb, part.data() + s * M * N, N, true);
+    });
+    parallel_for(0, M, std::max(1L, 4096 / N), [&](long lo, long hi) {
+      for (long i = lo; i < hi; ++i)
+        for (long s = 0; s < slices; ++s) {
+          const T* pr = part.data() + (s * M + i) * N;
+          T* cr = C + i * ldc;
+          for (long j = 0; j < N; ++j) cr[j] += pr[j];
+        }
+    });
+    return;
+  }
+  gemm_accumulate(fam, ta, tb, M, N, 0, K, alpha, A, lda, B, ldb, C, ldc, in_parallel_region());
+}
+
+using F512 = Family<float, 6, 32, 192, 256, 4096>;
+using D512 = Family<double, 6, 16, 96, 256, 2048>;
+using F256 = Family<float, 6, 16, 144, 256, 3072>;
+using D256 = Family<double, 6, 8, 96, 256, 1536>;
 
 }  // namespace
 
 void gemm(bool ta, bool tb, long M, long N, long K, float alpha, const float* A, long lda, const float* B, long ldb,
           float beta, float* C, long ldc) {
-  gemm_impl<float>(ta, tb, M, N, K, alpha, A, lda, B, ldb, beta, C, ldc);
+  if (has_avx512())
+    gemm_impl(F512{&micro_avx512_f}, ta, tb, M, N, K, alpha, A, lda, B, ldb, beta, C, ldc);
+  else if (has_avx2_fma())
+    gemm_impl(F256{&micro_avx2_f}, ta, tb, M, N, K, alpha, A, lda, B, ldb, beta, C, ldc);
+  else
+    gemm_impl(F256{&micro_scalar<float, 6, 16>}, ta, tb, M, N, K, alpha, A, lda, B, ldb, beta, C, ldc);
 }
 void gemm(bool ta, bool tb, long M, long N, long K, double alpha, const double* A, long lda, const double* B, long ldb,
           double beta, double* C, long ldc) {
-  gemm_impl<double>(ta, tb, M, N, K, alpha, A, lda, B, ldb, beta, C, ldc);
+  if (has_avx512())
+    gemm_impl(D512{&micro_avx512_d}, ta, tb, M, N, K, alpha, A, lda, B, ldb, beta, C, ldc);
+  else if (has_avx2_fma())
+    gemm_impl(D256{&micro_avx2_d}, ta, tb, M, N, K, alpha, A, lda, B, ldb, beta, C, ldc);
+  else
+    gemm_impl(D256{&micro_scalar<double, 6, 8>}, ta, tb, M, N, K, alpha, A, lda, B, ldb, beta, C, ldc);
 }
 bool gemm_uses_avx2() { return has_avx2_fma(); }
+bool gemm_uses_avx512() { return has_avx512(); }
 
 }  // namespace cpu
 }  // namespace dcnn_native

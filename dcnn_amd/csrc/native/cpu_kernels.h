@@ -17,6 +17,7 @@ void gemm(bool ta, bool tb, long M, long N, long K, float alpha, const float* A,
 void gemm(bool ta, bool tb, long M, long N, long K, double alpha, const double* A, long lda, const double* B, long ldb,
           double beta, double* C, long ldc);
 bool gemm_uses_avx2();
+bool gemm_uses_avx512();
 
 template <typename T> void elementwise(int mode, int op, const T* a, const T* b, T* c, long n, double s0, double s1);
 template <typename T> double reduce(int op, const T* a, const T* b, long n);

@@ -57,67 +57,79 @@ inline int out_dim(int in, int k, int s, int p) { return (in + 2 * p - k) / s + 
 }  // namespace
 
 // ------------------------------------------------------------------ elementwise
-// codes shared with the GPU generic ops (ops/generic.py, csrc/kernels/ops.hip)
+// codes shared with the GPU generic ops (ops/generic.py, csrc/kernels/ops.hip). The op switch is
+// resolved once per call; each op body is a plain loop the compiler vectorises.
+namespace {
+template <typename T, typename F>
+void map1(const T* a, T* c, long n, F f) {
+  for_chunks(n, kGrain, [&](long lo, long hi) {
+    for (long i = lo; i < hi; ++i) c[i] = f(a[i]);
+  });
+}
+template <typename T, typename F>
+void map2(const T* a, const T* b, T* c, long n, F f) {
+  for_chunks(n, kGrain, [&](long lo, long hi) {
+    for (long i = lo; i < hi; ++i) c[i] = f(a[i], b[i]);
+  });
+}
+}  // namespace
+
 template <typename T>
 void elementwise(int mode, int op, const T* a, const T* b, T* c, long n, double s0, double s1) {
   const T x0 = (T)s0, x1 = (T)s1;
-  for_chunks(n, kGrain, [&](long lo, long hi) {
-    switch (mode) {
-      case 0:  // binary
-      case 1: {  // tensor-scalar
-        for (long i = lo; i < hi; ++i) {
-          const T u = a[i], v = mode == 0 ? b[i] : x0;
-          T r;
-          switch (op) {
-            case 0: r = u + v; break;
-            case 1: r = u - v; break;
-            case 2: r = u * v; break;
-            case 3: r = u / v; break;
-            case 4: r = std::min(u, v); break;
-            case 5: r = std::max(u, v); break;
-            case 6: r = (T)(u == v); break;
-            case 7: r = (T)(u > v); break;
-            default: throw std::invalid_argument("elementwise: bad binary op");
-          }
-          c[i] = r;
-        }
-        break;
-      }
-      case 2: {  // unary / parametrised unary
-        for (long i = lo; i < hi; ++i) {
-          const T u = a[i];
-          T r;
-          switch (op) {
-            case 16: r = std::sqrt(u); break;
-            case 17: r = T(1) / std::sqrt(u); break;
-            case 18: r = T(1) / u; break;
-            case 19: r = std::abs(u); break;
-            case 20: r = -u; break;
-            case 21: r = std::exp(u); break;
-            case 22: r = std::log(u); break;
-            case 23: r = u; break;
-            case 48: r = std::min(std::max(u, x0), x1); break;  // clamp
-            case 49: r = (u - x0) * x1; break;                  // sub_mul
-            case 50: r = u * x0 + x1; break;                    // mul_add
-            default: throw std::invalid_argument("elementwise: bad unary op");
-          }
-          c[i] = r;
-        }
-        break;
-      }
-      case 3:  // ternary, in place on c
-        for (long i = lo; i < hi; ++i) {
-          const T p = a[i] * b[i];
-          c[i] = op == 32 ? p + c[i] : op == 33 ? p - c[i] : c[i] - p;
-        }
-        break;
-      case 4:  // axpy: c += s0 * a
-        for (long i = lo; i < hi; ++i) c[i] += x0 * a[i];
-        break;
-      default:
-        throw std::invalid_argument("elementwise: bad mode");
+  if (mode == 0 || mode == 1) {
+    auto bin = [&](auto f) {
+      if (mode == 0)
+        map2(a, b, c, n, f);
+      else
+        map1(a, c, n, [&](T u) { return f(u, x0); });
+    };
+    switch (op) {
+      case 0: return bin([](T u, T v) { return u + v; });
+      case 1: return bin([](T u, T v) { return u - v; });
+      case 2: return bin([](T u, T v) { return u * v; });
+      case 3: return bin([](T u, T v) { return u / v; });
+      case 4: return bin([](T u, T v) { return u < v ? u : v; });
+      case 5: return bin([](T u, T v) { return u > v ? u : v; });
+      case 6: return bin([](T u, T v) { return (T)(u == v); });
+      case 7: return bin([](T u, T v) { return (T)(u > v); });
     }
-  });
+    throw std::invalid_argument("elementwise: bad binary op");
+  }
+  if (mode == 2) {
+    switch (op) {
+      case 16: return map1(a, c, n, [](T u) { return std::sqrt(u); });
+      case 17: return map1(a, c, n, [](T u) { return T(1) / std::sqrt(u); });
+      case 18: return map1(a, c, n, [](T u) { return T(1) / u; });
+      case 19: return map1(a, c, n, [](T u) { return std::abs(u); });
+      case 20: return map1(a, c, n, [](T u) { return -u; });
+      case 21: return map1(a, c, n, [](T u) { return std::exp(u); });
+      case 22: return map1(a, c, n, [](T u) { return std::log(u); });
+      case 23: return map1(a, c, n, [](T u) { return u; });
+      case 48: return map1(a, c, n, [&](T u) { return u < x0 ? x0 : (u > x1 ? x1 : u); });  // clamp
+      case 49: return map1(a, c, n, [&](T u) { return (u - x0) * x1; });                   // sub_mul
+      case 50: return map1(a, c, n, [&](T u) { return u * x0 + x1; });                     // mul_add
+    }
+    throw std::invalid_argument("elementwise: bad unary op");
+  }
+  if (mode == 3) {  // ternary, in place on c
+    for_chunks(n, kGrain, [&](long lo, long hi) {
+      if (op == 32)
+        for (long i = lo; i < hi; ++i) c[i] = a[i] * b[i] + c[i];
+      else if (op == 33)
+        for (long i = lo; i < hi; ++i) c[i] = a[i] * b[i] - c[i];
+      else
+        for (long i = lo; i < hi; ++i) c[i] = c[i] - a[i] * b[i];
+    });
+    return;
+  }
+  if (mode == 4) {  // axpy: c += s0 * a
+    for_chunks(n, kGrain, [&](long lo, long hi) {
+      for (long i = lo; i < hi; ++i) c[i] += x0 * a[i];
+    });
+    return;
+  }
+  throw std::invalid_argument("elementwise: bad mode");
 }
 
 // op 0 sum(a), 1 dot(a, b), 2 sum(a^2), 3 sum((a-b)^2)
@@ -329,13 +341,43 @@ void per_sample(long N, F&& fn) {
 }
 }  // namespace
 
-// y[n] = W[Co, C*KH*KW] @ col_n + bias
+// Two schedules:
+// * batched (small feature maps, where one sample's GEMM is too small to run efficiently):
+//   col[K][N*L] for the whole batch (the reference's layout), ONE GEMM W[Co][K] @ col -> Y'[Co][N*L],
+//   then CNHW -> NCHW; the backward runs the weight gradient as one GEMM over the N*L axis;
+// * per sample (large feature maps): a per-sample im2col panel from a thread-local buffer and
+//   the GEMM writing straight into the NCHW output.
+namespace {
+template <typename T>
+bool conv_batched(long N, long K, long L) {
+  return L < 1024 && (double)K * N * L * sizeof(T) <= 256.0 * (1 << 20);
+}
+template <typename T>
+void add_bias_nchw(T* y, const T* bias, long N, long Co, long L) {
+  parallel_for(0, N * Co, std::max(1L, 8192 / std::max(1L, L)), [&](long lo, long hi) {
+    for (long t = lo; t < hi; ++t) {
+      T* r = y + t * L;
+      const T bv = bias[t % Co];
+      for (long i = 0; i < L; ++i) r[i] += bv;
+    }
+  });
+}
+}  // namespace
+
 template <typename T>
 void conv2d_fwd(const T* x, const T* w, const T* bias, T* y, int N, int C, int H, int W, int Co, int KH, int KW, int SH,
                 int SW, int PH, int PW) {
   const int OH = out_dim(H, KH, SH, PH), OW = out_dim(W, KW, SW, PW);
   const long L = (long)OH * OW, K = (long)C * KH * KW;
   const bool direct = is_1x1_direct(KH, KW, SH, SW, PH, PW);
+  if (conv_batched<T>(N, K, L) && N > 1) {
+    std::vector<T> col((size_t)K * N * L), yc((size_t)Co * N * L);
+    im2col(x, col.data(), N, C, H, W, KH, KW, SH, SW, PH, PW);
+    gemm(false, false, Co, N * L, K, T(1), w, K, col.data(), N * L, T(0), yc.data(), N * L);
+    swap01(yc.data(), y, Co, N, L);
+    if (bias) add_bias_nchw(y, bias, N, Co, L);
+    return;
+  }
   per_sample(N, [&](long n) {
     const T* xn = x + n * C * H * W;
     T* yn = y + n * Co * L;
@@ -346,13 +388,8 @@ void conv2d_fwd(const T* x, const T* w, const T* bias, T* y, int N, int C, int H
       col = buf.data();
     }
     gemm(false, false, Co, L, K, T(1), w, K, col, L, T(0), yn, L);
-    if (bias)
-      for (int co = 0; co < Co; ++co) {
-        T* r = yn + co * L;
-        const T bv = bias[co];
-        for (long i = 0; i < L; ++i) r[i] += bv;
-      }
   });
+  if (bias) add_bias_nchw(y, bias, N, Co, L);
 }
 
 // dx (overwrite, may be null), dw += sum_n dy_n @ col_n^T, db += sum dy (may be null).
@@ -363,6 +400,30 @@ void conv2d_bwd(const T* x, const T* w, const T* dy, T* dx, T* dw, T* db, int N,
   const int OH = out_dim(H, KH, SH, PH), OW = out_dim(W, KW, SW, PW);
   const long L = (long)OH * OW, K = (long)C * KH * KW;
   const bool direct = is_1x1_direct(KH, KW, SH, SW, PH, PW);
+  // ---- bias gradient (per channel, samples then pixels in order)
+  if (db) {
+    parallel_for(0, Co, 1, [&](long lo, long hi) {
+      for (long co = lo; co < hi; ++co) {
+        double s = 0.0;
+        for (long n = 0; n < N; ++n) {
+          const T* r = dy + (n * Co + co) * L;
+          for (long i = 0; i < L; ++i) s += r[i];
+        }
+        db[co] += (T)s;
+      }
+    });
+  }
+  if (conv_batched<T>(N, K, L) && N > 1) {
+    std::vector<T> col((size_t)K * N * L), dyc((size_t)Co * N * L);
+    im2col(x, col.data(), N, C, H, W, KH, KW, SH, SW, PH, PW);
+    swap01(dy, dyc.data(), N, Co, L);  // [Co][N*L]
+    gemm(false, true, Co, K, N * L, T(1), dyc.data(), N * L, col.data(), N * L, T(1), dw, K);
+    if (dx) {
+      gemm(true, false, K, N * L, Co, T(1), w, K, dyc.data(), N * L, T(0), col.data(), N * L);
+      col2im(col.data(), dx, N, C, H, W, KH, KW, SH, SW, PH, PW);
+    }
+    return;
+  }
   // ---- weight gradient: fixed sample chunks (independent of the thread count), each chunk's
   // partial in its own slab, slabs summed in chunk order
   const long nch = std::min<long>(N, 16);
@@ -394,19 +455,6 @@ void conv2d_bwd(const T* x, const T* w, const T* dy, T* dx, T* dw, T* db, int N,
     });
   } else {
     wgrad_range(0, N, dw, T(1));
-  }
-  // ---- bias gradient (per channel, samples then pixels in order)
-  if (db) {
-    parallel_for(0, Co, 1, [&](long lo, long hi) {
-      for (long co = lo; co < hi; ++co) {
-        double s = 0.0;
-        for (long n = 0; n < N; ++n) {
-          const T* r = dy + (n * Co + co) * L;
-          for (long i = 0; i < L; ++i) s += r[i];
-        }
-        db[co] += (T)s;
-      }
-    });
   }
   // ---- data gradient: col_n = W^T @ dy_n, scattered back
   if (dx) {
@@ -632,31 +680,29 @@ template <typename T>
 void maxpool_fwd(const T* x, T* y, int32_t* idx, long NC, int H, int W, int KH, int KW, int SH, int SW, int PH,
                  int PW) {
   const int OH = out_dim(H, KH, SH, PH), OW = out_dim(W, KW, SW, PW);
-  parallel_for(0, NC, 1, [&](long lo, long hi) {
+  parallel_for(0, NC, std::max(1L, 4096L / std::max(1, H * W)), [&](long lo, long hi) {
     for (long p = lo; p < hi; ++p) {
       const T* xp = x + p * H * W;
-      for (int oh = 0; oh < OH; ++oh)
+      T* yp = y + p * OH * OW;
+      int32_t* ip = idx + p * OH * OW;
+      for (int oh = 0; oh < OH; ++oh) {
+        const int y0 = std::max(0, oh * SH - PH), y1 = std::min(H, oh * SH - PH + KH);
         for (int ow = 0; ow < OW; ++ow) {
-          T best = -INFINITY;
+          const int x0 = std::max(0, ow * SW - PW), x1 = std::min(W, ow * SW - PW + KW);
           int32_t bi = -1;
-          for (int kh = 0; kh < KH; ++kh) {
-            const int iy = oh * SH - PH + kh;
-            if (iy < 0 || iy >= H) continue;
-            for (int kw = 0; kw < KW; ++kw) {
-              const int ix = ow * SW - PW + kw;
-              if (ix < 0 || ix >= W) continue;
-              const T v = xp[iy * W + ix];
-              if (bi < 0 || v > best || std::isnan(v)) {
-                best = v;
+          T best = T(0);
+          for (int iy = y0; iy < y1; ++iy) {
+            const T* r = xp + iy * W;
+            for (int ix = x0; ix < x1; ++ix)
+              if (bi < 0 || r[ix] > best) {  // ties: first element in window order
+                best = r[ix];
                 bi = iy * W + ix;
-                if (std::isnan(v)) break;
               }
-            }
           }
-          const long o = (p * OH + oh) * OW + ow;
-          y[o] = bi < 0 ? T(0) : best;
-          idx[o] = bi;
+          yp[oh * OW + ow] = best;
+          ip[oh * OW + ow] = bi;
         }
+      }
     }
   });
 }
@@ -731,49 +777,33 @@ void avgpool_bwd(const T* dy, T* dx, long NC, int H, int W, int KH, int KW, int 
 template <typename T>
 void act_fwd(int type, const T* x, T* y, long n, double alpha) {
   const T a = (T)alpha;
-  for_chunks(n, kGrain, [&](long lo, long hi) {
-    for (long i = lo; i < hi; ++i) {
-      const T v = x[i];
-      T r;
-      switch (type) {
-        case 1: r = v > T(0) ? v : T(0); break;
-        case 2: r = v > T(0) ? v : v * a; break;
-        case 3: r = v > T(0) ? v : a * (std::exp(v) - T(1)); break;
-        case 4: r = T(1) / (T(1) + std::exp(-v)); break;
-        case 5: r = std::tanh(v); break;
-        default: r = v;
-      }
-      y[i] = r;
-    }
-  });
+  switch (type) {
+    case 1: return map1(x, y, n, [](T v) { return v > T(0) ? v : T(0); });
+    case 2: return map1(x, y, n, [&](T v) { return v > T(0) ? v : v * a; });
+    case 3: return map1(x, y, n, [&](T v) { return v > T(0) ? v : a * (std::exp(v) - T(1)); });
+    case 4: return map1(x, y, n, [](T v) { return T(1) / (T(1) + std::exp(-v)); });
+    case 5: return map1(x, y, n, [](T v) { return std::tanh(v); });
+    default: return map1(x, y, n, [](T v) { return v; });
+  }
 }
 
 template <typename T>
 void act_bwd(int type, const T* x, const T* dy, T* dx, long n, double alpha) {
   const T a = (T)alpha;
-  for_chunks(n, kGrain, [&](long lo, long hi) {
-    for (long i = lo; i < hi; ++i) {
-      const T v = x[i], g = dy[i];
-      T r;
-      switch (type) {
-        case 1: r = v > T(0) ? g : T(0); break;
-        case 2: r = v > T(0) ? g : g * a; break;
-        case 3: r = v > T(0) ? g : g * a * std::exp(v); break;
-        case 4: {
-          const T s = T(1) / (T(1) + std::exp(-v));
-          r = g * s * (T(1) - s);
-          break;
-        }
-        case 5: {
-          const T t = std::tanh(v);
-          r = g * (T(1) - t * t);
-          break;
-        }
-        default: r = g;
-      }
-      dx[i] = r;
-    }
-  });
+  switch (type) {
+    case 1: return map2(x, dy, dx, n, [](T v, T g) { return v > T(0) ? g : T(0); });
+    case 2: return map2(x, dy, dx, n, [&](T v, T g) { return v > T(0) ? g : g * a; });
+    case 3: return map2(x, dy, dx, n, [&](T v, T g) { return v > T(0) ? g : g * a * std::exp(v); });
+    case 4: return map2(x, dy, dx, n, [](T v, T g) {
+      const T s = T(1) / (T(1) + std::exp(-v));
+      return g * s * (T(1) - s);
+    });
+    case 5: return map2(x, dy, dx, n, [](T v, T g) {
+      const T t = std::tanh(v);
+      return g * (T(1) - t * t);
+    });
+    default: return map2(x, dy, dx, n, [](T, T g) { return g; });
+  }
 }
 
 // softmax over the channel dim at every (n, spatial) position: x [N][C][HW]

@@ -35,6 +35,7 @@ ThreadPool::~ThreadPool() { stop(); }
 void ThreadPool::start(int n) {
   nthreads_ = std::max(1, n);
   quit_ = false;
+  quit_atomic_.store(false, std::memory_order_relaxed);
   for (int i = 1; i < nthreads_; ++i) workers_.emplace_back(&ThreadPool::worker, this, i);
 }
 
@@ -42,6 +43,7 @@ void ThreadPool::stop() {
   {
     std::lock_guard<std::mutex> g(mu_);
     quit_ = true;
+    quit_atomic_.store(true, std::memory_order_relaxed);
   }
   cv_.notify_all();
   for (auto& t : workers_) t.join();
@@ -56,12 +58,31 @@ void ThreadPool::set_num_threads(int n) {
   start(n);
 }
 
+// Optional spin-before-block (DCNN_POOL_SPIN=<iterations>): workers poll the generation word and
+// the caller polls the completion count before sleeping on the condition variables. Off by default:
+// on virtualised hosts PAUSE loops trap to the hypervisor and spinning threads steal the vCPUs the
+// work needs (measured: 8 spinning workers made a 100 us loop take 3 ms); on bare metal a few
+// thousand iterations cut the hand-off from a futex round trip to about a microsecond.
+namespace {
+int spin_iters() {
+  static const int v = [] {
+    const char* e = std::getenv("DCNN_POOL_SPIN");
+    return e ? std::max(0, std::atoi(e)) : 0;
+  }();
+  return v;
+}
+inline void cpu_relax() { __builtin_ia32_pause(); }
+}  // namespace
+
 void ThreadPool::worker(int) {
   long seen = 0;
   for (;;) {
+    for (int i = 0, n = spin_iters(); i < n && gen_atomic_.load(std::memory_order_acquire) == seen &&
+                    !quit_atomic_.load(std::memory_order_relaxed);
+         ++i)
+      cpu_relax();
     const std::function<void(long)>* job;
     long ntasks;
-    Schedule sched;
     {
       std::unique_lock<std::mutex> lk(mu_);
       cv_.wait(lk, [&] { return quit_ || generation_ != seen; });
@@ -69,12 +90,10 @@ void ThreadPool::worker(int) {
       seen = generation_;
       job = job_;
       ntasks = ntasks_;
-      sched = sched_;
     }
     tl_in_region = true;
     for (long t; (t = next_.fetch_add(1, std::memory_order_relaxed)) < ntasks;) (*job)(t);
     tl_in_region = false;
-    (void)sched;
     if (active_.fetch_sub(1, std::memory_order_acq_rel) == 1) {
       std::lock_guard<std::mutex> g(mu_);
       done_cv_.notify_all();
@@ -88,27 +107,28 @@ void ThreadPool::run(long ntasks, const std::function<void(long)>& fn, Schedule 
     for (long t = 0; t < ntasks; ++t) fn(t);
     return;
   }
+  (void)sched;  // tasks are sized by the callers to fixed index ranges: dynamic dispatch of them
+                // never changes results, whichever thread runs a task
   std::lock_guard<std::mutex> r(run_mu_);
-  // Static scheduling is implemented as dynamic dispatch of contiguous task blocks: callers
-  // already size tasks so that each covers a fixed index range, so results never depend on
-  // which thread ran a task.
   {
     std::lock_guard<std::mutex> g(mu_);
     job_ = &fn;
     ntasks_ = ntasks;
-    sched_ = Schedule::Dynamic;
     next_.store(0, std::memory_order_relaxed);
     active_.store((int)workers_.size(), std::memory_order_relaxed);
     ++generation_;
+    gen_atomic_.store(generation_, std::memory_order_release);
   }
   cv_.notify_all();
   tl_in_region = true;
   for (long t; (t = next_.fetch_add(1, std::memory_order_relaxed)) < ntasks;) fn(t);
   tl_in_region = false;
-  std::unique_lock<std::mutex> lk(mu_);
-  done_cv_.wait(lk, [&] { return active_.load(std::memory_order_acquire) == 0; });
+  for (int i = 0, n = spin_iters(); i < n && active_.load(std::memory_order_acquire) != 0; ++i) cpu_relax();
+  if (active_.load(std::memory_order_acquire) != 0) {
+    std::unique_lock<std::mutex> lk(mu_);
+    done_cv_.wait(lk, [&] { return active_.load(std::memory_order_acquire) == 0; });
+  }
   job_ = nullptr;
-  (void)sched;
 }
 
 int get_num_threads() { return ThreadPool::instance().num_threads(); }

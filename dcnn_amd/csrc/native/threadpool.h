@@ -46,7 +46,9 @@ class ThreadPool {
   std::atomic<long> next_{0};
   std::atomic<int> active_{0};
   long generation_ = 0;
+  std::atomic<long> gen_atomic_{0};   // mirrors generation_ for lock-free spinning
   bool quit_ = false;
+  std::atomic<bool> quit_atomic_{false};
   std::mutex run_mu_;  // one parallel region at a time from outside the pool
 };
 
