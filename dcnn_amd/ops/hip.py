@@ -9,6 +9,7 @@ training step can be captured into a hipGraph.
 """
 from __future__ import annotations
 
+import contextlib
 import os
 import threading
 
@@ -377,8 +378,12 @@ class _DeferredReduce:
 
     def flush(self):
         if self.pending:
-            kernels().multi_splitk_reduce([(t[0].data_ptr(), t[1].data_ptr(), t[2], t[3]) for t in self.pending],
-                                          stream_ptr())
+            ws = wgrad_stream
+            with ws.on_side() if ws.forked else contextlib.nullcontext():
+                # (on the side stream when the weight gradients run there: the slabs were
+                # allocated on it, so the caching allocator's stream order covers this read)
+                kernels().multi_splitk_reduce([(t[0].data_ptr(), t[1].data_ptr(), t[2], t[3])
+                                               for t in self.pending], stream_ptr())
             self.pending.clear()
 
     def end(self):
@@ -405,6 +410,82 @@ class _ThreadReducer:
 
 
 grad_reducer = _ThreadReducer()
+
+_WGRAD_STREAM = os.environ.get("DCNN_WGRAD_STREAM", "0") == "1"
+
+
+class _SideStream:
+    """Weight gradients on a side stream, overlapping the data-gradient chain.
+
+    In a layer's backward the weight gradient (wgrad GEMM + its deferred split-K reduce) and the
+    data gradient (dgrad GEMM -> BN statistics reduce -> BN backward apply -> the next layer) both
+    read the incoming gradient but not each other's output. The data-gradient chain is full of
+    short, latency-bound kernels; forking every wgrad onto a side stream (an event fork from the
+    compute stream) lets the GPU run those short kernels beside the MFMA-heavy wgrad instead of
+    after it. Inside a captured graph the forks/joins become graph edges. The tensors a wgrad
+    reads that were allocated on the compute stream are kept referenced until the join, so the
+    caching allocator cannot hand their memory to later compute-stream work while the side stream
+    may still read it. Joined (compute stream waits for the side stream) before any gradient
+    consumer: ``flush_gradients`` (data-parallel bucket all-reduce) and ``finish_backward``.
+    Active between ``begin()`` / ``end()`` on the calling thread (``Sequential.prepare_backward``
+    / ``finish_backward``) when ``DCNN_WGRAD_STREAM=1``.
+
+    OFF by default — measured slower on MI355X (profiles/experiment_wgrad_side_stream.md): two
+    full-grid MFMA kernels sharing the CUs run slower together (dgrad 50 -> 94 us beside a wgrad
+    47 -> 123 us) than back to back, and every captured fork/join edge opens a 10-15 us dispatch
+    gap; 64.9k vs 69.4k img/s on ResNet-18 at batch 256."""
+
+    def __init__(self):
+        self.active = False
+        self.forked = False
+        self.stream = None
+        self.keep = []
+
+    def begin(self):
+        self.active = _WGRAD_STREAM
+
+    @contextlib.contextmanager
+    def on_side(self, *keep):
+        main = torch.cuda.current_stream()
+        if self.stream is None or self.stream.device != main.device:
+            self.stream = torch.cuda.Stream(device=main.device)
+        if not self.forked or keep:
+            self.stream.wait_stream(main)  # fork after everything issued so far on the compute stream
+        self.forked = True
+        self.keep.extend(keep)
+        with torch.cuda.stream(self.stream):
+            yield
+
+    def run(self, fn, *keep):
+        """fn() on the side stream when active, else inline."""
+        if not self.active:
+            return fn()
+        with self.on_side(*keep):
+            return fn()
+
+    def join(self):
+        if self.forked:
+            torch.cuda.current_stream().wait_stream(self.stream)
+            self.forked = False
+            self.keep.clear()
+
+    def end(self):
+        self.join()
+        self.active = False
+
+
+class _ThreadSide:
+    def _get(self):
+        r = getattr(_tls, "side", None)
+        if r is None:
+            r = _tls.side = _SideStream()
+        return r
+
+    def __getattr__(self, k):
+        return getattr(self._get(), k)
+
+
+wgrad_stream = _ThreadSide()
 
 
 def _dense(t):
