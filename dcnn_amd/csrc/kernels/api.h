@@ -108,15 +108,15 @@ void bn_partial(int dtype, const void* x, const void* dy, const void* yout, void
 int bn_stat_parts(int rows);
 void bn_stat_reduce(int mode, const float* slab, int rows, int C, float* out, float* part, unsigned* ticket,
                     hipStream_t s);
-void bn_apply(int dtype, const void* x, void* y, long R, int C, const float* sums, float count, const float* gamma,
+void bn_apply(int dtype, const void* x, void* y, long R, int C, const float* sums, int parts, float count, const float* gamma,
               const float* beta, float eps, const void* residual, int relu, float* save_mean, float* save_istd,
               float* run_mean, float* run_var, float momentum, int use_running, hipStream_t s);
 void bn_bwd_apply(int dtype, const void* dy, const void* yout, const void* x, void* dx, long R, int C, const float* mean,
-                  const float* istd, const float* gamma, const float* sums, float count, float* dgamma, float* dbeta,
-                  int eval_mode, hipStream_t s);
+                  const float* istd, const float* gamma, const float* sums, int parts, float count, float* dgamma,
+                  float* dbeta, int eval_mode, hipStream_t s);
 // training BatchNorm + ReLU + non-overlapping max-pool in one pass (stem), bf16 NHWC
 bool bn_relu_maxpool_supported(PoolGeom g);
-void bn_relu_maxpool(const bf16* x, bf16* y, uint8_t* idx, PoolGeom g, const float* sums, float count,
+void bn_relu_maxpool(const bf16* x, bf16* y, uint8_t* idx, PoolGeom g, const float* sums, int parts, float count,
                      const float* gamma, const float* beta, float eps, float* save_mean, float* save_istd,
                      float* run_mean, float* run_var, float momentum, hipStream_t s);
 void gn_fwd(int dtype, const void* x, void* y, int N, int HW, int C, int G, const float* gamma, const float* beta,

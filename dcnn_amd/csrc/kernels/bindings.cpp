@@ -187,19 +187,20 @@ PYBIND11_MODULE(_kernels, m) {
                              uintptr_t st) {
     bn_stat_reduce(mode, P<const float*>(slab), rows, C, P<float*>(out), P<float*>(part), P<unsigned*>(ticket), S(st));
   });
-  m.def("bn_apply", [](int dt, uintptr_t x, uintptr_t y, long R, int C, uintptr_t sums, float count, uintptr_t gamma,
-                       uintptr_t beta, float eps, uintptr_t residual, int relu, uintptr_t save_mean,
+  m.def("bn_apply", [](int dt, uintptr_t x, uintptr_t y, long R, int C, uintptr_t sums, int parts, float count,
+                       uintptr_t gamma, uintptr_t beta, float eps, uintptr_t residual, int relu, uintptr_t save_mean,
                        uintptr_t save_istd, uintptr_t run_mean, uintptr_t run_var, float momentum, int use_running,
                        uintptr_t st) {
-    bn_apply(dt, P<const void*>(x), P<void*>(y), R, C, P<const float*>(sums), count, P<const float*>(gamma),
+    bn_apply(dt, P<const void*>(x), P<void*>(y), R, C, P<const float*>(sums), parts, count, P<const float*>(gamma),
              P<const float*>(beta), eps, P<const void*>(residual), relu, P<float*>(save_mean), P<float*>(save_istd),
              P<float*>(run_mean), P<float*>(run_var), momentum, use_running, S(st));
   });
   m.def("bn_bwd_apply", [](int dt, uintptr_t dy, uintptr_t yout, uintptr_t x, uintptr_t dx, long R, int C,
-                           uintptr_t mean, uintptr_t istd, uintptr_t gamma, uintptr_t sums, float count,
+                           uintptr_t mean, uintptr_t istd, uintptr_t gamma, uintptr_t sums, int parts, float count,
                            uintptr_t dgamma, uintptr_t dbeta, int eval_mode, uintptr_t st) {
     bn_bwd_apply(dt, P<const void*>(dy), P<const void*>(yout), P<const void*>(x), P<void*>(dx), R, C,
-                 P<const float*>(mean), P<const float*>(istd), P<const float*>(gamma), P<const float*>(sums), count,
+                 P<const float*>(mean), P<const float*>(istd), P<const float*>(gamma), P<const float*>(sums), parts,
+                 count,
                  P<float*>(dgamma), P<float*>(dbeta), eval_mode, S(st));
   });
   m.def("gn_fwd", [](int dt, uintptr_t x, uintptr_t y, int N, int HW, int C, int G, uintptr_t gamma, uintptr_t beta,
@@ -235,11 +236,12 @@ PYBIND11_MODULE(_kernels, m) {
     return bn_relu_maxpool_supported(geom(N, H, W, C, OH, OW, ph, pw, sh, sw, padh, padw));
   });
   m.def("bn_relu_maxpool", [geom](uintptr_t x, uintptr_t y, uintptr_t idx, int N, int H, int W, int C, int OH, int OW,
-                                  int ph, int pw, int sh, int sw, int padh, int padw, uintptr_t sums, float count,
+                                  int ph, int pw, int sh, int sw, int padh, int padw, uintptr_t sums, int parts,
+                                  float count,
                                   uintptr_t gamma, uintptr_t beta, float eps, uintptr_t save_mean, uintptr_t save_istd,
                                   uintptr_t run_mean, uintptr_t run_var, float momentum, uintptr_t st) {
     bn_relu_maxpool(P<const bf16*>(x), P<bf16*>(y), P<uint8_t*>(idx), geom(N, H, W, C, OH, OW, ph, pw, sh, sw, padh, padw),
-                    P<const float*>(sums), count, P<const float*>(gamma), P<const float*>(beta), eps,
+                    P<const float*>(sums), parts, count, P<const float*>(gamma), P<const float*>(beta), eps,
                     P<float*>(save_mean), P<float*>(save_istd), P<float*>(run_mean), P<float*>(run_var), momentum,
                     S(st));
   });

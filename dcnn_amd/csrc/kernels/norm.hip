@@ -147,9 +147,10 @@ __global__ void __launch_bounds__(256) bn_partial_kernel(const T* __restrict__ x
 //   MODE 0: rows are (count, mean, M2) triples -> stats = (mean, biased variance)
 //   MODE 1: rows are (sum a, sum b) pairs      -> stats = (sum a, sum b)
 // Grid (C/64, ny): lane = channel, each 1024-thread block merges 256 rows (each of its 16 waves
-// 16 rows, all loads in flight, pairwise trees in registers and then across the waves in LDS). With ny > 1 the blocks publish their partials
-// (agent release) and take a ticket; the last block of a channel column merges the ny partials
-// in block order (agent acquire). Every merge order is fixed: the result does not depend on timing.
+// 16 rows, all loads in flight, pairwise trees in registers and then across the waves in LDS).
+// With ny > 1 every block writes its partial and the consumer merges the ny partials (read_stats):
+// an in-kernel second level (ticket + agent release/acquire + a serial last block) cost ~10 us per
+// reduce on the 32x32 layers. Every merge order is fixed: the result does not depend on timing.
 // ---------------------------------------------------------------------------------------
 template <int MODE>
 struct StatAcc {
@@ -203,7 +204,6 @@ __global__ void __launch_bounds__(1024) bn_stat_reduce_kernel(const float* __res
                                                               float* __restrict__ out) {
   constexpr int NV = MODE == 0 ? 3 : 2;
   __shared__ StatAcc<MODE> red[kStatWaves][64];
-  __shared__ int last;
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   const int c = blockIdx.x * 64 + lane;
   const bool cok = c < C;
@@ -226,45 +226,46 @@ __global__ void __launch_bounds__(1024) bn_stat_reduce_kernel(const float* __res
     if (w == 0 && cok) finish(red[0][lane]);
     return;
   }
-  if (w == 0) {
-    if (cok) {
-      const StatAcc<MODE> t = red[0][lane];
-      part[((long)by * 3 + 0) * C + c] = t.a;
-      part[((long)by * 3 + 1) * C + c] = t.b;
-      part[((long)by * 3 + 2) * C + c] = t.c;
-    }
-    // publish: this wave's stores drained, agent-scope release, then the ticket
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    if (lane == 0) {
-      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      const unsigned old = __hip_atomic_fetch_add(&ticket[blockIdx.x], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      last = old == (unsigned)(ny - 1);
-      if (last) {
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      }
-    }
+  // ny > 1: publish this block's partial; the consuming apply kernel merges the ny partials of
+  // its channels in part order in its prologue (read_stats), so there is no second level here:
+  // no ticket, no release/acquire fences, no serial last block (the kernel boundary publishes)
+  if (w == 0 && cok) {
+    const StatAcc<MODE> t = red[0][lane];
+    part[((long)by * 3 + 0) * C + c] = t.a;
+    part[((long)by * 3 + 1) * C + c] = t.b;
+    part[((long)by * 3 + 2) * C + c] = t.c;
   }
-  __syncthreads();
-  if (!last) return;
-  // ---- level 2 (last block of this channel column): wave w merges partials [16w, 16w + 16) ----
-  StatAcc<MODE> t = StatAcc<MODE>::zero();
-  if (cok)
-    for (int k0 = w * kStatRW; k0 < ny; k0 += kStatRowsPerBlock)
-      t = t.merge(stat_tree<MODE, kStatRW>(part, 3L * C, k0, min(ny, k0 + kStatRW), C, c));
-  red[w][lane] = t;
-  stat_tree_lds<MODE>(red, w, lane);
-  if (w == 0) {
-    if (cok) finish(red[0][lane]);
-    if (lane == 0) ticket[blockIdx.x] = 0u;  // ready for the next reduce on this stream
+}
+
+// Statistics as the consumers see them: parts == 1 -> buf is the finished [2][C] result of
+// bn_stat_reduce; parts > 1 -> buf holds its [parts][3][C] level-1 partials, merged here in part
+// order (fixed: deterministic). MODE 0 -> (mean, biased variance), MODE 1 -> (sum a, sum b).
+template <int MODE>
+__device__ __forceinline__ void read_stats(const float* __restrict__ buf, int parts, int C, int c, float& s0,
+                                           float& s1) {
+  if (parts <= 1) {
+    s0 = buf[c];
+    s1 = buf[C + c];
+    return;
+  }
+  StatAcc<MODE> t{buf[c], buf[C + c], buf[2 * C + c]};
+  for (int p = 1; p < parts; ++p) {
+    const float* q = buf + (long)p * 3 * C + c;
+    t = t.merge(StatAcc<MODE>{q[0], q[C], q[2 * C]});
+  }
+  if constexpr (MODE == 0) {
+    s0 = t.b;
+    s1 = t.a > 0.f ? t.c / t.a : 0.f;
+  } else {
+    s0 = t.a;
+    s1 = t.b;
   }
 }
 
 // y = x*scale + shift (+ residual) (ReLU); scale/shift from batch sums or running stats.
 template <typename T, int V>
 __global__ void __launch_bounds__(256) bn_apply_kernel(const T* __restrict__ x, T* __restrict__ y, long R, int C,
-                                                       const float* __restrict__ sums, float count,
+                                                       const float* __restrict__ sums, int parts, float count,
                                                        const float* __restrict__ gamma,
                                                        const float* __restrict__ beta, float eps,
                                                        const T* __restrict__ residual, int relu,
@@ -280,8 +281,8 @@ __global__ void __launch_bounds__(256) bn_apply_kernel(const T* __restrict__ x, 
       mean = run_mean[c];
       istd = rsqrtf(run_var[c] + eps);
     } else {
-      mean = sums[c];  // stats from bn_stat_reduce: (mean, biased variance)
-      const float var = sums[C + c];
+      float var;
+      read_stats<0>(sums, parts, C, c, mean, var);  // (mean, biased variance)
       istd = rsqrtf(var + eps);
       if (blockIdx.x == 0) {
         if (save_mean) { save_mean[c] = mean; save_istd[c] = istd; }
@@ -323,8 +324,8 @@ __global__ void __launch_bounds__(256) bn_apply_kernel(const T* __restrict__ x, 
 // pooled value and recomputes xhat from x.
 __global__ void __launch_bounds__(256) bn_relu_maxpool_kernel(const bf16* __restrict__ x, bf16* __restrict__ y,
                                                               uint8_t* __restrict__ idx, PoolGeom g,
-                                                              const float* __restrict__ sums, float count,
-                                                              const float* __restrict__ gamma,
+                                                              const float* __restrict__ sums, int parts,
+                                                              float count, const float* __restrict__ gamma,
                                                               const float* __restrict__ beta, float eps,
                                                               float* __restrict__ save_mean,
                                                               float* __restrict__ save_istd,
@@ -334,7 +335,8 @@ __global__ void __launch_bounds__(256) bn_relu_maxpool_kernel(const bf16* __rest
   float* scale = sh;
   float* shift = sh + g.C;
   for (int c = threadIdx.x; c < g.C; c += blockDim.x) {
-    const float mean = sums[c], var = sums[g.C + c];  // (mean, biased variance)
+    float mean, var;
+    read_stats<0>(sums, parts, g.C, c, mean, var);  // (mean, biased variance)
     const float istd = rsqrtf(var + eps);
     if (blockIdx.x == 0) {
       if (save_mean) { save_mean[c] = mean; save_istd[c] = istd; }
@@ -384,9 +386,9 @@ __global__ void __launch_bounds__(256) bn_bwd_apply_kernel(const T* __restrict__
                                                            int C, const float* __restrict__ mean,
                                                            const float* __restrict__ istd,
                                                            const float* __restrict__ gamma,
-                                                           const float* __restrict__ sums, float count,
-                                                           float* __restrict__ dgamma, float* __restrict__ dbeta,
-                                                           int eval_mode) {
+                                                           const float* __restrict__ sums, int parts,
+                                                           float count, float* __restrict__ dgamma,
+                                                           float* __restrict__ dbeta, int eval_mode) {
   extern __shared__ __attribute__((aligned(16))) float sh[];
   float* ca = sh;          // gamma*istd
   float* cb = sh + C;      // mean(dy')
@@ -395,14 +397,16 @@ __global__ void __launch_bounds__(256) bn_bwd_apply_kernel(const T* __restrict__
   float* ci = sh + 4 * C;  // istd
   for (int c = threadIdx.x; c < C; c += blockDim.x) {
     const float g = gamma ? gamma[c] : 1.f;
+    float sdy = 0.f, sdyx = 0.f;
+    if (sums) read_stats<1>(sums, parts, C, c, sdy, sdyx);
     ca[c] = g * istd[c];
-    cb[c] = eval_mode ? 0.f : sums[c] / count;
-    cc[c] = eval_mode ? 0.f : sums[C + c] / count;
+    cb[c] = eval_mode ? 0.f : sdy / count;
+    cc[c] = eval_mode ? 0.f : sdyx / count;
     cm[c] = mean[c];
     ci[c] = istd[c];
     if (blockIdx.x == 0 && sums) {
-      if (dgamma) dgamma[c] += sums[C + c];
-      if (dbeta) dbeta[c] += sums[c];
+      if (dgamma) dgamma[c] += sdyx;
+      if (dbeta) dbeta[c] += sdy;
     }
   }
   __syncthreads();
@@ -568,8 +572,9 @@ int bn_stat_parts(int rows) { return (rows + kStatRowsPerBlock - 1) / kStatRowsP
 // words, left zeroed again (one ticket array per stream).
 void bn_stat_reduce(int mode, const float* slab, int rows, int C, float* out, float* part, unsigned* ticket,
                     hipStream_t s) {
+  (void)ticket;  // (the in-kernel second level is gone: consumers merge the partials)
   const int ny = bn_stat_parts(rows);
-  if (ny > 1 && (!part || !ticket)) throw std::runtime_error("bn_stat_reduce: workspace required");
+  if (ny > 1 && !part) throw std::runtime_error("bn_stat_reduce: partials buffer required");
   const dim3 grid((unsigned)((C + 63) / 64), (unsigned)ny);
   if (mode == 0)
     hipLaunchKernelGGL(bn_stat_reduce_kernel<0>, grid, dim3(64 * kStatWaves), 0, s, slab, rows, C, part, ticket, out);
@@ -583,71 +588,72 @@ bool bn_relu_maxpool_supported(PoolGeom g) {
          g.OH == g.H / g.ph && g.OW == g.W / g.pw;
 }
 
-void bn_relu_maxpool(const bf16* x, bf16* y, uint8_t* idx, PoolGeom g, const float* sums, float count,
+void bn_relu_maxpool(const bf16* x, bf16* y, uint8_t* idx, PoolGeom g, const float* sums, int parts, float count,
                      const float* gamma, const float* beta, float eps, float* save_mean, float* save_istd,
                      float* run_mean, float* run_var, float momentum, hipStream_t s) {
   if (!bn_relu_maxpool_supported(g)) throw std::runtime_error("bn_relu_maxpool: unsupported geometry");
   const long total = (long)g.N * g.OH * g.OW * g.C / 8;
   hipLaunchKernelGGL(bn_relu_maxpool_kernel, dim3(grid_for(total, 256, 2048)), dim3(256), 2 * g.C * sizeof(float), s,
-                     x, y, idx, g, sums, count, gamma, beta, eps, save_mean, save_istd, run_mean, run_var, momentum);
+                     x, y, idx, g, sums, parts, count, gamma, beta, eps, save_mean, save_istd, run_mean, run_var,
+                     momentum);
   DCNN_LAUNCH_CHECK();
 }
 
 template <typename T>
-static void bn_apply_t(const T* x, T* y, long R, int C, const float* sums, float count, const float* gamma,
+static void bn_apply_t(const T* x, T* y, long R, int C, const float* sums, int parts, float count, const float* gamma,
                        const float* beta, float eps, const T* residual, int relu, float* save_mean,
                        float* save_istd, float* run_mean, float* run_var, float momentum, int use_running,
                        hipStream_t s) {
   const size_t shm = 2 * C * sizeof(float);
   if (C % 8 == 0) {
     const int g = grid_for(R * C / 8, 256, 2048);
-    hipLaunchKernelGGL((bn_apply_kernel<T, 8>), dim3(g), dim3(256), shm, s, x, y, R, C, sums, count, gamma, beta,
+    hipLaunchKernelGGL((bn_apply_kernel<T, 8>), dim3(g), dim3(256), shm, s, x, y, R, C, sums, parts, count, gamma, beta,
                        eps, residual, relu, save_mean, save_istd, run_mean, run_var, momentum, use_running);
   } else {
     const int g = grid_for(R * C, 256, 2048);
-    hipLaunchKernelGGL((bn_apply_kernel<T, 1>), dim3(g), dim3(256), shm, s, x, y, R, C, sums, count, gamma, beta,
+    hipLaunchKernelGGL((bn_apply_kernel<T, 1>), dim3(g), dim3(256), shm, s, x, y, R, C, sums, parts, count, gamma, beta,
                        eps, residual, relu, save_mean, save_istd, run_mean, run_var, momentum, use_running);
   }
   DCNN_LAUNCH_CHECK();
 }
 
-void bn_apply(int dtype, const void* x, void* y, long R, int C, const float* sums, float count,
+void bn_apply(int dtype, const void* x, void* y, long R, int C, const float* sums, int parts, float count,
               const float* gamma, const float* beta, float eps, const void* residual, int relu, float* save_mean,
               float* save_istd, float* run_mean, float* run_var, float momentum, int use_running, hipStream_t s) {
   if (dtype == 0)
-    bn_apply_t<float>((const float*)x, (float*)y, R, C, sums, count, gamma, beta, eps, (const float*)residual, relu,
-                      save_mean, save_istd, run_mean, run_var, momentum, use_running, s);
+    bn_apply_t<float>((const float*)x, (float*)y, R, C, sums, parts, count, gamma, beta, eps, (const float*)residual,
+                      relu, save_mean, save_istd, run_mean, run_var, momentum, use_running, s);
   else
-    bn_apply_t<bf16>((const bf16*)x, (bf16*)y, R, C, sums, count, gamma, beta, eps, (const bf16*)residual, relu,
-                     save_mean, save_istd, run_mean, run_var, momentum, use_running, s);
+    bn_apply_t<bf16>((const bf16*)x, (bf16*)y, R, C, sums, parts, count, gamma, beta, eps, (const bf16*)residual,
+                     relu, save_mean, save_istd, run_mean, run_var, momentum, use_running, s);
 }
 
 template <typename T>
 static void bn_bwd_apply_t(const T* dy, const T* yout, const T* x, T* dx, long R, int C, const float* mean,
-                           const float* istd, const float* gamma, const float* sums, float count, float* dgamma,
-                           float* dbeta, int eval_mode, hipStream_t s) {
+                           const float* istd, const float* gamma, const float* sums, int parts, float count,
+                           float* dgamma, float* dbeta, int eval_mode, hipStream_t s) {
   const size_t shm = 5 * C * sizeof(float);
   if (C % 8 == 0) {
     const int g = grid_for(R * C / 8, 256, 2048);
     hipLaunchKernelGGL((bn_bwd_apply_kernel<T, 8>), dim3(g), dim3(256), shm, s, dy, yout, x, dx, R, C, mean, istd,
-                       gamma, sums, count, dgamma, dbeta, eval_mode);
+                       gamma, sums, parts, count, dgamma, dbeta, eval_mode);
   } else {
     const int g = grid_for(R * C, 256, 2048);
     hipLaunchKernelGGL((bn_bwd_apply_kernel<T, 1>), dim3(g), dim3(256), shm, s, dy, yout, x, dx, R, C, mean, istd,
-                       gamma, sums, count, dgamma, dbeta, eval_mode);
+                       gamma, sums, parts, count, dgamma, dbeta, eval_mode);
   }
   DCNN_LAUNCH_CHECK();
 }
 
 void bn_bwd_apply(int dtype, const void* dy, const void* yout, const void* x, void* dx, long R, int C,
-                  const float* mean, const float* istd, const float* gamma, const float* sums, float count,
+                  const float* mean, const float* istd, const float* gamma, const float* sums, int parts, float count,
                   float* dgamma, float* dbeta, int eval_mode, hipStream_t s) {
   if (dtype == 0)
     bn_bwd_apply_t<float>((const float*)dy, (const float*)yout, (const float*)x, (float*)dx, R, C, mean, istd, gamma,
-                          sums, count, dgamma, dbeta, eval_mode, s);
+                          sums, parts, count, dgamma, dbeta, eval_mode, s);
   else
     bn_bwd_apply_t<bf16>((const bf16*)dy, (const bf16*)yout, (const bf16*)x, (bf16*)dx, R, C, mean, istd, gamma,
-                         sums, count, dgamma, dbeta, eval_mode, s);
+                         sums, parts, count, dgamma, dbeta, eval_mode, s);
 }
 
 void gn_fwd(int dtype, const void* x, void* y, int N, int HW, int C, int G, const float* gamma, const float* beta,

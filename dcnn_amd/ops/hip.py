@@ -660,15 +660,65 @@ def _ticket(device, C, slot="stat"):
     return t
 
 
+class Stats:
+    """Per-channel statistics for the BN apply kernels: ``parts == 1`` -> ``buf`` is the finished
+    [2][C] result; ``parts > 1`` -> ``buf`` holds [parts][3][C] level-1 partials that the
+    consuming kernel merges in its prologue (norm.hip read_stats). Used as a tensor (tests,
+    inspection) it materialises the finished [2][C] statistics (``final()``, torch ops: off the
+    training hot path)."""
+    __slots__ = ("buf", "parts", "mode", "_final")
+
+    def __init__(self, buf, parts, mode=0):
+        self.buf, self.parts, self.mode, self._final = buf, int(parts), int(mode), None
+
+    def final(self):
+        if self.parts == 1:
+            return self.buf
+        if self._final is None:
+            p = self.buf.double()
+            C = p.shape[2]
+            if self.mode == 0:  # Chan merges in part order (as read_stats)
+                n, mean, m2 = p[0, 0].clone(), p[0, 1].clone(), p[0, 2].clone()
+                for k in range(1, self.parts):
+                    nb, mb, m2b = p[k, 0], p[k, 1], p[k, 2]
+                    tot = n + nb
+                    d = mb - mean
+                    safe = torch.where(tot > 0, tot, torch.ones_like(tot))
+                    mean = torch.where(tot > 0, mean + d * nb / safe, mean)
+                    m2 = m2 + m2b + d * d * n * nb / safe
+                    n = tot
+                var = torch.where(n > 0, m2 / torch.where(n > 0, n, torch.ones_like(n)), torch.zeros_like(n))
+                out = torch.cat([mean, var])
+            else:
+                out = torch.cat([p[:, 0].sum(0), p[:, 1].sum(0)])
+            self._final = out.float().reshape(2 * C)
+        return self._final
+
+    def __getattr__(self, k):
+        return getattr(self.final(), k)
+
+    def __getitem__(self, i):
+        return self.final()[i]
+
+
 def stat_reduce(mode, slab, rows, C, out):
     """Deterministic slab reduce (norm.hip bn_stat_reduce): mode 0 = Welford (count, mean, M2)
-    tile triples -> out = (mean, biased var); mode 1 = (sum a, sum b) rows -> out = sums."""
+    tile triples -> (mean, biased var); mode 1 = (sum a, sum b) rows -> sums. Returns
+    :class:`Stats` (``out`` when one block covered all rows, else the partials buffer)."""
     K = kernels()
     ny = K.bn_stat_parts(rows)
     part = torch.empty((ny, 3, C), dtype=F32, device=slab.device) if ny > 1 else None
-    K.bn_stat_reduce(mode, slab.data_ptr(), rows, C, out.data_ptr(), ptr(part),
-                     _ticket(slab.device, C).data_ptr() if ny > 1 else 0, stream_ptr())
-    return out
+    K.bn_stat_reduce(mode, slab.data_ptr(), rows, C, out.data_ptr(), ptr(part), 0, stream_ptr())
+    return Stats(part if ny > 1 else out, ny, mode)
+
+
+def _stats(s):
+    """(pointer, parts) of a Stats / plain finished [2][C] tensor / None."""
+    if s is None:
+        return 0, 1
+    if isinstance(s, Stats):
+        return s.buf.data_ptr(), s.parts
+    return s.data_ptr(), 1
 
 
 def bn_stats(x, partial=None):
@@ -694,7 +744,8 @@ def bn_apply(x, sums, count, gamma, beta, eps, *, residual=None, relu=False, sav
     y = torch.empty_like(x, memory_format=CL)
     sm, si = save if save is not None else (None, None)
     rm, rv = running if running is not None else (None, None)
-    kernels().bn_apply(dt_code(x.dtype), x.data_ptr(), y.data_ptr(), R, C, ptr(sums), float(count), ptr(gamma),
+    sp, parts = _stats(sums)
+    kernels().bn_apply(dt_code(x.dtype), x.data_ptr(), y.data_ptr(), R, C, sp, parts, float(count), ptr(gamma),
                        ptr(beta), float(eps), ptr(residual), int(relu), ptr(sm), ptr(si), ptr(rm), ptr(rv),
                        float(momentum), int(use_running), stream_ptr())
     return y
@@ -722,8 +773,9 @@ def bn_relu_maxpool(x, sums, count, gamma, beta, eps, pool, *, save, running, mo
     idx = torch.empty((N, OH, OW, C), dtype=torch.uint8, device=x.device)
     sm, si = save
     rm, rv = running
+    sp, parts = _stats(sums)
     kernels().bn_relu_maxpool(x.data_ptr(), y.data_ptr(), idx.data_ptr(), N, H, W, C, OH, OW, ph, pw, sh, sw, pdh, pdw,
-                              sums.data_ptr(), float(count), ptr(gamma), ptr(beta), float(eps), sm.data_ptr(),
+                              sp, parts, float(count), ptr(gamma), ptr(beta), float(eps), sm.data_ptr(),
                               si.data_ptr(), ptr(rm), ptr(rv), float(momentum), stream_ptr())
     return y, idx
 
@@ -741,10 +793,10 @@ def bn_backward(dy, x, yout, mean, istd, gamma, dgamma, dbeta, *, want_masked=Fa
     dt = dt_code(x.dtype)
     if fused is not None and not eval_mode:
         slab, rows, sums = fused
-        stat_reduce(1, slab, rows, C, sums)
+        sp, parts = _stats(stat_reduce(1, slab, rows, C, sums))
         dx = torch.empty_like(x, memory_format=CL)
         K.bn_bwd_apply(dt, dy.data_ptr(), 0, x.data_ptr(), dx.data_ptr(), R, C, mean.data_ptr(), istd.data_ptr(),
-                       ptr(gamma), sums.data_ptr(), float(R), ptr(dgamma), ptr(dbeta), 0, st)
+                       ptr(gamma), sp, parts, float(R), ptr(dgamma), ptr(dbeta), 0, st)
         return dx, (dy if want_masked else None)
     dmask = torch.empty_like(dy, memory_format=CL) if (want_masked and yout is not None) else None
     sums = None
@@ -754,13 +806,14 @@ def bn_backward(dy, x, yout, mean, istd, gamma, dgamma, dbeta, *, want_masked=Fa
         sums = torch.empty((2 * C,), dtype=F32, device=x.device)
         K.bn_partial(dt, x.data_ptr(), dy.data_ptr(), ptr(yout), ptr(dmask), mean.data_ptr(), istd.data_ptr(), R, C,
                      slab.data_ptr(), 1, 0, st)
-        stat_reduce(1, slab, rows, C, sums)
+        sums = stat_reduce(1, slab, rows, C, sums)
     elif want_masked and yout is not None:
         dmask = dy * (yout > 0)
     dx = torch.empty_like(x, memory_format=CL)
     src = dmask if dmask is not None else dy
+    sp, parts = _stats(sums)
     K.bn_bwd_apply(dt, src.data_ptr(), 0 if dmask is not None else ptr(yout), x.data_ptr(), dx.data_ptr(), R, C,
-                   mean.data_ptr(), istd.data_ptr(), ptr(gamma), ptr(sums), float(R), ptr(dgamma), ptr(dbeta),
+                   mean.data_ptr(), istd.data_ptr(), ptr(gamma), sp, parts, float(R), ptr(dgamma), ptr(dbeta),
                    int(eval_mode), st)
     if eval_mode and (dgamma is not None or dbeta is not None):
         # frozen-statistics backward still accumulates the affine gradients

@@ -573,7 +573,7 @@ def test_conv_epilogue_stats_large_mean_and_deterministic(hip, shape):
 
 def test_stat_reduce_many_rows_deterministic(hip):
     """bn_stat_reduce with several hundred slab rows in both modes: equals an fp64 reference and
-    is bit-identical across runs (ticketed last-block merge in fixed order)."""
+    is bit-identical across runs (fixed-order partials, merged in part order by the consumer)."""
     torch.manual_seed(13)
     rows, C = 1000, 200
     n = torch.randint(1, 50, (rows, 1)).float().expand(rows, C)
