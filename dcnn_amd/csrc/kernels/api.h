@@ -87,6 +87,8 @@ void gemm_g2f(const G2Args& a, hipStream_t s);
 int gemm_g2f_stat_rows(int M, int N);
 void gemm_t2f(T2Args a, int splits, hipStream_t s);
 int gemm_t2f_splits(int M, int N, int P);
+void set_f32_mode(int mode);  // 0 exact f32 MFMA (default), 1 split-bf16 (3 MFMAs)
+int get_f32_mode();
 void conv_weight_transpose_f32(const float* w, float* wt, int Co, int T_, int Ci, hipStream_t s);
 void gemm_tn(TnArgs a, int splits, hipStream_t s);
 int gemm_tn_splits(int M, int N, int P);

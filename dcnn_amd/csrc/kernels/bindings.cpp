@@ -107,6 +107,8 @@ PYBIND11_MODULE(_kernels, m) {
           gemm_g2f(a, S(stream));
         });
   m.def("gemm_g2f_stat_rows", &gemm_g2f_stat_rows);
+  m.def("set_f32_mode", &set_f32_mode);
+  m.def("get_f32_mode", &get_f32_mode);
   m.def("gemm_t2f",
         [](uintptr_t dY, uintptr_t X, uintptr_t slab, uintptr_t bias_slab, int M, int N, int Pn, int ldy, int Cs,
            int H, int W, int GH, int GW, int SY, int SX, std::vector<std::array<int, 2>> taps, int splits,

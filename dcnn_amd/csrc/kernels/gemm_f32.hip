@@ -13,6 +13,8 @@
 // * Padding / out-of-image taps are zero-filled from a per-row tap-validity mask.
 // * Epilogue: bias, residual add, ReLU and per-channel BatchNorm (sum, sum^2) partials, with
 //   the strided output-row scatter of a dgrad phase.
+#include <cstdlib>
+
 #include "common.h"
 #include "api.h"
 
@@ -297,10 +299,335 @@ __global__ void __launch_bounds__(256, 2) gemm_t2f_kernel(T2Args p) {
   if (p.bias_slab && tn == 0 && tid < FBM && m0 + tid < p.M) p.bias_slab[(long)split * p.M + m0 + tid] = bias_acc;
 }
 
+// ------------------------------------------------------------------------------------------
+// fp32 GEMMs on bf16 MFMA with split precision ("3xbf16"): every fp32 operand x is split once,
+// when its tile is staged into LDS, into hi = bf16(x) and lo = bf16(x - hi), and each 16x16x32
+// product block is accumulated in fp32 as  a_hi*b_hi + a_hi*b_lo + a_lo*b_hi  (the a_lo*b_lo
+// term, ~2^-16 relative, is dropped). That is 16 significant bits per operand instead of 24, at
+// 3 bf16 MFMAs = 3/16 of the cycles of the exact 16x16x4 f32 MFMA chain for the same K: the fp32
+// path's GEMMs become ~4-5x cheaper in matrix-pipe time. Same tiling, tap gathers, epilogue
+// (bias / residual / ReLU / BN statistics) and split-K slabs as the exact kernels above.
+// Opt-in (set_f32_mode(1), DCNN_F32_SPLIT=1): on ResNet-18/ResNet-9 fp32 these gathered-GEMM
+// kernels are bound by their tap-gather loads, not the matrix pipe, so the split forward/dgrad
+// kernel was 18% faster and the split wgrad 26% slower than exact (profiles/fp32_split_r2.md) —
+// the exact f32 MFMA path stays the default. tests/test_gpu_kernels.py bounds the split error
+// against an fp64 reference (4.5e-6 relative on a K = 4608 conv).
+// ------------------------------------------------------------------------------------------
+namespace {
+constexpr int XBK = 32, XP = XBK + 8;  // bf16 row pitch 80 B: conflict-free ds_read_b128 over 16 rows
+int g_f32_mode = -1;                   // 0 exact f32 MFMA (default), 1 split bf16 (3 MFMAs)
+
+__device__ __forceinline__ void split8(const float (&v)[8], bf16x8& hi, bf16x8& lo) {
+#pragma unroll
+  for (int e = 0; e < 8; ++e) {
+    const bf16 h = (bf16)v[e];
+    hi[e] = h;
+    lo[e] = (bf16)(v[e] - (float)h);
+  }
+}
+
+__device__ __forceinline__ f32x4 mfma3(const bf16x8& ah, const bf16x8& al, const bf16x8& bh, const bf16x8& bl,
+                                       f32x4 c) {
+  c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(al, bh, c, 0, 0, 0);  // small terms first
+  c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ah, bl, c, 0, 0, 0);
+  c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ah, bh, c, 0, 0, 0);
+  return c;
+}
+}  // namespace
+
+__global__ void __launch_bounds__(256, 2) gemm_g2x_kernel(G2Args p) {
+  __shared__ __attribute__((aligned(16))) bf16 Ah[2][FBM * XP], Al[2][FBM * XP];
+  __shared__ __attribute__((aligned(16))) bf16 Bh[2][FBN * XP], Bl[2][FBN * XP];
+  __shared__ float red[2][4][FBN];
+  const float* A = reinterpret_cast<const float*>(p.A);
+  const float* B = reinterpret_cast<const float*>(p.B);
+  float* C = reinterpret_cast<float*>(p.C);
+  const float* R = reinterpret_cast<const float*>(p.residual);
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int wm = wid >> 1, wn = wid & 1;
+  const int tiles_n = (p.N + FBN - 1) / FBN;
+  const int lt = xcd_remap_f(blockIdx.x, gridDim.x);
+  const int tm = lt / tiles_n, tn = lt % tiles_n;
+  const int m0 = tm * FBM, n0 = tn * FBN;
+  if (p.zero_ptr && blockIdx.x == 0)
+    for (int i = tid; i < p.zero_n; i += 256) p.zero_ptr[i] = 0.f;
+
+  // this thread stages row lr, k chunk lc of 8 (4 chunks = XBK 32)
+  const int lr = tid >> 2, lc = tid & 3;
+  long a_base = 0;
+  uint64_t a_mask = 0;
+  {
+    const int m = m0 + lr;
+    if (m < p.M) {
+      const int ghw = p.GH * p.GW;
+      const int img = m / ghw, rem = m - img * ghw;
+      const int gy = rem / p.GW, gx = rem - gy * p.GW;
+      const int y0 = gy * p.SY, x0 = gx * p.SX;
+      a_base = (((long)img * p.H + y0) * p.W + x0) * p.Cs;
+      for (int t = 0; t < p.ntaps; ++t) {
+        const int sy = y0 + p.tap_dy[t], sx = x0 + p.tap_dx[t];
+        if (sy >= 0 && sy < p.H && sx >= 0 && sx < p.W) a_mask |= (1ull << t);
+      }
+    }
+  }
+  const int bn_row = n0 + lr;
+  const bool b_ok = bn_row < p.N;
+  const long b_base = (long)bn_row * p.ldb;
+  const bool vec = (p.Cs & 3) == 0;
+
+  auto load = [&](int k0, float (&va)[8], float (&vb)[8]) {
+#pragma unroll
+    for (int e = 0; e < 8; ++e) { va[e] = 0.f; vb[e] = 0.f; }
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      const int k = k0 + lc * 8 + h * 4;
+      if (vec) {  // 4 elements share one tap
+        const int t = k / p.Cs, c = k - t * p.Cs;
+        if (t < p.ntaps) {
+          if ((a_mask >> t) & 1ull) {
+            const float4 v = *reinterpret_cast<const float4*>(A + a_base + p.tap_srcoff[t] + c);
+            va[h * 4 + 0] = v.x; va[h * 4 + 1] = v.y; va[h * 4 + 2] = v.z; va[h * 4 + 3] = v.w;
+          }
+          if (b_ok) {
+            const float4 v = *reinterpret_cast<const float4*>(B + b_base + p.tap_b[t] + c);
+            vb[h * 4 + 0] = v.x; vb[h * 4 + 1] = v.y; vb[h * 4 + 2] = v.z; vb[h * 4 + 3] = v.w;
+          }
+        }
+      } else {
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const int kk = k + e, t = kk / p.Cs, c = kk - t * p.Cs;
+          if (t < p.ntaps) {
+            if ((a_mask >> t) & 1ull) va[h * 4 + e] = A[a_base + p.tap_srcoff[t] + c];
+            if (b_ok) vb[h * 4 + e] = B[b_base + p.tap_b[t] + c];
+          }
+        }
+      }
+    }
+  };
+
+  f32x4 acc[2][2];
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int j = 0; j < 2; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  const int K = p.ntaps * p.Cs;
+  const int nk = (K + XBK - 1) / XBK;
+  float va[8], vb[8];
+  load(0, va, vb);
+  int cur = 0;
+  for (int kt = 0; kt < nk; ++kt) {
+    {
+      bf16x8 h, l;
+      split8(va, h, l);
+      *reinterpret_cast<bf16x8*>(&Ah[cur][lr * XP + lc * 8]) = h;
+      *reinterpret_cast<bf16x8*>(&Al[cur][lr * XP + lc * 8]) = l;
+      split8(vb, h, l);
+      *reinterpret_cast<bf16x8*>(&Bh[cur][lr * XP + lc * 8]) = h;
+      *reinterpret_cast<bf16x8*>(&Bl[cur][lr * XP + lc * 8]) = l;
+    }
+    __syncthreads();
+    if (kt + 1 < nk) load((kt + 1) * XBK, va, vb);
+    const int g = lane >> 4;
+    bf16x8 ah[2], al[2], bh[2], bl[2];
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      const int o = (wm * 32 + i * 16 + (lane & 15)) * XP + g * 8;
+      ah[i] = *reinterpret_cast<const bf16x8*>(&Ah[cur][o]);
+      al[i] = *reinterpret_cast<const bf16x8*>(&Al[cur][o]);
+    }
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      const int o = (wn * 32 + j * 16 + (lane & 15)) * XP + g * 8;
+      bh[j] = *reinterpret_cast<const bf16x8*>(&Bh[cur][o]);
+      bl[j] = *reinterpret_cast<const bf16x8*>(&Bl[cur][o]);
+    }
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+      for (int j = 0; j < 2; ++j) acc[i][j] = mfma3(ah[i], al[i], bh[j], bl[j], acc[i][j]);
+    cur ^= 1;
+  }
+
+  // ---- epilogue (identical to gemm_g2f_kernel) ----
+  const int ghw = p.GH * p.GW;
+#pragma unroll
+  for (int j = 0; j < 2; ++j) {
+    const int col = n0 + wn * 32 + j * 16 + (lane & 15);
+    const bool cok = col < p.N;
+    const float bv = (p.bias && cok) ? p.bias[col] : 0.f;
+    const float piv = __shfl(acc[0][j][0] + bv, lane & 15, 64);
+    float s = 0.f, q = 0.f, n = 0.f;
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int m = m0 + wm * 32 + i * 16 + (lane >> 4) * 4 + r;
+        if (m >= p.M || !cok) continue;
+        const int img = m / ghw, rem = m - img * ghw;
+        const int gy = rem / p.GW, gx = rem - gy * p.GW;
+        const long orow = ((long)img * p.OH + gy * p.OSY + p.ORY) * p.OW + gx * p.OSX + p.ORX;
+        float v = acc[i][j][r] + bv;
+        if (R) v += R[orow * p.ldc + col];
+        if (p.relu) v = fmaxf(v, 0.f);
+        C[orow * p.ldc + col] = v;
+        const float d = v - piv;
+        s += d;
+        q += d * d;
+        n += 1.f;
+      }
+    if (p.stats) {
+      s += __shfl_xor(s, 16, 64);
+      s += __shfl_xor(s, 32, 64);
+      q += __shfl_xor(q, 16, 64);
+      q += __shfl_xor(q, 32, 64);
+      n += __shfl_xor(n, 16, 64);
+      n += __shfl_xor(n, 32, 64);
+      if (lane < 16) {
+        const int c = wn * 32 + j * 16 + lane;
+        red[wm][0][c] = s;
+        red[wm][1][c] = q;
+        red[wm][2][c] = piv;
+        red[wm][3][c] = n;
+      }
+    }
+  }
+  if (p.stats) {
+    __syncthreads();
+    if (tid < FBN && n0 + tid < p.N) {
+      Welford t = welford_from_shifted(red[0][3][tid], red[0][2][tid], red[0][0][tid], red[0][1][tid]);
+      t = welford_merge(t, welford_from_shifted(red[1][3][tid], red[1][2][tid], red[1][0][tid], red[1][1][tid]));
+      store_welford(p.stats, tm, p.N, n0 + tid, t);
+    }
+  }
+}
+
+// split-precision weight gradient: thread (column tcol = tid & 63, k group tk = tid >> 6 of 8
+// pixels) loads 8 pixels of one dY column and of one gathered X column (coalesced across the
+// wave's 64 lanes), splits them and stores contiguous bf16x8 k-runs.
+__global__ void __launch_bounds__(256, 2) gemm_t2x_kernel(T2Args p) {
+  __shared__ __attribute__((aligned(16))) bf16 Ah[FBM * XP], Al[FBM * XP];
+  __shared__ __attribute__((aligned(16))) bf16 Bh[FBN * XP], Bl[FBN * XP];
+  const float* dY = reinterpret_cast<const float*>(p.dY);
+  const float* X = reinterpret_cast<const float*>(p.X);
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int wm = wid >> 1, wn = wid & 1;
+  const int tiles_m = (p.M + FBM - 1) / FBM, tiles_n = (p.N + FBN - 1) / FBN;
+  const int tiles = tiles_m * tiles_n;
+  const int lt = xcd_remap_f(blockIdx.x, gridDim.x);
+  const int split = lt / tiles, tt = lt % tiles;
+  const int tm = tt / tiles_n, tn = tt % tiles_n;
+  const int m0 = tm * FBM, n0 = tn * FBN;
+  const long pbeg = (long)split * p.k_per_split;
+  const long pend = pbeg + p.k_per_split < p.P ? pbeg + p.k_per_split : p.P;
+
+  const int tcol = tid & 63, tk = tid >> 6;
+  const int am = m0 + tcol, bn = n0 + tcol;
+  const bool aok = am < p.M, bok = bn < p.N;
+  const int bt = bok ? bn / p.Cs : 0, bc = bok ? bn - bt * p.Cs : 0;
+  const int bdy = bok ? p.tap_dy[bt] : 0, bdx = bok ? p.tap_dx[bt] : 0;
+  float bias_acc = 0.f;
+
+  f32x4 acc[2][2];
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int j = 0; j < 2; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  const int ghw = p.GH * p.GW;
+  for (long k0 = pbeg; k0 < pend; k0 += XBK) {
+    float va[8], vb[8];
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      const long pix = k0 + tk * 8 + e;
+      va[e] = 0.f;
+      vb[e] = 0.f;
+      if (pix < pend) {
+        if (aok) va[e] = dY[pix * p.ldy + am];
+        if (bok) {
+          const int img = (int)(pix / ghw), rem = (int)(pix - (long)img * ghw);
+          const int gy = rem / p.GW, gx = rem - gy * p.GW;
+          const int sy = gy * p.SY + bdy, sx = gx * p.SX + bdx;
+          if (sy >= 0 && sy < p.H && sx >= 0 && sx < p.W) vb[e] = X[(((long)img * p.H + sy) * p.W + sx) * p.Cs + bc];
+        }
+      }
+    }
+    if (p.bias_slab && tn == 0) {
+#pragma unroll
+      for (int e = 0; e < 8; ++e) bias_acc += va[e];  // this thread's column, pixels in order
+    }
+    __syncthreads();  // previous tile fully consumed
+    {
+      bf16x8 h, l;
+      split8(va, h, l);
+      *reinterpret_cast<bf16x8*>(&Ah[tcol * XP + tk * 8]) = h;
+      *reinterpret_cast<bf16x8*>(&Al[tcol * XP + tk * 8]) = l;
+      split8(vb, h, l);
+      *reinterpret_cast<bf16x8*>(&Bh[tcol * XP + tk * 8]) = h;
+      *reinterpret_cast<bf16x8*>(&Bl[tcol * XP + tk * 8]) = l;
+    }
+    __syncthreads();
+    const int g = lane >> 4;
+    bf16x8 ah[2], al[2], bh[2], bl[2];
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      const int o = (wm * 32 + i * 16 + (lane & 15)) * XP + g * 8;
+      ah[i] = *reinterpret_cast<const bf16x8*>(&Ah[o]);
+      al[i] = *reinterpret_cast<const bf16x8*>(&Al[o]);
+    }
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      const int o = (wn * 32 + j * 16 + (lane & 15)) * XP + g * 8;
+      bh[j] = *reinterpret_cast<const bf16x8*>(&Bh[o]);
+      bl[j] = *reinterpret_cast<const bf16x8*>(&Bl[o]);
+    }
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+      for (int j = 0; j < 2; ++j) acc[i][j] = mfma3(ah[i], al[i], bh[j], bl[j], acc[i][j]);
+  }
+  float* out = p.slab + (long)split * p.M * p.N;
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      const int col = n0 + wn * 32 + j * 16 + (lane & 15);
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int row = m0 + wm * 32 + i * 16 + (lane >> 4) * 4 + r;
+        if (row < p.M && col < p.N) out[(long)row * p.N + col] = acc[i][j][r];
+      }
+    }
+  if (p.bias_slab && tn == 0) {
+    // fixed-order sum of the 4 k-group partials of each column (LDS, after the last tile)
+    __shared__ float bred[4][FBM];
+    bred[tk][tcol] = bias_acc;
+    __syncthreads();
+    if (tid < FBM && m0 + tid < p.M)
+      p.bias_slab[(long)split * p.M + m0 + tid] = (bred[0][tid] + bred[1][tid]) + (bred[2][tid] + bred[3][tid]);
+  }
+}
+
+static bool f32_split() {
+  if (g_f32_mode < 0) {
+    const char* e = std::getenv("DCNN_F32_SPLIT");
+    g_f32_mode = (e && e[0] == '1') ? 1 : 0;
+  }
+  return g_f32_mode == 1;
+}
+
+void set_f32_mode(int mode) { g_f32_mode = mode ? 1 : 0; }
+int get_f32_mode() { return f32_split() ? 1 : 0; }
+
 void gemm_g2f(const G2Args& a, hipStream_t s) {
   if (a.ntaps > 64) throw std::runtime_error("gemm_g2f: at most 64 taps");
   const int tiles = ((a.M + FBM - 1) / FBM) * ((a.N + FBN - 1) / FBN);
-  hipLaunchKernelGGL(gemm_g2f_kernel, dim3(tiles), dim3(256), 0, s, a);
+  if (f32_split())
+    hipLaunchKernelGGL(gemm_g2x_kernel, dim3(tiles), dim3(256), 0, s, a);
+  else
+    hipLaunchKernelGGL(gemm_g2f_kernel, dim3(tiles), dim3(256), 0, s, a);
+  DCNN_LAUNCH_CHECK();
 }
 
 int gemm_g2f_stat_rows(int M, int N) { return (M + FBM - 1) / FBM; }
@@ -319,9 +646,14 @@ int gemm_t2f_splits(int M, int N, int P) {
 void gemm_t2f(T2Args a, int splits, hipStream_t s) {
   if (a.ntaps > 64) throw std::runtime_error("gemm_t2f: at most 64 taps");
   const long per = (a.P + splits - 1) / splits;
-  a.k_per_split = (int)(((per + FBK - 1) / FBK) * FBK);
+  const int bk = f32_split() ? XBK : FBK;
+  a.k_per_split = (int)(((per + bk - 1) / bk) * bk);
   const int tiles = ((a.M + FBM - 1) / FBM) * ((a.N + FBN - 1) / FBN);
-  hipLaunchKernelGGL(gemm_t2f_kernel, dim3(tiles * splits), dim3(256), 0, s, a);
+  if (f32_split())
+    hipLaunchKernelGGL(gemm_t2x_kernel, dim3(tiles * splits), dim3(256), 0, s, a);
+  else
+    hipLaunchKernelGGL(gemm_t2f_kernel, dim3(tiles * splits), dim3(256), 0, s, a);
+  DCNN_LAUNCH_CHECK();
 }
 
 // [Co][T][Ci] fp32 -> [Ci][T][Co] fp32 (dgrad B operand of the fp32 path)

@@ -487,8 +487,19 @@ def test_dropout_regenerates_mask(hip):
 F32_CASES = CONV_CASES + [(2, 3, 32, 32, 64, 3, 1, 1), (2, 6, 9, 9, 10, 3, 2, 1), (1, 5, 7, 7, 7, 1, 1, 0)]
 
 
+@pytest.fixture(params=[0, 1], ids=["f32exact", "f32split"])
+def f32mode(request):
+    """fp32 GEMMs: 0 = exact v_mfma_f32_16x16x4_f32 (the default), 1 = split-precision 3xbf16."""
+    from dcnn_amd.ops._ext import kernels
+    K = kernels()
+    prev = K.get_f32_mode()
+    K.set_f32_mode(request.param)
+    yield request.param
+    K.set_f32_mode(prev)
+
+
 @pytest.mark.parametrize("case", F32_CASES)
-def test_conv_fp32_fwd_dgrad_wgrad(hip, case):
+def test_conv_fp32_fwd_dgrad_wgrad(hip, case, f32mode):
     N, Ci, H, W, Co, k, s, p = case
     torch.manual_seed(1)
     x = torch.randn(N, Ci, H, W)
@@ -520,7 +531,7 @@ def test_conv_fp32_fwd_dgrad_wgrad(hip, case):
 
 
 @pytest.mark.parametrize("shape", [(8, 512, 200), (5, 27, 10), (64, 256, 128)])
-def test_dense_fp32(hip, shape):
+def test_dense_fp32(hip, shape, f32mode):
     N, In, Out = shape
     torch.manual_seed(2)
     x, w, b = torch.randn(N, In), torch.randn(Out, In) / math.sqrt(In), torch.randn(Out)
@@ -592,3 +603,27 @@ def test_stat_reduce_many_rows_deterministic(hip):
     assert torch.equal(s1[0], s1[1])
     ref = slab1.double().sum(0).reshape(-1).cpu()
     assert (s1[0].double().cpu() - ref).abs().max() < 1e-4
+
+
+def test_fp32_split_precision_error_bound(hip):
+    """The 3xbf16 split GEMM against an fp64 reference on a deep reduction (K = 4608, the
+    ResNet layer-4 conv): relative error <= 1e-5 in norm and close to the exact f32 MFMA's."""
+    from dcnn_amd.ops._ext import kernels
+    K = kernels()
+    prev = K.get_f32_mode()
+    torch.manual_seed(7)
+    x = torch.randn(8, 512, 8, 8)
+    w = torch.randn(256, 512, 3, 3) / math.sqrt(512 * 9)
+    ref = F.conv2d(x.double(), w.double(), None, 1, 1)
+    errs = {}
+    try:
+        for mode in (0, 1):
+            K.set_f32_mode(mode)
+            y, _ = hip.conv2d_fwd(x.cuda().contiguous(memory_format=CL), w.cuda().contiguous(memory_format=CL),
+                                  None, (1, 1), (1, 1))
+            errs[mode] = ((y.double().cpu() - ref).norm() / ref.norm()).item()
+    finally:
+        K.set_f32_mode(prev)
+    assert errs[1] < 1e-5, errs
+    assert errs[0] < 3e-6, errs
+
