@@ -31,7 +31,7 @@ def main(argv=None):
     ap = argparse.ArgumentParser()
     ap.add_argument("--model", default="resnet50_tiny_imagenet")
     ap.add_argument("--stages", type=int, default=4)
-    ap.add_argument("--schedule", default="sync", choices=["sync", "semi_async"])
+    ap.add_argument("--schedule", default="sync", choices=["sync", "semi_async", "1f1b"])
     ap.add_argument("--batch", type=int, default=256)
     ap.add_argument("--microbatches", type=int, default=8)
     ap.add_argument("--steps", type=int, default=10)

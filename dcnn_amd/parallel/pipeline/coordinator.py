@@ -10,6 +10,11 @@ steps then exchange micro-batches with the first / last stage:
 * ``async_process_batch`` — the reference's semi-async schedule (coordinator.hpp:273-326):
   every forward is issued at once, and each output's loss + backward is launched the moment
   it arrives while stages keep prioritising forwards.
+* ``one_f_one_b_process_batch`` — 1F1B (PipeDream-flush): at most ``max_in_flight`` micro-batches
+  (default: the number of stages) are between their forward and the end of their backward; a new
+  forward is injected each time a backward completes. Every stage then holds the activations of
+  at most that many micro-batches (GPipe / semi-async hold all of them) while the steady state
+  alternates one forward with one backward per stage.
 * ``update_parameters()`` — UPDATE_PARAMETERS broadcast + join PARAMETERS_UPDATED.
 
 Gradient semantics: each micro-batch's loss gradient is the micro-batch mean; by default it
@@ -243,9 +248,52 @@ class Coordinator:
         self.join(C.BACKWARD_JOB, m)
         return self._finish(losses, corrects)
 
+    def one_f_one_b_process_batch(self, xs: Sequence[torch.Tensor], ys: Sequence[torch.Tensor],
+                                  max_in_flight: Optional[int] = None) -> float:
+        m = len(xs)
+        cap = max(1, int(max_in_flight or self.num_stages))
+        losses, corrects = [], []
+        sent = done = 0
+        while sent < min(m, cap):
+            self.forward(xs[sent], sent)
+            sent += 1
+        self.max_in_flight_seen = sent
+        deadline = time.time() + self.timeout_s
+        while done < m:
+            self._check_errors()
+            got = False
+            msg = self.comm.recv_command(int(C.FORWARD_JOB), 0)
+            if msg is not None:  # an output: loss, then its backward
+                got = True
+                mb = int(msg.mb_id)
+                loss, grad, c = self._loss_grad(self._output(msg), ys[mb], mb)
+                self.backward(grad, mb)
+                losses.append(loss)
+                corrects.append(c)
+            msg = self.comm.recv_command(int(C.BACKWARD_JOB), 0 if got else 20)
+            if msg is not None:  # a backward finished: admit the next forward
+                got = True
+                done += 1
+                if sent < m:
+                    self.forward(xs[sent], sent)
+                    sent += 1
+                    self.max_in_flight_seen = max(self.max_in_flight_seen, sent - done)
+            if not got and time.time() > deadline:
+                raise PipelineError(f"1F1B: timeout ({done}/{m} backwards done)")
+        return self._finish(losses, corrects)
+
+    SCHEDULES = ("sync", "gpipe", "semi_async", "1f1b")
+
     def train_step(self, x: torch.Tensor, y: torch.Tensor, schedule: str = "semi_async") -> float:
         xs, ys = self.split(x, y)
-        fn = self.sync_process_batch if schedule in ("sync", "gpipe") else self.async_process_batch
+        if schedule in ("sync", "gpipe"):
+            fn = self.sync_process_batch
+        elif schedule in ("semi_async", "async"):
+            fn = self.async_process_batch
+        elif schedule in ("1f1b", "one_f_one_b"):
+            fn = self.one_f_one_b_process_batch
+        else:
+            raise ValueError(f"unknown pipeline schedule '{schedule}' (one of {self.SCHEDULES})")
         loss = fn(xs, ys)
         self.update_parameters()
         return loss

@@ -52,14 +52,14 @@ def _pipeline_run(use_graph, schedule, steps=4, stages=2, mbs=4):
         coord.stop()
 
 
-@pytest.mark.parametrize("schedule", ["sync", "semi_async"])
+@pytest.mark.parametrize("schedule", ["sync", "semi_async", "1f1b"])
 def test_gpu_pipeline_graph_matches_eager(schedule):
     """Stages replaying per-micro-batch hipGraphs (from step 2 on) train exactly like eager stages:
     sync (fixed accumulation order) bit-for-bit, semi-async up to the gradient-accumulation order."""
     le, pe, _ = _pipeline_run(False, schedule)
     lg, pg, st = _pipeline_run(True, schedule)
     assert all(s["graphs"]["replays"] > 0 for s in st), st
-    if schedule == "sync":
+    if schedule in ("sync", "1f1b"):
         assert le == lg
         for a, b in zip(pe, pg):
             assert torch.equal(a, b)

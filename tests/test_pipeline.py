@@ -168,3 +168,44 @@ def test_multiprocess_pipeline_gloo(transport, schedule):
     line = [l for l in r.stdout.splitlines() if l.startswith("{") and "pipeline" in l][-1]
     d = json.loads(line)
     assert d["stages"] == 3 and d["value"] > 0 and d["loss"] == d["loss"]
+
+
+def _run_schedule(schedule, steps=2, stages=3, mbs=6):
+    model = zoo.create_model("mnist_cnn")
+    coord = InProcessCoordinator(model, SGD(0.05, 0.9), "softmax_crossentropy", num_stages=stages,
+                                 num_microbatches=mbs, partitioner=NaivePartitioner(), seed=5)
+    try:
+        coord.initialize()
+        coord.deploy_stages()
+        coord.start()
+        g = torch.Generator().manual_seed(2)
+        x = torch.randn(12, 1, 28, 28, generator=g)
+        y = torch.randint(0, 10, (12,), generator=g)
+        losses = [coord.train_step(x, y, schedule) for _ in range(steps)]
+        return losses, coord.collect_parameters(), getattr(coord, "max_in_flight_seen", None)
+    finally:
+        coord.stop()
+
+
+def test_one_f_one_b_matches_sync_and_bounds_in_flight():
+    """1F1B (at most num_stages micro-batches between forward and backward completion) trains
+    exactly like GPipe: per stage the backwards arrive in micro-batch order in both schedules and
+    the native CPU kernels are deterministic, so losses and parameters are bit-identical."""
+    ls, ps, _ = _run_schedule("sync")
+    lf, pf, inflight = _run_schedule("1f1b")
+    assert inflight is not None and inflight <= 3
+    assert ls == lf
+    for a, b in zip(ps, pf):
+        assert torch.equal(a, b)
+
+
+def test_unknown_schedule_rejected():
+    model = zoo.create_model("mnist_cnn")
+    coord = InProcessCoordinator(model, SGD(0.05), "softmax_crossentropy", num_stages=1, num_microbatches=1)
+    try:
+        coord.initialize()
+        coord.deploy_stages()
+        with pytest.raises(ValueError):
+            coord.train_step(torch.randn(2, 1, 28, 28), torch.randint(0, 10, (2,)), "zigzag")
+    finally:
+        coord.stop()
