@@ -15,6 +15,7 @@ namespace py = pybind11;
 
 
 using namespace dcnn;
+void bind_runtime(py::module_& m);  // runtime.cpp: native Device / Flow / Task / Allocator
 template <typename T>
 static inline T P(uintptr_t x) { return reinterpret_cast<T>(x); }
 static inline hipStream_t S(uintptr_t x) { return reinterpret_cast<hipStream_t>(x); }
@@ -22,6 +23,7 @@ static inline hipStream_t S(uintptr_t x) { return reinterpret_cast<hipStream_t>(
 PYBIND11_MODULE(_kernels, m) {
   m.doc() = "dcnn_amd HIP/CDNA4 (gfx950) kernel library";
   m.attr("arch") = "gfx950";
+  bind_runtime(m);
 
   m.def("gemm_nt",
         [](uintptr_t A, uintptr_t B, uintptr_t C, int M, int N, int K, int lda, int ldb, int ldc, int mode, int nb,

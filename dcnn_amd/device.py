@@ -4,15 +4,23 @@ MI355X-native replacement for the reference's L2 device runtime
 (`include/device/device.hpp:12`, `include/device/device_manager.hpp:9`,
 `include/device/flow.hpp:11`, `include/device/task.hpp:26`).
 
-Design differences (intentional):
-  * memory comes from PyTorch-ROCm's stream-ordered caching allocator
-    (`hipMallocAsync`-style pools) instead of raw `cudaMalloc` per tensor;
-  * a `Flow` is a real HIP stream (`torch.cuda.Stream`), and several flows per
-    device are used (compute / comm / h2d) instead of a single "default" one;
-  * a `Task` is a HIP event recorded on the flow — `sync()` waits for that
-    event only, it never device-synchronises;
-  * every call honours the tensor's own device (`GPU:i`), there is no global
-    "GPU 0" (reference defect G6).
+The GPU side is a thin Python layer over the native HIP runtime of the kernel library
+(``_kernels.rt``, csrc/kernels/runtime.cpp):
+
+  * memory: ``Device.allocate`` draws from a per-device stream-ordered caching pool
+    (``hipMallocFromPoolAsync`` on the caller's flow, release threshold "keep everything") and
+    hands the buffer to PyTorch zero-copy through DLPack — the framework's flat parameter /
+    gradient / optimizer arenas live there; ``allocator_stats()`` shows reuse (steady-state
+    training allocates without growing the reservation) instead of the reference's cudaMalloc
+    per tensor;
+  * a ``Flow`` is a native HIP stream (non-blocking, optional priority); the "default" flow wraps
+    PyTorch's *current* stream handle, so captured hipGraphs and user-set streams are honoured,
+    and ``Flow.stream`` exposes any flow to PyTorch as an external stream;
+  * a ``Task`` is a native HIP event recorded on a flow — ``sync()`` waits for that event only,
+    it never device-synchronises;
+  * every call honours the device it is made on (``GPU:i``), there is no global "GPU 0"
+    (reference defect G6).
+CPU devices keep host semantics (synchronous flows, no events).
 """
 from __future__ import annotations
 
@@ -21,6 +29,16 @@ import threading
 from typing import Dict, List, Optional
 
 import torch
+
+
+def _rt():
+    from .ops._ext import kernels
+    return kernels().rt
+
+
+_DLPACK_CODES = {torch.float32: (2, 32), torch.float64: (2, 64), torch.float16: (2, 16), torch.bfloat16: (4, 16),
+                 torch.int32: (0, 32), torch.int64: (0, 64), torch.int16: (0, 16), torch.int8: (0, 8),
+                 torch.uint8: (1, 8)}
 
 
 class DeviceType(enum.Enum):
@@ -68,26 +86,54 @@ class Device:
                 return cpu_model_name()
             except Exception:
                 return "CPU"
-        return torch.cuda.get_device_name(self.index)
+        return _rt().device_properties(self.index)["name"]
+
+    def properties(self) -> dict:
+        """Native device properties (name, gfx arch, memory, CU count, LDS, L2, ...)."""
+        if self.device_type == DeviceType.CPU:
+            return {"name": self.name()}
+        return dict(_rt().device_properties(self.index))
 
     def get_total_memory(self) -> int:
         if self.device_type == DeviceType.CPU:
             from .utils.hardware import total_memory_bytes
             return total_memory_bytes()
-        return torch.cuda.get_device_properties(self.index).total_memory
+        return int(_rt().mem_info(self.index)[1])
 
     def get_available_memory(self) -> int:
         if self.device_type == DeviceType.CPU:
             from .utils.hardware import available_memory_bytes
             return available_memory_bytes()
-        free, _ = torch.cuda.mem_get_info(self.index)
-        return free
+        return int(_rt().mem_info(self.index)[0])
 
-    def allocate(self, numel: int, dtype=torch.float32) -> torch.Tensor:
-        return torch.empty(numel, dtype=dtype, device=self.torch_device)
+    def allocate(self, numel, dtype=torch.float32, zero: bool = False, flow: str = "default") -> torch.Tensor:
+        """A buffer of ``numel`` (int or shape) elements. GPU: from the native stream-ordered pool
+        on ``flow`` (zero-copy PyTorch tensor via DLPack); CPU: host memory."""
+        shape = [int(numel)] if isinstance(numel, int) else [int(s) for s in numel]
+        if self.device_type == DeviceType.CPU:
+            return torch.zeros(shape, dtype=dtype) if zero else torch.empty(shape, dtype=dtype)
+        code, bits = _DLPACK_CODES[dtype]
+        cap = _rt().alloc_dlpack(self.index, shape, code, bits, self.get_flow(flow).native, zero)
+        return torch.from_dlpack(cap)
 
-    def copy_to_device(self, dst: torch.Tensor, src: torch.Tensor) -> None:
+    def allocator_stats(self) -> dict:
+        if self.device_type == DeviceType.CPU:
+            return {}
+        return dict(_rt().Allocator.get(self.index).stats())
+
+    def copy_to_device(self, dst: torch.Tensor, src: torch.Tensor, flow: str = "default") -> None:
+        """dst <- src, asynchronous on ``flow`` for GPU copies of dense same-dtype tensors."""
+        if (self.device_type == DeviceType.GPU and dst.dtype == src.dtype and dst.numel() == src.numel()
+                and dst.is_contiguous() and src.is_contiguous() and (dst.is_cuda or src.is_cuda)):
+            kind = 2 if (dst.is_cuda and src.is_cuda) else (0 if dst.is_cuda else 1)
+            _rt().memcpy_async(dst.data_ptr(), src.data_ptr(), dst.numel() * dst.element_size(), kind,
+                               self.get_flow(flow).native)
+            return
         dst.copy_(src, non_blocking=True)
+
+    def synchronize(self) -> None:
+        if self.device_type == DeviceType.GPU:
+            _rt().device_synchronize(self.index)
 
     # --- flows ----------------------------------------------------------------------
     def get_flow(self, name: str = "default") -> "Flow":
@@ -100,52 +146,71 @@ class Device:
 
 
 class Flow:
-    """Named execution queue. CPU flows are synchronous; GPU flows own a HIP stream.
+    """Named execution queue. CPU flows are synchronous; GPU flows are native HIP streams.
 
-    The "default" GPU flow maps to PyTorch's *current* stream so that captured hipGraphs and
-    user-set streams are honoured; other names get dedicated non-blocking streams (e.g. "comm").
+    The "default" GPU flow wraps PyTorch's *current* stream handle (looked up at every use) so
+    that captured hipGraphs and user-set streams are honoured; other names own dedicated
+    non-blocking streams (e.g. "comm", "h2d"); ``priority`` < 0 is a high-priority stream.
     """
 
-    def __init__(self, device: Device, name: str):
+    def __init__(self, device: Device, name: str, priority: int = 0):
         self.device = device
         self.name = name
-        self._stream: Optional[torch.cuda.Stream] = None
+        self._native = None
         if device.is_gpu() and name != "default":
-            self._stream = torch.cuda.Stream(device=device.torch_device)
+            self._native = _rt().Flow(device.index, int(priority))
+        self._torch_stream = None
+
+    @property
+    def native(self):
+        """The native ``rt.Flow`` (for the default flow: a wrapper of the current stream)."""
+        if self._native is not None:
+            return self._native
+        h = torch.cuda.current_stream(self.device.torch_device).cuda_stream
+        return _rt().Flow(self.device.index, int(h))
 
     @property
     def stream(self):
+        """This flow as a PyTorch stream (``with torch.cuda.stream(flow.stream): ...``)."""
         if not self.device.is_gpu():
             return None
-        if self._stream is None:
+        if self._native is None:
             return torch.cuda.current_stream(self.device.torch_device)
-        return self._stream
+        if self._torch_stream is None:
+            self._torch_stream = torch.cuda.ExternalStream(self._native.handle, device=self.device.torch_device)
+        return self._torch_stream
 
     def synchronize(self) -> None:
         if self.device.is_gpu():
-            self.stream.synchronize()
+            self.native.synchronize()
 
     def wait(self, task: "Task") -> None:
-        if self.device.is_gpu() and task.event is not None:
-            self.stream.wait_event(task.event)
+        if self.device.is_gpu() and task.native is not None:
+            self.native.wait(task.native)
+
+    def query(self) -> bool:
+        return True if not self.device.is_gpu() else bool(self.native.query())
 
 
 class Task:
-    """Completion handle of asynchronously launched work (a recorded HIP event)."""
+    """Completion handle of asynchronously launched work (a native HIP event on the flow)."""
 
-    def __init__(self, flow: Optional[Flow] = None):
+    def __init__(self, flow: Optional[Flow] = None, timing: bool = False):
         self.flow = flow
-        self.event = None
+        self.native = None
         if flow is not None and flow.device.is_gpu():
-            self.event = torch.cuda.Event()
-            self.event.record(flow.stream)
+            self.native = _rt().Task(flow.device.index, bool(timing))
+            self.native.record(flow.native)
 
     def sync(self) -> None:
-        if self.event is not None:
-            self.event.synchronize()
+        if self.native is not None:
+            self.native.sync()
 
     def is_ready(self) -> bool:
-        return True if self.event is None else self.event.query()
+        return True if self.native is None else bool(self.native.is_ready())
+
+    def elapsed_ms(self, end: "Task") -> float:
+        return float(self.native.elapsed_ms(end.native))
 
 
 def task_sync_all(tasks: List[Task]) -> None:
@@ -229,5 +294,5 @@ def get_device(device_id) -> Device:
     return DeviceManager.instance().get_device(device_id)
 
 
-def create_task(device: Device, flow: str = "default") -> Task:
-    return Task(device.get_flow(flow))
+def create_task(device: Device, flow: str = "default", timing: bool = False) -> Task:
+    return Task(device.get_flow(flow), timing)

@@ -142,7 +142,7 @@ class SGD(Optimizer):
     def _on_attach(self):
         if self.momentum > 0:
             if self.arena is not None:
-                self.velocity = [torch.zeros_like(self._flat_p)]
+                self.velocity = [self.arena.new_zeros()]
             else:
                 self.velocity = [torch.zeros_like(p) for p in self.params]
 
@@ -211,8 +211,8 @@ class Adam(Optimizer):
 
     def _on_attach(self):
         if self.arena is not None:
-            self.m = [torch.zeros_like(self._flat_p)]
-            self.v = [torch.zeros_like(self._flat_p)]
+            self.m = [self.arena.new_zeros()]
+            self.v = [self.arena.new_zeros()]
         else:
             self.m = [torch.zeros_like(p) for p in self.params]
             self.v = [torch.zeros_like(p) for p in self.params]

@@ -52,12 +52,21 @@ class ParamArena:
                 n *= d
             off += (n + ALIGN - 1) // ALIGN * ALIGN
         self.numel = max(off, ALIGN)
-        self.data = torch.zeros(self.numel, dtype=dtype, device=self.device)
-        self.grad = torch.zeros(self.numel, dtype=dtype, device=self.device)
-        self.shadow = (torch.zeros(self.numel, dtype=shadow_dtype, device=self.device)
-                       if shadow_dtype is not None else None)
+        self.data = self.new_zeros(dtype)
+        self.grad = self.new_zeros(dtype)
+        self.shadow = self.new_zeros(shadow_dtype) if shadow_dtype is not None else None
         self._synced_version = -1
         self.step = 0  # optimizer steps applied (graph-replay safe counter lives in the optimizer)
+
+    def new_zeros(self, dtype=None) -> torch.Tensor:
+        """A zeroed flat buffer of the arena's size. On the GPU it comes from the native runtime's
+        stream-ordered pool (device.py / csrc/kernels/runtime.cpp) — arenas, optimizer moments and
+        their bf16 shadow are allocated once and live outside PyTorch's caching allocator."""
+        dtype = dtype or self.dtype
+        if self.device.type == "cuda":
+            from ..device import get_device
+            return get_device(self.device).allocate(self.numel, dtype, zero=True)
+        return torch.zeros(self.numel, dtype=dtype, device=self.device)
 
     def _view(self, buf, i):
         s = self.specs[i]
