@@ -169,6 +169,7 @@ void adam_step(float* p, const float* g, float* m, float* v, bf16* shadow, long 
                float eps, float bc1, float bc2, float wd, int decoupled, const float* hyper, hipStream_t s);
 void sgd_step(float* p, const float* g, float* vel, bf16* shadow, long n, float lr, float mom, const float* hyper,
               hipStream_t s);
+void adam_scalars(float* hyper, float b1, float b2, hipStream_t s);
 // data-parallel bf16 gradient wire format (comm.hip)
 void grad_pack_bf16(const float* g, bf16* out, long n, float scale, hipStream_t s);
 void grad_sum_chunks_bf16(const bf16* src, int w, long ld, long n, bf16* dst, hipStream_t s);

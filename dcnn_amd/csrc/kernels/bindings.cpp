@@ -361,6 +361,9 @@ PYBIND11_MODULE(_kernels, m) {
     adam_step(P<float*>(p), P<const float*>(g), P<float*>(mm), P<float*>(v), P<bf16*>(shadow), n, lr, b1, b2, eps, bc1,
               bc2, wd, dec, P<const float*>(hyper), S(st));
   });
+  m.def("adam_scalars", [](uintptr_t hyper, float b1, float b2, uintptr_t st) {
+    adam_scalars(P<float*>(hyper), b1, b2, S(st));
+  });
   m.def("sgd_step", [](uintptr_t p, uintptr_t g, uintptr_t vel, uintptr_t shadow, long n, float lr, float mom,
                        uintptr_t hyper, uintptr_t st) {
     sgd_step(P<float*>(p), P<const float*>(g), P<float*>(vel), P<bf16*>(shadow), n, lr, mom, P<const float*>(hyper),

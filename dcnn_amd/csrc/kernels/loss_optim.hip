@@ -239,6 +239,22 @@ void adam_step(float* p, const float* g, float* m, float* v, bf16* shadow, long 
   DCNN_LAUNCH_CHECK();
 }
 
+// Adam step scalars on the device: t += 1, bc1 = 1 - b1^t, bc2 = 1 - b2^t (hyper = {lr, bc1, bc2, t}).
+// Captured in the step graph ahead of adam_kernel, so a replay needs no host upload at all.
+__global__ void adam_scalars_kernel(float* hyper, float b1, float b2) {
+  if (threadIdx.x == 0) {
+    const float t = hyper[3] + 1.f;
+    hyper[3] = t;
+    hyper[1] = 1.f - powf(b1, t);
+    hyper[2] = 1.f - powf(b2, t);
+  }
+}
+
+void adam_scalars(float* hyper, float b1, float b2, hipStream_t s) {
+  hipLaunchKernelGGL(adam_scalars_kernel, dim3(1), dim3(64), 0, s, hyper, b1, b2);
+  DCNN_LAUNCH_CHECK();
+}
+
 void sgd_step(float* p, const float* g, float* vel, bf16* shadow, long n, float lr, float mom, const float* hyper,
               hipStream_t s) {
   hipLaunchKernelGGL(sgd_kernel, dim3(grid_for(n, 256, 4096)), dim3(256), 0, s, p, g, vel, shadow, n, lr, mom, hyper);

@@ -368,7 +368,10 @@ void bind_runtime(py::module_& parent) {
   m.def("can_access_peer", &can_access_peer);
   py::class_<Flow>(m, "Flow")
       .def(py::init<int, int>(), py::arg("device"), py::arg("priority") = 0)
-      .def(py::init<int, uintptr_t>(), py::arg("device"), py::arg("external_stream"))
+      // (a separate factory, not an overloaded constructor: the null stream's handle is 0, which
+      // an (int, int) overload would take as a priority and silently create a NEW stream)
+      .def_static("wrap", [](int dev, uintptr_t handle) { return std::make_unique<Flow>(dev, handle); },
+                  py::arg("device"), py::arg("external_stream"))
       .def_property_readonly("handle", &Flow::handle)
       .def_property_readonly("device", &Flow::device)
       .def_property_readonly("owned", &Flow::owned)

@@ -167,7 +167,7 @@ class Flow:
         if self._native is not None:
             return self._native
         h = torch.cuda.current_stream(self.device.torch_device).cuda_stream
-        return _rt().Flow(self.device.index, int(h))
+        return _rt().Flow.wrap(self.device.index, int(h))
 
     @property
     def stream(self):

@@ -2,9 +2,11 @@
 
 ``attach(params, grads)`` as in the reference. When the attached tensors are exactly the views
 of one :class:`ParamArena` (the normal case: a Sequential or a pipeline stage), the update is
-ONE fused kernel over the flat buffer which also refreshes the bf16 shadow weights; the
-step-dependent scalars (lr, bias corrections) are read from a tiny device tensor so a
-hipGraph-captured training step replays correctly. A CPU arena is updated by the native
+ONE fused kernel over the flat buffer which also refreshes the bf16 shadow weights. The step
+scalars live in a tiny device tensor ``{lr, bc1, bc2, t}``: Adam's step counter and bias
+corrections advance ON THE DEVICE (``adam_scalars``, captured in the step graph ahead of the
+update), and the learning rate is uploaded only when it changes — a replayed training step needs
+no host-to-device transfer besides its input batch. A CPU arena is updated by the native
 backend's flat-buffer loops (``ops/cpu.py``), in the arena's dtype (float32 or float64).
 """
 from __future__ import annotations
@@ -52,6 +54,7 @@ class Optimizer:
         self.arena = None
         self._flat_p = self._flat_g = None
         self._hyper = None
+        self._hyper_dirty = True  # device scalars must be (re)uploaded before the next step
 
     def attach(self, params, grads=None, arena=None) -> None:
         if grads is None and hasattr(params, "parameters"):
@@ -89,6 +92,8 @@ class Optimizer:
     zero_grad = clear_gradients
 
     def set_learning_rate(self, lr: float) -> None:
+        if float(lr) != self.learning_rate:
+            self._hyper_dirty = True
         self.learning_rate = float(lr)
 
     def get_learning_rate(self) -> float:
@@ -147,8 +152,9 @@ class SGD(Optimizer):
                 self.velocity = [torch.zeros_like(p) for p in self.params]
 
     def prepare_step(self):
-        if self.arena is not None and self._flat_p.is_cuda:
+        if self.arena is not None and self._flat_p.is_cuda and (self._hyper_dirty or self._hyper is None):
             self._device_hyper([self.learning_rate])
+            self._hyper_dirty = False
 
     def launch_step(self):
         from ..ops import hip
@@ -222,15 +228,22 @@ class Adam(Optimizer):
         return self.arena is not None and self._flat_p.is_cuda
 
     def prepare_step(self):
-        """Host side of a step (graph-replay safe): advance t, upload lr / bias corrections."""
+        """Host side of a step (graph-replay safe): advance the host step counter; upload the
+        device scalars only when stale (first step, learning-rate change, loaded state) — the
+        device counter then equals t - 1 and ``launch_step`` advances it on the device."""
         self.t += 1
         self._bc = (1.0 - self.beta1 ** self.t, 1.0 - self.beta2 ** self.t)
-        if self.fused():
-            self._device_hyper([self.learning_rate, self._bc[0], self._bc[1]])
+        if self.fused() and (self._hyper_dirty or self._hyper is None):
+            self._device_hyper([self.learning_rate, 0.0, 0.0, float(self.t - 1)])
+            self._hyper_dirty = False
 
     def launch_step(self):
-        """Device side: ONE kernel over the flat buffer, reading lr/bc from device memory."""
+        """Device side: the scalar update (t, bias corrections) and ONE kernel over the flat
+        buffer, both reading their scalars from device memory."""
         from ..ops import hip
+        from ..ops._ext import kernels, stream_ptr
+        kernels().adam_scalars(self._hyper.data_ptr(), float(self.beta1), float(self.beta2),
+                               stream_ptr(self._flat_p.device))
         bc1, bc2 = self._bc
         hip.adam_step(self._flat_p, self._flat_g, self.m[0], self.v[0], self.arena.shadow, self.learning_rate,
                       self.beta1, self.beta2, self.epsilon, bc1, bc2, self.weight_decay,
@@ -286,6 +299,7 @@ class Adam(Optimizer):
 
     def load_state_dict(self, d):
         self.t = int(d.get("t", 0))
+        self._hyper_dirty = True
         for dst, src in zip(self.m or [], d.get("m", [])):
             dst.copy_(src)
         for dst, src in zip(self.v or [], d.get("v", [])):

@@ -83,7 +83,11 @@ class ParamArena:
         return None if self.shadow is None else self._view(self.shadow, i)
 
     def zero_grad(self):
-        self.grad.zero_()
+        if self.grad.is_cuda:
+            from ..ops import hip
+            hip.zero_(self.grad)  # hipMemsetAsync (a memset node in the step graph)
+        else:
+            self.grad.zero_()
 
     def sync_shadow(self, force: bool = False):
         """Refresh the bf16 shadow from the fp32 master if the master changed in place."""

@@ -318,8 +318,12 @@ def conv2d_dgrad(dy, wt, x_shape, stride, pad, *, residual=None, bnb=None):
                 empty_class = True
     odt = F32 if f32 else BF16
     if empty_class:
-        dx = residual.clone() if residual is not None else torch.empty(
-            (N, Ci, H, W), dtype=odt, device=dy.device, memory_format=CL).zero_()
+        # positions no tap reaches keep the residual (or zero); a memset / async copy node, not a kernel
+        dx = torch.empty((N, Ci, H, W), dtype=odt, device=dy.device, memory_format=CL)
+        if residual is not None:
+            dx.copy_(residual)
+        else:
+            zero_(dx)
     else:
         dx = torch.empty((N, Ci, H, W), dtype=odt, device=dy.device, memory_format=CL)
     st = stream_ptr()
@@ -655,7 +659,7 @@ def _ticket(device, C, slot="stat"):
     t = _tickets.get(key)
     need = (C + 63) // 64
     if t is None or t.numel() < need:
-        t = torch.zeros(max(need, 64), dtype=torch.int32, device=device)
+        t = zero_(torch.empty(max(need, 64), dtype=torch.int32, device=device))
         _tickets[key] = t
     return t
 
@@ -699,6 +703,13 @@ class Stats:
 
     def __getitem__(self, i):
         return self.final()[i]
+
+
+def prewarm_tickets(device, slots=("loss",)):
+    """Create the calling stream's ticket words now (call it on a graph's capture stream before the
+    capture): created during a capture, their zeroing would be re-run by every replay."""
+    for s in slots:
+        _ticket(torch.device(device), 0, slot=s)
 
 
 def stat_reduce(mode, slab, rows, C, out):
@@ -993,6 +1004,18 @@ def adam_step(p, g, m, v, shadow, lr, b1, b2, eps, bc1, bc2, wd, decoupled, hype
 def sgd_step(p, g, vel, shadow, lr, momentum, hyper=None):
     kernels().sgd_step(p.data_ptr(), g.data_ptr(), ptr(vel), ptr(shadow), p.numel(), float(lr), float(momentum),
                        ptr(hyper), stream_ptr())
+
+
+def zero_(t):
+    """Zero a dense GPU tensor with hipMemsetAsync on the current stream (a memset node inside a
+    captured graph; no ATen fill kernel on the hot path)."""
+    assert t.is_cuda and (t.is_contiguous() or t.is_contiguous(memory_format=CL))
+    if os.environ.get("DCNN_MEMSET", "1") == "0":
+        return t.zero_()
+    from ._ext import kernels as _k
+    _k().rt.memset_async(t.data_ptr(), 0, t.numel() * t.element_size(),
+                         _k().rt.Flow.wrap(t.device.index, stream_ptr(t.device)))
+    return t
 
 
 def cast_bf16(src, dst):

@@ -36,6 +36,7 @@ class TrainStep:
         self.graphs: Optional[List[torch.cuda.CUDAGraph]] = None
         self.capture_collectives = os.environ.get("DCNN_DP_CAPTURE", "1") != "0"
         self._whole = False
+        self._cap_stream = None
         self.last_loss = None
         self.last_correct = None
         self._static_x = self._static_y = None
@@ -81,6 +82,17 @@ class TrainStep:
             ts += _bn_buffers(l)
         return ts
 
+    def _capture_stream(self):
+        """The stream graphs are captured on, with its per-stream ticket words created eagerly."""
+        if self._cap_stream is None:
+            from ..ops import hip
+            self._cap_stream = torch.cuda.Stream(device=self.model.device.torch_device)
+            self._cap_stream.wait_stream(torch.cuda.current_stream())
+            with torch.cuda.stream(self._cap_stream):
+                hip.prewarm_tickets(self.model.device.torch_device)
+            torch.cuda.current_stream().wait_stream(self._cap_stream)
+        return self._cap_stream
+
     def _capture(self, x, y):
         self._static_x = x.clone()
         self._static_y = y.clone()
@@ -103,6 +115,7 @@ class TrainStep:
         del saved
         if saved_t is not None:
             self.opt.t = saved_t
+        self.opt._hyper_dirty = True  # device step scalars re-synced from the restored host state
         self.model.arena.sync_shadow(force=True)
         torch.cuda.synchronize()
         fused_opt = hasattr(self.opt, "fused") and self.opt.fused()
@@ -135,7 +148,7 @@ class TrainStep:
         active = self.dp.active
         for k, (hi, lo) in enumerate(segs):
             g = torch.cuda.CUDAGraph()
-            with torch.cuda.graph(g, pool=pool):
+            with torch.cuda.graph(g, pool=pool, stream=self._capture_stream()):
                 if k == 0:
                     self.opt.clear_gradients()
                     out = self.dp.forward(self._static_x)
@@ -157,7 +170,7 @@ class TrainStep:
             self.graphs.append(g)
         if active:
             g = torch.cuda.CUDAGraph()
-            with torch.cuda.graph(g, pool=pool):
+            with torch.cuda.graph(g, pool=pool, stream=self._capture_stream()):
                 self.opt.launch_step()
             self.graphs.append(g)
         torch.cuda.synchronize()
@@ -172,7 +185,7 @@ class TrainStep:
         m.enable_profiling_ = False
         g = torch.cuda.CUDAGraph()
         try:
-            with torch.cuda.graph(g, capture_error_mode="thread_local"):
+            with torch.cuda.graph(g, stream=self._capture_stream(), capture_error_mode="thread_local"):
                 self.opt.clear_gradients()
                 out = self.dp.forward(self._static_x)
                 loss, grad, correct = self.loss_fn.loss_and_grad(out, self._static_y)
