@@ -174,4 +174,5 @@ void adam_scalars(float* hyper, float b1, float b2, hipStream_t s);
 void grad_pack_bf16(const float* g, bf16* out, long n, float scale, hipStream_t s);
 void grad_sum_chunks_bf16(const bf16* src, int w, long ld, long n, bf16* dst, hipStream_t s);
 void grad_unpack_bf16(const bf16* in, float* g, long n, hipStream_t s);
+void zero_bytes(void* p, long nbytes, hipStream_t s);
 }  // namespace dcnn

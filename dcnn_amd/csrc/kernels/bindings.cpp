@@ -369,6 +369,7 @@ PYBIND11_MODULE(_kernels, m) {
     sgd_step(P<float*>(p), P<const float*>(g), P<float*>(vel), P<bf16*>(shadow), n, lr, mom, P<const float*>(hyper),
              S(st));
   });
+  m.def("zero_bytes", [](uintptr_t p, long nbytes, uintptr_t st) { zero_bytes(P<void*>(p), nbytes, S(st)); });
   m.def("grad_pack_bf16", [](uintptr_t g, uintptr_t out, long n, float scale, uintptr_t st) {
     grad_pack_bf16(P<const float*>(g), P<bf16*>(out), n, scale, S(st));
   });

@@ -72,6 +72,25 @@ inline int stream_grid(long n) { return grid_for((n + 7) / 8, 256); }
 
 }  // namespace
 
+// byte-exact zero fill (16-byte stores + tail). Used instead of hipMemsetAsync for buffers zeroed
+// inside captured graphs: on ROCm 7.2 a captured memset node wrote garbage from its second replay
+// on (tools/dbg/memset_graph.py), a kernel node replays correctly.
+__global__ void zero_bytes_kernel(unsigned char* __restrict__ p, long nbytes) {
+  const long n16 = nbytes / 16;
+  const long stride = (long)gridDim.x * blockDim.x;
+  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < n16; i += stride)
+    reinterpret_cast<uint4*>(p)[i] = make_uint4(0u, 0u, 0u, 0u);
+  for (long i = n16 * 16 + blockIdx.x * (long)blockDim.x + threadIdx.x; i < nbytes; i += stride) p[i] = 0;
+}
+
+void zero_bytes(void* p, long nbytes, hipStream_t s) {
+  if (nbytes <= 0) return;
+  if (reinterpret_cast<uintptr_t>(p) % 16) throw std::runtime_error("zero_bytes: 16-byte aligned buffers only");
+  hipLaunchKernelGGL(zero_bytes_kernel, dim3(grid_for((nbytes + 15) / 16, 256)), dim3(256), 0, s,
+                     static_cast<unsigned char*>(p), nbytes);
+  DCNN_LAUNCH_CHECK();
+}
+
 void grad_pack_bf16(const float* g, bf16* out, long n, float scale, hipStream_t s) {
   if (n <= 0) return;
   hipLaunchKernelGGL(grad_pack_kernel, dim3(stream_grid(n)), dim3(256), 0, s, g, out, n, scale);

@@ -194,6 +194,7 @@ class Allocator {
 
   uintptr_t allocate(uint64_t nbytes, const Flow& f) {
     if (nbytes == 0) nbytes = 1;
+    release_deferred();
     DeviceGuard g(dev_);
     const uint64_t before = reserved();
     void* p = nullptr;
@@ -212,15 +213,30 @@ class Allocator {
     ++frees_;
     in_use_ -= std::min(in_use_, nbytes);
   }
-  // synchronous free for buffers whose last user is unknown (DLPack exports)
-  void free_sync(uintptr_t p, uint64_t nbytes) {
+  // Buffers whose last user is unknown (DLPack exports, freed by whoever drops the last tensor
+  // reference — possibly Python's GC inside another thread's graph capture, where no HIP call may
+  // run): only queued here, released by release_deferred() at the next allocation or an explicit
+  // device synchronize.
+  void defer_free(uintptr_t p, uint64_t nbytes) {
+    std::lock_guard<std::mutex> l(mu_);
+    deferred_.push_back({p, nbytes});
+  }
+  void release_deferred() {
+    std::vector<std::pair<uintptr_t, uint64_t>> todo;
+    {
+      std::lock_guard<std::mutex> l(mu_);
+      todo.swap(deferred_);
+    }
+    if (todo.empty()) return;
     DeviceGuard g(dev_);
-    RT_CHECK(hipDeviceSynchronize());
-    RT_CHECK(hipFreeAsync(reinterpret_cast<void*>(p), nullptr));
+    RT_CHECK(hipDeviceSynchronize());  // every stream done with them
+    for (auto& d : todo) RT_CHECK(hipFreeAsync(reinterpret_cast<void*>(d.first), nullptr));
     RT_CHECK(hipStreamSynchronize(nullptr));
     std::lock_guard<std::mutex> l(mu_);
-    ++frees_;
-    in_use_ -= std::min(in_use_, nbytes);
+    for (auto& d : todo) {
+      ++frees_;
+      in_use_ -= std::min(in_use_, d.second);
+    }
   }
   uint64_t reserved() const {
     uint64_t v = 0;
@@ -241,6 +257,7 @@ class Allocator {
     d["frees"] = frees_;
     d["reservation_grows"] = grows_;
     d["in_use_bytes"] = in_use_;
+    d["deferred_frees"] = (uint64_t)deferred_.size();
     d["peak_in_use_bytes"] = peak_;
     return d;
   }
@@ -267,6 +284,7 @@ class Allocator {
   hipMemPool_t pool_ = nullptr;
   mutable std::mutex mu_;
   uint64_t allocs_ = 0, frees_ = 0, grows_ = 0, in_use_ = 0, peak_ = 0;
+  std::vector<std::pair<uintptr_t, uint64_t>> deferred_;
 };
 
 // ------------------------------------------------------------------ DLPack export (zero copy)
@@ -287,12 +305,9 @@ struct Export {
   uint64_t nbytes = 0;
 };
 
-void export_deleter(DLManagedTensor* m) {
+void export_deleter(DLManagedTensor* m) {  // no HIP call here (see Allocator::defer_free)
   Export* e = static_cast<Export*>(m->manager_ctx);
-  try {
-    Allocator::get(e->dev).free_sync(e->ptr, e->nbytes);
-  } catch (...) {
-  }
+  Allocator::get(e->dev).defer_free(e->ptr, e->nbytes);
   delete e;
 }
 
@@ -390,6 +405,7 @@ void bind_runtime(py::module_& parent) {
       .def("free", &Allocator::free)
       .def("stats", &Allocator::stats)
       .def("trim", &Allocator::trim, py::arg("keep_bytes") = 0)
+      .def("release_deferred", &Allocator::release_deferred, py::call_guard<py::gil_scoped_release>())
       .def_property_readonly("device", &Allocator::device);
   m.def("alloc_dlpack", &alloc_dlpack, py::arg("device"), py::arg("shape"), py::arg("code"), py::arg("bits"),
         py::arg("flow"), py::arg("zero") = false);

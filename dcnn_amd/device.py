@@ -132,8 +132,11 @@ class Device:
         dst.copy_(src, non_blocking=True)
 
     def synchronize(self) -> None:
+        """Device-wide synchronize; also returns buffers released since the last allocation to
+        the native pool (their frees are deferred: see runtime.cpp Allocator::defer_free)."""
         if self.device_type == DeviceType.GPU:
             _rt().device_synchronize(self.index)
+            _rt().Allocator.get(self.index).release_deferred()
 
     # --- flows ----------------------------------------------------------------------
     def get_flow(self, name: str = "default") -> "Flow":

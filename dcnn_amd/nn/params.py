@@ -85,7 +85,7 @@ class ParamArena:
     def zero_grad(self):
         if self.grad.is_cuda:
             from ..ops import hip
-            hip.zero_(self.grad)  # hipMemsetAsync (a memset node in the step graph)
+            hip.zero_(self.grad)  # the library's zero-fill kernel (no ATen fill in the step graph)
         else:
             self.grad.zero_()
 

@@ -1007,14 +1007,11 @@ def sgd_step(p, g, vel, shadow, lr, momentum, hyper=None):
 
 
 def zero_(t):
-    """Zero a dense GPU tensor with hipMemsetAsync on the current stream (a memset node inside a
-    captured graph; no ATen fill kernel on the hot path)."""
+    """Zero a dense GPU tensor on the current stream with the library's own fill kernel (no ATen
+    fill on the hot path). Not hipMemsetAsync: captured into a hipGraph, a memset node wrote
+    garbage from its second replay on (ROCm 7.2, tools/dbg/memset_graph.py)."""
     assert t.is_cuda and (t.is_contiguous() or t.is_contiguous(memory_format=CL))
-    if os.environ.get("DCNN_MEMSET", "1") == "0":
-        return t.zero_()
-    from ._ext import kernels as _k
-    _k().rt.memset_async(t.data_ptr(), 0, t.numel() * t.element_size(),
-                         _k().rt.Flow.wrap(t.device.index, stream_ptr(t.device)))
+    kernels().zero_bytes(t.data_ptr(), t.numel() * t.element_size(), stream_ptr(t.device))
     return t
 
 

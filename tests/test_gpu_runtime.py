@@ -93,3 +93,20 @@ def test_training_step_allocation_steady_state():
     assert t1["segment.all.allocated"] == t0["segment.all.allocated"]
     assert t1["reserved_bytes.all.current"] == t0["reserved_bytes.all.current"]
     assert s1["in_use_bytes"] >= 3 * m.arena.numel * 4  # data + grad + Adam moments live in the pool
+
+
+def test_zero_fill_replays_in_graph():
+    """hip.zero_ inside a captured graph zeroes on EVERY replay (a captured hipMemsetAsync node
+    did not on ROCm 7.2: garbage from the second replay on)."""
+    from dcnn_amd.ops import hip
+    for n in (1000, 11_300_000):
+        t = get_gpu(0).allocate(n, torch.float32)
+        s = torch.cuda.Stream()
+        g = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(g, stream=s):
+            hip.zero_(t)
+        for _ in range(3):
+            t.fill_(1.0)
+            g.replay()
+            torch.cuda.synchronize()
+            assert float(t.abs().sum()) == 0.0
