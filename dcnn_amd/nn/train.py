@@ -103,8 +103,9 @@ def _shard(loader):
 
 
 def train_class_epoch(model, train_loader, optimizer, loss_function, config: Optional[TrainingConfig] = None,
-                      step=None) -> tuple:
-    """One epoch; returns (avg loss, accuracy). ``step`` is a prebuilt ``TrainStep``."""
+                      step=None, metrics=None) -> tuple:
+    """One epoch; returns (avg loss, accuracy). ``step`` is a prebuilt ``TrainStep``; ``metrics``
+    a :class:`~dcnn_amd.utils.metrics.MetricsSink` that gets a record per print interval."""
     from ..runtime.step import TrainStep
     config = config or TrainingConfig()
     model.set_training(True)
@@ -135,6 +136,9 @@ def train_class_epoch(model, train_loader, optimizer, loss_function, config: Opt
             l, a = acc.result()
             print(f"Batch ID: {acc.batches}, Batch's Loss: {float(loss):.4f}, Cumulative Accuracy: {a * 100:.2f}%",
                   flush=True)
+            if metrics is not None:
+                metrics.log("batch", batch=acc.batches, loss=float(loss), cumulative_acc=a,
+                            lr=optimizer.get_learning_rate())
         if model.enable_profiling_ and config.profiler_type == ProfilerType.NORMAL:
             model.clear_profiling_data()
         if config.max_batches_per_epoch and acc.batches >= config.max_batches_per_epoch:
@@ -190,9 +194,12 @@ def load_checkpoint(model, optimizer, path: str) -> int:
 
 def train_classification_model(model, train_loader, test_loader, optimizer, loss_function,
                                config: Optional[TrainingConfig] = None, scheduler=None, data_parallel=None,
-                               start_epoch: int = 0) -> list:
+                               start_epoch: int = 0, metrics=None) -> list:
+    """Epoch loop (reference include/nn/train.hpp:191-268). ``metrics``: a MetricsSink (default:
+    one on ``METRICS_FILE`` when set) receiving per-interval and per-epoch JSON records."""
     from ..parallel.dp import DataParallel
     from ..runtime.step import TrainStep
+    from ..utils.metrics import MetricsSink
     config = config or TrainingConfig()
     if not model.initialized:
         model.initialize()
@@ -206,13 +213,16 @@ def train_classification_model(model, train_loader, test_loader, optimizer, loss
         print(f"Training batches: {train_loader.num_batches()}\nValidation batches: {test_loader.num_batches()}")
         model.print_summary([config.batch_size] + train_loader.get_data_shape())
     step = TrainStep(dp, loss_function, optimizer, use_graph=config.use_graph and model.device.is_gpu())
+    if metrics is None and rank == 0:
+        metrics = MetricsSink(tag=model.name())
     best = -math.inf
     history = []
     for epoch in range(start_epoch, config.epochs):
         if rank == 0:
             print(f"Epoch {epoch + 1}/{config.epochs}", flush=True)
         t0 = time.perf_counter()
-        tr_loss, tr_acc = train_class_epoch(model, train_loader, optimizer, loss_function, config, step)
+        tr_loss, tr_acc = train_class_epoch(model, train_loader, optimizer, loss_function, config, step,
+                                            metrics if rank == 0 else None)
         if model.device.is_gpu():
             torch.cuda.synchronize()
         train_ms = (time.perf_counter() - t0) * 1e3
@@ -223,6 +233,8 @@ def train_classification_model(model, train_loader, test_loader, optimizer, loss
         rec = {"epoch": epoch + 1, "train_loss": tr_loss, "train_acc": tr_acc, "val_loss": va_loss, "val_acc": va_acc,
                "train_ms": train_ms, "images_per_sec": n_img / (train_ms / 1e3) if train_ms else 0.0}
         history.append(rec)
+        if rank == 0 and metrics is not None:
+            metrics.log("epoch", lr=optimizer.get_learning_rate(), host_mem_mb=get_memory_usage_kb() // 1024, **rec)
         if rank == 0:
             if va_acc > best:
                 best = va_acc

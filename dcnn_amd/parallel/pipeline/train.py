@@ -14,7 +14,7 @@ from . import messages as M
 
 
 def train_semi_async_epoch(coord, loader, schedule: str = "semi_async", print_interval: int = 0,
-                           max_batches: Optional[int] = None) -> dict:
+                           max_batches: Optional[int] = None, metrics=None) -> dict:
     coord.broadcast(M.CommandType.TRAIN_MODE)
     loader.reset()
     tot_loss, tot_correct, n_samples, n_batches = 0.0, 0, 0, 0
@@ -35,6 +35,9 @@ def train_semi_async_epoch(coord, loader, schedule: str = "semi_async", print_in
         if print_interval and n_batches % print_interval == 0:
             print(f"  batch {n_batches}: loss {loss:.4f} acc {coord.last_correct / x.shape[0]:.4f} "
                   f"({batch_us[-1]:.0f} us)", flush=True)
+            if metrics is not None:
+                metrics.log("pipeline_batch", batch=n_batches, loss=loss, acc=coord.last_correct / x.shape[0],
+                            batch_us=batch_us[-1], schedule=schedule)
         if max_batches and n_batches >= max_batches:
             break
     secs = time.perf_counter() - t_epoch
@@ -65,10 +68,15 @@ def validate_semi_async_epoch(coord, loader, max_batches: Optional[int] = None) 
 
 
 def train_model(coord, train_loader, test_loader=None, epochs: int = 1, schedule: str = "semi_async",
-                scheduler=None, print_interval: int = 0, max_batches: Optional[int] = None) -> list:
+                scheduler=None, print_interval: int = 0, max_batches: Optional[int] = None, metrics=None) -> list:
+    """Epoch loop; ``metrics`` (default: a MetricsSink on ``METRICS_FILE`` when set) gets per-interval
+    and per-epoch JSON records."""
+    from ...utils.metrics import MetricsSink
+    if metrics is None:
+        metrics = MetricsSink(tag="pipeline")
     history = []
     for ep in range(epochs):
-        tr = train_semi_async_epoch(coord, train_loader, schedule, print_interval, max_batches)
+        tr = train_semi_async_epoch(coord, train_loader, schedule, print_interval, max_batches, metrics)
         rec = {"epoch": ep + 1, "train": tr}
         if test_loader is not None:
             rec["val"] = validate_semi_async_epoch(coord, test_loader, max_batches)
@@ -82,4 +90,7 @@ def train_model(coord, train_loader, test_loader=None, epochs: int = 1, schedule
             else:
                 scheduler.step()
         history.append(rec)
+        metrics.log("pipeline_epoch", epoch=ep + 1, schedule=schedule,
+                    **{f"train_{k}": v for k, v in tr.items()},
+                    **({f"val_{k}": v for k, v in rec["val"].items()} if "val" in rec else {}))
     return history

@@ -30,11 +30,15 @@ class NetworkStageWorker:
         self.default_device = device or ("GPU" if use_gpu else "CPU")
 
     def run(self) -> None:
+        from ...utils.metrics import maybe_start_cpu_logger
+        cpu_log = maybe_start_cpu_logger(f"worker-{self.port}")  # CPU_LOG_DIR: tools/plot_cpu_range.py input
         try:
             self.stage.run()
         finally:
             self.stage.transport.flush()
             self.comm.close()
+            if cpu_log is not None:
+                cpu_log.stop()
 
     def start_thread(self):
         return self.stage.start_thread()

@@ -40,6 +40,8 @@ else:
 coord.initialize()
 print("partitions:", coord.partitions)
 coord.deploy_stages()
+from dcnn_amd.utils.metrics import maybe_start_cpu_logger  # noqa: E402
+cpu_log = maybe_start_cpu_logger("coordinator")  # CPU_LOG_DIR=./logs -> tools/plot_cpu_range.py
 coord.start()
 tr.prepare_batches(cfg.batch_size)
 te.prepare_batches(cfg.batch_size)
@@ -48,3 +50,5 @@ train_model(coord, tr, te, epochs=cfg.epochs, schedule="semi_async", print_inter
 for line in coord.print_profiling_on_all_stages():
     pass
 coord.stop()
+if cpu_log is not None:
+    print(f"CPU log: {cpu_log.stop()}")

@@ -39,6 +39,8 @@ else:
                                    port=get_env("COORDINATOR_PORT", 0), **kw)
 coord.initialize()
 coord.deploy_stages()
+from dcnn_amd.utils.metrics import maybe_start_cpu_logger  # noqa: E402
+cpu_log = maybe_start_cpu_logger("coordinator")  # CPU_LOG_DIR=./logs -> tools/plot_cpu_range.py
 coord.start()
 tr.prepare_batches(cfg.batch_size)
 for ep in range(cfg.epochs):
@@ -80,3 +82,5 @@ for ep in range(cfg.epochs):
     print(f"epoch {ep + 1}: val loss {v['loss']:.4f} acc {v['accuracy'] * 100:.2f}%", flush=True)
 coord.print_profiling_on_all_stages()
 coord.stop()
+if cpu_log is not None:
+    print(f"CPU log: {cpu_log.stop()}")
