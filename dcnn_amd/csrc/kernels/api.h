@@ -52,6 +52,9 @@ struct HConvArgs {
   const float* bias; const bf16* residual; float* stats; int relu;
   float* zero_ptr; int zero_n;  // zeroed by workgroup 0 (BN sums accumulated by the next kernel)
   BnbArgs bnb;
+  // fp32 output (split-precision fp32 convs, ops/hip.py): when Cf is set the result (+ the fp32
+  // residual residual_f) is written to Cf as fp32 instead of C as bf16 (no backward-BN fusion)
+  float* Cf; const float* residual_f;
 };
 void hconv(HConvArgs a, hipStream_t s);
 bool hconv_supported(int NB, int H, int W, int Cs, int N, int ntaps);
@@ -63,6 +66,12 @@ struct HWArgs {
   int NB, H, W, Cs, Co, ntaps;
   int tap_dy[9], tap_dx[9];
   int TH, TW, IMG, HPR, tiles_per_split, dbg;  // filled by the launcher
+  // operand pairs (grid.y): pair q reads dY channels [yoff_q, yoff_q + Co) of rows ldy wide and
+  // X channels [xoff_q, xoff_q + Cs) of rows ldx wide, into slabs [q * splits + split]; its bias
+  // partial is the dY column sum if bias_q else 0. One pair with ldy = Co, ldx = Cs is the plain
+  // wgrad; three over [hi|lo|hi] rows are the split-precision fp32 one (ops/hip.py).
+  int ldy, ldx, npairs;
+  int pair_yoff[3], pair_xoff[3], pair_bias[3];
 };
 void hwgrad(HWArgs a, int splits, hipStream_t s);
 bool hwgrad_supported(int NB, int H, int W, int Cs, int Co, int ntaps);
@@ -175,4 +184,7 @@ void grad_pack_bf16(const float* g, bf16* out, long n, float scale, hipStream_t 
 void grad_sum_chunks_bf16(const bf16* src, int w, long ld, long n, bf16* dst, hipStream_t s);
 void grad_unpack_bf16(const bf16* in, float* g, long n, hipStream_t s);
 void zero_bytes(void* p, long nbytes, hipStream_t s);
+// fp32 rows [rows][C] -> bf16 [rows][3C]: pattern 0 = [hi | lo | hi], 1 = [hi | hi | lo]
+// (hi = bf16(x), lo = bf16(x - hi)); a conv over the concatenations sums hi*hi + lo*hi + hi*lo
+void split3_bf16(const float* in, bf16* out, long rows, int C, int pattern, hipStream_t s);
 }  // namespace dcnn

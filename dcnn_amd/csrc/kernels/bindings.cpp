@@ -58,8 +58,10 @@ PYBIND11_MODULE(_kernels, m) {
   m.def("hconv",
         [](uintptr_t A, uintptr_t B, uintptr_t C, unsigned a_bytes, unsigned b_bytes, int NB, int H, int W, int Cs,
            int N, int ldb, std::vector<std::array<int, 3>> taps, uintptr_t bias, uintptr_t residual, uintptr_t stats,
-           int relu, uintptr_t zero_ptr, int zero_n, std::array<uintptr_t, 4> bnb, uintptr_t stream) {
+           int relu, uintptr_t zero_ptr, int zero_n, std::array<uintptr_t, 4> bnb, uintptr_t Cf, uintptr_t residual_f,
+           uintptr_t stream) {
           HConvArgs a{};
+          a.Cf = P<float*>(Cf); a.residual_f = P<const float*>(residual_f);
           a.bnb = BnbArgs{P<const bf16*>(bnb[0]), P<const bf16*>(bnb[1]), P<const float*>(bnb[2]), P<const float*>(bnb[3])};
           a.zero_ptr = P<float*>(zero_ptr); a.zero_n = zero_n;
           a.A = P<const bf16*>(A); a.B = P<const bf16*>(B); a.C = P<bf16*>(C);
@@ -75,8 +77,14 @@ PYBIND11_MODULE(_kernels, m) {
   m.def("hconv_stat_rows", &hconv_stat_rows);
   m.def("hwgrad",
         [](uintptr_t dY, uintptr_t X, uintptr_t slab, uintptr_t bias_slab, unsigned dy_bytes, unsigned x_bytes, int NB,
-           int H, int W, int Cs, int Co, std::vector<std::array<int, 2>> taps, int splits, uintptr_t stream) {
+           int H, int W, int Cs, int Co, std::vector<std::array<int, 2>> taps, int splits, int ldy, int ldx,
+           std::vector<std::array<int, 3>> pairs, uintptr_t stream) {
           HWArgs a{};
+          if (pairs.size() > 3) throw std::runtime_error("hwgrad: at most 3 operand pairs");
+          a.npairs = (int)pairs.size(); a.ldy = ldy; a.ldx = ldx;  // no pairs: the plain wgrad
+          for (size_t q = 0; q < pairs.size(); ++q) {
+            a.pair_yoff[q] = pairs[q][0]; a.pair_xoff[q] = pairs[q][1]; a.pair_bias[q] = pairs[q][2];
+          }
           a.dY = P<const bf16*>(dY); a.X = P<const bf16*>(X); a.slab = P<float*>(slab);
           a.bias_slab = P<float*>(bias_slab);
           a.dy_bytes = dy_bytes; a.x_bytes = x_bytes;
@@ -87,6 +95,9 @@ PYBIND11_MODULE(_kernels, m) {
           hwgrad(a, splits, S(stream));
         });
   m.def("hwgrad_supported", &hwgrad_supported);
+  m.def("split3_bf16", [](uintptr_t in, uintptr_t out, long rows, int C, int pattern, uintptr_t st) {
+    split3_bf16(P<const float*>(in), P<bf16*>(out), rows, C, pattern, S(st));
+  });
   m.def("hwgrad_splits", &hwgrad_splits);
   m.def("gemm_g2f",
         [](uintptr_t A, uintptr_t B, uintptr_t C, unsigned a_bytes, unsigned b_bytes, int M, int N, int Cs, int H,

@@ -91,6 +91,35 @@ void zero_bytes(void* p, long nbytes, hipStream_t s) {
   DCNN_LAUNCH_CHECK();
 }
 
+// fp32 -> [hi | lo | hi] (pattern 0) or [hi | hi | lo] (pattern 1) bf16 rows, 4 channels a thread
+__global__ void split3_kernel(const float* __restrict__ in, bf16* __restrict__ out, long rows, int C, int pattern) {
+  const int c4n = C / 4;
+  const long n = rows * c4n;
+  const long stride = (long)gridDim.x * blockDim.x;
+  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < n; i += stride) {
+    const long r = i / c4n;
+    const int c = (int)(i - r * c4n) * 4;
+    const f32x4 v = *reinterpret_cast<const f32x4*>(in + r * C + c);
+    bf16x4 hi, lo;
+    for (int k = 0; k < 4; ++k) {
+      hi[k] = (bf16)v[k];
+      lo[k] = (bf16)(v[k] - (float)hi[k]);
+    }
+    bf16* o = out + r * 3 * C + c;
+    *reinterpret_cast<bf16x4*>(o) = hi;
+    *reinterpret_cast<bf16x4*>(o + C) = pattern ? hi : lo;
+    *reinterpret_cast<bf16x4*>(o + 2 * C) = pattern ? lo : hi;
+  }
+}
+
+void split3_bf16(const float* in, bf16* out, long rows, int C, int pattern, hipStream_t s) {
+  if (rows <= 0) return;
+  if (C % 4 || reinterpret_cast<uintptr_t>(in) % 16 || reinterpret_cast<uintptr_t>(out) % 8)
+    throw std::runtime_error("split3_bf16: C % 4 == 0 and aligned buffers only");
+  hipLaunchKernelGGL(split3_kernel, dim3(grid_for(rows * (C / 4), 256)), dim3(256), 0, s, in, out, rows, C, pattern);
+  DCNN_LAUNCH_CHECK();
+}
+
 void grad_pack_bf16(const float* g, bf16* out, long n, float scale, hipStream_t s) {
   if (n <= 0) return;
   hipLaunchKernelGGL(grad_pack_kernel, dim3(stream_grid(n)), dim3(256), 0, s, g, out, n, scale);

@@ -57,13 +57,14 @@ __device__ __forceinline__ int hoff(int row, int ch) { return row * 128 + ((ch ^
 
 // TPS taps per K step (one barrier per step), NHB halo buffers (1 when there is a single
 // 64-channel chunk: nothing to prefetch), NBS weight stages (NBS - 1 steps in flight)
-template <int BM, int BN, int TPS, int NHB, int NBS>
+template <int BM, int BN, int TPS, int NHB, int NBS, bool F32O = false>
 struct HC {
   static constexpr int TM = BM / 32, TN = BN / 32;      // 16x16 subtiles per wave (2x2 waves)
   static constexpr int BTAP = BN * 128;                  // bytes of one tap's weight slice
   static constexpr int BST = TPS * BTAP;                 // bytes per weight stage
   static constexpr int B_INS = BN / 32;                  // glds per wave per tap slice
-  static constexpr int EPI_PITCH = BN * 2 + 16;
+  static constexpr int OB = F32O ? 4 : 2;                // bytes per staged output element
+  static constexpr int EPI_PITCH = BN * OB + 16;
   // dynamic LDS: NHB halo buffers of HALO = 128 * (halo rows padded to 32) bytes, then NBS weight stages
   static int lds_bytes(int halo) {
     const int main = NHB * halo + NBS * BST, epi = BM * EPI_PITCH;
@@ -71,13 +72,23 @@ struct HC {
   }
 };
 
-// Shared epilogue of the halo convs: acc (+bias) -> bf16 tile staged in LDS `smem` (>= BM x
-// EPI_PITCH bytes) -> NHWC rows (+residual, ReLU, backward-BN mask) and the tile's BatchNorm
-// statistics row `tm`. Contains block barriers: every thread of the workgroup must call it.
-template <int BM, int BN>
+// Shared epilogue of the halo convs: acc (+bias) -> bf16 (F32O: fp32) tile staged in LDS `smem`
+// (>= BM x EPI_PITCH bytes) -> NHWC rows (+residual, ReLU, backward-BN mask) and the tile's
+// BatchNorm statistics row `tm`. Contains block barriers: every thread of the workgroup must call it.
+template <bool F32O>
+__device__ __forceinline__ void load_row8(const char* src, float* f) {
+  if (F32O) {
+    const float4 a = *reinterpret_cast<const float4*>(src), b = *reinterpret_cast<const float4*>(src + 16);
+    f[0] = a.x; f[1] = a.y; f[2] = a.z; f[3] = a.w; f[4] = b.x; f[5] = b.y; f[6] = b.z; f[7] = b.w;
+  } else {
+    unpack8(*reinterpret_cast<const uint4*>(src), f);
+  }
+}
+
+template <int BM, int BN, bool F32O>
 __device__ __forceinline__ void hc_epilogue(const HConvArgs& p, f32x4 (&acc)[BM / 32][BN / 32], char* smem, int n0,
                                             int tm, int img0, int y0, int x0) {
-  using T = HC<BM, BN, 1, 1, 2>;
+  using T = HC<BM, BN, 1, 1, 2, F32O>;
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const int wm = wid >> 1, wn = wid & 1;
   // ---- epilogue 1: acc (+bias) -> bf16 LDS tile [BM][BN] ----
@@ -90,7 +101,10 @@ __device__ __forceinline__ void hc_epilogue(const HConvArgs& p, f32x4 (&acc)[BM 
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
         const int row = wm * (BM / 2) + i * 16 + (lane >> 4) * 4 + r;
-        *reinterpret_cast<bf16*>(smem + row * T::EPI_PITCH + col * 2) = (bf16)(acc[i][j][r] + bv);
+        if (F32O)
+          *reinterpret_cast<float*>(smem + row * T::EPI_PITCH + col * 4) = acc[i][j][r] + bv;
+        else
+          *reinterpret_cast<bf16*>(smem + row * T::EPI_PITCH + col * 2) = (bf16)(acc[i][j][r] + bv);
       }
   }
   __syncthreads();
@@ -102,7 +116,7 @@ __device__ __forceinline__ void hc_epilogue(const HConvArgs& p, f32x4 (&acc)[BM 
   float s[8], q[8], mu[8], is[8], pv[8];
 #pragma unroll
   for (int v = 0; v < 8; ++v) s[v] = q[v] = mu[v] = is[v] = pv[v] = 0.f;
-  const bool bnb = p.bnb.x != nullptr;  // backward-BN fusion (api.h BnbArgs)
+  const bool bnb = !F32O && p.bnb.x != nullptr;  // backward-BN fusion (api.h BnbArgs; bf16 output only)
   if (bnb && true) {
 #pragma unroll
     for (int v = 0; v < 8; ++v) { mu[v] = p.bnb.mean[ncol + v]; is[v] = p.bnb.istd[ncol + v]; }
@@ -111,8 +125,9 @@ __device__ __forceinline__ void hc_epilogue(const HConvArgs& p, f32x4 (&acc)[BM 
   // itself) and leave as a (count, mean, M2) triple: no E[x^2] - mean^2 cancellation
   float piv_col = 0.f;
   if (p.stats && !bnb) {
-    unpack8(*reinterpret_cast<const uint4*>(smem + cg * 16), pv);
-    if (tid < BN) piv_col = (float)*reinterpret_cast<const bf16*>(smem + tid * 2);
+    load_row8<F32O>(smem + cg * 8 * T::OB, pv);
+    if (tid < BN)
+      piv_col = F32O ? *reinterpret_cast<const float*>(smem + tid * 4) : (float)*reinterpret_cast<const bf16*>(smem + tid * 2);
   }
   const int tpx = p.TH * p.TW;
   for (int row = r0; row < BM; row += RSTEP) {
@@ -121,10 +136,13 @@ __device__ __forceinline__ void hc_epilogue(const HConvArgs& p, f32x4 (&acc)[BM 
     if (n >= p.NB) continue;
     const long orow = ((long)n * p.H + y0 + r2 / p.TW) * p.W + x0 + r2 % p.TW;
     float f[8];
-    unpack8(*reinterpret_cast<const uint4*>(smem + row * T::EPI_PITCH + cg * 16), f);
-    if (p.residual) {
+    load_row8<F32O>(smem + row * T::EPI_PITCH + cg * 8 * T::OB, f);
+    if (F32O ? p.residual_f != nullptr : p.residual != nullptr) {
       float rr[8];
-      unpack8(*reinterpret_cast<const uint4*>(p.residual + orow * p.N + ncol), rr);
+      if (F32O)
+        load_row8<true>(reinterpret_cast<const char*>(p.residual_f + orow * p.N + ncol), rr);
+      else
+        unpack8(*reinterpret_cast<const uint4*>(p.residual + orow * p.N + ncol), rr);
 #pragma unroll
       for (int v = 0; v < 8; ++v) f[v] += rr[v];
     }
@@ -138,11 +156,19 @@ __device__ __forceinline__ void hc_epilogue(const HConvArgs& p, f32x4 (&acc)[BM 
 #pragma unroll
       for (int v = 0; v < 8; ++v) f[v] = yo[v] > 0.f ? f[v] : 0.f;
     }
-    const uint4 o = pack8(f);
-    *reinterpret_cast<uint4*>(p.C + orow * p.N + ncol) = o;
+    float g[8];
+    if (F32O) {
+      float* dst = p.Cf + orow * p.N + ncol;
+      *reinterpret_cast<float4*>(dst) = make_float4(f[0], f[1], f[2], f[3]);
+      *reinterpret_cast<float4*>(dst + 4) = make_float4(f[4], f[5], f[6], f[7]);
+#pragma unroll
+      for (int v = 0; v < 8; ++v) g[v] = f[v];
+    } else {
+      const uint4 o = pack8(f);
+      *reinterpret_cast<uint4*>(p.C + orow * p.N + ncol) = o;
+      unpack8(o, g);  // statistics of the values actually stored
+    }
     if (p.stats) {
-      float g[8];
-      unpack8(o, g);
       if (bnb) {
         float xv[8];
         unpack8(*reinterpret_cast<const uint4*>(p.bnb.x + orow * p.N + ncol), xv);
@@ -179,9 +205,9 @@ __device__ __forceinline__ void hc_epilogue(const HConvArgs& p, f32x4 (&acc)[BM 
   }
 }
 
-template <int BM, int BN, int TPS, int NHB, int NBS>
+template <int BM, int BN, int TPS, int NHB, int NBS, bool F32O>
 __global__ void __launch_bounds__(256, 1) hconv_kernel(HConvArgs p) {
-  using T = HC<BM, BN, TPS, NHB, NBS>;
+  using T = HC<BM, BN, TPS, NHB, NBS, F32O>;
   static_assert(NBS >= 2 && NBS <= 4 && (NBS == 2 || TPS == 1), "deep weight ring needs 1 tap per step");
   extern __shared__ __attribute__((aligned(16))) char smem[];
   struct { int HALO; } T_rt{p.HPR * 128};
@@ -339,7 +365,7 @@ __global__ void __launch_bounds__(256, 1) hconv_kernel(HConvArgs p) {
     bcur = bcur == NBS - 1 ? 0 : bcur + 1;
   }
 
-  hc_epilogue<BM, BN>(p, acc, smem, n0, tm, img0, y0, x0);
+  hc_epilogue<BM, BN, F32O>(p, acc, smem, n0, tm, img0, y0, x0);
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -385,7 +411,7 @@ int hconv_stat_rows(int NB, int H, int W, int N) {
   return (NB * H * W + bm - 1) / bm;
 }
 
-template <int BM, int BN>
+template <int BM, int BN, bool F32O>
 static void launch_hconv(HConvArgs a, hipStream_t s) {
   if (!hconv_geometry(a.NB, a.H, a.W, BM, &a.TH, &a.TW, &a.IMG)) throw std::runtime_error("hconv: bad geometry");
   const long mt = (long)(a.NB / a.IMG) * (a.H / a.TH) * (a.W / a.TW);
@@ -406,15 +432,15 @@ static void launch_hconv(HConvArgs a, hipStream_t s) {
   // only where the extra stage keeps the workgroups per CU (LDS-bound occupancy: losing one
   // costs more than the deeper prefetch gains, measured 63.4k vs 65.0k img/s on ResNet-18)
   auto wg_per_cu = [&](int nb) {
-    const int main = (multi ? 2 : 1) * a.HPR * 128 + nb * BN * 128, epi = BM * (BN * 2 + 16);
+    const int main = (multi ? 2 : 1) * a.HPR * 128 + nb * BN * 128, epi = BM * (BN * (F32O ? 4 : 2) + 16);
     return 163840 / (main > epi ? main : epi);
   };
   int nbs = (tps == 1 && a.ntaps >= bstages) ? bstages : 2;
   while (nbs > 2 && wg_per_cu(nbs) < wg_per_cu(2)) --nbs;
 #define DCNN_HC(TPS, NHB, NBS)                                                                         \
   {                                                                                                    \
-    auto k = hconv_kernel<BM, BN, TPS, NHB, NBS>;                                                      \
-    const int lds = HC<BM, BN, TPS, NHB, NBS>::lds_bytes(a.HPR * 128);                                 \
+    auto k = hconv_kernel<BM, BN, TPS, NHB, NBS, F32O>;                                                \
+    const int lds = HC<BM, BN, TPS, NHB, NBS, F32O>::lds_bytes(a.HPR * 128);                           \
     DCNN_HIP_CHECK(hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, lds)); \
     hipLaunchKernelGGL(k, dim3(grid), dim3(256), lds, s, a);                                           \
   }
@@ -438,10 +464,17 @@ void hconv(HConvArgs a, hipStream_t s) {
       throw std::runtime_error("hconv: taps must reach at most 1 pixel");
   int bm, bn;
   hconv_pick(a, &bm, &bn);
-  if (bm == 128 && bn == 128) return launch_hconv<128, 128>(a, s);
-  if (bm == 128 && bn == 64) return launch_hconv<128, 64>(a, s);
-  if (bm == 64 && bn == 128) return launch_hconv<64, 128>(a, s);
-  return launch_hconv<64, 64>(a, s);
+  if (a.Cf) {
+    if (a.bnb.x) throw std::runtime_error("hconv: no backward-BN fusion with fp32 output");
+    if (bm == 128 && bn == 128) return launch_hconv<128, 128, true>(a, s);
+    if (bm == 128 && bn == 64) return launch_hconv<128, 64, true>(a, s);
+    if (bm == 64 && bn == 128) return launch_hconv<64, 128, true>(a, s);
+    return launch_hconv<64, 64, true>(a, s);
+  }
+  if (bm == 128 && bn == 128) return launch_hconv<128, 128, false>(a, s);
+  if (bm == 128 && bn == 64) return launch_hconv<128, 64, false>(a, s);
+  if (bm == 64 && bn == 128) return launch_hconv<64, 128, false>(a, s);
+  return launch_hconv<64, 64, false>(a, s);
 }
 
 }  // namespace dcnn

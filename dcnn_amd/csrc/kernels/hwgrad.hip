@@ -73,6 +73,8 @@ __global__ void __launch_bounds__(256, 1) hwgrad_kernel(HWArgs p) {
   const int per_split = co_tiles * ci_chunks;
   const int lt = xcd_remap_w(blockIdx.x, gridDim.x);
   const int split = lt / per_split, rem = lt - split * per_split;
+  const int pair = blockIdx.y, nsplits = gridDim.x / per_split;
+  const int yoff = p.pair_yoff[pair], xoff = p.pair_xoff[pair];
   const int co0 = (rem / ci_chunks) * 64, c0 = (rem % ci_chunks) * 64;
 
   const int tx_tiles = p.W / TW, ty_tiles = p.H / TH, tpi = tx_tiles * ty_tiles;
@@ -93,7 +95,7 @@ __global__ void __launch_bounds__(256, 1) hwgrad_kernel(HWArgs p) {
     const int row = (wid * 4 + i) * 8 + (lane >> 3);
     const int im = row / TPX, r2 = row - im * TPX;
     y_rel[i] = (unsigned)((im * p.H + r2 / TW) * p.W + r2 % TW);
-    y_col[i] = (unsigned)((co0 + ((slot ^ wswz(row)) * 8)) * 2);
+    y_col[i] = (unsigned)((yoff + co0 + ((slot ^ wswz(row)) * 8)) * 2);
   }
   // ---- halo loader: row (im, hy, hx) of each lane fixed; only the validity test and a
   //      uniform base move with the tile (6 VALU per 16-byte load) ----
@@ -106,7 +108,7 @@ __global__ void __launch_bounds__(256, 1) hwgrad_kernel(HWArgs p) {
     const bool real = row < HP;
     h_hy[j] = real ? hy : -(1 << 20);  // padding rows of the buffer: never valid
     h_hx[j] = hx;
-    h_rel[j] = ((im * p.H + hy) * p.W + hx) * p.Cs * 2 + (c0 + ((slot ^ wswz(row)) * 8)) * 2;
+    h_rel[j] = ((im * p.H + hy) * p.W + hx) * p.ldx * 2 + (xoff + c0 + ((slot ^ wswz(row)) * 8)) * 2;
   }
   auto load_tile = [&](int buf, int tile) {
     char* Ys = smem + buf * STAGE;
@@ -116,8 +118,8 @@ __global__ void __launch_bounds__(256, 1) hwgrad_kernel(HWArgs p) {
     const int g0 = (ig * IMG * p.H + y0) * p.W + x0;  // tile origin pixel
 #pragma unroll
     for (int i = 0; i < 4; ++i)
-      glds16w(rsY, Ys + (wid * 4 + i) * 1024, (unsigned)(g0 + y_rel[i]) * (unsigned)(p.Co * 2) + y_col[i]);
-    const int gx = g0 * p.Cs * 2;
+      glds16w(rsY, Ys + (wid * 4 + i) * 1024, (unsigned)(g0 + y_rel[i]) * (unsigned)(p.ldy * 2) + y_col[i]);
+    const int gx = g0 * p.ldx * 2;
 #pragma unroll
     for (int j = 0; j < HNI; ++j) {
       const bool ok = (unsigned)(y0 + h_hy[j]) < (unsigned)p.H && (unsigned)(x0 + h_hx[j]) < (unsigned)p.W;
@@ -217,7 +219,8 @@ __global__ void __launch_bounds__(256, 1) hwgrad_kernel(HWArgs p) {
   // ---- slab[split][co][t*Cs + ci]: taps staged through LDS (pitch 68 floats) so every lane
   //      stores 16 contiguous bytes and each 16-lane group a whole 256-byte row segment ----
   const long Ng = 9l * p.Cs;
-  float* out = p.slab + (long)split * p.Co * Ng;
+  const long slab_idx = (long)pair * nsplits + split;
+  float* out = p.slab + slab_idx * p.Co * Ng;
   float* stg = reinterpret_cast<float*>(smem);
   constexpr int ET = G::EPI_TAPS;
 #pragma unroll
@@ -246,7 +249,9 @@ __global__ void __launch_bounds__(256, 1) hwgrad_kernel(HWArgs p) {
     __syncthreads();
     stg[tid] = bias_acc;
     __syncthreads();
-    if (tid < 64) p.bias_slab[(long)split * p.Co + co0 + tid] = stg[tid] + stg[tid + 64] + stg[tid + 128] + stg[tid + 192];
+    if (tid < 64)
+      p.bias_slab[slab_idx * p.Co + co0 + tid] =
+          p.pair_bias[pair] ? stg[tid] + stg[tid + 64] + stg[tid + 128] + stg[tid + 192] : 0.f;
   }
 }
 
@@ -297,6 +302,17 @@ void hwgrad(HWArgs a, int splits, hipStream_t s) {
     if (a.tap_dy[t] < -1 || a.tap_dy[t] > 1 || a.tap_dx[t] < -1 || a.tap_dx[t] > 1)
       throw std::runtime_error("hwgrad: taps must reach at most 1 pixel");
   if (splits != hwgrad_splits(a.NB, a.H, a.W, a.Cs, a.Co)) throw std::runtime_error("hwgrad: split count mismatch");
+  if (a.npairs == 0) {  // plain wgrad
+    a.npairs = 1; a.ldy = a.Co; a.ldx = a.Cs;
+    a.pair_yoff[0] = a.pair_xoff[0] = 0; a.pair_bias[0] = 1;
+  }
+  if (a.npairs < 1 || a.npairs > 3 || a.ldy % 8 || a.ldx % 8) throw std::runtime_error("hwgrad: bad operand pairs");
+  for (int q = 0; q < a.npairs; ++q)
+    if (a.pair_yoff[q] < 0 || a.pair_yoff[q] + a.Co > a.ldy || a.pair_xoff[q] < 0 || a.pair_xoff[q] + a.Cs > a.ldx ||
+        a.pair_yoff[q] % 8 || a.pair_xoff[q] % 8)
+      throw std::runtime_error("hwgrad: pair channel window outside the rows");
+  if ((long)a.NB * a.H * a.W * (a.ldx > a.ldy ? a.ldx : a.ldy) * 2 >= (1l << 31))
+    throw std::runtime_error("hwgrad: operands exceed 32-bit buffer offsets");
   hw_geometry(a.H, a.W, &a.TH, &a.TW, &a.IMG);
   const int total = (a.NB / a.IMG) * (a.H / a.TH) * (a.W / a.TW);
   a.tiles_per_split = (total + splits - 1) / splits;
@@ -312,7 +328,7 @@ void hwgrad(HWArgs a, int splits, hipStream_t s) {
     auto k = hwgrad_kernel<TW_, TH_, IMG_, NS_>;                                                        \
     const int lds = NS_ * HWGeo<TW_, TH_, IMG_>::STAGE;                                                 \
     DCNN_HIP_CHECK(hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, lds)); \
-    hipLaunchKernelGGL(k, dim3(grid), dim3(256), lds, s, a);                                            \
+    hipLaunchKernelGGL(k, dim3(grid, a.npairs), dim3(256), lds, s, a);                                  \
     DCNN_LAUNCH_CHECK();                                                                                \
     return;                                                                                             \
   }

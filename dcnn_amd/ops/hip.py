@@ -74,6 +74,52 @@ def _g2_ok(Cs, N):
 _HCONV = os.environ.get("DCNN_HCONV", "1") != "0"
 _HWGRAD = os.environ.get("DCNN_HWGRAD", "1") != "0"
 
+# ---- split-precision fp32 convolutions on the bf16 halo kernels
+# An fp32 operand x is split once into bf16 hi = bf16(x), lo = bf16(x - hi). A conv sums over
+# input channels, so concatenating channels computes the three significant partial products in
+# ONE bf16 MFMA conv with fp32 accumulation:  X3 = [xh | xl | xh], W3 = [wh | wh | wl] (per tap)
+# gives sum xh*wh + xl*wh + xh*wl = x*w up to the dropped xl*wl (~2^-16 relative). The fp32 3x3
+# stride-1 convs (forward and dgrad) therefore run on hconv (3x the channels, fp32 epilogue), and
+# their weight gradients on hwgrad with three (dY, X) channel windows of the same split rows:
+# (dyh, xh), (dyh, xl), (dyl, xh). Other fp32 convs keep the exact f32-MFMA gathered GEMMs.
+_F32_CONCAT = os.environ.get("DCNN_F32_CONCAT", "1") != "0"
+
+
+def set_f32_concat(on: bool) -> None:
+    """Route eligible fp32 convs through the split-precision halo kernels (True) or the exact
+    f32-MFMA gathered GEMMs (False)."""
+    global _F32_CONCAT
+    _F32_CONCAT = bool(on)
+
+
+def get_f32_concat() -> bool:
+    return _F32_CONCAT
+
+
+def split3_rows(t, rows, C, pattern, out=None):
+    """fp32 [rows][C] (dense) -> bf16 [rows][3C]: pattern 0 [hi|lo|hi], 1 [hi|hi|lo]."""
+    if out is None:
+        out = torch.empty((rows, 3 * C), dtype=BF16, device=t.device)
+    kernels().split3_bf16(t.data_ptr(), out.data_ptr(), rows, C, pattern, stream_ptr())
+    return out
+
+
+def act_split3(t):
+    """[xh | xl | xh] channel concatenation of an fp32 NHWC activation (N, 3C, H, W) channels_last
+    bf16; cached on the tensor (a conv's forward split serves its weight gradient too)."""
+    s = getattr(t, "_s3", None)
+    if s is None:
+        N, C, H, W = t.shape
+        assert t.dtype == F32 and t.is_contiguous(memory_format=CL)
+        s = torch.empty((N, 3 * C, H, W), dtype=BF16, device=t.device, memory_format=CL)
+        split3_rows(t, N * H * W, C, 0, out=s)
+        t._s3 = s
+    return s
+
+
+def _f32_concat_ok(C, Co):
+    return _F32_CONCAT and C % 64 == 0 and Co % 64 == 0
+
 
 def _hconv_ok(N, OH, OW, H, W, sh, sw, Cs, Co, taps, wop):
     """Halo-tiled direct conv applies to stride-1 'same' convs with a 1-pixel reach (3x3/pad 1
@@ -110,6 +156,21 @@ def conv2d_fwd(x, w, bias, stride, pad, *, stats=False, residual=None, relu=Fals
     M = N * OH * OW
     if residual is not None:
         assert tuple(residual.shape) == (N, Co, OH, OW) and residual.is_contiguous(memory_format=CL)
+    if x.dtype == F32 and _f32_concat_ok(Ci, Co) and _hconv_ok(N, OH, OW, H, W, sh, sw, 3 * Ci, Co,
+                                                                 _fwd_taps(3 * Ci, W, KH, KW, ph, pw), w):
+        # split-precision fp32 on the bf16 halo conv (see _F32_CONCAT)
+        xs = act_split3(x)
+        ws = split3_rows(w, Co * KH * KW, Ci, 1)
+        y = torch.empty((N, Co, OH, OW), dtype=F32, device=x.device, memory_format=CL)
+        slab, rows, sums = None, 0, None
+        if stats:
+            rows = K.hconv_stat_rows(N, H, W, Co)
+            slab = torch.empty((rows, 3, Co), dtype=F32, device=x.device)
+            sums = torch.empty((2 * Co,), dtype=F32, device=x.device)  # zeroed in-kernel
+        K.hconv(xs.data_ptr(), ws.data_ptr(), 0, _nbytes(xs), _nbytes(ws), N, H, W, 3 * Ci, Co, KH * KW * 3 * Ci,
+                [(t[0], t[1], t[3]) for t in _fwd_taps(3 * Ci, W, KH, KW, ph, pw)], ptr(bias), 0, ptr(slab),
+                int(relu), ptr(sums), 2 * Co if stats else 0, _NOBNB, y.data_ptr(), ptr(residual), stream_ptr())
+        return y, ((slab, rows, sums) if stats else None)
     if x.dtype == F32:  # fp32 compute path: MFMA f32 16x16x4 gathered GEMM
         y = torch.empty((N, Co, OH, OW), dtype=F32, device=x.device, memory_format=CL)
         slab, rows, sums = None, 0, None
@@ -131,7 +192,7 @@ def conv2d_fwd(x, w, bias, stride, pad, *, stats=False, residual=None, relu=Fals
             sums = torch.empty((2 * Co,), dtype=F32, device=x.device)  # zeroed in-kernel
         K.hconv(x.data_ptr(), w.data_ptr(), y.data_ptr(), _nbytes(x), _nbytes(w), N, H, W, Ci, Co, KH * KW * Ci,
                 [(t[0], t[1], t[3]) for t in taps], ptr(bias), ptr(residual), ptr(slab), int(relu), ptr(sums),
-                2 * Co if stats else 0, _NOBNB, stream_ptr())
+                2 * Co if stats else 0, _NOBNB, 0, 0, stream_ptr())
         return y, ((slab, rows, sums) if stats else None)
     if _g2_ok(Ci, Co) and not out_fp32:
         y = torch.empty((N, Co, OH, OW), dtype=BF16, device=x.device, memory_format=CL)
@@ -327,6 +388,15 @@ def conv2d_dgrad(dy, wt, x_shape, stride, pad, *, residual=None, bnb=None):
     else:
         dx = torch.empty((N, Ci, H, W), dtype=odt, device=dy.device, memory_format=CL)
     st = stream_ptr()
+    if (f32 and len(classes) == 1 and not empty_class and _f32_concat_ok(Co, Ci)
+            and _hconv_ok(N, H, W, OH, OW, sh, sw, 3 * Co, Ci, classes[0][4], wt)):
+        # split-precision fp32 dgrad on the bf16 halo conv (see _F32_CONCAT)
+        dys = act_split3(dy)
+        wts = split3_rows(wt, Ci * KH * KW, Co, 1)
+        K.hconv(dys.data_ptr(), wts.data_ptr(), 0, _nbytes(dys), _nbytes(wts), N, OH, OW, 3 * Co, Ci,
+                KH * KW * 3 * Co, [(t[0], t[1], 3 * t[3]) for t in classes[0][4]], 0, 0, 0, 0, 0, 0, _NOBNB,
+                dx.data_ptr(), ptr(residual), st)
+        return dx
     g2 = K.gemm_g2f if f32 else K.gemm_g2
     fuse = (bnb is not None and _BNB and not bnb.pooled and not f32 and not empty_class and bnb.x.dtype == BF16
             and tuple(bnb.x.shape) == (N, Ci, H, W))
@@ -340,7 +410,7 @@ def conv2d_dgrad(dy, wt, x_shape, stride, pad, *, residual=None, bnb=None):
             sums = torch.empty((2 * Ci,), dtype=F32, device=dy.device)  # zeroed in-kernel
         K.hconv(dy.data_ptr(), wt.data_ptr(), dx.data_ptr(), _nbytes(dy), _nbytes(wt), N, OH, OW, Co, Ci, KH * KW * Co,
                 [(t[0], t[1], t[3]) for t in classes[0][4]], 0, ptr(residual), ptr(slab), 0, ptr(sums),
-                2 * Ci if fuse else 0, bnb.args() if fuse else _NOBNB, st)
+                2 * Ci if fuse else 0, bnb.args() if fuse else _NOBNB, 0, 0, st)
         if fuse:
             dx._bnb = (bnb.bn, slab, rows, sums)
         return dx
@@ -522,6 +592,22 @@ def conv2d_wgrad(dy, x, w_shape, stride, pad, grad_w, grad_b=None):
     OH, OW = dy.shape[2], dy.shape[3]
     P = N * OH * OW
     st = stream_ptr()
+    taps = [(ky - pad[0], kx - pad[1]) for ky in range(KH) for kx in range(KW)]
+    hw_ok = (Cx == Ci and _HWGRAD and tuple(stride) == (1, 1) and (OH, OW) == (H, W)
+             and 1 < len(taps) <= 9 and all(abs(a) <= 1 and abs(b) <= 1 for a, b in taps)
+             and K.hwgrad_supported(N, H, W, Ci, Co, len(taps)))
+    if dy.dtype == F32 and hw_ok and _f32_concat_ok(Ci, Co):
+        # split-precision fp32 on the halo wgrad: three (dY, X) channel windows of the split rows
+        # (dyh, xh), (dyh, xl), (dyl, xh); the bias partial is sum(dyh) + sum(dyl)
+        dys, xs = act_split3(dy), act_split3(x)
+        Ng = KH * KW * Ci
+        splits = K.hwgrad_splits(N, H, W, Ci, Co)
+        slab = torch.empty((3 * splits, Co, Ng), dtype=F32, device=x.device)
+        bslab = torch.empty((3 * splits, Co), dtype=F32, device=x.device) if grad_b is not None else None
+        K.hwgrad(dys.data_ptr(), xs.data_ptr(), slab.data_ptr(), ptr(bslab), _nbytes(dys), _nbytes(xs), N, H, W, Ci,
+                 Co, taps, splits, 3 * Co, 3 * Ci, [(0, 0, 1), (0, Ci, 0), (Co, 0, 1)], st)
+        _reduce_wb(K, slab, grad_w, Co * Ng, bslab, grad_b, Co, 3 * splits, st)
+        return
     if dy.dtype == F32:
         assert x.dtype == F32 and Cx == Ci
         Ng = KH * KW * Ci
@@ -534,17 +620,14 @@ def conv2d_wgrad(dy, x, w_shape, stride, pad, grad_w, grad_b=None):
         assert grad_w.is_contiguous(memory_format=CL) or KH * KW == 1 or Ci == 1
         _reduce_wb(K, slab, grad_w, Co * Ng, bslab, grad_b, Co, splits, st)
         return
-    taps = [(ky - pad[0], kx - pad[1]) for ky in range(KH) for kx in range(KW)]
-    if (Cx == Ci and _HWGRAD and tuple(stride) == (1, 1) and (OH, OW) == (H, W)
-            and 1 < len(taps) <= 9 and all(abs(a) <= 1 and abs(b) <= 1 for a, b in taps)
-            and K.hwgrad_supported(N, H, W, Ci, Co, len(taps))):
+    if hw_ok:
         # halo-tiled wgrad: X read ~1.4x instead of once per tap
         Ng = KH * KW * Ci
         splits = K.hwgrad_splits(N, H, W, Ci, Co)
         slab = torch.empty((splits, Co, Ng), dtype=F32, device=x.device)
         bslab = torch.empty((splits, Co), dtype=F32, device=x.device) if grad_b is not None else None
         K.hwgrad(dy.data_ptr(), x.data_ptr(), slab.data_ptr(), ptr(bslab), _nbytes(dy), _nbytes(x), N, H, W, Ci, Co,
-                 taps, splits, st)
+                 taps, splits, Co, Ci, [], st)
         _reduce_wb(K, slab, grad_w, Co * Ng, bslab, grad_b, Co, splits, st)
         return
     if _g2_ok(Cx, Co) and P < (1 << 24):

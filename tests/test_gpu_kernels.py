@@ -484,18 +484,25 @@ def test_dropout_regenerates_mask(hip):
 
 
 # ------------------------------------------------------------------ fp32 compute path (MFMA f32)
-F32_CASES = CONV_CASES + [(2, 3, 32, 32, 64, 3, 1, 1), (2, 6, 9, 9, 10, 3, 2, 1), (1, 5, 7, 7, 7, 1, 1, 0)]
+F32_CASES = CONV_CASES + [(2, 3, 32, 32, 64, 3, 1, 1), (2, 6, 9, 9, 10, 3, 2, 1), (1, 5, 7, 7, 7, 1, 1, 0),
+                          (4, 64, 16, 16, 64, 3, 1, 1), (2, 128, 8, 8, 64, 3, 1, 1), (8, 64, 4, 4, 128, 3, 1, 1),
+                          (2, 64, 32, 32, 128, 3, 1, 1)]
 
 
-@pytest.fixture(params=[0, 1], ids=["f32exact", "f32split"])
+@pytest.fixture(params=["exact", "split", "concat"], ids=["f32exact", "f32split", "f32concat"])
 def f32mode(request):
-    """fp32 GEMMs: 0 = exact v_mfma_f32_16x16x4_f32 (the default), 1 = split-precision 3xbf16."""
+    """fp32 convs/GEMMs: exact v_mfma_f32_16x16x4_f32 gathered GEMMs; their split-precision 3xbf16
+    variant; or (the default) 64-multiple 3x3 stride-1 convs on the bf16 halo kernels over
+    [hi|lo|hi] channel concatenations (ops/hip.py _F32_CONCAT), the rest exact."""
+    from dcnn_amd.ops import hip as H
     from dcnn_amd.ops._ext import kernels
     K = kernels()
-    prev = K.get_f32_mode()
-    K.set_f32_mode(request.param)
+    prev, prev_c = K.get_f32_mode(), H.get_f32_concat()
+    K.set_f32_mode(1 if request.param == "split" else 0)
+    H.set_f32_concat(request.param == "concat")
     yield request.param
     K.set_f32_mode(prev)
+    H.set_f32_concat(prev_c)
 
 
 @pytest.mark.parametrize("case", F32_CASES)
@@ -512,6 +519,9 @@ def test_conv_fp32_fwd_dgrad_wgrad(hip, case, f32mode):
                                 residual=r.cuda().contiguous(memory_format=CL), relu=True)
     y_ref = torch.relu(F.conv2d(x, w, b, s, p) + r)
     assert y.dtype == torch.float32
+    concat = (f32mode == "concat" and Ci % 64 == 0 and Co % 64 == 0 and k == 3 and s == 1 and p == 1
+              and hip.kernels().hconv_supported(N, H, W, 3 * Ci, Co, 9))
+    assert hasattr(xg, "_s3") == concat  # the split-precision halo path ran exactly when eligible
     assert rel_err(y, y_ref) < 1e-5, rel_err(y, y_ref)
     stats = hip.bn_stats(y, partial)  # (mean, biased variance)
     assert rel_err(stats[:Co], y_ref.double().mean((0, 2, 3))) < 1e-5
@@ -606,24 +616,40 @@ def test_stat_reduce_many_rows_deterministic(hip):
 
 
 def test_fp32_split_precision_error_bound(hip):
-    """The 3xbf16 split GEMM against an fp64 reference on a deep reduction (K = 4608, the
-    ResNet layer-4 conv): relative error <= 1e-5 in norm and close to the exact f32 MFMA's."""
+    """The 3xbf16 split GEMM and the split-precision halo conv ([hi|lo|hi] channel concatenation)
+    against an fp64 reference on a deep reduction (K = 4608, the ResNet layer-4 conv): relative
+    error <= 1e-5 in norm and close to the exact f32 MFMA's."""
     from dcnn_amd.ops._ext import kernels
     K = kernels()
-    prev = K.get_f32_mode()
+    prev, prev_c = K.get_f32_mode(), hip.get_f32_concat()
     torch.manual_seed(7)
     x = torch.randn(8, 512, 8, 8)
     w = torch.randn(256, 512, 3, 3) / math.sqrt(512 * 9)
     ref = F.conv2d(x.double(), w.double(), None, 1, 1)
     errs = {}
     try:
-        for mode in (0, 1):
-            K.set_f32_mode(mode)
+        for mode in ("exact", "split", "concat"):
+            K.set_f32_mode(1 if mode == "split" else 0)
+            hip.set_f32_concat(mode == "concat")
             y, _ = hip.conv2d_fwd(x.cuda().contiguous(memory_format=CL), w.cuda().contiguous(memory_format=CL),
                                   None, (1, 1), (1, 1))
             errs[mode] = ((y.double().cpu() - ref).norm() / ref.norm()).item()
     finally:
         K.set_f32_mode(prev)
-    assert errs[1] < 1e-5, errs
-    assert errs[0] < 3e-6, errs
+        hip.set_f32_concat(prev_c)
+    print(errs)
+    assert errs["split"] < 1e-5 and errs["concat"] < 1e-5, errs
+    assert errs["exact"] < 3e-6, errs
 
+
+def test_split3_rows(hip):
+    """fp32 -> [hi|lo|hi] / [hi|hi|lo] bf16 rows: hi is the bf16 rounding, hi + lo within 2^-16."""
+    torch.manual_seed(8)
+    x = (torch.randn(37, 64) * 10).cuda()
+    for pattern in (0, 1):
+        s = hip.split3_rows(x, 37, 64, pattern).float()
+        hi = x.bfloat16().float()
+        lo = s[:, 64:128] if pattern == 0 else s[:, 128:]
+        assert torch.equal(s[:, :64], hi)
+        assert torch.equal(s[:, 128:] if pattern == 0 else s[:, 64:128], hi)
+        assert ((hi + lo - x).abs() <= x.abs() * 2.0 ** -16 + 1e-30).all()

@@ -271,22 +271,26 @@ def test_training_decreases_loss():
     assert last < first * 0.5, (first, last)
 
 
-@pytest.mark.parametrize("f32mode", [0, 1], ids=["exact", "split"])
+@pytest.mark.parametrize("f32mode", ["exact", "split", "concat"])
 @pytest.mark.parametrize("name", ["resnet9_cifar10", "mnist_cnn"])
 def test_fp32_gpu_model_matches_cpu(name, f32mode):
     """fp32 compute path on the GPU (BASELINE config 'CIFAR-10 ResNet-9 fp32'): the forward agrees
     with the fp32 CPU reference (native backend) to 1e-4, input and parameter gradients to a few
-    1e-3 — for the exact f32 MFMA GEMMs (the default) and the opt-in split-precision 3xbf16 GEMMs."""
+    1e-3 — for the exact f32 MFMA GEMMs, their split-precision 3xbf16 variant, and the default
+    split-precision halo convs over [hi|lo|hi] channel concatenations."""
+    from dcnn_amd.ops import hip as H
     from dcnn_amd.ops._ext import kernels
     K = kernels()
-    prev = K.get_f32_mode()
-    K.set_f32_mode(f32mode)
+    prev, prev_c = K.get_f32_mode(), H.get_f32_concat()
+    K.set_f32_mode(1 if f32mode == "split" else 0)
+    H.set_f32_concat(f32mode == "concat")
     try:
         # split precision (~4.5e-6 per GEMM, tests/test_gpu_kernels.py) ends between the exact
         # fp32 path and the bf16 path after the BatchNorm backward chain at batch 8
-        _fp32_model_vs_cpu(name, 3e-3 if f32mode == 0 else 2e-2)
+        _fp32_model_vs_cpu(name, 2e-2 if f32mode == "split" else 3e-3)
     finally:
         K.set_f32_mode(prev)
+        H.set_f32_concat(prev_c)
 
 
 def _fp32_model_vs_cpu(name, dx_tol):
