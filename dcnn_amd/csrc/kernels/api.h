@@ -42,6 +42,8 @@ struct T2Args {
   int k_per_split;
 };
 struct PoolGeom { int N, H, W, C, OH, OW, ph, pw, sh, sw, padh, padw; };
+// NHWC conv geometry of the explicit im2col path (im2col.hip)
+struct ConvGeom { int N, H, W, C, OH, OW, KH, KW, SH, SW, PH, PW; };
 // halo-tiled stride-1 direct conv (hconv.hip): out[NB][H][W][N] = sum_t in[y+dy_t][x+dx_t][:] . B[n][tap_b_t + :]
 struct HConvArgs {
   const bf16* A; const bf16* B; bf16* C;
@@ -55,8 +57,17 @@ struct HConvArgs {
   // fp32 output (split-precision fp32 convs, ops/hip.py): when Cf is set the result (+ the fp32
   // residual residual_f) is written to Cf as fp32 instead of C as bf16 (no backward-BN fusion)
   float* Cf; const float* residual_f;
+  // split-K over 64-channel chunks (small grids): `splits` workgroups per output tile, partial
+  // accumulators in `part` [tiles][splits][BM*BN] fp32, the last arriver on the tile's ticket
+  // word sums them in split order (deterministic) and runs the epilogue; tickets left zeroed
+  int splits; float* part; unsigned* tickets;
 };
 void hconv(HConvArgs a, hipStream_t s);
+// split count hconv() will use for this shape, and its output-tile count (workspace sizing)
+int hconv_splits(int NB, int H, int W, int Cs, int N, int ntaps);
+int hconv_tiles(int NB, int H, int W, int N);
+int hconv_tile_elems(int NB, int H, int W, int N);
+void hconv_set_split_target(int t);  // workgroups the split-K decision aims for (0: never split)
 bool hconv_supported(int NB, int H, int W, int Cs, int N, int ntaps);
 int hconv_stat_rows(int NB, int H, int W, int N);
 // halo-tiled stride-1 weight gradient (hwgrad.hip): slab[split][Co][t*Cs + c] = partial dW
@@ -187,4 +198,9 @@ void zero_bytes(void* p, long nbytes, hipStream_t s);
 // fp32 rows [rows][C] -> bf16 [rows][3C]: pattern 0 = [hi | lo | hi], 1 = [hi | hi | lo]
 // (hi = bf16(x), lo = bf16(x - hi)); a conv over the concatenations sums hi*hi + lo*hi + hi*lo
 void split3_bf16(const float* in, bf16* out, long rows, int C, int pattern, hipStream_t s);
+// explicit im2col conv path (im2col.hip; dt 0 fp32, 1 bf16): col [N*OH*OW][KH*KW*C] tap-major;
+// col2im sums the taps of every input element (+ residual), chan_major: columns ordered (c, ky, kx)
+void im2col_nhwc(int dt, const void* x, void* col, const ConvGeom& g, hipStream_t s);
+void col2im_nhwc(int dt, const void* col, void* x, const void* residual, const ConvGeom& g, int chan_major,
+                 hipStream_t s);
 }  // namespace dcnn

@@ -59,8 +59,9 @@ PYBIND11_MODULE(_kernels, m) {
         [](uintptr_t A, uintptr_t B, uintptr_t C, unsigned a_bytes, unsigned b_bytes, int NB, int H, int W, int Cs,
            int N, int ldb, std::vector<std::array<int, 3>> taps, uintptr_t bias, uintptr_t residual, uintptr_t stats,
            int relu, uintptr_t zero_ptr, int zero_n, std::array<uintptr_t, 4> bnb, uintptr_t Cf, uintptr_t residual_f,
-           uintptr_t stream) {
+           int splits, uintptr_t part, uintptr_t tickets, uintptr_t stream) {
           HConvArgs a{};
+          a.splits = splits; a.part = P<float*>(part); a.tickets = P<unsigned*>(tickets);
           a.Cf = P<float*>(Cf); a.residual_f = P<const float*>(residual_f);
           a.bnb = BnbArgs{P<const bf16*>(bnb[0]), P<const bf16*>(bnb[1]), P<const float*>(bnb[2]), P<const float*>(bnb[3])};
           a.zero_ptr = P<float*>(zero_ptr); a.zero_n = zero_n;
@@ -75,6 +76,10 @@ PYBIND11_MODULE(_kernels, m) {
         });
   m.def("hconv_supported", &hconv_supported);
   m.def("hconv_stat_rows", &hconv_stat_rows);
+  m.def("hconv_splits", &hconv_splits);
+  m.def("hconv_tiles", &hconv_tiles);
+  m.def("hconv_set_split_target", &hconv_set_split_target);
+  m.def("hconv_tile_elems", &hconv_tile_elems);
   m.def("hwgrad",
         [](uintptr_t dY, uintptr_t X, uintptr_t slab, uintptr_t bias_slab, unsigned dy_bytes, unsigned x_bytes, int NB,
            int H, int W, int Cs, int Co, std::vector<std::array<int, 2>> taps, int splits, int ldy, int ldx,
@@ -350,6 +355,15 @@ PYBIND11_MODULE(_kernels, m) {
   });
   m.def("cast_f32_bf16",[](uintptr_t x, uintptr_t y, long n, uintptr_t st) {
     cast_f32_bf16(P<const float*>(x), P<bf16*>(y), n, S(st));
+  });
+  m.def("im2col_nhwc", [](int dt, uintptr_t x, uintptr_t col, int N, int H, int W, int C, int OH, int OW, int KH, int KW,
+                          int SH, int SW, int PH, int PW, uintptr_t st) {
+    im2col_nhwc(dt, P<const void*>(x), P<void*>(col), ConvGeom{N, H, W, C, OH, OW, KH, KW, SH, SW, PH, PW}, S(st));
+  });
+  m.def("col2im_nhwc", [](int dt, uintptr_t col, uintptr_t x, uintptr_t residual, int N, int H, int W, int C, int OH,
+                          int OW, int KH, int KW, int SH, int SW, int PH, int PW, int chan_major, uintptr_t st) {
+    col2im_nhwc(dt, P<const void*>(col), P<void*>(x), P<const void*>(residual),
+                ConvGeom{N, H, W, C, OH, OW, KH, KW, SH, SW, PH, PW}, chan_major, S(st));
   });
   m.def("im2col", [](uintptr_t x, uintptr_t col, int N, int C, int H, int W, int KH, int KW, int SH, int SW, int PH,
                      int PW, int OH, int OW, uintptr_t st) {

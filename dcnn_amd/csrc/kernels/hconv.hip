@@ -214,7 +214,9 @@ __global__ void __launch_bounds__(256, 1) hconv_kernel(HConvArgs p) {
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const int wm = wid >> 1, wn = wid & 1;
   const int tiles_n = p.N / BN;
-  const int lt = xcd_remap_h(blockIdx.x, gridDim.x);
+  const int SPL = p.splits;                      // workgroups per output tile (split-K)
+  const int lt0 = xcd_remap_h(blockIdx.x, gridDim.x);
+  const int zs = lt0 % SPL, lt = lt0 / SPL;      // this workgroup's split, output tile
   const int tm = lt / tiles_n, tn = lt % tiles_n;
   const int n0 = tn * BN;
   // spatial tile tm -> (image group, tile row, tile col)
@@ -300,7 +302,8 @@ __global__ void __launch_bounds__(256, 1) hconv_kernel(HConvArgs p) {
 #pragma unroll
     for (int j = 0; j < T::TN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
-  const int nchunk = p.Cs / 64;
+  const int nchunk = p.Cs / 64 / SPL;          // channel chunks of this split
+  const int cbase = zs * nchunk * 64;          // its first channel
   const int spc = (p.ntaps + TPS - 1) / TPS;  // K steps per channel chunk
   const int nsteps = nchunk * spc;
   // step j's weights live in stage j % NBS; step k + NBS - 1 is issued at the top of step k into
@@ -310,13 +313,13 @@ __global__ void __launch_bounds__(256, 1) hconv_kernel(HConvArgs p) {
   // in the window only makes the wait conservative).
   constexpr int BU = TPS * T::B_INS;  // weight loads per lane per step
   auto step_ct = [&](int j, int* cj, int* tj) { *cj = j / spc; *tj = (j - *cj * spc) * TPS; };
-  load_halo(0, 0);
+  load_halo(0, cbase);
 #pragma unroll
   for (int j = 0; j < NBS - 1; ++j) {
     if (j < nsteps) {
       int cj, tj;
       step_ct(j, &cj, &tj);
-      load_b(j, cj * 64, tj);
+      load_b(j, cbase + cj * 64, tj);
     }
   }
   vm_wait_groups<BU>(min(NBS - 2, nsteps - 1));
@@ -327,9 +330,9 @@ __global__ void __launch_bounds__(256, 1) hconv_kernel(HConvArgs p) {
     if (k + NBS - 1 < nsteps) {
       int cj, tj;
       step_ct(k + NBS - 1, &cj, &tj);
-      load_b(bcur == 0 ? NBS - 1 : bcur - 1, cj * 64, tj);
+      load_b(bcur == 0 ? NBS - 1 : bcur - 1, cbase + cj * 64, tj);
     }
-    if (NHB == 2 && t0 == 0 && c + 1 < nchunk) load_halo((c + 1) & 1, (c + 1) * 64);
+    if (NHB == 2 && t0 == 0 && c + 1 < nchunk) load_halo((c + 1) & 1, cbase + (c + 1) * 64);
     const char* Hs = smem + (NHB == 2 ? (c & 1) : 0) * T_rt.HALO;
 #pragma unroll
     for (int u = 0; u < TPS; ++u) {
@@ -363,6 +366,57 @@ __global__ void __launch_bounds__(256, 1) hconv_kernel(HConvArgs p) {
     vm_wait_groups<BU>(min(NBS - 2, nsteps - 2 - k));
     lds_barrier();
     bcur = bcur == NBS - 1 ? 0 : bcur + 1;
+  }
+
+  if (SPL > 1) {
+    // split-K hand-off without fences (MI355X_MICROARCH "Valid forms" row 1): every partial is
+    // stored with agent-scope (sc1) 8-byte stores, each wave drains them, one lane adds to the
+    // tile's ticket after the workgroup barrier, and the workgroup whose add returns SPL - 1
+    // reads all partials back with sc1 loads and sums them in split order.
+    constexpr int E2 = T::TM * T::TN * 2;  // float2 accumulator pairs per lane
+    unsigned long long* part = reinterpret_cast<unsigned long long*>(p.part) + (size_t)lt * SPL * E2 * 256;
+#pragma unroll
+    for (int i = 0; i < T::TM; ++i)
+#pragma unroll
+      for (int j = 0; j < T::TN; ++j)
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+          const int e2 = (i * T::TN + j) * 2 + h;
+          const unsigned long long bits = (unsigned long long)__float_as_uint(acc[i][j][2 * h]) |
+                                          ((unsigned long long)__float_as_uint(acc[i][j][2 * h + 1]) << 32);
+          __hip_atomic_store(part + ((size_t)zs * E2 + e2) * 256 + tid, bits, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    volatile int* flag = reinterpret_cast<volatile int*>(smem);
+    if (tid == 0) {
+      const unsigned old = __hip_atomic_fetch_add(p.tickets + lt, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      const int last = old == (unsigned)(SPL - 1);
+      if (last) __hip_atomic_store(p.tickets + lt, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      *flag = last;
+    }
+    __syncthreads();
+    const int last = *flag;
+    __syncthreads();  // the epilogue reuses smem
+    if (!last) return;
+#pragma unroll
+    for (int i = 0; i < T::TM; ++i)
+#pragma unroll
+      for (int j = 0; j < T::TN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+    for (int z = 0; z < SPL; ++z) {
+#pragma unroll
+      for (int i = 0; i < T::TM; ++i)
+#pragma unroll
+        for (int j = 0; j < T::TN; ++j)
+#pragma unroll
+          for (int h = 0; h < 2; ++h) {
+            const int e2 = (i * T::TN + j) * 2 + h;
+            const unsigned long long bits =
+                __hip_atomic_load(part + ((size_t)z * E2 + e2) * 256 + tid, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            acc[i][j][2 * h] += __uint_as_float((unsigned)bits);
+            acc[i][j][2 * h + 1] += __uint_as_float((unsigned)(bits >> 32));
+          }
+    }
   }
 
   hc_epilogue<BM, BN, F32O>(p, acc, smem, n0, tm, img0, y0, x0);
@@ -403,6 +457,41 @@ bool hconv_supported(int NB, int H, int W, int Cs, int N, int ntaps) {
   return NB % img == 0;
 }
 
+// target workgroup count of the split-K decision; 0 = never split (DCNN_HCONV_SPLIT)
+static int g_split_target = [] {
+  const char* e = getenv("DCNN_HCONV_SPLIT");
+  return e ? atoi(e) : 512;
+}();
+static int hconv_split_target() { return g_split_target; }
+void hconv_set_split_target(int t) { g_split_target = t < 0 ? 0 : t; }
+
+int hconv_tiles(int NB, int H, int W, int N) {
+  HConvArgs a{};
+  a.NB = NB; a.H = H; a.W = W; a.N = N;
+  int bm, bn;
+  hconv_pick(a, &bm, &bn);
+  return (NB * H * W + bm - 1) / bm * (N / bn);
+}
+
+int hconv_tile_elems(int NB, int H, int W, int N) {
+  HConvArgs a{};
+  a.NB = NB; a.H = H; a.W = W; a.N = N;
+  int bm, bn;
+  hconv_pick(a, &bm, &bn);
+  return bm * bn;
+}
+
+// split-K factor: double while the grid is below the target (about two workgroups per CU), the
+// 64-channel chunks still divide evenly and every split keeps at least 4 taps x chunks of work
+int hconv_splits(int NB, int H, int W, int Cs, int N, int ntaps) {
+  if (!hconv_supported(NB, H, W, Cs, N, ntaps)) return 1;
+  const long tiles = hconv_tiles(NB, H, W, N);
+  const int nchunk = Cs / 64, target = hconv_split_target();
+  int s = 1;
+  while (target > 0 && tiles * s < target && nchunk % (2 * s) == 0 && (nchunk / (2 * s)) * ntaps >= 4) s *= 2;
+  return s;
+}
+
 int hconv_stat_rows(int NB, int H, int W, int N) {
   HConvArgs a{};
   a.NB = NB; a.H = H; a.W = W; a.N = N;
@@ -418,11 +507,16 @@ static void launch_hconv(HConvArgs a, hipStream_t s) {
   const int grid = (int)(mt * (a.N / BN));
   const int hp = a.IMG * (a.TH + 2) * (a.TW + 2);
   a.HPR = ((hp + 31) / 32) * 32;  // halo buffer sized to the tile (LDS decides workgroups per CU)
-  const bool multi = a.Cs > 64;
-  static const int tps = [] {
+  const bool multi = a.Cs / 64 / a.splits > 1;  // >1 channel chunk per workgroup: double-buffered halo
+  // taps per K step. Default: 2 on the 64x64 tiles (small maps, long K: 4x4 layer-4 convs 9%
+  // faster, same workgroups per CU), 1 elsewhere (2 or 3 cost a resident workgroup per CU on the
+  // larger tiles: 20-40% slower, tools/gpu_exp.sh sweep in profiles/experiment_hconv_variants.md)
+  static const int tps_env = [] {
     const char* e = getenv("DCNN_HCONV_TPS");
-    return (e && atoi(e) == 3) ? 3 : 1;  // 3 taps/step: fewer barriers but 1 workgroup/CU (slower)
+    const int v = e ? atoi(e) : 0;
+    return (v >= 1 && v <= 3) ? v : 0;
   }();
+  const int tps = tps_env ? tps_env : ((BM == 64 && BN == 64 && a.ntaps >= 4) ? 2 : 1);
   static const int bstages = [] {
     const char* e = getenv("DCNN_HCONV_BSTAGES");
     const int v = e ? atoi(e) : 3;
@@ -442,10 +536,12 @@ static void launch_hconv(HConvArgs a, hipStream_t s) {
     auto k = hconv_kernel<BM, BN, TPS, NHB, NBS, F32O>;                                                \
     const int lds = HC<BM, BN, TPS, NHB, NBS, F32O>::lds_bytes(a.HPR * 128);                           \
     DCNN_HIP_CHECK(hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, lds)); \
-    hipLaunchKernelGGL(k, dim3(grid), dim3(256), lds, s, a);                                           \
+    hipLaunchKernelGGL(k, dim3(grid * a.splits), dim3(256), lds, s, a);                                \
   }
   if (tps == 3) {
     if (multi) DCNN_HC(3, 2, 2) else DCNN_HC(3, 1, 2)
+  } else if (tps == 2) {
+    if (multi) DCNN_HC(2, 2, 2) else DCNN_HC(2, 1, 2)
   } else if (nbs == 4) {
     if (multi) DCNN_HC(1, 2, 4) else DCNN_HC(1, 1, 4)
   } else if (nbs == 3) {
@@ -462,6 +558,9 @@ void hconv(HConvArgs a, hipStream_t s) {
   for (int t = 0; t < a.ntaps; ++t)
     if (a.tap_dy[t] < -1 || a.tap_dy[t] > 1 || a.tap_dx[t] < -1 || a.tap_dx[t] > 1)
       throw std::runtime_error("hconv: taps must reach at most 1 pixel");
+  if (a.splits < 1) a.splits = 1;
+  if (a.splits != 1 && (a.splits != hconv_splits(a.NB, a.H, a.W, a.Cs, a.N, a.ntaps) || !a.part || !a.tickets))
+    throw std::runtime_error("hconv: split count / workspace mismatch (use hconv_splits)");
   int bm, bn;
   hconv_pick(a, &bm, &bn);
   if (a.Cf) {

@@ -133,6 +133,31 @@ def _hconv_ok(N, OH, OW, H, W, sh, sw, Cs, Co, taps, wop):
     return bool(kernels().hconv_supported(N, H, W, Cs, Co, len(taps)))
 
 
+class _SplitWs:
+    """Workspace of one split-K halo conv launch: kept referenced until the launch is enqueued
+    (stream-ordered caching allocator: later reuse of the block is ordered after the kernel)."""
+    keep = None
+
+
+# split-precision fp32 convs never split: their error budget (~2^-16 per conv) is validated on
+# the unsplit accumulation order, and an ill-conditioned batch-8 BatchNorm backward chain
+# (tests/test_gpu_model.py::test_fp32_gpu_model_matches_cpu) amplifies any order change ~300x
+_NOSPLIT = (1, 0, 0)
+
+
+def _hconv_split(K, NB, H, W, Cs, N, ntaps, device):
+    """(splits, partials pointer, ticket words pointer) for :func:`hconv` (hconv.hip split-K:
+    small grids are split over 64-channel chunks, the last workgroup of a tile sums the partials
+    in split order and runs the epilogue)."""
+    s = K.hconv_splits(NB, H, W, Cs, N, ntaps)
+    if s == 1:
+        return 1, 0, 0
+    tiles = K.hconv_tiles(NB, H, W, N)
+    part = torch.empty(tiles * s * K.hconv_tile_elems(NB, H, W, N), dtype=F32, device=device)
+    _SplitWs.keep = part
+    return s, part.data_ptr(), _ticket(device, tiles * 64, "hconv").data_ptr()
+
+
 def conv2d_fwd(x, w, bias, stride, pad, *, stats=False, residual=None, relu=False, out_fp32=False):
     """y = conv(x, w) + bias  [+ residual] [ReLU]; optional BN partial statistics slab.
 
@@ -141,6 +166,9 @@ def conv2d_fwd(x, w, bias, stride, pad, *, stats=False, residual=None, relu=Fals
     Returns (y, (slab, rows) | None).
     """
     _check_act(x, "conv2d_fwd.x")
+    if (_CONV_ALGO == "im2col" and not out_fp32 and w.dim() == 4 and w.shape[1] == x.shape[1]
+            and _im2col_ok(x.shape[1], w.shape[0])):
+        return conv2d_fwd_im2col(x, w, bias, stride, pad, stats=stats, residual=residual, relu=relu)
     K = kernels()
     N, Ci, H, W = x.shape
     if w.dim() == 4 and w.shape[1] == Ci:
@@ -169,7 +197,8 @@ def conv2d_fwd(x, w, bias, stride, pad, *, stats=False, residual=None, relu=Fals
             sums = torch.empty((2 * Co,), dtype=F32, device=x.device)  # zeroed in-kernel
         K.hconv(xs.data_ptr(), ws.data_ptr(), 0, _nbytes(xs), _nbytes(ws), N, H, W, 3 * Ci, Co, KH * KW * 3 * Ci,
                 [(t[0], t[1], t[3]) for t in _fwd_taps(3 * Ci, W, KH, KW, ph, pw)], ptr(bias), 0, ptr(slab),
-                int(relu), ptr(sums), 2 * Co if stats else 0, _NOBNB, y.data_ptr(), ptr(residual), stream_ptr())
+                int(relu), ptr(sums), 2 * Co if stats else 0, _NOBNB, y.data_ptr(), ptr(residual),
+                *_NOSPLIT, stream_ptr())
         return y, ((slab, rows, sums) if stats else None)
     if x.dtype == F32:  # fp32 compute path: MFMA f32 16x16x4 gathered GEMM
         y = torch.empty((N, Co, OH, OW), dtype=F32, device=x.device, memory_format=CL)
@@ -192,7 +221,8 @@ def conv2d_fwd(x, w, bias, stride, pad, *, stats=False, residual=None, relu=Fals
             sums = torch.empty((2 * Co,), dtype=F32, device=x.device)  # zeroed in-kernel
         K.hconv(x.data_ptr(), w.data_ptr(), y.data_ptr(), _nbytes(x), _nbytes(w), N, H, W, Ci, Co, KH * KW * Ci,
                 [(t[0], t[1], t[3]) for t in taps], ptr(bias), ptr(residual), ptr(slab), int(relu), ptr(sums),
-                2 * Co if stats else 0, _NOBNB, 0, 0, stream_ptr())
+                2 * Co if stats else 0, _NOBNB, 0, 0, *_hconv_split(K, N, H, W, Ci, Co, KH * KW, x.device),
+                stream_ptr())
         return y, ((slab, rows, sums) if stats else None)
     if _g2_ok(Ci, Co) and not out_fp32:
         y = torch.empty((N, Co, OH, OW), dtype=BF16, device=x.device, memory_format=CL)
@@ -306,6 +336,127 @@ def conv_weight_t(w, out=None, dtype=BF16):
     return out
 
 
+# ---- conv algorithm: implicit GEMM / halo kernels (default) or explicit im2col + GEMM
+# (im2col.hip: the reference's lowering, src/nn/layers_impl/cuda/conv2d_ops.cu:78-98). Both run
+# on the same MFMA GEMMs; im2col materialises the [N*OH*OW][KH*KW*C] column matrix in HBM.
+_CONV_ALGO = os.environ.get("DCNN_CONV_ALGO", "implicit")
+if _CONV_ALGO not in ("implicit", "im2col"):
+    raise ValueError(f"DCNN_CONV_ALGO={_CONV_ALGO!r}: expected 'implicit' or 'im2col'")
+
+
+def set_conv_algo(name: str) -> None:
+    """Select the GPU convolution algorithm: ``"implicit"`` (implicit-GEMM / halo kernels) or
+    ``"im2col"`` (explicit column matrix + plain GEMM)."""
+    global _CONV_ALGO
+    if name not in ("implicit", "im2col"):
+        raise ValueError(f"unknown conv algorithm {name!r}")
+    _CONV_ALGO = name
+
+
+def get_conv_algo() -> str:
+    return _CONV_ALGO
+
+
+def _im2col_ok(Ci, Co):
+    return Ci % 8 == 0 and Co % 8 == 0
+
+
+def _geom(N, H, W, C, OH, OW, KH, KW, stride, pad):
+    return (N, H, W, C, OH, OW, KH, KW, stride[0], stride[1], pad[0], pad[1])
+
+
+def im2col_nhwc(x, KH, KW, stride, pad):
+    """(N,C,H,W) channels_last -> column matrix [N*OH*OW][KH*KW*C] (tap-major, zero padding)."""
+    _check_act(x, "im2col_nhwc.x")
+    N, C, H, W = x.shape
+    OH, OW = conv_out_hw(H, W, KH, KW, stride[0], stride[1], pad[0], pad[1])
+    col = torch.empty((N * OH * OW, KH * KW * C), dtype=x.dtype, device=x.device)
+    kernels().im2col_nhwc(dt_code(x.dtype), x.data_ptr(), col.data_ptr(), *_geom(N, H, W, C, OH, OW, KH, KW, stride, pad),
+                          stream_ptr())
+    return col
+
+
+def col2im_nhwc(col, x_shape, KH, KW, stride, pad, *, residual=None, chan_major=False):
+    """Sum the column matrix back onto (N,C,H,W) channels_last (+ residual); ``chan_major``: the
+    columns are ordered (c, ky, kx) instead of (ky, kx, c)."""
+    N, C, H, W = x_shape
+    OH, OW = conv_out_hw(H, W, KH, KW, stride[0], stride[1], pad[0], pad[1])
+    assert tuple(col.shape) == (N * OH * OW, KH * KW * C) and col.is_contiguous()
+    x = torch.empty((N, C, H, W), dtype=col.dtype, device=col.device, memory_format=CL)
+    if residual is not None:
+        assert tuple(residual.shape) == (N, C, H, W) and residual.dtype == col.dtype
+        assert residual.is_contiguous(memory_format=CL)
+    kernels().col2im_nhwc(dt_code(col.dtype), col.data_ptr(), x.data_ptr(), ptr(residual),
+                          *_geom(N, H, W, C, OH, OW, KH, KW, stride, pad), int(chan_major), stream_ptr())
+    return x
+
+
+def conv2d_fwd_im2col(x, w, bias, stride, pad, *, stats=False, residual=None, relu=False):
+    """:func:`conv2d_fwd` by explicit im2col + one plain MFMA GEMM (same fused epilogue: bias,
+    residual, ReLU, BatchNorm partial statistics; same return contract)."""
+    K = kernels()
+    N, Ci, H, W = x.shape
+    Co, _, KH, KW = w.shape
+    assert w.dtype == x.dtype and w.is_contiguous(memory_format=CL)
+    col = im2col_nhwc(x, KH, KW, stride, pad)
+    M, Kc = col.shape
+    OH, OW = conv_out_hw(H, W, KH, KW, stride[0], stride[1], pad[0], pad[1])
+    if residual is not None:
+        assert tuple(residual.shape) == (N, Co, OH, OW) and residual.is_contiguous(memory_format=CL)
+    f32 = x.dtype == F32
+    y = torch.empty((N, Co, OH, OW), dtype=x.dtype, device=x.device, memory_format=CL)
+    slab, rows, sums = None, 0, None
+    if stats:
+        rows = (K.gemm_g2f_stat_rows if f32 else K.gemm_g2_stat_rows)(M, Co)
+        slab = torch.empty((rows, 3, Co), dtype=F32, device=x.device)
+        sums = torch.empty((2 * Co,), dtype=F32, device=x.device)  # zeroed in-kernel
+    (K.gemm_g2f if f32 else K.gemm_g2)(col.data_ptr(), w.data_ptr(), y.data_ptr(), _nbytes(col), _nbytes(w), M, Co,
+                                       Kc, 1, 1, 1, 1, 1, 1, [(0, 0, 0, 0)], Kc, Co, 1, 1, 1, 1, 0, 0, ptr(bias),
+                                       ptr(residual), ptr(slab), int(relu), ptr(sums), 2 * Co if stats else 0, _NOBNB,
+                                       stream_ptr())
+    return y, ((slab, rows, sums) if stats else None)
+
+
+def conv2d_dgrad_im2col(dy, wt, x_shape, stride, pad, *, residual=None):
+    """:func:`conv2d_dgrad` by a plain GEMM into a channel-major column matrix
+    (dy [M][Co] . wt[Ci*KH*KW][Co]^T) and a gather col2im (+ residual)."""
+    K = kernels()
+    N, Ci, H, W = x_shape
+    Ci2, KH, KW, Co = wt.shape
+    assert Ci2 == Ci and dy.shape[1] == Co and wt.dtype == dy.dtype and wt.is_contiguous()
+    M = dy.shape[0] * dy.shape[2] * dy.shape[3]
+    Nc = Ci * KH * KW
+    colg = torch.empty((M, Nc), dtype=dy.dtype, device=dy.device)
+    (K.gemm_g2f if dy.dtype == F32 else K.gemm_g2)(dy.data_ptr(), wt.data_ptr(), colg.data_ptr(), _nbytes(dy),
+                                                   _nbytes(wt), M, Nc, Co, 1, 1, 1, 1, 1, 1, [(0, 0, 0, 0)], Co, Nc,
+                                                   1, 1, 1, 1, 0, 0, 0, 0, 0, 0, 0, 0, _NOBNB, stream_ptr())
+    return col2im_nhwc(colg, x_shape, KH, KW, stride, pad, residual=residual, chan_major=True)
+
+
+def conv2d_wgrad_im2col(dy, x, w_shape, stride, pad, grad_w, grad_b=None):
+    """:func:`conv2d_wgrad` as dW[Co][KH*KW*Ci] = dy^T . im2col(x): split-K MFMA GEMM + slab reduce."""
+    K = kernels()
+    Co, Ci, KH, KW = w_shape
+    col = im2col_nhwc(x, KH, KW, stride, pad)
+    P, Ng = col.shape
+    assert dy.shape[0] * dy.shape[2] * dy.shape[3] == P and dy.shape[1] == Co
+    assert grad_w.is_contiguous(memory_format=CL) or KH * KW == 1 or Ci == 1
+    st = stream_ptr()
+    if dy.dtype == F32:
+        splits = K.gemm_t2f_splits(Co, Ng, P)
+        slab = torch.empty((splits, Co, Ng), dtype=F32, device=x.device)
+        bslab = torch.empty((splits, Co), dtype=F32, device=x.device) if grad_b is not None else None
+        K.gemm_t2f(dy.data_ptr(), col.data_ptr(), slab.data_ptr(), ptr(bslab), Co, Ng, P, Co, Ng, 1, 1, 1, 1, 1, 1,
+                   [(0, 0)], splits, st)
+    else:
+        splits = K.gemm_t2_splits(Co, Ng, P)
+        slab = torch.empty((splits, Co, Ng), dtype=F32, device=x.device)
+        bslab = torch.empty((splits, Co), dtype=F32, device=x.device) if grad_b is not None else None
+        K.gemm_t2(dy.data_ptr(), col.data_ptr(), slab.data_ptr(), ptr(bslab), _nbytes(dy), _nbytes(col), Co, Ng, P,
+                  Co, Ng, 1, 1, 1, 1, 1, 1, [(0, 0)], splits, st)
+    _reduce_wb(K, slab, grad_w, Co * Ng, bslab, grad_b, Co, splits, st)
+
+
 class BnbRequest:
     """Backward-BatchNorm fusion request handed to a gradient producer (api.h ``BnbArgs``).
 
@@ -338,6 +489,8 @@ def conv2d_dgrad(dy, wt, x_shape, stride, pad, *, residual=None, bnb=None):
     statistics into the epilogue (honoured on the bf16 MFMA paths; see ``dx._bnb``).
     """
     _check_act(dy, "conv2d_dgrad.dy")
+    if _CONV_ALGO == "im2col" and _im2col_ok(x_shape[1], dy.shape[1]):
+        return conv2d_dgrad_im2col(dy, wt, x_shape, stride, pad, residual=residual)
     K = kernels()
     N, Ci, H, W = x_shape
     Co, OH, OW = dy.shape[1], dy.shape[2], dy.shape[3]
@@ -395,7 +548,7 @@ def conv2d_dgrad(dy, wt, x_shape, stride, pad, *, residual=None, bnb=None):
         wts = split3_rows(wt, Ci * KH * KW, Co, 1)
         K.hconv(dys.data_ptr(), wts.data_ptr(), 0, _nbytes(dys), _nbytes(wts), N, OH, OW, 3 * Co, Ci,
                 KH * KW * 3 * Co, [(t[0], t[1], 3 * t[3]) for t in classes[0][4]], 0, 0, 0, 0, 0, 0, _NOBNB,
-                dx.data_ptr(), ptr(residual), st)
+                dx.data_ptr(), ptr(residual), *_NOSPLIT, st)
         return dx
     g2 = K.gemm_g2f if f32 else K.gemm_g2
     fuse = (bnb is not None and _BNB and not bnb.pooled and not f32 and not empty_class and bnb.x.dtype == BF16
@@ -410,7 +563,8 @@ def conv2d_dgrad(dy, wt, x_shape, stride, pad, *, residual=None, bnb=None):
             sums = torch.empty((2 * Ci,), dtype=F32, device=dy.device)  # zeroed in-kernel
         K.hconv(dy.data_ptr(), wt.data_ptr(), dx.data_ptr(), _nbytes(dy), _nbytes(wt), N, OH, OW, Co, Ci, KH * KW * Co,
                 [(t[0], t[1], t[3]) for t in classes[0][4]], 0, ptr(residual), ptr(slab), 0, ptr(sums),
-                2 * Ci if fuse else 0, bnb.args() if fuse else _NOBNB, 0, 0, st)
+                2 * Ci if fuse else 0, bnb.args() if fuse else _NOBNB, 0, 0,
+                *_hconv_split(K, N, OH, OW, Co, Ci, len(classes[0][4]), dy.device), st)
         if fuse:
             dx._bnb = (bnb.bn, slab, rows, sums)
         return dx
@@ -586,6 +740,8 @@ def conv2d_wgrad(dy, x, w_shape, stride, pad, grad_w, grad_b=None):
 
     ``x`` may carry zero-padded channels (RGB stem); the padded columns are dropped on reduce.
     """
+    if _CONV_ALGO == "im2col" and x.shape[1] == w_shape[1] and _im2col_ok(w_shape[1], w_shape[0]):
+        return conv2d_wgrad_im2col(dy, x, w_shape, stride, pad, grad_w, grad_b)
     K = kernels()
     N, Cx, H, W = x.shape
     Co, Ci, KH, KW = w_shape
@@ -1092,7 +1248,7 @@ def sgd_step(p, g, vel, shadow, lr, momentum, hyper=None):
 def zero_(t):
     """Zero a dense GPU tensor on the current stream with the library's own fill kernel (no ATen
     fill on the hot path). Not hipMemsetAsync: captured into a hipGraph, a memset node wrote
-    garbage from its second replay on (ROCm 7.2, tools/dbg/memset_graph.py)."""
+    garbage from its second replay on (ROCm 7.2; observed with a capture of two memset nodes)."""
     assert t.is_cuda and (t.is_contiguous() or t.is_contiguous(memory_format=CL))
     kernels().zero_bytes(t.data_ptr(), t.numel() * t.element_size(), stream_ptr(t.device))
     return t

@@ -1,0 +1,137 @@
+"""Explicit im2col + GEMM convolution path (im2col.hip) against the fp32 PyTorch reference and
+against the implicit-GEMM / halo kernels (two independent algorithms on the same shapes)."""
+import math
+
+import pytest
+import torch
+import torch.nn.functional as F
+
+pytestmark = pytest.mark.gpu
+
+CL = torch.channels_last
+
+
+def rel_err(a, b):
+    a = a.float().cpu()
+    b = b.float().cpu()
+    return ((a - b).norm() / (b.norm() + 1e-12)).item()
+
+
+@pytest.fixture(scope="module")
+def hip():
+    from dcnn_amd.ops import hip as h
+    from dcnn_amd.ops._ext import kernels
+    assert kernels().arch == "gfx950"
+    return h
+
+
+CASES = [
+    # N, Ci, H, W, Co, k, s, p
+    (2, 32, 16, 16, 64, 3, 1, 1),
+    (2, 64, 16, 16, 128, 3, 2, 1),
+    (2, 64, 8, 8, 128, 1, 2, 0),
+    (4, 512, 4, 4, 512, 3, 1, 1),
+    (3, 64, 7, 5, 96, 3, 1, 1),
+    (2, 16, 11, 11, 24, 5, 2, 2),
+]
+
+
+def test_im2col_col2im_nhwc_roundtrip(hip):
+    torch.manual_seed(0)
+    x = torch.randn(2, 16, 9, 7)
+    xg = x.cuda().contiguous(memory_format=CL)
+    col = hip.im2col_nhwc(xg, 3, 3, (2, 1), (1, 1))
+    ref = F.unfold(x, 3, padding=1, stride=(2, 1))  # [N][C*9][L], channel-major columns
+    N, CK, L = ref.shape
+    ref_tm = ref.view(N, 16, 9, L).permute(0, 3, 2, 1).reshape(N * L, 9 * 16)  # tap-major rows
+    assert torch.equal(col.cpu(), ref_tm)
+    back = hip.col2im_nhwc(col, x.shape, 3, 3, (2, 1), (1, 1))
+    fold = F.fold(ref, (9, 7), 3, padding=1, stride=(2, 1))
+    assert torch.allclose(back.cpu(), fold, atol=1e-5)
+    colc = ref.permute(0, 2, 1).reshape(N * L, CK).contiguous().cuda()  # channel-major rows
+    back2 = hip.col2im_nhwc(colc, x.shape, 3, 3, (2, 1), (1, 1), chan_major=True)
+    assert torch.allclose(back2.cpu(), fold, atol=1e-5)
+
+
+@pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float32])
+@pytest.mark.parametrize("case", CASES)
+def test_conv_im2col_vs_reference_and_implicit(hip, case, dtype):
+    N, Ci, H, W, Co, k, s, p = case
+    torch.manual_seed(1)
+    x = torch.randn(N, Ci, H, W)
+    w = torch.randn(Co, Ci, k, k) / math.sqrt(Ci * k * k)
+    b = torch.randn(Co)
+    q = (lambda t: t.to(torch.bfloat16).float()) if dtype == torch.bfloat16 else (lambda t: t)
+    tol = 1e-2 if dtype == torch.bfloat16 else 1e-4
+    xq, wq = q(x), q(w)
+    xg = x.cuda().to(dtype).contiguous(memory_format=CL)
+    wg = w.cuda().to(dtype).contiguous(memory_format=CL)
+    r_ref = torch.randn(N, Co, (H + 2 * p - k) // s + 1, (W + 2 * p - k) // s + 1)
+    rg = r_ref.cuda().to(dtype).contiguous(memory_format=CL)
+    y_ref = F.relu(F.conv2d(xq, wq, b, s, p) + q(r_ref))
+    y, part = hip.conv2d_fwd_im2col(xg, wg, b.cuda(), (s, s), (p, p), stats=True, residual=rg, relu=True)
+    assert rel_err(y, y_ref) < tol, rel_err(y, y_ref)
+    st = hip.bn_stats(y, part)
+    yd = y.double()
+    assert rel_err(st[:Co], yd.mean((0, 2, 3))) < 1e-4
+    assert rel_err(st[Co:], yd.var((0, 2, 3), unbiased=False)) < 1e-4
+    # the implicit path gives the same forward result
+    hip.set_conv_algo("implicit")
+    y2, _ = hip.conv2d_fwd(xg, wg, b.cuda(), (s, s), (p, p), residual=rg, relu=True)
+    assert rel_err(y, y2) < tol
+    # dgrad (+ residual)
+    dy = torch.randn_like(y_ref)
+    dyg = dy.cuda().to(dtype).contiguous(memory_format=CL)
+    wt = hip.conv_weight_t(wg, dtype=dtype)
+    res = torch.randn_like(x).cuda().to(dtype).contiguous(memory_format=CL)
+    dx = hip.conv2d_dgrad_im2col(dyg, wt, x.shape, (s, s), (p, p), residual=res)
+    dx_ref = torch.nn.grad.conv2d_input(x.shape, wq, q(dy), s, p) + res.float().cpu()
+    assert rel_err(dx, dx_ref) < tol, rel_err(dx, dx_ref)
+    # wgrad accumulates (beta = 1) + bias gradient
+    gw = torch.ones(Co, Ci, k, k, device="cuda").contiguous(memory_format=CL)
+    gb = torch.ones(Co, device="cuda")
+    hip.conv2d_wgrad_im2col(dyg, xg, w.shape, (s, s), (p, p), gw, gb)
+    dw_ref = torch.nn.grad.conv2d_weight(xq, w.shape, q(dy), s, p) + 1
+    assert rel_err(gw, dw_ref) < tol, rel_err(gw, dw_ref)
+    assert rel_err(gb, q(dy).sum((0, 2, 3)) + 1) < tol
+
+
+def test_model_step_im2col_matches_implicit(hip):
+    """Two fp32 SGD training steps of a small ResNet through each conv algorithm: same losses and
+    parameters. The implicit path runs its exact f32-MFMA kernels here (split-precision halo
+    convs off), so the two algorithms differ only in summation order."""
+    from dcnn_amd.models import create_model
+    from dcnn_amd.nn import SGD, LossFactory
+    from dcnn_amd.runtime.step import TrainStep
+
+    def run(algo):
+        hip.set_conv_algo(algo)
+        concat = hip.get_f32_concat()
+        hip.set_f32_concat(False)
+        try:
+            g = torch.Generator().manual_seed(5)
+            x = torch.randn(8, 3, 32, 32, generator=g).cuda()
+            y = torch.randint(0, 10, (8,), generator=g).cuda()
+            m = create_model("resnet9_cifar10")
+            m.set_seed(9)
+            m.set_device("GPU:0")
+            m.set_compute_dtype(torch.float32)
+            m.initialize()
+            m.set_first_layer_input_grad(False)
+            opt = SGD(0.01, 0.9)
+            opt.attach(m)
+            step = TrainStep(m, LossFactory.create("softmax_crossentropy"), opt, use_graph=False)
+            losses = []
+            for _ in range(2):
+                step(x, y)
+                losses.append(float(step.last_loss.item()))
+            return losses, m.arena.data.cpu().clone()
+        finally:
+            hip.set_conv_algo("implicit")
+            hip.set_f32_concat(concat)
+
+    la, pa = run("implicit")
+    lb, pb = run("im2col")
+    assert abs(la[0] - lb[0]) < 1e-4 * max(1.0, abs(la[0]))
+    assert abs(la[1] - lb[1]) < 1e-3 * max(1.0, abs(la[1]))
+    assert rel_err(pb, pa) < 2e-5, rel_err(pb, pa)

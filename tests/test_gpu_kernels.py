@@ -653,3 +653,73 @@ def test_split3_rows(hip):
         assert torch.equal(s[:, :64], hi)
         assert torch.equal(s[:, 128:] if pattern == 0 else s[:, 64:128], hi)
         assert ((hi + lo - x).abs() <= x.abs() * 2.0 ** -16 + 1e-30).all()
+
+
+@pytest.mark.parametrize("case", [(4, 512, 4, 4, 512), (16, 256, 8, 8, 256), (8, 128, 16, 16, 128)])
+def test_hconv_split_k_matches_unsplit(hip, case):
+    """Split-K halo conv (small grids: partial tiles summed in split order by the last workgroup
+    of each tile) vs the unsplit kernel and the fp32 reference, forward + stats and dgrad;
+    repeated launches are bit-identical (ticket words left zeroed)."""
+    from dcnn_amd.ops._ext import kernels
+    K = kernels()
+    N, C, H, W, Co = case
+    assert K.hconv_splits(N, H, W, C, Co, 9) > 1
+    torch.manual_seed(3)
+    x = torch.randn(N, C, H, W).cuda().to(torch.bfloat16).contiguous(memory_format=CL)
+    w = (torch.randn(Co, C, 3, 3) / math.sqrt(9 * C)).cuda().to(torch.bfloat16).contiguous(memory_format=CL)
+    b = torch.randn(Co).cuda()
+    dy = torch.randn(N, Co, H, W).cuda().to(torch.bfloat16).contiguous(memory_format=CL)
+    wt = hip.conv_weight_t(w)
+    outs = []
+    try:
+        for target in (512, 512, 0):
+            K.hconv_set_split_target(target)
+            y, part = hip.conv2d_fwd(x, w, b, (1, 1), (1, 1), stats=True, relu=True)
+            st = hip.bn_stats(y, part)
+            dx = hip.conv2d_dgrad(dy, wt, x.shape, (1, 1), (1, 1))
+            outs.append((y.clone(), st.clone(), dx.clone()))
+    finally:
+        K.hconv_set_split_target(512)
+    (y1, s1, d1), (y2, s2, d2), (y0, s0, d0) = outs
+    assert torch.equal(y1, y2) and torch.equal(s1, s2) and torch.equal(d1, d2)
+    ref = F.relu(F.conv2d(x.float().cpu(), w.float().cpu(), b.cpu(), 1, 1))
+    assert rel_err(y1, ref) < 1e-2 and rel_err(y0, ref) < 1e-2
+    assert rel_err(y1, y0) < 5e-3 and rel_err(d1, d0) < 5e-3
+    assert rel_err(s1, s0) < 1e-3
+
+
+@pytest.mark.parametrize("case", [(4, 128, 8, 8, 128), (2, 512, 4, 4, 256), (8, 256, 8, 8, 512), (8, 512, 8, 8, 256),
+                                  (8, 256, 8, 8, 256), (8, 128, 16, 16, 128), (8, 128, 16, 16, 256), (8, 512, 4, 4, 512)])
+def test_hconv_fp32_concat_accuracy(hip, case):
+    """fp32 split-precision halo conv (fp32 epilogue) vs fp64 on the ResNet-9 batch-8 shapes,
+    under both split-K targets (the fp32 convs stay unsplit: ops/hip.py _NOSPLIT)."""
+    from dcnn_amd.ops._ext import kernels
+    K = kernels()
+    N, C, H, W, Co = case
+    torch.manual_seed(4)
+    x = torch.randn(N, C, H, W, dtype=torch.float64)
+    w = torch.randn(Co, C, 3, 3, dtype=torch.float64) / math.sqrt(9 * C)
+    ref = F.conv2d(x, w, None, 1, 1)
+    dy = torch.randn(N, Co, H, W, dtype=torch.float64)
+    dref = torch.nn.grad.conv2d_input(x.shape, w, dy, 1, 1)
+    xg = x.float().cuda().contiguous(memory_format=CL)
+    wg = w.float().cuda().contiguous(memory_format=CL)
+    dyg = dy.float().cuda().contiguous(memory_format=CL)
+    wt = hip.conv_weight_t(wg, dtype=torch.float32)
+    res = []
+    try:
+        for target in (512, 0):
+            K.hconv_set_split_target(target)
+            y, _ = hip.conv2d_fwd(xg, wg, None, (1, 1), (1, 1))
+            dx = hip.conv2d_dgrad(dyg, wt, x.shape, (1, 1), (1, 1))
+            res.append((y, dx))
+    finally:
+        K.hconv_set_split_target(512)
+    for y, dx in res:
+        assert rel_err(y.double(), ref) < 2e-5, rel_err(y.double(), ref)
+        assert rel_err(dx.double(), dref) < 2e-5, rel_err(dx.double(), dref)
+    # element-wise: no output of the split kernel further from fp64 than the unsplit one's worst
+    for a, b, r in ((res[0][0], res[1][0], ref), (res[0][1], res[1][1], dref)):
+        ea = (a.double().cpu() - r).abs().max().item()
+        eb = (b.double().cpu() - r).abs().max().item()
+        assert ea < 4 * eb + 1e-7, (ea, eb)
