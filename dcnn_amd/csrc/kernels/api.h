@@ -33,6 +33,12 @@ struct G2Args {
   const float* bias; const bf16* residual; float* stats; int relu;
   float* zero_ptr; int zero_n;  // zeroed by workgroup 0 (BN sums consumed by the next kernel)
   BnbArgs bnb;
+  // grouped launch of up to 4 row classes (the stride phases of a strided dgrad): class c owns
+  // rows [c * cls_rows, (c + 1) * cls_rows) (cls_rows a multiple of the row tile), taps
+  // [cls_t0[c], cls_t0[c] + cls_nt[c]) of the tap arrays and the output phase (cls_ory, cls_orx).
+  // ncls <= 1: the single class (taps 0..ntaps-1, ORY/ORX), filled in by gemm_g2().
+  int ncls, cls_rows;
+  int cls_t0[4], cls_nt[4], cls_ory[4], cls_orx[4];
 };
 struct T2Args {
   const bf16* dY; const bf16* X; float* slab; float* bias_slab;
@@ -91,6 +97,7 @@ int hwgrad_splits(int NB, int H, int W, int Cs, int Co);
 void gemm_nt(const NtArgs& a, hipStream_t s);
 void gemm_g2(const G2Args& a, hipStream_t s);
 int gemm_g2_stat_rows(int M, int N);
+int gemm_g2_row_tile(int M, int N);  // BM the launcher picks for an M x N output
 void gemm_t2(T2Args a, int splits, hipStream_t s);
 int gemm_t2_splits(int M, int N, int P);
 int gemm_nt_stat_rows(int M, int N);

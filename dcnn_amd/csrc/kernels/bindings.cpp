@@ -20,6 +20,34 @@ template <typename T>
 static inline T P(uintptr_t x) { return reinterpret_cast<T>(x); }
 static inline hipStream_t S(uintptr_t x) { return reinterpret_cast<hipStream_t>(x); }
 
+static void bind_gemm_g2(uintptr_t A, uintptr_t B, uintptr_t C, unsigned a_bytes, unsigned b_bytes, int M, int N, int Cs,
+                         int H, int W, int GH, int GW, int SY, int SX, std::vector<std::array<int, 4>> taps, int ldb,
+                         int ldc, int OH, int OW, int OSY, int OSX, int ORY, int ORX, uintptr_t bias, uintptr_t residual,
+                         uintptr_t stats, int relu, uintptr_t zero_ptr, int zero_n, std::array<uintptr_t, 4> bnb,
+                         uintptr_t stream, std::vector<std::array<int, 4>> classes = {}) {
+  G2Args a{};
+  // classes: (first tap, taps, ORY, ORX) per row class of a grouped launch (empty: one class)
+  if (classes.size() > 4) throw std::runtime_error("gemm_g2: at most 4 row classes");
+  a.ncls = (int)classes.size();
+  a.cls_rows = classes.empty() ? 0 : M / (int)classes.size();
+  for (size_t c = 0; c < classes.size(); ++c) {
+    a.cls_t0[c] = classes[c][0]; a.cls_nt[c] = classes[c][1]; a.cls_ory[c] = classes[c][2]; a.cls_orx[c] = classes[c][3];
+  }
+  a.bnb = BnbArgs{P<const bf16*>(bnb[0]), P<const bf16*>(bnb[1]), P<const float*>(bnb[2]), P<const float*>(bnb[3])};
+  a.A = P<const bf16*>(A); a.B = P<const bf16*>(B); a.C = P<bf16*>(C);
+  a.a_bytes = a_bytes; a.b_bytes = b_bytes;
+  a.M = M; a.N = N; a.Cs = Cs; a.H = H; a.W = W; a.GH = GH; a.GW = GW; a.SY = SY; a.SX = SX;
+  if (taps.size() > 64) throw std::runtime_error("gemm_g2: more than 64 taps");
+  a.ntaps = (int)taps.size();
+  for (size_t i = 0; i < taps.size(); ++i) {
+    a.tap_dy[i] = taps[i][0]; a.tap_dx[i] = taps[i][1]; a.tap_srcoff[i] = taps[i][2]; a.tap_b[i] = taps[i][3];
+  }
+  a.ldb = ldb; a.ldc = ldc; a.OH = OH; a.OW = OW; a.OSY = OSY; a.OSX = OSX; a.ORY = ORY; a.ORX = ORX;
+  a.bias = P<const float*>(bias); a.residual = P<const bf16*>(residual); a.stats = P<float*>(stats); a.relu = relu;
+  a.zero_ptr = P<float*>(zero_ptr); a.zero_n = zero_n;
+  gemm_g2(a, S(stream));
+}
+
 PYBIND11_MODULE(_kernels, m) {
   m.doc() = "dcnn_amd HIP/CDNA4 (gfx950) kernel library";
   m.attr("arch") = "gfx950";
@@ -143,27 +171,18 @@ PYBIND11_MODULE(_kernels, m) {
   m.def("conv_weight_transpose_f32", [](uintptr_t w, uintptr_t wt, int Co, int T_, int Ci, uintptr_t st) {
     conv_weight_transpose_f32(P<const float*>(w), P<float*>(wt), Co, T_, Ci, S(st));
   });
-  m.def("gemm_g2",
-        [](uintptr_t A, uintptr_t B, uintptr_t C, unsigned a_bytes, unsigned b_bytes, int M, int N, int Cs, int H,
-           int W, int GH, int GW, int SY, int SX, std::vector<std::array<int, 4>> taps, int ldb, int ldc, int OH,
-           int OW, int OSY, int OSX, int ORY, int ORX, uintptr_t bias, uintptr_t residual, uintptr_t stats, int relu,
-           uintptr_t zero_ptr, int zero_n, std::array<uintptr_t, 4> bnb, uintptr_t stream) {
-          G2Args a{};
-          a.bnb = BnbArgs{P<const bf16*>(bnb[0]), P<const bf16*>(bnb[1]), P<const float*>(bnb[2]), P<const float*>(bnb[3])};
-          a.A = P<const bf16*>(A); a.B = P<const bf16*>(B); a.C = P<bf16*>(C);
-          a.a_bytes = a_bytes; a.b_bytes = b_bytes;
-          a.M = M; a.N = N; a.Cs = Cs; a.H = H; a.W = W; a.GH = GH; a.GW = GW; a.SY = SY; a.SX = SX;
-          if (taps.size() > 64) throw std::runtime_error("gemm_g2: more than 64 taps");
-          a.ntaps = (int)taps.size();
-          for (size_t i = 0; i < taps.size(); ++i) {
-            a.tap_dy[i] = taps[i][0]; a.tap_dx[i] = taps[i][1]; a.tap_srcoff[i] = taps[i][2]; a.tap_b[i] = taps[i][3];
-          }
-          a.ldb = ldb; a.ldc = ldc; a.OH = OH; a.OW = OW; a.OSY = OSY; a.OSX = OSX; a.ORY = ORY; a.ORX = ORX;
-          a.bias = P<const float*>(bias); a.residual = P<const bf16*>(residual); a.stats = P<float*>(stats); a.relu = relu;
-          a.zero_ptr = P<float*>(zero_ptr); a.zero_n = zero_n;
-          gemm_g2(a, S(stream));
-        });
+  m.def("gemm_g2", [](uintptr_t A, uintptr_t B, uintptr_t C, unsigned a_bytes, unsigned b_bytes, int M, int N, int Cs,
+                      int H, int W, int GH, int GW, int SY, int SX, std::vector<std::array<int, 4>> taps, int ldb,
+                      int ldc, int OH, int OW, int OSY, int OSX, int ORY, int ORX, uintptr_t bias, uintptr_t residual,
+                      uintptr_t stats, int relu, uintptr_t zero_ptr, int zero_n, std::array<uintptr_t, 4> bnb,
+                      uintptr_t stream) {
+    bind_gemm_g2(A, B, C, a_bytes, b_bytes, M, N, Cs, H, W, GH, GW, SY, SX, std::move(taps), ldb, ldc, OH, OW, OSY, OSX,
+                 ORY, ORX, bias, residual, stats, relu, zero_ptr, zero_n, bnb, stream, {});
+  });
+  // grouped row classes (strided-dgrad phases in one launch): classes = (first tap, taps, ORY, ORX)
+  m.def("gemm_g2_grouped", &bind_gemm_g2);
   m.def("gemm_g2_stat_rows", &gemm_g2_stat_rows);
+  m.def("gemm_g2_row_tile", &gemm_g2_row_tile);
   m.def("gemm_t2",
         [](uintptr_t dY, uintptr_t X, uintptr_t slab, uintptr_t bias_slab, unsigned a_bytes, unsigned b_bytes, int M,
            int N, int Pn, int ldy, int Cs, int H, int W, int GH, int GW, int SY, int SX,

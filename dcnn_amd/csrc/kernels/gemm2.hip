@@ -67,6 +67,11 @@ __global__ void __launch_bounds__(256, 2) gemm_g2_kernel(G2Args p) {
   const int lt = xcd_remap2(blockIdx.x, gridDim.x);
   const int tm = lt / tiles_n, tn = lt % tiles_n;
   const int m0 = tm * BM, n0 = tn * BN;
+  // row class of this tile (grouped strided-dgrad phases; one class otherwise)
+  const int cls = p.ncls > 1 ? m0 / p.cls_rows : 0;
+  const int mcls = cls * p.cls_rows;                 // first row of the class
+  const int ct0 = p.cls_t0[cls], ntp = p.cls_nt[cls];
+  const int ory = p.cls_ory[cls], orx = p.cls_orx[cls];
 
   const __amdgpu_buffer_rsrc_t rsA = __builtin_amdgcn_make_buffer_rsrc((void*)p.A, (short)0, p.a_bytes, 0x00020000);
   const __amdgpu_buffer_rsrc_t rsB = __builtin_amdgcn_make_buffer_rsrc((void*)p.B, (short)0, p.b_bytes, 0x00020000);
@@ -89,12 +94,13 @@ __global__ void __launch_bounds__(256, 2) gemm_g2_kernel(G2Args p) {
     unsigned base = 0;
     if (m < p.M) {
       const int ghw = p.GH * p.GW;
-      const int img = m / ghw, rem = m - img * ghw;
+      const int ml = m - mcls;
+      const int img = ml / ghw, rem = ml - img * ghw;
       const int gy = rem / p.GW, gx = rem - gy * p.GW;
       const int y0 = gy * p.SY, x0 = gx * p.SX;
       base = (unsigned)((((long)img * p.H + y0) * p.W + x0) * p.Cs * 2);
-      for (int t = 0; t < p.ntaps; ++t) {
-        const int sy = y0 + p.tap_dy[t], sx = x0 + p.tap_dx[t];
+      for (int t = 0; t < ntp; ++t) {
+        const int sy = y0 + p.tap_dy[ct0 + t], sx = x0 + p.tap_dx[ct0 + t];
         if (sy >= 0 && sy < p.H && sx >= 0 && sx < p.W) mask |= (1ull << t);
       }
     }
@@ -124,8 +130,8 @@ __global__ void __launch_bounds__(256, 2) gemm_g2_kernel(G2Args p) {
       int t, c;
       if constexpr (UNI) { t = tU; c = cU + a_lch[i] * 8; }
       else { const int k = k0 + a_lch[i] * 8; t = k / p.Cs; c = k - t * p.Cs; }
-      const bool ok = t < p.ntaps && c < p.Cs && ((a_mask[i] >> t) & 1ull);
-      const unsigned voff = ok ? a_base[i] + (unsigned)(p.tap_srcoff[t] * 2 + c * 2) : kOOB;
+      const bool ok = t < ntp && c < p.Cs && ((a_mask[i] >> t) & 1ull);
+      const unsigned voff = ok ? a_base[i] + (unsigned)(p.tap_srcoff[ct0 + t] * 2 + c * 2) : kOOB;
       glds16(rsA, As + (wid * T::A_INS + i) * 1024, voff);
     }
 #pragma unroll
@@ -133,8 +139,8 @@ __global__ void __launch_bounds__(256, 2) gemm_g2_kernel(G2Args p) {
       int t, c;
       if constexpr (UNI) { t = tU; c = cU + b_lch[i] * 8; }
       else { const int k = k0 + b_lch[i] * 8; t = k / p.Cs; c = k - t * p.Cs; }
-      const bool ok = b_ok[i] && t < p.ntaps && c < p.Cs;
-      const unsigned voff = ok ? b_base[i] + (unsigned)((p.tap_b[t] + c) * 2) : kOOB;
+      const bool ok = b_ok[i] && t < ntp && c < p.Cs;
+      const unsigned voff = ok ? b_base[i] + (unsigned)((p.tap_b[ct0 + t] + c) * 2) : kOOB;
       glds16(rsB, Bs + (wid * T::B_INS + i) * 1024, voff);
     }
   };
@@ -145,7 +151,7 @@ __global__ void __launch_bounds__(256, 2) gemm_g2_kernel(G2Args p) {
 #pragma unroll
     for (int j = 0; j < T::TN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
-  const int K = p.ntaps * p.Cs;
+  const int K = ntp * p.Cs;
   const int nk = (K + BK - 1) / BK;
   auto compute = [&](int buf) {
     const char* As = smem + buf * T::STAGE;
@@ -245,9 +251,10 @@ __global__ void __launch_bounds__(256, 2) gemm_g2_kernel(G2Args p) {
   for (int row = r0; row < BM; row += RSTEP) {
     const int m = m0 + row;
     if (m >= p.M || !col_ok) continue;
-    const int img = m / ghw, rem = m - img * ghw;
+    const int ml = m - mcls;
+    const int img = ml / ghw, rem = ml - img * ghw;
     const int gy = rem / p.GW, gx = rem - gy * p.GW;
-    const long orow = ((long)img * p.OH + gy * p.OSY + p.ORY) * p.OW + gx * p.OSX + p.ORX;
+    const long orow = ((long)img * p.OH + gy * p.OSY + ory) * p.OW + gx * p.OSX + orx;
     float f[8];
     unpack8(*reinterpret_cast<const uint4*>(smem + row * T::EPI_PITCH + cg * 16), f);
     if (p.residual) {
@@ -566,11 +573,28 @@ int gemm_g2_stat_rows(int M, int N) {
   return (M + bm - 1) / bm;
 }
 
-void gemm_g2(const G2Args& a, hipStream_t s) {
+int gemm_g2_row_tile(int M, int N) {
+  int bm, bn;
+  g2_tile(M, N, &bm, &bn);
+  return bm;
+}
+
+void gemm_g2(const G2Args& a_in, hipStream_t s) {
+  G2Args a = a_in;
   if (a.N % 8 != 0 || a.Cs % 8 != 0 || a.ldb % 8 != 0 || a.ldc % 8 != 0 || a.ntaps > 64 || a.ntaps < 1)
     throw std::runtime_error("gemm_g2: unsupported shape (needs N, Cs, ldb, ldc multiples of 8, 1..64 taps)");
   int bm, bn;
   g2_tile(a.M, a.N, &bm, &bn);
+  if (a.ncls <= 1) {
+    a.ncls = 1; a.cls_rows = a.M;
+    a.cls_t0[0] = 0; a.cls_nt[0] = a.ntaps; a.cls_ory[0] = a.ORY; a.cls_orx[0] = a.ORX;
+  } else {
+    if (a.ncls > 4 || a.cls_rows <= 0 || a.cls_rows % bm || a.ncls * a.cls_rows != a.M)
+      throw std::runtime_error("gemm_g2: grouped classes need <= 4 classes of equal rows, a multiple of the row tile");
+    for (int c = 0; c < a.ncls; ++c)
+      if (a.cls_nt[c] < 1 || a.cls_t0[c] < 0 || a.cls_t0[c] + a.cls_nt[c] > a.ntaps)
+        throw std::runtime_error("gemm_g2: class tap range out of bounds");
+  }
   const int bk = (a.Cs % 64 == 0) ? 64 : 32;
   const bool uni = a.Cs % bk == 0;
 #define DCNN_G2(BM, BN, BK, U) if (bm == BM && bn == BN && bk == BK && uni == U) return launch_g2<BM, BN, BK, U>(a, s)

@@ -477,6 +477,7 @@ class BnbRequest:
 
 
 _BNB = os.environ.get("DCNN_BNB_FUSE", "1") != "0"
+_G2_GROUP = os.environ.get("DCNN_G2_GROUP", "1") != "0"  # strided dgrad phases in one launch
 _BNB_POOL = os.environ.get("DCNN_BNB_POOL", "1") != "0"  # the stem max-pool part of the fusion
 
 
@@ -565,6 +566,25 @@ def conv2d_dgrad(dy, wt, x_shape, stride, pad, *, residual=None, bnb=None):
                 [(t[0], t[1], t[3]) for t in classes[0][4]], 0, ptr(residual), ptr(slab), 0, ptr(sums),
                 2 * Ci if fuse else 0, bnb.args() if fuse else _NOBNB, 0, 0,
                 *_hconv_split(K, N, OH, OW, Co, Ci, len(classes[0][4]), dy.device), st)
+        if fuse:
+            dx._bnb = (bnb.bn, slab, rows, sums)
+        return dx
+    if (not f32 and _G2_GROUP and len(classes) > 1 and len({(c[2], c[3]) for c in classes}) == 1
+            and (N * classes[0][2] * classes[0][3]) % 128 == 0):
+        # all stride phases in ONE grouped launch (gemm_g2 row classes): no per-phase launch
+        # boundaries, and the grid covers the whole dgrad instead of a quarter of it
+        GH, GW = classes[0][2], classes[0][3]
+        M = len(classes) * N * GH * GW
+        taps_all, groups = [], []
+        for ry, rx, _, _, taps in classes:
+            groups.append((len(taps_all), len(taps), ry, rx))
+            taps_all += taps
+        rows = K.gemm_g2_stat_rows(M, Ci) if fuse else 0
+        slab = torch.empty((rows, 2, Ci), dtype=F32, device=dy.device) if fuse else None
+        sums = torch.empty((2 * Ci,), dtype=F32, device=dy.device) if fuse else None
+        K.gemm_g2_grouped(dy.data_ptr(), wt.data_ptr(), dx.data_ptr(), _nbytes(dy), _nbytes(wt), M, Ci, Co, OH, OW,
+                          GH, GW, 1, 1, taps_all, KH * KW * Co, Ci, H, W, sh, sw, 0, 0, 0, ptr(residual), ptr(slab), 0,
+                          ptr(sums), 2 * Ci if fuse else 0, bnb.args() if fuse else _NOBNB, st, groups)
         if fuse:
             dx._bnb = (bnb.bn, slab, rows, sums)
         return dx

@@ -52,6 +52,8 @@ class StageConfig:
     ranks: Optional[Dict[str, int]] = None   # torch.distributed ranks: {"prev": r, "next": r, "coordinator": r}
     profiling: bool = True
     use_graph: bool = False                  # GPU: replay per-micro-batch hipGraphs after the first step
+    heartbeat_s: float = 0.0                 # > 0: unsolicited HEALTH_CHECK beats to the coordinator (faults.py)
+    fault: Optional[list] = None             # fault-injection specs (faults.FaultSpec.parse), tests / drills
 
     def to_json(self) -> dict:
         d = dict(self.__dict__)

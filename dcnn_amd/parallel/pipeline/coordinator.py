@@ -38,9 +38,10 @@ from ...nn.loss import Loss, LossFactory
 from ...nn.sequential import Partition, Sequential
 from . import messages as M
 from .config import Endpoint, StageConfig
+from .faults import HEARTBEAT_TEXT
 from .partitioner import CostPartitioner, NaivePartitioner, Partitioner
 from .stage import PipelineStage, flat_state, load_flat_state
-from .transport import LocalTransport, MessageTransport, P2PTransport
+from .transport import MAILBOX, LocalTransport, MessageTransport, P2PTransport
 
 C = M.CommandType
 
@@ -49,12 +50,21 @@ class PipelineError(RuntimeError):
     pass
 
 
+class StageFailure(PipelineError):
+    """A stage stopped responding: missed heartbeats or a lost control-plane connection."""
+
+    def __init__(self, stage: str, why: str):
+        super().__init__(f"{stage}: {why}")
+        self.stage = stage
+
+
 class Coordinator:
     def __init__(self, model: Sequential, optimizer, loss, num_stages: int, num_microbatches: int = 1,
                  partitioner: Optional[Partitioner] = None, input_shape: Optional[Sequence[int]] = None,
                  device: str = "CPU", stage_devices: Optional[Sequence[str]] = None, transport: str = "message",
                  codec: str = "none", grad_scale: str = "mean", seed: Optional[int] = None,
-                 timeout_s: float = 120.0, use_graph: Optional[bool] = None, profiling: bool = True):
+                 timeout_s: float = 120.0, use_graph: Optional[bool] = None, profiling: bool = True,
+                 heartbeat_s: float = 0.0, heartbeat_misses: int = 3):
         self.model = model
         self.optimizer_config = optimizer.get_config() if hasattr(optimizer, "get_config") else dict(optimizer)
         self.loss: Loss = LossFactory.create(loss) if isinstance(loss, str) else loss
@@ -78,6 +88,19 @@ class Coordinator:
         self.transport = None
         self.deployed = False
         self.last_correct = 0
+        # failure detection (faults.py): stage heartbeats every heartbeat_s; a stage silent for
+        # heartbeat_s * heartbeat_misses is declared failed
+        self.heartbeat_s = float(heartbeat_s)
+        self.heartbeat_misses = int(heartbeat_misses)
+        self._last_beat: Dict[str, float] = {}
+        self._stash: Dict[int, list] = {}
+        # recovery: parameter snapshots every snapshot_every steps, re-deploy + reload on failure
+        self.snapshot_every = 0
+        self.max_recoveries = 0
+        self.recoveries = 0
+        self.steps = 0
+        self._snapshot: Optional[List[torch.Tensor]] = None
+        self._snapshot_step = -1
 
     # ------------------------------------------------------------------ topology
     def set_partitioner(self, p: Partitioner) -> None:
@@ -102,7 +125,8 @@ class Coordinator:
                 device=self.stage_devices[i], transport=self.transport_kind, codec=self.codec,
                 seed=None if self.seed is None else self.seed + i, profiling=self.profiling,
                 use_graph=(self.stage_devices[i].upper().startswith("GPU") if self.use_graph is None
-                           else bool(self.use_graph))))
+                           else bool(self.use_graph)),
+                heartbeat_s=self.heartbeat_s))
         self._init_topology()
 
     def _init_topology(self) -> None:
@@ -128,6 +152,8 @@ class Coordinator:
             self.comm.send(M.text_message(self.stage_names[i], C.CONFIG_TRANSFER, self.stage_configs[i].dumps()))
             self.join(C.CONFIG_RECEIVED, 1, self.timeout_s)
         self.deployed = True
+        now = time.time()
+        self._last_beat = {s: now for s in self.stage_names}
 
     def start(self) -> None:
         self.broadcast(C.TRAIN_MODE)
@@ -149,20 +175,51 @@ class Coordinator:
 
     # ------------------------------------------------------------------ messaging
     def _check_errors(self) -> None:
+        """Raise on a stage's ERROR_REPORT / JOB_FAILURE, on missed heartbeats and on a lost
+        control-plane connection (called by every waiting loop)."""
         for kind in (C.ERROR_REPORT, C.JOB_FAILURE):
             if self.comm.count(kind):
                 m = self.comm.recv_command(kind, 0)
                 raise PipelineError(m.text.decode() if m is not None else "stage error")
+        if not self.deployed:
+            return
+        if self.heartbeat_s > 0:
+            while self.comm.count(int(C.HEALTH_CHECK)):
+                m = self.comm.recv_command(int(C.HEALTH_CHECK), 0)
+                if m is None:
+                    break
+                if not self._take_beat(m):
+                    self._stash.setdefault(int(C.HEALTH_CHECK), []).append(m)
+            now = time.time()
+            limit = self.heartbeat_s * self.heartbeat_misses
+            for s in self.stage_names:
+                last = self._last_beat.get(s, now)
+                if now - last > limit:
+                    raise StageFailure(s, f"no heartbeat for {now - last:.1f} s (interval {self.heartbeat_s} s)")
+        self._check_links()
+
+    def _check_links(self) -> None:
+        """Transport-level liveness (network coordinators: a dropped TCP connection)."""
+
+    def _take_beat(self, m) -> bool:
+        if m.command == C.HEALTH_CHECK and bytes(m.text) == HEARTBEAT_TEXT:
+            self._last_beat[m.sender.split("/", 1)[-1]] = time.time()
+            return True
+        return False
 
     def join(self, command, n: int, timeout_s: Optional[float] = None) -> List:
-        """Collect ``n`` messages of ``command`` (raises on stage errors / timeout)."""
+        """Collect ``n`` messages of ``command`` (raises on stage errors / failures / timeout)."""
         deadline = time.time() + (timeout_s or self.timeout_s)
         out = []
+        stash = self._stash.get(int(command))
+        while stash and len(out) < n:
+            out.append(stash.pop(0))
         while len(out) < n:
             self._check_errors()
             m = self.comm.recv_command(int(command), 50)
             if m is not None:
-                out.append(m)
+                if not self._take_beat(m):
+                    out.append(m)
             elif time.time() > deadline:
                 raise PipelineError(f"timeout waiting for {n} x {M.command_name(command)} (got {len(out)})")
         return out
@@ -294,9 +351,63 @@ class Coordinator:
             fn = self.one_f_one_b_process_batch
         else:
             raise ValueError(f"unknown pipeline schedule '{schedule}' (one of {self.SCHEDULES})")
-        loss = fn(xs, ys)
-        self.update_parameters()
-        return loss
+        if self.max_recoveries <= 0:
+            loss = fn(xs, ys)
+            self.update_parameters()
+            self.steps += 1
+            return loss
+        while True:
+            try:
+                if self._snapshot is None:
+                    self.snapshot()
+                loss = fn(xs, ys)
+                self.update_parameters()
+                self.steps += 1
+                if self.steps % self.snapshot_every == 0:
+                    self.snapshot()
+                return loss
+            except PipelineError:
+                if self.recoveries >= self.max_recoveries:
+                    raise
+                self.recover()  # then retry this batch from the last snapshot
+
+    # ------------------------------------------------------------------ recovery
+    def enable_recovery(self, snapshot_every: int = 1, max_recoveries: int = 3) -> None:
+        """Survive stage failures: snapshot every stage's parameters + BN statistics every
+        ``snapshot_every`` steps; on a failed step (stage error, missed heartbeats, lost
+        connection, timeout) re-deploy every stage, reload the last snapshot and retry the batch,
+        at most ``max_recoveries`` times. Optimizer moments restart from zero on recovery."""
+        self.snapshot_every = max(1, int(snapshot_every))
+        self.max_recoveries = int(max_recoveries)
+
+    def snapshot(self) -> None:
+        self._snapshot = self.collect_parameters()
+        self._snapshot_step = self.steps
+
+    def recover(self) -> None:
+        """Restart failed stages, re-deploy the topology and reload the last snapshot."""
+        self.recoveries += 1
+        self.deployed = False
+        for c in self.stage_configs:  # a drill's injected faults fire once (DCNN_FAULT re-arms per deployment)
+            c.fault = None
+        self._restart_stages()
+        self._drain()
+        self.deploy_stages()
+        if self._snapshot is not None:
+            for i, flat in enumerate(self._snapshot):
+                self.comm.send(M.job_message(self.stage_names[i], C.LOAD_PARAMS, 0, flat))
+            self.join(C.PARAMS_LOADED, self.num_stages)
+            self.steps = self._snapshot_step
+        self.start()
+
+    def _restart_stages(self) -> None:
+        """Bring every stage back to an accepting state (subclasses: re-create / re-dial)."""
+
+    def _drain(self) -> None:
+        """Drop every message left over from the failed attempt."""
+        self._stash.clear()
+        while self.comm.recv(0) is not None:
+            pass
 
     def evaluate_batch(self, x: torch.Tensor, y: torch.Tensor):
         """Forward-only pass in eval mode: (mean loss, correct)."""
@@ -450,6 +561,24 @@ class InProcessCoordinator(Coordinator):
     def _cid(self, name):
         return f"{self._tag}/{name}"
 
+    def _restart_stages(self) -> None:
+        """Every stage gets a fresh thread and communicator (a crashed or hung stage's thread is
+        abandoned: its communicator is closed, so it can no longer send)."""
+        comm_mod = M.comm()
+        new = []
+        for s, st in zip(self.stage_names, self.stages):
+            st.stop()
+            st.comm.close()
+            c = comm_mod.InProcessCommunicator(self._cid(s))
+            ns = PipelineStage(c)
+            ns.start_thread()
+            new.append(ns)
+        old, self.stages = self.stages, new
+        for st in old:
+            if st.thread is not None:
+                st.thread.join(timeout=1.0)
+        MAILBOX.purge(self._tag + "/")
+
     def _init_topology(self) -> None:
         comm_mod = M.comm()
         self.comm = comm_mod.InProcessCommunicator(self._cid("coordinator"))
@@ -529,6 +658,18 @@ class DistributedCoordinator(Coordinator):
             self.transport = P2PTransport("coordinator", ranks, self.p2p_groups)
         else:
             self.transport = MessageTransport(self.codec)
+
+    def _check_links(self) -> None:
+        alive = set(self.comm.peers())
+        for s in self.stage_names:
+            if s not in alive:
+                raise StageFailure(s, "control-plane connection lost")
+
+    def _restart_stages(self) -> None:
+        """Re-dial every stage endpoint (the connect loop retries until the worker, restarted by
+        its supervisor, listens again) and send it a fresh configuration."""
+        for i, ep in enumerate(self.stage_endpoints):
+            self.comm.connect(self.stage_names[i], ep.get("host"), int(ep.get("port")), int(self.timeout_s * 1000))
 
     def _endpoint(self, i):
         ep = self.stage_endpoints[i]

@@ -32,6 +32,7 @@ from ...nn.sequential import Sequential, _all_layers
 from ...nn.layers import BatchNorm
 from . import messages as M
 from .config import StageConfig
+from .faults import FaultInjector, FaultSpec, Heartbeat, InjectedFault, env_faults
 from .graphs import StageGraphs
 from .transport import LocalTransport, MessageTransport, P2PTransport
 
@@ -86,6 +87,9 @@ class PipelineStage:
         self.stream: Optional[torch.cuda.Stream] = None
         self.graphs: Optional[StageGraphs] = None
         self.steps_done = 0
+        self.faults = FaultInjector([])
+        self.heartbeat: Optional[Heartbeat] = None
+        self.crashed = False
 
     # ------------------------------------------------------------------ loop
     def run(self, poll_ms: int = 200) -> None:
@@ -103,6 +107,13 @@ class PipelineStage:
 
     def stop(self) -> None:
         self.running = False
+        if self.heartbeat is not None:
+            self.heartbeat.stop()
+
+    def _crash(self) -> None:
+        """Injected crash: the stage goes silent (no reply, no heartbeat, loop exits)."""
+        self.crashed = True
+        self.stop()
 
     def _device(self):
         return self.model.device.torch_device
@@ -135,6 +146,15 @@ class PipelineStage:
     def _process(self, msg) -> None:
         cmd = msg.command
         try:
+            if self.faults:
+                act = self.faults.check(cmd)
+                if act == "drop":
+                    return
+                if act == "crash":
+                    self._crash()
+                    return
+                if act == "raise":
+                    raise InjectedFault(f"{self.id}: injected fault on {M.command_name(cmd)}")
             if cmd == C.FORWARD_JOB:
                 self._forward(msg)
             elif cmd == C.BACKWARD_JOB:
@@ -155,7 +175,7 @@ class PipelineStage:
                 self.model.set_training(False)
             elif cmd == C.SHUTDOWN:
                 self.transport.flush()
-                self.running = False
+                self.stop()
             elif cmd == C.CONFIG_TRANSFER:
                 self._configure(msg.text.decode())
             elif cmd == C.SEND_PARAMS:
@@ -237,6 +257,12 @@ class PipelineStage:
             self.id = cfg.stage_id
         self._connect_peers(cfg)
         self._make_transport(cfg)
+        self.faults = FaultInjector([FaultSpec.parse(f) for f in (cfg.fault or [])] + env_faults(cfg.stage_id))
+        if self.heartbeat is not None:
+            self.heartbeat.stop()
+            self.heartbeat = None
+        if cfg.heartbeat_s and cfg.heartbeat_s > 0:
+            self.heartbeat = Heartbeat(self._send, cfg.heartbeat_s).start()
         self._reply(C.CONFIG_RECEIVED, self.id)
 
     def _connect_peers(self, cfg: StageConfig) -> None:

@@ -52,6 +52,15 @@ class _Mailbox:
                 del self._d[key]
             return t
 
+    def purge(self, target_prefix: str) -> int:
+        """Drop every undelivered tensor addressed to a comm id starting with ``target_prefix``
+        (pipeline recovery: activations of a failed attempt must not be claimed by its retry)."""
+        with self._cv:
+            dead = [k for k in self._d if str(k[0]).startswith(target_prefix)]
+            for k in dead:
+                del self._d[k]
+            return len(dead)
+
 
 MAILBOX = _Mailbox()
 

@@ -723,3 +723,23 @@ def test_hconv_fp32_concat_accuracy(hip, case):
         ea = (a.double().cpu() - r).abs().max().item()
         eb = (b.double().cpu() - r).abs().max().item()
         assert ea < 4 * eb + 1e-7, (ea, eb)
+
+
+@pytest.mark.parametrize("case", [(8, 64, 32, 32, 128, 3, 2, 1), (16, 256, 8, 8, 512, 3, 2, 1), (4, 32, 16, 16, 64, 5, 2, 2)])
+def test_strided_dgrad_grouped_launch(hip, case, monkeypatch):
+    """All stride phases of a strided dgrad in one grouped gemm_g2 launch == one launch per phase
+    (bit-identical: same per-row K order), with residual and the fused backward-BN request."""
+    N, Ci, H, W, Co, k, s, p = case
+    torch.manual_seed(7)
+    OH, OW = (H + 2 * p - k) // s + 1, (W + 2 * p - k) // s + 1
+    w = (torch.randn(Co, Ci, k, k) / math.sqrt(Ci * k * k)).cuda().to(torch.bfloat16).contiguous(memory_format=CL)
+    dy = torch.randn(N, Co, OH, OW).cuda().to(torch.bfloat16).contiguous(memory_format=CL)
+    res = torch.randn(N, Ci, H, W).cuda().to(torch.bfloat16).contiguous(memory_format=CL)
+    wt = hip.conv_weight_t(w)
+    outs = []
+    for grouped in (True, False):
+        monkeypatch.setattr(hip, "_G2_GROUP", grouped)
+        outs.append(hip.conv2d_dgrad(dy, wt, (N, Ci, H, W), (s, s), (p, p), residual=res))
+    assert torch.equal(outs[0], outs[1])
+    ref = torch.nn.grad.conv2d_input((N, Ci, H, W), w.float().cpu(), dy.float().cpu(), s, p) + res.float().cpu()
+    assert rel_err(outs[0], ref) < 1e-2
