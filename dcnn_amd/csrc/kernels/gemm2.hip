@@ -535,10 +535,13 @@ __global__ void __launch_bounds__(256, 2) gemm_t2_kernel(T2Args p) {
 // ---------------------------------------------------------------------------------------------
 // launchers
 // ---------------------------------------------------------------------------------------------
+// LDS ring depth: DCNN_G2_STAGES=2 / 3 forces it; default (0) = 3 stages wherever the deeper ring
+// still leaves two workgroups per CU (every tile but 128x128), else 2
 static int g2_stages() {
   static int st = [] {
     const char* e = getenv("DCNN_G2_STAGES");
-    return (e && atoi(e) == 3) ? 3 : 2;  // 3-stage ring: opt-in (measured slower on the ResNet shapes)
+    const int v = e ? atoi(e) : 0;
+    return (v == 2 || v == 3) ? v : 0;
   }();
   return st;
 }
@@ -546,7 +549,8 @@ static int g2_stages() {
 template <int BM, int BN, int BK, bool UNI>
 static void launch_g2(const G2Args& a, hipStream_t s) {
   const int tiles = ((a.M + BM - 1) / BM) * ((a.N + BN - 1) / BN);
-  if (g2_stages() == 3)
+  const int stages = g2_stages() ? g2_stages() : (2 * G2<BM, BN, BK, UNI, 3>::LDS <= 163840 ? 3 : 2);
+  if (stages == 3)
     hipLaunchKernelGGL((gemm_g2_kernel<BM, BN, BK, UNI, 3>), dim3(tiles), dim3(256), 0, s, a);
   else
     hipLaunchKernelGGL((gemm_g2_kernel<BM, BN, BK, UNI, 2>), dim3(tiles), dim3(256), 0, s, a);

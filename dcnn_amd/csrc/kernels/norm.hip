@@ -165,7 +165,14 @@ struct StatAcc {
     }
   }
 };
-constexpr int kStatRW = 16, kStatWaves = 16, kStatRowsPerBlock = kStatWaves * kStatRW;
+constexpr int kStatRW = 16;
+// waves per reduce block (rows per block = 16 x waves): fewer rows per block = more blocks in the
+// (latency-bound) reduce and more partials for the consumers to merge (DCNN_STAT_WAVES 4/8/16)
+static int g_stat_waves = [] {
+  const char* e = getenv("DCNN_STAT_WAVES");
+  const int v = e ? atoi(e) : 16;
+  return (v == 4 || v == 8) ? v : 16;
+}();
 
 // Merge up to kStatRW rows [r0, r1) of channel c: every load in flight at once, then a pairwise
 // tree (log2 16 = 4 dependent merge levels instead of a 16-long chain). Fixed order.
@@ -188,22 +195,23 @@ __device__ __forceinline__ StatAcc<MODE> stat_tree(const float* __restrict__ src
 }
 
 // the 16 waves' results in LDS merged by a fixed pairwise tree; result in red[0][lane]
-template <int MODE>
+template <int MODE, int WAVES>
 __device__ __forceinline__ void stat_tree_lds(StatAcc<MODE> (*red)[64], int w, int lane) {
 #pragma unroll
-  for (int o = kStatWaves / 2; o > 0; o >>= 1) {
+  for (int o = WAVES / 2; o > 0; o >>= 1) {
     __syncthreads();
     if (w < o) red[w][lane] = red[w][lane].merge(red[w + o][lane]);
   }
   __syncthreads();
 }
 
-template <int MODE>
-__global__ void __launch_bounds__(1024) bn_stat_reduce_kernel(const float* __restrict__ slab, int rows, int C,
-                                                              float* __restrict__ part, unsigned* __restrict__ ticket,
-                                                              float* __restrict__ out) {
+template <int MODE, int WAVES>
+__global__ void __launch_bounds__(64 * WAVES) bn_stat_reduce_kernel(const float* __restrict__ slab, int rows, int C,
+                                                                    float* __restrict__ part,
+                                                                    unsigned* __restrict__ ticket,
+                                                                    float* __restrict__ out) {
   constexpr int NV = MODE == 0 ? 3 : 2;
-  __shared__ StatAcc<MODE> red[kStatWaves][64];
+  __shared__ StatAcc<MODE> red[WAVES][64];
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   const int c = blockIdx.x * 64 + lane;
   const bool cok = c < C;
@@ -218,10 +226,10 @@ __global__ void __launch_bounds__(1024) bn_stat_reduce_kernel(const float* __res
     }
   };
   // ---- level 1: wave w merges rows [b0 + 16w, b0 + 16w + 16) of this block ----
-  const int w0 = by * kStatRowsPerBlock + w * kStatRW;
+  const int w0 = by * (WAVES * kStatRW) + w * kStatRW;
   red[w][lane] = cok ? stat_tree<MODE, kStatRW>(slab, (long)NV * C, w0, min(rows, w0 + kStatRW), C, c)
                      : StatAcc<MODE>::zero();
-  stat_tree_lds<MODE>(red, w, lane);
+  stat_tree_lds<MODE, WAVES>(red, w, lane);
   if (ny == 1) {
     if (w == 0 && cok) finish(red[0][lane]);
     return;
@@ -565,7 +573,10 @@ void bn_partial(int dtype, const void* x, const void* dy, const void* yout, void
                        mode, zero_sums, s);
 }
 
-int bn_stat_parts(int rows) { return (rows + kStatRowsPerBlock - 1) / kStatRowsPerBlock; }
+int bn_stat_parts(int rows) {
+  const int per = g_stat_waves * kStatRW;
+  return (rows + per - 1) / per;
+}
 
 // mode 0: slab [rows][3][C] Welford triples -> out = (mean, var); mode 1: slab [rows][2][C] sums.
 // part: bn_stat_parts(rows) x 3 x C floats (unused when that is 1); ticket: ceil(C/64) zeroed
@@ -576,10 +587,15 @@ void bn_stat_reduce(int mode, const float* slab, int rows, int C, float* out, fl
   const int ny = bn_stat_parts(rows);
   if (ny > 1 && !part) throw std::runtime_error("bn_stat_reduce: partials buffer required");
   const dim3 grid((unsigned)((C + 63) / 64), (unsigned)ny);
-  if (mode == 0)
-    hipLaunchKernelGGL(bn_stat_reduce_kernel<0>, grid, dim3(64 * kStatWaves), 0, s, slab, rows, C, part, ticket, out);
-  else
-    hipLaunchKernelGGL(bn_stat_reduce_kernel<1>, grid, dim3(64 * kStatWaves), 0, s, slab, rows, C, part, ticket, out);
+#define DCNN_SR(W)                                                                                           \
+  if (g_stat_waves == W) {                                                                                   \
+    if (mode == 0)                                                                                           \
+      hipLaunchKernelGGL((bn_stat_reduce_kernel<0, W>), grid, dim3(64 * W), 0, s, slab, rows, C, part, ticket, out); \
+    else                                                                                                     \
+      hipLaunchKernelGGL((bn_stat_reduce_kernel<1, W>), grid, dim3(64 * W), 0, s, slab, rows, C, part, ticket, out); \
+  }
+  DCNN_SR(4) DCNN_SR(8) DCNN_SR(16)
+#undef DCNN_SR
   DCNN_LAUNCH_CHECK();
 }
 

@@ -20,3 +20,8 @@ run python benchmarks/pipeline_bench.py --stages 8 --schedule semi_async --steps
 run python bench.py --batch 512 --steps 20 --warmup 5 || exit $?
 run python bench.py --batch 1024 --steps 20 --warmup 5 || exit $?
 run python bench.py --pg --steps 30 --warmup 5 || exit $?
+run python bench.py --batch 128 --steps 30 --warmup 5 || exit $?
+run python bench.py --batch 64 --steps 30 --warmup 5 || exit $?
+run python bench.py --model resnet50_tiny_imagenet --dtype bf16 --batch 32 --steps 30 --warmup 5 || exit $?
+run python benchmarks/pipeline_bench.py --stages 4 --schedule 1f1b --steps 10 --warmup 3 || exit $?
+run python benchmarks/pipeline_bench.py --stages 8 --schedule sync --steps 10 --warmup 3 || exit $?
