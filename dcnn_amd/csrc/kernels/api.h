@@ -13,6 +13,13 @@ namespace dcnn {
 struct BnbArgs {
   const bf16* y; const bf16* x; const float* mean; const float* istd;
 };
+// In-launch fold of a producer's per-tile statistics rows (statfold.h): the workgroup completing
+// row group g (rows [g*group, (g+1)*group)) of a column tile merges the group's rows into
+// part[g][3][N] (one group: the finished [2][N] statistics). Inactive when part == nullptr.
+// tickets: ngroups x (N / 64) zeroed words, left zeroed.
+struct StatFold {
+  float* part; unsigned* tickets; int group; int ngroups; int rows;
+};
 struct NtArgs {
   const bf16* A; const bf16* B; void* C;
   int M, N, K; int lda, ldb, ldc; int mode;
@@ -33,6 +40,7 @@ struct G2Args {
   const float* bias; const bf16* residual; float* stats; int relu;
   float* zero_ptr; int zero_n;  // zeroed by workgroup 0 (BN sums consumed by the next kernel)
   BnbArgs bnb;
+  StatFold fold;
   // grouped launch of up to 4 row classes (the stride phases of a strided dgrad): class c owns
   // rows [c * cls_rows, (c + 1) * cls_rows) (cls_rows a multiple of the row tile), taps
   // [cls_t0[c], cls_t0[c] + cls_nt[c]) of the tap arrays and the output phase (cls_ory, cls_orx).
@@ -67,6 +75,7 @@ struct HConvArgs {
   // accumulators in `part` [tiles][splits][BM*BN] fp32, the last arriver on the tile's ticket
   // word sums them in split order (deterministic) and runs the epilogue; tickets left zeroed
   int splits; float* part; unsigned* tickets;
+  StatFold fold;
 };
 void hconv(HConvArgs a, hipStream_t s);
 // split count hconv() will use for this shape, and its output-tile count (workspace sizing)

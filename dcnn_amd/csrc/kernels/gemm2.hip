@@ -21,6 +21,7 @@
 // ds_read_b64_tr_b16 transposed fragment reads; split-K partials go to an fp32 slab.
 #include "common.h"
 #include "api.h"
+#include "statfold.h"
 
 namespace dcnn {
 
@@ -298,20 +299,27 @@ __global__ void __launch_bounds__(256, 2) gemm_g2_kernel(G2Args p) {
       red[(r0 * 2 + 1) * BN + cg * 8 + v] = q[v];
     }
     __syncthreads();
+    const bool fold = p.fold.part != nullptr;  // (host: only when N % BN == 0)
     if (bnb) {  // backward: plain sums [tiles][2][N]
       for (int c = tid; c < 2 * BN; c += 256) {
         const int which = c / BN, cc = c % BN;
         if (n0 + cc < p.N) {
           float a = 0.f;
           for (int k = 0; k < RSTEP; ++k) a += red[(k * 2 + which) * BN + cc];
-          p.stats[((long)tm * 2 + which) * p.N + n0 + cc] = a;
+          stat_store(&p.stats[((long)tm * 2 + which) * p.N + n0 + cc], a, fold);
         }
       }
     } else if (tid < BN && n0 + tid < p.N) {  // forward: Welford triple [tiles][3][N]
       float a = 0.f, b = 0.f;
       for (int k = 0; k < RSTEP; ++k) { a += red[(k * 2 + 0) * BN + tid]; b += red[(k * 2 + 1) * BN + tid]; }
       const float cnt = (float)min(BM, p.M - m0);
-      store_welford(p.stats, tm, p.N, n0 + tid, welford_from_shifted(cnt, piv_col, a, b));
+      const Welford w = welford_from_shifted(cnt, piv_col, a, b);
+      if (fold) store_welford_agent(p.stats, tm, p.N, n0 + tid, w);
+      else store_welford(p.stats, tm, p.N, n0 + tid, w);
+    }
+    if (fold) {  // merge the row group's statistics in this launch (statfold.h)
+      if (bnb) stat_fold<1, BN>(p.stats, p.N, tm, n0, p.fold, reinterpret_cast<float*>(smem));
+      else stat_fold<0, BN>(p.stats, p.N, tm, n0, p.fold, reinterpret_cast<float*>(smem));
     }
   }
 }
@@ -589,6 +597,11 @@ void gemm_g2(const G2Args& a_in, hipStream_t s) {
     throw std::runtime_error("gemm_g2: unsupported shape (needs N, Cs, ldb, ldc multiples of 8, 1..64 taps)");
   int bm, bn;
   g2_tile(a.M, a.N, &bm, &bn);
+  if (a.fold.part) {
+    if (!a.stats || a.N % bn || a.N % 64 || a.fold.group < 1 || a.fold.rows != (a.M + bm - 1) / bm ||
+        a.fold.ngroups != (a.fold.rows + a.fold.group - 1) / a.fold.group || !a.fold.tickets)
+      throw std::runtime_error("gemm_g2: statistics fold needs N % column tile == 0 and matching row groups");
+  }
   if (a.ncls <= 1) {
     a.ncls = 1; a.cls_rows = a.M;
     a.cls_t0[0] = 0; a.cls_nt[0] = a.ntaps; a.cls_ory[0] = a.ORY; a.cls_orx[0] = a.ORX;

@@ -22,6 +22,7 @@
 // stores through an LDS-staged bf16 tile), with the spatial-tile -> NHWC row mapping.
 #include "common.h"
 #include "api.h"
+#include "statfold.h"
 
 namespace dcnn {
 
@@ -189,18 +190,25 @@ __device__ __forceinline__ void hc_epilogue(const HConvArgs& p, f32x4 (&acc)[BM 
       red[(r0 * 2 + 1) * BN + cg * 8 + v] = q[v];
     }
     __syncthreads();
+    const bool fold = p.fold.part != nullptr;
     if (bnb) {  // backward: plain sums [tiles][2][N]
       for (int cc = tid; cc < 2 * BN; cc += 256) {
         const int which = cc / BN, c2 = cc % BN;
         float a = 0.f;
         for (int k = 0; k < RSTEP; ++k) a += red[(k * 2 + which) * BN + c2];
-        p.stats[((long)tm * 2 + which) * p.N + n0 + c2] = a;
+        stat_store(&p.stats[((long)tm * 2 + which) * p.N + n0 + c2], a, fold);
       }
     } else if (tid < BN) {  // forward: Welford triple [tiles][3][N], fixed summation order
       float a = 0.f, b = 0.f;
       for (int k = 0; k < RSTEP; ++k) { a += red[(k * 2 + 0) * BN + tid]; b += red[(k * 2 + 1) * BN + tid]; }
       const float cnt = (float)(min(p.IMG, p.NB - img0) * tpx);
-      store_welford(p.stats, tm, p.N, n0 + tid, welford_from_shifted(cnt, piv_col, a, b));
+      const Welford w = welford_from_shifted(cnt, piv_col, a, b);
+      if (fold) store_welford_agent(p.stats, tm, p.N, n0 + tid, w);
+      else store_welford(p.stats, tm, p.N, n0 + tid, w);
+    }
+    if (fold) {  // merge the row group's statistics in this launch (statfold.h)
+      if (bnb) stat_fold<1, BN>(p.stats, p.N, tm, n0, p.fold, reinterpret_cast<float*>(smem));
+      else stat_fold<0, BN>(p.stats, p.N, tm, n0, p.fold, reinterpret_cast<float*>(smem));
     }
   }
 }
@@ -563,6 +571,12 @@ void hconv(HConvArgs a, hipStream_t s) {
     throw std::runtime_error("hconv: split count / workspace mismatch (use hconv_splits)");
   int bm, bn;
   hconv_pick(a, &bm, &bn);
+  if (a.fold.part) {
+    const int rows = (a.NB * a.H * a.W + bm - 1) / bm;
+    if (!a.stats || a.fold.group < 1 || a.fold.rows != rows || !a.fold.tickets ||
+        a.fold.ngroups != (rows + a.fold.group - 1) / a.fold.group)
+      throw std::runtime_error("hconv: statistics fold rows / groups mismatch");
+  }
   if (a.Cf) {
     if (a.bnb.x) throw std::runtime_error("hconv: no backward-BN fusion with fp32 output");
     if (bm == 128 && bn == 128) return launch_hconv<128, 128, true>(a, s);

@@ -158,6 +158,31 @@ def _hconv_split(K, NB, H, W, Cs, N, ntaps, device):
     return s, part.data_ptr(), _ticket(device, tiles * 64, "hconv").data_ptr()
 
 
+_FOLD = os.environ.get("DCNN_STAT_FOLD", "0") == "1"  # opt-in: measured slower (profiles/experiment_inlaunch_stat_fold_r2.md)
+# only small row counts fold: the merging workgroup's group of rows must be cheap next to a launch
+_FOLD_MAX_ROWS = int(os.environ.get("DCNN_STAT_FOLD_ROWS", "128"))
+_NOFOLD = (0, 0, 0, 0, 0)
+
+
+def set_stat_fold(on: bool) -> None:
+    """Fold the BatchNorm statistics rows inside the producing conv launch (statfold.h) instead of
+    a separate bn_stat_reduce launch (bf16 hconv / gemm_g2 producers)."""
+    global _FOLD
+    _FOLD = bool(on)
+
+
+def _fold(rows, N, mode, device, g2=False):
+    """(kernel fold args, :class:`Stats` the consumers read) for a producer writing ``rows``
+    statistics rows of N channels; (_NOFOLD, None) when the launch does not fold."""
+    if not _FOLD or rows < 2 or rows > _FOLD_MAX_ROWS or N % 64 or (g2 and N % 128 and N != 64):
+        return _NOFOLD, None
+    group = -(-rows // 8)           # <= 8 partials for the consumers' prologue merge
+    ng = -(-rows // group)
+    part = torch.empty((ng, 3, N) if ng > 1 else (2 * N,), dtype=F32, device=device)
+    tk = _ticket(device, ng * (N // 64) * 64, "fold")
+    return (part.data_ptr(), tk.data_ptr(), group, ng, rows), Stats(part, ng, mode)
+
+
 def conv2d_fwd(x, w, bias, stride, pad, *, stats=False, residual=None, relu=False, out_fp32=False):
     """y = conv(x, w) + bias  [+ residual] [ReLU]; optional BN partial statistics slab.
 
@@ -198,7 +223,7 @@ def conv2d_fwd(x, w, bias, stride, pad, *, stats=False, residual=None, relu=Fals
         K.hconv(xs.data_ptr(), ws.data_ptr(), 0, _nbytes(xs), _nbytes(ws), N, H, W, 3 * Ci, Co, KH * KW * 3 * Ci,
                 [(t[0], t[1], t[3]) for t in _fwd_taps(3 * Ci, W, KH, KW, ph, pw)], ptr(bias), 0, ptr(slab),
                 int(relu), ptr(sums), 2 * Co if stats else 0, _NOBNB, y.data_ptr(), ptr(residual),
-                *_NOSPLIT, stream_ptr())
+                *_NOSPLIT, stream_ptr(), _NOFOLD)
         return y, ((slab, rows, sums) if stats else None)
     if x.dtype == F32:  # fp32 compute path: MFMA f32 16x16x4 gathered GEMM
         y = torch.empty((N, Co, OH, OW), dtype=F32, device=x.device, memory_format=CL)
@@ -215,26 +240,31 @@ def conv2d_fwd(x, w, bias, stride, pad, *, stats=False, residual=None, relu=Fals
     if not out_fp32 and _hconv_ok(N, OH, OW, H, W, sh, sw, Ci, Co, taps, w):
         y = torch.empty((N, Co, OH, OW), dtype=BF16, device=x.device, memory_format=CL)
         slab, rows, sums = None, 0, None
+        fold, fst = _NOFOLD, None
         if stats:
             rows = K.hconv_stat_rows(N, H, W, Co)
             slab = torch.empty((rows, 3, Co), dtype=F32, device=x.device)
             sums = torch.empty((2 * Co,), dtype=F32, device=x.device)  # zeroed in-kernel
+            fold, fst = _fold(rows, Co, 0, x.device)
         K.hconv(x.data_ptr(), w.data_ptr(), y.data_ptr(), _nbytes(x), _nbytes(w), N, H, W, Ci, Co, KH * KW * Ci,
                 [(t[0], t[1], t[3]) for t in taps], ptr(bias), ptr(residual), ptr(slab), int(relu), ptr(sums),
                 2 * Co if stats else 0, _NOBNB, 0, 0, *_hconv_split(K, N, H, W, Ci, Co, KH * KW, x.device),
-                stream_ptr())
-        return y, ((slab, rows, sums) if stats else None)
+                stream_ptr(), fold)
+        return y, ((fst if fst is not None else slab, rows, sums) if stats else None)
     if _g2_ok(Ci, Co) and not out_fp32:
         y = torch.empty((N, Co, OH, OW), dtype=BF16, device=x.device, memory_format=CL)
         slab, rows, sums = None, 0, None
+        fold, fst = _NOFOLD, None
         if stats:
             rows = K.gemm_g2_stat_rows(M, Co)
             slab = torch.empty((rows, 3, Co), dtype=F32, device=x.device)
             sums = torch.empty((2 * Co,), dtype=F32, device=x.device)  # zeroed in-kernel
-        K.gemm_g2(x.data_ptr(), w.data_ptr(), y.data_ptr(), _nbytes(x), _nbytes(w), M, Co, Ci, H, W, OH, OW, sh, sw,
-                  _fwd_taps(Ci, W, KH, KW, ph, pw), KH * KW * Ci, Co, OH, OW, 1, 1, 0, 0, ptr(bias), ptr(residual),
-                  ptr(slab), int(relu), ptr(sums), 2 * Co if stats else 0, _NOBNB, stream_ptr())
-        return y, ((slab, rows, sums) if stats else None)
+            fold, fst = _fold(rows, Co, 0, x.device, g2=True)
+        K.gemm_g2_grouped(x.data_ptr(), w.data_ptr(), y.data_ptr(), _nbytes(x), _nbytes(w), M, Co, Ci, H, W, OH, OW,
+                          sh, sw, _fwd_taps(Ci, W, KH, KW, ph, pw), KH * KW * Ci, Co, OH, OW, 1, 1, 0, 0, ptr(bias),
+                          ptr(residual), ptr(slab), int(relu), ptr(sums), 2 * Co if stats else 0, _NOBNB,
+                          stream_ptr(), [], fold)
+        return y, ((fst if fst is not None else slab, rows, sums) if stats else None)
     # generic fallback (odd channel counts): v1 kernels
     y = torch.empty((N, Co, OH, OW), dtype=F32 if out_fp32 else BF16, device=x.device, memory_format=CL)
     slab, rows = None, 0
@@ -549,7 +579,7 @@ def conv2d_dgrad(dy, wt, x_shape, stride, pad, *, residual=None, bnb=None):
         wts = split3_rows(wt, Ci * KH * KW, Co, 1)
         K.hconv(dys.data_ptr(), wts.data_ptr(), 0, _nbytes(dys), _nbytes(wts), N, OH, OW, 3 * Co, Ci,
                 KH * KW * 3 * Co, [(t[0], t[1], 3 * t[3]) for t in classes[0][4]], 0, 0, 0, 0, 0, 0, _NOBNB,
-                dx.data_ptr(), ptr(residual), *_NOSPLIT, st)
+                dx.data_ptr(), ptr(residual), *_NOSPLIT, st, _NOFOLD)
         return dx
     g2 = K.gemm_g2f if f32 else K.gemm_g2
     fuse = (bnb is not None and _BNB and not bnb.pooled and not f32 and not empty_class and bnb.x.dtype == BF16
@@ -558,16 +588,18 @@ def conv2d_dgrad(dy, wt, x_shape, stride, pad, *, residual=None, bnb=None):
             _hconv_ok(N, H, W, OH, OW, sh, sw, Co, Ci, classes[0][4], wt):
         slab = sums = None
         rows = 0
+        fold, fst = _NOFOLD, None
         if fuse:
             rows = K.hconv_stat_rows(N, H, W, Ci)
             slab = torch.empty((rows, 2, Ci), dtype=F32, device=dy.device)
             sums = torch.empty((2 * Ci,), dtype=F32, device=dy.device)  # zeroed in-kernel
+            fold, fst = _fold(rows, Ci, 1, dy.device)
         K.hconv(dy.data_ptr(), wt.data_ptr(), dx.data_ptr(), _nbytes(dy), _nbytes(wt), N, OH, OW, Co, Ci, KH * KW * Co,
                 [(t[0], t[1], t[3]) for t in classes[0][4]], 0, ptr(residual), ptr(slab), 0, ptr(sums),
                 2 * Ci if fuse else 0, bnb.args() if fuse else _NOBNB, 0, 0,
-                *_hconv_split(K, N, OH, OW, Co, Ci, len(classes[0][4]), dy.device), st)
+                *_hconv_split(K, N, OH, OW, Co, Ci, len(classes[0][4]), dy.device), st, fold)
         if fuse:
-            dx._bnb = (bnb.bn, slab, rows, sums)
+            dx._bnb = (bnb.bn, fst if fst is not None else slab, rows, sums)
         return dx
     if (not f32 and _G2_GROUP and len(classes) > 1 and len({(c[2], c[3]) for c in classes}) == 1
             and (N * classes[0][2] * classes[0][3]) % 128 == 0):
@@ -582,11 +614,12 @@ def conv2d_dgrad(dy, wt, x_shape, stride, pad, *, residual=None, bnb=None):
         rows = K.gemm_g2_stat_rows(M, Ci) if fuse else 0
         slab = torch.empty((rows, 2, Ci), dtype=F32, device=dy.device) if fuse else None
         sums = torch.empty((2 * Ci,), dtype=F32, device=dy.device) if fuse else None
+        fold, fst = _fold(rows, Ci, 1, dy.device, g2=True) if fuse else (_NOFOLD, None)
         K.gemm_g2_grouped(dy.data_ptr(), wt.data_ptr(), dx.data_ptr(), _nbytes(dy), _nbytes(wt), M, Ci, Co, OH, OW,
                           GH, GW, 1, 1, taps_all, KH * KW * Co, Ci, H, W, sh, sw, 0, 0, 0, ptr(residual), ptr(slab), 0,
-                          ptr(sums), 2 * Ci if fuse else 0, bnb.args() if fuse else _NOBNB, st, groups)
+                          ptr(sums), 2 * Ci if fuse else 0, bnb.args() if fuse else _NOBNB, st, groups, fold)
         if fuse:
-            dx._bnb = (bnb.bn, slab, rows, sums)
+            dx._bnb = (bnb.bn, fst if fst is not None else slab, rows, sums)
         return dx
     crow = [K.gemm_g2_stat_rows(N * GH * GW, Ci) if fuse else 0 for _, _, GH, GW, _ in classes]
     rows = sum(crow)
@@ -975,6 +1008,8 @@ def stat_reduce(mode, slab, rows, C, out):
     """Deterministic slab reduce (norm.hip bn_stat_reduce): mode 0 = Welford (count, mean, M2)
     tile triples -> (mean, biased var); mode 1 = (sum a, sum b) rows -> sums. Returns
     :class:`Stats` (``out`` when one block covered all rows, else the partials buffer)."""
+    if isinstance(slab, Stats):  # already folded inside the producing launch (statfold.h)
+        return slab
     K = kernels()
     ny = K.bn_stat_parts(rows)
     part = torch.empty((ny, 3, C), dtype=F32, device=slab.device) if ny > 1 else None

@@ -743,3 +743,46 @@ def test_strided_dgrad_grouped_launch(hip, case, monkeypatch):
     assert torch.equal(outs[0], outs[1])
     ref = torch.nn.grad.conv2d_input((N, Ci, H, W), w.float().cpu(), dy.float().cpu(), s, p) + res.float().cpu()
     assert rel_err(outs[0], ref) < 1e-2
+
+
+@pytest.mark.parametrize("case", [(64, 64, 32, 32, 64, 1), (16, 128, 16, 16, 256, 2), (256, 256, 8, 8, 256, 1),
+                                  (8, 512, 4, 4, 512, 1)])
+def test_stat_fold_matches_reduce(hip, case, monkeypatch):
+    """BatchNorm statistics folded inside the producing conv launch (statfold.h: per-group
+    tickets, last workgroup merges) == the separate bn_stat_reduce, forward (Welford) and
+    backward (fused dgrad sums); repeated launches are bit-identical."""
+    N, C, H, W, Co, s = case
+    torch.manual_seed(2)
+    x = (torch.randn(N, C, H, W) * 3 + 5).cuda().to(torch.bfloat16).contiguous(memory_format=CL)
+    w = (torch.randn(Co, C, 3, 3) / math.sqrt(9 * C)).cuda().to(torch.bfloat16).contiguous(memory_format=CL)
+    outs = []
+    for fold in (True, True, False):
+        monkeypatch.setattr(hip, "_FOLD", fold)
+        y, part = hip.conv2d_fwd(x, w, None, (s, s), (1, 1), stats=True)
+        st = hip.bn_stats(y, part)
+        outs.append((y, st.final().clone() if hasattr(st, "final") else st.clone()))
+    (y1, s1), (y2, s2), (y0, s0) = outs
+    assert torch.equal(y1, y0) and torch.equal(s1, s2)
+    yd = y1.double()
+    ref = torch.cat([yd.mean((0, 2, 3)), yd.var((0, 2, 3), unbiased=False)]).cpu()
+    assert rel_err(s1.double(), ref) < 1e-5 and rel_err(s0.double(), ref) < 1e-5
+    # backward: dgrad with the fused BN request (mask + sums), folded vs reduced
+    from dcnn_amd.ops.hip import BnbRequest
+    xb = torch.randn(N, C, H, W).cuda().to(torch.bfloat16).contiguous(memory_format=CL)
+    mean = xb.float().mean((0, 2, 3))
+    istd = 1.0 / (xb.float().var((0, 2, 3), unbiased=False) + 1e-5).sqrt()
+    yb = torch.relu(xb)
+    dy = torch.randn_like(y1)
+    wt = hip.conv_weight_t(w)
+
+    class _BN:
+        pass
+    bn = _BN()
+    sums = []
+    for fold in (True, False):
+        monkeypatch.setattr(hip, "_FOLD", fold)
+        dx = hip.conv2d_dgrad(dy, wt, (N, C, H, W), (s, s), (1, 1), bnb=BnbRequest(bn, yb, xb, mean, istd))
+        assert dx._bnb[0] is bn
+        _, slab, rows, sm = dx._bnb
+        sums.append(hip.stat_reduce(1, slab, rows, C, sm).final().clone())
+    assert rel_err(sums[0], sums[1]) < 1e-5
