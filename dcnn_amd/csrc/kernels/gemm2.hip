@@ -609,7 +609,7 @@ void gemm_g2(const G2Args& a_in, hipStream_t s) {
     if (a.ncls > 4 || a.cls_rows <= 0 || a.cls_rows % bm || a.ncls * a.cls_rows != a.M)
       throw std::runtime_error("gemm_g2: grouped classes need <= 4 classes of equal rows, a multiple of the row tile");
     for (int c = 0; c < a.ncls; ++c)
-      if (a.cls_nt[c] < 1 || a.cls_t0[c] < 0 || a.cls_t0[c] + a.cls_nt[c] > a.ntaps)
+      if (a.cls_nt[c] < 0 || a.cls_t0[c] < 0 || a.cls_t0[c] + a.cls_nt[c] > a.ntaps)
         throw std::runtime_error("gemm_g2: class tap range out of bounds");
   }
   const int bk = (a.Cs % 64 == 0) ? 64 : 32;

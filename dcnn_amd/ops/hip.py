@@ -541,6 +541,7 @@ def conv2d_dgrad(dy, wt, x_shape, stride, pad, *, residual=None, bnb=None):
                   N, OH, OW, Co, H, W, KH, KW, sh, sw, ph, pw, 0, ptr(residual), 0, 0, 0, stream_ptr())
         return dx
     classes = []
+    empty = []  # phase classes no tap reaches: (ry, rx, GH, GW, [])
     empty_class = False
     for ry in range(sh):
         for rx in range(sw):
@@ -561,7 +562,24 @@ def conv2d_dgrad(dy, wt, x_shape, stride, pad, *, residual=None, bnb=None):
                 classes.append((ry, rx, GH, GW, taps))
             else:
                 empty_class = True
+                empty.append((ry, rx, GH, GW, []))
     odt = F32 if f32 else BF16
+    allc = classes + empty
+    if (not f32 and empty_class and _G2_GROUP and len(allc) <= 4 and len({(c[2], c[3]) for c in allc}) == 1
+            and (N * allc[0][2] * allc[0][3]) % 128 == 0):
+        # phases no tap reaches join the grouped launch as zero-tap classes: their epilogue writes
+        # the residual (or zeros), so there is no separate fill / copy pass
+        GH, GW = allc[0][2], allc[0][3]
+        M = len(allc) * N * GH * GW
+        taps_all, groups = [], []
+        for ry, rx, _, _, taps in allc:
+            groups.append((len(taps_all), len(taps), ry, rx))
+            taps_all += taps
+        dx = torch.empty((N, Ci, H, W), dtype=BF16, device=dy.device, memory_format=CL)
+        K.gemm_g2_grouped(dy.data_ptr(), wt.data_ptr(), dx.data_ptr(), _nbytes(dy), _nbytes(wt), M, Ci, Co, OH, OW,
+                          GH, GW, 1, 1, taps_all, KH * KW * Co, Ci, H, W, sh, sw, 0, 0, 0, ptr(residual), 0, 0, 0, 0,
+                          _NOBNB, stream_ptr(), groups, _NOFOLD)
+        return dx
     if empty_class:
         # positions no tap reaches keep the residual (or zero); a memset / async copy node, not a kernel
         dx = torch.empty((N, Ci, H, W), dtype=odt, device=dy.device, memory_format=CL)
@@ -1105,32 +1123,23 @@ def bn_backward(dy, x, yout, mean, istd, gamma, dgamma, dbeta, *, want_masked=Fa
         return dx, (dy if want_masked else None)
     dmask = torch.empty_like(dy, memory_format=CL) if (want_masked and yout is not None) else None
     sums = None
-    if not eval_mode:
+    # the (sum dy', sum dy' * xhat) pass: the batch-statistics backward needs it, and so does a
+    # frozen-statistics (eval-mode) backward that still accumulates the affine gradients or
+    # returns the masked gradient (bn_bwd_apply adds the sums to dgamma / dbeta either way and
+    # uses them for dx only in training mode)
+    if not eval_mode or dgamma is not None or dbeta is not None or dmask is not None:
         rows = K.bn_partial_rows(R, C)
         slab = torch.empty((rows, 2, C), dtype=F32, device=x.device)
         sums = torch.empty((2 * C,), dtype=F32, device=x.device)
         K.bn_partial(dt, x.data_ptr(), dy.data_ptr(), ptr(yout), ptr(dmask), mean.data_ptr(), istd.data_ptr(), R, C,
                      slab.data_ptr(), 1, 0, st)
         sums = stat_reduce(1, slab, rows, C, sums)
-    elif want_masked and yout is not None:
-        dmask = dy * (yout > 0)
     dx = torch.empty_like(x, memory_format=CL)
     src = dmask if dmask is not None else dy
     sp, parts = _stats(sums)
     K.bn_bwd_apply(dt, src.data_ptr(), 0 if dmask is not None else ptr(yout), x.data_ptr(), dx.data_ptr(), R, C,
                    mean.data_ptr(), istd.data_ptr(), ptr(gamma), sp, parts, float(R), ptr(dgamma), ptr(dbeta),
                    int(eval_mode), st)
-    if eval_mode and (dgamma is not None or dbeta is not None):
-        # frozen-statistics backward still accumulates the affine gradients
-        xf = x.float()
-        d = (src if dmask is None else dmask).float()
-        if yout is not None and dmask is None:
-            d = d * (yout > 0)
-        xhat = (xf - mean.view(1, -1, 1, 1)) * istd.view(1, -1, 1, 1)
-        if dgamma is not None:
-            dgamma += (d * xhat).sum((0, 2, 3))
-        if dbeta is not None:
-            dbeta += d.sum((0, 2, 3))
     return dx, dmask
 
 

@@ -725,7 +725,8 @@ def test_hconv_fp32_concat_accuracy(hip, case):
         assert ea < 4 * eb + 1e-7, (ea, eb)
 
 
-@pytest.mark.parametrize("case", [(8, 64, 32, 32, 128, 3, 2, 1), (16, 256, 8, 8, 512, 3, 2, 1), (4, 32, 16, 16, 64, 5, 2, 2)])
+@pytest.mark.parametrize("case", [(8, 64, 32, 32, 128, 3, 2, 1), (16, 256, 8, 8, 512, 3, 2, 1), (4, 32, 16, 16, 64, 5, 2, 2),
+                                  (8, 64, 16, 16, 128, 1, 2, 0), (16, 256, 8, 8, 512, 1, 2, 0)])
 def test_strided_dgrad_grouped_launch(hip, case, monkeypatch):
     """All stride phases of a strided dgrad in one grouped gemm_g2 launch == one launch per phase
     (bit-identical: same per-row K order), with residual and the fused backward-BN request."""
@@ -786,3 +787,26 @@ def test_stat_fold_matches_reduce(hip, case, monkeypatch):
         _, slab, rows, sm = dx._bnb
         sums.append(hip.stat_reduce(1, slab, rows, C, sm).final().clone())
     assert rel_err(sums[0], sums[1]) < 1e-5
+
+
+@pytest.mark.parametrize("relu", [False, True])
+def test_bn_backward_eval_mode_kernels(hip, relu):
+    """Frozen-statistics (eval-mode) BatchNorm backward: dx = gamma * istd * dy' and the affine
+    gradients, all on the HIP kernels (bn_partial + bn_bwd_apply), vs fp32 reference math."""
+    torch.manual_seed(8)
+    N, C, H, W = 4, 64, 8, 8
+    x = torch.randn(N, C, H, W).cuda().to(torch.bfloat16).contiguous(memory_format=CL)
+    dy = torch.randn(N, C, H, W).cuda().to(torch.bfloat16).contiguous(memory_format=CL)
+    rm, rv = torch.randn(C).cuda() * 0.1, torch.rand(C).cuda() + 0.5
+    istd = 1.0 / (rv + 1e-5).sqrt()
+    gamma = torch.randn(C).cuda()
+    yout = torch.relu(x) if relu else None
+    dg, db = torch.zeros(C, device="cuda"), torch.zeros(C, device="cuda")
+    dx, dmask = hip.bn_backward(dy, x, yout, rm, istd, gamma, dg, db, want_masked=True, eval_mode=True)
+    d = dy.float() * ((yout.float() > 0).float() if relu else 1.0)
+    xhat = (x.float() - rm.view(1, -1, 1, 1)) * istd.view(1, -1, 1, 1)
+    assert rel_err(dx, d * (gamma * istd).view(1, -1, 1, 1)) < 1e-2
+    assert rel_err(dg, (d * xhat).sum((0, 2, 3))) < 1e-4
+    assert rel_err(db, d.sum((0, 2, 3))) < 1e-4
+    if relu:
+        assert rel_err(dmask, d) < 1e-2
