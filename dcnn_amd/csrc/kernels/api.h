@@ -102,6 +102,7 @@ struct HWArgs {
 void hwgrad(HWArgs a, int splits, hipStream_t s);
 bool hwgrad_supported(int NB, int H, int W, int Cs, int Co, int ntaps);
 int hwgrad_splits(int NB, int H, int W, int Cs, int Co);
+void hwgrad_set_version(int v);  // 2: tap-shift-invariant kernel where it applies, 1: first kernel
 
 void gemm_nt(const NtArgs& a, hipStream_t s);
 void gemm_g2(const G2Args& a, hipStream_t s);

@@ -138,6 +138,7 @@ PYBIND11_MODULE(_kernels, m) {
     split3_bf16(P<const float*>(in), P<bf16*>(out), rows, C, pattern, S(st));
   });
   m.def("hwgrad_splits", &hwgrad_splits);
+  m.def("hwgrad_set_version", &hwgrad_set_version);
   m.def("gemm_g2f",
         [](uintptr_t A, uintptr_t B, uintptr_t C, unsigned a_bytes, unsigned b_bytes, int M, int N, int Cs, int H,
            int W, int GH, int GW, int SY, int SX, std::vector<std::array<int, 4>> taps, int ldb, int ldc, int OH,

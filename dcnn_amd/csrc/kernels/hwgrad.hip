@@ -256,6 +256,231 @@ __global__ void __launch_bounds__(256, 1) hwgrad_kernel(HWArgs p) {
 }
 
 // ---------------------------------------------------------------------------------------------
+// Variant with tap-shift-invariant LDS addressing (hwgrad2): the halo's pixel rows are padded to
+// HW2P = round_up(TW + 2, 8) LDS rows and the 16-byte chunk swizzle depends only on row bits 1-2,
+// so a tap's dy shift (dy * HW2P rows) leaves the swizzle unchanged and becomes an immediate
+// ds_read offset; the three dx shifts get a base address each. Per 128-pixel tile the 104
+// fragment reads then need 32 base registers and no per-read address arithmetic (the first
+// kernel computes ~180 address VALU per tile and keeps 72 hoisted addresses live, 479 registers).
+// The pixel -> MFMA-k mapping puts pixels p..p+7 of an image row in one 32-lane read group
+// (rows r..r+7: same-parity rows r, r+2, r+4, r+6 differ in bits 1-2 -> conflict-free).
+// Standard 3x3 / pad-1 taps only (t = ky * 3 + kx, dy = ky - 1, dx = kx - 1).
+// ---------------------------------------------------------------------------------------------
+namespace {
+__device__ __forceinline__ int wswz2(int row) { return ((row >> 1) & 3) << 1; }
+}  // namespace
+
+template <int TW, int TH, int IMG>
+struct HWGeo2 {
+  static constexpr int HW2P = ((TW + 2 + 7) / 8) * 8, HPIP = (TH + 2) * HW2P, HPP = IMG * HPIP;
+  static constexpr int HNI = (HPP + 31) / 32;
+  static constexpr int HPR = HNI * 32;
+  static constexpr int TPX = TH * TW;
+  static constexpr int STAGE = PT * 128 + HPR * 128;
+  static constexpr int EPI_TAPS = (2 * STAGE) / (64 * 68 * 4);
+  static_assert(TPX * IMG == PT, "tile must hold 128 pixels");
+  static_assert(TW % 8 == 0, "8 consecutive pixels of a read group must share an image row");
+};
+
+__device__ __forceinline__ bf16x4 tr4_at(const char* addr) {
+  return __builtin_amdgcn_ds_read_tr16_b64_v4bf16((__attribute__((address_space(3))) bf16x4*)(const_cast<char*>(addr)));
+}
+
+template <int TW, int TH, int IMG, int NS>
+__global__ void __launch_bounds__(256, 1) hwgrad2_kernel(HWArgs p) {
+  using G = HWGeo2<TW, TH, IMG>;
+  constexpr int HNI = G::HNI, HW2P = G::HW2P, HPIP = G::HPIP, HPP = G::HPP, TPX = G::TPX, STAGE = G::STAGE;
+  constexpr int INS = 4 + HNI;
+  static_assert(NS == 2 || NS == 3, "2 or 3 stages");
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int co_tiles = p.Co / 64, ci_chunks = p.Cs / 64;
+  const int per_split = co_tiles * ci_chunks;
+  const int lt = xcd_remap_w(blockIdx.x, gridDim.x);
+  const int split = lt / per_split, rem = lt - split * per_split;
+  const int pair = blockIdx.y, nsplits = gridDim.x / per_split;
+  const int yoff = p.pair_yoff[pair], xoff = p.pair_xoff[pair];
+  const int co0 = (rem / ci_chunks) * 64, c0 = (rem % ci_chunks) * 64;
+
+  const int tx_tiles = p.W / TW, ty_tiles = p.H / TH, tpi = tx_tiles * ty_tiles;
+  const int total_tiles = (p.NB / IMG) * tpi;
+  const int tbeg = split * p.tiles_per_split;
+  const int tend = min(total_tiles, tbeg + p.tiles_per_split);
+  const i32x4 rsY = raw_rsrc(p.dY, p.dy_bytes);
+  const i32x4 rsX = raw_rsrc(p.X, p.x_bytes);
+
+  // ---- dY loader (tile rows = pixels, 128 B each) ----
+  const int slot = lane & 7;
+  unsigned y_rel[4], y_col[4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int row = (wid * 4 + i) * 8 + (lane >> 3);
+    const int im = row / TPX, r2 = row - im * TPX;
+    y_rel[i] = (unsigned)((im * p.H + r2 / TW) * p.W + r2 % TW);
+    y_col[i] = (unsigned)((yoff + co0 + ((slot ^ wswz2(row)) * 8)) * 2);
+  }
+  // ---- halo loader: padded rows (hx >= TW + 1) are never valid ----
+  int h_rel[HNI], h_hy[HNI], h_hx[HNI];
+#pragma unroll
+  for (int j = 0; j < HNI; ++j) {
+    const int row = (wid * HNI + j) * 8 + (lane >> 3);
+    const int im = row / HPIP, r2 = row - im * HPIP;
+    const int hy = r2 / HW2P - 1, hx = r2 % HW2P - 1;
+    const bool real = row < HPP && hx <= TW;
+    h_hy[j] = real ? hy : -(1 << 20);
+    h_hx[j] = hx;
+    h_rel[j] = ((im * p.H + hy) * p.W + hx) * p.ldx * 2 + (xoff + c0 + ((slot ^ wswz2(row)) * 8)) * 2;
+  }
+  auto load_tile = [&](int buf, int tile) {
+    char* Ys = smem + buf * STAGE;
+    char* Hs = Ys + PT * 128;
+    const int ig = tile / tpi, tr = tile - ig * tpi;
+    const int y0 = (tr / tx_tiles) * TH, x0 = (tr % tx_tiles) * TW;
+    const int g0 = (ig * IMG * p.H + y0) * p.W + x0;
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+      glds16w(rsY, Ys + (wid * 4 + i) * 1024, (unsigned)(g0 + y_rel[i]) * (unsigned)(p.ldy * 2) + y_col[i]);
+    const int gx = g0 * p.ldx * 2;
+#pragma unroll
+    for (int j = 0; j < HNI; ++j) {
+      const bool ok = (unsigned)(y0 + h_hy[j]) < (unsigned)p.H && (unsigned)(x0 + h_hx[j]) < (unsigned)p.W;
+      glds16w(rsX, Hs + (wid * HNI + j) * 1024, ok ? (unsigned)(gx + h_rel[j]) : kOOBw);
+    }
+  };
+
+  // ---- fragment base addresses (stage-relative bytes) ----
+  // pixel of (k-step kk, half h) for this lane: kk*32 + h*16 + 4*(lane>>4) + ((lane&15)>>2)
+  const int lpx = 4 * (lane >> 4) + ((lane & 15) >> 2);
+  // A (dY tile): row = kk*32 + h*16 + lpx, column i*16 + 4*(lane&3); kk and h shift the row by
+  // multiples of 8 (swizzle unchanged) -> immediate offsets kk*4096 + h*2048
+  int abase[4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int col = i * 16 + 4 * (lane & 3);
+    abase[i] = lpx * 128 + (((col >> 3) ^ wswz2(lpx)) << 4) + (col & 7) * 2;
+  }
+  // B (halo): row of pixel px, tap (dy, dx) = hrow(px) + dy*HW2P + dx; base per (kk, h, dx) at
+  // dy = -1, dy = 0 / +1 as immediate offsets HW2P*128 / 2*HW2P*128
+  const int bcol = wid * 16 + 4 * (lane & 3);
+  int bbase[8][3];
+#pragma unroll
+  for (int sidx = 0; sidx < 8; ++sidx) {
+    const int px = (sidx >> 1) * 32 + (sidx & 1) * 16 + lpx;
+    const int im = px / TPX, r2 = px - im * TPX;
+    const int hr = im * HPIP + (r2 / TW + 1) * HW2P + r2 % TW + 1;
+#pragma unroll
+    for (int d = 0; d < 3; ++d) {
+      const int row = hr + (d - 1) - HW2P;  // dx = d - 1, dy = -1
+      bbase[sidx][d] = PT * 128 + row * 128 + (((bcol >> 3) ^ wswz2(row)) << 4) + (bcol & 7) * 2;
+    }
+  }
+
+  f32x4 acc[4][9];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int t = 0; t < 9; ++t) acc[i][t] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  const bool do_bias = p.bias_slab != nullptr && c0 == 0;
+  float bias_acc = 0.f;
+  const int nt = tend - tbeg;
+  if (nt > 0) load_tile(0, tbeg);
+  if (NS == 3 && nt > 1) load_tile(1, tbeg + 1);
+  if (NS == 3 && nt > 1)
+    asm volatile("s_waitcnt vmcnt(%0)" ::"n"(INS) : "memory");
+  else
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  int cur = 0;
+  for (int it = 0; it < nt; ++it) {
+    if (it + NS - 1 < nt) load_tile(cur == 0 ? NS - 1 : cur - 1, tbeg + it + NS - 1);
+    const char* S0 = smem + cur * STAGE;
+    bf16x8 a[2][4], b[2][9];
+    auto read_step = [&](int kk, bf16x8* av, bf16x8* bv) {
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const char* q = S0 + abase[i] + kk * 4096;
+        const bf16x4 lo = tr4_at(q), hi = tr4_at(q + 2048);
+        av[i] = bf16x8{lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+      }
+#pragma unroll
+      for (int t = 0; t < 9; ++t) {
+        const int dy = t / 3, dx = t % 3;  // dy index 0..2 = dy + 1
+        const bf16x4 lo = tr4_at(S0 + bbase[kk * 2][dx] + dy * HW2P * 128);
+        const bf16x4 hi = tr4_at(S0 + bbase[kk * 2 + 1][dx] + dy * HW2P * 128);
+        bv[t] = bf16x8{lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+      }
+    };
+    read_step(0, a[0], b[0]);
+#pragma unroll
+    for (int kk = 0; kk < 4; ++kk) {
+      const int c = kk & 1;
+      __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0)
+      if (kk + 1 < 4) read_step(kk + 1, a[c ^ 1], b[c ^ 1]);
+#pragma unroll
+      for (int t = 0; t < 9; ++t)
+#pragma unroll
+        for (int i = 0; i < 4; ++i) acc[i][t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[c][i], b[c][t], acc[i][t], 0, 0, 0);
+      if (kk + 1 < 4) {
+#pragma unroll
+        for (int g = 0; g < 26; ++g) {
+          __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);  // MFMA
+          __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);  // DS read
+        }
+        __builtin_amdgcn_sched_group_barrier(0x008, 10, 0);
+      }
+    }
+    if (do_bias) {
+      const int col = tid & 63, chn = col >> 3, w = (col & 7) * 2;
+      for (int r = tid >> 6; r < PT; r += 4)
+        bias_acc += (float)*reinterpret_cast<const bf16*>(S0 + r * 128 + ((chn ^ wswz2(r)) << 4) + w);
+    }
+    if (NS == 3 && it + 2 < nt)
+      asm volatile("s_waitcnt vmcnt(%0)\n\ts_waitcnt lgkmcnt(0)\n\ts_barrier" ::"n"(INS) : "memory");
+    else
+      asm volatile("s_waitcnt vmcnt(0)\n\ts_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+    cur = cur == NS - 1 ? 0 : cur + 1;
+  }
+
+  // ---- slab[split][co][t*Cs + ci] (as hwgrad_kernel) ----
+  const long Ng = 9l * p.Cs;
+  const long slab_idx = (long)pair * nsplits + split;
+  float* out = p.slab + slab_idx * p.Co * Ng;
+  float* stg = reinterpret_cast<float*>(smem);
+  constexpr int ET = G::EPI_TAPS;
+#pragma unroll
+  for (int t0 = 0; t0 < 9; t0 += ET) {
+    __syncthreads();
+#pragma unroll
+    for (int u = 0; u < ET; ++u) {
+      if (t0 + u < 9) {
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+#pragma unroll
+          for (int r = 0; r < 4; ++r)
+            stg[(u * 64 + i * 16 + (lane >> 4) * 4 + r) * 68 + wid * 16 + (lane & 15)] = acc[i][t0 + u][r];
+      }
+    }
+    __syncthreads();
+    const int nrows = (9 - t0 < ET ? 9 - t0 : ET) * 64;
+    for (int q = tid; q < nrows * 16; q += 256) {
+      const int row = q >> 4, c4 = (q & 15) * 4;
+      const int u = row >> 6, co = co0 + (row & 63);
+      const float4 v = *reinterpret_cast<const float4*>(stg + row * 68 + c4);
+      *reinterpret_cast<float4*>(out + (long)co * Ng + (t0 + u) * p.Cs + c0 + c4) = v;
+    }
+  }
+  if (do_bias) {
+    __syncthreads();
+    stg[tid] = bias_acc;
+    __syncthreads();
+    if (tid < 64)
+      p.bias_slab[slab_idx * p.Co + co0 + tid] =
+          p.pair_bias[pair] ? stg[tid] + stg[tid + 64] + stg[tid + 128] + stg[tid + 192] : 0.f;
+  }
+}
+
+// ---------------------------------------------------------------------------------------------
 // host side
 // ---------------------------------------------------------------------------------------------
 // supported tile geometries (TW, TH, IMG): W multiple of 16 and H of 8; 8x8; 4x4 maps
@@ -296,6 +521,13 @@ int hwgrad_splits(int NB, int H, int W, int Cs, int Co) {
   return (total + tps - 1) / tps;
 }
 
+// kernel generation: 2 = tap-shift-invariant addressing where it applies, 1 = first kernel only
+static int g_hwgrad_version = [] {
+  const char* e = getenv("DCNN_HWGRAD_V");
+  return e ? atoi(e) : 2;
+}();
+void hwgrad_set_version(int v) { g_hwgrad_version = v; }
+
 void hwgrad(HWArgs a, int splits, hipStream_t s) {
   if (!hwgrad_supported(a.NB, a.H, a.W, a.Cs, a.Co, a.ntaps)) throw std::runtime_error("hwgrad: unsupported shape");
   for (int t = 0; t < a.ntaps; ++t)
@@ -323,6 +555,25 @@ void hwgrad(HWArgs a, int splits, hipStream_t s) {
     const char* e = getenv("DCNN_HWGRAD_STAGES");
     return (e && atoi(e) == 2) ? 2 : 3;
   }();
+  // tap-shift-invariant variant (hwgrad2_kernel) for the standard 3x3 / pad-1 taps on 16- and
+  // 8-wide maps (DCNN_HWGRAD_V=1 keeps the first kernel)
+  const int ver = g_hwgrad_version;
+  bool std_taps = a.ntaps == 9;
+  for (int t = 0; t < a.ntaps && std_taps; ++t) std_taps = a.tap_dy[t] == t / 3 - 1 && a.tap_dx[t] == t % 3 - 1;
+  if (ver == 2 && std_taps && a.TW % 8 == 0 && !a.dbg) {
+#define DCNN_HW2(TW_, TH_, IMG_, NS_)                                                                   \
+    if (a.TW == TW_ && a.TH == TH_ && a.IMG == IMG_) {                                                  \
+      auto k = hwgrad2_kernel<TW_, TH_, IMG_, NS_>;                                                     \
+      const int lds = NS_ * HWGeo2<TW_, TH_, IMG_>::STAGE;                                              \
+      DCNN_HIP_CHECK(hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, lds)); \
+      hipLaunchKernelGGL(k, dim3(grid, a.npairs), dim3(256), lds, s, a);                                \
+      DCNN_LAUNCH_CHECK();                                                                              \
+      return;                                                                                           \
+    }
+    DCNN_HW2(16, 8, 1, 3)  // 3 x 48 KB
+    DCNN_HW2(8, 8, 2, 2)   // 2 x 56 KB (three stages would need 168 KB)
+#undef DCNN_HW2
+  }
 #define DCNN_HW(TW_, TH_, IMG_, NS_)                                                                    \
   if (a.TW == TW_ && a.TH == TH_ && a.IMG == IMG_ && stages == NS_) {                                   \
     auto k = hwgrad_kernel<TW_, TH_, IMG_, NS_>;                                                        \

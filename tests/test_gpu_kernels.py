@@ -106,7 +106,18 @@ def test_hconv_layer4_shape(hip):
     (4, 64, 32, 32, 64), (6, 128, 16, 16, 64), (4, 64, 16, 16, 192), (8, 256, 8, 8, 128), (16, 128, 4, 4, 256),
     (3, 64, 16, 48, 64),
 ])
-def test_halo_wgrad(hip, case):
+@pytest.mark.parametrize("version", [2, 1])
+def test_halo_wgrad(hip, case, version):
+    """Both halo wgrad generations (2: tap-shift-invariant LDS addressing, 1: first kernel)."""
+    from dcnn_amd.ops._ext import kernels
+    kernels().hwgrad_set_version(version)
+    try:
+        _halo_wgrad_case(hip, case)
+    finally:
+        kernels().hwgrad_set_version(2)
+
+
+def _halo_wgrad_case(hip, case):
     from dcnn_amd.ops._ext import kernels
     N, Ci, H, W, Co = case
     assert kernels().hwgrad_supported(N, H, W, Ci, Co, 9)
