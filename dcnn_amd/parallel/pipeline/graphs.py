@@ -28,6 +28,8 @@ from typing import Dict, List, Optional, Tuple
 
 import torch
 
+from ...runtime.capture import capture_guard
+
 from ...nn.sequential import Sequential, _all_layers
 
 _CAPTURE_LOCK = threading.Lock()  # one capture per process at a time
@@ -83,7 +85,7 @@ class StageGraphs:
         prof = m.enable_profiling_
         m.enable_profiling_ = False  # per-layer timing events are not capturable
         try:
-            with _CAPTURE_LOCK, torch.cuda.stream(self.capture_stream):
+            with _CAPTURE_LOCK, capture_guard(), torch.cuda.stream(self.capture_stream):
                 g.capture_begin(capture_error_mode="thread_local")
                 try:
                     out = fn(static_in)

@@ -20,6 +20,8 @@ import os
 from typing import List, Optional
 
 import torch
+
+from .capture import capture_guard
 import torch.distributed as dist
 
 
@@ -148,7 +150,7 @@ class TrainStep:
         active = self.dp.active
         for k, (hi, lo) in enumerate(segs):
             g = torch.cuda.CUDAGraph()
-            with torch.cuda.graph(g, pool=pool, stream=self._capture_stream()):
+            with capture_guard(), torch.cuda.graph(g, pool=pool, stream=self._capture_stream()):
                 if k == 0:
                     self.opt.clear_gradients()
                     out = self.dp.forward(self._static_x)
@@ -170,7 +172,7 @@ class TrainStep:
             self.graphs.append(g)
         if active:
             g = torch.cuda.CUDAGraph()
-            with torch.cuda.graph(g, pool=pool, stream=self._capture_stream()):
+            with capture_guard(), torch.cuda.graph(g, pool=pool, stream=self._capture_stream()):
                 self.opt.launch_step()
             self.graphs.append(g)
         torch.cuda.synchronize()
@@ -185,7 +187,7 @@ class TrainStep:
         m.enable_profiling_ = False
         g = torch.cuda.CUDAGraph()
         try:
-            with torch.cuda.graph(g, stream=self._capture_stream(), capture_error_mode="thread_local"):
+            with capture_guard(), torch.cuda.graph(g, stream=self._capture_stream(), capture_error_mode="thread_local"):
                 self.opt.clear_gradients()
                 out = self.dp.forward(self._static_x)
                 loss, grad, correct = self.loss_fn.loss_and_grad(out, self._static_y)

@@ -20,6 +20,7 @@ def test_flow_task_ordering_and_timing():
     g = get_gpu(0)
     flow = g.get_flow("worker", )
     x = torch.randn(1 << 22, device="cuda")
+    flow.wait(create_task(g, "default"))    # the worker flow reads x: order it after x's producer
     t0 = create_task(g, "worker", timing=True)
     with torch.cuda.stream(flow.stream):
         y = x * 2 + 1
