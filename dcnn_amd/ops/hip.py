@@ -10,6 +10,7 @@ training step can be captured into a hipGraph.
 from __future__ import annotations
 
 import contextlib
+import functools
 import os
 import threading
 
@@ -57,14 +58,16 @@ def _nbytes(t):
     return t.numel() * t.element_size()
 
 
+@functools.lru_cache(maxsize=1024)
 def _fwd_taps(C, W, KH, KW, ph, pw):
-    """Tap list of a forward conv: (dy, dx, src element offset, B-row element offset)."""
+    """Tap list of a forward conv: (dy, dx, src element offset, B-row element offset). Cached per
+    geometry (eager launches rebuild no Python lists); the tuple is never mutated."""
     taps = []
     for ky in range(KH):
         for kx in range(KW):
             dy, dx = ky - ph, kx - pw
             taps.append((dy, dx, (dy * W + dx) * C, (ky * KW + kx) * C))
-    return taps
+    return tuple(taps)
 
 
 def _g2_ok(Cs, N):
@@ -511,6 +514,31 @@ _G2_GROUP = os.environ.get("DCNN_G2_GROUP", "1") != "0"  # strided dgrad phases 
 _BNB_POOL = os.environ.get("DCNN_BNB_POOL", "1") != "0"  # the stem max-pool part of the fusion
 
 
+@functools.lru_cache(maxsize=1024)
+def _dgrad_classes(H, W, OW, Co, KH, KW, sh, sw, ph, pw):
+    """Stride-phase decomposition of a dgrad: ((ry, rx, GH, GW, taps) with taps, ...) and the
+    phases no tap reaches; taps = (dy offset, dx offset, dy element offset, B-row offset).
+    Cached per geometry (tuples, never mutated)."""
+    classes, empty = [], []
+    for ry in range(sh):
+        for rx in range(sw):
+            GH, GW = (H - ry + sh - 1) // sh, (W - rx + sw - 1) // sw
+            if GH <= 0 or GW <= 0:
+                continue
+            taps = []
+            for ky in range(KH):
+                if (ry + ph - ky) % sh:
+                    continue
+                dyo = (ry + ph - ky) // sh
+                for kx in range(KW):
+                    if (rx + pw - kx) % sw:
+                        continue
+                    dxo = (rx + pw - kx) // sw
+                    taps.append((dyo, dxo, (dyo * OW + dxo) * Co, (ky * KW + kx) * Co))
+            (classes if taps else empty).append((ry, rx, GH, GW, tuple(taps)))
+    return tuple(classes), tuple(empty)
+
+
 def conv2d_dgrad(dy, wt, x_shape, stride, pad, *, residual=None, bnb=None):
     """dx = conv_transpose(dy, w) [+ residual];  wt = conv_weight_t(w).
 
@@ -540,29 +568,8 @@ def conv2d_dgrad(dy, wt, x_shape, stride, pad, *, residual=None, bnb=None):
         K.gemm_nt(dy.data_ptr(), wt.data_ptr(), dx.data_ptr(), N * H * W, Ci, Kd, 0, Kd, Ci, CONV_DGRAD,
                   N, OH, OW, Co, H, W, KH, KW, sh, sw, ph, pw, 0, ptr(residual), 0, 0, 0, stream_ptr())
         return dx
-    classes = []
-    empty = []  # phase classes no tap reaches: (ry, rx, GH, GW, [])
-    empty_class = False
-    for ry in range(sh):
-        for rx in range(sw):
-            GH, GW = (H - ry + sh - 1) // sh, (W - rx + sw - 1) // sw
-            if GH <= 0 or GW <= 0:
-                continue
-            taps = []
-            for ky in range(KH):
-                if (ry + ph - ky) % sh:
-                    continue
-                dyo = (ry + ph - ky) // sh
-                for kx in range(KW):
-                    if (rx + pw - kx) % sw:
-                        continue
-                    dxo = (rx + pw - kx) // sw
-                    taps.append((dyo, dxo, (dyo * OW + dxo) * Co, (ky * KW + kx) * Co))
-            if taps:
-                classes.append((ry, rx, GH, GW, taps))
-            else:
-                empty_class = True
-                empty.append((ry, rx, GH, GW, []))
+    classes, empty = _dgrad_classes(H, W, OW, Co, KH, KW, sh, sw, ph, pw)
+    empty_class = bool(empty)
     odt = F32 if f32 else BF16
     allc = classes + empty
     if (not f32 and empty_class and len(classes) > 1 and _G2_GROUP and len(allc) <= 4
