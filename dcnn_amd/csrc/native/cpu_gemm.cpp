@@ -240,6 +240,37 @@ void gemm_accumulate(const F& fam, bool ta, bool tb, long M, long N, long k0, lo
                      const T* B, long ldb, T* C, long ldc, bool serial) {
   constexpr int MR = F::MR, NR = F::NR, MC = F::MC, KC = F::KC, NC = F::NC;
   std::vector<T> bpack, apack;
+  if (!serial && M <= MC) {
+    // one row block (small M, e.g. a conv's output channels over the whole batch's pixels): no
+    // packed B panel is reused by another row block, so there is nothing to gain from NC
+    // blocking or a shared B pack. A (M x kc) is packed once; ONE parallel region per K panel,
+    // each task packing its own B panels into a thread-local buffer right before using them
+    // (the NC-blocked schedule took two pool dispatches per 4096 columns: 40x slower on
+    // 8 x 36864 x 25).
+    // K panels of up to 4 x KC: one pool dispatch per panel is the dominant cost at these sizes
+    // (an A panel of MC x 4KC and a 4KC x NR B panel still fit the L2)
+    for (long pc = k0; pc < k1; pc += 4 * KC) {
+      const long kc = std::min<long>(4 * KC, k1 - pc);
+      apack.resize((size_t)((M + MR - 1) / MR) * MR * kc);
+      pack_a<T, MR>(A, lda, ta, 0, M, pc, kc, apack.data());
+      const long npan = (N + NR - 1) / NR;
+      const long tasks = std::min<long>(npan, (long)get_num_threads() * 4);
+      ThreadPool::instance().run(tasks, [&](long task) {
+        thread_local std::vector<T> bl;
+        bl.resize((size_t)kc * NR);
+        const long q0 = task * npan / tasks, q1 = (task + 1) * npan / tasks;
+        for (long q = q0; q < q1; ++q) {
+          const int cols = (int)std::min<long>(NR, N - q * NR);
+          pack_b_panel<T, NR>(B, ldb, tb, pc, kc, q * NR, cols, bl.data());
+          for (long p = 0; p < M; p += MR) {
+            const int rows = (int)std::min<long>(MR, M - p);
+            fam.micro(kc, apack.data() + p * kc, bl.data(), C + p * ldc + q * NR, ldc, alpha, rows, cols);
+          }
+        }
+      });
+    }
+    return;
+  }
   for (long jc = 0; jc < N; jc += NC) {
     const long nc = std::min<long>(NC, N - jc);
     const long npan = (nc + NR - 1) / NR;
@@ -299,15 +330,20 @@ void gemm_impl(const F& fam, bool ta, bool tb, long M, long N, long K, T alpha, 
   // small output, long reduction: fixed K slices into private partials, summed in slice order
   const long slices = std::min<long>(16, K / (4L * F::KC));
   if (slices >= 2 && M * N <= 96L * 1024) {  // (inside a parallel region the slices run serially)
-    std::vector<T> part((size_t)slices * M * N, T(0));
+    // the calling thread's reusable partials buffer (no per-call allocation / page faults); the
+    // pool tasks use it through this pointer (a thread_local named inside the lambda would be
+    // each worker's own instance)
+    thread_local std::vector<T> part_tl;
+    part_tl.assign((size_t)slices * M * N, T(0));
+    T* const part_p = part_tl.data();
     ThreadPool::instance().run(slices, [&](long s) {
       const long k0 = s * K / slices, k1 = (s + 1) * K / slices;
-      gemm_accumulate(fam, ta, tb, M, N, k0, k1, alpha, A, lda, B, ldb, part.data() + s * M * N, N, true);
+      gemm_accumulate(fam, ta, tb, M, N, k0, k1, alpha, A, lda, B, ldb, part_p + s * M * N, N, true);
     });
     parallel_for(0, M, std::max(1L, 4096 / N), [&](long lo, long hi) {
       for (long i = lo; i < hi; ++i)
         for (long s = 0; s < slices; ++s) {
-          const T* pr = part.data() + (s * M + i) * N;
+          const T* pr = part_p + (s * M + i) * N;
           T* cr = C + i * ldc;
           for (long j = 0; j < N; ++j) cr[j] += pr[j];
         }

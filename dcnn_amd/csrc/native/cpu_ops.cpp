@@ -320,7 +320,10 @@ void col2im(const T* col, T* x, int N, int C, int H, int W, int KH, int KW, int 
 
 // ------------------------------------------------------------------ convolution
 namespace {
-template <typename T>
+// per-thread reusable buffers (slot 0: per-sample im2col panels; slots 1/2: the batched
+// schedule's column matrix and channel-major output): no per-call allocation, zeroing or page
+// faults of multi-MB vectors
+template <typename T, int SLOT = 0>
 std::vector<T>& scratch(size_t n) {
   thread_local std::vector<T> buf;
   if (buf.size() < n) buf.resize(n);
@@ -371,7 +374,8 @@ void conv2d_fwd(const T* x, const T* w, const T* bias, T* y, int N, int C, int H
   const long L = (long)OH * OW, K = (long)C * KH * KW;
   const bool direct = is_1x1_direct(KH, KW, SH, SW, PH, PW);
   if (conv_batched<T>(N, K, L) && N > 1) {
-    std::vector<T> col((size_t)K * N * L), yc((size_t)Co * N * L);
+    auto& col = scratch<T, 1>((size_t)K * N * L);
+    auto& yc = scratch<T, 2>((size_t)Co * N * L);
     im2col(x, col.data(), N, C, H, W, KH, KW, SH, SW, PH, PW);
     gemm(false, false, Co, N * L, K, T(1), w, K, col.data(), N * L, T(0), yc.data(), N * L);
     swap01(yc.data(), y, Co, N, L);
@@ -414,7 +418,8 @@ void conv2d_bwd(const T* x, const T* w, const T* dy, T* dx, T* dw, T* db, int N,
     });
   }
   if (conv_batched<T>(N, K, L) && N > 1) {
-    std::vector<T> col((size_t)K * N * L), dyc((size_t)Co * N * L);
+    auto& col = scratch<T, 1>((size_t)K * N * L);
+    auto& dyc = scratch<T, 2>((size_t)Co * N * L);
     im2col(x, col.data(), N, C, H, W, KH, KW, SH, SW, PH, PW);
     swap01(dy, dyc.data(), N, Co, L);  // [Co][N*L]
     gemm(false, true, Co, K, N * L, T(1), dyc.data(), N * L, col.data(), N * L, T(1), dw, K);
