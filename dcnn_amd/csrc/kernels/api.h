@@ -83,6 +83,7 @@ int hconv_splits(int NB, int H, int W, int Cs, int N, int ntaps);
 int hconv_tiles(int NB, int H, int W, int N);
 int hconv_tile_elems(int NB, int H, int W, int N);
 void hconv_set_split_target(int t);  // workgroups the split-K decision aims for (0: never split)
+void hconv_set_wide(int on);         // 256 x 64 tiles (4 x 1 waves) for 64-channel outputs
 bool hconv_supported(int NB, int H, int W, int Cs, int N, int ntaps);
 int hconv_stat_rows(int NB, int H, int W, int N);
 // halo-tiled stride-1 weight gradient (hwgrad.hip): slab[split][Co][t*Cs + c] = partial dW

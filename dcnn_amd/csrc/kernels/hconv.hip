@@ -60,7 +60,10 @@ __device__ __forceinline__ int hoff(int row, int ch) { return row * 128 + ((ch ^
 // 64-channel chunk: nothing to prefetch), NBS weight stages (NBS - 1 steps in flight)
 template <int BM, int BN, int TPS, int NHB, int NBS, bool F32O = false>
 struct HC {
-  static constexpr int TM = BM / 32, TN = BN / 32;      // 16x16 subtiles per wave (2x2 waves)
+  // wave layout: 2 x 2 waves, or 4 x 1 (all four waves along M) for tall 256 x 64 tiles, where
+  // each wave then owns a 64 x 64 block (twice the MFMAs per LDS fragment read of a 2 x 2 split)
+  static constexpr int WN = (BM >= 4 * BN) ? 1 : 2, WM = 4 / WN;
+  static constexpr int TM = BM / (16 * WM), TN = BN / (16 * WN);  // 16x16 subtiles per wave
   static constexpr int BTAP = BN * 128;                  // bytes of one tap's weight slice
   static constexpr int BST = TPS * BTAP;                 // bytes per weight stage
   static constexpr int B_INS = BN / 32;                  // glds per wave per tap slice
@@ -87,21 +90,23 @@ __device__ __forceinline__ void load_row8(const char* src, float* f) {
 }
 
 template <int BM, int BN, bool F32O>
-__device__ __forceinline__ void hc_epilogue(const HConvArgs& p, f32x4 (&acc)[BM / 32][BN / 32], char* smem, int n0,
+__device__ __forceinline__ void hc_epilogue(const HConvArgs& p,
+                                            f32x4 (&acc)[HC<BM, BN, 1, 1, 2, F32O>::TM][HC<BM, BN, 1, 1, 2, F32O>::TN],
+                                            char* smem, int n0,
                                             int tm, int img0, int y0, int x0) {
   using T = HC<BM, BN, 1, 1, 2, F32O>;
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
-  const int wm = wid >> 1, wn = wid & 1;
+  const int wm = wid / T::WN, wn = wid % T::WN;
   // ---- epilogue 1: acc (+bias) -> bf16 LDS tile [BM][BN] ----
 #pragma unroll
   for (int j = 0; j < T::TN; ++j) {
-    const int col = wn * (BN / 2) + j * 16 + (lane & 15);
+    const int col = wn * (BN / T::WN) + j * 16 + (lane & 15);
     const float bv = p.bias ? p.bias[n0 + col] : 0.f;
 #pragma unroll
     for (int i = 0; i < T::TM; ++i)
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
-        const int row = wm * (BM / 2) + i * 16 + (lane >> 4) * 4 + r;
+        const int row = wm * (BM / T::WM) + i * 16 + (lane >> 4) * 4 + r;
         if (F32O)
           *reinterpret_cast<float*>(smem + row * T::EPI_PITCH + col * 4) = acc[i][j][r] + bv;
         else
@@ -220,7 +225,7 @@ __global__ void __launch_bounds__(256, 1) hconv_kernel(HConvArgs p) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   struct { int HALO; } T_rt{p.HPR * 128};
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
-  const int wm = wid >> 1, wn = wid & 1;
+  const int wm = wid / T::WN, wn = wid % T::WN;
   const int tiles_n = p.N / BN;
   const int SPL = p.splits;                      // workgroups per output tile (split-K)
   const int lt0 = xcd_remap_h(blockIdx.x, gridDim.x);
@@ -244,10 +249,11 @@ __global__ void __launch_bounds__(256, 1) hconv_kernel(HConvArgs p) {
   // ---- halo loader: per-lane pixel base offsets for its rows (fixed across chunks) ----
   const int hch = lane & 7;                               // physical chunk slot
   const int HNI = (HP + 31) / 32;                         // glds per wave per halo chunk (8 rows each)
-  unsigned h_base[10];
-  int h_row[10];
+  constexpr int HMAX = BM >= 256 ? 12 : 10;  // halo loads per lane (the wide tiles' 18x18 halo: 11)
+  unsigned h_base[HMAX];
+  int h_row[HMAX];
 #pragma unroll
-  for (int j = 0; j < 10; ++j) {
+  for (int j = 0; j < HMAX; ++j) {
     h_base[j] = kOOBh;
     h_row[j] = 0;
     if (j < HNI) {
@@ -265,7 +271,7 @@ __global__ void __launch_bounds__(256, 1) hconv_kernel(HConvArgs p) {
   auto load_halo = [&](int buf, int c0) {
     char* Hs = smem + buf * T_rt.HALO;
 #pragma unroll
-    for (int j = 0; j < 10; ++j) {
+    for (int j = 0; j < HMAX; ++j) {
       if (j < HNI) {
         const int lch = hch ^ (h_row[j] & 7);
         const unsigned voff = h_base[j] == kOOBh ? kOOBh : h_base[j] + (unsigned)((c0 + lch * 8) * 2);
@@ -298,7 +304,7 @@ __global__ void __launch_bounds__(256, 1) hconv_kernel(HConvArgs p) {
   int arow0[T::TM];
 #pragma unroll
   for (int i = 0; i < T::TM; ++i) {
-    const int m = wm * (BM / 2) + i * 16 + (lane & 15);   // tile-local output row
+    const int m = wm * (BM / T::WM) + i * 16 + (lane & 15);   // tile-local output row
     const int tpx = p.TH * p.TW;
     const int im = m / tpx, r2 = m - im * tpx;
     arow0[i] = im * HPI + (r2 / p.TW + 1) * HW2 + (r2 % p.TW + 1);
@@ -358,7 +364,7 @@ __global__ void __launch_bounds__(256, 1) hconv_kernel(HConvArgs p) {
         for (int i = 0; i < T::TM; ++i) a[kk][i] = *reinterpret_cast<const bf16x8*>(Hs + hoff(arow0[i] + toff, ch));
 #pragma unroll
         for (int j = 0; j < T::TN; ++j)
-          b[kk][j] = *reinterpret_cast<const bf16x8*>(Bs + hoff(wn * (BN / 2) + j * 16 + (lane & 15), ch));
+          b[kk][j] = *reinterpret_cast<const bf16x8*>(Bs + hoff(wn * (BN / T::WN) + j * 16 + (lane & 15), ch));
       }
       __builtin_amdgcn_s_setprio(1);
 #pragma unroll
@@ -376,7 +382,7 @@ __global__ void __launch_bounds__(256, 1) hconv_kernel(HConvArgs p) {
     bcur = bcur == NBS - 1 ? 0 : bcur + 1;
   }
 
-  if (SPL > 1) {
+  if constexpr (T::WN == 2) if (SPL > 1) {  // (the 4 x 1 wide tiles never split: host)
     // split-K hand-off without fences (MI355X_MICROARCH "Valid forms" row 1): every partial is
     // stored with agent-scope (sc1) 8-byte stores, each wave drains them, one lane adds to the
     // tile's ticket after the workgroup barrier, and the workgroup whose add returns SPL - 1
@@ -441,15 +447,29 @@ static bool hconv_geometry(int NB, int H, int W, int BM, int* TH, int* TW, int* 
   if (th > H) th = H;
   if (th <= 0 || H % th || BM % (th * tw)) return false;
   const int img = BM / (th * tw);
-  if ((img * (th + 2) * (tw + 2)) > 320) return false;
+  if ((img * (th + 2) * (tw + 2)) > 384) return false;  // halo loader: <= 12 x 32 rows
   *TH = th; *TW = tw; *IMG = img;
   (void)NB;
   return true;
 }
 
+// 256 x 64 tiles (4 x 1 waves) for 64-channel outputs on 16x16-divisible maps: opt-in
+// (DCNN_HCONV_WIDE=1), measured no faster than 128 x 64 on the ResNet-18 layer-1 convs
+// (profiles/experiment_hconv_variants.md)
+static int g_hconv_wide = [] {
+  const char* e = getenv("DCNN_HCONV_WIDE");
+  return e ? atoi(e) : 0;
+}();
+void hconv_set_wide(int on) { g_hconv_wide = on; }
+
 static void hconv_pick(const HConvArgs& a, int* bm, int* bn) {
   // prefer 128 x 128 when it still gives >= ~1.5 workgroups per CU, else shrink
   auto tiles = [&](int m, int n) { return (long)((a.NB * a.H * a.W + m - 1) / m) * (a.N / n); };
+  if (g_hconv_wide && a.N == 64 && a.W % 16 == 0 && a.H % 16 == 0 && tiles(256, 64) >= 512) {
+    *bm = 256;
+    *bn = 64;
+    return;
+  }
   *bm = 128;
   *bn = (a.N % 128 == 0 && tiles(128, 128) >= 384) ? 128 : 64;
   if (tiles(*bm, *bn) < 384) *bm = 64;
@@ -579,11 +599,13 @@ void hconv(HConvArgs a, hipStream_t s) {
   }
   if (a.Cf) {
     if (a.bnb.x) throw std::runtime_error("hconv: no backward-BN fusion with fp32 output");
+    if (bm == 256 && bn == 64) return launch_hconv<256, 64, true>(a, s);
     if (bm == 128 && bn == 128) return launch_hconv<128, 128, true>(a, s);
     if (bm == 128 && bn == 64) return launch_hconv<128, 64, true>(a, s);
     if (bm == 64 && bn == 128) return launch_hconv<64, 128, true>(a, s);
     return launch_hconv<64, 64, true>(a, s);
   }
+  if (bm == 256 && bn == 64) return launch_hconv<256, 64, false>(a, s);
   if (bm == 128 && bn == 128) return launch_hconv<128, 128, false>(a, s);
   if (bm == 128 && bn == 64) return launch_hconv<128, 64, false>(a, s);
   if (bm == 64 && bn == 128) return launch_hconv<64, 128, false>(a, s);

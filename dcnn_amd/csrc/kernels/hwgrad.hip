@@ -279,7 +279,8 @@ struct HWGeo2 {
   static constexpr int STAGE = PT * 128 + HPR * 128;
   static constexpr int EPI_TAPS = (2 * STAGE) / (64 * 68 * 4);
   static_assert(TPX * IMG == PT, "tile must hold 128 pixels");
-  static_assert(TW % 8 == 0, "8 consecutive pixels of a read group must share an image row");
+  // (TW = 4: a 32-lane read group spans two image rows, 8 halo rows apart: 2-way LDS conflicts
+  // on those reads, accepted — the addressing savings are the same)
 };
 
 __device__ __forceinline__ bf16x4 tr4_at(const char* addr) {
@@ -395,39 +396,37 @@ __global__ void __launch_bounds__(256, 1) hwgrad2_kernel(HWArgs p) {
   for (int it = 0; it < nt; ++it) {
     if (it + NS - 1 < nt) load_tile(cur == 0 ? NS - 1 : cur - 1, tbeg + it + NS - 1);
     const char* S0 = smem + cur * STAGE;
-    bf16x8 a[2][4], b[2][9];
-    auto read_step = [&](int kk, bf16x8* av, bf16x8* bv) {
+    // A double-buffered; each tap's B fragment re-read in place right after the step's 4 MFMAs
+    // that consume it (9 live B fragments instead of 18: the multi-image geometries otherwise
+    // spill through AGPRs)
+    bf16x8 a[2][4], b[9];
+    auto read_a = [&](int kk, bf16x8* av) {
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
         const char* q = S0 + abase[i] + kk * 4096;
         const bf16x4 lo = tr4_at(q), hi = tr4_at(q + 2048);
         av[i] = bf16x8{lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
       }
-#pragma unroll
-      for (int t = 0; t < 9; ++t) {
-        const int dy = t / 3, dx = t % 3;  // dy index 0..2 = dy + 1
-        const bf16x4 lo = tr4_at(S0 + bbase[kk * 2][dx] + dy * HW2P * 128);
-        const bf16x4 hi = tr4_at(S0 + bbase[kk * 2 + 1][dx] + dy * HW2P * 128);
-        bv[t] = bf16x8{lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
-      }
     };
-    read_step(0, a[0], b[0]);
+    auto read_b = [&](int kk, int t) {
+      const int dy = t / 3, dx = t % 3;
+      const bf16x4 lo = tr4_at(S0 + bbase[kk * 2][dx] + dy * HW2P * 128);
+      const bf16x4 hi = tr4_at(S0 + bbase[kk * 2 + 1][dx] + dy * HW2P * 128);
+      return bf16x8{lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+    };
+    read_a(0, a[0]);
+#pragma unroll
+    for (int t = 0; t < 9; ++t) b[t] = read_b(0, t);
 #pragma unroll
     for (int kk = 0; kk < 4; ++kk) {
       const int c = kk & 1;
       __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0)
-      if (kk + 1 < 4) read_step(kk + 1, a[c ^ 1], b[c ^ 1]);
+      if (kk + 1 < 4) read_a(kk + 1, a[c ^ 1]);
 #pragma unroll
-      for (int t = 0; t < 9; ++t)
+      for (int t = 0; t < 9; ++t) {
 #pragma unroll
-        for (int i = 0; i < 4; ++i) acc[i][t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[c][i], b[c][t], acc[i][t], 0, 0, 0);
-      if (kk + 1 < 4) {
-#pragma unroll
-        for (int g = 0; g < 26; ++g) {
-          __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);  // MFMA
-          __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);  // DS read
-        }
-        __builtin_amdgcn_sched_group_barrier(0x008, 10, 0);
+        for (int i = 0; i < 4; ++i) acc[i][t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[c][i], b[t], acc[i][t], 0, 0, 0);
+        if (kk + 1 < 4) b[t] = read_b(kk + 1, t);
       }
     }
     if (do_bias) {
@@ -527,6 +526,11 @@ static int g_hwgrad_version = [] {
   return e ? atoi(e) : 2;
 }();
 void hwgrad_set_version(int v) { g_hwgrad_version = v; }
+// second-generation kernel on 4x4 maps too (DCNN_HWGRAD4=0: keep the first kernel there)
+static int g_hwgrad4 = [] {
+  const char* e = getenv("DCNN_HWGRAD4");
+  return e ? atoi(e) : 1;
+}();
 
 void hwgrad(HWArgs a, int splits, hipStream_t s) {
   if (!hwgrad_supported(a.NB, a.H, a.W, a.Cs, a.Co, a.ntaps)) throw std::runtime_error("hwgrad: unsupported shape");
@@ -560,7 +564,7 @@ void hwgrad(HWArgs a, int splits, hipStream_t s) {
   const int ver = g_hwgrad_version;
   bool std_taps = a.ntaps == 9;
   for (int t = 0; t < a.ntaps && std_taps; ++t) std_taps = a.tap_dy[t] == t / 3 - 1 && a.tap_dx[t] == t % 3 - 1;
-  if (ver == 2 && std_taps && a.TW % 8 == 0 && !a.dbg) {
+  if (ver == 2 && std_taps && !a.dbg) {
 #define DCNN_HW2(TW_, TH_, IMG_, NS_)                                                                   \
     if (a.TW == TW_ && a.TH == TH_ && a.IMG == IMG_) {                                                  \
       auto k = hwgrad2_kernel<TW_, TH_, IMG_, NS_>;                                                     \
@@ -572,6 +576,14 @@ void hwgrad(HWArgs a, int splits, hipStream_t s) {
     }
     DCNN_HW2(16, 8, 1, 3)  // 3 x 48 KB
     DCNN_HW2(8, 8, 2, 2)   // 2 x 56 KB (three stages would need 168 KB)
+    if (g_hwgrad_version == 2 && a.TW == 4 && a.TH == 4 && a.IMG == 8 && g_hwgrad4 != 0) {
+      auto k = hwgrad2_kernel<4, 4, 8, 2>;  // 2 x 64 KB
+      const int lds = 2 * HWGeo2<4, 4, 8>::STAGE;
+      DCNN_HIP_CHECK(hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, lds));
+      hipLaunchKernelGGL(k, dim3(grid, a.npairs), dim3(256), lds, s, a);
+      DCNN_LAUNCH_CHECK();
+      return;
+    }
 #undef DCNN_HW2
   }
 #define DCNN_HW(TW_, TH_, IMG_, NS_)                                                                    \

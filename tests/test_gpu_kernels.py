@@ -821,3 +821,36 @@ def test_bn_backward_eval_mode_kernels(hip, relu):
     assert rel_err(db, d.sum((0, 2, 3))) < 1e-4
     if relu:
         assert rel_err(dmask, d) < 1e-2
+
+
+@pytest.mark.parametrize("case", [(128, 64, 32, 32, 64), (32, 64, 64, 64, 64), (128, 128, 32, 32, 64)])
+def test_hconv_wide_tiles(hip, case):
+    """256 x 64 halo-conv tiles (4 x 1 wave layout) == the 128 x 64 tiles: forward (+stats,
+    residual, ReLU) bit-identical per element (same K order), dgrad too; statistics close."""
+    from dcnn_amd.ops._ext import kernels
+    K = kernels()
+    N, C, H, W, Co = case
+    torch.manual_seed(6)
+    x = torch.randn(N, C, H, W).cuda().to(torch.bfloat16).contiguous(memory_format=CL)
+    w = (torch.randn(Co, C, 3, 3) / math.sqrt(9 * C)).cuda().to(torch.bfloat16).contiguous(memory_format=CL)
+    r = torch.randn(N, Co, H, W).cuda().to(torch.bfloat16).contiguous(memory_format=CL)
+    b = torch.randn(Co).cuda()
+    dy = torch.randn(N, Co, H, W).cuda().to(torch.bfloat16).contiguous(memory_format=CL)
+    wt = hip.conv_weight_t(w)
+    outs = []
+    try:
+        for wide in (1, 0):
+            K.hconv_set_wide(wide)
+            y, part = hip.conv2d_fwd(x, w, b, (1, 1), (1, 1), stats=True, residual=r, relu=True)
+            st = hip.bn_stats(y, part)
+            dx = hip.conv2d_dgrad(dy, wt, x.shape, (1, 1), (1, 1)) if C == 64 else None
+            outs.append((y, st.final().clone(), dx))
+    finally:
+        K.hconv_set_wide(0)
+    (y1, s1, d1), (y0, s0, d0) = outs
+    assert torch.equal(y1, y0)
+    assert rel_err(s1, s0) < 1e-5
+    if d1 is not None:
+        assert torch.equal(d1, d0)
+    ref = F.relu(F.conv2d(x.float().cpu(), w.float().cpu(), b.cpu(), 1, 1) + r.float().cpu())
+    assert rel_err(y1, ref) < 1e-2
