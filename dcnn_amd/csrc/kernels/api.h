@@ -83,6 +83,7 @@ int hconv_splits(int NB, int H, int W, int Cs, int N, int ntaps);
 int hconv_tiles(int NB, int H, int W, int N);
 int hconv_tile_elems(int NB, int H, int W, int N);
 void hconv_set_split_target(int t);  // workgroups the split-K decision aims for (0: never split)
+void bn_set_vectorised(int on);   // bf16 BatchNorm apply passes on the vectorised kernels (default on)
 void hconv_set_wide(int on);         // 256 x 64 tiles (4 x 1 waves) for 64-channel outputs
 bool hconv_supported(int NB, int H, int W, int Cs, int N, int ntaps);
 int hconv_stat_rows(int NB, int H, int W, int N);
@@ -137,7 +138,7 @@ void splitk_reduce2(const float* slab, float* out, long n, const float* bslab, f
 
 // many split-K slab reductions in one launch (grad += sum over splits), kernel-argument table
 constexpr int kMaxRed = 48;
-struct RedEnt { const float* slab; float* out; long n; int splits, unit0, chunks, groups, vec, pad_; };
+struct RedEnt { const float* slab; float* out; long n; int splits, unit0, chunks, groups, vec, wpc; };  // wpc: waves per chunk
 struct MultiRed { int count; RedEnt e[kMaxRed]; };
 void multi_splitk_reduce(MultiRed t, hipStream_t s);
 

@@ -114,6 +114,7 @@ PYBIND11_MODULE(_kernels, m) {
   m.def("hconv_tiles", &hconv_tiles);
   m.def("hconv_set_split_target", &hconv_set_split_target);
   m.def("hconv_set_wide", &hconv_set_wide);
+  m.def("bn_set_vectorised", &bn_set_vectorised);
   m.def("hconv_tile_elems", &hconv_tile_elems);
   m.def("hwgrad",
         [](uintptr_t dY, uintptr_t X, uintptr_t slab, uintptr_t bias_slab, unsigned dy_bytes, unsigned x_bytes, int NB,

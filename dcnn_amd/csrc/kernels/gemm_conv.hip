@@ -22,6 +22,8 @@
 // fragment reads are bank-conflict free; global->LDS staging is register-pipelined (tile k+1
 // loads in flight while tile k is multiplied, one barrier per K-step); the block index is
 // remapped so that each XCD (private L2) works on a contiguous range of output tiles.
+#include <algorithm>
+
 #include "common.h"
 #include "api.h"
 
@@ -561,23 +563,25 @@ __global__ void splitk_reduce_kernel(SplitkSeg a, SplitkSeg b, int gxa, int spli
 }
 
 // Deferred split-K reduction: the fp32 slabs of many weight gradients summed into their
-// gradients in ONE launch (api.h MultiRed). A work unit is (entry, chunk of 256 floats); wave w
-// sums splits {32g + 8w .. 32g + 8w + 7} for every group g in order, all 8 loads of a group in
-// flight, the 4 waves meet in LDS in wave order and wave 0 adds into the gradient. Fixed
-// summation order throughout: bit-reproducible, no atomics.
+// gradients in ONE launch (api.h MultiRed). A work unit is (entry, 4 / wpc chunks of 256 floats):
+// each chunk gets wpc waves (1, 2 or 4 by split count, so few-split slabs do not leave waves
+// idle), wave j of a chunk sums splits {8 wpc g + 8j .. + 7} for every group g in order with all 8
+// loads of a group in flight, the chunk's waves meet in LDS in wave order and its first wave adds
+// into the gradient. Entries run longest (most groups) first so the many-split slabs' long
+// blocks are not the launch's tail. Fixed summation order throughout: bit-reproducible, no atomics.
 __global__ void __launch_bounds__(256) multi_splitk_reduce_kernel(MultiRed t) {
   int k = 0;
   while (k + 1 < t.count && (int)blockIdx.x >= t.e[k + 1].unit0) ++k;
   const float* slab = t.e[k].slab;
   float* out = t.e[k].out;
   const long n = t.e[k].n;
-  const int splits = t.e[k].splits, groups = t.e[k].groups, vec = t.e[k].vec;
-  const int chunk = blockIdx.x - t.e[k].unit0;
+  const int splits = t.e[k].splits, groups = t.e[k].groups, vec = t.e[k].vec, wpc = t.e[k].wpc;
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-  __shared__ float4 red[3][64];
+  const int chunk = (blockIdx.x - t.e[k].unit0) * (4 / wpc) + w / wpc, wj = w % wpc;
+  __shared__ float4 red[4][64];
   float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
   for (int g = 0; g < groups; ++g) {
-    const int s0 = g * 32 + w * 8;
+    const int s0 = g * 8 * wpc + wj * 8;
     if (vec) {  // n % 4 == 0: lane owns 4 consecutive floats
       const long i4 = (long)chunk * 64 + lane;
       const bool ok = i4 * 4 < n;
@@ -598,12 +602,14 @@ __global__ void __launch_bounds__(256) multi_splitk_reduce_kernel(MultiRed t) {
       for (int u = 0; u < 8; ++u) acc.x += v[u];
     }
   }
-  if (w > 0) red[w - 1][lane] = acc;
-  __syncthreads();
-  if (w > 0) return;
-#pragma unroll
-  for (int j = 0; j < 3; ++j) {
-    acc.x += red[j][lane].x; acc.y += red[j][lane].y; acc.z += red[j][lane].z; acc.w += red[j][lane].w;
+  if (wpc > 1) {
+    red[w][lane] = acc;
+    __syncthreads();
+    if (wj > 0) return;
+    for (int j = 1; j < wpc; ++j) {
+      const float4 r = red[w + j][lane];
+      acc.x += r.x; acc.y += r.y; acc.z += r.z; acc.w += r.w;
+    }
   }
   if (vec) {
     const long i4 = (long)chunk * 64 + lane;
@@ -621,15 +627,22 @@ __global__ void __launch_bounds__(256) multi_splitk_reduce_kernel(MultiRed t) {
 void multi_splitk_reduce(MultiRed t, hipStream_t s) {
   if (t.count <= 0) return;
   if (t.count > kMaxRed) throw std::runtime_error("multi_splitk_reduce: too many entries");
-  int units = 0;
   for (int k = 0; k < t.count; ++k) {
     RedEnt& e = t.e[k];
     e.vec = (e.n % 4 == 0 && ((uintptr_t)e.slab % 16) == 0 && ((uintptr_t)e.out % 16) == 0) ? 1 : 0;
+    e.wpc = e.splits <= 8 ? 1 : (e.splits <= 16 ? 2 : 4);
+    e.groups = (e.splits + 8 * e.wpc - 1) / (8 * e.wpc);
+  }
+  // longest blocks first (stable: equal-length entries keep their queue order)
+  std::stable_sort(t.e, t.e + t.count, [](const RedEnt& a, const RedEnt& b) { return a.groups > b.groups; });
+  int units = 0;
+  for (int k = 0; k < t.count; ++k) {
+    RedEnt& e = t.e[k];
     const long per = e.vec ? 256 : 64;
     e.chunks = (int)((e.n + per - 1) / per);
-    e.groups = (e.splits + 31) / 32;
     e.unit0 = units;
-    units += e.chunks;
+    const int cpb = 4 / e.wpc;
+    units += (e.chunks + cpb - 1) / cpb;
   }
   hipLaunchKernelGGL(multi_splitk_reduce_kernel, dim3(units), dim3(256), 0, s, t);
   DCNN_LAUNCH_CHECK();

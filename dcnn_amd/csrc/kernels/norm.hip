@@ -257,7 +257,19 @@ __device__ __forceinline__ void read_stats(const float* __restrict__ buf, int pa
     return;
   }
   StatAcc<MODE> t{buf[c], buf[C + c], buf[2 * C + c]};
-  for (int p = 1; p < parts; ++p) {
+  // four partials' loads in flight at once, merged in part order (same order as one at a time)
+  int p = 1;
+  for (; p + 3 < parts; p += 4) {
+    StatAcc<MODE> q[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const float* r = buf + (long)(p + u) * 3 * C + c;
+      q[u] = StatAcc<MODE>{r[0], r[C], r[2 * C]};
+    }
+#pragma unroll
+    for (int u = 0; u < 4; ++u) t = t.merge(q[u]);
+  }
+  for (; p < parts; ++p) {
     const float* q = buf + (long)p * 3 * C + c;
     t = t.merge(StatAcc<MODE>{q[0], q[C], q[2 * C]});
   }
@@ -442,6 +454,207 @@ __global__ void __launch_bounds__(256) bn_bwd_apply_kernel(const T* __restrict__
 }
 
 // ---------------------------------------------------------------------------------------
+// bf16 apply passes at HBM speed (C % 8 == 0, fewer than 2^31 elements). The generic kernels
+// above move one 16-byte vector per thread per trip with the per-channel prologue (a chain of
+// statistics-partial merges) in front of the first load, so the short ResNet passes spent a
+// large share of their time in that prologue and with one load in flight per lane. Here each
+// thread owns U vectors per trip (all U loads issued together), its FIRST trip's loads are
+// issued before the prologue (the prologue's latency hides behind them), channel coefficients
+// come from LDS as float4s, and indexing is 32-bit.
+// ---------------------------------------------------------------------------------------
+__device__ __forceinline__ uint4 ldg16(const bf16* p) { return *reinterpret_cast<const uint4*>(p); }
+
+// y = x*scale + shift (+ residual) (ReLU)
+template <int U, bool RES>
+__global__ void __launch_bounds__(256) bn_apply_v_kernel(const bf16* __restrict__ x, bf16* __restrict__ y,
+                                                         unsigned nv, int C, const float* __restrict__ sums,
+                                                         int parts, float count, const float* __restrict__ gamma,
+                                                         const float* __restrict__ beta, float eps,
+                                                         const bf16* __restrict__ residual, int relu,
+                                                         float* __restrict__ save_mean,
+                                                         float* __restrict__ save_istd,
+                                                         float* __restrict__ run_mean, float* __restrict__ run_var,
+                                                         float momentum, int use_running) {
+  extern __shared__ __attribute__((aligned(16))) float sh[];
+  float* scale = sh;
+  float* shift = sh + C;
+  const unsigned stride = gridDim.x * 256u, cv = (unsigned)C / 8;
+  unsigned i = blockIdx.x * 256u + threadIdx.x;
+  uint4 xv[U], rv[U];
+#pragma unroll
+  for (int u = 0; u < U; ++u) {
+    const unsigned k = i + u * stride;
+    if (k < nv) {
+      xv[u] = ldg16(x + (size_t)k * 8);
+      if (RES) rv[u] = ldg16(residual + (size_t)k * 8);
+    }
+  }
+  for (int c = threadIdx.x; c < C; c += 256) {
+    float mean, istd;
+    if (use_running) {
+      mean = run_mean[c];
+      istd = rsqrtf(run_var[c] + eps);
+    } else {
+      float var;
+      read_stats<0>(sums, parts, C, c, mean, var);
+      istd = rsqrtf(var + eps);
+      if (blockIdx.x == 0) {
+        if (save_mean) { save_mean[c] = mean; save_istd[c] = istd; }
+        if (run_mean) {
+          const float unbiased = count > 1.f ? var * count / (count - 1.f) : var;
+          run_mean[c] = (1.f - momentum) * run_mean[c] + momentum * mean;
+          run_var[c] = (1.f - momentum) * run_var[c] + momentum * unbiased;
+        }
+      }
+    }
+    const float g = gamma ? gamma[c] : 1.f, b = beta ? beta[c] : 0.f;
+    scale[c] = g * istd;
+    shift[c] = b - mean * g * istd;
+  }
+  __syncthreads();
+  while (true) {
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const unsigned k = i + u * stride;
+      if (k < nv) {
+        const int c0 = (int)(k % cv) * 8;
+        const float4 s0 = *reinterpret_cast<const float4*>(scale + c0), s1 = *reinterpret_cast<const float4*>(scale + c0 + 4);
+        const float4 h0 = *reinterpret_cast<const float4*>(shift + c0), h1 = *reinterpret_cast<const float4*>(shift + c0 + 4);
+        const float sc[8] = {s0.x, s0.y, s0.z, s0.w, s1.x, s1.y, s1.z, s1.w};
+        const float sf[8] = {h0.x, h0.y, h0.z, h0.w, h1.x, h1.y, h1.z, h1.w};
+        float f[8], r[8];
+        unpack8(xv[u], f);
+        if (RES) unpack8(rv[u], r);
+#pragma unroll
+        for (int v = 0; v < 8; ++v) {
+          float t = f[v] * sc[v] + sf[v];
+          if (RES) t += r[v];
+          if (relu) t = fmaxf(t, 0.f);
+          f[v] = t;
+        }
+        *reinterpret_cast<uint4*>(y + (size_t)k * 8) = pack8(f);
+      }
+    }
+    i += U * stride;
+    if (i >= nv) break;
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const unsigned k = i + u * stride;
+      if (k < nv) {
+        xv[u] = ldg16(x + (size_t)k * 8);
+        if (RES) rv[u] = ldg16(residual + (size_t)k * 8);
+      }
+    }
+  }
+}
+
+// dx = A*dy' + B*(x - mean) + D per channel, with A = gamma*istd, B = -A*istd*mean(dy' xhat),
+// D = -A*mean(dy') (the same algebra as bn_bwd_apply_kernel, three coefficients instead of five)
+template <int U, bool MASK>
+__global__ void __launch_bounds__(256) bn_bwd_apply_v_kernel(const bf16* __restrict__ dy,
+                                                             const bf16* __restrict__ yout,
+                                                             const bf16* __restrict__ x, bf16* __restrict__ dx,
+                                                             unsigned nv, int C, const float* __restrict__ mean,
+                                                             const float* __restrict__ istd,
+                                                             const float* __restrict__ gamma,
+                                                             const float* __restrict__ sums, int parts, float count,
+                                                             float* __restrict__ dgamma, float* __restrict__ dbeta,
+                                                             int eval_mode) {
+  extern __shared__ __attribute__((aligned(16))) float sh[];
+  float* ca = sh;          // A
+  float* cbm = sh + C;     // B
+  float* cm = sh + 2 * C;  // mean
+  float* cd = sh + 3 * C;  // D
+  const unsigned stride = gridDim.x * 256u, cv = (unsigned)C / 8;
+  unsigned i = blockIdx.x * 256u + threadIdx.x;
+  uint4 dv[U], xv[U], yv[U];
+#pragma unroll
+  for (int u = 0; u < U; ++u) {
+    const unsigned k = i + u * stride;
+    if (k < nv) {
+      dv[u] = ldg16(dy + (size_t)k * 8);
+      xv[u] = ldg16(x + (size_t)k * 8);
+      if (MASK) yv[u] = ldg16(yout + (size_t)k * 8);
+    }
+  }
+  for (int c = threadIdx.x; c < C; c += 256) {
+    const float g = gamma ? gamma[c] : 1.f, is = istd[c];
+    float sdy = 0.f, sdyx = 0.f;
+    if (sums) read_stats<1>(sums, parts, C, c, sdy, sdyx);
+    const float a = g * is;
+    ca[c] = a;
+    cbm[c] = eval_mode ? 0.f : -a * is * (sdyx / count);
+    cm[c] = mean[c];
+    cd[c] = eval_mode ? 0.f : -a * (sdy / count);
+    if (blockIdx.x == 0 && sums) {
+      if (dgamma) dgamma[c] += sdyx;
+      if (dbeta) dbeta[c] += sdy;
+    }
+  }
+  __syncthreads();
+  auto ld8 = [](const float* p, float* o) {
+    const float4 a = *reinterpret_cast<const float4*>(p), b = *reinterpret_cast<const float4*>(p + 4);
+    o[0] = a.x; o[1] = a.y; o[2] = a.z; o[3] = a.w; o[4] = b.x; o[5] = b.y; o[6] = b.z; o[7] = b.w;
+  };
+  while (true) {
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const unsigned k = i + u * stride;
+      if (k < nv) {
+        const int c0 = (int)(k % cv) * 8;
+        float A[8], B[8], M[8], D[8], d[8], xf[8];
+        ld8(ca + c0, A);
+        ld8(cbm + c0, B);
+        ld8(cm + c0, M);
+        ld8(cd + c0, D);
+        unpack8(dv[u], d);
+        unpack8(xv[u], xf);
+        if (MASK) {
+          float yo[8];
+          unpack8(yv[u], yo);
+#pragma unroll
+          for (int v = 0; v < 8; ++v) d[v] = yo[v] > 0.f ? d[v] : 0.f;
+        }
+#pragma unroll
+        for (int v = 0; v < 8; ++v) d[v] = A[v] * d[v] + B[v] * (xf[v] - M[v]) + D[v];
+        *reinterpret_cast<uint4*>(dx + (size_t)k * 8) = pack8(d);
+      }
+    }
+    i += U * stride;
+    if (i >= nv) break;
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const unsigned k = i + u * stride;
+      if (k < nv) {
+        dv[u] = ldg16(dy + (size_t)k * 8);
+        xv[u] = ldg16(x + (size_t)k * 8);
+        if (MASK) yv[u] = ldg16(yout + (size_t)k * 8);
+      }
+    }
+  }
+}
+
+// vectors per thread per trip and grid of the bf16 apply passes: about 1024-2048 workgroups,
+// more vectors per lane only once the grid is that large
+static void bn_v_launch_shape(long nv, int* U, int* grid) {
+  const long t = 256l * 1024;
+  *U = nv >= 4 * t ? 4 : (nv >= 2 * t ? 2 : 1);
+  long g = (nv + 256l * *U - 1) / (256l * *U);
+  if (g > 2048) g = 2048;
+  if (g < 1) g = 1;
+  *grid = (int)g;
+}
+
+static bool g_bn_v = [] {
+  const char* e = getenv("DCNN_BN_V");
+  return e ? atoi(e) != 0 : true;
+}();
+
+void bn_set_vectorised(int on) { g_bn_v = on != 0; }
+
+static bool bn_v_ok(long R, int C) { return g_bn_v && C % 8 == 0 && R * (long)C < (1l << 31); }
+
+// ---------------------------------------------------------------------------------------
 // GroupNorm (NHWC): one workgroup per (image, group)
 // ---------------------------------------------------------------------------------------
 template <typename T>
@@ -621,6 +834,21 @@ static void bn_apply_t(const T* x, T* y, long R, int C, const float* sums, int p
                        float* save_istd, float* run_mean, float* run_var, float momentum, int use_running,
                        hipStream_t s) {
   const size_t shm = 2 * C * sizeof(float);
+  if constexpr (std::is_same<T, bf16>::value) {
+    if (bn_v_ok(R, C)) {
+      int U, g;
+      const unsigned nv = (unsigned)(R * C / 8);
+      bn_v_launch_shape(nv, &U, &g);
+#define DCNN_BNV(U_, RES_)                                                                                    \
+  if (U == U_ && (residual != nullptr) == RES_)                                                               \
+    hipLaunchKernelGGL((bn_apply_v_kernel<U_, RES_>), dim3(g), dim3(256), shm, s, x, y, nv, C, sums, parts, count, \
+                       gamma, beta, eps, residual, relu, save_mean, save_istd, run_mean, run_var, momentum, use_running);
+      DCNN_BNV(1, false) DCNN_BNV(2, false) DCNN_BNV(4, false) DCNN_BNV(1, true) DCNN_BNV(2, true) DCNN_BNV(4, true)
+#undef DCNN_BNV
+      DCNN_LAUNCH_CHECK();
+      return;
+    }
+  }
   if (C % 8 == 0) {
     const int g = grid_for(R * C / 8, 256, 2048);
     hipLaunchKernelGGL((bn_apply_kernel<T, 8>), dim3(g), dim3(256), shm, s, x, y, R, C, sums, parts, count, gamma, beta,
@@ -648,6 +876,22 @@ template <typename T>
 static void bn_bwd_apply_t(const T* dy, const T* yout, const T* x, T* dx, long R, int C, const float* mean,
                            const float* istd, const float* gamma, const float* sums, int parts, float count,
                            float* dgamma, float* dbeta, int eval_mode, hipStream_t s) {
+  if constexpr (std::is_same<T, bf16>::value) {
+    if (bn_v_ok(R, C)) {
+      int U, g;
+      const unsigned nv = (unsigned)(R * C / 8);
+      bn_v_launch_shape(nv, &U, &g);
+      const size_t shm4 = 4 * C * sizeof(float);
+#define DCNN_BNBV(U_, MASK_)                                                                                   \
+  if (U == U_ && (yout != nullptr) == MASK_)                                                                   \
+    hipLaunchKernelGGL((bn_bwd_apply_v_kernel<U_, MASK_>), dim3(g), dim3(256), shm4, s, dy, yout, x, dx, nv, C, mean, \
+                       istd, gamma, sums, parts, count, dgamma, dbeta, eval_mode);
+      DCNN_BNBV(1, false) DCNN_BNBV(2, false) DCNN_BNBV(4, false) DCNN_BNBV(1, true) DCNN_BNBV(2, true) DCNN_BNBV(4, true)
+#undef DCNN_BNBV
+      DCNN_LAUNCH_CHECK();
+      return;
+    }
+  }
   const size_t shm = 5 * C * sizeof(float);
   if (C % 8 == 0) {
     const int g = grid_for(R * C / 8, 256, 2048);
