@@ -84,6 +84,7 @@ int hconv_tiles(int NB, int H, int W, int N);
 int hconv_tile_elems(int NB, int H, int W, int N);
 void hconv_set_split_target(int t);  // workgroups the split-K decision aims for (0: never split)
 void bn_set_vectorised(int on);   // bf16 BatchNorm apply passes on the vectorised kernels (default on)
+void hconv_set_ws(int on);           // weight-stationary kernel for 64 -> 64 channel 3x3 convs
 void hconv_set_wide(int on);         // 256 x 64 tiles (4 x 1 waves) for 64-channel outputs
 bool hconv_supported(int NB, int H, int W, int Cs, int N, int ntaps);
 int hconv_stat_rows(int NB, int H, int W, int N);

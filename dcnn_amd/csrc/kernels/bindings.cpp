@@ -114,6 +114,7 @@ PYBIND11_MODULE(_kernels, m) {
   m.def("hconv_tiles", &hconv_tiles);
   m.def("hconv_set_split_target", &hconv_set_split_target);
   m.def("hconv_set_wide", &hconv_set_wide);
+  m.def("hconv_set_ws", &hconv_set_ws);
   m.def("bn_set_vectorised", &bn_set_vectorised);
   m.def("hconv_tile_elems", &hconv_tile_elems);
   m.def("hwgrad",

@@ -437,6 +437,122 @@ __global__ void __launch_bounds__(256, 1) hconv_kernel(HConvArgs p) {
 }
 
 // ---------------------------------------------------------------------------------------------
+// Weight-stationary variant for the 64 -> 64 channel 3x3 convs (ResNet layer 1, forward and
+// dgrad): with one 64-channel input chunk the K loop of hconv_kernel is only 9 taps long, and
+// each of its 9 steps waits for a freshly streamed 8 KB weight slice (one L2 round trip per
+// tap, one step of prefetch) plus a workgroup barrier, so a 128 x 64 tile spends most of its
+// life waiting. Here the whole 64 x 576 weight matrix is loaded ONCE per workgroup into
+// registers (each wave's 32-column slice: 9 taps x 2 k-halves x 2 fragments), and the
+// workgroup walks a contiguous range of output tiles: the halo of tile i + 1 streams into the
+// second LDS buffer (direct-to-LDS loads) while tile i runs its 9 taps barrier-free out of LDS
+// + registers, and tile i's epilogue stores drain while tile i + 1 computes.
+//
+//   prologue: halo(t0) -> H[0], weights -> registers
+//   per tile i: issue halo(i + 1) -> H[(i + 1) & 1];  9 taps of MFMAs on H[i & 1];
+//               wait (halo i + 1 landed), barrier;  epilogue(i) (bias/residual/ReLU/BN stats)
+// ---------------------------------------------------------------------------------------------
+template <int HN>
+__global__ void __launch_bounds__(256, 1) hconv_ws_kernel(HConvArgs p, int tiles, int per_wg) {
+  constexpr int BM = 128, BN = 64;
+  using T = HC<BM, BN, 1, 1, 2, false>;  // 2 x 2 waves, TM = 4, TN = 2
+  static_assert(T::WN == 2 && T::TN == 2 && T::TM == 4, "layout");
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const int HALO = p.HPR * 128;
+  char* epi = smem + 2 * HALO;
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int wm = wid / T::WN, wn = wid % T::WN;
+  if (p.zero_ptr && blockIdx.x == 0)
+    for (int i = tid; i < p.zero_n; i += 256) p.zero_ptr[i] = 0.f;
+  // this workgroup's contiguous tile range (neighbouring ranges on one XCD share halo rows in L2)
+  const int g = xcd_remap_h(blockIdx.x, gridDim.x);
+  const int t_begin = g * per_wg, t_end = min(tiles, t_begin + per_wg);
+  if (t_begin >= t_end) return;
+
+  const i32x4 rsA = raw_rsrc(p.A, p.a_bytes);
+  const int HW2 = p.TW + 2, HPI = (p.TH + 2) * HW2, HP = p.IMG * HPI;
+  const int tx_tiles = p.W / p.TW, tpi = tx_tiles * (p.H / p.TH);
+  const int hch = lane & 7;
+  auto load_halo = [&](int buf, int tm) {
+    const int ig = tm / tpi, trem = tm - ig * tpi;
+    const int y0 = (trem / tx_tiles) * p.TH, x0 = (trem % tx_tiles) * p.TW, img0 = ig * p.IMG;
+    char* Hs = smem + buf * HALO;
+#pragma unroll
+    for (int j = 0; j < HN; ++j) {
+      const int row = (wid * HN + j) * 8 + (lane >> 3);
+      unsigned voff = kOOBh;
+      if (row < HP) {
+        const int im = row / HPI, r2 = row - im * HPI;
+        const int sy = y0 + r2 / HW2 - 1, sx = x0 + r2 % HW2 - 1, n = img0 + im;
+        if (sy >= 0 && sy < p.H && sx >= 0 && sx < p.W && n < p.NB)
+          voff = (unsigned)((((long)n * p.H + sy) * p.W + sx) * 128) + (unsigned)((hch ^ (row & 7)) << 4);
+      }
+      glds16h(rsA, Hs + (wid * HN + j) * 1024, voff);
+    }
+  };
+  load_halo(0, t_begin);
+  // weights: this wave's 32 output channels, all taps, both 32-channel k-halves
+  bf16x8 b[9][2][2];
+#pragma unroll
+  for (int t = 0; t < 9; ++t)
+#pragma unroll
+    for (int kk = 0; kk < 2; ++kk)
+#pragma unroll
+      for (int j = 0; j < 2; ++j) {
+        const int nrow = wn * 32 + j * 16 + (lane & 15);
+        b[t][kk][j] = *reinterpret_cast<const bf16x8*>(p.B + (long)nrow * p.ldb + p.tap_b[t] + (kk * 4 + (lane >> 4)) * 8);
+      }
+  int arow0[T::TM];
+#pragma unroll
+  for (int i = 0; i < T::TM; ++i) {
+    const int m = wm * (BM / T::WM) + i * 16 + (lane & 15);
+    const int tpx = p.TH * p.TW;
+    const int im = m / tpx, r2 = m - im * tpx;
+    arow0[i] = im * HPI + (r2 / p.TW + 1) * HW2 + (r2 % p.TW + 1);
+  }
+  int toff[9];
+#pragma unroll
+  for (int t = 0; t < 9; ++t) toff[t] = p.tap_dy[t] * HW2 + p.tap_dx[t];
+  vm_wait_groups<1>(0);
+  lds_barrier();
+  int buf = 0;
+  for (int tm = t_begin; tm < t_end; ++tm) {
+    // H[buf ^ 1] was last read by tile tm - 1's taps, which every wave finished before the
+    // barrier that ended that tile
+    if (tm + 1 < t_end) load_halo(buf ^ 1, tm + 1);
+    const char* Hs = smem + buf * HALO;
+    f32x4 acc[T::TM][T::TN];
+#pragma unroll
+    for (int i = 0; i < T::TM; ++i)
+#pragma unroll
+      for (int j = 0; j < T::TN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int t = 0; t < 9; ++t) {
+      bf16x8 a[2][T::TM];
+#pragma unroll
+      for (int kk = 0; kk < 2; ++kk)
+#pragma unroll
+        for (int i = 0; i < T::TM; ++i)
+          a[kk][i] = *reinterpret_cast<const bf16x8*>(Hs + hoff(arow0[i] + toff[t], kk * 4 + (lane >> 4)));
+      __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+      for (int kk = 0; kk < 2; ++kk)
+#pragma unroll
+        for (int i = 0; i < T::TM; ++i)
+#pragma unroll
+          for (int j = 0; j < T::TN; ++j)
+            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[kk][i], b[t][kk][j], acc[i][j], 0, 0, 0);
+      __builtin_amdgcn_s_setprio(0);
+    }
+    // the next tile's halo (and this lane's older stores) landed, then for the whole workgroup
+    vm_wait_groups<1>(0);
+    lds_barrier();
+    const int ig = tm / tpi, trem = tm - ig * tpi;
+    hc_epilogue<BM, BN, false>(p, acc, epi, 0, tm, ig * p.IMG, (trem / tx_tiles) * p.TH, (trem % tx_tiles) * p.TW);
+    buf ^= 1;
+  }
+}
+
+// ---------------------------------------------------------------------------------------------
 // host side: tile geometry + dispatch
 // ---------------------------------------------------------------------------------------------
 // Output tile = IMG images x TH x TW pixels = BM rows; needs W % TW == 0, H % TH == 0.
@@ -581,6 +697,54 @@ static void launch_hconv(HConvArgs a, hipStream_t s) {
   DCNN_LAUNCH_CHECK();
 }
 
+// weight-stationary 64 -> 64 channel path (hconv_ws_kernel): opt-in (DCNN_HCONV_WS=1). Measured
+// slower than the weight ring on ResNet-18 layer 1 (batch 256: forward 56.5 vs 45.5 us, dgrad
+// 47.4 vs 42.3 us; batch 64: 22.0 vs 19.0 us): the 144 weight registers leave one wave per SIMD,
+// and the epilogue's global-memory latency is no longer hidden by other resident workgroups
+static int g_hconv_ws = [] {
+  const char* e = getenv("DCNN_HCONV_WS");
+  return e ? atoi(e) : 0;
+}();
+void hconv_set_ws(int on) { g_hconv_ws = on; }
+
+static bool launch_hconv_ws(HConvArgs a, hipStream_t s) {
+  if (!g_hconv_ws || a.Cf || a.Cs != 64 || a.N != 64 || a.ntaps != 9 || a.splits != 1 || a.fold.part ||
+      a.ldb < 9 * 64)
+    return false;
+  int bm, bn;
+  hconv_pick(a, &bm, &bn);
+  if (bm != 128 || bn != 64 || !hconv_geometry(a.NB, a.H, a.W, bm, &a.TH, &a.TW, &a.IMG)) return false;
+  const int hp = a.IMG * (a.TH + 2) * (a.TW + 2);
+  const int hn = (hp + 31) / 32;
+  a.HPR = hn * 32;
+  const int tiles = (a.NB / a.IMG) * (a.H / a.TH) * (a.W / a.TW);
+  const int lds = 2 * a.HPR * 128 + 128 * HC<128, 64, 1, 1, 2, false>::EPI_PITCH;
+#define DCNN_HWS(HN_)                                                                                     \
+  if (hn == HN_) {                                                                                        \
+    auto k = hconv_ws_kernel<HN_>;                                                                        \
+    static int per_cu = -1, cus = 0;                                                                      \
+    if (per_cu < 0) {                                                                                     \
+      DCNN_HIP_CHECK(hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, lds)); \
+      int dev = 0;                                                                                        \
+      DCNN_HIP_CHECK(hipGetDevice(&dev));                                                                 \
+      DCNN_HIP_CHECK(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev));            \
+      DCNN_HIP_CHECK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, (const void*)k, 256, lds));    \
+      if (per_cu < 1) per_cu = 1;                                                                         \
+    }                                                                                                     \
+    DCNN_HIP_CHECK(hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, lds));   \
+    int grid = cus * per_cu;                                                                              \
+    if (grid > tiles) grid = tiles;                                                                       \
+    const int per_wg = (tiles + grid - 1) / grid;                                                         \
+    grid = (tiles + per_wg - 1) / per_wg;                                                                 \
+    hipLaunchKernelGGL(k, dim3(grid), dim3(256), lds, s, a, tiles, per_wg);                               \
+    DCNN_LAUNCH_CHECK();                                                                                  \
+    return true;                                                                                          \
+  }
+  DCNN_HWS(6) DCNN_HWS(7) DCNN_HWS(9)
+#undef DCNN_HWS
+  return false;
+}
+
 void hconv(HConvArgs a, hipStream_t s) {
   if (!hconv_supported(a.NB, a.H, a.W, a.Cs, a.N, a.ntaps)) throw std::runtime_error("hconv: unsupported shape");
   for (int t = 0; t < a.ntaps; ++t)
@@ -597,6 +761,7 @@ void hconv(HConvArgs a, hipStream_t s) {
         a.fold.ngroups != (rows + a.fold.group - 1) / a.fold.group)
       throw std::runtime_error("hconv: statistics fold rows / groups mismatch");
   }
+  if (launch_hconv_ws(a, s)) return;
   if (a.Cf) {
     if (a.bnb.x) throw std::runtime_error("hconv: no backward-BN fusion with fp32 output");
     if (bm == 256 && bn == 64) return launch_hconv<256, 64, true>(a, s);

@@ -854,3 +854,37 @@ def test_hconv_wide_tiles(hip, case):
         assert torch.equal(d1, d0)
     ref = F.relu(F.conv2d(x.float().cpu(), w.float().cpu(), b.cpu(), 1, 1) + r.float().cpu())
     assert rel_err(y1, ref) < 1e-2
+
+
+@pytest.mark.parametrize("case", [(64, 64, 32, 32), (256, 64, 16, 16), (768, 64, 8, 8), (3072, 64, 4, 4), (3, 64, 32, 32)])
+def test_hconv_weight_stationary_matches_ring(hip, case):
+    """64 -> 64 channel 3x3 convs on the weight-stationary halo kernel (hconv_ws_kernel: weights
+    in registers, persistent tile walk, double-buffered halo) == the weight-ring kernel: forward
+    (+bias, residual, ReLU, BN statistics) and dgrad bit-identical (same K order)."""
+    from dcnn_amd.ops._ext import kernels
+    K = kernels()
+    N, C, H, W = case
+    torch.manual_seed(7)
+    x = torch.randn(N, C, H, W).cuda().to(torch.bfloat16).contiguous(memory_format=CL)
+    w = (torch.randn(C, C, 3, 3) / math.sqrt(9 * C)).cuda().to(torch.bfloat16).contiguous(memory_format=CL)
+    r = torch.randn(N, C, H, W).cuda().to(torch.bfloat16).contiguous(memory_format=CL)
+    b = torch.randn(C).cuda()
+    dy = torch.randn(N, C, H, W).cuda().to(torch.bfloat16).contiguous(memory_format=CL)
+    wt = hip.conv_weight_t(w)
+    outs = []
+    try:
+        for ws in (1, 0):  # (opt-in kernel, default off)
+            K.hconv_set_ws(ws)
+            y, part = hip.conv2d_fwd(x, w, b, (1, 1), (1, 1), stats=True, residual=r, relu=True)
+            st = hip.bn_stats(y, part)
+            dx = hip.conv2d_dgrad(dy, wt, x.shape, (1, 1), (1, 1))
+            torch.cuda.synchronize()
+            outs.append((y, st.final().clone(), dx))
+    finally:
+        K.hconv_set_ws(0)
+    (y1, s1, d1), (y0, s0, d0) = outs
+    assert torch.equal(y1, y0)
+    assert torch.equal(s1, s0)
+    assert torch.equal(d1, d0)
+    ref = F.relu(F.conv2d(x.float().cpu(), w.float().cpu(), b.cpu(), 1, 1) + r.float().cpu())
+    assert rel_err(y1, ref) < 1e-2
