@@ -689,7 +689,11 @@ static void launch_hconv(HConvArgs a, hipStream_t s) {
     return 163840 / (main > epi ? main : epi);
   };
   int nbs = (tps == 1 && a.ntaps >= bstages) ? bstages : 2;
-  while (nbs > 2 && wg_per_cu(nbs) < wg_per_cu(2)) --nbs;
+  static const int keep_occ = [] {  // DCNN_HCONV_KEEP_OCC=0: deepest ring even at fewer workgroups per CU
+    const char* e = getenv("DCNN_HCONV_KEEP_OCC");
+    return e ? atoi(e) : 1;
+  }();
+  while (keep_occ && nbs > 2 && wg_per_cu(nbs) < wg_per_cu(2)) --nbs;
 #define DCNN_HC(TPS, NHB, NBS)                                                                         \
   {                                                                                                    \
     auto k = hconv_kernel<BM, BN, TPS, NHB, NBS, F32O>;                                                \
