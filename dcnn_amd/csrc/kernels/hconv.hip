@@ -20,6 +20,8 @@
 //
 // The epilogue is the gemm2 one (bias, residual, ReLU, BatchNorm partial statistics, 16-byte
 // stores through an LDS-staged bf16 tile), with the spatial-tile -> NHWC row mapping.
+#include <cstdio>
+
 #include "common.h"
 #include "api.h"
 #include "statfold.h"
@@ -601,9 +603,27 @@ static void hconv_pick(const HConvArgs& a, int* bm, int* bn) {
     *bn = 64;
     return;
   }
+  // DCNN_HCONV_TILE=MxN (64/128 each): fixed tile for A/B experiments where N divides
+  static const int fixed = [] {
+    const char* e = getenv("DCNN_HCONV_TILE");
+    int m = 0, n = 0;
+    if (e && sscanf(e, "%dx%d", &m, &n) == 2 && (m == 64 || m == 128) && (n == 64 || n == 128)) return m * 1000 + n;
+    return 0;
+  }();
+  if (fixed && a.N % (fixed % 1000) == 0) {
+    *bm = fixed / 1000;
+    *bn = fixed % 1000;
+    return;
+  }
   *bm = 128;
   *bn = (a.N % 128 == 0 && tiles(128, 128) >= 384) ? 128 : 64;
-  if (tiles(*bm, *bn) < 384) *bm = 64;
+  if (tiles(*bm, *bn) < 384) {
+    // small maps (4x4 layer-4 convs at batch 256): 64 x 128 tiles (twice the MFMAs per K step,
+    // split-K refills the grid) while they still give one tile per CU; 64 x 64 below that.
+    // Measured: 4x4x512 forward 46.5 -> 40.9 us, dgrad 44.8 -> 39.5 us (tools/gpu_convsplit.sh tile)
+    *bm = 64;
+    *bn = (a.N % 128 == 0 && tiles(64, 128) >= 256) ? 128 : 64;
+  }
 }
 
 bool hconv_supported(int NB, int H, int W, int Cs, int N, int ntaps) {
