@@ -19,6 +19,8 @@
 //
 // The weight-gradient kernel (tn2) uses the same loader on both operands (pixels = K) and
 // ds_read_b64_tr_b16 transposed fragment reads; split-K partials go to an fp32 slab.
+#include <cstdio>
+
 #include "common.h"
 #include "api.h"
 #include "statfold.h"
@@ -566,9 +568,22 @@ static void launch_g2(const G2Args& a, hipStream_t s) {
 }
 
 // Tile choice: the largest tile that still gives >= ~2 workgroups per CU.
+// DCNN_G2_TILE / DCNN_T2_TILE = MxN (64 / 128 each): fixed tiles for A/B experiments
+static int fixed_tile(const char* var) {
+  const char* e = getenv(var);
+  int m = 0, n = 0;
+  if (e && sscanf(e, "%dx%d", &m, &n) == 2 && (m == 64 || m == 128) && (n == 64 || n == 128)) return m * 1000 + n;
+  return 0;
+}
+
 void g2_tile(int M, int N, int* bm, int* bn) {
+  static const int fixed = fixed_tile("DCNN_G2_TILE");
+  if (fixed) { *bm = fixed / 1000; *bn = fixed % 1000; return; }
   auto tiles = [&](int m, int n) { return (long)((M + m - 1) / m) * ((N + n - 1) / n); };
   if (N >= 128 && tiles(128, 128) >= 480) { *bm = 128; *bn = 128; return; }
+  // wide-N, mid-M (8x8-map convs of 256 channels, M = 16384): 64 x 128 beats 128 x 64 at the
+  // same tile count (layer-3 strided forward 32.7 -> 29.5 us, layer-4 strided dgrad 42.7 -> 40.0)
+  if (N >= 128 && tiles(64, 128) >= 480 && tiles(128, 64) < 640) { *bm = 64; *bn = 128; return; }
   if (tiles(128, 64) >= 480 || N < 128) {
     *bm = tiles(128, 64) >= 400 ? 128 : 64;
     *bn = 64;
@@ -639,8 +654,13 @@ static void launch_t2(T2Args a, int splits, hipStream_t s) {
 }
 
 void t2_tile(int M, int N, int* bm, int* bn) {
+  static const int fixed = fixed_tile("DCNN_T2_TILE");
+  if (fixed) { *bm = fixed / 1000; *bn = fixed % 1000; return; }
+  // 128 x 64 once M >= 128: twice the tiles of 128 x 128, so half the split-K slices and slab
+  // traffic (strided 3x3 weight gradients of layers 2-4: 43 / 39 / 38 -> 33 / 33 / 32 us at
+  // batch 256); 128-wide N tiles only when M is a single 64-row tile
   *bm = M >= 128 ? 128 : 64;
-  *bn = N >= 128 ? 128 : 64;
+  *bn = (N >= 128 && M < 128) ? 128 : 64;
 }
 
 int gemm_t2_splits(int M, int N, int P) {
