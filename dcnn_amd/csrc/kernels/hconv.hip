@@ -118,7 +118,7 @@ __device__ __forceinline__ void hc_epilogue(const HConvArgs& p,
 #pragma unroll
   for (int j = 0; j < T::TN; ++j) {
     const int col = wn * (BN / T::WN) + j * 16 + (lane & 15);
-    const float bv = p.bias ? p.bias[n0 + col] : 0.f;
+    const float bv = (p.bias && n0 + col < p.N) ? p.bias[n0 + col] : 0.f;
 #pragma unroll
     for (int i = 0; i < T::TM; ++i)
 #pragma unroll
@@ -136,11 +136,12 @@ __device__ __forceinline__ void hc_epilogue(const HConvArgs& p,
   constexpr int RSTEP = 256 / CG;
   const int cg = tid % CG, r0 = tid / CG;
   const int ncol = n0 + cg * 8;
+  const bool cok = ncol < p.N;  // (N = 32: the upper half of the 64-column tile is padding)
   float s[8], q[8], mu[8], is[8], pv[8];
 #pragma unroll
   for (int v = 0; v < 8; ++v) s[v] = q[v] = mu[v] = is[v] = pv[v] = 0.f;
   const bool bnb = !F32O && p.bnb.x != nullptr;  // backward-BN fusion (api.h BnbArgs; bf16 output only)
-  if (bnb && true) {
+  if (bnb && cok) {
 #pragma unroll
     for (int v = 0; v < 8; ++v) { mu[v] = p.bnb.mean[ncol + v]; is[v] = p.bnb.istd[ncol + v]; }
   }
@@ -156,7 +157,7 @@ __device__ __forceinline__ void hc_epilogue(const HConvArgs& p,
   for (int row = r0; row < BM; row += RSTEP) {
     const int im = row / tpx, r2 = row - im * tpx;
     const int n = img0 + im;
-    if (n >= p.NB) continue;
+    if (n >= p.NB || !cok) continue;
     const long orow = ((long)n * p.H + y0 + r2 / p.TW) * p.W + x0 + r2 % p.TW;
     float f[8];
     load_row8<F32O>(smem + row * T::EPI_PITCH + cg * 8 * T::OB, f);
@@ -216,11 +217,12 @@ __device__ __forceinline__ void hc_epilogue(const HConvArgs& p,
     if (bnb) {  // backward: plain sums [tiles][2][N]
       for (int cc = tid; cc < 2 * BN; cc += 256) {
         const int which = cc / BN, c2 = cc % BN;
+        if (n0 + c2 >= p.N) continue;
         float a = 0.f;
         for (int k = 0; k < RSTEP; ++k) a += red[(k * 2 + which) * BN + c2];
         stat_store(&p.stats[((long)tm * 2 + which) * p.N + n0 + c2], a, fold);
       }
-    } else if (tid < BN) {  // forward: Welford triple [tiles][3][N], fixed summation order
+    } else if (tid < BN && n0 + tid < p.N) {  // forward: Welford triple [tiles][3][N], fixed summation order
       float a = 0.f, b = 0.f;
       for (int k = 0; k < RSTEP; ++k) { a += red[(k * 2 + 0) * BN + tid]; b += red[(k * 2 + 1) * BN + tid]; }
       const float cnt = (float)(min(p.IMG, p.NB - img0) * tpx);
@@ -243,7 +245,7 @@ __global__ void __launch_bounds__(256, 1) hconv_kernel(HConvArgs p) {
   struct { int HALO; } T_rt{p.HPR * 128};
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const int wm = wid / T::WN, wn = wid % T::WN;
-  const int tiles_n = p.N / BN;
+  const int tiles_n = (p.N + BN - 1) / BN;  // (N = 32: one half-filled column tile)
   const int SPL = p.splits;                      // workgroups per output tile (split-K)
   const int lt0 = xcd_remap_h(blockIdx.x, gridDim.x);
   const int zs = lt0 % SPL, lt = lt0 / SPL;      // this workgroup's split, output tile
@@ -597,7 +599,7 @@ void hconv_set_wide(int on) { g_hconv_wide = on; }
 
 static void hconv_pick(const HConvArgs& a, int* bm, int* bn) {
   // prefer 128 x 128 when it still gives >= ~1.5 workgroups per CU, else shrink
-  auto tiles = [&](int m, int n) { return (long)((a.NB * a.H * a.W + m - 1) / m) * (a.N / n); };
+  auto tiles = [&](int m, int n) { return (long)((a.NB * a.H * a.W + m - 1) / m) * ((a.N + n - 1) / n); };
   if (g_hconv_wide && a.N == 64 && a.W % 16 == 0 && a.H % 16 == 0 && tiles(256, 64) >= 512) {
     *bm = 256;
     *bn = 64;
@@ -627,7 +629,9 @@ static void hconv_pick(const HConvArgs& a, int* bm, int* bn) {
 }
 
 bool hconv_supported(int NB, int H, int W, int Cs, int N, int ntaps) {
-  if (Cs % 64 || N % 64 || ntaps < 1 || ntaps > 9) return false;
+  // N = 32 runs as a 64-column tile whose upper half reads zero weights (buffer range check) and
+  // is never stored: the 32-channel data gradient of a 32 -> 64 channel conv (ResNet-18 layer 1)
+  if (Cs % 64 || (N % 64 && N != 32) || ntaps < 1 || ntaps > 9) return false;
   HConvArgs a{};
   a.NB = NB; a.H = H; a.W = W; a.N = N;
   int bm, bn, th, tw, img;
@@ -649,7 +653,7 @@ int hconv_tiles(int NB, int H, int W, int N) {
   a.NB = NB; a.H = H; a.W = W; a.N = N;
   int bm, bn;
   hconv_pick(a, &bm, &bn);
-  return (NB * H * W + bm - 1) / bm * (N / bn);
+  return (NB * H * W + bm - 1) / bm * ((N + bn - 1) / bn);
 }
 
 int hconv_tile_elems(int NB, int H, int W, int N) {
@@ -683,7 +687,7 @@ template <int BM, int BN, bool F32O>
 static void launch_hconv(HConvArgs a, hipStream_t s) {
   if (!hconv_geometry(a.NB, a.H, a.W, BM, &a.TH, &a.TW, &a.IMG)) throw std::runtime_error("hconv: bad geometry");
   const long mt = (long)(a.NB / a.IMG) * (a.H / a.TH) * (a.W / a.TW);
-  const int grid = (int)(mt * (a.N / BN));
+  const int grid = (int)(mt * ((a.N + BN - 1) / BN));
   const int hp = a.IMG * (a.TH + 2) * (a.TW + 2);
   a.HPR = ((hp + 31) / 32) * 32;  // halo buffer sized to the tile (LDS decides workgroups per CU)
   const bool multi = a.Cs / 64 / a.splits > 1;  // >1 channel chunk per workgroup: double-buffered halo
@@ -794,6 +798,7 @@ void hconv(HConvArgs a, hipStream_t s) {
     throw std::runtime_error("hconv: split count / workspace mismatch (use hconv_splits)");
   int bm, bn;
   hconv_pick(a, &bm, &bn);
+  if (a.fold.part && a.N % 64) throw std::runtime_error("hconv: statistics fold needs N % 64 == 0");
   if (a.fold.part) {
     const int rows = (a.NB * a.H * a.W + bm - 1) / bm;
     if (!a.stats || a.fold.group < 1 || a.fold.rows != rows || !a.fold.tickets ||

@@ -41,6 +41,8 @@ CONV_CASES = [
     (2, 128, 9, 9, 64, 3, 1, 1),
     (3, 64, 7, 5, 96, 3, 1, 1),
     (2, 256, 8, 8, 256, 1, 1, 0),
+    (4, 32, 32, 32, 64, 3, 1, 1),   # dgrad: 32 output channels on the halo conv (half-filled tile)
+    (2, 64, 16, 16, 32, 3, 1, 1),   # forward: 32 output channels on the halo conv
 ]
 
 
