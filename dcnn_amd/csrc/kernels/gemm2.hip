@@ -559,7 +559,16 @@ static int g2_stages() {
 template <int BM, int BN, int BK, bool UNI>
 static void launch_g2(const G2Args& a, hipStream_t s) {
   const int tiles = ((a.M + BM - 1) / BM) * ((a.N + BN - 1) / BN);
-  const int stages = g2_stages() ? g2_stages() : (2 * G2<BM, BN, BK, UNI, 3>::LDS <= 163840 ? 3 : 2);
+  // single-step K loops (1x1 convs on 32-64 channels and their data gradients) never use a third
+  // ring stage: 2 stages there free LDS for one more resident workgroup per CU (layer-1 1x1 dgrad
+  // 27.0 -> 22.3 us; two-step loops keep 3 stages: both steps in flight from the prologue)
+  int ksteps = 0;
+  for (int c = 0; c < a.ncls; ++c) {
+    const int k = a.cls_nt[c] * ((a.Cs + BK - 1) / BK);
+    ksteps = k > ksteps ? k : ksteps;
+  }
+  const int stages = g2_stages() ? g2_stages()
+                                 : ((2 * G2<BM, BN, BK, UNI, 3>::LDS <= 163840 && ksteps > 1) ? 3 : 2);
   if (stages == 3)
     hipLaunchKernelGGL((gemm_g2_kernel<BM, BN, BK, UNI, 3>), dim3(tiles), dim3(256), 0, s, a);
   else
