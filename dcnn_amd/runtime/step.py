@@ -126,19 +126,31 @@ class TrainStep:
         if self.dp.active and self.capture_collectives and dist.get_backend(self.dp.pg) == "nccl":
             # (gloo moves CUDA tensors through the host: not capturable, keeps the segments)
             t0 = getattr(self.opt, "t", None)
+            err = None
             try:
                 self._capture_whole()
-                return
             except Exception as e:  # e.g. a collective library build without capture support
-                import warnings
-                warnings.warn(f"capturing the bucket collectives into the step graph failed ({e}); "
-                              "falling back to the segmented capture")
-                self.dp._works.clear()
-                self.dp._pending_unpack.clear()
-                if t0 is not None:
-                    self.opt.t = t0
-                self.graphs, self._whole = None, False
-                torch.cuda.synchronize()
+                err = e
+            # every rank must replay the same kind of step (a whole-graph rank and a segmented
+            # rank would issue different collective sequences and hang): agree before the first
+            # replay, falling back everywhere if any rank's capture failed
+            if self.dp.world > 1:
+                flag = torch.tensor([0 if err is not None else 1], dtype=torch.int32,
+                                    device=self.model.device.torch_device)
+                dist.all_reduce(flag, op=dist.ReduceOp.MIN, group=self.dp.pg)
+                if int(flag.item()) == 0 and err is None:
+                    err = RuntimeError("another rank's capture failed")
+            if err is None:
+                return
+            import warnings
+            warnings.warn(f"capturing the bucket collectives into the step graph failed ({err}); "
+                          "falling back to the segmented capture")
+            self.dp._works.clear()
+            self.dp._pending_unpack.clear()
+            if t0 is not None:
+                self.opt.t = t0
+            self.graphs, self._whole = None, False
+            torch.cuda.synchronize()
         segs, fires = self._segments()
         self._segs, self._fires = segs, fires
         self.graphs = []
