@@ -199,7 +199,8 @@ def test_multi_splitk_reduce(hip):
     from dcnn_amd.ops._ext import kernels
     torch.manual_seed(3)
     K = kernels()
-    shapes = [(1, 64), (5, 1000), (40, 36864), (100, 12), (33, 4608), (7, 3)] * 9  # 54 > one launch
+    # 1-8 splits: one wave per chunk, 9-16: two, more: four (multi_splitk_reduce_kernel)
+    shapes = [(1, 64), (5, 1000), (40, 36864), (100, 12), (33, 4608), (7, 3), (12, 500), (16, 4096), (256, 1024)] * 6
     slabs = [torch.randn(s, n, device="cuda") for s, n in shapes]
     outs = [torch.randn(n, device="cuda") for _, n in shapes]
     refs = [o.cpu() + sl.cpu().sum(0) for o, sl in zip(outs, slabs)]
@@ -890,3 +891,54 @@ def test_hconv_weight_stationary_matches_ring(hip, case):
     assert torch.equal(d1, d0)
     ref = F.relu(F.conv2d(x.float().cpu(), w.float().cpu(), b.cpu(), 1, 1) + r.float().cpu())
     assert rel_err(y1, ref) < 1e-2
+
+
+@pytest.mark.parametrize("shape", [(256, 64, 32, 32), (64, 128, 16, 16), (32, 256, 8, 8), (16, 512, 4, 4), (3, 24, 5, 7)])
+def test_bn_apply_vectorised_matches_generic(hip, shape):
+    """Vectorised bf16 BatchNorm apply passes (bn_apply_v / bn_bwd_apply_v: U = 1 / 2 / 4 vectors per
+    lane by size, statistics prologue behind the first loads) == the generic kernels: forward
+    (+residual, ReLU, running statistics) bit-identical; backward (3-coefficient form, ReLU mask)
+    within bf16 rounding; dgamma / dbeta identical."""
+    from dcnn_amd.ops._ext import kernels
+    K = kernels()
+    N, C, H, W = shape
+    torch.manual_seed(11)
+    mk = lambda: torch.randn(N, C, H, W).cuda().to(torch.bfloat16).contiguous(memory_format=CL)
+    x, r, dy, yo = mk(), mk(), mk(), mk()
+    R = N * H * W
+    parts = 3
+    part = torch.empty(parts, 3, C, device="cuda")
+    part[:, 0] = R / parts
+    part[:, 1] = torch.randn(parts, C, device="cuda") * 0.2
+    part[:, 2] = (R / parts) * (0.5 + torch.rand(parts, C, device="cuda"))
+    stats = hip.Stats(part, parts, 0)
+    g, b = torch.rand(C, device="cuda") + 0.5, torch.randn(C, device="cuda")
+    mean, istd = torch.randn(C, device="cuda") * 0.1, torch.rand(C, device="cuda") + 0.5
+    sums = torch.randn(2 * C, device="cuda") * R * 0.01
+    outs = []
+    try:
+        for vec in (1, 0):
+            K.bn_set_vectorised(vec)
+            rm, rv = torch.zeros(C, device="cuda"), torch.ones(C, device="cuda")
+            sm, si = torch.empty(C, device="cuda"), torch.empty(C, device="cuda")
+            y1 = hip.bn_apply(x, stats, R, g, b, 1e-5, relu=True, save=(sm, si), running=(rm, rv))
+            y2 = hip.bn_apply(x, stats, R, g, b, 1e-5, residual=r, relu=True)
+            res = []
+            for mask in (0, 1):
+                dx = torch.empty_like(x)
+                dg, db = torch.zeros(C, device="cuda"), torch.zeros(C, device="cuda")
+                K.bn_bwd_apply(1, dy.data_ptr(), yo.data_ptr() if mask else 0, x.data_ptr(), dx.data_ptr(), R, C,
+                               mean.data_ptr(), istd.data_ptr(), g.data_ptr(), sums.data_ptr(), 1, float(R),
+                               dg.data_ptr(), db.data_ptr(), 0, hip.stream_ptr())
+                res.append((dx, dg, db))
+            torch.cuda.synchronize()
+            outs.append((y1, y2, rm, rv, sm, si, res))
+    finally:
+        K.bn_set_vectorised(1)
+    (a1, a2, arm, arv, asm, asi, ares), (b1, b2, brm, brv, bsm, bsi, bres) = outs
+    assert torch.equal(a1, b1) and torch.equal(a2, b2)
+    for u, v in ((arm, brm), (arv, brv), (asm, bsm), (asi, bsi)):
+        assert torch.equal(u, v)
+    for (dxa, dga, dba), (dxb, dgb, dbb) in zip(ares, bres):
+        assert torch.equal(dga, dgb) and torch.equal(dba, dbb)
+        assert (dxa.float() - dxb.float()).abs().max().item() <= 2e-2 * dxb.float().abs().max().item()
