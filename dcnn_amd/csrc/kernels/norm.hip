@@ -513,6 +513,17 @@ __global__ void __launch_bounds__(256) bn_apply_v_kernel(const bf16* __restrict_
   }
   __syncthreads();
   while (true) {
+    // the next trip's loads go out before this trip's stores (loads and stores overlap)
+    const unsigned inx = i + U * stride;
+    uint4 xn[U], rn[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const unsigned k = inx + u * stride;
+      if (inx < nv && k < nv) {
+        xn[u] = ldg16(x + (size_t)k * 8);
+        if (RES) rn[u] = ldg16(residual + (size_t)k * 8);
+      }
+    }
 #pragma unroll
     for (int u = 0; u < U; ++u) {
       const unsigned k = i + u * stride;
@@ -535,15 +546,12 @@ __global__ void __launch_bounds__(256) bn_apply_v_kernel(const bf16* __restrict_
         *reinterpret_cast<uint4*>(y + (size_t)k * 8) = pack8(f);
       }
     }
-    i += U * stride;
-    if (i >= nv) break;
+    if (inx >= nv) break;
+    i = inx;
 #pragma unroll
     for (int u = 0; u < U; ++u) {
-      const unsigned k = i + u * stride;
-      if (k < nv) {
-        xv[u] = ldg16(x + (size_t)k * 8);
-        if (RES) rv[u] = ldg16(residual + (size_t)k * 8);
-      }
+      xv[u] = xn[u];
+      if (RES) rv[u] = rn[u];
     }
   }
 }
@@ -597,6 +605,17 @@ __global__ void __launch_bounds__(256) bn_bwd_apply_v_kernel(const bf16* __restr
     o[0] = a.x; o[1] = a.y; o[2] = a.z; o[3] = a.w; o[4] = b.x; o[5] = b.y; o[6] = b.z; o[7] = b.w;
   };
   while (true) {
+    const unsigned inx = i + U * stride;  // next trip's loads before this trip's stores
+    uint4 dn[U], xn[U], yn[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const unsigned k = inx + u * stride;
+      if (inx < nv && k < nv) {
+        dn[u] = ldg16(dy + (size_t)k * 8);
+        xn[u] = ldg16(x + (size_t)k * 8);
+        if (MASK) yn[u] = ldg16(yout + (size_t)k * 8);
+      }
+    }
 #pragma unroll
     for (int u = 0; u < U; ++u) {
       const unsigned k = i + u * stride;
@@ -620,27 +639,30 @@ __global__ void __launch_bounds__(256) bn_bwd_apply_v_kernel(const bf16* __restr
         *reinterpret_cast<uint4*>(dx + (size_t)k * 8) = pack8(d);
       }
     }
-    i += U * stride;
-    if (i >= nv) break;
+    if (inx >= nv) break;
+    i = inx;
 #pragma unroll
     for (int u = 0; u < U; ++u) {
-      const unsigned k = i + u * stride;
-      if (k < nv) {
-        dv[u] = ldg16(dy + (size_t)k * 8);
-        xv[u] = ldg16(x + (size_t)k * 8);
-        if (MASK) yv[u] = ldg16(yout + (size_t)k * 8);
-      }
+      dv[u] = dn[u];
+      xv[u] = xn[u];
+      if (MASK) yv[u] = yn[u];
     }
   }
 }
 
-// vectors per thread per trip and grid of the bf16 apply passes: about 1024-2048 workgroups,
-// more vectors per lane only once the grid is that large
+// vectors per thread per trip and grid of the bf16 apply passes
 static void bn_v_launch_shape(long nv, int* U, int* grid) {
-  const long t = 256l * 1024;
-  *U = nv >= 4 * t ? 4 : (nv >= 2 * t ? 2 : 1);
+  // DCNN_BN_U (1 / 2 / 4) and DCNN_BN_GRID (workgroup cap) override the choice (A/B experiments)
+  static const int u_env = [] { const char* e = getenv("DCNN_BN_U"); const int v = e ? atoi(e) : 0; return (v == 1 || v == 2 || v == 4) ? v : 0; }();
+  // default: 1 vector per lane per trip, at most 1024 workgroups, so the large passes make
+  // several software-pipelined trips (next trip's loads in flight under this trip's stores).
+  // Measured on the ResNet-18 shapes (benchmarks/bn_bench.py, tools/gpu_bnsweep.sh): one pass
+  // over all 12 shape/op cases 117.9 us with 4 vectors per lane over <= 2048 workgroups ->
+  // 107.7 us (2 vectors: 107.0 us, but 0.5% slower end to end at batch 64 / 128)
+  static const long g_cap = [] { const char* e = getenv("DCNN_BN_GRID"); const long v = e ? atol(e) : 0; return v > 0 ? v : 1024l; }();
+  *U = u_env ? u_env : 1;
   long g = (nv + 256l * *U - 1) / (256l * *U);
-  if (g > 2048) g = 2048;
+  if (g > g_cap) g = g_cap;
   if (g < 1) g = 1;
   *grid = (int)g;
 }
