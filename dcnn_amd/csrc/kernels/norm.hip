@@ -373,13 +373,25 @@ __global__ void __launch_bounds__(256) bn_relu_maxpool_kernel(const bf16* __rest
   __syncthreads();
   const int CV = g.C / 8;
   const long total = (long)g.N * g.OH * g.OW * CV;
+  const bool small = total < (1l << 32);  // 32-bit index math (64-bit div/mod chains are ALU heavy)
   for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < total; i += (long)gridDim.x * blockDim.x) {
-    const int cv = (int)(i % CV);
-    long t = i / CV;
-    const int ox = (int)(t % g.OW);
-    t /= g.OW;
-    const int oy = (int)(t % g.OH);
-    const int n = (int)(t / g.OH);
+    int cv, ox, oy, n;
+    if (small) {
+      const unsigned iu = (unsigned)i;
+      unsigned t = iu / (unsigned)CV;
+      cv = (int)(iu - t * (unsigned)CV);
+      ox = (int)(t % (unsigned)g.OW);
+      t /= (unsigned)g.OW;
+      oy = (int)(t % (unsigned)g.OH);
+      n = (int)(t / (unsigned)g.OH);
+    } else {
+      cv = (int)(i % CV);
+      long t = i / CV;
+      ox = (int)(t % g.OW);
+      t /= g.OW;
+      oy = (int)(t % g.OH);
+      n = (int)(t / g.OH);
+    }
     float sc[8], sf[8], best[8], v[8];
     uint8_t bi[8];
 #pragma unroll

@@ -576,6 +576,73 @@ static void avgpool_bwd_t(const void* dy, void* dx, PoolGeom g, hipStream_t s) {
   DCNN_LAUNCH_CHECK();
 }
 
+// Same result per element as maxpool_bwd_bnb_kernel for windows that tile the input exactly
+// (H % ph == 0, W % pw == 0): one thread per POOLED vector walks its window, so the pooled
+// gradient / pooled output / argmax are read once instead of once per window pixel and the
+// index arithmetic is 32-bit and per window (the per-pixel 64-bit div/mod chains of the generic
+// kernel made it ALU bound). Statistics partials per block in the same [blocks][2][C] layout.
+__global__ void __launch_bounds__(256) maxpool_bwd_bnb_w_kernel(const bf16* __restrict__ dy,
+                                                                const uint8_t* __restrict__ idx,
+                                                                const bf16* __restrict__ ypool,
+                                                                const bf16* __restrict__ x,
+                                                                const float* __restrict__ mean,
+                                                                const float* __restrict__ istd,
+                                                                bf16* __restrict__ dx, PoolGeom g,
+                                                                float* __restrict__ slab,
+                                                                float* __restrict__ zero_sums) {
+  __shared__ float red[256 * 16];
+  if (zero_sums && blockIdx.x == 0)
+    for (int j = threadIdx.x; j < 2 * g.C; j += blockDim.x) zero_sums[j] = 0.f;
+  const unsigned CV = g.C / 8;
+  const unsigned total = (unsigned)g.N * g.OH * g.OW * CV;
+  const int cv = threadIdx.x % CV;  // fixed: blockDim and the grid stride are multiples of CV
+  float mu[8], is[8], s[8], q[8];
+#pragma unroll
+  for (int e = 0; e < 8; ++e) {
+    mu[e] = mean[cv * 8 + e];
+    is[e] = istd[cv * 8 + e];
+    s[e] = q[e] = 0.f;
+  }
+  for (unsigned i = blockIdx.x * 256u + threadIdx.x; i < total; i += gridDim.x * 256u) {
+    unsigned t = i / CV;
+    const int ox = (int)(t % g.OW);
+    t /= g.OW;
+    const int oy = (int)(t % g.OH);
+    const int n = (int)(t / g.OH);
+    float d[8], yp[8];
+    unpack8(*reinterpret_cast<const uint4*>(dy + (size_t)i * 8), d);
+    unpack8(*reinterpret_cast<const uint4*>(ypool + (size_t)i * 8), yp);
+    const uint2 ib = *reinterpret_cast<const uint2*>(idx + (size_t)i * 8);
+    const uint8_t* b = reinterpret_cast<const uint8_t*>(&ib);
+    for (int ky = 0; ky < g.ph; ++ky)
+      for (int kx = 0; kx < g.pw; ++kx) {
+        const int local = ky * g.pw + kx;
+        const size_t xi = (((size_t)n * g.H + oy * g.ph + ky) * g.W + ox * g.pw + kx) * g.C + cv * 8;
+        float xv[8], out[8];
+        unpack8(*reinterpret_cast<const uint4*>(x + xi), xv);
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+          out[e] = (b[e] == local && yp[e] > 0.f) ? d[e] : 0.f;
+          s[e] += out[e];
+          q[e] += out[e] * (xv[e] - mu[e]) * is[e];
+        }
+        *reinterpret_cast<uint4*>(dx + xi) = pack8(out);
+      }
+  }
+#pragma unroll
+  for (int e = 0; e < 8; ++e) {
+    red[threadIdx.x * 16 + e] = s[e];
+    red[threadIdx.x * 16 + 8 + e] = q[e];
+  }
+  __syncthreads();
+  for (int j = threadIdx.x; j < 2 * g.C; j += blockDim.x) {
+    const int which = j / g.C, c = j % g.C, grp = c / 8, e = c % 8;
+    float a = 0.f;
+    for (int tt = grp; tt < (int)blockDim.x; tt += CV) a += red[tt * 16 + which * 8 + e];
+    slab[((long)blockIdx.x * 2 + which) * g.C + c] = a;
+  }
+}
+
 static int bnb_pool_blocks(const PoolGeom& g) {
   const long total = (long)g.N * g.H * g.W * g.C / 8;
   return grid_for(total, 256, 1024);
@@ -588,6 +655,14 @@ int maxpool_bwd_bnb_rows(PoolGeom g) { return bnb_pool_blocks(g); }
 void maxpool_bwd_bnb(const bf16* dy, const uint8_t* idx, const bf16* ypool, const bf16* x, const float* mean,
                      const float* istd, bf16* dx, PoolGeom g, float* slab, float* zero_sums, hipStream_t s) {
   if (!maxpool_bwd_bnb_supported(g)) throw std::runtime_error("maxpool_bwd_bnb: unsupported geometry");
+  static const bool win = [] { const char* e = getenv("DCNN_POOL_BWD_WIN"); return e ? atoi(e) != 0 : true; }();
+  if (win && g.H % g.ph == 0 && g.W % g.pw == 0 && g.OH == g.H / g.ph && g.OW == g.W / g.pw &&
+      (long)g.N * g.H * g.W * g.C < (1l << 31)) {
+    hipLaunchKernelGGL(maxpool_bwd_bnb_w_kernel, dim3(bnb_pool_blocks(g)), dim3(256), 0, s, dy, idx, ypool, x, mean,
+                       istd, dx, g, slab, zero_sums);
+    DCNN_LAUNCH_CHECK();
+    return;
+  }
   hipLaunchKernelGGL(maxpool_bwd_bnb_kernel, dim3(bnb_pool_blocks(g)), dim3(256), 0, s, dy, idx, ypool, x, mean, istd,
                      dx, g, slab, zero_sums);
   DCNN_LAUNCH_CHECK();
