@@ -153,6 +153,15 @@ void bn_stat_reduce(int mode, const float* slab, int rows, int C, float* out, fl
 void bn_apply(int dtype, const void* x, void* y, long R, int C, const float* sums, int parts, float count, const float* gamma,
               const float* beta, float eps, const void* residual, int relu, float* save_mean, float* save_istd,
               float* run_mean, float* run_var, float momentum, int use_running, hipStream_t s);
+// one BatchNorm's operands for bn_apply_dual (statistics as bn_apply: sums/parts or running)
+struct BnSide {
+  const void* x; const float* sums; int parts; float count; const float* gamma; const float* beta; float eps;
+  float* save_mean; float* save_istd; float* run_mean; float* run_var; float momentum; int use_running;
+};
+// y = act(bn_a(a.x) + bn_b(b.x)): a residual block's tail BatchNorm with its projection
+// shortcut's BatchNorm applied on the fly (bf16, C % 8 == 0); false = unsupported, nothing launched
+bool bn_apply_dual(const BnSide& a, const BnSide& b, void* y, long R, int C, int relu, hipStream_t s);
+bool bn_apply_dual_supported(long R, int C);
 void bn_bwd_apply(int dtype, const void* dy, const void* yout, const void* x, void* dx, long R, int C, const float* mean,
                   const float* istd, const float* gamma, const float* sums, int parts, float count, float* dgamma,
                   float* dbeta, int eval_mode, hipStream_t s);

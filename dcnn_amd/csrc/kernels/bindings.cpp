@@ -2,6 +2,7 @@
 // (uintptr_t, from torch.Tensor.data_ptr()) and the hipStream_t of the caller's current
 // stream, so launches land on whatever stream PyTorch-ROCm is using (including a stream
 // under hipGraph capture). No torch headers, no hipify: plain HIP + pybind11.
+#include <tuple>
 #include <pybind11/pybind11.h>
 #include <pybind11/stl.h>
 #include <algorithm>
@@ -244,6 +245,22 @@ PYBIND11_MODULE(_kernels, m) {
              P<const float*>(beta), eps, P<const void*>(residual), relu, P<float*>(save_mean), P<float*>(save_istd),
              P<float*>(run_mean), P<float*>(run_var), momentum, use_running, S(st));
   });
+  // side = (x, sums, parts, count, gamma, beta, eps, save_mean, save_istd, run_mean, run_var, momentum, use_running)
+  using SideT = std::tuple<uintptr_t, uintptr_t, int, float, uintptr_t, uintptr_t, float, uintptr_t, uintptr_t, uintptr_t,
+                           uintptr_t, float, int>;
+  auto side = [](const SideT& t) {
+    BnSide b{};
+    b.x = P<const void*>(std::get<0>(t)); b.sums = P<const float*>(std::get<1>(t)); b.parts = std::get<2>(t);
+    b.count = std::get<3>(t); b.gamma = P<const float*>(std::get<4>(t)); b.beta = P<const float*>(std::get<5>(t));
+    b.eps = std::get<6>(t); b.save_mean = P<float*>(std::get<7>(t)); b.save_istd = P<float*>(std::get<8>(t));
+    b.run_mean = P<float*>(std::get<9>(t)); b.run_var = P<float*>(std::get<10>(t)); b.momentum = std::get<11>(t);
+    b.use_running = std::get<12>(t);
+    return b;
+  };
+  m.def("bn_apply_dual", [side](SideT a, SideT b, uintptr_t y, long R, int C, int relu, uintptr_t st) {
+    return bn_apply_dual(side(a), side(b), P<void*>(y), R, C, relu, S(st));
+  });
+  m.def("bn_apply_dual_supported", &bn_apply_dual_supported);
   m.def("bn_bwd_apply", [](int dt, uintptr_t dy, uintptr_t yout, uintptr_t x, uintptr_t dx, long R, int C,
                            uintptr_t mean, uintptr_t istd, uintptr_t gamma, uintptr_t sums, int parts, float count,
                            uintptr_t dgamma, uintptr_t dbeta, int eval_mode, uintptr_t st) {

@@ -662,6 +662,102 @@ __global__ void __launch_bounds__(256) bn_bwd_apply_v_kernel(const bf16* __restr
   }
 }
 
+// y = act(a.x * sa + ha + b.x * sb + hb): the tail BatchNorm of a residual block and its
+// projection shortcut's BatchNorm in one pass (the shortcut's normalised output is never
+// written or re-read). Same trips / prologue scheme as bn_apply_v_kernel; workgroup 0 saves both
+// layers' (mean, istd) and updates both running statistics.
+__device__ __forceinline__ void bn_side_coeffs(const BnSide& b, int C, float* scale, float* shift, bool first) {
+  for (int c = threadIdx.x; c < C; c += 256) {
+    float mean, istd;
+    if (b.use_running) {
+      mean = b.run_mean[c];
+      istd = rsqrtf(b.run_var[c] + b.eps);
+    } else {
+      float var;
+      read_stats<0>(b.sums, b.parts, C, c, mean, var);
+      istd = rsqrtf(var + b.eps);
+      if (first) {
+        if (b.save_mean) { b.save_mean[c] = mean; b.save_istd[c] = istd; }
+        if (b.run_mean) {
+          const float unbiased = b.count > 1.f ? var * b.count / (b.count - 1.f) : var;
+          b.run_mean[c] = (1.f - b.momentum) * b.run_mean[c] + b.momentum * mean;
+          b.run_var[c] = (1.f - b.momentum) * b.run_var[c] + b.momentum * unbiased;
+        }
+      }
+    }
+    const float g = b.gamma ? b.gamma[c] : 1.f, be = b.beta ? b.beta[c] : 0.f;
+    scale[c] = g * istd;
+    shift[c] = be - mean * g * istd;
+  }
+}
+
+__global__ void __launch_bounds__(256) bn_apply_dual_kernel(BnSide a, BnSide b, bf16* __restrict__ y, unsigned nv,
+                                                            int C, int relu) {
+  extern __shared__ __attribute__((aligned(16))) float sh[];
+  float* sa = sh;
+  float* ha = sh + C;
+  float* sb = sh + 2 * C;
+  float* hb = sh + 3 * C;
+  const bf16* __restrict__ xa = static_cast<const bf16*>(a.x);
+  const bf16* __restrict__ xb = static_cast<const bf16*>(b.x);
+  const unsigned stride = gridDim.x * 256u, cv = (unsigned)C / 8;
+  unsigned i = blockIdx.x * 256u + threadIdx.x;
+  uint4 va{}, vb{};
+  if (i < nv) {
+    va = ldg16(xa + (size_t)i * 8);
+    vb = ldg16(xb + (size_t)i * 8);
+  }
+  bn_side_coeffs(a, C, sa, ha, blockIdx.x == 0);
+  bn_side_coeffs(b, C, sb, hb, blockIdx.x == 0);
+  __syncthreads();
+  auto ld8 = [](const float* p, float* o) {
+    const float4 u = *reinterpret_cast<const float4*>(p), v = *reinterpret_cast<const float4*>(p + 4);
+    o[0] = u.x; o[1] = u.y; o[2] = u.z; o[3] = u.w; o[4] = v.x; o[5] = v.y; o[6] = v.z; o[7] = v.w;
+  };
+  while (i < nv) {
+    const unsigned inx = i + stride;  // next trip's loads before this trip's store
+    uint4 na{}, nb{};
+    if (inx < nv) {
+      na = ldg16(xa + (size_t)inx * 8);
+      nb = ldg16(xb + (size_t)inx * 8);
+    }
+    const int c0 = (int)(i % cv) * 8;
+    float A[8], HA[8], B[8], HB[8], fa[8], fb[8];
+    ld8(sa + c0, A);
+    ld8(ha + c0, HA);
+    ld8(sb + c0, B);
+    ld8(hb + c0, HB);
+    unpack8(va, fa);
+    unpack8(vb, fb);
+#pragma unroll
+    for (int v = 0; v < 8; ++v) {
+      float t = fa[v] * A[v] + HA[v];
+      // the shortcut branch rounded to bf16 as the materialised shortcut tensor would be
+      t += (float)(bf16)(fb[v] * B[v] + HB[v]);
+      if (relu) t = fmaxf(t, 0.f);
+      fa[v] = t;
+    }
+    *reinterpret_cast<uint4*>(y + (size_t)i * 8) = pack8(fa);
+    i = inx;
+    va = na;
+    vb = nb;
+  }
+}
+
+bool bn_apply_dual_supported(long R, int C) { return C % 8 == 0 && R * (long)C < (1l << 31); }
+
+bool bn_apply_dual(const BnSide& a, const BnSide& b, void* y, long R, int C, int relu, hipStream_t s) {
+  if (!bn_apply_dual_supported(R, C)) return false;
+  const unsigned nv = (unsigned)(R * C / 8);
+  long g = (nv + 255) / 256;
+  if (g > 1024) g = 1024;
+  if (g < 1) g = 1;
+  hipLaunchKernelGGL(bn_apply_dual_kernel, dim3((unsigned)g), dim3(256), 4 * C * sizeof(float), s, a, b,
+                     static_cast<bf16*>(y), nv, C, relu);
+  DCNN_LAUNCH_CHECK();
+  return true;
+}
+
 // vectors per thread per trip and grid of the bf16 apply passes
 static void bn_v_launch_shape(long nv, int* U, int* grid) {
   // DCNN_BN_U (1 / 2 / 4) and DCNN_BN_GRID (workgroup cap) override the choice (A/B experiments)

@@ -94,17 +94,21 @@ class BatchNorm(ParameterizedLayer):
                 # hands this layer its statistics; there is no full-resolution ReLU output
                 self._cache[mb_id] = (xa, _POOLED, mean, istd, True)
                 return y
+            dual = isinstance(residual, hip.BnDeferred)
+            if dual and not hip.bn_dual_ok(xa):
+                residual, dual = residual.materialize(), False
+            apply = hip.bn_apply_dual if dual else hip.bn_apply
+            args = dict(other=residual) if dual else dict(residual=residual)
             if self.training:
                 sums = hip.bn_stats(xa, getattr(x, "_bn_partial", None))
                 count = xa.numel() // C
                 mean = torch.empty(C, dtype=torch.float32, device=xa.device)
                 istd = torch.empty_like(mean)
-                y = hip.bn_apply(xa, sums, count, self._gamma(), self._beta(), self.epsilon, residual=residual,
-                                 relu=do_relu, save=(mean, istd), running=(self.running_mean, self.running_var),
-                                 momentum=self.momentum)
+                y = apply(xa, sums, count, self._gamma(), self._beta(), self.epsilon, relu=do_relu, save=(mean, istd),
+                          running=(self.running_mean, self.running_var), momentum=self.momentum, **args)
             else:
-                y = hip.bn_apply(xa, None, 1, self._gamma(), self._beta(), self.epsilon, residual=residual,
-                                 relu=do_relu, running=(self.running_mean, self.running_var), use_running=True)
+                y = apply(xa, None, 1, self._gamma(), self._beta(), self.epsilon, relu=do_relu,
+                          running=(self.running_mean, self.running_var), use_running=True, **args)
                 mean = self.running_mean
                 istd = torch.rsqrt(self.running_var + self.epsilon)
             self._cache[mb_id] = (xa, y if do_relu else None, mean, istd, self.training)
@@ -120,6 +124,28 @@ class BatchNorm(ParameterizedLayer):
                                           residual=res)
         self._cache[mb_id] = (x, y if do_relu else None, mean, istd, self.training)
         return y
+
+    def forward_deferred(self, x, mb_id=0):
+        """GPU: statistics now, the apply deferred into the consumer (:class:`hip.BnDeferred`,
+        fused by a residual block's tail BatchNorm). The backward is the plain one: it needs
+        only this layer's input and statistics, which the consumer's kernel saves."""
+        from ...ops import hip
+        x = self._to_layer_device(x)
+        xa = hip.to_act(x, self.compute_dtype)
+        C = self.num_features
+        if self.training:
+            sums = hip.bn_stats(xa, getattr(x, "_bn_partial", None))
+            mean = torch.empty(C, dtype=torch.float32, device=xa.device)
+            istd = torch.empty_like(mean)
+            d = hip.BnDeferred(xa, sums, xa.numel() // C, self._gamma(), self._beta(), self.epsilon, (mean, istd),
+                               (self.running_mean, self.running_var), self.momentum, False)
+        else:
+            mean = self.running_mean
+            istd = torch.rsqrt(self.running_var + self.epsilon)
+            d = hip.BnDeferred(xa, None, 1, self._gamma(), self._beta(), self.epsilon, None,
+                               (self.running_mean, self.running_var), self.momentum, True)
+        self._cache[mb_id] = (xa, None, mean, istd, self.training)
+        return d
 
     def backward(self, grad, mb_id=0):
         ent = self._cache.pop(mb_id, None)

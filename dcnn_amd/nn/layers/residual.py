@@ -130,12 +130,18 @@ class ResidualBlock(Layer):
             from ...ops import hip
             xa = hip.to_act(x, self.compute_dtype)
             s = xa
-            for l in self.shortcut_path:
+            sp = self.shortcut_path
+            # a projection shortcut ending in BatchNorm is applied inside the tail BatchNorm's
+            # pass (hip.bn_apply_dual): its normalised output is never written
+            defer = bool(sp) and isinstance(sp[-1], BatchNorm) and self.compute_dtype == torch.bfloat16
+            for l in (sp[:-1] if defer else sp):
                 s = l.forward(s, mb_id)
+            if defer:
+                s = sp[-1].forward_deferred(s, mb_id)
             h = xa
             for l in self.main_path[:-1]:
                 h = l.forward(h, mb_id)
-            out = self.main_path[-1].forward(h, mb_id, residual=hip.to_act(s, self.compute_dtype),
+            out = self.main_path[-1].forward(h, mb_id, residual=s if defer else hip.to_act(s, self.compute_dtype),
                                              relu=self.activation_type == "relu")
             self._cache[mb_id] = ("fused", None)
             return out

@@ -1083,6 +1083,47 @@ def bn_apply(x, sums, count, gamma, beta, eps, *, residual=None, relu=False, sav
     return y
 
 
+class BnDeferred:
+    """A BatchNorm whose apply is deferred into the consumer (a residual block's tail BatchNorm
+    applies its projection shortcut's BatchNorm on the fly: :func:`bn_apply_dual`)."""
+    __slots__ = ("x", "sums", "count", "gamma", "beta", "eps", "save", "running", "momentum", "use_running")
+
+    def __init__(self, x, sums, count, gamma, beta, eps, save, running, momentum, use_running):
+        self.x, self.sums, self.count, self.gamma, self.beta, self.eps = x, sums, count, gamma, beta, eps
+        self.save, self.running, self.momentum, self.use_running = save, running, momentum, use_running
+
+    def side(self):
+        sp, parts = _stats(self.sums)
+        sm, si = self.save if self.save is not None else (None, None)
+        rm, rv = self.running if self.running is not None else (None, None)
+        return (self.x.data_ptr(), sp, parts, float(self.count), ptr(self.gamma), ptr(self.beta), float(self.eps),
+                ptr(sm), ptr(si), ptr(rm), ptr(rv), float(self.momentum), int(self.use_running))
+
+    def materialize(self):
+        """The deferred BatchNorm's output as a tensor (when the consumer cannot fuse it)."""
+        return bn_apply(self.x, self.sums, self.count, self.gamma, self.beta, self.eps, save=self.save,
+                        running=self.running, momentum=self.momentum, use_running=self.use_running)
+
+
+_BN_DUAL = os.environ.get("DCNN_BN_DUAL", "1") != "0"
+
+
+def bn_dual_ok(x):
+    return _BN_DUAL and x.dtype == BF16 and bool(kernels().bn_apply_dual_supported(*_rc(x)))
+
+
+def bn_apply_dual(x, sums, count, gamma, beta, eps, other: BnDeferred, *, relu=False, save=None, running=None,
+                  momentum=0.1, use_running=False):
+    """act(bn(x) + other's BatchNorm output) in one pass (norm.hip bn_apply_dual)."""
+    R, C = _rc(x)
+    assert tuple(other.x.shape) == tuple(x.shape) and other.x.dtype == x.dtype == BF16
+    y = torch.empty_like(x, memory_format=CL)
+    me = BnDeferred(x, sums, count, gamma, beta, eps, save, running, momentum, use_running)
+    if not kernels().bn_apply_dual(me.side(), other.side(), y.data_ptr(), R, C, int(relu), stream_ptr()):
+        raise RuntimeError("bn_apply_dual: unsupported shape")
+    return y
+
+
 def bn_relu_maxpool_ok(x, ph, pw, sh, sw, pdh, pdw):
     """Can :func:`bn_relu_maxpool` take this BatchNorm+ReLU+max-pool? Its backward relies on the
     fused max-pool backward (:func:`maxpool_bwd` with ``bnb``), so both must be available."""

@@ -326,3 +326,42 @@ def _fp32_model_vs_cpu(name, dx_tol):
         # gradients (3.3e-3 seen); the bf16 path sits at ~1e-2
         g_tol = 5e-3 if dx_tol <= 3e-3 else 3e-2
         assert (gc.float().cpu() - pc).norm() < g_tol * pc.norm() + 1e-5 * pc.numel() ** 0.5
+
+
+@pytest.mark.gpu
+def test_projection_shortcut_bn_dual_apply_matches_separate():
+    """A projection shortcut's BatchNorm applied inside the tail BatchNorm's pass
+    (hip.bn_apply_dual) == its separate apply + residual add: ResNet-18-tiny forward output, loss,
+    every parameter gradient and the BatchNorm running statistics bit-identical, train and eval."""
+    from dcnn_amd.models import create_model
+    from dcnn_amd.nn import LossFactory
+    from dcnn_amd.ops import hip
+    from dcnn_amd.parallel.dp import _bn_buffers
+    torch.manual_seed(5)
+    x = torch.randn(8, 3, 64, 64, device="cuda")
+    y = torch.randint(0, 200, (8,), device="cuda")
+    res = []
+    saved = hip._BN_DUAL
+    try:
+        for dual in (True, False):
+            hip._BN_DUAL = dual
+            m = create_model("resnet18_tiny_imagenet")
+            m.set_seed(3)
+            m.set_device("GPU:0")
+            m.initialize()
+            lf = LossFactory.create("softmax_crossentropy")
+            out = m.forward(x)
+            loss, grad, _ = lf.loss_and_grad(out, y)
+            m.backward(grad)
+            torch.cuda.synchronize()
+            bufs = [t.clone() for l in m.layers for t in _bn_buffers(l)]
+            m.set_training(False)
+            ev = m.forward(x).clone()
+            res.append((out.clone(), loss.clone(), m.arena.grad.clone(), bufs, ev))
+    finally:
+        hip._BN_DUAL = saved
+    (o1, l1, g1, b1, e1), (o0, l0, g0, b0, e0) = res
+    assert torch.equal(o1, o0) and torch.equal(l1, l0)
+    assert torch.equal(g1, g0)
+    assert all(torch.equal(u, v) for u, v in zip(b1, b0))
+    assert torch.equal(e1, e0)
