@@ -148,6 +148,9 @@ void bn_partial(int dtype, const void* x, const void* dy, const void* yout, void
                 const float* istd, long R, int C, float* slab, int mode, float* zero_sums, hipStream_t s);
 // deterministic slab reduce: mode 0 Welford triples [rows][3][C] -> (mean, var); mode 1 sums [rows][2][C]
 int bn_stat_parts(int rows);
+// two independent reduces of the same C in one launch (segment 2 optional: slab2 = nullptr)
+void bn_stat_reduce2(int mode, const float* slab, int rows, float* out, float* part, const float* slab2, int rows2,
+                     float* out2, float* part2, int C, hipStream_t s);
 void bn_stat_reduce(int mode, const float* slab, int rows, int C, float* out, float* part, unsigned* ticket,
                     hipStream_t s);
 void bn_apply(int dtype, const void* x, void* y, long R, int C, const float* sums, int parts, float count, const float* gamma,

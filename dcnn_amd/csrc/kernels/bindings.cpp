@@ -261,6 +261,11 @@ PYBIND11_MODULE(_kernels, m) {
     return bn_apply_dual(side(a), side(b), P<void*>(y), R, C, relu, S(st));
   });
   m.def("bn_apply_dual_supported", &bn_apply_dual_supported);
+  m.def("bn_stat_reduce2", [](int mode, uintptr_t slab, int rows, uintptr_t out, uintptr_t part, uintptr_t slab2, int rows2,
+                              uintptr_t out2, uintptr_t part2, int C, uintptr_t st) {
+    bn_stat_reduce2(mode, P<const float*>(slab), rows, P<float*>(out), P<float*>(part), P<const float*>(slab2), rows2,
+                    P<float*>(out2), P<float*>(part2), C, S(st));
+  });
   m.def("bn_bwd_apply", [](int dt, uintptr_t dy, uintptr_t yout, uintptr_t x, uintptr_t dx, long R, int C,
                            uintptr_t mean, uintptr_t istd, uintptr_t gamma, uintptr_t sums, int parts, float count,
                            uintptr_t dgamma, uintptr_t dbeta, int eval_mode, uintptr_t st) {

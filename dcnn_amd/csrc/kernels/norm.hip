@@ -205,17 +205,31 @@ __device__ __forceinline__ void stat_tree_lds(StatAcc<MODE> (*red)[64], int w, i
   __syncthreads();
 }
 
+// blockIdx.z selects one of up to two independent reductions of the same C (a residual block's
+// tail and projection-shortcut BatchNorms, reduced in one launch); each has its own ny partial
+// rows (blocks past a segment's ny exit before any barrier)
 template <int MODE, int WAVES>
 __global__ void __launch_bounds__(64 * WAVES) bn_stat_reduce_kernel(const float* __restrict__ slab, int rows, int C,
                                                                     float* __restrict__ part,
                                                                     unsigned* __restrict__ ticket,
-                                                                    float* __restrict__ out) {
+                                                                    float* __restrict__ out, int ny1,
+                                                                    const float* __restrict__ slab2, int rows2,
+                                                                    float* __restrict__ part2,
+                                                                    float* __restrict__ out2, int ny2) {
+  if (blockIdx.z == 1) {
+    slab = slab2;
+    rows = rows2;
+    part = part2;
+    out = out2;
+    ny1 = ny2;
+  }
+  if ((int)blockIdx.y >= ny1) return;
   constexpr int NV = MODE == 0 ? 3 : 2;
   __shared__ StatAcc<MODE> red[WAVES][64];
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   const int c = blockIdx.x * 64 + lane;
   const bool cok = c < C;
-  const int ny = gridDim.y, by = blockIdx.y;
+  const int ny = ny1, by = blockIdx.y;
   auto finish = [&](StatAcc<MODE> t) {
     if constexpr (MODE == 0) {
       out[c] = t.b;
@@ -924,22 +938,29 @@ int bn_stat_parts(int rows) {
 // mode 0: slab [rows][3][C] Welford triples -> out = (mean, var); mode 1: slab [rows][2][C] sums.
 // part: bn_stat_parts(rows) x 3 x C floats (unused when that is 1); ticket: ceil(C/64) zeroed
 // words, left zeroed again (one ticket array per stream).
-void bn_stat_reduce(int mode, const float* slab, int rows, int C, float* out, float* part, unsigned* ticket,
-                    hipStream_t s) {
-  (void)ticket;  // (the in-kernel second level is gone: consumers merge the partials)
-  const int ny = bn_stat_parts(rows);
-  if (ny > 1 && !part) throw std::runtime_error("bn_stat_reduce: partials buffer required");
-  const dim3 grid((unsigned)((C + 63) / 64), (unsigned)ny);
+void bn_stat_reduce2(int mode, const float* slab, int rows, float* out, float* part, const float* slab2, int rows2,
+                     float* out2, float* part2, int C, hipStream_t s) {
+  const int ny = bn_stat_parts(rows), ny2 = slab2 ? bn_stat_parts(rows2) : 0;
+  if ((ny > 1 && !part) || (ny2 > 1 && !part2)) throw std::runtime_error("bn_stat_reduce: partials buffer required");
+  const dim3 grid((unsigned)((C + 63) / 64), (unsigned)(ny > ny2 ? ny : ny2), slab2 ? 2u : 1u);
 #define DCNN_SR(W)                                                                                           \
   if (g_stat_waves == W) {                                                                                   \
     if (mode == 0)                                                                                           \
-      hipLaunchKernelGGL((bn_stat_reduce_kernel<0, W>), grid, dim3(64 * W), 0, s, slab, rows, C, part, ticket, out); \
+      hipLaunchKernelGGL((bn_stat_reduce_kernel<0, W>), grid, dim3(64 * W), 0, s, slab, rows, C, part, nullptr, out, \
+                         ny, slab2, rows2, part2, out2, ny2);                                                \
     else                                                                                                     \
-      hipLaunchKernelGGL((bn_stat_reduce_kernel<1, W>), grid, dim3(64 * W), 0, s, slab, rows, C, part, ticket, out); \
+      hipLaunchKernelGGL((bn_stat_reduce_kernel<1, W>), grid, dim3(64 * W), 0, s, slab, rows, C, part, nullptr, out, \
+                         ny, slab2, rows2, part2, out2, ny2);                                                \
   }
   DCNN_SR(4) DCNN_SR(8) DCNN_SR(16)
 #undef DCNN_SR
   DCNN_LAUNCH_CHECK();
+}
+
+void bn_stat_reduce(int mode, const float* slab, int rows, int C, float* out, float* part, unsigned* ticket,
+                    hipStream_t s) {
+  (void)ticket;  // (the in-kernel second level is gone: consumers merge the partials)
+  bn_stat_reduce2(mode, slab, rows, out, part, nullptr, 0, nullptr, nullptr, C, s);
 }
 
 bool bn_relu_maxpool_supported(PoolGeom g) {

@@ -100,7 +100,12 @@ class BatchNorm(ParameterizedLayer):
             apply = hip.bn_apply_dual if dual else hip.bn_apply
             args = dict(other=residual) if dual else dict(residual=residual)
             if self.training:
-                sums = hip.bn_stats(xa, getattr(x, "_bn_partial", None))
+                part = getattr(x, "_bn_partial", None)
+                if dual and isinstance(residual.sums, tuple) and not (part is not None and isinstance(part[0], hip.Stats)):
+                    # this layer's and the deferred shortcut BatchNorm's reduces in one launch
+                    sums, residual.sums = hip.stat_reduce_pair(0, hip.bn_stats_raw(xa, part), residual.sums, C)
+                else:
+                    sums = hip.bn_stats(xa, part)
                 count = xa.numel() // C
                 mean = torch.empty(C, dtype=torch.float32, device=xa.device)
                 istd = torch.empty_like(mean)
@@ -134,7 +139,9 @@ class BatchNorm(ParameterizedLayer):
         xa = hip.to_act(x, self.compute_dtype)
         C = self.num_features
         if self.training:
-            sums = hip.bn_stats(xa, getattr(x, "_bn_partial", None))
+            part = getattr(x, "_bn_partial", None)
+            # raw statistics rows: the consumer reduces them together with its own
+            sums = part[0] if (part is not None and isinstance(part[0], hip.Stats)) else hip.bn_stats_raw(xa, part)
             mean = torch.empty(C, dtype=torch.float32, device=xa.device)
             istd = torch.empty_like(mean)
             d = hip.BnDeferred(xa, sums, xa.numel() // C, self._gamma(), self._beta(), self.epsilon, (mean, istd),

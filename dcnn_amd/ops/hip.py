@@ -1053,6 +1053,35 @@ def _stats(s):
     return s.data_ptr(), 1
 
 
+def bn_stats_raw(x, partial=None):
+    """The (slab, rows, sums) statistics rows of x before the reduce (the producing conv's
+    epilogue slab, else a bn_partial pass), or an already reduced :class:`Stats` (folded)."""
+    if partial is not None:
+        return partial[0] if isinstance(partial[0], Stats) else partial
+    K = kernels()
+    R, C = _rc(x)
+    rows = K.bn_partial_rows(R, C)
+    slab = torch.empty((rows, 3, C), dtype=F32, device=x.device)
+    sums = torch.empty((2 * C,), dtype=F32, device=x.device)
+    K.bn_partial(dt_code(x.dtype), x.data_ptr(), 0, 0, 0, 0, 0, R, C, slab.data_ptr(), 0, 0, stream_ptr())
+    return slab, rows, sums
+
+
+def stat_reduce_pair(mode, a, b, C):
+    """Two independent forward/backward statistics reduces of the same C in ONE launch
+    (norm.hip bn_stat_reduce2); ``a``/``b`` = (slab, rows, out). Returns two :class:`Stats`."""
+    K = kernels()
+    res, ptrs = [], []
+    for slab, rows, out in (a, b):
+        ny = K.bn_stat_parts(rows)
+        part = torch.empty((ny, 3, C), dtype=F32, device=slab.device) if ny > 1 else None
+        ptrs.append((slab.data_ptr(), rows, out.data_ptr(), ptr(part)))
+        res.append(Stats(part if ny > 1 else out, ny, mode))
+    (s1, r1, o1, p1), (s2, r2, o2, p2) = ptrs
+    K.bn_stat_reduce2(mode, s1, r1, o1, p1, s2, r2, o2, p2, C, stream_ptr())
+    return res[0], res[1]
+
+
 def bn_stats(x, partial=None):
     """Per-channel (mean, biased variance) of x (NHWC), as one [2][C] fp32 tensor. Uses the
     producing conv's epilogue Welford slab if given, else a bn_partial pass; the reduction is
@@ -1092,7 +1121,15 @@ class BnDeferred:
         self.x, self.sums, self.count, self.gamma, self.beta, self.eps = x, sums, count, gamma, beta, eps
         self.save, self.running, self.momentum, self.use_running = save, running, momentum, use_running
 
+    def reduced(self):
+        """Reduce raw statistics rows (left raw so a consumer can pair the reduce with its own)."""
+        if isinstance(self.sums, tuple):
+            slab, rows, out = self.sums
+            self.sums = stat_reduce(0, slab, rows, out.numel() // 2, out)
+        return self
+
     def side(self):
+        self.reduced()
         sp, parts = _stats(self.sums)
         sm, si = self.save if self.save is not None else (None, None)
         rm, rv = self.running if self.running is not None else (None, None)
@@ -1101,6 +1138,7 @@ class BnDeferred:
 
     def materialize(self):
         """The deferred BatchNorm's output as a tensor (when the consumer cannot fuse it)."""
+        self.reduced()
         return bn_apply(self.x, self.sums, self.count, self.gamma, self.beta, self.eps, save=self.save,
                         running=self.running, momentum=self.momentum, use_running=self.use_running)
 
