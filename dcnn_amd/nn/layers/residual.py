@@ -160,9 +160,10 @@ class ResidualBlock(Layer):
         kind, ent = self._cache.pop(mb_id)
         if kind == "fused":
             last = self.main_path[-1]
+            d_pair = self._pair_backward_stats(grad, mb_id)
             g = last.backward(grad, mb_id)
             d_pre = last.pop_masked_grad(mb_id)
-            d_s = d_pre
+            d_s = d_pair if d_pair is not None else d_pre
             for l in reversed(self.shortcut_path):
                 d_s = l.backward(d_s, mb_id)
             for k in range(len(self.main_path) - 2, 0, -1):
@@ -195,6 +196,31 @@ class ResidualBlock(Layer):
         if not self.needs_input_grad:
             return None
         return d_main + d_s
+
+    def _pair_backward_stats(self, grad, mb_id):
+        """When the tail BatchNorm's backward statistics come fused from the producer of ``grad``
+        (the ReLU-masked gradient that both the tail and the projection shortcut's BatchNorm
+        receive), reduce the shortcut BatchNorm's statistics in the same launch as the tail's
+        (hip.stat_reduce_pair). Returns the shortcut's incoming gradient carrying its reduced
+        statistics, or None (unpaired path)."""
+        from ...ops import hip
+        sp = self.shortcut_path
+        pre = getattr(grad, "_bnb", None)
+        bns = sp[-1] if sp and isinstance(sp[-1], BatchNorm) else None
+        if (bns is None or pre is None or pre[0] is not self.main_path[-1] or not hip._BN_DUAL
+                or isinstance(pre[1], hip.Stats) or grad.dtype != torch.bfloat16
+                or not grad.is_contiguous(memory_format=torch.channels_last)):
+            return None
+        ent = bns._cache.get(mb_id)
+        if ent is None or not ent[4] or ent[0].dtype != torch.bfloat16 or tuple(ent[0].shape) != tuple(grad.shape):
+            return None
+        xs, _, ms, iss, _ = ent
+        raw = hip.bn_bwd_stats_raw(grad, xs, ms, iss)
+        sa, sb = hip.stat_reduce_pair(1, (pre[1], pre[2], pre[3]), raw, grad.shape[1])
+        grad._bnb = (pre[0], sa, pre[2], pre[3])
+        d = grad.detach()  # same storage, its own fused-statistics tag
+        d._bnb = (bns, sb, raw[1], raw[2])
+        return d
 
     def bwd_bn_spec(self, mb_id=0):
         ent = self._cache.get(mb_id)

@@ -1067,6 +1067,18 @@ def bn_stats_raw(x, partial=None):
     return slab, rows, sums
 
 
+def bn_bwd_stats_raw(dy, x, mean, istd):
+    """Backward statistics rows (sum dy, sum dy * xhat) of x before the reduce: (slab, rows, sums)."""
+    K = kernels()
+    R, C = _rc(x)
+    rows = K.bn_partial_rows(R, C)
+    slab = torch.empty((rows, 2, C), dtype=F32, device=x.device)
+    sums = torch.empty((2 * C,), dtype=F32, device=x.device)
+    K.bn_partial(dt_code(x.dtype), x.data_ptr(), dy.data_ptr(), 0, 0, mean.data_ptr(), istd.data_ptr(), R, C,
+                 slab.data_ptr(), 1, 0, stream_ptr())
+    return slab, rows, sums
+
+
 def stat_reduce_pair(mode, a, b, C):
     """Two independent forward/backward statistics reduces of the same C in ONE launch
     (norm.hip bn_stat_reduce2); ``a``/``b`` = (slab, rows, out). Returns two :class:`Stats`."""
