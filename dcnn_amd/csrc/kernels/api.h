@@ -165,6 +165,13 @@ struct BnSide {
 // shortcut's BatchNorm applied on the fly (bf16, C % 8 == 0); false = unsupported, nothing launched
 bool bn_apply_dual(const BnSide& a, const BnSide& b, void* y, long R, int C, int relu, hipStream_t s);
 bool bn_apply_dual_supported(long R, int C);
+// one BatchNorm of bn_bwd_apply_dual: input x, output dx, saved (mean, istd), backward sums
+struct BnBwdSide {
+  const void* x; void* dx; const float* mean; const float* istd; const float* gamma; const float* sums; int parts;
+  float count; float* dgamma; float* dbeta;
+};
+// dx_a, dx_b of two BatchNorms fed the same gradient dy, one pass (bf16, training statistics)
+bool bn_bwd_apply_dual(const void* dy, const BnBwdSide& a, const BnBwdSide& b, long R, int C, hipStream_t s);
 void bn_bwd_apply(int dtype, const void* dy, const void* yout, const void* x, void* dx, long R, int C, const float* mean,
                   const float* istd, const float* gamma, const float* sums, int parts, float count, float* dgamma,
                   float* dbeta, int eval_mode, hipStream_t s);

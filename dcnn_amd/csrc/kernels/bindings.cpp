@@ -261,6 +261,20 @@ PYBIND11_MODULE(_kernels, m) {
     return bn_apply_dual(side(a), side(b), P<void*>(y), R, C, relu, S(st));
   });
   m.def("bn_apply_dual_supported", &bn_apply_dual_supported);
+  // bside = (x, dx, mean, istd, gamma, sums, parts, count, dgamma, dbeta)
+  using BSideT = std::tuple<uintptr_t, uintptr_t, uintptr_t, uintptr_t, uintptr_t, uintptr_t, int, float, uintptr_t,
+                            uintptr_t>;
+  auto bside = [](const BSideT& t) {
+    BnBwdSide b{};
+    b.x = P<const void*>(std::get<0>(t)); b.dx = P<void*>(std::get<1>(t)); b.mean = P<const float*>(std::get<2>(t));
+    b.istd = P<const float*>(std::get<3>(t)); b.gamma = P<const float*>(std::get<4>(t));
+    b.sums = P<const float*>(std::get<5>(t)); b.parts = std::get<6>(t); b.count = std::get<7>(t);
+    b.dgamma = P<float*>(std::get<8>(t)); b.dbeta = P<float*>(std::get<9>(t));
+    return b;
+  };
+  m.def("bn_bwd_apply_dual", [bside](uintptr_t dy, BSideT a, BSideT b, long R, int C, uintptr_t st) {
+    return bn_bwd_apply_dual(P<const void*>(dy), bside(a), bside(b), R, C, S(st));
+  });
   m.def("bn_stat_reduce2", [](int mode, uintptr_t slab, int rows, uintptr_t out, uintptr_t part, uintptr_t slab2, int rows2,
                               uintptr_t out2, uintptr_t part2, int C, uintptr_t st) {
     bn_stat_reduce2(mode, P<const float*>(slab), rows, P<float*>(out), P<float*>(part), P<const float*>(slab2), rows2,

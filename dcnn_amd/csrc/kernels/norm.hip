@@ -760,6 +760,96 @@ __global__ void __launch_bounds__(256) bn_apply_dual_kernel(BnSide a, BnSide b, 
 
 bool bn_apply_dual_supported(long R, int C) { return C % 8 == 0 && R * (long)C < (1l << 31); }
 
+// Backward of two BatchNorms fed the same gradient dy (a residual block's tail and its projection
+// shortcut): dx_a and dx_b from one read of dy, each side with bn_bwd_apply_v_kernel's
+// 3-coefficient algebra (identical per-element results) and workgroup 0 accumulating its dgamma
+// / dbeta.
+__device__ __forceinline__ void bn_bwd_side_coeffs(const BnBwdSide& b, int C, float* ca, float* cbm, float* cm,
+                                                   float* cd, bool first) {
+  for (int c = threadIdx.x; c < C; c += 256) {
+    const float g = b.gamma ? b.gamma[c] : 1.f, is = b.istd[c];
+    float sdy = 0.f, sdyx = 0.f;
+    if (b.sums) read_stats<1>(b.sums, b.parts, C, c, sdy, sdyx);
+    const float a = g * is;
+    ca[c] = a;
+    cbm[c] = -a * is * (sdyx / b.count);
+    cm[c] = b.mean[c];
+    cd[c] = -a * (sdy / b.count);
+    if (first && b.sums) {
+      if (b.dgamma) b.dgamma[c] += sdyx;
+      if (b.dbeta) b.dbeta[c] += sdy;
+    }
+  }
+}
+
+__global__ void __launch_bounds__(256) bn_bwd_apply_dual_kernel(const bf16* __restrict__ dy, BnBwdSide a,
+                                                                BnBwdSide b, unsigned nv, int C) {
+  extern __shared__ __attribute__((aligned(16))) float sh[];
+  float* k = sh;  // [2 sides][4 coefficient arrays][C]
+  const bf16* __restrict__ xa = static_cast<const bf16*>(a.x);
+  const bf16* __restrict__ xb = static_cast<const bf16*>(b.x);
+  bf16* __restrict__ da = static_cast<bf16*>(a.dx);
+  bf16* __restrict__ db = static_cast<bf16*>(b.dx);
+  const unsigned stride = gridDim.x * 256u, cv = (unsigned)C / 8;
+  unsigned i = blockIdx.x * 256u + threadIdx.x;
+  uint4 vd{}, va{}, vb{};
+  if (i < nv) {
+    vd = ldg16(dy + (size_t)i * 8);
+    va = ldg16(xa + (size_t)i * 8);
+    vb = ldg16(xb + (size_t)i * 8);
+  }
+  bn_bwd_side_coeffs(a, C, k, k + C, k + 2 * C, k + 3 * C, blockIdx.x == 0);
+  bn_bwd_side_coeffs(b, C, k + 4 * C, k + 5 * C, k + 6 * C, k + 7 * C, blockIdx.x == 0);
+  __syncthreads();
+  auto ld8 = [](const float* p, float* o) {
+    const float4 u = *reinterpret_cast<const float4*>(p), v = *reinterpret_cast<const float4*>(p + 4);
+    o[0] = u.x; o[1] = u.y; o[2] = u.z; o[3] = u.w; o[4] = v.x; o[5] = v.y; o[6] = v.z; o[7] = v.w;
+  };
+  while (i < nv) {
+    const unsigned inx = i + stride;
+    uint4 nd{}, na{}, nb{};
+    if (inx < nv) {
+      nd = ldg16(dy + (size_t)inx * 8);
+      na = ldg16(xa + (size_t)inx * 8);
+      nb = ldg16(xb + (size_t)inx * 8);
+    }
+    const int c0 = (int)(i % cv) * 8;
+    float d[8];
+    unpack8(vd, d);
+#pragma unroll
+    for (int side = 0; side < 2; ++side) {
+      const float* ks = k + side * 4 * C;
+      float A[8], B[8], M[8], D[8], xf[8], o[8];
+      ld8(ks + c0, A);
+      ld8(ks + C + c0, B);
+      ld8(ks + 2 * C + c0, M);
+      ld8(ks + 3 * C + c0, D);
+      unpack8(side == 0 ? va : vb, xf);
+#pragma unroll
+      for (int v = 0; v < 8; ++v) o[v] = A[v] * d[v] + B[v] * (xf[v] - M[v]) + D[v];
+      *reinterpret_cast<uint4*>((side == 0 ? da : db) + (size_t)i * 8) = pack8(o);
+    }
+    i = inx;
+    vd = nd;
+    va = na;
+    vb = nb;
+  }
+}
+
+bool bn_bwd_apply_dual(const void* dy, const BnBwdSide& a, const BnBwdSide& b, long R, int C, hipStream_t s) {
+  if (!bn_apply_dual_supported(R, C)) return false;
+  const unsigned nv = (unsigned)(R * C / 8);
+  long g = (nv + 255) / 256;
+  if (g > 1024) g = 1024;
+  if (g < 1) g = 1;
+  hipLaunchKernelGGL(bn_bwd_apply_dual_kernel, dim3((unsigned)g), dim3(256), 8 * C * sizeof(float), s,
+                     static_cast<const bf16*>(dy), a, b, nv, C);
+  DCNN_LAUNCH_CHECK();
+  return true;
+}
+
+
+
 bool bn_apply_dual(const BnSide& a, const BnSide& b, void* y, long R, int C, int relu, hipStream_t s) {
   if (!bn_apply_dual_supported(R, C)) return false;
   const unsigned nv = (unsigned)(R * C / 8);

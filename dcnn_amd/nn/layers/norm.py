@@ -165,6 +165,12 @@ class BatchNorm(ParameterizedLayer):
         if x.is_cuda:
             from ...ops import hip
             pre = getattr(grad, "_bnb", None)
+            if pre is not None and pre[0] is self and isinstance(pre[1], str) and pre[1] == "done":
+                # data gradient (and dgamma / dbeta) already produced by a residual block's paired
+                # backward (hip.bn_bwd_apply_dual); the incoming gradient is the masked one
+                if self.emit_masked_grad:
+                    self._last_masked[mb_id] = grad
+                return pre[2]
             fused = pre[1:] if (pre is not None and pre[0] is self) else None
             if yout is _POOLED:
                 if fused is None:

@@ -217,9 +217,18 @@ class ResidualBlock(Layer):
         xs, _, ms, iss, _ = ent
         raw = hip.bn_bwd_stats_raw(grad, xs, ms, iss)
         sa, sb = hip.stat_reduce_pair(1, (pre[1], pre[2], pre[3]), raw, grad.shape[1])
-        grad._bnb = (pre[0], sa, pre[2], pre[3])
-        d = grad.detach()  # same storage, its own fused-statistics tag
-        d._bnb = (bns, sb, raw[1], raw[2])
+        d = grad.detach()  # same storage, its own tag for the shortcut BatchNorm
+        tail = self.main_path[-1]
+        tent = tail._cache.get(mb_id)
+        done = tent is not None and hip.bn_dual_ok(tent[0]) and tuple(tent[0].shape) == tuple(xs.shape)
+        if done:
+            # both data gradients from one read of the shared gradient (hip.bn_bwd_apply_dual)
+            dx_t, dx_s = hip.bn_bwd_apply_dual(grad, (tail, tent, sa), (bns, ent, sb))
+            grad._bnb = (tail, "done", dx_t)
+            d._bnb = (bns, "done", dx_s)
+        else:
+            grad._bnb = (pre[0], sa, pre[2], pre[3])
+            d._bnb = (bns, sb, raw[1], raw[2])
         return d
 
     def bwd_bn_spec(self, mb_id=0):

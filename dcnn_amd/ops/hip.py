@@ -1079,6 +1079,26 @@ def bn_bwd_stats_raw(dy, x, mean, istd):
     return slab, rows, sums
 
 
+def bn_bwd_apply_dual(dy, a, b):
+    """Data gradients of two training BatchNorms fed the same (masked) gradient ``dy`` in one pass
+    (norm.hip bn_bwd_apply_dual); ``a``/``b`` = (layer, its forward cache entry (x, _, mean, istd,
+    _), reduced backward :class:`Stats`). Accumulates each layer's dgamma / dbeta."""
+    R, C = _rc(dy)
+    outs, sides = [], []
+    for layer, ent, st in (a, b):
+        x, _, mean, istd, _ = ent
+        dx = torch.empty_like(x, memory_format=CL)
+        sp, parts = _stats(st)
+        dg = layer._grads[0].view(-1) if layer.affine else None
+        db = layer._grads[1].view(-1) if layer.affine else None
+        sides.append((x.data_ptr(), dx.data_ptr(), mean.data_ptr(), istd.data_ptr(), ptr(layer._gamma()), sp, parts,
+                      float(R), ptr(dg), ptr(db)))
+        outs.append(dx)
+    if not kernels().bn_bwd_apply_dual(dy.data_ptr(), sides[0], sides[1], R, C, stream_ptr()):
+        raise RuntimeError("bn_bwd_apply_dual: unsupported shape")
+    return outs[0], outs[1]
+
+
 def stat_reduce_pair(mode, a, b, C):
     """Two independent forward/backward statistics reduces of the same C in ONE launch
     (norm.hip bn_stat_reduce2); ``a``/``b`` = (slab, rows, out). Returns two :class:`Stats`."""
