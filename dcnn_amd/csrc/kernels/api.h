@@ -223,7 +223,8 @@ void col2im(const float* col, float* x, int N, int C, int H, int W, int KH, int 
             int OH, int OW, hipStream_t s);
 int loss_workspace_floats(int N);
 void loss_fused(int dt, const void* pred, const float* target, const int64_t* labels, void* grad, float* loss_out,
-                int* correct, int N, int C, int type, float param, float* ws, unsigned* ticket, hipStream_t s);
+                int* correct, int N, int C, int type, float param, float gscale, float* ws, unsigned* ticket,
+                hipStream_t s);
 void adam_step(float* p, const float* g, float* m, float* v, bf16* shadow, long n, float lr, float b1, float b2,
                float eps, float bc1, float bc2, float wd, int decoupled, const float* hyper, hipStream_t s);
 void sgd_step(float* p, const float* g, float* vel, bf16* shadow, long n, float lr, float mom, const float* hyper,

@@ -440,10 +440,11 @@ PYBIND11_MODULE(_kernels, m) {
   });
   m.def("loss_workspace_floats", &loss_workspace_floats);
   m.def("loss_fused", [](int dt, uintptr_t pred, uintptr_t target, uintptr_t labels, uintptr_t grad, uintptr_t loss,
-                         uintptr_t correct, int N, int C, int type, float param, uintptr_t ws, uintptr_t ticket,
-                         uintptr_t st) {
+                         uintptr_t correct, int N, int C, int type, float param, float gscale, uintptr_t ws,
+                         uintptr_t ticket, uintptr_t st) {
     loss_fused(dt, P<const void*>(pred), P<const float*>(target), P<const int64_t*>(labels), P<void*>(grad),
-               P<float*>(loss), P<int*>(correct), N, C, type, param, P<float*>(ws), P<unsigned*>(ticket), S(st));
+               P<float*>(loss), P<int*>(correct), N, C, type, param, gscale, P<float*>(ws), P<unsigned*>(ticket),
+               S(st));
   });
   m.def("adam_step", [](uintptr_t p, uintptr_t g, uintptr_t mm, uintptr_t v, uintptr_t shadow, long n, float lr,
                         float b1, float b2, float eps, float bc1, float bc2, float wd, int dec, uintptr_t hyper,

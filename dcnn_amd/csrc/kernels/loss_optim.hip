@@ -22,7 +22,8 @@ enum LossType { kCE = 0, kSoftmaxCE = 1, kLogSoftmaxCE = 2, kMSE = 3, kMAE = 4, 
 template <typename T>
 __device__ __forceinline__ void loss_row(const T* __restrict__ pred, const float* __restrict__ target,
                                          const int64_t* __restrict__ labels, T* __restrict__ grad, int row, int N,
-                                         int C, int type, float param, int lane, float* lsum_out, int* hit) {
+                                         int C, int type, float param, float gscale, int lane, float* lsum_out,
+                                         int* hit) {
   const T* p = pred + (long)row * C;
   auto tgt = [&](int c) -> float {
     if (labels) return (int64_t)c == labels[row] ? 1.f : 0.f;
@@ -44,6 +45,9 @@ __device__ __forceinline__ void loss_row(const T* __restrict__ pred, const float
     if (tv > tm || (tv == tm && tj < ti)) { tm = tv; ti = tj; }
   }
   const float invN = 1.f / (float)N, invNC = 1.f / ((float)N * (float)C);
+  // gradient scale: gscale = 1 / world under data parallelism (the gradient average folded into
+  // the loss gradient, so no separate pass scales it)
+  const float ginvN = invN * gscale, ginvNC = invNC * gscale;
   float lsum = 0.f;
   if (type == kSoftmaxCE || type == kLogSoftmaxCE) {
     float s = 0.f;
@@ -59,7 +63,7 @@ __device__ __forceinline__ void loss_row(const T* __restrict__ pred, const float
     if (grad) {
       const float inv_s = 1.f / s;
       for (int c = lane; c < C; c += 64)
-        grad[(long)row * C + c] = from_f<T>((__expf(to_f(p[c]) - pm) * inv_s - tgt(c)) * invN);
+        grad[(long)row * C + c] = from_f<T>((__expf(to_f(p[c]) - pm) * inv_s - tgt(c)) * ginvN);
     }
   } else if (type == kCE) {
     int hot = 0x7fffffff;
@@ -72,16 +76,16 @@ __device__ __forceinline__ void loss_row(const T* __restrict__ pred, const float
     }
     if (grad)
       for (int c = lane; c < C; c += 64)
-        grad[(long)row * C + c] = from_f<T>((to_f(p[c]) - tgt(c)) * invN);
+        grad[(long)row * C + c] = from_f<T>((to_f(p[c]) - tgt(c)) * ginvN);
   } else {
     for (int c = lane; c < C; c += 64) {
       const float d = to_f(p[c]) - tgt(c), ad = fabsf(d);
       float l, g;
-      if (type == kMSE) { l = d * d; g = 2.f * d * invNC; }
-      else if (type == kMAE) { l = ad; g = d > 0.f ? invNC : -invNC; }
+      if (type == kMSE) { l = d * d; g = 2.f * d * ginvNC; }
+      else if (type == kMAE) { l = ad; g = d > 0.f ? ginvNC : -ginvNC; }
       else {
-        if (ad <= param) { l = 0.5f * d * d; g = d * invNC; }
-        else { l = param * ad - 0.5f * param * param; g = (d > 0.f ? param : -param) * invNC; }
+        if (ad <= param) { l = 0.5f * d * d; g = d * ginvNC; }
+        else { l = param * ad - 0.5f * param * param; g = (d > 0.f ? param : -param) * ginvNC; }
       }
       lsum += l;
       if (grad) grad[(long)row * C + c] = from_f<T>(g);
@@ -96,8 +100,8 @@ template <typename T>
 __global__ void __launch_bounds__(256) loss_kernel(const T* __restrict__ pred, const float* __restrict__ target,
                                                    const int64_t* __restrict__ labels, T* __restrict__ grad,
                                                    float* __restrict__ loss_out, int* __restrict__ correct, int N,
-                                                   int C, int type, float param, float* __restrict__ rowv,
-                                                   unsigned* __restrict__ ticket) {
+                                                   int C, int type, float param, float gscale,
+                                                   float* __restrict__ rowv, unsigned* __restrict__ ticket) {
   __shared__ float sl[256];
   __shared__ int sc[256];
   __shared__ int last;
@@ -105,7 +109,7 @@ __global__ void __launch_bounds__(256) loss_kernel(const T* __restrict__ pred, c
   const int row = blockIdx.x * 4 + w;
   float lsum = 0.f;
   int hits = 0;
-  if (row < N) loss_row<T>(pred, target, labels, grad, row, N, C, type, param, lane, &lsum, &hits);
+  if (row < N) loss_row<T>(pred, target, labels, grad, row, N, C, type, param, gscale, lane, &lsum, &hits);
   if (gridDim.x == 1) {
     if (lane == 0) { sl[w] = lsum; sc[w] = hits; }
     __syncthreads();
@@ -154,15 +158,16 @@ __global__ void __launch_bounds__(256) loss_kernel(const T* __restrict__ pred, c
 int loss_workspace_floats(int N) { return 2 * N; }
 
 void loss_fused(int dt, const void* pred, const float* target, const int64_t* labels, void* grad, float* loss_out,
-                int* correct, int N, int C, int type, float param, float* ws, unsigned* ticket, hipStream_t s) {
+                int* correct, int N, int C, int type, float param, float gscale, float* ws, unsigned* ticket,
+                hipStream_t s) {
   const int blocks = (N + 3) / 4;
   if (blocks > 1 && (!ws || !ticket)) throw std::runtime_error("loss_fused: workspace required");
   if (dt == 0)
     hipLaunchKernelGGL(loss_kernel<float>, dim3(blocks), dim3(256), 0, s, (const float*)pred, target, labels,
-                       (float*)grad, loss_out, correct, N, C, type, param, ws, ticket);
+                       (float*)grad, loss_out, correct, N, C, type, param, gscale, ws, ticket);
   else
     hipLaunchKernelGGL(loss_kernel<bf16>, dim3(blocks), dim3(256), 0, s, (const bf16*)pred, target, labels,
-                       (bf16*)grad, loss_out, correct, N, C, type, param, ws, ticket);
+                       (bf16*)grad, loss_out, correct, N, C, type, param, gscale, ws, ticket);
   DCNN_LAUNCH_CHECK();
 }
 

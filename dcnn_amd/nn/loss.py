@@ -60,19 +60,22 @@ class Loss:
         return self._2d(target).to(pred2d.device), None
 
     # ---- fused device path
-    def loss_and_grad(self, pred, target, want_grad: bool = True):
-        """(loss[1] device tensor, grad shaped like pred | None, correct[1] int32)."""
+    def loss_and_grad(self, pred, target, want_grad: bool = True, grad_scale: float = 1.0):
+        """(loss[1] device tensor, grad shaped like pred | None, correct[1] int32). The gradient is
+        scaled by an extra ``grad_scale`` (data parallel folds its 1 / world average in here)."""
         p2 = self._2d(pred)
         if p2.is_cuda:
             from ..ops import hip
             t2, lab = self._targets(p2, target)
-            loss, grad, correct = hip.loss_fused(p2, t2, lab, self.kind, self.param, want_grad)
+            loss, grad, correct = hip.loss_fused(p2, t2, lab, self.kind, self.param, want_grad, grad_scale)
             return loss, (grad.view(pred.shape) if grad is not None else None), correct
         from ..ops import cpu
         t2, lab = self._targets(p2, target)
         if p2.dtype not in (torch.float32, torch.float64):
             p2 = p2.float()
         loss, grad, correct = cpu.loss_fused(p2, t2, lab, self.kind, self.param, want_grad)
+        if grad is not None and grad_scale != 1.0:
+            grad.mul_(grad_scale)
         return loss, (grad.view(pred.shape) if grad is not None else None), correct
 
     # ---- reference API

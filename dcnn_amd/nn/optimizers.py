@@ -72,6 +72,9 @@ class Optimizer:
                 self.arena = None
         if self.arena is not None:
             self._flat_p, self._flat_g = self.arena.data, self.arena.grad
+        # re-attaching resets the step state (Adam t, m, v): the device scalars (step counter,
+        # learning rate) must be re-uploaded too, or the device keeps counting from the old t
+        self._hyper_dirty = True
         self._on_attach()
 
     def _on_attach(self):

@@ -1399,8 +1399,10 @@ LOSS_CODES = {"crossentropy": 0, "softmax_crossentropy": 1, "logsoftmax_crossent
               "huber": 5}
 
 
-def loss_fused(pred2d, target2d=None, labels=None, kind="softmax_crossentropy", param=1e-15, want_grad=True):
-    """Returns (loss[1] f32 device, grad|None, correct[1] int32 device). No host sync."""
+def loss_fused(pred2d, target2d=None, labels=None, kind="softmax_crossentropy", param=1e-15, want_grad=True,
+               grad_scale=1.0):
+    """Returns (loss[1] f32 device, grad|None, correct[1] int32 device). No host sync. The gradient
+    is additionally multiplied by ``grad_scale`` inside the kernel (data parallel: 1 / world)."""
     N, C = pred2d.shape
     pred2d = pred2d.contiguous()
     grad = torch.empty_like(pred2d) if want_grad else None
@@ -1414,7 +1416,8 @@ def loss_fused(pred2d, target2d=None, labels=None, kind="softmax_crossentropy", 
     ws = torch.empty((K.loss_workspace_floats(N),), dtype=F32, device=pred2d.device) if N > 4 else None
     tk = _ticket(pred2d.device, 0, slot="loss") if N > 4 else None
     K.loss_fused(dt_code(pred2d.dtype), pred2d.data_ptr(), ptr(tgt), ptr(lab), ptr(grad), loss.data_ptr(),
-                 correct.data_ptr(), N, C, LOSS_CODES[kind], float(param), ptr(ws), ptr(tk), stream_ptr())
+                 correct.data_ptr(), N, C, LOSS_CODES[kind], float(param), float(grad_scale), ptr(ws), ptr(tk),
+                 stream_ptr())
     return loss, grad, correct
 
 

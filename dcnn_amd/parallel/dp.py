@@ -9,9 +9,9 @@ layer backwards, so ResNet-18-tiny gets 19 / 15 / 4.7 / 4.9 / 1.5 MB buckets): t
 all-reduce that cannot overlap compute is the trailing one after the stem's backward, so it
 should be small, while every bucket stays large enough to run near per-link xGMI bandwidth.
 
-The 1/world factor of the gradient average is folded into the incoming loss gradient (every
-gradient is linear in it), so the all-reduce is a plain SUM and no extra pass over the
-45 MB gradient buffer is needed.
+The 1/world factor of the gradient average is folded into the loss gradient (every gradient is
+linear in it) — the fused loss kernel multiplies it in (``grad_scale``) — so the all-reduce is a
+plain SUM and neither the gradient buffer nor the loss gradient needs an extra pass.
 
 ``grad_dtype="bf16"`` halves the wire bytes: a bucket is packed to bf16, exchanged as shards
 (``all_to_all``), each rank sums the world copies of its shard in fp32 in rank order
@@ -70,6 +70,11 @@ class DataParallel:
         if grad_dtype not in ("fp32", "bf16"):
             raise ValueError("grad_dtype must be 'fp32' or 'bf16'")
         self.grad_dtype = grad_dtype
+        # at world size 1 a SUM all-reduce is the identity: skip the RCCL launches (the --pg
+        # bench and single-GPU runs pay nothing for the group). DCNN_DP_FORCE_COLLECTIVES=1 keeps
+        # them, so a one-GPU box can still exercise RCCL capture / replay (tests/test_gpu_dp.py).
+        import os
+        self.force_collectives = os.environ.get("DCNN_DP_FORCE_COLLECTIVES", "0") == "1"
         self._works: List = []
         self._pending_unpack: List = []
         self._wire = {}          # (lo, hi) -> persistent bf16 wire buffers of that bucket
@@ -137,8 +142,15 @@ class DataParallel:
 
     __call__ = forward
 
-    def backward(self, grad, mb_id: int = 0, sync: bool = True):
-        if self.world > 1:
+    @property
+    def grad_scale(self) -> float:
+        """Factor the loss gradient carries (``Loss.loss_and_grad(grad_scale=...)``): 1 / world."""
+        return 1.0 / self.world if self.world > 1 else 1.0
+
+    def backward(self, grad, mb_id: int = 0, sync: bool = True, prescaled: bool = False):
+        """Backward + bucketed SUM all-reduce. ``prescaled``: ``grad`` already carries the 1 / world
+        average (the fused loss kernel applied ``grad_scale``), else it is scaled here."""
+        if self.world > 1 and not prescaled:
             grad = grad * (1.0 / self.world)
         m = self.model
         cur = grad
@@ -159,6 +171,8 @@ class DataParallel:
     # ---------------------------------------------------------------- bucket collectives
     def reduce_bucket(self, lo: int, hi: int) -> None:
         """Start the SUM all-reduce of ``arena.grad[lo:hi]`` (completed by :meth:`finish`)."""
+        if self.world == 1 and not self.force_collectives:
+            return
         flat = self.model.arena.grad
         if self.grad_dtype == "fp32" or self.world == 1:
             self._works.append(dist.all_reduce(flat[lo:hi], op=dist.ReduceOp.SUM, group=self.pg, async_op=True))

@@ -96,6 +96,7 @@ class Coordinator:
         self._stash: Dict[int, list] = {}
         # recovery: parameter snapshots every snapshot_every steps, re-deploy + reload on failure
         self.snapshot_every = 0
+        self._replay_log, self._replay_pending = [], False
         self.max_recoveries = 0
         self.recoveries = 0
         self.steps = 0
@@ -234,10 +235,10 @@ class Coordinator:
         return self.transport.recv(msg, self.device)
 
     def _loss_grad(self, out, y, mb):
-        loss, grad, correct = self.loss.loss_and_grad(out, y.to(out.device, non_blocking=True))
-        if self.grad_scale == "mean" and self.num_microbatches > 1:
-            grad = grad.mul_(1.0 / self.num_microbatches)
-        return loss, grad.to(out.dtype), correct
+        # the micro-batch mean (1 / num_microbatches) is applied inside the fused loss kernel
+        scale = 1.0 / self.num_microbatches if self.grad_scale == "mean" and self.num_microbatches > 1 else 1.0
+        loss, grad, correct = self.loss.loss_and_grad(out, y.to(out.device, non_blocking=True), grad_scale=scale)
+        return loss, (grad if grad.dtype == out.dtype else grad.to(out.dtype)), correct
 
     def _finish(self, losses, corrects) -> float:
         """ONE host sync per step: the micro-batch losses / correct counts stay on the device
@@ -360,16 +361,26 @@ class Coordinator:
             try:
                 if self._snapshot is None:
                     self.snapshot()
+                if self._replay_pending:
+                    # a recovery rolled the stages back to the last snapshot: re-train the batches
+                    # stepped since then (same order, same schedule) before this one
+                    for rfn, rxs, rys in self._replay_log:
+                        rfn(rxs, rys)
+                        self.update_parameters()
+                        self.steps += 1
+                    self._replay_pending = False
                 loss = fn(xs, ys)
                 self.update_parameters()
                 self.steps += 1
                 if self.steps % self.snapshot_every == 0:
                     self.snapshot()
+                else:
+                    self._replay_log.append((fn, xs, ys))
                 return loss
             except PipelineError:
                 if self.recoveries >= self.max_recoveries:
                     raise
-                self.recover()  # then retry this batch from the last snapshot
+                self.recover()  # then replay the batches since the snapshot and retry this one
 
     # ------------------------------------------------------------------ recovery
     def enable_recovery(self, snapshot_every: int = 1, max_recoveries: int = 3) -> None:
@@ -383,6 +394,8 @@ class Coordinator:
     def snapshot(self) -> None:
         self._snapshot = self.collect_parameters()
         self._snapshot_step = self.steps
+        self._replay_log = []  # (schedule fn, micro-batches x, y) of every step after the snapshot
+        self._replay_pending = False
 
     def recover(self) -> None:
         """Restart failed stages, re-deploy the topology and reload the last snapshot."""
@@ -398,6 +411,7 @@ class Coordinator:
                 self.comm.send(M.job_message(self.stage_names[i], C.LOAD_PARAMS, 0, flat))
             self.join(C.PARAMS_LOADED, self.num_stages)
             self.steps = self._snapshot_step
+            self._replay_pending = bool(self._replay_log)
         self.start()
 
     def _restart_stages(self) -> None:

@@ -47,8 +47,8 @@ class TrainStep:
     def eager(self, x, y):
         self.opt.clear_gradients()
         out = self.dp.forward(x)
-        loss, grad, correct = self.loss_fn.loss_and_grad(out, y)
-        self.dp.backward(grad)
+        loss, grad, correct = self.loss_fn.loss_and_grad(out, y, grad_scale=self.dp.grad_scale)
+        self.dp.backward(grad, prescaled=True)
         self.opt.update()
         self.last_loss, self.last_correct = loss, correct
         return loss
@@ -158,7 +158,6 @@ class TrainStep:
         self.opt.prepare_step()  # upload scalars used during capture (replays re-upload)
         if hasattr(self.opt, "t"):
             self.opt.t -= 1  # the capture itself is not a training step
-        world = self.dp.world
         active = self.dp.active
         for k, (hi, lo) in enumerate(segs):
             g = torch.cuda.CUDAGraph()
@@ -166,9 +165,9 @@ class TrainStep:
                 if k == 0:
                     self.opt.clear_gradients()
                     out = self.dp.forward(self._static_x)
-                    loss, grad, correct = self.loss_fn.loss_and_grad(out, self._static_y)
+                    loss, cur, correct = self.loss_fn.loss_and_grad(out, self._static_y,
+                                                                    grad_scale=self.dp.grad_scale)
                     self._g_loss, self._g_correct = loss, correct
-                    cur = grad * (1.0 / world) if world > 1 else grad
                     self.model.prepare_backward()
                 else:
                     cur = self._carry
@@ -202,9 +201,9 @@ class TrainStep:
             with capture_guard(), torch.cuda.graph(g, stream=self._capture_stream(), capture_error_mode="thread_local"):
                 self.opt.clear_gradients()
                 out = self.dp.forward(self._static_x)
-                loss, grad, correct = self.loss_fn.loss_and_grad(out, self._static_y)
+                loss, grad, correct = self.loss_fn.loss_and_grad(out, self._static_y, grad_scale=self.dp.grad_scale)
                 self._g_loss, self._g_correct = loss, correct
-                self.dp.backward(grad, sync=True)
+                self.dp.backward(grad, sync=True, prescaled=True)
                 self.opt.launch_step()
         finally:
             m.enable_profiling_ = prof
@@ -221,16 +220,14 @@ class TrainStep:
             self.last_loss, self.last_correct = self._g_loss, self._g_correct
             return self.last_loss
         active = self.dp.active
-        flat = self.model.arena.grad
-        works = []
         for k, (hi, lo) in enumerate(self._segs):
             self.graphs[k].replay()
             if active and k < len(self._fires):
-                a, b = self.dp.fire[self._fires[k]]
-                works.append(dist.all_reduce(flat[a:b], op=dist.ReduceOp.SUM, group=self.dp.pg, async_op=True))
+                # the same bucket collective as the eager / whole-graph steps (fp32 SUM, or the
+                # bf16 wire pipeline when DataParallel(grad_dtype="bf16"))
+                self.dp.reduce_bucket(*self.dp.fire[self._fires[k]])
         if active:
-            for w in works:
-                w.wait()
+            self.dp.finish()
             self.graphs[-1].replay()
         self.last_loss, self.last_correct = self._g_loss, self._g_correct
         return self.last_loss

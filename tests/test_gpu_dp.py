@@ -63,7 +63,8 @@ def _rccl_worker(rank, port, out, with_pg, use_graph, whole=True):
     process group's watchdog; the bucket all-reduces are captured inside the step graph
     (``whole``) or run between segment replays (DCNN_DP_CAPTURE=0)."""
     import torch.distributed as dist
-    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), DCNN_DP_CAPTURE="1" if whole else "0")
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), DCNN_DP_CAPTURE="1" if whole else "0",
+                      DCNN_DP_FORCE_COLLECTIVES="1")  # world 1 skips the identity all-reduce otherwise
     torch.cuda.set_device(0)
     if with_pg:
         dist.init_process_group("nccl", rank=0, world_size=1, device_id=torch.device("cuda", 0))
@@ -74,8 +75,8 @@ def _rccl_worker(rank, port, out, with_pg, use_graph, whole=True):
     m = zoo.create_model("resnet18_tiny_imagenet")
     m.set_seed(5)
     m.set_device("GPU:0")
-    # fp32 compute: run-to-run noise of the statistics atomics is ~1e-3 of a first-step weight
-    # gradient there (bf16 roundings amplify it to ~20% at random init)
+    # fp32 compute (the kernels are deterministic: eager and graph steps run the same kernels in
+    # the same order, so every variant must agree bit for bit)
     m.set_compute_dtype(torch.float32)
     m.initialize()
     m.set_first_layer_input_grad(False)
@@ -100,8 +101,8 @@ def _rccl_worker(rank, port, out, with_pg, use_graph, whole=True):
 
 def test_gpu_dp_rccl_world1_graph_segments(tmp_path):
     """RCCL group, collectives captured in the step graph == segmented graph step == graph step
-    without a group == eager step; the graph warm-up must not train (first-step losses agree
-    with eager). The deterministic kernels make the three graph variants bit-identical."""
+    without a group == eager step, bit for bit (deterministic kernels; an all-reduce over one rank
+    is exact); the graph warm-up must not train (first-step losses equal eager)."""
     for with_pg, use_graph, whole in ((True, True, True), (True, True, False), (False, True, True),
                                       (False, False, True)):
         mp.spawn(_rccl_worker, args=(_port(), str(tmp_path), with_pg, use_graph, whole), nprocs=1, join=True)
@@ -114,13 +115,8 @@ def test_gpu_dp_rccl_world1_graph_segments(tmp_path):
     assert w["losses"] == a["losses"] == b["losses"], (w["losses"], a["losses"], b["losses"])
     assert torch.equal(w["g"], a["g"]) and torch.equal(w["g"], b["g"])
     for r in (w, a, b):
-        # weight gradients (biases ahead of a BatchNorm have ~zero true gradient: skipped)
-        for o, n in e["big"]:
-            ge, gr = e["g"][o:o + n], r["g"][o:o + n]
-            assert (ge - gr).norm() <= 3e-2 * ge.norm(), (o, n, (ge - gr).norm(), ge.norm())
-        assert abs(r["losses"][0] - e["losses"][0]) < 1e-5 * abs(e["losses"][0]), (r["losses"], e["losses"])
-        for lr_, le in zip(r["losses"], e["losses"]):
-            assert abs(lr_ - le) < 3e-2 * max(1.0, abs(le)), (r["losses"], e["losses"])
+        assert torch.equal(r["g"], e["g"]), (r["g"] - e["g"]).abs().max()
+        assert r["losses"] == e["losses"], (r["losses"], e["losses"])
 
 
 def _bnfree_model(seed):

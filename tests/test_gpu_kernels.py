@@ -476,6 +476,29 @@ def test_adam_sgd_flat():
         assert rel_err(ar.shadow_view(0).float(), ar.param(0)) < 1e-2
 
 
+def test_adam_reattach_restarts_device_step_counter():
+    """An optimizer attached a second time restarts t, m, v: the device-side step counter and
+    bias corrections must restart too, matching the host (CPU arena) update."""
+    from dcnn_amd.nn.params import ParamArena, ParamSpec
+    from dcnn_amd.nn.optimizers import Adam
+    res = []
+    for dev in ["cpu", "cuda"]:
+        torch.manual_seed(7)
+        ar = ParamArena([ParamSpec("a", (5, 4, 3, 3), True)], torch.device(dev),
+                        torch.bfloat16 if dev == "cuda" else None)
+        ar.param(0).copy_(torch.randn(5, 4, 3, 3))
+        ar.sync_shadow(force=True)
+        opt = Adam(1e-2)
+        grads = [torch.randn(5, 4, 3, 3) for _ in range(5)]
+        for attach_round in range(2):
+            opt.attach([ar.param(0)], [ar.grad_view(0)], ar)
+            for g in grads[:3] if attach_round == 0 else grads[3:]:
+                ar.grad_view(0).copy_(g)
+                opt.update()
+        res.append(ar.param(0).cpu().clone())
+    assert rel_err(res[1], res[0]) < 1e-5
+
+
 def test_im2col_col2im(hip):
     x = torch.randn(2, 3, 7, 7)
     col = hip.im2col(x.cuda(), 3, 3, 2, 2, 1, 1)

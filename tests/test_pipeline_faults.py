@@ -119,3 +119,27 @@ def test_recovery_gives_up_after_max_recoveries():
         assert coord.recoveries == 0
     finally:
         coord.stop()
+
+
+def test_recovery_replays_steps_since_an_older_snapshot():
+    """snapshot_every=2 and a crash in step 4: the stages roll back to the step-2 snapshot, the
+    coordinator re-trains step 3 from its logged micro-batches, then retries step 4 — the final
+    parameters equal an uninterrupted run (no step silently lost)."""
+    data = _batches(4)
+    ref = _coord()
+    try:
+        ref_losses = [ref.train_step(x, y, "sync") for x, y in data]
+        ref_params = [p.clone() for p in ref.gather_model().parameters()]
+    finally:
+        ref.stop()
+    # 2 micro-batches per step: stage_1's 7th forward is the first micro-batch of step 4
+    coord = _coord({1: ["FORWARD_JOB:7:crash"]}, heartbeat_s=0.2, heartbeat_misses=3, timeout_s=60.0)
+    coord.enable_recovery(snapshot_every=2, max_recoveries=2)
+    try:
+        losses = [coord.train_step(x, y, "sync") for x, y in data]
+        assert coord.recoveries == 1 and coord.steps == 4
+        assert losses == pytest.approx(ref_losses, rel=1e-6)
+        for a, b in zip(coord.gather_model().parameters(), ref_params):
+            torch.testing.assert_close(a, b, rtol=1e-6, atol=1e-7)
+    finally:
+        coord.stop()
