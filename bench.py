@@ -46,6 +46,12 @@ def main():
     ap.add_argument("--device", default="cuda")
     ap.add_argument("--dtype", default="bf16", choices=["bf16", "fp32"],
                     help="compute dtype (fp32: the MFMA f32 path, e.g. the ResNet-9 CIFAR-10 fp32 config)")
+    ap.add_argument("--f32-mode", default=os.environ.get("DCNN_BENCH_F32_MODE", "concat"),
+                    choices=["concat", "split", "exact"],
+                    help="fp32 convolution arithmetic: exact = IEEE fp32 inputs on the f32 MFMA "
+                         "(v_mfma_f32_16x16x4_f32) everywhere; concat = 3xbf16 split precision on the "
+                         "halo convs ([hi|lo|hi] channels, ~2^-16 relative per product) + exact elsewhere; "
+                         "split = 3xbf16 on the gathered GEMMs too")
     a = ap.parse_args()
 
     from dcnn_amd.parallel.dp import DataParallel, init_distributed
@@ -67,6 +73,11 @@ def main():
     dev = torch.device("cuda", local) if a.device == "cuda" else torch.device("cpu")
     if dev.type == "cuda":
         torch.cuda.set_device(dev)
+
+    if a.dtype == "fp32" and dev.type == "cuda":
+        from dcnn_amd.ops import hip as _hip
+        _hip.set_f32_concat(a.f32_mode == "concat")
+        _hip.kernels().set_f32_mode(1 if a.f32_mode == "split" else 0)
 
     model = create_model(a.model)
     model.set_seed(1234)
@@ -120,7 +131,8 @@ def main():
             "config": {"model": a.model, "global_batch": a.batch * world, "per_gpu_batch": a.batch, "seq_len": None,
                        "image_size": [C, H, W], "parallelism": f"dp{world}", "optimizer": "adam",
                        "grad_allreduce": a.grad_dtype if world > 1 else None,
-                       "hipgraph": timed_with_graph, "final_loss": round(loss_val, 4)},
+                       "hipgraph": timed_with_graph, "final_loss": round(loss_val, 4),
+                       "f32_mode": (a.f32_mode if a.dtype == "fp32" and dev.type == "cuda" else None)},
         }), flush=True)
     if a.profile and rank == 0:
         # per-layer HIP-event profile, after the JSON line (eager steps: one event pair per layer)

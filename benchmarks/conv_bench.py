@@ -36,8 +36,11 @@ def main():
     ap.add_argument("--iters", type=int, default=20)
     ap.add_argument("--only", default="")
     ap.add_argument("--shapes", default="", help="comma-separated shape names (default: all)")
+    ap.add_argument("--v3", type=int, default=1, help="third-generation 3x3 halo conv (hconv3.hip) on/off")
+    ap.add_argument("--eager", action="store_true", help="time eager launches instead of one hipGraph replay")
     a = ap.parse_args()
     from dcnn_amd.ops import hip
+    hip.kernels().hconv3_enable(a.v3)
     CL = torch.channels_last
     N = a.batch
     tot = {"fwd": 0.0, "dgrad": 0.0, "wgrad": 0.0}
@@ -71,10 +74,26 @@ def main():
                 fn()
             torch.cuda.synchronize()
             e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-            e0.record()
-            for _ in range(a.iters):
-                fn()
-            e1.record()
+            if a.eager:
+                e0.record()
+                for _ in range(a.iters):
+                    fn()
+                e1.record()
+            else:
+                # device time without host launch overhead: the calls captured into one graph
+                g = torch.cuda.CUDAGraph()
+                s_ = torch.cuda.Stream()
+                s_.wait_stream(torch.cuda.current_stream())
+                with torch.cuda.stream(s_):
+                    with torch.cuda.graph(g, stream=s_):
+                        for _ in range(a.iters):
+                            fn()
+                torch.cuda.current_stream().wait_stream(s_)
+                g.replay()
+                torch.cuda.synchronize()
+                e0.record()
+                g.replay()
+                e1.record()
             torch.cuda.synchronize()
             us = e0.elapsed_time(e1) * 1000 / a.iters
             tot[op] += us

@@ -93,7 +93,7 @@ def build_kernels(force=False, verbose=False, max_workers=None):
     _compile_many(jobs, verbose, max_workers or min(8, os.cpu_count() or 4))
     target = PKG / f"_kernels{EXT_SUFFIX}"
     if force or not target.exists() or any(o.stat().st_mtime > target.stat().st_mtime for o in objs):
-        _run([HIPCC, "-shared", "-fPIC", f"--offload-arch={ARCH}", *map(str, objs), "-o", str(target)],
+        _run([HIPCC, "-shared", "-fPIC", f"--offload-arch={ARCH}", *map(str, objs), "-o", str(target), "-ldl"],
              verbose)
     return target
 

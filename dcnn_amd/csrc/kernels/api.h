@@ -80,14 +80,17 @@ struct HConvArgs {
 void hconv(HConvArgs a, hipStream_t s);
 // split count hconv() will use for this shape, and its output-tile count (workspace sizing)
 int hconv_splits(int NB, int H, int W, int Cs, int N, int ntaps);
-int hconv_tiles(int NB, int H, int W, int N);
-int hconv_tile_elems(int NB, int H, int W, int N);
+int hconv_tiles(int NB, int H, int W, int Cs, int N, int ntaps);
+int hconv_tile_elems(int NB, int H, int W, int Cs, int N, int ntaps);
 void hconv_set_split_target(int t);  // workgroups the split-K decision aims for (0: never split)
 void bn_set_vectorised(int on);   // bf16 BatchNorm apply passes on the vectorised kernels (default on)
 void hconv_set_ws(int on);           // weight-stationary kernel for 64 -> 64 channel 3x3 convs
 void hconv_set_wide(int on);         // 256 x 64 tiles (4 x 1 waves) for 64-channel outputs
 bool hconv_supported(int NB, int H, int W, int Cs, int N, int ntaps);
-int hconv_stat_rows(int NB, int H, int W, int N);
+int hconv_stat_rows(int NB, int H, int W, int Cs, int N, int ntaps, int f32out);
+bool hconv_v3(int NB, int H, int W, int Cs, int N, int ntaps);  // shape runs on hconv3
+void hconv3_enable(int on);
+void hconv3_set_stamps(uintptr_t p);  // diagnostic per-wave timeline buffer (u64 [grid][8][8]) or 0  // third-generation 3x3 kernel (hconv3.hip), default on (DCNN_HCONV3)
 // halo-tiled stride-1 weight gradient (hwgrad.hip): slab[split][Co][t*Cs + c] = partial dW
 struct HWArgs {
   const bf16* dY; const bf16* X; float* slab; float* bias_slab;  // bias_slab[split][Co] (optional)

@@ -17,6 +17,7 @@ namespace py = pybind11;
 
 using namespace dcnn;
 void bind_runtime(py::module_& m);  // runtime.cpp: native Device / Flow / Task / Allocator
+void bind_rccl(py::module_& m);     // rccl.cpp: in-tree RCCL communicator (dlopen)
 template <typename T>
 static inline T P(uintptr_t x) { return reinterpret_cast<T>(x); }
 static inline hipStream_t S(uintptr_t x) { return reinterpret_cast<hipStream_t>(x); }
@@ -57,6 +58,7 @@ PYBIND11_MODULE(_kernels, m) {
   m.doc() = "dcnn_amd HIP/CDNA4 (gfx950) kernel library";
   m.attr("arch") = "gfx950";
   bind_runtime(m);
+  bind_rccl(m);
 
   m.def("gemm_nt",
         [](uintptr_t A, uintptr_t B, uintptr_t C, int M, int N, int K, int lda, int ldb, int ldc, int mode, int nb,
@@ -118,6 +120,9 @@ PYBIND11_MODULE(_kernels, m) {
   m.def("hconv_set_ws", &hconv_set_ws);
   m.def("bn_set_vectorised", &bn_set_vectorised);
   m.def("hconv_tile_elems", &hconv_tile_elems);
+  m.def("hconv3_enable", &hconv3_enable);
+  m.def("hconv_v3", &hconv_v3);
+  m.def("hconv3_set_stamps", &hconv3_set_stamps);
   m.def("hwgrad",
         [](uintptr_t dY, uintptr_t X, uintptr_t slab, uintptr_t bias_slab, unsigned dy_bytes, unsigned x_bytes, int NB,
            int H, int W, int Cs, int Co, std::vector<std::array<int, 2>> taps, int splits, int ldy, int ldx,

@@ -28,6 +28,13 @@
 
 namespace dcnn {
 
+// third-generation kernel (hconv3.hip): 8-wave 64x64-per-wave tiles, 3 taps per barrier
+struct H3Plan {
+  int WC, TWC, HN, NWI, TH, TW, IMG, pitch, splits, tiles_m, tiles_n;
+};
+bool hconv3_plan(int NB, int H, int W, int Cs, int N, int ntaps, H3Plan* pl);
+bool hconv3_try(const HConvArgs& a, hipStream_t s);
+
 namespace {
 constexpr unsigned kOOBh = 0x80000000u;
 
@@ -645,10 +652,12 @@ static int g_split_target = [] {
   const char* e = getenv("DCNN_HCONV_SPLIT");
   return e ? atoi(e) : 512;
 }();
-static int hconv_split_target() { return g_split_target; }
+int hconv_split_target() { return g_split_target; }
 void hconv_set_split_target(int t) { g_split_target = t < 0 ? 0 : t; }
 
-int hconv_tiles(int NB, int H, int W, int N) {
+int hconv_tiles(int NB, int H, int W, int Cs, int N, int ntaps) {
+  H3Plan pl;
+  if (hconv3_plan(NB, H, W, Cs, N, ntaps, &pl)) return pl.tiles_m * pl.tiles_n;
   HConvArgs a{};
   a.NB = NB; a.H = H; a.W = W; a.N = N;
   int bm, bn;
@@ -656,7 +665,9 @@ int hconv_tiles(int NB, int H, int W, int N) {
   return (NB * H * W + bm - 1) / bm * ((N + bn - 1) / bn);
 }
 
-int hconv_tile_elems(int NB, int H, int W, int N) {
+int hconv_tile_elems(int NB, int H, int W, int Cs, int N, int ntaps) {
+  H3Plan pl;
+  if (hconv3_plan(NB, H, W, Cs, N, ntaps, &pl)) return 32768;  // 8 waves x 64 x 64
   HConvArgs a{};
   a.NB = NB; a.H = H; a.W = W; a.N = N;
   int bm, bn;
@@ -668,14 +679,23 @@ int hconv_tile_elems(int NB, int H, int W, int N) {
 // 64-channel chunks still divide evenly and every split keeps at least 4 taps x chunks of work
 int hconv_splits(int NB, int H, int W, int Cs, int N, int ntaps) {
   if (!hconv_supported(NB, H, W, Cs, N, ntaps)) return 1;
-  const long tiles = hconv_tiles(NB, H, W, N);
+  H3Plan pl;
+  if (hconv3_plan(NB, H, W, Cs, N, ntaps, &pl)) return pl.splits;
+  const long tiles = hconv_tiles(NB, H, W, Cs, N, ntaps);
   const int nchunk = Cs / 64, target = hconv_split_target();
   int s = 1;
   while (target > 0 && tiles * s < target && nchunk % (2 * s) == 0 && (nchunk / (2 * s)) * ntaps >= 4) s *= 2;
   return s;
 }
 
-int hconv_stat_rows(int NB, int H, int W, int N) {
+bool hconv_v3(int NB, int H, int W, int Cs, int N, int ntaps) {
+  H3Plan pl;
+  return hconv3_plan(NB, H, W, Cs, N, ntaps, &pl);
+}
+
+int hconv_stat_rows(int NB, int H, int W, int Cs, int N, int ntaps, int f32out) {
+  H3Plan pl;  // (fp32-output launches stay on hconv_kernel)
+  if (!f32out && hconv3_plan(NB, H, W, Cs, N, ntaps, &pl)) return pl.tiles_m;
   HConvArgs a{};
   a.NB = NB; a.H = H; a.W = W; a.N = N;
   int bm, bn;
@@ -799,12 +819,15 @@ void hconv(HConvArgs a, hipStream_t s) {
   int bm, bn;
   hconv_pick(a, &bm, &bn);
   if (a.fold.part && a.N % 64) throw std::runtime_error("hconv: statistics fold needs N % 64 == 0");
+  if (a.fold.part && !a.Cf && hconv_v3(a.NB, a.H, a.W, a.Cs, a.N, a.ntaps))
+    throw std::runtime_error("hconv: no statistics fold on the hconv3 path (check hconv_v3 first)");
   if (a.fold.part) {
     const int rows = (a.NB * a.H * a.W + bm - 1) / bm;
     if (!a.stats || a.fold.group < 1 || a.fold.rows != rows || !a.fold.tickets ||
         a.fold.ngroups != (rows + a.fold.group - 1) / a.fold.group)
       throw std::runtime_error("hconv: statistics fold rows / groups mismatch");
   }
+  if (!a.fold.part && !a.Cf && hconv3_try(a, s)) return;
   if (launch_hconv_ws(a, s)) return;
   if (a.Cf) {
     if (a.bnb.x) throw std::runtime_error("hconv: no backward-BN fusion with fp32 output");

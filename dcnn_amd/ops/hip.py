@@ -155,8 +155,8 @@ def _hconv_split(K, NB, H, W, Cs, N, ntaps, device):
     s = K.hconv_splits(NB, H, W, Cs, N, ntaps)
     if s == 1:
         return 1, 0, 0
-    tiles = K.hconv_tiles(NB, H, W, N)
-    part = torch.empty(tiles * s * K.hconv_tile_elems(NB, H, W, N), dtype=F32, device=device)
+    tiles = K.hconv_tiles(NB, H, W, Cs, N, ntaps)
+    part = torch.empty(tiles * s * K.hconv_tile_elems(NB, H, W, Cs, N, ntaps), dtype=F32, device=device)
     _SplitWs.keep = part
     return s, part.data_ptr(), _ticket(device, tiles * 64, "hconv").data_ptr()
 
@@ -220,7 +220,7 @@ def conv2d_fwd(x, w, bias, stride, pad, *, stats=False, residual=None, relu=Fals
         y = torch.empty((N, Co, OH, OW), dtype=F32, device=x.device, memory_format=CL)
         slab, rows, sums = None, 0, None
         if stats:
-            rows = K.hconv_stat_rows(N, H, W, Co)
+            rows = K.hconv_stat_rows(N, H, W, 3 * Ci, Co, KH * KW, 1)
             slab = torch.empty((rows, 3, Co), dtype=F32, device=x.device)
             sums = torch.empty((2 * Co,), dtype=F32, device=x.device)  # zeroed in-kernel
         K.hconv(xs.data_ptr(), ws.data_ptr(), 0, _nbytes(xs), _nbytes(ws), N, H, W, 3 * Ci, Co, KH * KW * 3 * Ci,
@@ -245,10 +245,11 @@ def conv2d_fwd(x, w, bias, stride, pad, *, stats=False, residual=None, relu=Fals
         slab, rows, sums = None, 0, None
         fold, fst = _NOFOLD, None
         if stats:
-            rows = K.hconv_stat_rows(N, H, W, Co)
+            rows = K.hconv_stat_rows(N, H, W, Ci, Co, len(taps), 0)
             slab = torch.empty((rows, 3, Co), dtype=F32, device=x.device)
             sums = torch.empty((2 * Co,), dtype=F32, device=x.device)  # zeroed in-kernel
-            fold, fst = _fold(rows, Co, 0, x.device)
+            if not K.hconv_v3(N, H, W, Ci, Co, len(taps)):  # (no in-launch fold on hconv3)
+                fold, fst = _fold(rows, Co, 0, x.device)
         K.hconv(x.data_ptr(), w.data_ptr(), y.data_ptr(), _nbytes(x), _nbytes(w), N, H, W, Ci, Co, KH * KW * Ci,
                 [(t[0], t[1], t[3]) for t in taps], ptr(bias), ptr(residual), ptr(slab), int(relu), ptr(sums),
                 2 * Co if stats else 0, _NOBNB, 0, 0, *_hconv_split(K, N, H, W, Ci, Co, KH * KW, x.device),
@@ -617,10 +618,11 @@ def conv2d_dgrad(dy, wt, x_shape, stride, pad, *, residual=None, bnb=None):
         rows = 0
         fold, fst = _NOFOLD, None
         if fuse:
-            rows = K.hconv_stat_rows(N, H, W, Ci)
+            rows = K.hconv_stat_rows(N, H, W, Co, Ci, len(classes[0][4]), 0)
             slab = torch.empty((rows, 2, Ci), dtype=F32, device=dy.device)
             sums = torch.empty((2 * Ci,), dtype=F32, device=dy.device)  # zeroed in-kernel
-            fold, fst = _fold(rows, Ci, 1, dy.device)
+            if not K.hconv_v3(N, H, W, Co, Ci, len(classes[0][4])):
+                fold, fst = _fold(rows, Ci, 1, dy.device)
         K.hconv(dy.data_ptr(), wt.data_ptr(), dx.data_ptr(), _nbytes(dy), _nbytes(wt), N, OH, OW, Co, Ci, KH * KW * Co,
                 [(t[0], t[1], t[3]) for t in classes[0][4]], 0, ptr(residual), ptr(slab), 0, ptr(sums),
                 2 * Ci if fuse else 0, bnb.args() if fuse else _NOBNB, 0, 0,

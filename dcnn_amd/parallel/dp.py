@@ -55,7 +55,7 @@ def init_distributed(backend: Optional[str] = None) -> Tuple[int, int, int]:
 
 class DataParallel:
     def __init__(self, model: Sequential, process_group=None, bucket_mb: float = 4.0, broadcast: bool = True,
-                 grad_dtype: str = "fp32"):
+                 grad_dtype: str = "fp32", comm_backend: Optional[str] = None):
         if not model.initialized:
             model.initialize()
         self.model = model
@@ -66,6 +66,17 @@ class DataParallel:
         # exercises the RCCL + segmented-graph path on a single GPU); plain single-process
         # training has no group and skips it
         self.active = dist.is_initialized()
+        # gradient data plane: "torch" = torch.distributed (ProcessGroupNCCL = RCCL on ROCm, gloo on
+        # CPU), "rccl" = the framework's own RCCL communicator (parallel/rccl.py), bootstrapped over
+        # the native TCP control plane, collectives on the compute stream (captured in the graph)
+        import os
+        self.comm_backend = comm_backend or os.environ.get("DCNN_DP_BACKEND", "torch")
+        self.rccl = None
+        if self.comm_backend == "rccl" and self.active and model.arena.grad.is_cuda:
+            from .rccl import RcclCommunicator
+            self.rccl = RcclCommunicator(self.rank, self.world, model.arena.grad.device)
+        elif self.comm_backend not in ("torch", "rccl"):
+            raise ValueError("comm_backend must be 'torch' or 'rccl'")
         self.bucket_bytes = int(bucket_mb * 2**20)
         if grad_dtype not in ("fp32", "bf16"):
             raise ValueError("grad_dtype must be 'fp32' or 'bf16'")
@@ -130,6 +141,13 @@ class DataParallel:
         self.buckets = sorted(self.fire.values())
 
     def broadcast_parameters(self):
+        if self.rccl is not None:
+            self.rccl.broadcast(self.model.arena.data, 0)
+            for l in self.model.layers:
+                for t in _bn_buffers(l):
+                    self.rccl.broadcast(t, 0)
+            self.model.arena.sync_shadow(force=True)
+            return
         dist.broadcast(self.model.arena.data, 0, group=self.pg)
         for l in self.model.layers:
             for t in _bn_buffers(l):
@@ -174,6 +192,12 @@ class DataParallel:
         if self.world == 1 and not self.force_collectives:
             return
         flat = self.model.arena.grad
+        if self.rccl is not None:
+            if self.grad_dtype == "fp32" or self.world == 1:
+                self.rccl.all_reduce(flat[lo:hi])  # stream-ordered: no Work object to wait on
+                return
+            self._reduce_bf16_gpu(lo, hi)
+            return
         if self.grad_dtype == "fp32" or self.world == 1:
             self._works.append(dist.all_reduce(flat[lo:hi], op=dist.ReduceOp.SUM, group=self.pg, async_op=True))
             return
@@ -206,9 +230,19 @@ class DataParallel:
         with torch.cuda.stream(cs):
             st = stream_ptr(flat.device)
             K.grad_pack_bf16(flat[lo:hi].data_ptr(), packed.data_ptr(), n, 1.0, st)
-            dist.all_to_all_single(recv, packed, group=self.pg, async_op=True).wait()
+            if self.rccl is not None:  # all_to_all as grouped send/recv pairs on this stream
+                K.rccl.group_start()
+                for r in range(self.world):
+                    self.rccl.send(packed[r * shard:(r + 1) * shard], r)
+                    self.rccl.recv(recv[r * shard:(r + 1) * shard], r)
+                K.rccl.group_end()
+            else:
+                dist.all_to_all_single(recv, packed, group=self.pg, async_op=True).wait()
             K.grad_sum_chunks_bf16(recv.data_ptr(), self.world, shard, shard, red.data_ptr(), st)
-            dist.all_gather_into_tensor(gathered, red, group=self.pg, async_op=True).wait()
+            if self.rccl is not None:
+                self.rccl.all_gather(gathered, red)
+            else:
+                dist.all_gather_into_tensor(gathered, red, group=self.pg, async_op=True).wait()
             K.grad_unpack_bf16(gathered.data_ptr(), flat[lo:hi].data_ptr(), n, st)
         self._pending_unpack.append(cs)
 
@@ -248,7 +282,10 @@ class DataParallel:
             return
         for l in self.model.layers:
             for t in _bn_buffers(l):
-                dist.all_reduce(t, group=self.pg)
+                if self.rccl is not None:
+                    self.rccl.all_reduce(t)
+                else:
+                    dist.all_reduce(t, group=self.pg)
                 t.div_(self.world)
 
 

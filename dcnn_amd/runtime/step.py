@@ -43,11 +43,23 @@ class TrainStep:
         self.last_correct = None
         self._static_x = self._static_y = None
 
+    def _loss_grad(self, out, y):
+        """Loss, gradient already carrying the data-parallel 1 / world factor, correct count. A
+        user loss without ``grad_scale`` support gets the factor applied to its gradient instead."""
+        sc = self.dp.grad_scale
+        if sc == 1.0:
+            return self.loss_fn.loss_and_grad(out, y)
+        try:
+            return self.loss_fn.loss_and_grad(out, y, grad_scale=sc)
+        except TypeError:
+            loss, grad, correct = self.loss_fn.loss_and_grad(out, y)
+            return loss, grad * sc, correct
+
     # ------------------------------------------------------------------ eager
     def eager(self, x, y):
         self.opt.clear_gradients()
         out = self.dp.forward(x)
-        loss, grad, correct = self.loss_fn.loss_and_grad(out, y, grad_scale=self.dp.grad_scale)
+        loss, grad, correct = self._loss_grad(out, y)
         self.dp.backward(grad, prescaled=True)
         self.opt.update()
         self.last_loss, self.last_correct = loss, correct
@@ -123,7 +135,8 @@ class TrainStep:
         fused_opt = hasattr(self.opt, "fused") and self.opt.fused()
         if not fused_opt:
             raise RuntimeError("graph capture needs the fused flat-buffer optimizer on the GPU")
-        if self.dp.active and self.capture_collectives and dist.get_backend(self.dp.pg) == "nccl":
+        if self.dp.active and self.capture_collectives and (self.dp.rccl is not None
+                                                            or dist.get_backend(self.dp.pg) == "nccl"):
             # (gloo moves CUDA tensors through the host: not capturable, keeps the segments)
             t0 = getattr(self.opt, "t", None)
             err = None
@@ -165,8 +178,7 @@ class TrainStep:
                 if k == 0:
                     self.opt.clear_gradients()
                     out = self.dp.forward(self._static_x)
-                    loss, cur, correct = self.loss_fn.loss_and_grad(out, self._static_y,
-                                                                    grad_scale=self.dp.grad_scale)
+                    loss, cur, correct = self._loss_grad(out, self._static_y)
                     self._g_loss, self._g_correct = loss, correct
                     self.model.prepare_backward()
                 else:
@@ -201,7 +213,7 @@ class TrainStep:
             with capture_guard(), torch.cuda.graph(g, stream=self._capture_stream(), capture_error_mode="thread_local"):
                 self.opt.clear_gradients()
                 out = self.dp.forward(self._static_x)
-                loss, grad, correct = self.loss_fn.loss_and_grad(out, self._static_y, grad_scale=self.dp.grad_scale)
+                loss, grad, correct = self._loss_grad(out, self._static_y)
                 self._g_loss, self._g_correct = loss, correct
                 self.dp.backward(grad, sync=True, prescaled=True)
                 self.opt.launch_step()
