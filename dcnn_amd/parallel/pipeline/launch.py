@@ -101,6 +101,11 @@ def run(argv=None) -> dict:
         worker.comm.close()
     else:
         worker.run()
+    # receive buffers ever allocated by this rank's P2P data plane (persistent per-(peer, command,
+    # micro-batch) slots: a fixed number however many steps ran)
+    allocs = sum(getattr(getattr(o, "transport", None), "slot_allocs", 0)
+                 for o in ([coord] if rank == 0 else []) + [getattr(worker, "stage", None)])
+    print(json.dumps({"rank": rank, "slot_allocs": allocs, "steps": a.warmup + a.steps}), flush=True)
     dist.barrier()
     dist.destroy_process_group()
     return result

@@ -134,15 +134,24 @@ class LocalTransport(Transport):
 
 
 class P2PTransport(Transport):
-    """torch.distributed point-to-point data plane (RCCL on GPU, gloo on CPU)."""
+    """Point-to-point data plane between ranks: torch.distributed isend/irecv (RCCL on GPU, gloo
+    on CPU), or the framework's own RCCL communicator (``rccl=``, parallel/rccl.py: ncclSend /
+    ncclRecv enqueued on the current stream, no side stream, no Work objects).
 
-    def __init__(self, my_id: str, ranks: Dict[str, int], groups: Dict[str, object], resolve=None):
+    Receive buffers are persistent slots keyed by (peer, command, micro-batch, shape, dtype): a
+    steady-state step allocates nothing (the previous step's tensor in that slot is dead by then —
+    a stage consumes a micro-batch's activation / gradient within the step)."""
+
+    def __init__(self, my_id: str, ranks: Dict[str, int], groups: Dict[str, object], resolve=None, rccl=None):
         self.my_id = my_id
         self.ranks = dict(ranks)          # logical name / comm id -> rank
         self.groups = groups              # {"fwd", "bwd", "cfwd", "cbwd"}
-        self.rank = dist.get_rank()
+        self.rank = dist.get_rank() if rccl is None else rccl.rank
         self.local = LocalTransport(my_id, resolve)
+        self.rccl = rccl
         self._pending = deque()
+        self._slots: Dict = {}
+        self.slot_allocs = 0              # receive buffers ever allocated (tests: flat after step 1)
 
     def _group(self, command, peer_name):
         coord = "coordinator" in (peer_name, self.my_id)
@@ -163,10 +172,23 @@ class P2PTransport(Transport):
             phys, _ = M._physical(t.detach())
             if not phys.is_contiguous():
                 phys = phys.contiguous()
-            w = dist.isend(phys, dst, group=self._group(command, recipient))
-            self._pending.append((w, phys))
-            self._prune()
+            if self.rccl is not None:
+                self.rccl.send(phys, dst)  # stream-ordered; the caching allocator keeps phys alive
+                if phys.is_cuda:
+                    phys.record_stream(torch.cuda.current_stream(phys.device))
+            else:
+                w = dist.isend(phys, dst, group=self._group(command, recipient))
+                self._pending.append((w, phys))
+                self._prune()
         comm.send(M.meta_message(recipient, command, mb_id, t))
+
+    def _slot(self, msg, src, dev):
+        key = (src, int(msg.command), int(msg.mb_id), tuple(msg.shape), int(msg.dtype), str(dev))
+        buf = self._slots.get(key)
+        if buf is None:
+            buf = self._slots[key] = M.alloc_for(msg, dev)
+            self.slot_allocs += 1
+        return buf
 
     def recv(self, msg, device):
         if not M.has_tensor(msg):
@@ -176,8 +198,11 @@ class P2PTransport(Transport):
         if src is None or src == self.rank:
             return self.local.recv(msg, device)
         dev = torch.device(device) if device is not None else torch.device("cpu")
-        phys, logical = M.alloc_for(msg, dev)
-        dist.irecv(phys, src, group=self._group(msg.command, src_name)).wait()
+        phys, logical = self._slot(msg, src, dev)
+        if self.rccl is not None:
+            self.rccl.recv(phys, src)
+        else:
+            dist.irecv(phys, src, group=self._group(msg.command, src_name)).wait()
         return logical
 
     def flush(self):

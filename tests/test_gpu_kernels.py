@@ -965,3 +965,29 @@ def test_bn_apply_vectorised_matches_generic(hip, shape):
     for (dxa, dga, dba), (dxb, dgb, dbb) in zip(ares, bres):
         assert torch.equal(dga, dgb) and torch.equal(dba, dbb)
         assert (dxa.float() - dxb.float()).abs().max().item() <= 2e-2 * dxb.float().abs().max().item()
+
+
+@pytest.mark.parametrize("geom", [(3, 3, 2, 2, 1, 1), (2, 2, 2, 2, 0, 0), (3, 3, 1, 1, 1, 1)])
+def test_maxpool_vectorised_vs_torch(hip, geom):
+    """bf16 max-pool forward / backward on the 8-channel vector kernels (overlapping windows: the
+    ResNet-50 stem 3x3 / s2 / p1) against torch.nn.functional.max_pool2d. Inputs are distinct bf16
+    values, so the argmax is unique: pooled values match exactly, gradients to bf16 rounding."""
+    ph, pw, sh, sw, pad_h, pad_w = geom
+    N, C, H, W = 1, 64, 18, 18
+    torch.manual_seed(21)
+    n = N * C * H * W
+    # n distinct finite bf16 values (consecutive positive bit patterns), shuffled, random signs
+    bits = (torch.arange(n, dtype=torch.int32) + 0x0800)[torch.randperm(n)]
+    vals = bits.to(torch.int16).view(torch.bfloat16).float()
+    vals = torch.where(torch.rand(n) < 0.5, -vals, vals)
+    x = vals.view(N, C, H, W)
+    xr = x.clone().requires_grad_(True)
+    yr = F.max_pool2d(xr, (ph, pw), (sh, sw), (pad_h, pad_w))
+    dy = torch.randn_like(yr).bfloat16().float()
+    yr.backward(dy)
+    xg = x.cuda().bfloat16().contiguous(memory_format=CL)
+    y, idx = hip.maxpool_fwd(xg, ph, pw, sh, sw, pad_h, pad_w)
+    assert torch.equal(y.float().cpu(), yr.detach().bfloat16().float())
+    dx = hip.maxpool_bwd(dy.cuda().bfloat16().contiguous(memory_format=CL), idx, (N, C, H, W), ph, pw, sh, sw, pad_h,
+                         pad_w)
+    assert rel_err(dx, xr.grad) < 1e-2  # bf16 rounding of summed window gradients only

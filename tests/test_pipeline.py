@@ -168,6 +168,12 @@ def test_multiprocess_pipeline_gloo(transport, schedule):
     line = [l for l in r.stdout.splitlines() if l.startswith("{") and "pipeline" in l][-1]
     d = json.loads(line)
     assert d["stages"] == 3 and d["value"] > 0 and d["loss"] == d["loss"]
+    # persistent receive slots: every rank allocates at most one buffer per (peer, command,
+    # micro-batch) — 4 micro-batches x (activation in, gradient in) — over all 3 steps
+    allocs = [json.loads(l) for l in r.stdout.splitlines() if l.startswith("{") and "slot_allocs" in l]
+    assert len(allocs) == 3
+    for a in allocs:
+        assert a["steps"] == 3 and a["slot_allocs"] <= (8 if transport == "p2p" else 0), allocs
 
 
 def _run_schedule(schedule, steps=2, stages=3, mbs=6):
