@@ -251,46 +251,67 @@ __global__ void __launch_bounds__(256, 2) gemm_g2_kernel(G2Args p) {
     if (tid < BN) piv_col = (float)*reinterpret_cast<const bf16*>(smem + tid * 2);
   }
   const int ghw = p.GH * p.GW;
-  for (int row = r0; row < BM; row += RSTEP) {
-    const int m = m0 + row;
-    if (m >= p.M || !col_ok) continue;
-    const int ml = m - mcls;
+  auto orow_of = [&](int row) {
+    const int ml = m0 + row - mcls;
     const int img = ml / ghw, rem = ml - img * ghw;
     const int gy = rem / p.GW, gx = rem - gy * p.GW;
-    const long orow = ((long)img * p.OH + gy * p.OSY + ory) * p.OW + gx * p.OSX + orx;
-    float f[8];
-    unpack8(*reinterpret_cast<const uint4*>(smem + row * T::EPI_PITCH + cg * 16), f);
-    if (p.residual) {
-      float rr[8];
-      unpack8(*reinterpret_cast<const uint4*>(p.residual + orow * p.ldc + ncol), rr);
+    return ((long)img * p.OH + gy * p.OSY + ory) * p.OW + gx * p.OSX + orx;
+  };
+  // the operands of row + RSTEP are loaded before row's store: a load's wait also waits for every
+  // older store, so loading after the previous row's store would serialise each row on a store
+  const bool has_res = p.residual != nullptr, has_y = bnb && p.bnb.y != nullptr, has_x = bnb && p.stats;
+  uint4 c_res{}, c_y{}, c_x{};
+  auto fetch = [&](int row, uint4& r_, uint4& y_, uint4& x_) {
+    if (row >= BM || m0 + row >= p.M || !col_ok) return;
+    const long o = orow_of(row) * p.ldc + ncol;
+    if (has_res) r_ = *reinterpret_cast<const uint4*>(p.residual + o);
+    if (has_y) y_ = *reinterpret_cast<const uint4*>(p.bnb.y + o);
+    if (has_x) x_ = *reinterpret_cast<const uint4*>(p.bnb.x + o);
+  };
+  fetch(r0, c_res, c_y, c_x);
+  for (int row = r0; row < BM; row += RSTEP) {
+    uint4 n_res{}, n_y{}, n_x{};
+    fetch(row + RSTEP, n_res, n_y, n_x);
+    const int m = m0 + row;
+    if (m < p.M && col_ok) {
+      const long orow = orow_of(row);
+      float f[8];
+      unpack8(*reinterpret_cast<const uint4*>(smem + row * T::EPI_PITCH + cg * 16), f);
+      if (has_res) {
+        float rr[8];
+        unpack8(c_res, rr);
 #pragma unroll
-      for (int v = 0; v < 8; ++v) f[v] += rr[v];
-    }
-    if (p.relu) {
+        for (int v = 0; v < 8; ++v) f[v] += rr[v];
+      }
+      if (p.relu) {
 #pragma unroll
-      for (int v = 0; v < 8; ++v) f[v] = fmaxf(f[v], 0.f);
-    }
-    if (bnb && p.bnb.y) {
-      float yo[8];
-      unpack8(*reinterpret_cast<const uint4*>(p.bnb.y + orow * p.ldc + ncol), yo);
+        for (int v = 0; v < 8; ++v) f[v] = fmaxf(f[v], 0.f);
+      }
+      if (has_y) {
+        float yo[8];
+        unpack8(c_y, yo);
 #pragma unroll
-      for (int v = 0; v < 8; ++v) f[v] = yo[v] > 0.f ? f[v] : 0.f;
-    }
-    const uint4 o = pack8(f);
-    *reinterpret_cast<uint4*>(reinterpret_cast<bf16*>(p.C) + orow * p.ldc + ncol) = o;
-    if (p.stats) {
-      float g[8];
-      unpack8(o, g);
-      if (bnb) {
-        float xv[8];
-        unpack8(*reinterpret_cast<const uint4*>(p.bnb.x + orow * p.ldc + ncol), xv);
+        for (int v = 0; v < 8; ++v) f[v] = yo[v] > 0.f ? f[v] : 0.f;
+      }
+      const uint4 o = pack8(f);
+      *reinterpret_cast<uint4*>(reinterpret_cast<bf16*>(p.C) + orow * p.ldc + ncol) = o;
+      if (p.stats) {
+        float g[8];
+        unpack8(o, g);
+        if (bnb) {
+          float xv[8];
+          unpack8(c_x, xv);
 #pragma unroll
-        for (int v = 0; v < 8; ++v) { s[v] += g[v]; q[v] += g[v] * (xv[v] - mu[v]) * is[v]; }
-      } else {
+          for (int v = 0; v < 8; ++v) { s[v] += g[v]; q[v] += g[v] * (xv[v] - mu[v]) * is[v]; }
+        } else {
 #pragma unroll
-        for (int v = 0; v < 8; ++v) { const float d = g[v] - pv[v]; s[v] += d; q[v] += d * d; }
+          for (int v = 0; v < 8; ++v) { const float d = g[v] - pv[v]; s[v] += d; q[v] += d * d; }
+        }
       }
     }
+    c_res = n_res;
+    c_y = n_y;
+    c_x = n_x;
   }
   if (p.stats) {
     __syncthreads();

@@ -667,7 +667,7 @@ int hconv_tiles(int NB, int H, int W, int Cs, int N, int ntaps) {
 
 int hconv_tile_elems(int NB, int H, int W, int Cs, int N, int ntaps) {
   H3Plan pl;
-  if (hconv3_plan(NB, H, W, Cs, N, ntaps, &pl)) return 32768;  // 8 waves x 64 x 64
+  if (hconv3_plan(NB, H, W, Cs, N, ntaps, &pl)) return 16384;  // 4 waves x 64 x 64
   HConvArgs a{};
   a.NB = NB; a.H = H; a.W = W; a.N = N;
   int bm, bn;

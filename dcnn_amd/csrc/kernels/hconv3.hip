@@ -96,6 +96,15 @@ __device__ __forceinline__ void glds16_at(i32x4 rsrc, unsigned base, unsigned vo
                : "memory", "m0");
 }
 
+// value of lane 0 of this lane's 16-lane DPP row (row_bcast-free: readlane of the 4 row heads)
+__device__ __forceinline__ float h3_row_first(float v) {
+  const int x = __float_as_int(v);
+  const int r0 = __builtin_amdgcn_readlane(x, 0), r1 = __builtin_amdgcn_readlane(x, 16);
+  const int r2 = __builtin_amdgcn_readlane(x, 32), r3 = __builtin_amdgcn_readlane(x, 48);
+  const int row = (threadIdx.x & 63) >> 4;
+  return __int_as_float(row == 0 ? r0 : row == 1 ? r1 : row == 2 ? r2 : r3);
+}
+
 __device__ __forceinline__ bf16x8 lds_b128(const char* smem, int off) {
   return *reinterpret_cast<const bf16x8*>(smem + off);
 }
@@ -111,27 +120,30 @@ struct H3Geo {
   unsigned long long* stamps;  // diagnostic: per-wave s_memtime at 8 points (hconv3_set_stamps), or null
 };
 
-template <int WC, int TWC, int HN, int NWI, int PITCH>
-struct H3 {
-  static constexpr int BN = 64 * WC, WP = 8 / WC, BM = 64 * WP;
-  static constexpr int HALO = 8 * HN * 1024;   // one halo buffer
-  static constexpr int WST = 8 * NWI * 1024;   // one weight stage (3 taps x BN rows x 64 B, padded)
-  static constexpr int RED = 2 * HALO + 3 * WST;          // epilogue scratch: [WP][BN][3] floats + flag
-  static constexpr int RED_BYTES = WP * BN * 3 * 4 + 16;
-  static constexpr int LDS = RED + RED_BYTES;
-  static_assert(3 * BN * 64 <= WST, "weight stage");
-  static_assert(LDS <= 163840, "LDS budget");
-};
-
+// NW waves per workgroup (8: one workgroup per CU; 4: two per CU, whose prologue / epilogue
+// memory phases overlap each other's MFMA phases), WC of them along the output channels (64
+// each), NW / WC along the pixels (64 each). NWS weight stages (3: two steps in flight; 2: one).
 // PITCH > 0: compile-time halo row pitch, a multiple of 8 pixels, so a kernel-row (dy) shift keeps
 // the bit-2 chunk swizzle and becomes an immediate ds_read offset: 12 halo fragment addresses per
-// lane (4 pixel subtiles x 3 dx) instead of 36. PITCH == 0: runtime pitch (4-wide tiles), 36.
-template <int WC, int TWC, int HN, int NWI, int PITCH>
-__global__ void __launch_bounds__(512, 1) hconv3_kernel(HConvArgs p, H3Geo g) {
-  using T = H3<WC, TWC, HN, NWI, PITCH>;
+// lane (4 pixel subtiles x 3 dx) instead of 36. PITCH == 0: runtime pitch, 36 addresses.
+template <int NW, int WC, int TWC, int HN, int NWI, int NWS, int PITCH>
+struct H3 {
+  static constexpr int BN = 64 * WC, WP = NW / WC, BM = 64 * WP;
+  static constexpr int HALO = NW * HN * 1024;   // one halo buffer
+  static constexpr int WST = NW * NWI * 1024;   // one weight stage (3 taps x BN rows x 64 B, padded)
+  static constexpr int LDS = 2 * HALO + NWS * WST;
+  static_assert(3 * BN * 64 <= WST, "weight stage");
+  static_assert(WP * BN * 3 * 4 + 16 <= HALO, "epilogue scratch lives in halo buffer 0");
+  static_assert(LDS <= 163840, "LDS budget");
+  static_assert(NWS == 2 || NWS == 3, "weight stages");
+};
+
+template <int NW, int WC, int TWC, int HN, int NWI, int NWS, int PITCH>
+__global__ void __launch_bounds__(NW * 64, 8 / NW) hconv3_kernel(HConvArgs p, H3Geo g) {
+  using T = H3<NW, WC, TWC, HN, NWI, NWS, PITCH>;
   constexpr int BN = T::BN, WP = T::WP;
+  constexpr int NT = NW * 64;
   extern __shared__ __attribute__((aligned(16))) char smem[];
-  float* red = reinterpret_cast<float*>(smem + T::RED);  // epilogue scratch (never a DMA target)
   using I0 = std::integral_constant<int, 0>;
   using I1 = std::integral_constant<int, 1>;
   using I2 = std::integral_constant<int, 2>;
@@ -139,67 +151,46 @@ __global__ void __launch_bounds__(512, 1) hconv3_kernel(HConvArgs p, H3Geo g) {
   const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int wc = wid % WC, wp = wid / WC;
   const int lr = lane & 15, lh = lane >> 4;
-  bool first_unit = true;
-  // diagnostic timeline of the first unit (off unless hconv3_set_stamps): lane 0 of every wave
+  // diagnostic timeline (off unless hconv3_set_stamps): lane 0 of every wave
   auto stamp = [&](int k) {
-    if (g.stamps && first_unit && lane == 0)
-      g.stamps[((size_t)blockIdx.x * 8 + wid) * 8 + k] = __builtin_amdgcn_s_memtime();
+    if (g.stamps && lane == 0) g.stamps[((size_t)blockIdx.x * 8 + wid) * 8 + k] = __builtin_amdgcn_s_memtime();
   };
   stamp(0);
   const int SPL = p.splits;
-  const int nunits = g.tiles_m * g.tiles_n * SPL;
-  const int G = gridDim.x;
+  const int u0 = xcd_remap3(blockIdx.x, gridDim.x);
+  const int zs = u0 % SPL, lt = u0 / SPL;
+  const int tm = lt / g.tiles_n, tn = lt % g.tiles_n;
+  const int n0 = tn * BN;
+  const int tx_tiles = p.W / g.TW, tpi = tx_tiles * (p.H / g.TH);
+  const int ig = tm / tpi, trem = tm - ig * tpi;
+  const int y0 = (trem / tx_tiles) * g.TH, x0 = (trem % tx_tiles) * g.TW, img0 = ig * g.IMG;
   const int HW2 = g.TW + 2, HH2 = g.TH + 2, pitch = PITCH > 0 ? PITCH : g.pitch;
   const int HPI = HH2 * pitch;  // halo pixels per image (pitch-padded)
   const int HPX = g.IMG * HPI;  // halo pixels per tile
-  const int tx_tiles = p.W / g.TW, tpi = tx_tiles * (p.H / g.TH);
   if (p.zero_ptr && blockIdx.x == 0)
-    for (int i = tid; i < p.zero_n; i += 512) p.zero_ptr[i] = 0.f;
+    for (int i = tid; i < p.zero_n; i += NT) p.zero_ptr[i] = 0.f;
   const i32x4 rsA = raw_rsrc(p.A, p.a_bytes);
   const i32x4 rsB = raw_rsrc(p.B, p.b_bytes);
+  const int cbase = zs * g.nchunk * 32;  // first input channel of this split
 
-  // ---- work units: (output tile, split) pairs; this workgroup takes u0, u0 + G, ...
-  struct Unit { int zs, lt, tm, n0, img0, y0, x0; };
-  auto unit_of = [&](int u) {
-    Unit U;
-    U.zs = u % SPL;
-    U.lt = u / SPL;
-    U.tm = U.lt / g.tiles_n;
-    U.n0 = (U.lt - U.tm * g.tiles_n) * BN;
-    const int ig = U.tm / tpi, trem = U.tm - ig * tpi;
-    U.y0 = (trem / tx_tiles) * g.TH;
-    U.x0 = (trem - (trem / tx_tiles) * tx_tiles) * g.TW;
-    U.img0 = ig * g.IMG;
-    return U;
-  };
-
-  // ---- halo loader. Instruction k of this wave fills tile halo pixels [16(wid*HN + k), +16): the
-  // tile-local coordinates are unit independent, the source address is re-based per unit.
-  // packed per instruction: [0:8) x + 1, [8:16) y + 1, [16:22) swizzled chunk * 16 / 16, [22:32) image
-  // (1023: no pixel — beyond the tile's halo or in the pitch padding)
-  int hpk[HN];
+  // ---- halo loader: instruction k of this wave fills halo pixels [16(wid*HN + k), +16)
+  unsigned hsrc[HN];
 #pragma unroll
   for (int k = 0; k < HN; ++k) {
     const int P = (wid * HN + k) * 16 + (lane >> 2);
-    const int im = P / HPI, r = P - im * HPI;
-    const int hy = r / pitch, hx = r - hy * pitch;
-    const int imv = (P < HPX && hx < HW2) ? im : 1023;
-    hpk[k] = hx | (hy << 8) | (((lane & 3) ^ h3_swz<TWC>(P)) << 16) | (imv << 22);
-  }
-  unsigned hsrc[HN];  // source byte offsets (channel 0 of the unit's split) of the unit being loaded
-  auto set_halo_src = [&](const Unit& U) {
-    const int cb = U.zs * g.nchunk * 32;
-#pragma unroll
-    for (int k = 0; k < HN; ++k) {
-      const int im = (unsigned)hpk[k] >> 22, sw = (hpk[k] >> 16) & 63;
-      const int sy = U.y0 + ((hpk[k] >> 8) & 255) - 1, sx = U.x0 + (hpk[k] & 255) - 1, n = U.img0 + im;
-      hsrc[k] = (im != 1023 && sy >= 0 && sy < p.H && sx >= 0 && sx < p.W && n < p.NB)
-                    ? (unsigned)((((long)n * p.H + sy) * p.W + sx) * p.Cs * 2) + (unsigned)((cb + sw * 8) * 2)
-                    : kOOB3;
+    unsigned v = kOOB3;
+    if (P < HPX) {
+      const int im = P / HPI, r = P - im * HPI;
+      const int hy = r / pitch, hx = r - hy * pitch;
+      const int sy = y0 + hy - 1, sx = x0 + hx - 1, n = img0 + im;
+      if (hx < HW2 && sy >= 0 && sy < p.H && sx >= 0 && sx < p.W && n < p.NB)
+        v = (unsigned)((((long)n * p.H + sy) * p.W + sx) * p.Cs * 2) +
+            (unsigned)((cbase + ((lane & 3) ^ h3_swz<TWC>(P)) * 8) * 2);
     }
-  };
+    hsrc[k] = v;
+  }
   // ---- weight loader: stage row R = dx * BN + n (3 taps x BN output channels), 64 B each
-  unsigned wfix[NWI];
+  unsigned wsrc[NWI];
   int wtb[NWI][3];  // byte offset of the instruction's tap column for kernel rows dy = 0..2 (SGPRs)
 #pragma unroll
   for (int k = 0; k < NWI; ++k) {
@@ -208,11 +199,10 @@ __global__ void __launch_bounds__(512, 1) hconv3_kernel(HConvArgs p, H3Geo g) {
     const int dx = R0 / BN, n = R - dx * BN;
 #pragma unroll
     for (int dy = 0; dy < 3; ++dy) wtb[k][dy] = __builtin_amdgcn_readfirstlane(dx < 3 ? g.tb[dy * 3 + dx] * 2 : 0);
-    wfix[k] = dx < 3 ? (unsigned)(((long)n * p.ldb + ((lane & 3) ^ h3_wswz(n)) * 8) * 2) : kOOB3;
+    wsrc[k] = (dx < 3 && n0 + n < p.N)
+                  ? (unsigned)(((long)(n0 + n) * p.ldb + cbase + ((lane & 3) ^ h3_wswz(n)) * 8) * 2)
+                  : kOOB3;
   }
-  auto w_base = [&](const Unit& U) {  // scalar: the unit's first output channel and first input channel
-    return (unsigned)(((long)U.n0 * p.ldb + U.zs * g.nchunk * 32) * 2);
-  };
   // LDS byte address of this wave's first halo / weight DMA slot (wave-uniform SGPRs)
   const unsigned lds0 = __builtin_amdgcn_readfirstlane(
       (unsigned)(uintptr_t)((const __attribute__((address_space(3))) char*)smem));
@@ -225,40 +215,33 @@ __global__ void __launch_bounds__(512, 1) hconv3_kernel(HConvArgs p, H3Geo g) {
       glds16_at<BUF * T::HALO + K * 1024>(rsA, hbase, hsrc[K] + co);
     });
   };
-  auto load_w = [&](auto stage_c, unsigned wb, int c, int dy) {
+  auto load_w = [&](auto stage_c, int c, int dy) {
     constexpr int ST = decltype(stage_c)::value;
     h3_static_for<0, NWI>([&](auto kc) {
       constexpr int K = decltype(kc)::value;
-      glds16_at<ST * T::WST + K * 1024>(rsB, wbase_lds,
-                                        wfix[K] == kOOB3 ? kOOB3 : wfix[K] + wb + (unsigned)(wtb[K][dy] + c * 64));
+      glds16_at<ST * T::WST + K * 1024>(rsB, wbase_lds, wsrc[K] + (unsigned)(wtb[K][dy] + c * 64));
     });
   };
 
-  // ---- fragment addresses (unit independent; recomputed per unit from a laundered lane id so
-  // that they are dead — not spilled — across the epilogue)
+  // ---- fragment addresses
   // A (weights): row n = wc*64 + i*16 + lr of stage tap dx: stage + dx*BN*64 + (wc*64 + i*16)*64 + abase
-  // B (halo): pixel subtile j of this wave, tap (dy, dx): 36 per-lane byte offsets
-  constexpr int NBA = PITCH > 0 ? 3 : 9;  // halo fragment addresses per pixel subtile
-  int abase, baddr[4][NBA];
-  auto set_frag_addr = [&]() {
-    int l = lane;
-    asm volatile("" : "+v"(l));
-    const int r16 = l & 15, h4 = l >> 4;
-    abase = 2 * T::HALO + (wc * 64 + r16) * 64 + ((h4 ^ h3_wswz(r16)) << 4);
-#pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      const int q = wp * 64 + j * 16 + h3_perm<TWC>(r16);  // tile-local output pixel
-      const int tpx = g.TH * g.TW;
-      const int im = q / tpx, r = q - im * tpx;
-      const int P0 = im * HPI + (r / g.TW) * pitch + (r % g.TW);  // halo pixel of tap (-1, -1)
-#pragma unroll
-      for (int t = 0; t < NBA; ++t) {
-        const int P = P0 + (NBA == 3 ? t : (t / 3) * pitch + (t % 3));
-        baddr[j][t] = P * 64 + ((h4 ^ h3_swz<TWC>(P)) << 4);
-      }
-    }
-  };
+  const int abase = 2 * T::HALO + (wc * 64 + lr) * 64 + ((lh ^ h3_wswz(lr)) << 4);
+  // B (halo): pixel subtile j of this wave, tap (dy, dx)
+  constexpr int NBA = PITCH > 0 ? 3 : 9;
   static_assert(PITCH == 0 || (PITCH % 8 == 0 && TWC != 4), "dy-invariant swizzle needs pitch % 8 == 0");
+  int baddr[4][NBA];
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const int q = wp * 64 + j * 16 + h3_perm<TWC>(lr);  // tile-local output pixel
+    const int tpx = g.TH * g.TW;
+    const int im = q / tpx, r = q - im * tpx;
+    const int P0 = im * HPI + (r / g.TW) * pitch + (r % g.TW);  // halo pixel of tap (-1, -1)
+#pragma unroll
+    for (int t = 0; t < NBA; ++t) {
+      const int P = P0 + (NBA == 3 ? t : (t / 3) * pitch + (t % 3));
+      baddr[j][t] = P * 64 + ((lh ^ h3_swz<TWC>(P)) << 4);
+    }
+  }
   auto baddr_of = [&](int j, int dy, int dx) {
     if constexpr (PITCH > 0) return baddr[j][dx] + dy * PITCH * 64;
     else return baddr[j][dy * 3 + dx];
@@ -270,18 +253,18 @@ __global__ void __launch_bounds__(512, 1) hconv3_kernel(HConvArgs p, H3Geo g) {
 #pragma unroll
     for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
-  // one K step: chunk c (halo buffer HB), kernel row DY (weight stage DY). The fragments of tap
+  // one K step: chunk c (halo buffer HB), kernel row DY, weight stage ST. The fragments of tap
   // dx + 1 are read while tap dx's 16 MFMAs run (two register sets in flight), so the LDS latency
   // after the barrier is paid once per step, not once per tap. The step's direct-to-LDS loads
-  // (`issue`: next weight stages / next halo, into buffers no wave reads this step) go out after
+  // (`issue`: next weight stage / next halo, into buffers no wave reads this step) go out after
   // the first MFMAs: an LDS-DMA issue among queued MFMAs costs the wave ~60 cycles instead of
   // delaying the step's first MFMA by its full issue cost (MI355X_MICROARCH cycle constants).
-  auto step = [&](auto hb_c, auto dy_c, auto issue) {
-    constexpr int HB = decltype(hb_c)::value, DY = decltype(dy_c)::value;
+  auto step = [&](auto hb_c, auto dy_c, auto st_c, auto issue) {
+    constexpr int HB = decltype(hb_c)::value, DY = decltype(dy_c)::value, ST = decltype(st_c)::value;
     bf16x8 a[3][4], b[3][4];
     auto rd = [&](int dx) {
 #pragma unroll
-      for (int i = 0; i < 4; ++i) a[dx][i] = lds_b128(smem, abase + DY * T::WST + dx * BN * 64 + i * 16 * 64);
+      for (int i = 0; i < 4; ++i) a[dx][i] = lds_b128(smem, abase + ST * T::WST + dx * BN * 64 + i * 16 * 64);
 #pragma unroll
       for (int j = 0; j < 4; ++j) b[dx][j] = lds_b128(smem, baddr_of(j, DY, dx) + HB * T::HALO);
     };
@@ -302,64 +285,32 @@ __global__ void __launch_bounds__(512, 1) hconv3_kernel(HConvArgs p, H3Geo g) {
     mm(1, 0, 4);
     mm(2, 0, 4);
   };
-  const int nch = g.nchunk;  // chunks per unit (even: the host guarantees it)
+  const int nch = g.nchunk;  // chunks of this split (even: the host guarantees it)
 
-  // ---- prologue: the first unit's halo(0), W(0,0), W(0,1); the wait leaves W(0,1) in flight
-  int u = xcd_remap3(blockIdx.x, G);
-  if (u >= nunits) return;
-  Unit U = unit_of(u);
-  unsigned wbU = w_base(U);
-  set_halo_src(U);
-  load_halo(I0{}, 0);
-  load_w(I0{}, wbU, 0, 0);
-  load_w(I1{}, wbU, 0, 1);
-  vmwait<NWI>();
-  h3_barrier();
-  stamp(1);
-
-  // The step stream runs across units: while unit U computes its last chunk, the next unit V's
-  // halo(0) and first two weight stages are already streaming in (its halo into buffer 0, which
-  // the even chunk count leaves free), and V's K loop starts while U's epilogue stores drain.
-  // Step (c, dy) issues the weights of the step two ahead (and, at dy = 0, the next chunk's halo);
-  // the wait after step s retires W(s + 1) and everything older. The first wait of a unit that
-  // follows an epilogue also has that epilogue's >= 16 vector stores per lane younger than W(s + 1).
-  for (;;) {
-    set_frag_addr();
-    const int v = u + G;
-    const bool hasV = v < nunits;
-    const unsigned wbV = hasV ? w_base(unit_of(v)) : 0u;
-    const bool after_epi = !first_unit;
+  if constexpr (NWS == 3) {
+    // 3-stage ring, stage = kernel row: step (c, dy) issues the weights of the step two ahead
+    // ((c,2) / (c+1,0) / (c+1,1)) and, at dy = 0, the next chunk's halo; the wait after step s
+    // retires W(s + 1) and everything older.
+    load_halo(I0{}, 0);
+    load_w(I0{}, 0, 0);
+    load_w(I1{}, 0, 1);
+    vmwait<NWI>();
+    h3_barrier();
+    stamp(1);
     auto chunk = [&](int c, auto hb_c) {
       constexpr int HB = decltype(hb_c)::value;
-      const bool more = c + 1 < nch;            // another chunk of this unit
-      const bool nxt = !more && hasV;           // ... else the next unit's first chunk
-      // (the next unit's halo sources are computed between steps, where no fragments are live)
-      if (nxt) set_halo_src(unit_of(v));
-      // ---- (c, 0)
-      step(hb_c, I0{}, [&] {
-        load_w(I2{}, wbU, c, 2);
+      const bool more = c + 1 < nch;
+      step(hb_c, I0{}, I0{}, [&] {
+        load_w(I2{}, c, 2);
         if (more) load_halo(std::integral_constant<int, HB ^ 1>{}, c + 1);
-        else if (nxt) load_halo(I0{}, 0);
       });
-      if (c == 0 && after_epi) {
-        if (more || nxt) vmwait<NWI + HN + 16>(); else vmwait<NWI + 16>();
-      } else {
-        if (more || nxt) vmwait<NWI + HN>(); else vmwait<NWI>();
-      }
+      if (more) vmwait<NWI + HN>(); else vmwait<NWI>();
       h3_barrier();
-      // ---- (c, 1)
-      step(hb_c, I1{}, [&] {
-        if (more) load_w(I0{}, wbU, c + 1, 0);
-        else if (nxt) load_w(I0{}, wbV, 0, 0);
-      });
-      if (more || nxt) vmwait<NWI>(); else vmwait<0>();
+      step(hb_c, I1{}, I1{}, [&] { if (more) load_w(I0{}, c + 1, 0); });
+      if (more) vmwait<NWI>(); else vmwait<0>();
       h3_barrier();
-      // ---- (c, 2)
-      step(hb_c, I2{}, [&] {
-        if (more) load_w(I1{}, wbU, c + 1, 1);
-        else if (nxt) load_w(I1{}, wbV, 0, 1);
-      });
-      if (more || nxt) vmwait<NWI>(); else vmwait<0>();
+      step(hb_c, I2{}, I2{}, [&] { if (more) load_w(I1{}, c + 1, 1); });
+      if (more) vmwait<NWI>(); else vmwait<0>();
       h3_barrier();
     };
     for (int c = 0; c < nch; c += 2) {
@@ -367,17 +318,77 @@ __global__ void __launch_bounds__(512, 1) hconv3_kernel(HConvArgs p, H3Geo g) {
       if (c == 0) stamp(2);
       chunk(c + 1, I1{});
     }
-    stamp(3);
+  } else {
+    // 2-stage ring: step s uses stage s & 1 = (c + dy) & 1 and issues W(s + 1) (and, at dy = 0, the
+    // next chunk's halo after it); the wait after step s retires W(s + 1) and everything older
+    load_halo(I0{}, 0);
+    load_w(I0{}, 0, 0);
+    vmwait<0>();
+    h3_barrier();
+    stamp(1);
+    auto chunk = [&](int c, auto hb_c) {
+      constexpr int HB = decltype(hb_c)::value;
+      using S0 = std::integral_constant<int, HB>;
+      using S1 = std::integral_constant<int, HB ^ 1>;
+      const bool more = c + 1 < nch;
+      step(hb_c, I0{}, S0{}, [&] {
+        load_w(S1{}, c, 1);
+        if (more) load_halo(std::integral_constant<int, HB ^ 1>{}, c + 1);
+      });
+      if (more) vmwait<HN>(); else vmwait<0>();
+      h3_barrier();
+      step(hb_c, I1{}, S1{}, [&] { load_w(S0{}, c, 2); });
+      vmwait<0>();
+      h3_barrier();
+      step(hb_c, I2{}, S0{}, [&] { if (more) load_w(S1{}, c + 1, 0); });
+      vmwait<0>();
+      h3_barrier();
+    };
+    for (int c = 0; c < nch; c += 2) {
+      chunk(c, I0{});
+      if (c == 0) stamp(2);
+      chunk(c + 1, I1{});
+    }
+  }
+  stamp(3);
 
-    U = unit_of(u);  // (recomputed: scalar math, fewer live SGPRs through the K loop)
-    // ---------------------------------------------------------------- split-K hand-off
-    bool do_epi = true;
-    if (SPL > 1) {
-      // every partial leaves with agent-scope (sc1) 8-byte stores, each wave drains them, one lane
-      // adds to the tile's ticket behind the workgroup barrier, and the workgroup whose add returns
-      // SPL - 1 reads all partials back with sc1 loads and sums them in split order
-      constexpr int E2 = 32;  // float2 pairs per lane
-      unsigned long long* part = reinterpret_cast<unsigned long long*>(p.part) + (size_t)U.lt * SPL * E2 * 512;
+  // ---------------------------------------------------------------- split-K hand-off
+  float* red = reinterpret_cast<float*>(smem);  // epilogue scratch in halo buffer 0 (K loop done)
+  if (SPL > 1) {
+    // every partial leaves with agent-scope (sc1) 8-byte stores, each wave drains them, one lane
+    // adds to the tile's ticket behind the workgroup barrier, and the workgroup whose add returns
+    // SPL - 1 reads all partials back with sc1 loads and sums them in split order
+    constexpr int E2 = 32;  // float2 pairs per lane
+    unsigned long long* part = reinterpret_cast<unsigned long long*>(p.part) + (size_t)lt * SPL * E2 * NT;
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+          const int e2 = (i * 4 + j) * 2 + h;
+          const unsigned long long bits = (unsigned long long)__float_as_uint(acc[i][j][2 * h]) |
+                                          ((unsigned long long)__float_as_uint(acc[i][j][2 * h + 1]) << 32);
+          __hip_atomic_store(part + ((size_t)zs * E2 + e2) * NT + tid, bits, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    volatile int* flag = reinterpret_cast<volatile int*>(smem + T::HALO - 16);
+    if (tid == 0) {
+      const unsigned old = __hip_atomic_fetch_add(p.tickets + lt, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      const int last = old == (unsigned)(SPL - 1);
+      if (last) __hip_atomic_store(p.tickets + lt, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      *flag = last;
+    }
+    __syncthreads();
+    const int last = *flag;
+    __syncthreads();
+    if (!last) return;
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+    for (int z = 0; z < SPL; ++z) {
 #pragma unroll
       for (int i = 0; i < 4; ++i)
 #pragma unroll
@@ -385,169 +396,137 @@ __global__ void __launch_bounds__(512, 1) hconv3_kernel(HConvArgs p, H3Geo g) {
 #pragma unroll
           for (int h = 0; h < 2; ++h) {
             const int e2 = (i * 4 + j) * 2 + h;
-            const unsigned long long bits = (unsigned long long)__float_as_uint(acc[i][j][2 * h]) |
-                                            ((unsigned long long)__float_as_uint(acc[i][j][2 * h + 1]) << 32);
-            __hip_atomic_store(part + ((size_t)U.zs * E2 + e2) * 512 + tid, bits, __ATOMIC_RELAXED,
-                               __HIP_MEMORY_SCOPE_AGENT);
+            const unsigned long long bits =
+                __hip_atomic_load(part + ((size_t)z * E2 + e2) * NT + tid, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            acc[i][j][2 * h] += __uint_as_float((unsigned)bits);
+            acc[i][j][2 * h + 1] += __uint_as_float((unsigned)(bits >> 32));
           }
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      __syncthreads();
-      volatile int* flag = reinterpret_cast<volatile int*>(smem + T::RED + T::RED_BYTES - 16);
-      if (tid == 0) {
-        const unsigned old = __hip_atomic_fetch_add(p.tickets + U.lt, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        const int last = old == (unsigned)(SPL - 1);
-        if (last) __hip_atomic_store(p.tickets + U.lt, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        *flag = last;
-      }
-      __syncthreads();
-      do_epi = *flag != 0;
-      __syncthreads();
-      if (do_epi) {
-#pragma unroll
-        for (int i = 0; i < 4; ++i)
-#pragma unroll
-          for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-        for (int z = 0; z < SPL; ++z) {
-#pragma unroll
-          for (int i = 0; i < 4; ++i)
-#pragma unroll
-            for (int j = 0; j < 4; ++j)
-#pragma unroll
-              for (int h = 0; h < 2; ++h) {
-                const int e2 = (i * 4 + j) * 2 + h;
-                const unsigned long long bits = __hip_atomic_load(part + ((size_t)z * E2 + e2) * 512 + tid,
-                                                                  __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                acc[i][j][2 * h] += __uint_as_float((unsigned)bits);
-                acc[i][j][2 * h + 1] += __uint_as_float((unsigned)(bits >> 32));
-              }
-        }
-      }
-      // (a non-last split drained every vector-memory op above: the next unit's first counted
-      // wait is trivially satisfied)
     }
+  }
 
-    // ---------------------------------------------------------------- epilogue (from registers)
-    // acc[i][j][r]: channel n0 + wc*64 + i*16 + 4*lh + r, tile pixel wp*64 + j*16 + perm(lr)
-    if (do_epi) {
-      long orow[4];
+  // ---------------------------------------------------------------- epilogue (from registers)
+  // acc[i][j][r]: channel n0 + wc*64 + i*16 + 4*lh + r, tile pixel wp*64 + j*16 + perm(lr).
+  // Every operand load (bias, BN mean / istd, residual, ReLU output, BN input) is issued before the
+  // first store: a load's wait also waits for every older store, so interleaving them would make
+  // each channel group wait for the previous group's stores to drain.
+  bf16* crow[4];                   // output row of pixel subtile j (channel 0)
+  const bf16 *rrow[4], *yrow[4], *xrow[4];
 #pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        const int q = wp * 64 + j * 16 + h3_perm<TWC>(lr);
-        const int tpx = g.TH * g.TW;
-        const int im = q / tpx, r = q - im * tpx;
-        orow[j] = ((long)(U.img0 + im) * p.H + U.y0 + r / g.TW) * p.W + U.x0 + r % g.TW;
+  for (int j = 0; j < 4; ++j) {
+    const int q = wp * 64 + j * 16 + h3_perm<TWC>(lr);
+    const int tpx = g.TH * g.TW;
+    const int im = q / tpx, r = q - im * tpx;
+    const size_t o = (((size_t)(img0 + im) * p.H + y0 + r / g.TW) * p.W + x0 + r % g.TW) * (size_t)p.N;
+    crow[j] = p.C + o;
+    rrow[j] = p.residual + o;
+    yrow[j] = p.bnb.y + o;
+    xrow[j] = p.bnb.x + o;
+  }
+  const bool bnb = p.bnb.x != nullptr;
+  const bool stats = p.stats != nullptr;
+  const bool has_res = p.residual != nullptr, has_y = bnb && p.bnb.y != nullptr, has_x = bnb && stats;
+  const int nl = n0 + wc * 64 + 4 * lh;  // this lane's first channel (+ i*16 + r)
+  float bv[4][4], mu[4][4], is[4][4];
+  uint2 rr[4][4], yy[4][4], xx[4][4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      bv[i][r] = p.bias ? p.bias[nl + i * 16 + r] : 0.f;
+      mu[i][r] = has_x ? p.bnb.mean[nl + i * 16 + r] : 0.f;
+      is[i][r] = has_x ? p.bnb.istd[nl + i * 16 + r] : 0.f;
+    }
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int c = nl + i * 16;
+      rr[i][j] = has_res ? *reinterpret_cast<const uint2*>(rrow[j] + c) : make_uint2(0u, 0u);
+      yy[i][j] = has_y ? *reinterpret_cast<const uint2*>(yrow[j] + c) : make_uint2(0u, 0u);
+      xx[i][j] = has_x ? *reinterpret_cast<const uint2*>(xrow[j] + c) : make_uint2(0u, 0u);
+    }
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int cl0 = wc * 64 + i * 16 + 4 * lh;  // tile-local first of this lane's 4 channels
+    float gv[4][4], xh[4][4];  // [j][r]: stored value, and (bnb) stored value * xhat
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      float f[4];
+      const bf16* rb = reinterpret_cast<const bf16*>(&rr[i][j]);
+      const bf16* yb = reinterpret_cast<const bf16*>(&yy[i][j]);
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        f[r] = acc[i][j][r] + bv[i][r];
+        if (has_res) f[r] += (float)rb[r];
+        if (p.relu) f[r] = fmaxf(f[r], 0.f);
+        if (has_y) f[r] = (float)yb[r] > 0.f ? f[r] : 0.f;
       }
-      const bool bnb = p.bnb.x != nullptr;
-      const bool stats = p.stats != nullptr;
+      uint2 o;
+      bf16* ob = reinterpret_cast<bf16*>(&o);
 #pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        const int cl0 = wc * 64 + i * 16 + 4 * lh;  // tile-local first of this lane's 4 channels
-        const int nb = U.n0 + cl0;
-        float bv[4], mu[4], is[4];
+      for (int r = 0; r < 4; ++r) ob[r] = (bf16)f[r];
+      *reinterpret_cast<uint2*>(crow[j] + nl + i * 16) = o;
+      const bf16* xb = reinterpret_cast<const bf16*>(&xx[i][j]);
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        gv[j][r] = (float)ob[r];  // statistics of the values actually stored
+        xh[j][r] = gv[j][r] * (((float)xb[r] - mu[i][r]) * is[i][r]);
+      }
+    }
+    if (stats) {
+      float pv[4], sa[4], sb[4];
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        if (bnb) {
+          pv[r] = 0.f;
+          sa[r] = (gv[0][r] + gv[1][r]) + (gv[2][r] + gv[3][r]);
+          sb[r] = (xh[0][r] + xh[1][r]) + (xh[2][r] + xh[3][r]);
+        } else {
+          // forward Welford rows: sums about a pivot (the wave's first pixel of the channel: lane
+          // 16*lh of the DPP row, broadcast by a row rotation chain-free read)
+          pv[r] = h3_row_first(gv[0][r]);
+          float a = 0.f, b = 0.f;
+#pragma unroll
+          for (int j = 0; j < 4; ++j) { const float d = gv[j][r] - pv[r]; a += d; b += d * d; }
+          sa[r] = a;
+          sb[r] = b;
+        }
+        sa[r] = h3_row_sum(sa[r]);  // fixed-order sum over the 16 lanes (pixels) of the DPP row
+        sb[r] = h3_row_sum(sb[r]);
+      }
+      if (lr == 0) {
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
-          bv[r] = p.bias ? p.bias[nb + r] : 0.f;
-          mu[r] = (bnb && stats) ? p.bnb.mean[nb + r] : 0.f;
-          is[r] = (bnb && stats) ? p.bnb.istd[nb + r] : 0.f;
-        }
-        // all operand loads of this channel group first (one latency, not one per pixel)
-        uint2 rr[4], yy[4], xx[4];
-#pragma unroll
-        for (int j = 0; j < 4; ++j) {
-          const long off = orow[j] * p.N + nb;
-          rr[j] = p.residual ? *reinterpret_cast<const uint2*>(p.residual + off) : make_uint2(0u, 0u);
-          yy[j] = (bnb && p.bnb.y) ? *reinterpret_cast<const uint2*>(p.bnb.y + off) : make_uint2(0u, 0u);
-          xx[j] = (bnb && stats) ? *reinterpret_cast<const uint2*>(p.bnb.x + off) : make_uint2(0u, 0u);
-        }
-        float gv[4][4], xh[4][4];  // [j][r]: stored value, and (bnb) stored value * xhat
-#pragma unroll
-        for (int j = 0; j < 4; ++j) {
-          float f[4];
-          const bf16* rb = reinterpret_cast<const bf16*>(&rr[j]);
-          const bf16* yb = reinterpret_cast<const bf16*>(&yy[j]);
-#pragma unroll
-          for (int r = 0; r < 4; ++r) {
-            f[r] = acc[i][j][r] + bv[r];
-            if (p.residual) f[r] += (float)rb[r];
-            if (p.relu) f[r] = fmaxf(f[r], 0.f);
-            if (bnb && p.bnb.y) f[r] = (float)yb[r] > 0.f ? f[r] : 0.f;
-          }
-          uint2 o;
-          bf16* ob = reinterpret_cast<bf16*>(&o);
-#pragma unroll
-          for (int r = 0; r < 4; ++r) ob[r] = (bf16)f[r];
-          *reinterpret_cast<uint2*>(p.C + orow[j] * p.N + nb) = o;
-          const bf16* xb = reinterpret_cast<const bf16*>(&xx[j]);
-#pragma unroll
-          for (int r = 0; r < 4; ++r) {
-            gv[j][r] = (float)ob[r];  // statistics of the values actually stored
-            xh[j][r] = gv[j][r] * (((float)xb[r] - mu[r]) * is[r]);
-          }
-        }
-        if (stats) {
-          float pv[4], sa[4], sb[4];
-#pragma unroll
-          for (int r = 0; r < 4; ++r) {
-            if (bnb) {
-              pv[r] = 0.f;
-              sa[r] = (gv[0][r] + gv[1][r]) + (gv[2][r] + gv[3][r]);
-              sb[r] = (xh[0][r] + xh[1][r]) + (xh[2][r] + xh[3][r]);
-            } else {
-              // forward Welford rows: sums about a pivot (the wave's first pixel of the channel)
-              pv[r] = __shfl(gv[0][r], lane & 0x30, 64);
-              float a = 0.f, b = 0.f;
-#pragma unroll
-              for (int j = 0; j < 4; ++j) { const float d = gv[j][r] - pv[r]; a += d; b += d * d; }
-              sa[r] = a;
-              sb[r] = b;
-            }
-            sa[r] = h3_row_sum(sa[r]);  // fixed-order sum over the 16 lanes (pixels) of the DPP row
-            sb[r] = h3_row_sum(sb[r]);
-          }
-          if (lr == 0) {
-#pragma unroll
-            for (int r = 0; r < 4; ++r) {
-              float* e = red + (wp * BN + cl0 + r) * 3;
-              e[0] = pv[r];
-              e[1] = sa[r];
-              e[2] = sb[r];
-            }
-          }
+          float* e = red + (wp * BN + cl0 + r) * 3;
+          e[0] = pv[r];
+          e[1] = sa[r];
+          e[2] = sb[r];
         }
       }
-      stamp(4);
-      if (stats) {
-        __syncthreads();
-        if (tid < BN) {
-          if (bnb) {
-            float a = 0.f, b = 0.f;
-#pragma unroll
-            for (int w = 0; w < WP; ++w) { a += red[(w * BN + tid) * 3 + 1]; b += red[(w * BN + tid) * 3 + 2]; }
-            p.stats[((long)U.tm * 2 + 0) * p.N + U.n0 + tid] = a;
-            p.stats[((long)U.tm * 2 + 1) * p.N + U.n0 + tid] = b;
-          } else {
-            Welford w = welford_from_shifted(64.f, red[tid * 3 + 0], red[tid * 3 + 1], red[tid * 3 + 2]);
-#pragma unroll
-            for (int k = 1; k < WP; ++k) {
-              const float* e = red + (k * BN + tid) * 3;
-              w = welford_merge(w, welford_from_shifted(64.f, e[0], e[1], e[2]));
-            }
-            store_welford(p.stats, U.tm, p.N, U.n0 + tid, w);
-          }
-        }
-      }
-      stamp(5);
     }
-    if (!hasV) break;
-    // next unit: zero the accumulators; V's halo(0), W(0,0), W(0,1) are in flight
-#pragma unroll
-    for (int i = 0; i < 4; ++i)
-#pragma unroll
-      for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-    first_unit = false;
-    u = v;
-    wbU = wbV;
   }
+  stamp(4);
+  if (stats) {
+    __syncthreads();
+    if (tid < BN) {
+      if (bnb) {
+        float a = 0.f, b = 0.f;
+#pragma unroll
+        for (int w = 0; w < WP; ++w) { a += red[(w * BN + tid) * 3 + 1]; b += red[(w * BN + tid) * 3 + 2]; }
+        p.stats[((long)tm * 2 + 0) * p.N + n0 + tid] = a;
+        p.stats[((long)tm * 2 + 1) * p.N + n0 + tid] = b;
+      } else {
+        Welford w = welford_from_shifted(64.f, red[tid * 3 + 0], red[tid * 3 + 1], red[tid * 3 + 2]);
+#pragma unroll
+        for (int k = 1; k < WP; ++k) {
+          const float* e = red + (k * BN + tid) * 3;
+          w = welford_merge(w, welford_from_shifted(64.f, e[0], e[1], e[2]));
+        }
+        store_welford(p.stats, tm, p.N, n0 + tid, w);
+      }
+    }
+  }
+  stamp(5);
 }
 
 // ------------------------------------------------------------------------------------------------
@@ -570,61 +549,46 @@ struct H3Plan {
 // tile plan for a 3x3 stride-1 conv of NB x H x W pixels, Cs input / N output channels
 bool hconv3_plan(int NB, int H, int W, int Cs, int N, int ntaps, H3Plan* pl) {
   if (!g_h3 || ntaps != 9 || Cs % 64 || N % 64) return false;  // even 32-channel chunk count
-  const int WC = (N % 128 == 0) ? 2 : 1;
-  const int BN = 64 * WC, BM = 512 / WC;
-  int TW, TWC;
-  if (WC == 1 && W % 32 == 0) { TW = 32; TWC = 16; }
-  else if (W % 16 == 0) { TW = 16; TWC = 16; }
-  else if (W == 8) { TW = 8; TWC = 8; }
-  else if (W == 4) { TW = 4; TWC = 4; }
-  else return false;
-  int TH = BM / TW;
-  if (TH > H) TH = H;
-  if (H % TH || BM % (TH * TW)) return false;
-  const int IMG = BM / (TH * TW);
-  if (NB % IMG) return false;
-  const int NWI = (3 * BN / 16 + 7) / 8;
-  const int pitch = TWC == 4 ? TW + 2 : (TW + 2 + 7) / 8 * 8;
-  const int HN = (IMG * (TH + 2) * pitch + 127) / 128;
-  const int red = (8 / WC) * BN * 12 + 16;
-  if (2 * HN * 8192 + 3 * NWI * 8192 + red > 163840) return false;
-  // kernel instances (launch_h3_plan): (WC, TWC, HN, pitch) = (1,16,6,40) (2,16,4,24) (2,8,5,16) (2,4,5,runtime)
-  const bool inst = (WC == 1 && TWC == 16 && HN == 6 && pitch == 40) || (WC == 2 && TWC == 16 && HN == 4 && pitch == 24) ||
-                    (WC == 2 && TWC == 8 && HN == 5 && pitch == 16) || (WC == 2 && TWC == 4 && HN == 5);
-  if (!inst) return false;
+  // 16-wide (and wider) maps: 4-wave workgroups of 64 channels x one 16x16 tile, two per CU
+  // (LDS 72 KB). The 8- and 4-wide maps stay on hconv_kernel (measured faster there: their split-K
+  // grids of single 8-wave workgroups lose more to the serial prologue / epilogue than the K loop
+  // gains).
+  if (W % 16 || H % 16) return false;
+  const int WC = 1, NW = 4, BN = 64, BM = 256;
+  const int TW = 16, TWC = 16, TH = 16, IMG = 1;
+  const int NWI = (3 * BN / 16 + NW - 1) / NW;
+  const int pitch = TW + 2;
+  const int HN = (IMG * (TH + 2) * pitch + 16 * NW - 1) / (16 * NW);
+  if (HN != 6 || NWI != 3) return false;  // the one instance: <4, 1, 16, 6, 3, 2, 0>
   pl->WC = WC; pl->TWC = TWC; pl->HN = HN; pl->NWI = NWI;
   pl->TH = TH; pl->TW = TW; pl->IMG = IMG; pl->pitch = pitch;
   pl->tiles_m = NB * H * W / BM;
   pl->tiles_n = N / BN;
-  // split-K over 32-channel chunks until the grid covers the CUs (one 512-thread workgroup per
-  // CU: half the 256-thread kernels' workgroup target)
+  // split-K over 32-channel chunks until the grid holds the target workgroup count (two resident
+  // per CU), keeping an even chunk count per split
   const long tiles = (long)pl->tiles_m * pl->tiles_n;
-  const int nchunk = Cs / 32, target = hconv_split_target() / 2;
+  const int nchunk = Cs / 32, target = hconv_split_target();
   int s = 1;
-  while (tiles * s < target && nchunk % (4 * s) == 0) s *= 2;  // keeps an even chunk count per split
+  while (tiles * s < target && nchunk % (4 * s) == 0) s *= 2;
   pl->splits = s;
   return true;
 }
 
-template <int WC, int TWC, int HN, int PITCH>
+template <int NW, int WC, int TWC, int HN, int NWI, int NWS, int PITCH>
 static void launch_h3(const HConvArgs& a, const H3Geo& g, int grid, hipStream_t s) {
-  constexpr int NWI = WC == 1 ? 2 : 3;
-  using T = H3<WC, TWC, HN, NWI, PITCH>;
-  auto k = hconv3_kernel<WC, TWC, HN, NWI, PITCH>;
+  using T = H3<NW, WC, TWC, HN, NWI, NWS, PITCH>;
+  auto k = hconv3_kernel<NW, WC, TWC, HN, NWI, NWS, PITCH>;
   static bool attr = false;
   if (!attr) {
     DCNN_HIP_CHECK(hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, T::LDS));
     attr = true;
   }
-  hipLaunchKernelGGL(k, dim3(grid), dim3(512), T::LDS, s, a, g);
+  hipLaunchKernelGGL(k, dim3(grid), dim3(NW * 64), T::LDS, s, a, g);
   DCNN_LAUNCH_CHECK();
 }
 
 static void launch_h3_plan(const H3Plan& pl, const HConvArgs& a, const H3Geo& g, int grid, hipStream_t s) {
-  if (pl.WC == 1 && pl.TWC == 16 && pl.HN == 6 && pl.pitch == 40) return launch_h3<1, 16, 6, 40>(a, g, grid, s);
-  if (pl.WC == 2 && pl.TWC == 16 && pl.HN == 4 && pl.pitch == 24) return launch_h3<2, 16, 4, 24>(a, g, grid, s);
-  if (pl.WC == 2 && pl.TWC == 8 && pl.HN == 5 && pl.pitch == 16) return launch_h3<2, 8, 5, 16>(a, g, grid, s);
-  if (pl.WC == 2 && pl.TWC == 4 && pl.HN == 5) return launch_h3<2, 4, 5, 0>(a, g, grid, s);
+  if (pl.WC == 1 && pl.TWC == 16 && pl.HN == 6 && pl.NWI == 3) return launch_h3<4, 1, 16, 6, 3, 2, 0>(a, g, grid, s);
   throw std::runtime_error("hconv3: no kernel instance for this plan");
 }
 
@@ -648,17 +612,9 @@ bool hconv3_try(const HConvArgs& a0, hipStream_t s) {
   g.TH = pl.TH; g.TW = pl.TW; g.IMG = pl.IMG; g.pitch = pl.pitch;
   g.tiles_n = pl.tiles_n; g.tiles_m = pl.tiles_m;
   g.nchunk = a.Cs / 32 / pl.splits;
-  g.halo_bytes = 8 * pl.HN * 1024;
+  g.halo_bytes = 4 * pl.HN * 1024;
   g.stamps = g_h3_stamps;
-  // persistent grid: one workgroup per CU (LDS-bound), each walking units blockIdx, + grid, ...
-  static int cus = 0;
-  if (!cus) {
-    int dev = 0;
-    DCNN_HIP_CHECK(hipGetDevice(&dev));
-    DCNN_HIP_CHECK(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev));
-  }
-  const int units = pl.tiles_m * pl.tiles_n * pl.splits;
-  const int grid = units < cus ? units : cus;
+  const int grid = pl.tiles_m * pl.tiles_n * pl.splits;
   launch_h3_plan(pl, a, g, grid, s);
   return true;
 }

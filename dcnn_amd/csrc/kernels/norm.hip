@@ -759,7 +759,12 @@ __global__ void __launch_bounds__(256) bn_apply_dual_kernel(BnSide a, BnSide b, 
   }
 }
 
-bool bn_apply_dual_supported(long R, int C) { return C % 8 == 0 && R * (long)C < (1l << 31); }
+// (the dual backward stages 8 coefficient arrays of C floats in dynamic LDS: 32*C bytes must fit
+// the 64 KB a launch gets without a raised limit, i.e. C <= 2048; wider layers use the separate
+// per-side passes)
+bool bn_apply_dual_supported(long R, int C) {
+  return C % 8 == 0 && 8L * C * (long)sizeof(float) <= 65536 && R * (long)C < (1l << 31);
+}
 
 // Backward of two BatchNorms fed the same gradient dy (a residual block's tail and its projection
 // shortcut): dx_a and dx_b from one read of dy, each side with bn_bwd_apply_v_kernel's

@@ -194,7 +194,10 @@ class Allocator {
 
   uintptr_t allocate(uint64_t nbytes, const Flow& f) {
     if (nbytes == 0) nbytes = 1;
-    release_deferred();
+    // dropped DLPack exports are reclaimed in batches only (the reclaim synchronises the device):
+    // one allocation no longer drains every stream — other pipeline stages mid-step or mid-capture
+    // keep running — until the queue holds >= 256 MiB or 256 buffers
+    if (deferred_bytes_ >= (256ull << 20) || deferred_.size() >= 256) release_deferred();
     DeviceGuard g(dev_);
     const uint64_t before = reserved();
     void* p = nullptr;
@@ -220,18 +223,28 @@ class Allocator {
   void defer_free(uintptr_t p, uint64_t nbytes) {
     std::lock_guard<std::mutex> l(mu_);
     deferred_.push_back({p, nbytes});
+    deferred_bytes_ += nbytes;
   }
   void release_deferred() {
     std::vector<std::pair<uintptr_t, uint64_t>> todo;
     {
       std::lock_guard<std::mutex> l(mu_);
       todo.swap(deferred_);
+      deferred_bytes_ = 0;
     }
     if (todo.empty()) return;
     DeviceGuard g(dev_);
-    RT_CHECK(hipDeviceSynchronize());  // every stream done with them
-    for (auto& d : todo) RT_CHECK(hipFreeAsync(reinterpret_cast<void*>(d.first), nullptr));
-    RT_CHECK(hipStreamSynchronize(nullptr));
+    auto drain = [&] {  // every stream done with them
+      RT_CHECK(hipDeviceSynchronize());
+      for (auto& d : todo) RT_CHECK(hipFreeAsync(reinterpret_cast<void*>(d.first), nullptr));
+      RT_CHECK(hipStreamSynchronize(nullptr));
+    };
+    if (PyGILState_Check()) {  // other Python threads (pipeline stages) keep running meanwhile
+      py::gil_scoped_release nogil;
+      drain();
+    } else {
+      drain();
+    }
     std::lock_guard<std::mutex> l(mu_);
     for (auto& d : todo) {
       ++frees_;
@@ -285,6 +298,7 @@ class Allocator {
   mutable std::mutex mu_;
   uint64_t allocs_ = 0, frees_ = 0, grows_ = 0, in_use_ = 0, peak_ = 0;
   std::vector<std::pair<uintptr_t, uint64_t>> deferred_;
+  uint64_t deferred_bytes_ = 0;
 };
 
 // ------------------------------------------------------------------ DLPack export (zero copy)

@@ -1,5 +1,5 @@
-"""Third-generation halo conv (csrc/kernels/hconv3.hip): 8-wave 64x64-per-wave tiles, weights as
-the MFMA A operand, epilogue from registers. Checked against a plain PyTorch fp32 reference of
+"""Third-generation halo conv (csrc/kernels/hconv3.hip): 64x64-per-wave tiles, 3 taps per barrier,
+weights as the MFMA A operand, epilogue from registers. Checked against a plain PyTorch fp32 reference of
 the same op and against the previous-generation kernel (hconv3_enable(0)) on every ResNet layer
 geometry, with every epilogue option (bias, residual, ReLU, forward BN statistics, backward-BN
 fusion) and split-K."""
@@ -24,10 +24,10 @@ def hip():
     return H
 
 
-# N, C (input channels), H, W, Co — ResNet-18/50 layer geometries at small batch (16-, 8-, 4-wide
-# tiles, 64- and 128-channel tiles, several images per tile, split-K on the small grids)
-CASES = [(4, 64, 32, 32, 64), (2, 64, 32, 64, 64), (4, 128, 16, 16, 128), (8, 256, 8, 8, 256),
-         (32, 512, 4, 4, 512), (4, 64, 16, 16, 128), (16, 128, 8, 8, 256), (64, 64, 32, 32, 64)]
+# N, C (input channels), H, W, Co — the 16-wide-and-wider ResNet-18/50 layer geometries hconv3 runs
+# (several 16x16 tiles per image, 64-channel tiles, split-K on the small grids)
+CASES = [(4, 64, 32, 32, 64), (2, 64, 32, 64, 64), (4, 128, 16, 16, 128), (2, 64, 16, 16, 64),
+         (4, 64, 16, 16, 128), (2, 256, 16, 16, 256), (64, 64, 32, 32, 64), (4, 512, 16, 16, 128)]
 
 
 def _both(K, fn):
@@ -89,7 +89,7 @@ def test_hconv3_dgrad(hip, case):
     assert rel_err(d3, d2) < 5e-3
 
 
-@pytest.mark.parametrize("case", [(4, 64, 32, 32, 64), (4, 128, 16, 16, 128), (8, 256, 8, 8, 256)])
+@pytest.mark.parametrize("case", [(4, 64, 32, 32, 64), (4, 128, 16, 16, 128), (2, 256, 16, 16, 128)])
 def test_hconv3_dgrad_bn_fusion(hip, case):
     """dgrad with the consuming BatchNorm's ReLU mask + backward statistics in the hconv3
     epilogue == the standalone BN backward of the unfused dgrad."""
@@ -120,10 +120,10 @@ def test_hconv3_dgrad_bn_fusion(hip, case):
 
 
 def test_hconv3_split_k_matches_unsplit(hip):
-    """Layer-4 geometry at batch 32: split-K (partials summed in split order by the tile's last
-    workgroup) vs one workgroup per tile; repeated split launches bit-identical."""
+    """A deep small grid: split-K (partials summed in split order by the tile's last workgroup) vs
+    one workgroup per tile; repeated split launches bit-identical."""
     K = hip.kernels()
-    N, C, H, W, Co = 32, 512, 4, 4, 512
+    N, C, H, W, Co = 4, 512, 16, 16, 128
     assert K.hconv_splits(N, H, W, C, Co, 9) > 1
     torch.manual_seed(34)
     x = torch.randn(N, C, H, W).cuda().bfloat16().contiguous(memory_format=CL)
