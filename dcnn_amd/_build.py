@@ -127,8 +127,58 @@ def build_native(force=False, verbose=False, max_workers=None):
     return target
 
 
+# kernel-library / native objects the C++ host API links (the pybind layers stay out)
+_HOST_SKIP_KERNELS = {"bindings", "runtime", "rccl"}
+_HOST_NATIVE = ("cpu_ops", "cpu_gemm", "threadpool")
+
+
+def build_host(force=False, verbose=False, max_workers=None):
+    """C++ host API (csrc/host): ``libdcnn.so`` next to this file (host layers + the HIP kernel
+    library + the native CPU kernels, no Python) and the C++ examples (examples/cpp/*.cpp) as
+    executables under ``dcnn_amd/bin/``."""
+    build_native(force, verbose, max_workers)
+    build_kernels(force, verbose, max_workers)
+    src_dir = PKG / "csrc" / "host"
+    out_dir = BUILD / "host"
+    out_dir.mkdir(parents=True, exist_ok=True)
+    cxx = os.environ.get("CXX", "g++")
+    inc = [f"-I{src_dir}"]
+    cflags = ["-O3", "-fPIC", "-std=c++17", "-pthread", "-Wall", "-Wno-unused-function"]
+    hflags = ["-O3", "-fPIC", "-std=c++17", f"--offload-arch={ARCH}", "-Wno-unused-result", "-DNDEBUG"]
+    hdrs = _headers(src_dir / "dcnn") + _headers(PKG / "csrc" / "kernels") + _headers(PKG / "csrc" / "native")
+    jobs, objs = [], []
+    for src in sorted(src_dir.glob("*.cpp")) + sorted(src_dir.glob("*.hip")):
+        obj = out_dir / (src.stem + ".o")
+        if src.suffix == ".hip":
+            cmd = [HIPCC, *hflags, *inc, "-x", "hip", "-c", str(src), "-o", str(obj)]
+        else:
+            cmd = [cxx, *cflags, *inc, "-c", str(src), "-o", str(obj)]
+        sig = hashlib.sha1(" ".join(cmd).encode()).hexdigest()
+        jobs.append((cmd, obj, sig, force or _needs_build(obj, src, hdrs, sig)))
+        objs.append(obj)
+    _compile_many(jobs, verbose, max_workers or min(8, os.cpu_count() or 4))
+    kobjs = [o for o in sorted((BUILD / "kernels").glob("*.o")) if o.stem not in _HOST_SKIP_KERNELS]
+    nobjs = [BUILD / "native" / f"{n}.o" for n in _HOST_NATIVE]
+    lib = PKG / "libdcnn.so"
+    deps = objs + kobjs + nobjs
+    if force or not lib.exists() or any(o.stat().st_mtime > lib.stat().st_mtime for o in deps):
+        _run([HIPCC, "-shared", "-fPIC", f"--offload-arch={ARCH}", *map(str, deps), "-o", str(lib), "-pthread"],
+             verbose)
+    bins = []
+    bin_dir = PKG / "bin"
+    bin_dir.mkdir(exist_ok=True)
+    for src in sorted((ROOT / "examples" / "cpp").glob("*.cpp")):
+        exe = bin_dir / src.stem
+        if force or not exe.exists() or exe.stat().st_mtime < max(lib.stat().st_mtime, src.stat().st_mtime,
+                                                                  *(h.stat().st_mtime for h in hdrs)):
+            _run([cxx, *cflags, *inc, str(src), "-o", str(exe), f"-L{PKG}", "-ldcnn", "-Wl,-rpath,$ORIGIN/..",
+                  f"-L{ROCM}/lib", "-lamdhip64", f"-Wl,-rpath,{ROCM}/lib"], verbose)
+        bins.append(exe)
+    return lib, bins
+
+
 def build_all(force=False, verbose=False):
-    return build_native(force, verbose), build_kernels(force, verbose)
+    return build_native(force, verbose), build_kernels(force, verbose), build_host(force, verbose)
 
 
 def main(argv=None):
@@ -136,12 +186,15 @@ def main(argv=None):
     ap = argparse.ArgumentParser()
     ap.add_argument("--force", action="store_true")
     ap.add_argument("--verbose", action="store_true")
-    ap.add_argument("--only", choices=["kernels", "native"])
+    ap.add_argument("--only", choices=["kernels", "native", "host"])
     a = ap.parse_args(argv)
     if a.only in (None, "native"):
         print("built", build_native(a.force, a.verbose))
     if a.only in (None, "kernels"):
         print("built", build_kernels(a.force, a.verbose))
+    if a.only in (None, "host"):
+        lib, bins = build_host(a.force, a.verbose)
+        print("built", lib, *bins)
 
 
 if __name__ == "__main__":

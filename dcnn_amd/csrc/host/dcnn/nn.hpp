@@ -1,0 +1,327 @@
+// C++ host API: layers, Sequential / SequentialBuilder, loss, optimizers, training loop.
+//
+// A C++ program builds, trains, saves and reloads a model without Python:
+//
+//   auto model = dcnn::SequentialBuilder("mnist_cnn").input({1, 28, 28})
+//                    .conv2d(16, 3, 3, 1, 1, 1, 1).batchnorm().activation("relu").maxpool2d(2, 2)
+//                    .flatten().dense(10).build();
+//   model.set_device(dcnn::Device::gpu(0));
+//   model.initialize(42);
+//   dcnn::Adam opt(1e-3f);
+//   dcnn::train_classification_model(model, train_source, &test_source, opt, cfg);
+//   model.save_to_file("snapshots/mnist_cnn");   // path.json + path.bin, readable by Python
+//
+// CPU: fp32 NCHW on the native CPU kernels. GPU: bf16 NHWC activations on the HIP/CDNA4 kernel
+// library with fp32 master parameters (Adam / SGD write the bf16 operand shadows in the same
+// kernel). The architecture JSON and the .bin weight records are the formats of the Python front
+// end (dcnn_amd/nn/sequential.py) and of the reference, so a model moves between the two.
+// Reference parity: include/nn/sequential.hpp:39-1340 (Sequential, SequentialBuilder),
+// include/nn/train.hpp:202 (train_classification_model), include/nn/optimizers.hpp,
+// include/nn/loss.hpp, examples/mnist_cnn_trainer.cpp.
+#pragma once
+#include <functional>
+#include <memory>
+#include <string>
+#include <vector>
+
+#include "json.hpp"
+#include "ops.hpp"
+#include "tensor.hpp"
+
+namespace dcnn {
+
+// One trainable tensor. `value` / `grad` are fp32 on the layer's device in `layout` (GPU conv
+// weights: physical [Co][KH][KW][Ci] = NHWC of the logical (Co, Ci, KH, KW)); `shadow` is the bf16
+// GEMM operand copy on the GPU. `shape` is the logical 4-D shape of the .bin record.
+struct Param {
+  std::string name;
+  std::vector<int64_t> shape;
+  Layout layout = Layout::NCHW;
+  Tensor value, grad, shadow;
+  Tensor m, v;  // optimizer state (lazily created)
+};
+
+class Layer {
+ public:
+  explicit Layer(std::string name) : name_(std::move(name)) {}
+  virtual ~Layer() = default;
+  virtual std::string type() const = 0;
+  virtual json::Value parameters_config() const = 0;
+  // logical (N, C, H, W) output shape for a logical input shape
+  virtual std::vector<int64_t> output_shape(const std::vector<int64_t>& in) const = 0;
+  // create parameters for the given input shape on `dev` (deterministic in `seed`)
+  virtual void build(const std::vector<int64_t>& in, Device dev, uint64_t seed) { (void)in; (void)seed; dev_ = dev; }
+  virtual Tensor forward(const Tensor& x, bool training) = 0;
+  virtual Tensor backward(const Tensor& dy) = 0;
+  // refresh the bf16 operand shadows from the fp32 masters (after loading weights)
+  void sync_shadow();
+  std::vector<Param>& params() { return params_; }
+  const std::string& name() const { return name_; }
+  Device device() const { return dev_; }
+
+ protected:
+  Param& add_param(const std::string& n, const std::vector<int64_t>& shape, Layout phys, const std::vector<float>& init);
+  std::string name_;
+  Device dev_ = Device::cpu();
+  std::vector<Param> params_;
+};
+
+class Conv2D : public Layer {
+ public:
+  Conv2D(int in_ch, int out_ch, int kh, int kw, int sh = 1, int sw = 1, int ph = 0, int pw = 0, bool bias = true,
+         std::string name = "conv2d");
+  std::string type() const override { return "conv2d"; }
+  json::Value parameters_config() const override;
+  std::vector<int64_t> output_shape(const std::vector<int64_t>& in) const override;
+  void build(const std::vector<int64_t>& in, Device dev, uint64_t seed) override;
+  Tensor forward(const Tensor& x, bool training) override;
+  Tensor backward(const Tensor& dy) override;
+
+ private:
+  ConvShape shape_for(const std::vector<int64_t>& in) const;
+  int ci_, co_, kh_, kw_, sh_, sw_, ph_, pw_;
+  bool bias_;
+  Tensor x_;
+};
+
+class Dense : public Layer {
+ public:
+  Dense(int in_features, int out_features, bool bias = true, std::string name = "dense");
+  std::string type() const override { return "dense"; }
+  json::Value parameters_config() const override;
+  std::vector<int64_t> output_shape(const std::vector<int64_t>& in) const override;
+  void build(const std::vector<int64_t>& in, Device dev, uint64_t seed) override;
+  Tensor forward(const Tensor& x, bool training) override;
+  Tensor backward(const Tensor& dy) override;
+
+ private:
+  int in_, out_;
+  bool bias_;
+  Tensor x_;
+};
+
+class BatchNorm : public Layer {
+ public:
+  explicit BatchNorm(int num_features, float eps = 1e-5f, float momentum = 0.1f, bool affine = true,
+                     std::string name = "batchnorm");
+  std::string type() const override { return "batchnorm"; }
+  json::Value parameters_config() const override;
+  std::vector<int64_t> output_shape(const std::vector<int64_t>& in) const override { return in; }
+  void build(const std::vector<int64_t>& in, Device dev, uint64_t seed) override;
+  Tensor forward(const Tensor& x, bool training) override;
+  Tensor backward(const Tensor& dy) override;
+  Tensor running_mean, running_var;
+
+ private:
+  int c_;
+  float eps_, momentum_;
+  bool affine_;
+  bool train_ = true;
+  Tensor x_, mean_, istd_;
+};
+
+class Activation : public Layer {
+ public:
+  explicit Activation(std::string kind = "relu", std::string name = "activation");
+  std::string type() const override { return "activation"; }
+  json::Value parameters_config() const override;
+  std::vector<int64_t> output_shape(const std::vector<int64_t>& in) const override { return in; }
+  Tensor forward(const Tensor& x, bool training) override;
+  Tensor backward(const Tensor& dy) override;
+
+ private:
+  std::string kind_;
+  int code_;
+  Tensor x_;
+};
+
+class Pool2D : public Layer {
+ public:
+  Pool2D(bool max, int kh, int kw, int sh, int sw, int ph, int pw, std::string name);
+  std::string type() const override { return max_ ? "maxpool2d" : "avgpool2d"; }
+  json::Value parameters_config() const override;
+  std::vector<int64_t> output_shape(const std::vector<int64_t>& in) const override;
+  Tensor forward(const Tensor& x, bool training) override;
+  Tensor backward(const Tensor& dy) override;
+
+ private:
+  PoolShape shape_for(const std::vector<int64_t>& in) const;
+  bool max_;
+  int kh_, kw_, sh_, sw_, ph_, pw_;
+  std::vector<int64_t> in_shape_;
+  Tensor idx_;
+};
+
+class Flatten : public Layer {
+ public:
+  explicit Flatten(std::string name = "flatten") : Layer(std::move(name)) {}
+  std::string type() const override { return "flatten"; }
+  json::Value parameters_config() const override { return json::Value::object(); }
+  std::vector<int64_t> output_shape(const std::vector<int64_t>& in) const override;
+  Tensor forward(const Tensor& x, bool training) override;
+  Tensor backward(const Tensor& dy) override;
+
+ private:
+  std::vector<int64_t> in_shape_;
+};
+
+// layer from its JSON record {"type", "name", "parameters"} (the LayerFactory of the formats)
+std::unique_ptr<Layer> create_layer(const json::Value& rec);
+
+class Sequential {
+ public:
+  explicit Sequential(std::string name = "sequential") : name_(std::move(name)) {}
+  Sequential(Sequential&&) = default;
+  Sequential& operator=(Sequential&&) = default;
+  void add(std::unique_ptr<Layer> l) { layers_.push_back(std::move(l)); }
+  void set_input_shape(const std::vector<int64_t>& chw) { input_chw_ = chw; }
+  void set_device(Device d);
+  Device device() const { return dev_; }
+  void initialize(uint64_t seed = 0);
+  void set_training(bool t) { training_ = t; }
+  bool is_training() const { return training_; }
+  // x: fp32 logical NCHW (host or device); returns the logits [N, classes] as a device tensor
+  Tensor forward(const Tensor& x);
+  void backward(const Tensor& dlogits);
+  std::vector<Param*> parameters();
+  void zero_grad();
+  size_t num_parameters();
+  const std::vector<std::unique_ptr<Layer>>& layers() const { return layers_; }
+  const std::string& name() const { return name_; }
+
+  json::Value get_config() const;
+  void print_config() const;
+  static Sequential load_from_config(const json::Value& cfg);
+  // path.json (architecture) + path.bin (parameters in layer order, logical NCHW fp32) +
+  // path.bnstats (BatchNorm running statistics)
+  void save_to_file(const std::string& path) const;
+  void load_weights_file(const std::string& path);
+  // BatchNorm running statistics sidecar (path.bnstats, written by save_to_file)
+  void load_bn_stats(const std::string& path);
+  static Sequential from_file(const std::string& path, Device dev = Device::cpu());
+
+ private:
+  std::string name_;
+  std::vector<std::unique_ptr<Layer>> layers_;
+  std::vector<int64_t> input_chw_;
+  Device dev_ = Device::cpu();
+  bool training_ = true;
+  bool initialized_ = false;
+};
+
+class SequentialBuilder {
+ public:
+  explicit SequentialBuilder(std::string name = "sequential") : model_(std::move(name)) {}
+  SequentialBuilder& input(const std::vector<int64_t>& chw);
+  SequentialBuilder& conv2d(int out_ch, int kh, int kw, int sh = 1, int sw = 1, int ph = 0, int pw = 0,
+                            bool bias = true, const std::string& name = "");
+  SequentialBuilder& batchnorm(float eps = 1e-5f, float momentum = 0.1f, bool affine = true,
+                               const std::string& name = "");
+  SequentialBuilder& activation(const std::string& kind = "relu", const std::string& name = "");
+  SequentialBuilder& maxpool2d(int kh, int kw, int sh = 0, int sw = 0, int ph = 0, int pw = 0,
+                               const std::string& name = "");
+  SequentialBuilder& avgpool2d(int kh, int kw, int sh = 1, int sw = 1, int ph = 0, int pw = 0,
+                               const std::string& name = "");
+  SequentialBuilder& flatten(const std::string& name = "");
+  SequentialBuilder& dense(int out_features, bool bias = true, const std::string& name = "");
+  Sequential build();
+
+ private:
+  std::string auto_name(const std::string& given, const std::string& kind);
+  Sequential model_;
+  std::vector<int64_t> cur_;  // current (C, H, W)
+  int count_ = 0;
+};
+
+// ---- loss: softmax cross-entropy over logits [N, C] (mean over the batch)
+struct LossResult {
+  double loss = 0;
+  long correct = 0;
+  Tensor grad;  // d loss / d logits, same device / dtype as the logits
+};
+LossResult softmax_cross_entropy(const Tensor& logits, const Tensor& labels);
+
+class Optimizer {
+ public:
+  explicit Optimizer(float lr) : lr_(lr) {}
+  virtual ~Optimizer() = default;
+  virtual void step(const std::vector<Param*>& params) = 0;
+  void set_learning_rate(float lr) { lr_ = lr; }
+  float learning_rate() const { return lr_; }
+
+ protected:
+  float lr_;
+};
+
+class SGD : public Optimizer {
+ public:
+  explicit SGD(float lr, float momentum = 0.f) : Optimizer(lr), momentum_(momentum) {}
+  void step(const std::vector<Param*>& params) override;
+
+ private:
+  float momentum_;
+};
+
+class Adam : public Optimizer {
+ public:
+  explicit Adam(float lr, float b1 = 0.9f, float b2 = 0.999f, float eps = 1e-8f, float wd = 0.f,
+                bool decoupled = false)
+      : Optimizer(lr), b1_(b1), b2_(b2), eps_(eps), wd_(wd), decoupled_(decoupled) {}
+  void step(const std::vector<Param*>& params) override;
+
+ private:
+  float b1_, b2_, eps_, wd_;
+  bool decoupled_;
+  long t_ = 0;
+};
+
+// ---- data
+class DataSource {
+ public:
+  virtual ~DataSource() = default;
+  virtual void reset(uint64_t epoch) = 0;
+  // next batch: x fp32 host NCHW, labels int64; false at the end of the epoch
+  virtual bool next(int batch, Tensor& x, Tensor& labels) = 0;
+  virtual size_t size() const = 0;
+};
+
+// learnable synthetic classification set: class k images carry a class-specific spatial
+// pattern plus noise (deterministic in the seed)
+class SyntheticClassification : public DataSource {
+ public:
+  SyntheticClassification(size_t n, int c, int h, int w, int classes, uint64_t seed, float noise = 0.5f);
+  void reset(uint64_t epoch) override;
+  bool next(int batch, Tensor& x, Tensor& labels) override;
+  size_t size() const override { return n_; }
+
+ private:
+  size_t n_;
+  int c_, h_, w_, classes_;
+  uint64_t seed_;
+  float noise_;
+  std::vector<float> proto_;
+  std::vector<size_t> order_;
+  size_t pos_ = 0;
+};
+
+struct TrainingConfig {
+  int epochs = 1;
+  int batch_size = 64;
+  int max_steps = -1;          // per epoch, -1 = whole epoch
+  int progress_interval = 50;  // steps between progress lines, 0 = quiet
+  float lr_decay = 1.0f;       // multiplicative per epoch
+  uint64_t seed = 0;
+};
+
+struct EpochStats {
+  double train_loss = 0, train_acc = 0, val_loss = 0, val_acc = 0, seconds = 0;
+};
+
+// one optimisation step; returns (loss, correct)
+LossResult train_step(Sequential& model, Optimizer& opt, const Tensor& x, const Tensor& labels);
+// mean loss / accuracy over a source
+EpochStats evaluate(Sequential& model, DataSource& src, int batch_size);
+std::vector<EpochStats> train_classification_model(Sequential& model, DataSource& train, DataSource* val,
+                                                   Optimizer& opt, const TrainingConfig& cfg);
+
+}  // namespace dcnn

@@ -1,0 +1,75 @@
+// Device backends of the C++ host API's layers. The layer code (nn.cpp, plain C++) calls these;
+// cpu_* run the native fp32 NCHW CPU kernels (csrc/native/cpu_ops.cpp, cpu_gemm.cpp), gpu_* the
+// HIP/CDNA4 kernel library (csrc/kernels/*.hip) on bf16 NHWC activations with fp32 master
+// parameters and bf16 operand shadows — the same kernels the Python front end launches.
+#pragma once
+#include <cstdint>
+
+namespace dcnn {
+
+struct ConvShape {
+  int N, C, H, W, Co, KH, KW, SH, SW, PH, PW, OH, OW;
+};
+struct PoolShape {
+  int N, C, H, W, OH, OW, KH, KW, SH, SW, PH, PW;
+};
+enum ActKind { ACT_RELU = 0, ACT_LEAKY_RELU = 1, ACT_ELU = 2, ACT_SIGMOID = 3, ACT_TANH = 4, ACT_LINEAR = 5 };
+
+namespace cpu_ops {
+void conv_fwd(const float* x, const float* w, const float* b, float* y, const ConvShape& s);
+void conv_bwd(const float* x, const float* w, const float* dy, float* dx, float* dw, float* db, const ConvShape& s);
+void dense_fwd(const float* x, const float* w, const float* b, float* y, long N, long In, long Out);
+void dense_bwd(const float* x, const float* w, const float* dy, float* dx, float* dw, float* db, long N, long In,
+               long Out);
+void bn_fwd(const float* x, float* y, long N, long C, long HW, const float* g, const float* b, float eps, bool train,
+            float* rmean, float* rvar, float momentum, float* smean, float* sistd);
+void bn_bwd(const float* x, const float* dy, const float* mean, const float* istd, const float* g, float* dx,
+            float* dg, float* db, long N, long C, long HW, bool train);
+void maxpool_fwd(const float* x, float* y, int32_t* idx, const PoolShape& p);
+void maxpool_bwd(const float* dy, const int32_t* idx, float* dx, const PoolShape& p);
+void avgpool_fwd(const float* x, float* y, const PoolShape& p);
+void avgpool_bwd(const float* dy, float* dx, const PoolShape& p);
+void act_fwd(int kind, const float* x, float* y, long n, float alpha);
+void act_bwd(int kind, const float* x, const float* dy, float* dx, long n, float alpha);
+double softmax_ce(const float* pred, const int64_t* labels, float* grad, long N, long C, long* correct);
+void adam(float* p, const float* g, float* m, float* v, long n, float lr, float b1, float b2, float eps, float bc1,
+          float bc2, float wd, bool decoupled);
+void sgd(float* p, const float* g, float* vel, long n, float lr, float momentum);
+}  // namespace cpu_ops
+
+namespace gpu_ops {
+// fp32 NCHW network input -> bf16 NHWC activation
+void input_to_nhwc(const float* x, void* y, int N, int C, int HW);
+// bf16 [N][HW][C] <-> [N][C][HW] (Flatten keeps the NCHW feature order of the reference)
+void nhwc_to_nchw(const void* x, void* y, int N, int HW, int C);
+void nchw_to_nhwc_bf16(const void* x, void* y, int N, int HW, int C);
+void cast_bf16(const float* x, void* y, long n);
+void zero(void* p, long nbytes);
+// w: bf16 [Co][KH][KW][C]; bias fp32 or null
+void conv_fwd(const void* x, const void* w, const float* bias, void* y, const ConvShape& s);
+void conv_dgrad(const void* dy, const void* w, void* dx, const ConvShape& s);
+// gw fp32 [Co][KH][KW][C] and gb fp32 [Co] accumulate (+=); gb may be null
+void conv_wgrad(const void* dy, const void* x, float* gw, float* gb, const ConvShape& s);
+// w: bf16 [Out][In]
+void dense_fwd(const void* x, const void* w, const float* bias, void* y, int N, int In, int Out);
+void dense_dgrad(const void* dy, const void* w, void* dx, int N, int In, int Out);
+void dense_wgrad(const void* dy, const void* x, float* gw, float* gb, int N, int In, int Out);
+// training: batch statistics (saved mean / istd, running stats updated); eval: running stats
+void bn_fwd(const void* x, void* y, long R, int C, const float* g, const float* b, float eps, bool train,
+            float* rmean, float* rvar, float momentum, float* smean, float* sistd);
+void bn_bwd(const void* dy, const void* x, void* dx, long R, int C, const float* mean, const float* istd,
+            const float* g, float* dg, float* db, bool train);
+void maxpool_fwd(const void* x, void* y, uint8_t* idx, const PoolShape& p);
+void maxpool_bwd(const void* dy, const uint8_t* idx, void* dx, const PoolShape& p);
+void avgpool_fwd(const void* x, void* y, const PoolShape& p);
+void avgpool_bwd(const void* dy, void* dx, const PoolShape& p);
+void act_fwd(int kind, const void* x, void* y, long n, float alpha);
+void act_bwd(int kind, const void* x, const void* dy, void* dx, long n, float alpha);
+// pred / grad bf16 [N][C]; returns the mean loss, correct count in *correct
+double softmax_ce(const void* pred, const int64_t* labels, void* grad, int N, int C, long* correct);
+void adam(float* p, const float* g, float* m, float* v, void* shadow, long n, float lr, float b1, float b2, float eps,
+          float bc1, float bc2, float wd, bool decoupled);
+void sgd(float* p, const float* g, float* vel, void* shadow, long n, float lr, float momentum);
+}  // namespace gpu_ops
+
+}  // namespace dcnn

@@ -1,0 +1,118 @@
+// Tensor of the C++ host API: logical shape + layout + dtype + device, shared storage.
+//
+// CPU tensors are fp32 NCHW (the reference's CPU form). GPU activations are bf16 NHWC — the
+// layout the MFMA kernels read — and GPU parameters fp32 masters with bf16 operand shadows (see
+// nn.hpp). Storage is shared (copies of a Tensor alias it); `ensure` is the reference's grow-only
+// reallocation; `save` / `load` are the reference's .bin tensor format (uint64 shape[4] + fp32
+// data in logical NCHW order), shared with the Python front end (nn/sequential.py).
+// Reference parity: include/tensor/tensor.hpp:53-654 (to_device :424, resize :478, ensure :511,
+// save/load :625), include/device/device_ptr.hpp:80-285.
+#pragma once
+#include <cstdint>
+#include <cstring>
+#include <iosfwd>
+#include <memory>
+#include <string>
+#include <vector>
+
+#include "layout.hpp"
+
+namespace dcnn {
+
+enum class DeviceType { CPU, GPU };
+
+struct Device {
+  DeviceType type = DeviceType::CPU;
+  int index = 0;
+  static Device cpu() { return {DeviceType::CPU, 0}; }
+  static Device gpu(int i = 0) { return {DeviceType::GPU, i}; }
+  static Device parse(const std::string& s);  // "CPU", "GPU", "GPU:1"
+  bool is_gpu() const { return type == DeviceType::GPU; }
+  std::string str() const;
+  bool operator==(const Device& o) const { return type == o.type && index == o.index; }
+  bool operator!=(const Device& o) const { return !(*this == o); }
+};
+
+enum class DType { F32, BF16, I32, I64, U8 };
+size_t dtype_size(DType t);
+const char* dtype_name(DType t);
+
+// host bf16 <-> fp32 (round to nearest even)
+uint16_t f32_to_bf16(float f);
+float bf16_to_f32(uint16_t b);
+
+// device memory entry points (implemented by the GPU backend, ops_gpu.hip)
+namespace gpu {
+int device_count();
+void set_device(int dev);
+void* alloc(size_t nbytes);
+void free(void* p);
+void copy(void* dst, const void* src, size_t nbytes, int kind);  // 0 h2d, 1 d2h, 2 d2d
+void synchronize();
+}  // namespace gpu
+
+class Storage {
+ public:
+  Storage(Device d, size_t nbytes);
+  ~Storage();
+  Storage(const Storage&) = delete;
+  Storage& operator=(const Storage&) = delete;
+  void* data() const { return p_; }
+  size_t nbytes() const { return n_; }
+  Device device() const { return dev_; }
+
+ private:
+  Device dev_;
+  void* p_ = nullptr;
+  size_t n_ = 0;
+};
+
+class Tensor {
+ public:
+  Tensor() = default;
+  static Tensor empty(const std::vector<int64_t>& shape, DType dt, Device dev, Layout layout = Layout::NCHW);
+  static Tensor zeros(const std::vector<int64_t>& shape, DType dt, Device dev, Layout layout = Layout::NCHW);
+  // fp32 host values in LOGICAL (row-major NCHW) order -> tensor of the given dtype / device / layout
+  static Tensor from_host(const std::vector<float>& v, const std::vector<int64_t>& shape, Device dev,
+                          DType dt = DType::F32, Layout layout = Layout::NCHW);
+  static Tensor from_host_i64(const std::vector<int64_t>& v, Device dev);
+
+  bool defined() const { return (bool)st_; }
+  const std::vector<int64_t>& shape() const { return shape_; }
+  int64_t dim(int k) const { return shape_.at(k); }
+  int rank() const { return (int)shape_.size(); }
+  int64_t numel() const;
+  size_t nbytes() const { return (size_t)numel() * dtype_size(dt_); }
+  DType dtype() const { return dt_; }
+  Device device() const { return st_ ? st_->device() : Device::cpu(); }
+  Layout layout() const { return layout_; }
+  void* data() const { return st_ ? st_->data() : nullptr; }
+  template <typename T>
+  T* ptr() const { return static_cast<T*>(data()); }
+
+  // same storage, new logical shape / layout (element count must match)
+  Tensor view(const std::vector<int64_t>& shape, Layout layout = Layout::NCHW) const;
+  // grow-only: reallocate only when the new shape needs more bytes than the storage holds
+  void ensure(const std::vector<int64_t>& shape, DType dt, Device dev, Layout layout = Layout::NCHW);
+  Tensor clone() const;
+  // copy to another device (same dtype / layout)
+  Tensor to(Device dev) const;
+  // fp32 values in LOGICAL row-major (NCHW) order, from any dtype / layout / device
+  std::vector<float> to_host_f32() const;
+  std::vector<int64_t> to_host_i64() const;
+  void zero_();
+
+  // reference .bin tensor record
+  void save(std::ostream& os) const;
+  static Tensor load(std::istream& is, Device dev = Device::cpu());
+
+ private:
+  std::shared_ptr<Storage> st_;
+  std::vector<int64_t> shape_;
+  DType dt_ = DType::F32;
+  Layout layout_ = Layout::NCHW;
+};
+
+std::string shape_str(const std::vector<int64_t>& s);
+
+}  // namespace dcnn

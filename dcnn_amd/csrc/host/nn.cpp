@@ -1,0 +1,838 @@
+// Layers, Sequential, loss, optimizers and the training loop of the C++ host API (dcnn/nn.hpp).
+#include "dcnn/nn.hpp"
+
+#include <algorithm>
+#include <chrono>
+#include <cmath>
+#include <cstdio>
+#include <filesystem>
+#include <fstream>
+#include <iostream>
+#include <sstream>
+#include <stdexcept>
+
+namespace dcnn {
+
+namespace {
+// splitmix64 stream: deterministic initialisation independent of the platform RNG
+struct Rng {
+  uint64_t s;
+  explicit Rng(uint64_t seed) : s(seed * 0x9e3779b97f4a7c15ull + 0x632be59bd9b4e019ull) {}
+  uint64_t next() {
+    uint64_t z = (s += 0x9e3779b97f4a7c15ull);
+    z = (z ^ (z >> 30)) * 0xbf58476d1ce4e5b9ull;
+    z = (z ^ (z >> 27)) * 0x94d049bb133111ebull;
+    return z ^ (z >> 31);
+  }
+  float uniform() { return (float)((next() >> 40) * (1.0 / 16777216.0)); }  // [0, 1)
+  float normal() {
+    const float u1 = std::max(uniform(), 1e-7f), u2 = uniform();
+    return std::sqrt(-2.f * std::log(u1)) * std::cos(6.2831853f * u2);
+  }
+};
+
+std::vector<float> uniform_init(size_t n, float bound, uint64_t seed) {
+  Rng r(seed);
+  std::vector<float> v(n);
+  for (auto& x : v) x = (2.f * r.uniform() - 1.f) * bound;
+  return v;
+}
+
+// activations: CPU fp32 NCHW, GPU bf16 NHWC
+Tensor act_empty(const std::vector<int64_t>& shape, Device dev) {
+  return dev.is_gpu() ? Tensor::empty(shape, DType::BF16, dev, Layout::NHWC) : Tensor::empty(shape, DType::F32, dev);
+}
+
+void check_act(const Tensor& x, Device dev, const char* who) {
+  if (x.device() != dev) throw std::runtime_error(std::string(who) + ": input on " + x.device().str() +
+                                                  ", layer on " + dev.str());
+  if (x.rank() != 4) throw std::runtime_error(std::string(who) + ": expected an (N, C, H, W) tensor");
+}
+
+int act_code(const std::string& k) {
+  if (k == "relu") return ACT_RELU;
+  if (k == "leaky_relu") return ACT_LEAKY_RELU;
+  if (k == "elu") return ACT_ELU;
+  if (k == "sigmoid") return ACT_SIGMOID;
+  if (k == "tanh") return ACT_TANH;
+  if (k == "linear") return ACT_LINEAR;
+  throw std::invalid_argument("unknown activation '" + k + "'");
+}
+}  // namespace
+
+// ------------------------------------------------------------------ Layer
+Param& Layer::add_param(const std::string& n, const std::vector<int64_t>& shape, Layout phys,
+                        const std::vector<float>& init) {
+  Param p;
+  p.name = n;
+  p.shape = shape;
+  p.layout = phys;
+  p.value = Tensor::from_host(init, shape, dev_, DType::F32, phys);
+  p.grad = Tensor::zeros(shape, DType::F32, dev_, phys);
+  if (dev_.is_gpu()) {
+    p.shadow = Tensor::empty(shape, DType::BF16, dev_, phys);
+    gpu_ops::cast_bf16(p.value.ptr<float>(), p.shadow.data(), p.value.numel());
+  }
+  params_.push_back(std::move(p));
+  return params_.back();
+}
+
+void Layer::sync_shadow() {
+  for (auto& p : params_)
+    if (p.shadow.defined()) gpu_ops::cast_bf16(p.value.ptr<float>(), p.shadow.data(), p.value.numel());
+}
+
+// ------------------------------------------------------------------ Conv2D
+Conv2D::Conv2D(int in_ch, int out_ch, int kh, int kw, int sh, int sw, int ph, int pw, bool bias, std::string name)
+    : Layer(std::move(name)), ci_(in_ch), co_(out_ch), kh_(kh), kw_(kw), sh_(sh), sw_(sw), ph_(ph), pw_(pw),
+      bias_(bias) {}
+
+json::Value Conv2D::parameters_config() const {
+  json::Value p = json::Value::object();
+  p["in_channels"] = ci_;
+  p["out_channels"] = co_;
+  p["kernel_h"] = kh_;
+  p["kernel_w"] = kw_;
+  p["stride_h"] = sh_;
+  p["stride_w"] = sw_;
+  p["pad_h"] = ph_;
+  p["pad_w"] = pw_;
+  p["use_bias"] = bias_;
+  p["optimized"] = "mfma";
+  return p;
+}
+
+ConvShape Conv2D::shape_for(const std::vector<int64_t>& in) const {
+  ConvShape s{};
+  s.N = (int)in[0];
+  s.C = (int)in[1];
+  s.H = (int)in[2];
+  s.W = (int)in[3];
+  s.Co = co_;
+  s.KH = kh_;
+  s.KW = kw_;
+  s.SH = sh_;
+  s.SW = sw_;
+  s.PH = ph_;
+  s.PW = pw_;
+  s.OH = (s.H + 2 * ph_ - kh_) / sh_ + 1;
+  s.OW = (s.W + 2 * pw_ - kw_) / sw_ + 1;
+  if (s.C != ci_) throw std::runtime_error(name_ + ": input has " + std::to_string(s.C) + " channels, expected " +
+                                           std::to_string(ci_));
+  return s;
+}
+
+std::vector<int64_t> Conv2D::output_shape(const std::vector<int64_t>& in) const {
+  const ConvShape s = shape_for(in);
+  return {in[0], co_, s.OH, s.OW};
+}
+
+void Conv2D::build(const std::vector<int64_t>& in, Device dev, uint64_t seed) {
+  (void)in;
+  dev_ = dev;
+  params_.clear();
+  const float bound = 1.f / std::sqrt((float)(ci_ * kh_ * kw_));
+  // GPU: physical [Co][KH][KW][Ci] (the GEMM B operand); CPU: NCHW
+  const Layout wl = dev.is_gpu() ? Layout::NHWC : Layout::NCHW;
+  add_param("weights", {co_, ci_, kh_, kw_}, wl, uniform_init((size_t)co_ * ci_ * kh_ * kw_, bound, seed));
+  if (bias_) add_param("bias", {co_, 1, 1, 1}, Layout::NCHW, uniform_init((size_t)co_, bound, seed + 1));
+}
+
+Tensor Conv2D::forward(const Tensor& x, bool training) {
+  (void)training;
+  check_act(x, dev_, "conv2d");
+  const ConvShape s = shape_for(x.shape());
+  Tensor y = act_empty({s.N, s.Co, s.OH, s.OW}, dev_);
+  const float* b = bias_ ? params_[1].value.ptr<float>() : nullptr;
+  if (dev_.is_gpu())
+    gpu_ops::conv_fwd(x.data(), params_[0].shadow.data(), b, y.data(), s);
+  else
+    cpu_ops::conv_fwd(x.ptr<float>(), params_[0].value.ptr<float>(), b, y.ptr<float>(), s);
+  x_ = x;
+  return y;
+}
+
+Tensor Conv2D::backward(const Tensor& dy) {
+  const ConvShape s = shape_for(x_.shape());
+  Tensor dx = act_empty(x_.shape(), dev_);
+  float* gb = bias_ ? params_[1].grad.ptr<float>() : nullptr;
+  if (dev_.is_gpu()) {
+    gpu_ops::conv_wgrad(dy.data(), x_.data(), params_[0].grad.ptr<float>(), gb, s);
+    gpu_ops::conv_dgrad(dy.data(), params_[0].shadow.data(), dx.data(), s);
+  } else {
+    cpu_ops::conv_bwd(x_.ptr<float>(), params_[0].value.ptr<float>(), dy.ptr<float>(), dx.ptr<float>(),
+                      params_[0].grad.ptr<float>(), gb, s);
+  }
+  return dx;
+}
+
+// ------------------------------------------------------------------ Dense
+Dense::Dense(int in_features, int out_features, bool bias, std::string name)
+    : Layer(std::move(name)), in_(in_features), out_(out_features), bias_(bias) {}
+
+json::Value Dense::parameters_config() const {
+  json::Value p = json::Value::object();
+  p["input_features"] = in_;
+  p["output_features"] = out_;
+  p["use_bias"] = bias_;
+  p["optimized"] = "mfma";
+  return p;
+}
+
+std::vector<int64_t> Dense::output_shape(const std::vector<int64_t>& in) const {
+  if (in[1] * in[2] * in[3] != in_)
+    throw std::runtime_error(name_ + ": " + std::to_string(in[1] * in[2] * in[3]) + " input features, expected " +
+                             std::to_string(in_));
+  return {in[0], out_, 1, 1};
+}
+
+void Dense::build(const std::vector<int64_t>& in, Device dev, uint64_t seed) {
+  (void)in;
+  dev_ = dev;
+  params_.clear();
+  const float bound = 1.f / std::sqrt((float)in_);
+  add_param("weights", {out_, in_, 1, 1}, Layout::NCHW, uniform_init((size_t)out_ * in_, bound, seed));
+  if (bias_) add_param("bias", {out_, 1, 1, 1}, Layout::NCHW, uniform_init((size_t)out_, bound, seed + 1));
+}
+
+Tensor Dense::forward(const Tensor& x, bool training) {
+  (void)training;
+  check_act(x, dev_, "dense");
+  const int N = (int)x.dim(0);
+  output_shape(x.shape());
+  Tensor y = act_empty({N, out_, 1, 1}, dev_);
+  const float* b = bias_ ? params_[1].value.ptr<float>() : nullptr;
+  if (dev_.is_gpu())
+    gpu_ops::dense_fwd(x.data(), params_[0].shadow.data(), b, y.data(), N, in_, out_);
+  else
+    cpu_ops::dense_fwd(x.ptr<float>(), params_[0].value.ptr<float>(), b, y.ptr<float>(), N, in_, out_);
+  x_ = x;
+  return y;
+}
+
+Tensor Dense::backward(const Tensor& dy) {
+  const int N = (int)x_.dim(0);
+  Tensor dx = act_empty(x_.shape(), dev_);
+  float* gb = bias_ ? params_[1].grad.ptr<float>() : nullptr;
+  if (dev_.is_gpu()) {
+    gpu_ops::dense_wgrad(dy.data(), x_.data(), params_[0].grad.ptr<float>(), gb, N, in_, out_);
+    gpu_ops::dense_dgrad(dy.data(), params_[0].shadow.data(), dx.data(), N, in_, out_);
+  } else {
+    cpu_ops::dense_bwd(x_.ptr<float>(), params_[0].value.ptr<float>(), dy.ptr<float>(), dx.ptr<float>(),
+                       params_[0].grad.ptr<float>(), gb, N, in_, out_);
+  }
+  return dx;
+}
+
+// ------------------------------------------------------------------ BatchNorm
+BatchNorm::BatchNorm(int num_features, float eps, float momentum, bool affine, std::string name)
+    : Layer(std::move(name)), c_(num_features), eps_(eps), momentum_(momentum), affine_(affine) {}
+
+json::Value BatchNorm::parameters_config() const {
+  json::Value p = json::Value::object();
+  p["num_features"] = c_;
+  p["epsilon"] = (double)eps_;
+  p["momentum"] = (double)momentum_;
+  p["affine"] = affine_;
+  return p;
+}
+
+void BatchNorm::build(const std::vector<int64_t>& in, Device dev, uint64_t seed) {
+  (void)in;
+  (void)seed;
+  dev_ = dev;
+  params_.clear();
+  if (affine_) {
+    add_param("gamma", {c_, 1, 1, 1}, Layout::NCHW, std::vector<float>((size_t)c_, 1.f));
+    add_param("beta", {c_, 1, 1, 1}, Layout::NCHW, std::vector<float>((size_t)c_, 0.f));
+  }
+  running_mean = Tensor::zeros({c_}, DType::F32, dev);
+  running_var = Tensor::from_host(std::vector<float>((size_t)c_, 1.f), {c_}, dev);
+  mean_ = Tensor::zeros({c_}, DType::F32, dev);
+  istd_ = Tensor::zeros({c_}, DType::F32, dev);
+}
+
+Tensor BatchNorm::forward(const Tensor& x, bool training) {
+  check_act(x, dev_, "batchnorm");
+  if (x.dim(1) != c_) throw std::runtime_error(name_ + ": channel count mismatch");
+  train_ = training;
+  const long N = x.dim(0), HW = x.dim(2) * x.dim(3);
+  Tensor y = act_empty(x.shape(), dev_);
+  const float* g = affine_ ? params_[0].value.ptr<float>() : nullptr;
+  const float* b = affine_ ? params_[1].value.ptr<float>() : nullptr;
+  if (dev_.is_gpu())
+    gpu_ops::bn_fwd(x.data(), y.data(), N * HW, c_, g, b, eps_, training, running_mean.ptr<float>(),
+                    running_var.ptr<float>(), momentum_, mean_.ptr<float>(), istd_.ptr<float>());
+  else
+    cpu_ops::bn_fwd(x.ptr<float>(), y.ptr<float>(), N, c_, HW, g, b, eps_, training, running_mean.ptr<float>(),
+                    running_var.ptr<float>(), momentum_, mean_.ptr<float>(), istd_.ptr<float>());
+  x_ = x;
+  return y;
+}
+
+Tensor BatchNorm::backward(const Tensor& dy) {
+  const long N = x_.dim(0), HW = x_.dim(2) * x_.dim(3);
+  Tensor dx = act_empty(x_.shape(), dev_);
+  const float* g = affine_ ? params_[0].value.ptr<float>() : nullptr;
+  float* dg = affine_ ? params_[0].grad.ptr<float>() : nullptr;
+  float* db = affine_ ? params_[1].grad.ptr<float>() : nullptr;
+  if (dev_.is_gpu())
+    gpu_ops::bn_bwd(dy.data(), x_.data(), dx.data(), N * HW, c_, mean_.ptr<float>(), istd_.ptr<float>(), g, dg, db,
+                    train_);
+  else
+    cpu_ops::bn_bwd(x_.ptr<float>(), dy.ptr<float>(), mean_.ptr<float>(), istd_.ptr<float>(), g, dx.ptr<float>(), dg,
+                    db, N, c_, HW, train_);
+  return dx;
+}
+
+// ------------------------------------------------------------------ Activation
+Activation::Activation(std::string kind, std::string name)
+    : Layer(std::move(name)), kind_(std::move(kind)), code_(act_code(kind_)) {}
+
+json::Value Activation::parameters_config() const {
+  json::Value p = json::Value::object();
+  p["activation"] = kind_;
+  return p;
+}
+
+Tensor Activation::forward(const Tensor& x, bool training) {
+  (void)training;
+  check_act(x, dev_, "activation");
+  Tensor y = act_empty(x.shape(), dev_);
+  if (dev_.is_gpu())
+    gpu_ops::act_fwd(code_, x.data(), y.data(), x.numel(), 0.01f);
+  else
+    cpu_ops::act_fwd(code_, x.ptr<float>(), y.ptr<float>(), x.numel(), 0.01f);
+  x_ = x;
+  return y;
+}
+
+Tensor Activation::backward(const Tensor& dy) {
+  Tensor dx = act_empty(x_.shape(), dev_);
+  if (dev_.is_gpu())
+    gpu_ops::act_bwd(code_, x_.data(), dy.data(), dx.data(), x_.numel(), 0.01f);
+  else
+    cpu_ops::act_bwd(code_, x_.ptr<float>(), dy.ptr<float>(), dx.ptr<float>(), x_.numel(), 0.01f);
+  return dx;
+}
+
+// ------------------------------------------------------------------ pooling
+Pool2D::Pool2D(bool max, int kh, int kw, int sh, int sw, int ph, int pw, std::string name)
+    : Layer(std::move(name)), max_(max), kh_(kh), kw_(kw), sh_(sh > 0 ? sh : kh), sw_(sw > 0 ? sw : kw), ph_(ph),
+      pw_(pw) {}
+
+json::Value Pool2D::parameters_config() const {
+  json::Value p = json::Value::object();
+  p["pool_h"] = kh_;
+  p["pool_w"] = kw_;
+  p["stride_h"] = sh_;
+  p["stride_w"] = sw_;
+  p["pad_h"] = ph_;
+  p["pad_w"] = pw_;
+  return p;
+}
+
+PoolShape Pool2D::shape_for(const std::vector<int64_t>& in) const {
+  PoolShape p{};
+  p.N = (int)in[0];
+  p.C = (int)in[1];
+  p.H = (int)in[2];
+  p.W = (int)in[3];
+  p.KH = kh_;
+  p.KW = kw_;
+  p.SH = sh_;
+  p.SW = sw_;
+  p.PH = ph_;
+  p.PW = pw_;
+  p.OH = (p.H + 2 * ph_ - kh_) / sh_ + 1;
+  p.OW = (p.W + 2 * pw_ - kw_) / sw_ + 1;
+  return p;
+}
+
+std::vector<int64_t> Pool2D::output_shape(const std::vector<int64_t>& in) const {
+  const PoolShape p = shape_for(in);
+  return {in[0], in[1], p.OH, p.OW};
+}
+
+Tensor Pool2D::forward(const Tensor& x, bool training) {
+  (void)training;
+  check_act(x, dev_, "pool2d");
+  const PoolShape p = shape_for(x.shape());
+  Tensor y = act_empty({p.N, p.C, p.OH, p.OW}, dev_);
+  in_shape_ = x.shape();
+  if (max_) {
+    const int64_t n = (int64_t)p.N * p.C * p.OH * p.OW;
+    if (dev_.is_gpu()) {
+      idx_.ensure({n}, DType::U8, dev_);
+      gpu_ops::maxpool_fwd(x.data(), y.data(), idx_.ptr<uint8_t>(), p);
+    } else {
+      idx_.ensure({n}, DType::I32, dev_);
+      cpu_ops::maxpool_fwd(x.ptr<float>(), y.ptr<float>(), idx_.ptr<int32_t>(), p);
+    }
+  } else if (dev_.is_gpu()) {
+    gpu_ops::avgpool_fwd(x.data(), y.data(), p);
+  } else {
+    cpu_ops::avgpool_fwd(x.ptr<float>(), y.ptr<float>(), p);
+  }
+  return y;
+}
+
+Tensor Pool2D::backward(const Tensor& dy) {
+  const PoolShape p = shape_for(in_shape_);
+  Tensor dx = act_empty(in_shape_, dev_);
+  if (max_) {
+    if (dev_.is_gpu())
+      gpu_ops::maxpool_bwd(dy.data(), idx_.ptr<uint8_t>(), dx.data(), p);
+    else
+      cpu_ops::maxpool_bwd(dy.ptr<float>(), idx_.ptr<int32_t>(), dx.ptr<float>(), p);
+  } else if (dev_.is_gpu()) {
+    gpu_ops::avgpool_bwd(dy.data(), dx.data(), p);
+  } else {
+    cpu_ops::avgpool_bwd(dy.ptr<float>(), dx.ptr<float>(), p);
+  }
+  return dx;
+}
+
+// ------------------------------------------------------------------ Flatten
+std::vector<int64_t> Flatten::output_shape(const std::vector<int64_t>& in) const {
+  return {in[0], in[1] * in[2] * in[3], 1, 1};
+}
+
+Tensor Flatten::forward(const Tensor& x, bool training) {
+  (void)training;
+  check_act(x, dev_, "flatten");
+  in_shape_ = x.shape();
+  const auto os = output_shape(x.shape());
+  const int64_t HW = x.dim(2) * x.dim(3);
+  if (!dev_.is_gpu()) return x.view(os);            // NCHW: already in feature order
+  if (HW == 1) return x.view(os, Layout::NHWC);     // nothing to reorder
+  Tensor y = act_empty(os, dev_);
+  gpu_ops::nhwc_to_nchw(x.data(), y.data(), (int)x.dim(0), (int)HW, (int)x.dim(1));  // NCHW feature order
+  return y;
+}
+
+Tensor Flatten::backward(const Tensor& dy) {
+  const int64_t HW = in_shape_[2] * in_shape_[3];
+  if (!dev_.is_gpu()) return dy.view(in_shape_);
+  if (HW == 1) return dy.view(in_shape_, Layout::NHWC);
+  Tensor dx = act_empty(in_shape_, dev_);
+  gpu_ops::nchw_to_nhwc_bf16(dy.data(), dx.data(), (int)in_shape_[0], (int)HW, (int)in_shape_[1]);
+  return dx;
+}
+
+// ------------------------------------------------------------------ factory
+std::unique_ptr<Layer> create_layer(const json::Value& rec) {
+  const std::string type = rec.get_string("type", "");
+  const std::string name = rec.get_string("name", type);
+  static const json::Value empty = json::Value::object();
+  const json::Value& p = rec.has("parameters") ? rec.at("parameters") : empty;
+  auto I = [&](const char* k, int64_t d) { return (int)p.get_int(k, d); };
+  if (type == "conv2d")
+    return std::make_unique<Conv2D>(I("in_channels", 0), I("out_channels", 0), I("kernel_h", 1), I("kernel_w", 1),
+                                    I("stride_h", 1), I("stride_w", 1), I("pad_h", 0), I("pad_w", 0),
+                                    p.get_bool("use_bias", true), name);
+  if (type == "dense")
+    return std::make_unique<Dense>(I("input_features", 0), I("output_features", 0), p.get_bool("use_bias", true),
+                                   name);
+  if (type == "batchnorm")
+    return std::make_unique<BatchNorm>(I("num_features", 0), (float)p.get_number("epsilon", 1e-5),
+                                       (float)p.get_number("momentum", 0.1), p.get_bool("affine", true), name);
+  if (type == "activation") return std::make_unique<Activation>(p.get_string("activation", "relu"), name);
+  if (type == "maxpool2d" || type == "avgpool2d")
+    return std::make_unique<Pool2D>(type == "maxpool2d", I("pool_h", 2), I("pool_w", 2), I("stride_h", 0),
+                                    I("stride_w", 0), I("pad_h", 0), I("pad_w", 0), name);
+  if (type == "flatten") return std::make_unique<Flatten>(name);
+  throw std::invalid_argument("C++ host API: unsupported layer type '" + type + "'");
+}
+
+// ------------------------------------------------------------------ Sequential
+void Sequential::set_device(Device d) {
+  if (d.is_gpu() && gpu::device_count() <= d.index) throw std::runtime_error(d.str() + " not available");
+  if (initialized_ && d != dev_) {
+    // move: rebuild on the new device with the current values
+    std::vector<std::vector<float>> vals;
+    for (auto* p : parameters()) vals.push_back(p->value.to_host_f32());
+    dev_ = d;
+    initialized_ = false;
+    initialize(0);
+    size_t i = 0;
+    for (auto* p : parameters()) p->value = Tensor::from_host(vals[i++], p->shape, dev_, DType::F32, p->layout);
+    for (auto& l : layers_) l->sync_shadow();
+    return;
+  }
+  dev_ = d;
+}
+
+void Sequential::initialize(uint64_t seed) {
+  if (input_chw_.empty()) {
+    // infer the input channels from the first parameterised layer (spatial size is not needed to
+    // create parameters)
+    input_chw_ = {0, 0, 0};
+  }
+  std::vector<int64_t> shape{1, input_chw_[0], input_chw_[1], input_chw_[2]};
+  uint64_t k = 0;
+  for (auto& l : layers_) {
+    l->build(shape, dev_, seed * 1000003ull + (k++) * 7919ull);
+    if (shape[1] > 0 && shape[2] > 0) shape = l->output_shape(shape);
+  }
+  initialized_ = true;
+}
+
+std::vector<Param*> Sequential::parameters() {
+  std::vector<Param*> out;
+  for (auto& l : layers_)
+    for (auto& p : l->params()) out.push_back(&p);
+  return out;
+}
+
+size_t Sequential::num_parameters() {
+  size_t n = 0;
+  for (auto* p : parameters()) n += (size_t)p->value.numel();
+  return n;
+}
+
+void Sequential::zero_grad() {
+  for (auto* p : parameters()) {
+    if (dev_.is_gpu())
+      gpu_ops::zero(p->grad.data(), (long)p->grad.nbytes());
+    else
+      p->grad.zero_();
+  }
+}
+
+Tensor Sequential::forward(const Tensor& x_in) {
+  if (!initialized_) throw std::runtime_error("Sequential::forward before initialize()");
+  if (x_in.rank() != 4 || x_in.dtype() != DType::F32) throw std::runtime_error("forward: expected fp32 (N, C, H, W)");
+  Tensor x = x_in.device() == dev_ ? x_in : x_in.to(dev_);
+  if (dev_.is_gpu()) {
+    Tensor a = Tensor::empty(x.shape(), DType::BF16, dev_, Layout::NHWC);
+    gpu_ops::input_to_nhwc(x.ptr<float>(), a.data(), (int)x.dim(0), (int)x.dim(1), (int)(x.dim(2) * x.dim(3)));
+    x = a;
+  }
+  for (auto& l : layers_) x = l->forward(x, training_);
+  return x.view({x.dim(0), x.dim(1) * x.dim(2) * x.dim(3)}, x.layout());
+}
+
+void Sequential::backward(const Tensor& dlogits) {
+  Tensor g = dlogits.view({dlogits.dim(0), dlogits.dim(1), 1, 1}, dev_.is_gpu() ? Layout::NHWC : Layout::NCHW);
+  for (size_t i = layers_.size(); i-- > 0;) g = layers_[i]->backward(g);
+}
+
+json::Value Sequential::get_config() const {
+  json::Value c = json::Value::object();
+  c["name"] = name_;
+  c["is_training"] = training_;
+  json::Value ls = json::Value::array();
+  for (auto& l : layers_) {
+    json::Value r = json::Value::object();
+    r["type"] = l->type();
+    r["name"] = l->name();
+    r["parameters"] = l->parameters_config();
+    ls.push(std::move(r));
+  }
+  c["layers"] = std::move(ls);
+  if (!input_chw_.empty() && input_chw_[0] > 0) {
+    json::Value in = json::Value::array();
+    for (auto v : input_chw_) in.push(v);
+    c["input_shape"] = std::move(in);
+  }
+  return c;
+}
+
+void Sequential::print_config() const { std::cout << get_config().dump(2) << std::endl; }
+
+Sequential Sequential::load_from_config(const json::Value& cfg) {
+  Sequential m(cfg.get_string("name", "sequential"));
+  for (auto& r : cfg.at("layers").items()) m.add(create_layer(r));
+  m.set_training(cfg.get_bool("is_training", true));
+  if (const json::Value* in = cfg.find("input_shape")) {
+    std::vector<int64_t> chw;
+    for (auto& v : in->items()) chw.push_back(v.as_int());
+    m.set_input_shape(chw);
+  }
+  return m;
+}
+
+void Sequential::save_to_file(const std::string& path) const {
+  const std::filesystem::path dir = std::filesystem::path(path).parent_path();
+  if (!dir.empty()) std::filesystem::create_directories(dir);
+  {
+    std::ofstream f(path + ".json");
+    if (!f) throw std::runtime_error("cannot write " + path + ".json");
+    f << get_config().dump(4);
+  }
+  std::ofstream f(path + ".bin", std::ios::binary);
+  if (!f) throw std::runtime_error("cannot write " + path + ".bin");
+  for (auto& l : layers_)
+    for (auto& p : const_cast<Layer&>(*l).params()) p.value.view(p.shape, p.layout).save(f);
+  // BatchNorm running statistics: language-neutral sidecar of .bin records (running_mean,
+  // running_var per BatchNorm in layer order), read by both front ends
+  std::ofstream s(path + ".bnstats", std::ios::binary);
+  for (auto& l : layers_)
+    if (auto* bn = dynamic_cast<const BatchNorm*>(l.get())) {
+      const int64_t c = bn->running_mean.numel();
+      bn->running_mean.view({c, 1, 1, 1}).save(s);
+      bn->running_var.view({c, 1, 1, 1}).save(s);
+    }
+}
+
+void Sequential::load_bn_stats(const std::string& path) {
+  std::ifstream f(path, std::ios::binary);
+  if (!f) throw std::runtime_error("cannot read " + path);
+  for (auto& l : layers_)
+    if (auto* bn = dynamic_cast<BatchNorm*>(l.get())) {
+      const int64_t c = bn->running_mean.numel();
+      Tensor m = Tensor::load(f), v = Tensor::load(f);
+      if (m.numel() != c || v.numel() != c) throw std::runtime_error("bnstats: channel count mismatch");
+      bn->running_mean = Tensor::from_host(m.to_host_f32(), {c}, dev_);
+      bn->running_var = Tensor::from_host(v.to_host_f32(), {c}, dev_);
+    }
+}
+
+void Sequential::load_weights_file(const std::string& path) {
+  if (!initialized_) initialize(0);
+  std::ifstream f(path, std::ios::binary);
+  if (!f) throw std::runtime_error("cannot read " + path);
+  for (auto* p : parameters()) {
+    Tensor t = Tensor::load(f);
+    if (t.numel() != p->value.numel())
+      throw std::runtime_error("checkpoint tensor " + shape_str(t.shape()) + " does not match parameter " +
+                               shape_str(p->shape));
+    p->value = Tensor::from_host(t.to_host_f32(), p->shape, dev_, DType::F32, p->layout);
+  }
+  for (auto& l : layers_) l->sync_shadow();
+}
+
+Sequential Sequential::from_file(const std::string& path, Device dev) {
+  std::ifstream f(path + ".json");
+  if (!f) throw std::runtime_error("cannot read " + path + ".json");
+  std::stringstream ss;
+  ss << f.rdbuf();
+  Sequential m = load_from_config(json::Value::parse(ss.str()));
+  m.set_device(dev);
+  m.initialize(0);
+  m.load_weights_file(path + ".bin");
+  if (std::ifstream(path + ".bnstats").good()) m.load_bn_stats(path + ".bnstats");
+  return m;
+}
+
+// ------------------------------------------------------------------ builder
+std::string SequentialBuilder::auto_name(const std::string& given, const std::string& kind) {
+  ++count_;
+  return given.empty() ? kind + "_" + std::to_string(count_) : given;
+}
+
+SequentialBuilder& SequentialBuilder::input(const std::vector<int64_t>& chw) {
+  if (chw.size() != 3) throw std::invalid_argument("input: expected {C, H, W}");
+  cur_ = chw;
+  model_.set_input_shape(chw);
+  return *this;
+}
+
+SequentialBuilder& SequentialBuilder::conv2d(int out_ch, int kh, int kw, int sh, int sw, int ph, int pw, bool bias,
+                                             const std::string& name) {
+  if (cur_.empty()) throw std::logic_error("SequentialBuilder: call input() first");
+  auto l = std::make_unique<Conv2D>((int)cur_[0], out_ch, kh, kw, sh, sw, ph, pw, bias, auto_name(name, "conv2d"));
+  const auto o = l->output_shape({1, cur_[0], cur_[1], cur_[2]});
+  cur_ = {o[1], o[2], o[3]};
+  model_.add(std::move(l));
+  return *this;
+}
+
+SequentialBuilder& SequentialBuilder::batchnorm(float eps, float momentum, bool affine, const std::string& name) {
+  model_.add(std::make_unique<BatchNorm>((int)cur_.at(0), eps, momentum, affine, auto_name(name, "batchnorm")));
+  return *this;
+}
+
+SequentialBuilder& SequentialBuilder::activation(const std::string& kind, const std::string& name) {
+  model_.add(std::make_unique<Activation>(kind, auto_name(name, kind)));
+  return *this;
+}
+
+SequentialBuilder& SequentialBuilder::maxpool2d(int kh, int kw, int sh, int sw, int ph, int pw,
+                                                const std::string& name) {
+  auto l = std::make_unique<Pool2D>(true, kh, kw, sh, sw, ph, pw, auto_name(name, "maxpool2d"));
+  const auto o = l->output_shape({1, cur_.at(0), cur_[1], cur_[2]});
+  cur_ = {o[1], o[2], o[3]};
+  model_.add(std::move(l));
+  return *this;
+}
+
+SequentialBuilder& SequentialBuilder::avgpool2d(int kh, int kw, int sh, int sw, int ph, int pw,
+                                                const std::string& name) {
+  auto l = std::make_unique<Pool2D>(false, kh, kw, sh, sw, ph, pw, auto_name(name, "avgpool2d"));
+  const auto o = l->output_shape({1, cur_.at(0), cur_[1], cur_[2]});
+  cur_ = {o[1], o[2], o[3]};
+  model_.add(std::move(l));
+  return *this;
+}
+
+SequentialBuilder& SequentialBuilder::flatten(const std::string& name) {
+  model_.add(std::make_unique<Flatten>(auto_name(name, "flatten")));
+  cur_ = {cur_.at(0) * cur_[1] * cur_[2], 1, 1};
+  return *this;
+}
+
+SequentialBuilder& SequentialBuilder::dense(int out_features, bool bias, const std::string& name) {
+  const int in = (int)(cur_.at(0) * cur_[1] * cur_[2]);
+  model_.add(std::make_unique<Dense>(in, out_features, bias, auto_name(name, "dense")));
+  cur_ = {out_features, 1, 1};
+  return *this;
+}
+
+Sequential SequentialBuilder::build() { return std::move(model_); }
+
+// ------------------------------------------------------------------ loss
+LossResult softmax_cross_entropy(const Tensor& logits, const Tensor& labels_in) {
+  if (logits.rank() != 2) throw std::runtime_error("softmax_cross_entropy: expected [N, C] logits");
+  const int N = (int)logits.dim(0), C = (int)logits.dim(1);
+  const Device dev = logits.device();
+  Tensor labels = labels_in.device() == dev ? labels_in : labels_in.to(dev);
+  LossResult r;
+  if (dev.is_gpu()) {
+    r.grad = Tensor::empty({N, C}, DType::BF16, dev, Layout::NHWC);
+    r.loss = gpu_ops::softmax_ce(logits.data(), labels.ptr<int64_t>(), r.grad.data(), N, C, &r.correct);
+  } else {
+    r.grad = Tensor::empty({N, C}, DType::F32, dev);
+    r.loss = cpu_ops::softmax_ce(logits.ptr<float>(), labels.ptr<int64_t>(), r.grad.ptr<float>(), N, C, &r.correct);
+  }
+  return r;
+}
+
+// ------------------------------------------------------------------ optimizers
+void SGD::step(const std::vector<Param*>& params) {
+  for (auto* p : params) {
+    if (momentum_ != 0.f && !p->m.defined()) p->m = Tensor::zeros(p->value.shape(), DType::F32, p->value.device());
+    float* vel = momentum_ != 0.f ? p->m.ptr<float>() : nullptr;
+    if (p->value.device().is_gpu())
+      gpu_ops::sgd(p->value.ptr<float>(), p->grad.ptr<float>(), vel, p->shadow.data(), p->value.numel(), lr_,
+                   momentum_);
+    else
+      cpu_ops::sgd(p->value.ptr<float>(), p->grad.ptr<float>(), vel, p->value.numel(), lr_, momentum_);
+  }
+}
+
+void Adam::step(const std::vector<Param*>& params) {
+  ++t_;
+  const float bc1 = 1.f - std::pow(b1_, (float)t_), bc2 = 1.f - std::pow(b2_, (float)t_);
+  for (auto* p : params) {
+    if (!p->m.defined()) {
+      p->m = Tensor::zeros(p->value.shape(), DType::F32, p->value.device());
+      p->v = Tensor::zeros(p->value.shape(), DType::F32, p->value.device());
+    }
+    if (p->value.device().is_gpu())
+      gpu_ops::adam(p->value.ptr<float>(), p->grad.ptr<float>(), p->m.ptr<float>(), p->v.ptr<float>(),
+                    p->shadow.data(), p->value.numel(), lr_, b1_, b2_, eps_, bc1, bc2, wd_, decoupled_);
+    else
+      cpu_ops::adam(p->value.ptr<float>(), p->grad.ptr<float>(), p->m.ptr<float>(), p->v.ptr<float>(),
+                    p->value.numel(), lr_, b1_, b2_, eps_, bc1, bc2, wd_, decoupled_);
+  }
+}
+
+// ------------------------------------------------------------------ data
+SyntheticClassification::SyntheticClassification(size_t n, int c, int h, int w, int classes, uint64_t seed,
+                                                 float noise)
+    : n_(n), c_(c), h_(h), w_(w), classes_(classes), seed_(seed), noise_(noise) {
+  Rng r(seed ^ 0x5151u);
+  proto_.resize((size_t)classes * c * h * w);
+  for (auto& v : proto_) v = r.normal();
+  order_.resize(n);
+  for (size_t i = 0; i < n; ++i) order_[i] = i;
+}
+
+void SyntheticClassification::reset(uint64_t epoch) {
+  Rng r(seed_ + 977 * (epoch + 1));
+  for (size_t i = n_; i > 1; --i) std::swap(order_[i - 1], order_[(size_t)(r.next() % i)]);
+  pos_ = 0;
+}
+
+bool SyntheticClassification::next(int batch, Tensor& x, Tensor& labels) {
+  if (pos_ >= n_) return false;
+  const int b = (int)std::min<size_t>((size_t)batch, n_ - pos_);
+  const size_t per = (size_t)c_ * h_ * w_;
+  std::vector<float> xs((size_t)b * per);
+  std::vector<int64_t> ys((size_t)b);
+  for (int i = 0; i < b; ++i) {
+    const size_t idx = order_[pos_ + i];
+    Rng r(seed_ * 1315423911ull + idx);
+    const int cls = (int)(idx % (size_t)classes_);
+    ys[i] = cls;
+    const float* pr = proto_.data() + (size_t)cls * per;
+    for (size_t k = 0; k < per; ++k) xs[i * per + k] = pr[k] + noise_ * r.normal();
+  }
+  pos_ += (size_t)b;
+  x = Tensor::from_host(xs, {b, c_, h_, w_}, Device::cpu());
+  labels = Tensor::from_host_i64(ys, Device::cpu());
+  return true;
+}
+
+// ------------------------------------------------------------------ training loop
+LossResult train_step(Sequential& model, Optimizer& opt, const Tensor& x, const Tensor& labels) {
+  model.set_training(true);
+  model.zero_grad();
+  Tensor logits = model.forward(x);
+  LossResult r = softmax_cross_entropy(logits, labels);
+  model.backward(r.grad);
+  opt.step(model.parameters());
+  return r;
+}
+
+EpochStats evaluate(Sequential& model, DataSource& src, int batch_size) {
+  const bool was = model.is_training();
+  model.set_training(false);
+  src.reset(0);
+  Tensor x, y;
+  double loss = 0;
+  long correct = 0, seen = 0;
+  while (src.next(batch_size, x, y)) {
+    Tensor logits = model.forward(x);
+    LossResult r = softmax_cross_entropy(logits, y);
+    loss += r.loss * x.dim(0);
+    correct += r.correct;
+    seen += x.dim(0);
+  }
+  model.set_training(was);
+  EpochStats s;
+  s.val_loss = seen ? loss / seen : 0;
+  s.val_acc = seen ? (double)correct / seen : 0;
+  return s;
+}
+
+std::vector<EpochStats> train_classification_model(Sequential& model, DataSource& train, DataSource* val,
+                                                   Optimizer& opt, const TrainingConfig& cfg) {
+  std::vector<EpochStats> hist;
+  for (int e = 0; e < cfg.epochs; ++e) {
+    const auto t0 = std::chrono::steady_clock::now();
+    train.reset(cfg.seed + (uint64_t)e);
+    Tensor x, y;
+    double loss = 0;
+    long correct = 0, seen = 0;
+    int step = 0;
+    while ((cfg.max_steps < 0 || step < cfg.max_steps) && train.next(cfg.batch_size, x, y)) {
+      LossResult r = train_step(model, opt, x, y);
+      loss += r.loss * x.dim(0);
+      correct += r.correct;
+      seen += x.dim(0);
+      ++step;
+      if (cfg.progress_interval > 0 && step % cfg.progress_interval == 0)
+        std::printf("epoch %d step %d  loss %.4f  acc %.2f%%\n", e + 1, step, loss / seen, 100.0 * correct / seen);
+    }
+    EpochStats s;
+    s.train_loss = seen ? loss / seen : 0;
+    s.train_acc = seen ? (double)correct / seen : 0;
+    if (val) {
+      EpochStats v = evaluate(model, *val, cfg.batch_size);
+      s.val_loss = v.val_loss;
+      s.val_acc = v.val_acc;
+    }
+    if (model.device().is_gpu()) gpu::synchronize();
+    s.seconds = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+    std::printf("epoch %d/%d  train loss %.4f acc %.2f%%  val loss %.4f acc %.2f%%  (%.2f s)\n", e + 1, cfg.epochs,
+                s.train_loss, 100 * s.train_acc, s.val_loss, 100 * s.val_acc, s.seconds);
+    hist.push_back(s);
+    opt.set_learning_rate(opt.learning_rate() * cfg.lr_decay);
+  }
+  return hist;
+}
+
+}  // namespace dcnn

@@ -363,6 +363,159 @@ py::capsule alloc_dlpack(int dev, std::vector<int64_t> shape, int code, int bits
   });
 }
 
+// ------------------------------------------------------------------ ActArena
+// Per-step activation arena: every activation, statistics slab and split-K workspace of one
+// training step is bump-allocated from device chunks owned here (drawn from the native pool), and
+// the bump pointer is reset at the next step — no allocator call per tensor, identical addresses
+// every step (so a hipGraph captured from a step sees the same buffers eager steps use), and no
+// activation on PyTorch's caching allocator.
+//
+// Growth only on first use: a step that overruns the chunks appends a chunk (at least the current
+// capacity: doubling); the next reset() coalesces every chunk into one of the high-water size, so
+// from the second step on the arena neither grows nor allocates. Chunks are exported to PyTorch
+// once each (DLPack, shared ownership): a tensor that outlives its step keeps its chunk alive, and
+// the memory returns to the pool (Allocator::defer_free) only when the last view is gone.
+// Reference parity: include/nn/mem_pool.hpp:11-101, include/device/device_ptr.hpp:184-217
+// (grow-only ensure), include/tensor/tensor.hpp:424-511.
+struct ArenaChunk {
+  int dev = 0;
+  uintptr_t ptr = 0;
+  uint64_t nbytes = 0;
+  int64_t id = 0;
+  ~ArenaChunk() {
+    if (ptr) Allocator::get(dev).defer_free(ptr, nbytes);  // no HIP call: any thread, any time
+  }
+};
+
+struct ChunkExport {
+  DLManagedTensor m{};
+  std::shared_ptr<ArenaChunk> chunk;
+  int64_t shape[1] = {0};
+};
+
+void chunk_export_deleter(DLManagedTensor* m) { delete static_cast<ChunkExport*>(m->manager_ctx); }
+
+class ActArena {
+ public:
+  static constexpr uint64_t kAlign = 256;
+  ActArena(int dev, uint64_t initial_bytes) : dev_(dev), initial_(std::max<uint64_t>(initial_bytes, 1u << 20)) {}
+
+  // (chunk id, byte offset) of nbytes in the current step; (-1, 0) when it does not fit and the
+  // arena is frozen (graph capture: no allocation may be recorded into the graph)
+  std::pair<int64_t, uint64_t> alloc(uint64_t nbytes) {
+    nbytes = (std::max<uint64_t>(nbytes, 1) + kAlign - 1) & ~(kAlign - 1);
+    while (cur_ < chunks_.size()) {
+      ArenaChunk& c = *chunks_[cur_];
+      if (off_ + nbytes <= c.nbytes) {
+        const uint64_t o = off_;
+        off_ += nbytes;
+        used_ += nbytes;
+        high_ = std::max(high_, used_);
+        ++allocs_;
+        return {c.id, o};
+      }
+      ++cur_;  // the rest of this chunk stays unused this step (counted by the coalesce)
+      used_ += c.nbytes - off_;
+      off_ = 0;
+    }
+    if (frozen_) {
+      ++refused_;
+      return {-1, 0};
+    }
+    add_chunk(std::max<uint64_t>(nbytes, chunks_.empty() ? initial_ : capacity()));
+    return alloc(nbytes);
+  }
+
+  // start of a step: rewind; merge a multi-chunk arena into one chunk of the high-water size
+  // (allocated on `stream`, ordered after everything already queued there)
+  bool reset(uintptr_t stream) {
+    stream_ = stream;
+    bool rebuilt = false;
+    if (chunks_.size() > 1 && !frozen_) {
+      const uint64_t want = (std::max(high_, capacity()) + (2u << 20) - 1) & ~((uint64_t)(2u << 20) - 1);
+      chunks_.clear();
+      add_chunk(want);
+      ++coalesces_;
+      rebuilt = true;
+    }
+    cur_ = 0;
+    off_ = 0;
+    used_ = 0;
+    ++steps_;
+    return rebuilt;
+  }
+  void set_frozen(bool f) { frozen_ = f; }
+  bool frozen() const { return frozen_; }
+
+  // the chunk as a flat uint8 DLPack tensor sharing ownership of its memory
+  py::capsule chunk_capsule(int64_t id) {
+    for (auto& c : chunks_) {
+      if (c->id != id) continue;
+      auto* e = new ChunkExport();
+      e->chunk = c;
+      e->shape[0] = (int64_t)c->nbytes;
+      DLTensor& t = e->m.dl_tensor;
+      t.data = reinterpret_cast<void*>(c->ptr);
+      t.device = DLDevice{kDLROCM, dev_};
+      t.ndim = 1;
+      t.dtype = DLDataType{1, 8, 1};
+      t.shape = e->shape;
+      t.strides = nullptr;
+      t.byte_offset = 0;
+      e->m.manager_ctx = e;
+      e->m.deleter = chunk_export_deleter;
+      return py::capsule(&e->m, "dltensor", [](PyObject* cap) {
+        if (PyCapsule_IsValid(cap, "dltensor")) {
+          auto* m = static_cast<DLManagedTensor*>(PyCapsule_GetPointer(cap, "dltensor"));
+          if (m && m->deleter) m->deleter(m);
+        }
+      });
+    }
+    throw std::out_of_range("ActArena: no live chunk with this id");
+  }
+
+  uint64_t capacity() const {
+    uint64_t v = 0;
+    for (auto& c : chunks_) v += c->nbytes;
+    return v;
+  }
+  py::dict stats() const {
+    py::dict d;
+    d["capacity_bytes"] = capacity();
+    d["chunks"] = (uint64_t)chunks_.size();
+    d["used_bytes"] = used_;
+    d["high_water_bytes"] = high_;
+    d["allocations"] = allocs_;
+    d["grows"] = grows_;
+    d["coalesces"] = coalesces_;
+    d["steps"] = steps_;
+    d["refused"] = refused_;
+    return d;
+  }
+  int device() const { return dev_; }
+
+ private:
+  void add_chunk(uint64_t nbytes) {
+    auto c = std::make_shared<ArenaChunk>();
+    c->dev = dev_;
+    c->nbytes = nbytes;
+    c->id = next_id_++;
+    Flow f(dev_, stream_);
+    c->ptr = Allocator::get(dev_).allocate(nbytes, f);
+    chunks_.push_back(std::move(c));
+    ++grows_;
+  }
+  int dev_;
+  uint64_t initial_;
+  uintptr_t stream_ = 0;
+  std::vector<std::shared_ptr<ArenaChunk>> chunks_;
+  size_t cur_ = 0;
+  uint64_t off_ = 0, used_ = 0, high_ = 0;
+  uint64_t allocs_ = 0, grows_ = 0, coalesces_ = 0, steps_ = 0, refused_ = 0;
+  int64_t next_id_ = 0;
+  bool frozen_ = false;
+};
+
 // ------------------------------------------------------------------ copies
 // kind: 0 host->device, 1 device->host, 2 device->device, 3 default (unified addressing)
 void memcpy_async(uintptr_t dst, uintptr_t src, uint64_t nbytes, int kind, const Flow& f) {
@@ -421,6 +574,16 @@ void bind_runtime(py::module_& parent) {
       .def("trim", &Allocator::trim, py::arg("keep_bytes") = 0)
       .def("release_deferred", &Allocator::release_deferred, py::call_guard<py::gil_scoped_release>())
       .def_property_readonly("device", &Allocator::device);
+  py::class_<ActArena>(m, "ActArena")
+      .def(py::init<int, uint64_t>(), py::arg("device"), py::arg("initial_bytes") = (uint64_t)256 << 20)
+      .def("alloc", &ActArena::alloc)
+      .def("reset", &ActArena::reset, py::arg("stream"))
+      .def("set_frozen", &ActArena::set_frozen)
+      .def_property_readonly("frozen", &ActArena::frozen)
+      .def("chunk", &ActArena::chunk_capsule)
+      .def("capacity", &ActArena::capacity)
+      .def("stats", &ActArena::stats)
+      .def_property_readonly("device", &ActArena::device);
   m.def("alloc_dlpack", &alloc_dlpack, py::arg("device"), py::arg("shape"), py::arg("code"), py::arg("bits"),
         py::arg("flow"), py::arg("zero") = false);
   m.def("memcpy_async", &memcpy_async);

@@ -119,7 +119,10 @@ class Device:
     def allocator_stats(self) -> dict:
         if self.device_type == DeviceType.CPU:
             return {}
-        return dict(_rt().Allocator.get(self.index).stats())
+        d = dict(_rt().Allocator.get(self.index).stats())
+        from .runtime.arena import device_stats
+        d.update(device_stats(self.index))  # the per-step activation arenas' share of in_use_bytes
+        return d
 
     def copy_to_device(self, dst: torch.Tensor, src: torch.Tensor, flow: str = "default") -> None:
         """dst <- src, asynchronous on ``flow`` for GPU copies of dense same-dtype tensors."""

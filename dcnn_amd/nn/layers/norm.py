@@ -14,6 +14,7 @@ from typing import Optional
 
 import torch
 
+from ...runtime.arena import empty as _arena_empty
 from ..params import ParamSpec
 from .base import LayerConfig, ParameterizedLayer
 
@@ -83,8 +84,8 @@ class BatchNorm(ParameterizedLayer):
                 # BatchNorm + ReLU + max-pool in one pass: the full-resolution output is never
                 # stored; the pool layer finds its cache filled and passes the result through
                 sums = hip.bn_stats(xa, getattr(x, "_bn_partial", None))
-                mean = torch.empty(C, dtype=torch.float32, device=xa.device)
-                istd = torch.empty_like(mean)
+                mean = _arena_empty((C,), torch.float32, xa.device)
+                istd = _arena_empty((C,), torch.float32, xa.device)
                 y, idx = hip.bn_relu_maxpool(xa, sums, xa.numel() // C, self._gamma(), self._beta(), self.epsilon,
                                              pool._geom(), save=(mean, istd),
                                              running=(self.running_mean, self.running_var), momentum=self.momentum)
@@ -107,8 +108,8 @@ class BatchNorm(ParameterizedLayer):
                 else:
                     sums = hip.bn_stats(xa, part)
                 count = xa.numel() // C
-                mean = torch.empty(C, dtype=torch.float32, device=xa.device)
-                istd = torch.empty_like(mean)
+                mean = _arena_empty((C,), torch.float32, xa.device)
+                istd = _arena_empty((C,), torch.float32, xa.device)
                 y = apply(xa, sums, count, self._gamma(), self._beta(), self.epsilon, relu=do_relu, save=(mean, istd),
                           running=(self.running_mean, self.running_var), momentum=self.momentum, **args)
             else:
@@ -142,8 +143,8 @@ class BatchNorm(ParameterizedLayer):
             part = getattr(x, "_bn_partial", None)
             # raw statistics rows: the consumer reduces them together with its own
             sums = part[0] if (part is not None and isinstance(part[0], hip.Stats)) else hip.bn_stats_raw(xa, part)
-            mean = torch.empty(C, dtype=torch.float32, device=xa.device)
-            istd = torch.empty_like(mean)
+            mean = _arena_empty((C,), torch.float32, xa.device)
+            istd = _arena_empty((C,), torch.float32, xa.device)
             d = hip.BnDeferred(xa, sums, xa.numel() // C, self._gamma(), self._beta(), self.epsilon, (mean, istd),
                                (self.running_mean, self.running_var), self.momentum, False)
         else:

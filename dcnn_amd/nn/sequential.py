@@ -553,6 +553,7 @@ class Sequential:
                 save_tensor(f, p)
         if save_state:
             self.save_state(path + ".state")
+        self.save_bn_stats(path + ".bnstats")
 
     def load_weights_file(self, path: str) -> None:
         if not self.initialized:
@@ -575,7 +576,26 @@ class Sequential:
         m.load_weights_file(path + ".bin")
         if os.path.exists(path + ".state"):
             m.load_state(path + ".state")
+        elif os.path.exists(path + ".bnstats"):
+            m.load_bn_stats(path + ".bnstats")
         return m
+
+    # language-neutral BatchNorm running statistics (.bin records: running_mean, running_var per
+    # BatchNorm in layer order) shared with the C++ host API (csrc/host/nn.cpp)
+    def save_bn_stats(self, path: str) -> None:
+        with open(path, "wb") as f:
+            for l in _all_layers(self.layers):
+                if isinstance(l, BatchNorm):
+                    save_tensor(f, l.running_mean.detach().reshape(-1, 1, 1, 1))
+                    save_tensor(f, l.running_var.detach().reshape(-1, 1, 1, 1))
+
+    def load_bn_stats(self, path: str) -> None:
+        with open(path, "rb") as f:
+            for l in _all_layers(self.layers):
+                if isinstance(l, BatchNorm):
+                    dev = l.running_mean.device
+                    l.running_mean = load_tensor(f).reshape(-1).to(dev)
+                    l.running_var = load_tensor(f).reshape(-1).to(dev)
 
     # sidecar: BN running statistics (not in the reference .bin, gap G11)
     def save_state(self, path: str, extra: Optional[dict] = None) -> None:

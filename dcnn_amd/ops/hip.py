@@ -4,8 +4,9 @@ Activations are NHWC in memory (torch ``channels_last``) so the channel dimensio
 contiguous GEMM-K dimension of the implicit-GEMM convolution; the logical shape stays NCHW
 (the reference API/checkpoint layout). Conv weights are ``channels_last`` too, i.e. physical
 ``[Cout][KH][KW][Cin]`` — the K-contiguous B operand of the MFMA GEMM. All launches go to
-PyTorch's current HIP stream and allocate workspaces from its caching allocator, so a whole
-training step can be captured into a hipGraph.
+PyTorch's current HIP stream; activations, statistics slabs and workspaces come from the native
+per-step activation arena while a training step runs (runtime/arena.py; PyTorch's caching
+allocator otherwise), so a whole training step can be captured into a hipGraph.
 """
 from __future__ import annotations
 
@@ -16,6 +17,7 @@ import threading
 
 import torch
 
+from ..runtime import arena as _arena
 from ._ext import dt_code, kernels, ptr, stream_ptr
 
 CL = torch.channels_last
@@ -27,6 +29,18 @@ _NOBNB = (0, 0, 0, 0)
 
 # gather modes of gemm_nt
 PLAIN, CONV_FWD, CONV_DGRAD = 0, 1, 2
+
+
+def _empty(shape, dtype, device, cl=False):
+    """Per-step buffer (activation, statistics slab, workspace): the native activation arena of
+    the running step (runtime/arena.py), else PyTorch's allocator. ``cl``: NHWC strides."""
+    return _arena.empty(shape, dtype, device, cl)
+
+
+def _empty_like(x):
+    """Per-step buffer shaped and laid out (dense or channels_last) like x."""
+    cl = x.dim() == 4 and not x.is_contiguous() and x.is_contiguous(memory_format=CL)
+    return _arena.empty(x.shape, x.dtype, x.device, cl)
 
 
 def _check_act(x: torch.Tensor, what: str):
@@ -43,7 +57,7 @@ def to_act(x: torch.Tensor, dtype: torch.dtype) -> torch.Tensor:
     if x.dim() == 4 and x.dtype == F32 and x.is_contiguous():
         # fused NCHW fp32 -> NHWC (bf16|fp32) conversion kernel (network input path)
         N, C, H, W = x.shape
-        y = torch.empty((N, C, H, W), dtype=dtype, device=x.device, memory_format=CL)
+        y = _empty((N, C, H, W), dtype, x.device, True)
         kernels().nchw_to_nhwc(dt_code(dtype), x.data_ptr(), y.data_ptr(), N, C, H * W, stream_ptr())
         return y
     return x.to(dtype=dtype).contiguous(memory_format=CL)
@@ -102,7 +116,7 @@ def get_f32_concat() -> bool:
 def split3_rows(t, rows, C, pattern, out=None):
     """fp32 [rows][C] (dense) -> bf16 [rows][3C]: pattern 0 [hi|lo|hi], 1 [hi|hi|lo]."""
     if out is None:
-        out = torch.empty((rows, 3 * C), dtype=BF16, device=t.device)
+        out = _empty((rows, 3 * C), BF16, t.device)
     kernels().split3_bf16(t.data_ptr(), out.data_ptr(), rows, C, pattern, stream_ptr())
     return out
 
@@ -114,7 +128,7 @@ def act_split3(t):
     if s is None:
         N, C, H, W = t.shape
         assert t.dtype == F32 and t.is_contiguous(memory_format=CL)
-        s = torch.empty((N, 3 * C, H, W), dtype=BF16, device=t.device, memory_format=CL)
+        s = _empty((N, 3 * C, H, W), BF16, t.device, True)
         split3_rows(t, N * H * W, C, 0, out=s)
         t._s3 = s
     return s
@@ -156,7 +170,7 @@ def _hconv_split(K, NB, H, W, Cs, N, ntaps, device):
     if s == 1:
         return 1, 0, 0
     tiles = K.hconv_tiles(NB, H, W, Cs, N, ntaps)
-    part = torch.empty(tiles * s * K.hconv_tile_elems(NB, H, W, Cs, N, ntaps), dtype=F32, device=device)
+    part = _empty((tiles * s * K.hconv_tile_elems(NB, H, W, Cs, N, ntaps),), F32, device)
     _SplitWs.keep = part
     return s, part.data_ptr(), _ticket(device, tiles * 64, "hconv").data_ptr()
 
@@ -181,7 +195,7 @@ def _fold(rows, N, mode, device, g2=False):
         return _NOFOLD, None
     group = -(-rows // 8)           # <= 8 partials for the consumers' prologue merge
     ng = -(-rows // group)
-    part = torch.empty((ng, 3, N) if ng > 1 else (2 * N,), dtype=F32, device=device)
+    part = _empty((ng, 3, N) if ng > 1 else (2 * N,), F32, device)
     tk = _ticket(device, ng * (N // 64) * 64, "fold")
     return (part.data_ptr(), tk.data_ptr(), group, ng, rows), Stats(part, ng, mode)
 
@@ -217,37 +231,37 @@ def conv2d_fwd(x, w, bias, stride, pad, *, stats=False, residual=None, relu=Fals
         # split-precision fp32 on the bf16 halo conv (see _F32_CONCAT)
         xs = act_split3(x)
         ws = split3_rows(w, Co * KH * KW, Ci, 1)
-        y = torch.empty((N, Co, OH, OW), dtype=F32, device=x.device, memory_format=CL)
+        y = _empty((N, Co, OH, OW), F32, x.device, True)
         slab, rows, sums = None, 0, None
         if stats:
             rows = K.hconv_stat_rows(N, H, W, 3 * Ci, Co, KH * KW, 1)
-            slab = torch.empty((rows, 3, Co), dtype=F32, device=x.device)
-            sums = torch.empty((2 * Co,), dtype=F32, device=x.device)  # zeroed in-kernel
+            slab = _empty((rows, 3, Co), F32, x.device)
+            sums = _empty((2 * Co,), F32, x.device)  # zeroed in-kernel
         K.hconv(xs.data_ptr(), ws.data_ptr(), 0, _nbytes(xs), _nbytes(ws), N, H, W, 3 * Ci, Co, KH * KW * 3 * Ci,
                 [(t[0], t[1], t[3]) for t in _fwd_taps(3 * Ci, W, KH, KW, ph, pw)], ptr(bias), 0, ptr(slab),
                 int(relu), ptr(sums), 2 * Co if stats else 0, _NOBNB, y.data_ptr(), ptr(residual),
                 *_NOSPLIT, stream_ptr(), _NOFOLD)
         return y, ((slab, rows, sums) if stats else None)
     if x.dtype == F32:  # fp32 compute path: MFMA f32 16x16x4 gathered GEMM
-        y = torch.empty((N, Co, OH, OW), dtype=F32, device=x.device, memory_format=CL)
+        y = _empty((N, Co, OH, OW), F32, x.device, True)
         slab, rows, sums = None, 0, None
         if stats:
             rows = K.gemm_g2f_stat_rows(M, Co)
-            slab = torch.empty((rows, 3, Co), dtype=F32, device=x.device)
-            sums = torch.empty((2 * Co,), dtype=F32, device=x.device)  # zeroed in-kernel
+            slab = _empty((rows, 3, Co), F32, x.device)
+            sums = _empty((2 * Co,), F32, x.device)  # zeroed in-kernel
         K.gemm_g2f(x.data_ptr(), w.data_ptr(), y.data_ptr(), _nbytes(x), _nbytes(w), M, Co, Ci, H, W, OH, OW, sh, sw,
                    _fwd_taps(Ci, W, KH, KW, ph, pw), KH * KW * Ci, Co, OH, OW, 1, 1, 0, 0, ptr(bias), ptr(residual),
                    ptr(slab), int(relu), ptr(sums), 2 * Co if stats else 0, _NOBNB, stream_ptr())
         return y, ((slab, rows, sums) if stats else None)
     taps = _fwd_taps(Ci, W, KH, KW, ph, pw)
     if not out_fp32 and _hconv_ok(N, OH, OW, H, W, sh, sw, Ci, Co, taps, w):
-        y = torch.empty((N, Co, OH, OW), dtype=BF16, device=x.device, memory_format=CL)
+        y = _empty((N, Co, OH, OW), BF16, x.device, True)
         slab, rows, sums = None, 0, None
         fold, fst = _NOFOLD, None
         if stats:
             rows = K.hconv_stat_rows(N, H, W, Ci, Co, len(taps), 0)
-            slab = torch.empty((rows, 3, Co), dtype=F32, device=x.device)
-            sums = torch.empty((2 * Co,), dtype=F32, device=x.device)  # zeroed in-kernel
+            slab = _empty((rows, 3, Co), F32, x.device)
+            sums = _empty((2 * Co,), F32, x.device)  # zeroed in-kernel
             if not K.hconv_v3(N, H, W, Ci, Co, len(taps)):  # (no in-launch fold on hconv3)
                 fold, fst = _fold(rows, Co, 0, x.device)
         K.hconv(x.data_ptr(), w.data_ptr(), y.data_ptr(), _nbytes(x), _nbytes(w), N, H, W, Ci, Co, KH * KW * Ci,
@@ -256,13 +270,13 @@ def conv2d_fwd(x, w, bias, stride, pad, *, stats=False, residual=None, relu=Fals
                 stream_ptr(), fold)
         return y, ((fst if fst is not None else slab, rows, sums) if stats else None)
     if _g2_ok(Ci, Co) and not out_fp32:
-        y = torch.empty((N, Co, OH, OW), dtype=BF16, device=x.device, memory_format=CL)
+        y = _empty((N, Co, OH, OW), BF16, x.device, True)
         slab, rows, sums = None, 0, None
         fold, fst = _NOFOLD, None
         if stats:
             rows = K.gemm_g2_stat_rows(M, Co)
-            slab = torch.empty((rows, 3, Co), dtype=F32, device=x.device)
-            sums = torch.empty((2 * Co,), dtype=F32, device=x.device)  # zeroed in-kernel
+            slab = _empty((rows, 3, Co), F32, x.device)
+            sums = _empty((2 * Co,), F32, x.device)  # zeroed in-kernel
             fold, fst = _fold(rows, Co, 0, x.device, g2=True)
         K.gemm_g2_grouped(x.data_ptr(), w.data_ptr(), y.data_ptr(), _nbytes(x), _nbytes(w), M, Co, Ci, H, W, OH, OW,
                           sh, sw, _fwd_taps(Ci, W, KH, KW, ph, pw), KH * KW * Ci, Co, OH, OW, 1, 1, 0, 0, ptr(bias),
@@ -270,15 +284,15 @@ def conv2d_fwd(x, w, bias, stride, pad, *, stats=False, residual=None, relu=Fals
                           stream_ptr(), [], fold)
         return y, ((fst if fst is not None else slab, rows, sums) if stats else None)
     # generic fallback (odd channel counts): v1 kernels
-    y = torch.empty((N, Co, OH, OW), dtype=F32 if out_fp32 else BF16, device=x.device, memory_format=CL)
+    y = _empty((N, Co, OH, OW), F32 if out_fp32 else BF16, x.device, True)
     slab, rows = None, 0
     if stats:
         rows = K.gemm_nt_stat_rows(M, Co)
-        slab = torch.empty((rows, 3, Co), dtype=F32, device=x.device)
+        slab = _empty((rows, 3, Co), F32, x.device)
     K.gemm_nt(x.data_ptr(), w.data_ptr(), y.data_ptr(), M, Co, KH * KW * Ci, 0, KH * KW * Ci, Co, CONV_FWD,
               N, H, W, Ci, OH, OW, KH, KW, sh, sw, ph, pw, ptr(bias), ptr(residual), ptr(slab),
               int(out_fp32), int(relu), stream_ptr())
-    sums = torch.empty((2 * Co,), dtype=F32, device=x.device) if stats else None
+    sums = _empty((2 * Co,), F32, x.device) if stats else None
     return y, ((slab, rows, sums) if stats else None)
 
 
@@ -302,13 +316,13 @@ def stem_conv_fwd(x, w, bias=None, stats=False):
     N, Ci, H, W = x.shape
     Co = w.shape[0]
     K = kernels()
-    y = torch.empty((N, Co, H, W), dtype=BF16, device=x.device, memory_format=CL)
+    y = _empty((N, Co, H, W), BF16, x.device, True)
     slab = sums = None
     rows = 0
     if stats:
         rows = K.stem_tiles(N, H, W)
-        slab = torch.empty((rows, 3, Co), dtype=F32, device=x.device)
-        sums = torch.empty((2 * Co,), dtype=F32, device=x.device)  # zeroed in-kernel
+        slab = _empty((rows, 3, Co), F32, x.device)
+        sums = _empty((2 * Co,), F32, x.device)  # zeroed in-kernel
     assert w.dtype in (F32, BF16) and tuple(w.shape) == (Co, Ci, 3, 3)
     K.stem_fwd(x.data_ptr(), w.data_ptr(), int(w.dtype == BF16), list(w.stride()), ptr(bias), y.data_ptr(),
                ptr(slab), ptr(sums), 2 * Co if stats else 0, N, Ci, H, W, Co, stream_ptr())
@@ -325,8 +339,8 @@ def stem_conv_wgrad(dy, x, grad_w, grad_b=None):
     assert grad_w.is_contiguous() or grad_w.is_contiguous(memory_format=CL), "dense fp32 weight gradient"
     blocks = K.stem_wgrad_blocks(N, H, W)
     n = Co * Ci * 9
-    slab = torch.empty((blocks, n), dtype=F32, device=x.device)
-    bslab = torch.empty((blocks, Co), dtype=F32, device=x.device) if grad_b is not None else None
+    slab = _empty((blocks, n), F32, x.device)
+    bslab = _empty((blocks, Co), F32, x.device) if grad_b is not None else None
     st = stream_ptr()
     K.stem_wgrad(x.data_ptr(), dy.data_ptr(), slab.data_ptr(), ptr(bslab), list(grad_w.stride()), N, Ci, H, W, Co,
                  blocks, st)
@@ -337,7 +351,7 @@ def to_act_padded(x, cp):
     """(N,C,H,W) -> NHWC bf16 with channels zero-padded to cp (RGB stem: 3 -> 8) so the stem
     conv runs on the vectorised MFMA path. One HIP pass from an NCHW fp32 input."""
     N, C, H, W = x.shape
-    y = torch.empty((N, cp, H, W), dtype=BF16, device=x.device, memory_format=CL)
+    y = _empty((N, cp, H, W), BF16, x.device, True)
     src = x if (x.dtype == F32 and x.is_contiguous()) else x.float().contiguous()
     kernels().nchw_to_nhwc_pad(dt_code(BF16), src.data_ptr(), y.data_ptr(), N, C, cp, H * W, stream_ptr())
     return y
@@ -348,7 +362,7 @@ def pad_weight_channels(w, cp, out=None):
     previous result to refresh in place (one copy of the real channels, padding already zero)."""
     Co, Ci, KH, KW = w.shape
     if out is None or tuple(out.shape) != (Co, KH, KW, cp) or out.device != w.device:
-        out = torch.zeros((Co, KH, KW, cp), dtype=BF16, device=w.device)
+        out = _arena.persistent((Co, KH, KW, cp), BF16, w.device, zero=True)  # cached by the layer
     out[..., :Ci] = w.permute(0, 2, 3, 1).to(BF16)
     return out
 
@@ -361,11 +375,11 @@ def conv_weight_t(w, out=None, dtype=BF16):
         src = w if (w.dtype == F32 and (w.is_contiguous(memory_format=CL) or KH * KW == 1 or Ci == 1)) \
             else w.float().contiguous(memory_format=CL)
         if out is None:
-            out = torch.empty((Ci, KH, KW, Co), dtype=F32, device=w.device)
+            out = _empty((Ci, KH, KW, Co), F32, w.device)
         kernels().conv_weight_transpose_f32(src.data_ptr(), out.data_ptr(), Co, KH * KW, Ci, stream_ptr())
         return out
     if out is None:
-        out = torch.empty((Ci, KH, KW, Co), dtype=BF16, device=w.device)
+        out = _empty((Ci, KH, KW, Co), BF16, w.device)
     kernels().conv_weight_transpose(dt_code(w.dtype), w.data_ptr(), out.data_ptr(), Co, KH * KW, Ci, stream_ptr())
     return out
 
@@ -404,7 +418,7 @@ def im2col_nhwc(x, KH, KW, stride, pad):
     _check_act(x, "im2col_nhwc.x")
     N, C, H, W = x.shape
     OH, OW = conv_out_hw(H, W, KH, KW, stride[0], stride[1], pad[0], pad[1])
-    col = torch.empty((N * OH * OW, KH * KW * C), dtype=x.dtype, device=x.device)
+    col = _empty((N * OH * OW, KH * KW * C), x.dtype, x.device)
     kernels().im2col_nhwc(dt_code(x.dtype), x.data_ptr(), col.data_ptr(), *_geom(N, H, W, C, OH, OW, KH, KW, stride, pad),
                           stream_ptr())
     return col
@@ -416,7 +430,7 @@ def col2im_nhwc(col, x_shape, KH, KW, stride, pad, *, residual=None, chan_major=
     N, C, H, W = x_shape
     OH, OW = conv_out_hw(H, W, KH, KW, stride[0], stride[1], pad[0], pad[1])
     assert tuple(col.shape) == (N * OH * OW, KH * KW * C) and col.is_contiguous()
-    x = torch.empty((N, C, H, W), dtype=col.dtype, device=col.device, memory_format=CL)
+    x = _empty((N, C, H, W), col.dtype, col.device, True)
     if residual is not None:
         assert tuple(residual.shape) == (N, C, H, W) and residual.dtype == col.dtype
         assert residual.is_contiguous(memory_format=CL)
@@ -438,12 +452,12 @@ def conv2d_fwd_im2col(x, w, bias, stride, pad, *, stats=False, residual=None, re
     if residual is not None:
         assert tuple(residual.shape) == (N, Co, OH, OW) and residual.is_contiguous(memory_format=CL)
     f32 = x.dtype == F32
-    y = torch.empty((N, Co, OH, OW), dtype=x.dtype, device=x.device, memory_format=CL)
+    y = _empty((N, Co, OH, OW), x.dtype, x.device, True)
     slab, rows, sums = None, 0, None
     if stats:
         rows = (K.gemm_g2f_stat_rows if f32 else K.gemm_g2_stat_rows)(M, Co)
-        slab = torch.empty((rows, 3, Co), dtype=F32, device=x.device)
-        sums = torch.empty((2 * Co,), dtype=F32, device=x.device)  # zeroed in-kernel
+        slab = _empty((rows, 3, Co), F32, x.device)
+        sums = _empty((2 * Co,), F32, x.device)  # zeroed in-kernel
     (K.gemm_g2f if f32 else K.gemm_g2)(col.data_ptr(), w.data_ptr(), y.data_ptr(), _nbytes(col), _nbytes(w), M, Co,
                                        Kc, 1, 1, 1, 1, 1, 1, [(0, 0, 0, 0)], Kc, Co, 1, 1, 1, 1, 0, 0, ptr(bias),
                                        ptr(residual), ptr(slab), int(relu), ptr(sums), 2 * Co if stats else 0, _NOBNB,
@@ -460,7 +474,7 @@ def conv2d_dgrad_im2col(dy, wt, x_shape, stride, pad, *, residual=None):
     assert Ci2 == Ci and dy.shape[1] == Co and wt.dtype == dy.dtype and wt.is_contiguous()
     M = dy.shape[0] * dy.shape[2] * dy.shape[3]
     Nc = Ci * KH * KW
-    colg = torch.empty((M, Nc), dtype=dy.dtype, device=dy.device)
+    colg = _empty((M, Nc), dy.dtype, dy.device)
     (K.gemm_g2f if dy.dtype == F32 else K.gemm_g2)(dy.data_ptr(), wt.data_ptr(), colg.data_ptr(), _nbytes(dy),
                                                    _nbytes(wt), M, Nc, Co, 1, 1, 1, 1, 1, 1, [(0, 0, 0, 0)], Co, Nc,
                                                    1, 1, 1, 1, 0, 0, 0, 0, 0, 0, 0, 0, _NOBNB, stream_ptr())
@@ -478,14 +492,14 @@ def conv2d_wgrad_im2col(dy, x, w_shape, stride, pad, grad_w, grad_b=None):
     st = stream_ptr()
     if dy.dtype == F32:
         splits = K.gemm_t2f_splits(Co, Ng, P)
-        slab = torch.empty((splits, Co, Ng), dtype=F32, device=x.device)
-        bslab = torch.empty((splits, Co), dtype=F32, device=x.device) if grad_b is not None else None
+        slab = _empty((splits, Co, Ng), F32, x.device)
+        bslab = _empty((splits, Co), F32, x.device) if grad_b is not None else None
         K.gemm_t2f(dy.data_ptr(), col.data_ptr(), slab.data_ptr(), ptr(bslab), Co, Ng, P, Co, Ng, 1, 1, 1, 1, 1, 1,
                    [(0, 0)], splits, st)
     else:
         splits = K.gemm_t2_splits(Co, Ng, P)
-        slab = torch.empty((splits, Co, Ng), dtype=F32, device=x.device)
-        bslab = torch.empty((splits, Co), dtype=F32, device=x.device) if grad_b is not None else None
+        slab = _empty((splits, Co, Ng), F32, x.device)
+        bslab = _empty((splits, Co), F32, x.device) if grad_b is not None else None
         K.gemm_t2(dy.data_ptr(), col.data_ptr(), slab.data_ptr(), ptr(bslab), _nbytes(dy), _nbytes(col), Co, Ng, P,
                   Co, Ng, 1, 1, 1, 1, 1, 1, [(0, 0)], splits, st)
     _reduce_wb(K, slab, grad_w, Co * Ng, bslab, grad_b, Co, splits, st)
@@ -564,7 +578,7 @@ def conv2d_dgrad(dy, wt, x_shape, stride, pad, *, residual=None, bnb=None):
     if f32:
         assert wt.dtype == F32, "fp32 dgrad needs an fp32 transposed weight (conv_weight_t(..., dtype=F32))"
     if not f32 and not _g2_ok(Co, Ci):
-        dx = torch.empty((N, Ci, H, W), dtype=BF16, device=dy.device, memory_format=CL)
+        dx = _empty((N, Ci, H, W), BF16, dy.device, True)
         Kd = KH * KW * Co
         K.gemm_nt(dy.data_ptr(), wt.data_ptr(), dx.data_ptr(), N * H * W, Ci, Kd, 0, Kd, Ci, CONV_DGRAD,
                   N, OH, OW, Co, H, W, KH, KW, sh, sw, ph, pw, 0, ptr(residual), 0, 0, 0, stream_ptr())
@@ -585,20 +599,20 @@ def conv2d_dgrad(dy, wt, x_shape, stride, pad, *, residual=None, bnb=None):
         for ry, rx, _, _, taps in allc:
             groups.append((len(taps_all), len(taps), ry, rx))
             taps_all += taps
-        dx = torch.empty((N, Ci, H, W), dtype=BF16, device=dy.device, memory_format=CL)
+        dx = _empty((N, Ci, H, W), BF16, dy.device, True)
         K.gemm_g2_grouped(dy.data_ptr(), wt.data_ptr(), dx.data_ptr(), _nbytes(dy), _nbytes(wt), M, Ci, Co, OH, OW,
                           GH, GW, 1, 1, taps_all, KH * KW * Co, Ci, H, W, sh, sw, 0, 0, 0, ptr(residual), 0, 0, 0, 0,
                           _NOBNB, stream_ptr(), groups, _NOFOLD)
         return dx
     if empty_class:
         # positions no tap reaches keep the residual (or zero); a memset / async copy node, not a kernel
-        dx = torch.empty((N, Ci, H, W), dtype=odt, device=dy.device, memory_format=CL)
+        dx = _empty((N, Ci, H, W), odt, dy.device, True)
         if residual is not None:
             dx.copy_(residual)
         else:
             zero_(dx)
     else:
-        dx = torch.empty((N, Ci, H, W), dtype=odt, device=dy.device, memory_format=CL)
+        dx = _empty((N, Ci, H, W), odt, dy.device, True)
     st = stream_ptr()
     if (f32 and len(classes) == 1 and not empty_class and _f32_concat_ok(Co, Ci)
             and _hconv_ok(N, H, W, OH, OW, sh, sw, 3 * Co, Ci, classes[0][4], wt)):
@@ -619,8 +633,8 @@ def conv2d_dgrad(dy, wt, x_shape, stride, pad, *, residual=None, bnb=None):
         fold, fst = _NOFOLD, None
         if fuse:
             rows = K.hconv_stat_rows(N, H, W, Co, Ci, len(classes[0][4]), 0)
-            slab = torch.empty((rows, 2, Ci), dtype=F32, device=dy.device)
-            sums = torch.empty((2 * Ci,), dtype=F32, device=dy.device)  # zeroed in-kernel
+            slab = _empty((rows, 2, Ci), F32, dy.device)
+            sums = _empty((2 * Ci,), F32, dy.device)  # zeroed in-kernel
             if not K.hconv_v3(N, H, W, Co, Ci, len(classes[0][4])):
                 fold, fst = _fold(rows, Ci, 1, dy.device)
         K.hconv(dy.data_ptr(), wt.data_ptr(), dx.data_ptr(), _nbytes(dy), _nbytes(wt), N, OH, OW, Co, Ci, KH * KW * Co,
@@ -641,8 +655,8 @@ def conv2d_dgrad(dy, wt, x_shape, stride, pad, *, residual=None, bnb=None):
             groups.append((len(taps_all), len(taps), ry, rx))
             taps_all += taps
         rows = K.gemm_g2_stat_rows(M, Ci) if fuse else 0
-        slab = torch.empty((rows, 2, Ci), dtype=F32, device=dy.device) if fuse else None
-        sums = torch.empty((2 * Ci,), dtype=F32, device=dy.device) if fuse else None
+        slab = _empty((rows, 2, Ci), F32, dy.device) if fuse else None
+        sums = _empty((2 * Ci,), F32, dy.device) if fuse else None
         fold, fst = _fold(rows, Ci, 1, dy.device, g2=True) if fuse else (_NOFOLD, None)
         K.gemm_g2_grouped(dy.data_ptr(), wt.data_ptr(), dx.data_ptr(), _nbytes(dy), _nbytes(wt), M, Ci, Co, OH, OW,
                           GH, GW, 1, 1, taps_all, KH * KW * Co, Ci, H, W, sh, sw, 0, 0, 0, ptr(residual), ptr(slab), 0,
@@ -652,8 +666,8 @@ def conv2d_dgrad(dy, wt, x_shape, stride, pad, *, residual=None, bnb=None):
         return dx
     crow = [K.gemm_g2_stat_rows(N * GH * GW, Ci) if fuse else 0 for _, _, GH, GW, _ in classes]
     rows = sum(crow)
-    slab = torch.empty((rows, 2, Ci), dtype=F32, device=dy.device) if fuse else None
-    sums = torch.empty((2 * Ci,), dtype=F32, device=dy.device) if fuse else None
+    slab = _empty((rows, 2, Ci), F32, dy.device) if fuse else None
+    sums = _empty((2 * Ci,), F32, dy.device) if fuse else None
     r0 = 0
     for k, (ry, rx, GH, GW, taps) in enumerate(classes):
         sp = slab.data_ptr() + r0 * 2 * Ci * 4 if fuse else 0
@@ -840,8 +854,8 @@ def conv2d_wgrad(dy, x, w_shape, stride, pad, grad_w, grad_b=None):
         dys, xs = act_split3(dy), act_split3(x)
         Ng = KH * KW * Ci
         splits = K.hwgrad_splits(N, H, W, Ci, Co)
-        slab = torch.empty((3 * splits, Co, Ng), dtype=F32, device=x.device)
-        bslab = torch.empty((3 * splits, Co), dtype=F32, device=x.device) if grad_b is not None else None
+        slab = _empty((3 * splits, Co, Ng), F32, x.device)
+        bslab = _empty((3 * splits, Co), F32, x.device) if grad_b is not None else None
         K.hwgrad(dys.data_ptr(), xs.data_ptr(), slab.data_ptr(), ptr(bslab), _nbytes(dys), _nbytes(xs), N, H, W, Ci,
                  Co, taps, splits, 3 * Co, 3 * Ci, [(0, 0, 1), (0, Ci, 0), (Co, 0, 1)], st)
         _reduce_wb(K, slab, grad_w, Co * Ng, bslab, grad_b, Co, 3 * splits, st)
@@ -850,8 +864,8 @@ def conv2d_wgrad(dy, x, w_shape, stride, pad, grad_w, grad_b=None):
         assert x.dtype == F32 and Cx == Ci
         Ng = KH * KW * Ci
         splits = K.gemm_t2f_splits(Co, Ng, P)
-        slab = torch.empty((splits, Co, Ng), dtype=F32, device=x.device)
-        bslab = torch.empty((splits, Co), dtype=F32, device=x.device) if grad_b is not None else None
+        slab = _empty((splits, Co, Ng), F32, x.device)
+        bslab = _empty((splits, Co), F32, x.device) if grad_b is not None else None
         taps = [(ky - pad[0], kx - pad[1]) for ky in range(KH) for kx in range(KW)]
         K.gemm_t2f(dy.data_ptr(), x.data_ptr(), slab.data_ptr(), ptr(bslab), Co, Ng, P, Co, Ci, H, W, OH, OW,
                    stride[0], stride[1], taps, splits, st)
@@ -862,8 +876,8 @@ def conv2d_wgrad(dy, x, w_shape, stride, pad, grad_w, grad_b=None):
         # halo-tiled wgrad: X read ~1.4x instead of once per tap
         Ng = KH * KW * Ci
         splits = K.hwgrad_splits(N, H, W, Ci, Co)
-        slab = torch.empty((splits, Co, Ng), dtype=F32, device=x.device)
-        bslab = torch.empty((splits, Co), dtype=F32, device=x.device) if grad_b is not None else None
+        slab = _empty((splits, Co, Ng), F32, x.device)
+        bslab = _empty((splits, Co), F32, x.device) if grad_b is not None else None
         K.hwgrad(dy.data_ptr(), x.data_ptr(), slab.data_ptr(), ptr(bslab), _nbytes(dy), _nbytes(x), N, H, W, Ci, Co,
                  taps, splits, Co, Ci, [], st)
         _reduce_wb(K, slab, grad_w, Co * Ng, bslab, grad_b, Co, splits, st)
@@ -871,15 +885,15 @@ def conv2d_wgrad(dy, x, w_shape, stride, pad, grad_w, grad_b=None):
     if _g2_ok(Cx, Co) and P < (1 << 24):
         Ng = KH * KW * Cx
         splits = K.gemm_t2_splits(Co, Ng, P)
-        slab = torch.empty((splits, Co, Ng), dtype=F32, device=x.device)
-        bslab = torch.empty((splits, Co), dtype=F32, device=x.device) if grad_b is not None else None
+        slab = _empty((splits, Co, Ng), F32, x.device)
+        bslab = _empty((splits, Co), F32, x.device) if grad_b is not None else None
         taps = [(ky - pad[0], kx - pad[1]) for ky in range(KH) for kx in range(KW)]
         K.gemm_t2(dy.data_ptr(), x.data_ptr(), slab.data_ptr(), ptr(bslab), _nbytes(dy), _nbytes(x), Co, Ng, P, Co, Cx,
                   H, W, OH, OW, stride[0], stride[1], taps, splits, st)
         if Cx == Ci:
             _reduce_wb(K, slab, grad_w, Co * Ng, bslab, grad_b, Co, splits, st)
             return
-        tmp = torch.empty((Co, KH, KW, Cx), dtype=F32, device=x.device)
+        tmp = _empty((Co, KH, KW, Cx), F32, x.device)
         K.splitk_reduce(slab.data_ptr(), tmp.data_ptr(), Co * Ng, splits, 0, st)
         grad_w.add_(tmp[..., :Ci].permute(0, 3, 1, 2))
         if grad_b is not None:
@@ -887,8 +901,8 @@ def conv2d_wgrad(dy, x, w_shape, stride, pad, grad_w, grad_b=None):
         return
     Ng = KH * KW * Ci
     splits = K.gemm_tn_splits(Co, Ng, P)
-    slab = torch.empty((splits, Co, Ng), dtype=F32, device=x.device)
-    bslab = torch.empty((splits, Co), dtype=F32, device=x.device) if grad_b is not None else None
+    slab = _empty((splits, Co, Ng), F32, x.device)
+    bslab = _empty((splits, Co), F32, x.device) if grad_b is not None else None
     K.gemm_tn(dy.data_ptr(), x.data_ptr(), slab.data_ptr(), ptr(bslab), Co, Ng, P, CONV_FWD,
               N, H, W, Ci, OH, OW, KH, KW, stride[0], stride[1], pad[0], pad[1], 0, splits, st)
     assert grad_w.is_contiguous(memory_format=CL) or KH * KW == 1 or Ci == 1
@@ -900,12 +914,12 @@ def dense_fwd(x2d, w2d, bias):
     N, In = x2d.shape
     Out = w2d.shape[0]
     if x2d.dtype == F32:
-        y = torch.empty((N, Out), dtype=F32, device=x2d.device)
+        y = _empty((N, Out), F32, x2d.device)
         kernels().gemm_g2f(x2d.data_ptr(), w2d.data_ptr(), y.data_ptr(), _nbytes(x2d), _nbytes(w2d), N, Out, In, 1, 1,
                            1, 1, 1, 1, [(0, 0, 0, 0)], In, Out, 1, 1, 1, 1, 0, 0, ptr(bias), 0, 0, 0, 0, 0, _NOBNB,
                            stream_ptr())
         return y
-    y = torch.empty((N, Out), dtype=BF16, device=x2d.device)
+    y = _empty((N, Out), BF16, x2d.device)
     if _g2_ok(In, Out):
         kernels().gemm_g2(x2d.data_ptr(), w2d.data_ptr(), y.data_ptr(), _nbytes(x2d), _nbytes(w2d), N, Out, In, 1, 1,
                           1, 1, 1, 1, [(0, 0, 0, 0)], In, Out, 1, 1, 1, 1, 0, 0, ptr(bias), 0, 0, 0, 0, 0, _NOBNB,
@@ -921,12 +935,12 @@ def dense_dgrad(dy2d, wt2d):
     N, Out = dy2d.shape
     In = wt2d.shape[0]
     if dy2d.dtype == F32:
-        dx = torch.empty((N, In), dtype=F32, device=dy2d.device)
+        dx = _empty((N, In), F32, dy2d.device)
         kernels().gemm_g2f(dy2d.data_ptr(), wt2d.data_ptr(), dx.data_ptr(), _nbytes(dy2d), _nbytes(wt2d), N, In, Out,
                            1, 1, 1, 1, 1, 1, [(0, 0, 0, 0)], Out, In, 1, 1, 1, 1, 0, 0, 0, 0, 0, 0, 0, 0, _NOBNB,
                            stream_ptr())
         return dx
-    dx = torch.empty((N, In), dtype=BF16, device=dy2d.device)
+    dx = _empty((N, In), BF16, dy2d.device)
     if _g2_ok(Out, In):
         kernels().gemm_g2(dy2d.data_ptr(), wt2d.data_ptr(), dx.data_ptr(), _nbytes(dy2d), _nbytes(wt2d), N, In, Out, 1,
                           1, 1, 1, 1, 1, [(0, 0, 0, 0)], Out, In, 1, 1, 1, 1, 0, 0, 0, 0, 0, 0, 0, 0, _NOBNB,
@@ -944,20 +958,20 @@ def dense_wgrad(dy2d, x2d, grad_w, grad_b=None):
     st = stream_ptr()
     if dy2d.dtype == F32:
         splits = K.gemm_t2f_splits(Out, In, N)
-        slab = torch.empty((splits, Out, In), dtype=F32, device=x2d.device)
-        bslab = torch.empty((splits, Out), dtype=F32, device=x2d.device) if grad_b is not None else None
+        slab = _empty((splits, Out, In), F32, x2d.device)
+        bslab = _empty((splits, Out), F32, x2d.device) if grad_b is not None else None
         K.gemm_t2f(dy2d.data_ptr(), x2d.data_ptr(), slab.data_ptr(), ptr(bslab), Out, In, N, Out, In, 1, 1, 1, 1,
                    1, 1, [(0, 0)], splits, st)
     elif _g2_ok(In, Out):
         splits = K.gemm_t2_splits(Out, In, N)
-        slab = torch.empty((splits, Out, In), dtype=F32, device=x2d.device)
-        bslab = torch.empty((splits, Out), dtype=F32, device=x2d.device) if grad_b is not None else None
+        slab = _empty((splits, Out, In), F32, x2d.device)
+        bslab = _empty((splits, Out), F32, x2d.device) if grad_b is not None else None
         K.gemm_t2(dy2d.data_ptr(), x2d.data_ptr(), slab.data_ptr(), ptr(bslab), _nbytes(dy2d), _nbytes(x2d), Out, In,
                   N, Out, In, 1, 1, 1, 1, 1, 1, [(0, 0)], splits, st)
     else:
         splits = K.gemm_tn_splits(Out, In, N)
-        slab = torch.empty((splits, Out, In), dtype=F32, device=x2d.device)
-        bslab = torch.empty((splits, Out), dtype=F32, device=x2d.device) if grad_b is not None else None
+        slab = _empty((splits, Out, In), F32, x2d.device)
+        bslab = _empty((splits, Out), F32, x2d.device) if grad_b is not None else None
         K.gemm_tn(dy2d.data_ptr(), x2d.data_ptr(), slab.data_ptr(), ptr(bslab), Out, In, N, PLAIN,
                   0, 0, 0, 0, 1, 1, 1, 1, 1, 1, 0, 0, In, splits, st)
     _reduce_wb(K, slab, grad_w, Out * In, bslab, grad_b, Out, splits, st)
@@ -980,7 +994,7 @@ def _ticket(device, C, slot="stat"):
     t = _tickets.get(key)
     need = (C + 63) // 64
     if t is None or t.numel() < need:
-        t = zero_(torch.empty(max(need, 64), dtype=torch.int32, device=device))
+        t = _arena.persistent((max(need, 64),), torch.int32, torch.device(device), zero=True)
         _tickets[key] = t
     return t
 
@@ -1041,7 +1055,7 @@ def stat_reduce(mode, slab, rows, C, out):
         return slab
     K = kernels()
     ny = K.bn_stat_parts(rows)
-    part = torch.empty((ny, 3, C), dtype=F32, device=slab.device) if ny > 1 else None
+    part = _empty((ny, 3, C), F32, slab.device) if ny > 1 else None
     K.bn_stat_reduce(mode, slab.data_ptr(), rows, C, out.data_ptr(), ptr(part), 0, stream_ptr())
     return Stats(part if ny > 1 else out, ny, mode)
 
@@ -1063,8 +1077,8 @@ def bn_stats_raw(x, partial=None):
     K = kernels()
     R, C = _rc(x)
     rows = K.bn_partial_rows(R, C)
-    slab = torch.empty((rows, 3, C), dtype=F32, device=x.device)
-    sums = torch.empty((2 * C,), dtype=F32, device=x.device)
+    slab = _empty((rows, 3, C), F32, x.device)
+    sums = _empty((2 * C,), F32, x.device)
     K.bn_partial(dt_code(x.dtype), x.data_ptr(), 0, 0, 0, 0, 0, R, C, slab.data_ptr(), 0, 0, stream_ptr())
     return slab, rows, sums
 
@@ -1074,8 +1088,8 @@ def bn_bwd_stats_raw(dy, x, mean, istd):
     K = kernels()
     R, C = _rc(x)
     rows = K.bn_partial_rows(R, C)
-    slab = torch.empty((rows, 2, C), dtype=F32, device=x.device)
-    sums = torch.empty((2 * C,), dtype=F32, device=x.device)
+    slab = _empty((rows, 2, C), F32, x.device)
+    sums = _empty((2 * C,), F32, x.device)
     K.bn_partial(dt_code(x.dtype), x.data_ptr(), dy.data_ptr(), 0, 0, mean.data_ptr(), istd.data_ptr(), R, C,
                  slab.data_ptr(), 1, 0, stream_ptr())
     return slab, rows, sums
@@ -1089,7 +1103,7 @@ def bn_bwd_apply_dual(dy, a, b):
     outs, sides = [], []
     for layer, ent, st in (a, b):
         x, _, mean, istd, _ = ent
-        dx = torch.empty_like(x, memory_format=CL)
+        dx = _empty(x.shape, x.dtype, x.device, True)
         sp, parts = _stats(st)
         dg = layer._grads[0].view(-1) if layer.affine else None
         db = layer._grads[1].view(-1) if layer.affine else None
@@ -1108,7 +1122,7 @@ def stat_reduce_pair(mode, a, b, C):
     res, ptrs = [], []
     for slab, rows, out in (a, b):
         ny = K.bn_stat_parts(rows)
-        part = torch.empty((ny, 3, C), dtype=F32, device=slab.device) if ny > 1 else None
+        part = _empty((ny, 3, C), F32, slab.device) if ny > 1 else None
         ptrs.append((slab.data_ptr(), rows, out.data_ptr(), ptr(part)))
         res.append(Stats(part if ny > 1 else out, ny, mode))
     (s1, r1, o1, p1), (s2, r2, o2, p2) = ptrs
@@ -1125,8 +1139,8 @@ def bn_stats(x, partial=None):
     st = stream_ptr()
     if partial is None:
         rows = K.bn_partial_rows(R, C)
-        slab = torch.empty((rows, 3, C), dtype=F32, device=x.device)
-        sums = torch.empty((2 * C,), dtype=F32, device=x.device)
+        slab = _empty((rows, 3, C), F32, x.device)
+        sums = _empty((2 * C,), F32, x.device)
         K.bn_partial(dt_code(x.dtype), x.data_ptr(), 0, 0, 0, 0, 0, R, C, slab.data_ptr(), 0, 0, st)
     else:
         slab, rows, sums = partial
@@ -1136,7 +1150,7 @@ def bn_stats(x, partial=None):
 def bn_apply(x, sums, count, gamma, beta, eps, *, residual=None, relu=False, save=None, running=None,
              momentum=0.1, use_running=False):
     R, C = _rc(x)
-    y = torch.empty_like(x, memory_format=CL)
+    y = _empty(x.shape, x.dtype, x.device, True)
     sm, si = save if save is not None else (None, None)
     rm, rv = running if running is not None else (None, None)
     sp, parts = _stats(sums)
@@ -1189,7 +1203,7 @@ def bn_apply_dual(x, sums, count, gamma, beta, eps, other: BnDeferred, *, relu=F
     """act(bn(x) + other's BatchNorm output) in one pass (norm.hip bn_apply_dual)."""
     R, C = _rc(x)
     assert tuple(other.x.shape) == tuple(x.shape) and other.x.dtype == x.dtype == BF16
-    y = torch.empty_like(x, memory_format=CL)
+    y = _empty(x.shape, x.dtype, x.device, True)
     me = BnDeferred(x, sums, count, gamma, beta, eps, save, running, momentum, use_running)
     if not kernels().bn_apply_dual(me.side(), other.side(), y.data_ptr(), R, C, int(relu), stream_ptr()):
         raise RuntimeError("bn_apply_dual: unsupported shape")
@@ -1214,8 +1228,8 @@ def bn_relu_maxpool(x, sums, count, gamma, beta, eps, pool, *, save, running, mo
     N, C, H, W = x.shape
     ph, pw, sh, sw, pdh, pdw = pool
     OH, OW = pool_out_hw(H, W, ph, pw, sh, sw, pdh, pdw)
-    y = torch.empty((N, C, OH, OW), dtype=BF16, device=x.device, memory_format=CL)
-    idx = torch.empty((N, OH, OW, C), dtype=torch.uint8, device=x.device)
+    y = _empty((N, C, OH, OW), BF16, x.device, True)
+    idx = _empty((N, OH, OW, C), torch.uint8, x.device)
     sm, si = save
     rm, rv = running
     sp, parts = _stats(sums)
@@ -1239,11 +1253,11 @@ def bn_backward(dy, x, yout, mean, istd, gamma, dgamma, dbeta, *, want_masked=Fa
     if fused is not None and not eval_mode:
         slab, rows, sums = fused
         sp, parts = _stats(stat_reduce(1, slab, rows, C, sums))
-        dx = torch.empty_like(x, memory_format=CL)
+        dx = _empty(x.shape, x.dtype, x.device, True)
         K.bn_bwd_apply(dt, dy.data_ptr(), 0, x.data_ptr(), dx.data_ptr(), R, C, mean.data_ptr(), istd.data_ptr(),
                        ptr(gamma), sp, parts, float(R), ptr(dgamma), ptr(dbeta), 0, st)
         return dx, (dy if want_masked else None)
-    dmask = torch.empty_like(dy, memory_format=CL) if (want_masked and yout is not None) else None
+    dmask = _empty(dy.shape, dy.dtype, dy.device, True) if (want_masked and yout is not None) else None
     sums = None
     # the (sum dy', sum dy' * xhat) pass: the batch-statistics backward needs it, and so does a
     # frozen-statistics (eval-mode) backward that still accumulates the affine gradients or
@@ -1251,12 +1265,12 @@ def bn_backward(dy, x, yout, mean, istd, gamma, dgamma, dbeta, *, want_masked=Fa
     # uses them for dx only in training mode)
     if not eval_mode or dgamma is not None or dbeta is not None or dmask is not None:
         rows = K.bn_partial_rows(R, C)
-        slab = torch.empty((rows, 2, C), dtype=F32, device=x.device)
-        sums = torch.empty((2 * C,), dtype=F32, device=x.device)
+        slab = _empty((rows, 2, C), F32, x.device)
+        sums = _empty((2 * C,), F32, x.device)
         K.bn_partial(dt, x.data_ptr(), dy.data_ptr(), ptr(yout), ptr(dmask), mean.data_ptr(), istd.data_ptr(), R, C,
                      slab.data_ptr(), 1, 0, st)
         sums = stat_reduce(1, slab, rows, C, sums)
-    dx = torch.empty_like(x, memory_format=CL)
+    dx = _empty(x.shape, x.dtype, x.device, True)
     src = dmask if dmask is not None else dy
     sp, parts = _stats(sums)
     K.bn_bwd_apply(dt, src.data_ptr(), 0 if dmask is not None else ptr(yout), x.data_ptr(), dx.data_ptr(), R, C,
@@ -1267,9 +1281,9 @@ def bn_backward(dy, x, yout, mean, istd, gamma, dgamma, dbeta, *, want_masked=Fa
 
 def gn_fwd(x, groups, gamma, beta, eps):
     N, C, H, W = x.shape
-    y = torch.empty_like(x, memory_format=CL)
-    mean = torch.empty((N * groups,), dtype=F32, device=x.device)
-    istd = torch.empty_like(mean)
+    y = _empty(x.shape, x.dtype, x.device, True)
+    mean = _empty((N * groups,), F32, x.device)
+    istd = _empty_like(mean)
     kernels().gn_fwd(dt_code(x.dtype), x.data_ptr(), y.data_ptr(), N, H * W, C, groups, ptr(gamma), ptr(beta),
                      float(eps), mean.data_ptr(), istd.data_ptr(), stream_ptr())
     return y, mean, istd
@@ -1277,8 +1291,8 @@ def gn_fwd(x, groups, gamma, beta, eps):
 
 def gn_bwd(dy, x, groups, gamma, mean, istd, dgamma, dbeta):
     N, C, H, W = x.shape
-    dx = torch.empty_like(x, memory_format=CL)
-    aff = torch.empty((N, 2, C), dtype=F32, device=x.device)  # per-image affine partials
+    dx = _empty(x.shape, x.dtype, x.device, True)
+    aff = _empty((N, 2, C), F32, x.device)  # per-image affine partials
     kernels().gn_bwd(dt_code(x.dtype), dy.data_ptr(), x.data_ptr(), dx.data_ptr(), N, H * W, C, groups, ptr(gamma),
                      mean.data_ptr(), istd.data_ptr(), ptr(dgamma), ptr(dbeta), aff.data_ptr(), stream_ptr())
     return dx
@@ -1293,8 +1307,8 @@ def maxpool_fwd(x, ph, pw, sh, sw, pdh, pdw):
     _check_act(x, "maxpool")
     N, C, H, W = x.shape
     OH, OW = pool_out_hw(H, W, ph, pw, sh, sw, pdh, pdw)
-    y = torch.empty((N, C, OH, OW), dtype=x.dtype, device=x.device, memory_format=CL)
-    idx = torch.empty((N, OH, OW, C), dtype=torch.uint8, device=x.device)
+    y = _empty((N, C, OH, OW), x.dtype, x.device, True)
+    idx = _empty((N, OH, OW, C), torch.uint8, x.device)
     assert ph * pw <= 256
     kernels().maxpool_fwd(dt_code(x.dtype), x.data_ptr(), y.data_ptr(), idx.data_ptr(), N, H, W, C, OH, OW, ph, pw,
                           sh, sw, pdh, pdw, stream_ptr())
@@ -1308,15 +1322,15 @@ def maxpool_bwd(dy, idx, x_shape, ph, pw, sh, sw, pdh, pdw, *, ypool=None, bnb=N
     N, C, H, W = x_shape
     OH, OW = dy.shape[2], dy.shape[3]
     K = kernels()
-    dx = torch.empty((N, C, H, W), dtype=dy.dtype, device=dy.device, memory_format=CL)
+    dx = _empty((N, C, H, W), dy.dtype, dy.device, True)
     g = (N, H, W, C, OH, OW, ph, pw, sh, sw, pdh, pdw)
     # the kernel masks with (pooled value > 0): only valid when a ReLU sits between BN and pool
     if (bnb is not None and _BNB and _BNB_POOL and (bnb.y is not None or bnb.pooled) and ypool is not None and dy.dtype == BF16 and bnb.x.dtype == BF16
             and tuple(bnb.x.shape) == (N, C, H, W) and bnb.x.is_contiguous(memory_format=CL)
             and K.maxpool_bwd_bnb_supported(*g)):
         rows = K.maxpool_bwd_bnb_rows(*g)
-        slab = torch.empty((rows, 2, C), dtype=F32, device=dy.device)
-        sums = torch.empty((2 * C,), dtype=F32, device=dy.device)  # zeroed in-kernel
+        slab = _empty((rows, 2, C), F32, dy.device)
+        sums = _empty((2 * C,), F32, dy.device)  # zeroed in-kernel
         K.maxpool_bwd_bnb(dy.data_ptr(), idx.data_ptr(), ypool.data_ptr(), bnb.x.data_ptr(), bnb.mean.data_ptr(),
                           bnb.istd.data_ptr(), dx.data_ptr(), *g, slab.data_ptr(), sums.data_ptr(), stream_ptr())
         dx._bnb = (bnb.bn, slab, rows, sums)
@@ -1329,7 +1343,7 @@ def avgpool_fwd(x, ph, pw, sh, sw, pdh, pdw):
     _check_act(x, "avgpool")
     N, C, H, W = x.shape
     OH, OW = pool_out_hw(H, W, ph, pw, sh, sw, pdh, pdw)
-    y = torch.empty((N, C, OH, OW), dtype=x.dtype, device=x.device, memory_format=CL)
+    y = _empty((N, C, OH, OW), x.dtype, x.device, True)
     kernels().avgpool_fwd(dt_code(x.dtype), x.data_ptr(), y.data_ptr(), N, H, W, C, OH, OW, ph, pw, sh, sw, pdh, pdw,
                           stream_ptr())
     return y
@@ -1339,7 +1353,7 @@ def avgpool_bwd(dy, x_shape, ph, pw, sh, sw, pdh, pdw):
     N, C, H, W = x_shape
     OH, OW = dy.shape[2], dy.shape[3]
     dy = dy.contiguous(memory_format=CL)
-    dx = torch.empty((N, C, H, W), dtype=dy.dtype, device=dy.device, memory_format=CL)
+    dx = _empty((N, C, H, W), dy.dtype, dy.device, True)
     kernels().avgpool_bwd(dt_code(dy.dtype), dy.data_ptr(), dx.data_ptr(), N, H, W, C, OH, OW, ph, pw, sh, sw, pdh,
                           pdw, stream_ptr())
     return dx
@@ -1350,7 +1364,7 @@ ACT_CODES = {"relu": 0, "leaky_relu": 1, "elu": 2, "sigmoid": 3, "tanh": 4, "lin
 
 
 def act_fwd(x, kind, alpha=0.01):
-    y = torch.empty_like(x)
+    y = _empty_like(x)
     kernels().act_fwd(dt_code(x.dtype), x.data_ptr(), y.data_ptr(), x.numel(), ACT_CODES[kind], float(alpha),
                       stream_ptr())
     return y
@@ -1358,7 +1372,7 @@ def act_fwd(x, kind, alpha=0.01):
 
 def act_bwd(x, dy, kind, alpha=0.01):
     dy = dy.contiguous(memory_format=CL) if x.dim() == 4 and x.is_contiguous(memory_format=CL) else dy.contiguous()
-    dx = torch.empty_like(x)
+    dx = _empty_like(x)
     kernels().act_bwd(dt_code(x.dtype), x.data_ptr(), dy.data_ptr(), dx.data_ptr(), x.numel(), ACT_CODES[kind],
                       float(alpha), stream_ptr())
     return dx
@@ -1368,7 +1382,7 @@ def softmax_channels(x):
     """softmax over dim 1 of an NCHW-logical / NHWC-physical tensor (channel innermost)."""
     N, C = x.shape[0], x.shape[1]
     rows = x.numel() // C
-    y = torch.empty_like(x)
+    y = _empty_like(x)
     kernels().softmax_rows(dt_code(x.dtype), x.data_ptr(), y.data_ptr(), rows, C, stream_ptr())
     return y
 
@@ -1377,7 +1391,7 @@ def softmax_channels_bwd(y, dy):
     C = y.shape[1]
     rows = y.numel() // C
     dy = dy.contiguous(memory_format=CL) if y.dim() == 4 else dy.contiguous()
-    dx = torch.empty_like(y)
+    dx = _empty_like(y)
     kernels().softmax_rows_bwd(dt_code(y.dtype), y.data_ptr(), dy.data_ptr(), dx.data_ptr(), rows, C, stream_ptr())
     return dx
 
@@ -1385,7 +1399,7 @@ def softmax_channels_bwd(y, dy):
 def dropout(x, p, seed, slot=None):
     """Inverted dropout with a Philox mask of (seed, *slot). ``slot``: a 1-element int64 device
     tensor written by :func:`counter_bump` (graph-replay safe: the draw index lives on the device)."""
-    y = torch.empty_like(x)
+    y = _empty_like(x)
     kernels().dropout(dt_code(x.dtype), x.data_ptr(), y.data_ptr(), x.numel(), float(p), int(seed) & ((1 << 64) - 1),
                       ptr(slot), stream_ptr())
     return y
@@ -1407,7 +1421,7 @@ def loss_fused(pred2d, target2d=None, labels=None, kind="softmax_crossentropy", 
     is additionally multiplied by ``grad_scale`` inside the kernel (data parallel: 1 / world)."""
     N, C = pred2d.shape
     pred2d = pred2d.contiguous()
-    grad = torch.empty_like(pred2d) if want_grad else None
+    grad = _empty_like(pred2d) if want_grad else None
     loss = torch.empty((1,), dtype=F32, device=pred2d.device)
     correct = torch.empty((1,), dtype=torch.int32, device=pred2d.device)
     tgt = None
@@ -1415,7 +1429,7 @@ def loss_fused(pred2d, target2d=None, labels=None, kind="softmax_crossentropy", 
         tgt = target2d.reshape(N, C).to(F32).contiguous()
     lab = labels.to(torch.int64).contiguous() if labels is not None else None
     K = kernels()
-    ws = torch.empty((K.loss_workspace_floats(N),), dtype=F32, device=pred2d.device) if N > 4 else None
+    ws = _empty((K.loss_workspace_floats(N),), F32, pred2d.device) if N > 4 else None
     tk = _ticket(pred2d.device, 0, slot="loss") if N > 4 else None
     K.loss_fused(dt_code(pred2d.dtype), pred2d.data_ptr(), ptr(tgt), ptr(lab), ptr(grad), loss.data_ptr(),
                  correct.data_ptr(), N, C, LOSS_CODES[kind], float(param), float(grad_scale), ptr(ws), ptr(tk),
@@ -1458,7 +1472,7 @@ class WeightTransposer:
         for c in self.convs:
             w = c.weight_operand(0)
             Co, Ci, KH, KW = w.shape
-            c._wt_buf = torch.empty((Ci, KH, KW, Co), dtype=BF16, device=w.device)
+            c._wt_buf = _arena.persistent((Ci, KH, KW, Co), BF16, w.device)
             rows.append([w.data_ptr(), c._wt_buf.data_ptr(), Co, KH * KW, Ci])
             self.max_tiles = max(self.max_tiles, KH * KW * ((Co + 63) // 64) * ((Ci + 63) // 64))
         self.table = torch.tensor(rows, dtype=torch.int64).to(self.convs[0]._wt_buf.device) if rows else None
@@ -1479,7 +1493,7 @@ def im2col(x, kh, kw, sh, sw, ph, pw):
     N, C, H, W = x.shape
     OH, OW = conv_out_hw(H, W, kh, kw, sh, sw, ph, pw)
     x = x.contiguous().float()
-    col = torch.empty((C * kh * kw, N * OH * OW), dtype=F32, device=x.device)
+    col = _empty((C * kh * kw, N * OH * OW), F32, x.device)
     kernels().im2col(x.data_ptr(), col.data_ptr(), N, C, H, W, kh, kw, sh, sw, ph, pw, OH, OW, stream_ptr())
     return col
 
@@ -1487,7 +1501,7 @@ def im2col(x, kh, kw, sh, sw, ph, pw):
 def col2im(col, x_shape, kh, kw, sh, sw, ph, pw):
     N, C, H, W = x_shape
     OH, OW = conv_out_hw(H, W, kh, kw, sh, sw, ph, pw)
-    x = torch.empty((N, C, H, W), dtype=F32, device=col.device)
+    x = _empty((N, C, H, W), F32, col.device)
     kernels().col2im(col.contiguous().data_ptr(), x.data_ptr(), N, C, H, W, kh, kw, sh, sw, ph, pw, OH, OW,
                      stream_ptr())
     return x

@@ -42,6 +42,16 @@ class TrainStep:
         self.last_loss = None
         self.last_correct = None
         self._static_x = self._static_y = None
+        # native per-step activation arena (runtime/arena.py): every activation / slab /
+        # workspace of a step on the GPU; the captured graphs pin the chunks they address
+        from . import arena as _arena
+        dev = self.model.device
+        self.arena = (_arena.ActivationArena(dev.index) if _arena.enabled() and dev.is_gpu() else None)
+        self._pins = None
+
+    def _arena_step(self, capture=False):
+        import contextlib
+        return self.arena.step(capture=capture) if self.arena is not None else contextlib.nullcontext()
 
     def _loss_grad(self, out, y):
         """Loss, gradient already carrying the data-parallel 1 / world factor, correct count. A
@@ -57,11 +67,12 @@ class TrainStep:
 
     # ------------------------------------------------------------------ eager
     def eager(self, x, y):
-        self.opt.clear_gradients()
-        out = self.dp.forward(x)
-        loss, grad, correct = self._loss_grad(out, y)
-        self.dp.backward(grad, prescaled=True)
-        self.opt.update()
+        with self._arena_step():
+            self.opt.clear_gradients()
+            out = self.dp.forward(x)
+            loss, grad, correct = self._loss_grad(out, y)
+            self.dp.backward(grad, prescaled=True)
+            self.opt.update()
         self.last_loss, self.last_correct = loss, correct
         return loss
 
@@ -172,32 +183,38 @@ class TrainStep:
         if hasattr(self.opt, "t"):
             self.opt.t -= 1  # the capture itself is not a training step
         active = self.dp.active
-        for k, (hi, lo) in enumerate(segs):
-            g = torch.cuda.CUDAGraph()
-            with capture_guard(), torch.cuda.graph(g, pool=pool, stream=self._capture_stream()):
-                if k == 0:
-                    self.opt.clear_gradients()
-                    out = self.dp.forward(self._static_x)
-                    loss, cur, correct = self._loss_grad(out, self._static_y)
-                    self._g_loss, self._g_correct = loss, correct
-                    self.model.prepare_backward()
-                else:
-                    cur = self._carry
-                cur = self._run_bwd(cur, hi, lo)
-                self.model.flush_gradients()  # the bucket all-reduced after this segment is complete
-                self._carry = cur
-                if k == len(segs) - 1:
-                    self.model.finish_backward()
-                if not active and k == len(segs) - 1:
+        arena_scope = self._arena_step(capture=True)
+        arena_scope.__enter__()  # one arena step across the segments (segment k+1 reads k's carry)
+        try:
+            for k, (hi, lo) in enumerate(segs):
+                g = torch.cuda.CUDAGraph()
+                with capture_guard(), torch.cuda.graph(g, pool=pool, stream=self._capture_stream()):
+                    if k == 0:
+                        self.opt.clear_gradients()
+                        out = self.dp.forward(self._static_x)
+                        loss, cur, correct = self._loss_grad(out, self._static_y)
+                        self._g_loss, self._g_correct = loss, correct
+                        self.model.prepare_backward()
+                    else:
+                        cur = self._carry
+                    cur = self._run_bwd(cur, hi, lo)
+                    self.model.flush_gradients()  # the bucket all-reduced after this segment is complete
+                    self._carry = cur
+                    if k == len(segs) - 1:
+                        self.model.finish_backward()
+                    if not active and k == len(segs) - 1:
+                        self.opt.launch_step()
+                if pool is None:
+                    pool = g.pool()
+                self.graphs.append(g)
+            if active:
+                g = torch.cuda.CUDAGraph()
+                with capture_guard(), torch.cuda.graph(g, pool=pool, stream=self._capture_stream()):
                     self.opt.launch_step()
-            if pool is None:
-                pool = g.pool()
-            self.graphs.append(g)
-        if active:
-            g = torch.cuda.CUDAGraph()
-            with capture_guard(), torch.cuda.graph(g, pool=pool, stream=self._capture_stream()):
-                self.opt.launch_step()
-            self.graphs.append(g)
+                self.graphs.append(g)
+        finally:
+            arena_scope.__exit__(None, None, None)
+        self._pins = self.arena.pin() if self.arena is not None else None
         torch.cuda.synchronize()
 
     def _capture_whole(self):
@@ -210,7 +227,8 @@ class TrainStep:
         m.enable_profiling_ = False
         g = torch.cuda.CUDAGraph()
         try:
-            with capture_guard(), torch.cuda.graph(g, stream=self._capture_stream(), capture_error_mode="thread_local"):
+            with self._arena_step(capture=True), capture_guard(), \
+                    torch.cuda.graph(g, stream=self._capture_stream(), capture_error_mode="thread_local"):
                 self.opt.clear_gradients()
                 out = self.dp.forward(self._static_x)
                 loss, grad, correct = self._loss_grad(out, self._static_y)
@@ -219,6 +237,7 @@ class TrainStep:
                 self.opt.launch_step()
         finally:
             m.enable_profiling_ = prof
+        self._pins = self.arena.pin() if self.arena is not None else None
         self.graphs = [g]
         self._whole = True
         torch.cuda.synchronize()

@@ -1,0 +1,184 @@
+// Self-test of the C++ host API (run by tests/test_cpp_host_api.py; exit code 0 = pass):
+// layout traits, relayout, bf16 rounding, JSON round trip, tensor records, grow-only ensure,
+// config round trip through the layer factory, and a finite-difference gradient check of every
+// layer type on the CPU backend. With "--device GPU" it also checks the GPU backend's forward /
+// backward against the CPU backend on the same weights.
+#include <cmath>
+#include <cstdio>
+#include <sstream>
+#include <string>
+
+#include "dcnn/nn.hpp"
+
+using namespace dcnn;
+
+static int failures = 0;
+#define CHECK(c)                                                        \
+  do {                                                                  \
+    if (!(c)) {                                                         \
+      std::fprintf(stderr, "FAIL %s:%d: %s\n", __FILE__, __LINE__, #c); \
+      ++failures;                                                       \
+    }                                                                   \
+  } while (0)
+
+static void test_layout() {
+  using NHWC = LayoutTrait<Layout::NHWC>;
+  static_assert(NHWC::rank == 4 && NHWC::channels_last, "NHWC trait");
+  static_assert(LayoutTrait<Layout::NDHWC>::perm[4] == 1, "NDHWC keeps C innermost");
+  constexpr std::array<int64_t, 4> d{2, 3, 4, 5};
+  constexpr auto s = strides_of<Layout::NHWC>(d);
+  static_assert(s[1] == 1 && s[3] == 3 && s[2] == 15 && s[0] == 60, "NHWC strides");
+  static_assert(offset_of<Layout::NCHW>(d, {1, 2, 3, 4}) == 60 + 40 + 15 + 4, "NCHW offset");
+  static_assert(physical_dims<Layout::NHWC>(d)[3] == 3, "NHWC physical dims");
+  const auto s5 = layout_strides(Layout::NDHWC, {2, 3, 4, 5, 6});
+  CHECK(s5[1] == 1 && s5[4] == 3 && s5[3] == 18 && s5[2] == 90 && s5[0] == 360);
+  CHECK(layout_info(Layout::NCDHW).rank == 5 && !layout_info(Layout::NCDHW).channels_last);
+  std::vector<float> a(120), b(120), c(120);
+  for (int i = 0; i < 120; ++i) a[i] = (float)i;
+  relayout(a.data(), Layout::NCHW, b.data(), Layout::NHWC, {2, 3, 4, 5});
+  CHECK(b[1] == a[20]);  // NHWC element (n0, h0, w0, c1) = NCHW (0, 1, 0, 0)
+  relayout(b.data(), Layout::NHWC, c.data(), Layout::NCHW, {2, 3, 4, 5});
+  CHECK(a == c);
+}
+
+static void test_bf16_json_tensor() {
+  CHECK(bf16_to_f32(f32_to_bf16(1.0f)) == 1.0f);
+  CHECK(f32_to_bf16(1.00390625f) == 0x3f80);   // tie -> even
+  CHECK(f32_to_bf16(1.01171875f) == 0x3f82);   // tie -> even (odd below)
+  json::Value v = json::Value::object();
+  v["name"] = "m";
+  v["x"] = 1.5;
+  v["n"] = 3;
+  v["b"] = true;
+  json::Value arr = json::Value::array();
+  arr.push("a\"b");
+  arr.push(json::Value());
+  v["arr"] = arr;
+  const json::Value w = json::Value::parse(v.dump(2));
+  CHECK(w.at("x").as_number() == 1.5 && w.at("n").as_int() == 3 && w.at("b").as_bool());
+  CHECK(w.at("arr").items()[0].as_string() == "a\"b" && w.at("arr").items()[1].is_null());
+  CHECK(w.dump(0) == v.dump(0));
+
+  std::vector<float> vals(2 * 3 * 2 * 2);
+  for (size_t i = 0; i < vals.size(); ++i) vals[i] = 0.25f * (float)i - 1.f;
+  Tensor t = Tensor::from_host(vals, {2, 3, 2, 2}, Device::cpu(), DType::F32, Layout::NHWC);
+  CHECK(t.to_host_f32() == vals);  // logical order survives the NHWC storage
+  std::stringstream ss;
+  t.save(ss);
+  Tensor u = Tensor::load(ss);
+  CHECK(u.to_host_f32() == vals && u.shape() == t.shape());
+  Tensor g;
+  g.ensure({4, 4}, DType::F32, Device::cpu());
+  void* p0 = g.data();
+  g.ensure({2, 2}, DType::F32, Device::cpu());
+  CHECK(g.data() == p0 && g.numel() == 4);  // grow-only: no reallocation when smaller
+  g.ensure({8, 8}, DType::F32, Device::cpu());
+  CHECK(g.numel() == 64);
+}
+
+static Sequential small_model(bool with_bn) {
+  SequentialBuilder b("selftest");
+  b.input({2, 6, 6}).conv2d(4, 3, 3, 1, 1, 1, 1);
+  if (with_bn) b.batchnorm();
+  b.activation("tanh").maxpool2d(2, 2).conv2d(3, 2, 2, 1, 1, 0, 0).activation("elu").avgpool2d(2, 2, 1, 1)
+      .flatten().dense(5);
+  return b.build();
+}
+
+static double loss_of(Sequential& m, const Tensor& x, const Tensor& y) {
+  return softmax_cross_entropy(m.forward(x), y).loss;
+}
+
+// central differences of the mean loss against the analytic gradients (fp32 CPU backend)
+static void test_gradcheck(bool with_bn) {
+  Sequential m = small_model(with_bn);
+  m.initialize(3);
+  SyntheticClassification src(4, 2, 6, 6, 5, 11, 1.0f);
+  src.reset(0);
+  Tensor x, y;
+  src.next(4, x, y);
+  m.set_training(true);
+  m.zero_grad();
+  auto r = softmax_cross_entropy(m.forward(x), y);
+  m.backward(r.grad);
+  double worst = 0;
+  int checked = 0;
+  for (auto* p : m.parameters()) {
+    float* v = p->value.ptr<float>();
+    const float* g = p->grad.ptr<float>();
+    const int64_t n = p->value.numel();
+    for (int64_t i = 0; i < n; i += std::max<int64_t>(1, n / 6)) {
+      const float keep = v[i], h = 1e-3f;
+      v[i] = keep + h;
+      const double lp = loss_of(m, x, y);
+      v[i] = keep - h;
+      const double lm = loss_of(m, x, y);
+      v[i] = keep;
+      const double num = (lp - lm) / (2.0 * h);
+      const double err = std::abs(num - g[i]) / std::max(1e-3, std::abs(num) + std::abs((double)g[i]));
+      worst = std::max(worst, err);
+      if (err > 5e-2) std::printf("  %s[%ld] num %.6g ana %.6g\n", p->name.c_str(), (long)i, num, (double)g[i]);
+      ++checked;
+    }
+  }
+  std::printf("gradcheck (bn=%d): %d entries, worst rel err %.3g\n", (int)with_bn, checked, worst);
+  CHECK(checked > 20 && worst < 5e-2);
+}
+
+static void test_config_roundtrip() {
+  Sequential m = small_model(true);
+  const json::Value c = m.get_config();
+  Sequential n = Sequential::load_from_config(json::Value::parse(c.dump(4)));
+  CHECK(n.get_config().dump(0) == c.dump(0));
+  CHECK(n.layers().size() == m.layers().size());
+}
+
+// GPU backend vs CPU backend on identical weights (bf16 activations: loose tolerance)
+static void test_gpu_vs_cpu() {
+  Sequential c = small_model(true), g = small_model(true);
+  c.initialize(5);
+  g.set_device(Device::gpu(0));
+  g.initialize(5);
+  SyntheticClassification src(16, 2, 6, 6, 5, 13, 1.0f);
+  src.reset(0);
+  Tensor x, y;
+  src.next(16, x, y);
+  auto rc = softmax_cross_entropy(c.forward(x), y);
+  auto rg = softmax_cross_entropy(g.forward(x), y);
+  std::printf("gpu vs cpu loss %.5f %.5f\n", rg.loss, rc.loss);
+  CHECK(std::abs(rg.loss - rc.loss) < 2e-2 * std::max(1.0, std::abs(rc.loss)));
+  c.zero_grad();
+  g.zero_grad();
+  c.backward(rc.grad);
+  g.backward(rg.grad);
+  auto pc = c.parameters(), pg = g.parameters();
+  for (size_t k = 0; k < pc.size(); ++k) {
+    const auto a = pc[k]->grad.view(pc[k]->shape, pc[k]->layout).to_host_f32();
+    const auto b = pg[k]->grad.view(pg[k]->shape, pg[k]->layout).to_host_f32();
+    double num = 0, den = 0;
+    for (size_t i = 0; i < a.size(); ++i) {
+      num += (double)(a[i] - b[i]) * (a[i] - b[i]);
+      den += (double)a[i] * a[i];
+    }
+    const double rel = std::sqrt(num / std::max(den, 1e-30));
+    std::printf("  grad %s/%s rel l2 %.3g\n", c.layers()[0]->name().c_str(), pc[k]->name.c_str(), rel);
+    CHECK(rel < 5e-2);
+  }
+}
+
+int main(int argc, char** argv) {
+  const bool gpu = argc > 2 && std::string(argv[1]) == "--device" && std::string(argv[2]) == "GPU";
+  try {
+    test_layout();
+    test_bf16_json_tensor();
+    test_config_roundtrip();
+    test_gradcheck(false);
+    test_gradcheck(true);
+    if (gpu) test_gpu_vs_cpu();
+  } catch (const std::exception& e) {
+    std::fprintf(stderr, "exception: %s\n", e.what());
+    return 1;
+  }
+  std::printf("%s (%d failures)\n", failures ? "FAILED" : "OK", failures);
+  return failures ? 1 : 0;
+}

@@ -1,0 +1,115 @@
+"""C++ host API (csrc/host, examples/cpp): a C++ program builds, trains, saves and reloads a
+model; the saved files load in the Python front end and give the same logits; the self-test
+covers the layout traits, tensor records, the JSON config round trip and a finite-difference
+gradient check of every layer type. GPU variants run the same programs on the HIP backend."""
+import os
+import re
+import subprocess
+
+import numpy as np
+import pytest
+import torch
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+BIN = os.path.join(ROOT, "dcnn_amd", "bin")
+
+
+NAMES = ("host_api_selftest", "mnist_cnn_trainer")
+
+
+@pytest.fixture(scope="module")
+def host_bins():
+    have = all(os.path.exists(os.path.join(BIN, n)) for n in NAMES)
+    if not (have and torch.cuda.is_available()):
+        # (on a GPU box the in-tree binaries built here are used as shipped: the object cache
+        # under build/ does not travel, and nothing is compiled inside a GPU run)
+        from dcnn_amd import _build
+        _build.build_host()
+    return {n: os.path.join(BIN, n) for n in NAMES}
+
+
+def _run(cmd, cwd, timeout=600):
+    r = subprocess.run(cmd, cwd=cwd, stdout=subprocess.PIPE, stderr=subprocess.STDOUT, text=True, timeout=timeout)
+    return r.returncode, r.stdout
+
+
+def _result(out):
+    m = re.search(r"RESULT first_loss=(\S+) last_loss=(\S+) val_acc=(\S+) reload_diff=(\S+)", out)
+    assert m, out[-2000:]
+    return [float(v) for v in m.groups()]
+
+
+def test_selftest_cpu(host_bins, tmp_path):
+    rc, out = _run([host_bins["host_api_selftest"]], tmp_path)
+    assert rc == 0, out
+    assert "OK (0 failures)" in out
+
+
+def test_cpp_trainer_cpu_and_python_interop(host_bins, tmp_path):
+    rc, out = _run([host_bins["mnist_cnn_trainer"], "--device", "CPU", "--epochs", "2", "--steps", "25",
+                    "--batch", "32", "--save", "snap/mnist"], tmp_path)
+    assert rc == 0, out
+    first, last, val_acc, reload_diff = _result(out)
+    assert last < first and reload_diff == 0.0
+    # the C++-saved model in the Python front end: same architecture, weights, BN statistics
+    from dcnn_amd.nn.sequential import Sequential, load_tensor
+    m = Sequential.from_file(str(tmp_path / "snap" / "mnist"))
+    assert [l.type() for l in m.layers][:3] == ["conv2d", "batchnorm", "activation"]
+    m.set_training(False)
+    with open(tmp_path / "snap" / "mnist.probe_x.bin", "rb") as f:
+        x = load_tensor(f).reshape(8, 1, 28, 28)
+    with torch.no_grad():
+        logits = m.forward(x).reshape(8, -1).double().numpy()
+    ref = np.loadtxt(tmp_path / "snap" / "mnist.probe.txt").reshape(8, -1)
+    rel = np.linalg.norm(logits - ref) / np.linalg.norm(ref)
+    assert rel < 1e-4, rel
+
+
+def test_python_saved_model_loads_in_cpp(host_bins, tmp_path):
+    """Python -> C++: a model saved by the Python front end reloads in the C++ API (selftest of
+    the reverse direction through the trainer's from_file path is covered above; here the C++
+    factory parses the Python JSON)."""
+    from dcnn_amd.nn.sequential import SequentialBuilder
+    b = SequentialBuilder("py_model")
+    m = (b.input([1, 28, 28]).conv2d(8, 3, 3, 1, 1, 1, 1).batchnorm().activation("relu").maxpool2d(2, 2)
+         .flatten().dense(10).build())
+    m.initialize()
+    m.save_to_file(str(tmp_path / "py" / "model"))
+    src = tmp_path / "load.cpp"
+    src.write_text(r'''
+#include <cstdio>
+#include "dcnn/nn.hpp"
+int main() {
+  auto m = dcnn::Sequential::from_file("py/model");
+  std::printf("layers %zu params %zu\n", m.layers().size(), m.num_parameters());
+  return m.layers().size() == 6 ? 0 : 1;
+}
+''')
+    inc = os.path.join(ROOT, "dcnn_amd", "csrc", "host")
+    lib = os.path.join(ROOT, "dcnn_amd")
+    rc, out = _run(["g++", "-std=c++17", "-O1", f"-I{inc}", str(src), "-o", str(tmp_path / "load"), f"-L{lib}",
+                    "-ldcnn", f"-Wl,-rpath,{lib}", "-L/opt/rocm/lib", "-lamdhip64", "-Wl,-rpath,/opt/rocm/lib"],
+                   tmp_path)
+    assert rc == 0, out
+    rc, out = _run([str(tmp_path / "load")], tmp_path)
+    assert rc == 0, out
+    n = sum(p.numel() for p in m.parameters())
+    assert f"params {n}" in out, out
+
+
+@pytest.mark.gpu
+def test_selftest_gpu_matches_cpu_backend(host_bins, tmp_path):
+    rc, out = _run([host_bins["host_api_selftest"], "--device", "GPU"], tmp_path, timeout=300)
+    assert rc == 0, out
+    assert "gpu vs cpu loss" in out
+
+
+@pytest.mark.gpu
+def test_cpp_trainer_gpu(host_bins, tmp_path):
+    rc, out = _run([host_bins["mnist_cnn_trainer"], "--device", "GPU", "--epochs", "2", "--steps", "40",
+                    "--batch", "64", "--save", "snap/mnist"], tmp_path, timeout=300)
+    assert rc == 0, out
+    first, last, val_acc, reload_diff = _result(out)
+    assert last < first and reload_diff == 0.0
+    m = re.search(r"GPU vs CPU logits: rel l2 (\S+)", out)
+    assert m and float(m.group(1)) < 5e-2, out[-1500:]
