@@ -194,10 +194,13 @@ class Allocator {
 
   uintptr_t allocate(uint64_t nbytes, const Flow& f) {
     if (nbytes == 0) nbytes = 1;
-    // dropped DLPack exports are reclaimed in batches only (the reclaim synchronises the device):
-    // one allocation no longer drains every stream — other pipeline stages mid-step or mid-capture
-    // keep running — until the queue holds >= 256 MiB or 256 buffers
-    if (deferred_bytes_ >= (256ull << 20) || deferred_.size() >= 256) release_deferred();
+    // dropped DLPack exports are reclaimed only when that can serve this request from the pool
+    // (the queue holds at least nbytes) or the queue is large (>= 256 MiB / 256 buffers): the
+    // reclaim synchronises the device, so small allocations next to a few small pending frees do
+    // not drain every stream (other pipeline stages mid-step keep running)
+    if (deferred_bytes_ >= std::max<uint64_t>(nbytes, 1) || deferred_bytes_ >= (256ull << 20) ||
+        deferred_.size() >= 256)
+      release_deferred();
     DeviceGuard g(dev_);
     const uint64_t before = reserved();
     void* p = nullptr;

@@ -15,18 +15,22 @@ def _setup(arena_on, batch=32, seed=5):
     from dcnn_amd.nn import Adam, LossFactory
     from dcnn_amd.runtime import arena
     from dcnn_amd.runtime.step import TrainStep
-    arena.set_enabled(arena_on)
-    try:
-        m = zoo.create_model("resnet18_tiny_imagenet")
-        m.set_seed(seed)
-        m.set_device("GPU:0")
-        m.initialize()
-        m.set_first_layer_input_grad(False)
-        opt = Adam(1e-3)
-        opt.attach(m)
-        return m, opt, LossFactory.create("softmax_crossentropy"), TrainStep
-    finally:
-        arena.set_enabled(True)
+
+    def make_step(*a, **k):
+        arena.set_enabled(arena_on)
+        try:
+            return TrainStep(*a, **k)
+        finally:
+            arena.set_enabled(True)
+
+    m = zoo.create_model("resnet18_tiny_imagenet")
+    m.set_seed(seed)
+    m.set_device("GPU:0")
+    m.initialize()
+    m.set_first_layer_input_grad(False)
+    opt = Adam(1e-3)
+    opt.attach(m)
+    return m, opt, LossFactory.create("softmax_crossentropy"), make_step
 
 
 def _data(batch, seed=11):

