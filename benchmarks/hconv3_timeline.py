@@ -21,9 +21,12 @@ def main():
     ap.add_argument("--batch", type=int, default=256)
     ap.add_argument("--shapes", default="l1.c,l2.c,l3.c,l4.c")
     ap.add_argument("--op", default="fwd", choices=["fwd", "dgrad"])
+    ap.add_argument("--stagger", type=int, default=-1)
     a = ap.parse_args()
     from dcnn_amd.ops import hip
     K = hip.kernels()
+    if a.stagger >= 0:
+        K.hconv3_set_stagger(a.stagger)
     CL = torch.channels_last
     N = a.batch
     for nm in a.shapes.split(","):
@@ -46,10 +49,25 @@ def main():
         fn()
         torch.cuda.synchronize()
         K.hconv3_set_stamps(0)
-        t = buf.view(grid * 8, 8).cpu().double()
-        t0 = t[:, 0].min()
+        raw = buf.view(grid, 8, 8).cpu()
+        arr = raw[:, 0, 6]
+        if int(arr.abs().sum()) != 0:
+            # stagger diagnostics: workgroups per hardware CU key, arrival index histogram
+            keys = (arr >> 8).tolist()
+            olds = (arr & 0xff).tolist()
+            per = {}
+            for kk in keys:
+                per[kk] = per.get(kk, 0) + 1
+            hist = {}
+            for o in olds:
+                hist[o] = hist.get(o, 0) + 1
+            print(f"   stagger: {len(per)} CU keys, workgroups/key min {min(per.values())} max {max(per.values())}, "
+                  f"arrival index histogram {dict(sorted(hist.items()))}")
+            raw[:, 0, 6] = 0
+        t = raw.view(grid * 8, 8).double()
         live = t[:, 0] > 0
         t = t[live]
+        t0 = t[:, 0].min()
         ph = {"prologue": t[:, 1] - t[:, 0], "chunk0": t[:, 2] - t[:, 1], "kloop_rest": t[:, 3] - t[:, 2],
               "epilogue": t[:, 4] - t[:, 3], "stats": t[:, 5] - t[:, 4], "wave_total": t[:, 5] - t[:, 0]}
         print(f"{nm} {a.op} batch {N}: grid {grid}, waves stamped {int(live.sum())}, "

@@ -117,6 +117,9 @@ struct H3Geo {
   int nchunk;              // 32-channel chunks per split
   int tb[9];               // weight column offset (elements) of tap (dy + 1) * 3 + (dx + 1)
   int halo_bytes;          // bytes of one halo buffer (= 8 waves x HN x 1 KiB)
+  int stagger;             // s_sleep(127) count of the second workgroup to arrive on a CU
+  unsigned* cu_ctr;        // [2048] per-CU arrival counters + [1] exit ticket (stagger), or null
+  int dbg;                 // diagnostic ablations (DCNN_HCONV3_DBG): 1 = no output stores, 2 = no statistics
   unsigned long long* stamps;  // diagnostic: per-wave s_memtime at 8 points (hconv3_set_stamps), or null
 };
 
@@ -156,6 +159,30 @@ __global__ void __launch_bounds__(NW * 64, 8 / NW) hconv3_kernel(HConvArgs p, H3
     if (g.stamps && lane == 0) g.stamps[((size_t)blockIdx.x * 8 + wid) * 8 + k] = __builtin_amdgcn_s_memtime();
   };
   stamp(0);
+  // Phase shift of co-resident workgroups: the workgroups of a round run prologue (halo read),
+  // K loop and epilogue (output write) in lockstep, so the memory phases are chip-wide bursts
+  // during which the MFMAs idle. The second workgroup to arrive on each CU in a launch starts
+  // `stagger` x 8K cycles late, so the pair alternates memory and MFMA phases (later rounds
+  // inherit the offset: a replacement arrives when its predecessor leaves). Arrival order comes
+  // from counters keyed by the hardware CU id (XCC, SE, SH, CU); the grid's last workgroup
+  // resets them for the next launch.
+  const bool stag = g.stagger > 0 && g.cu_ctr;
+  if (stag) {
+    volatile int* flag = reinterpret_cast<volatile int*>(smem + T::HALO - 32);
+    if (tid == 0) {
+      const unsigned hw = __builtin_amdgcn_s_getreg((31 << 11) | 4);   // HW_REG_HW_ID
+      const unsigned xcc = __builtin_amdgcn_s_getreg((3 << 11) | 20);  // HW_REG_XCC_ID
+      const unsigned key = ((xcc & 7u) << 8) | (((hw >> 13) & 7u) << 5) | (((hw >> 12) & 1u) << 4) | ((hw >> 8) & 15u);
+      const unsigned old = __hip_atomic_fetch_add(g.cu_ctr + key, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      *flag = (int)(old == 1u);
+      if (g.stamps) g.stamps[((size_t)blockIdx.x * 8) * 8 + 6] = ((unsigned long long)key << 8) | old;
+    }
+    __syncthreads();
+    const int late = *flag;
+    __syncthreads();  // (the flag lives in halo buffer 0, which the prologue overwrites)
+    if (late)
+      for (int k = 0; k < g.stagger; ++k) __builtin_amdgcn_s_sleep(127);
+  }
   const int SPL = p.splits;
   const int u0 = xcd_remap3(blockIdx.x, gridDim.x);
   const int zs = u0 % SPL, lt = u0 / SPL;
@@ -465,7 +492,7 @@ __global__ void __launch_bounds__(NW * 64, 8 / NW) hconv3_kernel(HConvArgs p, H3
       bf16* ob = reinterpret_cast<bf16*>(&o);
 #pragma unroll
       for (int r = 0; r < 4; ++r) ob[r] = (bf16)f[r];
-      *reinterpret_cast<uint2*>(crow[j] + nl + i * 16) = o;
+      if (!(g.dbg & 1)) *reinterpret_cast<uint2*>(crow[j] + nl + i * 16) = o;
       const bf16* xb = reinterpret_cast<const bf16*>(&xx[i][j]);
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
@@ -473,7 +500,7 @@ __global__ void __launch_bounds__(NW * 64, 8 / NW) hconv3_kernel(HConvArgs p, H3
         xh[j][r] = gv[j][r] * (((float)xb[r] - mu[i][r]) * is[i][r]);
       }
     }
-    if (stats) {
+    if (stats && !(g.dbg & 2)) {
       float pv[4], sa[4], sb[4];
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
@@ -527,6 +554,18 @@ __global__ void __launch_bounds__(NW * 64, 8 / NW) hconv3_kernel(HConvArgs p, H3
     }
   }
   stamp(5);
+  if (stag) {
+    __syncthreads();
+    volatile int* flag = reinterpret_cast<volatile int*>(smem + T::HALO - 32);
+    if (tid == 0) {
+      const unsigned done = __hip_atomic_fetch_add(g.cu_ctr + 2048, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      *flag = (int)(done == gridDim.x - 1);
+    }
+    __syncthreads();
+    if (*flag) {  // every workgroup has arrived: counters back to zero for the next launch
+      for (int i = tid; i <= 2048; i += NT) __hip_atomic_store(g.cu_ctr + i, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+  }
 }
 
 // ------------------------------------------------------------------------------------------------
@@ -540,6 +579,15 @@ static int g_h3 = [] {
 }();
 void hconv3_enable(int on) { g_h3 = on; }
 static unsigned long long* g_h3_stamps = nullptr;
+static int g_h3_dbg = [] {
+  const char* e = getenv("DCNN_HCONV3_DBG");
+  return e ? atoi(e) : 0;
+}();
+static int g_h3_stagger = [] {
+  const char* e = getenv("DCNN_HCONV3_STAGGER");
+  return e ? atoi(e) : 0;
+}();
+void hconv3_set_stagger(int sleeps) { g_h3_stagger = sleeps; }
 void hconv3_set_stamps(uintptr_t p) { g_h3_stamps = reinterpret_cast<unsigned long long*>(p); }
 
 struct H3Plan {
@@ -614,7 +662,20 @@ bool hconv3_try(const HConvArgs& a0, hipStream_t s) {
   g.nchunk = a.Cs / 32 / pl.splits;
   g.halo_bytes = 4 * pl.HN * 1024;
   g.stamps = g_h3_stamps;
+  g.dbg = g_h3_dbg;
   const int grid = pl.tiles_m * pl.tiles_n * pl.splits;
+  static unsigned* ctr = nullptr;
+  if (pl.splits == 1 && g_h3_stagger > 0) {
+    hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+    DCNN_HIP_CHECK(hipStreamIsCapturing(s, &cs));
+    if (!ctr && cs == hipStreamCaptureStatusNone) {  // (never allocated inside a capture)
+      DCNN_HIP_CHECK(hipMalloc(&ctr, 2049 * sizeof(unsigned)));
+      DCNN_HIP_CHECK(hipMemset(ctr, 0, 2049 * sizeof(unsigned)));
+      DCNN_HIP_CHECK(hipDeviceSynchronize());
+    }
+    g.cu_ctr = ctr;
+    g.stagger = ctr ? g_h3_stagger : 0;
+  }
   launch_h3_plan(pl, a, g, grid, s);
   return true;
 }

@@ -693,12 +693,18 @@ class _DeferredReduce:
     def __init__(self):
         self.active = False
         self.pending = []  # (slab, out, n, splits) — tensors kept alive until the launch
+        self.pending_bytes = 0
 
     def begin(self):
         self.active = _DEFER_REDUCE
 
     def add(self, slab, out, n, splits):
         self.pending.append((slab, out, int(n), int(splits)))
+        self.pending_bytes += int(n) * int(splits) * 4
+        # a queue larger than the last-level cache would read its first slabs back from HBM:
+        # launch once the pending slabs reach the threshold (DCNN_DEFER_REDUCE_MB)
+        if self.pending_bytes >= _DEFER_REDUCE_BYTES:
+            self.flush()
 
     def flush(self):
         if self.pending:
@@ -709,6 +715,7 @@ class _DeferredReduce:
                 kernels().multi_splitk_reduce([(t[0].data_ptr(), t[1].data_ptr(), t[2], t[3])
                                                for t in self.pending], stream_ptr())
             self.pending.clear()
+            self.pending_bytes = 0
 
     def end(self):
         self.flush()
@@ -716,6 +723,7 @@ class _DeferredReduce:
 
 
 _DEFER_REDUCE = os.environ.get("DCNN_DEFER_REDUCE", "1") != "0"
+_DEFER_REDUCE_BYTES = int(float(os.environ.get("DCNN_DEFER_REDUCE_MB", "1e9")) * (1 << 20))
 _tls = threading.local()
 
 

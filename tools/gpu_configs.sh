@@ -10,6 +10,8 @@ E=gpurun_out/configs_$TAG.err; : > $E
 run() { echo "== $*" >> $E; timeout -k 10 240 "$@" > gpurun_out/cur.out 2>>$E; rc=$?; grep '^{' gpurun_out/cur.out >> $O; return $rc; }
 run python bench.py --model resnet9_cifar10 --dtype fp32 --batch 128 --steps 30 --warmup 5 || exit $?
 run python bench.py --model resnet9_cifar10 --dtype fp32 --batch 256 --steps 30 --warmup 5 || exit $?
+run python bench.py --model resnet9_cifar10 --dtype fp32 --f32-mode exact --batch 128 --steps 30 --warmup 5 || exit $?
+run python bench.py --model resnet18_tiny_imagenet --dtype fp32 --f32-mode exact --batch 256 --steps 20 --warmup 5 || exit $?
 run python bench.py --model resnet9_cifar10 --dtype bf16 --batch 256 --steps 30 --warmup 5 || exit $?
 run python bench.py --model resnet18_tiny_imagenet --dtype fp32 --batch 256 --steps 20 --warmup 5 || exit $?
 run python bench.py --model resnet50_tiny_imagenet --dtype bf16 --batch 256 --steps 20 --warmup 5 || exit $?
