@@ -29,6 +29,26 @@ SHAPES = [
     ("l4.proj", 256, 8, 8, 512, 1, 2, 0),
 ]
 
+# ResNet-50-tiny bottleneck shapes (64x64 input, stride-2 max-pool stem: layer 1 at 32x32);
+# --set r50 (include/nn/example_models.hpp:369-402 block structure)
+SHAPES_R50 = [
+    ("r1.c1a", 64, 32, 32, 64, 1, 1, 0),     # layer1_block1 1x1 reduce (64 in)
+    ("r1.c1", 256, 32, 32, 64, 1, 1, 0),     # layer1 1x1 reduce
+    ("r1.c2", 64, 32, 32, 64, 3, 1, 1),      # layer1 3x3
+    ("r1.c3", 64, 32, 32, 256, 1, 1, 0),     # layer1 1x1 expand
+    ("r2.c1", 512, 16, 16, 128, 1, 1, 0),
+    ("r2.c2", 128, 16, 16, 128, 3, 1, 1),
+    ("r2.c3", 128, 16, 16, 512, 1, 1, 0),
+    ("r2.s2", 128, 32, 32, 128, 3, 2, 1),    # layer2_block1 strided 3x3
+    ("r2.proj", 256, 32, 32, 512, 1, 2, 0),
+    ("r3.c1", 1024, 8, 8, 256, 1, 1, 0),
+    ("r3.c2", 256, 8, 8, 256, 3, 1, 1),
+    ("r3.c3", 256, 8, 8, 1024, 1, 1, 0),
+    ("r4.c1", 2048, 4, 4, 512, 1, 1, 0),
+    ("r4.c2", 512, 4, 4, 512, 3, 1, 1),
+    ("r4.c3", 512, 4, 4, 2048, 1, 1, 0),
+]
+
 
 def main():
     ap = argparse.ArgumentParser()
@@ -36,6 +56,7 @@ def main():
     ap.add_argument("--iters", type=int, default=20)
     ap.add_argument("--only", default="")
     ap.add_argument("--shapes", default="", help="comma-separated shape names (default: all)")
+    ap.add_argument("--set", default="r18", choices=["r18", "r50"], help="ResNet-18-tiny or ResNet-50-tiny shapes")
     ap.add_argument("--v3", type=int, default=1, help="third-generation 3x3 halo conv (hconv3.hip) on/off")
     ap.add_argument("--eager", action="store_true", help="time eager launches instead of one hipGraph replay")
     ap.add_argument("--stagger", type=int, default=-1, help="hconv3 co-resident phase shift (s_sleep count; -1: default)")
@@ -47,9 +68,9 @@ def main():
     CL = torch.channels_last
     N = a.batch
     tot = {"fwd": 0.0, "dgrad": 0.0, "wgrad": 0.0}
-    print(f"{'shape':<10}{'op':<7}{'us':>9}{'TFLOP/s':>9}")
+    print(f"{'shape':<10}{'op':<7}{'us':>9}{'TFLOP/s':>9}{'TB/s':>7}")
     keep = set(a.shapes.split(",")) if a.shapes else None
-    for (nm, Ci, H, W, Co, k, s, p) in SHAPES:
+    for (nm, Ci, H, W, Co, k, s, p) in (SHAPES_R50 if a.set == "r50" else SHAPES):
         if keep is not None and nm not in keep:
             continue
         x = torch.randn(N, Ci, H, W, device="cuda").bfloat16().contiguous(memory_format=CL)
@@ -63,6 +84,10 @@ def main():
         gw = torch.zeros(Co, Ci, k, k, device="cuda").contiguous(memory_format=CL)
         wt = hip.conv_weight_t(w)
         flops = 2.0 * N * OH * OW * Co * Ci * k * k
+        # compulsory HBM bytes (bf16 operands read once, result written once; wgrad: fp32 result)
+        hbm = {"fwd": 2.0 * (N * H * W * Ci + N * OH * OW * Co + Co * Ci * k * k),
+               "dgrad": 2.0 * (N * H * W * Ci + N * OH * OW * Co + Co * Ci * k * k),
+               "wgrad": 2.0 * (N * H * W * Ci + N * OH * OW * Co) + 4.0 * Co * Ci * k * k}
         ops = {
             "fwd": lambda: hip.conv2d_fwd(x, wf, None, (s, s), (p, p), stats=True),
             "dgrad": lambda: hip.conv2d_dgrad(dy, wt, x.shape, (s, s), (p, p)),
@@ -100,7 +125,7 @@ def main():
             torch.cuda.synchronize()
             us = e0.elapsed_time(e1) * 1000 / a.iters
             tot[op] += us
-            print(f"{nm:<10}{op:<7}{us:9.1f}{flops / us / 1e6:9.1f}")
+            print(f"{nm:<10}{op:<7}{us:9.1f}{flops / us / 1e6:9.1f}{hbm[op] / us / 1e6:7.2f}")
     print("totals (us, one pass over the shapes):", {k: round(v, 1) for k, v in tot.items()})
 
 

@@ -12,7 +12,6 @@ import math
 from typing import List, Optional
 
 import torch
-import torch.nn.functional as F
 
 from ..params import ParamSpec
 from .base import LayerConfig, ParameterizedLayer

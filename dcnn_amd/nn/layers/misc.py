@@ -10,7 +10,6 @@ from __future__ import annotations
 import random
 
 import torch
-import torch.nn.functional as F
 
 from ..activations import ActivationFactory
 from .base import LayerConfig, StatelessLayer
