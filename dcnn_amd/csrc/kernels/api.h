@@ -117,6 +117,12 @@ void gemm_g2(const G2Args& a, hipStream_t s);
 int gemm_g2_stat_rows(int M, int N);
 int gemm_g2_row_tile(int M, int N);  // BM the launcher picks for an M x N output
 void gemm_t2(T2Args a, int splits, hipStream_t s);
+// streaming 1x1 conv (g1s.hip): mode 0 plain, 1 forward + Welford statistics, 2 dgrad + bnb sums
+int g1s_rows(int M, int N, int K, int mode);
+void g1s_enable(int on);
+void g1s(const bf16* X, const bf16* Wt, bf16* Y, int M, int N, int K, int H, int W, int OH, int OW, int S,
+         const float* bias, const bf16* residual, float* stats, int relu, float* zero_ptr, int zero_n, BnbArgs bnb,
+         int mode, hipStream_t s);
 int gemm_t2_splits(int M, int N, int P);
 int gemm_nt_stat_rows(int M, int N);
 // generic tensor ops (ops.hip)

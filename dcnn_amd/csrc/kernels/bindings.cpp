@@ -199,6 +199,16 @@ PYBIND11_MODULE(_kernels, m) {
   // grouped row classes (strided-dgrad phases in one launch): classes = (first tap, taps, ORY, ORX)
   m.def("gemm_g2_grouped", &bind_gemm_g2);
   m.def("gemm_g2_stat_rows", &gemm_g2_stat_rows);
+  m.def("g1s_rows", &g1s_rows);
+  m.def("g1s_enable", &g1s_enable);
+  m.def("g1s", [](uintptr_t X, uintptr_t Wt, uintptr_t Y, int M, int N, int K, int H, int W, int OH, int OW, int stride,
+                  uintptr_t bias, uintptr_t residual, uintptr_t stats, int relu, uintptr_t zero_ptr, int zero_n,
+                  std::array<uintptr_t, 4> bnb, int mode, uintptr_t stream) {
+    g1s(P<const bf16*>(X), P<const bf16*>(Wt), P<bf16*>(Y), M, N, K, H, W, OH, OW, stride, P<const float*>(bias),
+        P<const bf16*>(residual), P<float*>(stats), relu, P<float*>(zero_ptr), zero_n,
+        BnbArgs{P<const bf16*>(bnb[0]), P<const bf16*>(bnb[1]), P<const float*>(bnb[2]), P<const float*>(bnb[3])},
+        mode, S(stream));
+  });
   m.def("gemm_g2_row_tile", &gemm_g2_row_tile);
   m.def("gemm_t2",
         [](uintptr_t dY, uintptr_t X, uintptr_t slab, uintptr_t bias_slab, unsigned a_bytes, unsigned b_bytes, int M,

@@ -1,0 +1,353 @@
+// Streaming 1x1 convolution (and its stride-1 data gradient) for CDNA4: wave-independent,
+// weight-stationary, no barriers (LDS only for per-wave channel constants).
+//
+// Why (profiles/conv_r50_r3.md): the 1x1 convs of a ResNet bottleneck have K = 64..128 input
+// channels, so the gathered GEMM (gemm2.hip) runs ONE K step per 128x128 tile and then a
+// two-barrier LDS epilogue; each workgroup is a latency chain (load -> 32 MFMAs -> LDS round trip
+// -> stores + statistics) and the expand convs (64 -> 256 at 32x32, batch 256) ran at 1.6 TB/s,
+// 5x off their HBM floor.
+//
+// Here every wave is its own pipeline:
+//  * a wave owns 64 output channels (the A operand: its weights [64][K] live in VGPRs for the
+//    whole kernel, loaded once) and a contiguous range of 32-pixel tiles;
+//  * per tile it loads the B fragments (16 pixels x 8 channels per lane, 16-byte global loads
+//    straight into registers), issues 16 x K/32 mfma_f32_16x16x32_bf16, starts the NEXT tile's
+//    loads, and runs the epilogue from registers: an accumulator quad is 4 consecutive channels
+//    of one pixel, stored as 8 bytes of an NHWC row;
+//  * BatchNorm statistics accumulate in registers across all tiles of the wave (pivot-shifted
+//    sums, packed fp32 math) and are reduced over the 16 lanes of a DPP row ONCE per wave, so the
+//    statistics slab has one row per pixel range instead of one per 128-pixel tile (the
+//    bn_stat_reduce that follows reads 8-16x fewer rows);
+//  * the waves of a CU drift into different phases (no barriers), so one wave's epilogue VALU
+//    and stores overlap another's MFMAs and loads.
+//
+// Modes: 0 plain (optional bias / residual / ReLU), 1 forward with Welford statistics of the
+// stored values, 2 data gradient with the backward-BatchNorm fusion of the producing layer
+// (ReLU mask from its output y, sums of g and g * xhat: the same contract as gemm_g2's bnb
+// epilogue, api.h BnbArgs).
+//
+// Reference parity: the reference runs 1x1 convs through im2col + cuBLAS / cuDNN
+// (src/nn/layers_impl/cuda/conv2d_ops.cu:18-128, cudnn_conv2d_ops.cu:187-244).
+#include <cstdlib>
+
+#include "common.h"
+#include "api.h"
+
+namespace dcnn {
+
+namespace {
+typedef float f32x2 __attribute__((ext_vector_type(2)));
+
+__device__ __forceinline__ int xcd_remap_g1(int bid, int nwg) {
+  const int xcd = bid & 7, q = nwg >> 3, r = nwg & 7;
+  const int base = xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q;
+  return base + (bid >> 3);
+}
+
+// fixed-order sum over the 16 lanes of a DPP row; every lane of the row gets the total
+__device__ __forceinline__ float g1_row_sum(float v) {
+  v += __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0x128, 0xf, 0xf, false));  // row_ror:8
+  v += __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0x124, 0xf, 0xf, false));  // row_ror:4
+  v += __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0x4e, 0xf, 0xf, false));   // quad xor 2
+  v += __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0xb1, 0xf, 0xf, false));   // quad xor 1
+  return v;
+}
+
+// value held by lane 0 of this lane's 16-lane row
+__device__ __forceinline__ float g1_row_first(float v) {
+  const int x = __float_as_int(v);
+  const int r0 = __builtin_amdgcn_readlane(x, 0), r1 = __builtin_amdgcn_readlane(x, 16);
+  const int r2 = __builtin_amdgcn_readlane(x, 32), r3 = __builtin_amdgcn_readlane(x, 48);
+  const int row = (threadIdx.x & 63) >> 4;
+  return __int_as_float(row == 0 ? r0 : row == 1 ? r1 : row == 2 ? r2 : r3);
+}
+
+// two bf16 of one 32-bit word -> fp32 pair (exact)
+__device__ __forceinline__ f32x2 bf2_to_f2(unsigned w) {
+  return f32x2{__uint_as_float(w << 16), __uint_as_float(w & 0xffff0000u)};
+}
+__device__ __forceinline__ unsigned f2_to_bf2(float a, float b) {
+  bf16 x = (bf16)a, y = (bf16)b;
+  return (unsigned)__builtin_bit_cast(unsigned short, x) | ((unsigned)__builtin_bit_cast(unsigned short, y) << 16);
+}
+}  // namespace
+
+struct G1sArgs {
+  const bf16* X; const bf16* Wt; bf16* Y;
+  int M, N, K, H, W, OH, OW, S;  // output pixels M = NB * OH * OW, input NB x H x W x K (NHWC)
+  int PR, tpr, tiles;            // pixel ranges (statistics rows), tiles per range, M / tile pixels
+  const float* bias; const bf16* residual; float* stats; int relu;
+  float* zero_ptr; int zero_n;
+  BnbArgs bnb;
+  int dbg;  // DCNN_G1S_DBG experiments: 1 = no output stores, 2 = 16-byte stores through row swaps,
+           // 4 = full-line stores through a per-wave LDS stage
+};
+
+// per-instance shape: TJ 16-pixel subtiles per tile, OCC waves per SIMD the registers allow
+// (K = 64: 32-pixel tiles keep the forward at ~150 VGPRs, three waves per SIMD to hide the
+// load latency behind each other's epilogues)
+// waves per SIMD of an instance (the register budget it is compiled for): 2, or 3 for the K = 64
+// forward when DCNN_G1S_OCC=3 (~168 VGPRs)
+static int g_g1s_occ3 = [] {
+  const char* e = getenv("DCNN_G1S_OCC");
+  return e ? atoi(e) == 3 : 0;
+}();
+static int g1s_occ_rt(int K, int mode) { return (K == 64 && mode != 2 && g_g1s_occ3) ? 3 : 2; }
+constexpr int kG1sTile = 32;  // pixels per tile (16 * TJ)
+
+template <int K, int MODE, int OCC>
+__global__ void __launch_bounds__(256, OCC) g1s_kernel(G1sArgs p) {
+  constexpr int KK = K / 32, TJ = 2, TP = 16 * TJ;
+  static_assert(TP == kG1sTile, "tile size");
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  const int lr = lane & 15, lh = lane >> 4;
+  // per-wave channel constants (bias or BatchNorm mean / 1/std, and the statistics pivots of this
+  // wave's 64 channels), read back with ds_read: LDS reads never wait for outstanding stores
+  __shared__ __attribute__((aligned(16))) float cst[4][2][64];
+  __shared__ __attribute__((aligned(16))) char stage[4][32 * 128];  // per-wave output tile (dbg & 4)
+  char* stg = stage[threadIdx.x >> 6];
+  if (p.zero_ptr && blockIdx.x == 0)
+    for (int i = threadIdx.x; i < p.zero_n; i += 256) p.zero_ptr[i] = 0.f;
+  const int CS = p.N >> 6;
+  const int gw = xcd_remap_g1(blockIdx.x, gridDim.x) * 4 + wid;
+  if (gw >= p.PR * CS) return;
+  const int cs = gw % CS, pr = gw / CS;
+  const int n0 = cs * 64;
+  const int t0 = pr * p.tpr, t1 = min(p.tiles, t0 + p.tpr);
+
+  if (MODE == 2) {
+    cst[wid][0][lane] = p.bnb.mean[n0 + lane];
+    cst[wid][1][lane] = p.bnb.istd[n0 + lane];
+  } else {
+    cst[wid][0][lane] = p.bias ? p.bias[n0 + lane] : 0.f;
+  }
+  // weights: A fragment (channel subtile i, k step kk): row n0 + 16 i + lr, k = 32 kk + 8 lh
+  bf16x8 wa[4][KK];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int kk = 0; kk < KK; ++kk)
+      wa[i][kk] = *reinterpret_cast<const bf16x8*>(p.Wt + (size_t)(n0 + i * 16 + lr) * K + kk * 32 + lh * 8);
+
+  const bool plain = p.S == 1 && p.OH == p.H && p.OW == p.W;
+  const int ohw = p.OH * p.OW;
+  auto src_px = [&](int m) -> long {  // input pixel of output pixel m
+    if (plain) return m;
+    const int img = m / ohw, rem = m - img * ohw;
+    const int oy = rem / p.OW, ox = rem - oy * p.OW;
+    return ((long)img * p.H + oy * p.S) * p.W + ox * p.S;
+  };
+  bf16x8 b[TJ][KK];
+  auto load_b = [&](int t) {
+#pragma unroll
+    for (int j = 0; j < TJ; ++j) {
+      const bf16* q = p.X + src_px(t * TP + j * 16 + lr) * K + lh * 8;
+#pragma unroll
+      for (int kk = 0; kk < KK; ++kk) b[j][kk] = *reinterpret_cast<const bf16x8*>(q + kk * 32);
+    }
+  };
+
+  // statistics accumulators: channel n0 + 16 i + 4 lh + r, summed over this lane's pixels
+  f32x2 sa[4][2], sb[4][2];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int h = 0; h < 2; ++h) sa[i][h] = sb[i][h] = f32x2{0.f, 0.f};
+  const bool has_res = MODE == 0 && p.residual != nullptr;
+  const bool has_y = MODE == 2 && p.bnb.y != nullptr;
+  const bool relu = MODE == 0 && p.relu;
+
+  if (t0 < t1) load_b(t0);
+  for (int t = t0; t < t1; ++t) {
+    f32x4 acc[4][TJ];
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int j = 0; j < TJ; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int kk = 0; kk < KK; ++kk)
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < TJ; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wa[i][kk], b[j][kk], acc[i][j], 0, 0, 0);
+    if (t + 1 < t1) load_b(t + 1);  // in flight during this tile's epilogue
+
+    // epilogue operand loads first (a load's wait also waits for every older store)
+    uint2 ro[4][TJ], xo[4][TJ];
+#pragma unroll
+    for (int j = 0; j < TJ; ++j) {
+      const size_t row = (size_t)(t * TP + j * 16 + lr) * p.N + n0 + lh * 4;
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        ro[i][j] = has_res ? *reinterpret_cast<const uint2*>(p.residual + row + i * 16)
+                   : has_y ? *reinterpret_cast<const uint2*>(p.bnb.y + row + i * 16) : make_uint2(0u, 0u);
+        xo[i][j] = MODE == 2 ? *reinterpret_cast<const uint2*>(p.bnb.x + row + i * 16) : make_uint2(0u, 0u);
+      }
+    }
+    const bool first = t == t0;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const float4 c0 = *reinterpret_cast<const float4*>(&cst[wid][0][i * 16 + lh * 4]);
+      if (MODE == 1 && first) {
+        // statistics pivot of each channel: the stored value of the wave's first pixel
+        const float v0 = (float)(bf16)(acc[i][0][0] + c0.x), v1 = (float)(bf16)(acc[i][0][1] + c0.y);
+        const float v2 = (float)(bf16)(acc[i][0][2] + c0.z), v3 = (float)(bf16)(acc[i][0][3] + c0.w);
+        const float p0 = g1_row_first(v0), p1 = g1_row_first(v1), p2 = g1_row_first(v2), p3 = g1_row_first(v3);
+        if (lr == 0) *reinterpret_cast<float4*>(&cst[wid][1][i * 16 + lh * 4]) = make_float4(p0, p1, p2, p3);
+      }
+      const float4 c1 = MODE != 0 ? *reinterpret_cast<const float4*>(&cst[wid][1][i * 16 + lh * 4]) : c0;
+      uint2 ov[TJ];
+#pragma unroll
+      for (int j = 0; j < TJ; ++j) {
+        bf16* yrow = p.Y + (size_t)(t * TP + j * 16 + lr) * p.N + n0 + lh * 4;
+        float f[4];
+        if (MODE == 2) {
+#pragma unroll
+          for (int r = 0; r < 4; ++r) f[r] = acc[i][j][r];
+        } else {
+          f[0] = acc[i][j][0] + c0.x; f[1] = acc[i][j][1] + c0.y; f[2] = acc[i][j][2] + c0.z; f[3] = acc[i][j][3] + c0.w;
+        }
+        if (has_res) {
+          const f32x2 r01 = bf2_to_f2(ro[i][j].x), r23 = bf2_to_f2(ro[i][j].y);
+          f[0] += r01.x; f[1] += r01.y; f[2] += r23.x; f[3] += r23.y;
+        }
+        if (relu) {
+#pragma unroll
+          for (int r = 0; r < 4; ++r) f[r] = fmaxf(f[r], 0.f);
+        }
+        if (has_y) {
+          const f32x2 y01 = bf2_to_f2(ro[i][j].x), y23 = bf2_to_f2(ro[i][j].y);
+          f[0] = y01.x > 0.f ? f[0] : 0.f; f[1] = y01.y > 0.f ? f[1] : 0.f;
+          f[2] = y23.x > 0.f ? f[2] : 0.f; f[3] = y23.y > 0.f ? f[3] : 0.f;
+        }
+        const uint2 o = make_uint2(f2_to_bf2(f[0], f[1]), f2_to_bf2(f[2], f[3]));
+        ov[j] = o;
+        if (p.dbg & 4) {
+          // full-line stores: stage the tile's 32 pixel rows (128 B each, 16-byte chunks XOR-swizzled
+          // by the pixel) in this wave's LDS slice; read back below as 8 lanes per pixel row
+          const int P = j * 16 + lr, c = i * 2 + (lh >> 1);
+          *reinterpret_cast<uint2*>(stg + P * 128 + ((c ^ (P & 7)) << 4) + (lh & 1) * 8) = o;
+        } else if (!(p.dbg & 3)) {
+          *reinterpret_cast<uint2*>(yrow + i * 16) = o;
+        }
+        if constexpr (MODE == 1) {
+          // statistics of the values actually stored, about the pivots
+          const f32x2 g01 = bf2_to_f2(o.x), g23 = bf2_to_f2(o.y);
+          const f32x2 d01 = g01 - f32x2{c1.x, c1.y}, d23 = g23 - f32x2{c1.z, c1.w};
+          sa[i][0] += d01; sa[i][1] += d23;
+          sb[i][0] += d01 * d01; sb[i][1] += d23 * d23;
+        } else if constexpr (MODE == 2) {
+          const f32x2 g01 = bf2_to_f2(o.x), g23 = bf2_to_f2(o.y);
+          const f32x2 x01 = bf2_to_f2(xo[i][j].x), x23 = bf2_to_f2(xo[i][j].y);
+          const f32x2 h01 = (x01 - f32x2{c0.x, c0.y}) * f32x2{c1.x, c1.y};
+          const f32x2 h23 = (x23 - f32x2{c0.z, c0.w}) * f32x2{c1.z, c1.w};
+          sa[i][0] += g01; sa[i][1] += g23;
+          sb[i][0] += g01 * h01; sb[i][1] += g23 * h23;
+        }
+      }
+      if (p.dbg & 2) {
+        // 16-byte stores: rows 0 <-> 1 and 2 <-> 3 trade halves (v_permlane16_swap), so each lane
+        // holds 8 consecutive channels of one pixel (even rows: subtile 0, odd rows: subtile 1)
+        const auto sx = __builtin_amdgcn_permlane16_swap(ov[0].x, ov[1].x, false, false);
+        const auto sy = __builtin_amdgcn_permlane16_swap(ov[0].y, ov[1].y, false, false);
+        const int odd = lh & 1;
+        bf16* dst = p.Y + (size_t)(t * TP + odd * 16 + lr) * p.N + n0 + i * 16 + (lh & 2) * 4;
+        *reinterpret_cast<uint4*>(dst) = make_uint4(sx[0], sy[0], sx[1], sy[1]);
+      }
+    }
+    if (p.dbg & 4) {
+#pragma unroll
+      for (int k = 0; k < TP / 8; ++k) {
+        const int P = k * 8 + (lane >> 3), c = lane & 7;
+        const uint4 v = *reinterpret_cast<const uint4*>(stg + P * 128 + ((c ^ (P & 7)) << 4));
+        *reinterpret_cast<uint4*>(p.Y + (size_t)(t * TP + P) * p.N + n0 + c * 8) = v;
+      }
+    }
+  }
+  if constexpr (MODE != 0) {
+    const float npx = (float)((t1 - t0) * TP);
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const float a = g1_row_sum(r < 2 ? sa[i][0][r] : sa[i][1][r - 2]);
+        const float q = g1_row_sum(r < 2 ? sb[i][0][r] : sb[i][1][r - 2]);
+        if (lr == 0) {
+          const int c = n0 + i * 16 + lh * 4 + r;
+          if constexpr (MODE == 1) {
+            store_welford(p.stats, pr, p.N, c, welford_from_shifted(npx, cst[wid][1][c - n0], a, q));
+          } else {
+            p.stats[((long)pr * 2 + 0) * p.N + c] = a;
+            p.stats[((long)pr * 2 + 1) * p.N + c] = q;
+          }
+        }
+      }
+  }
+}
+
+// ------------------------------------------------------------------------------------------------
+// host side
+// ------------------------------------------------------------------------------------------------
+static int g_g1s = [] {
+  const char* e = getenv("DCNN_G1S");
+  return e ? atoi(e) : 1;
+}();
+void g1s_enable(int on) { g_g1s = on; }
+
+// statistics rows (= pixel ranges) of a streaming 1x1 conv with M output pixels, N output and K
+// input channels in `mode`; 0 when the shape does not run on it. The ranges are sized so every
+// resident wave slot holds one wave (two per SIMD when the registers allow, else one).
+int g1s_rows(int M, int N, int K, int mode) {
+  if (!g_g1s || M % 64 || N % 64 || (K != 64 && K != 128)) return 0;
+  const int tiles = M / kG1sTile, CS = N / 64;
+  const long waves = 256l * 4 * g1s_occ_rt(K, mode);
+  int pr = (int)((waves + CS - 1) / CS);
+  if (pr > tiles) pr = tiles;
+  const int tpr = (tiles + pr - 1) / pr;
+  return (tiles + tpr - 1) / tpr;
+}
+
+template <int K, int MODE, int OCC = 2>
+static void launch_g1s(const G1sArgs& a, hipStream_t s) {
+  const int waves = a.PR * (a.N / 64);
+  hipLaunchKernelGGL((g1s_kernel<K, MODE, OCC>), dim3((waves + 3) / 4), dim3(256), 0, s, a);
+  DCNN_LAUNCH_CHECK();
+}
+
+// mode: 0 plain, 1 forward + Welford statistics ([rows][3][N]), 2 data gradient + bnb sums
+// ([rows][2][N]); rows must be g1s_rows(M, N, K)
+void g1s(const bf16* X, const bf16* Wt, bf16* Y, int M, int N, int K, int H, int W, int OH, int OW, int S,
+         const float* bias, const bf16* residual, float* stats, int relu, float* zero_ptr, int zero_n, BnbArgs bnb,
+         int mode, hipStream_t s) {
+  const int rows = g1s_rows(M, N, K, mode);
+  if (!rows) throw std::runtime_error("g1s: unsupported shape");
+  if (mode < 0 || mode > 2 || (mode != 0 && !stats)) throw std::runtime_error("g1s: bad mode / statistics slab");
+  if (mode == 2 && (!bnb.x || !bnb.mean || !bnb.istd || S != 1)) throw std::runtime_error("g1s: bnb operands missing");
+  if (mode != 0 && (residual || relu)) throw std::runtime_error("g1s: residual / ReLU only without statistics");
+  if ((long)M != (long)(M / (OH * OW)) * OH * OW || OH != (H - 1) / S + 1 || OW != (W - 1) / S + 1)
+    throw std::runtime_error("g1s: inconsistent geometry");
+  G1sArgs a{};
+  a.X = X; a.Wt = Wt; a.Y = Y;
+  a.M = M; a.N = N; a.K = K; a.H = H; a.W = W; a.OH = OH; a.OW = OW; a.S = S;
+  a.tiles = M / kG1sTile;
+  a.tpr = (a.tiles + rows - 1) / rows;
+  a.PR = rows;
+  a.bias = bias; a.residual = residual; a.stats = stats; a.relu = relu;
+  a.zero_ptr = zero_ptr; a.zero_n = zero_n;
+  a.bnb = bnb;
+  static const int dbg = [] { const char* e = getenv("DCNN_G1S_DBG"); return e ? atoi(e) : 0; }();
+  a.dbg = dbg;
+#define DCNN_G1S(K_)                                          \
+  if (K == K_) {                                              \
+    if (mode == 0) return launch_g1s<K_, 0>(a, s);            \
+    if (mode == 1 && g1s_occ_rt(K_, 1) == 3) return launch_g1s<K_, 1, (K_ == 64 ? 3 : 2)>(a, s); \
+    if (mode == 1) return launch_g1s<K_, 1>(a, s);            \
+    return launch_g1s<K_, 2>(a, s);                           \
+  }
+  DCNN_G1S(64)
+  DCNN_G1S(128)
+#undef DCNN_G1S
+  throw std::runtime_error("g1s: no kernel instance");
+}
+
+}  // namespace dcnn

@@ -253,6 +253,17 @@ def conv2d_fwd(x, w, bias, stride, pad, *, stats=False, residual=None, relu=Fals
                    _fwd_taps(Ci, W, KH, KW, ph, pw), KH * KW * Ci, Co, OH, OW, 1, 1, 0, 0, ptr(bias), ptr(residual),
                    ptr(slab), int(relu), ptr(sums), 2 * Co if stats else 0, _NOBNB, stream_ptr())
         return y, ((slab, rows, sums) if stats else None)
+    if (KH, KW) == (1, 1) and (ph, pw) == (0, 0) and sh == sw and not out_fp32 and x.dtype == BF16 \
+            and w.dim() == 4 and (not stats or (residual is None and not relu)):
+        # streaming 1x1 conv (g1s.hip): weights in registers, one statistics row per pixel range
+        rows = K.g1s_rows(M, Co, Ci, 1 if stats else 0)
+        if rows:
+            y = _empty((N, Co, OH, OW), BF16, x.device, True)
+            slab = _empty((rows, 3, Co), F32, x.device) if stats else None
+            sums = _empty((2 * Co,), F32, x.device) if stats else None  # zeroed in-kernel
+            K.g1s(x.data_ptr(), w.data_ptr(), y.data_ptr(), M, Co, Ci, H, W, OH, OW, sh, ptr(bias), ptr(residual),
+                  ptr(slab), int(relu), ptr(sums), 2 * Co if stats else 0, _NOBNB, 1 if stats else 0, stream_ptr())
+            return y, ((slab, rows, sums) if stats else None)
     taps = _fwd_taps(Ci, W, KH, KW, ph, pw)
     if not out_fp32 and _hconv_ok(N, OH, OW, H, W, sh, sw, Ci, Co, taps, w):
         y = _empty((N, Co, OH, OW), BF16, x.device, True)
@@ -664,6 +675,18 @@ def conv2d_dgrad(dy, wt, x_shape, stride, pad, *, residual=None, bnb=None):
         if fuse:
             dx._bnb = (bnb.bn, fst if fst is not None else slab, rows, sums)
         return dx
+    if (not f32 and (KH, KW) == (1, 1) and (sh, sw) == (1, 1) and (ph, pw) == (0, 0) and not empty_class
+            and len(classes) == 1 and (residual is None or not fuse)):
+        # streaming 1x1 data gradient (g1s.hip), backward-BatchNorm fusion in its epilogue
+        rows = K.g1s_rows(N * H * W, Ci, Co, 2 if fuse else 0)
+        if rows:
+            slab = _empty((rows, 2, Ci), F32, dy.device) if fuse else None
+            sums = _empty((2 * Ci,), F32, dy.device) if fuse else None
+            K.g1s(dy.data_ptr(), wt.data_ptr(), dx.data_ptr(), N * H * W, Ci, Co, H, W, H, W, 1, 0, ptr(residual),
+                  ptr(slab), 0, ptr(sums), 2 * Ci if fuse else 0, bnb.args() if fuse else _NOBNB, 2 if fuse else 0, st)
+            if fuse:
+                dx._bnb = (bnb.bn, slab, rows, sums)
+            return dx
     crow = [K.gemm_g2_stat_rows(N * GH * GW, Ci) if fuse else 0 for _, _, GH, GW, _ in classes]
     rows = sum(crow)
     slab = _empty((rows, 2, Ci), F32, dy.device) if fuse else None
