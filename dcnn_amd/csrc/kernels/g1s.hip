@@ -79,8 +79,8 @@ struct G1sArgs {
   const float* bias; const bf16* residual; float* stats; int relu;
   float* zero_ptr; int zero_n;
   BnbArgs bnb;
-  int dbg;  // DCNN_G1S_DBG experiments: 1 = no output stores, 2 = 16-byte stores through row swaps,
-           // 4 = full-line stores through a per-wave LDS stage
+  int dbg;  // DCNN_G1S_DBG experiments: 2 = direct 8-byte stores instead of the LDS-staged full
+           // lines, 3 = no output stores (timing only)
 };
 
 // per-instance shape: TJ 16-pixel subtiles per tile, OCC waves per SIMD the registers allow
@@ -92,20 +92,27 @@ static int g_g1s_occ3 = [] {
   const char* e = getenv("DCNN_G1S_OCC");
   return e ? atoi(e) == 3 : 0;
 }();
+static int g_g1s_pf = [] {
+  const char* e = getenv("DCNN_G1S_PF");
+  return e ? atoi(e) : 2;
+}();
 static int g1s_occ_rt(int K, int mode) { return (K == 64 && mode != 2 && g_g1s_occ3) ? 3 : 2; }
 constexpr int kG1sTile = 32;  // pixels per tile (16 * TJ)
 
-template <int K, int MODE, int OCC>
+template <int K, int MODE, int OCC, int PF, bool EP>
 __global__ void __launch_bounds__(256, OCC) g1s_kernel(G1sArgs p) {
   constexpr int KK = K / 32, TJ = 2, TP = 16 * TJ;
   static_assert(TP == kG1sTile, "tile size");
+  static_assert(PF == 1 || PF == 2 || PF == 4, "prefetch depth (the tile loop is unrolled by it)");
+  static_assert(PF == 2 || !EP, "epilogue-operand ping-pong assumes the 2-tile unroll");
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
   const int lr = lane & 15, lh = lane >> 4;
   // per-wave channel constants (bias or BatchNorm mean / 1/std, and the statistics pivots of this
-  // wave's 64 channels), read back with ds_read: LDS reads never wait for outstanding stores
+  // wave's 64 channels) and the per-wave output stage; each wave touches only its own slices
+  // (no barrier: LDS ops of one wave execute in order, and LDS reads never wait for stores)
   __shared__ __attribute__((aligned(16))) float cst[4][2][64];
-  __shared__ __attribute__((aligned(16))) char stage[4][32 * 128];  // per-wave output tile (dbg & 4)
-  char* stg = stage[threadIdx.x >> 6];
+  __shared__ __attribute__((aligned(16))) char stage[4][TP * 128];
+  char* stg = stage[wid];
   if (p.zero_ptr && blockIdx.x == 0)
     for (int i = threadIdx.x; i < p.zero_n; i += 256) p.zero_ptr[i] = 0.f;
   const int CS = p.N >> 6;
@@ -137,13 +144,32 @@ __global__ void __launch_bounds__(256, OCC) g1s_kernel(G1sArgs p) {
     const int oy = rem / p.OW, ox = rem - oy * p.OW;
     return ((long)img * p.H + oy * p.S) * p.W + ox * p.S;
   };
-  bf16x8 b[TJ][KK];
-  auto load_b = [&](int t) {
+  // B fragments of PF tiles in flight (ring, statically indexed by the unrolled loop)
+  bf16x8 bb[PF][TJ][KK];
+  auto load_b = [&](bf16x8 (&b)[TJ][KK], int t) {
 #pragma unroll
     for (int j = 0; j < TJ; ++j) {
       const bf16* q = p.X + src_px(t * TP + j * 16 + lr) * K + lh * 8;
 #pragma unroll
       for (int kk = 0; kk < KK; ++kk) b[j][kk] = *reinterpret_cast<const bf16x8*>(q + kk * 32);
+    }
+  };
+  // epilogue operands (residual or the BatchNorm's y, and its x), one tile ahead (ping-pong)
+  const bool has_res = MODE == 0 && p.residual != nullptr;
+  const bool has_y = MODE == 2 && p.bnb.y != nullptr;
+  const bool has_e = has_res || MODE == 2;
+  const bool relu = MODE == 0 && p.relu;
+  uint2 eo[2][2][4][TJ];
+  auto load_e = [&](uint2 (&e)[2][4][TJ], int t) {
+#pragma unroll
+    for (int j = 0; j < TJ; ++j) {
+      const size_t row = (size_t)(t * TP + j * 16 + lr) * p.N + n0 + lh * 4;
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        e[0][i][j] = has_res ? *reinterpret_cast<const uint2*>(p.residual + row + i * 16)
+                     : has_y ? *reinterpret_cast<const uint2*>(p.bnb.y + row + i * 16) : make_uint2(0u, 0u);
+        e[1][i][j] = MODE == 2 ? *reinterpret_cast<const uint2*>(p.bnb.x + row + i * 16) : make_uint2(0u, 0u);
+      }
     }
   };
 
@@ -153,12 +179,11 @@ __global__ void __launch_bounds__(256, OCC) g1s_kernel(G1sArgs p) {
   for (int i = 0; i < 4; ++i)
 #pragma unroll
     for (int h = 0; h < 2; ++h) sa[i][h] = sb[i][h] = f32x2{0.f, 0.f};
-  const bool has_res = MODE == 0 && p.residual != nullptr;
-  const bool has_y = MODE == 2 && p.bnb.y != nullptr;
-  const bool relu = MODE == 0 && p.relu;
 
-  if (t0 < t1) load_b(t0);
-  for (int t = t0; t < t1; ++t) {
+  // one tile: the load of tile t + PF - 1 goes out first (into the buffer tile t - 1 used), then
+  // the MFMAs, the next tile's epilogue operands, and the epilogue of this one
+  auto tile = [&](int t, bf16x8 (&bc)[TJ][KK], bf16x8 (&bn)[TJ][KK], uint2 (&ec)[2][4][TJ], uint2 (&en)[2][4][TJ]) {
+    if (PF > 1 && t + PF - 1 < t1) load_b(bn, t + PF - 1);
     f32x4 acc[4][TJ];
 #pragma unroll
     for (int i = 0; i < 4; ++i)
@@ -169,20 +194,11 @@ __global__ void __launch_bounds__(256, OCC) g1s_kernel(G1sArgs p) {
 #pragma unroll
       for (int i = 0; i < 4; ++i)
 #pragma unroll
-        for (int j = 0; j < TJ; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wa[i][kk], b[j][kk], acc[i][j], 0, 0, 0);
-    if (t + 1 < t1) load_b(t + 1);  // in flight during this tile's epilogue
-
-    // epilogue operand loads first (a load's wait also waits for every older store)
-    uint2 ro[4][TJ], xo[4][TJ];
-#pragma unroll
-    for (int j = 0; j < TJ; ++j) {
-      const size_t row = (size_t)(t * TP + j * 16 + lr) * p.N + n0 + lh * 4;
-#pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        ro[i][j] = has_res ? *reinterpret_cast<const uint2*>(p.residual + row + i * 16)
-                   : has_y ? *reinterpret_cast<const uint2*>(p.bnb.y + row + i * 16) : make_uint2(0u, 0u);
-        xo[i][j] = MODE == 2 ? *reinterpret_cast<const uint2*>(p.bnb.x + row + i * 16) : make_uint2(0u, 0u);
-      }
+        for (int j = 0; j < TJ; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wa[i][kk], bc[j][kk], acc[i][j], 0, 0, 0);
+    if (PF == 1 && t + 1 < t1) load_b(bc, t + 1);  // one buffer: reloaded once the MFMAs have read it
+    if (has_e) {
+      if (EP) { if (t + 1 < t1) load_e(en, t + 1); }
+      else load_e(ec, t);  // operand loads still ahead of this tile's stores
     }
     const bool first = t == t0;
 #pragma unroll
@@ -196,10 +212,8 @@ __global__ void __launch_bounds__(256, OCC) g1s_kernel(G1sArgs p) {
         if (lr == 0) *reinterpret_cast<float4*>(&cst[wid][1][i * 16 + lh * 4]) = make_float4(p0, p1, p2, p3);
       }
       const float4 c1 = MODE != 0 ? *reinterpret_cast<const float4*>(&cst[wid][1][i * 16 + lh * 4]) : c0;
-      uint2 ov[TJ];
 #pragma unroll
       for (int j = 0; j < TJ; ++j) {
-        bf16* yrow = p.Y + (size_t)(t * TP + j * 16 + lr) * p.N + n0 + lh * 4;
         float f[4];
         if (MODE == 2) {
 #pragma unroll
@@ -208,7 +222,7 @@ __global__ void __launch_bounds__(256, OCC) g1s_kernel(G1sArgs p) {
           f[0] = acc[i][j][0] + c0.x; f[1] = acc[i][j][1] + c0.y; f[2] = acc[i][j][2] + c0.z; f[3] = acc[i][j][3] + c0.w;
         }
         if (has_res) {
-          const f32x2 r01 = bf2_to_f2(ro[i][j].x), r23 = bf2_to_f2(ro[i][j].y);
+          const f32x2 r01 = bf2_to_f2(ec[0][i][j].x), r23 = bf2_to_f2(ec[0][i][j].y);
           f[0] += r01.x; f[1] += r01.y; f[2] += r23.x; f[3] += r23.y;
         }
         if (relu) {
@@ -216,19 +230,18 @@ __global__ void __launch_bounds__(256, OCC) g1s_kernel(G1sArgs p) {
           for (int r = 0; r < 4; ++r) f[r] = fmaxf(f[r], 0.f);
         }
         if (has_y) {
-          const f32x2 y01 = bf2_to_f2(ro[i][j].x), y23 = bf2_to_f2(ro[i][j].y);
+          const f32x2 y01 = bf2_to_f2(ec[0][i][j].x), y23 = bf2_to_f2(ec[0][i][j].y);
           f[0] = y01.x > 0.f ? f[0] : 0.f; f[1] = y01.y > 0.f ? f[1] : 0.f;
           f[2] = y23.x > 0.f ? f[2] : 0.f; f[3] = y23.y > 0.f ? f[3] : 0.f;
         }
         const uint2 o = make_uint2(f2_to_bf2(f[0], f[1]), f2_to_bf2(f[2], f[3]));
-        ov[j] = o;
-        if (p.dbg & 4) {
-          // full-line stores: stage the tile's 32 pixel rows (128 B each, 16-byte chunks XOR-swizzled
-          // by the pixel) in this wave's LDS slice; read back below as 8 lanes per pixel row
+        if (p.dbg & 2) {  // direct 8-byte stores (16 pixel rows x 32 B per instruction)
+          if (!(p.dbg & 1)) *reinterpret_cast<uint2*>(p.Y + (size_t)(t * TP + j * 16 + lr) * p.N + n0 + lh * 4 + i * 16) = o;
+        } else {
+          // full-line stores: the tile's 32 pixel rows (128 B each, 16-byte chunks XOR-swizzled by
+          // the pixel) are staged in this wave's LDS slice and read back as 8 lanes per pixel row
           const int P = j * 16 + lr, c = i * 2 + (lh >> 1);
           *reinterpret_cast<uint2*>(stg + P * 128 + ((c ^ (P & 7)) << 4) + (lh & 1) * 8) = o;
-        } else if (!(p.dbg & 3)) {
-          *reinterpret_cast<uint2*>(yrow + i * 16) = o;
         }
         if constexpr (MODE == 1) {
           // statistics of the values actually stored, about the pivots
@@ -238,30 +251,39 @@ __global__ void __launch_bounds__(256, OCC) g1s_kernel(G1sArgs p) {
           sb[i][0] += d01 * d01; sb[i][1] += d23 * d23;
         } else if constexpr (MODE == 2) {
           const f32x2 g01 = bf2_to_f2(o.x), g23 = bf2_to_f2(o.y);
-          const f32x2 x01 = bf2_to_f2(xo[i][j].x), x23 = bf2_to_f2(xo[i][j].y);
+          const f32x2 x01 = bf2_to_f2(ec[1][i][j].x), x23 = bf2_to_f2(ec[1][i][j].y);
           const f32x2 h01 = (x01 - f32x2{c0.x, c0.y}) * f32x2{c1.x, c1.y};
           const f32x2 h23 = (x23 - f32x2{c0.z, c0.w}) * f32x2{c1.z, c1.w};
           sa[i][0] += g01; sa[i][1] += g23;
           sb[i][0] += g01 * h01; sb[i][1] += g23 * h23;
         }
       }
-      if (p.dbg & 2) {
-        // 16-byte stores: rows 0 <-> 1 and 2 <-> 3 trade halves (v_permlane16_swap), so each lane
-        // holds 8 consecutive channels of one pixel (even rows: subtile 0, odd rows: subtile 1)
-        const auto sx = __builtin_amdgcn_permlane16_swap(ov[0].x, ov[1].x, false, false);
-        const auto sy = __builtin_amdgcn_permlane16_swap(ov[0].y, ov[1].y, false, false);
-        const int odd = lh & 1;
-        bf16* dst = p.Y + (size_t)(t * TP + odd * 16 + lr) * p.N + n0 + i * 16 + (lh & 2) * 4;
-        *reinterpret_cast<uint4*>(dst) = make_uint4(sx[0], sy[0], sx[1], sy[1]);
-      }
     }
-    if (p.dbg & 4) {
+    if (!(p.dbg & 3)) {
 #pragma unroll
       for (int k = 0; k < TP / 8; ++k) {
         const int P = k * 8 + (lane >> 3), c = lane & 7;
         const uint4 v = *reinterpret_cast<const uint4*>(stg + P * 128 + ((c ^ (P & 7)) << 4));
         *reinterpret_cast<uint4*>(p.Y + (size_t)(t * TP + P) * p.N + n0 + c * 8) = v;
       }
+    }
+  };
+
+#pragma unroll
+  for (int d = 0; d < (PF > 1 ? PF - 1 : 1); ++d)
+    if (t0 + d < t1) load_b(bb[d], t0 + d);
+  if (EP && has_e && t0 < t1) load_e(eo[0], t0);
+  if constexpr (PF == 1) {
+    for (int t = t0; t < t1; ++t) tile(t, bb[0], bb[0], eo[0], eo[0]);
+  } else for (int t = t0; t < t1; t += PF) {
+    tile(t, bb[0], bb[PF - 1], eo[0], eo[1]);
+    if (t + 1 >= t1) break;
+    tile(t + 1, bb[1 % PF], bb[0], eo[1], eo[0]);
+    if constexpr (PF == 4) {
+      if (t + 2 >= t1) break;
+      tile(t + 2, bb[2 % PF], bb[1], eo[0], eo[1]);
+      if (t + 3 >= t1) break;
+      tile(t + 3, bb[3 % PF], bb[2 % PF], eo[1], eo[0]);
     }
   }
   if constexpr (MODE != 0) {
@@ -310,7 +332,15 @@ int g1s_rows(int M, int N, int K, int mode) {
 template <int K, int MODE, int OCC = 2>
 static void launch_g1s(const G1sArgs& a, hipStream_t s) {
   const int waves = a.PR * (a.N / 64);
-  hipLaunchKernelGGL((g1s_kernel<K, MODE, OCC>), dim3((waves + 3) / 4), dim3(256), 0, s, a);
+  // B fragments two tiles deep; epilogue operands (residual / BatchNorm y, x) one tile ahead only
+  // with DCNN_G1S_PF=3 (more registers: spills on the wider instances)
+  // (K = 128: one B buffer, reloaded after the MFMAs — the two-deep ring spills there)
+  if (K == 128 || g_g1s_pf == 1)
+    hipLaunchKernelGGL((g1s_kernel<K, MODE, OCC, 1, false>), dim3((waves + 3) / 4), dim3(256), 0, s, a);
+  else if (g_g1s_pf == 3)
+    hipLaunchKernelGGL((g1s_kernel<K, MODE, OCC, 2, true>), dim3((waves + 3) / 4), dim3(256), 0, s, a);
+  else
+    hipLaunchKernelGGL((g1s_kernel<K, MODE, OCC, 2, false>), dim3((waves + 3) / 4), dim3(256), 0, s, a);
   DCNN_LAUNCH_CHECK();
 }
 
