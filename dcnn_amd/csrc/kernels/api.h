@@ -130,6 +130,8 @@ void elementwise(int mode, int op, const float* a, const float* b, float* c, lon
 void reduce(int op, const float* a, const float* b, long n, float* workspace, float* out, hipStream_t s);
 void fill_random(float* out, long n, uint64_t seed, float a, float b, int normal, hipStream_t s);
 void transpose_batched(const float* in, float* out, int batch, int rows, int cols, hipStream_t s);
+void transpose_batched16(const void* in, void* out, int batch, int rows, int cols, hipStream_t s);
+void rows_copy(int kind, const void* src, int lds, void* dst, int ldd, long rows, int cols, hipStream_t s);
 void nchw_cnhw(const float* in, float* out, int N, int C, int HW, int to_cnhw, hipStream_t s);
 void pad_crop(const float* in, float* out, int NC, int H, int W, int OH, int OW, int top, int left, float value,
               hipStream_t s);

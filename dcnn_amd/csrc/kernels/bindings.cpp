@@ -80,6 +80,12 @@ PYBIND11_MODULE(_kernels, m) {
   m.def("fill_random", [](uintptr_t out, long n, uint64_t seed, float a, float b, int normal, uintptr_t st) {
     fill_random(P<float*>(out), n, seed, a, b, normal, S(st));
   });
+  m.def("transpose_batched16", [](uintptr_t in, uintptr_t out, int batch, int rows, int cols, uintptr_t st) {
+    transpose_batched16(P<const void*>(in), P<void*>(out), batch, rows, cols, S(st));
+  });
+  m.def("rows_copy", [](int kind, uintptr_t src, int lds, uintptr_t dst, int ldd, long rows, int cols, uintptr_t st) {
+    rows_copy(kind, P<const void*>(src), lds, P<void*>(dst), ldd, rows, cols, S(st));
+  });
   m.def("transpose_batched", [](uintptr_t in, uintptr_t out, int batch, int rows, int cols, uintptr_t st) {
     transpose_batched(P<const float*>(in), P<float*>(out), batch, rows, cols, S(st));
   });

@@ -1,5 +1,5 @@
 // Streaming 1x1 convolution (and its stride-1 data gradient) for CDNA4: wave-independent,
-// weight-stationary, no barriers (LDS only for per-wave channel constants).
+// weight-stationary, no barriers in the tile loop.
 //
 // Why (profiles/conv_r50_r3.md): the 1x1 convs of a ResNet bottleneck have K = 64..128 input
 // channels, so the gathered GEMM (gemm2.hip) runs ONE K step per 128x128 tile and then a
@@ -8,18 +8,22 @@
 // 5x off their HBM floor.
 //
 // Here every wave is its own pipeline:
-//  * a wave owns 64 output channels (the A operand: its weights [64][K] live in VGPRs for the
-//    whole kernel, loaded once) and a contiguous range of 32-pixel tiles;
+//  * a wave owns 64 output channels (the A operand) and a contiguous range of 32-pixel tiles.
+//    K = 64 / 128: its weights [64][K] live in VGPRs for the whole kernel (loaded once);
+//    K = 256 / 512 (and the K = 128 data gradient): the workgroup's 4 waves share one channel slice
+//    whose weights sit in LDS (rows padded by 16 B: conflict-free, immediate-offset fragment
+//    reads), and B streams in 128-channel chunks through a two-buffer register ring;
 //  * per tile it loads the B fragments (16 pixels x 8 channels per lane, 16-byte global loads
-//    straight into registers), issues 16 x K/32 mfma_f32_16x16x32_bf16, starts the NEXT tile's
-//    loads, and runs the epilogue from registers: an accumulator quad is 4 consecutive channels
-//    of one pixel, stored as 8 bytes of an NHWC row;
+//    straight into registers, the next tile's issued before this tile's MFMAs), issues
+//    16 x K/32 mfma_f32_16x16x32_bf16 per 64 channels, and runs the epilogue from registers: an
+//    accumulator quad is 4 consecutive channels of one pixel, staged in the wave's LDS slice and
+//    stored as full 128-byte pixel rows (8 lanes per row);
 //  * BatchNorm statistics accumulate in registers across all tiles of the wave (pivot-shifted
 //    sums, packed fp32 math) and are reduced over the 16 lanes of a DPP row ONCE per wave, so the
 //    statistics slab has one row per pixel range instead of one per 128-pixel tile (the
 //    bn_stat_reduce that follows reads 8-16x fewer rows);
-//  * the waves of a CU drift into different phases (no barriers), so one wave's epilogue VALU
-//    and stores overlap another's MFMAs and loads.
+//  * no barriers after the prologue: the waves of a CU drift into different phases, so one
+//    wave's epilogue VALU and stores overlap another's MFMAs and loads.
 //
 // Modes: 0 plain (optional bias / residual / ReLU), 1 forward with Welford statistics of the
 // stored values, 2 data gradient with the backward-BatchNorm fusion of the producing layer
@@ -98,10 +102,18 @@ static int g_g1s_pf = [] {
 }();
 static int g1s_occ_rt(int K, int mode) { return (K == 64 && mode != 2 && g_g1s_occ3) ? 3 : 2; }
 constexpr int kG1sTile = 32;  // pixels per tile (16 * TJ)
+// weights in LDS (shared by the workgroup's 4 waves) instead of VGPRs: K >= 256, and the K = 128
+// data gradient (its three epilogue operands leave no room for 64 weight VGPRs)
+constexpr bool g1s_wl(int K, int mode) { return K >= 256 || (K == 128 && mode == 2); }
 
 template <int K, int MODE, int OCC, int PF, bool EP>
 __global__ void __launch_bounds__(256, OCC) g1s_kernel(G1sArgs p) {
   constexpr int KK = K / 32, TJ = 2, TP = 16 * TJ;
+  // K >= 256: the 64 x K weight slice lives in LDS, shared by the workgroup's 4 waves (same
+  // channel slice, 4 pixel ranges), instead of K / 2 VGPRs per lane
+  constexpr bool WL = g1s_wl(K, MODE);
+  // output stage only where the LDS budget keeps two workgroups per CU
+  constexpr bool STG = K <= 256;
   static_assert(TP == kG1sTile, "tile size");
   static_assert(PF == 1 || PF == 2 || PF == 4, "prefetch depth (the tile loop is unrolled by it)");
   static_assert(PF == 2 || !EP, "epilogue-operand ping-pong assumes the 2-tile unroll");
@@ -111,16 +123,35 @@ __global__ void __launch_bounds__(256, OCC) g1s_kernel(G1sArgs p) {
   // wave's 64 channels) and the per-wave output stage; each wave touches only its own slices
   // (no barrier: LDS ops of one wave execute in order, and LDS reads never wait for stores)
   __shared__ __attribute__((aligned(16))) float cst[4][2][64];
-  __shared__ __attribute__((aligned(16))) char stage[4][TP * 128];
+  __shared__ __attribute__((aligned(16))) char stage[4][STG ? TP * 128 : 16];
+  constexpr int WPITCH = K * 2 + 16;
+  __shared__ __attribute__((aligned(16))) char wlds[WL ? 64 * WPITCH : 16];
   char* stg = stage[wid];
   if (p.zero_ptr && blockIdx.x == 0)
     for (int i = threadIdx.x; i < p.zero_n; i += 256) p.zero_ptr[i] = 0.f;
   const int CS = p.N >> 6;
-  const int gw = xcd_remap_g1(blockIdx.x, gridDim.x) * 4 + wid;
-  if (gw >= p.PR * CS) return;
-  const int cs = gw % CS, pr = gw / CS;
+  const int blk = xcd_remap_g1(blockIdx.x, gridDim.x);
+  int cs, pr;
+  if (WL) {  // workgroup = one channel slice x 4 consecutive pixel ranges
+    cs = blk % CS;
+    pr = (blk / CS) * 4 + wid;
+    // rows padded by one 16-byte chunk (pitch WPITCH): the 16 rows an A-fragment read group
+    // touches start on 16 distinct bank slots (conflict-free ds_read_b128), and every fragment
+    // address is one per-lane base plus an immediate
+    for (int q = threadIdx.x; q < 64 * (K / 8); q += 256) {
+      const int r = q / (K / 8), c = q % (K / 8);
+      *reinterpret_cast<uint4*>(wlds + r * WPITCH + c * 16) =
+          *reinterpret_cast<const uint4*>(p.Wt + (size_t)(cs * 64 + r) * K + c * 8);
+    }
+    __syncthreads();
+  } else {
+    const int gw = blk * 4 + wid;
+    if (gw >= p.PR * CS) return;
+    cs = gw % CS;
+    pr = gw / CS;
+  }
   const int n0 = cs * 64;
-  const int t0 = pr * p.tpr, t1 = min(p.tiles, t0 + p.tpr);
+  const int t0 = min(p.tiles, pr * p.tpr), t1 = min(p.tiles, t0 + p.tpr);
 
   if (MODE == 2) {
     cst[wid][0][lane] = p.bnb.mean[n0 + lane];
@@ -129,12 +160,22 @@ __global__ void __launch_bounds__(256, OCC) g1s_kernel(G1sArgs p) {
     cst[wid][0][lane] = p.bias ? p.bias[n0 + lane] : 0.f;
   }
   // weights: A fragment (channel subtile i, k step kk): row n0 + 16 i + lr, k = 32 kk + 8 lh
-  bf16x8 wa[4][KK];
+  bf16x8 wa[4][WL ? 1 : KK];
+  if constexpr (!WL) {
 #pragma unroll
-  for (int i = 0; i < 4; ++i)
+    for (int i = 0; i < 4; ++i)
 #pragma unroll
-    for (int kk = 0; kk < KK; ++kk)
-      wa[i][kk] = *reinterpret_cast<const bf16x8*>(p.Wt + (size_t)(n0 + i * 16 + lr) * K + kk * 32 + lh * 8);
+      for (int kk = 0; kk < KK; ++kk)
+        wa[i][kk] = *reinterpret_cast<const bf16x8*>(p.Wt + (size_t)(n0 + i * 16 + lr) * K + kk * 32 + lh * 8);
+  }
+  int wl_off = lr * WPITCH + lh * 16;
+  auto afrag = [&](int i, int kk) -> bf16x8 {
+    if constexpr (WL) {
+      return *reinterpret_cast<const bf16x8*>(wlds + wl_off + i * 16 * WPITCH + kk * 64);
+    } else {
+      return wa[i][kk];
+    }
+  };
 
   const bool plain = p.S == 1 && p.OH == p.H && p.OW == p.W;
   const int ohw = p.OH * p.OW;
@@ -145,8 +186,9 @@ __global__ void __launch_bounds__(256, OCC) g1s_kernel(G1sArgs p) {
     return ((long)img * p.H + oy * p.S) * p.W + ox * p.S;
   };
   // B fragments of PF tiles in flight (ring, statically indexed by the unrolled loop)
-  bf16x8 bb[PF][TJ][KK];
-  auto load_b = [&](bf16x8 (&b)[TJ][KK], int t) {
+  bf16x8 bb[PF][TJ][WL ? 1 : KK];
+  auto load_b = [&](bf16x8 (&b)[TJ][WL ? 1 : KK], int t) {
+    if constexpr (WL) return;
 #pragma unroll
     for (int j = 0; j < TJ; ++j) {
       const bf16* q = p.X + src_px(t * TP + j * 16 + lr) * K + lh * 8;
@@ -155,20 +197,24 @@ __global__ void __launch_bounds__(256, OCC) g1s_kernel(G1sArgs p) {
     }
   };
   // epilogue operands (residual or the BatchNorm's y, and its x), one tile ahead (ping-pong)
-  const bool has_res = MODE == 0 && p.residual != nullptr;
+  const bool has_res = MODE != 1 && p.residual != nullptr;
   const bool has_y = MODE == 2 && p.bnb.y != nullptr;
   const bool has_e = has_res || MODE == 2;
   const bool relu = MODE == 0 && p.relu;
-  uint2 eo[2][2][4][TJ];
-  auto load_e = [&](uint2 (&e)[2][4][TJ], int t) {
+  // e[0]: residual (modes 0 / 2), e[1]: the BatchNorm's x (mode 2), e[2]: its output y (mode 2)
+  constexpr int NE = MODE == 2 ? 3 : 1;
+  uint2 eo[2][NE][4][TJ];
+  auto load_e = [&](uint2 (&e)[NE][4][TJ], int t) {
 #pragma unroll
     for (int j = 0; j < TJ; ++j) {
       const size_t row = (size_t)(t * TP + j * 16 + lr) * p.N + n0 + lh * 4;
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
-        e[0][i][j] = has_res ? *reinterpret_cast<const uint2*>(p.residual + row + i * 16)
-                     : has_y ? *reinterpret_cast<const uint2*>(p.bnb.y + row + i * 16) : make_uint2(0u, 0u);
-        e[1][i][j] = MODE == 2 ? *reinterpret_cast<const uint2*>(p.bnb.x + row + i * 16) : make_uint2(0u, 0u);
+        e[0][i][j] = has_res ? *reinterpret_cast<const uint2*>(p.residual + row + i * 16) : make_uint2(0u, 0u);
+        if constexpr (MODE == 2) {
+          e[1][i][j] = *reinterpret_cast<const uint2*>(p.bnb.x + row + i * 16);
+          e[2][i][j] = has_y ? *reinterpret_cast<const uint2*>(p.bnb.y + row + i * 16) : make_uint2(0u, 0u);
+        }
       }
     }
   };
@@ -182,20 +228,54 @@ __global__ void __launch_bounds__(256, OCC) g1s_kernel(G1sArgs p) {
 
   // one tile: the load of tile t + PF - 1 goes out first (into the buffer tile t - 1 used), then
   // the MFMAs, the next tile's epilogue operands, and the epilogue of this one
-  auto tile = [&](int t, bf16x8 (&bc)[TJ][KK], bf16x8 (&bn)[TJ][KK], uint2 (&ec)[2][4][TJ], uint2 (&en)[2][4][TJ]) {
-    if (PF > 1 && t + PF - 1 < t1) load_b(bn, t + PF - 1);
+  // K >= 256: B streams in 128-channel chunks through a two-buffer ring (bq), the next tile's
+  // first chunk loading during this tile's last chunk
+  constexpr int NC = WL ? KK / 4 : 1;
+  bf16x8 bq[2][TJ][4];
+  auto load_chunk = [&](bf16x8 (&b)[TJ][4], int t, int c) {
+#pragma unroll
+    for (int j = 0; j < TJ; ++j) {
+      const bf16* q = p.X + src_px(t * TP + j * 16 + lr) * K + c * 128 + lh * 8;
+#pragma unroll
+      for (int u = 0; u < 4; ++u) b[j][u] = *reinterpret_cast<const bf16x8*>(q + u * 32);
+    }
+  };
+  auto tile = [&](int t, bf16x8 (&bc)[TJ][WL ? 1 : KK], bf16x8 (&bn)[TJ][WL ? 1 : KK], uint2 (&ec)[NE][4][TJ], uint2 (&en)[NE][4][TJ]) {
     f32x4 acc[4][TJ];
 #pragma unroll
     for (int i = 0; i < 4; ++i)
 #pragma unroll
       for (int j = 0; j < TJ; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+    if constexpr (WL) {
+      // the weight slice never changes after the barrier: keep the compiler from hoisting all
+      // 4 x K / 32 fragment reads out of the tile loop (K / 2 VGPRs of live fragments)
+      asm volatile("" : "+v"(wl_off));
 #pragma unroll
-    for (int kk = 0; kk < KK; ++kk)
+      for (int c = 0; c < NC; ++c) {
+        if (c + 1 < NC) load_chunk(bq[(c + 1) & 1], t, c + 1);
+        else if (t + 1 < t1) load_chunk(bq[(c + 1) & 1], t + 1, 0);
 #pragma unroll
-      for (int i = 0; i < 4; ++i)
+        for (int u = 0; u < 4; ++u)
 #pragma unroll
-        for (int j = 0; j < TJ; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wa[i][kk], bc[j][kk], acc[i][j], 0, 0, 0);
-    if (PF == 1 && t + 1 < t1) load_b(bc, t + 1);  // one buffer: reloaded once the MFMAs have read it
+          for (int i = 0; i < 4; ++i) {
+            const bf16x8 av = afrag(i, c * 4 + u);
+#pragma unroll
+            for (int j = 0; j < TJ; ++j)
+              acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(av, bq[c & 1][j][u], acc[i][j], 0, 0, 0);
+          }
+      }
+    } else {
+      if (PF > 1 && t + PF - 1 < t1) load_b(bn, t + PF - 1);
+#pragma unroll
+      for (int kk = 0; kk < KK; ++kk)
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          const bf16x8 av = afrag(i, kk);
+#pragma unroll
+          for (int j = 0; j < TJ; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(av, bc[j][kk], acc[i][j], 0, 0, 0);
+        }
+      if (PF == 1 && t + 1 < t1) load_b(bc, t + 1);  // one buffer: reloaded once the MFMAs have read it
+    }
     if (has_e) {
       if (EP) { if (t + 1 < t1) load_e(en, t + 1); }
       else load_e(ec, t);  // operand loads still ahead of this tile's stores
@@ -230,12 +310,12 @@ __global__ void __launch_bounds__(256, OCC) g1s_kernel(G1sArgs p) {
           for (int r = 0; r < 4; ++r) f[r] = fmaxf(f[r], 0.f);
         }
         if (has_y) {
-          const f32x2 y01 = bf2_to_f2(ec[0][i][j].x), y23 = bf2_to_f2(ec[0][i][j].y);
+          const f32x2 y01 = bf2_to_f2(ec[NE - 1][i][j].x), y23 = bf2_to_f2(ec[NE - 1][i][j].y);
           f[0] = y01.x > 0.f ? f[0] : 0.f; f[1] = y01.y > 0.f ? f[1] : 0.f;
           f[2] = y23.x > 0.f ? f[2] : 0.f; f[3] = y23.y > 0.f ? f[3] : 0.f;
         }
         const uint2 o = make_uint2(f2_to_bf2(f[0], f[1]), f2_to_bf2(f[2], f[3]));
-        if (p.dbg & 2) {  // direct 8-byte stores (16 pixel rows x 32 B per instruction)
+        if (!STG || (p.dbg & 2)) {  // direct 8-byte stores (16 pixel rows x 32 B per instruction)
           if (!(p.dbg & 1)) *reinterpret_cast<uint2*>(p.Y + (size_t)(t * TP + j * 16 + lr) * p.N + n0 + lh * 4 + i * 16) = o;
         } else {
           // full-line stores: the tile's 32 pixel rows (128 B each, 16-byte chunks XOR-swizzled by
@@ -251,7 +331,7 @@ __global__ void __launch_bounds__(256, OCC) g1s_kernel(G1sArgs p) {
           sb[i][0] += d01 * d01; sb[i][1] += d23 * d23;
         } else if constexpr (MODE == 2) {
           const f32x2 g01 = bf2_to_f2(o.x), g23 = bf2_to_f2(o.y);
-          const f32x2 x01 = bf2_to_f2(ec[1][i][j].x), x23 = bf2_to_f2(ec[1][i][j].y);
+          const f32x2 x01 = bf2_to_f2(ec[NE > 1 ? 1 : 0][i][j].x), x23 = bf2_to_f2(ec[NE > 1 ? 1 : 0][i][j].y);
           const f32x2 h01 = (x01 - f32x2{c0.x, c0.y}) * f32x2{c1.x, c1.y};
           const f32x2 h23 = (x23 - f32x2{c0.z, c0.w}) * f32x2{c1.z, c1.w};
           sa[i][0] += g01; sa[i][1] += g23;
@@ -259,7 +339,7 @@ __global__ void __launch_bounds__(256, OCC) g1s_kernel(G1sArgs p) {
         }
       }
     }
-    if (!(p.dbg & 3)) {
+    if (STG && !(p.dbg & 3)) {
 #pragma unroll
       for (int k = 0; k < TP / 8; ++k) {
         const int P = k * 8 + (lane >> 3), c = lane & 7;
@@ -269,9 +349,13 @@ __global__ void __launch_bounds__(256, OCC) g1s_kernel(G1sArgs p) {
     }
   };
 
+  if constexpr (WL) {
+    if (t0 < t1) load_chunk(bq[0], t0, 0);
+  } else {
 #pragma unroll
-  for (int d = 0; d < (PF > 1 ? PF - 1 : 1); ++d)
-    if (t0 + d < t1) load_b(bb[d], t0 + d);
+    for (int d = 0; d < (PF > 1 ? PF - 1 : 1); ++d)
+      if (t0 + d < t1) load_b(bb[d], t0 + d);
+  }
   if (EP && has_e && t0 < t1) load_e(eo[0], t0);
   if constexpr (PF == 1) {
     for (int t = t0; t < t1; ++t) tile(t, bb[0], bb[0], eo[0], eo[0]);
@@ -287,7 +371,7 @@ __global__ void __launch_bounds__(256, OCC) g1s_kernel(G1sArgs p) {
     }
   }
   if constexpr (MODE != 0) {
-    const float npx = (float)((t1 - t0) * TP);
+    const float npx = (float)((t1 - t0) * TP);  // (0 for an empty trailing range: a zero row)
 #pragma unroll
     for (int i = 0; i < 4; ++i)
 #pragma unroll
@@ -320,13 +404,22 @@ void g1s_enable(int on) { g_g1s = on; }
 // input channels in `mode`; 0 when the shape does not run on it. The ranges are sized so every
 // resident wave slot holds one wave (two per SIMD when the registers allow, else one).
 int g1s_rows(int M, int N, int K, int mode) {
-  if (!g_g1s || M % 64 || N % 64 || (K != 64 && K != 128)) return 0;
+  if (!g_g1s || M % 64 || N % 64 || (K != 64 && K != 128 && K != 256 && K != 512)) return 0;
   const int tiles = M / kG1sTile, CS = N / 64;
   const long waves = 256l * 4 * g1s_occ_rt(K, mode);
   int pr = (int)((waves + CS - 1) / CS);
   if (pr > tiles) pr = tiles;
   const int tpr = (tiles + pr - 1) / pr;
-  return (tiles + tpr - 1) / tpr;
+  pr = (tiles + tpr - 1) / tpr;
+  if (g1s_wl(K, mode)) pr = (pr + 3) / 4 * 4;  // 4 pixel ranges per workgroup (trailing ones may be empty)
+  return pr;
+}
+static int g1s_tpr(int M, int N, int K, int mode) {
+  const int tiles = M / kG1sTile, CS = N / 64;
+  const long waves = 256l * 4 * g1s_occ_rt(K, mode);
+  int pr = (int)((waves + CS - 1) / CS);
+  if (pr > tiles) pr = tiles;
+  return (tiles + pr - 1) / pr;
 }
 
 template <int K, int MODE, int OCC = 2>
@@ -334,8 +427,8 @@ static void launch_g1s(const G1sArgs& a, hipStream_t s) {
   const int waves = a.PR * (a.N / 64);
   // B fragments two tiles deep; epilogue operands (residual / BatchNorm y, x) one tile ahead only
   // with DCNN_G1S_PF=3 (more registers: spills on the wider instances)
-  // (K = 128: one B buffer, reloaded after the MFMAs — the two-deep ring spills there)
-  if (K == 128 || g_g1s_pf == 1)
+  // (K >= 128: one B buffer, reloaded after the MFMAs — the two-deep ring spills there)
+  if (K >= 128 || g_g1s_pf == 1)
     hipLaunchKernelGGL((g1s_kernel<K, MODE, OCC, 1, false>), dim3((waves + 3) / 4), dim3(256), 0, s, a);
   else if (g_g1s_pf == 3)
     hipLaunchKernelGGL((g1s_kernel<K, MODE, OCC, 2, true>), dim3((waves + 3) / 4), dim3(256), 0, s, a);
@@ -353,14 +446,15 @@ void g1s(const bf16* X, const bf16* Wt, bf16* Y, int M, int N, int K, int H, int
   if (!rows) throw std::runtime_error("g1s: unsupported shape");
   if (mode < 0 || mode > 2 || (mode != 0 && !stats)) throw std::runtime_error("g1s: bad mode / statistics slab");
   if (mode == 2 && (!bnb.x || !bnb.mean || !bnb.istd || S != 1)) throw std::runtime_error("g1s: bnb operands missing");
-  if (mode != 0 && (residual || relu)) throw std::runtime_error("g1s: residual / ReLU only without statistics");
+  if (mode == 1 && residual) throw std::runtime_error("g1s: no residual with forward statistics");
+  if (mode != 0 && relu) throw std::runtime_error("g1s: ReLU only without statistics");
   if ((long)M != (long)(M / (OH * OW)) * OH * OW || OH != (H - 1) / S + 1 || OW != (W - 1) / S + 1)
     throw std::runtime_error("g1s: inconsistent geometry");
   G1sArgs a{};
   a.X = X; a.Wt = Wt; a.Y = Y;
   a.M = M; a.N = N; a.K = K; a.H = H; a.W = W; a.OH = OH; a.OW = OW; a.S = S;
   a.tiles = M / kG1sTile;
-  a.tpr = (a.tiles + rows - 1) / rows;
+  a.tpr = g1s_tpr(M, N, K, mode);
   a.PR = rows;
   a.bias = bias; a.residual = residual; a.stats = stats; a.relu = relu;
   a.zero_ptr = zero_ptr; a.zero_n = zero_n;
@@ -376,6 +470,8 @@ void g1s(const bf16* X, const bf16* Wt, bf16* Y, int M, int N, int K, int H, int
   }
   DCNN_G1S(64)
   DCNN_G1S(128)
+  DCNN_G1S(256)
+  DCNN_G1S(512)
 #undef DCNN_G1S
   throw std::runtime_error("g1s: no kernel instance");
 }

@@ -172,6 +172,62 @@ void transpose_batched(const float* in, float* out, int batch, int rows, int col
   hipLaunchKernelGGL(transpose_kernel, g, dim3(256), 0, s, in, out, rows, cols);
 }
 
+// the same for 16-bit elements (bf16 activations): NCHW <-> NHWC around the NCHW-order Flatten of
+// a spatial map (per image [C][HW] <-> [HW][C])
+__global__ void transpose16_kernel(const unsigned short* __restrict__ in, unsigned short* __restrict__ out, int rows,
+                                   int cols) {
+  __shared__ unsigned short tile[64][66];
+  const long boff = (long)blockIdx.z * rows * cols;
+  const int r0 = blockIdx.y * 64, c0 = blockIdx.x * 64;
+  const int tx = threadIdx.x & 63, ty = threadIdx.x >> 6;
+  for (int j = ty; j < 64; j += 4) {
+    const int r = r0 + j, c = c0 + tx;
+    tile[j][tx] = (r < rows && c < cols) ? in[boff + (long)r * cols + c] : (unsigned short)0;
+  }
+  __syncthreads();
+  for (int j = ty; j < 64; j += 4) {
+    const int c = c0 + j, r = r0 + tx;
+    if (c < cols && r < rows) out[boff + (long)c * rows + r] = tile[tx][j];
+  }
+}
+
+void transpose_batched16(const void* in, void* out, int batch, int rows, int cols, hipStream_t s) {
+  dim3 g((cols + 63) / 64, (rows + 63) / 64, batch);
+  hipLaunchKernelGGL(transpose16_kernel, g, dim3(256), 0, s, (const unsigned short*)in, (unsigned short*)out, rows,
+                     cols);
+  DCNN_LAUNCH_CHECK();
+}
+
+// ---- strided row copy / accumulate: dst[r][c] (+)= src[r][c], c < cols, row pitches lds / ldd
+// (channel-padded conv operands: the RGB-like conv's bf16 weight rows into an 8-channel padded
+// operand, and its padded weight gradient back into the real channels). kind: 0 bf16 -> bf16
+// copy, 1 fp32 -> fp32 accumulate.
+template <class TI, class TO, bool ACC>
+__global__ void rows_copy_kernel(const TI* __restrict__ src, int lds, TO* __restrict__ dst, int ldd, long rows,
+                                 int cols) {
+  const long total = rows * cols;
+  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < total; i += (long)gridDim.x * blockDim.x) {
+    const long r = i / cols;
+    const int c = (int)(i - r * cols);
+    const float v = to_f(src[r * lds + c]);
+    TO* d = dst + r * ldd + c;
+    *d = from_f<TO>(ACC ? to_f(*d) + v : v);
+  }
+}
+
+void rows_copy(int kind, const void* src, int lds, void* dst, int ldd, long rows, int cols, hipStream_t s) {
+  const int g = grid_for(rows * cols, 256);
+  if (kind == 0)
+    hipLaunchKernelGGL((rows_copy_kernel<bf16, bf16, false>), dim3(g), dim3(256), 0, s, (const bf16*)src, lds,
+                       (bf16*)dst, ldd, rows, cols);
+  else if (kind == 1)
+    hipLaunchKernelGGL((rows_copy_kernel<float, float, true>), dim3(g), dim3(256), 0, s, (const float*)src, lds,
+                       (float*)dst, ldd, rows, cols);
+  else
+    throw std::runtime_error("rows_copy: bad kind");
+  DCNN_LAUNCH_CHECK();
+}
+
 // NCHW [N][C][HW] <-> CNHW [C][N][HW]: a permutation of HW-contiguous rows
 __global__ void nchw_cnhw_kernel(const float* __restrict__ in, float* __restrict__ out, int N, int C, int HW,
                                  int to_cnhw) {

@@ -259,7 +259,8 @@ class Dense(ParameterizedLayer):
         if len(in_shape) == 4 and (in_shape[2] != 1 or in_shape[3] != 1):
             dx = dx.view(in_shape)
             if dx.is_cuda:
-                dx = dx.contiguous(memory_format=torch.channels_last)
+                from ...ops import hip
+                dx = hip.nchw_nhwc(dx, True)  # NCHW-order rows -> the NHWC activation layout
             return dx
         return dx.view(in_shape)
 

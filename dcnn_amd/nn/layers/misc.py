@@ -199,15 +199,20 @@ class Flatten(StatelessLayer):
         x = self._to_layer_device(x)
         self._cache[mb_id] = tuple(x.shape)
         n = x.shape[0]
-        if x.dim() == 4 and (x.shape[2] != 1 or x.shape[3] != 1):
-            x = x.contiguous()
+        if x.dim() == 4 and (x.shape[2] != 1 or x.shape[3] != 1) and not x.is_contiguous():
+            if x.is_cuda and x.is_contiguous(memory_format=torch.channels_last):
+                from ...ops import hip
+                x = hip.nchw_nhwc(x, False)  # NHWC activation -> NCHW order (reference flatten order)
+            else:
+                x = x.contiguous()
         return x.reshape(n, -1, 1, 1)
 
     def backward(self, grad, mb_id=0):
         shape = self._cache.pop(mb_id)
         g = grad.reshape(shape)
-        if g.is_cuda and len(shape) == 4:
-            g = g.contiguous(memory_format=torch.channels_last)
+        if g.is_cuda and len(shape) == 4 and not g.is_contiguous(memory_format=torch.channels_last):
+            from ...ops import hip
+            g = hip.nchw_nhwc(g.contiguous(), True)
         return g
 
     def compute_output_shape(self, s):

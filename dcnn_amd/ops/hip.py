@@ -63,6 +63,26 @@ def to_act(x: torch.Tensor, dtype: torch.dtype) -> torch.Tensor:
     return x.to(dtype=dtype).contiguous(memory_format=CL)
 
 
+def nchw_nhwc(x: torch.Tensor, to_nhwc: bool) -> torch.Tensor:
+    """Physical layout change of a 4-D GPU activation (the NCHW-order Flatten of a spatial map):
+    NCHW-contiguous -> channels_last (to_nhwc) or back, one transpose kernel per call (fp32 / bf16)."""
+    N, C, H, W = x.shape
+    if to_nhwc:
+        assert x.is_contiguous()
+        y = _empty((N, C, H, W), x.dtype, x.device, True)
+        rows, cols = C, H * W
+    else:
+        assert x.is_contiguous(memory_format=CL)
+        y = _empty((N, C, H, W), x.dtype, x.device, False)
+        rows, cols = H * W, C
+    if x.dtype == F32:
+        kernels().transpose_batched(x.data_ptr(), y.data_ptr(), N, rows, cols, stream_ptr())
+    else:
+        assert x.element_size() == 2
+        kernels().transpose_batched16(x.data_ptr(), y.data_ptr(), N, rows, cols, stream_ptr())
+    return y
+
+
 def conv_out_hw(H, W, kh, kw, sh, sw, ph, pw):
     return (H + 2 * ph - kh) // sh + 1, (W + 2 * pw - kw) // sw + 1
 
@@ -374,7 +394,11 @@ def pad_weight_channels(w, cp, out=None):
     Co, Ci, KH, KW = w.shape
     if out is None or tuple(out.shape) != (Co, KH, KW, cp) or out.device != w.device:
         out = _arena.persistent((Co, KH, KW, cp), BF16, w.device, zero=True)  # cached by the layer
-    out[..., :Ci] = w.permute(0, 2, 3, 1).to(BF16)
+    if w.dtype == BF16 and w.is_contiguous(memory_format=CL):
+        # the layer's bf16 shadow: [Co*KH*KW] rows of Ci channels into rows of cp (one HIP pass)
+        kernels().rows_copy(0, w.data_ptr(), Ci, out.data_ptr(), cp, Co * KH * KW, Ci, stream_ptr())
+    else:
+        out[..., :Ci] = w.permute(0, 2, 3, 1).to(BF16)
     return out
 
 
@@ -676,7 +700,7 @@ def conv2d_dgrad(dy, wt, x_shape, stride, pad, *, residual=None, bnb=None):
             dx._bnb = (bnb.bn, fst if fst is not None else slab, rows, sums)
         return dx
     if (not f32 and (KH, KW) == (1, 1) and (sh, sw) == (1, 1) and (ph, pw) == (0, 0) and not empty_class
-            and len(classes) == 1 and (residual is None or not fuse)):
+            and len(classes) == 1):
         # streaming 1x1 data gradient (g1s.hip), backward-BatchNorm fusion in its epilogue
         rows = K.g1s_rows(N * H * W, Ci, Co, 2 if fuse else 0)
         if rows:
@@ -926,7 +950,10 @@ def conv2d_wgrad(dy, x, w_shape, stride, pad, grad_w, grad_b=None):
             return
         tmp = _empty((Co, KH, KW, Cx), F32, x.device)
         K.splitk_reduce(slab.data_ptr(), tmp.data_ptr(), Co * Ng, splits, 0, st)
-        grad_w.add_(tmp[..., :Ci].permute(0, 3, 1, 2))
+        if grad_w.is_contiguous(memory_format=CL):
+            K.rows_copy(1, tmp.data_ptr(), Cx, grad_w.data_ptr(), Ci, Co * KH * KW, Ci, st)
+        else:
+            grad_w.add_(tmp[..., :Ci].permute(0, 3, 1, 2))
         if grad_b is not None:
             K.splitk_reduce(bslab.data_ptr(), grad_b.data_ptr(), Co, splits, 1, st)
         return

@@ -3,7 +3,7 @@ against the gathered-GEMM path it replaces (gemm2.hip, DCNN_G1S=0 / g1s_enable(0
 
 Forward (+ bias / residual / ReLU, + Welford BatchNorm statistics of the stored values) and the
 stride-1 data gradient with the backward-BatchNorm fusion (ReLU mask + g / g*xhat sums) of the
-producing layer, on ResNet-50 bottleneck shapes (K = 64 / 128 input channels).
+producing layer, on ResNet-50 bottleneck shapes (K = 64 / 128 in VGPRs, 256 / 512 in LDS).
 """
 import math
 
@@ -42,6 +42,10 @@ FWD_CASES = [
     (8, 64, 8, 8, 128, 2),       # strided projection (ResNet-18 layer 2)
     (2, 128, 16, 16, 256, 2),    # strided projection, K = 128
     (64, 128, 4, 4, 128, 1),     # 4x4 maps: several images per 64-pixel tile
+    (4, 256, 16, 16, 64, 1),     # layer-1 reduce (K = 256: weights in LDS)
+    (2, 512, 8, 8, 128, 1),      # layer-2 reduce (K = 512)
+    (4, 256, 16, 16, 128, 2),    # strided projection, K = 256
+    (4, 256, 4, 4, 64, 1),       # 2 tiles: trailing pixel ranges of a workgroup stay empty
 ]
 
 
@@ -114,10 +118,13 @@ def test_g1s_forward_residual_relu(hip, relu):
 
 
 DGRAD_CASES = [
-    # N, C (dgrad output = the BN'd input channels), H, W, Co (dgrad K), relu
-    (4, 256, 16, 16, 64, True),   # layer-1 reduce conv's input gradient (K = 64, N = 256)
-    (4, 512, 8, 8, 128, True),    # layer-2 reduce conv (K = 128)
-    (4, 64, 16, 16, 64, False),   # BN without a ReLU
+    # N, C (dgrad output = the BN'd input channels), H, W, Co (dgrad K), relu, residual
+    (4, 256, 16, 16, 64, True, False),   # layer-1 reduce conv's input gradient (K = 64, N = 256)
+    (4, 512, 8, 8, 128, True, False),    # layer-2 reduce conv (K = 128)
+    (4, 64, 16, 16, 64, False, False),   # BN without a ReLU
+    (4, 256, 16, 16, 64, True, True),    # + the shortcut's gradient (block input)
+    (4, 64, 16, 16, 256, True, False),   # expand conv's input gradient (K = 256)
+    (2, 128, 8, 8, 512, True, True),     # K = 512 with residual
 ]
 
 
@@ -125,7 +132,7 @@ DGRAD_CASES = [
 def test_g1s_dgrad_bwd_bn_fusion(hip, case):
     """1x1 dgrad with the producing BatchNorm's ReLU mask + backward sums fused == dgrad then the
     standalone BN backward; and the unfused dgrad equals torch."""
-    N, C, H, W, Co, relu = case
+    N, C, H, W, Co, relu, resid = case
     K = hip.kernels()
     assert K.g1s_rows(N * H * W, C, Co, 2) > 0
     torch.manual_seed(5)
@@ -138,13 +145,16 @@ def test_g1s_dgrad_bwd_bn_fusion(hip, case):
     w = (torch.randn(Co, C, 1, 1) / math.sqrt(C)).cuda().bfloat16().contiguous(memory_format=CL)
     wt = hip.conv_weight_t(w)
     dy = torch.randn(N, Co, H, W).cuda().bfloat16().contiguous(memory_format=CL)
-    d_ref = hip.conv2d_dgrad(dy, wt, (N, C, H, W), (1, 1), (0, 0))
+    r = torch.randn(N, C, H, W).cuda().bfloat16().contiguous(memory_format=CL) if resid else None
+    d_ref = hip.conv2d_dgrad(dy, wt, (N, C, H, W), (1, 1), (0, 0), residual=r)
     dx_t = torch.nn.grad.conv2d_input((N, C, H, W), w.float(), dy.float(), 1, 0)
+    if resid:
+        dx_t = dx_t + r.float()
     assert rel_err(d_ref, dx_t) < 1e-2
     dg0, db0 = torch.zeros(C, device="cuda"), torch.zeros(C, device="cuda")
     dx0, m0 = hip.bn_backward(d_ref, xb, yout, mean, istd, g, dg0, db0, want_masked=True)
     req = hip.BnbRequest("bn", yout, xb, mean, istd)
-    d = hip.conv2d_dgrad(dy, wt, (N, C, H, W), (1, 1), (0, 0), bnb=req)
+    d = hip.conv2d_dgrad(dy, wt, (N, C, H, W), (1, 1), (0, 0), residual=r, bnb=req)
     assert d._bnb[2] == K.g1s_rows(N * H * W, C, Co, 2)
     masked = d_ref.float() * (y.float() > 0) if relu else d_ref.float()
     assert rel_err(d, masked) < 1e-6
@@ -154,5 +164,5 @@ def test_g1s_dgrad_bwd_bn_fusion(hip, case):
     assert rel_err(dg1, dg0) < 1e-3, rel_err(dg1, dg0)
     assert rel_err(db1, db0) < 1e-3, rel_err(db1, db0)
     # deterministic
-    d2 = hip.conv2d_dgrad(dy, wt, (N, C, H, W), (1, 1), (0, 0), bnb=req)
+    d2 = hip.conv2d_dgrad(dy, wt, (N, C, H, W), (1, 1), (0, 0), residual=r, bnb=req)
     assert torch.equal(d, d2) and torch.equal(d._bnb[1], d2._bnb[1])
