@@ -601,13 +601,17 @@ bool hconv3_plan(int NB, int H, int W, int Cs, int N, int ntaps, H3Plan* pl) {
   // (LDS 72 KB). The 8- and 4-wide maps stay on hconv_kernel (measured faster there: their split-K
   // grids of single 8-wave workgroups lose more to the serial prologue / epilogue than the K loop
   // gains).
-  if (W % 16 || H % 16) return false;
+  // 8x8 maps (DCNN_HCONV3_8=1, experiment): 4 images of 8x8 per 256-pixel tile, halo pitch 10
+  static const int on8 = [] { const char* e = getenv("DCNN_HCONV3_8"); return e ? atoi(e) : 0; }();
+  const bool m8 = on8 && W == 8 && H == 8 && NB % 4 == 0;
+  if (!m8 && (W % 16 || H % 16)) return false;
   const int WC = 1, NW = 4, BN = 64, BM = 256;
-  const int TW = 16, TWC = 16, TH = 16, IMG = 1;
+  const int TW = m8 ? 8 : 16, TWC = TW, TH = m8 ? 8 : 16, IMG = m8 ? 4 : 1;
   const int NWI = (3 * BN / 16 + NW - 1) / NW;
   const int pitch = TW + 2;
   const int HN = (IMG * (TH + 2) * pitch + 16 * NW - 1) / (16 * NW);
-  if (HN != 6 || NWI != 3) return false;  // the one instance: <4, 1, 16, 6, 3, 2, 0>
+  // the instances: <4, 1, 16, 6, 3, 2, 0> (16-wide maps), <4, 1, 8, 7, 3, 2, 0> (8x8 maps)
+  if (!((TWC == 16 && HN == 6) || (TWC == 8 && HN == 7)) || NWI != 3) return false;
   pl->WC = WC; pl->TWC = TWC; pl->HN = HN; pl->NWI = NWI;
   pl->TH = TH; pl->TW = TW; pl->IMG = IMG; pl->pitch = pitch;
   pl->tiles_m = NB * H * W / BM;
@@ -637,6 +641,7 @@ static void launch_h3(const HConvArgs& a, const H3Geo& g, int grid, hipStream_t 
 
 static void launch_h3_plan(const H3Plan& pl, const HConvArgs& a, const H3Geo& g, int grid, hipStream_t s) {
   if (pl.WC == 1 && pl.TWC == 16 && pl.HN == 6 && pl.NWI == 3) return launch_h3<4, 1, 16, 6, 3, 2, 0>(a, g, grid, s);
+  if (pl.WC == 1 && pl.TWC == 8 && pl.HN == 7 && pl.NWI == 3) return launch_h3<4, 1, 8, 7, 3, 2, 0>(a, g, grid, s);
   throw std::runtime_error("hconv3: no kernel instance for this plan");
 }
 

@@ -4,6 +4,7 @@ the same op and against the previous-generation kernel (hconv3_enable(0)) on eve
 geometry, with every epilogue option (bias, residual, ReLU, forward BN statistics, backward-BN
 fusion) and split-K."""
 import math
+import os
 
 import pytest
 import torch
@@ -28,6 +29,8 @@ def hip():
 # (several 16x16 tiles per image, 64-channel tiles, split-K on the small grids)
 CASES = [(4, 64, 32, 32, 64), (2, 64, 32, 64, 64), (4, 128, 16, 16, 128), (2, 64, 16, 16, 64),
          (4, 64, 16, 16, 128), (2, 256, 16, 16, 256), (64, 64, 32, 32, 64), (4, 512, 16, 16, 128)]
+if os.environ.get("DCNN_HCONV3_8") == "1":  # 8x8 maps: 4 images per tile (experiment instance)
+    CASES += [(4, 256, 8, 8, 256), (8, 128, 8, 8, 64), (16, 512, 8, 8, 256), (64, 256, 8, 8, 256)]
 
 
 def _both(K, fn):
