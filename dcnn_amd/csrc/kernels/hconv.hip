@@ -638,6 +638,11 @@ static void hconv_pick(const HConvArgs& a, int* bm, int* bn) {
 bool hconv_supported(int NB, int H, int W, int Cs, int N, int ntaps) {
   // N = 32 runs as a 64-column tile whose upper half reads zero weights (buffer range check) and
   // is never stored: the 32-channel data gradient of a 32 -> 64 channel conv (ResNet-18 layer 1)
+  // Cs = 32 (one 32-channel chunk) only on the hconv3 kernel
+  if (Cs == 32) {
+    H3Plan pl;
+    return hconv3_plan(NB, H, W, Cs, N, ntaps, &pl);
+  }
   if (Cs % 64 || (N % 64 && N != 32) || ntaps < 1 || ntaps > 9) return false;
   HConvArgs a{};
   a.NB = NB; a.H = H; a.W = W; a.N = N;

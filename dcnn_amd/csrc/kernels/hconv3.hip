@@ -312,7 +312,7 @@ __global__ void __launch_bounds__(NW * 64, 8 / NW) hconv3_kernel(HConvArgs p, H3
     mm(1, 0, 4);
     mm(2, 0, 4);
   };
-  const int nch = g.nchunk;  // chunks of this split (even: the host guarantees it)
+  const int nch = g.nchunk;  // chunks of this split (even, or the single chunk of a 32-channel input)
 
   if constexpr (NWS == 3) {
     // 3-stage ring, stage = kernel row: step (c, dy) issues the weights of the step two ahead
@@ -343,7 +343,7 @@ __global__ void __launch_bounds__(NW * 64, 8 / NW) hconv3_kernel(HConvArgs p, H3
     for (int c = 0; c < nch; c += 2) {
       chunk(c, I0{});
       if (c == 0) stamp(2);
-      chunk(c + 1, I1{});
+      if (c + 1 < nch) chunk(c + 1, I1{});
     }
   } else {
     // 2-stage ring: step s uses stage s & 1 = (c + dy) & 1 and issues W(s + 1) (and, at dy = 0, the
@@ -374,7 +374,7 @@ __global__ void __launch_bounds__(NW * 64, 8 / NW) hconv3_kernel(HConvArgs p, H3
     for (int c = 0; c < nch; c += 2) {
       chunk(c, I0{});
       if (c == 0) stamp(2);
-      chunk(c + 1, I1{});
+      if (c + 1 < nch) chunk(c + 1, I1{});
     }
   }
   stamp(3);
@@ -596,7 +596,9 @@ struct H3Plan {
 
 // tile plan for a 3x3 stride-1 conv of NB x H x W pixels, Cs input / N output channels
 bool hconv3_plan(int NB, int H, int W, int Cs, int N, int ntaps, H3Plan* pl) {
-  if (!g_h3 || ntaps != 9 || Cs % 64 || N % 64) return false;  // even 32-channel chunk count
+  // an even 32-channel chunk count (split-K pairs), or one chunk (32 input channels: ResNet-18's
+  // first residual conv)
+  if (!g_h3 || ntaps != 9 || (Cs % 64 && Cs != 32) || N % 64) return false;
   // 16-wide (and wider) maps: 4-wave workgroups of 64 channels x one 16x16 tile, two per CU
   // (LDS 72 KB). The 8- and 4-wide maps stay on hconv_kernel (measured faster there: their split-K
   // grids of single 8-wave workgroups lose more to the serial prologue / epilogue than the K loop

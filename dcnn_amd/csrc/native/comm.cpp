@@ -342,6 +342,28 @@ bool MessageQueue::pop_command(uint16_t cmd, Message& out, int timeout_ms) {
   return true;
 }
 
+bool MessageQueue::pop_any(const std::vector<uint16_t>& cmds, Message& out, int timeout_ms) {
+  std::unique_lock<std::mutex> lk(mu_);
+  auto ready = [&] {
+    if (closed_) return true;
+    for (uint16_t c : cmds)
+      if (c < CMD_COUNT && !q_[c].empty()) return true;
+    return false;
+  };
+  if (timeout_ms < 0)
+    cv_.wait(lk, ready);
+  else if (!cv_.wait_until(lk, deadline_ms(timeout_ms), ready))
+    return false;
+  uint16_t best = CMD_COUNT;
+  for (uint16_t c : cmds)
+    if (c < CMD_COUNT && !q_[c].empty() && c < best) best = c;
+  if (best == CMD_COUNT) return false;
+  out = std::move(q_[best].front());
+  q_[best].pop_front();
+  --total_;
+  return true;
+}
+
 size_t MessageQueue::size() const {
   std::lock_guard<std::mutex> g(mu_);
   return total_;

@@ -84,6 +84,9 @@ class MessageQueue {
   // Pops the highest-priority (lowest command value) message; false on timeout (ms < 0: wait).
   bool pop(Message& out, int timeout_ms);
   bool pop_command(uint16_t cmd, Message& out, int timeout_ms);
+  // Pops the first queued message of the lowest-valued command in `cmds` that has one, waiting up
+  // to timeout_ms for any of them (a scheduler serving several kinds of completion at once)
+  bool pop_any(const std::vector<uint16_t>& cmds, Message& out, int timeout_ms);
   size_t size() const;
   size_t count(uint16_t cmd) const;
   void close();

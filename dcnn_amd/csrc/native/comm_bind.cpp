@@ -167,6 +167,18 @@ void bind_comm(py::module_& m) {
              return py::cast(std::move(out));
            },
            py::arg("command"), py::arg("timeout_ms") = -1)
+      .def("recv_any",
+           [](Communicator& self, std::vector<uint16_t> cmds, int timeout_ms) -> py::object {
+             Message out;
+             bool ok;
+             {
+               py::gil_scoped_release nogil;
+               ok = self.queue().pop_any(cmds, out, timeout_ms);
+             }
+             if (!ok) return py::none();
+             return py::cast(std::move(out));
+           },
+           py::arg("commands"), py::arg("timeout_ms") = -1)
       .def("deliver_local", [](Communicator& self, Message& msg) { self.queue().push(std::move(msg)); })
       .def("pending", [](Communicator& self) { return self.queue().size(); })
       .def("count", [](Communicator& self, uint16_t cmd) { return self.queue().count(cmd); })

@@ -317,27 +317,28 @@ class Coordinator:
             sent += 1
         self.max_in_flight_seen = sent
         deadline = time.time() + self.timeout_s
+        kinds = [int(C.FORWARD_JOB), int(C.BACKWARD_JOB)]
         while done < m:
             self._check_errors()
-            got = False
-            msg = self.comm.recv_command(int(C.FORWARD_JOB), 0)
-            if msg is not None:  # an output: loss, then its backward
-                got = True
+            # wait for EITHER completion: polling one queue with a timeout while the other kind
+            # arrives left the GPU idle for the rest of the timeout (profiles/pipeline_1f1b_r3.md)
+            msg = self.comm.recv_any(kinds, 20)
+            if msg is None:
+                if time.time() > deadline:
+                    raise PipelineError(f"1F1B: timeout ({done}/{m} backwards done)")
+                continue
+            if int(msg.command) == int(C.FORWARD_JOB):  # an output: loss, then its backward
                 mb = int(msg.mb_id)
                 loss, grad, c = self._loss_grad(self._output(msg), ys[mb], mb)
                 self.backward(grad, mb)
                 losses.append(loss)
                 corrects.append(c)
-            msg = self.comm.recv_command(int(C.BACKWARD_JOB), 0 if got else 20)
-            if msg is not None:  # a backward finished: admit the next forward
-                got = True
+            else:  # a backward finished: admit the next forward
                 done += 1
                 if sent < m:
                     self.forward(xs[sent], sent)
                     sent += 1
                     self.max_in_flight_seen = max(self.max_in_flight_seen, sent - done)
-            if not got and time.time() > deadline:
-                raise PipelineError(f"1F1B: timeout ({done}/{m} backwards done)")
         return self._finish(losses, corrects)
 
     SCHEDULES = ("sync", "gpipe", "semi_async", "1f1b")

@@ -28,7 +28,8 @@ def hip():
 # N, C (input channels), H, W, Co — the 16-wide-and-wider ResNet-18/50 layer geometries hconv3 runs
 # (several 16x16 tiles per image, 64-channel tiles, split-K on the small grids)
 CASES = [(4, 64, 32, 32, 64), (2, 64, 32, 64, 64), (4, 128, 16, 16, 128), (2, 64, 16, 16, 64),
-         (4, 64, 16, 16, 128), (2, 256, 16, 16, 256), (64, 64, 32, 32, 64), (4, 512, 16, 16, 128)]
+         (4, 64, 16, 16, 128), (2, 256, 16, 16, 256), (64, 64, 32, 32, 64), (4, 512, 16, 16, 128),
+         (4, 32, 32, 32, 64)]  # 32 input channels: one chunk
 if os.environ.get("DCNN_HCONV3_8") == "1":  # 8x8 maps: 4 images per tile (experiment instance)
     CASES += [(4, 256, 8, 8, 256), (8, 128, 8, 8, 64), (16, 512, 8, 8, 256), (64, 256, 8, 8, 256)]
 
