@@ -101,6 +101,7 @@ static int g_g1s_pf = [] {
   return e ? atoi(e) : 2;
 }();
 static int g1s_occ_rt(int K, int mode) { return (K == 64 && mode != 2 && g_g1s_occ3) ? 3 : 2; }
+// (K = 32: one MFMA k step per subtile; weights 16 VGPRs)
 constexpr int kG1sTile = 32;  // pixels per tile (16 * TJ)
 // weights in LDS (shared by the workgroup's 4 waves) instead of VGPRs: K >= 256, and the K = 128
 // data gradient (its three epilogue operands leave no room for 64 weight VGPRs)
@@ -404,7 +405,7 @@ void g1s_enable(int on) { g_g1s = on; }
 // input channels in `mode`; 0 when the shape does not run on it. The ranges are sized so every
 // resident wave slot holds one wave (two per SIMD when the registers allow, else one).
 int g1s_rows(int M, int N, int K, int mode) {
-  if (!g_g1s || M % 64 || N % 64 || (K != 64 && K != 128 && K != 256 && K != 512)) return 0;
+  if (!g_g1s || M % 64 || N % 64 || (K != 32 && K != 64 && K != 128 && K != 256 && K != 512)) return 0;
   const int tiles = M / kG1sTile, CS = N / 64;
   const long waves = 256l * 4 * g1s_occ_rt(K, mode);
   int pr = (int)((waves + CS - 1) / CS);
@@ -468,6 +469,7 @@ void g1s(const bf16* X, const bf16* Wt, bf16* Y, int M, int N, int K, int H, int
     if (mode == 1) return launch_g1s<K_, 1>(a, s);            \
     return launch_g1s<K_, 2>(a, s);                           \
   }
+  DCNN_G1S(32)
   DCNN_G1S(64)
   DCNN_G1S(128)
   DCNN_G1S(256)

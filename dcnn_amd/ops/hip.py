@@ -1127,6 +1127,24 @@ def _stats(s):
     return s.data_ptr(), 1
 
 
+_TRACE_PARTIAL = os.environ.get("DCNN_TRACE_PARTIAL", "0") == "1"
+_traced_partial = set()
+
+
+def _trace_partial(kind, x):
+    """DCNN_TRACE_PARTIAL=1: report (once per call site and shape) every standalone BatchNorm
+    statistics pass, i.e. a BatchNorm whose producer / consumer kernel could not emit its sums."""
+    if not _TRACE_PARTIAL:
+        return
+    import sys
+    import traceback
+    fr = [f"{os.path.basename(f.filename)}:{f.lineno}:{f.name}" for f in traceback.extract_stack(limit=8)[:-2]]
+    key = (kind, tuple(x.shape), tuple(fr))
+    if key not in _traced_partial:
+        _traced_partial.add(key)
+        print(f"[bn_partial] {kind} {tuple(x.shape)} <- {' <- '.join(reversed(fr))}", file=sys.stderr)
+
+
 def bn_stats_raw(x, partial=None):
     """The (slab, rows, sums) statistics rows of x before the reduce (the producing conv's
     epilogue slab, else a bn_partial pass), or an already reduced :class:`Stats` (folded)."""
@@ -1137,6 +1155,7 @@ def bn_stats_raw(x, partial=None):
     rows = K.bn_partial_rows(R, C)
     slab = _empty((rows, 3, C), F32, x.device)
     sums = _empty((2 * C,), F32, x.device)
+    _trace_partial("fwd", x)
     K.bn_partial(dt_code(x.dtype), x.data_ptr(), 0, 0, 0, 0, 0, R, C, slab.data_ptr(), 0, 0, stream_ptr())
     return slab, rows, sums
 
@@ -1148,6 +1167,7 @@ def bn_bwd_stats_raw(dy, x, mean, istd):
     rows = K.bn_partial_rows(R, C)
     slab = _empty((rows, 2, C), F32, x.device)
     sums = _empty((2 * C,), F32, x.device)
+    _trace_partial("bwd_raw", x)
     K.bn_partial(dt_code(x.dtype), x.data_ptr(), dy.data_ptr(), 0, 0, mean.data_ptr(), istd.data_ptr(), R, C,
                  slab.data_ptr(), 1, 0, stream_ptr())
     return slab, rows, sums
@@ -1199,6 +1219,7 @@ def bn_stats(x, partial=None):
         rows = K.bn_partial_rows(R, C)
         slab = _empty((rows, 3, C), F32, x.device)
         sums = _empty((2 * C,), F32, x.device)
+        _trace_partial("fwd", x)
         K.bn_partial(dt_code(x.dtype), x.data_ptr(), 0, 0, 0, 0, 0, R, C, slab.data_ptr(), 0, 0, st)
     else:
         slab, rows, sums = partial
@@ -1325,6 +1346,7 @@ def bn_backward(dy, x, yout, mean, istd, gamma, dgamma, dbeta, *, want_masked=Fa
         rows = K.bn_partial_rows(R, C)
         slab = _empty((rows, 2, C), F32, x.device)
         sums = _empty((2 * C,), F32, x.device)
+        _trace_partial("bwd", x)
         K.bn_partial(dt, x.data_ptr(), dy.data_ptr(), ptr(yout), ptr(dmask), mean.data_ptr(), istd.data_ptr(), R, C,
                      slab.data_ptr(), 1, 0, st)
         sums = stat_reduce(1, slab, rows, C, sums)

@@ -45,6 +45,7 @@ FWD_CASES = [
     (4, 256, 16, 16, 64, 1),     # layer-1 reduce (K = 256: weights in LDS)
     (2, 512, 8, 8, 128, 1),      # layer-2 reduce (K = 512)
     (4, 256, 16, 16, 128, 2),    # strided projection, K = 256
+    (4, 32, 32, 32, 64, 1),      # K = 32 (ResNet-18 layer-1 projection)
     (4, 256, 4, 4, 64, 1),       # 2 tiles: trailing pixel ranges of a workgroup stay empty
 ]
 
