@@ -569,6 +569,7 @@ __global__ void splitk_reduce_kernel(SplitkSeg a, SplitkSeg b, int gxa, int spli
 // loads of a group in flight, the chunk's waves meet in LDS in wave order and its first wave adds
 // into the gradient. Entries run longest (most groups) first so the many-split slabs' long
 // blocks are not the launch's tail. Fixed summation order throughout: bit-reproducible, no atomics.
+template <int G>
 __global__ void __launch_bounds__(256) multi_splitk_reduce_kernel(MultiRed t) {
   int k = 0;
   while (k + 1 < t.count && (int)blockIdx.x >= t.e[k + 1].unit0) ++k;
@@ -581,25 +582,25 @@ __global__ void __launch_bounds__(256) multi_splitk_reduce_kernel(MultiRed t) {
   __shared__ float4 red[4][64];
   float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
   for (int g = 0; g < groups; ++g) {
-    const int s0 = g * 8 * wpc + wj * 8;
+    const int s0 = g * G * wpc + wj * G;
     if (vec) {  // n % 4 == 0: lane owns 4 consecutive floats
       const long i4 = (long)chunk * 64 + lane;
       const bool ok = i4 * 4 < n;
-      float4 v[8];
+      float4 v[G];
 #pragma unroll
-      for (int u = 0; u < 8; ++u)
+      for (int u = 0; u < G; ++u)
         v[u] = (ok && s0 + u < splits) ? reinterpret_cast<const float4*>(slab + (long)(s0 + u) * n)[i4]
                                        : make_float4(0.f, 0.f, 0.f, 0.f);
 #pragma unroll
-      for (int u = 0; u < 8; ++u) { acc.x += v[u].x; acc.y += v[u].y; acc.z += v[u].z; acc.w += v[u].w; }
+      for (int u = 0; u < G; ++u) { acc.x += v[u].x; acc.y += v[u].y; acc.z += v[u].z; acc.w += v[u].w; }
     } else {  // one float per lane
       const long i = (long)chunk * 64 + lane;
       const bool ok = i < n;
-      float v[8];
+      float v[G];
 #pragma unroll
-      for (int u = 0; u < 8; ++u) v[u] = (ok && s0 + u < splits) ? slab[(long)(s0 + u) * n + i] : 0.f;
+      for (int u = 0; u < G; ++u) v[u] = (ok && s0 + u < splits) ? slab[(long)(s0 + u) * n + i] : 0.f;
 #pragma unroll
-      for (int u = 0; u < 8; ++u) acc.x += v[u];
+      for (int u = 0; u < G; ++u) acc.x += v[u];
     }
   }
   if (wpc > 1) {
@@ -624,6 +625,13 @@ __global__ void __launch_bounds__(256) multi_splitk_reduce_kernel(MultiRed t) {
   }
 }
 
+// slab loads in flight per wave and group (DCNN_RED_G: 8 or 16; the summation order is fixed for
+// a given setting)
+static int g_red_g = [] {
+  const char* e = getenv("DCNN_RED_G");
+  return (e && atoi(e) == 8) ? 8 : 16;
+}();
+
 void multi_splitk_reduce(MultiRed t, hipStream_t s) {
   if (t.count <= 0) return;
   if (t.count > kMaxRed) throw std::runtime_error("multi_splitk_reduce: too many entries");
@@ -631,7 +639,7 @@ void multi_splitk_reduce(MultiRed t, hipStream_t s) {
     RedEnt& e = t.e[k];
     e.vec = (e.n % 4 == 0 && ((uintptr_t)e.slab % 16) == 0 && ((uintptr_t)e.out % 16) == 0) ? 1 : 0;
     e.wpc = e.splits <= 8 ? 1 : (e.splits <= 16 ? 2 : 4);
-    e.groups = (e.splits + 8 * e.wpc - 1) / (8 * e.wpc);
+    e.groups = (e.splits + g_red_g * e.wpc - 1) / (g_red_g * e.wpc);
   }
   // longest blocks first (stable: equal-length entries keep their queue order)
   std::stable_sort(t.e, t.e + t.count, [](const RedEnt& a, const RedEnt& b) { return a.groups > b.groups; });
@@ -644,7 +652,10 @@ void multi_splitk_reduce(MultiRed t, hipStream_t s) {
     const int cpb = 4 / e.wpc;
     units += (e.chunks + cpb - 1) / cpb;
   }
-  hipLaunchKernelGGL(multi_splitk_reduce_kernel, dim3(units), dim3(256), 0, s, t);
+  if (g_red_g == 16)
+    hipLaunchKernelGGL(multi_splitk_reduce_kernel<16>, dim3(units), dim3(256), 0, s, t);
+  else
+    hipLaunchKernelGGL(multi_splitk_reduce_kernel<8>, dim3(units), dim3(256), 0, s, t);
   DCNN_LAUNCH_CHECK();
 }
 
