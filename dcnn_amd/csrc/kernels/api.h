@@ -123,6 +123,10 @@ void g1s_enable(int on);
 void g1s(const bf16* X, const bf16* Wt, bf16* Y, int M, int N, int K, int H, int W, int OH, int OW, int S,
          const float* bias, const bf16* residual, float* stats, int relu, float* zero_ptr, int zero_n, BnbArgs bnb,
          int mode, hipStream_t s);
+int g1s_gen_rows(int M, int N, int Kc, int ntaps, int mode);
+void g1s_gen(const bf16* X, const bf16* Wt, bf16* Y, int NB, int GH, int GW, int N, int Kc, int ldw,
+             const std::vector<std::array<int, 3>>& taps, int H, int W, int OHo, int OWo, int OS, int ORY, int ORX,
+             const bf16* residual, float* stats, float* zero_ptr, int zero_n, BnbArgs bnb, int mode, hipStream_t s);
 int gemm_t2_splits(int M, int N, int P);
 int gemm_nt_stat_rows(int M, int N);
 // generic tensor ops (ops.hip)

@@ -207,6 +207,16 @@ PYBIND11_MODULE(_kernels, m) {
   m.def("gemm_g2_stat_rows", &gemm_g2_stat_rows);
   m.def("g1s_rows", &g1s_rows);
   m.def("g1s_enable", &g1s_enable);
+  m.def("g1s_gen_rows", &g1s_gen_rows);
+  m.def("g1s_gen", [](uintptr_t X, uintptr_t Wt, uintptr_t Y, int NB, int GH, int GW, int N, int Kc, int ldw,
+                      std::vector<std::array<int, 3>> taps, int H, int W, int OHo, int OWo, int OS, int ORY, int ORX,
+                      uintptr_t residual, uintptr_t stats, uintptr_t zero_ptr, int zero_n, std::array<uintptr_t, 4> bnb,
+                      int mode, uintptr_t stream) {
+    g1s_gen(P<const bf16*>(X), P<const bf16*>(Wt), P<bf16*>(Y), NB, GH, GW, N, Kc, ldw, taps, H, W, OHo, OWo, OS, ORY,
+            ORX, P<const bf16*>(residual), P<float*>(stats), P<float*>(zero_ptr), zero_n,
+            BnbArgs{P<const bf16*>(bnb[0]), P<const bf16*>(bnb[1]), P<const float*>(bnb[2]), P<const float*>(bnb[3])},
+            mode, S(stream));
+  });
   m.def("g1s", [](uintptr_t X, uintptr_t Wt, uintptr_t Y, int M, int N, int K, int H, int W, int OH, int OW, int stride,
                   uintptr_t bias, uintptr_t residual, uintptr_t stats, int relu, uintptr_t zero_ptr, int zero_n,
                   std::array<uintptr_t, 4> bnb, int mode, uintptr_t stream) {

@@ -32,7 +32,9 @@
 //
 // Reference parity: the reference runs 1x1 convs through im2col + cuBLAS / cuDNN
 // (src/nn/layers_impl/cuda/conv2d_ops.cu:18-128, cudnn_conv2d_ops.cu:187-244).
+#include <array>
 #include <cstdlib>
+#include <vector>
 
 #include "common.h"
 #include "api.h"
@@ -85,6 +87,14 @@ struct G1sArgs {
   BnbArgs bnb;
   int dbg;  // DCNN_G1S_DBG experiments: 2 = direct 8-byte stores instead of the LDS-staged full
            // lines, 3 = no output stores (timing only)
+  // gathered form (gen = 1): one stride-phase class of a strided data gradient. GEMM row m is
+  // class-grid pixel (img, gy, gx) of GH x GW; K = ntaps x Kc, tap t reads input pixel
+  // (gy + tap_dy[t], gx + tap_dx[t]) of the H x W x Kc input (zero outside) against weight
+  // columns tap_k[t] .. + Kc of rows ldw wide; the result goes to output pixel
+  // (gy * OS + ORY, gx * OS + ORX) of the OHo x OWo output. ntaps = 0: no MFMA work (a phase no
+  // tap reaches: residual / zero through the same epilogue). gen = 0: Kc = ldw = K, one tap.
+  int gen, ntaps, Kc, ldw, GH, GW, OS, ORY, ORX, OHo, OWo;
+  int tap_dy[4], tap_dx[4], tap_k[4];
 };
 
 // per-instance shape: TJ 16-pixel subtiles per tile, OCC waves per SIMD the registers allow
@@ -107,7 +117,7 @@ constexpr int kG1sTile = 32;  // pixels per tile (16 * TJ)
 // data gradient (its three epilogue operands leave no room for 64 weight VGPRs)
 constexpr bool g1s_wl(int K, int mode) { return K >= 256 || (K == 128 && mode == 2); }
 
-template <int K, int MODE, int OCC, int PF, bool EP>
+template <int K, int MODE, int OCC, int PF, bool EP, bool GEN = false>
 __global__ void __launch_bounds__(256, OCC) g1s_kernel(G1sArgs p) {
   constexpr int KK = K / 32, TJ = 2, TP = 16 * TJ;
   // K >= 256: the 64 x K weight slice lives in LDS, shared by the workgroup's 4 waves (same
@@ -132,6 +142,8 @@ __global__ void __launch_bounds__(256, OCC) g1s_kernel(G1sArgs p) {
     for (int i = threadIdx.x; i < p.zero_n; i += 256) p.zero_ptr[i] = 0.f;
   const int CS = p.N >> 6;
   const int blk = xcd_remap_g1(blockIdx.x, gridDim.x);
+  // weight-row column of GEMM channel k (k .. k + 7 stay inside one tap: Kc % 32 == 0)
+  auto wcol = [&](int k) { return p.tap_k[k / p.Kc] + k % p.Kc; };
   int cs, pr;
   if (WL) {  // workgroup = one channel slice x 4 consecutive pixel ranges
     cs = blk % CS;
@@ -142,7 +154,7 @@ __global__ void __launch_bounds__(256, OCC) g1s_kernel(G1sArgs p) {
     for (int q = threadIdx.x; q < 64 * (K / 8); q += 256) {
       const int r = q / (K / 8), c = q % (K / 8);
       *reinterpret_cast<uint4*>(wlds + r * WPITCH + c * 16) =
-          *reinterpret_cast<const uint4*>(p.Wt + (size_t)(cs * 64 + r) * K + c * 8);
+          *reinterpret_cast<const uint4*>(p.Wt + (size_t)(cs * 64 + r) * p.ldw + wcol(c * 8));
     }
     __syncthreads();
   } else {
@@ -167,7 +179,7 @@ __global__ void __launch_bounds__(256, OCC) g1s_kernel(G1sArgs p) {
     for (int i = 0; i < 4; ++i)
 #pragma unroll
       for (int kk = 0; kk < KK; ++kk)
-        wa[i][kk] = *reinterpret_cast<const bf16x8*>(p.Wt + (size_t)(n0 + i * 16 + lr) * K + kk * 32 + lh * 8);
+        wa[i][kk] = *reinterpret_cast<const bf16x8*>(p.Wt + (size_t)(n0 + i * 16 + lr) * p.ldw + wcol(kk * 32 + lh * 8));
   }
   int wl_off = lr * WPITCH + lh * 16;
   auto afrag = [&](int i, int kk) -> bf16x8 {
@@ -178,18 +190,47 @@ __global__ void __launch_bounds__(256, OCC) g1s_kernel(G1sArgs p) {
     }
   };
 
-  const bool plain = p.S == 1 && p.OH == p.H && p.OW == p.W;
-  const int ohw = p.OH * p.OW;
-  auto src_px = [&](int m) -> long {  // input pixel of output pixel m
+  const bool plain = !GEN && p.S == 1 && p.OH == p.H && p.OW == p.W;
+  const int ohw = p.OH * p.OW, ghw = p.GH * p.GW;
+  auto src_px = [&](int m) -> long {  // input pixel of output pixel m (gen = 0)
     if (plain) return m;
     const int img = m / ohw, rem = m - img * ohw;
     const int oy = rem / p.OW, ox = rem - oy * p.OW;
     return ((long)img * p.H + oy * p.S) * p.W + ox * p.S;
   };
+  // gen = 1: element offset of (GEMM row m, channel k) in the input, or -1 outside the image
+  auto src_gen = [&](int m, int k) -> long {
+    const int img = m / ghw, rem = m - img * ghw;
+    const int gy = rem / p.GW, gx = rem - gy * p.GW;
+    const int t = k / p.Kc, c = k - t * p.Kc;
+    const int sy = gy + p.tap_dy[t], sx = gx + p.tap_dx[t];
+    if ((unsigned)sy >= (unsigned)p.H || (unsigned)sx >= (unsigned)p.W) return -1;
+    return (((long)img * p.H + sy) * p.W + sx) * p.Kc + c;
+  };
+  // output pixel row of GEMM row m
+  auto orow = [&](int m) -> long {
+    if (!GEN) return m;
+    const int img = m / ghw, rem = m - img * ghw;
+    const int gy = rem / p.GW, gx = rem - gy * p.GW;
+    return ((long)img * p.OHo + gy * p.OS + p.ORY) * p.OWo + gx * p.OS + p.ORX;
+  };
+  const bf16x8 zero8 = {};
+  auto ldb8 = [&](int m, int k) -> bf16x8 {  // one B fragment, gathered form
+    const long o = src_gen(m, k);
+    return o >= 0 ? *reinterpret_cast<const bf16x8*>(p.X + o) : zero8;
+  };
   // B fragments of PF tiles in flight (ring, statically indexed by the unrolled loop)
   bf16x8 bb[PF][TJ][WL ? 1 : KK];
   auto load_b = [&](bf16x8 (&b)[TJ][WL ? 1 : KK], int t) {
     if constexpr (WL) return;
+    if (GEN) {
+      if (p.ntaps == 0) return;
+#pragma unroll
+      for (int j = 0; j < TJ; ++j)
+#pragma unroll
+        for (int kk = 0; kk < KK; ++kk) b[j][kk] = ldb8(t * TP + j * 16 + lr, kk * 32 + lh * 8);
+      return;
+    }
 #pragma unroll
     for (int j = 0; j < TJ; ++j) {
       const bf16* q = p.X + src_px(t * TP + j * 16 + lr) * K + lh * 8;
@@ -208,7 +249,7 @@ __global__ void __launch_bounds__(256, OCC) g1s_kernel(G1sArgs p) {
   auto load_e = [&](uint2 (&e)[NE][4][TJ], int t) {
 #pragma unroll
     for (int j = 0; j < TJ; ++j) {
-      const size_t row = (size_t)(t * TP + j * 16 + lr) * p.N + n0 + lh * 4;
+      const size_t row = (size_t)orow(t * TP + j * 16 + lr) * p.N + n0 + lh * 4;
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
         e[0][i][j] = has_res ? *reinterpret_cast<const uint2*>(p.residual + row + i * 16) : make_uint2(0u, 0u);
@@ -234,6 +275,14 @@ __global__ void __launch_bounds__(256, OCC) g1s_kernel(G1sArgs p) {
   constexpr int NC = WL ? KK / 4 : 1;
   bf16x8 bq[2][TJ][4];
   auto load_chunk = [&](bf16x8 (&b)[TJ][4], int t, int c) {
+    if (GEN) {
+      if (p.ntaps == 0) return;
+#pragma unroll
+      for (int j = 0; j < TJ; ++j)
+#pragma unroll
+        for (int u = 0; u < 4; ++u) b[j][u] = ldb8(t * TP + j * 16 + lr, c * 128 + u * 32 + lh * 8);
+      return;
+    }
 #pragma unroll
     for (int j = 0; j < TJ; ++j) {
       const bf16* q = p.X + src_px(t * TP + j * 16 + lr) * K + c * 128 + lh * 8;
@@ -247,7 +296,9 @@ __global__ void __launch_bounds__(256, OCC) g1s_kernel(G1sArgs p) {
     for (int i = 0; i < 4; ++i)
 #pragma unroll
       for (int j = 0; j < TJ; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-    if constexpr (WL) {
+    if (GEN && p.ntaps == 0) {
+      // a stride phase no tap reaches: the epilogue alone (residual or zero)
+    } else if constexpr (WL) {
       // the weight slice never changes after the barrier: keep the compiler from hoisting all
       // 4 x K / 32 fragment reads out of the tile loop (K / 2 VGPRs of live fragments)
       asm volatile("" : "+v"(wl_off));
@@ -317,7 +368,7 @@ __global__ void __launch_bounds__(256, OCC) g1s_kernel(G1sArgs p) {
         }
         const uint2 o = make_uint2(f2_to_bf2(f[0], f[1]), f2_to_bf2(f[2], f[3]));
         if (!STG || (p.dbg & 2)) {  // direct 8-byte stores (16 pixel rows x 32 B per instruction)
-          if (!(p.dbg & 1)) *reinterpret_cast<uint2*>(p.Y + (size_t)(t * TP + j * 16 + lr) * p.N + n0 + lh * 4 + i * 16) = o;
+          if (!(p.dbg & 1)) *reinterpret_cast<uint2*>(p.Y + (size_t)orow(t * TP + j * 16 + lr) * p.N + n0 + lh * 4 + i * 16) = o;
         } else {
           // full-line stores: the tile's 32 pixel rows (128 B each, 16-byte chunks XOR-swizzled by
           // the pixel) are staged in this wave's LDS slice and read back as 8 lanes per pixel row
@@ -345,7 +396,7 @@ __global__ void __launch_bounds__(256, OCC) g1s_kernel(G1sArgs p) {
       for (int k = 0; k < TP / 8; ++k) {
         const int P = k * 8 + (lane >> 3), c = lane & 7;
         const uint4 v = *reinterpret_cast<const uint4*>(stg + P * 128 + ((c ^ (P & 7)) << 4));
-        *reinterpret_cast<uint4*>(p.Y + (size_t)(t * TP + P) * p.N + n0 + c * 8) = v;
+        *reinterpret_cast<uint4*>(p.Y + (size_t)orow(t * TP + P) * p.N + n0 + c * 8) = v;
       }
     }
   };
@@ -426,6 +477,12 @@ static int g1s_tpr(int M, int N, int K, int mode) {
 template <int K, int MODE, int OCC = 2>
 static void launch_g1s(const G1sArgs& a, hipStream_t s) {
   const int waves = a.PR * (a.N / 64);
+  if (a.gen) {  // gathered stride-phase form: single B buffer (its addressing needs the registers)
+    if constexpr (MODE != 1)
+      hipLaunchKernelGGL((g1s_kernel<K, MODE, OCC, 1, false, true>), dim3((waves + 3) / 4), dim3(256), 0, s, a);
+    DCNN_LAUNCH_CHECK();
+    return;
+  }
   // B fragments two tiles deep; epilogue operands (residual / BatchNorm y, x) one tile ahead only
   // with DCNN_G1S_PF=3 (more registers: spills on the wider instances)
   // (K >= 128: one B buffer, reloaded after the MFMAs — the two-deep ring spills there)
@@ -440,26 +497,17 @@ static void launch_g1s(const G1sArgs& a, hipStream_t s) {
 
 // mode: 0 plain, 1 forward + Welford statistics ([rows][3][N]), 2 data gradient + bnb sums
 // ([rows][2][N]); rows must be g1s_rows(M, N, K)
-void g1s(const bf16* X, const bf16* Wt, bf16* Y, int M, int N, int K, int H, int W, int OH, int OW, int S,
-         const float* bias, const bf16* residual, float* stats, int relu, float* zero_ptr, int zero_n, BnbArgs bnb,
-         int mode, hipStream_t s) {
-  const int rows = g1s_rows(M, N, K, mode);
+static void g1s_launch(G1sArgs& a, int mode, hipStream_t s) {
+  const int K = a.K;
+  const int rows = g1s_rows(a.M, a.N, K, mode);
   if (!rows) throw std::runtime_error("g1s: unsupported shape");
-  if (mode < 0 || mode > 2 || (mode != 0 && !stats)) throw std::runtime_error("g1s: bad mode / statistics slab");
-  if (mode == 2 && (!bnb.x || !bnb.mean || !bnb.istd || S != 1)) throw std::runtime_error("g1s: bnb operands missing");
-  if (mode == 1 && residual) throw std::runtime_error("g1s: no residual with forward statistics");
-  if (mode != 0 && relu) throw std::runtime_error("g1s: ReLU only without statistics");
-  if ((long)M != (long)(M / (OH * OW)) * OH * OW || OH != (H - 1) / S + 1 || OW != (W - 1) / S + 1)
-    throw std::runtime_error("g1s: inconsistent geometry");
-  G1sArgs a{};
-  a.X = X; a.Wt = Wt; a.Y = Y;
-  a.M = M; a.N = N; a.K = K; a.H = H; a.W = W; a.OH = OH; a.OW = OW; a.S = S;
-  a.tiles = M / kG1sTile;
-  a.tpr = g1s_tpr(M, N, K, mode);
+  if (mode < 0 || mode > 2 || (mode != 0 && !a.stats)) throw std::runtime_error("g1s: bad mode / statistics slab");
+  if (mode == 2 && (!a.bnb.x || !a.bnb.mean || !a.bnb.istd)) throw std::runtime_error("g1s: bnb operands missing");
+  if (mode == 1 && a.residual) throw std::runtime_error("g1s: no residual with forward statistics");
+  if (mode != 0 && a.relu) throw std::runtime_error("g1s: ReLU only without statistics");
+  a.tiles = a.M / kG1sTile;
+  a.tpr = g1s_tpr(a.M, a.N, K, mode);
   a.PR = rows;
-  a.bias = bias; a.residual = residual; a.stats = stats; a.relu = relu;
-  a.zero_ptr = zero_ptr; a.zero_n = zero_n;
-  a.bnb = bnb;
   static const int dbg = [] { const char* e = getenv("DCNN_G1S_DBG"); return e ? atoi(e) : 0; }();
   a.dbg = dbg;
 #define DCNN_G1S(K_)                                          \
@@ -476,6 +524,48 @@ void g1s(const bf16* X, const bf16* Wt, bf16* Y, int M, int N, int K, int H, int
   DCNN_G1S(512)
 #undef DCNN_G1S
   throw std::runtime_error("g1s: no kernel instance");
+}
+
+void g1s(const bf16* X, const bf16* Wt, bf16* Y, int M, int N, int K, int H, int W, int OH, int OW, int S,
+         const float* bias, const bf16* residual, float* stats, int relu, float* zero_ptr, int zero_n, BnbArgs bnb,
+         int mode, hipStream_t s) {
+  if (mode == 2 && S != 1) throw std::runtime_error("g1s: bnb fusion needs stride 1 (use g1s_gen)");
+  if ((long)M != (long)(M / (OH * OW)) * OH * OW || OH != (H - 1) / S + 1 || OW != (W - 1) / S + 1)
+    throw std::runtime_error("g1s: inconsistent geometry");
+  G1sArgs a{};
+  a.X = X; a.Wt = Wt; a.Y = Y;
+  a.M = M; a.N = N; a.K = K; a.H = H; a.W = W; a.OH = OH; a.OW = OW; a.S = S;
+  a.bias = bias; a.residual = residual; a.stats = stats; a.relu = relu;
+  a.zero_ptr = zero_ptr; a.zero_n = zero_n;
+  a.bnb = bnb;
+  a.gen = 0; a.ntaps = 1; a.Kc = K; a.ldw = K; a.GH = OH; a.GW = OW;
+  g1s_launch(a, mode, s);
+}
+
+// gathered form: one stride-phase class of a strided data gradient (see G1sArgs)
+int g1s_gen_rows(int M, int N, int Kc, int ntaps, int mode) {
+  if (Kc % 32 || ntaps < 0 || ntaps > 4) return 0;
+  return g1s_rows(M, N, ntaps == 0 ? 32 : ntaps * Kc, mode);
+}
+
+void g1s_gen(const bf16* X, const bf16* Wt, bf16* Y, int NB, int GH, int GW, int N, int Kc, int ldw,
+             const std::vector<std::array<int, 3>>& taps, int H, int W, int OHo, int OWo, int OS, int ORY, int ORX,
+             const bf16* residual, float* stats, float* zero_ptr, int zero_n, BnbArgs bnb, int mode, hipStream_t s) {
+  const int nt = (int)taps.size();
+  if (nt > 4 || Kc % 32) throw std::runtime_error("g1s_gen: at most 4 taps of 32-multiple channels");
+  if (mode == 1) throw std::runtime_error("g1s_gen: data-gradient modes only (0 / 2)");
+  for (int t = 0; t < nt; ++t)
+    if (taps[t][2] < 0 || taps[t][2] + Kc > ldw) throw std::runtime_error("g1s_gen: tap weight columns out of the row");
+  G1sArgs a{};
+  a.X = X; a.Wt = Wt; a.Y = Y;
+  a.M = NB * GH * GW; a.N = N; a.K = nt == 0 ? 32 : nt * Kc;
+  a.H = H; a.W = W; a.OH = GH; a.OW = GW; a.S = 1;
+  a.residual = residual; a.stats = stats; a.zero_ptr = zero_ptr; a.zero_n = zero_n; a.bnb = bnb;
+  a.gen = 1; a.ntaps = nt; a.Kc = nt == 0 ? 32 : Kc; a.ldw = ldw;
+  a.GH = GH; a.GW = GW; a.OS = OS; a.ORY = ORY; a.ORX = ORX; a.OHo = OHo; a.OWo = OWo;
+  for (int t = 0; t < nt; ++t) { a.tap_dy[t] = taps[t][0]; a.tap_dx[t] = taps[t][1]; a.tap_k[t] = taps[t][2]; }
+  if (nt == 0) a.ldw = 32;  // (no weight reads happen; keeps wcol in range)
+  g1s_launch(a, mode, s);
 }
 
 }  // namespace dcnn

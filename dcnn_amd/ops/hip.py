@@ -589,6 +589,60 @@ def _dgrad_classes(H, W, OW, Co, KH, KW, sh, sw, ph, pw):
     return tuple(classes), tuple(empty)
 
 
+_G1S_STRIDED = os.environ.get("DCNN_G1S_STRIDED", "1") != "0"
+
+
+def set_g1s_strided(on: bool) -> None:
+    """Strided data gradients on the streaming kernel's gathered form (default) or the grouped
+    gathered GEMM (gemm2.hip)."""
+    global _G1S_STRIDED
+    _G1S_STRIDED = bool(on)
+
+
+def _g1s_strided_dgrad(K, dy, wt, x_shape, allc, s, residual, bnb):
+    """Strided data gradient as one streaming launch per stride-phase class (g1s.hip gathered form):
+    class (ry, rx) is a GEMM over its taps' 64..512-deep K, written straight to its output phase;
+    phases no tap reaches run the same epilogue with no MFMA work (residual or zeros, and their
+    share of the fused BatchNorm statistics). None when a class does not fit the kernel."""
+    N, Ci, H, W = x_shape
+    Co, OH, OW = dy.shape[1], dy.shape[2], dy.shape[3]
+    fuse = (bnb is not None and _BNB and not bnb.pooled and bnb.x.dtype == BF16
+            and tuple(bnb.x.shape) == (N, Ci, H, W))
+    mode = 2 if fuse else 0
+    rows, use = [], []
+    for ry, rx, GH, GW, taps in allc:
+        r = K.g1s_gen_rows(N * GH * GW, Ci, Co, len(taps), mode)
+        use.append(r > 0)
+        if r <= 0:  # (a class deeper than 512: the gathered GEMM takes it, in the same slab)
+            if not taps or (N * GH * GW) % 64:
+                return None
+            r = K.gemm_g2_stat_rows(N * GH * GW, Ci) if fuse else 0
+        rows.append(r)
+    if not any(use):
+        return None
+    dx = _empty((N, Ci, H, W), BF16, dy.device, True)
+    slab = _empty((sum(rows), 2, Ci), F32, dy.device) if fuse else None
+    sums = _empty((2 * Ci,), F32, dy.device) if fuse else None
+    ldw = wt.shape[1] * wt.shape[2] * Co
+    st = stream_ptr()
+    r0 = 0
+    for k, (ry, rx, GH, GW, taps) in enumerate(allc):
+        sp = slab.data_ptr() + r0 * 2 * Ci * 4 if fuse else 0
+        zp = ptr(sums) if (fuse and k == 0) else 0
+        if use[k]:
+            K.g1s_gen(dy.data_ptr(), wt.data_ptr(), dx.data_ptr(), N, GH, GW, Ci, Co, ldw,
+                      [(t[0], t[1], t[3]) for t in taps], OH, OW, H, W, s, ry, rx, ptr(residual), sp, zp,
+                      2 * Ci if zp else 0, bnb.args() if fuse else _NOBNB, mode, st)
+        else:
+            K.gemm_g2(dy.data_ptr(), wt.data_ptr(), dx.data_ptr(), _nbytes(dy), _nbytes(wt), N * GH * GW, Ci, Co,
+                      OH, OW, GH, GW, 1, 1, taps, ldw, Ci, H, W, s, s, ry, rx, 0, ptr(residual), sp, 0, zp,
+                      2 * Ci if zp else 0, bnb.args() if fuse else _NOBNB, st)
+        r0 += rows[k]
+    if fuse:
+        dx._bnb = (bnb.bn, slab, sum(rows), sums)
+    return dx
+
+
 def conv2d_dgrad(dy, wt, x_shape, stride, pad, *, residual=None, bnb=None):
     """dx = conv_transpose(dy, w) [+ residual];  wt = conv_weight_t(w).
 
@@ -622,6 +676,10 @@ def conv2d_dgrad(dy, wt, x_shape, stride, pad, *, residual=None, bnb=None):
     empty_class = bool(empty)
     odt = F32 if f32 else BF16
     allc = classes + empty
+    if not f32 and _G1S_STRIDED and sh == sw and sh > 1:
+        dx = _g1s_strided_dgrad(K, dy, wt, (N, Ci, H, W), allc, sh, residual, bnb)
+        if dx is not None:
+            return dx
     if (not f32 and empty_class and len(classes) > 1 and _G2_GROUP and len(allc) <= 4
             and len({(c[2], c[3]) for c in allc}) == 1 and (N * allc[0][2] * allc[0][3]) % 128 == 0):
         # phases no tap reaches join the grouped launch as zero-tap classes: their epilogue writes
