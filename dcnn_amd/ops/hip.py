@@ -589,14 +589,20 @@ def _dgrad_classes(H, W, OW, Co, KH, KW, sh, sw, ph, pw):
     return tuple(classes), tuple(empty)
 
 
-_G1S_STRIDED = os.environ.get("DCNN_G1S_STRIDED", "1") != "0"
+# opt-in (DCNN_G1S_STRIDED=1): per-class launches measured slower end to end (profiles/g1s_r3.md:
+# ResNet-18 l2.b1c1 dgrad 66.8 -> 52.9 us alone, but the whole step 78.8k -> 77.6k img/s with the
+# fused statistics and residual of the model; l3 / l4 classes and the 1-tap + 3-empty-phase
+# projections were slower than the one grouped launch even alone)
+_G1S_STRIDED = os.environ.get("DCNN_G1S_STRIDED", "0") == "1"
+_G1S_STRIDED_MIN_ROWS = int(os.environ.get("DCNN_G1S_STRIDED_MIN_ROWS", "32768"))
 
 
-def set_g1s_strided(on: bool) -> None:
-    """Strided data gradients on the streaming kernel's gathered form (default) or the grouped
-    gathered GEMM (gemm2.hip)."""
-    global _G1S_STRIDED
+def set_g1s_strided(on: bool, min_rows: int = 32768) -> None:
+    """Strided data gradients on the streaming kernel's gathered form (for classes of at least
+    ``min_rows`` GEMM rows and no empty phases) or the grouped gathered GEMM (gemm2.hip)."""
+    global _G1S_STRIDED, _G1S_STRIDED_MIN_ROWS
     _G1S_STRIDED = bool(on)
+    _G1S_STRIDED_MIN_ROWS = int(min_rows)
 
 
 def _g1s_strided_dgrad(K, dy, wt, x_shape, allc, s, residual, bnb):
@@ -606,6 +612,9 @@ def _g1s_strided_dgrad(K, dy, wt, x_shape, allc, s, residual, bnb):
     share of the fused BatchNorm statistics). None when a class does not fit the kernel."""
     N, Ci, H, W = x_shape
     Co, OH, OW = dy.shape[1], dy.shape[2], dy.shape[3]
+    if _G1S_STRIDED_MIN_ROWS > 0 and any(not taps or N * GH * GW < _G1S_STRIDED_MIN_ROWS
+                                         for _, _, GH, GW, taps in allc):
+        return None
     fuse = (bnb is not None and _BNB and not bnb.pooled and bnb.x.dtype == BF16
             and tuple(bnb.x.shape) == (N, Ci, H, W))
     mode = 2 if fuse else 0

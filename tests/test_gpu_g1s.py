@@ -198,22 +198,30 @@ def test_g1s_strided_dgrad(hip, case):
     r = torch.randn(N, C, H, W).cuda().bfloat16().contiguous(memory_format=CL) if resid else None
     out = {}
     for on in (True, False):
-        hip.set_g1s_strided(on)
+        hip.set_g1s_strided(on, min_rows=0)  # (the default gate keeps small phase grids grouped)
         try:
             d = hip.conv2d_dgrad(dy, wt, (N, C, H, W), (s, s), (p, p), residual=r)
             req = hip.BnbRequest("bn", yout, xb, mean, istd)
             df = hip.conv2d_dgrad(dy, wt, (N, C, H, W), (s, s), (p, p), residual=r, bnb=req)
             dg, db = torch.zeros(C, device="cuda"), torch.zeros(C, device="cuda")
-            dx, _ = hip.bn_backward(df, xb, yout, mean, istd, g, dg, db, want_masked=True, fused=df._bnb[1:])
-            out[on] = (d.clone(), df.clone(), dx.clone(), dg.clone(), db.clone())
+            fz = getattr(df, "_bnb", None)  # (the grouped path does not fuse a 1x1 stride-2 dgrad)
+            assert fz is not None or not on
+            dx, _ = hip.bn_backward(df, xb, yout, mean, istd, g, dg, db, want_masked=True,
+                                    fused=fz[1:] if fz is not None else None)
+            dfm = df.float() * (y.float() > 0) if relu else df.float()
+            out[on] = (d.clone(), dfm, dx.clone(), dg.clone(), db.clone())
         finally:
             hip.set_g1s_strided(True)
     ref = torch.nn.grad.conv2d_input((N, C, H, W), w.float(), dy.float(), s, p)
     if resid:
         ref = ref + r.float()
     assert rel_err(out[True][0], ref) < 1e-2, rel_err(out[True][0], ref)
-    # same products in the same order within a class: identical data gradients
-    assert torch.equal(out[True][0], out[False][0])
-    assert torch.equal(out[True][1], out[False][1])
+    # same products in the same order within a class: identical data gradients; with a residual
+    # the gathered GEMM rounds the product to bf16 before adding it (two roundings, g1s one)
+    for a, b in zip(out[True][:2], out[False][:2]):
+        if resid:
+            assert rel_err(a, b) < 5e-3, rel_err(a, b)
+        else:
+            assert torch.equal(a, b)
     for a, b in zip(out[True][2:], out[False][2:]):
-        assert rel_err(a, b) < 1e-4, rel_err(a, b)
+        assert rel_err(a, b) < (1e-2 if resid else 1e-4), rel_err(a, b)
