@@ -17,6 +17,8 @@
 // Workgroups of one split (same pixel tiles) are adjacent in the XCD-remapped order, so the
 // dY/X tiles they share stay in one XCD's L2. Split-K partials go to an fp32 slab
 // [split][Co][9*Cs] (same layout as gemm_t2) reduced by splitk_reduce.
+#include <type_traits>
+
 #include "common.h"
 #include "api.h"
 
@@ -287,14 +289,21 @@ __device__ __forceinline__ bf16x4 tr4_at(const char* addr) {
   return __builtin_amdgcn_ds_read_tr16_b64_v4bf16((__attribute__((address_space(3))) bf16x4*)(const_cast<char*>(addr)));
 }
 
-template <int TW, int TH, int IMG, int NS>
-__global__ void __launch_bounds__(256, 1) hwgrad2_kernel(HWArgs p) {
+// TSP = 2: 8 waves, two per SIMD — wave w + 4 shares wave w's 16 input channels and takes taps
+// 5..8 while wave w takes 0..4 (20 / 16 accumulator tiles instead of 36), so a SIMD always has a
+// second wave to issue while one waits on LDS or the tile barrier (the 4-wave kernel runs one
+// wave per SIMD: every wait is exposed). TSP = 3: 12 waves, taps in thirds. The first four waves
+// issue the tile loads. Measured (batch 256): TSP 2 wgrad l1..l4 42.5/35.3/37.4/40.0 ->
+// 40.8/33.7/35.5/38.1 us, whole step 78.3k -> 80.0k img/s.
+template <int TW, int TH, int IMG, int NS, int TSP = 1>
+__global__ void __launch_bounds__(256 * TSP, 1) hwgrad2_kernel(HWArgs p) {
   using G = HWGeo2<TW, TH, IMG>;
   constexpr int HNI = G::HNI, HW2P = G::HW2P, HPIP = G::HPIP, HPP = G::HPP, TPX = G::TPX, STAGE = G::STAGE;
   constexpr int INS = 4 + HNI;
   static_assert(NS == 2 || NS == 3, "2 or 3 stages");
   extern __shared__ __attribute__((aligned(16))) char smem[];
-  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int tid = threadIdx.x, lane = tid & 63, wid = (tid >> 6) & 3, th = tid >> 8;
+  constexpr int NT = 256 * TSP;
   const int co_tiles = p.Co / 64, ci_chunks = p.Cs / 64;
   const int per_split = co_tiles * ci_chunks;
   const int lt = xcd_remap_w(blockIdx.x, gridDim.x);
@@ -333,6 +342,7 @@ __global__ void __launch_bounds__(256, 1) hwgrad2_kernel(HWArgs p) {
     h_rel[j] = ((im * p.H + hy) * p.W + hx) * p.ldx * 2 + (xoff + c0 + ((slot ^ wswz2(row)) * 8)) * 2;
   }
   auto load_tile = [&](int buf, int tile) {
+    if (TSP > 1 && th != 0) return;
     char* Ys = smem + buf * STAGE;
     char* Hs = Ys + PT * 128;
     const int ig = tile / tpi, tr = tile - ig * tpi;
@@ -376,106 +386,123 @@ __global__ void __launch_bounds__(256, 1) hwgrad2_kernel(HWArgs p) {
     }
   }
 
-  f32x4 acc[4][9];
-#pragma unroll
-  for (int i = 0; i < 4; ++i)
-#pragma unroll
-    for (int t = 0; t < 9; ++t) acc[i][t] = f32x4{0.f, 0.f, 0.f, 0.f};
+  // the tile loop and epilogue for taps TB .. TB + NTW - 1 (compile-time: register arrays indexed
+  // by tap stay static)
+  auto run = [&](auto tb_c, auto ntw_c) {
+    constexpr int TB = decltype(tb_c)::value, NTW = decltype(ntw_c)::value;
+    f32x4 acc[4][NTW];
+  #pragma unroll
+    for (int i = 0; i < 4; ++i)
+  #pragma unroll
+      for (int t = 0; t < NTW; ++t) acc[i][t] = f32x4{0.f, 0.f, 0.f, 0.f};
 
-  const bool do_bias = p.bias_slab != nullptr && c0 == 0;
-  float bias_acc = 0.f;
-  const int nt = tend - tbeg;
-  if (nt > 0) load_tile(0, tbeg);
-  if (NS == 3 && nt > 1) load_tile(1, tbeg + 1);
-  if (NS == 3 && nt > 1)
-    asm volatile("s_waitcnt vmcnt(%0)" ::"n"(INS) : "memory");
-  else
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __syncthreads();
-  int cur = 0;
-  for (int it = 0; it < nt; ++it) {
-    if (it + NS - 1 < nt) load_tile(cur == 0 ? NS - 1 : cur - 1, tbeg + it + NS - 1);
-    const char* S0 = smem + cur * STAGE;
-    // A double-buffered; each tap's B fragment re-read in place right after the step's 4 MFMAs
-    // that consume it (9 live B fragments instead of 18: the multi-image geometries otherwise
-    // spill through AGPRs)
-    bf16x8 a[2][4], b[9];
-    auto read_a = [&](int kk, bf16x8* av) {
-#pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        const char* q = S0 + abase[i] + kk * 4096;
-        const bf16x4 lo = tr4_at(q), hi = tr4_at(q + 2048);
-        av[i] = bf16x8{lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
-      }
-    };
-    auto read_b = [&](int kk, int t) {
-      const int dy = t / 3, dx = t % 3;
-      const bf16x4 lo = tr4_at(S0 + bbase[kk * 2][dx] + dy * HW2P * 128);
-      const bf16x4 hi = tr4_at(S0 + bbase[kk * 2 + 1][dx] + dy * HW2P * 128);
-      return bf16x8{lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
-    };
-    read_a(0, a[0]);
-#pragma unroll
-    for (int t = 0; t < 9; ++t) b[t] = read_b(0, t);
-#pragma unroll
-    for (int kk = 0; kk < 4; ++kk) {
-      const int c = kk & 1;
-      __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0)
-      if (kk + 1 < 4) read_a(kk + 1, a[c ^ 1]);
-#pragma unroll
-      for (int t = 0; t < 9; ++t) {
-#pragma unroll
-        for (int i = 0; i < 4; ++i) acc[i][t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[c][i], b[t], acc[i][t], 0, 0, 0);
-        if (kk + 1 < 4) b[t] = read_b(kk + 1, t);
-      }
-    }
-    if (do_bias) {
-      const int col = tid & 63, chn = col >> 3, w = (col & 7) * 2;
-      for (int r = tid >> 6; r < PT; r += 4)
-        bias_acc += (float)*reinterpret_cast<const bf16*>(S0 + r * 128 + ((chn ^ wswz2(r)) << 4) + w);
-    }
-    if (NS == 3 && it + 2 < nt)
-      asm volatile("s_waitcnt vmcnt(%0)\n\ts_waitcnt lgkmcnt(0)\n\ts_barrier" ::"n"(INS) : "memory");
+    const bool do_bias = p.bias_slab != nullptr && c0 == 0 && th == 0;
+    float bias_acc = 0.f;
+    const int nt = tend - tbeg;
+    if (nt > 0) load_tile(0, tbeg);
+    if (NS == 3 && nt > 1) load_tile(1, tbeg + 1);
+    if (NS == 3 && nt > 1)
+      asm volatile("s_waitcnt vmcnt(%0)" ::"n"(INS) : "memory");
     else
-      asm volatile("s_waitcnt vmcnt(0)\n\ts_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
-    cur = cur == NS - 1 ? 0 : cur + 1;
-  }
-
-  // ---- slab[split][co][t*Cs + ci] (as hwgrad_kernel) ----
-  const long Ng = 9l * p.Cs;
-  const long slab_idx = (long)pair * nsplits + split;
-  float* out = p.slab + slab_idx * p.Co * Ng;
-  float* stg = reinterpret_cast<float*>(smem);
-  constexpr int ET = G::EPI_TAPS;
-#pragma unroll
-  for (int t0 = 0; t0 < 9; t0 += ET) {
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
-#pragma unroll
-    for (int u = 0; u < ET; ++u) {
-      if (t0 + u < 9) {
-#pragma unroll
-        for (int i = 0; i < 4; ++i)
-#pragma unroll
-          for (int r = 0; r < 4; ++r)
-            stg[(u * 64 + i * 16 + (lane >> 4) * 4 + r) * 68 + wid * 16 + (lane & 15)] = acc[i][t0 + u][r];
+    int cur = 0;
+    for (int it = 0; it < nt; ++it) {
+      if (it + NS - 1 < nt) load_tile(cur == 0 ? NS - 1 : cur - 1, tbeg + it + NS - 1);
+      const char* S0 = smem + cur * STAGE;
+      // A double-buffered; each tap's B fragment re-read in place right after the step's 4 MFMAs
+      // that consume it (9 live B fragments instead of 18: the multi-image geometries otherwise
+      // spill through AGPRs)
+      bf16x8 a[2][4], b[NTW];
+      auto read_a = [&](int kk, bf16x8* av) {
+  #pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          const char* q = S0 + abase[i] + kk * 4096;
+          const bf16x4 lo = tr4_at(q), hi = tr4_at(q + 2048);
+          av[i] = bf16x8{lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+        }
+      };
+      auto read_b = [&](int kk, int t) {
+        const int dy = t / 3, dx = t % 3;
+        const bf16x4 lo = tr4_at(S0 + bbase[kk * 2][dx] + dy * HW2P * 128);
+        const bf16x4 hi = tr4_at(S0 + bbase[kk * 2 + 1][dx] + dy * HW2P * 128);
+        return bf16x8{lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+      };
+      read_a(0, a[0]);
+  #pragma unroll
+      for (int t = 0; t < NTW; ++t) b[t] = read_b(0, TB + t);
+  #pragma unroll
+      for (int kk = 0; kk < 4; ++kk) {
+        const int c = kk & 1;
+        __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0)
+        if (kk + 1 < 4) read_a(kk + 1, a[c ^ 1]);
+  #pragma unroll
+        for (int t = 0; t < NTW; ++t) {
+  #pragma unroll
+          for (int i = 0; i < 4; ++i) acc[i][t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[c][i], b[t], acc[i][t], 0, 0, 0);
+          if (kk + 1 < 4) b[t] = read_b(kk + 1, TB + t);
+        }
+      }
+      if (do_bias) {
+        const int col = tid & 63, chn = col >> 3, w = (col & 7) * 2;
+        for (int r = wid; r < PT; r += 4)
+          bias_acc += (float)*reinterpret_cast<const bf16*>(S0 + r * 128 + ((chn ^ wswz2(r)) << 4) + w);
+      }
+      if (NS == 3 && it + 2 < nt)
+        asm volatile("s_waitcnt vmcnt(%0)\n\ts_waitcnt lgkmcnt(0)\n\ts_barrier" ::"n"(INS) : "memory");
+      else
+        asm volatile("s_waitcnt vmcnt(0)\n\ts_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+      cur = cur == NS - 1 ? 0 : cur + 1;
+    }
+
+    // ---- slab[split][co][t*Cs + ci] (as hwgrad_kernel) ----
+    const long Ng = 9l * p.Cs;
+    const long slab_idx = (long)pair * nsplits + split;
+    float* out = p.slab + slab_idx * p.Co * Ng;
+    float* stg = reinterpret_cast<float*>(smem);
+    constexpr int ET = G::EPI_TAPS;
+  #pragma unroll
+    for (int t0 = 0; t0 < 9; t0 += ET) {
+      __syncthreads();
+  #pragma unroll
+      for (int u = 0; u < ET; ++u) {
+        const int tl = t0 + u - TB;  // this wave's accumulator slot of tap t0 + u
+        if (t0 + u < 9 && tl >= 0 && tl < NTW) {
+  #pragma unroll
+          for (int i = 0; i < 4; ++i)
+  #pragma unroll
+            for (int r = 0; r < 4; ++r)
+              stg[(u * 64 + i * 16 + (lane >> 4) * 4 + r) * 68 + wid * 16 + (lane & 15)] = acc[i][tl][r];
+        }
+      }
+      __syncthreads();
+      const int nrows = (9 - t0 < ET ? 9 - t0 : ET) * 64;
+      for (int q = tid; q < nrows * 16; q += NT) {
+        const int row = q >> 4, c4 = (q & 15) * 4;
+        const int u = row >> 6, co = co0 + (row & 63);
+        const float4 v = *reinterpret_cast<const float4*>(stg + row * 68 + c4);
+        *reinterpret_cast<float4*>(out + (long)co * Ng + (t0 + u) * p.Cs + c0 + c4) = v;
       }
     }
-    __syncthreads();
-    const int nrows = (9 - t0 < ET ? 9 - t0 : ET) * 64;
-    for (int q = tid; q < nrows * 16; q += 256) {
-      const int row = q >> 4, c4 = (q & 15) * 4;
-      const int u = row >> 6, co = co0 + (row & 63);
-      const float4 v = *reinterpret_cast<const float4*>(stg + row * 68 + c4);
-      *reinterpret_cast<float4*>(out + (long)co * Ng + (t0 + u) * p.Cs + c0 + c4) = v;
+    if (p.bias_slab != nullptr && c0 == 0) {  // (every wave passes the same barriers)
+      __syncthreads();
+      if (tid < 256) stg[tid] = bias_acc;
+      __syncthreads();
+      if (tid < 64)
+        p.bias_slab[slab_idx * p.Co + co0 + tid] =
+            p.pair_bias[pair] ? stg[tid] + stg[tid + 64] + stg[tid + 128] + stg[tid + 192] : 0.f;
     }
-  }
-  if (do_bias) {
-    __syncthreads();
-    stg[tid] = bias_acc;
-    __syncthreads();
-    if (tid < 64)
-      p.bias_slab[slab_idx * p.Co + co0 + tid] =
-          p.pair_bias[pair] ? stg[tid] + stg[tid + 64] + stg[tid + 128] + stg[tid + 192] : 0.f;
+
+  };
+  if constexpr (TSP == 1) {
+    run(std::integral_constant<int, 0>{}, std::integral_constant<int, 9>{});
+  } else if constexpr (TSP == 2) {
+    if (th == 0) run(std::integral_constant<int, 0>{}, std::integral_constant<int, 5>{});
+    else run(std::integral_constant<int, 5>{}, std::integral_constant<int, 4>{});
+  } else {
+    if (th == 0) run(std::integral_constant<int, 0>{}, std::integral_constant<int, 3>{});
+    else if (th == 1) run(std::integral_constant<int, 3>{}, std::integral_constant<int, 3>{});
+    else run(std::integral_constant<int, 6>{}, std::integral_constant<int, 3>{});
   }
 }
 
@@ -532,6 +559,14 @@ static int g_hwgrad4 = [] {
   return e ? atoi(e) : 1;
 }();
 
+// tap-split variants of hwgrad2: 2 (default) = 8 waves, two per SIMD (taps 0-4 / 5-8); 3 = 12 waves
+// (taps in thirds); 1 = the 4-wave kernel (DCNN_HWGRAD_TS)
+static int g_hw_ts = [] {
+  const char* e = getenv("DCNN_HWGRAD_TS");
+  const int v = e ? atoi(e) : 2;
+  return v == 1 || v == 3 ? v : 2;
+}();
+
 void hwgrad(HWArgs a, int splits, hipStream_t s) {
   if (!hwgrad_supported(a.NB, a.H, a.W, a.Cs, a.Co, a.ntaps)) throw std::runtime_error("hwgrad: unsupported shape");
   for (int t = 0; t < a.ntaps; ++t)
@@ -567,20 +602,22 @@ void hwgrad(HWArgs a, int splits, hipStream_t s) {
   if (ver == 2 && std_taps && !a.dbg) {
 #define DCNN_HW2(TW_, TH_, IMG_, NS_)                                                                   \
     if (a.TW == TW_ && a.TH == TH_ && a.IMG == IMG_) {                                                  \
-      auto k = hwgrad2_kernel<TW_, TH_, IMG_, NS_>;                                                     \
+      auto k = g_hw_ts == 3 ? hwgrad2_kernel<TW_, TH_, IMG_, NS_, 3>                                    \
+             : g_hw_ts == 2 ? hwgrad2_kernel<TW_, TH_, IMG_, NS_, 2> : hwgrad2_kernel<TW_, TH_, IMG_, NS_, 1>; \
       const int lds = NS_ * HWGeo2<TW_, TH_, IMG_>::STAGE;                                              \
       DCNN_HIP_CHECK(hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, lds)); \
-      hipLaunchKernelGGL(k, dim3(grid, a.npairs), dim3(256), lds, s, a);                                \
+      hipLaunchKernelGGL(k, dim3(grid, a.npairs), dim3(256 * g_hw_ts), lds, s, a);                      \
       DCNN_LAUNCH_CHECK();                                                                              \
       return;                                                                                           \
     }
     DCNN_HW2(16, 8, 1, 3)  // 3 x 48 KB
     DCNN_HW2(8, 8, 2, 2)   // 2 x 56 KB (three stages would need 168 KB)
     if (g_hwgrad_version == 2 && a.TW == 4 && a.TH == 4 && a.IMG == 8 && g_hwgrad4 != 0) {
-      auto k = hwgrad2_kernel<4, 4, 8, 2>;  // 2 x 64 KB
+      auto k = g_hw_ts == 3   ? hwgrad2_kernel<4, 4, 8, 2, 3>
+               : g_hw_ts == 2 ? hwgrad2_kernel<4, 4, 8, 2, 2> : hwgrad2_kernel<4, 4, 8, 2, 1>;  // 2 x 64 KB
       const int lds = 2 * HWGeo2<4, 4, 8>::STAGE;
       DCNN_HIP_CHECK(hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, lds));
-      hipLaunchKernelGGL(k, dim3(grid, a.npairs), dim3(256), lds, s, a);
+      hipLaunchKernelGGL(k, dim3(grid, a.npairs), dim3(256 * g_hw_ts), lds, s, a);
       DCNN_LAUNCH_CHECK();
       return;
     }
