@@ -61,11 +61,9 @@ __device__ __forceinline__ float g1_row_sum(float v) {
 
 // value held by lane 0 of this lane's 16-lane row
 __device__ __forceinline__ float g1_row_first(float v) {
-  const int x = __float_as_int(v);
-  const int r0 = __builtin_amdgcn_readlane(x, 0), r1 = __builtin_amdgcn_readlane(x, 16);
-  const int r2 = __builtin_amdgcn_readlane(x, 32), r3 = __builtin_amdgcn_readlane(x, 48);
-  const int row = (threadIdx.x & 63) >> 4;
-  return __int_as_float(row == 0 ? r0 : row == 1 ? r1 : row == 2 ? r2 : r3);
+  // DPP row_newbcast:0 (gfx90a+): lane 0 of each 16-lane row to the whole row, one instruction
+  // (four readlanes + selects before)
+  return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0x150, 0xf, 0xf, false));
 }
 
 // two bf16 of one 32-bit word -> fp32 pair (exact)

@@ -96,13 +96,11 @@ __device__ __forceinline__ void glds16_at(i32x4 rsrc, unsigned base, unsigned vo
                : "memory", "m0");
 }
 
-// value of lane 0 of this lane's 16-lane DPP row (row_bcast-free: readlane of the 4 row heads)
+// value of lane 0 of this lane's 16-lane DPP row
 __device__ __forceinline__ float h3_row_first(float v) {
-  const int x = __float_as_int(v);
-  const int r0 = __builtin_amdgcn_readlane(x, 0), r1 = __builtin_amdgcn_readlane(x, 16);
-  const int r2 = __builtin_amdgcn_readlane(x, 32), r3 = __builtin_amdgcn_readlane(x, 48);
-  const int row = (threadIdx.x & 63) >> 4;
-  return __int_as_float(row == 0 ? r0 : row == 1 ? r1 : row == 2 ? r2 : r3);
+  // DPP row_newbcast:0 (gfx90a+): lane 0 of each 16-lane row to the whole row, one instruction
+  // (four readlanes + selects before)
+  return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0x150, 0xf, 0xf, false));
 }
 
 __device__ __forceinline__ bf16x8 lds_b128(const char* smem, int off) {
@@ -141,7 +139,10 @@ struct H3 {
   static_assert(NWS == 2 || NWS == 3, "weight stages");
 };
 
-template <int NW, int WC, int TWC, int HN, int NWI, int NWS, int PITCH>
+// EPI: epilogue specialisation (compile-time, so the common cases carry no per-option branches
+// or selects): 1 = forward with BatchNorm statistics and no bias / residual / ReLU; 2 = data
+// gradient with the backward-BatchNorm fusion (optional residual); 0 = any option at run time
+template <int NW, int WC, int TWC, int HN, int NWI, int NWS, int PITCH, int EPI = 0>
 __global__ void __launch_bounds__(NW * 64, 8 / NW) hconv3_kernel(HConvArgs p, H3Geo g) {
   using T = H3<NW, WC, TWC, HN, NWI, NWS, PITCH>;
   constexpr int BN = T::BN, WP = T::WP;
@@ -449,9 +450,10 @@ __global__ void __launch_bounds__(NW * 64, 8 / NW) hconv3_kernel(HConvArgs p, H3
     yrow[j] = p.bnb.y + o;
     xrow[j] = p.bnb.x + o;
   }
-  const bool bnb = p.bnb.x != nullptr;
-  const bool stats = p.stats != nullptr;
-  const bool has_res = p.residual != nullptr, has_y = bnb && p.bnb.y != nullptr, has_x = bnb && stats;
+  const bool bnb = EPI == 2 || (EPI == 0 && p.bnb.x != nullptr);
+  const bool stats = EPI != 0 || p.stats != nullptr;
+  const bool has_res = EPI != 1 && p.residual != nullptr, has_y = bnb && p.bnb.y != nullptr, has_x = bnb && stats;
+  const bool has_bias = EPI == 0 && p.bias != nullptr, relu = EPI == 0 && p.relu;
   const int nl = n0 + wc * 64 + 4 * lh;  // this lane's first channel (+ i*16 + r)
   float bv[4][4], mu[4][4], is[4][4];
   uint2 rr[4][4], yy[4][4], xx[4][4];
@@ -459,7 +461,7 @@ __global__ void __launch_bounds__(NW * 64, 8 / NW) hconv3_kernel(HConvArgs p, H3
   for (int i = 0; i < 4; ++i)
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
-      bv[i][r] = p.bias ? p.bias[nl + i * 16 + r] : 0.f;
+      bv[i][r] = has_bias ? p.bias[nl + i * 16 + r] : 0.f;
       mu[i][r] = has_x ? p.bnb.mean[nl + i * 16 + r] : 0.f;
       is[i][r] = has_x ? p.bnb.istd[nl + i * 16 + r] : 0.f;
     }
@@ -485,7 +487,7 @@ __global__ void __launch_bounds__(NW * 64, 8 / NW) hconv3_kernel(HConvArgs p, H3
       for (int r = 0; r < 4; ++r) {
         f[r] = acc[i][j][r] + bv[i][r];
         if (has_res) f[r] += (float)rb[r];
-        if (p.relu) f[r] = fmaxf(f[r], 0.f);
+        if (relu) f[r] = fmaxf(f[r], 0.f);
         if (has_y) f[r] = (float)yb[r] > 0.f ? f[r] : 0.f;
       }
       uint2 o;
@@ -628,10 +630,10 @@ bool hconv3_plan(int NB, int H, int W, int Cs, int N, int ntaps, H3Plan* pl) {
   return true;
 }
 
-template <int NW, int WC, int TWC, int HN, int NWI, int NWS, int PITCH>
-static void launch_h3(const HConvArgs& a, const H3Geo& g, int grid, hipStream_t s) {
+template <int NW, int WC, int TWC, int HN, int NWI, int NWS, int PITCH, int EPI>
+static void launch_h3e(const HConvArgs& a, const H3Geo& g, int grid, hipStream_t s) {
   using T = H3<NW, WC, TWC, HN, NWI, NWS, PITCH>;
-  auto k = hconv3_kernel<NW, WC, TWC, HN, NWI, NWS, PITCH>;
+  auto k = hconv3_kernel<NW, WC, TWC, HN, NWI, NWS, PITCH, EPI>;
   static bool attr = false;
   if (!attr) {
     DCNN_HIP_CHECK(hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, T::LDS));
@@ -639,6 +641,20 @@ static void launch_h3(const HConvArgs& a, const H3Geo& g, int grid, hipStream_t 
   }
   hipLaunchKernelGGL(k, dim3(grid), dim3(NW * 64), T::LDS, s, a, g);
   DCNN_LAUNCH_CHECK();
+}
+
+static int g_h3_epi = [] {  // DCNN_HCONV3_EPI=0: always the generic epilogue (A/B)
+  const char* e = getenv("DCNN_HCONV3_EPI");
+  return e ? atoi(e) : 1;
+}();
+
+template <int NW, int WC, int TWC, int HN, int NWI, int NWS, int PITCH>
+static void launch_h3(const HConvArgs& a, const H3Geo& g, int grid, hipStream_t s) {
+  const bool plain_fwd = a.stats && !a.bnb.x && !a.residual && !a.relu && !a.bias;
+  const bool bnb_dgrad = a.stats && a.bnb.x && !a.relu && !a.bias;
+  if (g_h3_epi && plain_fwd) return launch_h3e<NW, WC, TWC, HN, NWI, NWS, PITCH, 1>(a, g, grid, s);
+  if (g_h3_epi && bnb_dgrad) return launch_h3e<NW, WC, TWC, HN, NWI, NWS, PITCH, 2>(a, g, grid, s);
+  launch_h3e<NW, WC, TWC, HN, NWI, NWS, PITCH, 0>(a, g, grid, s);
 }
 
 static void launch_h3_plan(const H3Plan& pl, const HConvArgs& a, const H3Geo& g, int grid, hipStream_t s) {
