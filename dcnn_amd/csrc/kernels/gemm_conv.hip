@@ -565,8 +565,8 @@ __global__ void splitk_reduce_kernel(SplitkSeg a, SplitkSeg b, int gxa, int spli
 // Deferred split-K reduction: the fp32 slabs of many weight gradients summed into their
 // gradients in ONE launch (api.h MultiRed). A work unit is (entry, 4 / wpc chunks of 256 floats):
 // each chunk gets wpc waves (1, 2 or 4 by split count, so few-split slabs do not leave waves
-// idle), wave j of a chunk sums splits {8 wpc g + 8j .. + 7} for every group g in order with all 8
-// loads of a group in flight, the chunk's waves meet in LDS in wave order and its first wave adds
+// idle), wave j of a chunk sums splits {G wpc g + G j .. + G - 1} for every group g in order with
+// all G loads of a group in flight, the chunk's waves meet in LDS in wave order and its first wave adds
 // into the gradient. Entries run longest (most groups) first so the many-split slabs' long
 // blocks are not the launch's tail. Fixed summation order throughout: bit-reproducible, no atomics.
 template <int G>
@@ -638,7 +638,8 @@ void multi_splitk_reduce(MultiRed t, hipStream_t s) {
   for (int k = 0; k < t.count; ++k) {
     RedEnt& e = t.e[k];
     e.vec = (e.n % 4 == 0 && ((uintptr_t)e.slab % 16) == 0 && ((uintptr_t)e.out % 16) == 0) ? 1 : 0;
-    e.wpc = e.splits <= 8 ? 1 : (e.splits <= 16 ? 2 : 4);
+    // (a wave covers G splits per group: a second wave only pays once the splits exceed G)
+    e.wpc = e.splits <= g_red_g ? 1 : (e.splits <= 2 * g_red_g ? 2 : 4);
     e.groups = (e.splits + g_red_g * e.wpc - 1) / (g_red_g * e.wpc);
   }
   // longest blocks first (stable: equal-length entries keep their queue order)
