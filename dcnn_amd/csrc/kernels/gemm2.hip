@@ -698,7 +698,12 @@ int gemm_t2_splits(int M, int N, int P) {
   t2_tile(M, N, &bm, &bn);
   const long tiles = (long)((M + bm - 1) / bm) * ((N + bn - 1) / bn);
   long splits = (512 + tiles - 1) / tiles;
-  const long max_by_k = P / (64 * 4) > 0 ? P / (64 * 4) : 1;
+  // at least DCNN_T2_MIN_K (default 256) reduction pixels per split
+  static const long min_k = [] {
+    const char* e = getenv("DCNN_T2_MIN_K");
+    return e && atoi(e) >= 64 ? (long)atoi(e) : 256l;
+  }();
+  const long max_by_k = P / min_k > 0 ? P / min_k : 1;
   if (splits > max_by_k) splits = max_by_k;
   const long max_by_mem = (48l << 20) / (4l * M * N) > 0 ? (48l << 20) / (4l * M * N) : 1;
   if (splits > max_by_mem) splits = max_by_mem;

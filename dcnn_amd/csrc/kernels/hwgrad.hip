@@ -543,6 +543,14 @@ int hwgrad_splits(int NB, int H, int W, int Cs, int Co) {
   int want = (hw_target_blocks() + per_split - 1) / per_split;
   if (want < 1) want = 1;
   if (want > total) want = total;
+  // at least DCNN_HWGRAD_MIN_TPS (default 2) tiles per split: a one-tile block writes ~4.6x the
+  // bytes it reads as fp32 partials (64x576 per 128 pixels). ResNet-50 batch 32 (one-tile splits on
+  // its 32x32 maps): 7.76k -> 7.90k img/s with 2 (4: same; profiles/wgrad_splits_r3.md)
+  static const int min_tps = [] {
+    const char* e = getenv("DCNN_HWGRAD_MIN_TPS");
+    return e ? atoi(e) : 2;
+  }();
+  if (min_tps > 1 && want > total / min_tps) want = total / min_tps > 1 ? total / min_tps : 1;
   const int tps = (total + want - 1) / want;
   return (total + tps - 1) / tps;
 }

@@ -821,6 +821,10 @@ class _DeferredReduce:
             self.flush()
 
     def flush(self):
+        if self.pending and _TRACE_REDUCE:
+            import sys
+            print(f"[splitk_reduce] {len(self.pending)} slabs, {self.pending_bytes / 2**20:.1f} MiB: "
+                  + " ".join(f"{t[2]}x{t[3]}" for t in self.pending), file=sys.stderr)
         if self.pending:
             ws = wgrad_stream
             with ws.on_side() if ws.forked else contextlib.nullcontext():
@@ -837,6 +841,7 @@ class _DeferredReduce:
 
 
 _DEFER_REDUCE = os.environ.get("DCNN_DEFER_REDUCE", "1") != "0"
+_TRACE_REDUCE = os.environ.get("DCNN_TRACE_REDUCE", "0") == "1"  # print each batched reduce's slabs
 _DEFER_REDUCE_BYTES = int(float(os.environ.get("DCNN_DEFER_REDUCE_MB", "1e9")) * (1 << 20))
 _tls = threading.local()
 
