@@ -158,6 +158,9 @@ def _f32_concat_ok(C, Co):
     return _F32_CONCAT and C % 64 == 0 and Co % 64 == 0
 
 
+_HCONV_1X1 = os.environ.get("DCNN_HCONV_1X1", "1") != "0"
+
+
 def _hconv_ok(N, OH, OW, H, W, sh, sw, Cs, Co, taps, wop):
     """Halo-tiled direct conv applies to stride-1 'same' convs with a 1-pixel reach (3x3/pad 1
     forward and its dgrad) on 64-multiple channel counts."""
@@ -165,7 +168,10 @@ def _hconv_ok(N, OH, OW, H, W, sh, sw, Cs, Co, taps, wop):
         return False
     if any(abs(t[0]) > 1 or abs(t[1]) > 1 for t in taps):
         return False
-    if len(taps) == 1:  # 1x1: the plain GEMM is already read-once
+    if len(taps) == 1 and not (_HCONV_1X1 and Cs >= 1024 and (N * OH * OW // 64) * (Co // 64) < 256):
+        # 1x1: the plain GEMM is already read-once. Except K >= 1024 1x1 convs (not on the
+        # streaming kernel) whose GEMM grid would be < 256 tiles: the halo kernel splits their K
+        # over the channel chunks (ResNet-50 b32: 7.87k -> 7.92k img/s; DCNN_HCONV_1X1=0 = off)
         return False
     return bool(kernels().hconv_supported(N, H, W, Cs, Co, len(taps)))
 

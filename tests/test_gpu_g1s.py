@@ -225,3 +225,37 @@ def test_g1s_strided_dgrad(hip, case):
             assert torch.equal(a, b)
     for a, b in zip(out[True][2:], out[False][2:]):
         assert rel_err(a, b) < (1e-2 if resid else 1e-4), rel_err(a, b)
+
+
+@pytest.mark.parametrize("case", [(32, 1024, 8, 8, 256), (32, 2048, 4, 4, 512), (8, 1024, 4, 4, 64)])
+def test_hconv_1x1_k1024(hip, case, monkeypatch):
+    """DCNN_HCONV_1X1: K >= 1024 1x1 convs on small grids (not on g1s) on the split-K halo
+    kernel — forward with statistics and the data gradient, against torch fp32 and the gathered
+    GEMM (the switch off)."""
+    N, Ci, H, W, Co = case
+    torch.manual_seed(7)
+    x = torch.randn(N, Ci, H, W)
+    w = torch.randn(Co, Ci, 1, 1) / math.sqrt(Ci)
+    xg = x.cuda().bfloat16().contiguous(memory_format=CL)
+    wg = w.cuda().bfloat16().contiguous(memory_format=CL)
+    dy = torch.randn(N, Co, H, W).cuda().bfloat16().contiguous(memory_format=CL)
+    wt = hip.conv_weight_t(wg)
+    outs = {}
+    for on in (False, True):
+        monkeypatch.setattr(hip, "_HCONV_1X1", on)
+        y, partial = hip.conv2d_fwd(xg, wg, None, (1, 1), (0, 0), stats=True)
+        st = hip.bn_stats(y, partial).clone()
+        dx = hip.conv2d_dgrad(dy, wt, (N, Ci, H, W), (1, 1), (0, 0))
+        torch.cuda.synchronize()
+        outs[on] = (y, st, dx)
+    y, st, dx = outs[True]
+    y_ref = F.conv2d(bf(x), bf(w))
+    assert rel_err(y, y_ref) < 1e-2
+    assert rel_err(y, outs[False][0]) < 1e-2
+    yd = y.double()
+    assert rel_err(st[:Co], yd.mean((0, 2, 3))) < 1e-5
+    var = yd.var((0, 2, 3), unbiased=False).cpu()
+    assert ((st[Co:].double().cpu() - var).abs() / var).max() < 1e-3
+    dx_t = torch.nn.grad.conv2d_input((N, Ci, H, W), wg.float(), dy.float(), 1, 0)
+    assert rel_err(dx, dx_t) < 1e-2
+    assert rel_err(dx, outs[False][2]) < 1e-2
