@@ -1,0 +1,45 @@
+"""Conv algorithm routing rules of ops/hip.py (`_hconv_ok`), checked on the CPU with the kernel
+library's shape query stubbed: which convs go to the halo kernel (hconv / hconv3) instead of the
+gathered GEMM or the streaming 1x1 kernel."""
+import pytest
+
+from dcnn_amd.ops import hip
+
+
+class _Stub:
+    def hconv_supported(self, *args):
+        return True
+
+
+@pytest.fixture
+def stub(monkeypatch):
+    monkeypatch.setattr(hip, "kernels", lambda: _Stub())
+    monkeypatch.setattr(hip, "_HCONV", True)
+    monkeypatch.setattr(hip, "_HCONV_1X1", True)
+
+
+TAP1 = [(0, 0, 0, 0)]
+TAPS9 = [(dy, dx, 0, 0) for dy in (-1, 0, 1) for dx in (-1, 0, 1)]
+
+
+def test_3x3_same_stride1(stub):
+    assert hip._hconv_ok(256, 32, 32, 32, 32, 1, 1, 64, 64, TAPS9, None)
+    assert not hip._hconv_ok(256, 16, 16, 32, 32, 2, 2, 64, 128, TAPS9, None)  # strided
+    # a tap two pixels away (5x5 reach) or more than 9 taps: not a halo-1 conv
+    assert not hip._hconv_ok(256, 32, 32, 32, 32, 1, 1, 64, 64, [(2, 0, 0, 0), (0, 0, 0, 0)], None)
+    assert not hip._hconv_ok(256, 32, 32, 32, 32, 1, 1, 64, 64, TAPS9 + [(0, 0, 0, 0)], None)
+
+
+def test_1x1_only_k1024_small_grid(stub):
+    # ResNet-50 batch 32: layer-3 reduce (1024 -> 256 at 8x8: 128 GEMM tiles) -> halo kernel
+    assert hip._hconv_ok(32, 8, 8, 8, 8, 1, 1, 1024, 256, TAP1, None)
+    assert hip._hconv_ok(32, 4, 4, 4, 4, 1, 1, 2048, 512, TAP1, None)
+    # batch 256: 1024 tiles, the GEMM grid fills the chip
+    assert not hip._hconv_ok(256, 8, 8, 8, 8, 1, 1, 1024, 256, TAP1, None)
+    # K <= 512 1x1 convs belong to the streaming kernel / plain GEMM
+    assert not hip._hconv_ok(32, 8, 8, 8, 8, 1, 1, 512, 256, TAP1, None)
+
+
+def test_1x1_switch_off(stub, monkeypatch):
+    monkeypatch.setattr(hip, "_HCONV_1X1", False)
+    assert not hip._hconv_ok(32, 8, 8, 8, 8, 1, 1, 1024, 256, TAP1, None)
