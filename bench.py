@@ -9,7 +9,10 @@ weights, Adam, softmax cross-entropy. Data parallel over RCCL, one process per G
   python -m torch.distributed.run --nnodes=1 --nproc-per-node 8 --master-addr 127.0.0.1 \
       --master-port 29500 bench.py --gpus 8 --steps 50 --warmup 10
 
-Weak scaling: every rank trains --batch images per step (global batch = batch x gpus).
+Weak scaling: every rank trains --batch images per step (global batch = batch x gpus). The
+gradient all-reduce runs on the framework's own RCCL communicator (parallel/rccl.py; bucketed,
+on a comm stream overlapping the backward, captured in the step graph); --dp-backend torch uses
+torch.distributed's ProcessGroupNCCL instead.
 Exactly K steps are timed between a barrier + device synchronisation on both sides; the
 slowest rank's time is reported. Every timed step runs the full forward, loss, backward,
 gradient all-reduce and optimizer update.
@@ -41,7 +44,11 @@ def main():
     ap.add_argument("--grad-dtype", default="fp32", choices=["fp32", "bf16"],
                     help="gradient all-reduce wire format (bf16: all_to_all shards + fp32 sum + all_gather)")
     ap.add_argument("--pg", action="store_true",
-                    help="create the RCCL process group even at world size 1 (segmented DP step on one GPU)")
+                    help="create the RCCL process group even at world size 1 (torch data plane)")
+    ap.add_argument("--dp-backend", default=os.environ.get("DCNN_DP_BACKEND", "rccl"), choices=["rccl", "torch"],
+                    help="gradient data plane on GPUs: the framework's own RCCL communicator (rank/world from "
+                         "the launcher env, unique id over the native TCP plane, no torch.distributed) or "
+                         "torch.distributed's ProcessGroupNCCL (also the fallback if the in-tree plane fails)")
     ap.add_argument("--profile", action="store_true", help="print per-layer device times")
     ap.add_argument("--device", default="cuda")
     ap.add_argument("--dtype", default="bf16", choices=["bf16", "fp32"],
@@ -55,11 +62,16 @@ def main():
     a = ap.parse_args()
 
     from dcnn_amd.parallel.dp import DataParallel, init_distributed
+    from dcnn_amd.parallel.rccl import env_rank_world
     from dcnn_amd.models import INPUT_SHAPES, NUM_CLASSES, create_model
     from dcnn_amd.nn import Adam, LossFactory
     from dcnn_amd.runtime.step import TrainStep
 
-    rank, world, local = init_distributed("nccl" if a.device == "cuda" else "gloo")
+    in_tree = a.device == "cuda" and a.dp_backend == "rccl" and not a.pg
+    if in_tree:
+        rank, world, local = env_rank_world()  # no torch.distributed: the in-tree plane bootstraps itself
+    else:
+        rank, world, local = init_distributed("nccl" if a.device == "cuda" else "gloo")
     if a.pg and not dist.is_initialized():
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
         os.environ.setdefault("MASTER_PORT", "29533")
@@ -86,7 +98,21 @@ def main():
         model.set_compute_dtype(torch.float32)
     model.initialize()
     model.set_first_layer_input_grad(False)
-    dp = DataParallel(model, bucket_mb=a.bucket_mb, grad_dtype=a.grad_dtype)
+    plane = "torch"
+    if in_tree:
+        try:
+            dp = DataParallel(model, bucket_mb=a.bucket_mb, grad_dtype=a.grad_dtype, comm_backend="rccl")
+            plane = "rccl" if dp.rccl is not None else "none"
+        except Exception as e:  # (symmetric failures, e.g. no librccl: every rank falls back)
+            print(f"[bench] in-tree RCCL plane unavailable ({e}); falling back to torch.distributed",
+                  file=sys.stderr)
+            in_tree = False
+            init_distributed("nccl")
+            dp = DataParallel(model, bucket_mb=a.bucket_mb, grad_dtype=a.grad_dtype, comm_backend="torch")
+    else:
+        dp = DataParallel(model, bucket_mb=a.bucket_mb, grad_dtype=a.grad_dtype, comm_backend="torch")
+    if plane == "torch" and not dist.is_initialized():
+        plane = "none"
     opt = Adam(1e-3)
     opt.attach(model)
     loss_fn = LossFactory.create("softmax_crossentropy")
@@ -104,7 +130,7 @@ def main():
         if dev.type == "cuda":
             torch.cuda.synchronize(dev)
         if world > 1:
-            dist.barrier()
+            dp.barrier()
 
     for i in range(a.warmup):
         step(xs[i % nbuf], ys[i % nbuf])
@@ -114,10 +140,7 @@ def main():
         step(xs[i % nbuf], ys[i % nbuf])
     sync()
     t1 = time.perf_counter()
-    elapsed = torch.tensor([t1 - t0], dtype=torch.float64, device=dev)
-    if world > 1:
-        dist.all_reduce(elapsed, op=dist.ReduceOp.MAX)
-    el = float(elapsed.item())
+    el = dp.max_over_ranks(t1 - t0)  # the slowest rank's time
     loss_val = float(step.last_loss.item()) if step.last_loss is not None else float("nan")
     ms = el / a.steps * 1e3
     imgs = a.batch * world * a.steps / el
@@ -131,6 +154,7 @@ def main():
             "config": {"model": a.model, "global_batch": a.batch * world, "per_gpu_batch": a.batch, "seq_len": None,
                        "image_size": [C, H, W], "parallelism": f"dp{world}", "optimizer": "adam",
                        "grad_allreduce": a.grad_dtype if world > 1 else None,
+                       "data_plane": plane if world > 1 else None,
                        "hipgraph": timed_with_graph, "final_loss": round(loss_val, 4),
                        "f32_mode": (a.f32_mode if a.dtype == "fp32" and dev.type == "cuda" else None)},
         }), flush=True)
@@ -141,6 +165,10 @@ def main():
         for i in range(3):
             step(xs[0], ys[0])
         print(model.print_profiling_summary(), file=sys.stderr)
+    if world > 1:
+        dp.barrier()
+    if dp.rccl is not None:
+        dp.rccl.close()
     if dist.is_initialized():
         dist.barrier()
         dist.destroy_process_group()

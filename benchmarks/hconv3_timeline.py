@@ -19,14 +19,11 @@ SHAPES = {"l1.c": (64, 32, 32, 64), "l2.c": (128, 16, 16, 128), "l3.c": (256, 8,
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--batch", type=int, default=256)
-    ap.add_argument("--shapes", default="l1.c,l2.c,l3.c,l4.c")
+    ap.add_argument("--shapes", default="l1.c,l2.c")
     ap.add_argument("--op", default="fwd", choices=["fwd", "dgrad"])
-    ap.add_argument("--stagger", type=int, default=-1)
     a = ap.parse_args()
     from dcnn_amd.ops import hip
     K = hip.kernels()
-    if a.stagger >= 0:
-        K.hconv3_set_stagger(a.stagger)
     CL = torch.channels_last
     N = a.batch
     for nm in a.shapes.split(","):
@@ -37,11 +34,13 @@ def main():
         wt = hip.conv_weight_t(w)
         if a.op == "fwd":
             fn = lambda: hip.conv2d_fwd(x, w, None, (1, 1), (1, 1), stats=True)
-            grid = K.hconv_tiles(N, H, W, C, Co, 9) * K.hconv_splits(N, H, W, C, Co, 9)
+            items = K.hconv_tiles(N, H, W, C, Co, 9) * K.hconv_splits(N, H, W, C, Co, 9)
         else:
             fn = lambda: hip.conv2d_dgrad(dy, wt, x.shape, (1, 1), (1, 1))
-            grid = K.hconv_tiles(N, H, W, Co, C, 9) * K.hconv_splits(N, H, W, Co, C, 9)
-        buf = torch.zeros(grid * 8 * 8, dtype=torch.int64, device="cuda")
+            items = K.hconv_tiles(N, H, W, Co, C, 9) * K.hconv_splits(N, H, W, Co, C, 9)
+        # per item u and wave: [0] item start, [1] first chunk done, [2] K loop done, [3] epilogue
+        # computed + stored, [4] item end (statistics merged); [5] workgroup start (first item)
+        buf = torch.zeros(items * 4 * 8, dtype=torch.int64, device="cuda")
         for _ in range(3):
             fn()
         torch.cuda.synchronize()
@@ -49,32 +48,24 @@ def main():
         fn()
         torch.cuda.synchronize()
         K.hconv3_set_stamps(0)
-        raw = buf.view(grid, 8, 8).cpu()
-        arr = raw[:, 0, 6]
-        if int(arr.abs().sum()) != 0:
-            # stagger diagnostics: workgroups per hardware CU key, arrival index histogram
-            keys = (arr >> 8).tolist()
-            olds = (arr & 0xff).tolist()
-            per = {}
-            for kk in keys:
-                per[kk] = per.get(kk, 0) + 1
-            hist = {}
-            for o in olds:
-                hist[o] = hist.get(o, 0) + 1
-            print(f"   stagger: {len(per)} CU keys, workgroups/key min {min(per.values())} max {max(per.values())}, "
-                  f"arrival index histogram {dict(sorted(hist.items()))}")
-            raw[:, 0, 6] = 0
-        t = raw.view(grid * 8, 8).double()
-        live = t[:, 0] > 0
-        t = t[live]
-        t0 = t[:, 0].min()
-        ph = {"prologue": t[:, 1] - t[:, 0], "chunk0": t[:, 2] - t[:, 1], "kloop_rest": t[:, 3] - t[:, 2],
-              "epilogue": t[:, 4] - t[:, 3], "stats": t[:, 5] - t[:, 4], "wave_total": t[:, 5] - t[:, 0]}
-        print(f"{nm} {a.op} batch {N}: grid {grid}, waves stamped {int(live.sum())}, "
-              f"span {float(t[:, 5].max() - t0):.0f} cyc, start skew p50/p90/max "
-              f"{float((t[:, 0] - t0).median()):.0f}/{float((t[:, 0] - t0).quantile(0.9)):.0f}/"
-              f"{float((t[:, 0] - t0).max()):.0f}")
-        print("   " + "  ".join(f"{k} {float(v.median()):.0f}" for k, v in ph.items()))
+        t = buf.view(items, 4, 8).double().cpu()
+        t0 = t[:, :, 0][t[:, :, 0] > 0].min()
+        kloop = (t[:, :, 2] - t[:, :, 0]).sum()
+        epi = (t[:, :, 4] - t[:, :, 2]).sum()
+        first = t[:, :, 5] > 0
+        # a wave's life: from its workgroup's start to its last item's end; items of one workgroup
+        # are the ones whose start stamp falls inside it (grid-strided), summed over all waves
+        life_end = t[:, :, 4].max()
+        per_item = {"kloop": t[:, :, 2] - t[:, :, 0], "chunk0": t[:, :, 1] - t[:, :, 0],
+                    "epilogue": t[:, :, 3] - t[:, :, 2], "stats": t[:, :, 4] - t[:, :, 3]}
+        prologue = (t[:, :, 0] - t[:, :, 5])[first]
+        span = float(life_end - t0)
+        wg = int(first.sum()) // 4
+        print(f"{nm} {a.op} batch {N}: {items} items on {wg} workgroups, span {span:.0f} cyc; "
+              f"K loop share of item time {float(kloop / (kloop + epi)) * 100:.1f}%, "
+              f"of wave life {float(kloop / ((t[:, :, 4].max() - t0) * 4 * wg)) * 100:.1f}%")
+        print("   medians per item: " + "  ".join(f"{k} {float(v.median()):.0f}" for k, v in per_item.items())
+              + f"  prologue {float(prologue.median()):.0f}")
 
 
 if __name__ == "__main__":

@@ -90,9 +90,8 @@ bool hconv_supported(int NB, int H, int W, int Cs, int N, int ntaps);
 int hconv_stat_rows(int NB, int H, int W, int Cs, int N, int ntaps, int f32out);
 bool hconv_v3(int NB, int H, int W, int Cs, int N, int ntaps);  // shape runs on hconv3
 void hconv3_enable(int on);
-// co-resident workgroup phase shift (s_sleep(127) count of the later arrival) and persistent grid
-void hconv3_set_stagger(int sleeps);
-void hconv3_set_stamps(uintptr_t p);  // diagnostic per-wave timeline buffer (u64 [grid][8][8]) or 0  // third-generation 3x3 kernel (hconv3.hip), default on (DCNN_HCONV3)
+void hconv3_set_grid_cap(int n);      // test hook: cap the persistent grid (0: resident workgroups)
+void hconv3_set_stamps(uintptr_t p);  // diagnostic per-item timeline buffer (u64 [items][4][8]) or 0
 // halo-tiled stride-1 weight gradient (hwgrad.hip): slab[split][Co][t*Cs + c] = partial dW
 struct HWArgs {
   const bf16* dY; const bf16* X; float* slab; float* bias_slab;  // bias_slab[split][Co] (optional)

@@ -126,7 +126,7 @@ PYBIND11_MODULE(_kernels, m) {
   m.def("hconv_set_ws", &hconv_set_ws);
   m.def("bn_set_vectorised", &bn_set_vectorised);
   m.def("hconv_tile_elems", &hconv_tile_elems);
-  m.def("hconv3_set_stagger", &hconv3_set_stagger);
+  m.def("hconv3_set_grid_cap", &hconv3_set_grid_cap);
   m.def("hconv3_enable", &hconv3_enable);
   m.def("hconv_v3", &hconv_v3);
   m.def("hconv3_set_stamps", &hconv3_set_stamps);

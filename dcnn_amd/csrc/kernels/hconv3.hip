@@ -1,31 +1,39 @@
-// Third-generation halo-tiled 3x3 stride-1 convolution (forward and dgrad) for CDNA4.
+// Third-generation halo-tiled 3x3 stride-1 convolution (forward and dgrad) for CDNA4:
+// a persistent, cross-tile pipelined kernel.
 //
-// Why a new kernel (profiles/pmc_conv_r2.md): hconv_kernel runs one 64-deep tap per barrier
-// (16 MFMAs per wave between barriers), recomputes every swizzled LDS address per tap (~130
-// VALU/SALU instructions per 16 MFMAs) and relies on 2-3 resident workgroups to hide the weight
-// ring's latency: 15-21% MFMA busy. This kernel is built around the opposite budget:
+// Work item = one output tile (IMG images x TH x TW = 256 pixels, 64 output channels) and, on
+// small grids, one split-K slice of its input channels. The grid is sized to the resident
+// workgroups (2 per CU) and every workgroup walks its items in a strided order, so that:
 //
-//  * 8 waves (512 threads), ONE workgroup per CU, each wave owning a 64 (output channels) x 64
+//  * the next item's first halo chunk and first weight stage are DMA'd into LDS during the
+//    current item's last K steps (the (item, chunk, kernel-row) sequence is ONE stream: the halo
+//    double buffer and the 2-stage weight ring never restart);
+//  * the current item's output stores are NOT issued in its epilogue: the epilogue computes the
+//    bf16 output rows and the BatchNorm statistics in registers, and the stores go out inside the
+//    next item's first two K steps, behind that step's DMA issue, where the counted vmcnt waits
+//    let them drain under the MFMAs. The chip-wide write burst at the end of every tile round
+//    (profiles/experiment_hconv_variants.md: epilogue phase as long as the K loop) becomes a
+//    trickle beside the matrix work.
+//
+// Per item the structure is the round-3 one:
+//
+//  * 4 waves (256 threads), two workgroups per CU, each wave owning a 64 (output channels) x 64
 //    (pixels) block: 16 accumulator tiles of mfma_f32_16x16x32_bf16.
-//  * Roles swapped against hconv_kernel: the weights are the A operand (rows = output
-//    channels) and the input halo the B operand (columns = pixels), so an accumulator register
-//    quad holds 4 consecutive channels of ONE pixel — the epilogue stores 8 bytes of an NHWC row
-//    straight from registers (no LDS staging), and residual / BN masks load the same way.
-//  * K step = 32 input channels x one kernel row (3 taps): 48 MFMAs per wave per barrier.
-//    The 32-channel halo chunk (64-byte LDS rows) is loaded once per chunk and serves its 3
-//    steps; weights stream through a 3-stage ring, two steps ahead, with counted vmcnt waits
-//    and raw s_barrier (direct-to-LDS loads stay in flight across barriers).
-//  * Every LDS fragment address is precomputed: the A (weight) side is one per-lane base plus
-//    immediates; the B (halo) side is 36 per-lane addresses (4 pixel subtiles x 9 taps) plus an
-//    immediate buffer offset. The K loop issues 24 ds_read_b128 + 48 MFMA + 3-6 buffer loads
-//    and a handful of scalar ops per step.
-//  * Bank conflicts: 64-byte rows hold 4 16-byte chunks. A ds_read_b128 is served in four
-//    16-lane groups; halo rows read by a group are 16 pixels at an arbitrary tap shift. Pixel
-//    subtile row l carries pixel perm(l) (rows 4-11 <- pixels 8-15, rows 12-15 <- pixels 4-7) and
-//    the chunk is XOR-swizzled by bit 2 of the halo pixel index: every group then covers 16
-//    distinct 16-byte slots for ANY shift (exhaustively checked for 16- and 8-wide tiles); 4-wide
-//    tiles use the identity row order and bit 3 (conflict-free at halo pitch 8). Weight rows are
-//    16-aligned: swizzle by bit 3 of the row.
+//  * Weights are the A operand (rows = output channels), the input halo the B operand (columns =
+//    pixels). The weight rows are loaded in a permuted channel order so that an accumulator
+//    quad pair (i = 2h, 2h+1) holds 8 CONSECUTIVE channels of one pixel: the epilogue stores
+//    16 bytes per lane, 64 contiguous bytes per pixel and wave instruction (8 dwordx4 stores per
+//    lane instead of 16 dwordx2).
+//  * K step = 32 input channels x one kernel row (3 taps): 48 MFMAs per wave per barrier. The
+//    32-channel halo chunk (64-byte LDS rows) is loaded once per chunk and serves its 3 steps;
+//    weights stream through a 2-stage ring with counted vmcnt waits and raw s_barrier
+//    (direct-to-LDS loads stay in flight across barriers).
+//  * Every LDS fragment address is precomputed (per-lane bases + immediates); halo source
+//    addresses are decoded once per workgroup (pixel -> image / row / column of the halo) and
+//    re-based per item with a handful of integer ops.
+//  * Bank conflicts: 64-byte rows hold 4 16-byte chunks; pixel subtile row l carries pixel
+//    perm(l) and the chunk is XOR-swizzled by bit 2 of the halo pixel index, so every 16-lane
+//    ds_read_b128 group covers 16 distinct slots for any tap shift.
 //
 // Reference parity: the reference runs this GEMM as im2col + cuBLAS SGEMM or cuDNN
 // (src/nn/layers_impl/cuda/conv2d_ops.cu:18-128, cudnn_conv2d_ops.cu:187-244).
@@ -61,6 +69,15 @@ __device__ __forceinline__ int h3_swz(int P) {
 }
 __device__ __forceinline__ int h3_wswz(int n) { return ((n >> 3) & 1) << 1; }
 
+// output channel (within the workgroup's BN) of weight-stage row n. Row m = 16 i + q of a wave's
+// 64 is MFMA row q of accumulator tile i, which lands in lane group q >> 2, register q & 3; the
+// channel 32 (i >> 1) + 8 (q >> 2) + 4 (i & 1) + (q & 3) gives lane group lh the 8 consecutive
+// channels 32 h + 8 lh .. + 7 in tiles (2h, 2h+1)
+__device__ __forceinline__ int h3_rowch(int n) {
+  const int m = n & 63, i = m >> 4, q = m & 15;
+  return (n & ~63) + 32 * (i >> 1) + 8 * (q >> 2) + 4 * (i & 1) + (q & 3);
+}
+
 template <int N>
 __device__ __forceinline__ void vmwait() {
   asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
@@ -68,14 +85,17 @@ __device__ __forceinline__ void vmwait() {
 __device__ __forceinline__ void h3_barrier() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
 
 // fixed-order sum over the 16 lanes of a DPP row (rotations by 8 and 4, then quad swaps): every
-// lane of the row gets the row total, with no LDS traffic (ds_swizzle / bpermute shuffles cost ~100
-// cycles of latency each)
+// lane of the row gets the row total, with no LDS traffic
 __device__ __forceinline__ float h3_row_sum(float v) {
   v += __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0x128, 0xf, 0xf, false));  // row_ror:8
   v += __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0x124, 0xf, 0xf, false));  // row_ror:4
   v += __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0x4e, 0xf, 0xf, false));   // quad xor 2
   v += __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0xb1, 0xf, 0xf, false));   // quad xor 1
   return v;
+}
+// value of lane 0 of this lane's 16-lane DPP row (row_newbcast:0)
+__device__ __forceinline__ float h3_row_first(float v) {
+  return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0x150, 0xf, 0xf, false));
 }
 
 template <int K, int N, class F>
@@ -87,20 +107,18 @@ __device__ __forceinline__ void h3_static_for(F&& f) {
 }
 
 // direct-to-LDS 16-byte load to LDS byte address `base + OFF` (base: one wave-uniform SGPR for the
-// whole kernel, OFF an immediate), so the compiler keeps no per-destination M0 constant alive
+// whole kernel, OFF an immediate)
 template <int OFF>
 __device__ __forceinline__ void glds16_at(i32x4 rsrc, unsigned base, unsigned voff) {
+  // (the operands are wave-uniform; readfirstlane pins them to SGPRs where the compiler's
+  // divergence analysis loses track of that through the persistent loop's control flow)
+  base = __builtin_amdgcn_readfirstlane(base);
+#pragma unroll
+  for (int i = 0; i < 4; ++i) rsrc[i] = __builtin_amdgcn_readfirstlane(rsrc[i]);
   asm volatile("s_add_u32 m0, %0, %3\n\ts_nop 0\n\tbuffer_load_dwordx4 %1, %2, 0 offen lds"
                :
                : "s"(base), "v"(voff), "s"(rsrc), "n"(OFF)
                : "memory", "m0");
-}
-
-// value of lane 0 of this lane's 16-lane DPP row
-__device__ __forceinline__ float h3_row_first(float v) {
-  // DPP row_newbcast:0 (gfx90a+): lane 0 of each 16-lane row to the whole row, one instruction
-  // (four readlanes + selects before)
-  return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0x150, 0xf, 0xf, false));
 }
 
 __device__ __forceinline__ bf16x8 lds_b128(const char* smem, int off) {
@@ -108,43 +126,42 @@ __device__ __forceinline__ bf16x8 lds_b128(const char* smem, int off) {
 }
 }  // namespace
 
+// every lambda of the kernel is force-inlined: an outlined one receives its captures through a
+// stack frame (scratch + flat loads of every captured register)
+#define H3L __attribute__((always_inline))
+
 // geometry the launcher computes once per call
 struct H3Geo {
   int TH, TW, IMG, pitch;  // spatial tile IMG x TH x TW pixels; halo row pitch (>= TW + 2)
   int tiles_n, tiles_m;    // channel tiles (N / BN), pixel tiles
   int nchunk;              // 32-channel chunks per split
+  int nitems;              // tiles_m * tiles_n * splits
   int tb[9];               // weight column offset (elements) of tap (dy + 1) * 3 + (dx + 1)
-  int halo_bytes;          // bytes of one halo buffer (= 8 waves x HN x 1 KiB)
-  int stagger;             // s_sleep(127) count of the second workgroup to arrive on a CU
-  unsigned* cu_ctr;        // [2048] per-CU arrival counters + [1] exit ticket (stagger), or null
-  int dbg;                 // diagnostic ablations (DCNN_HCONV3_DBG): 1 = no output stores, 2 = no statistics
-  unsigned long long* stamps;  // diagnostic: per-wave s_memtime at 8 points (hconv3_set_stamps), or null
+  unsigned c_bytes;        // output bytes (32-bit store offsets)
+  unsigned long long* stamps;  // diagnostic timeline [nitems][NW][8] (STAMP instance only)
 };
 
-// NW waves per workgroup (8: one workgroup per CU; 4: two per CU, whose prologue / epilogue
-// memory phases overlap each other's MFMA phases), WC of them along the output channels (64
-// each), NW / WC along the pixels (64 each). NWS weight stages (3: two steps in flight; 2: one).
-// PITCH > 0: compile-time halo row pitch, a multiple of 8 pixels, so a kernel-row (dy) shift keeps
-// the bit-2 chunk swizzle and becomes an immediate ds_read offset: 12 halo fragment addresses per
-// lane (4 pixel subtiles x 3 dx) instead of 36. PITCH == 0: runtime pitch, 36 addresses.
-template <int NW, int WC, int TWC, int HN, int NWI, int NWS, int PITCH>
+// NW waves per workgroup, WC of them along the output channels (64 each), NW / WC along the
+// pixels (64 each). PITCH > 0: compile-time halo row pitch (multiple of 8 pixels: a kernel-row
+// shift keeps the chunk swizzle and becomes an immediate ds_read offset); 0: runtime pitch.
+template <int NW, int WC, int TWC, int HN, int NWI, int PITCH>
 struct H3 {
   static constexpr int BN = 64 * WC, WP = NW / WC, BM = 64 * WP;
   static constexpr int HALO = NW * HN * 1024;   // one halo buffer
   static constexpr int WST = NW * NWI * 1024;   // one weight stage (3 taps x BN rows x 64 B, padded)
-  static constexpr int LDS = 2 * HALO + NWS * WST;
+  static constexpr int LDS = 2 * HALO + 2 * WST;
   static_assert(3 * BN * 64 <= WST, "weight stage");
-  static_assert(WP * BN * 3 * 4 + 16 <= HALO, "epilogue scratch lives in halo buffer 0");
+  static_assert(WP * BN * 3 * 4 + 16 <= HALO, "epilogue scratch lives in the last chunk's halo buffer");
   static_assert(LDS <= 163840, "LDS budget");
-  static_assert(NWS == 2 || NWS == 3, "weight stages");
 };
 
 // EPI: epilogue specialisation (compile-time, so the common cases carry no per-option branches
 // or selects): 1 = forward with BatchNorm statistics and no bias / residual / ReLU; 2 = data
-// gradient with the backward-BatchNorm fusion (optional residual); 0 = any option at run time
-template <int NW, int WC, int TWC, int HN, int NWI, int NWS, int PITCH, int EPI = 0>
+// gradient with the backward-BatchNorm fusion (optional residual); 0 = any option at run time.
+// STAMP: diagnostic instance with s_memtime stamps (benchmarks/hconv3_timeline.py).
+template <int NW, int WC, int TWC, int HN, int NWI, int PITCH, int EPI, bool STAMP>
 __global__ void __launch_bounds__(NW * 64, 8 / NW) hconv3_kernel(HConvArgs p, H3Geo g) {
-  using T = H3<NW, WC, TWC, HN, NWI, NWS, PITCH>;
+  using T = H3<NW, WC, TWC, HN, NWI, PITCH>;
   constexpr int BN = T::BN, WP = T::WP;
   constexpr int NT = NW * 64;
   extern __shared__ __attribute__((aligned(16))) char smem[];
@@ -155,70 +172,42 @@ __global__ void __launch_bounds__(NW * 64, 8 / NW) hconv3_kernel(HConvArgs p, H3
   const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int wc = wid % WC, wp = wid / WC;
   const int lr = lane & 15, lh = lane >> 4;
-  // diagnostic timeline (off unless hconv3_set_stamps): lane 0 of every wave
-  auto stamp = [&](int k) {
-    if (g.stamps && lane == 0) g.stamps[((size_t)blockIdx.x * 8 + wid) * 8 + k] = __builtin_amdgcn_s_memtime();
-  };
-  stamp(0);
-  // Phase shift of co-resident workgroups: the workgroups of a round run prologue (halo read),
-  // K loop and epilogue (output write) in lockstep, so the memory phases are chip-wide bursts
-  // during which the MFMAs idle. The second workgroup to arrive on each CU in a launch starts
-  // `stagger` x 8K cycles late, so the pair alternates memory and MFMA phases (later rounds
-  // inherit the offset: a replacement arrives when its predecessor leaves). Arrival order comes
-  // from counters keyed by the hardware CU id (XCC, SE, SH, CU); the grid's last workgroup
-  // resets them for the next launch.
-  const bool stag = g.stagger > 0 && g.cu_ctr;
-  if (stag) {
-    volatile int* flag = reinterpret_cast<volatile int*>(smem + T::HALO - 32);
-    if (tid == 0) {
-      const unsigned hw = __builtin_amdgcn_s_getreg((31 << 11) | 4);   // HW_REG_HW_ID
-      const unsigned xcc = __builtin_amdgcn_s_getreg((3 << 11) | 20);  // HW_REG_XCC_ID
-      const unsigned key = ((xcc & 7u) << 8) | (((hw >> 13) & 7u) << 5) | (((hw >> 12) & 1u) << 4) | ((hw >> 8) & 15u);
-      const unsigned old = __hip_atomic_fetch_add(g.cu_ctr + key, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      *flag = (int)(old == 1u);
-      if (g.stamps) g.stamps[((size_t)blockIdx.x * 8) * 8 + 6] = ((unsigned long long)key << 8) | old;
+  auto stamp = [&](int u, int k) H3L {
+    if constexpr (STAMP) {
+      if (lane == 0) g.stamps[((size_t)u * NW + wid) * 8 + k] = __builtin_amdgcn_s_memtime();
     }
-    __syncthreads();
-    const int late = *flag;
-    __syncthreads();  // (the flag lives in halo buffer 0, which the prologue overwrites)
-    if (late)
-      for (int k = 0; k < g.stagger; ++k) __builtin_amdgcn_s_sleep(127);
-  }
+  };
   const int SPL = p.splits;
-  const int u0 = xcd_remap3(blockIdx.x, gridDim.x);
-  const int zs = u0 % SPL, lt = u0 / SPL;
-  const int tm = lt / g.tiles_n, tn = lt % g.tiles_n;
-  const int n0 = tn * BN;
-  const int tx_tiles = p.W / g.TW, tpi = tx_tiles * (p.H / g.TH);
-  const int ig = tm / tpi, trem = tm - ig * tpi;
-  const int y0 = (trem / tx_tiles) * g.TH, x0 = (trem % tx_tiles) * g.TW, img0 = ig * g.IMG;
-  const int HW2 = g.TW + 2, HH2 = g.TH + 2, pitch = PITCH > 0 ? PITCH : g.pitch;
-  const int HPI = HH2 * pitch;  // halo pixels per image (pitch-padded)
-  const int HPX = g.IMG * HPI;  // halo pixels per tile
+  const int G = gridDim.x;
+  int u = xcd_remap3(blockIdx.x, G);  // this workgroup's items: u, u + G, u + 2G, ...
+  if (u >= g.nitems) return;          // (the launcher sizes the grid <= nitems)
+  stamp(u, 5);
   if (p.zero_ptr && blockIdx.x == 0)
     for (int i = tid; i < p.zero_n; i += NT) p.zero_ptr[i] = 0.f;
   const i32x4 rsA = raw_rsrc(p.A, p.a_bytes);
   const i32x4 rsB = raw_rsrc(p.B, p.b_bytes);
-  const int cbase = zs * g.nchunk * 32;  // first input channel of this split
+  const int tx_tiles = p.W / g.TW, tpi = tx_tiles * (p.H / g.TH);
+  const int HW2 = g.TW + 2, pitch = PITCH > 0 ? PITCH : g.pitch;
+  const int HPI = (g.TH + 2) * pitch;  // halo pixels per image (pitch-padded)
+  const int HPX = g.IMG * HPI;         // halo pixels per tile
+  const int nch = g.nchunk;            // chunks per item (even, or 1: a 32-channel input)
 
-  // ---- halo loader: instruction k of this wave fills halo pixels [16(wid*HN + k), +16)
-  unsigned hsrc[HN];
+  // ---- halo loader, item-invariant part: instruction k of this wave fills halo pixels
+  // [16(wid*HN + k), +16); lane -> (image, halo row, halo column, chunk slot), packed
+  unsigned hpk[HN];
 #pragma unroll
   for (int k = 0; k < HN; ++k) {
     const int P = (wid * HN + k) * 16 + (lane >> 2);
-    unsigned v = kOOB3;
+    unsigned v = 0xffffffffu;
     if (P < HPX) {
       const int im = P / HPI, r = P - im * HPI;
       const int hy = r / pitch, hx = r - hy * pitch;
-      const int sy = y0 + hy - 1, sx = x0 + hx - 1, n = img0 + im;
-      if (hx < HW2 && sy >= 0 && sy < p.H && sx >= 0 && sx < p.W && n < p.NB)
-        v = (unsigned)((((long)n * p.H + sy) * p.W + sx) * p.Cs * 2) +
-            (unsigned)((cbase + ((lane & 3) ^ h3_swz<TWC>(P)) * 8) * 2);
+      if (hx < HW2) v = (unsigned)hx | ((unsigned)hy << 8) | ((unsigned)im << 16) | ((unsigned)((lane & 3) ^ h3_swz<TWC>(P)) << 24);
     }
-    hsrc[k] = v;
+    hpk[k] = v;
   }
-  // ---- weight loader: stage row R = dx * BN + n (3 taps x BN output channels), 64 B each
-  unsigned wsrc[NWI];
+  // ---- weight loader, item-invariant part: stage row R = dx * BN + n (3 taps x BN rows, 64 B)
+  unsigned wrc[NWI];  // (stage row's output channel + 1) | chunk slot byte offset << 16
   int wtb[NWI][3];  // byte offset of the instruction's tap column for kernel rows dy = 0..2 (SGPRs)
 #pragma unroll
   for (int k = 0; k < NWI; ++k) {
@@ -227,27 +216,70 @@ __global__ void __launch_bounds__(NW * 64, 8 / NW) hconv3_kernel(HConvArgs p, H3
     const int dx = R0 / BN, n = R - dx * BN;
 #pragma unroll
     for (int dy = 0; dy < 3; ++dy) wtb[k][dy] = __builtin_amdgcn_readfirstlane(dx < 3 ? g.tb[dy * 3 + dx] * 2 : 0);
-    wsrc[k] = (dx < 3 && n0 + n < p.N)
-                  ? (unsigned)(((long)(n0 + n) * p.ldb + cbase + ((lane & 3) ^ h3_wswz(n)) * 8) * 2)
-                  : kOOB3;
+    wrc[k] = (unsigned)(dx < 3 ? h3_rowch(n) + 1 : 0) | ((unsigned)(((lane & 3) ^ h3_wswz(n)) * 16) << 16);
   }
+
+  // ---- per-item geometry and source addresses
+  struct Item {
+    int lt, zs, tm, n0, y0, x0, img0, cbase;
+  };
+  auto decode = [&](int v) H3L {
+    Item t;
+    t.zs = v % SPL;
+    t.lt = v / SPL;
+    t.tm = t.lt / g.tiles_n;
+    t.n0 = (t.lt - t.tm * g.tiles_n) * BN;
+    const int ig = t.tm / tpi, trem = t.tm - ig * tpi;
+    t.y0 = (trem / tx_tiles) * g.TH;
+    t.x0 = (trem % tx_tiles) * g.TW;
+    t.img0 = ig * g.IMG;
+    t.cbase = t.zs * nch * 32;  // first input channel of this split
+    return t;
+  };
+  auto addrs_h = [&](const Item& t, unsigned* hs) H3L {
+#pragma unroll
+    for (int k = 0; k < HN; ++k) {
+      const unsigned pk = hpk[k];
+      unsigned v = kOOB3;
+      if (!(pk >> 31)) {
+        const int sy = t.y0 + (int)((pk >> 8) & 255) - 1, sx = t.x0 + (int)(pk & 255) - 1;
+        const int n = t.img0 + (int)((pk >> 16) & 255);
+        if (sy >= 0 && sy < p.H && sx >= 0 && sx < p.W && n < p.NB)
+          v = ((((unsigned)n * p.H + sy) * p.W + sx) * (unsigned)p.Cs + t.cbase + (pk >> 24) * 8) * 2u;
+      }
+      hs[k] = v;
+    }
+  };
+  auto addrs_w = [&](const Item& t, unsigned* ws) H3L {
+#pragma unroll
+    for (int k = 0; k < NWI; ++k) {
+      const int wr = (int)(wrc[k] & 0xffff) - 1;  // -1: padding row
+      const int ch = t.n0 + wr;
+      ws[k] = (wr >= 0 && ch < p.N) ? ((unsigned)ch * p.ldb + t.cbase) * 2u + (wrc[k] >> 16) : kOOB3;
+    }
+  };
+  auto addrs = [&](const Item& t, unsigned* hs, unsigned* ws) H3L {
+    addrs_h(t, hs);
+    addrs_w(t, ws);
+  };
+
   // LDS byte address of this wave's first halo / weight DMA slot (wave-uniform SGPRs)
   const unsigned lds0 = __builtin_amdgcn_readfirstlane(
       (unsigned)(uintptr_t)((const __attribute__((address_space(3))) char*)smem));
   const unsigned hbase = lds0 + wid * HN * 1024, wbase_lds = lds0 + 2 * T::HALO + wid * NWI * 1024;
-  auto load_halo = [&](auto buf_c, int c) {
+  auto load_halo = [&](auto buf_c, int c, const unsigned* hs) H3L {
     constexpr int BUF = decltype(buf_c)::value;
     const unsigned co = (unsigned)(c * 64);
-    h3_static_for<0, HN>([&](auto kc) {
+    h3_static_for<0, HN>([&](auto kc) H3L {
       constexpr int K = decltype(kc)::value;
-      glds16_at<BUF * T::HALO + K * 1024>(rsA, hbase, hsrc[K] + co);
+      glds16_at<BUF * T::HALO + K * 1024>(rsA, hbase, hs[K] + co);
     });
   };
-  auto load_w = [&](auto stage_c, int c, int dy) {
+  auto load_w = [&](auto stage_c, int c, int dy, const unsigned* ws) H3L {
     constexpr int ST = decltype(stage_c)::value;
-    h3_static_for<0, NWI>([&](auto kc) {
+    h3_static_for<0, NWI>([&](auto kc) H3L {
       constexpr int K = decltype(kc)::value;
-      glds16_at<ST * T::WST + K * 1024>(rsB, wbase_lds, wsrc[K] + (unsigned)(wtb[K][dy] + c * 64));
+      glds16_at<ST * T::WST + K * 1024>(rsB, wbase_lds, ws[K] + (unsigned)(wtb[K][dy] + c * 64));
     });
   };
 
@@ -257,46 +289,55 @@ __global__ void __launch_bounds__(NW * 64, 8 / NW) hconv3_kernel(HConvArgs p, H3
   // B (halo): pixel subtile j of this wave, tap (dy, dx)
   constexpr int NBA = PITCH > 0 ? 3 : 9;
   static_assert(PITCH == 0 || (PITCH % 8 == 0 && TWC != 4), "dy-invariant swizzle needs pitch % 8 == 0");
+  // (re-derived at the start of every item from an opaque zero, so the 4 x NBA addresses are not
+  // kept live through the epilogue, where the persistent loop has no registers to spare)
   int baddr[4][NBA];
+  auto set_baddr = [&](int zero) H3L {
 #pragma unroll
-  for (int j = 0; j < 4; ++j) {
-    const int q = wp * 64 + j * 16 + h3_perm<TWC>(lr);  // tile-local output pixel
-    const int tpx = g.TH * g.TW;
-    const int im = q / tpx, r = q - im * tpx;
-    const int P0 = im * HPI + (r / g.TW) * pitch + (r % g.TW);  // halo pixel of tap (-1, -1)
+    for (int j = 0; j < 4; ++j) {
+      const int q = wp * 64 + j * 16 + h3_perm<TWC>(lr);  // tile-local output pixel
+      const int tpx = g.TH * g.TW;
+      const int im = q / tpx, r = q - im * tpx;
+      const int P0 = im * HPI + (r / g.TW) * pitch + (r % g.TW) + zero;  // halo pixel of tap (-1, -1)
 #pragma unroll
-    for (int t = 0; t < NBA; ++t) {
-      const int P = P0 + (NBA == 3 ? t : (t / 3) * pitch + (t % 3));
-      baddr[j][t] = P * 64 + ((lh ^ h3_swz<TWC>(P)) << 4);
+      for (int t = 0; t < NBA; ++t) {
+        const int P = P0 + (NBA == 3 ? t : (t / 3) * pitch + (t % 3));
+        baddr[j][t] = P * 64 + ((lh ^ h3_swz<TWC>(P)) << 4);
+      }
     }
-  }
-  auto baddr_of = [&](int j, int dy, int dx) {
+  };
+  set_baddr(0);
+  auto baddr_of = [&](int j, int dy, int dx) H3L {
     if constexpr (PITCH > 0) return baddr[j][dx] + dy * PITCH * 64;
     else return baddr[j][dy * 3 + dx];
   };
+  // output row offsets (bytes, first channel of the lane group) of the tile's pixel subtiles
+  auto out_offsets = [&](const Item& t, unsigned* oo) H3L {
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int q = wp * 64 + j * 16 + h3_perm<TWC>(lr);
+      const int tpx = g.TH * g.TW;
+      const int im = q / tpx, r = q - im * tpx;
+      const unsigned pix = ((unsigned)(t.img0 + im) * p.H + t.y0 + r / g.TW) * p.W + t.x0 + r % g.TW;
+      oo[j] = (pix * (unsigned)p.N + t.n0 + wc * 64 + 8 * lh) * 2u;
+    }
+  };
 
   f32x4 acc[4][4];
-#pragma unroll
-  for (int i = 0; i < 4; ++i)
-#pragma unroll
-    for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-
   // one K step: chunk c (halo buffer HB), kernel row DY, weight stage ST. The fragments of tap
-  // dx + 1 are read while tap dx's 16 MFMAs run (two register sets in flight), so the LDS latency
-  // after the barrier is paid once per step, not once per tap. The step's direct-to-LDS loads
-  // (`issue`: next weight stage / next halo, into buffers no wave reads this step) go out after
-  // the first MFMAs: an LDS-DMA issue among queued MFMAs costs the wave ~60 cycles instead of
-  // delaying the step's first MFMA by its full issue cost (MI355X_MICROARCH cycle constants).
-  auto step = [&](auto hb_c, auto dy_c, auto st_c, auto issue) {
+  // dx + 1 are read while tap dx's 16 MFMAs run, so the LDS latency after the barrier is paid
+  // once per step. The step's direct-to-LDS loads and deferred stores (`issue`) go out after the
+  // first MFMAs.
+  auto step = [&](auto hb_c, auto dy_c, auto st_c, auto pre, auto issue) H3L {
     constexpr int HB = decltype(hb_c)::value, DY = decltype(dy_c)::value, ST = decltype(st_c)::value;
     bf16x8 a[3][4], b[3][4];
-    auto rd = [&](int dx) {
+    auto rd = [&](int dx) H3L {
 #pragma unroll
       for (int i = 0; i < 4; ++i) a[dx][i] = lds_b128(smem, abase + ST * T::WST + dx * BN * 64 + i * 16 * 64);
 #pragma unroll
       for (int j = 0; j < 4; ++j) b[dx][j] = lds_b128(smem, baddr_of(j, DY, dx) + HB * T::HALO);
     };
-    auto mm = [&](int dx, int i0, int i1) {
+    auto mm = [&](int dx, int i0, int i1) H3L {
       __builtin_amdgcn_s_setprio(1);
 #pragma unroll
       for (int i = i0; i < i1; ++i)
@@ -304,6 +345,7 @@ __global__ void __launch_bounds__(NW * 64, 8 / NW) hconv3_kernel(HConvArgs p, H3
         for (int j = 0; j < 4; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[dx][i], b[dx][j], acc[i][j], 0, 0, 0);
       __builtin_amdgcn_s_setprio(0);
     };
+    pre();
     rd(0);
     rd(1);
     mm(0, 0, 2);
@@ -313,110 +355,117 @@ __global__ void __launch_bounds__(NW * 64, 8 / NW) hconv3_kernel(HConvArgs p, H3
     mm(1, 0, 4);
     mm(2, 0, 4);
   };
-  const int nch = g.nchunk;  // chunks of this split (even, or the single chunk of a 32-channel input)
 
-  if constexpr (NWS == 3) {
-    // 3-stage ring, stage = kernel row: step (c, dy) issues the weights of the step two ahead
-    // ((c,2) / (c+1,0) / (c+1,1)) and, at dy = 0, the next chunk's halo; the wait after step s
-    // retires W(s + 1) and everything older.
-    load_halo(I0{}, 0);
-    load_w(I0{}, 0, 0);
-    load_w(I1{}, 0, 1);
-    vmwait<NWI>();
-    h3_barrier();
-    stamp(1);
-    auto chunk = [&](int c, auto hb_c) {
-      constexpr int HB = decltype(hb_c)::value;
-      const bool more = c + 1 < nch;
-      step(hb_c, I0{}, I0{}, [&] {
-        load_w(I2{}, c, 2);
-        if (more) load_halo(std::integral_constant<int, HB ^ 1>{}, c + 1);
-      });
-      if (more) vmwait<NWI + HN>(); else vmwait<NWI>();
-      h3_barrier();
-      step(hb_c, I1{}, I1{}, [&] { if (more) load_w(I0{}, c + 1, 0); });
-      if (more) vmwait<NWI>(); else vmwait<0>();
-      h3_barrier();
-      step(hb_c, I2{}, I2{}, [&] { if (more) load_w(I1{}, c + 1, 1); });
-      if (more) vmwait<NWI>(); else vmwait<0>();
-      h3_barrier();
-    };
-    for (int c = 0; c < nch; c += 2) {
-      chunk(c, I0{});
-      if (c == 0) stamp(2);
-      if (c + 1 < nch) chunk(c + 1, I1{});
-    }
-  } else {
-    // 2-stage ring: step s uses stage s & 1 = (c + dy) & 1 and issues W(s + 1) (and, at dy = 0, the
-    // next chunk's halo after it); the wait after step s retires W(s + 1) and everything older
-    load_halo(I0{}, 0);
-    load_w(I0{}, 0, 0);
-    vmwait<0>();
-    h3_barrier();
-    stamp(1);
-    auto chunk = [&](int c, auto hb_c) {
-      constexpr int HB = decltype(hb_c)::value;
-      using S0 = std::integral_constant<int, HB>;
-      using S1 = std::integral_constant<int, HB ^ 1>;
-      const bool more = c + 1 < nch;
-      step(hb_c, I0{}, S0{}, [&] {
-        load_w(S1{}, c, 1);
-        if (more) load_halo(std::integral_constant<int, HB ^ 1>{}, c + 1);
-      });
-      if (more) vmwait<HN>(); else vmwait<0>();
-      h3_barrier();
-      step(hb_c, I1{}, S1{}, [&] { load_w(S0{}, c, 2); });
-      vmwait<0>();
-      h3_barrier();
-      step(hb_c, I2{}, S0{}, [&] { if (more) load_w(S1{}, c + 1, 0); });
-      vmwait<0>();
-      h3_barrier();
-    };
-    for (int c = 0; c < nch; c += 2) {
-      chunk(c, I0{});
-      if (c == 0) stamp(2);
-      if (c + 1 < nch) chunk(c + 1, I1{});
-    }
-  }
-  stamp(3);
+  unsigned oo[4];  // output row offsets of the item's pixel subtiles
+  char* const cbytes = reinterpret_cast<char*>(p.C);
+  auto nothing = []() H3L {};
 
-  // ---------------------------------------------------------------- split-K hand-off
-  float* red = reinterpret_cast<float*>(smem);  // epilogue scratch in halo buffer 0 (K loop done)
-  if (SPL > 1) {
-    // every partial leaves with agent-scope (sc1) 8-byte stores, each wave drains them, one lane
-    // adds to the tile's ticket behind the workgroup barrier, and the workgroup whose add returns
-    // SPL - 1 reads all partials back with sc1 loads and sums them in split order
-    constexpr int E2 = 32;  // float2 pairs per lane
-    unsigned long long* part = reinterpret_cast<unsigned long long*>(p.part) + (size_t)lt * SPL * E2 * NT;
-#pragma unroll
-    for (int i = 0; i < 4; ++i)
-#pragma unroll
-      for (int j = 0; j < 4; ++j)
-#pragma unroll
-        for (int h = 0; h < 2; ++h) {
-          const int e2 = (i * 4 + j) * 2 + h;
-          const unsigned long long bits = (unsigned long long)__float_as_uint(acc[i][j][2 * h]) |
-                                          ((unsigned long long)__float_as_uint(acc[i][j][2 * h + 1]) << 32);
-          __hip_atomic_store(part + ((size_t)zs * E2 + e2) * NT + tid, bits, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        }
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
-    volatile int* flag = reinterpret_cast<volatile int*>(smem + T::HALO - 16);
-    if (tid == 0) {
-      const unsigned old = __hip_atomic_fetch_add(p.tickets + lt, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      const int last = old == (unsigned)(SPL - 1);
-      if (last) __hip_atomic_store(p.tickets + lt, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      *flag = last;
-    }
-    __syncthreads();
-    const int last = *flag;
-    __syncthreads();
-    if (!last) return;
+  // ---- first item's prologue: halo chunk 0, W(0, 0) landed; W(0, 1) in flight
+  unsigned hs[HN], ws[NWI];
+  addrs(decode(u), hs, ws);
+  load_halo(I0{}, 0, hs);
+  load_w(I0{}, 0, 0, ws);
+  load_w(I1{}, 0, 1, ws);
+  vmwait<NWI>();
+  h3_barrier();
+  int nst = 0;  // output stores issued after the item's W(0, 1) (the previous item's epilogue)
+
+  while (true) {
+    stamp(u, 0);
+
+    const int un = u + G;
+    const bool has_next = un < g.nitems;
 #pragma unroll
     for (int i = 0; i < 4; ++i)
 #pragma unroll
       for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-    for (int z = 0; z < SPL; ++z) {
+
+    // 2-stage ring: step s uses stage s & 1 = (chunk + dy) & 1 (3 steps per chunk) = the chunk's
+    // halo buffer at dy = 0. Step (c, 0) issues W(c, 1) and the next halo chunk (this item's
+    // c + 1, or the next item's chunk 0); step (c, 1) issues W(c, 2); step (c, 2) issues the next
+    // chunk's W(., 0) (this item's, or the next item's). The wait after a step retires that step's
+    // weights and the halo issued before it. In the last chunk the next item's source addresses
+    // replace this item's (halo after step 0's issue, weights after step 1's), so no second set
+    // of address registers stays live.
+    // Item boundary: the next item's W(0, 1) goes out at the start of this item's epilogue (its
+    // stage is free once the last step's barrier has passed), BEFORE the epilogue's output stores.
+    // So the first step of the next item does not issue W(0, 1) and its wait leaves the stores in
+    // flight: they drain under that step's MFMAs instead of stalling the workgroup.
+    auto chunk = [&](int c, auto hb_c, auto first_c) H3L {
+      constexpr int HB = decltype(hb_c)::value;
+      constexpr bool FIRST = decltype(first_c)::value;
+      using S0 = std::integral_constant<int, HB>;
+      using S1 = std::integral_constant<int, HB ^ 1>;
+      const bool last = c + 1 == nch;
+      const bool more = !last || has_next;
+      auto dma0 = [&]() H3L {
+        if constexpr (!FIRST) load_w(S1{}, c, 1, ws);
+        if (!last) {
+          load_halo(S1{}, c + 1, hs);
+        } else if (has_next) {
+          addrs_h(decode(un), hs);
+          load_halo(S1{}, 0, hs);
+        }
+      };
+      step(hb_c, I0{}, S0{}, nothing, dma0);
+      if constexpr (FIRST) {
+        // W(c, 1) is older than the stores and the halo
+        if (nst) {
+          if (more) vmwait<HN + 8>(); else vmwait<8>();
+        } else {
+          if (more) vmwait<HN>(); else vmwait<0>();
+        }
+      } else {
+        if (more) vmwait<HN>(); else vmwait<0>();
+      }
+      h3_barrier();
+      step(hb_c, I1{}, S1{}, nothing, [&]() H3L { load_w(S0{}, c, 2, ws); });
+      vmwait<0>();
+      h3_barrier();
+      step(hb_c, I2{}, S0{}, nothing, [&]() H3L {
+        if (!last) {
+          load_w(S1{}, c + 1, 0, ws);
+        } else if (has_next) {
+          addrs_w(decode(un), ws);
+          load_w(S1{}, 0, 0, ws);
+        }
+      });
+      vmwait<0>();
+      h3_barrier();
+    };
+    auto kloop = [&](auto h0_c) H3L {
+      constexpr int H0 = decltype(h0_c)::value;
+      using F = std::integral_constant<bool, false>;
+      chunk(0, std::integral_constant<int, H0>{}, std::integral_constant<bool, true>{});
+      stamp(u, 1);
+      for (int c = 1; c < nch; c += 2) {
+        chunk(c, std::integral_constant<int, H0 ^ 1>{}, F{});
+        if (c + 1 < nch) chunk(c + 1, std::integral_constant<int, H0>{}, F{});
+      }
+    };
+    kloop(I0{});
+    stamp(u, 2);
+    nst = 0;
+    const int hb_last = (nch - 1) & 1;  // (nch even, or one item per workgroup)
+    // the next item's W(0, 1) into the stage the last step read (ws holds the next item's weight
+    // addresses since the last step's issue)
+    if (has_next) {
+      if (hb_last) load_w(I1{}, 0, 1, ws); else load_w(I0{}, 0, 1, ws);
+    }
+    // epilogue scratch: the last chunk's halo buffer, free until the next item's first step issues
+    // its second halo chunk into it (after the closing barrier below)
+    float* red = reinterpret_cast<float*>(smem + hb_last * T::HALO);
+    volatile int* flag = reinterpret_cast<volatile int*>(smem + hb_last * T::HALO + WP * BN * 12);
+
+    const Item it = decode(u);
+    bool run_epi = true;
+    // ---------------------------------------------------------------- split-K hand-off
+    if (SPL > 1) {
+      // every partial leaves with agent-scope (sc1) 8-byte stores, each wave drains them, one lane
+      // adds to the tile's ticket behind the workgroup barrier, and the workgroup whose add returns
+      // SPL - 1 reads all partials back with sc1 loads and sums them in split order
+      constexpr int E2 = 32;  // float2 pairs per lane
+      unsigned long long* part = reinterpret_cast<unsigned long long*>(p.part) + (size_t)it.lt * SPL * E2 * NT;
 #pragma unroll
       for (int i = 0; i < 4; ++i)
 #pragma unroll
@@ -424,149 +473,154 @@ __global__ void __launch_bounds__(NW * 64, 8 / NW) hconv3_kernel(HConvArgs p, H3
 #pragma unroll
           for (int h = 0; h < 2; ++h) {
             const int e2 = (i * 4 + j) * 2 + h;
-            const unsigned long long bits =
-                __hip_atomic_load(part + ((size_t)z * E2 + e2) * NT + tid, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            acc[i][j][2 * h] += __uint_as_float((unsigned)bits);
-            acc[i][j][2 * h + 1] += __uint_as_float((unsigned)(bits >> 32));
+            const unsigned long long bits = (unsigned long long)__float_as_uint(acc[i][j][2 * h]) |
+                                            ((unsigned long long)__float_as_uint(acc[i][j][2 * h + 1]) << 32);
+            __hip_atomic_store(part + ((size_t)it.zs * E2 + e2) * NT + tid, bits, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
           }
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __syncthreads();
+      if (tid == 0) {
+        const unsigned old = __hip_atomic_fetch_add(p.tickets + it.lt, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        const int lst = old == (unsigned)(SPL - 1);
+        if (lst) __hip_atomic_store(p.tickets + it.lt, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        *flag = lst;
+      }
+      __syncthreads();
+      run_epi = __builtin_amdgcn_readfirstlane(*flag) != 0;  // (uniform: keeps the DMA operands in SGPRs)
+      __syncthreads();
+      if (run_epi) {
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+#pragma unroll
+          for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+        for (int z = 0; z < SPL; ++z) {
+#pragma unroll
+          for (int i = 0; i < 4; ++i)
+#pragma unroll
+            for (int j = 0; j < 4; ++j)
+#pragma unroll
+              for (int h = 0; h < 2; ++h) {
+                const int e2 = (i * 4 + j) * 2 + h;
+                const unsigned long long bits =
+                    __hip_atomic_load(part + ((size_t)z * E2 + e2) * NT + tid, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                acc[i][j][2 * h] += __uint_as_float((unsigned)bits);
+                acc[i][j][2 * h + 1] += __uint_as_float((unsigned)(bits >> 32));
+              }
+        }
+      }
     }
-  }
 
-  // ---------------------------------------------------------------- epilogue (from registers)
-  // acc[i][j][r]: channel n0 + wc*64 + i*16 + 4*lh + r, tile pixel wp*64 + j*16 + perm(lr).
-  // Every operand load (bias, BN mean / istd, residual, ReLU output, BN input) is issued before the
-  // first store: a load's wait also waits for every older store, so interleaving them would make
-  // each channel group wait for the previous group's stores to drain.
-  bf16* crow[4];                   // output row of pixel subtile j (channel 0)
-  const bf16 *rrow[4], *yrow[4], *xrow[4];
+    if (run_epi) {
+      // -------------------------------------------------------------- epilogue (from registers)
+      // lane (lh, lr): pixel subtile j -> tile pixel wp*64 + j*16 + perm(lr); channel half h ->
+      // channels cb + 32 h + e (e = 0..7) = acc[2h + (e >> 2)][j][e & 3], cb = n0 + wc*64 + 8*lh.
+      // Per channel half: operand loads (bias, BN mean / istd, residual, ReLU output, BN input),
+      // arithmetic, 4 x 16-byte stores, statistics rows.
+      const bool bnb = EPI == 2 || (EPI == 0 && p.bnb.x != nullptr);
+      const bool stats = EPI != 0 || p.stats != nullptr;
+      const bool has_res = EPI != 1 && p.residual != nullptr, has_y = bnb && p.bnb.y != nullptr;
+      const bool has_x = bnb && stats;
+      const bool has_bias = EPI == 0 && p.bias != nullptr, relu = EPI == 0 && p.relu;
+      const int cb = it.n0 + wc * 64 + 8 * lh;
+      out_offsets(it, oo);
+      const char* rbytes = reinterpret_cast<const char*>(p.residual);
+      const char* ybytes = reinterpret_cast<const char*>(p.bnb.y);
+      const char* xbytes = reinterpret_cast<const char*>(p.bnb.x);
+      // one channel half at a time (keeps the epilogue's operand registers to a half)
 #pragma unroll
-  for (int j = 0; j < 4; ++j) {
-    const int q = wp * 64 + j * 16 + h3_perm<TWC>(lr);
-    const int tpx = g.TH * g.TW;
-    const int im = q / tpx, r = q - im * tpx;
-    const size_t o = (((size_t)(img0 + im) * p.H + y0 + r / g.TW) * p.W + x0 + r % g.TW) * (size_t)p.N;
-    crow[j] = p.C + o;
-    rrow[j] = p.residual + o;
-    yrow[j] = p.bnb.y + o;
-    xrow[j] = p.bnb.x + o;
-  }
-  const bool bnb = EPI == 2 || (EPI == 0 && p.bnb.x != nullptr);
-  const bool stats = EPI != 0 || p.stats != nullptr;
-  const bool has_res = EPI != 1 && p.residual != nullptr, has_y = bnb && p.bnb.y != nullptr, has_x = bnb && stats;
-  const bool has_bias = EPI == 0 && p.bias != nullptr, relu = EPI == 0 && p.relu;
-  const int nl = n0 + wc * 64 + 4 * lh;  // this lane's first channel (+ i*16 + r)
-  float bv[4][4], mu[4][4], is[4][4];
-  uint2 rr[4][4], yy[4][4], xx[4][4];
+      for (int h = 0; h < 2; ++h) {
+        float bv[8], mu[8], is[8];
 #pragma unroll
-  for (int i = 0; i < 4; ++i)
-#pragma unroll
-    for (int r = 0; r < 4; ++r) {
-      bv[i][r] = has_bias ? p.bias[nl + i * 16 + r] : 0.f;
-      mu[i][r] = has_x ? p.bnb.mean[nl + i * 16 + r] : 0.f;
-      is[i][r] = has_x ? p.bnb.istd[nl + i * 16 + r] : 0.f;
-    }
-#pragma unroll
-  for (int i = 0; i < 4; ++i)
-#pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      const int c = nl + i * 16;
-      rr[i][j] = has_res ? *reinterpret_cast<const uint2*>(rrow[j] + c) : make_uint2(0u, 0u);
-      yy[i][j] = has_y ? *reinterpret_cast<const uint2*>(yrow[j] + c) : make_uint2(0u, 0u);
-      xx[i][j] = has_x ? *reinterpret_cast<const uint2*>(xrow[j] + c) : make_uint2(0u, 0u);
-    }
-#pragma unroll
-  for (int i = 0; i < 4; ++i) {
-    const int cl0 = wc * 64 + i * 16 + 4 * lh;  // tile-local first of this lane's 4 channels
-    float gv[4][4], xh[4][4];  // [j][r]: stored value, and (bnb) stored value * xhat
-#pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      float f[4];
-      const bf16* rb = reinterpret_cast<const bf16*>(&rr[i][j]);
-      const bf16* yb = reinterpret_cast<const bf16*>(&yy[i][j]);
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        f[r] = acc[i][j][r] + bv[i][r];
-        if (has_res) f[r] += (float)rb[r];
-        if (relu) f[r] = fmaxf(f[r], 0.f);
-        if (has_y) f[r] = (float)yb[r] > 0.f ? f[r] : 0.f;
-      }
-      uint2 o;
-      bf16* ob = reinterpret_cast<bf16*>(&o);
-#pragma unroll
-      for (int r = 0; r < 4; ++r) ob[r] = (bf16)f[r];
-      if (!(g.dbg & 1)) *reinterpret_cast<uint2*>(crow[j] + nl + i * 16) = o;
-      const bf16* xb = reinterpret_cast<const bf16*>(&xx[i][j]);
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        gv[j][r] = (float)ob[r];  // statistics of the values actually stored
-        xh[j][r] = gv[j][r] * (((float)xb[r] - mu[i][r]) * is[i][r]);
-      }
-    }
-    if (stats && !(g.dbg & 2)) {
-      float pv[4], sa[4], sb[4];
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        if (bnb) {
-          pv[r] = 0.f;
-          sa[r] = (gv[0][r] + gv[1][r]) + (gv[2][r] + gv[3][r]);
-          sb[r] = (xh[0][r] + xh[1][r]) + (xh[2][r] + xh[3][r]);
-        } else {
-          // forward Welford rows: sums about a pivot (the wave's first pixel of the channel: lane
-          // 16*lh of the DPP row, broadcast by a row rotation chain-free read)
-          pv[r] = h3_row_first(gv[0][r]);
-          float a = 0.f, b = 0.f;
-#pragma unroll
-          for (int j = 0; j < 4; ++j) { const float d = gv[j][r] - pv[r]; a += d; b += d * d; }
-          sa[r] = a;
-          sb[r] = b;
+        for (int e = 0; e < 8; ++e) {
+          bv[e] = has_bias ? p.bias[cb + 32 * h + e] : 0.f;
+          mu[e] = has_x ? p.bnb.mean[cb + 32 * h + e] : 0.f;
+          is[e] = has_x ? p.bnb.istd[cb + 32 * h + e] : 0.f;
         }
-        sa[r] = h3_row_sum(sa[r]);  // fixed-order sum over the 16 lanes (pixels) of the DPP row
-        sb[r] = h3_row_sum(sb[r]);
-      }
-      if (lr == 0) {
+        uint4 rr[4], yy[4], xx[4];
 #pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          float* e = red + (wp * BN + cl0 + r) * 3;
-          e[0] = pv[r];
-          e[1] = sa[r];
-          e[2] = sb[r];
+        for (int j = 0; j < 4; ++j) {
+          const unsigned o = oo[j] + h * 64;
+          rr[j] = has_res ? *reinterpret_cast<const uint4*>(rbytes + o) : make_uint4(0u, 0u, 0u, 0u);
+          yy[j] = has_y ? *reinterpret_cast<const uint4*>(ybytes + o) : make_uint4(0u, 0u, 0u, 0u);
+          xx[j] = has_x ? *reinterpret_cast<const uint4*>(xbytes + o) : make_uint4(0u, 0u, 0u, 0u);
+        }
+        float gv[4][8], xh[4][8];  // [j][e]: stored value, and (bnb) stored value * xhat
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          float f[8], rf[8], yf[8], xf[8];
+          unpack8(rr[j], rf);
+          unpack8(yy[j], yf);
+          unpack8(xx[j], xf);
+#pragma unroll
+          for (int e = 0; e < 8; ++e) {
+            f[e] = acc[2 * h + (e >> 2)][j][e & 3] + bv[e];
+            if (has_res) f[e] += rf[e];
+            if (relu) f[e] = fmaxf(f[e], 0.f);
+            if (has_y) f[e] = yf[e] > 0.f ? f[e] : 0.f;
+          }
+          const uint4 ov = pack8(f);
+          *reinterpret_cast<uint4*>(cbytes + oo[j] + h * 64) = ov;
+          unpack8(ov, gv[j]);  // statistics of the values actually stored
+#pragma unroll
+          for (int e = 0; e < 8; ++e) xh[j][e] = has_x ? gv[j][e] * ((xf[e] - mu[e]) * is[e]) : 0.f;
+        }
+        if (stats) {
+#pragma unroll
+          for (int e = 0; e < 8; ++e) {
+            float pv, sa, sb;
+            if (bnb) {
+              pv = 0.f;
+              sa = (gv[0][e] + gv[1][e]) + (gv[2][e] + gv[3][e]);
+              sb = (xh[0][e] + xh[1][e]) + (xh[2][e] + xh[3][e]);
+            } else {
+              // forward Welford rows: sums about a pivot (the wave's first pixel of the channel:
+              // lane 16*lh of the DPP row)
+              pv = h3_row_first(gv[0][e]);
+              float a = 0.f, b = 0.f;
+#pragma unroll
+              for (int j = 0; j < 4; ++j) { const float d = gv[j][e] - pv; a += d; b += d * d; }
+              sa = a;
+              sb = b;
+            }
+            sa = h3_row_sum(sa);  // fixed-order sum over the 16 lanes (pixels) of the DPP row
+            sb = h3_row_sum(sb);
+            if (lr == 0) {
+              float* q = red + (wp * BN + wc * 64 + 32 * h + 8 * lh + e) * 3;
+              q[0] = pv;
+              q[1] = sa;
+              q[2] = sb;
+            }
+          }
         }
       }
-    }
-  }
-  stamp(4);
-  if (stats) {
-    __syncthreads();
-    if (tid < BN) {
-      if (bnb) {
-        float a = 0.f, b = 0.f;
+      nst = 8;
+      stamp(u, 3);
+      if (stats) {
+        __syncthreads();
+        if (tid < BN) {
+          if (bnb) {
+            float a = 0.f, b = 0.f;
 #pragma unroll
-        for (int w = 0; w < WP; ++w) { a += red[(w * BN + tid) * 3 + 1]; b += red[(w * BN + tid) * 3 + 2]; }
-        p.stats[((long)tm * 2 + 0) * p.N + n0 + tid] = a;
-        p.stats[((long)tm * 2 + 1) * p.N + n0 + tid] = b;
-      } else {
-        Welford w = welford_from_shifted(64.f, red[tid * 3 + 0], red[tid * 3 + 1], red[tid * 3 + 2]);
+            for (int w = 0; w < WP; ++w) { a += red[(w * BN + tid) * 3 + 1]; b += red[(w * BN + tid) * 3 + 2]; }
+            p.stats[((long)it.tm * 2 + 0) * p.N + it.n0 + tid] = a;
+            p.stats[((long)it.tm * 2 + 1) * p.N + it.n0 + tid] = b;
+          } else {
+            Welford w = welford_from_shifted(64.f, red[tid * 3 + 0], red[tid * 3 + 1], red[tid * 3 + 2]);
 #pragma unroll
-        for (int k = 1; k < WP; ++k) {
-          const float* e = red + (k * BN + tid) * 3;
-          w = welford_merge(w, welford_from_shifted(64.f, e[0], e[1], e[2]));
+            for (int k = 1; k < WP; ++k) {
+              const float* e = red + (k * BN + tid) * 3;
+              w = welford_merge(w, welford_from_shifted(64.f, e[0], e[1], e[2]));
+            }
+            store_welford(p.stats, it.tm, p.N, it.n0 + tid, w);
+          }
         }
-        store_welford(p.stats, tm, p.N, n0 + tid, w);
+        // the scratch stage is the next item's first DMA target
+        __syncthreads();
       }
     }
-  }
-  stamp(5);
-  if (stag) {
-    __syncthreads();
-    volatile int* flag = reinterpret_cast<volatile int*>(smem + T::HALO - 32);
-    if (tid == 0) {
-      const unsigned done = __hip_atomic_fetch_add(g.cu_ctr + 2048, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      *flag = (int)(done == gridDim.x - 1);
-    }
-    __syncthreads();
-    if (*flag) {  // every workgroup has arrived: counters back to zero for the next launch
-      for (int i = tid; i <= 2048; i += NT) __hip_atomic_store(g.cu_ctr + i, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    }
+    stamp(u, 4);
+    if (!has_next) break;
+    u = un;
   }
 }
 
@@ -581,16 +635,9 @@ static int g_h3 = [] {
 }();
 void hconv3_enable(int on) { g_h3 = on; }
 static unsigned long long* g_h3_stamps = nullptr;
-static int g_h3_dbg = [] {
-  const char* e = getenv("DCNN_HCONV3_DBG");
-  return e ? atoi(e) : 0;
-}();
-static int g_h3_stagger = [] {
-  const char* e = getenv("DCNN_HCONV3_STAGGER");
-  return e ? atoi(e) : 0;
-}();
-void hconv3_set_stagger(int sleeps) { g_h3_stagger = sleeps; }
 void hconv3_set_stamps(uintptr_t p) { g_h3_stamps = reinterpret_cast<unsigned long long*>(p); }
+static int g_h3_grid_cap = 0;  // test hook: at most this many persistent workgroups (0: resident count)
+void hconv3_set_grid_cap(int n) { g_h3_grid_cap = n < 0 ? 0 : n; }
 
 struct H3Plan {
   int WC, TWC, HN, NWI, TH, TW, IMG, pitch, splits, tiles_m, tiles_n;
@@ -602,10 +649,7 @@ bool hconv3_plan(int NB, int H, int W, int Cs, int N, int ntaps, H3Plan* pl) {
   // first residual conv)
   if (!g_h3 || ntaps != 9 || (Cs % 64 && Cs != 32) || N % 64) return false;
   // 16-wide (and wider) maps: 4-wave workgroups of 64 channels x one 16x16 tile, two per CU
-  // (LDS 72 KB). The 8- and 4-wide maps stay on hconv_kernel (measured faster there: their split-K
-  // grids of single 8-wave workgroups lose more to the serial prologue / epilogue than the K loop
-  // gains).
-  // 8x8 maps (DCNN_HCONV3_8=1, experiment): 4 images of 8x8 per 256-pixel tile, halo pitch 10
+  // (LDS 72 KB). 8x8 maps (DCNN_HCONV3_8=1, experiment): 4 images of 8x8 per tile, halo pitch 10.
   static const int on8 = [] { const char* e = getenv("DCNN_HCONV3_8"); return e ? atoi(e) : 0; }();
   const bool m8 = on8 && W == 8 && H == 8 && NB % 4 == 0;
   if (!m8 && (W % 16 || H % 16)) return false;
@@ -614,7 +658,7 @@ bool hconv3_plan(int NB, int H, int W, int Cs, int N, int ntaps, H3Plan* pl) {
   const int NWI = (3 * BN / 16 + NW - 1) / NW;
   const int pitch = TW + 2;
   const int HN = (IMG * (TH + 2) * pitch + 16 * NW - 1) / (16 * NW);
-  // the instances: <4, 1, 16, 6, 3, 2, 0> (16-wide maps), <4, 1, 8, 7, 3, 2, 0> (8x8 maps)
+  // the instances: <4, 1, 16, 6, 3, 0> (16-wide maps), <4, 1, 8, 7, 3, 0> (8x8 maps)
   if (!((TWC == 16 && HN == 6) || (TWC == 8 && HN == 7)) || NWI != 3) return false;
   pl->WC = WC; pl->TWC = TWC; pl->HN = HN; pl->NWI = NWI;
   pl->TH = TH; pl->TW = TW; pl->IMG = IMG; pl->pitch = pitch;
@@ -630,15 +674,28 @@ bool hconv3_plan(int NB, int H, int W, int Cs, int N, int ntaps, H3Plan* pl) {
   return true;
 }
 
-template <int NW, int WC, int TWC, int HN, int NWI, int NWS, int PITCH, int EPI>
-static void launch_h3e(const HConvArgs& a, const H3Geo& g, int grid, hipStream_t s) {
-  using T = H3<NW, WC, TWC, HN, NWI, NWS, PITCH>;
-  auto k = hconv3_kernel<NW, WC, TWC, HN, NWI, NWS, PITCH, EPI>;
-  static bool attr = false;
-  if (!attr) {
+template <int NW, int WC, int TWC, int HN, int NWI, int PITCH, int EPI, bool STAMP>
+static void launch_h3e(const HConvArgs& a, const H3Geo& g, hipStream_t s) {
+  using T = H3<NW, WC, TWC, HN, NWI, PITCH>;
+  auto k = hconv3_kernel<NW, WC, TWC, HN, NWI, PITCH, EPI, STAMP>;
+  static int resident = 0;  // workgroups of this instance the device holds at once
+  if (!resident) {
     DCNN_HIP_CHECK(hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, T::LDS));
-    attr = true;
+    int dev = 0, cus = 0, per_cu = 0;
+    DCNN_HIP_CHECK(hipGetDevice(&dev));
+    DCNN_HIP_CHECK(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev));
+    DCNN_HIP_CHECK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, (const void*)k, NW * 64, T::LDS));
+    resident = cus * (per_cu > 0 ? per_cu : 1);
   }
+  // persistent grid: at most the resident workgroups, items spread evenly (every workgroup walks
+  // ceil or floor of nitems / grid items)
+  int grid = g.nitems < resident ? g.nitems : resident;
+  if (g_h3_grid_cap > 0 && grid > g_h3_grid_cap) grid = g_h3_grid_cap;
+  // an odd chunk count (one 32-channel chunk) would alternate the halo buffer parity from item to
+  // item; the kernel is compiled for items starting in buffer 0, so those run one item each
+  if (g.nchunk & 1) grid = g.nitems;
+  const int per = (g.nitems + grid - 1) / grid;
+  grid = (g.nitems + per - 1) / per;
   hipLaunchKernelGGL(k, dim3(grid), dim3(NW * 64), T::LDS, s, a, g);
   DCNN_LAUNCH_CHECK();
 }
@@ -648,18 +705,19 @@ static int g_h3_epi = [] {  // DCNN_HCONV3_EPI=0: always the generic epilogue (A
   return e ? atoi(e) : 1;
 }();
 
-template <int NW, int WC, int TWC, int HN, int NWI, int NWS, int PITCH>
-static void launch_h3(const HConvArgs& a, const H3Geo& g, int grid, hipStream_t s) {
+template <int NW, int WC, int TWC, int HN, int NWI, int PITCH>
+static void launch_h3(const HConvArgs& a, const H3Geo& g, hipStream_t s) {
+  if (g.stamps) return launch_h3e<NW, WC, TWC, HN, NWI, PITCH, 0, true>(a, g, s);
   const bool plain_fwd = a.stats && !a.bnb.x && !a.residual && !a.relu && !a.bias;
   const bool bnb_dgrad = a.stats && a.bnb.x && !a.relu && !a.bias;
-  if (g_h3_epi && plain_fwd) return launch_h3e<NW, WC, TWC, HN, NWI, NWS, PITCH, 1>(a, g, grid, s);
-  if (g_h3_epi && bnb_dgrad) return launch_h3e<NW, WC, TWC, HN, NWI, NWS, PITCH, 2>(a, g, grid, s);
-  launch_h3e<NW, WC, TWC, HN, NWI, NWS, PITCH, 0>(a, g, grid, s);
+  if (g_h3_epi && plain_fwd) return launch_h3e<NW, WC, TWC, HN, NWI, PITCH, 1, false>(a, g, s);
+  if (g_h3_epi && bnb_dgrad) return launch_h3e<NW, WC, TWC, HN, NWI, PITCH, 2, false>(a, g, s);
+  launch_h3e<NW, WC, TWC, HN, NWI, PITCH, 0, false>(a, g, s);
 }
 
-static void launch_h3_plan(const H3Plan& pl, const HConvArgs& a, const H3Geo& g, int grid, hipStream_t s) {
-  if (pl.WC == 1 && pl.TWC == 16 && pl.HN == 6 && pl.NWI == 3) return launch_h3<4, 1, 16, 6, 3, 2, 0>(a, g, grid, s);
-  if (pl.WC == 1 && pl.TWC == 8 && pl.HN == 7 && pl.NWI == 3) return launch_h3<4, 1, 8, 7, 3, 2, 0>(a, g, grid, s);
+static void launch_h3_plan(const H3Plan& pl, const HConvArgs& a, const H3Geo& g, hipStream_t s) {
+  if (pl.WC == 1 && pl.TWC == 16 && pl.HN == 6 && pl.NWI == 3) return launch_h3<4, 1, 16, 6, 3, 0>(a, g, s);
+  if (pl.WC == 1 && pl.TWC == 8 && pl.HN == 7 && pl.NWI == 3) return launch_h3<4, 1, 8, 7, 3, 0>(a, g, s);
   throw std::runtime_error("hconv3: no kernel instance for this plan");
 }
 
@@ -676,30 +734,18 @@ bool hconv3_try(const HConvArgs& a0, hipStream_t s) {
   }
   for (int t = 0; t < 9; ++t)
     if (g.tb[t] < 0) return false;
-  if (a0.a_bytes >= 0x80000000u || a0.b_bytes >= 0x80000000u) return false;
+  const long c_bytes = (long)a0.NB * a0.H * a0.W * a0.N * 2;
+  if (a0.a_bytes >= 0x80000000u || a0.b_bytes >= 0x80000000u || c_bytes >= 0x80000000l) return false;
   HConvArgs a = a0;
   if (a.splits != pl.splits) throw std::runtime_error("hconv3: split count mismatch (use hconv_splits)");
   if (pl.splits > 1 && (!a.part || !a.tickets)) throw std::runtime_error("hconv3: split-K workspace missing");
   g.TH = pl.TH; g.TW = pl.TW; g.IMG = pl.IMG; g.pitch = pl.pitch;
   g.tiles_n = pl.tiles_n; g.tiles_m = pl.tiles_m;
   g.nchunk = a.Cs / 32 / pl.splits;
-  g.halo_bytes = 4 * pl.HN * 1024;
+  g.nitems = pl.tiles_m * pl.tiles_n * pl.splits;
+  g.c_bytes = (unsigned)c_bytes;
   g.stamps = g_h3_stamps;
-  g.dbg = g_h3_dbg;
-  const int grid = pl.tiles_m * pl.tiles_n * pl.splits;
-  static unsigned* ctr = nullptr;
-  if (pl.splits == 1 && g_h3_stagger > 0) {
-    hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
-    DCNN_HIP_CHECK(hipStreamIsCapturing(s, &cs));
-    if (!ctr && cs == hipStreamCaptureStatusNone) {  // (never allocated inside a capture)
-      DCNN_HIP_CHECK(hipMalloc(&ctr, 2049 * sizeof(unsigned)));
-      DCNN_HIP_CHECK(hipMemset(ctr, 0, 2049 * sizeof(unsigned)));
-      DCNN_HIP_CHECK(hipDeviceSynchronize());
-    }
-    g.cu_ctr = ctr;
-    g.stagger = ctr ? g_h3_stagger : 0;
-  }
-  launch_h3_plan(pl, a, g, grid, s);
+  launch_h3_plan(pl, a, g, s);
   return true;
 }
 

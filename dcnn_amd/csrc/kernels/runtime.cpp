@@ -198,9 +198,13 @@ class Allocator {
     // (the queue holds at least nbytes) or the queue is large (>= 256 MiB / 256 buffers): the
     // reclaim synchronises the device, so small allocations next to a few small pending frees do
     // not drain every stream (other pipeline stages mid-step keep running)
-    if (deferred_bytes_ >= std::max<uint64_t>(nbytes, 1) || deferred_bytes_ >= (256ull << 20) ||
-        deferred_.size() >= 256)
-      release_deferred();
+    bool reclaim;
+    {
+      std::lock_guard<std::mutex> l(mu_);  // defer_free runs on any thread (DLPack deleters)
+      reclaim = deferred_bytes_ >= std::max<uint64_t>(nbytes, 1) || deferred_bytes_ >= (256ull << 20) ||
+                deferred_.size() >= 256;
+    }
+    if (reclaim) release_deferred();
     DeviceGuard g(dev_);
     const uint64_t before = reserved();
     void* p = nullptr;

@@ -53,7 +53,7 @@ struct Message {
   uint64_t payload_type = P_NONE;
   // job payloads
   uint64_t mb_id = 0;
-  uint8_t dtype = 0;   // 0 f32, 1 bf16, 2 f16, 3 i64, 4 u8
+  uint8_t dtype = 0;   // 0 f32, 1 bf16, 2 f16, 3 i64, 4 u8, 5 f64
   uint8_t codec = CODEC_NONE;
   std::vector<uint64_t> shape;
   std::string data;    // raw (possibly compressed) tensor bytes

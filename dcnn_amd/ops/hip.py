@@ -161,14 +161,15 @@ def _f32_concat_ok(C, Co):
 _HCONV_1X1 = os.environ.get("DCNN_HCONV_1X1", "1") != "0"
 
 
-def _hconv_ok(N, OH, OW, H, W, sh, sw, Cs, Co, taps, wop):
+def _hconv_ok(N, OH, OW, H, W, sh, sw, Cs, Co, taps, wop, split3=False):
     """Halo-tiled direct conv applies to stride-1 'same' convs with a 1-pixel reach (3x3/pad 1
-    forward and its dgrad) on 64-multiple channel counts."""
+    forward and its dgrad) on 64-multiple channel counts. ``split3``: the caller is a 3 x bf16
+    fp32 concat path (Cs = 3 x the real channels): 1x1 convs stay on the exact fp32 GEMM there."""
     if not _HCONV or (sh, sw) != (1, 1) or (OH, OW) != (H, W) or len(taps) > 9:
         return False
     if any(abs(t[0]) > 1 or abs(t[1]) > 1 for t in taps):
         return False
-    if len(taps) == 1 and not (_HCONV_1X1 and Cs >= 1024 and (N * OH * OW // 64) * (Co // 64) < 256):
+    if len(taps) == 1 and not (_HCONV_1X1 and not split3 and Cs >= 1024 and (N * OH * OW // 64) * (Co // 64) < 256):
         # 1x1: the plain GEMM is already read-once. Except K >= 1024 1x1 convs (not on the
         # streaming kernel) whose GEMM grid would be < 256 tiles: the halo kernel splits their K
         # over the channel chunks (ResNet-50 b32: 7.87k -> 7.92k img/s; DCNN_HCONV_1X1=0 = off)
@@ -253,7 +254,7 @@ def conv2d_fwd(x, w, bias, stride, pad, *, stats=False, residual=None, relu=Fals
     if residual is not None:
         assert tuple(residual.shape) == (N, Co, OH, OW) and residual.is_contiguous(memory_format=CL)
     if x.dtype == F32 and _f32_concat_ok(Ci, Co) and _hconv_ok(N, OH, OW, H, W, sh, sw, 3 * Ci, Co,
-                                                                 _fwd_taps(3 * Ci, W, KH, KW, ph, pw), w):
+                                                                 _fwd_taps(3 * Ci, W, KH, KW, ph, pw), w, True):
         # split-precision fp32 on the bf16 halo conv (see _F32_CONCAT)
         xs = act_split3(x)
         ws = split3_rows(w, Co * KH * KW, Ci, 1)
@@ -723,7 +724,7 @@ def conv2d_dgrad(dy, wt, x_shape, stride, pad, *, residual=None, bnb=None):
         dx = _empty((N, Ci, H, W), odt, dy.device, True)
     st = stream_ptr()
     if (f32 and len(classes) == 1 and not empty_class and _f32_concat_ok(Co, Ci)
-            and _hconv_ok(N, H, W, OH, OW, sh, sw, 3 * Co, Ci, classes[0][4], wt)):
+            and _hconv_ok(N, H, W, OH, OW, sh, sw, 3 * Co, Ci, classes[0][4], wt, True)):
         # split-precision fp32 dgrad on the bf16 halo conv (see _F32_CONCAT)
         dys = act_split3(dy)
         wts = split3_rows(wt, Ci * KH * KW, Co, 1)

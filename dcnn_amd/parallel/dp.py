@@ -60,23 +60,38 @@ class DataParallel:
             model.initialize()
         self.model = model
         self.pg = process_group
-        self.world = dist.get_world_size(process_group) if dist.is_initialized() else 1
-        self.rank = dist.get_rank(process_group) if dist.is_initialized() else 0
-        # bucketed all-reduce runs whenever a process group exists (also at world size 1, which
-        # exercises the RCCL + segmented-graph path on a single GPU); plain single-process
-        # training has no group and skips it
-        self.active = dist.is_initialized()
-        # gradient data plane: "torch" = torch.distributed (ProcessGroupNCCL = RCCL on ROCm, gloo on
-        # CPU), "rccl" = the framework's own RCCL communicator (parallel/rccl.py), bootstrapped over
-        # the native TCP control plane, collectives on the compute stream (captured in the graph)
+        # gradient data plane: "rccl" = the framework's own RCCL communicator (parallel/rccl.py):
+        # rank / world from the launcher's environment, the unique id over the native TCP control
+        # plane (no torch.distributed at all), bucket all-reduces on a framework comm stream forked
+        # from / joined to the compute stream with events (captured in the step graph); "torch" =
+        # torch.distributed (ProcessGroupNCCL = RCCL on ROCm, gloo on CPU). Default: "rccl" when
+        # torch.distributed is not initialised and the model is on a GPU, else "torch".
         import os
-        self.comm_backend = comm_backend or os.environ.get("DCNN_DP_BACKEND", "torch")
+        from .rccl import env_rank_world
+        want = comm_backend or os.environ.get("DCNN_DP_BACKEND")
+        if want is None:
+            want = "rccl" if (not dist.is_initialized() and model.arena.grad.is_cuda) else "torch"
+        if want not in ("torch", "rccl"):
+            raise ValueError("comm_backend must be 'torch' or 'rccl'")
+        if want == "rccl" and not model.arena.grad.is_cuda:
+            want = "torch"  # (the in-tree plane is GPU-only)
+        self.comm_backend = want
+        self.force_collectives = os.environ.get("DCNN_DP_FORCE_COLLECTIVES", "0") == "1"
+        if dist.is_initialized():
+            self.world = dist.get_world_size(process_group)
+            self.rank = dist.get_rank(process_group)
+        elif want == "rccl":
+            self.rank, self.world, _ = env_rank_world()
+        else:
+            self.rank, self.world = 0, 1
+        # bucketed all-reduce runs whenever there is more than one replica, or a process group
+        # exists / collectives are forced at world size 1 (exercises the RCCL + graph path on one
+        # GPU); plain single-process training skips it
+        self.active = dist.is_initialized() or self.world > 1 or (want == "rccl" and self.force_collectives)
         self.rccl = None
-        if self.comm_backend == "rccl" and self.active and model.arena.grad.is_cuda:
+        if want == "rccl" and self.active:
             from .rccl import RcclCommunicator
             self.rccl = RcclCommunicator(self.rank, self.world, model.arena.grad.device)
-        elif self.comm_backend not in ("torch", "rccl"):
-            raise ValueError("comm_backend must be 'torch' or 'rccl'")
         self.bucket_bytes = int(bucket_mb * 2**20)
         if grad_dtype not in ("fp32", "bf16"):
             raise ValueError("grad_dtype must be 'fp32' or 'bf16'")
@@ -84,10 +99,7 @@ class DataParallel:
         # at world size 1 a SUM all-reduce is the identity: skip the RCCL launches (the --pg
         # bench and single-GPU runs pay nothing for the group). DCNN_DP_FORCE_COLLECTIVES=1 keeps
         # them, so a one-GPU box can still exercise RCCL capture / replay (tests/test_gpu_dp.py).
-        import os
-        self.force_collectives = os.environ.get("DCNN_DP_FORCE_COLLECTIVES", "0") == "1"
         self._works: List = []
-        self._pending_unpack: List = []
         self._wire = {}          # (lo, hi) -> persistent bf16 wire buffers of that bucket
         self._comm_stream = None
         self._build_buckets()
@@ -194,7 +206,11 @@ class DataParallel:
         flat = self.model.arena.grad
         if self.rccl is not None:
             if self.grad_dtype == "fp32" or self.world == 1:
-                self.rccl.all_reduce(flat[lo:hi])  # stream-ordered: no Work object to wait on
+                # on the comm stream: forked after the bucket's last gradient kernel, joined in
+                # finish(); the remaining backward keeps the compute stream busy meanwhile
+                cs = self._cstream(flat.device)
+                with cs.fork():
+                    self.rccl.all_reduce(flat[lo:hi])
                 return
             self._reduce_bf16_gpu(lo, hi)
             return
@@ -222,12 +238,7 @@ class DataParallel:
         K = kernels()
         flat = self.model.arena.grad
         n, shard, packed, recv, red, gathered = self._wire_bufs(lo, hi, flat.device)
-        main = torch.cuda.current_stream(flat.device)
-        if self._comm_stream is None:
-            self._comm_stream = torch.cuda.Stream(device=flat.device)
-        cs = self._comm_stream
-        cs.wait_stream(main)  # fork: the bucket's gradients are complete on the compute stream
-        with torch.cuda.stream(cs):
+        with self._cstream(flat.device).fork():  # the bucket's gradients are complete on the compute stream
             st = stream_ptr(flat.device)
             K.grad_pack_bf16(flat[lo:hi].data_ptr(), packed.data_ptr(), n, 1.0, st)
             if self.rccl is not None:  # all_to_all as grouped send/recv pairs on this stream
@@ -244,7 +255,6 @@ class DataParallel:
             else:
                 dist.all_gather_into_tensor(gathered, red, group=self.pg, async_op=True).wait()
             K.grad_unpack_bf16(gathered.data_ptr(), flat[lo:hi].data_ptr(), n, st)
-        self._pending_unpack.append(cs)
 
     def _reduce_bf16_cpu(self, lo, hi):
         """Same wire format over gloo (bf16 payloads moved as int32 bit-pattern pairs)."""
@@ -259,15 +269,35 @@ class DataParallel:
         dist.all_gather_into_tensor(gathered.view(torch.int32), red.view(torch.int32), group=self.pg)
         flat[lo:hi].copy_(gathered[:n].float())
 
+    def _cstream(self, device):
+        if self._comm_stream is None:
+            from .rccl import CommStream
+            self._comm_stream = CommStream(device)
+        return self._comm_stream
+
     def finish(self):
         for w in self._works:
             w.wait()
         self._works.clear()
-        if self._pending_unpack:
-            main = torch.cuda.current_stream(self.model.arena.grad.device)
-            for cs in self._pending_unpack:
-                main.wait_stream(cs)  # join the side-stream bf16 pipelines
-            self._pending_unpack.clear()
+        if self._comm_stream is not None:
+            self._comm_stream.join()  # the compute stream (optimizer) waits for every bucket
+
+    # ---------------------------------------------------------------- host-side sync (bench / timing)
+    def barrier(self) -> None:
+        if self.rccl is not None and self.world > 1:
+            self.rccl.barrier()
+        elif dist.is_initialized():
+            dist.barrier(group=self.pg)
+
+    def max_over_ranks(self, v: float) -> float:
+        if self.world <= 1:
+            return float(v)
+        if self.rccl is not None:
+            return self.rccl.reduce_scalar(v, "max")
+        t = torch.tensor([float(v)], dtype=torch.float64,
+                         device=self.model.arena.grad.device if dist.get_backend(self.pg) == "nccl" else "cpu")
+        dist.all_reduce(t, op=dist.ReduceOp.MAX, group=self.pg)
+        return float(t.item())
 
     def allreduce_gradients(self):
         """Non-overlapped fallback: one SUM all-reduce per bucket after backward."""

@@ -40,7 +40,7 @@ from . import messages as M
 from .config import Endpoint, StageConfig
 from .faults import HEARTBEAT_TEXT
 from .partitioner import CostPartitioner, NaivePartitioner, Partitioner
-from .stage import PipelineStage, flat_state, load_flat_state
+from .stage import FULL_STATE, PipelineStage, flat_state, load_flat_state
 from .transport import MAILBOX, LocalTransport, MessageTransport, P2PTransport
 
 C = M.CommandType
@@ -363,20 +363,29 @@ class Coordinator:
                 if self._snapshot is None:
                     self.snapshot()
                 if self._replay_pending:
-                    # a recovery rolled the stages back to the last snapshot: re-train the batches
-                    # stepped since then (same order, same schedule) before this one
-                    for rfn, rxs, rys in self._replay_log:
+                    # a recovery rolled the stages (parameters, BN statistics and optimizer state)
+                    # back to the last snapshot: re-train the batches stepped since then (same
+                    # order, same schedule, same learning rate) before this one
+                    cur_lr = self.get_learning_rate()
+                    for rfn, rxs, rys, rlr in self._replay_log:
+                        if rlr != self.get_learning_rate():
+                            self.set_learning_rate(rlr)
                         rfn(rxs, rys)
                         self.update_parameters()
                         self.steps += 1
+                    if cur_lr != self.get_learning_rate():
+                        self.set_learning_rate(cur_lr)
                     self._replay_pending = False
+                lr = self.get_learning_rate()
                 loss = fn(xs, ys)
                 self.update_parameters()
                 self.steps += 1
                 if self.steps % self.snapshot_every == 0:
                     self.snapshot()
                 else:
-                    self._replay_log.append((fn, xs, ys))
+                    # clones: a loader that refills its batch buffers in place must not change
+                    # what a replay trains on
+                    self._replay_log.append((fn, [x.clone() for x in xs], [y.clone() for y in ys], lr))
                 return loss
             except PipelineError:
                 if self.recoveries >= self.max_recoveries:
@@ -388,12 +397,14 @@ class Coordinator:
         """Survive stage failures: snapshot every stage's parameters + BN statistics every
         ``snapshot_every`` steps; on a failed step (stage error, missed heartbeats, lost
         connection, timeout) re-deploy every stage, reload the last snapshot and retry the batch,
-        at most ``max_recoveries`` times. Optimizer moments restart from zero on recovery."""
+        at most ``max_recoveries`` times. The snapshot holds each stage's optimizer state too
+        (Adam moments and step counter, SGD momentum, the learning rate in effect), so a replay
+        neither double-counts nor drops an update."""
         self.snapshot_every = max(1, int(snapshot_every))
         self.max_recoveries = int(max_recoveries)
 
     def snapshot(self) -> None:
-        self._snapshot = self.collect_parameters()
+        self._snapshot = self.collect_parameters(full=True)
         self._snapshot_step = self.steps
         self._replay_log = []  # (schedule fn, micro-batches x, y) of every step after the snapshot
         self._replay_pending = False
@@ -409,9 +420,10 @@ class Coordinator:
         self.deploy_stages()
         if self._snapshot is not None:
             for i, flat in enumerate(self._snapshot):
-                self.comm.send(M.job_message(self.stage_names[i], C.LOAD_PARAMS, 0, flat))
+                self.comm.send(M.job_message(self.stage_names[i], C.LOAD_PARAMS, FULL_STATE, flat))
             self.join(C.PARAMS_LOADED, self.num_stages)
             self.steps = self._snapshot_step
+            self._lr_dirty = True  # the next update re-broadcasts the coordinator's learning rate
             self._replay_pending = bool(self._replay_log)
         self.start()
 
@@ -458,10 +470,11 @@ class Coordinator:
         self._lr_dirty = True
 
     # ------------------------------------------------------------------ parameters / checkpoints
-    def collect_parameters(self) -> List[torch.Tensor]:
-        """SEND_PARAMS -> PARAMS_TRANSFER: flat fp32 state per stage (params + BN stats)."""
+    def collect_parameters(self, full: bool = False) -> List[torch.Tensor]:
+        """SEND_PARAMS -> PARAMS_TRANSFER: flat fp32 state per stage (params + BN stats); with
+        ``full`` the fp64 parameter + optimizer state (stage.pack_full_state)."""
         for s in self.stage_names:
-            self.comm.send(M.Message(s, C.SEND_PARAMS))
+            self.comm.send(M.text_message(s, C.SEND_PARAMS, "full") if full else M.Message(s, C.SEND_PARAMS))
         got = {m.sender: M.message_tensor(m) for m in self.join(C.PARAMS_TRANSFER, self.num_stages)}
         return [got[self._sender_key(i)] for i in range(self.num_stages)]
 

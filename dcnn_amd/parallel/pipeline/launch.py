@@ -7,9 +7,12 @@
 Rank r hosts stage r on GPU r (pipeline neighbours are direct xGMI peers); rank 0 also runs
 the coordinator (loss, micro-batch schedule) on its main thread while its stage runs on a
 worker thread.  The control plane is the native TCP communicator on 127.0.0.1
-(``--base-port`` + rank); activations and gradients move GPU-to-GPU with RCCL
-``isend``/``irecv`` on dedicated forward/backward process groups (``transport="p2p"``), or
-inline through TCP with ``--transport message``.  On the CPU the same code runs over gloo.
+(``--base-port`` + rank); activations and gradients move GPU-to-GPU over RCCL
+(``transport="p2p"``) or inline through TCP (``--transport message``).  On GPUs the P2P plane is
+the framework's own (``--p2p rccl``, default: parallel/rccl.py ``RcclP2P``, one communicator and
+one HIP stream per direction, bootstrapped over the native TCP plane — no torch.distributed);
+``--p2p torch`` uses torch.distributed isend/irecv on four process groups instead. On the CPU the
+same code runs over gloo. Schedules: ``sync`` (GPipe), ``semi_async``, ``1f1b``.
 """
 from __future__ import annotations
 
@@ -27,7 +30,9 @@ def run(argv=None) -> dict:
     ap.add_argument("--model", default="resnet50_tiny_imagenet")
     ap.add_argument("--batch", type=int, default=256)
     ap.add_argument("--microbatches", type=int, default=8)
-    ap.add_argument("--schedule", default="semi_async", choices=["semi_async", "sync"])
+    ap.add_argument("--schedule", default="semi_async", choices=["semi_async", "sync", "1f1b"])
+    ap.add_argument("--p2p", default=os.environ.get("DCNN_P2P_BACKEND", "rccl"), choices=["rccl", "torch"],
+                    help="GPU data plane: the in-tree RCCL plane (no c10d) or torch.distributed groups")
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=2)
     ap.add_argument("--transport", default="p2p", choices=["p2p", "message"])
@@ -50,15 +55,22 @@ def run(argv=None) -> dict:
     world = int(os.environ.get("WORLD_SIZE", "1"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     use_gpu = torch.cuda.is_available() and not a.cpu
-    backend = "nccl" if use_gpu else "gloo"
-    if use_gpu:
+    in_tree = use_gpu and a.p2p == "rccl"
+    if in_tree:
+        from ..rccl import RcclP2P
         torch.cuda.set_device(local)
-        dist.init_process_group(backend, device_id=torch.device("cuda", local))
+        groups = RcclP2P(rank, world, torch.device("cuda", local))
+        barrier = groups.barrier
     else:
-        dist.init_process_group(backend)
-    groups = make_groups()
+        if use_gpu:
+            torch.cuda.set_device(local)
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        else:
+            dist.init_process_group("gloo")
+        groups = make_groups()
+        barrier = dist.barrier
     worker = NetworkStageWorker(a.base_port + rank, host="127.0.0.1", p2p_groups=groups, verbose=True)
-    dist.barrier()  # every stage listens before the coordinator dials
+    barrier()  # every stage listens before the coordinator dials
     result = {}
     if rank == 0:
         worker.start_thread()
@@ -93,7 +105,7 @@ def run(argv=None) -> dict:
         dt = time.perf_counter() - t0
         result = {"metric": f"pipeline images/sec {a.model}", "value": round(a.batch * a.steps / dt, 1),
                   "unit": "images/sec", "stages": world, "microbatches": a.microbatches,
-                  "schedule": a.schedule, "transport": a.transport, "ms_per_step": round(dt / a.steps * 1e3, 3),
+                  "schedule": a.schedule, "transport": a.transport, "p2p": "rccl" if in_tree else "torch", "ms_per_step": round(dt / a.steps * 1e3, 3),
                   "partitions": [(p.start_layer, p.end_layer) for p in coord.partitions], "loss": round(loss, 4)}
         print(json.dumps(result), flush=True)
         coord.stop()
@@ -106,8 +118,11 @@ def run(argv=None) -> dict:
     allocs = sum(getattr(getattr(o, "transport", None), "slot_allocs", 0)
                  for o in ([coord] if rank == 0 else []) + [getattr(worker, "stage", None)])
     print(json.dumps({"rank": rank, "slot_allocs": allocs, "steps": a.warmup + a.steps}), flush=True)
-    dist.barrier()
-    dist.destroy_process_group()
+    barrier()
+    if in_tree:
+        groups.close()
+    else:
+        dist.destroy_process_group()
     return result
 
 

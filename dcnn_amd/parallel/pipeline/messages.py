@@ -28,9 +28,9 @@ CommandType = enum.IntEnum("CommandType", {k: v for k, v in sorted(native().comm
 P_NONE, P_JOB, P_STRING, P_BOOL, P_LOAD, P_TYPED_JOB = range(6)
 CODECS = {"none": 0, "zlib": 1, "zstd": 2}
 
-_DT = {torch.float32: 0, torch.bfloat16: 1, torch.float16: 2, torch.int64: 3, torch.uint8: 4}
+_DT = {torch.float32: 0, torch.bfloat16: 1, torch.float16: 2, torch.int64: 3, torch.uint8: 4, torch.float64: 5}
 _DT_INV = {v: k for k, v in _DT.items()}
-_NP = {0: np.float32, 1: np.uint16, 2: np.float16, 3: np.int64, 4: np.uint8}
+_NP = {0: np.float32, 1: np.uint16, 2: np.float16, 3: np.int64, 4: np.uint8, 5: np.float64}
 CL_FLAG = 0x10  # dtype bit: payload is the NHWC physical buffer of a channels_last NCHW tensor
 
 

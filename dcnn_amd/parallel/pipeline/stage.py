@@ -68,6 +68,56 @@ def load_flat_state(model: Sequential, flat: torch.Tensor) -> None:
         model.arena.sync_shadow(force=True)
 
 
+def flat_optimizer_state(opt) -> torch.Tensor:
+    """Optimizer state as one fp64 vector: [learning rate, step counter t, then every state
+    tensor of ``state_dict()`` in key order] (Adam: m, v; SGD with momentum: velocity)."""
+    d = opt.state_dict() if opt is not None else {}
+    parts = [torch.tensor([float(opt.get_learning_rate()) if opt is not None else 0.0, float(d.get("t", 0))],
+                          dtype=torch.float64)]
+    for k in sorted(d):
+        if isinstance(d[k], list):
+            parts += [x.detach().reshape(-1).double().cpu() for x in d[k]]
+    return torch.cat(parts)
+
+
+def load_flat_optimizer_state(opt, flat: torch.Tensor) -> None:
+    """Inverse of :func:`flat_optimizer_state` (the optimizer must already be attached)."""
+    flat = flat.reshape(-1).double().cpu()
+    d = opt.state_dict()
+    off = 2
+    out = {"t": int(flat[1].item())}
+    for k in sorted(d):
+        if isinstance(d[k], list):
+            lst = []
+            for x in d[k]:
+                n = x.numel()
+                lst.append(flat[off:off + n].view(x.shape).to(x.dtype))
+                off += n
+            out[k] = lst
+    if off != flat.numel():
+        raise RuntimeError(f"optimizer state size mismatch: consumed {off} of {flat.numel()}")
+    opt.load_state_dict(out)
+    opt.set_learning_rate(float(flat[0].item()))
+
+
+# SEND_PARAMS / LOAD_PARAMS with micro-batch id FULL_STATE carry the optimizer state too: the
+# parameter vector (fp32, flat_state) is followed by flat_optimizer_state widened into the same
+# fp64 message, headed by the parameter count
+FULL_STATE = 1
+
+
+def pack_full_state(model, opt) -> torch.Tensor:
+    fp = flat_state(model).double()
+    return torch.cat([torch.tensor([float(fp.numel())], dtype=torch.float64), fp, flat_optimizer_state(opt)])
+
+
+def unpack_full_state(model, opt, flat: torch.Tensor) -> None:
+    flat = flat.reshape(-1).double()
+    n = int(flat[0].item())
+    load_flat_state(model, flat[1:1 + n].float())
+    load_flat_optimizer_state(opt, flat[1 + n:])
+
+
 class PipelineStage:
     def __init__(self, communicator, p2p_groups=None, verbose: bool = False):
         self.comm = communicator
@@ -180,9 +230,16 @@ class PipelineStage:
                 self._configure(msg.text.decode())
             elif cmd == C.SEND_PARAMS:
                 self._wait_peer("coordinator")
-                self.comm.send(M.job_message("coordinator", C.PARAMS_TRANSFER, 0, flat_state(self.model)))
+                if msg.payload_type == M.P_STRING and msg.text.decode() == "full":
+                    self.comm.send(M.job_message("coordinator", C.PARAMS_TRANSFER, FULL_STATE,
+                                                 pack_full_state(self.model, self.optimizer)))
+                else:
+                    self.comm.send(M.job_message("coordinator", C.PARAMS_TRANSFER, 0, flat_state(self.model)))
             elif cmd in (C.LOAD_PARAMS, C.PARAMS_TRANSFER):
-                load_flat_state(self.model, M.message_tensor(msg))
+                if msg.payload_type in (M.P_JOB, M.P_TYPED_JOB) and int(msg.mb_id) == FULL_STATE:
+                    unpack_full_state(self.model, self.optimizer, M.message_tensor(msg))
+                else:
+                    load_flat_state(self.model, M.message_tensor(msg))
                 self._reply(C.PARAMS_LOADED)
             elif cmd == C.STATUS_REQUEST:
                 self._reply(C.STATUS_RESPONSE, json.dumps(self.status()))

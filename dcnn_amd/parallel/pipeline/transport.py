@@ -135,17 +135,21 @@ class LocalTransport(Transport):
 
 class P2PTransport(Transport):
     """Point-to-point data plane between ranks: torch.distributed isend/irecv (RCCL on GPU, gloo
-    on CPU), or the framework's own RCCL communicator (``rccl=``, parallel/rccl.py: ncclSend /
-    ncclRecv enqueued on the current stream, no side stream, no Work objects).
+    on CPU), or the framework's own RCCL plane (``rccl=`` a :class:`parallel.rccl.RcclP2P`: one
+    communicator and one HIP stream per direction — forward, backward, and the coordinator's two —
+    forked from / joined to the compute stream with events, no Work objects).
 
     Receive buffers are persistent slots keyed by (peer, command, micro-batch, shape, dtype): a
     steady-state step allocates nothing (the previous step's tensor in that slot is dead by then —
     a stage consumes a micro-batch's activation / gradient within the step)."""
 
-    def __init__(self, my_id: str, ranks: Dict[str, int], groups: Dict[str, object], resolve=None, rccl=None):
+    def __init__(self, my_id: str, ranks: Dict[str, int], groups, resolve=None, rccl=None):
+        from ..rccl import RcclP2P
+        if rccl is None and isinstance(groups, RcclP2P):  # the launcher hands the in-tree plane over
+            rccl, groups = groups, None
         self.my_id = my_id
         self.ranks = dict(ranks)          # logical name / comm id -> rank
-        self.groups = groups              # {"fwd", "bwd", "cfwd", "cbwd"}
+        self.groups = groups              # torch process groups {"fwd", "bwd", "cfwd", "cbwd"}
         self.rank = dist.get_rank() if rccl is None else rccl.rank
         self.local = LocalTransport(my_id, resolve)
         self.rccl = rccl
@@ -153,11 +157,14 @@ class P2PTransport(Transport):
         self._slots: Dict = {}
         self.slot_allocs = 0              # receive buffers ever allocated (tests: flat after step 1)
 
-    def _group(self, command, peer_name):
+    def _key(self, command, peer_name):
         coord = "coordinator" in (peer_name, self.my_id)
         if int(command) == M.CommandType.FORWARD_JOB:
-            return self.groups["cfwd" if coord else "fwd"]
-        return self.groups["cbwd" if coord else "bwd"]
+            return "cfwd" if coord else "fwd"
+        return "cbwd" if coord else "bwd"
+
+    def _group(self, command, peer_name):
+        return self.groups[self._key(command, peer_name)]
 
     def _prune(self):
         while self._pending and self._pending[0][0].is_completed():
@@ -173,9 +180,7 @@ class P2PTransport(Transport):
             if not phys.is_contiguous():
                 phys = phys.contiguous()
             if self.rccl is not None:
-                self.rccl.send(phys, dst)  # stream-ordered; the caching allocator keeps phys alive
-                if phys.is_cuda:
-                    phys.record_stream(torch.cuda.current_stream(phys.device))
+                self.rccl.send(self._key(command, recipient), phys, dst)  # direction stream; phys kept alive
             else:
                 w = dist.isend(phys, dst, group=self._group(command, recipient))
                 self._pending.append((w, phys))
@@ -200,7 +205,7 @@ class P2PTransport(Transport):
         dev = torch.device(device) if device is not None else torch.device("cpu")
         phys, logical = self._slot(msg, src, dev)
         if self.rccl is not None:
-            self.rccl.recv(phys, src)
+            self.rccl.recv(self._key(msg.command, src_name), phys, src)
         else:
             dist.irecv(phys, src, group=self._group(msg.command, src_name)).wait()
         return logical

@@ -6,8 +6,8 @@ Instead of a tracing compiler the whole per-step launch sequence (input layout c
 
 Data-parallel steps are captured WHOLE: the bucket collectives that
 :class:`~dcnn_amd.parallel.dp.DataParallel` fires from inside the backward pass are RCCL
-kernels on the process group's internal stream, forked from the capturing stream at each fire
-point and joined back before the optimizer, so one replay runs forward, backward, every
+kernels on the framework's comm stream (or the process group's internal stream), forked from the
+capturing stream at each fire point and joined back before the optimizer, so one replay runs forward, backward, every
 overlapped all-reduce and the update with no host involvement. ``DCNN_DP_CAPTURE=0`` selects
 the older *segmented* capture instead: one graph per backward segment between fire points, the
 host enqueuing each bucket's asynchronous all-reduce between two segment replays.
@@ -161,7 +161,10 @@ class TrainStep:
             if self.dp.world > 1:
                 flag = torch.tensor([0 if err is not None else 1], dtype=torch.int32,
                                     device=self.model.device.torch_device)
-                dist.all_reduce(flag, op=dist.ReduceOp.MIN, group=self.dp.pg)
+                if self.dp.rccl is not None:
+                    self.dp.rccl.all_reduce(flag, "min")
+                else:
+                    dist.all_reduce(flag, op=dist.ReduceOp.MIN, group=self.dp.pg)
                 if int(flag.item()) == 0 and err is None:
                     err = RuntimeError("another rank's capture failed")
             if err is None:
@@ -170,7 +173,8 @@ class TrainStep:
             warnings.warn(f"capturing the bucket collectives into the step graph failed ({err}); "
                           "falling back to the segmented capture")
             self.dp._works.clear()
-            self.dp._pending_unpack.clear()
+            if self.dp._comm_stream is not None:
+                self.dp._comm_stream.forked = False
             if t0 is not None:
                 self.opt.t = t0
             self.graphs, self._whole = None, False

@@ -43,3 +43,12 @@ def test_1x1_only_k1024_small_grid(stub):
 def test_1x1_switch_off(stub, monkeypatch):
     monkeypatch.setattr(hip, "_HCONV_1X1", False)
     assert not hip._hconv_ok(32, 8, 8, 8, 8, 1, 1, 1024, 256, TAP1, None)
+
+
+def test_1x1_split3_concat_stays_exact(stub):
+    # fp32 concat callers pass Cs = 3 x Ci: a 384-channel fp32 1x1 conv (Cs = 1152) must not
+    # leave the exact fp32 GEMM for the 3 x bf16 halo kernel (the K >= 1024 rule is bf16-only)
+    assert not hip._hconv_ok(32, 8, 8, 8, 8, 1, 1, 3 * 384, 256, TAP1, None, True)
+    assert not hip._hconv_ok(32, 4, 4, 4, 4, 1, 1, 3 * 2048, 512, TAP1, None, True)
+    # 3x3 convs still take the split-precision halo path
+    assert hip._hconv_ok(256, 32, 32, 32, 32, 1, 1, 3 * 64, 64, TAPS9, None, True)

@@ -1,5 +1,5 @@
-"""Third-generation halo conv (csrc/kernels/hconv3.hip): 64x64-per-wave tiles, 3 taps per barrier,
-weights as the MFMA A operand, epilogue from registers. Checked against a plain PyTorch fp32 reference of
+"""Third-generation halo conv (csrc/kernels/hconv3.hip): persistent, cross-tile pipelined; 64x64-per-wave
+tiles, 3 taps per barrier, weights as the MFMA A operand (permuted rows: 16-byte epilogue stores). Checked against a plain PyTorch fp32 reference of
 the same op and against the previous-generation kernel (hconv3_enable(0)) on every ResNet layer
 geometry, with every epilogue option (bias, residual, ReLU, forward BN statistics, backward-BN
 fusion) and split-K."""
@@ -146,3 +146,59 @@ def test_hconv3_split_k_matches_unsplit(hip):
     assert rel_err(y1, y0) < 5e-3 and rel_err(s1, s0) < 1e-3
     ref = F.relu(F.conv2d(x.float().cpu(), w.float().cpu(), b.cpu(), 1, 1))
     assert rel_err(y1, ref) < 1e-2
+
+
+@pytest.fixture
+def grid_cap(hip):
+    K = hip.kernels()
+    yield K
+    K.hconv3_set_grid_cap(0)
+
+
+@pytest.mark.parametrize("cap", [1, 3, 7])
+@pytest.mark.parametrize("case", [(4, 64, 32, 32, 64), (4, 128, 16, 16, 128), (2, 256, 16, 16, 256),
+                                  (4, 512, 16, 16, 128), (4, 32, 32, 32, 64)])
+def test_hconv3_persistent_items_match(hip, grid_cap, case, cap):
+    """Few workgroups walking many items (cross-item halo / weight prefetch, the next item's W(0,1)
+    issued before the epilogue stores, split-K items in the stream): bit-identical to one item per
+    workgroup, for the forward with every epilogue option and the dgrad with the BN fusion."""
+    K = grid_cap
+    N, C, H, W, Co = case
+    torch.manual_seed(35)
+    x = torch.randn(N, C, H, W).cuda().bfloat16().contiguous(memory_format=CL)
+    w = (torch.randn(Co, C, 3, 3) / math.sqrt(9 * C)).cuda().bfloat16().contiguous(memory_format=CL)
+    b = torch.randn(Co).cuda() * 0.1 + 1.0
+    r = torch.randn(N, Co, H, W).cuda().bfloat16().contiguous(memory_format=CL)
+
+    def fwd():
+        y, part = hip.conv2d_fwd(x, w, b, (1, 1), (1, 1), stats=True, residual=r, relu=True)
+        y1, part1 = hip.conv2d_fwd(x, w, None, (1, 1), (1, 1), stats=True)  # EPI=1 instance
+        return y.clone(), hip.bn_stats(y, part).clone(), y1.clone(), hip.bn_stats(y1, part1).clone()
+
+    K.hconv3_set_grid_cap(0)
+    ref = fwd()
+    K.hconv3_set_grid_cap(cap)
+    got = fwd()
+    for a_, b_ in zip(got, ref):
+        assert torch.equal(a_, b_)
+    if not K.hconv_v3(N, H, W, Co, C, 9) or C % 64:
+        return
+    # dgrad + backward-BN fusion (EPI=2 instance)
+    xb = (torch.randn(N, C, H, W) * 1.5 + 0.3).cuda().bfloat16().contiguous(memory_format=CL)
+    sums = hip.bn_stats(xb)
+    mean, istd = torch.empty(C, device="cuda"), torch.empty(C, device="cuda")
+    g_, bt = (torch.rand(C) + 0.5).cuda(), torch.randn(C).cuda()
+    y = hip.bn_apply(xb, sums, N * H * W, g_, bt, 1e-5, relu=True, save=(mean, istd))
+    wt = hip.conv_weight_t(w)
+    dy = torch.randn(N, Co, H, W).cuda().bfloat16().contiguous(memory_format=CL)
+    req = hip.BnbRequest("bn", y, xb, mean, istd)
+
+    def dgrad():
+        d = hip.conv2d_dgrad(dy, wt, (N, C, H, W), (1, 1), (1, 1), bnb=req)
+        return d.clone(), d._bnb[1].clone()
+
+    K.hconv3_set_grid_cap(0)
+    d0, s0 = dgrad()
+    K.hconv3_set_grid_cap(cap)
+    d1, s1 = dgrad()
+    assert torch.equal(d0, d1) and torch.equal(s0, s1)

@@ -153,10 +153,11 @@ def test_stage_error_is_reported():
         coord.stop()
 
 
-@pytest.mark.parametrize("transport,schedule", [("p2p", "semi_async"), ("message", "sync")])
+@pytest.mark.parametrize("transport,schedule", [("p2p", "semi_async"), ("p2p", "1f1b"), ("message", "sync")])
 def test_multiprocess_pipeline_gloo(transport, schedule):
-    """3 processes (coordinator co-located with stage 0) over TCP control + gloo P2P data."""
-    port = 29800 + (0 if transport == "p2p" else 40)
+    """3 processes (coordinator co-located with stage 0) over TCP control + gloo P2P data; the
+    separate forward / backward groups carry 1F1B's interleaved traffic without blocking."""
+    port = 29800 + {"semi_async": 0, "1f1b": 20, "sync": 40}[schedule]
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "3",
            "--master-addr", "127.0.0.1", "--master-port", str(port - 100),
            "-m", "dcnn_amd.parallel.pipeline.launch", "--model", "mnist_cnn", "--batch", "8",

@@ -6,7 +6,7 @@ import pytest
 import torch
 
 from dcnn_amd.models import zoo
-from dcnn_amd.nn.optimizers import SGD
+from dcnn_amd.nn.optimizers import SGD, Adam
 from dcnn_amd.parallel.pipeline import FlopPartitioner, InProcessCoordinator
 from dcnn_amd.parallel.pipeline.coordinator import PipelineError, StageFailure
 from dcnn_amd.parallel.pipeline.faults import FaultInjector, FaultSpec, env_faults
@@ -15,11 +15,11 @@ from dcnn_amd.parallel.pipeline import messages as M
 C = M.CommandType
 
 
-def _coord(faults=None, **kw):
+def _coord(faults=None, opt=None, **kw):
     model = zoo.create_model("mnist_cnn")
     model.set_seed(5)
     model.initialize()
-    coord = InProcessCoordinator(model, SGD(0.05), "softmax_crossentropy", num_stages=2, num_microbatches=2,
+    coord = InProcessCoordinator(model, opt if opt is not None else SGD(0.05), "softmax_crossentropy", num_stages=2, num_microbatches=2,
                                  partitioner=FlopPartitioner([2, 1, 28, 28]), **kw)
     coord.initialize()
     for i, f in (faults or {}).items():
@@ -141,5 +141,54 @@ def test_recovery_replays_steps_since_an_older_snapshot():
         assert losses == pytest.approx(ref_losses, rel=1e-6)
         for a, b in zip(coord.gather_model().parameters(), ref_params):
             torch.testing.assert_close(a, b, rtol=1e-6, atol=1e-7)
+    finally:
+        coord.stop()
+
+
+@pytest.mark.parametrize("make_opt", [lambda: Adam(1e-3), lambda: SGD(0.05, momentum=0.9)], ids=["adam", "sgd_momentum"])
+def test_recovery_replay_restores_optimizer_state(make_opt):
+    """Stateful optimizers: the snapshot carries Adam's moments + step counter (SGD's velocity),
+    so replaying step 3 after a crash in step 4 neither double-counts an update on the surviving
+    stage nor restarts the restarted stage's moments; a learning-rate change between logged steps
+    is replayed too. Final parameters equal an uninterrupted run."""
+    data = _batches(4)
+    lrs = [None, None, 0.5, None]  # scale the LR before step 3 (a scheduler would)
+
+    def run(coord):
+        out = []
+        for (x, y), f in zip(data, lrs):
+            if f is not None:
+                coord.set_learning_rate(coord.get_learning_rate() * f)
+            out.append(coord.train_step(x, y, "sync"))
+        return out
+
+    ref = _coord(opt=make_opt())
+    try:
+        ref_losses = run(ref)
+        ref_params = [p.clone() for p in ref.gather_model().parameters()]
+    finally:
+        ref.stop()
+    xs_seen = []
+    coord = _coord({1: ["FORWARD_JOB:7:crash"]}, opt=make_opt(), heartbeat_s=0.2, heartbeat_misses=3, timeout_s=60.0)
+    coord.enable_recovery(snapshot_every=2, max_recoveries=2)
+    try:
+        losses = run(coord)
+        assert coord.recoveries == 1 and coord.steps == 4
+        assert losses == pytest.approx(ref_losses, rel=1e-5)
+        for a, b in zip(coord.gather_model().parameters(), ref_params):
+            torch.testing.assert_close(a, b, rtol=1e-5, atol=1e-6)
+    finally:
+        coord.stop()
+
+
+def test_replay_log_clones_micro_batches():
+    coord = _coord()
+    coord.enable_recovery(snapshot_every=3, max_recoveries=1)
+    try:
+        (x, y), = _batches(1)
+        coord.train_step(x, y, "sync")
+        logged = coord._replay_log[-1][1][0].clone()
+        x.fill_(7.0)  # a loader refilling its buffer in place
+        torch.testing.assert_close(coord._replay_log[-1][1][0], logged)
     finally:
         coord.stop()
