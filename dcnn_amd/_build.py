@@ -129,7 +129,7 @@ def build_native(force=False, verbose=False, max_workers=None):
 
 # kernel-library / native objects the C++ host API links (the pybind layers stay out)
 _HOST_SKIP_KERNELS = {"bindings", "runtime", "rccl"}
-_HOST_NATIVE = ("cpu_ops", "cpu_gemm", "threadpool")
+_HOST_NATIVE = ("cpu_ops", "cpu_gemm", "threadpool", "jpeg")
 
 
 def build_host(force=False, verbose=False, max_workers=None):

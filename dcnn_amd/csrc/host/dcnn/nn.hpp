@@ -54,7 +54,13 @@ class Layer {
   virtual Tensor forward(const Tensor& x, bool training) = 0;
   virtual Tensor backward(const Tensor& dy) = 0;
   // refresh the bf16 operand shadows from the fp32 masters (after loading weights)
-  void sync_shadow();
+  virtual void sync_shadow();
+  // this layer's parameters, then those of its sub-layers (ResidualBlock), in checkpoint order
+  virtual void collect_params(std::vector<Param*>& out) {
+    for (auto& p : params_) out.push_back(&p);
+  }
+  // this layer and, depth-first, every sub-layer (BatchNorm statistics sidecar order)
+  virtual void collect_layers(std::vector<Layer*>& out) { out.push_back(this); }
   std::vector<Param>& params() { return params_; }
   const std::string& name() const { return name_; }
   Device device() const { return dev_; }
@@ -120,6 +126,8 @@ class BatchNorm : public Layer {
   Tensor x_, mean_, istd_;
 };
 
+// activation kinds: relu, leaky_relu (0.01), elu (alpha 1), sigmoid, tanh, linear, softmax (over the
+// channels of every pixel)
 class Activation : public Layer {
  public:
   explicit Activation(std::string kind = "relu", std::string name = "activation");
@@ -132,7 +140,45 @@ class Activation : public Layer {
  private:
   std::string kind_;
   int code_;
-  Tensor x_;
+  Tensor x_, y_;
+};
+
+// GroupNorm over G channel groups per image; gamma / beta per channel
+// (reference include/nn/layers_impl/groupnorm_layer.tpp:21-321)
+class GroupNorm : public Layer {
+ public:
+  GroupNorm(int num_groups, int num_channels, float eps = 1e-5f, bool affine = true, std::string name = "groupnorm");
+  std::string type() const override { return "groupnorm"; }
+  json::Value parameters_config() const override;
+  std::vector<int64_t> output_shape(const std::vector<int64_t>& in) const override { return in; }
+  void build(const std::vector<int64_t>& in, Device dev, uint64_t seed) override;
+  Tensor forward(const Tensor& x, bool training) override;
+  Tensor backward(const Tensor& dy) override;
+
+ private:
+  int g_, c_;
+  float eps_;
+  bool affine_;
+  bool gb_identity_ = false;
+  Tensor x_, mean_, istd_, ident_, scratch_;
+};
+
+// inverted dropout (scale 1 / (1 - p)), identity in eval; the mask is a counter-based function
+// of (seed, element), regenerated in backward (reference include/nn/layers_impl/dropout_layer.tpp)
+class Dropout : public Layer {
+ public:
+  explicit Dropout(float rate = 0.5f, std::string name = "dropout");
+  std::string type() const override { return "dropout"; }
+  json::Value parameters_config() const override;
+  std::vector<int64_t> output_shape(const std::vector<int64_t>& in) const override { return in; }
+  void build(const std::vector<int64_t>& in, Device dev, uint64_t seed) override;
+  Tensor forward(const Tensor& x, bool training) override;
+  Tensor backward(const Tensor& dy) override;
+
+ private:
+  float p_;
+  uint64_t seed_ = 0, draw_ = 0, cur_ = 0;
+  bool active_ = false;
 };
 
 class Pool2D : public Layer {
@@ -165,6 +211,32 @@ class Flatten : public Layer {
   std::vector<int64_t> in_shape_;
 };
 
+// out = act(F(x) + S(x)): F the main path, S the projection shortcut (identity when empty).
+// Backward sums the main and shortcut input gradients. Config: sub-layer records as JSON strings
+// ("main_path", "shortcut_path"), as the Python front end and the reference write them
+// (include/nn/blocks_impl/residual_block.hpp:30-476).
+class ResidualBlock : public Layer {
+ public:
+  ResidualBlock(std::vector<std::unique_ptr<Layer>> main, std::vector<std::unique_ptr<Layer>> shortcut,
+                std::string activation = "relu", std::string name = "residual_block");
+  std::string type() const override { return "residual_block"; }
+  json::Value parameters_config() const override;
+  std::vector<int64_t> output_shape(const std::vector<int64_t>& in) const override;
+  void build(const std::vector<int64_t>& in, Device dev, uint64_t seed) override;
+  Tensor forward(const Tensor& x, bool training) override;
+  Tensor backward(const Tensor& dy) override;
+  void sync_shadow() override;
+  void collect_params(std::vector<Param*>& out) override;
+  void collect_layers(std::vector<Layer*>& out) override;
+  const std::vector<std::unique_ptr<Layer>>& main_path() const { return main_; }
+  const std::vector<std::unique_ptr<Layer>>& shortcut_path() const { return short_; }
+
+ private:
+  std::vector<std::unique_ptr<Layer>> main_, short_;
+  std::string act_;
+  Tensor y_;
+};
+
 // layer from its JSON record {"type", "name", "parameters"} (the LayerFactory of the formats)
 std::unique_ptr<Layer> create_layer(const json::Value& rec);
 
@@ -184,6 +256,8 @@ class Sequential {
   Tensor forward(const Tensor& x);
   void backward(const Tensor& dlogits);
   std::vector<Param*> parameters();
+  // every BatchNorm, depth-first through residual blocks (the .bnstats record order)
+  std::vector<BatchNorm*> batchnorms();
   void zero_grad();
   size_t num_parameters();
   const std::vector<std::unique_ptr<Layer>>& layers() const { return layers_; }
@@ -224,6 +298,17 @@ class SequentialBuilder {
                                const std::string& name = "");
   SequentialBuilder& flatten(const std::string& name = "");
   SequentialBuilder& dense(int out_features, bool bias = true, const std::string& name = "");
+  SequentialBuilder& groupnorm(int num_groups, float eps = 1e-5f, bool affine = true, const std::string& name = "");
+  SequentialBuilder& dropout(float rate, const std::string& name = "");
+  // generic residual block from prebuilt paths (shapes must agree)
+  SequentialBuilder& residual(std::vector<std::unique_ptr<Layer>> main, std::vector<std::unique_ptr<Layer>> shortcut,
+                              const std::string& activation = "relu", const std::string& name = "");
+  // 3x3-BN-ReLU-3x3-BN (+ 1x1-BN projection when the stride or width changes), ReLU after the add
+  // (reference include/nn/sequential.hpp:1253)
+  SequentialBuilder& basic_residual_block(int in_ch, int out_ch, int stride = 1, const std::string& name = "");
+  // 1x1-BN-ReLU-3x3(stride)-BN-ReLU-1x1-BN, BN eps 1e-3 (reference include/nn/sequential.hpp:1288)
+  SequentialBuilder& bottleneck_residual_block(int in_ch, int mid_ch, int out_ch, int stride = 1,
+                                               const std::string& name = "");
   Sequential build();
 
  private:

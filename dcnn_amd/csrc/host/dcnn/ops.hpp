@@ -32,6 +32,22 @@ void avgpool_bwd(const float* dy, float* dx, const PoolShape& p);
 void act_fwd(int kind, const float* x, float* y, long n, float alpha);
 void act_bwd(int kind, const float* x, const float* dy, float* dx, long n, float alpha);
 double softmax_ce(const float* pred, const int64_t* labels, float* grad, long N, long C, long* correct);
+// the six losses (kind: 0 ce, 1 softmax ce, 2 log-softmax ce, 3 mse, 4 mae, 5 huber); target
+// [N][C] fp32 or null (then `labels` are one-hot targets)
+double loss(int kind, const float* pred, const float* target, const int64_t* labels, float* grad, long N, long C,
+            float param, long* correct);
+void groupnorm_fwd(const float* x, float* y, long N, long C, long HW, long G, const float* g, const float* b, float eps,
+                   float* smean, float* sistd);
+void groupnorm_bwd(const float* x, const float* dy, const float* mean, const float* istd, const float* g, float* dx,
+                   float* dg, float* db, long N, long C, long HW, long G);
+void softmax_fwd(const float* x, float* y, long N, long C, long HW);
+void softmax_bwd(const float* y, const float* dy, float* dx, long N, long C, long HW);
+// inverted dropout with a counter-based mask of (seed, element index): the same call on dy
+// applies the forward's mask in backward
+void dropout(const float* x, float* y, long n, float p, uint64_t seed);
+// residual join: y = a + b (+ ReLU); ReLU mask of a gradient by the join's output; dx = a + b
+void add(const float* a, const float* b, float* y, long n, bool relu);
+void relu_mask(const float* dy, const float* y, float* dx, long n);
 void adam(float* p, const float* g, float* m, float* v, long n, float lr, float b1, float b2, float eps, float bc1,
           float bc2, float wd, bool decoupled);
 void sgd(float* p, const float* g, float* vel, long n, float lr, float momentum);
@@ -67,6 +83,19 @@ void act_fwd(int kind, const void* x, void* y, long n, float alpha);
 void act_bwd(int kind, const void* x, const void* dy, void* dx, long n, float alpha);
 // pred / grad bf16 [N][C]; returns the mean loss, correct count in *correct
 double softmax_ce(const void* pred, const int64_t* labels, void* grad, int N, int C, long* correct);
+double loss(int kind, const void* pred, const float* target, const int64_t* labels, void* grad, int N, int C,
+            float param, long* correct);
+// GroupNorm over bf16 NHWC rows [N][HW][C]
+void groupnorm_fwd(const void* x, void* y, int N, int HW, int C, int G, const float* g, const float* b, float eps,
+                   float* smean, float* sistd);
+void groupnorm_bwd(const void* dy, const void* x, void* dx, int N, int HW, int C, int G, const float* g,
+                   const float* mean, const float* istd, float* dg, float* db);
+// softmax over the channels of every pixel (bf16 NHWC rows)
+void softmax_fwd(const void* x, void* y, long rows, int C);
+void softmax_bwd(const void* y, const void* dy, void* dx, long rows, int C);
+void dropout(const void* x, void* y, long n, float p, uint64_t seed);
+void add(const void* a, const void* b, void* y, long n, bool relu);
+void relu_mask(const void* dy, const void* y, void* dx, long n);
 void adam(float* p, const float* g, float* m, float* v, void* shadow, long n, float lr, float b1, float b2, float eps,
           float bc1, float bc2, float wd, bool decoupled);
 void sgd(float* p, const float* g, float* vel, void* shadow, long n, float lr, float momentum);

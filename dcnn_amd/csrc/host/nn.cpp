@@ -49,7 +49,10 @@ void check_act(const Tensor& x, Device dev, const char* who) {
   if (x.rank() != 4) throw std::runtime_error(std::string(who) + ": expected an (N, C, H, W) tensor");
 }
 
+constexpr int ACT_SOFTMAX = 100;  // (channel softmax: its own kernels, not an elementwise one)
+
 int act_code(const std::string& k) {
+  if (k == "softmax") return ACT_SOFTMAX;
   if (k == "relu") return ACT_RELU;
   if (k == "leaky_relu") return ACT_LEAKY_RELU;
   if (k == "elu") return ACT_ELU;
@@ -295,25 +298,260 @@ json::Value Activation::parameters_config() const {
   return p;
 }
 
+static float act_alpha(int code) { return code == ACT_ELU ? 1.0f : 0.01f; }
+
 Tensor Activation::forward(const Tensor& x, bool training) {
   (void)training;
   check_act(x, dev_, "activation");
   Tensor y = act_empty(x.shape(), dev_);
+  const long N = x.dim(0), C = x.dim(1), HW = x.dim(2) * x.dim(3);
+  if (code_ == ACT_SOFTMAX) {
+    if (dev_.is_gpu())
+      gpu_ops::softmax_fwd(x.data(), y.data(), N * HW, (int)C);
+    else
+      cpu_ops::softmax_fwd(x.ptr<float>(), y.ptr<float>(), N, C, HW);
+    y_ = y;
+    return y;
+  }
   if (dev_.is_gpu())
-    gpu_ops::act_fwd(code_, x.data(), y.data(), x.numel(), 0.01f);
+    gpu_ops::act_fwd(code_, x.data(), y.data(), x.numel(), act_alpha(code_));
   else
-    cpu_ops::act_fwd(code_, x.ptr<float>(), y.ptr<float>(), x.numel(), 0.01f);
+    cpu_ops::act_fwd(code_, x.ptr<float>(), y.ptr<float>(), x.numel(), act_alpha(code_));
   x_ = x;
   return y;
 }
 
 Tensor Activation::backward(const Tensor& dy) {
+  if (code_ == ACT_SOFTMAX) {
+    Tensor dx = act_empty(y_.shape(), dev_);
+    const long N = y_.dim(0), C = y_.dim(1), HW = y_.dim(2) * y_.dim(3);
+    if (dev_.is_gpu())
+      gpu_ops::softmax_bwd(y_.data(), dy.data(), dx.data(), N * HW, (int)C);
+    else
+      cpu_ops::softmax_bwd(y_.ptr<float>(), dy.ptr<float>(), dx.ptr<float>(), N, C, HW);
+    return dx;
+  }
   Tensor dx = act_empty(x_.shape(), dev_);
   if (dev_.is_gpu())
-    gpu_ops::act_bwd(code_, x_.data(), dy.data(), dx.data(), x_.numel(), 0.01f);
+    gpu_ops::act_bwd(code_, x_.data(), dy.data(), dx.data(), x_.numel(), act_alpha(code_));
   else
-    cpu_ops::act_bwd(code_, x_.ptr<float>(), dy.ptr<float>(), dx.ptr<float>(), x_.numel(), 0.01f);
+    cpu_ops::act_bwd(code_, x_.ptr<float>(), dy.ptr<float>(), dx.ptr<float>(), x_.numel(), act_alpha(code_));
   return dx;
+}
+
+// ------------------------------------------------------------------ GroupNorm
+GroupNorm::GroupNorm(int num_groups, int num_channels, float eps, bool affine, std::string name)
+    : Layer(std::move(name)), g_(num_groups), c_(num_channels), eps_(eps), affine_(affine) {
+  if (g_ <= 0 || c_ % g_) throw std::invalid_argument("groupnorm: channels must divide into the groups");
+}
+
+json::Value GroupNorm::parameters_config() const {
+  json::Value p = json::Value::object();
+  p["num_groups"] = g_;
+  p["num_channels"] = c_;
+  p["epsilon"] = (double)eps_;
+  p["affine"] = affine_;
+  return p;
+}
+
+void GroupNorm::build(const std::vector<int64_t>& in, Device dev, uint64_t seed) {
+  (void)in;
+  (void)seed;
+  dev_ = dev;
+  params_.clear();
+  // (the kernels take gamma / beta always: non-affine runs with the identity pair)
+  add_param("gamma", {c_, 1, 1, 1}, Layout::NCHW, std::vector<float>((size_t)c_, 1.f));
+  add_param("beta", {c_, 1, 1, 1}, Layout::NCHW, std::vector<float>((size_t)c_, 0.f));
+  if (!affine_) {
+    params_.clear();
+    gb_identity_ = true;
+  }
+}
+
+Tensor GroupNorm::forward(const Tensor& x, bool training) {
+  (void)training;
+  check_act(x, dev_, "groupnorm");
+  if (x.dim(1) != c_) throw std::runtime_error(name_ + ": channel count mismatch");
+  const long N = x.dim(0), HW = x.dim(2) * x.dim(3);
+  mean_.ensure({N * g_}, DType::F32, dev_);
+  istd_.ensure({N * g_}, DType::F32, dev_);
+  if (!affine_ && !ident_.defined()) {
+    std::vector<float> gb((size_t)2 * c_, 0.f);
+    std::fill(gb.begin(), gb.begin() + c_, 1.f);
+    ident_ = Tensor::from_host(gb, {2 * c_}, dev_);
+  }
+  const float* g = affine_ ? params_[0].value.ptr<float>() : ident_.ptr<float>();
+  const float* b = affine_ ? params_[1].value.ptr<float>() : ident_.ptr<float>() + c_;
+  Tensor y = act_empty(x.shape(), dev_);
+  if (dev_.is_gpu())
+    gpu_ops::groupnorm_fwd(x.data(), y.data(), (int)N, (int)HW, c_, g_, g, b, eps_, mean_.ptr<float>(),
+                           istd_.ptr<float>());
+  else
+    cpu_ops::groupnorm_fwd(x.ptr<float>(), y.ptr<float>(), N, c_, HW, g_, g, b, eps_, mean_.ptr<float>(),
+                           istd_.ptr<float>());
+  x_ = x;
+  return y;
+}
+
+Tensor GroupNorm::backward(const Tensor& dy) {
+  const long N = x_.dim(0), HW = x_.dim(2) * x_.dim(3);
+  Tensor dx = act_empty(x_.shape(), dev_);
+  const float* g = affine_ ? params_[0].value.ptr<float>() : ident_.ptr<float>();
+  if (!affine_ && !scratch_.defined()) scratch_ = Tensor::zeros({2 * c_}, DType::F32, dev_);
+  float* dg = affine_ ? params_[0].grad.ptr<float>() : scratch_.ptr<float>();
+  float* db = affine_ ? params_[1].grad.ptr<float>() : scratch_.ptr<float>() + c_;
+  if (dev_.is_gpu())
+    gpu_ops::groupnorm_bwd(dy.data(), x_.data(), dx.data(), (int)N, (int)HW, c_, g_, g, mean_.ptr<float>(),
+                           istd_.ptr<float>(), dg, db);
+  else
+    cpu_ops::groupnorm_bwd(x_.ptr<float>(), dy.ptr<float>(), mean_.ptr<float>(), istd_.ptr<float>(), g,
+                           dx.ptr<float>(), dg, db, N, c_, HW, g_);
+  return dx;
+}
+
+// ------------------------------------------------------------------ Dropout
+Dropout::Dropout(float rate, std::string name) : Layer(std::move(name)), p_(rate) {
+  if (!(rate >= 0.f && rate < 1.f)) throw std::invalid_argument("dropout: rate must be in [0, 1)");
+}
+
+json::Value Dropout::parameters_config() const {
+  json::Value p = json::Value::object();
+  p["dropout_rate"] = (double)p_;
+  return p;
+}
+
+void Dropout::build(const std::vector<int64_t>& in, Device dev, uint64_t seed) {
+  (void)in;
+  dev_ = dev;
+  seed_ = seed * 0x2545f4914f6cdd1dull + 0x1234567ull;
+}
+
+Tensor Dropout::forward(const Tensor& x, bool training) {
+  check_act(x, dev_, "dropout");
+  active_ = training && p_ > 0.f;
+  if (!active_) return x;
+  cur_ = seed_ + 0x9e3779b97f4a7c15ull * (++draw_);  // a new mask per forward
+  Tensor y = act_empty(x.shape(), dev_);
+  if (dev_.is_gpu())
+    gpu_ops::dropout(x.data(), y.data(), x.numel(), p_, cur_);
+  else
+    cpu_ops::dropout(x.ptr<float>(), y.ptr<float>(), x.numel(), p_, cur_);
+  return y;
+}
+
+Tensor Dropout::backward(const Tensor& dy) {
+  if (!active_) return dy;
+  Tensor dx = act_empty(dy.shape(), dev_);
+  if (dev_.is_gpu())
+    gpu_ops::dropout(dy.data(), dx.data(), dy.numel(), p_, cur_);  // the forward's mask and scale
+  else
+    cpu_ops::dropout(dy.ptr<float>(), dx.ptr<float>(), dy.numel(), p_, cur_);
+  return dx;
+}
+
+// ------------------------------------------------------------------ ResidualBlock
+ResidualBlock::ResidualBlock(std::vector<std::unique_ptr<Layer>> main, std::vector<std::unique_ptr<Layer>> shortcut,
+                             std::string activation, std::string name)
+    : Layer(std::move(name)), main_(std::move(main)), short_(std::move(shortcut)), act_(std::move(activation)) {
+  if (act_ != "relu" && act_ != "none" && act_ != "linear")
+    throw std::invalid_argument("residual_block: activation must be relu, none or linear");
+}
+
+static json::Value path_config(const std::vector<std::unique_ptr<Layer>>& path) {
+  json::Value arr = json::Value::array();
+  for (auto& l : path) {
+    json::Value r = json::Value::object();
+    r["type"] = l->type();
+    r["name"] = l->name();
+    r["parameters"] = l->parameters_config();
+    arr.push(std::move(r));
+  }
+  return arr;
+}
+
+json::Value ResidualBlock::parameters_config() const {
+  json::Value p = json::Value::object();
+  p["activation"] = act_;
+  p["has_projection"] = !short_.empty();
+  p["main_path"] = path_config(main_).dump();
+  p["shortcut_path"] = path_config(short_).dump();
+  return p;
+}
+
+std::vector<int64_t> ResidualBlock::output_shape(const std::vector<int64_t>& in) const {
+  std::vector<int64_t> s = in;
+  for (auto& l : main_) s = l->output_shape(s);
+  return s;
+}
+
+void ResidualBlock::build(const std::vector<int64_t>& in, Device dev, uint64_t seed) {
+  dev_ = dev;
+  std::vector<int64_t> s = in;
+  uint64_t k = 0;
+  for (auto& l : main_) {
+    l->build(s, dev, seed * 31ull + (k++) * 104729ull);
+    if (s[1] > 0) s = l->output_shape(s);
+  }
+  s = in;
+  for (auto& l : short_) {
+    l->build(s, dev, seed * 31ull + (k++) * 104729ull);
+    if (s[1] > 0) s = l->output_shape(s);
+  }
+}
+
+Tensor ResidualBlock::forward(const Tensor& x, bool training) {
+  check_act(x, dev_, "residual_block");
+  Tensor m = x;
+  for (auto& l : main_) m = l->forward(m, training);
+  Tensor sc = x;
+  for (auto& l : short_) sc = l->forward(sc, training);
+  if (m.shape() != sc.shape())
+    throw std::runtime_error(name_ + ": main path " + shape_str(m.shape()) + " vs shortcut " + shape_str(sc.shape()));
+  Tensor y = act_empty(m.shape(), dev_);
+  const bool relu = act_ == "relu";
+  if (dev_.is_gpu())
+    gpu_ops::add(m.data(), sc.data(), y.data(), y.numel(), relu);
+  else
+    cpu_ops::add(m.ptr<float>(), sc.ptr<float>(), y.ptr<float>(), y.numel(), relu);
+  y_ = y;
+  return y;
+}
+
+Tensor ResidualBlock::backward(const Tensor& dy) {
+  Tensor g = dy;
+  if (act_ == "relu") {
+    g = act_empty(dy.shape(), dev_);
+    if (dev_.is_gpu())
+      gpu_ops::relu_mask(dy.data(), y_.data(), g.data(), dy.numel());
+    else
+      cpu_ops::relu_mask(dy.ptr<float>(), y_.ptr<float>(), g.ptr<float>(), dy.numel());
+  }
+  Tensor gm = g;
+  for (size_t i = main_.size(); i-- > 0;) gm = main_[i]->backward(gm);
+  Tensor gs = g;
+  for (size_t i = short_.size(); i-- > 0;) gs = short_[i]->backward(gs);
+  Tensor dx = act_empty(gm.shape(), dev_);
+  if (dev_.is_gpu())
+    gpu_ops::add(gm.data(), gs.data(), dx.data(), dx.numel(), false);
+  else
+    cpu_ops::add(gm.ptr<float>(), gs.ptr<float>(), dx.ptr<float>(), dx.numel(), false);
+  return dx;
+}
+
+void ResidualBlock::sync_shadow() {
+  for (auto& l : main_) l->sync_shadow();
+  for (auto& l : short_) l->sync_shadow();
+}
+
+void ResidualBlock::collect_params(std::vector<Param*>& out) {
+  for (auto& l : main_) l->collect_params(out);
+  for (auto& l : short_) l->collect_params(out);
+}
+
+void ResidualBlock::collect_layers(std::vector<Layer*>& out) {
+  out.push_back(this);
+  for (auto& l : main_) l->collect_layers(out);
+  for (auto& l : short_) l->collect_layers(out);
 }
 
 // ------------------------------------------------------------------ pooling
@@ -442,6 +680,23 @@ std::unique_ptr<Layer> create_layer(const json::Value& rec) {
     return std::make_unique<Pool2D>(type == "maxpool2d", I("pool_h", 2), I("pool_w", 2), I("stride_h", 0),
                                     I("stride_w", 0), I("pad_h", 0), I("pad_w", 0), name);
   if (type == "flatten") return std::make_unique<Flatten>(name);
+  if (type == "groupnorm")
+    return std::make_unique<GroupNorm>(I("num_groups", 1), I("num_channels", 0), (float)p.get_number("epsilon", 1e-5),
+                                       p.get_bool("affine", true), name);
+  if (type == "dropout") return std::make_unique<Dropout>((float)p.get_number("dropout_rate", 0.5), name);
+  if (type == "residual_block") {
+    auto path = [&](const char* key) {
+      std::vector<std::unique_ptr<Layer>> out;
+      const std::string txt = p.get_string(key, "[]");
+      const json::Value arr = json::Value::parse(txt.empty() ? "[]" : txt);  // (kept alive for the loop)
+      for (auto& r : arr.items()) out.push_back(create_layer(r));
+      return out;
+    };
+    auto main = path("main_path");
+    std::vector<std::unique_ptr<Layer>> sc;
+    if (p.get_bool("has_projection", false)) sc = path("shortcut_path");
+    return std::make_unique<ResidualBlock>(std::move(main), std::move(sc), p.get_string("activation", "relu"), name);
+  }
   throw std::invalid_argument("C++ host API: unsupported layer type '" + type + "'");
 }
 
@@ -480,8 +735,16 @@ void Sequential::initialize(uint64_t seed) {
 
 std::vector<Param*> Sequential::parameters() {
   std::vector<Param*> out;
-  for (auto& l : layers_)
-    for (auto& p : l->params()) out.push_back(&p);
+  for (auto& l : layers_) l->collect_params(out);
+  return out;
+}
+
+std::vector<BatchNorm*> Sequential::batchnorms() {
+  std::vector<Layer*> all;
+  for (auto& l : layers_) l->collect_layers(all);
+  std::vector<BatchNorm*> out;
+  for (auto* l : all)
+    if (auto* bn = dynamic_cast<BatchNorm*>(l)) out.push_back(bn);
   return out;
 }
 
@@ -563,30 +826,28 @@ void Sequential::save_to_file(const std::string& path) const {
   }
   std::ofstream f(path + ".bin", std::ios::binary);
   if (!f) throw std::runtime_error("cannot write " + path + ".bin");
-  for (auto& l : layers_)
-    for (auto& p : const_cast<Layer&>(*l).params()) p.value.view(p.shape, p.layout).save(f);
+  auto& self = const_cast<Sequential&>(*this);
+  for (auto* p : self.parameters()) p->value.view(p->shape, p->layout).save(f);
   // BatchNorm running statistics: language-neutral sidecar of .bin records (running_mean,
-  // running_var per BatchNorm in layer order), read by both front ends
+  // running_var per BatchNorm in depth-first layer order), read by both front ends
   std::ofstream s(path + ".bnstats", std::ios::binary);
-  for (auto& l : layers_)
-    if (auto* bn = dynamic_cast<const BatchNorm*>(l.get())) {
-      const int64_t c = bn->running_mean.numel();
-      bn->running_mean.view({c, 1, 1, 1}).save(s);
-      bn->running_var.view({c, 1, 1, 1}).save(s);
-    }
+  for (auto* bn : self.batchnorms()) {
+    const int64_t c = bn->running_mean.numel();
+    bn->running_mean.view({c, 1, 1, 1}).save(s);
+    bn->running_var.view({c, 1, 1, 1}).save(s);
+  }
 }
 
 void Sequential::load_bn_stats(const std::string& path) {
   std::ifstream f(path, std::ios::binary);
   if (!f) throw std::runtime_error("cannot read " + path);
-  for (auto& l : layers_)
-    if (auto* bn = dynamic_cast<BatchNorm*>(l.get())) {
-      const int64_t c = bn->running_mean.numel();
-      Tensor m = Tensor::load(f), v = Tensor::load(f);
-      if (m.numel() != c || v.numel() != c) throw std::runtime_error("bnstats: channel count mismatch");
-      bn->running_mean = Tensor::from_host(m.to_host_f32(), {c}, dev_);
-      bn->running_var = Tensor::from_host(v.to_host_f32(), {c}, dev_);
-    }
+  for (auto* bn : batchnorms()) {
+    const int64_t c = bn->running_mean.numel();
+    Tensor m = Tensor::load(f), v = Tensor::load(f);
+    if (m.numel() != c || v.numel() != c) throw std::runtime_error("bnstats: channel count mismatch");
+    bn->running_mean = Tensor::from_host(m.to_host_f32(), {c}, dev_);
+    bn->running_var = Tensor::from_host(v.to_host_f32(), {c}, dev_);
+  }
 }
 
 void Sequential::load_weights_file(const std::string& path) {
@@ -678,6 +939,61 @@ SequentialBuilder& SequentialBuilder::dense(int out_features, bool bias, const s
   model_.add(std::make_unique<Dense>(in, out_features, bias, auto_name(name, "dense")));
   cur_ = {out_features, 1, 1};
   return *this;
+}
+
+SequentialBuilder& SequentialBuilder::groupnorm(int num_groups, float eps, bool affine, const std::string& name) {
+  model_.add(std::make_unique<GroupNorm>(num_groups, (int)cur_.at(0), eps, affine, auto_name(name, "groupnorm")));
+  return *this;
+}
+
+SequentialBuilder& SequentialBuilder::dropout(float rate, const std::string& name) {
+  model_.add(std::make_unique<Dropout>(rate, auto_name(name, "dropout")));
+  return *this;
+}
+
+SequentialBuilder& SequentialBuilder::residual(std::vector<std::unique_ptr<Layer>> main,
+                                               std::vector<std::unique_ptr<Layer>> shortcut,
+                                               const std::string& activation, const std::string& name) {
+  auto l = std::make_unique<ResidualBlock>(std::move(main), std::move(shortcut), activation,
+                                           auto_name(name, "residual_block"));
+  const auto o = l->output_shape({1, cur_.at(0), cur_[1], cur_[2]});
+  cur_ = {o[1], o[2], o[3]};
+  model_.add(std::move(l));
+  return *this;
+}
+
+SequentialBuilder& SequentialBuilder::basic_residual_block(int in_ch, int out_ch, int stride, const std::string& name) {
+  std::vector<std::unique_ptr<Layer>> m, sc;
+  m.push_back(std::make_unique<Conv2D>(in_ch, out_ch, 3, 3, stride, stride, 1, 1, true, "conv2d_0"));
+  m.push_back(std::make_unique<BatchNorm>(out_ch, 1e-5f, 0.1f, true, "bn0"));
+  m.push_back(std::make_unique<Activation>("relu", "relu_0"));
+  m.push_back(std::make_unique<Conv2D>(out_ch, out_ch, 3, 3, 1, 1, 1, 1, true, "conv2d_1"));
+  m.push_back(std::make_unique<BatchNorm>(out_ch, 1e-5f, 0.1f, true, "bn0"));
+  if (stride != 1 || in_ch != out_ch) {
+    sc.push_back(std::make_unique<Conv2D>(in_ch, out_ch, 1, 1, stride, stride, 0, 0, false, "conv2d_0"));
+    sc.push_back(std::make_unique<BatchNorm>(out_ch, 1e-5f, 0.1f, true, "bn0"));
+  }
+  return residual(std::move(m), std::move(sc), "relu",
+                  name.empty() ? "basic_residual_block_" + std::to_string(model_.layers().size()) : name);
+}
+
+SequentialBuilder& SequentialBuilder::bottleneck_residual_block(int in_ch, int mid_ch, int out_ch, int stride,
+                                                                const std::string& name) {
+  std::vector<std::unique_ptr<Layer>> m, sc;
+  m.push_back(std::make_unique<Conv2D>(in_ch, mid_ch, 1, 1, 1, 1, 0, 0, false, "conv2d_0"));
+  m.push_back(std::make_unique<BatchNorm>(mid_ch, 1e-3f, 0.1f, true, "bn0"));
+  m.push_back(std::make_unique<Activation>("relu", "relu_0"));
+  m.push_back(std::make_unique<Conv2D>(mid_ch, mid_ch, 3, 3, stride, stride, 1, 1, false, "conv2d_1"));
+  m.push_back(std::make_unique<BatchNorm>(mid_ch, 1e-3f, 0.1f, true, "bn0"));
+  m.push_back(std::make_unique<Activation>("relu", "relu_1"));
+  m.push_back(std::make_unique<Conv2D>(mid_ch, out_ch, 1, 1, 1, 1, 0, 0, false, "conv2d_2"));
+  m.push_back(std::make_unique<BatchNorm>(out_ch, 1e-3f, 0.1f, true, "bn0"));
+  if (stride != 1 || in_ch != out_ch) {
+    sc.push_back(std::make_unique<Conv2D>(in_ch, out_ch, 1, 1, stride, stride, 0, 0, false, "conv2d_0"));
+    sc.push_back(std::make_unique<BatchNorm>(out_ch, 1e-3f, 0.1f, true, "bn0"));
+  }
+  return residual(std::move(m), std::move(sc), "relu",
+                  name.empty() ? "bottleneck_residual_block_" + std::to_string(model_.layers().size()) : name);
 }
 
 Sequential SequentialBuilder::build() { return std::move(model_); }

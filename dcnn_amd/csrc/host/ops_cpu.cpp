@@ -3,6 +3,8 @@
 #include "../native/cpu_kernels.h"
 #include "dcnn/ops.hpp"
 
+#include <stdexcept>
+
 namespace dcnn {
 namespace cpu_ops {
 namespace C = dcnn_native::cpu;
@@ -64,6 +66,53 @@ void act_bwd(int kind, const float* x, const float* dy, float* dx, long n, float
 
 double softmax_ce(const float* pred, const int64_t* labels, float* grad, long N, long Cc, long* correct) {
   return C::loss_fused(1, pred, (const float*)nullptr, labels, grad, N, Cc, 1e-15, correct);
+}
+
+double loss(int kind, const float* pred, const float* target, const int64_t* labels, float* grad, long N, long Cc,
+            float param, long* correct) {
+  // the CPU kernels number the losses 0 ce, 1 softmax ce (= log-softmax ce), 2 mse, 3 mae, 4 huber
+  static const int map[] = {0, 1, 1, 2, 3, 4};
+  if (kind < 0 || kind > 5) throw std::invalid_argument("loss: unknown kind");
+  return C::loss_fused(map[kind], pred, target, labels, grad, N, Cc, param, correct);
+}
+
+void groupnorm_fwd(const float* x, float* y, long N, long Cc, long HW, long G, const float* g, const float* b, float eps,
+                   float* smean, float* sistd) {
+  C::groupnorm_fwd<float>(x, y, N, Cc, HW, G, g, b, eps, smean, sistd);
+}
+
+void groupnorm_bwd(const float* x, const float* dy, const float* mean, const float* istd, const float* g, float* dx,
+                   float* dg, float* db, long N, long Cc, long HW, long G) {
+  C::groupnorm_bwd<float>(x, dy, mean, istd, g, dx, dg, db, N, Cc, HW, G);
+}
+
+void softmax_fwd(const float* x, float* y, long N, long Cc, long HW) { C::softmax_channels<float>(x, y, N, Cc, HW); }
+void softmax_bwd(const float* y, const float* dy, float* dx, long N, long Cc, long HW) {
+  C::softmax_channels_bwd<float>(y, dy, dx, N, Cc, HW);
+}
+
+void dropout(const float* x, float* y, long n, float p, uint64_t seed) {
+  // counter-based mask (splitmix64 of seed ^ index): the backward call regenerates it exactly
+  const float scale = 1.f / (1.f - p);
+  for (long i = 0; i < n; ++i) {
+    uint64_t z = seed + 0x9e3779b97f4a7c15ull * (uint64_t)(i + 1);
+    z = (z ^ (z >> 30)) * 0xbf58476d1ce4e5b9ull;
+    z = (z ^ (z >> 27)) * 0x94d049bb133111ebull;
+    z ^= z >> 31;
+    const float u = (float)((z >> 40) * (1.0 / 16777216.0));
+    y[i] = u >= p ? x[i] * scale : 0.f;
+  }
+}
+
+void add(const float* a, const float* b, float* y, long n, bool relu) {
+  for (long i = 0; i < n; ++i) {
+    const float v = a[i] + b[i];
+    y[i] = relu && v < 0.f ? 0.f : v;
+  }
+}
+
+void relu_mask(const float* dy, const float* y, float* dx, long n) {
+  for (long i = 0; i < n; ++i) dx[i] = y[i] > 0.f ? dy[i] : 0.f;
 }
 
 void adam(float* p, const float* g, float* m, float* v, long n, float lr, float b1, float b2, float eps, float bc1,

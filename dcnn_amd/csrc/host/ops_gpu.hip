@@ -1,9 +1,14 @@
 // GPU backend of the C++ host API: the HIP/CDNA4 kernel library (csrc/kernels/*.hip) driven
-// from C++ — bf16 NHWC activations, fp32 master parameters, bf16 operand shadows. Convolutions
-// and dense layers run on the generic implicit-GEMM MFMA kernels (gemm_nt forward / dgrad,
-// gemm_tn + split-K reduce weight gradients), BatchNorm on the deterministic slab statistics,
-// the loss and the optimizers on the fused kernels. Work goes to the null stream in order;
-// workspaces are grow-only device buffers reused across calls.
+// from C++ — bf16 NHWC activations, fp32 master parameters, bf16 operand shadows.
+//
+// Convolution routing (the same kernels and the same rules as the Python front end's main
+// routes, ops/hip.py): 3x3 stride-1 'same' convs and their data gradients on the persistent halo
+// kernel (hconv / hconv3, split-K on small grids), their weight gradients on the halo wgrad
+// (hwgrad); 1x1 convs on the streaming kernel (g1s); everything else on the gathered MFMA GEMM
+// (gemm_g2 forward, the stride-phase-grouped gemm_g2 data gradient, gemm_t2 weight gradient);
+// odd channel counts on the generic implicit GEMM (gemm_nt / gemm_tn). BatchNorm runs on the
+// deterministic slab statistics, the losses and the optimizers on the fused kernels. Work goes to
+// the null stream in order; workspaces are grow-only device buffers reused across calls.
 #include <hip/hip_runtime.h>
 
 #include <cstring>
@@ -50,7 +55,8 @@ constexpr int kBF16 = 1;
 const hipStream_t S = nullptr;
 
 // grow-only workspace per purpose
-enum Slot { W_T = 0, SLAB, BSLAB, STAT_SLAB, STAT_SUMS, STAT_PART, LOSS_WS, LOSS_OUT, TICKETS, NSLOTS };
+enum Slot { W_T = 0, SLAB, BSLAB, STAT_SLAB, STAT_SUMS, STAT_PART, LOSS_WS, LOSS_OUT, TICKETS, HPART, HTICKETS, GN_AFF,
+            NSLOTS };
 void* scratch(Slot s, size_t bytes) {
   static void* p[NSLOTS] = {};
   static size_t n[NSLOTS] = {};
@@ -89,6 +95,76 @@ void transpose16(const void* in, void* out, int batch, int rows, int cols) {
 
 PoolGeom geom(const PoolShape& p) { return PoolGeom{p.N, p.H, p.W, p.C, p.OH, p.OW, p.KH, p.KW, p.SH, p.SW, p.PH, p.PW}; }
 
+// ---- residual join / masks on bf16 (8 elements per thread when aligned)
+__global__ void add_bf16_kernel(const bf16* __restrict__ a, const bf16* __restrict__ b, bf16* __restrict__ y, long n,
+                                int relu) {
+  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < n; i += (long)gridDim.x * blockDim.x) {
+    float v = (float)a[i] + (float)b[i];
+    if (relu) v = fmaxf(v, 0.f);
+    y[i] = (bf16)v;
+  }
+}
+__global__ void relu_mask_bf16_kernel(const bf16* __restrict__ dy, const bf16* __restrict__ yv, bf16* __restrict__ dx,
+                                      long n) {
+  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < n; i += (long)gridDim.x * blockDim.x)
+    dx[i] = (float)yv[i] > 0.f ? dy[i] : (bf16)0.f;
+}
+int grid_of(long n) {
+  long g = (n + 255) / 256;
+  return (int)(g > 8192 ? 8192 : (g < 1 ? 1 : g));
+}
+
+// split-K workspace of a halo conv: (partials, zeroed ticket words) — the kernel leaves them zeroed
+void hconv_workspace(HConvArgs& a) {
+  a.splits = hconv_splits(a.NB, a.H, a.W, a.Cs, a.N, a.ntaps);
+  a.part = nullptr;
+  a.tickets = nullptr;
+  if (a.splits <= 1) {
+    a.splits = 1;
+    return;
+  }
+  const long tiles = hconv_tiles(a.NB, a.H, a.W, a.Cs, a.N, a.ntaps);
+  a.part = static_cast<float*>(scratch(HPART, (size_t)tiles * a.splits * hconv_tile_elems(a.NB, a.H, a.W, a.Cs, a.N,
+                                                                                          a.ntaps) * 4));
+  static size_t zeroed = 0;  // ticket words zeroed so far (grown only; left zeroed by every launch)
+  const size_t need = (size_t)tiles * 64 * 4;
+  a.tickets = static_cast<unsigned*>(scratch(HTICKETS, need));
+  if (zeroed < need) {
+    HOST_HIP_CHECK(hipMemset(a.tickets, 0, need));
+    zeroed = need;
+  }
+}
+
+bool is_same3x3(const ConvShape& s) {
+  return s.KH == 3 && s.KW == 3 && s.SH == 1 && s.SW == 1 && s.PH == 1 && s.PW == 1;
+}
+
+// gathered-GEMM argument block (gemm2.hip) for a forward conv
+G2Args g2_fwd_args(const void* x, const void* w, void* y, const float* bias, const ConvShape& s) {
+  G2Args a{};
+  a.A = static_cast<const bf16*>(x);
+  a.B = static_cast<const bf16*>(w);
+  a.C = static_cast<bf16*>(y);
+  a.a_bytes = (unsigned)((long)s.N * s.H * s.W * s.C * 2);
+  a.b_bytes = (unsigned)((long)s.Co * s.KH * s.KW * s.C * 2);
+  a.M = s.N * s.OH * s.OW;
+  a.N = s.Co;
+  a.Cs = s.C;
+  a.H = s.H; a.W = s.W; a.GH = s.OH; a.GW = s.OW; a.SY = s.SH; a.SX = s.SW;
+  int t = 0;
+  for (int ky = 0; ky < s.KH; ++ky)
+    for (int kx = 0; kx < s.KW; ++kx, ++t) {
+      const int dy = ky - s.PH, dx = kx - s.PW;
+      a.tap_dy[t] = dy; a.tap_dx[t] = dx; a.tap_srcoff[t] = (dy * s.W + dx) * s.C; a.tap_b[t] = (ky * s.KW + kx) * s.C;
+    }
+  a.ntaps = t;
+  a.ldb = s.KH * s.KW * s.C;
+  a.ldc = s.Co;
+  a.OH = s.OH; a.OW = s.OW; a.OSY = 1; a.OSX = 1; a.ORY = 0; a.ORX = 0;
+  a.bias = bias;
+  return a;
+}
+
 void wgrad_reduce(const float* slab, float* gw, long n, const float* bslab, float* gb, long nb, int splits) {
   if (gb)
     splitk_reduce2(slab, gw, n, bslab, gb, nb, splits, 1, S);
@@ -104,6 +180,28 @@ void cast_bf16(const float* x, void* y, long n) { cast_f32_bf16(x, static_cast<b
 void zero(void* p, long nbytes) { zero_bytes(p, nbytes, S); }
 
 void conv_fwd(const void* x, const void* w, const float* bias, void* y, const ConvShape& s) {
+  const long xb = (long)s.N * s.H * s.W * s.C * 2, wb = (long)s.Co * s.KH * s.KW * s.C * 2;
+  if (is_same3x3(s) && hconv_supported(s.N, s.H, s.W, s.C, s.Co, 9) && xb < (1l << 31)) {
+    HConvArgs a{};
+    a.A = static_cast<const bf16*>(x); a.B = static_cast<const bf16*>(w); a.C = static_cast<bf16*>(y);
+    a.a_bytes = (unsigned)xb; a.b_bytes = (unsigned)wb;
+    a.NB = s.N; a.H = s.H; a.W = s.W; a.Cs = s.C; a.N = s.Co; a.ldb = 9 * s.C; a.ntaps = 9;
+    for (int t = 0; t < 9; ++t) { a.tap_dy[t] = t / 3 - 1; a.tap_dx[t] = t % 3 - 1; a.tap_b[t] = t * s.C; }
+    a.bias = bias;
+    hconv_workspace(a);
+    hconv(a, S);
+    return;
+  }
+  if (s.KH == 1 && s.KW == 1 && s.PH == 0 && s.PW == 0 && s.SH == s.SW &&
+      g1s_rows(s.N * s.OH * s.OW, s.Co, s.C, 0) > 0) {
+    g1s(static_cast<const bf16*>(x), static_cast<const bf16*>(w), static_cast<bf16*>(y), s.N * s.OH * s.OW, s.Co, s.C,
+        s.H, s.W, s.OH, s.OW, s.SH, bias, nullptr, nullptr, 0, nullptr, 0, BnbArgs{}, 0, S);
+    return;
+  }
+  if (s.C % 8 == 0 && s.Co % 8 == 0 && s.KH * s.KW <= 64 && xb < (1l << 31) && wb < (1l << 31)) {
+    gemm_g2(g2_fwd_args(x, w, y, bias, s), S);
+    return;
+  }
   const int K = s.KH * s.KW * s.C;
   NtArgs a{static_cast<const bf16*>(x), static_cast<const bf16*>(w), y, s.N * s.OH * s.OW, s.Co, K, 0, K, s.Co,
            kConvFwd, s.N, s.H, s.W, s.C, s.OH, s.OW, s.KH, s.KW, s.SH, s.SW, s.PH, s.PW, bias, nullptr, nullptr, 0, 0};
@@ -114,6 +212,69 @@ void conv_dgrad(const void* dy, const void* w, void* dx, const ConvShape& s) {
   const int T = s.KH * s.KW, K = T * s.Co;
   bf16* wt = static_cast<bf16*>(scratch(W_T, (size_t)s.Co * T * s.C * 2));
   conv_weight_transpose(kBF16, w, wt, s.Co, T, s.C, S);  // [Co][T][C] -> [C][T][Co]
+  const long dyb = (long)s.N * s.OH * s.OW * s.Co * 2, wtb = (long)s.C * T * s.Co * 2;
+  if (is_same3x3(s) && hconv_supported(s.N, s.OH, s.OW, s.Co, s.C, 9) && dyb < (1l << 31)) {
+    // transposed conv of a stride-1 conv: tap (ky, kx) reads dy at (1 - ky, 1 - kx)
+    HConvArgs a{};
+    a.A = static_cast<const bf16*>(dy); a.B = wt; a.C = static_cast<bf16*>(dx);
+    a.a_bytes = (unsigned)dyb; a.b_bytes = (unsigned)wtb;
+    a.NB = s.N; a.H = s.OH; a.W = s.OW; a.Cs = s.Co; a.N = s.C; a.ldb = 9 * s.Co; a.ntaps = 9;
+    for (int t = 0; t < 9; ++t) {
+      const int ky = t / 3, kx = t % 3;
+      a.tap_dy[t] = 1 - ky; a.tap_dx[t] = 1 - kx; a.tap_b[t] = t * s.Co;
+    }
+    hconv_workspace(a);
+    hconv(a, S);
+    return;
+  }
+  if (s.C % 8 == 0 && s.Co % 8 == 0 && dyb < (1l << 31) && wtb < (1l << 31)) {
+    // stride-phase decomposition: output phase (ry, rx) is a dense GEMM over the taps reaching
+    // it; all phases are row classes of ONE grouped launch (phases no tap reaches write zeros)
+    struct Cls { int ry, rx, GH, GW, t0, nt; };
+    std::vector<Cls> cls;
+    G2Args a{};
+    int nt = 0;
+    bool uniform = true;
+    for (int ry = 0; ry < s.SH; ++ry)
+      for (int rx = 0; rx < s.SW; ++rx) {
+        const int GH = (s.H - ry + s.SH - 1) / s.SH, GW = (s.W - rx + s.SW - 1) / s.SW;
+        if (GH <= 0 || GW <= 0) continue;
+        Cls c{ry, rx, GH, GW, nt, 0};
+        for (int ky = 0; ky < s.KH; ++ky) {
+          if ((ry + s.PH - ky) % s.SH) continue;
+          const int dyo = (ry + s.PH - ky) / s.SH;
+          for (int kx = 0; kx < s.KW; ++kx) {
+            if ((rx + s.PW - kx) % s.SW) continue;
+            const int dxo = (rx + s.PW - kx) / s.SW;
+            if (nt >= 64) throw std::runtime_error("conv_dgrad: more than 64 taps");
+            a.tap_dy[nt] = dyo; a.tap_dx[nt] = dxo; a.tap_srcoff[nt] = (dyo * s.OW + dxo) * s.Co;
+            a.tap_b[nt] = (ky * s.KW + kx) * s.Co;
+            ++nt;
+            ++c.nt;
+          }
+        }
+        if (!cls.empty() && (c.GH != cls[0].GH || c.GW != cls[0].GW)) uniform = false;
+        cls.push_back(c);
+      }
+    const long rows = (long)s.N * (cls.empty() ? 0 : cls[0].GH * cls[0].GW);
+    if (uniform && !cls.empty() && cls.size() <= 4 && (cls.size() == 1 || rows % 128 == 0)) {
+      a.A = static_cast<const bf16*>(dy); a.B = wt; a.C = static_cast<bf16*>(dx);
+      a.a_bytes = (unsigned)dyb; a.b_bytes = (unsigned)wtb;
+      a.M = (int)(rows * (long)cls.size()); a.N = s.C; a.Cs = s.Co;
+      a.H = s.OH; a.W = s.OW; a.GH = cls[0].GH; a.GW = cls[0].GW; a.SY = 1; a.SX = 1;
+      a.ntaps = nt; a.ldb = T * s.Co; a.ldc = s.C;
+      a.OH = s.H; a.OW = s.W; a.OSY = s.SH; a.OSX = s.SW; a.ORY = cls[0].ry; a.ORX = cls[0].rx;
+      if (cls.size() > 1) {
+        a.ncls = (int)cls.size();
+        a.cls_rows = (int)rows;
+        for (size_t k = 0; k < cls.size(); ++k) {
+          a.cls_t0[k] = cls[k].t0; a.cls_nt[k] = cls[k].nt; a.cls_ory[k] = cls[k].ry; a.cls_orx[k] = cls[k].rx;
+        }
+      }
+      gemm_g2(a, S);
+      return;
+    }
+  }
   NtArgs a{static_cast<const bf16*>(dy), wt, dx, s.N * s.H * s.W, s.C, K, 0, K, s.C, kConvDgrad, s.N, s.OH, s.OW,
            s.Co, s.H, s.W, s.KH, s.KW, s.SH, s.SW, s.PH, s.PW, nullptr, nullptr, nullptr, 0, 0};
   gemm_nt(a, S);
@@ -121,6 +282,37 @@ void conv_dgrad(const void* dy, const void* w, void* dx, const ConvShape& s) {
 
 void conv_wgrad(const void* dy, const void* x, float* gw, float* gb, const ConvShape& s) {
   const int Ng = s.KH * s.KW * s.C, P = s.N * s.OH * s.OW;
+  const long dyb = (long)P * s.Co * 2, xb = (long)s.N * s.H * s.W * s.C * 2;
+  if (is_same3x3(s) && hwgrad_supported(s.N, s.H, s.W, s.C, s.Co, 9)) {
+    const int splits = hwgrad_splits(s.N, s.H, s.W, s.C, s.Co);
+    float* slab = static_cast<float*>(scratch(SLAB, (size_t)splits * s.Co * Ng * 4));
+    float* bslab = gb ? static_cast<float*>(scratch(BSLAB, (size_t)splits * s.Co * 4)) : nullptr;
+    HWArgs a{};
+    a.dY = static_cast<const bf16*>(dy); a.X = static_cast<const bf16*>(x); a.slab = slab; a.bias_slab = bslab;
+    a.dy_bytes = (unsigned)dyb; a.x_bytes = (unsigned)xb;
+    a.NB = s.N; a.H = s.H; a.W = s.W; a.Cs = s.C; a.Co = s.Co; a.ntaps = 9;
+    for (int t = 0; t < 9; ++t) { a.tap_dy[t] = t / 3 - 1; a.tap_dx[t] = t % 3 - 1; }
+    hwgrad(a, splits, S);
+    wgrad_reduce(slab, gw, (long)s.Co * Ng, bslab, gb, s.Co, splits);
+    return;
+  }
+  if (s.C % 8 == 0 && s.Co % 8 == 0 && s.KH * s.KW <= 64 && dyb < (1l << 31) && xb < (1l << 31) && P < (1 << 24)) {
+    const int splits = gemm_t2_splits(s.Co, Ng, P);
+    float* slab = static_cast<float*>(scratch(SLAB, (size_t)splits * s.Co * Ng * 4));
+    float* bslab = gb ? static_cast<float*>(scratch(BSLAB, (size_t)splits * s.Co * 4)) : nullptr;
+    T2Args a{};
+    a.dY = static_cast<const bf16*>(dy); a.X = static_cast<const bf16*>(x); a.slab = slab; a.bias_slab = bslab;
+    a.a_bytes = (unsigned)dyb; a.b_bytes = (unsigned)xb;
+    a.M = s.Co; a.N = Ng; a.P = P; a.ldy = s.Co; a.Cs = s.C; a.H = s.H; a.W = s.W; a.GH = s.OH; a.GW = s.OW;
+    a.SY = s.SH; a.SX = s.SW;
+    int t = 0;
+    for (int ky = 0; ky < s.KH; ++ky)
+      for (int kx = 0; kx < s.KW; ++kx, ++t) { a.tap_dy[t] = ky - s.PH; a.tap_dx[t] = kx - s.PW; }
+    a.ntaps = t;
+    gemm_t2(a, splits, S);
+    wgrad_reduce(slab, gw, (long)s.Co * Ng, bslab, gb, s.Co, splits);
+    return;
+  }
   const int splits = gemm_tn_splits(s.Co, Ng, P);
   float* slab = static_cast<float*>(scratch(SLAB, (size_t)splits * s.Co * Ng * 4));
   float* bslab = gb ? static_cast<float*>(scratch(BSLAB, (size_t)splits * s.Co * 4)) : nullptr;
@@ -222,6 +414,56 @@ double softmax_ce(const void* pred, const int64_t* labels, void* grad, int N, in
   std::memcpy(&c, host + 8, 4);
   if (correct) *correct = c;
   return l;
+}
+
+double loss(int kind, const void* pred, const float* target, const int64_t* labels, void* grad, int N, int C,
+            float param, long* correct) {
+  float* ws = N > 4 ? static_cast<float*>(scratch(LOSS_WS, (size_t)loss_workspace_floats(N) * 4)) : nullptr;
+  static unsigned* tickets = nullptr;
+  if (N > 4 && !tickets) {
+    tickets = static_cast<unsigned*>(scratch(TICKETS, 64 * 4));
+    HOST_HIP_CHECK(hipMemset(tickets, 0, 64 * 4));
+  }
+  char* out = static_cast<char*>(scratch(LOSS_OUT, 16));
+  loss_fused(kBF16, pred, target, labels, grad, reinterpret_cast<float*>(out), reinterpret_cast<int*>(out + 8), N, C,
+             kind, param, 1.0f, ws, N > 4 ? tickets : nullptr, S);
+  char host[16];
+  HOST_HIP_CHECK(hipMemcpy(host, out, 16, hipMemcpyDeviceToHost));
+  float l;
+  int c;
+  std::memcpy(&l, host, 4);
+  std::memcpy(&c, host + 8, 4);
+  if (correct) *correct = c;
+  return l;
+}
+
+void groupnorm_fwd(const void* x, void* y, int N, int HW, int C, int G, const float* g, const float* b, float eps,
+                   float* smean, float* sistd) {
+  gn_fwd(kBF16, x, y, N, HW, C, G, g, b, eps, smean, sistd, S);
+}
+
+void groupnorm_bwd(const void* dy, const void* x, void* dx, int N, int HW, int C, int G, const float* g,
+                   const float* mean, const float* istd, float* dg, float* db) {
+  float* aff = static_cast<float*>(scratch(GN_AFF, (size_t)N * 2 * C * 4));  // per-image affine partials
+  gn_bwd(kBF16, dy, x, dx, N, HW, C, G, g, mean, istd, dg, db, aff, S);
+}
+
+void softmax_fwd(const void* x, void* y, long rows, int C) { softmax_rows(kBF16, x, y, rows, C, S); }
+void softmax_bwd(const void* y, const void* dy, void* dx, long rows, int C) {
+  softmax_rows_bwd(kBF16, y, dy, dx, rows, C, S);
+}
+void dropout(const void* x, void* y, long n, float p, uint64_t seed) { dcnn::dropout(kBF16, x, y, n, p, seed, nullptr, S); }
+
+void add(const void* a, const void* b, void* y, long n, bool relu) {
+  hipLaunchKernelGGL(add_bf16_kernel, dim3(grid_of(n)), dim3(256), 0, S, static_cast<const bf16*>(a),
+                     static_cast<const bf16*>(b), static_cast<bf16*>(y), n, relu ? 1 : 0);
+  HOST_HIP_CHECK(hipGetLastError());
+}
+
+void relu_mask(const void* dy, const void* y, void* dx, long n) {
+  hipLaunchKernelGGL(relu_mask_bf16_kernel, dim3(grid_of(n)), dim3(256), 0, S, static_cast<const bf16*>(dy),
+                     static_cast<const bf16*>(y), static_cast<bf16*>(dx), n);
+  HOST_HIP_CHECK(hipGetLastError());
 }
 
 void adam(float* p, const float* g, float* m, float* v, void* shadow, long n, float lr, float b1, float b2, float eps,

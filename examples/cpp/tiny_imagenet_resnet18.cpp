@@ -1,0 +1,132 @@
+// ResNet-18 (or -34 / -50 / ResNet-9) on Tiny-ImageNet trained from C++ on the dcnn host API —
+// residual blocks, the routed MFMA conv kernels, a scheduler and a loss of the factories; no Python.
+//
+//   dcnn_amd/bin/tiny_imagenet_resnet18 [--device CPU|GPU] [--model resnet18_tiny_imagenet]
+//        [--data data/tiny-imagenet-200] [--epochs E] [--steps S] [--batch B] [--lr 1e-3]
+//        [--loss logsoftmax_ce] [--scheduler cosine_annealing_lr] [--max-per-class K]
+//        [--save model_snapshots/resnet18] [--bench]
+//
+// Without --data it trains on a learnable synthetic 3x64x64 200-class set. --bench times
+// --steps training steps after 3 warm-up steps and prints one JSON line (images/sec). The saved
+// model (path.json + path.bin + path.bnstats) loads in Python with Sequential.from_file.
+// Honours the reference's .env keys DEVICE_TYPE / EPOCHS / BATCH_SIZE / LR_INITIAL.
+// Reference parity: examples/tiny_imagenet_resnet18.cpp:23-107 (Adam, logsoftmax-CE, profiling),
+// include/nn/example_models.hpp:306-331 (the model).
+#include <chrono>
+#include <cstdio>
+#include <cstdlib>
+#include <iostream>
+#include <memory>
+#include <string>
+
+#include "dcnn/nn.hpp"
+#include "dcnn/train.hpp"
+
+using namespace dcnn;
+
+namespace {
+std::string env_or(const char* k, const std::string& d) {
+  const char* v = std::getenv(k);
+  return v && *v ? v : d;
+}
+}  // namespace
+
+int main(int argc, char** argv) {
+  std::string device = env_or("DEVICE_TYPE", "CPU"), data, save, model_name = "resnet18_tiny_imagenet";
+  std::string loss_name = "logsoftmax_ce", sched_name;
+  int epochs = std::atoi(env_or("EPOCHS", "1").c_str()), steps = -1, max_per_class = 0;
+  int batch = std::atoi(env_or("BATCH_SIZE", "64").c_str());
+  float lr = std::atof(env_or("LR_INITIAL", "0.001").c_str());
+  bool bench = false;
+  for (int i = 1; i < argc; ++i) {
+    const std::string k = argv[i];
+    if (k == "--bench") { bench = true; continue; }
+    if (i + 1 >= argc) break;
+    const std::string v = argv[++i];
+    if (k == "--device") device = v;
+    else if (k == "--model") model_name = v;
+    else if (k == "--data") data = v;
+    else if (k == "--epochs") epochs = std::atoi(v.c_str());
+    else if (k == "--steps") steps = std::atoi(v.c_str());
+    else if (k == "--batch") batch = std::atoi(v.c_str());
+    else if (k == "--lr") lr = std::atof(v.c_str());
+    else if (k == "--loss") loss_name = v;
+    else if (k == "--scheduler") sched_name = v;
+    else if (k == "--max-per-class") max_per_class = std::atoi(v.c_str());
+    else if (k == "--save") save = v;
+  }
+  try {
+    Sequential model = create_model(model_name);
+    const Device dev = Device::parse(device);
+    model.set_device(dev);
+    model.initialize(42);
+    std::printf("%s on %s: %zu parameters\n", model.name().c_str(), dev.str().c_str(), model.num_parameters());
+    Adam opt(lr);
+    Loss loss = LossFactory::create(loss_name);
+    const bool cifar = model_name.find("cifar") != std::string::npos;
+    const int C = 3, HW = cifar ? 32 : 64, classes = cifar ? 10 : 200;
+    std::unique_ptr<DataSource> train, val;
+    if (!data.empty()) {
+      auto tr = std::make_unique<ImageDataset>(load_tiny_imagenet(data, "train", max_per_class, 1));
+      tr->set_random_flip(0.5f);
+      train = std::move(tr);
+      val = std::make_unique<ImageDataset>(load_tiny_imagenet(data, "val", 0, 2));
+    } else {
+      train = std::make_unique<SyntheticClassification>(bench ? (size_t)batch * (steps + 4) : (size_t)4 * batch, C, HW,
+                                                        HW, classes, 7, 0.5f);
+      val = std::make_unique<SyntheticClassification>((size_t)batch, C, HW, HW, classes, 7, 0.5f);
+    }
+    if (bench) {
+      // steady-state throughput: warm-up steps (kernel instances, workspaces), then timed steps
+      train->reset(0);
+      Tensor x, y;
+      const int timed = steps > 0 ? steps : 20;
+      auto one = [&] {
+        if (!train->next(batch, x, y)) {
+          train->reset(1);
+          train->next(batch, x, y);
+        }
+        model.zero_grad();
+        Tensor logits = model.forward(x);
+        LossResult r = loss(logits, y);
+        model.backward(r.grad);
+        opt.step(model.parameters());
+        return r.loss;
+      };
+      for (int i = 0; i < 3; ++i) one();
+      if (dev.is_gpu()) gpu::synchronize();
+      const auto t0 = std::chrono::steady_clock::now();
+      double last = 0;
+      for (int i = 0; i < timed; ++i) last = one();
+      if (dev.is_gpu()) gpu::synchronize();
+      const double s = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+      std::printf("{\"metric\": \"images/sec %s training (C++ host API)\", \"value\": %.1f, \"ms_per_step\": %.3f, "
+                  "\"batch\": %d, \"steps\": %d, \"device\": \"%s\", \"loss\": %.4f}\n",
+                  model_name.c_str(), (double)batch * timed / s, 1e3 * s / timed, batch, timed, dev.str().c_str(),
+                  last);
+      return 0;
+    }
+    std::unique_ptr<Scheduler> sched;
+    if (!sched_name.empty()) {
+      json::Value p = json::Value::object();
+      const long total = (long)epochs * (long)(steps > 0 ? steps : (long)(train->size() / batch));
+      p["T_max"] = (int64_t)std::max(1l, total);
+      p["total_steps"] = (int64_t)std::max(1l, total);
+      sched = SchedulerFactory::create(sched_name, &opt, p);
+    }
+    TrainingConfig cfg;
+    cfg.epochs = epochs;
+    cfg.batch_size = batch;
+    cfg.max_steps = steps;
+    cfg.progress_interval = 20;
+    train_model(model, *train, val.get(), opt, loss, cfg, sched.get());
+    if (!save.empty()) {
+      model.save_to_file(save);
+      std::printf("saved %s.json / .bin / .bnstats\n", save.c_str());
+    }
+  } catch (const std::exception& e) {
+    std::cerr << "error: " << e.what() << std::endl;
+    return 1;
+  }
+  return 0;
+}
