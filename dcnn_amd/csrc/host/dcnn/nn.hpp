@@ -20,6 +20,7 @@
 // include/nn/loss.hpp, examples/mnist_cnn_trainer.cpp.
 #pragma once
 #include <functional>
+#include <map>
 #include <memory>
 #include <string>
 #include <vector>
@@ -64,8 +65,22 @@ class Layer {
   std::vector<Param>& params() { return params_; }
   const std::string& name() const { return name_; }
   Device device() const { return dev_; }
+  // micro-batch whose forward state the next forward / backward call uses: every layer keeps its
+  // forward caches per micro-batch (the reference's unordered_map<size_t, ...> caches), so a
+  // pipeline stage can hold several micro-batches in flight (semi-async, 1F1B)
+  virtual void set_micro_batch(int mb) { mb_ = mb; }
+  void clear_caches() { caches_.clear(); }
 
  protected:
+  struct MbCache {
+    Tensor a, b, c;
+    std::vector<int64_t> shape;
+    uint64_t u = 0;
+    bool flag = false;
+  };
+  MbCache& mbc() { return caches_[mb_]; }
+  std::map<int, MbCache> caches_;
+  int mb_ = 0;
   Param& add_param(const std::string& n, const std::vector<int64_t>& shape, Layout phys, const std::vector<float>& init);
   std::string name_;
   Device dev_ = Device::cpu();
@@ -87,7 +102,6 @@ class Conv2D : public Layer {
   ConvShape shape_for(const std::vector<int64_t>& in) const;
   int ci_, co_, kh_, kw_, sh_, sw_, ph_, pw_;
   bool bias_;
-  Tensor x_;
 };
 
 class Dense : public Layer {
@@ -103,7 +117,6 @@ class Dense : public Layer {
  private:
   int in_, out_;
   bool bias_;
-  Tensor x_;
 };
 
 class BatchNorm : public Layer {
@@ -123,7 +136,6 @@ class BatchNorm : public Layer {
   float eps_, momentum_;
   bool affine_;
   bool train_ = true;
-  Tensor x_, mean_, istd_;
 };
 
 // activation kinds: relu, leaky_relu (0.01), elu (alpha 1), sigmoid, tanh, linear, softmax (over the
@@ -140,7 +152,6 @@ class Activation : public Layer {
  private:
   std::string kind_;
   int code_;
-  Tensor x_, y_;
 };
 
 // GroupNorm over G channel groups per image; gamma / beta per channel
@@ -160,7 +171,7 @@ class GroupNorm : public Layer {
   float eps_;
   bool affine_;
   bool gb_identity_ = false;
-  Tensor x_, mean_, istd_, ident_, scratch_;
+  Tensor ident_, scratch_;
 };
 
 // inverted dropout (scale 1 / (1 - p)), identity in eval; the mask is a counter-based function
@@ -177,8 +188,7 @@ class Dropout : public Layer {
 
  private:
   float p_;
-  uint64_t seed_ = 0, draw_ = 0, cur_ = 0;
-  bool active_ = false;
+  uint64_t seed_ = 0, draw_ = 0;
 };
 
 class Pool2D : public Layer {
@@ -194,8 +204,6 @@ class Pool2D : public Layer {
   PoolShape shape_for(const std::vector<int64_t>& in) const;
   bool max_;
   int kh_, kw_, sh_, sw_, ph_, pw_;
-  std::vector<int64_t> in_shape_;
-  Tensor idx_;
 };
 
 class Flatten : public Layer {
@@ -206,9 +214,6 @@ class Flatten : public Layer {
   std::vector<int64_t> output_shape(const std::vector<int64_t>& in) const override;
   Tensor forward(const Tensor& x, bool training) override;
   Tensor backward(const Tensor& dy) override;
-
- private:
-  std::vector<int64_t> in_shape_;
 };
 
 // out = act(F(x) + S(x)): F the main path, S the projection shortcut (identity when empty).
@@ -228,13 +233,13 @@ class ResidualBlock : public Layer {
   void sync_shadow() override;
   void collect_params(std::vector<Param*>& out) override;
   void collect_layers(std::vector<Layer*>& out) override;
+  void set_micro_batch(int mb) override;
   const std::vector<std::unique_ptr<Layer>>& main_path() const { return main_; }
   const std::vector<std::unique_ptr<Layer>>& shortcut_path() const { return short_; }
 
  private:
   std::vector<std::unique_ptr<Layer>> main_, short_;
   std::string act_;
-  Tensor y_;
 };
 
 // layer from its JSON record {"type", "name", "parameters"} (the LayerFactory of the formats)
@@ -253,8 +258,14 @@ class Sequential {
   void set_training(bool t) { training_ = t; }
   bool is_training() const { return training_; }
   // x: fp32 logical NCHW (host or device); returns the logits [N, classes] as a device tensor
-  Tensor forward(const Tensor& x);
-  void backward(const Tensor& dlogits);
+  Tensor forward(const Tensor& x, int mb = 0);
+  void backward(const Tensor& dlogits, int mb = 0);
+  // one partition of a pipeline: activations in the device layout in and out (GPU: bf16 NHWC,
+  // CPU: fp32 NCHW); backward returns the input gradient in the same layout
+  Tensor forward_activation(const Tensor& x, int mb);
+  Tensor backward_activation(const Tensor& g, int mb);
+  // the network input (fp32 NCHW, any device) as the first layer's activation
+  Tensor input_activation(const Tensor& x) const;
   std::vector<Param*> parameters();
   // every BatchNorm, depth-first through residual blocks (the .bnstats record order)
   std::vector<BatchNorm*> batchnorms();

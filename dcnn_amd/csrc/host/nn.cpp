@@ -143,6 +143,7 @@ void Conv2D::build(const std::vector<int64_t>& in, Device dev, uint64_t seed) {
 
 Tensor Conv2D::forward(const Tensor& x, bool training) {
   (void)training;
+  Tensor& x_ = mbc().a;
   check_act(x, dev_, "conv2d");
   const ConvShape s = shape_for(x.shape());
   Tensor y = act_empty({s.N, s.Co, s.OH, s.OW}, dev_);
@@ -156,6 +157,7 @@ Tensor Conv2D::forward(const Tensor& x, bool training) {
 }
 
 Tensor Conv2D::backward(const Tensor& dy) {
+  const Tensor& x_ = mbc().a;
   const ConvShape s = shape_for(x_.shape());
   Tensor dx = act_empty(x_.shape(), dev_);
   float* gb = bias_ ? params_[1].grad.ptr<float>() : nullptr;
@@ -200,6 +202,7 @@ void Dense::build(const std::vector<int64_t>& in, Device dev, uint64_t seed) {
 
 Tensor Dense::forward(const Tensor& x, bool training) {
   (void)training;
+  Tensor& x_ = mbc().a;
   check_act(x, dev_, "dense");
   const int N = (int)x.dim(0);
   output_shape(x.shape());
@@ -214,6 +217,7 @@ Tensor Dense::forward(const Tensor& x, bool training) {
 }
 
 Tensor Dense::backward(const Tensor& dy) {
+  const Tensor& x_ = mbc().a;
   const int N = (int)x_.dim(0);
   Tensor dx = act_empty(x_.shape(), dev_);
   float* gb = bias_ ? params_[1].grad.ptr<float>() : nullptr;
@@ -251,12 +255,17 @@ void BatchNorm::build(const std::vector<int64_t>& in, Device dev, uint64_t seed)
   }
   running_mean = Tensor::zeros({c_}, DType::F32, dev);
   running_var = Tensor::from_host(std::vector<float>((size_t)c_, 1.f), {c_}, dev);
-  mean_ = Tensor::zeros({c_}, DType::F32, dev);
-  istd_ = Tensor::zeros({c_}, DType::F32, dev);
+  caches_.clear();
 }
 
 Tensor BatchNorm::forward(const Tensor& x, bool training) {
   check_act(x, dev_, "batchnorm");
+  MbCache& mc = mbc();
+  Tensor& x_ = mc.a;
+  Tensor& mean_ = mc.b;
+  Tensor& istd_ = mc.c;
+  mean_.ensure({c_}, DType::F32, dev_);
+  istd_.ensure({c_}, DType::F32, dev_);
   if (x.dim(1) != c_) throw std::runtime_error(name_ + ": channel count mismatch");
   train_ = training;
   const long N = x.dim(0), HW = x.dim(2) * x.dim(3);
@@ -274,6 +283,10 @@ Tensor BatchNorm::forward(const Tensor& x, bool training) {
 }
 
 Tensor BatchNorm::backward(const Tensor& dy) {
+  MbCache& mc = mbc();
+  const Tensor& x_ = mc.a;
+  Tensor& mean_ = mc.b;
+  Tensor& istd_ = mc.c;
   const long N = x_.dim(0), HW = x_.dim(2) * x_.dim(3);
   Tensor dx = act_empty(x_.shape(), dev_);
   const float* g = affine_ ? params_[0].value.ptr<float>() : nullptr;
@@ -302,6 +315,8 @@ static float act_alpha(int code) { return code == ACT_ELU ? 1.0f : 0.01f; }
 
 Tensor Activation::forward(const Tensor& x, bool training) {
   (void)training;
+  Tensor& x_ = mbc().a;
+  Tensor& y_ = mbc().b;
   check_act(x, dev_, "activation");
   Tensor y = act_empty(x.shape(), dev_);
   const long N = x.dim(0), C = x.dim(1), HW = x.dim(2) * x.dim(3);
@@ -322,6 +337,8 @@ Tensor Activation::forward(const Tensor& x, bool training) {
 }
 
 Tensor Activation::backward(const Tensor& dy) {
+  const Tensor& x_ = mbc().a;
+  const Tensor& y_ = mbc().b;
   if (code_ == ACT_SOFTMAX) {
     Tensor dx = act_empty(y_.shape(), dev_);
     const long N = y_.dim(0), C = y_.dim(1), HW = y_.dim(2) * y_.dim(3);
@@ -370,6 +387,10 @@ void GroupNorm::build(const std::vector<int64_t>& in, Device dev, uint64_t seed)
 
 Tensor GroupNorm::forward(const Tensor& x, bool training) {
   (void)training;
+  MbCache& mc = mbc();
+  Tensor& x_ = mc.a;
+  Tensor& mean_ = mc.b;
+  Tensor& istd_ = mc.c;
   check_act(x, dev_, "groupnorm");
   if (x.dim(1) != c_) throw std::runtime_error(name_ + ": channel count mismatch");
   const long N = x.dim(0), HW = x.dim(2) * x.dim(3);
@@ -394,6 +415,10 @@ Tensor GroupNorm::forward(const Tensor& x, bool training) {
 }
 
 Tensor GroupNorm::backward(const Tensor& dy) {
+  MbCache& mc = mbc();
+  const Tensor& x_ = mc.a;
+  Tensor& mean_ = mc.b;
+  Tensor& istd_ = mc.c;
   const long N = x_.dim(0), HW = x_.dim(2) * x_.dim(3);
   Tensor dx = act_empty(x_.shape(), dev_);
   const float* g = affine_ ? params_[0].value.ptr<float>() : ident_.ptr<float>();
@@ -428,6 +453,8 @@ void Dropout::build(const std::vector<int64_t>& in, Device dev, uint64_t seed) {
 
 Tensor Dropout::forward(const Tensor& x, bool training) {
   check_act(x, dev_, "dropout");
+  uint64_t& cur_ = mbc().u;
+  bool& active_ = mbc().flag;
   active_ = training && p_ > 0.f;
   if (!active_) return x;
   cur_ = seed_ + 0x9e3779b97f4a7c15ull * (++draw_);  // a new mask per forward
@@ -440,6 +467,8 @@ Tensor Dropout::forward(const Tensor& x, bool training) {
 }
 
 Tensor Dropout::backward(const Tensor& dy) {
+  const uint64_t cur_ = mbc().u;
+  const bool active_ = mbc().flag;
   if (!active_) return dy;
   Tensor dx = act_empty(dy.shape(), dev_);
   if (dev_.is_gpu())
@@ -501,6 +530,7 @@ void ResidualBlock::build(const std::vector<int64_t>& in, Device dev, uint64_t s
 
 Tensor ResidualBlock::forward(const Tensor& x, bool training) {
   check_act(x, dev_, "residual_block");
+  Tensor& y_ = mbc().a;
   Tensor m = x;
   for (auto& l : main_) m = l->forward(m, training);
   Tensor sc = x;
@@ -518,6 +548,7 @@ Tensor ResidualBlock::forward(const Tensor& x, bool training) {
 }
 
 Tensor ResidualBlock::backward(const Tensor& dy) {
+  const Tensor& y_ = mbc().a;
   Tensor g = dy;
   if (act_ == "relu") {
     g = act_empty(dy.shape(), dev_);
@@ -536,6 +567,12 @@ Tensor ResidualBlock::backward(const Tensor& dy) {
   else
     cpu_ops::add(gm.ptr<float>(), gs.ptr<float>(), dx.ptr<float>(), dx.numel(), false);
   return dx;
+}
+
+void ResidualBlock::set_micro_batch(int mb) {
+  mb_ = mb;
+  for (auto& l : main_) l->set_micro_batch(mb);
+  for (auto& l : short_) l->set_micro_batch(mb);
 }
 
 void ResidualBlock::sync_shadow() {
@@ -594,6 +631,8 @@ std::vector<int64_t> Pool2D::output_shape(const std::vector<int64_t>& in) const 
 
 Tensor Pool2D::forward(const Tensor& x, bool training) {
   (void)training;
+  Tensor& idx_ = mbc().a;
+  std::vector<int64_t>& in_shape_ = mbc().shape;
   check_act(x, dev_, "pool2d");
   const PoolShape p = shape_for(x.shape());
   Tensor y = act_empty({p.N, p.C, p.OH, p.OW}, dev_);
@@ -616,6 +655,8 @@ Tensor Pool2D::forward(const Tensor& x, bool training) {
 }
 
 Tensor Pool2D::backward(const Tensor& dy) {
+  const Tensor& idx_ = mbc().a;
+  const std::vector<int64_t>& in_shape_ = mbc().shape;
   const PoolShape p = shape_for(in_shape_);
   Tensor dx = act_empty(in_shape_, dev_);
   if (max_) {
@@ -638,6 +679,7 @@ std::vector<int64_t> Flatten::output_shape(const std::vector<int64_t>& in) const
 
 Tensor Flatten::forward(const Tensor& x, bool training) {
   (void)training;
+  std::vector<int64_t>& in_shape_ = mbc().shape;
   check_act(x, dev_, "flatten");
   in_shape_ = x.shape();
   const auto os = output_shape(x.shape());
@@ -650,6 +692,7 @@ Tensor Flatten::forward(const Tensor& x, bool training) {
 }
 
 Tensor Flatten::backward(const Tensor& dy) {
+  const std::vector<int64_t>& in_shape_ = mbc().shape;
   const int64_t HW = in_shape_[2] * in_shape_[3];
   if (!dev_.is_gpu()) return dy.view(in_shape_);
   if (HW == 1) return dy.view(in_shape_, Layout::NHWC);
@@ -763,8 +806,7 @@ void Sequential::zero_grad() {
   }
 }
 
-Tensor Sequential::forward(const Tensor& x_in) {
-  if (!initialized_) throw std::runtime_error("Sequential::forward before initialize()");
+Tensor Sequential::input_activation(const Tensor& x_in) const {
   if (x_in.rank() != 4 || x_in.dtype() != DType::F32) throw std::runtime_error("forward: expected fp32 (N, C, H, W)");
   Tensor x = x_in.device() == dev_ ? x_in : x_in.to(dev_);
   if (dev_.is_gpu()) {
@@ -772,13 +814,36 @@ Tensor Sequential::forward(const Tensor& x_in) {
     gpu_ops::input_to_nhwc(x.ptr<float>(), a.data(), (int)x.dim(0), (int)x.dim(1), (int)(x.dim(2) * x.dim(3)));
     x = a;
   }
-  for (auto& l : layers_) x = l->forward(x, training_);
+  return x;
+}
+
+Tensor Sequential::forward_activation(const Tensor& x_in, int mb) {
+  if (!initialized_) throw std::runtime_error("Sequential::forward before initialize()");
+  Tensor x = x_in;
+  for (auto& l : layers_) {
+    l->set_micro_batch(mb);
+    x = l->forward(x, training_);
+  }
+  return x;
+}
+
+Tensor Sequential::backward_activation(const Tensor& g_in, int mb) {
+  Tensor g = g_in;
+  for (size_t i = layers_.size(); i-- > 0;) {
+    layers_[i]->set_micro_batch(mb);
+    g = layers_[i]->backward(g);
+  }
+  return g;
+}
+
+Tensor Sequential::forward(const Tensor& x_in, int mb) {
+  Tensor x = forward_activation(input_activation(x_in), mb);
   return x.view({x.dim(0), x.dim(1) * x.dim(2) * x.dim(3)}, x.layout());
 }
 
-void Sequential::backward(const Tensor& dlogits) {
+void Sequential::backward(const Tensor& dlogits, int mb) {
   Tensor g = dlogits.view({dlogits.dim(0), dlogits.dim(1), 1, 1}, dev_.is_gpu() ? Layout::NHWC : Layout::NCHW);
-  for (size_t i = layers_.size(); i-- > 0;) g = layers_[i]->backward(g);
+  backward_activation(g, mb);
 }
 
 json::Value Sequential::get_config() const {
