@@ -155,9 +155,11 @@ struct H3 {
   static_assert(LDS <= 163840, "LDS budget");
 };
 
-// EPI: epilogue specialisation (compile-time, so the common cases carry no per-option branches
-// or selects): 1 = forward with BatchNorm statistics and no bias / residual / ReLU; 2 = data
-// gradient with the backward-BatchNorm fusion (optional residual); 0 = any option at run time.
+// EPI: epilogue specialisation (compile-time: whether statistics rows are produced, and of which
+// kind, is never a run-time branch): 0 = no statistics (bias / residual / ReLU at run time);
+// 1 = forward BatchNorm statistics, no bias / residual / ReLU; 2 = data gradient with the
+// backward-BatchNorm fusion (optional residual); 3 = forward statistics with bias / residual /
+// ReLU at run time.
 // STAMP: diagnostic instance with s_memtime stamps (benchmarks/hconv3_timeline.py).
 template <int NW, int WC, int TWC, int HN, int NWI, int PITCH, int EPI, bool STAMP>
 __global__ void __launch_bounds__(NW * 64, 8 / NW) hconv3_kernel(HConvArgs p, H3Geo g) {
@@ -516,11 +518,10 @@ __global__ void __launch_bounds__(NW * 64, 8 / NW) hconv3_kernel(HConvArgs p, H3
       // channels cb + 32 h + e (e = 0..7) = acc[2h + (e >> 2)][j][e & 3], cb = n0 + wc*64 + 8*lh.
       // Per channel half: operand loads (bias, BN mean / istd, residual, ReLU output, BN input),
       // arithmetic, 4 x 16-byte stores, statistics rows.
-      const bool bnb = EPI == 2 || (EPI == 0 && p.bnb.x != nullptr);
-      const bool stats = EPI != 0 || p.stats != nullptr;
+      constexpr bool bnb = EPI == 2, stats = EPI != 0, opts = EPI == 0 || EPI == 3;
       const bool has_res = EPI != 1 && p.residual != nullptr, has_y = bnb && p.bnb.y != nullptr;
-      const bool has_x = bnb && stats;
-      const bool has_bias = EPI == 0 && p.bias != nullptr, relu = EPI == 0 && p.relu;
+      constexpr bool has_x = bnb;
+      const bool has_bias = opts && p.bias != nullptr, relu = opts && p.relu;
       const int cb = it.n0 + wc * 64 + 8 * lh;
       out_offsets(it, oo);
       const char* rbytes = reinterpret_cast<const char*>(p.residual);
@@ -700,18 +701,22 @@ static void launch_h3e(const HConvArgs& a, const H3Geo& g, hipStream_t s) {
   DCNN_LAUNCH_CHECK();
 }
 
-static int g_h3_epi = [] {  // DCNN_HCONV3_EPI=0: always the generic epilogue (A/B)
-  const char* e = getenv("DCNN_HCONV3_EPI");
-  return e ? atoi(e) : 1;
-}();
+// the epilogue instance for these options (-1: not covered)
+static int h3_epi(const HConvArgs& a) {
+  if (a.bnb.x) return (a.stats && !a.relu && !a.bias) ? 2 : -1;
+  if (!a.stats) return 0;
+  return (a.residual || a.relu || a.bias) ? 3 : 1;
+}
 
 template <int NW, int WC, int TWC, int HN, int NWI, int PITCH>
 static void launch_h3(const HConvArgs& a, const H3Geo& g, hipStream_t s) {
-  if (g.stamps) return launch_h3e<NW, WC, TWC, HN, NWI, PITCH, 0, true>(a, g, s);
-  const bool plain_fwd = a.stats && !a.bnb.x && !a.residual && !a.relu && !a.bias;
-  const bool bnb_dgrad = a.stats && a.bnb.x && !a.relu && !a.bias;
-  if (g_h3_epi && plain_fwd) return launch_h3e<NW, WC, TWC, HN, NWI, PITCH, 1, false>(a, g, s);
-  if (g_h3_epi && bnb_dgrad) return launch_h3e<NW, WC, TWC, HN, NWI, PITCH, 2, false>(a, g, s);
+  const int epi = h3_epi(a);
+  // (timeline instances: the statistics forward and the plain dgrad)
+  if (g.stamps && epi == 1) return launch_h3e<NW, WC, TWC, HN, NWI, PITCH, 1, true>(a, g, s);
+  if (g.stamps && epi == 0) return launch_h3e<NW, WC, TWC, HN, NWI, PITCH, 0, true>(a, g, s);
+  if (epi == 1) return launch_h3e<NW, WC, TWC, HN, NWI, PITCH, 1, false>(a, g, s);
+  if (epi == 2) return launch_h3e<NW, WC, TWC, HN, NWI, PITCH, 2, false>(a, g, s);
+  if (epi == 3) return launch_h3e<NW, WC, TWC, HN, NWI, PITCH, 3, false>(a, g, s);
   launch_h3e<NW, WC, TWC, HN, NWI, PITCH, 0, false>(a, g, s);
 }
 
@@ -724,7 +729,8 @@ static void launch_h3_plan(const H3Plan& pl, const HConvArgs& a, const H3Geo& g,
 // returns false when the shape / taps / epilogue options are not covered (caller falls back)
 bool hconv3_try(const HConvArgs& a0, hipStream_t s) {
   H3Plan pl;
-  if (a0.Cf || a0.fold.part || !hconv3_plan(a0.NB, a0.H, a0.W, a0.Cs, a0.N, a0.ntaps, &pl)) return false;
+  if (a0.Cf || a0.fold.part || h3_epi(a0) < 0 || !hconv3_plan(a0.NB, a0.H, a0.W, a0.Cs, a0.N, a0.ntaps, &pl))
+    return false;
   H3Geo g{};
   for (int t = 0; t < 9; ++t) g.tb[t] = -1;
   for (int t = 0; t < a0.ntaps; ++t) {
