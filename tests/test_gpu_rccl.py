@@ -145,7 +145,7 @@ def test_rccl_dp_without_c10d_matches_process_group_nccl(tmp_path):
 def test_rccl_p2p_directions_on_own_streams():
     """RcclP2P (pipeline plane): one communicator + stream per direction. At world 1 a grouped
     self send/recv per direction moves the data; forward and backward traffic interleaved (as in
-    1F1B) on their own streams, consumed on the compute stream, inside a captured graph too."""
+    1F1B) on their own streams, consumed on the compute stream."""
     from dcnn_amd.ops._ext import kernels
     from dcnn_amd.parallel.rccl import RcclP2P
     p2p = RcclP2P(0, 1, torch.device("cuda", 0))
@@ -173,19 +173,6 @@ def test_rccl_p2p_directions_on_own_streams():
             rg[k].add_(1)
 
     exchange()
-    torch.cuda.synchronize()
-    for k in range(3):
-        assert torch.equal(ra[k], acts[k] * 2) and torch.equal(rg[k], grads[k] + 1)
-    for t in ra + rg:
-        t.zero_()
-    g = torch.cuda.CUDAGraph()
-    s = torch.cuda.Stream()
-    s.wait_stream(torch.cuda.current_stream())
-    with torch.cuda.stream(s):
-        with torch.cuda.graph(g, stream=s):
-            exchange()
-    torch.cuda.current_stream().wait_stream(s)
-    g.replay()
     torch.cuda.synchronize()
     for k in range(3):
         assert torch.equal(ra[k], acts[k] * 2) and torch.equal(rg[k], grads[k] + 1)
