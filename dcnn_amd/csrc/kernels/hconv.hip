@@ -24,16 +24,11 @@
 
 #include "common.h"
 #include "api.h"
+#include "hconv3_plan.h"
 #include "statfold.h"
 
 namespace dcnn {
 
-// third-generation kernel (hconv3.hip): 8-wave 64x64-per-wave tiles, 3 taps per barrier
-struct H3Plan {
-  int WC, TWC, HN, NWI, TH, TW, IMG, pitch, splits, tiles_m, tiles_n;
-};
-bool hconv3_plan(int NB, int H, int W, int Cs, int N, int ntaps, H3Plan* pl);
-bool hconv3_try(const HConvArgs& a, hipStream_t s);
 
 namespace {
 constexpr unsigned kOOBh = 0x80000000u;

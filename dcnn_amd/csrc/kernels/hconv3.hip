@@ -1,19 +1,18 @@
 // Third-generation halo-tiled 3x3 stride-1 convolution (forward and dgrad) for CDNA4:
 // a persistent, cross-tile pipelined kernel.
 //
-// Work item = one output tile (IMG images x TH x TW = 256 pixels, 64 output channels) and, on
-// small grids, one split-K slice of its input channels. The grid is sized to the resident
-// workgroups (2 per CU) and every workgroup walks its items in a strided order, so that:
+// Work item = one 16 x 16 output pixel tile (an image window; on 8 x 8 / 4 x 4 maps a 2 x 2 /
+// 4 x 4 grid of whole images separated by shared zero gutters) x 64 output channels and, on small
+// grids, one split-K slice of its input channels. The grid is sized to the resident workgroups
+// (2 per CU) and every workgroup walks its items in a strided order, so that:
 //
-//  * the next item's first halo chunk and first weight stage are DMA'd into LDS during the
+//  * the next item's first halo chunk and first two weight stages are DMA'd into LDS during the
 //    current item's last K steps (the (item, chunk, kernel-row) sequence is ONE stream: the halo
 //    double buffer and the 2-stage weight ring never restart);
-//  * the current item's output stores are NOT issued in its epilogue: the epilogue computes the
-//    bf16 output rows and the BatchNorm statistics in registers, and the stores go out inside the
-//    next item's first two K steps, behind that step's DMA issue, where the counted vmcnt waits
-//    let them drain under the MFMAs. The chip-wide write burst at the end of every tile round
-//    (profiles/experiment_hconv_variants.md: epilogue phase as long as the K loop) becomes a
-//    trickle beside the matrix work.
+//  * the epilogue stores each 16-byte output row as soon as it is computed, AFTER issuing the
+//    next item's second weight stage: the next item's first K step waits only for the loads
+//    older than the stores, so the stores (and the statistics rows) drain under its MFMAs
+//    instead of stalling the workgroup.
 //
 // Per item the structure is the round-3 one:
 //
@@ -44,6 +43,7 @@
 
 #include "common.h"
 #include "api.h"
+#include "hconv3_plan.h"
 
 namespace dcnn {
 
@@ -131,8 +131,16 @@ __device__ __forceinline__ bf16x8 lds_b128(const char* smem, int off) {
 #define H3L __attribute__((always_inline))
 
 // geometry the launcher computes once per call
+// The output tile is TH x TW (16 x 16) pixels. Maps of 16 x 16 and larger: one image window
+// (GY = GX = 1, IH = TH, IW = TW) at (y0, x0), its halo the neighbouring pixels. Smaller maps
+// (8 x 8, 4 x 4): a GY x GX grid of whole IH x IW images side by side, separated by shared
+// one-pixel zero gutters, so the halo is (TH + GY + 1) x (TW + GX + 1) with the same tap
+// arithmetic (pixel (ty, tx) of the tile sits at halo (ty + ty / IH + 1, tx + tx / IW + 1)).
 struct H3Geo {
-  int TH, TW, IMG, pitch;  // spatial tile IMG x TH x TW pixels; halo row pitch (>= TW + 2)
+  int TH, TW, pitch;       // spatial tile (16 x 16); halo row pitch (>= TW + GX + 1)
+  int GY, GX, IH, IW;      // images per tile along y / x and their size (gutter layout if GY*GX > 1)
+  int lGX, lIH, lIW;       // log2 of GX, IH, IW (powers of two)
+  int tx_tiles, tpi;       // tiles per image row / per image group
   int tiles_n, tiles_m;    // channel tiles (N / BN), pixel tiles
   int nchunk;              // 32-channel chunks per split
   int nitems;              // tiles_m * tiles_n * splits
@@ -188,23 +196,33 @@ __global__ void __launch_bounds__(NW * 64, 8 / NW) hconv3_kernel(HConvArgs p, H3
     for (int i = tid; i < p.zero_n; i += NT) p.zero_ptr[i] = 0.f;
   const i32x4 rsA = raw_rsrc(p.A, p.a_bytes);
   const i32x4 rsB = raw_rsrc(p.B, p.b_bytes);
-  const int tx_tiles = p.W / g.TW, tpi = tx_tiles * (p.H / g.TH);
-  const int HW2 = g.TW + 2, pitch = PITCH > 0 ? PITCH : g.pitch;
-  const int HPI = (g.TH + 2) * pitch;  // halo pixels per image (pitch-padded)
-  const int HPX = g.IMG * HPI;         // halo pixels per tile
-  const int nch = g.nchunk;            // chunks per item (even, or 1: a 32-channel input)
+  const int tx_tiles = g.tx_tiles, tpi = g.tpi;
+  const int pitch = PITCH > 0 ? PITCH : g.pitch;
+  const bool gut = g.GY * g.GX > 1;                     // gutter layout (whole small images)
+  const int HW2 = g.TW + g.GX + 1;                       // halo columns
+  const int HPX = (g.TH + g.GY + 1) * pitch;             // halo pixels per tile (pitch-padded)
+  const int nch = g.nchunk;                              // chunks per item (even, or 1: a 32-channel input)
 
   // ---- halo loader, item-invariant part: instruction k of this wave fills halo pixels
-  // [16(wid*HN + k), +16); lane -> (image, halo row, halo column, chunk slot), packed
+  // [16(wid*HN + k), +16); lane -> (image, row + 1, column + 1 within the image window, chunk
+  // slot), packed; gutters and row padding are never loaded (zero-filled by the buffer range)
   unsigned hpk[HN];
 #pragma unroll
   for (int k = 0; k < HN; ++k) {
     const int P = (wid * HN + k) * 16 + (lane >> 2);
     unsigned v = 0xffffffffu;
     if (P < HPX) {
-      const int im = P / HPI, r = P - im * HPI;
-      const int hy = r / pitch, hx = r - hy * pitch;
-      if (hx < HW2) v = (unsigned)hx | ((unsigned)hy << 8) | ((unsigned)im << 16) | ((unsigned)((lane & 3) ^ h3_swz<TWC>(P)) << 24);
+      const int hy = P / pitch, hx = P - hy * pitch;
+      int cy = hy, cx = hx, im = 0;
+      bool ok = hx < HW2;
+      if (gut) {
+        const int iy = hy / (g.IH + 1), ix = hx / (g.IW + 1);
+        cy = hy - iy * (g.IH + 1);
+        cx = hx - ix * (g.IW + 1);
+        im = iy * g.GX + ix;
+        ok = ok && cy != 0 && cx != 0;
+      }
+      if (ok) v = (unsigned)cx | ((unsigned)cy << 8) | ((unsigned)im << 16) | ((unsigned)((lane & 3) ^ h3_swz<TWC>(P)) << 24);
     }
     hpk[k] = v;
   }
@@ -232,9 +250,9 @@ __global__ void __launch_bounds__(NW * 64, 8 / NW) hconv3_kernel(HConvArgs p, H3
     t.tm = t.lt / g.tiles_n;
     t.n0 = (t.lt - t.tm * g.tiles_n) * BN;
     const int ig = t.tm / tpi, trem = t.tm - ig * tpi;
-    t.y0 = (trem / tx_tiles) * g.TH;
-    t.x0 = (trem % tx_tiles) * g.TW;
-    t.img0 = ig * g.IMG;
+    t.y0 = (trem / tx_tiles) * 16;
+    t.x0 = (trem % tx_tiles) * 16;
+    t.img0 = ig * (g.GY * g.GX);
     t.cbase = t.zs * nch * 32;  // first input channel of this split
     return t;
   };
@@ -298,9 +316,9 @@ __global__ void __launch_bounds__(NW * 64, 8 / NW) hconv3_kernel(HConvArgs p, H3
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
       const int q = wp * 64 + j * 16 + h3_perm<TWC>(lr);  // tile-local output pixel
-      const int tpx = g.TH * g.TW;
-      const int im = q / tpx, r = q - im * tpx;
-      const int P0 = im * HPI + (r / g.TW) * pitch + (r % g.TW) + zero;  // halo pixel of tap (-1, -1)
+      const int ty = q >> 4, tx = q & 15;  // (16 x 16 tiles)
+      // halo pixel of tap (-1, -1) (gutter layout: one gutter row / column per image crossed)
+      const int P0 = (ty + (ty >> g.lIH)) * pitch + tx + (tx >> g.lIW) + zero;
 #pragma unroll
       for (int t = 0; t < NBA; ++t) {
         const int P = P0 + (NBA == 3 ? t : (t / 3) * pitch + (t % 3));
@@ -318,9 +336,10 @@ __global__ void __launch_bounds__(NW * 64, 8 / NW) hconv3_kernel(HConvArgs p, H3
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
       const int q = wp * 64 + j * 16 + h3_perm<TWC>(lr);
-      const int tpx = g.TH * g.TW;
-      const int im = q / tpx, r = q - im * tpx;
-      const unsigned pix = ((unsigned)(t.img0 + im) * p.H + t.y0 + r / g.TW) * p.W + t.x0 + r % g.TW;
+      const int ty = q >> 4, tx = q & 15;
+      const int iy = ty >> g.lIH, ix = tx >> g.lIW;  // (0, 0) unless gutter layout
+      const unsigned pix = ((unsigned)(t.img0 + (iy << g.lGX) + ix) * p.H + t.y0 + ty - (iy << g.lIH)) * p.W + t.x0 +
+                           tx - (ix << g.lIW);
       oo[j] = (pix * (unsigned)p.N + t.n0 + wc * 64 + 8 * lh) * 2u;
     }
   };
@@ -463,22 +482,20 @@ __global__ void __launch_bounds__(NW * 64, 8 / NW) hconv3_kernel(HConvArgs p, H3
     bool run_epi = true;
     // ---------------------------------------------------------------- split-K hand-off
     if (SPL > 1) {
-      // every partial leaves with agent-scope (sc1) 8-byte stores, each wave drains them, one lane
-      // adds to the tile's ticket behind the workgroup barrier, and the workgroup whose add returns
-      // SPL - 1 reads all partials back with sc1 loads and sums them in split order
-      constexpr int E2 = 32;  // float2 pairs per lane
-      unsigned long long* part = reinterpret_cast<unsigned long long*>(p.part) + (size_t)it.lt * SPL * E2 * NT;
+      // every partial leaves with agent-scope (sc1) 16-byte buffer stores ([split][tile i, j][lane]
+      // per output tile: one 4 KB row per instruction), each wave drains them, one lane adds to the
+      // tile's ticket behind the workgroup barrier, and the workgroup whose add returns SPL - 1
+      // reads the partials back with sc1 loads (16 in flight per split) and sums them in split order
+      const __amdgpu_buffer_rsrc_t rsP = __builtin_amdgcn_make_buffer_rsrc(
+          p.part + (size_t)it.lt * SPL * 16 * NT * 4, 0, SPL * 16 * NT * 16, 0x00020000);
+      constexpr int kSC1 = 16;  // cache policy: sc1 (agent-coherent)
+      using u32x4 = __attribute__((ext_vector_type(4))) unsigned;
 #pragma unroll
       for (int i = 0; i < 4; ++i)
 #pragma unroll
         for (int j = 0; j < 4; ++j)
-#pragma unroll
-          for (int h = 0; h < 2; ++h) {
-            const int e2 = (i * 4 + j) * 2 + h;
-            const unsigned long long bits = (unsigned long long)__float_as_uint(acc[i][j][2 * h]) |
-                                            ((unsigned long long)__float_as_uint(acc[i][j][2 * h + 1]) << 32);
-            __hip_atomic_store(part + ((size_t)it.zs * E2 + e2) * NT + tid, bits, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-          }
+          __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, acc[i][j]), rsP,
+                                                 ((it.zs * 16 + i * 4 + j) * NT + tid) * 16, 0, kSC1);
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       __syncthreads();
       if (tid == 0) {
@@ -496,18 +513,14 @@ __global__ void __launch_bounds__(NW * 64, 8 / NW) hconv3_kernel(HConvArgs p, H3
 #pragma unroll
           for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
         for (int z = 0; z < SPL; ++z) {
+          f32x4 t[16];
+#pragma unroll
+          for (int k = 0; k < 16; ++k)
+            t[k] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(rsP, ((z * 16 + k) * NT + tid) * 16, 0, kSC1));
 #pragma unroll
           for (int i = 0; i < 4; ++i)
 #pragma unroll
-            for (int j = 0; j < 4; ++j)
-#pragma unroll
-              for (int h = 0; h < 2; ++h) {
-                const int e2 = (i * 4 + j) * 2 + h;
-                const unsigned long long bits =
-                    __hip_atomic_load(part + ((size_t)z * E2 + e2) * NT + tid, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                acc[i][j][2 * h] += __uint_as_float((unsigned)bits);
-                acc[i][j][2 * h + 1] += __uint_as_float((unsigned)(bits >> 32));
-              }
+            for (int j = 0; j < 4; ++j) acc[i][j] += t[i * 4 + j];
         }
       }
     }
@@ -640,30 +653,30 @@ void hconv3_set_stamps(uintptr_t p) { g_h3_stamps = reinterpret_cast<unsigned lo
 static int g_h3_grid_cap = 0;  // test hook: at most this many persistent workgroups (0: resident count)
 void hconv3_set_grid_cap(int n) { g_h3_grid_cap = n < 0 ? 0 : n; }
 
-struct H3Plan {
-  int WC, TWC, HN, NWI, TH, TW, IMG, pitch, splits, tiles_m, tiles_n;
-};
-
 // tile plan for a 3x3 stride-1 conv of NB x H x W pixels, Cs input / N output channels
 bool hconv3_plan(int NB, int H, int W, int Cs, int N, int ntaps, H3Plan* pl) {
   // an even 32-channel chunk count (split-K pairs), or one chunk (32 input channels: ResNet-18's
   // first residual conv)
   if (!g_h3 || ntaps != 9 || (Cs % 64 && Cs != 32) || N % 64) return false;
-  // 16-wide (and wider) maps: 4-wave workgroups of 64 channels x one 16x16 tile, two per CU
-  // (LDS 72 KB). 8x8 maps (DCNN_HCONV3_8=1, experiment): 4 images of 8x8 per tile, halo pitch 10.
-  static const int on8 = [] { const char* e = getenv("DCNN_HCONV3_8"); return e ? atoi(e) : 0; }();
-  const bool m8 = on8 && W == 8 && H == 8 && NB % 4 == 0;
-  if (!m8 && (W % 16 || H % 16)) return false;
-  const int WC = 1, NW = 4, BN = 64, BM = 256;
-  const int TW = m8 ? 8 : 16, TWC = TW, TH = m8 ? 8 : 16, IMG = m8 ? 4 : 1;
-  const int NWI = (3 * BN / 16 + NW - 1) / NW;
-  const int pitch = TW + 2;
-  const int HN = (IMG * (TH + 2) * pitch + 16 * NW - 1) / (16 * NW);
-  // the instances: <4, 1, 16, 6, 3, 0> (16-wide maps), <4, 1, 8, 7, 3, 0> (8x8 maps)
-  if (!((TWC == 16 && HN == 6) || (TWC == 8 && HN == 7)) || NWI != 3) return false;
-  pl->WC = WC; pl->TWC = TWC; pl->HN = HN; pl->NWI = NWI;
-  pl->TH = TH; pl->TW = TW; pl->IMG = IMG; pl->pitch = pitch;
-  pl->tiles_m = NB * H * W / BM;
+  // 4-wave workgroups of 64 output channels x one 16 x 16 pixel tile, two per CU. Maps of 16 x 16
+  // and larger (multiples of 16): image windows, halo 18 x 18 (pitch 18, 6 DMA instructions per
+  // wave and chunk, LDS 72 KB). 8 x 8 maps: 2 x 2 images per tile, halo 19 x 19 (6 instructions);
+  // 4 x 4 maps: 4 x 4 images, halo 21 x 21 (7 instructions, LDS 80 KB).
+  constexpr int NW = 4, BN = 64, TH = 16, TW = 16;
+  int GY = 1, GX = 1;
+  if (H == 8 && W == 8) GY = GX = 2;
+  else if (H == 4 && W == 4) GY = GX = 4;
+  else if (H % TH || W % TW) return false;
+  if (NB % (GY * GX)) return false;
+  pl->TH = TH; pl->TW = TW; pl->GY = GY; pl->GX = GX;
+  pl->IH = GY > 1 ? H : TH;
+  pl->IW = GX > 1 ? W : TW;
+  pl->pitch = TW + GX + 1;
+  pl->HN = ((TH + GY + 1) * pl->pitch + 16 * NW - 1) / (16 * NW);
+  if (pl->HN != 6 && pl->HN != 7) return false;  // the compiled instances
+  pl->tx_tiles = GX > 1 ? 1 : W / TW;
+  pl->tpi = GX > 1 ? 1 : (W / TW) * (H / TH);
+  pl->tiles_m = NB * H * W / (TH * TW);
   pl->tiles_n = N / BN;
   // split-K over 32-channel chunks until the grid holds the target workgroup count (two resident
   // per CU), keeping an even chunk count per split
@@ -721,8 +734,8 @@ static void launch_h3(const HConvArgs& a, const H3Geo& g, hipStream_t s) {
 }
 
 static void launch_h3_plan(const H3Plan& pl, const HConvArgs& a, const H3Geo& g, hipStream_t s) {
-  if (pl.WC == 1 && pl.TWC == 16 && pl.HN == 6 && pl.NWI == 3) return launch_h3<4, 1, 16, 6, 3, 0>(a, g, s);
-  if (pl.WC == 1 && pl.TWC == 8 && pl.HN == 7 && pl.NWI == 3) return launch_h3<4, 1, 8, 7, 3, 0>(a, g, s);
+  if (pl.HN == 6) return launch_h3<4, 1, 16, 6, 3, 0>(a, g, s);
+  if (pl.HN == 7) return launch_h3<4, 1, 16, 7, 3, 0>(a, g, s);
   throw std::runtime_error("hconv3: no kernel instance for this plan");
 }
 
@@ -745,7 +758,10 @@ bool hconv3_try(const HConvArgs& a0, hipStream_t s) {
   HConvArgs a = a0;
   if (a.splits != pl.splits) throw std::runtime_error("hconv3: split count mismatch (use hconv_splits)");
   if (pl.splits > 1 && (!a.part || !a.tickets)) throw std::runtime_error("hconv3: split-K workspace missing");
-  g.TH = pl.TH; g.TW = pl.TW; g.IMG = pl.IMG; g.pitch = pl.pitch;
+  g.TH = pl.TH; g.TW = pl.TW; g.pitch = pl.pitch;
+  g.GY = pl.GY; g.GX = pl.GX; g.IH = pl.IH; g.IW = pl.IW;
+  g.lGX = __builtin_ctz(pl.GX); g.lIH = __builtin_ctz(pl.IH); g.lIW = __builtin_ctz(pl.IW);
+  g.tx_tiles = pl.tx_tiles; g.tpi = pl.tpi;
   g.tiles_n = pl.tiles_n; g.tiles_m = pl.tiles_m;
   g.nchunk = a.Cs / 32 / pl.splits;
   g.nitems = pl.tiles_m * pl.tiles_n * pl.splits;

@@ -4,7 +4,6 @@ the same op and against the previous-generation kernel (hconv3_enable(0)) on eve
 geometry, with every epilogue option (bias, residual, ReLU, forward BN statistics, backward-BN
 fusion) and split-K."""
 import math
-import os
 
 import pytest
 import torch
@@ -29,9 +28,10 @@ def hip():
 # (several 16x16 tiles per image, 64-channel tiles, split-K on the small grids)
 CASES = [(4, 64, 32, 32, 64), (2, 64, 32, 64, 64), (4, 128, 16, 16, 128), (2, 64, 16, 16, 64),
          (4, 64, 16, 16, 128), (2, 256, 16, 16, 256), (64, 64, 32, 32, 64), (4, 512, 16, 16, 128),
-         (4, 32, 32, 32, 64)]  # 32 input channels: one chunk
-if os.environ.get("DCNN_HCONV3_8") == "1":  # 8x8 maps: 4 images per tile (experiment instance)
-    CASES += [(4, 256, 8, 8, 256), (8, 128, 8, 8, 64), (16, 512, 8, 8, 256), (64, 256, 8, 8, 256)]
+         (4, 32, 32, 32, 64),  # 32 input channels: one chunk
+         # small maps in the gutter layout: 2 x 2 images of 8 x 8 / 4 x 4 images of 4 x 4 per tile
+         (4, 256, 8, 8, 256), (8, 128, 8, 8, 64), (64, 256, 8, 8, 256), (16, 512, 4, 4, 512),
+         (32, 256, 4, 4, 128), (64, 512, 4, 4, 512)]
 
 
 def _both(K, fn):
@@ -123,6 +123,14 @@ def test_hconv3_dgrad_bn_fusion(hip, case):
     assert rel_err(m1, m0) < 1e-6
 
 
+def test_hconv3_small_maps_need_whole_image_groups(hip):
+    """8 x 8 / 4 x 4 maps run as 2 x 2 / 4 x 4 image grids: a batch that does not fill the grid
+    stays on the previous kernel."""
+    K = hip.kernels()
+    assert K.hconv_v3(8, 8, 8, 64, 64, 9) and not K.hconv_v3(6, 8, 8, 64, 64, 9)
+    assert K.hconv_v3(16, 4, 4, 64, 64, 9) and not K.hconv_v3(8, 4, 4, 64, 64, 9)
+
+
 def test_hconv3_split_k_matches_unsplit(hip):
     """A deep small grid: split-K (partials summed in split order by the tile's last workgroup) vs
     one workgroup per tile; repeated split launches bit-identical."""
@@ -157,7 +165,8 @@ def grid_cap(hip):
 
 @pytest.mark.parametrize("cap", [1, 3, 7])
 @pytest.mark.parametrize("case", [(4, 64, 32, 32, 64), (4, 128, 16, 16, 128), (2, 256, 16, 16, 256),
-                                  (4, 512, 16, 16, 128), (4, 32, 32, 32, 64)])
+                                  (4, 512, 16, 16, 128), (4, 32, 32, 32, 64), (16, 256, 8, 8, 256),
+                                  (32, 512, 4, 4, 512)])
 def test_hconv3_persistent_items_match(hip, grid_cap, case, cap):
     """Few workgroups walking many items (cross-item halo / weight prefetch, the next item's W(0,1)
     issued before the epilogue stores, split-K items in the stream): bit-identical to one item per
