@@ -13,13 +13,6 @@ namespace dcnn {
 struct BnbArgs {
   const bf16* y; const bf16* x; const float* mean; const float* istd;
 };
-// In-launch fold of a producer's per-tile statistics rows (statfold.h): the workgroup completing
-// row group g (rows [g*group, (g+1)*group)) of a column tile merges the group's rows into
-// part[g][3][N] (one group: the finished [2][N] statistics). Inactive when part == nullptr.
-// tickets: ngroups x (N / 64) zeroed words, left zeroed.
-struct StatFold {
-  float* part; unsigned* tickets; int group; int ngroups; int rows;
-};
 struct NtArgs {
   const bf16* A; const bf16* B; void* C;
   int M, N, K; int lda, ldb, ldc; int mode;
@@ -40,7 +33,6 @@ struct G2Args {
   const float* bias; const bf16* residual; float* stats; int relu;
   float* zero_ptr; int zero_n;  // zeroed by workgroup 0 (BN sums consumed by the next kernel)
   BnbArgs bnb;
-  StatFold fold;
   // grouped launch of up to 4 row classes (the stride phases of a strided dgrad): class c owns
   // rows [c * cls_rows, (c + 1) * cls_rows) (cls_rows a multiple of the row tile), taps
   // [cls_t0[c], cls_t0[c] + cls_nt[c]) of the tap arrays and the output phase (cls_ory, cls_orx).
@@ -75,7 +67,6 @@ struct HConvArgs {
   // accumulators in `part` [tiles][splits][BM*BN] fp32, the last arriver on the tile's ticket
   // word sums them in split order (deterministic) and runs the epilogue; tickets left zeroed
   int splits; float* part; unsigned* tickets;
-  StatFold fold;
 };
 void hconv(HConvArgs a, hipStream_t s);
 // split count hconv() will use for this shape, and its output-tile count (workspace sizing)
@@ -84,8 +75,6 @@ int hconv_tiles(int NB, int H, int W, int Cs, int N, int ntaps);
 int hconv_tile_elems(int NB, int H, int W, int Cs, int N, int ntaps);
 void hconv_set_split_target(int t);  // workgroups the split-K decision aims for (0: never split)
 void bn_set_vectorised(int on);   // bf16 BatchNorm apply passes on the vectorised kernels (default on)
-void hconv_set_ws(int on);           // weight-stationary kernel for 64 -> 64 channel 3x3 convs
-void hconv_set_wide(int on);         // 256 x 64 tiles (4 x 1 waves) for 64-channel outputs
 bool hconv_supported(int NB, int H, int W, int Cs, int N, int ntaps);
 int hconv_stat_rows(int NB, int H, int W, int Cs, int N, int ntaps, int f32out);
 bool hconv_v3(int NB, int H, int W, int Cs, int N, int ntaps);  // shape runs on hconv3
@@ -98,7 +87,7 @@ struct HWArgs {
   unsigned dy_bytes, x_bytes;
   int NB, H, W, Cs, Co, ntaps;
   int tap_dy[9], tap_dx[9];
-  int TH, TW, IMG, HPR, tiles_per_split, dbg;  // filled by the launcher
+  int TH, TW, IMG, HPR, tiles_per_split;  // filled by the launcher
   // operand pairs (grid.y): pair q reads dY channels [yoff_q, yoff_q + Co) of rows ldy wide and
   // X channels [xoff_q, xoff_q + Cs) of rows ldx wide, into slabs [q * splits + split]; its bias
   // partial is the dY column sum if bias_q else 0. One pair with ldy = Co, ldx = Cs is the plain

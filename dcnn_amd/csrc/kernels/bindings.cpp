@@ -26,12 +26,8 @@ static void bind_gemm_g2(uintptr_t A, uintptr_t B, uintptr_t C, unsigned a_bytes
                          int H, int W, int GH, int GW, int SY, int SX, std::vector<std::array<int, 4>> taps, int ldb,
                          int ldc, int OH, int OW, int OSY, int OSX, int ORY, int ORX, uintptr_t bias, uintptr_t residual,
                          uintptr_t stats, int relu, uintptr_t zero_ptr, int zero_n, std::array<uintptr_t, 4> bnb,
-                         uintptr_t stream, std::vector<std::array<int, 4>> classes = {},
-                         std::array<int64_t, 5> fold = {}) {
+                         uintptr_t stream, std::vector<std::array<int, 4>> classes = {}) {
   G2Args a{};
-  // fold: (partials, tickets, rows per group, groups, rows) of the in-launch statistics fold
-  a.fold = StatFold{P<float*>((uintptr_t)fold[0]), P<unsigned*>((uintptr_t)fold[1]), (int)fold[2], (int)fold[3],
-                    (int)fold[4]};
   // classes: (first tap, taps, ORY, ORX) per row class of a grouped launch (empty: one class)
   if (classes.size() > 4) throw std::runtime_error("gemm_g2: at most 4 row classes");
   a.ncls = (int)classes.size();
@@ -100,10 +96,8 @@ PYBIND11_MODULE(_kernels, m) {
         [](uintptr_t A, uintptr_t B, uintptr_t C, unsigned a_bytes, unsigned b_bytes, int NB, int H, int W, int Cs,
            int N, int ldb, std::vector<std::array<int, 3>> taps, uintptr_t bias, uintptr_t residual, uintptr_t stats,
            int relu, uintptr_t zero_ptr, int zero_n, std::array<uintptr_t, 4> bnb, uintptr_t Cf, uintptr_t residual_f,
-           int splits, uintptr_t part, uintptr_t tickets, uintptr_t stream, std::array<int64_t, 5> fold) {
+           int splits, uintptr_t part, uintptr_t tickets, uintptr_t stream) {
           HConvArgs a{};
-          a.fold = StatFold{P<float*>((uintptr_t)fold[0]), P<unsigned*>((uintptr_t)fold[1]), (int)fold[2],
-                            (int)fold[3], (int)fold[4]};
           a.splits = splits; a.part = P<float*>(part); a.tickets = P<unsigned*>(tickets);
           a.Cf = P<float*>(Cf); a.residual_f = P<const float*>(residual_f);
           a.bnb = BnbArgs{P<const bf16*>(bnb[0]), P<const bf16*>(bnb[1]), P<const float*>(bnb[2]), P<const float*>(bnb[3])};
@@ -122,8 +116,6 @@ PYBIND11_MODULE(_kernels, m) {
   m.def("hconv_splits", &hconv_splits);
   m.def("hconv_tiles", &hconv_tiles);
   m.def("hconv_set_split_target", &hconv_set_split_target);
-  m.def("hconv_set_wide", &hconv_set_wide);
-  m.def("hconv_set_ws", &hconv_set_ws);
   m.def("bn_set_vectorised", &bn_set_vectorised);
   m.def("hconv_tile_elems", &hconv_tile_elems);
   m.def("hconv3_set_grid_cap", &hconv3_set_grid_cap);
@@ -200,7 +192,7 @@ PYBIND11_MODULE(_kernels, m) {
                       uintptr_t stats, int relu, uintptr_t zero_ptr, int zero_n, std::array<uintptr_t, 4> bnb,
                       uintptr_t stream) {
     bind_gemm_g2(A, B, C, a_bytes, b_bytes, M, N, Cs, H, W, GH, GW, SY, SX, std::move(taps), ldb, ldc, OH, OW, OSY, OSX,
-                 ORY, ORX, bias, residual, stats, relu, zero_ptr, zero_n, bnb, stream, {}, {});
+                 ORY, ORX, bias, residual, stats, relu, zero_ptr, zero_n, bnb, stream, {});
   });
   // grouped row classes (strided-dgrad phases in one launch): classes = (first tap, taps, ORY, ORX)
   m.def("gemm_g2_grouped", &bind_gemm_g2);

@@ -110,15 +110,6 @@ __device__ __forceinline__ void store_welford(float* slab, long tile, int C, int
   slab[(tile * 3 + 1) * C + c] = w.mean;
   slab[(tile * 3 + 2) * C + c] = w.m2;
 }
-// the same with agent-scope (sc1) stores: rows read back inside the launch (statfold.h)
-__device__ __forceinline__ void store_welford_agent(float* slab, long tile, int C, int c, Welford w) {
-  float* q = slab + tile * 3 * C + c;
-  __hip_atomic_store(reinterpret_cast<unsigned*>(q), __float_as_uint(w.n), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  __hip_atomic_store(reinterpret_cast<unsigned*>(q + C), __float_as_uint(w.mean), __ATOMIC_RELAXED,
-                     __HIP_MEMORY_SCOPE_AGENT);
-  __hip_atomic_store(reinterpret_cast<unsigned*>(q + 2 * C), __float_as_uint(w.m2), __ATOMIC_RELAXED,
-                     __HIP_MEMORY_SCOPE_AGENT);
-}
 
 // 8 x bf16 <-> 8 x f32 through one 16-byte access.
 struct alignas(16) Pack8 {

@@ -83,14 +83,6 @@ struct G1sArgs {
   const float* bias; const bf16* residual; float* stats; int relu;
   float* zero_ptr; int zero_n;
   BnbArgs bnb;
-  int dbg;  // DCNN_G1S_DBG experiments: 2 = direct 8-byte stores instead of the LDS-staged full
-           // lines, 3 = no output stores (timing only)
-  // gathered form (gen = 1): one stride-phase class of a strided data gradient. GEMM row m is
-  // class-grid pixel (img, gy, gx) of GH x GW; K = ntaps x Kc, tap t reads input pixel
-  // (gy + tap_dy[t], gx + tap_dx[t]) of the H x W x Kc input (zero outside) against weight
-  // columns tap_k[t] .. + Kc of rows ldw wide; the result goes to output pixel
-  // (gy * OS + ORY, gx * OS + ORX) of the OHo x OWo output. ntaps = 0: no MFMA work (a phase no
-  // tap reaches: residual / zero through the same epilogue). gen = 0: Kc = ldw = K, one tap.
   int gen, ntaps, Kc, ldw, GH, GW, OS, ORY, ORX, OHo, OWo;
   int tap_dy[4], tap_dx[4], tap_k[4];
 };
@@ -98,17 +90,7 @@ struct G1sArgs {
 // per-instance shape: TJ 16-pixel subtiles per tile, OCC waves per SIMD the registers allow
 // (K = 64: 32-pixel tiles keep the forward at ~150 VGPRs, three waves per SIMD to hide the
 // load latency behind each other's epilogues)
-// waves per SIMD of an instance (the register budget it is compiled for): 2, or 3 for the K = 64
-// forward when DCNN_G1S_OCC=3 (~168 VGPRs)
-static int g_g1s_occ3 = [] {
-  const char* e = getenv("DCNN_G1S_OCC");
-  return e ? atoi(e) == 3 : 0;
-}();
-static int g_g1s_pf = [] {
-  const char* e = getenv("DCNN_G1S_PF");
-  return e ? atoi(e) : 2;
-}();
-static int g1s_occ_rt(int K, int mode) { return (K == 64 && mode != 2 && g_g1s_occ3) ? 3 : 2; }
+static int g1s_occ_rt(int K, int mode) { (void)K; (void)mode; return 2; }  // waves per SIMD
 // (K = 32: one MFMA k step per subtile; weights 16 VGPRs)
 constexpr int kG1sTile = 32;  // pixels per tile (16 * TJ)
 // weights in LDS (shared by the workgroup's 4 waves) instead of VGPRs: K >= 256, and the K = 128
@@ -365,8 +347,8 @@ __global__ void __launch_bounds__(256, OCC) g1s_kernel(G1sArgs p) {
           f[2] = y23.x > 0.f ? f[2] : 0.f; f[3] = y23.y > 0.f ? f[3] : 0.f;
         }
         const uint2 o = make_uint2(f2_to_bf2(f[0], f[1]), f2_to_bf2(f[2], f[3]));
-        if (!STG || (p.dbg & 2)) {  // direct 8-byte stores (16 pixel rows x 32 B per instruction)
-          if (!(p.dbg & 1)) *reinterpret_cast<uint2*>(p.Y + (size_t)orow(t * TP + j * 16 + lr) * p.N + n0 + lh * 4 + i * 16) = o;
+        if (!STG) {  // direct 8-byte stores (16 pixel rows x 32 B per instruction)
+          *reinterpret_cast<uint2*>(p.Y + (size_t)orow(t * TP + j * 16 + lr) * p.N + n0 + lh * 4 + i * 16) = o;
         } else {
           // full-line stores: the tile's 32 pixel rows (128 B each, 16-byte chunks XOR-swizzled by
           // the pixel) are staged in this wave's LDS slice and read back as 8 lanes per pixel row
@@ -389,7 +371,7 @@ __global__ void __launch_bounds__(256, OCC) g1s_kernel(G1sArgs p) {
         }
       }
     }
-    if (STG && !(p.dbg & 3)) {
+    if (STG) {
 #pragma unroll
       for (int k = 0; k < TP / 8; ++k) {
         const int P = k * 8 + (lane >> 3), c = lane & 7;
@@ -444,10 +426,7 @@ __global__ void __launch_bounds__(256, OCC) g1s_kernel(G1sArgs p) {
 // ------------------------------------------------------------------------------------------------
 // host side
 // ------------------------------------------------------------------------------------------------
-static int g_g1s = [] {
-  const char* e = getenv("DCNN_G1S");
-  return e ? atoi(e) : 1;
-}();
+static int g_g1s = 1;  // g1s_enable(0): 1x1 convs back on the gathered GEMM (test hook)
 void g1s_enable(int on) { g_g1s = on; }
 
 // statistics rows (= pixel ranges) of a streaming 1x1 conv with M output pixels, N output and K
@@ -484,10 +463,8 @@ static void launch_g1s(const G1sArgs& a, hipStream_t s) {
   // B fragments two tiles deep; epilogue operands (residual / BatchNorm y, x) one tile ahead only
   // with DCNN_G1S_PF=3 (more registers: spills on the wider instances)
   // (K >= 128: one B buffer, reloaded after the MFMAs — the two-deep ring spills there)
-  if (K >= 128 || g_g1s_pf == 1)
+  if (K >= 128)
     hipLaunchKernelGGL((g1s_kernel<K, MODE, OCC, 1, false>), dim3((waves + 3) / 4), dim3(256), 0, s, a);
-  else if (g_g1s_pf == 3)
-    hipLaunchKernelGGL((g1s_kernel<K, MODE, OCC, 2, true>), dim3((waves + 3) / 4), dim3(256), 0, s, a);
   else
     hipLaunchKernelGGL((g1s_kernel<K, MODE, OCC, 2, false>), dim3((waves + 3) / 4), dim3(256), 0, s, a);
   DCNN_LAUNCH_CHECK();
@@ -506,12 +483,9 @@ static void g1s_launch(G1sArgs& a, int mode, hipStream_t s) {
   a.tiles = a.M / kG1sTile;
   a.tpr = g1s_tpr(a.M, a.N, K, mode);
   a.PR = rows;
-  static const int dbg = [] { const char* e = getenv("DCNN_G1S_DBG"); return e ? atoi(e) : 0; }();
-  a.dbg = dbg;
 #define DCNN_G1S(K_)                                          \
   if (K == K_) {                                              \
     if (mode == 0) return launch_g1s<K_, 0>(a, s);            \
-    if (mode == 1 && g1s_occ_rt(K_, 1) == 3) return launch_g1s<K_, 1, (K_ == 64 ? 3 : 2)>(a, s); \
     if (mode == 1) return launch_g1s<K_, 1>(a, s);            \
     return launch_g1s<K_, 2>(a, s);                           \
   }

@@ -23,7 +23,6 @@
 
 #include "common.h"
 #include "api.h"
-#include "statfold.h"
 
 namespace dcnn {
 
@@ -322,14 +321,13 @@ __global__ void __launch_bounds__(256, 2) gemm_g2_kernel(G2Args p) {
       red[(r0 * 2 + 1) * BN + cg * 8 + v] = q[v];
     }
     __syncthreads();
-    const bool fold = p.fold.part != nullptr;  // (host: only when N % BN == 0)
     if (bnb) {  // backward: plain sums [tiles][2][N]
       for (int c = tid; c < 2 * BN; c += 256) {
         const int which = c / BN, cc = c % BN;
         if (n0 + cc < p.N) {
           float a = 0.f;
           for (int k = 0; k < RSTEP; ++k) a += red[(k * 2 + which) * BN + cc];
-          stat_store(&p.stats[((long)tm * 2 + which) * p.N + n0 + cc], a, fold);
+          *&p.stats[((long)tm * 2 + which) * p.N + n0 + cc] = a;
         }
       }
     } else if (tid < BN && n0 + tid < p.N) {  // forward: Welford triple [tiles][3][N]
@@ -337,12 +335,7 @@ __global__ void __launch_bounds__(256, 2) gemm_g2_kernel(G2Args p) {
       for (int k = 0; k < RSTEP; ++k) { a += red[(k * 2 + 0) * BN + tid]; b += red[(k * 2 + 1) * BN + tid]; }
       const float cnt = (float)min(BM, p.M - m0);
       const Welford w = welford_from_shifted(cnt, piv_col, a, b);
-      if (fold) store_welford_agent(p.stats, tm, p.N, n0 + tid, w);
-      else store_welford(p.stats, tm, p.N, n0 + tid, w);
-    }
-    if (fold) {  // merge the row group's statistics in this launch (statfold.h)
-      if (bnb) stat_fold<1, BN>(p.stats, p.N, tm, n0, p.fold, reinterpret_cast<float*>(smem));
-      else stat_fold<0, BN>(p.stats, p.N, tm, n0, p.fold, reinterpret_cast<float*>(smem));
+      store_welford(p.stats, tm, p.N, n0 + tid, w);
     }
   }
 }
@@ -566,16 +559,9 @@ __global__ void __launch_bounds__(256, 2) gemm_t2_kernel(T2Args p) {
 // ---------------------------------------------------------------------------------------------
 // launchers
 // ---------------------------------------------------------------------------------------------
-// LDS ring depth: DCNN_G2_STAGES=2 / 3 forces it; default (0) = 3 stages wherever the deeper ring
-// still leaves two workgroups per CU (every tile but 128x128), else 2
-static int g2_stages() {
-  static int st = [] {
-    const char* e = getenv("DCNN_G2_STAGES");
-    const int v = e ? atoi(e) : 0;
-    return (v == 2 || v == 3) ? v : 0;
-  }();
-  return st;
-}
+// LDS ring depth: 3 stages wherever the deeper ring still leaves two workgroups per CU (every
+// tile but 128x128), else 2 (g2_stages() == 0: that rule)
+static int g2_stages() { return 0; }
 
 template <int BM, int BN, int BK, bool UNI>
 static void launch_g2(const G2Args& a, hipStream_t s) {
@@ -598,17 +584,7 @@ static void launch_g2(const G2Args& a, hipStream_t s) {
 }
 
 // Tile choice: the largest tile that still gives >= ~2 workgroups per CU.
-// DCNN_G2_TILE / DCNN_T2_TILE = MxN (64 / 128 each): fixed tiles for A/B experiments
-static int fixed_tile(const char* var) {
-  const char* e = getenv(var);
-  int m = 0, n = 0;
-  if (e && sscanf(e, "%dx%d", &m, &n) == 2 && (m == 64 || m == 128) && (n == 64 || n == 128)) return m * 1000 + n;
-  return 0;
-}
-
 void g2_tile(int M, int N, int* bm, int* bn) {
-  static const int fixed = fixed_tile("DCNN_G2_TILE");
-  if (fixed) { *bm = fixed / 1000; *bn = fixed % 1000; return; }
   auto tiles = [&](int m, int n) { return (long)((M + m - 1) / m) * ((N + n - 1) / n); };
   if (N >= 128 && tiles(128, 128) >= 480) { *bm = 128; *bn = 128; return; }
   // wide-N, mid-M (8x8-map convs of 256 channels, M = 16384): 64 x 128 beats 128 x 64 at the
@@ -642,11 +618,6 @@ void gemm_g2(const G2Args& a_in, hipStream_t s) {
     throw std::runtime_error("gemm_g2: unsupported shape (needs N, Cs, ldb, ldc multiples of 8, 1..64 taps)");
   int bm, bn;
   g2_tile(a.M, a.N, &bm, &bn);
-  if (a.fold.part) {
-    if (!a.stats || a.N % bn || a.N % 64 || a.fold.group < 1 || a.fold.rows != (a.M + bm - 1) / bm ||
-        a.fold.ngroups != (a.fold.rows + a.fold.group - 1) / a.fold.group || !a.fold.tickets)
-      throw std::runtime_error("gemm_g2: statistics fold needs N % column tile == 0 and matching row groups");
-  }
   if (a.ncls <= 1) {
     a.ncls = 1; a.cls_rows = a.M;
     a.cls_t0[0] = 0; a.cls_nt[0] = a.ntaps; a.cls_ory[0] = a.ORY; a.cls_orx[0] = a.ORX;
@@ -684,8 +655,6 @@ static void launch_t2(T2Args a, int splits, hipStream_t s) {
 }
 
 void t2_tile(int M, int N, int* bm, int* bn) {
-  static const int fixed = fixed_tile("DCNN_T2_TILE");
-  if (fixed) { *bm = fixed / 1000; *bn = fixed % 1000; return; }
   // 128 x 64 once M >= 128: twice the tiles of 128 x 128, so half the split-K slices and slab
   // traffic (strided 3x3 weight gradients of layers 2-4: 43 / 39 / 38 -> 33 / 33 / 32 us at
   // batch 256); 128-wide N tiles only when M is a single 64-row tile
@@ -698,11 +667,9 @@ int gemm_t2_splits(int M, int N, int P) {
   t2_tile(M, N, &bm, &bn);
   const long tiles = (long)((M + bm - 1) / bm) * ((N + bn - 1) / bn);
   long splits = (512 + tiles - 1) / tiles;
-  // at least DCNN_T2_MIN_K (default 256) reduction pixels per split
-  static const long min_k = [] {
-    const char* e = getenv("DCNN_T2_MIN_K");
-    return e && atoi(e) >= 64 ? (long)atoi(e) : 256l;
-  }();
+  // at least 256 reduction pixels per split (1024: ResNet-50 b32 7.9k -> 7.2k img/s,
+  // profiles/wgrad_splits_r3.md)
+  constexpr long min_k = 256;
   const long max_by_k = P / min_k > 0 ? P / min_k : 1;
   if (splits > max_by_k) splits = max_by_k;
   const long max_by_mem = (48l << 20) / (4l * M * N) > 0 ? (48l << 20) / (4l * M * N) : 1;

@@ -625,12 +625,8 @@ __global__ void __launch_bounds__(256) multi_splitk_reduce_kernel(MultiRed t) {
   }
 }
 
-// slab loads in flight per wave and group (DCNN_RED_G: 8 or 16; the summation order is fixed for
-// a given setting)
-static int g_red_g = [] {
-  const char* e = getenv("DCNN_RED_G");
-  return (e && atoi(e) == 8) ? 8 : 16;
-}();
+// slab loads in flight per wave and group (the summation order is fixed)
+static constexpr int g_red_g = 16;
 
 void multi_splitk_reduce(MultiRed t, hipStream_t s) {
   if (t.count <= 0) return;

@@ -610,10 +610,7 @@ __global__ void __launch_bounds__(256, 2) gemm_t2x_kernel(T2Args p) {
 }
 
 static bool f32_split() {
-  if (g_f32_mode < 0) {
-    const char* e = std::getenv("DCNN_F32_SPLIT");
-    g_f32_mode = (e && e[0] == '1') ? 1 : 0;
-  }
+  if (g_f32_mode < 0) g_f32_mode = 0;
   return g_f32_mode == 1;
 }
 

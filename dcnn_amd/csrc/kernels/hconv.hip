@@ -25,7 +25,6 @@
 #include "common.h"
 #include "api.h"
 #include "hconv3_plan.h"
-#include "statfold.h"
 
 namespace dcnn {
 
@@ -215,26 +214,20 @@ __device__ __forceinline__ void hc_epilogue(const HConvArgs& p,
       red[(r0 * 2 + 1) * BN + cg * 8 + v] = q[v];
     }
     __syncthreads();
-    const bool fold = p.fold.part != nullptr;
     if (bnb) {  // backward: plain sums [tiles][2][N]
       for (int cc = tid; cc < 2 * BN; cc += 256) {
         const int which = cc / BN, c2 = cc % BN;
         if (n0 + c2 >= p.N) continue;
         float a = 0.f;
         for (int k = 0; k < RSTEP; ++k) a += red[(k * 2 + which) * BN + c2];
-        stat_store(&p.stats[((long)tm * 2 + which) * p.N + n0 + c2], a, fold);
+        *&p.stats[((long)tm * 2 + which) * p.N + n0 + c2] = a;
       }
     } else if (tid < BN && n0 + tid < p.N) {  // forward: Welford triple [tiles][3][N], fixed summation order
       float a = 0.f, b = 0.f;
       for (int k = 0; k < RSTEP; ++k) { a += red[(k * 2 + 0) * BN + tid]; b += red[(k * 2 + 1) * BN + tid]; }
       const float cnt = (float)(min(p.IMG, p.NB - img0) * tpx);
       const Welford w = welford_from_shifted(cnt, piv_col, a, b);
-      if (fold) store_welford_agent(p.stats, tm, p.N, n0 + tid, w);
-      else store_welford(p.stats, tm, p.N, n0 + tid, w);
-    }
-    if (fold) {  // merge the row group's statistics in this launch (statfold.h)
-      if (bnb) stat_fold<1, BN>(p.stats, p.N, tm, n0, p.fold, reinterpret_cast<float*>(smem));
-      else stat_fold<0, BN>(p.stats, p.N, tm, n0, p.fold, reinterpret_cast<float*>(smem));
+      store_welford(p.stats, tm, p.N, n0 + tid, w);
     }
   }
 }
@@ -405,22 +398,21 @@ __global__ void __launch_bounds__(256, 1) hconv_kernel(HConvArgs p) {
 
   if constexpr (T::WN == 2) if (SPL > 1) {  // (the 4 x 1 wide tiles never split: host)
     // split-K hand-off without fences (MI355X_MICROARCH "Valid forms" row 1): every partial is
-    // stored with agent-scope (sc1) 8-byte stores, each wave drains them, one lane adds to the
-    // tile's ticket after the workgroup barrier, and the workgroup whose add returns SPL - 1
-    // reads all partials back with sc1 loads and sums them in split order.
-    constexpr int E2 = T::TM * T::TN * 2;  // float2 accumulator pairs per lane
-    unsigned long long* part = reinterpret_cast<unsigned long long*>(p.part) + (size_t)lt * SPL * E2 * 256;
+    // stored with agent-scope (sc1) 16-byte buffer stores ([split][tile i, j][lane]), each wave
+    // drains them, one lane adds to the tile's ticket after the workgroup barrier, and the
+    // workgroup whose add returns SPL - 1 reads the partials back with sc1 loads (all of a split
+    // in flight at once) and sums them in split order.
+    constexpr int NE = T::TM * T::TN;  // 16-byte accumulator tiles per lane
+    const __amdgpu_buffer_rsrc_t rsP =
+        __builtin_amdgcn_make_buffer_rsrc(p.part + (size_t)lt * SPL * NE * 256 * 4, 0, SPL * NE * 256 * 16, 0x00020000);
+    constexpr int kSC1 = 16;  // cache policy: sc1 (agent-coherent)
+    using u32x4 = __attribute__((ext_vector_type(4))) unsigned;
 #pragma unroll
     for (int i = 0; i < T::TM; ++i)
 #pragma unroll
       for (int j = 0; j < T::TN; ++j)
-#pragma unroll
-        for (int h = 0; h < 2; ++h) {
-          const int e2 = (i * T::TN + j) * 2 + h;
-          const unsigned long long bits = (unsigned long long)__float_as_uint(acc[i][j][2 * h]) |
-                                          ((unsigned long long)__float_as_uint(acc[i][j][2 * h + 1]) << 32);
-          __hip_atomic_store(part + ((size_t)zs * E2 + e2) * 256 + tid, bits, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        }
+        __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, acc[i][j]), rsP,
+                                               ((zs * NE + i * T::TN + j) * 256 + tid) * 16, 0, kSC1);
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
     volatile int* flag = reinterpret_cast<volatile int*>(smem);
@@ -439,139 +431,20 @@ __global__ void __launch_bounds__(256, 1) hconv_kernel(HConvArgs p) {
 #pragma unroll
       for (int j = 0; j < T::TN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
     for (int z = 0; z < SPL; ++z) {
+      f32x4 t[NE];
+#pragma unroll
+      for (int k = 0; k < NE; ++k)
+        t[k] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(rsP, ((z * NE + k) * 256 + tid) * 16, 0, kSC1));
 #pragma unroll
       for (int i = 0; i < T::TM; ++i)
 #pragma unroll
-        for (int j = 0; j < T::TN; ++j)
-#pragma unroll
-          for (int h = 0; h < 2; ++h) {
-            const int e2 = (i * T::TN + j) * 2 + h;
-            const unsigned long long bits =
-                __hip_atomic_load(part + ((size_t)z * E2 + e2) * 256 + tid, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            acc[i][j][2 * h] += __uint_as_float((unsigned)bits);
-            acc[i][j][2 * h + 1] += __uint_as_float((unsigned)(bits >> 32));
-          }
+        for (int j = 0; j < T::TN; ++j) acc[i][j] += t[i * T::TN + j];
     }
   }
 
   hc_epilogue<BM, BN, F32O>(p, acc, smem, n0, tm, img0, y0, x0);
 }
 
-// ---------------------------------------------------------------------------------------------
-// Weight-stationary variant for the 64 -> 64 channel 3x3 convs (ResNet layer 1, forward and
-// dgrad): with one 64-channel input chunk the K loop of hconv_kernel is only 9 taps long, and
-// each of its 9 steps waits for a freshly streamed 8 KB weight slice (one L2 round trip per
-// tap, one step of prefetch) plus a workgroup barrier, so a 128 x 64 tile spends most of its
-// life waiting. Here the whole 64 x 576 weight matrix is loaded ONCE per workgroup into
-// registers (each wave's 32-column slice: 9 taps x 2 k-halves x 2 fragments), and the
-// workgroup walks a contiguous range of output tiles: the halo of tile i + 1 streams into the
-// second LDS buffer (direct-to-LDS loads) while tile i runs its 9 taps barrier-free out of LDS
-// + registers, and tile i's epilogue stores drain while tile i + 1 computes.
-//
-//   prologue: halo(t0) -> H[0], weights -> registers
-//   per tile i: issue halo(i + 1) -> H[(i + 1) & 1];  9 taps of MFMAs on H[i & 1];
-//               wait (halo i + 1 landed), barrier;  epilogue(i) (bias/residual/ReLU/BN stats)
-// ---------------------------------------------------------------------------------------------
-template <int HN>
-__global__ void __launch_bounds__(256, 1) hconv_ws_kernel(HConvArgs p, int tiles, int per_wg) {
-  constexpr int BM = 128, BN = 64;
-  using T = HC<BM, BN, 1, 1, 2, false>;  // 2 x 2 waves, TM = 4, TN = 2
-  static_assert(T::WN == 2 && T::TN == 2 && T::TM == 4, "layout");
-  extern __shared__ __attribute__((aligned(16))) char smem[];
-  const int HALO = p.HPR * 128;
-  char* epi = smem + 2 * HALO;
-  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
-  const int wm = wid / T::WN, wn = wid % T::WN;
-  if (p.zero_ptr && blockIdx.x == 0)
-    for (int i = tid; i < p.zero_n; i += 256) p.zero_ptr[i] = 0.f;
-  // this workgroup's contiguous tile range (neighbouring ranges on one XCD share halo rows in L2)
-  const int g = xcd_remap_h(blockIdx.x, gridDim.x);
-  const int t_begin = g * per_wg, t_end = min(tiles, t_begin + per_wg);
-  if (t_begin >= t_end) return;
-
-  const i32x4 rsA = raw_rsrc(p.A, p.a_bytes);
-  const int HW2 = p.TW + 2, HPI = (p.TH + 2) * HW2, HP = p.IMG * HPI;
-  const int tx_tiles = p.W / p.TW, tpi = tx_tiles * (p.H / p.TH);
-  const int hch = lane & 7;
-  auto load_halo = [&](int buf, int tm) {
-    const int ig = tm / tpi, trem = tm - ig * tpi;
-    const int y0 = (trem / tx_tiles) * p.TH, x0 = (trem % tx_tiles) * p.TW, img0 = ig * p.IMG;
-    char* Hs = smem + buf * HALO;
-#pragma unroll
-    for (int j = 0; j < HN; ++j) {
-      const int row = (wid * HN + j) * 8 + (lane >> 3);
-      unsigned voff = kOOBh;
-      if (row < HP) {
-        const int im = row / HPI, r2 = row - im * HPI;
-        const int sy = y0 + r2 / HW2 - 1, sx = x0 + r2 % HW2 - 1, n = img0 + im;
-        if (sy >= 0 && sy < p.H && sx >= 0 && sx < p.W && n < p.NB)
-          voff = (unsigned)((((long)n * p.H + sy) * p.W + sx) * 128) + (unsigned)((hch ^ (row & 7)) << 4);
-      }
-      glds16h(rsA, Hs + (wid * HN + j) * 1024, voff);
-    }
-  };
-  load_halo(0, t_begin);
-  // weights: this wave's 32 output channels, all taps, both 32-channel k-halves
-  bf16x8 b[9][2][2];
-#pragma unroll
-  for (int t = 0; t < 9; ++t)
-#pragma unroll
-    for (int kk = 0; kk < 2; ++kk)
-#pragma unroll
-      for (int j = 0; j < 2; ++j) {
-        const int nrow = wn * 32 + j * 16 + (lane & 15);
-        b[t][kk][j] = *reinterpret_cast<const bf16x8*>(p.B + (long)nrow * p.ldb + p.tap_b[t] + (kk * 4 + (lane >> 4)) * 8);
-      }
-  int arow0[T::TM];
-#pragma unroll
-  for (int i = 0; i < T::TM; ++i) {
-    const int m = wm * (BM / T::WM) + i * 16 + hperm(lane & 15, p.TW);
-    const int tpx = p.TH * p.TW;
-    const int im = m / tpx, r2 = m - im * tpx;
-    arow0[i] = im * HPI + (r2 / p.TW + 1) * HW2 + (r2 % p.TW + 1);
-  }
-  int toff[9];
-#pragma unroll
-  for (int t = 0; t < 9; ++t) toff[t] = p.tap_dy[t] * HW2 + p.tap_dx[t];
-  vm_wait_groups<1>(0);
-  lds_barrier();
-  int buf = 0;
-  for (int tm = t_begin; tm < t_end; ++tm) {
-    // H[buf ^ 1] was last read by tile tm - 1's taps, which every wave finished before the
-    // barrier that ended that tile
-    if (tm + 1 < t_end) load_halo(buf ^ 1, tm + 1);
-    const char* Hs = smem + buf * HALO;
-    f32x4 acc[T::TM][T::TN];
-#pragma unroll
-    for (int i = 0; i < T::TM; ++i)
-#pragma unroll
-      for (int j = 0; j < T::TN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-    for (int t = 0; t < 9; ++t) {
-      bf16x8 a[2][T::TM];
-#pragma unroll
-      for (int kk = 0; kk < 2; ++kk)
-#pragma unroll
-        for (int i = 0; i < T::TM; ++i)
-          a[kk][i] = *reinterpret_cast<const bf16x8*>(Hs + hoff(arow0[i] + toff[t], kk * 4 + (lane >> 4)));
-      __builtin_amdgcn_s_setprio(1);
-#pragma unroll
-      for (int kk = 0; kk < 2; ++kk)
-#pragma unroll
-        for (int i = 0; i < T::TM; ++i)
-#pragma unroll
-          for (int j = 0; j < T::TN; ++j)
-            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[kk][i], b[t][kk][j], acc[i][j], 0, 0, 0);
-      __builtin_amdgcn_s_setprio(0);
-    }
-    // the next tile's halo (and this lane's older stores) landed, then for the whole workgroup
-    vm_wait_groups<1>(0);
-    lds_barrier();
-    const int ig = tm / tpi, trem = tm - ig * tpi;
-    hc_epilogue<BM, BN, false>(p, acc, epi, 0, tm, ig * p.IMG, (trem / tx_tiles) * p.TH, (trem % tx_tiles) * p.TW);
-    buf ^= 1;
-  }
-}
 
 // ---------------------------------------------------------------------------------------------
 // host side: tile geometry + dispatch
@@ -590,35 +463,9 @@ static bool hconv_geometry(int NB, int H, int W, int BM, int* TH, int* TW, int* 
   return true;
 }
 
-// 256 x 64 tiles (4 x 1 waves) for 64-channel outputs on 16x16-divisible maps: opt-in
-// (DCNN_HCONV_WIDE=1), measured no faster than 128 x 64 on the ResNet-18 layer-1 convs
-// (profiles/experiment_hconv_variants.md)
-static int g_hconv_wide = [] {
-  const char* e = getenv("DCNN_HCONV_WIDE");
-  return e ? atoi(e) : 0;
-}();
-void hconv_set_wide(int on) { g_hconv_wide = on; }
-
 static void hconv_pick(const HConvArgs& a, int* bm, int* bn) {
   // prefer 128 x 128 when it still gives >= ~1.5 workgroups per CU, else shrink
   auto tiles = [&](int m, int n) { return (long)((a.NB * a.H * a.W + m - 1) / m) * ((a.N + n - 1) / n); };
-  if (g_hconv_wide && a.N == 64 && a.W % 16 == 0 && a.H % 16 == 0 && tiles(256, 64) >= 512) {
-    *bm = 256;
-    *bn = 64;
-    return;
-  }
-  // DCNN_HCONV_TILE=MxN (64/128 each): fixed tile for A/B experiments where N divides
-  static const int fixed = [] {
-    const char* e = getenv("DCNN_HCONV_TILE");
-    int m = 0, n = 0;
-    if (e && sscanf(e, "%dx%d", &m, &n) == 2 && (m == 64 || m == 128) && (n == 64 || n == 128)) return m * 1000 + n;
-    return 0;
-  }();
-  if (fixed && a.N % (fixed % 1000) == 0) {
-    *bm = fixed / 1000;
-    *bn = fixed % 1000;
-    return;
-  }
   *bm = 128;
   *bn = (a.N % 128 == 0 && tiles(128, 128) >= 384) ? 128 : 64;
   if (tiles(*bm, *bn) < 384) {
@@ -647,11 +494,8 @@ bool hconv_supported(int NB, int H, int W, int Cs, int N, int ntaps) {
   return NB % img == 0;
 }
 
-// target workgroup count of the split-K decision; 0 = never split (DCNN_HCONV_SPLIT)
-static int g_split_target = [] {
-  const char* e = getenv("DCNN_HCONV_SPLIT");
-  return e ? atoi(e) : 512;
-}();
+// target workgroup count of the split-K decision; 0 = never split (test hook)
+static int g_split_target = 512;
 int hconv_split_target() { return g_split_target; }
 void hconv_set_split_target(int t) { g_split_target = t < 0 ? 0 : t; }
 
@@ -714,17 +558,8 @@ static void launch_hconv(HConvArgs a, hipStream_t s) {
   // taps per K step. Default: 2 on the 64x64 tiles (small maps, long K: 4x4 layer-4 convs 9%
   // faster, same workgroups per CU), 1 elsewhere (2 or 3 cost a resident workgroup per CU on the
   // larger tiles: 20-40% slower, tools/gpu_exp.sh sweep in profiles/experiment_hconv_variants.md)
-  static const int tps_env = [] {
-    const char* e = getenv("DCNN_HCONV_TPS");
-    const int v = e ? atoi(e) : 0;
-    return (v >= 1 && v <= 3) ? v : 0;
-  }();
-  const int tps = tps_env ? tps_env : ((BM == 64 && BN == 64 && a.ntaps >= 4) ? 2 : 1);
-  static const int bstages = [] {
-    const char* e = getenv("DCNN_HCONV_BSTAGES");
-    const int v = e ? atoi(e) : 3;
-    return v < 2 ? 2 : (v > 4 ? 4 : v);
-  }();
+  const int tps = (BM == 64 && BN == 64 && a.ntaps >= 4) ? 2 : 1;
+  constexpr int bstages = 3;
   // deep weight ring: one tap per step, every halo prefetch >= NBS steps ahead of its use, and
   // only where the extra stage keeps the workgroups per CU (LDS-bound occupancy: losing one
   // costs more than the deeper prefetch gains, measured 63.4k vs 65.0k img/s on ResNet-18)
@@ -733,11 +568,7 @@ static void launch_hconv(HConvArgs a, hipStream_t s) {
     return 163840 / (main > epi ? main : epi);
   };
   int nbs = (tps == 1 && a.ntaps >= bstages) ? bstages : 2;
-  static const int keep_occ = [] {  // DCNN_HCONV_KEEP_OCC=0: deepest ring even at fewer workgroups per CU
-    const char* e = getenv("DCNN_HCONV_KEEP_OCC");
-    return e ? atoi(e) : 1;
-  }();
-  while (keep_occ && nbs > 2 && wg_per_cu(nbs) < wg_per_cu(2)) --nbs;
+  while (nbs > 2 && wg_per_cu(nbs) < wg_per_cu(2)) --nbs;
 #define DCNN_HC(TPS, NHB, NBS)                                                                         \
   {                                                                                                    \
     auto k = hconv_kernel<BM, BN, TPS, NHB, NBS, F32O>;                                                \
@@ -745,12 +576,8 @@ static void launch_hconv(HConvArgs a, hipStream_t s) {
     DCNN_HIP_CHECK(hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, lds)); \
     hipLaunchKernelGGL(k, dim3(grid * a.splits), dim3(256), lds, s, a);                                \
   }
-  if (tps == 3) {
-    if (multi) DCNN_HC(3, 2, 2) else DCNN_HC(3, 1, 2)
-  } else if (tps == 2) {
+  if (tps == 2) {
     if (multi) DCNN_HC(2, 2, 2) else DCNN_HC(2, 1, 2)
-  } else if (nbs == 4) {
-    if (multi) DCNN_HC(1, 2, 4) else DCNN_HC(1, 1, 4)
   } else if (nbs == 3) {
     if (multi) DCNN_HC(1, 2, 3) else DCNN_HC(1, 1, 3)
   } else {
@@ -758,54 +585,6 @@ static void launch_hconv(HConvArgs a, hipStream_t s) {
   }
 #undef DCNN_HC
   DCNN_LAUNCH_CHECK();
-}
-
-// weight-stationary 64 -> 64 channel path (hconv_ws_kernel): opt-in (DCNN_HCONV_WS=1). Measured
-// slower than the weight ring on ResNet-18 layer 1 (batch 256: forward 56.5 vs 45.5 us, dgrad
-// 47.4 vs 42.3 us; batch 64: 22.0 vs 19.0 us): the 144 weight registers leave one wave per SIMD,
-// and the epilogue's global-memory latency is no longer hidden by other resident workgroups
-static int g_hconv_ws = [] {
-  const char* e = getenv("DCNN_HCONV_WS");
-  return e ? atoi(e) : 0;
-}();
-void hconv_set_ws(int on) { g_hconv_ws = on; }
-
-static bool launch_hconv_ws(HConvArgs a, hipStream_t s) {
-  if (!g_hconv_ws || a.Cf || a.Cs != 64 || a.N != 64 || a.ntaps != 9 || a.splits != 1 || a.fold.part ||
-      a.ldb < 9 * 64)
-    return false;
-  int bm, bn;
-  hconv_pick(a, &bm, &bn);
-  if (bm != 128 || bn != 64 || !hconv_geometry(a.NB, a.H, a.W, bm, &a.TH, &a.TW, &a.IMG)) return false;
-  const int hp = a.IMG * (a.TH + 2) * (a.TW + 2);
-  const int hn = (hp + 31) / 32;
-  a.HPR = hn * 32;
-  const int tiles = (a.NB / a.IMG) * (a.H / a.TH) * (a.W / a.TW);
-  const int lds = 2 * a.HPR * 128 + 128 * HC<128, 64, 1, 1, 2, false>::EPI_PITCH;
-#define DCNN_HWS(HN_)                                                                                     \
-  if (hn == HN_) {                                                                                        \
-    auto k = hconv_ws_kernel<HN_>;                                                                        \
-    static int per_cu = -1, cus = 0;                                                                      \
-    if (per_cu < 0) {                                                                                     \
-      DCNN_HIP_CHECK(hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, lds)); \
-      int dev = 0;                                                                                        \
-      DCNN_HIP_CHECK(hipGetDevice(&dev));                                                                 \
-      DCNN_HIP_CHECK(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev));            \
-      DCNN_HIP_CHECK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, (const void*)k, 256, lds));    \
-      if (per_cu < 1) per_cu = 1;                                                                         \
-    }                                                                                                     \
-    DCNN_HIP_CHECK(hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, lds));   \
-    int grid = cus * per_cu;                                                                              \
-    if (grid > tiles) grid = tiles;                                                                       \
-    const int per_wg = (tiles + grid - 1) / grid;                                                         \
-    grid = (tiles + per_wg - 1) / per_wg;                                                                 \
-    hipLaunchKernelGGL(k, dim3(grid), dim3(256), lds, s, a, tiles, per_wg);                               \
-    DCNN_LAUNCH_CHECK();                                                                                  \
-    return true;                                                                                          \
-  }
-  DCNN_HWS(6) DCNN_HWS(7) DCNN_HWS(9)
-#undef DCNN_HWS
-  return false;
 }
 
 void hconv(HConvArgs a, hipStream_t s) {
@@ -818,26 +597,14 @@ void hconv(HConvArgs a, hipStream_t s) {
     throw std::runtime_error("hconv: split count / workspace mismatch (use hconv_splits)");
   int bm, bn;
   hconv_pick(a, &bm, &bn);
-  if (a.fold.part && a.N % 64) throw std::runtime_error("hconv: statistics fold needs N % 64 == 0");
-  if (a.fold.part && !a.Cf && hconv_v3(a.NB, a.H, a.W, a.Cs, a.N, a.ntaps))
-    throw std::runtime_error("hconv: no statistics fold on the hconv3 path (check hconv_v3 first)");
-  if (a.fold.part) {
-    const int rows = (a.NB * a.H * a.W + bm - 1) / bm;
-    if (!a.stats || a.fold.group < 1 || a.fold.rows != rows || !a.fold.tickets ||
-        a.fold.ngroups != (rows + a.fold.group - 1) / a.fold.group)
-      throw std::runtime_error("hconv: statistics fold rows / groups mismatch");
-  }
-  if (!a.fold.part && !a.Cf && hconv3_try(a, s)) return;
-  if (launch_hconv_ws(a, s)) return;
+  if (!a.Cf && hconv3_try(a, s)) return;
   if (a.Cf) {
     if (a.bnb.x) throw std::runtime_error("hconv: no backward-BN fusion with fp32 output");
-    if (bm == 256 && bn == 64) return launch_hconv<256, 64, true>(a, s);
     if (bm == 128 && bn == 128) return launch_hconv<128, 128, true>(a, s);
     if (bm == 128 && bn == 64) return launch_hconv<128, 64, true>(a, s);
     if (bm == 64 && bn == 128) return launch_hconv<64, 128, true>(a, s);
     return launch_hconv<64, 64, true>(a, s);
   }
-  if (bm == 256 && bn == 64) return launch_hconv<256, 64, false>(a, s);
   if (bm == 128 && bn == 128) return launch_hconv<128, 128, false>(a, s);
   if (bm == 128 && bn == 64) return launch_hconv<128, 64, false>(a, s);
   if (bm == 64 && bn == 128) return launch_hconv<64, 128, false>(a, s);

@@ -641,12 +641,9 @@ __global__ void __launch_bounds__(NW * 64, 8 / NW) hconv3_kernel(HConvArgs p, H3
 // ------------------------------------------------------------------------------------------------
 // host side
 // ------------------------------------------------------------------------------------------------
-int hconv_split_target();  // hconv.hip (DCNN_HCONV_SPLIT / hconv_set_split_target; 0 = never split)
+int hconv_split_target();  // hconv.hip (hconv_set_split_target; 0 = never split)
 
-static int g_h3 = [] {
-  const char* e = getenv("DCNN_HCONV3");
-  return e ? atoi(e) : 1;
-}();
+static int g_h3 = 1;  // hconv3_enable(0): the previous kernel (test hook)
 void hconv3_enable(int on) { g_h3 = on; }
 static unsigned long long* g_h3_stamps = nullptr;
 void hconv3_set_stamps(uintptr_t p) { g_h3_stamps = reinterpret_cast<unsigned long long*>(p); }
@@ -742,7 +739,7 @@ static void launch_h3_plan(const H3Plan& pl, const HConvArgs& a, const H3Geo& g,
 // returns false when the shape / taps / epilogue options are not covered (caller falls back)
 bool hconv3_try(const HConvArgs& a0, hipStream_t s) {
   H3Plan pl;
-  if (a0.Cf || a0.fold.part || h3_epi(a0) < 0 || !hconv3_plan(a0.NB, a0.H, a0.W, a0.Cs, a0.N, a0.ntaps, &pl))
+  if (a0.Cf || h3_epi(a0) < 0 || !hconv3_plan(a0.NB, a0.H, a0.W, a0.Cs, a0.N, a0.ntaps, &pl))
     return false;
   H3Geo g{};
   for (int t = 0; t < 9; ++t) g.tb[t] = -1;

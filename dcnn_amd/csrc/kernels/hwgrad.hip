@@ -86,8 +86,8 @@ __global__ void __launch_bounds__(256, 1) hwgrad_kernel(HWArgs p) {
 
   // DCNN_HWGRAD_DBG (timing experiments only, results are wrong when set): bit 1 = no slab
   // stores, bit 2 = no global loads (zero-record descriptors), bit 16 = no pixel tiles
-  const i32x4 rsY = raw_rsrc(p.dY, (p.dbg & 2) ? 0u : p.dy_bytes);
-  const i32x4 rsX = raw_rsrc(p.X, (p.dbg & 2) ? 0u : p.x_bytes);
+  const i32x4 rsY = raw_rsrc(p.dY, p.dy_bytes);
+  const i32x4 rsX = raw_rsrc(p.X, p.x_bytes);
 
   // ---- dY loader: 4 glds per lane, rows (pixels) fixed relative to the tile origin ----
   const int slot = lane & 7;
@@ -150,7 +150,7 @@ __global__ void __launch_bounds__(256, 1) hwgrad_kernel(HWArgs p) {
   const int bcol = wid * 16 + 4 * (lane & 3);  // B column (input channel) this lane reads
   const bool do_bias = p.bias_slab != nullptr && c0 == 0;
   float bias_acc = 0.f;
-  const int nt = (p.dbg & 16) ? 0 : tend - tbeg;
+  const int nt = tend - tbeg;
   // tile it lives in stage it % NS; tile it + NS - 1 is issued at the top of iteration it into
   // the stage iteration it - 1 consumed (the barrier closing it - 1 retired every read of it)
   if (nt > 0) load_tile(0, tbeg);
@@ -244,7 +244,7 @@ __global__ void __launch_bounds__(256, 1) hwgrad_kernel(HWArgs p) {
       const int row = q >> 4, c4 = (q & 15) * 4;
       const int u = row >> 6, co = co0 + (row & 63);
       const float4 v = *reinterpret_cast<const float4*>(stg + row * 68 + c4);
-      if (!(p.dbg & 1)) *reinterpret_cast<float4*>(out + (long)co * Ng + (t0 + u) * p.Cs + c0 + c4) = v;
+      *reinterpret_cast<float4*>(out + (long)co * Ng + (t0 + u) * p.Cs + c0 + c4) = v;
     }
   }
   if (do_bias) {
@@ -525,14 +525,7 @@ bool hwgrad_supported(int NB, int H, int W, int Cs, int Co, int ntaps) {
   return (long)NB * H * W * (Cs > Co ? Cs : Co) * 2 < (1l << 31);
 }
 
-static int hw_target_blocks() {
-  static const int v = [] {
-    const char* e = getenv("DCNN_HWGRAD_BLOCKS");
-    const int x = e ? atoi(e) : 0;
-    return x > 0 ? x : 256;
-  }();
-  return v;
-}
+static constexpr int kHwTargetBlocks = 256;  // split-K target: one workgroup per CU
 
 // number of split-K partial slabs (the caller sizes the slab [splits][Co][ntaps*Cs])
 int hwgrad_splits(int NB, int H, int W, int Cs, int Co) {
@@ -540,40 +533,22 @@ int hwgrad_splits(int NB, int H, int W, int Cs, int Co) {
   if (!hw_geometry(H, W, &th, &tw, &img)) return 1;
   const int total = (NB / img) * (H / th) * (W / tw);
   const int per_split = (Co / 64) * (Cs / 64);
-  int want = (hw_target_blocks() + per_split - 1) / per_split;
+  int want = (kHwTargetBlocks + per_split - 1) / per_split;
   if (want < 1) want = 1;
   if (want > total) want = total;
-  // at least DCNN_HWGRAD_MIN_TPS (default 2) tiles per split: a one-tile block writes ~4.6x the
-  // bytes it reads as fp32 partials (64x576 per 128 pixels). ResNet-50 batch 32 (one-tile splits on
-  // its 32x32 maps): 7.76k -> 7.90k img/s with 2 (4: same; profiles/wgrad_splits_r3.md)
-  static const int min_tps = [] {
-    const char* e = getenv("DCNN_HWGRAD_MIN_TPS");
-    return e ? atoi(e) : 2;
-  }();
+  // at least 2 tiles per split: a one-tile block writes ~4.6x the bytes it reads as fp32
+  // partials (64x576 per 128 pixels). ResNet-50 batch 32 (one-tile splits on its 32x32 maps):
+  // 7.76k -> 7.90k img/s (profiles/wgrad_splits_r3.md)
+  constexpr int min_tps = 2;
   if (min_tps > 1 && want > total / min_tps) want = total / min_tps > 1 ? total / min_tps : 1;
   const int tps = (total + want - 1) / want;
   return (total + tps - 1) / tps;
 }
 
-// kernel generation: 2 = tap-shift-invariant addressing where it applies, 1 = first kernel only
-static int g_hwgrad_version = [] {
-  const char* e = getenv("DCNN_HWGRAD_V");
-  return e ? atoi(e) : 2;
-}();
+// kernel generation: 2 = tap-shift-invariant addressing where it applies (8 waves, taps split
+// 0-4 / 5-8 over two waves per SIMD), 1 = first kernel only (test hook)
+static int g_hwgrad_version = 2;
 void hwgrad_set_version(int v) { g_hwgrad_version = v; }
-// second-generation kernel on 4x4 maps too (DCNN_HWGRAD4=0: keep the first kernel there)
-static int g_hwgrad4 = [] {
-  const char* e = getenv("DCNN_HWGRAD4");
-  return e ? atoi(e) : 1;
-}();
-
-// tap-split variants of hwgrad2: 2 (default) = 8 waves, two per SIMD (taps 0-4 / 5-8); 3 = 12 waves
-// (taps in thirds); 1 = the 4-wave kernel (DCNN_HWGRAD_TS)
-static int g_hw_ts = [] {
-  const char* e = getenv("DCNN_HWGRAD_TS");
-  const int v = e ? atoi(e) : 2;
-  return v == 1 || v == 3 ? v : 2;
-}();
 
 void hwgrad(HWArgs a, int splits, hipStream_t s) {
   if (!hwgrad_supported(a.NB, a.H, a.W, a.Cs, a.Co, a.ntaps)) throw std::runtime_error("hwgrad: unsupported shape");
@@ -595,37 +570,30 @@ void hwgrad(HWArgs a, int splits, hipStream_t s) {
   hw_geometry(a.H, a.W, &a.TH, &a.TW, &a.IMG);
   const int total = (a.NB / a.IMG) * (a.H / a.TH) * (a.W / a.TW);
   a.tiles_per_split = (total + splits - 1) / splits;
-  static const int dbg = [] { const char* e = getenv("DCNN_HWGRAD_DBG"); return e ? atoi(e) : 0; }();
-  a.dbg = dbg;  // timing experiments only (results are wrong when set)
   const int grid = splits * (a.Co / 64) * (a.Cs / 64);
-  static const int stages = [] {
-    const char* e = getenv("DCNN_HWGRAD_STAGES");
-    return (e && atoi(e) == 2) ? 2 : 3;
-  }();
+  constexpr int stages = 3;
   // tap-shift-invariant variant (hwgrad2_kernel) for the standard 3x3 / pad-1 taps on 16- and
-  // 8-wide maps (DCNN_HWGRAD_V=1 keeps the first kernel)
+  // 8-wide maps (hwgrad_set_version(1) keeps the first kernel)
   const int ver = g_hwgrad_version;
   bool std_taps = a.ntaps == 9;
   for (int t = 0; t < a.ntaps && std_taps; ++t) std_taps = a.tap_dy[t] == t / 3 - 1 && a.tap_dx[t] == t % 3 - 1;
-  if (ver == 2 && std_taps && !a.dbg) {
+  if (ver == 2 && std_taps) {
 #define DCNN_HW2(TW_, TH_, IMG_, NS_)                                                                   \
     if (a.TW == TW_ && a.TH == TH_ && a.IMG == IMG_) {                                                  \
-      auto k = g_hw_ts == 3 ? hwgrad2_kernel<TW_, TH_, IMG_, NS_, 3>                                    \
-             : g_hw_ts == 2 ? hwgrad2_kernel<TW_, TH_, IMG_, NS_, 2> : hwgrad2_kernel<TW_, TH_, IMG_, NS_, 1>; \
+      auto k = hwgrad2_kernel<TW_, TH_, IMG_, NS_, 2>;                                                  \
       const int lds = NS_ * HWGeo2<TW_, TH_, IMG_>::STAGE;                                              \
       DCNN_HIP_CHECK(hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, lds)); \
-      hipLaunchKernelGGL(k, dim3(grid, a.npairs), dim3(256 * g_hw_ts), lds, s, a);                      \
+      hipLaunchKernelGGL(k, dim3(grid, a.npairs), dim3(512), lds, s, a);                                \
       DCNN_LAUNCH_CHECK();                                                                              \
       return;                                                                                           \
     }
     DCNN_HW2(16, 8, 1, 3)  // 3 x 48 KB
     DCNN_HW2(8, 8, 2, 2)   // 2 x 56 KB (three stages would need 168 KB)
-    if (g_hwgrad_version == 2 && a.TW == 4 && a.TH == 4 && a.IMG == 8 && g_hwgrad4 != 0) {
-      auto k = g_hw_ts == 3   ? hwgrad2_kernel<4, 4, 8, 2, 3>
-               : g_hw_ts == 2 ? hwgrad2_kernel<4, 4, 8, 2, 2> : hwgrad2_kernel<4, 4, 8, 2, 1>;  // 2 x 64 KB
+    if (g_hwgrad_version == 2 && a.TW == 4 && a.TH == 4 && a.IMG == 8) {
+      auto k = hwgrad2_kernel<4, 4, 8, 2, 2>;  // 2 x 64 KB
       const int lds = 2 * HWGeo2<4, 4, 8>::STAGE;
       DCNN_HIP_CHECK(hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, lds));
-      hipLaunchKernelGGL(k, dim3(grid, a.npairs), dim3(256 * g_hw_ts), lds, s, a);
+      hipLaunchKernelGGL(k, dim3(grid, a.npairs), dim3(512), lds, s, a);
       DCNN_LAUNCH_CHECK();
       return;
     }

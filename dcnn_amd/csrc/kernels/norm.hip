@@ -167,13 +167,9 @@ struct StatAcc {
 };
 constexpr int kStatRW = 16;
 // waves per reduce block (rows per block = 16 x waves): fewer rows per block = more blocks in the
-// (latency-bound) reduce and more partials for the consumers to merge (DCNN_STAT_WAVES 4/8/16)
-// (default 8: 0.1-0.6% faster end to end than 16 at batch 64 and 256, tools/gpu_envsweep.sh)
-static int g_stat_waves = [] {
-  const char* e = getenv("DCNN_STAT_WAVES");
-  const int v = e ? atoi(e) : 8;
-  return (v == 4 || v == 16) ? v : 8;
-}();
+// (latency-bound) reduce and more partials for the consumers to merge (8: 0.1-0.6% faster end
+// to end than 16 at batch 64 and 256)
+static constexpr int g_stat_waves = 8;
 
 // Merge up to kStatRW rows [r0, r1) of channel c: every load in flight at once, then a pairwise
 // tree (log2 16 = 4 dependent merge levels instead of a 16-long chain). Fixed order.
@@ -870,25 +866,20 @@ bool bn_apply_dual(const BnSide& a, const BnSide& b, void* y, long R, int C, int
 
 // vectors per thread per trip and grid of the bf16 apply passes
 static void bn_v_launch_shape(long nv, int* U, int* grid) {
-  // DCNN_BN_U (1 / 2 / 4) and DCNN_BN_GRID (workgroup cap) override the choice (A/B experiments)
-  static const int u_env = [] { const char* e = getenv("DCNN_BN_U"); const int v = e ? atoi(e) : 0; return (v == 1 || v == 2 || v == 4) ? v : 0; }();
   // default: 1 vector per lane per trip, at most 1024 workgroups, so the large passes make
   // several software-pipelined trips (next trip's loads in flight under this trip's stores).
   // Measured on the ResNet-18 shapes (benchmarks/bn_bench.py, tools/gpu_bnsweep.sh): one pass
   // over all 12 shape/op cases 117.9 us with 4 vectors per lane over <= 2048 workgroups ->
   // 107.7 us (2 vectors: 107.0 us, but 0.5% slower end to end at batch 64 / 128)
-  static const long g_cap = [] { const char* e = getenv("DCNN_BN_GRID"); const long v = e ? atol(e) : 0; return v > 0 ? v : 1024l; }();
-  *U = u_env ? u_env : 1;
+  constexpr long g_cap = 1024;
+  *U = 1;
   long g = (nv + 256l * *U - 1) / (256l * *U);
   if (g > g_cap) g = g_cap;
   if (g < 1) g = 1;
   *grid = (int)g;
 }
 
-static bool g_bn_v = [] {
-  const char* e = getenv("DCNN_BN_V");
-  return e ? atoi(e) != 0 : true;
-}();
+static bool g_bn_v = true;  // bn_set_vectorised(0): the generic kernels (test hook)
 
 void bn_set_vectorised(int on) { g_bn_v = on != 0; }
 

@@ -751,8 +751,7 @@ int maxpool_bwd_bnb_rows(PoolGeom g) { return bnb_pool_blocks(g); }
 void maxpool_bwd_bnb(const bf16* dy, const uint8_t* idx, const bf16* ypool, const bf16* x, const float* mean,
                      const float* istd, bf16* dx, PoolGeom g, float* slab, float* zero_sums, hipStream_t s) {
   if (!maxpool_bwd_bnb_supported(g)) throw std::runtime_error("maxpool_bwd_bnb: unsupported geometry");
-  static const bool win = [] { const char* e = getenv("DCNN_POOL_BWD_WIN"); return e ? atoi(e) != 0 : true; }();
-  if (win && g.H % g.ph == 0 && g.W % g.pw == 0 && g.OH == g.H / g.ph && g.OW == g.W / g.pw &&
+  if (g.H % g.ph == 0 && g.W % g.pw == 0 && g.OH == g.H / g.ph && g.OW == g.W / g.pw &&
       (long)g.N * g.H * g.W * g.C < (1l << 31)) {
     hipLaunchKernelGGL(maxpool_bwd_bnb_w_kernel, dim3(bnb_pool_blocks(g)), dim3(256), 0, s, dy, idx, ypool, x, mean,
                        istd, dx, g, slab, zero_sums);

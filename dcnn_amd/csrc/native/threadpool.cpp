@@ -58,19 +58,11 @@ void ThreadPool::set_num_threads(int n) {
   start(n);
 }
 
-// Optional spin-before-block (DCNN_POOL_SPIN=<iterations>): workers poll the generation word and
-// the caller polls the completion count before sleeping on the condition variables. Off by default:
-// on virtualised hosts PAUSE loops trap to the hypervisor and spinning threads steal the vCPUs the
-// work needs (measured: 8 spinning workers made a 100 us loop take 3 ms); on bare metal a few
-// thousand iterations cut the hand-off from a futex round trip to about a microsecond.
+// No spin-before-block: on virtualised hosts PAUSE loops trap to the hypervisor and spinning
+// threads steal the vCPUs the work needs (measured: 8 spinning workers made a 100 us loop take
+// 3 ms), so workers and the caller sleep on the condition variables right away.
 namespace {
-int spin_iters() {
-  static const int v = [] {
-    const char* e = std::getenv("DCNN_POOL_SPIN");
-    return e ? std::max(0, std::atoi(e)) : 0;
-  }();
-  return v;
-}
+constexpr int spin_iters() { return 0; }
 inline void cpu_relax() { __builtin_ia32_pause(); }
 }  // namespace
 

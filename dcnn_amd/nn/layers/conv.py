@@ -110,11 +110,10 @@ class Conv2D(ParameterizedLayer):
             g = hip.to_act(grad, self.compute_dtype)
             gb = self._grads[1].view(-1) if self.use_bias else None
             if stem:  # forward ran stem.hip (never with an input gradient)
-                hip.wgrad_stream.run(lambda: hip.stem_conv_wgrad(g, x, self._grads[0], gb), g, x)
+                hip.stem_conv_wgrad(g, x, self._grads[0], gb)
                 return None
-            # weight gradient on the side stream (hip._SideStream): overlaps the dgrad chain below
-            hip.wgrad_stream.run(lambda: hip.conv2d_wgrad(g, x, self.weights.shape, (self.stride_h, self.stride_w),
-                                                          (self.pad_h, self.pad_w), self._grads[0], gb), g, x)
+            hip.conv2d_wgrad(g, x, self.weights.shape, (self.stride_h, self.stride_w), (self.pad_h, self.pad_w),
+                             self._grads[0], gb)
             if not self.needs_input_grad:
                 return None
             if getattr(self, "_wt_valid", False):
@@ -240,8 +239,7 @@ class Dense(ParameterizedLayer):
         if x2.is_cuda:
             from ...ops import hip
             g2 = g2.to(self.compute_dtype).contiguous()
-            hip.wgrad_stream.run(lambda: hip.dense_wgrad(g2, x2, self._grads[0],
-                                                         self._grads[1].view(-1) if self.use_bias else None), g2, x2)
+            hip.dense_wgrad(g2, x2, self._grads[0], self._grads[1].view(-1) if self.use_bias else None)
             if not self.needs_input_grad:
                 return None
             w = self.weight_operand(0)

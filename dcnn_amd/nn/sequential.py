@@ -228,25 +228,22 @@ class Sequential:
         if getattr(self, "_transposer", None) is not None:
             self._transposer.run()
         if self.device.is_gpu():
-            from ..ops.hip import grad_reducer, wgrad_stream
+            from ..ops.hip import grad_reducer
             grad_reducer.begin()
-            wgrad_stream.begin()
 
     def flush_gradients(self) -> None:
-        """Complete every queued weight-gradient reduction and join the weight-gradient side
-        stream (before a gradient is consumed mid-backward, e.g. a data-parallel bucket all-reduce)."""
+        """Complete every queued weight-gradient reduction (before a gradient is consumed
+        mid-backward, e.g. a data-parallel bucket all-reduce)."""
         if self.device.is_gpu():
-            from ..ops.hip import grad_reducer, wgrad_stream
+            from ..ops.hip import grad_reducer
             grad_reducer.flush()
-            wgrad_stream.join()
 
     def finish_backward(self) -> None:
         if getattr(self, "_transposer", None) is not None:
             self._transposer.invalidate()
         if self.device.is_gpu():
-            from ..ops.hip import grad_reducer, wgrad_stream
+            from ..ops.hip import grad_reducer
             grad_reducer.end()
-            wgrad_stream.end()
 
     def set_first_layer_input_grad(self, need: bool) -> None:
         """Skip the (unused) input gradient of the first layer (reference G9 wasted it)."""

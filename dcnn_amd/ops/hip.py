@@ -10,7 +10,6 @@ allocator otherwise), so a whole training step can be captured into a hipGraph.
 """
 from __future__ import annotations
 
-import contextlib
 import functools
 import os
 import threading
@@ -108,8 +107,6 @@ def _g2_ok(Cs, N):
     return Cs % 8 == 0 and N % 8 == 0
 
 
-_HCONV = os.environ.get("DCNN_HCONV", "1") != "0"
-_HWGRAD = os.environ.get("DCNN_HWGRAD", "1") != "0"
 
 # ---- split-precision fp32 convolutions on the bf16 halo kernels
 # An fp32 operand x is split once into bf16 hi = bf16(x), lo = bf16(x - hi). A conv sums over
@@ -119,7 +116,7 @@ _HWGRAD = os.environ.get("DCNN_HWGRAD", "1") != "0"
 # stride-1 convs (forward and dgrad) therefore run on hconv (3x the channels, fp32 epilogue), and
 # their weight gradients on hwgrad with three (dY, X) channel windows of the same split rows:
 # (dyh, xh), (dyh, xl), (dyl, xh). Other fp32 convs keep the exact f32-MFMA gathered GEMMs.
-_F32_CONCAT = os.environ.get("DCNN_F32_CONCAT", "1") != "0"
+_F32_CONCAT = True
 
 
 def set_f32_concat(on: bool) -> None:
@@ -158,21 +155,23 @@ def _f32_concat_ok(C, Co):
     return _F32_CONCAT and C % 64 == 0 and Co % 64 == 0
 
 
-_HCONV_1X1 = os.environ.get("DCNN_HCONV_1X1", "1") != "0"
+
+
+_HCONV_1X1 = True  # K >= 1024 1x1 convs on small grids run on the split-K halo kernel
 
 
 def _hconv_ok(N, OH, OW, H, W, sh, sw, Cs, Co, taps, wop, split3=False):
     """Halo-tiled direct conv applies to stride-1 'same' convs with a 1-pixel reach (3x3/pad 1
     forward and its dgrad) on 64-multiple channel counts. ``split3``: the caller is a 3 x bf16
     fp32 concat path (Cs = 3 x the real channels): 1x1 convs stay on the exact fp32 GEMM there."""
-    if not _HCONV or (sh, sw) != (1, 1) or (OH, OW) != (H, W) or len(taps) > 9:
+    if (sh, sw) != (1, 1) or (OH, OW) != (H, W) or len(taps) > 9:
         return False
     if any(abs(t[0]) > 1 or abs(t[1]) > 1 for t in taps):
         return False
     if len(taps) == 1 and not (_HCONV_1X1 and not split3 and Cs >= 1024 and (N * OH * OW // 64) * (Co // 64) < 256):
         # 1x1: the plain GEMM is already read-once. Except K >= 1024 1x1 convs (not on the
         # streaming kernel) whose GEMM grid would be < 256 tiles: the halo kernel splits their K
-        # over the channel chunks (ResNet-50 b32: 7.87k -> 7.92k img/s; DCNN_HCONV_1X1=0 = off)
+        # over the channel chunks (ResNet-50 b32: 7.87k -> 7.92k img/s)
         return False
     return bool(kernels().hconv_supported(N, H, W, Cs, Co, len(taps)))
 
@@ -202,29 +201,6 @@ def _hconv_split(K, NB, H, W, Cs, N, ntaps, device):
     return s, part.data_ptr(), _ticket(device, tiles * 64, "hconv").data_ptr()
 
 
-_FOLD = os.environ.get("DCNN_STAT_FOLD", "0") == "1"  # opt-in: measured slower (profiles/experiment_inlaunch_stat_fold_r2.md)
-# only small row counts fold: the merging workgroup's group of rows must be cheap next to a launch
-_FOLD_MAX_ROWS = int(os.environ.get("DCNN_STAT_FOLD_ROWS", "128"))
-_NOFOLD = (0, 0, 0, 0, 0)
-
-
-def set_stat_fold(on: bool) -> None:
-    """Fold the BatchNorm statistics rows inside the producing conv launch (statfold.h) instead of
-    a separate bn_stat_reduce launch (bf16 hconv / gemm_g2 producers)."""
-    global _FOLD
-    _FOLD = bool(on)
-
-
-def _fold(rows, N, mode, device, g2=False):
-    """(kernel fold args, :class:`Stats` the consumers read) for a producer writing ``rows``
-    statistics rows of N channels; (_NOFOLD, None) when the launch does not fold."""
-    if not _FOLD or rows < 2 or rows > _FOLD_MAX_ROWS or N % 64 or (g2 and N % 128 and N != 64):
-        return _NOFOLD, None
-    group = -(-rows // 8)           # <= 8 partials for the consumers' prologue merge
-    ng = -(-rows // group)
-    part = _empty((ng, 3, N) if ng > 1 else (2 * N,), F32, device)
-    tk = _ticket(device, ng * (N // 64) * 64, "fold")
-    return (part.data_ptr(), tk.data_ptr(), group, ng, rows), Stats(part, ng, mode)
 
 
 def conv2d_fwd(x, w, bias, stride, pad, *, stats=False, residual=None, relu=False, out_fp32=False):
@@ -267,7 +243,7 @@ def conv2d_fwd(x, w, bias, stride, pad, *, stats=False, residual=None, relu=Fals
         K.hconv(xs.data_ptr(), ws.data_ptr(), 0, _nbytes(xs), _nbytes(ws), N, H, W, 3 * Ci, Co, KH * KW * 3 * Ci,
                 [(t[0], t[1], t[3]) for t in _fwd_taps(3 * Ci, W, KH, KW, ph, pw)], ptr(bias), 0, ptr(slab),
                 int(relu), ptr(sums), 2 * Co if stats else 0, _NOBNB, y.data_ptr(), ptr(residual),
-                *_NOSPLIT, stream_ptr(), _NOFOLD)
+                *_NOSPLIT, stream_ptr())
         return y, ((slab, rows, sums) if stats else None)
     if x.dtype == F32:  # fp32 compute path: MFMA f32 16x16x4 gathered GEMM
         y = _empty((N, Co, OH, OW), F32, x.device, True)
@@ -295,32 +271,27 @@ def conv2d_fwd(x, w, bias, stride, pad, *, stats=False, residual=None, relu=Fals
     if not out_fp32 and _hconv_ok(N, OH, OW, H, W, sh, sw, Ci, Co, taps, w):
         y = _empty((N, Co, OH, OW), BF16, x.device, True)
         slab, rows, sums = None, 0, None
-        fold, fst = _NOFOLD, None
         if stats:
             rows = K.hconv_stat_rows(N, H, W, Ci, Co, len(taps), 0)
             slab = _empty((rows, 3, Co), F32, x.device)
             sums = _empty((2 * Co,), F32, x.device)  # zeroed in-kernel
-            if not K.hconv_v3(N, H, W, Ci, Co, len(taps)):  # (no in-launch fold on hconv3)
-                fold, fst = _fold(rows, Co, 0, x.device)
         K.hconv(x.data_ptr(), w.data_ptr(), y.data_ptr(), _nbytes(x), _nbytes(w), N, H, W, Ci, Co, KH * KW * Ci,
                 [(t[0], t[1], t[3]) for t in taps], ptr(bias), ptr(residual), ptr(slab), int(relu), ptr(sums),
                 2 * Co if stats else 0, _NOBNB, 0, 0, *_hconv_split(K, N, H, W, Ci, Co, KH * KW, x.device),
-                stream_ptr(), fold)
-        return y, ((fst if fst is not None else slab, rows, sums) if stats else None)
+                stream_ptr())
+        return y, ((slab, rows, sums) if stats else None)
     if _g2_ok(Ci, Co) and not out_fp32:
         y = _empty((N, Co, OH, OW), BF16, x.device, True)
         slab, rows, sums = None, 0, None
-        fold, fst = _NOFOLD, None
         if stats:
             rows = K.gemm_g2_stat_rows(M, Co)
             slab = _empty((rows, 3, Co), F32, x.device)
             sums = _empty((2 * Co,), F32, x.device)  # zeroed in-kernel
-            fold, fst = _fold(rows, Co, 0, x.device, g2=True)
         K.gemm_g2_grouped(x.data_ptr(), w.data_ptr(), y.data_ptr(), _nbytes(x), _nbytes(w), M, Co, Ci, H, W, OH, OW,
                           sh, sw, _fwd_taps(Ci, W, KH, KW, ph, pw), KH * KW * Ci, Co, OH, OW, 1, 1, 0, 0, ptr(bias),
                           ptr(residual), ptr(slab), int(relu), ptr(sums), 2 * Co if stats else 0, _NOBNB,
-                          stream_ptr(), [], fold)
-        return y, ((fst if fst is not None else slab, rows, sums) if stats else None)
+                          stream_ptr(), [])
+        return y, ((slab, rows, sums) if stats else None)
     # generic fallback (odd channel counts): v1 kernels
     y = _empty((N, Co, OH, OW), F32 if out_fp32 else BF16, x.device, True)
     slab, rows = None, 0
@@ -334,12 +305,11 @@ def conv2d_fwd(x, w, bias, stride, pad, *, stats=False, residual=None, relu=Fals
     return y, ((slab, rows, sums) if stats else None)
 
 
-_STEM = os.environ.get("DCNN_STEM", "1") != "0"
 
 
 def stem_ok(x, w_shape, stride, pad):
     """The RGB stem kernels (stem.hip) take this conv: fp32 NCHW input, 3x3 s1 p1, Ci <= 4."""
-    if not _STEM or x.dtype != F32 or not x.is_contiguous() or x.dim() != 4:
+    if x.dtype != F32 or not x.is_contiguous() or x.dim() != 4:
         return False
     Co, Ci, KH, KW = w_shape
     N, C, H, W = x.shape
@@ -566,9 +536,12 @@ class BnbRequest:
         return (ptr(self.y), self.x.data_ptr(), self.mean.data_ptr(), self.istd.data_ptr())
 
 
-_BNB = os.environ.get("DCNN_BNB_FUSE", "1") != "0"
-_G2_GROUP = os.environ.get("DCNN_G2_GROUP", "1") != "0"  # strided dgrad phases in one launch
-_BNB_POOL = os.environ.get("DCNN_BNB_POOL", "1") != "0"  # the stem max-pool part of the fusion
+# fusion / batching choices, module constants so the GPU tests can compare each against the
+# unfused path it replaces
+_G2_GROUP = True  # strided dgrad phases in one launch
+_BNB = True  # backward-BatchNorm fusion (ReLU mask + statistics) into the producing dgrad epilogue
+_BN_DUAL = True  # projection-shortcut BatchNorm pairs in one pass
+_DEFER_REDUCE = True  # one batched split-K weight-gradient reduce per backward
 
 
 @functools.lru_cache(maxsize=1024)
@@ -594,69 +567,6 @@ def _dgrad_classes(H, W, OW, Co, KH, KW, sh, sw, ph, pw):
                     taps.append((dyo, dxo, (dyo * OW + dxo) * Co, (ky * KW + kx) * Co))
             (classes if taps else empty).append((ry, rx, GH, GW, tuple(taps)))
     return tuple(classes), tuple(empty)
-
-
-# opt-in (DCNN_G1S_STRIDED=1): per-class launches measured slower end to end (profiles/g1s_r3.md:
-# ResNet-18 l2.b1c1 dgrad 66.8 -> 52.9 us alone, but the whole step 78.8k -> 77.6k img/s with the
-# fused statistics and residual of the model; l3 / l4 classes and the 1-tap + 3-empty-phase
-# projections were slower than the one grouped launch even alone)
-_G1S_STRIDED = os.environ.get("DCNN_G1S_STRIDED", "0") == "1"
-_G1S_STRIDED_MIN_ROWS = int(os.environ.get("DCNN_G1S_STRIDED_MIN_ROWS", "32768"))
-
-
-def set_g1s_strided(on: bool, min_rows: int = 32768) -> None:
-    """Strided data gradients on the streaming kernel's gathered form (for classes of at least
-    ``min_rows`` GEMM rows and no empty phases) or the grouped gathered GEMM (gemm2.hip)."""
-    global _G1S_STRIDED, _G1S_STRIDED_MIN_ROWS
-    _G1S_STRIDED = bool(on)
-    _G1S_STRIDED_MIN_ROWS = int(min_rows)
-
-
-def _g1s_strided_dgrad(K, dy, wt, x_shape, allc, s, residual, bnb):
-    """Strided data gradient as one streaming launch per stride-phase class (g1s.hip gathered form):
-    class (ry, rx) is a GEMM over its taps' 64..512-deep K, written straight to its output phase;
-    phases no tap reaches run the same epilogue with no MFMA work (residual or zeros, and their
-    share of the fused BatchNorm statistics). None when a class does not fit the kernel."""
-    N, Ci, H, W = x_shape
-    Co, OH, OW = dy.shape[1], dy.shape[2], dy.shape[3]
-    if _G1S_STRIDED_MIN_ROWS > 0 and any(not taps or N * GH * GW < _G1S_STRIDED_MIN_ROWS
-                                         for _, _, GH, GW, taps in allc):
-        return None
-    fuse = (bnb is not None and _BNB and not bnb.pooled and bnb.x.dtype == BF16
-            and tuple(bnb.x.shape) == (N, Ci, H, W))
-    mode = 2 if fuse else 0
-    rows, use = [], []
-    for ry, rx, GH, GW, taps in allc:
-        r = K.g1s_gen_rows(N * GH * GW, Ci, Co, len(taps), mode)
-        use.append(r > 0)
-        if r <= 0:  # (a class deeper than 512: the gathered GEMM takes it, in the same slab)
-            if not taps or (N * GH * GW) % 64:
-                return None
-            r = K.gemm_g2_stat_rows(N * GH * GW, Ci) if fuse else 0
-        rows.append(r)
-    if not any(use):
-        return None
-    dx = _empty((N, Ci, H, W), BF16, dy.device, True)
-    slab = _empty((sum(rows), 2, Ci), F32, dy.device) if fuse else None
-    sums = _empty((2 * Ci,), F32, dy.device) if fuse else None
-    ldw = wt.shape[1] * wt.shape[2] * Co
-    st = stream_ptr()
-    r0 = 0
-    for k, (ry, rx, GH, GW, taps) in enumerate(allc):
-        sp = slab.data_ptr() + r0 * 2 * Ci * 4 if fuse else 0
-        zp = ptr(sums) if (fuse and k == 0) else 0
-        if use[k]:
-            K.g1s_gen(dy.data_ptr(), wt.data_ptr(), dx.data_ptr(), N, GH, GW, Ci, Co, ldw,
-                      [(t[0], t[1], t[3]) for t in taps], OH, OW, H, W, s, ry, rx, ptr(residual), sp, zp,
-                      2 * Ci if zp else 0, bnb.args() if fuse else _NOBNB, mode, st)
-        else:
-            K.gemm_g2(dy.data_ptr(), wt.data_ptr(), dx.data_ptr(), _nbytes(dy), _nbytes(wt), N * GH * GW, Ci, Co,
-                      OH, OW, GH, GW, 1, 1, taps, ldw, Ci, H, W, s, s, ry, rx, 0, ptr(residual), sp, 0, zp,
-                      2 * Ci if zp else 0, bnb.args() if fuse else _NOBNB, st)
-        r0 += rows[k]
-    if fuse:
-        dx._bnb = (bnb.bn, slab, sum(rows), sums)
-    return dx
 
 
 def conv2d_dgrad(dy, wt, x_shape, stride, pad, *, residual=None, bnb=None):
@@ -692,10 +602,6 @@ def conv2d_dgrad(dy, wt, x_shape, stride, pad, *, residual=None, bnb=None):
     empty_class = bool(empty)
     odt = F32 if f32 else BF16
     allc = classes + empty
-    if not f32 and _G1S_STRIDED and sh == sw and sh > 1:
-        dx = _g1s_strided_dgrad(K, dy, wt, (N, Ci, H, W), allc, sh, residual, bnb)
-        if dx is not None:
-            return dx
     if (not f32 and empty_class and len(classes) > 1 and _G2_GROUP and len(allc) <= 4
             and len({(c[2], c[3]) for c in allc}) == 1 and (N * allc[0][2] * allc[0][3]) % 128 == 0):
         # phases no tap reaches join the grouped launch as zero-tap classes: their epilogue writes
@@ -711,7 +617,7 @@ def conv2d_dgrad(dy, wt, x_shape, stride, pad, *, residual=None, bnb=None):
         dx = _empty((N, Ci, H, W), BF16, dy.device, True)
         K.gemm_g2_grouped(dy.data_ptr(), wt.data_ptr(), dx.data_ptr(), _nbytes(dy), _nbytes(wt), M, Ci, Co, OH, OW,
                           GH, GW, 1, 1, taps_all, KH * KW * Co, Ci, H, W, sh, sw, 0, 0, 0, ptr(residual), 0, 0, 0, 0,
-                          _NOBNB, stream_ptr(), groups, _NOFOLD)
+                          _NOBNB, stream_ptr(), groups)
         return dx
     if empty_class:
         # positions no tap reaches keep the residual (or zero); a memset / async copy node, not a kernel
@@ -730,7 +636,7 @@ def conv2d_dgrad(dy, wt, x_shape, stride, pad, *, residual=None, bnb=None):
         wts = split3_rows(wt, Ci * KH * KW, Co, 1)
         K.hconv(dys.data_ptr(), wts.data_ptr(), 0, _nbytes(dys), _nbytes(wts), N, OH, OW, 3 * Co, Ci,
                 KH * KW * 3 * Co, [(t[0], t[1], 3 * t[3]) for t in classes[0][4]], 0, 0, 0, 0, 0, 0, _NOBNB,
-                dx.data_ptr(), ptr(residual), *_NOSPLIT, st, _NOFOLD)
+                dx.data_ptr(), ptr(residual), *_NOSPLIT, st)
         return dx
     g2 = K.gemm_g2f if f32 else K.gemm_g2
     fuse = (bnb is not None and _BNB and not bnb.pooled and not f32 and not empty_class and bnb.x.dtype == BF16
@@ -739,19 +645,16 @@ def conv2d_dgrad(dy, wt, x_shape, stride, pad, *, residual=None, bnb=None):
             _hconv_ok(N, H, W, OH, OW, sh, sw, Co, Ci, classes[0][4], wt):
         slab = sums = None
         rows = 0
-        fold, fst = _NOFOLD, None
         if fuse:
             rows = K.hconv_stat_rows(N, H, W, Co, Ci, len(classes[0][4]), 0)
             slab = _empty((rows, 2, Ci), F32, dy.device)
             sums = _empty((2 * Ci,), F32, dy.device)  # zeroed in-kernel
-            if not K.hconv_v3(N, H, W, Co, Ci, len(classes[0][4])):
-                fold, fst = _fold(rows, Ci, 1, dy.device)
         K.hconv(dy.data_ptr(), wt.data_ptr(), dx.data_ptr(), _nbytes(dy), _nbytes(wt), N, OH, OW, Co, Ci, KH * KW * Co,
                 [(t[0], t[1], t[3]) for t in classes[0][4]], 0, ptr(residual), ptr(slab), 0, ptr(sums),
                 2 * Ci if fuse else 0, bnb.args() if fuse else _NOBNB, 0, 0,
-                *_hconv_split(K, N, OH, OW, Co, Ci, len(classes[0][4]), dy.device), st, fold)
+                *_hconv_split(K, N, OH, OW, Co, Ci, len(classes[0][4]), dy.device), st)
         if fuse:
-            dx._bnb = (bnb.bn, fst if fst is not None else slab, rows, sums)
+            dx._bnb = (bnb.bn, slab, rows, sums)
         return dx
     if (not f32 and _G2_GROUP and len(classes) > 1 and len({(c[2], c[3]) for c in classes}) == 1
             and (N * classes[0][2] * classes[0][3]) % 128 == 0):
@@ -766,12 +669,11 @@ def conv2d_dgrad(dy, wt, x_shape, stride, pad, *, residual=None, bnb=None):
         rows = K.gemm_g2_stat_rows(M, Ci) if fuse else 0
         slab = _empty((rows, 2, Ci), F32, dy.device) if fuse else None
         sums = _empty((2 * Ci,), F32, dy.device) if fuse else None
-        fold, fst = _fold(rows, Ci, 1, dy.device, g2=True) if fuse else (_NOFOLD, None)
         K.gemm_g2_grouped(dy.data_ptr(), wt.data_ptr(), dx.data_ptr(), _nbytes(dy), _nbytes(wt), M, Ci, Co, OH, OW,
                           GH, GW, 1, 1, taps_all, KH * KW * Co, Ci, H, W, sh, sw, 0, 0, 0, ptr(residual), ptr(slab), 0,
-                          ptr(sums), 2 * Ci if fuse else 0, bnb.args() if fuse else _NOBNB, st, groups, fold)
+                          ptr(sums), 2 * Ci if fuse else 0, bnb.args() if fuse else _NOBNB, st, groups)
         if fuse:
-            dx._bnb = (bnb.bn, fst if fst is not None else slab, rows, sums)
+            dx._bnb = (bnb.bn, slab, rows, sums)
         return dx
     if (not f32 and (KH, KW) == (1, 1) and (sh, sw) == (1, 1) and (ph, pw) == (0, 0) and not empty_class
             and len(classes) == 1):
@@ -823,7 +725,7 @@ class _DeferredReduce:
         self.pending.append((slab, out, int(n), int(splits)))
         self.pending_bytes += int(n) * int(splits) * 4
         # a queue larger than the last-level cache would read its first slabs back from HBM:
-        # launch once the pending slabs reach the threshold (DCNN_DEFER_REDUCE_MB)
+        # launch once the pending slabs reach the threshold
         if self.pending_bytes >= _DEFER_REDUCE_BYTES:
             self.flush()
 
@@ -833,12 +735,8 @@ class _DeferredReduce:
             print(f"[splitk_reduce] {len(self.pending)} slabs, {self.pending_bytes / 2**20:.1f} MiB: "
                   + " ".join(f"{t[2]}x{t[3]}" for t in self.pending), file=sys.stderr)
         if self.pending:
-            ws = wgrad_stream
-            with ws.on_side() if ws.forked else contextlib.nullcontext():
-                # (on the side stream when the weight gradients run there: the slabs were
-                # allocated on it, so the caching allocator's stream order covers this read)
-                kernels().multi_splitk_reduce([(t[0].data_ptr(), t[1].data_ptr(), t[2], t[3])
-                                               for t in self.pending], stream_ptr())
+            kernels().multi_splitk_reduce([(t[0].data_ptr(), t[1].data_ptr(), t[2], t[3]) for t in self.pending],
+                                          stream_ptr())
             self.pending.clear()
             self.pending_bytes = 0
 
@@ -847,9 +745,8 @@ class _DeferredReduce:
         self.active = False
 
 
-_DEFER_REDUCE = os.environ.get("DCNN_DEFER_REDUCE", "1") != "0"
 _TRACE_REDUCE = os.environ.get("DCNN_TRACE_REDUCE", "0") == "1"  # print each batched reduce's slabs
-_DEFER_REDUCE_BYTES = int(float(os.environ.get("DCNN_DEFER_REDUCE_MB", "1e9")) * (1 << 20))
+_DEFER_REDUCE_BYTES = 1 << 50  # (one batched reduce per backward)
 _tls = threading.local()
 
 
@@ -868,83 +765,6 @@ class _ThreadReducer:
 
 
 grad_reducer = _ThreadReducer()
-
-_WGRAD_STREAM = os.environ.get("DCNN_WGRAD_STREAM", "0") == "1"
-
-
-class _SideStream:
-    """Weight gradients on a side stream, overlapping the data-gradient chain.
-
-    In a layer's backward the weight gradient (wgrad GEMM + its deferred split-K reduce) and the
-    data gradient (dgrad GEMM -> BN statistics reduce -> BN backward apply -> the next layer) both
-    read the incoming gradient but not each other's output. The data-gradient chain is full of
-    short, latency-bound kernels; forking every wgrad onto a side stream (an event fork from the
-    compute stream) lets the GPU run those short kernels beside the MFMA-heavy wgrad instead of
-    after it. Inside a captured graph the forks/joins become graph edges. The tensors a wgrad
-    reads that were allocated on the compute stream are kept referenced until the join, so the
-    caching allocator cannot hand their memory to later compute-stream work while the side stream
-    may still read it. Joined (compute stream waits for the side stream) before any gradient
-    consumer: ``flush_gradients`` (data-parallel bucket all-reduce) and ``finish_backward``.
-    Active between ``begin()`` / ``end()`` on the calling thread (``Sequential.prepare_backward``
-    / ``finish_backward``) when ``DCNN_WGRAD_STREAM=1``.
-
-    OFF by default — measured slower on MI355X (profiles/experiment_wgrad_side_stream.md): two
-    full-grid MFMA kernels sharing the CUs run slower together (dgrad 50 -> 94 us beside a wgrad
-    47 -> 123 us) than back to back, and every captured fork/join edge opens a 10-15 us dispatch
-    gap; 64.9k vs 69.4k img/s on ResNet-18 at batch 256."""
-
-    def __init__(self):
-        self.active = False
-        self.forked = False
-        self.stream = None
-        self.keep = []
-
-    def begin(self):
-        self.active = _WGRAD_STREAM
-
-    @contextlib.contextmanager
-    def on_side(self, *keep):
-        main = torch.cuda.current_stream()
-        if self.stream is None or self.stream.device != main.device:
-            self.stream = torch.cuda.Stream(device=main.device)
-        if not self.forked or keep:
-            self.stream.wait_stream(main)  # fork after everything issued so far on the compute stream
-        self.forked = True
-        self.keep.extend(keep)
-        with torch.cuda.stream(self.stream):
-            yield
-
-    def run(self, fn, *keep):
-        """fn() on the side stream when active, else inline."""
-        if not self.active:
-            return fn()
-        with self.on_side(*keep):
-            return fn()
-
-    def join(self):
-        if self.forked:
-            torch.cuda.current_stream().wait_stream(self.stream)
-            self.forked = False
-            self.keep.clear()
-
-    def end(self):
-        self.join()
-        self.active = False
-
-
-class _ThreadSide:
-    def _get(self):
-        r = getattr(_tls, "side", None)
-        if r is None:
-            r = _tls.side = _SideStream()
-        return r
-
-    def __getattr__(self, k):
-        return getattr(self._get(), k)
-
-
-wgrad_stream = _ThreadSide()
-
 
 def _dense(t):
     """A gradient tensor whose storage is exactly its numel() elements (any dim order)."""
@@ -979,7 +799,7 @@ def conv2d_wgrad(dy, x, w_shape, stride, pad, grad_w, grad_b=None):
     P = N * OH * OW
     st = stream_ptr()
     taps = [(ky - pad[0], kx - pad[1]) for ky in range(KH) for kx in range(KW)]
-    hw_ok = (Cx == Ci and _HWGRAD and tuple(stride) == (1, 1) and (OH, OW) == (H, W)
+    hw_ok = (Cx == Ci and tuple(stride) == (1, 1) and (OH, OW) == (H, W)
              and 1 < len(taps) <= 9 and all(abs(a) <= 1 and abs(b) <= 1 for a, b in taps)
              and K.hwgrad_supported(N, H, W, Ci, Co, len(taps)))
     if dy.dtype == F32 and hw_ok and _f32_concat_ok(Ci, Co):
@@ -1349,7 +1169,6 @@ class BnDeferred:
                         running=self.running, momentum=self.momentum, use_running=self.use_running)
 
 
-_BN_DUAL = os.environ.get("DCNN_BN_DUAL", "1") != "0"
 
 
 def bn_dual_ok(x):
@@ -1371,7 +1190,7 @@ def bn_apply_dual(x, sums, count, gamma, beta, eps, other: BnDeferred, *, relu=F
 def bn_relu_maxpool_ok(x, ph, pw, sh, sw, pdh, pdw):
     """Can :func:`bn_relu_maxpool` take this BatchNorm+ReLU+max-pool? Its backward relies on the
     fused max-pool backward (:func:`maxpool_bwd` with ``bnb``), so both must be available."""
-    if not (_BNB and _BNB_POOL) or x.dtype != BF16 or not x.is_contiguous(memory_format=CL):
+    if not _BNB or x.dtype != BF16 or not x.is_contiguous(memory_format=CL):
         return False
     N, C, H, W = x.shape
     OH, OW = pool_out_hw(H, W, ph, pw, sh, sw, pdh, pdw)
@@ -1484,7 +1303,7 @@ def maxpool_bwd(dy, idx, x_shape, ph, pw, sh, sw, pdh, pdw, *, ypool=None, bnb=N
     dx = _empty((N, C, H, W), dy.dtype, dy.device, True)
     g = (N, H, W, C, OH, OW, ph, pw, sh, sw, pdh, pdw)
     # the kernel masks with (pooled value > 0): only valid when a ReLU sits between BN and pool
-    if (bnb is not None and _BNB and _BNB_POOL and (bnb.y is not None or bnb.pooled) and ypool is not None and dy.dtype == BF16 and bnb.x.dtype == BF16
+    if (bnb is not None and _BNB and (bnb.y is not None or bnb.pooled) and ypool is not None and dy.dtype == BF16 and bnb.x.dtype == BF16
             and tuple(bnb.x.shape) == (N, C, H, W) and bnb.x.is_contiguous(memory_format=CL)
             and K.maxpool_bwd_bnb_supported(*g)):
         rows = K.maxpool_bwd_bnb_rows(*g)

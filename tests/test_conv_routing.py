@@ -14,7 +14,6 @@ class _Stub:
 @pytest.fixture
 def stub(monkeypatch):
     monkeypatch.setattr(hip, "kernels", lambda: _Stub())
-    monkeypatch.setattr(hip, "_HCONV", True)
     monkeypatch.setattr(hip, "_HCONV_1X1", True)
 
 

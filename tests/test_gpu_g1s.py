@@ -1,5 +1,5 @@
 """Streaming 1x1 conv kernel (csrc/kernels/g1s.hip) against a plain PyTorch fp32 reference and
-against the gathered-GEMM path it replaces (gemm2.hip, DCNN_G1S=0 / g1s_enable(0)).
+against the gathered-GEMM path it replaces (gemm2.hip, g1s_enable(0)).
 
 Forward (+ bias / residual / ReLU, + Welford BatchNorm statistics of the stored values) and the
 stride-1 data gradient with the backward-BatchNorm fusion (ReLU mask + g / g*xhat sums) of the
@@ -169,67 +169,9 @@ def test_g1s_dgrad_bwd_bn_fusion(hip, case):
     assert torch.equal(d, d2) and torch.equal(d._bnb[1], d2._bnb[1])
 
 
-STRIDED_CASES = [
-    # N, C (dgrad output channels), H, W (dgrad output map), Co, k, stride, pad, relu, residual
-    (4, 64, 32, 32, 128, 3, 2, 1, True, False),   # ResNet-18 l2.b1c1: classes of 1/2/2/4 taps (K 128..512)
-    (4, 64, 32, 32, 128, 3, 2, 1, True, True),    # + the projection's gradient as residual
-    (4, 64, 16, 16, 128, 1, 2, 0, True, False),   # projection: one tap class + three empty phases
-    (4, 64, 16, 16, 128, 1, 2, 0, False, True),   # empty phases carry the residual
-    (4, 128, 16, 16, 256, 3, 2, 1, True, False),  # the 4-tap class is 1024 deep: gathered GEMM, same slab
-]
-
-
-@pytest.mark.parametrize("case", STRIDED_CASES)
-def test_g1s_strided_dgrad(hip, case):
-    """Strided dgrad on the g1s gathered form == the grouped gathered GEMM path (outputs and the
-    fused BatchNorm backward), and the plain output equals torch."""
-    N, C, H, W, Co, k, s, p, relu, resid = case
-    torch.manual_seed(7)
-    OH, OW = (H + 2 * p - k) // s + 1, (W + 2 * p - k) // s + 1
-    xb = (torch.randn(N, C, H, W) * 1.3 + 0.2).cuda().bfloat16().contiguous(memory_format=CL)
-    g, bt = (torch.rand(C) + 0.5).cuda(), torch.randn(C).cuda()
-    sums = hip.bn_stats(xb)
-    mean, istd = torch.empty(C, device="cuda"), torch.empty(C, device="cuda")
-    y = hip.bn_apply(xb, sums, N * H * W, g, bt, 1e-5, relu=relu, save=(mean, istd))
-    yout = y if relu else None
-    w = (torch.randn(Co, C, k, k) / math.sqrt(C * k * k)).cuda().bfloat16().contiguous(memory_format=CL)
-    wt = hip.conv_weight_t(w)
-    dy = torch.randn(N, Co, OH, OW).cuda().bfloat16().contiguous(memory_format=CL)
-    r = torch.randn(N, C, H, W).cuda().bfloat16().contiguous(memory_format=CL) if resid else None
-    out = {}
-    for on in (True, False):
-        hip.set_g1s_strided(on, min_rows=0)  # (the default gate keeps small phase grids grouped)
-        try:
-            d = hip.conv2d_dgrad(dy, wt, (N, C, H, W), (s, s), (p, p), residual=r)
-            req = hip.BnbRequest("bn", yout, xb, mean, istd)
-            df = hip.conv2d_dgrad(dy, wt, (N, C, H, W), (s, s), (p, p), residual=r, bnb=req)
-            dg, db = torch.zeros(C, device="cuda"), torch.zeros(C, device="cuda")
-            fz = getattr(df, "_bnb", None)  # (the grouped path does not fuse a 1x1 stride-2 dgrad)
-            assert fz is not None or not on
-            dx, _ = hip.bn_backward(df, xb, yout, mean, istd, g, dg, db, want_masked=True,
-                                    fused=fz[1:] if fz is not None else None)
-            dfm = df.float() * (y.float() > 0) if relu else df.float()
-            out[on] = (d.clone(), dfm, dx.clone(), dg.clone(), db.clone())
-        finally:
-            hip.set_g1s_strided(True)
-    ref = torch.nn.grad.conv2d_input((N, C, H, W), w.float(), dy.float(), s, p)
-    if resid:
-        ref = ref + r.float()
-    assert rel_err(out[True][0], ref) < 1e-2, rel_err(out[True][0], ref)
-    # same products in the same order within a class: identical data gradients; with a residual
-    # the gathered GEMM rounds the product to bf16 before adding it (two roundings, g1s one)
-    for a, b in zip(out[True][:2], out[False][:2]):
-        if resid:
-            assert rel_err(a, b) < 5e-3, rel_err(a, b)
-        else:
-            assert torch.equal(a, b)
-    for a, b in zip(out[True][2:], out[False][2:]):
-        assert rel_err(a, b) < (1e-2 if resid else 1e-4), rel_err(a, b)
-
-
 @pytest.mark.parametrize("case", [(32, 1024, 8, 8, 256), (32, 2048, 4, 4, 512), (8, 1024, 4, 4, 64)])
 def test_hconv_1x1_k1024(hip, case, monkeypatch):
-    """DCNN_HCONV_1X1: K >= 1024 1x1 convs on small grids (not on g1s) on the split-K halo
+    """K >= 1024 1x1 convs on small grids (not on g1s) on the split-K halo
     kernel — forward with statistics and the data gradient, against torch fp32 and the gathered
     GEMM (the switch off)."""
     N, Ci, H, W, Co = case

@@ -783,49 +783,6 @@ def test_strided_dgrad_grouped_launch(hip, case, monkeypatch):
     assert rel_err(outs[0], ref) < 1e-2
 
 
-@pytest.mark.parametrize("case", [(64, 64, 32, 32, 64, 1), (16, 128, 16, 16, 256, 2), (256, 256, 8, 8, 256, 1),
-                                  (8, 512, 4, 4, 512, 1)])
-def test_stat_fold_matches_reduce(hip, case, monkeypatch):
-    """BatchNorm statistics folded inside the producing conv launch (statfold.h: per-group
-    tickets, last workgroup merges) == the separate bn_stat_reduce, forward (Welford) and
-    backward (fused dgrad sums); repeated launches are bit-identical."""
-    N, C, H, W, Co, s = case
-    torch.manual_seed(2)
-    x = (torch.randn(N, C, H, W) * 3 + 5).cuda().to(torch.bfloat16).contiguous(memory_format=CL)
-    w = (torch.randn(Co, C, 3, 3) / math.sqrt(9 * C)).cuda().to(torch.bfloat16).contiguous(memory_format=CL)
-    outs = []
-    for fold in (True, True, False):
-        monkeypatch.setattr(hip, "_FOLD", fold)
-        y, part = hip.conv2d_fwd(x, w, None, (s, s), (1, 1), stats=True)
-        st = hip.bn_stats(y, part)
-        outs.append((y, st.final().clone() if hasattr(st, "final") else st.clone()))
-    (y1, s1), (y2, s2), (y0, s0) = outs
-    assert torch.equal(y1, y0) and torch.equal(s1, s2)
-    yd = y1.double()
-    ref = torch.cat([yd.mean((0, 2, 3)), yd.var((0, 2, 3), unbiased=False)]).cpu()
-    assert rel_err(s1.double(), ref) < 1e-5 and rel_err(s0.double(), ref) < 1e-5
-    # backward: dgrad with the fused BN request (mask + sums), folded vs reduced
-    from dcnn_amd.ops.hip import BnbRequest
-    xb = torch.randn(N, C, H, W).cuda().to(torch.bfloat16).contiguous(memory_format=CL)
-    mean = xb.float().mean((0, 2, 3))
-    istd = 1.0 / (xb.float().var((0, 2, 3), unbiased=False) + 1e-5).sqrt()
-    yb = torch.relu(xb)
-    dy = torch.randn_like(y1)
-    wt = hip.conv_weight_t(w)
-
-    class _BN:
-        pass
-    bn = _BN()
-    sums = []
-    for fold in (True, False):
-        monkeypatch.setattr(hip, "_FOLD", fold)
-        dx = hip.conv2d_dgrad(dy, wt, (N, C, H, W), (s, s), (1, 1), bnb=BnbRequest(bn, yb, xb, mean, istd))
-        assert dx._bnb[0] is bn
-        _, slab, rows, sm = dx._bnb
-        sums.append(hip.stat_reduce(1, slab, rows, C, sm).final().clone())
-    assert rel_err(sums[0], sums[1]) < 1e-5
-
-
 @pytest.mark.parametrize("relu", [False, True])
 def test_bn_backward_eval_mode_kernels(hip, relu):
     """Frozen-statistics (eval-mode) BatchNorm backward: dx = gamma * istd * dy' and the affine
@@ -847,73 +804,6 @@ def test_bn_backward_eval_mode_kernels(hip, relu):
     assert rel_err(db, d.sum((0, 2, 3))) < 1e-4
     if relu:
         assert rel_err(dmask, d) < 1e-2
-
-
-@pytest.mark.parametrize("case", [(128, 64, 32, 32, 64), (32, 64, 64, 64, 64), (128, 128, 32, 32, 64)])
-def test_hconv_wide_tiles(hip, case):
-    """256 x 64 halo-conv tiles (4 x 1 wave layout) == the 128 x 64 tiles: forward (+stats,
-    residual, ReLU) bit-identical per element (same K order), dgrad too; statistics close."""
-    from dcnn_amd.ops._ext import kernels
-    K = kernels()
-    N, C, H, W, Co = case
-    torch.manual_seed(6)
-    x = torch.randn(N, C, H, W).cuda().to(torch.bfloat16).contiguous(memory_format=CL)
-    w = (torch.randn(Co, C, 3, 3) / math.sqrt(9 * C)).cuda().to(torch.bfloat16).contiguous(memory_format=CL)
-    r = torch.randn(N, Co, H, W).cuda().to(torch.bfloat16).contiguous(memory_format=CL)
-    b = torch.randn(Co).cuda()
-    dy = torch.randn(N, Co, H, W).cuda().to(torch.bfloat16).contiguous(memory_format=CL)
-    wt = hip.conv_weight_t(w)
-    outs = []
-    try:
-        for wide in (1, 0):
-            K.hconv_set_wide(wide)
-            y, part = hip.conv2d_fwd(x, w, b, (1, 1), (1, 1), stats=True, residual=r, relu=True)
-            st = hip.bn_stats(y, part)
-            dx = hip.conv2d_dgrad(dy, wt, x.shape, (1, 1), (1, 1)) if C == 64 else None
-            outs.append((y, st.final().clone(), dx))
-    finally:
-        K.hconv_set_wide(0)
-    (y1, s1, d1), (y0, s0, d0) = outs
-    assert torch.equal(y1, y0)
-    assert rel_err(s1, s0) < 1e-5
-    if d1 is not None:
-        assert torch.equal(d1, d0)
-    ref = F.relu(F.conv2d(x.float().cpu(), w.float().cpu(), b.cpu(), 1, 1) + r.float().cpu())
-    assert rel_err(y1, ref) < 1e-2
-
-
-@pytest.mark.parametrize("case", [(64, 64, 32, 32), (256, 64, 16, 16), (768, 64, 8, 8), (3072, 64, 4, 4), (3, 64, 32, 32)])
-def test_hconv_weight_stationary_matches_ring(hip, case):
-    """64 -> 64 channel 3x3 convs on the weight-stationary halo kernel (hconv_ws_kernel: weights
-    in registers, persistent tile walk, double-buffered halo) == the weight-ring kernel: forward
-    (+bias, residual, ReLU, BN statistics) and dgrad bit-identical (same K order)."""
-    from dcnn_amd.ops._ext import kernels
-    K = kernels()
-    N, C, H, W = case
-    torch.manual_seed(7)
-    x = torch.randn(N, C, H, W).cuda().to(torch.bfloat16).contiguous(memory_format=CL)
-    w = (torch.randn(C, C, 3, 3) / math.sqrt(9 * C)).cuda().to(torch.bfloat16).contiguous(memory_format=CL)
-    r = torch.randn(N, C, H, W).cuda().to(torch.bfloat16).contiguous(memory_format=CL)
-    b = torch.randn(C).cuda()
-    dy = torch.randn(N, C, H, W).cuda().to(torch.bfloat16).contiguous(memory_format=CL)
-    wt = hip.conv_weight_t(w)
-    outs = []
-    try:
-        for ws in (1, 0):  # (opt-in kernel, default off)
-            K.hconv_set_ws(ws)
-            y, part = hip.conv2d_fwd(x, w, b, (1, 1), (1, 1), stats=True, residual=r, relu=True)
-            st = hip.bn_stats(y, part)
-            dx = hip.conv2d_dgrad(dy, wt, x.shape, (1, 1), (1, 1))
-            torch.cuda.synchronize()
-            outs.append((y, st.final().clone(), dx))
-    finally:
-        K.hconv_set_ws(0)
-    (y1, s1, d1), (y0, s0, d0) = outs
-    assert torch.equal(y1, y0)
-    assert torch.equal(s1, s0)
-    assert torch.equal(d1, d0)
-    ref = F.relu(F.conv2d(x.float().cpu(), w.float().cpu(), b.cpu(), 1, 1) + r.float().cpu())
-    assert rel_err(y1, ref) < 1e-2
 
 
 @pytest.mark.parametrize("shape", [(256, 64, 32, 32), (64, 128, 16, 16), (32, 256, 8, 8), (16, 512, 4, 4), (3, 24, 5, 7)])
