@@ -129,7 +129,7 @@ def build_native(force=False, verbose=False, max_workers=None):
 
 # kernel-library / native objects the C++ host API links (the pybind layers stay out)
 _HOST_SKIP_KERNELS = {"bindings", "runtime", "rccl"}
-_HOST_NATIVE = ("cpu_ops", "cpu_gemm", "threadpool", "jpeg")
+_HOST_NATIVE = ("cpu_ops", "cpu_gemm", "threadpool", "jpeg", "comm")
 
 
 def build_host(force=False, verbose=False, max_workers=None):
@@ -162,8 +162,8 @@ def build_host(force=False, verbose=False, max_workers=None):
     lib = PKG / "libdcnn.so"
     deps = objs + kobjs + nobjs
     if force or not lib.exists() or any(o.stat().st_mtime > lib.stat().st_mtime for o in deps):
-        _run([HIPCC, "-shared", "-fPIC", f"--offload-arch={ARCH}", *map(str, deps), "-o", str(lib), "-pthread"],
-             verbose)
+        _run([HIPCC, "-shared", "-fPIC", f"--offload-arch={ARCH}", *map(str, deps), "-o", str(lib), "-pthread",
+              "-lz", "-ldl"], verbose)
     bins = []
     bin_dir = PKG / "bin"
     bin_dir.mkdir(exist_ok=True)

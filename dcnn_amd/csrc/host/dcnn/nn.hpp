@@ -353,6 +353,7 @@ class SGD : public Optimizer {
  public:
   explicit SGD(float lr, float momentum = 0.f) : Optimizer(lr), momentum_(momentum) {}
   void step(const std::vector<Param*>& params) override;
+  float momentum() const { return momentum_; }
 
  private:
   float momentum_;
@@ -364,6 +365,8 @@ class Adam : public Optimizer {
                 bool decoupled = false)
       : Optimizer(lr), b1_(b1), b2_(b2), eps_(eps), wd_(wd), decoupled_(decoupled) {}
   void step(const std::vector<Param*>& params) override;
+  long step_count() const { return t_; }
+  void set_step_count(long t) { t_ = t; }
 
  private:
   float b1_, b2_, eps_, wd_;

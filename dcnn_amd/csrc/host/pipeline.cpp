@@ -1,0 +1,548 @@
+// Native pipeline stage (dcnn/pipeline.hpp): configuration, tensor payloads, the command handlers.
+#include "dcnn/pipeline.hpp"
+
+#include <unistd.h>
+
+#include <cmath>
+#include <cstdio>
+#include <cstring>
+#include <fstream>
+#include <sstream>
+#include <stdexcept>
+
+#include "../native/comm.h"
+
+using namespace dcnn_native;
+
+namespace dcnn {
+
+namespace {
+constexpr uint8_t kChannelsLast = 0x10;  // dtype flag: NHWC physical buffer of an NCHW tensor
+constexpr uint64_t kFullState = 1;        // SEND_PARAMS "full" / LOAD_PARAMS micro-batch id
+
+std::optional<Endpoint> parse_endpoint(const json::Value* v) {
+  if (v == nullptr || v->is_null()) return std::nullopt;
+  Endpoint e;
+  e.communication_type = v->get_string("communication_type", "tcp");
+  if (const json::Value* p = v->find("parameters")) e.parameters = *p;
+  return e;
+}
+
+std::string str_or(const json::Value& j, const char* k, const std::string& d) {
+  const json::Value* v = j.find(k);
+  return (v == nullptr || v->is_null()) ? d : v->as_string();
+}
+
+int64_t numel_of(const std::vector<int64_t>& s) {
+  int64_t n = 1;
+  for (auto d : s) n *= d;
+  return n;
+}
+
+// dst's storage <- src's bytes (same byte count, same device kind as dst)
+void copy_into(const Tensor& dst, const Tensor& src) {
+  if (dst.nbytes() != src.nbytes()) throw std::runtime_error("state size mismatch");
+  if (dst.device().is_gpu())
+    gpu::copy(dst.data(), src.data(), src.nbytes(), src.device().is_gpu() ? 2 : 0);
+  else
+    std::memcpy(dst.data(), src.data(), src.nbytes());
+}
+
+// t as (dt, layout) on dev
+Tensor convert(const Tensor& t, DType dt, Layout layout, Device dev) {
+  if (t.dtype() == dt && t.layout() == layout) return t.device() == dev ? t : t.to(dev);
+  return Tensor::from_host(t.to_host_f32(), t.shape(), dev, dt, layout);
+}
+
+double rss_mb() {
+  std::ifstream f("/proc/self/statm");
+  long pages = 0, rss = 0;
+  f >> pages >> rss;
+  return (double)rss * (double)sysconf(_SC_PAGESIZE) / (1024.0 * 1024.0);
+}
+}  // namespace
+
+StageConfig StageConfig::parse(const std::string& text) {
+  const json::Value j = json::Value::parse(text);
+  StageConfig c;
+  c.stage_id = str_or(j, "stage_id", "");
+  c.stage_index = (int)j.get_int("stage_index", 0);
+  c.num_stages = (int)j.get_int("num_stages", 1);
+  c.model_config = j.at("model_config");
+  c.optimizer_config = j.at("optimizer_config");
+  c.next_stage = parse_endpoint(j.find("next_stage_endpoint"));
+  c.prev_stage = parse_endpoint(j.find("prev_stage_endpoint"));
+  c.coordinator = parse_endpoint(j.find("coordinator_endpoint"));
+  c.device = str_or(j, "device", "CPU");
+  c.transport = str_or(j, "transport", "message");
+  c.codec = str_or(j, "codec", "none");
+  if (const json::Value* s = j.find("seed"); s != nullptr && !s->is_null()) c.seed = s->as_int();
+  if (const json::Value* f = j.find("first_layer_input_grad"); f != nullptr && !f->is_null())
+    c.first_layer_input_grad = f->as_bool();
+  if (const json::Value* h = j.find("heartbeat_s"); h != nullptr && !h->is_null()) c.heartbeat_s = h->as_number();
+  return c;
+}
+
+std::unique_ptr<Communicator> make_tcp_communicator(const std::string& id, const std::string& host, int port,
+                                                   int* bound_port) {
+  auto c = std::make_unique<TcpCommunicator>(id, host, port);
+  if (bound_port != nullptr) *bound_port = c->port();
+  return c;
+}
+
+std::unique_ptr<Optimizer> create_optimizer(const json::Value& cfg) {
+  std::string type = str_or(cfg, "type", "sgd");
+  for (auto& ch : type) ch = (char)std::tolower((unsigned char)ch);
+  const json::Value* pp = cfg.find("parameters");
+  const json::Value p = pp != nullptr ? *pp : json::Value::object();
+  const float lr = (float)p.get_number("learning_rate", type == "sgd" ? 0.01 : 0.001);
+  if (type == "sgd") return std::make_unique<SGD>(lr, (float)p.get_number("momentum", 0.0));
+  if (type == "adam" || type == "adamw") {
+    const bool dec = type == "adamw" || p.get_bool("decouple_weight_decay", false);
+    return std::make_unique<Adam>(lr, (float)p.get_number("beta1", 0.9), (float)p.get_number("beta2", 0.999),
+                                  (float)p.get_number("epsilon", 1e-8), (float)p.get_number("weight_decay", 0.0), dec);
+  }
+  throw std::runtime_error("unknown optimizer type '" + type + "'");
+}
+
+PipelineStage::PipelineStage(Communicator* comm, bool verbose) : comm_(comm), verbose_(verbose), id_(comm->id()) {}
+
+PipelineStage::~PipelineStage() { stop_heartbeat(); }
+
+void PipelineStage::run(int poll_ms) {
+  running_ = true;
+  while (running_) {
+    Message m;
+    if (!comm_->queue().pop(m, poll_ms)) {
+      if (comm_->queue().closed()) break;
+      continue;
+    }
+    process(m);
+  }
+  stop_heartbeat();
+}
+
+void PipelineStage::reply(uint16_t cmd, const std::string& text) {
+  Message m;
+  m.recipient = "coordinator";
+  m.command = cmd;
+  if (!text.empty()) {
+    m.payload_type = P_STRING;
+    m.text = text;
+  }
+  if (auto* tcp = dynamic_cast<TcpCommunicator*>(comm_)) tcp->wait_for_peer("coordinator", 30000);
+  comm_->send(std::move(m));
+}
+
+void PipelineStage::process(Message& m) {
+  const uint16_t cmd = m.command;
+  try {
+    switch (cmd) {
+      case FORWARD_JOB: forward(m); break;
+      case BACKWARD_JOB: backward(m); break;
+      case UPDATE_PARAMETERS: {
+        if (m.payload_type == P_STRING && !m.text.empty()) {
+          const json::Value hp = json::Value::parse(m.text);
+          if (hp.has("learning_rate")) opt_->set_learning_rate((float)hp.at("learning_rate").as_number());
+        }
+        opt_->step(model_->parameters());
+        model_->zero_grad();
+        ++n_upd_;
+        reply(PARAMETERS_UPDATED);
+        break;
+      }
+      case TRAIN_MODE: model_->set_training(true); break;
+      case EVAL_MODE: model_->set_training(false); break;
+      case SHUTDOWN: stop(); break;
+      case CONFIG_TRANSFER: configure(m.text); break;
+      case SEND_PARAMS: {
+        const bool full = m.payload_type == P_STRING && m.text == "full";
+        Message r;
+        r.recipient = "coordinator";
+        r.command = PARAMS_TRANSFER;
+        r.payload_type = P_TYPED_JOB;
+        r.mb_id = full ? kFullState : 0;
+        std::vector<double> st = flat_state();
+        if (full) {
+          std::vector<double> v{(double)st.size()};
+          v.insert(v.end(), st.begin(), st.end());
+          std::vector<double> o = optimizer_state();
+          v.insert(v.end(), o.begin(), o.end());
+          r.dtype = 5;  // f64
+          r.shape = {(uint64_t)v.size()};
+          r.data.assign(reinterpret_cast<const char*>(v.data()), v.size() * sizeof(double));
+        } else {
+          std::vector<float> f(st.begin(), st.end());
+          r.dtype = 0;
+          r.shape = {(uint64_t)f.size()};
+          r.data.assign(reinterpret_cast<const char*>(f.data()), f.size() * sizeof(float));
+        }
+        if (auto* tcp = dynamic_cast<TcpCommunicator*>(comm_)) tcp->wait_for_peer("coordinator", 30000);
+        comm_->send(std::move(r));
+        break;
+      }
+      case LOAD_PARAMS:
+      case PARAMS_TRANSFER: {
+        if (m.codec) m.data = decompress(m.data, (Codec)m.codec, 0);
+        const int code = m.payload_type == P_TYPED_JOB ? (m.dtype & 0x0F) : 0;
+        std::vector<double> v;
+        if (code == 5) {
+          v.resize(m.data.size() / sizeof(double));
+          std::memcpy(v.data(), m.data.data(), v.size() * sizeof(double));
+        } else if (code == 0) {
+          std::vector<float> f(m.data.size() / sizeof(float));
+          std::memcpy(f.data(), m.data.data(), f.size() * sizeof(float));
+          v.assign(f.begin(), f.end());
+        } else {
+          throw std::runtime_error("parameter state must be fp32 or fp64");
+        }
+        if (m.mb_id == kFullState && code == 5) {
+          const size_t n = (size_t)v.at(0);
+          load_flat_state(v.data() + 1, n);
+          load_optimizer_state(v.data() + 1 + n, v.size() - 1 - n);
+        } else {
+          load_flat_state(v.data(), v.size());
+        }
+        reply(PARAMS_LOADED);
+        break;
+      }
+      case STATUS_REQUEST: reply(STATUS_RESPONSE, status_json()); break;
+      case HEALTH_CHECK: {
+        Message r;
+        r.recipient = "coordinator";
+        r.command = HEALTH_CHECK;
+        r.payload_type = P_BOOL;
+        r.flag = true;
+        comm_->send(std::move(r));
+        break;
+      }
+      case BARRIER_SYNC:
+        if (dev_.is_gpu()) gpu::synchronize();
+        reply(BARRIER_SYNC);
+        break;
+      case CHECKPOINT_REQUEST:
+        model_->save_to_file(m.text);
+        reply(CHECKPOINT_COMPLETE, m.text);
+        break;
+      case REPORT_LOAD: {
+        Message r;
+        r.recipient = "coordinator";
+        r.command = LOAD_REPORT;
+        r.payload_type = P_LOAD;
+        r.load.avg_forward_ms = n_fwd_ ? (float)(fwd_ms_ / (double)n_fwd_) : 0.f;
+        r.load.avg_backward_ms = n_bwd_ ? (float)(bwd_ms_ / (double)n_bwd_) : 0.f;
+        r.load.avg_cpu_utilization = -1.f;
+        r.load.max_memory_mb = (float)rss_mb();
+        comm_->send(std::move(r));
+        break;
+      }
+      case UPDATE_LOAD: reply(LOAD_REPORT, status_json()); break;
+      case PRINT_PROFILING: {
+        char buf[256];
+        std::snprintf(buf, sizeof buf, "%s (native): %ld forward, %ld backward, %ld updates; avg forward %.3f ms, "
+                      "avg backward %.3f ms\n", id_.c_str(), n_fwd_, n_bwd_, n_upd_,
+                      n_fwd_ ? fwd_ms_ / (double)n_fwd_ : 0.0, n_bwd_ ? bwd_ms_ / (double)n_bwd_ : 0.0);
+        reply(PROFILING_PRINTED, buf);
+        break;
+      }
+      case CLEAR_PROFILING:
+        fwd_ms_ = bwd_ms_ = 0;
+        n_fwd_ = n_bwd_ = 0;
+        reply(PROFILING_CLEARED);
+        break;
+      default: throw std::runtime_error(std::string("unhandled command ") + command_name(cmd));
+    }
+  } catch (const std::exception& e) {
+    const uint16_t kind = (cmd == FORWARD_JOB || cmd == BACKWARD_JOB) ? JOB_FAILURE : ERROR_REPORT;
+    const std::string what = id_ + ": " + command_name(cmd) + " failed\n" + e.what();
+    if (verbose_) std::fprintf(stderr, "%s\n", what.c_str());
+    try {
+      reply(kind, what);
+    } catch (...) {
+    }
+  }
+}
+
+void PipelineStage::configure(const std::string& text) {
+  cfg_ = StageConfig::parse(text);
+  if (cfg_.transport != "message")
+    throw std::runtime_error("native stage: transport '" + cfg_.transport + "' not supported (inline tensors only)");
+  stop_heartbeat();
+  dev_ = Device::parse(cfg_.device);
+  if (dev_.is_gpu()) gpu::set_device(dev_.index);
+  model_ = std::make_unique<Sequential>(Sequential::load_from_config(cfg_.model_config));
+  model_->set_device(dev_);
+  model_->initialize((uint64_t)cfg_.seed.value_or(0));
+  opt_ = create_optimizer(cfg_.optimizer_config);
+  out_kind_.clear();
+  n_fwd_ = n_bwd_ = n_upd_ = 0;
+  fwd_ms_ = bwd_ms_ = 0;
+  id_ = cfg_.stage_id;
+  comm_->set_id(id_);
+  connect_peers();
+  if (cfg_.heartbeat_s > 0) start_heartbeat();
+  reply(CONFIG_RECEIVED, id_);
+}
+
+void PipelineStage::connect_peers() {
+  auto* tcp = dynamic_cast<TcpCommunicator*>(comm_);
+  auto* inproc = dynamic_cast<InProcessCommunicator*>(comm_);
+  const std::pair<const char*, const std::optional<Endpoint>*> eps[] = {
+      {"next_stage", &cfg_.next_stage}, {"prev_stage", &cfg_.prev_stage}, {"coordinator", &cfg_.coordinator}};
+  for (const auto& [name, ep] : eps) {
+    if (!ep->has_value()) continue;
+    const Endpoint& e = **ep;
+    const std::string peer = e.id();
+    if (e.communication_type == "in_process") {
+      if (inproc == nullptr) throw std::runtime_error("in_process endpoint needs an in-process communicator");
+      if (peer != name) inproc->alias(name, peer);
+    } else if (tcp != nullptr) {
+      if (std::string(name) == "next_stage") {
+        tcp->connect(name, e.host(), e.port(), 60000);
+        if (!peer.empty()) tcp->alias(peer, name);
+      } else if (!peer.empty()) {
+        tcp->alias(name, peer);  // prev stage / coordinator dial us
+      }
+    } else {
+      throw std::runtime_error("endpoint type " + e.communication_type + " needs a TCP communicator");
+    }
+  }
+}
+
+Tensor PipelineStage::decode(Message& m) const {
+  if (m.payload_type != P_JOB && m.payload_type != P_TYPED_JOB) throw std::runtime_error("job message without a tensor");
+  if (m.shape.empty()) return Tensor();
+  if (m.codec) {
+    m.data = decompress(m.data, (Codec)m.codec, 0);
+    m.codec = CODEC_NONE;
+  }
+  const int code = m.payload_type == P_TYPED_JOB ? m.dtype : 0;
+  std::vector<int64_t> shape(m.shape.begin(), m.shape.end());
+  Layout layout = Layout::NCHW;
+  if ((code & kChannelsLast) && shape.size() == 4) {
+    shape = {shape[0], shape[3], shape[1], shape[2]};
+    layout = Layout::NHWC;
+  }
+  DType dt;
+  switch (code & 0x0F) {
+    case 0: dt = DType::F32; break;
+    case 1: dt = DType::BF16; break;
+    default: throw std::runtime_error("activation payloads must be fp32 or bf16");
+  }
+  Tensor t = Tensor::empty(shape, dt, Device::cpu(), layout);
+  if (m.data.size() != t.nbytes()) throw std::runtime_error("tensor payload size does not match its shape");
+  std::memcpy(t.data(), m.data.data(), t.nbytes());
+  if (t.rank() == 2) t = t.view({shape[0], shape[1], 1, 1}, Layout::NCHW);  // (N, F): 1x1 spatial
+  return t;
+}
+
+void PipelineStage::send_tensor(const std::string& to, uint16_t cmd, uint64_t mb, const Tensor& t, bool as_logits) {
+  Message m;
+  m.recipient = to;
+  m.command = cmd;
+  m.payload_type = P_TYPED_JOB;
+  m.mb_id = mb;
+  if (t.defined()) {
+    const Tensor h = t.device().is_gpu() ? t.to(Device::cpu()) : t;
+    const auto& s = h.shape();
+    uint8_t code = h.dtype() == DType::F32 ? 0 : h.dtype() == DType::BF16 ? 1 : 0xff;
+    if (code == 0xff) throw std::runtime_error("activation dtype must be fp32 or bf16");
+    if (s.size() == 4 && s[2] == 1 && s[3] == 1 && as_logits) {
+      m.shape = {(uint64_t)s[0], (uint64_t)s[1]};  // logits (N, classes)
+    } else if (s.size() == 4 && h.layout() == Layout::NHWC) {
+      m.shape = {(uint64_t)s[0], (uint64_t)s[2], (uint64_t)s[3], (uint64_t)s[1]};
+      code |= kChannelsLast;
+    } else {
+      for (auto d : s) m.shape.push_back((uint64_t)d);
+    }
+    m.dtype = code;
+    m.data.assign(static_cast<const char*>(h.data()), h.nbytes());
+    if (cfg_.codec == "zlib" || cfg_.codec == "zstd") {
+      const Codec c = cfg_.codec == "zlib" ? CODEC_ZLIB : CODEC_ZSTD;
+      m.data = compress(m.data, c, 3);
+      m.codec = c;
+    }
+  }
+  comm_->send(std::move(m));
+}
+
+void PipelineStage::forward(Message& m) {
+  const auto t0 = std::chrono::steady_clock::now();
+  const uint64_t mb = m.mb_id;
+  Tensor x = decode(m);
+  Tensor a;
+  if (cfg_.stage_index == 0 && x.dtype() == DType::F32 && x.layout() == Layout::NCHW) {
+    a = model_->input_activation(x);  // the network input (fp32 NCHW)
+  } else if (dev_.is_gpu()) {
+    a = convert(x, DType::BF16, Layout::NHWC, dev_);
+  } else {
+    a = convert(x, DType::F32, Layout::NCHW, dev_);
+  }
+  const Tensor out = model_->forward_activation(a, (int)mb);
+  out_kind_[mb] = OutKind{out.dtype(), out.layout(), out.shape()};
+  const bool last = cfg_.stage_index == cfg_.num_stages - 1;
+  send_tensor(last ? "coordinator" : "next_stage", FORWARD_JOB, mb, out, last);
+  ++n_fwd_;
+  fwd_ms_ += std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+}
+
+void PipelineStage::backward(Message& m) {
+  const auto t0 = std::chrono::steady_clock::now();
+  const uint64_t mb = m.mb_id;
+  auto it = out_kind_.find(mb);
+  if (it == out_kind_.end()) throw std::runtime_error("backward for micro-batch " + std::to_string(mb) + " without a forward");
+  const OutKind k = it->second;
+  Tensor g = decode(m);
+  if (g.shape() != k.shape) {
+    if (g.numel() != numel_of(k.shape)) throw std::runtime_error("gradient shape does not match the forward output");
+    // (N, C) logits gradient for an (N, C, 1, 1) output: the same bytes in either layout
+    g = g.view(k.shape, k.layout);
+  }
+  g = convert(g, k.dt, k.layout, dev_);
+  Tensor gin = model_->backward_activation(g, (int)mb);
+  const bool first = cfg_.stage_index == 0;
+  if (first && !cfg_.first_layer_input_grad) gin = Tensor();
+  send_tensor(first ? "coordinator" : "prev_stage", BACKWARD_JOB, mb, gin, false);
+  ++n_bwd_;
+  bwd_ms_ += std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+}
+
+std::vector<double> PipelineStage::flat_state() {
+  std::vector<double> out;
+  for (Param* p : model_->parameters()) {
+    const std::vector<float> v = p->value.view(p->shape, p->layout).to_host_f32();
+    out.insert(out.end(), v.begin(), v.end());
+  }
+  for (BatchNorm* bn : model_->batchnorms()) {
+    for (const Tensor* t : {&bn->running_mean, &bn->running_var}) {
+      const std::vector<float> v = t->to_host_f32();
+      out.insert(out.end(), v.begin(), v.end());
+    }
+  }
+  return out;
+}
+
+void PipelineStage::load_flat_state(const double* v, size_t n) {
+  size_t off = 0;
+  auto take = [&](int64_t k) {
+    if (off + (size_t)k > n) throw std::runtime_error("flat state too short");
+    std::vector<float> f(v + off, v + off + k);
+    off += (size_t)k;
+    return f;
+  };
+  for (Param* p : model_->parameters()) {
+    const Tensor t = Tensor::from_host(take(numel_of(p->shape)), p->shape, p->value.device(), DType::F32, p->layout);
+    copy_into(p->value, t);
+  }
+  for (BatchNorm* bn : model_->batchnorms()) {
+    for (Tensor* t : {&bn->running_mean, &bn->running_var}) {
+      const Tensor h = Tensor::from_host(take(t->numel()), t->shape(), t->device(), DType::F32, t->layout());
+      copy_into(*t, h);
+    }
+  }
+  if (off != n) throw std::runtime_error("flat state size mismatch: consumed " + std::to_string(off) + " of " +
+                                         std::to_string(n));
+  for (auto& l : model_->layers()) l->sync_shadow();
+}
+
+// [learning rate, step count, then the state tensors by name (Adam: m, v; SGD with momentum:
+// velocity), each over every parameter in checkpoint order]
+std::vector<double> PipelineStage::optimizer_state() {
+  std::vector<double> out{(double)opt_->learning_rate(), 0.0};
+  auto* adam = dynamic_cast<Adam*>(opt_.get());
+  auto* sgd = dynamic_cast<SGD*>(opt_.get());
+  auto params = model_->parameters();
+  auto append = [&](Tensor Param::*field) {
+    for (Param* p : params) {
+      const Tensor& t = p->*field;
+      if (t.defined()) {
+        const std::vector<float> v = t.view(p->shape, p->layout).to_host_f32();
+        out.insert(out.end(), v.begin(), v.end());
+      } else {
+        out.insert(out.end(), (size_t)numel_of(p->shape), 0.0);
+      }
+    }
+  };
+  if (adam != nullptr) {
+    out[1] = (double)adam->step_count();
+    append(&Param::m);
+    append(&Param::v);
+  } else if (sgd != nullptr && sgd->momentum() != 0.f) {
+    append(&Param::m);  // (SGD keeps its velocity in Param::m)
+  }
+  return out;
+}
+
+void PipelineStage::load_optimizer_state(const double* v, size_t n) {
+  if (n < 2) throw std::runtime_error("optimizer state too short");
+  opt_->set_learning_rate((float)v[0]);
+  size_t off = 2;
+  auto params = model_->parameters();
+  auto fill = [&](Tensor Param::*field) {
+    for (Param* p : params) {
+      const int64_t k = numel_of(p->shape);
+      if (off + (size_t)k > n) throw std::runtime_error("optimizer state too short");
+      std::vector<float> f(v + off, v + off + k);
+      off += (size_t)k;
+      Tensor& dst = p->*field;
+      if (!dst.defined()) dst = Tensor::zeros(p->value.shape(), DType::F32, p->value.device(), p->value.layout());
+      copy_into(dst, Tensor::from_host(f, p->shape, p->value.device(), DType::F32, p->layout));
+    }
+  };
+  if (auto* adam = dynamic_cast<Adam*>(opt_.get())) {
+    adam->set_step_count((long)v[1]);
+    fill(&Param::m);
+    fill(&Param::v);
+  } else if (auto* sgd = dynamic_cast<SGD*>(opt_.get()); sgd != nullptr && sgd->momentum() != 0.f) {
+    fill(&Param::m);
+  }
+  if (off != n) throw std::runtime_error("optimizer state size mismatch");
+}
+
+std::string PipelineStage::status_json() {
+  json::Value d = json::Value::object();
+  d["id"] = id_;
+  json::Value c = json::Value::object();
+  c["forward"] = (int64_t)n_fwd_;
+  c["backward"] = (int64_t)n_bwd_;
+  c["update"] = (int64_t)n_upd_;
+  d["counts"] = std::move(c);
+  d["pid"] = (int64_t)getpid();
+  d["native"] = true;
+  if (model_) {
+    d["device"] = dev_.str();
+    json::Value ls = json::Value::array();
+    for (auto& l : model_->layers()) ls.push(l->name());
+    d["layers"] = std::move(ls);
+    d["num_parameters"] = (int64_t)model_->num_parameters();
+  }
+  return d.dump(-1);
+}
+
+void PipelineStage::start_heartbeat() {
+  beat_stop_ = false;
+  const double every = cfg_.heartbeat_s;
+  beat_ = std::thread([this, every] {
+    while (!beat_stop_) {
+      Message m;
+      m.recipient = "coordinator";
+      m.command = HEALTH_CHECK;
+      m.payload_type = P_STRING;
+      m.text = "heartbeat";
+      try {
+        comm_->send(std::move(m));
+      } catch (...) {
+      }
+      const auto until = std::chrono::steady_clock::now() + std::chrono::duration<double>(every);
+      while (!beat_stop_ && std::chrono::steady_clock::now() < until)
+        std::this_thread::sleep_for(std::chrono::milliseconds(20));
+    }
+  });
+}
+
+void PipelineStage::stop_heartbeat() {
+  beat_stop_ = true;
+  if (beat_.joinable()) beat_.join();
+}
+
+}  // namespace dcnn

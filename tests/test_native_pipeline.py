@@ -1,0 +1,185 @@
+"""Native pipeline stages (csrc/host/pipeline.cpp, dcnn_amd/bin/network_worker): separate C++
+worker processes driven over TCP by the Python DistributedCoordinator train like the Python
+stages of an in-process coordinator (same partitions, same initial weights pushed by
+LOAD_PARAMS): the same losses and parameters after sync / semi-async / 1F1B steps, and the
+full parameter + optimizer state survives a SEND_PARAMS "full" -> LOAD_PARAMS round trip
+(the coordinator's recovery path). Reference: examples/network_worker.cpp:14-194,
+include/pipeline/pipeline_stage.hpp:29-308."""
+import os
+import socket
+import subprocess
+
+import numpy as np
+import pytest
+import torch
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+WORKER = os.path.join(ROOT, "dcnn_amd", "bin", "network_worker")
+
+
+@pytest.fixture(scope="module")
+def worker_bin():
+    if not os.path.exists(WORKER):
+        from dcnn_amd import _build
+        _build.build_host()
+    return WORKER
+
+
+def _free_ports(n):
+    socks, ports = [], []
+    for _ in range(n):
+        s = socket.socket()
+        s.bind(("127.0.0.1", 0))
+        socks.append(s)
+        ports.append(s.getsockname()[1])
+    for s in socks:
+        s.close()
+    return ports
+
+
+def _model(seed=3):
+    from dcnn_amd.nn import SequentialBuilder
+    m = (SequentialBuilder("native_pipe").input([3, 12, 12])
+         .conv2d(8, 3, 3, 1, 1, 1, 1).batchnorm().activation("relu").maxpool2d(2, 2, 2, 2)
+         .conv2d(16, 3, 3, 1, 1, 1, 1).activation("relu")
+         .flatten().dense(10).build())
+    m.set_seed(seed)
+    m.initialize()
+    return m
+
+
+class _Workers:
+    def __init__(self, binary, n):
+        self.ports = _free_ports(n)
+        self.procs = [subprocess.Popen([binary, str(p), "--host", "127.0.0.1"], stdout=subprocess.PIPE,
+                                       stderr=subprocess.STDOUT, text=True) for p in self.ports]
+        for p in self.procs:  # wait for "listening"
+            line = p.stdout.readline()
+            assert "listening" in line, line
+
+    def close(self):
+        for p in self.procs:
+            try:
+                p.wait(timeout=20)
+            except subprocess.TimeoutExpired:
+                p.kill()
+                p.wait()
+
+
+def _train(coord, steps, schedule, seed=5):
+    g = torch.Generator().manual_seed(seed)
+    losses = []
+    for _ in range(steps):
+        x = torch.randn(8, 3, 12, 12, generator=g)
+        y = torch.randint(0, 10, (8,), generator=g)
+        losses.append(float(coord.train_step(x, y, schedule=schedule)))
+    return losses
+
+
+@pytest.mark.parametrize("schedule", ["sync", "semi_async", "1f1b"])
+@pytest.mark.parametrize("opt_name", ["adam", "sgd_momentum"])
+def test_native_stages_train_like_python_stages(worker_bin, schedule, opt_name):
+    from dcnn_amd.nn import SGD, Adam
+    from dcnn_amd.parallel.pipeline import DistributedCoordinator, Endpoint, InProcessCoordinator
+    mk_opt = (lambda: Adam(2e-3)) if opt_name == "adam" else (lambda: SGD(0.05, 0.9))
+    ref_model = _model()
+    ref = InProcessCoordinator(ref_model, mk_opt(), "softmax_crossentropy", num_stages=2, num_microbatches=2,
+                               transport="message")
+    ref.initialize()
+    ref.deploy_stages()
+    ref.start()
+    ref.send_parameters(ref_model)
+    ref_losses = _train(ref, 3, schedule)
+    ref_params = ref.collect_parameters()
+    ref.stop()
+
+    w = _Workers(worker_bin, 2)
+    try:
+        model = _model()
+        eps = [Endpoint.network("127.0.0.1", p) for p in w.ports]
+        coord = DistributedCoordinator(model, mk_opt(), "softmax_crossentropy", eps, num_microbatches=2,
+                                       host="127.0.0.1", timeout_s=60)
+        coord.initialize()
+        coord.deploy_stages()
+        coord.start()
+        coord.send_parameters(model)
+        st = coord.status()
+        assert all(s.get("native") for s in st), st
+        losses = _train(coord, 3, schedule)
+        params = coord.collect_parameters()
+        # recovery path: full state out, perturb, full state back in -> identical next step
+        full = coord.collect_parameters(full=True)
+        coord.send_parameters(_model(seed=99))  # clobber the weights
+        from dcnn_amd.parallel.pipeline import messages as M
+        from dcnn_amd.parallel.pipeline.messages import CommandType as C
+        for name, flat in zip(coord.stage_names, full):
+            coord.comm.send(M.job_message(name, C.LOAD_PARAMS, 1, flat))
+        coord.join(C.PARAMS_LOADED, coord.num_stages)
+        full2 = coord.collect_parameters(full=True)
+        coord.stop()
+    finally:
+        w.close()
+    np.testing.assert_allclose(losses, ref_losses, rtol=2e-4, atol=1e-6)
+    # (Adam normalises each update by sqrt(v): a weight whose gradients are ~0 moves by up to lr
+    # per step on the sign of fp32 rounding noise, so its tolerance is a fraction of lr)
+    atol = 5e-4 if opt_name == "adam" else 2e-5
+    for a, b in zip(params, ref_params):
+        np.testing.assert_allclose(a.numpy(), b.numpy(), rtol=1e-3, atol=atol)
+    for a, b in zip(full, full2):
+        assert torch.equal(a, b)
+    assert all(p.returncode == 0 for p in w.procs), [p.returncode for p in w.procs]
+
+
+def test_native_stage_reports_errors(worker_bin):
+    """A stage failure comes back as a JOB_FAILURE the coordinator raises (not a hang)."""
+    from dcnn_amd.nn import Adam
+    from dcnn_amd.parallel.pipeline import DistributedCoordinator, Endpoint, PipelineError
+    w = _Workers(worker_bin, 2)
+    try:
+        model = _model()
+        eps = [Endpoint.network("127.0.0.1", p) for p in w.ports]
+        coord = DistributedCoordinator(model, Adam(1e-3), "softmax_crossentropy", eps, num_microbatches=1,
+                                       host="127.0.0.1", timeout_s=30)
+        coord.initialize()
+        coord.deploy_stages()
+        coord.start()
+        with pytest.raises(PipelineError, match="FORWARD_JOB failed"):
+            coord.train_step(torch.randn(2, 5, 12, 12), torch.zeros(2, dtype=torch.long), schedule="sync")
+        coord.stop()
+    finally:
+        w.close()
+
+
+@pytest.mark.gpu
+def test_native_gpu_stages_train_like_python_gpu_stages(worker_bin):
+    """Native stages on the GPU backend (bf16 NHWC activations on the wire, flagged channels-last
+    like the Python transport) against Python GPU stages: the same loss curve to bf16 accuracy."""
+    from dcnn_amd.nn import Adam
+    from dcnn_amd.parallel.pipeline import DistributedCoordinator, Endpoint, InProcessCoordinator
+    kw = dict(num_microbatches=2, stage_devices=["GPU:0", "GPU:0"], device="GPU:0")
+    ref_model = _model()
+    ref = InProcessCoordinator(ref_model, Adam(1e-3), "softmax_crossentropy", num_stages=2, transport="message",
+                               use_graph=False, **kw)
+    ref.initialize()
+    ref.deploy_stages()
+    ref.start()
+    ref.send_parameters(ref_model)
+    ref_losses = _train(ref, 4, "semi_async")
+    ref.stop()
+    w = _Workers(worker_bin, 2)
+    try:
+        model = _model()
+        eps = [Endpoint.network("127.0.0.1", p) for p in w.ports]
+        coord = DistributedCoordinator(model, Adam(1e-3), "softmax_crossentropy", eps, host="127.0.0.1",
+                                       timeout_s=120, **kw)
+        coord.initialize()
+        coord.deploy_stages()
+        coord.start()
+        coord.send_parameters(model)
+        assert all(s.get("native") and s.get("device", "").startswith("GPU") for s in coord.status())
+        losses = _train(coord, 4, "semi_async")
+        coord.stop()
+    finally:
+        w.close()
+    np.testing.assert_allclose(losses, ref_losses, rtol=3e-2)
+    assert losses[-1] < losses[0]
