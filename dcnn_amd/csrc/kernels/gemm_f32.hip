@@ -197,6 +197,196 @@ __global__ void __launch_bounds__(256, 2) gemm_g2f_kernel(G2Args p) {
   }
 }
 
+// Wide-tile variant of gemm_g2f_kernel for the grids that fill the chip with it: a BM x BN = 128 x
+// 128 output tile, 4 waves of 64 x 64, each wave 2 x 2 tiles of v_mfma_f32_32x32x2_f32 (16
+// accumulators each). Twice the output columns share every gathered A row and twice the rows
+// every B row, so the tap-gather loads per FLOP halve (the 64 x 64 kernel is load-bound on the
+// ResNet shapes). K order: k-block rows are read as two float4 per lane (lane half h holds
+// k = 8h .. 8h + 7 of the block); MFMA step s takes k = s from half 0 and k = 8 + s from half 1 for
+// BOTH operands, so every k is summed once (the order differs from the 16x16x4 kernel: exact f32
+// arithmetic, a different fma chain).
+template <int BM, int BN>
+__global__ void __launch_bounds__(256, 2) gemm_g2f_wide_kernel(G2Args p) {
+  constexpr int WM = BM / 2, WN = BN / 2;     // per-wave tile
+  constexpr int TM = WM / 32, TN = WN / 32;   // 32x32 MFMA tiles per wave
+  constexpr int AR = BM / 64, BR = BN / 64;   // loader rows per thread (64 rows per pass)
+  __shared__ __attribute__((aligned(16))) float As[2][BM * FPITCH];
+  __shared__ __attribute__((aligned(16))) float Bs[2][BN * FPITCH];
+  __shared__ float red[2][4][BN];
+  const float* A = reinterpret_cast<const float*>(p.A);
+  const float* B = reinterpret_cast<const float*>(p.B);
+  float* C = reinterpret_cast<float*>(p.C);
+  const float* R = reinterpret_cast<const float*>(p.residual);
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int wm = wid >> 1, wn = wid & 1;
+  const int tiles_n = (p.N + BN - 1) / BN;
+  const int lt = xcd_remap_f(blockIdx.x, gridDim.x);
+  const int tm = lt / tiles_n, tn = lt % tiles_n;
+  const int m0 = tm * BM, n0 = tn * BN;
+  if (p.zero_ptr && blockIdx.x == 0)
+    for (int i = tid; i < p.zero_n; i += 256) p.zero_ptr[i] = 0.f;
+
+  const int lr = tid >> 2, lc = tid & 3;  // loader: rows lr + 64 r, float4 chunk lc
+  long a_base[AR];
+  uint64_t a_mask[AR];
+#pragma unroll
+  for (int r = 0; r < AR; ++r) {
+    a_base[r] = 0;
+    a_mask[r] = 0;
+    const int m = m0 + lr + 64 * r;
+    if (m < p.M) {
+      const int ghw = p.GH * p.GW;
+      const int img = m / ghw, rem = m - img * ghw;
+      const int gy = rem / p.GW, gx = rem - gy * p.GW;
+      const int y0 = gy * p.SY, x0 = gx * p.SX;
+      a_base[r] = (((long)img * p.H + y0) * p.W + x0) * p.Cs;
+      for (int t = 0; t < p.ntaps; ++t) {
+        const int sy = y0 + p.tap_dy[t], sx = x0 + p.tap_dx[t];
+        if (sy >= 0 && sy < p.H && sx >= 0 && sx < p.W) a_mask[r] |= (1ull << t);
+      }
+    }
+  }
+  bool b_ok[BR];
+  long b_base[BR];
+#pragma unroll
+  for (int r = 0; r < BR; ++r) {
+    const int n = n0 + lr + 64 * r;
+    b_ok[r] = n < p.N;
+    b_base[r] = (long)n * p.ldb;
+  }
+  const bool vec = (p.Cs & 3) == 0;
+
+  auto load = [&](int k0, float4 (&ra)[AR], float4 (&rb)[BR]) {
+    const int k = k0 + lc * 4;
+#pragma unroll
+    for (int r = 0; r < AR; ++r) ra[r] = make_float4(0.f, 0.f, 0.f, 0.f);
+#pragma unroll
+    for (int r = 0; r < BR; ++r) rb[r] = make_float4(0.f, 0.f, 0.f, 0.f);
+    if (vec) {  // the 4 elements share one tap
+      const int t = k / p.Cs, c = k - t * p.Cs;
+      if (t < p.ntaps) {
+#pragma unroll
+        for (int r = 0; r < AR; ++r)
+          if ((a_mask[r] >> t) & 1ull) ra[r] = *reinterpret_cast<const float4*>(A + a_base[r] + p.tap_srcoff[t] + c);
+#pragma unroll
+        for (int r = 0; r < BR; ++r)
+          if (b_ok[r]) rb[r] = *reinterpret_cast<const float4*>(B + b_base[r] + p.tap_b[t] + c);
+      }
+    } else {
+      float va[AR][4], vb[BR][4];
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const int kk = k + e, t = kk / p.Cs, c = kk - t * p.Cs;
+#pragma unroll
+        for (int r = 0; r < AR; ++r) va[r][e] = (t < p.ntaps && ((a_mask[r] >> t) & 1ull)) ? A[a_base[r] + p.tap_srcoff[t] + c] : 0.f;
+#pragma unroll
+        for (int r = 0; r < BR; ++r) vb[r][e] = (t < p.ntaps && b_ok[r]) ? B[b_base[r] + p.tap_b[t] + c] : 0.f;
+      }
+#pragma unroll
+      for (int r = 0; r < AR; ++r) ra[r] = make_float4(va[r][0], va[r][1], va[r][2], va[r][3]);
+#pragma unroll
+      for (int r = 0; r < BR; ++r) rb[r] = make_float4(vb[r][0], vb[r][1], vb[r][2], vb[r][3]);
+    }
+  };
+
+  f32x16 acc[TM][TN];
+#pragma unroll
+  for (int i = 0; i < TM; ++i)
+#pragma unroll
+    for (int j = 0; j < TN; ++j)
+#pragma unroll
+      for (int e = 0; e < 16; ++e) acc[i][j][e] = 0.f;
+
+  const int K = p.ntaps * p.Cs;
+  const int nk = (K + FBK - 1) / FBK;
+  float4 ra[AR], rb[BR];
+  load(0, ra, rb);
+  int cur = 0;
+  const int h = lane >> 5, l32 = lane & 31;
+  for (int kt = 0; kt < nk; ++kt) {
+#pragma unroll
+    for (int r = 0; r < AR; ++r) *reinterpret_cast<float4*>(&As[cur][(lr + 64 * r) * FPITCH + lc * 4]) = ra[r];
+#pragma unroll
+    for (int r = 0; r < BR; ++r) *reinterpret_cast<float4*>(&Bs[cur][(lr + 64 * r) * FPITCH + lc * 4]) = rb[r];
+    __syncthreads();
+    if (kt + 1 < nk) load((kt + 1) * FBK, ra, rb);
+    float a[TM][8], b[TN][8];
+#pragma unroll
+    for (int i = 0; i < TM; ++i) {
+      const float* src = &As[cur][(wm * WM + i * 32 + l32) * FPITCH + h * 8];
+      const float4 x0 = *reinterpret_cast<const float4*>(src), x1 = *reinterpret_cast<const float4*>(src + 4);
+      a[i][0] = x0.x; a[i][1] = x0.y; a[i][2] = x0.z; a[i][3] = x0.w;
+      a[i][4] = x1.x; a[i][5] = x1.y; a[i][6] = x1.z; a[i][7] = x1.w;
+    }
+#pragma unroll
+    for (int j = 0; j < TN; ++j) {
+      const float* src = &Bs[cur][(wn * WN + j * 32 + l32) * FPITCH + h * 8];
+      const float4 x0 = *reinterpret_cast<const float4*>(src), x1 = *reinterpret_cast<const float4*>(src + 4);
+      b[j][0] = x0.x; b[j][1] = x0.y; b[j][2] = x0.z; b[j][3] = x0.w;
+      b[j][4] = x1.x; b[j][5] = x1.y; b[j][6] = x1.z; b[j][7] = x1.w;
+    }
+#pragma unroll
+    for (int s2 = 0; s2 < 8; ++s2)
+#pragma unroll
+      for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int j = 0; j < TN; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(a[i][s2], b[j][s2], acc[i][j], 0, 0, 0);
+    cur ^= 1;
+  }
+
+  // ---- epilogue from the accumulators: lane owns column l32 of each 32x32 tile, rows
+  // (e & 3) + 8 (e >> 2) + 4 h of register e
+  const int ghw = p.GH * p.GW;
+#pragma unroll
+  for (int j = 0; j < TN; ++j) {
+    const int cl = wn * WN + j * 32 + l32;
+    const int col = n0 + cl;
+    const bool cok = col < p.N;
+    const float bv = (p.bias && cok) ? p.bias[col] : 0.f;
+    // pivot: the wave's first row of the column (register 0 of lane half 0)
+    const float piv = __shfl(acc[0][j][0] + bv, l32, 64);
+    float s = 0.f, q = 0.f, n = 0.f;
+#pragma unroll
+    for (int i = 0; i < TM; ++i)
+#pragma unroll
+      for (int e = 0; e < 16; ++e) {
+        const int m = m0 + wm * WM + i * 32 + (e & 3) + 8 * (e >> 2) + 4 * h;
+        if (m >= p.M || !cok) continue;
+        const int img = m / ghw, rem = m - img * ghw;
+        const int gy = rem / p.GW, gx = rem - gy * p.GW;
+        const long orow = ((long)img * p.OH + gy * p.OSY + p.ORY) * p.OW + gx * p.OSX + p.ORX;
+        float v = acc[i][j][e] + bv;
+        if (R) v += R[orow * p.ldc + col];
+        if (p.relu) v = fmaxf(v, 0.f);
+        C[orow * p.ldc + col] = v;
+        const float d = v - piv;
+        s += d;
+        q += d * d;
+        n += 1.f;
+      }
+    if (p.stats) {
+      s += __shfl_xor(s, 32, 64);
+      q += __shfl_xor(q, 32, 64);
+      n += __shfl_xor(n, 32, 64);
+      if (h == 0) {
+        red[wm][0][cl] = s;
+        red[wm][1][cl] = q;
+        red[wm][2][cl] = piv;
+        red[wm][3][cl] = n;
+      }
+    }
+  }
+  if (p.stats) {
+    __syncthreads();
+    for (int c = tid; c < BN; c += 256) {
+      if (n0 + c >= p.N) continue;
+      Welford t = welford_from_shifted(red[0][3][c], red[0][2][c], red[0][0][c], red[0][1][c]);
+      t = welford_merge(t, welford_from_shifted(red[1][3][c], red[1][2][c], red[1][0][c], red[1][1][c]));
+      store_welford(p.stats, tm, p.N, n0 + c, t);
+    }
+  }
+}
+
 // dW[m][n] (+ bias grad) = sum_p dY[p][m] * X[gather(p, tap(n))][c(n)] over this split's pixels
 __global__ void __launch_bounds__(256, 2) gemm_t2f_kernel(T2Args p) {
   __shared__ __attribute__((aligned(16))) float As[FBM * FPITCH];  // [m][k]
@@ -297,6 +487,137 @@ __global__ void __launch_bounds__(256, 2) gemm_t2f_kernel(T2Args p) {
       }
     }
   if (p.bias_slab && tn == 0 && tid < FBM && m0 + tid < p.M) p.bias_slab[(long)split * p.M + m0 + tid] = bias_acc;
+}
+
+// Wide-tile variant of gemm_t2f_kernel (128 x 128 dW tile per split, 32x32x2 MFMA; same K
+// permutation as gemm_g2f_wide_kernel): half the gathered loads per FLOP.
+template <int BM, int BN>
+__global__ void __launch_bounds__(256, 2) gemm_t2f_wide_kernel(T2Args p) {
+  constexpr int WM = BM / 2, WN = BN / 2, TM = WM / 32, TN = WN / 32;
+  constexpr int AQ = BM / 64, BQ = BN / 64;  // float4 column groups per thread (16 threads x 4 cols per pass)
+  __shared__ __attribute__((aligned(16))) float As[BM * FPITCH];  // [m][k]
+  __shared__ __attribute__((aligned(16))) float Bs[BN * FPITCH];  // [n][k]
+  const float* dY = reinterpret_cast<const float*>(p.dY);
+  const float* X = reinterpret_cast<const float*>(p.X);
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int wm = wid >> 1, wn = wid & 1;
+  const int tiles_m = (p.M + BM - 1) / BM, tiles_n = (p.N + BN - 1) / BN;
+  const int tiles = tiles_m * tiles_n;
+  const int lt = xcd_remap_f(blockIdx.x, gridDim.x);
+  const int split = lt / tiles, tt = lt % tiles;
+  const int tm = tt / tiles_n, tn = tt % tiles_n;
+  const int m0 = tm * BM, n0 = tn * BN;
+  const long pbeg = (long)split * p.k_per_split;
+  const long pend = pbeg + p.k_per_split < p.P ? pbeg + p.k_per_split : p.P;
+  const int lk = tid >> 4, lq = tid & 15;  // loader: pixel lk of the block, columns 4 lq + 64 r
+  float bias_acc = 0.f;
+  f32x16 acc[TM][TN];
+#pragma unroll
+  for (int i = 0; i < TM; ++i)
+#pragma unroll
+    for (int j = 0; j < TN; ++j)
+#pragma unroll
+      for (int e = 0; e < 16; ++e) acc[i][j][e] = 0.f;
+  const int ghw = p.GH * p.GW;
+  const int h = lane >> 5, l32 = lane & 31;
+  for (long k0 = pbeg; k0 < pend; k0 += FBK) {
+    const long pix = k0 + lk;
+    float va[AQ][4], vb[BQ][4];
+#pragma unroll
+    for (int r = 0; r < AQ; ++r)
+#pragma unroll
+      for (int e = 0; e < 4; ++e) va[r][e] = 0.f;
+#pragma unroll
+    for (int r = 0; r < BQ; ++r)
+#pragma unroll
+      for (int e = 0; e < 4; ++e) vb[r][e] = 0.f;
+    if (pix < pend) {
+#pragma unroll
+      for (int r = 0; r < AQ; ++r) {
+        const int am = m0 + lq * 4 + 64 * r;
+        if ((p.ldy & 3) == 0 && am + 3 < p.M) {
+          const float4 v = *reinterpret_cast<const float4*>(dY + pix * p.ldy + am);
+          va[r][0] = v.x; va[r][1] = v.y; va[r][2] = v.z; va[r][3] = v.w;
+        } else {
+#pragma unroll
+          for (int e = 0; e < 4; ++e)
+            if (am + e < p.M) va[r][e] = dY[pix * p.ldy + am + e];
+        }
+      }
+      const int img = (int)(pix / ghw), rem = (int)(pix - (long)img * ghw);
+      const int gy = rem / p.GW, gx = rem - gy * p.GW;
+      const int y0 = gy * p.SY, x0 = gx * p.SX;
+#pragma unroll
+      for (int r = 0; r < BQ; ++r) {
+        const int bn = n0 + lq * 4 + 64 * r;
+        if ((p.Cs & 3) == 0 && bn + 3 < p.N) {
+          const int t = bn / p.Cs, c = bn - t * p.Cs;
+          const int sy = y0 + p.tap_dy[t], sx = x0 + p.tap_dx[t];
+          if (sy >= 0 && sy < p.H && sx >= 0 && sx < p.W) {
+            const float4 v = *reinterpret_cast<const float4*>(X + (((long)img * p.H + sy) * p.W + sx) * p.Cs + c);
+            vb[r][0] = v.x; vb[r][1] = v.y; vb[r][2] = v.z; vb[r][3] = v.w;
+          }
+        } else {
+#pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            const int n = bn + e;
+            if (n >= p.N) continue;
+            const int t = n / p.Cs, c = n - t * p.Cs;
+            const int sy = y0 + p.tap_dy[t], sx = x0 + p.tap_dx[t];
+            if (sy >= 0 && sy < p.H && sx >= 0 && sx < p.W) vb[r][e] = X[(((long)img * p.H + sy) * p.W + sx) * p.Cs + c];
+          }
+        }
+      }
+    }
+    __syncthreads();  // previous tile fully consumed
+#pragma unroll
+    for (int r = 0; r < AQ; ++r)
+#pragma unroll
+      for (int e = 0; e < 4; ++e) As[(lq * 4 + 64 * r + e) * FPITCH + lk] = va[r][e];
+#pragma unroll
+    for (int r = 0; r < BQ; ++r)
+#pragma unroll
+      for (int e = 0; e < 4; ++e) Bs[(lq * 4 + 64 * r + e) * FPITCH + lk] = vb[r][e];
+    __syncthreads();
+    if (p.bias_slab && tn == 0 && tid < BM) {
+#pragma unroll
+      for (int k = 0; k < FBK; ++k) bias_acc += As[tid * FPITCH + k];
+    }
+    float a[TM][8], b[TN][8];
+#pragma unroll
+    for (int i = 0; i < TM; ++i) {
+      const float* src = &As[(wm * WM + i * 32 + l32) * FPITCH + h * 8];
+      const float4 x0 = *reinterpret_cast<const float4*>(src), x1 = *reinterpret_cast<const float4*>(src + 4);
+      a[i][0] = x0.x; a[i][1] = x0.y; a[i][2] = x0.z; a[i][3] = x0.w;
+      a[i][4] = x1.x; a[i][5] = x1.y; a[i][6] = x1.z; a[i][7] = x1.w;
+    }
+#pragma unroll
+    for (int j = 0; j < TN; ++j) {
+      const float* src = &Bs[(wn * WN + j * 32 + l32) * FPITCH + h * 8];
+      const float4 x0 = *reinterpret_cast<const float4*>(src), x1 = *reinterpret_cast<const float4*>(src + 4);
+      b[j][0] = x0.x; b[j][1] = x0.y; b[j][2] = x0.z; b[j][3] = x0.w;
+      b[j][4] = x1.x; b[j][5] = x1.y; b[j][6] = x1.z; b[j][7] = x1.w;
+    }
+#pragma unroll
+    for (int s2 = 0; s2 < 8; ++s2)
+#pragma unroll
+      for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int j = 0; j < TN; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(a[i][s2], b[j][s2], acc[i][j], 0, 0, 0);
+  }
+  float* out = p.slab + (long)split * p.M * p.N;
+#pragma unroll
+  for (int i = 0; i < TM; ++i)
+#pragma unroll
+    for (int j = 0; j < TN; ++j) {
+      const int col = n0 + wn * WN + j * 32 + l32;
+#pragma unroll
+      for (int e = 0; e < 16; ++e) {
+        const int row = m0 + wm * WM + i * 32 + (e & 3) + 8 * (e >> 2) + 4 * h;
+        if (row < p.M && col < p.N) out[(long)row * p.N + col] = acc[i][j][e];
+      }
+    }
+  if (p.bias_slab && tn == 0 && tid < BM && m0 + tid < p.M) p.bias_slab[(long)split * p.M + m0 + tid] = bias_acc;
 }
 
 // ------------------------------------------------------------------------------------------
@@ -617,21 +938,41 @@ static bool f32_split() {
 void set_f32_mode(int mode) { g_f32_mode = mode ? 1 : 0; }
 int get_f32_mode() { return f32_split() ? 1 : 0; }
 
+// exact-f32 forward / dgrad tile: 128 x 128 (32x32x2 MFMA) while that still gives >= 1.5
+// workgroups per CU, else the 64 x 64 16x16x4 kernel
+static int g2f_bm(int M, int N) {
+  const long wide = (long)((M + 127) / 128) * ((N + 127) / 128);
+  return (N >= 128 && wide >= 384) ? 128 : FBM;
+}
+
 void gemm_g2f(const G2Args& a, hipStream_t s) {
   if (a.ntaps > 64) throw std::runtime_error("gemm_g2f: at most 64 taps");
-  const int tiles = ((a.M + FBM - 1) / FBM) * ((a.N + FBN - 1) / FBN);
-  if (f32_split())
+  if (f32_split()) {
+    const int tiles = ((a.M + FBM - 1) / FBM) * ((a.N + FBN - 1) / FBN);
     hipLaunchKernelGGL(gemm_g2x_kernel, dim3(tiles), dim3(256), 0, s, a);
-  else
+  } else if (g2f_bm(a.M, a.N) == 128) {
+    const int tiles = ((a.M + 127) / 128) * ((a.N + 127) / 128);
+    hipLaunchKernelGGL((gemm_g2f_wide_kernel<128, 128>), dim3(tiles), dim3(256), 0, s, a);
+  } else {
+    const int tiles = ((a.M + FBM - 1) / FBM) * ((a.N + FBN - 1) / FBN);
     hipLaunchKernelGGL(gemm_g2f_kernel, dim3(tiles), dim3(256), 0, s, a);
+  }
   DCNN_LAUNCH_CHECK();
 }
 
-int gemm_g2f_stat_rows(int M, int N) { return (M + FBM - 1) / FBM; }
+int gemm_g2f_stat_rows(int M, int N) {
+  const int bm = f32_split() ? FBM : g2f_bm(M, N);
+  return (M + bm - 1) / bm;
+}
+
+// exact-f32 weight-gradient tile: 128 x 128 when both sides hold at least 128 (fewer, larger
+// split-K slabs: every split still gets one workgroup per CU or more)
+static int t2f_bm(int M, int N) { return (M >= 128 && N >= 128) ? 128 : FBM; }
 
 int gemm_t2f_splits(int M, int N, int P) {
-  const int tiles = ((M + FBM - 1) / FBM) * ((N + FBN - 1) / FBN);
-  int splits = (1024 + tiles - 1) / tiles;
+  const int bm = f32_split() ? FBM : t2f_bm(M, N);
+  const int tiles = ((M + bm - 1) / bm) * ((N + bm - 1) / bm);
+  int splits = ((bm == 128 ? 512 : 1024) + tiles - 1) / tiles;
   const long max_by_k = (P + 255) / 256;             // at least 256 pixels per split
   if (splits > max_by_k) splits = (int)max_by_k;
   const long slab_cap = (96l << 20) / (4l * M * N);  // <= 96 MB of fp32 partials
@@ -645,11 +986,16 @@ void gemm_t2f(T2Args a, int splits, hipStream_t s) {
   const long per = (a.P + splits - 1) / splits;
   const int bk = f32_split() ? XBK : FBK;
   a.k_per_split = (int)(((per + bk - 1) / bk) * bk);
-  const int tiles = ((a.M + FBM - 1) / FBM) * ((a.N + FBN - 1) / FBN);
-  if (f32_split())
+  if (f32_split()) {
+    const int tiles = ((a.M + FBM - 1) / FBM) * ((a.N + FBN - 1) / FBN);
     hipLaunchKernelGGL(gemm_t2x_kernel, dim3(tiles * splits), dim3(256), 0, s, a);
-  else
+  } else if (t2f_bm(a.M, a.N) == 128) {
+    const int tiles = ((a.M + 127) / 128) * ((a.N + 127) / 128);
+    hipLaunchKernelGGL((gemm_t2f_wide_kernel<128, 128>), dim3(tiles * splits), dim3(256), 0, s, a);
+  } else {
+    const int tiles = ((a.M + FBM - 1) / FBM) * ((a.N + FBN - 1) / FBN);
     hipLaunchKernelGGL(gemm_t2f_kernel, dim3(tiles * splits), dim3(256), 0, s, a);
+  }
   DCNN_LAUNCH_CHECK();
 }
 
