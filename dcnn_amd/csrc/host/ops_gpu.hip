@@ -135,10 +135,6 @@ void hconv_workspace(HConvArgs& a) {
   }
 }
 
-bool is_same3x3(const ConvShape& s) {
-  return s.KH == 3 && s.KW == 3 && s.SH == 1 && s.SW == 1 && s.PH == 1 && s.PW == 1;
-}
-
 // gathered-GEMM argument block (gemm2.hip) for a forward conv
 G2Args g2_fwd_args(const void* x, const void* w, void* y, const float* bias, const ConvShape& s) {
   G2Args a{};
@@ -165,6 +161,10 @@ G2Args g2_fwd_args(const void* x, const void* w, void* y, const float* bias, con
   return a;
 }
 
+ConvRouteGeom route_geom(const ConvShape& s, int g1s_mode) {
+  return ConvRouteGeom{s.N, s.C, s.H, s.W, s.Co, s.KH, s.KW, s.SH, s.SW, s.PH, s.PW, s.OH, s.OW, g1s_mode};
+}
+
 void wgrad_reduce(const float* slab, float* gw, long n, const float* bslab, float* gb, long nb, int splits) {
   if (gb)
     splitk_reduce2(slab, gw, n, bslab, gb, nb, splits, 1, S);
@@ -181,24 +181,27 @@ void zero(void* p, long nbytes) { zero_bytes(p, nbytes, S); }
 
 void conv_fwd(const void* x, const void* w, const float* bias, void* y, const ConvShape& s) {
   const long xb = (long)s.N * s.H * s.W * s.C * 2, wb = (long)s.Co * s.KH * s.KW * s.C * 2;
-  if (is_same3x3(s) && hconv_supported(s.N, s.H, s.W, s.C, s.Co, 9) && xb < (1l << 31)) {
+  // the shared routing table (conv_route.cpp): the same kernels as the Python front end
+  const int route = conv_fwd_route(route_geom(s, 0));
+  if (route == ROUTE_HALO && xb < (1l << 31)) {
     HConvArgs a{};
     a.A = static_cast<const bf16*>(x); a.B = static_cast<const bf16*>(w); a.C = static_cast<bf16*>(y);
     a.a_bytes = (unsigned)xb; a.b_bytes = (unsigned)wb;
-    a.NB = s.N; a.H = s.H; a.W = s.W; a.Cs = s.C; a.N = s.Co; a.ldb = 9 * s.C; a.ntaps = 9;
-    for (int t = 0; t < 9; ++t) { a.tap_dy[t] = t / 3 - 1; a.tap_dx[t] = t % 3 - 1; a.tap_b[t] = t * s.C; }
+    a.NB = s.N; a.H = s.H; a.W = s.W; a.Cs = s.C; a.N = s.Co; a.ldb = s.KH * s.KW * s.C; a.ntaps = s.KH * s.KW;
+    for (int t = 0; t < a.ntaps; ++t) {
+      a.tap_dy[t] = t / s.KW - s.PH; a.tap_dx[t] = t % s.KW - s.PW; a.tap_b[t] = t * s.C;
+    }
     a.bias = bias;
     hconv_workspace(a);
     hconv(a, S);
     return;
   }
-  if (s.KH == 1 && s.KW == 1 && s.PH == 0 && s.PW == 0 && s.SH == s.SW &&
-      g1s_rows(s.N * s.OH * s.OW, s.Co, s.C, 0) > 0) {
+  if (route == ROUTE_G1S) {
     g1s(static_cast<const bf16*>(x), static_cast<const bf16*>(w), static_cast<bf16*>(y), s.N * s.OH * s.OW, s.Co, s.C,
         s.H, s.W, s.OH, s.OW, s.SH, bias, nullptr, nullptr, 0, nullptr, 0, BnbArgs{}, 0, S);
     return;
   }
-  if (s.C % 8 == 0 && s.Co % 8 == 0 && s.KH * s.KW <= 64 && xb < (1l << 31) && wb < (1l << 31)) {
+  if (route != ROUTE_GENERIC && xb < (1l << 31) && wb < (1l << 31)) {
     gemm_g2(g2_fwd_args(x, w, y, bias, s), S);
     return;
   }
@@ -213,21 +216,27 @@ void conv_dgrad(const void* dy, const void* w, void* dx, const ConvShape& s) {
   bf16* wt = static_cast<bf16*>(scratch(W_T, (size_t)s.Co * T * s.C * 2));
   conv_weight_transpose(kBF16, w, wt, s.Co, T, s.C, S);  // [Co][T][C] -> [C][T][Co]
   const long dyb = (long)s.N * s.OH * s.OW * s.Co * 2, wtb = (long)s.C * T * s.Co * 2;
-  if (is_same3x3(s) && hconv_supported(s.N, s.OH, s.OW, s.Co, s.C, 9) && dyb < (1l << 31)) {
-    // transposed conv of a stride-1 conv: tap (ky, kx) reads dy at (1 - ky, 1 - kx)
+  const int route = conv_dgrad_route(route_geom(s, 0));  // shared routing table (conv_route.cpp)
+  if (route == ROUTE_HALO && dyb < (1l << 31)) {
+    // transposed conv of a stride-1 'same' conv: tap (ky, kx) reads dy at (PH - ky, PW - kx)
     HConvArgs a{};
     a.A = static_cast<const bf16*>(dy); a.B = wt; a.C = static_cast<bf16*>(dx);
     a.a_bytes = (unsigned)dyb; a.b_bytes = (unsigned)wtb;
-    a.NB = s.N; a.H = s.OH; a.W = s.OW; a.Cs = s.Co; a.N = s.C; a.ldb = 9 * s.Co; a.ntaps = 9;
-    for (int t = 0; t < 9; ++t) {
-      const int ky = t / 3, kx = t % 3;
-      a.tap_dy[t] = 1 - ky; a.tap_dx[t] = 1 - kx; a.tap_b[t] = t * s.Co;
+    a.NB = s.N; a.H = s.OH; a.W = s.OW; a.Cs = s.Co; a.N = s.C; a.ldb = T * s.Co; a.ntaps = T;
+    for (int t = 0; t < T; ++t) {
+      const int ky = t / s.KW, kx = t % s.KW;
+      a.tap_dy[t] = s.PH - ky; a.tap_dx[t] = s.PW - kx; a.tap_b[t] = t * s.Co;
     }
     hconv_workspace(a);
     hconv(a, S);
     return;
   }
-  if (s.C % 8 == 0 && s.Co % 8 == 0 && dyb < (1l << 31) && wtb < (1l << 31)) {
+  if (route == ROUTE_G1S) {  // streaming 1x1 data gradient
+    g1s(static_cast<const bf16*>(dy), wt, static_cast<bf16*>(dx), s.N * s.H * s.W, s.C, s.Co, s.H, s.W, s.H, s.W, 1,
+        nullptr, nullptr, nullptr, 0, nullptr, 0, BnbArgs{}, 0, S);
+    return;
+  }
+  if (route != ROUTE_GENERIC && dyb < (1l << 31) && wtb < (1l << 31)) {
     // stride-phase decomposition: output phase (ry, rx) is a dense GEMM over the taps reaching
     // it; all phases are row classes of ONE grouped launch (phases no tap reaches write zeros)
     struct Cls { int ry, rx, GH, GW, t0, nt; };
@@ -283,7 +292,8 @@ void conv_dgrad(const void* dy, const void* w, void* dx, const ConvShape& s) {
 void conv_wgrad(const void* dy, const void* x, float* gw, float* gb, const ConvShape& s) {
   const int Ng = s.KH * s.KW * s.C, P = s.N * s.OH * s.OW;
   const long dyb = (long)P * s.Co * 2, xb = (long)s.N * s.H * s.W * s.C * 2;
-  if (is_same3x3(s) && hwgrad_supported(s.N, s.H, s.W, s.C, s.Co, 9)) {
+  const int route = conv_wgrad_route(route_geom(s, -1));  // shared routing table (conv_route.cpp)
+  if (route == ROUTE_HALO) {
     const int splits = hwgrad_splits(s.N, s.H, s.W, s.C, s.Co);
     float* slab = static_cast<float*>(scratch(SLAB, (size_t)splits * s.Co * Ng * 4));
     float* bslab = gb ? static_cast<float*>(scratch(BSLAB, (size_t)splits * s.Co * 4)) : nullptr;
@@ -296,7 +306,7 @@ void conv_wgrad(const void* dy, const void* x, float* gw, float* gb, const ConvS
     wgrad_reduce(slab, gw, (long)s.Co * Ng, bslab, gb, s.Co, splits);
     return;
   }
-  if (s.C % 8 == 0 && s.Co % 8 == 0 && s.KH * s.KW <= 64 && dyb < (1l << 31) && xb < (1l << 31) && P < (1 << 24)) {
+  if (route == ROUTE_GEMM_G2 && dyb < (1l << 31) && xb < (1l << 31) && P < (1 << 24)) {
     const int splits = gemm_t2_splits(s.Co, Ng, P);
     float* slab = static_cast<float*>(scratch(SLAB, (size_t)splits * s.Co * Ng * 4));
     float* bslab = gb ? static_cast<float*>(scratch(BSLAB, (size_t)splits * s.Co * 4)) : nullptr;

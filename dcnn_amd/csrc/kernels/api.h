@@ -137,6 +137,17 @@ int get_f32_mode();
 void conv_weight_transpose_f32(const float* w, float* wt, int Co, int T_, int Ci, hipStream_t s);
 void gemm_tn(TnArgs a, int splits, hipStream_t s);
 int gemm_tn_splits(int M, int N, int P);
+// The shared conv routing table (conv_route.cpp): which kernel family runs a bf16 convolution,
+// asked by both front ends (ops/hip.py and the C++ host API's GPU backend). g1s_mode: the
+// streaming kernel's epilogue mode the caller needs (forward 0 / 1 = statistics, dgrad 0 / 2 =
+// backward-BatchNorm fusion), < 0 when the epilogue options rule it out.
+struct ConvRouteGeom {
+  int N, C, H, W, Co, KH, KW, SH, SW, PH, PW, OH, OW, g1s_mode;
+};
+enum ConvRoute : int { ROUTE_GENERIC = 0, ROUTE_GEMM_G2 = 1, ROUTE_HALO = 2, ROUTE_G1S = 3 };
+int conv_fwd_route(ConvRouteGeom g);
+int conv_dgrad_route(ConvRouteGeom g);
+int conv_wgrad_route(ConvRouteGeom g);
 void splitk_reduce(const float* slab, float* out, long n, int splits, int accumulate, hipStream_t s);
 // weight + bias slabs in one launch (nb = 0: bias segment absent)
 void splitk_reduce2(const float* slab, float* out, long n, const float* bslab, float* bout, long nb, int splits,

@@ -197,6 +197,14 @@ PYBIND11_MODULE(_kernels, m) {
   // grouped row classes (strided-dgrad phases in one launch): classes = (first tap, taps, ORY, ORX)
   m.def("gemm_g2_grouped", &bind_gemm_g2);
   m.def("gemm_g2_stat_rows", &gemm_g2_stat_rows);
+  for (auto [name, fn] : {std::pair<const char*, int (*)(ConvRouteGeom)>{"conv_fwd_route", &conv_fwd_route},
+                          {"conv_dgrad_route", &conv_dgrad_route}, {"conv_wgrad_route", &conv_wgrad_route}})
+    m.def(name, [fn](int N, int C, int H, int W, int Co, int KH, int KW, int SH, int SW, int PH, int PW, int OH, int OW,
+                     int g1s_mode) { return fn(ConvRouteGeom{N, C, H, W, Co, KH, KW, SH, SW, PH, PW, OH, OW, g1s_mode}); });
+  m.attr("ROUTE_GENERIC") = (int)ROUTE_GENERIC;
+  m.attr("ROUTE_GEMM_G2") = (int)ROUTE_GEMM_G2;
+  m.attr("ROUTE_HALO") = (int)ROUTE_HALO;
+  m.attr("ROUTE_G1S") = (int)ROUTE_G1S;
   m.def("g1s_rows", &g1s_rows);
   m.def("g1s_enable", &g1s_enable);
   m.def("g1s_gen_rows", &g1s_gen_rows);

@@ -256,8 +256,13 @@ def conv2d_fwd(x, w, bias, stride, pad, *, stats=False, residual=None, relu=Fals
                    _fwd_taps(Ci, W, KH, KW, ph, pw), KH * KW * Ci, Co, OH, OW, 1, 1, 0, 0, ptr(bias), ptr(residual),
                    ptr(slab), int(relu), ptr(sums), 2 * Co if stats else 0, _NOBNB, stream_ptr())
         return y, ((slab, rows, sums) if stats else None)
-    if (KH, KW) == (1, 1) and (ph, pw) == (0, 0) and sh == sw and not out_fp32 and x.dtype == BF16 \
-            and w.dim() == 4 and (not stats or (residual is None and not relu)):
+    # the shared routing table (csrc/kernels/conv_route.cpp, also used by the C++ host API)
+    g1s_mode = (1 if stats else 0) if (w.dim() == 4 and (not stats or (residual is None and not relu))) else -1
+    route = (K.conv_fwd_route(N, Ci, H, W, Co, KH, KW, sh, sw, ph, pw, OH, OW, g1s_mode)
+             if not out_fp32 else K.ROUTE_GENERIC)
+    if route == K.ROUTE_HALO and KH * KW == 1 and not _HCONV_1X1:
+        route = K.ROUTE_GEMM_G2
+    if route == K.ROUTE_G1S:
         # streaming 1x1 conv (g1s.hip): weights in registers, one statistics row per pixel range
         rows = K.g1s_rows(M, Co, Ci, 1 if stats else 0)
         if rows:
@@ -268,7 +273,7 @@ def conv2d_fwd(x, w, bias, stride, pad, *, stats=False, residual=None, relu=Fals
                   ptr(slab), int(relu), ptr(sums), 2 * Co if stats else 0, _NOBNB, 1 if stats else 0, stream_ptr())
             return y, ((slab, rows, sums) if stats else None)
     taps = _fwd_taps(Ci, W, KH, KW, ph, pw)
-    if not out_fp32 and _hconv_ok(N, OH, OW, H, W, sh, sw, Ci, Co, taps, w):
+    if route == K.ROUTE_HALO and len(taps) == KH * KW:
         y = _empty((N, Co, OH, OW), BF16, x.device, True)
         slab, rows, sums = None, 0, None
         if stats:
@@ -280,7 +285,7 @@ def conv2d_fwd(x, w, bias, stride, pad, *, stats=False, residual=None, relu=Fals
                 2 * Co if stats else 0, _NOBNB, 0, 0, *_hconv_split(K, N, H, W, Ci, Co, KH * KW, x.device),
                 stream_ptr())
         return y, ((slab, rows, sums) if stats else None)
-    if _g2_ok(Ci, Co) and not out_fp32:
+    if route in (K.ROUTE_GEMM_G2, K.ROUTE_HALO, K.ROUTE_G1S):
         y = _empty((N, Co, OH, OW), BF16, x.device, True)
         slab, rows, sums = None, 0, None
         if stats:
@@ -592,7 +597,14 @@ def conv2d_dgrad(dy, wt, x_shape, stride, pad, *, residual=None, bnb=None):
     f32 = dy.dtype == F32
     if f32:
         assert wt.dtype == F32, "fp32 dgrad needs an fp32 transposed weight (conv_weight_t(..., dtype=F32))"
-    if not f32 and not _g2_ok(Co, Ci):
+    fuse_req = bnb is not None and _BNB and not bnb.pooled and not f32 and bnb.x.dtype == BF16 \
+        and tuple(bnb.x.shape) == (N, Ci, H, W)
+    # the shared routing table (csrc/kernels/conv_route.cpp, also used by the C++ host API)
+    route = K.conv_dgrad_route(N, Ci, H, W, Co, KH, KW, sh, sw, ph, pw, OH, OW, 2 if fuse_req else 0) \
+        if not f32 else K.ROUTE_GEMM_G2
+    if route == K.ROUTE_HALO and KH * KW == 1 and not _HCONV_1X1:
+        route = K.ROUTE_GEMM_G2
+    if not f32 and route == K.ROUTE_GENERIC:
         dx = _empty((N, Ci, H, W), BF16, dy.device, True)
         Kd = KH * KW * Co
         K.gemm_nt(dy.data_ptr(), wt.data_ptr(), dx.data_ptr(), N * H * W, Ci, Kd, 0, Kd, Ci, CONV_DGRAD,
@@ -641,8 +653,8 @@ def conv2d_dgrad(dy, wt, x_shape, stride, pad, *, residual=None, bnb=None):
     g2 = K.gemm_g2f if f32 else K.gemm_g2
     fuse = (bnb is not None and _BNB and not bnb.pooled and not f32 and not empty_class and bnb.x.dtype == BF16
             and tuple(bnb.x.shape) == (N, Ci, H, W))
-    if not f32 and len(classes) == 1 and not empty_class and \
-            _hconv_ok(N, H, W, OH, OW, sh, sw, Co, Ci, classes[0][4], wt):
+    if not f32 and len(classes) == 1 and not empty_class and route == K.ROUTE_HALO and \
+            len(classes[0][4]) == KH * KW:
         slab = sums = None
         rows = 0
         if fuse:
@@ -675,8 +687,7 @@ def conv2d_dgrad(dy, wt, x_shape, stride, pad, *, residual=None, bnb=None):
         if fuse:
             dx._bnb = (bnb.bn, slab, rows, sums)
         return dx
-    if (not f32 and (KH, KW) == (1, 1) and (sh, sw) == (1, 1) and (ph, pw) == (0, 0) and not empty_class
-            and len(classes) == 1):
+    if not f32 and route == K.ROUTE_G1S and not empty_class and len(classes) == 1:
         # streaming 1x1 data gradient (g1s.hip), backward-BatchNorm fusion in its epilogue
         rows = K.g1s_rows(N * H * W, Ci, Co, 2 if fuse else 0)
         if rows:
@@ -826,7 +837,10 @@ def conv2d_wgrad(dy, x, w_shape, stride, pad, grad_w, grad_b=None):
         assert grad_w.is_contiguous(memory_format=CL) or KH * KW == 1 or Ci == 1
         _reduce_wb(K, slab, grad_w, Co * Ng, bslab, grad_b, Co, splits, st)
         return
-    if hw_ok:
+    # the shared routing table (csrc/kernels/conv_route.cpp, also used by the C++ host API)
+    route = (K.conv_wgrad_route(N, Ci, H, W, Co, KH, KW, stride[0], stride[1], pad[0], pad[1], OH, OW, -1)
+             if Cx == Ci else K.ROUTE_GEMM_G2)
+    if route == K.ROUTE_HALO:
         # halo-tiled wgrad: X read ~1.4x instead of once per tap
         Ng = KH * KW * Ci
         splits = K.hwgrad_splits(N, H, W, Ci, Co)

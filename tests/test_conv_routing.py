@@ -51,3 +51,28 @@ def test_1x1_split3_concat_stays_exact(stub):
     assert not hip._hconv_ok(32, 4, 4, 4, 4, 1, 1, 3 * 2048, 512, TAP1, None, True)
     # 3x3 convs still take the split-precision halo path
     assert hip._hconv_ok(256, 32, 32, 32, 32, 1, 1, 3 * 64, 64, TAPS9, None, True)
+
+
+def test_shared_route_table():
+    """The kernel library's routing table (csrc/kernels/conv_route.cpp), which both the Python
+    front end and the C++ host API's GPU backend ask: ResNet layer shapes land on the intended
+    kernel families (host-side query, no GPU needed)."""
+    from dcnn_amd.ops._ext import kernels
+    K = kernels()
+
+    def fwd(N, C, H, W, Co, k, s, p, mode=0):
+        OH, OW = (H + 2 * p - k) // s + 1, (W + 2 * p - k) // s + 1
+        return K.conv_fwd_route(N, C, H, W, Co, k, k, s, s, p, p, OH, OW, mode)
+
+    assert fwd(256, 64, 32, 32, 64, 3, 1, 1) == K.ROUTE_HALO          # layer-1 3x3
+    assert fwd(256, 256, 8, 8, 256, 3, 1, 1) == K.ROUTE_HALO          # 8x8 maps (gutter layout)
+    assert fwd(256, 128, 16, 16, 256, 3, 2, 1) == K.ROUTE_GEMM_G2     # strided 3x3
+    assert fwd(256, 64, 32, 32, 128, 1, 2, 0) == K.ROUTE_G1S          # strided 1x1 projection
+    assert fwd(32, 1024, 8, 8, 256, 1, 1, 0) == K.ROUTE_HALO          # K >= 1024 1x1, small grid
+    assert fwd(256, 1024, 8, 8, 256, 1, 1, 0) == K.ROUTE_GEMM_G2      # ... large grid
+    assert fwd(8, 3, 32, 32, 16, 3, 1, 1) == K.ROUTE_GENERIC          # odd channel count
+    assert fwd(256, 64, 32, 32, 256, 1, 1, 0, -1) != K.ROUTE_G1S      # epilogue not on g1s
+    assert K.conv_dgrad_route(256, 64, 32, 32, 64, 3, 3, 1, 1, 1, 1, 32, 32, 2) == K.ROUTE_HALO
+    assert K.conv_dgrad_route(256, 64, 32, 32, 256, 1, 1, 1, 1, 0, 0, 32, 32, 0) == K.ROUTE_G1S
+    assert K.conv_wgrad_route(256, 64, 32, 32, 64, 3, 3, 1, 1, 1, 1, 32, 32, -1) == K.ROUTE_HALO
+    assert K.conv_wgrad_route(256, 64, 32, 32, 128, 3, 3, 2, 2, 1, 1, 16, 16, -1) == K.ROUTE_GEMM_G2
