@@ -5,7 +5,9 @@
 // Reference parity: include/pipeline/pipeline_stage.hpp:29-308 (the event loop and its command
 // handlers), include/pipeline/stage_config.hpp:8-35 / endpoint.hpp:17-94 (the JSON configuration),
 // include/pipeline/network_stage_worker.hpp:25-114 + examples/network_worker.cpp:14-194 (the
-// worker process: `dcnn_amd/bin/network_worker`).
+// worker process: `dcnn_amd/bin/network_worker`), include/pipeline/coordinator.hpp:30-599 +
+// distributed_coordinator.hpp (the coordinator: `PipelineCoordinator`, driven by
+// `dcnn_amd/bin/pipeline_coordinator`, examples/semi_async_pipeline_coordinator.cpp).
 //
 // Wire compatibility with the Python stage (parallel/pipeline/stage.py): the same commands, the
 // same StageConfig JSON, tensors as typed job payloads (fp32 NCHW on the CPU; bf16 channels-last
@@ -22,8 +24,11 @@
 #include <thread>
 #include <vector>
 
+#include <stdexcept>
+
 #include "json.hpp"
 #include "nn.hpp"
+#include "train.hpp"
 
 namespace dcnn_native {
 struct Message;
@@ -59,6 +64,11 @@ std::unique_ptr<dcnn_native::Communicator> make_tcp_communicator(const std::stri
 
 // {"type": "sgd" | "adam" | "adamw", "parameters": {...}} (the Python OptimizerConfig)
 std::unique_ptr<Optimizer> create_optimizer(const json::Value& cfg);
+
+// flat state of a run of layers: every parameter in checkpoint order, then every BatchNorm's
+// running mean / variance (depth-first through residual blocks), fp32 values in logical order
+std::vector<double> pack_state(const std::vector<Layer*>& layers);
+void unpack_state(const std::vector<Layer*>& layers, const double* v, size_t n);
 
 class PipelineStage {
  public:
@@ -108,6 +118,141 @@ class PipelineStage {
   double fwd_ms_ = 0, bwd_ms_ = 0;
   std::thread beat_;
   std::atomic<bool> beat_stop_{false};
+};
+
+// ---------------------------------------------------------------- coordinator
+class PipelineError : public std::runtime_error {
+ public:
+  using std::runtime_error::runtime_error;
+};
+
+// a stage stopped answering: missed heartbeats or a lost control-plane connection
+class StageFailure : public PipelineError {
+ public:
+  StageFailure(const std::string& stage, const std::string& why) : PipelineError(stage + ": " + why), stage(stage) {}
+  std::string stage;
+};
+
+struct Partition {
+  int start = 0, end = 0;  // top-level layers [start, end)
+  bool operator==(const Partition& o) const { return start == o.start && end == o.end; }
+};
+// equal layer counts, the first L % S stages one layer more (reference naive_partitioner.hpp:13-32)
+std::vector<Partition> naive_partitions(int num_layers, int num_stages);
+// contiguous split minimising the largest per-stage cost (exact DP; the Python CostPartitioner)
+std::vector<Partition> balanced_partitions(const std::vector<double>& costs, int num_stages);
+
+enum class Schedule { Sync, SemiAsync, OneFOneB };
+// "sync" | "gpipe", "semi_async" | "async", "1f1b" | "one_f_one_b"
+Schedule parse_schedule(const std::string& s);
+
+struct CoordinatorOptions {
+  int num_microbatches = 1;
+  std::vector<std::string> stage_devices;  // per stage ("CPU", "GPU:0", ...); default CPU
+  std::string loss = "softmax_crossentropy";
+  std::string codec = "none";               // inline payload compression of the stages' sends
+  bool grad_scale_mean = true;              // micro-batch gradients * 1 / num_microbatches
+  double timeout_s = 120.0;
+  double heartbeat_s = 0.0;                 // > 0: stages beat every heartbeat_s ...
+  int heartbeat_misses = 3;                 // ... and are declared failed after this many misses
+  std::optional<int64_t> seed;              // stage i initialises with seed + i
+  std::string host = "127.0.0.1";           // the address stages reach the coordinator at
+  int port = 0;                             // 0: any free port
+};
+
+struct StepResult {
+  double loss = 0;  // mean of the micro-batch mean losses
+  long correct = 0;
+  long samples = 0;
+};
+
+// Coordinator of separate stage processes (native `network_worker`s or Python workers: the same
+// commands, StageConfig JSON and payloads) over the TCP control plane. The loss runs here on the
+// CPU; activations and gradients travel inline in the job messages.
+class PipelineCoordinator {
+ public:
+  PipelineCoordinator(json::Value model_config, json::Value optimizer_config, std::vector<Endpoint> stages,
+                      CoordinatorOptions opts = {});
+  ~PipelineCoordinator();
+  // partition (default: naive over the top-level layers), dial every stage, build the configs
+  void initialize(std::vector<Partition> parts = {});
+  void deploy_stages();  // CONFIG_TRANSFER back to front, join CONFIG_RECEIVED
+  void start();          // TRAIN_MODE
+  void stop();           // SHUTDOWN + close
+  void train_mode();
+  void eval_mode();
+
+  // one optimisation step over x (fp32 NCHW host) / labels (int64 host): split into micro-batches,
+  // run the schedule, UPDATE_PARAMETERS
+  StepResult train_step(const Tensor& x, const Tensor& labels, Schedule s = Schedule::SemiAsync);
+  StepResult evaluate_batch(const Tensor& x, const Tensor& labels);  // forward only
+  void update_parameters();
+
+  // LOAD_PARAMS: each stage's slice of a full model (same architecture) / flat states as given
+  void send_parameters(Sequential& model);
+  void load_parameters(const std::vector<std::vector<double>>& flats, bool full);
+  // SEND_PARAMS: per stage, pack_state (full: [n, state, optimizer state])
+  std::vector<std::vector<double>> collect_parameters(bool full = false);
+  // the trained weights / statistics into `model` (the full architecture)
+  void gather_into(Sequential& model);
+
+  float learning_rate() const { return lr_.learning_rate(); }
+  void set_learning_rate(float lr) { lr_.set_learning_rate(lr); }
+  // an Optimizer whose learning rate the next UPDATE_PARAMETERS broadcasts: give it to a Scheduler
+  Optimizer& lr_control() { return lr_; }
+
+  std::vector<json::Value> status();
+  std::vector<std::string> print_profiling();
+  void clear_profiling();
+  void barrier();
+  std::map<std::string, bool> health_check(double timeout_s = 10.0);
+  // re-partition from the stages' measured per-layer times (when they report them) and redeploy,
+  // carrying the trained weights over; returns the partitions in effect
+  std::vector<Partition> balance_load();
+
+  int num_stages() const { return (int)stages_.size(); }
+  const std::vector<Partition>& partitions() const { return parts_; }
+  const std::vector<std::string>& stage_names() const { return names_; }
+  int port() const { return port_; }
+  long steps() const { return steps_; }
+
+ private:
+  class LrControl : public Optimizer {
+   public:
+    using Optimizer::Optimizer;
+    void step(const std::vector<Param*>&) override {}
+  };
+  struct Pending;
+  json::Value stage_config(int i) const;
+  json::Value part_config(const Partition& p) const;
+  void broadcast(uint16_t cmd, const std::string& text = std::string());
+  std::vector<dcnn_native::Message> join(uint16_t cmd, size_t n, double timeout_s = 0);
+  bool recv_any(const std::vector<uint16_t>& cmds, dcnn_native::Message& out, int timeout_ms);
+  void check_errors();
+  bool take_beat(const dcnn_native::Message& m);
+  void send_job(const std::string& to, uint16_t cmd, uint64_t mb, const float* data, const std::vector<int64_t>& shape);
+  void forward_mb(const Pending& p);
+  void loss_and_backward(dcnn_native::Message& out, Pending& p, StepResult& r);
+  StepResult run_sync(std::vector<Pending>& mbs);
+  StepResult run_semi_async(std::vector<Pending>& mbs);
+  StepResult run_1f1b(std::vector<Pending>& mbs);
+  std::vector<Pending> split(const Tensor& x, const Tensor& labels) const;
+
+  json::Value model_cfg_, opt_cfg_;
+  std::vector<Endpoint> stages_;
+  CoordinatorOptions o_;
+  Loss loss_;
+  std::unique_ptr<dcnn_native::Communicator> comm_;
+  int port_ = 0;
+  std::vector<std::string> names_;
+  std::vector<Partition> parts_;
+  LrControl lr_;
+  float sent_lr_;
+  bool deployed_ = false;
+  long steps_ = 0;
+  std::map<std::string, std::chrono::steady_clock::time_point> last_beat_;
+  struct Stash;  // messages taken off the queue while waiting for another kind
+  std::unique_ptr<Stash> stash_;
 };
 
 }  // namespace dcnn

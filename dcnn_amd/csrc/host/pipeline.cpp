@@ -407,13 +407,34 @@ void PipelineStage::backward(Message& m) {
   bwd_ms_ += std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
 }
 
-std::vector<double> PipelineStage::flat_state() {
+namespace {
+void params_and_bns(const std::vector<Layer*>& layers, std::vector<Param*>& ps, std::vector<BatchNorm*>& bns) {
+  std::vector<Layer*> all;
+  for (Layer* l : layers) {
+    l->collect_params(ps);
+    l->collect_layers(all);
+  }
+  for (Layer* l : all)
+    if (auto* bn = dynamic_cast<BatchNorm*>(l)) bns.push_back(bn);
+}
+
+std::vector<Layer*> layers_of(const Sequential& m) {
+  std::vector<Layer*> out;
+  for (auto& l : m.layers()) out.push_back(l.get());
+  return out;
+}
+}  // namespace
+
+std::vector<double> pack_state(const std::vector<Layer*>& layers) {
+  std::vector<Param*> ps;
+  std::vector<BatchNorm*> bns;
+  params_and_bns(layers, ps, bns);
   std::vector<double> out;
-  for (Param* p : model_->parameters()) {
+  for (Param* p : ps) {
     const std::vector<float> v = p->value.view(p->shape, p->layout).to_host_f32();
     out.insert(out.end(), v.begin(), v.end());
   }
-  for (BatchNorm* bn : model_->batchnorms()) {
+  for (BatchNorm* bn : bns) {
     for (const Tensor* t : {&bn->running_mean, &bn->running_var}) {
       const std::vector<float> v = t->to_host_f32();
       out.insert(out.end(), v.begin(), v.end());
@@ -422,7 +443,10 @@ std::vector<double> PipelineStage::flat_state() {
   return out;
 }
 
-void PipelineStage::load_flat_state(const double* v, size_t n) {
+void unpack_state(const std::vector<Layer*>& layers, const double* v, size_t n) {
+  std::vector<Param*> ps;
+  std::vector<BatchNorm*> bns;
+  params_and_bns(layers, ps, bns);
   size_t off = 0;
   auto take = [&](int64_t k) {
     if (off + (size_t)k > n) throw std::runtime_error("flat state too short");
@@ -430,11 +454,11 @@ void PipelineStage::load_flat_state(const double* v, size_t n) {
     off += (size_t)k;
     return f;
   };
-  for (Param* p : model_->parameters()) {
+  for (Param* p : ps) {
     const Tensor t = Tensor::from_host(take(numel_of(p->shape)), p->shape, p->value.device(), DType::F32, p->layout);
     copy_into(p->value, t);
   }
-  for (BatchNorm* bn : model_->batchnorms()) {
+  for (BatchNorm* bn : bns) {
     for (Tensor* t : {&bn->running_mean, &bn->running_var}) {
       const Tensor h = Tensor::from_host(take(t->numel()), t->shape(), t->device(), DType::F32, t->layout());
       copy_into(*t, h);
@@ -442,8 +466,12 @@ void PipelineStage::load_flat_state(const double* v, size_t n) {
   }
   if (off != n) throw std::runtime_error("flat state size mismatch: consumed " + std::to_string(off) + " of " +
                                          std::to_string(n));
-  for (auto& l : model_->layers()) l->sync_shadow();
+  for (Layer* l : layers) l->sync_shadow();
 }
+
+std::vector<double> PipelineStage::flat_state() { return pack_state(layers_of(*model_)); }
+
+void PipelineStage::load_flat_state(const double* v, size_t n) { unpack_state(layers_of(*model_), v, n); }
 
 // [learning rate, step count, then the state tensors by name (Adam: m, v; SGD with momentum:
 // velocity), each over every parameter in checkpoint order]

@@ -3,8 +3,10 @@ worker processes driven over TCP by the Python DistributedCoordinator train like
 stages of an in-process coordinator (same partitions, same initial weights pushed by
 LOAD_PARAMS): the same losses and parameters after sync / semi-async / 1F1B steps, and the
 full parameter + optimizer state survives a SEND_PARAMS "full" -> LOAD_PARAMS round trip
-(the coordinator's recovery path). Reference: examples/network_worker.cpp:14-194,
-include/pipeline/pipeline_stage.hpp:29-308."""
+(the coordinator's recovery path). The native coordinator (csrc/host/coordinator.cpp,
+bin/pipeline_coordinator) driving those workers matches the Python coordinator step for step.
+Reference: examples/network_worker.cpp:14-194, include/pipeline/pipeline_stage.hpp:29-308,
+include/pipeline/coordinator.hpp:30-599, examples/semi_async_pipeline_coordinator.cpp."""
 import os
 import socket
 import subprocess
@@ -128,6 +130,82 @@ def test_native_stages_train_like_python_stages(worker_bin, schedule, opt_name):
     for a, b in zip(full, full2):
         assert torch.equal(a, b)
     assert all(p.returncode == 0 for p in w.procs), [p.returncode for p in w.procs]
+
+
+COORD = os.path.join(ROOT, "dcnn_amd", "bin", "pipeline_coordinator")
+
+
+@pytest.mark.parametrize("schedule", ["sync", "semi_async", "1f1b"])
+def test_native_coordinator_trains_like_python_coordinator(worker_bin, tmp_path, schedule):
+    """The C++ coordinator (csrc/host/coordinator.cpp, bin/pipeline_coordinator) driving native
+    workers: the same per-step losses and the same trained model (gathered from the stages and
+    saved by the C++ program, loaded in Python) as the Python coordinator on the same batches."""
+    import json
+    from dcnn_amd.nn import Adam, Sequential
+    from dcnn_amd.parallel.pipeline import InProcessCoordinator
+    init = str(tmp_path / "init")
+    _model().save_to_file(init)
+    g = torch.Generator().manual_seed(5)
+    xs, ys = [], []
+    for _ in range(3):
+        xs.append(torch.randn(8, 3, 12, 12, generator=g))
+        ys.append(torch.randint(0, 10, (8,), generator=g))
+    torch.cat(xs).numpy().astype(np.float32).tofile(tmp_path / "x.f32")
+    torch.cat(ys).numpy().astype(np.int64).tofile(tmp_path / "y.i64")
+
+    ref_model = _model()
+    ref = InProcessCoordinator(ref_model, Adam(2e-3), "softmax_crossentropy", num_stages=2, num_microbatches=2,
+                               transport="message")
+    ref.initialize()
+    ref.deploy_stages()
+    ref.start()
+    ref.send_parameters(ref_model)
+    ref_losses = _train(ref, 3, schedule)
+    trained = ref.gather_model()
+    ref.stop()
+
+    w = _Workers(worker_bin, 2)
+    try:
+        out = subprocess.run(
+            [COORD, "--workers", ",".join(f"127.0.0.1:{p}" for p in w.ports), "--init", init, "--schedule", schedule,
+             "--microbatches", "2", "--batch", "8", "--steps", "3", "--optimizer", "adam", "--lr", "2e-3",
+             "--data-x", str(tmp_path / "x.f32"), "--data-y", str(tmp_path / "y.i64"), "--input", "3,12,12",
+             "--json", "--save", str(tmp_path / "out")], capture_output=True, text=True, timeout=120)
+    finally:
+        w.close()
+    assert out.returncode == 0, out.stderr
+    losses = [json.loads(l)["loss"] for l in out.stdout.splitlines() if l.startswith("{")]
+    np.testing.assert_allclose(losses, ref_losses, rtol=2e-4, atol=1e-6)
+    got = Sequential.from_file(str(tmp_path / "out"))
+    for a, b in zip(got.parameters(), trained.parameters()):
+        np.testing.assert_allclose(a.detach().numpy(), b.detach().numpy(), rtol=1e-3, atol=5e-4)
+    bn_got = [l for l in got.layers if hasattr(l, "running_mean")]
+    bn_ref = [l for l in trained.layers if hasattr(l, "running_mean")]
+    assert len(bn_got) == len(bn_ref) == 1
+    np.testing.assert_allclose(bn_got[0].running_var.numpy(), bn_ref[0].running_var.numpy(), rtol=1e-4)
+
+
+@pytest.mark.gpu
+def test_native_coordinator_gpu_stages(worker_bin):
+    """All-native pipeline on the GPU: the C++ coordinator, two native GPU stages (routed MFMA
+    kernels), ResNet-9 on CIFAR-shaped synthetic data, 1F1B; the loss falls."""
+    import json
+    out = subprocess.run([COORD, "--spawn", "2", "--model", "resnet9_cifar10", "--device", "GPU:0", "--input", "3,32,32",
+                          "--classes", "10", "--batch", "64", "--microbatches", "4", "--steps", "12", "--schedule", "1f1b",
+                          "--json"], capture_output=True, text=True, timeout=240)
+    assert out.returncode == 0, out.stderr[-2000:]
+    steps = [json.loads(l) for l in out.stdout.splitlines() if l.startswith("{")]
+    assert len(steps) == 12 and all(np.isfinite(s["loss"]) for s in steps)
+    assert "GPU" in out.stderr
+    assert np.mean([s["loss"] for s in steps[-3:]]) < np.mean([s["loss"] for s in steps[:3]])
+
+
+def test_native_coordinator_rejects_bad_arguments(worker_bin):
+    out = subprocess.run([COORD, "--workers", "", "--steps", "0"], capture_output=True, text=True, timeout=30)
+    assert out.returncode == 1 and "no workers" in out.stderr
+    out = subprocess.run([COORD, "--spawn", "2", "--schedule", "zigzag", "--steps", "1"], capture_output=True,
+                         text=True, timeout=60)
+    assert out.returncode == 1 and "unknown pipeline schedule" in out.stderr
 
 
 def test_native_stage_reports_errors(worker_bin):
