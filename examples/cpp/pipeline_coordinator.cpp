@@ -59,10 +59,10 @@ std::string self_dir() {
 struct Spawned {
   pid_t pid;
   int port;
+  int out_fd;  // the worker's stdout (kept open: a later write must not raise SIGPIPE)
 };
-std::vector<Spawned> spawn_workers(int n) {
+void spawn_workers(int n, std::vector<Spawned>& out) {
   const std::string exe = self_dir() + "/network_worker";
-  std::vector<Spawned> out;
   for (int i = 0; i < n; ++i) {
     int fds[2];
     if (pipe(fds) != 0) throw std::runtime_error("pipe failed");
@@ -83,12 +83,10 @@ std::vector<Spawned> spawn_workers(int n) {
     std::string line;
     char ch;
     while (read(fds[0], &ch, 1) == 1 && ch != '\n') line.push_back(ch);
-    close(fds[0]);
     const auto at = line.find("port ");
+    out.push_back({pid, at == std::string::npos ? 0 : std::atoi(line.c_str() + at + 5), fds[0]});
     if (at == std::string::npos) throw std::runtime_error("worker did not report its port: " + line);
-    out.push_back({pid, std::atoi(line.c_str() + at + 5)});
   }
-  return out;
 }
 
 std::vector<char> read_file(const std::string& path) {
@@ -144,7 +142,7 @@ int main(int argc, char** argv) {
   try {
     std::vector<Endpoint> eps;
     if (spawn > 0) {
-      local = spawn_workers(spawn);
+      spawn_workers(spawn, local);
       for (auto& s : local) {
         Endpoint e;
         e.parameters["host"] = "127.0.0.1";
@@ -280,6 +278,7 @@ int main(int argc, char** argv) {
       kill(s.pid, SIGKILL);
       waitpid(s.pid, &st, 0);
     }
+    close(s.out_fd);
   }
   return rc;
 }

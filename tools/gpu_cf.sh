@@ -15,6 +15,7 @@ for B in 256 64; do
   timeout -k 10 240 python bench.py --batch $B --graph 0 --steps 20 --warmup 3 >> $L 2>&1 || exit $?
   timeout -k 10 300 dcnn_amd/bin/tiny_imagenet_resnet18 --device GPU --batch $B --steps 20 --bench >> $L 2>&1 || exit $?
 done
+timeout -k 10 300 dcnn_amd/bin/pipeline_coordinator --spawn 4 --model resnet50_tiny_imagenet --input 3,64,64 --classes 200 --device GPU:0 --batch 256 --microbatches 8 --schedule 1f1b --steps 8 --bench 2 >> $L 2>&1 || exit $?
 timeout -k 10 240 python bench.py --model resnet9_cifar10 --dtype fp32 --f32-mode exact --batch 128 --steps 30 --warmup 5 >> $L 2>&1 || exit $?
 timeout -k 10 240 python bench.py --model resnet18_tiny_imagenet --dtype fp32 --f32-mode exact --batch 256 --steps 20 --warmup 5 >> $L 2>&1 || exit $?
 cd /tmp && timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $R/gpurun_out/prof_f32$TAG -o run -- python3 $R/bench.py --model resnet9_cifar10 --dtype fp32 --f32-mode exact --batch 128 --steps 10 --warmup 3 > $R/gpurun_out/prof_f32$TAG.log 2>&1 || exit $?
