@@ -45,9 +45,14 @@ float bf16_to_f32(uint16_t b);
 namespace gpu {
 int device_count();
 void set_device(int dev);
+// caching allocator: freed blocks are reused by later allocations of the same size class (all
+// host API work runs on the null stream in order, so reuse is ordered after the last reader)
 void* alloc(size_t nbytes);
 void free(void* p);
+size_t cached_bytes();  // bytes held in the free lists
+void empty_cache();     // synchronise and return every cached block to the driver
 void copy(void* dst, const void* src, size_t nbytes, int kind);  // 0 h2d, 1 d2h, 2 d2d
+void zero(void* p, size_t nbytes);                                // stream-ordered memset
 void synchronize();
 }  // namespace gpu
 

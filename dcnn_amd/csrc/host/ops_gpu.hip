@@ -12,8 +12,11 @@
 #include <hip/hip_runtime.h>
 
 #include <cstring>
+#include <map>
+#include <mutex>
 #include <stdexcept>
 #include <string>
+#include <unordered_map>
 #include <vector>
 
 #include "../kernels/api.h"
@@ -29,6 +32,42 @@
 namespace dcnn {
 
 namespace gpu {
+namespace {
+// Caching device allocator: freed blocks go to a per-(device, size class) free list and are handed
+// out again instead of hipFree / hipMalloc per tensor (hipFree waits for the whole device, so a
+// step that releases its temporaries would otherwise serialise host and GPU at every op). All host
+// API work is on the null stream, in order, so a block released by the host while a queued
+// kernel still reads it is only reused by work queued after that kernel. Size classes are
+// quarter-power-of-two steps (at most 25% slack); on an out-of-memory the cached blocks are
+// released and the allocation retried.
+struct BlockPool {
+  std::mutex mu;
+  std::map<std::pair<int, size_t>, std::vector<void*>> free_blocks;
+  std::unordered_map<void*, std::pair<int, size_t>> owner;  // block -> (device, class bytes)
+  size_t cached = 0;
+};
+BlockPool& pool() {
+  static BlockPool* p = new BlockPool;  // never destroyed: tensors may outlive static teardown
+  return *p;
+}
+size_t size_class(size_t n) {
+  if (n <= 512) return 512;
+  int lg = 63 - __builtin_clzll((unsigned long long)(n - 1));  // 2^lg < n <= 2^(lg + 1)
+  const size_t step = (size_t)1 << (lg - 1);                   // quarter of 2^(lg + 1)
+  return (n + step - 1) / step * step;
+}
+void release_cached(BlockPool& bp) {
+  HOST_HIP_CHECK(hipDeviceSynchronize());
+  for (auto& kv : bp.free_blocks)
+    for (void* p : kv.second) {
+      bp.owner.erase(p);
+      (void)hipFree(p);
+    }
+  bp.free_blocks.clear();
+  bp.cached = 0;
+}
+}  // namespace
+
 int device_count() {
   int n = 0;
   if (hipGetDeviceCount(&n) != hipSuccess) return 0;
@@ -36,15 +75,57 @@ int device_count() {
 }
 void set_device(int dev) { HOST_HIP_CHECK(hipSetDevice(dev)); }
 void* alloc(size_t nbytes) {
+  int dev = 0;
+  HOST_HIP_CHECK(hipGetDevice(&dev));
+  const size_t cls = size_class(nbytes);
+  BlockPool& bp = pool();
+  std::lock_guard<std::mutex> g(bp.mu);
+  auto it = bp.free_blocks.find({dev, cls});
+  if (it != bp.free_blocks.end() && !it->second.empty()) {
+    void* p = it->second.back();
+    it->second.pop_back();
+    bp.cached -= cls;
+    return p;
+  }
   void* p = nullptr;
-  HOST_HIP_CHECK(hipMalloc(&p, nbytes));
+  if (hipMalloc(&p, cls) != hipSuccess) {
+    (void)hipGetLastError();
+    release_cached(bp);
+    HOST_HIP_CHECK(hipMalloc(&p, cls));
+  }
+  bp.owner[p] = {dev, cls};
   return p;
 }
-void free(void* p) { (void)hipFree(p); }
+void free(void* p) {
+  if (p == nullptr) return;
+  BlockPool& bp = pool();
+  std::lock_guard<std::mutex> g(bp.mu);
+  auto it = bp.owner.find(p);
+  if (it == bp.owner.end()) {
+    (void)hipFree(p);
+    return;
+  }
+  bp.free_blocks[it->second].push_back(p);
+  bp.cached += it->second.second;
+}
+size_t cached_bytes() {
+  BlockPool& bp = pool();
+  std::lock_guard<std::mutex> g(bp.mu);
+  return bp.cached;
+}
+void empty_cache() {
+  BlockPool& bp = pool();
+  std::lock_guard<std::mutex> g(bp.mu);
+  release_cached(bp);
+}
 void copy(void* dst, const void* src, size_t nbytes, int kind) {
   static const hipMemcpyKind k[] = {hipMemcpyHostToDevice, hipMemcpyDeviceToHost, hipMemcpyDeviceToDevice};
-  HOST_HIP_CHECK(hipMemcpy(dst, src, nbytes, k[kind]));
+  if (kind == 2)  // device to device: stream-ordered, the host does not wait
+    HOST_HIP_CHECK(hipMemcpyAsync(dst, src, nbytes, k[kind], nullptr));
+  else
+    HOST_HIP_CHECK(hipMemcpy(dst, src, nbytes, k[kind]));
 }
+void zero(void* p, size_t nbytes) { HOST_HIP_CHECK(hipMemsetAsync(p, 0, nbytes, nullptr)); }
 void synchronize() { HOST_HIP_CHECK(hipDeviceSynchronize()); }
 }  // namespace gpu
 

@@ -102,9 +102,8 @@ Tensor Tensor::zeros(const std::vector<int64_t>& shape, DType dt, Device dev, La
 void Tensor::zero_() {
   if (!st_) return;
   if (device().is_gpu()) {
-    std::vector<uint8_t> z(nbytes(), 0);
     gpu::set_device(device().index);
-    gpu::copy(data(), z.data(), z.size(), 0);
+    gpu::zero(data(), nbytes());
   } else {
     std::memset(data(), 0, nbytes());
   }
