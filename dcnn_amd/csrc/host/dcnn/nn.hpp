@@ -70,6 +70,12 @@ class Layer {
   // pipeline stage can hold several micro-batches in flight (semi-async, 1F1B)
   virtual void set_micro_batch(int mb) { mb_ = mb; }
   void clear_caches() { caches_.clear(); }
+  // false: backward need not produce the input gradient (the network's first layer); the layers
+  // that can skip their data-gradient GEMM (Conv2D, Dense) then return an undefined tensor
+  void set_input_grad(bool b) { input_grad_ = b; }
+  bool input_grad() const { return input_grad_; }
+  // the network input (fp32 NCHW, logical input shape `in`) is consumed as is (GPU RGB stem conv)
+  virtual bool takes_raw_input(const std::vector<int64_t>& in) const { (void)in; return false; }
 
  protected:
   struct MbCache {
@@ -81,6 +87,7 @@ class Layer {
   MbCache& mbc() { return caches_[mb_]; }
   std::map<int, MbCache> caches_;
   int mb_ = 0;
+  bool input_grad_ = true;
   Param& add_param(const std::string& n, const std::vector<int64_t>& shape, Layout phys, const std::vector<float>& init);
   std::string name_;
   Device dev_ = Device::cpu();
@@ -97,6 +104,7 @@ class Conv2D : public Layer {
   void build(const std::vector<int64_t>& in, Device dev, uint64_t seed) override;
   Tensor forward(const Tensor& x, bool training) override;
   Tensor backward(const Tensor& dy) override;
+  bool takes_raw_input(const std::vector<int64_t>& in) const override;
 
  private:
   ConvShape shape_for(const std::vector<int64_t>& in) const;

@@ -66,6 +66,11 @@ void conv_fwd(const void* x, const void* w, const float* bias, void* y, const Co
 void conv_dgrad(const void* dy, const void* w, void* dx, const ConvShape& s);
 // gw fp32 [Co][KH][KW][C] and gb fp32 [Co] accumulate (+=); gb may be null
 void conv_wgrad(const void* dy, const void* x, float* gw, float* gb, const ConvShape& s);
+// the network's first conv straight from the fp32 NCHW input (RGB stem kernel: <= 4 input
+// channels, 3x3 stride-1 'same', 16-multiple outputs up to 64); y bf16 NHWC
+bool stem_ok(const ConvShape& s);
+void stem_fwd(const float* x, const void* w, const float* bias, void* y, const ConvShape& s);
+void stem_wgrad(const void* dy, const float* x, float* gw, float* gb, const ConvShape& s);
 // w: bf16 [Out][In]
 void dense_fwd(const void* x, const void* w, const float* bias, void* y, int N, int In, int Out);
 void dense_dgrad(const void* dy, const void* w, void* dx, int N, int In, int Out);

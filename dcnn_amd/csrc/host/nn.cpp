@@ -141,6 +141,10 @@ void Conv2D::build(const std::vector<int64_t>& in, Device dev, uint64_t seed) {
   if (bias_) add_param("bias", {co_, 1, 1, 1}, Layout::NCHW, uniform_init((size_t)co_, bound, seed + 1));
 }
 
+bool Conv2D::takes_raw_input(const std::vector<int64_t>& in) const {
+  return dev_.is_gpu() && in.size() == 4 && in[1] == ci_ && gpu_ops::stem_ok(shape_for(in));
+}
+
 Tensor Conv2D::forward(const Tensor& x, bool training) {
   (void)training;
   Tensor& x_ = mbc().a;
@@ -148,6 +152,13 @@ Tensor Conv2D::forward(const Tensor& x, bool training) {
   const ConvShape s = shape_for(x.shape());
   Tensor y = act_empty({s.N, s.Co, s.OH, s.OW}, dev_);
   const float* b = bias_ ? params_[1].value.ptr<float>() : nullptr;
+  if (dev_.is_gpu() && x.dtype() == DType::F32) {
+    // the network input, fp32 NCHW, on the RGB stem kernel (Sequential::input_activation)
+    if (x.layout() != Layout::NCHW || !gpu_ops::stem_ok(s)) throw std::runtime_error(name_ + ": fp32 input");
+    gpu_ops::stem_fwd(x.ptr<float>(), params_[0].shadow.data(), b, y.data(), s);
+    x_ = x;
+    return y;
+  }
   if (dev_.is_gpu())
     gpu_ops::conv_fwd(x.data(), params_[0].shadow.data(), b, y.data(), s);
   else
@@ -159,12 +170,20 @@ Tensor Conv2D::forward(const Tensor& x, bool training) {
 Tensor Conv2D::backward(const Tensor& dy) {
   const Tensor& x_ = mbc().a;
   const ConvShape s = shape_for(x_.shape());
-  Tensor dx = act_empty(x_.shape(), dev_);
   float* gb = bias_ ? params_[1].grad.ptr<float>() : nullptr;
+  if (dev_.is_gpu() && x_.dtype() == DType::F32) {  // stem: the input needs no gradient
+    gpu_ops::stem_wgrad(dy.data(), x_.ptr<float>(), params_[0].grad.ptr<float>(), gb, s);
+    return Tensor();
+  }
   if (dev_.is_gpu()) {
     gpu_ops::conv_wgrad(dy.data(), x_.data(), params_[0].grad.ptr<float>(), gb, s);
+    if (!input_grad_) return Tensor();
+    Tensor dx = act_empty(x_.shape(), dev_);
     gpu_ops::conv_dgrad(dy.data(), params_[0].shadow.data(), dx.data(), s);
-  } else {
+    return dx;
+  }
+  Tensor dx = act_empty(x_.shape(), dev_);
+  {
     cpu_ops::conv_bwd(x_.ptr<float>(), params_[0].value.ptr<float>(), dy.ptr<float>(), dx.ptr<float>(),
                       params_[0].grad.ptr<float>(), gb, s);
   }
@@ -219,12 +238,16 @@ Tensor Dense::forward(const Tensor& x, bool training) {
 Tensor Dense::backward(const Tensor& dy) {
   const Tensor& x_ = mbc().a;
   const int N = (int)x_.dim(0);
-  Tensor dx = act_empty(x_.shape(), dev_);
   float* gb = bias_ ? params_[1].grad.ptr<float>() : nullptr;
   if (dev_.is_gpu()) {
     gpu_ops::dense_wgrad(dy.data(), x_.data(), params_[0].grad.ptr<float>(), gb, N, in_, out_);
+    if (!input_grad_) return Tensor();
+    Tensor dx = act_empty(x_.shape(), dev_);
     gpu_ops::dense_dgrad(dy.data(), params_[0].shadow.data(), dx.data(), N, in_, out_);
-  } else {
+    return dx;
+  }
+  Tensor dx = act_empty(x_.shape(), dev_);
+  {
     cpu_ops::dense_bwd(x_.ptr<float>(), params_[0].value.ptr<float>(), dy.ptr<float>(), dx.ptr<float>(),
                        params_[0].grad.ptr<float>(), gb, N, in_, out_);
   }
@@ -809,6 +832,7 @@ void Sequential::zero_grad() {
 Tensor Sequential::input_activation(const Tensor& x_in) const {
   if (x_in.rank() != 4 || x_in.dtype() != DType::F32) throw std::runtime_error("forward: expected fp32 (N, C, H, W)");
   Tensor x = x_in.device() == dev_ ? x_in : x_in.to(dev_);
+  if (dev_.is_gpu() && !layers_.empty() && layers_[0]->takes_raw_input(x.shape())) return x;  // (RGB stem)
   if (dev_.is_gpu()) {
     Tensor a = Tensor::empty(x.shape(), DType::BF16, dev_, Layout::NHWC);
     gpu_ops::input_to_nhwc(x.ptr<float>(), a.data(), (int)x.dim(0), (int)x.dim(1), (int)(x.dim(2) * x.dim(3)));
@@ -842,6 +866,7 @@ Tensor Sequential::forward(const Tensor& x_in, int mb) {
 }
 
 void Sequential::backward(const Tensor& dlogits, int mb) {
+  if (!layers_.empty()) layers_[0]->set_input_grad(false);  // (nothing consumes d loss / d input)
   Tensor g = dlogits.view({dlogits.dim(0), dlogits.dim(1), 1, 1}, dev_.is_gpu() ? Layout::NHWC : Layout::NCHW);
   backward_activation(g, mb);
 }

@@ -413,6 +413,35 @@ void conv_wgrad(const void* dy, const void* x, float* gw, float* gb, const ConvS
   wgrad_reduce(slab, gw, (long)s.Co * Ng, bslab, gb, s.Co, splits);
 }
 
+bool stem_ok(const ConvShape& s) {
+  return s.KH == 3 && s.KW == 3 && s.SH == 1 && s.SW == 1 && s.PH == 1 && s.PW == 1 &&
+         stem_supported(s.N, s.C, s.H, s.W, s.Co);
+}
+
+// weights / gradients: physical [Co][KH][KW][Ci] -> element strides of the logical (Co, Ci, ky, kx)
+void stem_fwd(const float* x, const void* w, const float* bias, void* y, const ConvShape& s) {
+  StemArgs a{};
+  a.x = x; a.w = w; a.w_bf16 = 1;
+  a.ws[0] = 9l * s.C; a.ws[1] = 1; a.ws[2] = 3l * s.C; a.ws[3] = s.C;
+  a.bias = bias; a.y = static_cast<bf16*>(y);
+  a.N = s.N; a.Ci = s.C; a.H = s.H; a.W = s.W; a.Co = s.Co;
+  dcnn::stem_fwd(a, S);
+}
+
+void stem_wgrad(const void* dy, const float* x, float* gw, float* gb, const ConvShape& s) {
+  const int blocks = stem_wgrad_blocks(s.N, s.H, s.W);
+  const long n = 9l * s.C * s.Co;
+  float* slab = static_cast<float*>(scratch(SLAB, (size_t)blocks * n * 4));
+  float* bslab = gb ? static_cast<float*>(scratch(BSLAB, (size_t)blocks * s.Co * 4)) : nullptr;
+  StemArgs a{};
+  a.x = x; a.dy = static_cast<const bf16*>(dy); a.slab = slab; a.bias_slab = bslab;
+  a.gs[0] = 9l * s.C; a.gs[1] = 1; a.gs[2] = 3l * s.C; a.gs[3] = s.C;
+  a.n_slab = n;
+  a.N = s.N; a.Ci = s.C; a.H = s.H; a.W = s.W; a.Co = s.Co;
+  dcnn::stem_wgrad(a, blocks, S);
+  wgrad_reduce(slab, gw, n, bslab, gb, s.Co, blocks);
+}
+
 void dense_fwd(const void* x, const void* w, const float* bias, void* y, int N, int In, int Out) {
   NtArgs a{static_cast<const bf16*>(x), static_cast<const bf16*>(w), y, N, Out, In, In, In, Out, kPlain, 0, 0, 0, 0,
            1, 1, 1, 1, 1, 1, 0, 0, bias, nullptr, nullptr, 0, 0};

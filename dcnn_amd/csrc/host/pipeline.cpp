@@ -273,6 +273,9 @@ void PipelineStage::configure(const std::string& text) {
   model_ = std::make_unique<Sequential>(Sequential::load_from_config(cfg_.model_config));
   model_->set_device(dev_);
   model_->initialize((uint64_t)cfg_.seed.value_or(0));
+  // the first stage's input gradient goes nowhere unless asked for: skip its data-gradient GEMM
+  if (cfg_.stage_index == 0 && !cfg_.first_layer_input_grad && !model_->layers().empty())
+    model_->layers()[0]->set_input_grad(false);
   opt_ = create_optimizer(cfg_.optimizer_config);
   out_kind_.clear();
   n_fwd_ = n_bwd_ = n_upd_ = 0;

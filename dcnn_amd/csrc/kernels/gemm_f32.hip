@@ -77,7 +77,7 @@ __global__ void __launch_bounds__(256, 2) gemm_g2f_kernel(G2Args p) {
   const int bn_row = n0 + lr;
   const bool b_ok = bn_row < p.N;
   const long b_base = (long)bn_row * p.ldb;
-  const bool vec = (p.Cs & 3) == 0;
+  const bool vec = (p.Cs & 3) == 0, uni = p.Cs % FBK == 0;
 
   auto load = [&](int k0, float4& ra, float4& rb) {
     float va[4], vb[4];
@@ -85,7 +85,10 @@ __global__ void __launch_bounds__(256, 2) gemm_g2f_kernel(G2Args p) {
     for (int e = 0; e < 4; ++e) { va[e] = 0.f; vb[e] = 0.f; }
     const int k = k0 + lc * 4;
     if (vec) {  // the 4 elements share one tap
-      const int t = k / p.Cs, c = k - t * p.Cs;
+      // (a 16-multiple channel count: the whole K block shares one tap -> wave-uniform t, a
+      // scalar division and scalar loads of the tap tables)
+      const int tu = k0 / p.Cs;
+      const int t = uni ? tu : k / p.Cs, c = uni ? k0 - tu * p.Cs + lc * 4 : k - t * p.Cs;
       if (t < p.ntaps) {
         if ((a_mask >> t) & 1ull) {
           const float4 v = *reinterpret_cast<const float4*>(A + a_base + p.tap_srcoff[t] + c);
@@ -254,7 +257,7 @@ __global__ void __launch_bounds__(256, 2) gemm_g2f_wide_kernel(G2Args p) {
     b_ok[r] = n < p.N;
     b_base[r] = (long)n * p.ldb;
   }
-  const bool vec = (p.Cs & 3) == 0;
+  const bool vec = (p.Cs & 3) == 0, uni = p.Cs % FBK == 0;
 
   auto load = [&](int k0, float4 (&ra)[AR], float4 (&rb)[BR]) {
     const int k = k0 + lc * 4;
@@ -262,8 +265,9 @@ __global__ void __launch_bounds__(256, 2) gemm_g2f_wide_kernel(G2Args p) {
     for (int r = 0; r < AR; ++r) ra[r] = make_float4(0.f, 0.f, 0.f, 0.f);
 #pragma unroll
     for (int r = 0; r < BR; ++r) rb[r] = make_float4(0.f, 0.f, 0.f, 0.f);
-    if (vec) {  // the 4 elements share one tap
-      const int t = k / p.Cs, c = k - t * p.Cs;
+    if (vec) {  // the 4 elements share one tap (16-multiple channels: wave-uniform, as above)
+      const int tu = k0 / p.Cs;
+      const int t = uni ? tu : k / p.Cs, c = uni ? k0 - tu * p.Cs + lc * 4 : k - t * p.Cs;
       if (t < p.ntaps) {
 #pragma unroll
         for (int r = 0; r < AR; ++r)
@@ -489,14 +493,21 @@ __global__ void __launch_bounds__(256, 2) gemm_t2f_kernel(T2Args p) {
   if (p.bias_slab && tn == 0 && tid < FBM && m0 + tid < p.M) p.bias_slab[(long)split * p.M + m0 + tid] = bias_acc;
 }
 
-// Wide-tile variant of gemm_t2f_kernel (128 x 128 dW tile per split, 32x32x2 MFMA; same K
-// permutation as gemm_g2f_wide_kernel): half the gathered loads per FLOP.
+// Wide-tile variant of gemm_t2f_kernel: a 128 x 128 dW tile per split on v_mfma_f32_32x32x2_f32
+// (4 waves of 64 x 64). Both operands arrive pixel-major (a pixel's dY row, a pixel's gathered X
+// row), so the LDS tiles are kept pixel-major too — [k][m] / [k][n], float4 stores along m / n
+// (conflict-free) — and every MFMA operand is one ds_read_b32: lane half h reads pixel 2s + h of
+// the 16-pixel tile, lane l32 its column. The next tile's global loads are issued right after the
+// barrier and land in registers while this tile's 32 MFMAs run (double-buffered LDS, one barrier
+// per tile); each thread's tap / channel / validity terms are fixed per column and its pixel
+// coordinates advance incrementally (no divisions in the loop).
 template <int BM, int BN>
 __global__ void __launch_bounds__(256, 2) gemm_t2f_wide_kernel(T2Args p) {
   constexpr int WM = BM / 2, WN = BN / 2, TM = WM / 32, TN = WN / 32;
   constexpr int AQ = BM / 64, BQ = BN / 64;  // float4 column groups per thread (16 threads x 4 cols per pass)
-  __shared__ __attribute__((aligned(16))) float As[BM * FPITCH];  // [m][k]
-  __shared__ __attribute__((aligned(16))) float Bs[BN * FPITCH];  // [n][k]
+  constexpr int PA = BM + 4, PB = BN + 4;    // LDS row pitch (floats)
+  __shared__ __attribute__((aligned(16))) float As[2][FBK * PA];  // [k][m]
+  __shared__ __attribute__((aligned(16))) float Bs[2][FBK * PB];  // [k][n]
   const float* dY = reinterpret_cast<const float*>(p.dY);
   const float* X = reinterpret_cast<const float*>(p.X);
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
@@ -509,7 +520,89 @@ __global__ void __launch_bounds__(256, 2) gemm_t2f_wide_kernel(T2Args p) {
   const int m0 = tm * BM, n0 = tn * BN;
   const long pbeg = (long)split * p.k_per_split;
   const long pend = pbeg + p.k_per_split < p.P ? pbeg + p.k_per_split : p.P;
-  const int lk = tid >> 4, lq = tid & 15;  // loader: pixel lk of the block, columns 4 lq + 64 r
+  const int lk = tid >> 4, lq = tid & 15;  // loader: pixel lk of the tile, columns 4 lq + 64 r
+  // per-column terms, fixed over the loop
+  bool a_vec[AQ];
+  int a_col[AQ];
+#pragma unroll
+  for (int r = 0; r < AQ; ++r) {
+    a_col[r] = m0 + lq * 4 + 64 * r;
+    a_vec[r] = (p.ldy & 3) == 0 && a_col[r] + 3 < p.M;
+  }
+  const bool b_vec = (p.Cs & 3) == 0;
+  int b_dy[BQ][4], b_dx[BQ][4], b_c[BQ][4];
+  bool b_ok[BQ][4];
+#pragma unroll
+  for (int r = 0; r < BQ; ++r)
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      const int n = n0 + lq * 4 + 64 * r + e;
+      b_ok[r][e] = n < p.N;
+      const int t = b_ok[r][e] ? n / p.Cs : 0;
+      b_c[r][e] = n - t * p.Cs;
+      b_dy[r][e] = p.tap_dy[t];
+      b_dx[r][e] = p.tap_dx[t];
+    }
+  // this thread's pixel: pbeg + lk, then + FBK per tile
+  const int ghw = p.GH * p.GW;
+  long pix = pbeg + lk;
+  int img = (int)(pix / ghw), gy, gx;
+  {
+    const int rem = (int)(pix - (long)img * ghw);
+    gy = rem / p.GW;
+    gx = rem - gy * p.GW;
+  }
+  auto advance = [&]() {
+    pix += FBK;
+    gx += FBK;
+    while (gx >= p.GW) {
+      gx -= p.GW;
+      if (++gy == p.GH) {
+        gy = 0;
+        ++img;
+      }
+    }
+  };
+  auto load = [&](float4 (&ra)[AQ], float4 (&rb)[BQ]) {
+#pragma unroll
+    for (int r = 0; r < AQ; ++r) ra[r] = make_float4(0.f, 0.f, 0.f, 0.f);
+#pragma unroll
+    for (int r = 0; r < BQ; ++r) rb[r] = make_float4(0.f, 0.f, 0.f, 0.f);
+    if (pix >= pend) return;
+#pragma unroll
+    for (int r = 0; r < AQ; ++r) {
+      const float* src = dY + pix * p.ldy + a_col[r];
+      if (a_vec[r]) {
+        ra[r] = *reinterpret_cast<const float4*>(src);
+      } else {
+        float v[4];
+#pragma unroll
+        for (int e = 0; e < 4; ++e) v[e] = a_col[r] + e < p.M ? src[e] : 0.f;
+        ra[r] = make_float4(v[0], v[1], v[2], v[3]);
+      }
+    }
+    const int y0 = gy * p.SY, x0 = gx * p.SX;
+    const long ibase = (long)img * p.H;
+#pragma unroll
+    for (int r = 0; r < BQ; ++r) {
+      if (b_vec && b_ok[r][3]) {  // the 4 columns share one tap
+        const int sy = y0 + b_dy[r][0], sx = x0 + b_dx[r][0];
+        if (sy >= 0 && sy < p.H && sx >= 0 && sx < p.W)
+          rb[r] = *reinterpret_cast<const float4*>(X + ((ibase + sy) * p.W + sx) * p.Cs + b_c[r][0]);
+      } else {
+        float v[4];
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const int sy = y0 + b_dy[r][e], sx = x0 + b_dx[r][e];
+          v[e] = (b_ok[r][e] && sy >= 0 && sy < p.H && sx >= 0 && sx < p.W)
+                     ? X[((ibase + sy) * p.W + sx) * p.Cs + b_c[r][e]]
+                     : 0.f;
+        }
+        rb[r] = make_float4(v[0], v[1], v[2], v[3]);
+      }
+    }
+  };
+
   float bias_acc = 0.f;
   f32x16 acc[TM][TN];
 #pragma unroll
@@ -518,92 +611,40 @@ __global__ void __launch_bounds__(256, 2) gemm_t2f_wide_kernel(T2Args p) {
     for (int j = 0; j < TN; ++j)
 #pragma unroll
       for (int e = 0; e < 16; ++e) acc[i][j][e] = 0.f;
-  const int ghw = p.GH * p.GW;
   const int h = lane >> 5, l32 = lane & 31;
-  for (long k0 = pbeg; k0 < pend; k0 += FBK) {
-    const long pix = k0 + lk;
-    float va[AQ][4], vb[BQ][4];
+  const int nt = (int)((pend - pbeg + FBK - 1) / FBK);
+  float4 ra[AQ], rb[BQ];
+  load(ra, rb);
+  int cur = 0;
+  for (int it = 0; it < nt; ++it) {
 #pragma unroll
-    for (int r = 0; r < AQ; ++r)
+    for (int r = 0; r < AQ; ++r) *reinterpret_cast<float4*>(&As[cur][lk * PA + lq * 4 + 64 * r]) = ra[r];
 #pragma unroll
-      for (int e = 0; e < 4; ++e) va[r][e] = 0.f;
-#pragma unroll
-    for (int r = 0; r < BQ; ++r)
-#pragma unroll
-      for (int e = 0; e < 4; ++e) vb[r][e] = 0.f;
-    if (pix < pend) {
-#pragma unroll
-      for (int r = 0; r < AQ; ++r) {
-        const int am = m0 + lq * 4 + 64 * r;
-        if ((p.ldy & 3) == 0 && am + 3 < p.M) {
-          const float4 v = *reinterpret_cast<const float4*>(dY + pix * p.ldy + am);
-          va[r][0] = v.x; va[r][1] = v.y; va[r][2] = v.z; va[r][3] = v.w;
-        } else {
-#pragma unroll
-          for (int e = 0; e < 4; ++e)
-            if (am + e < p.M) va[r][e] = dY[pix * p.ldy + am + e];
-        }
-      }
-      const int img = (int)(pix / ghw), rem = (int)(pix - (long)img * ghw);
-      const int gy = rem / p.GW, gx = rem - gy * p.GW;
-      const int y0 = gy * p.SY, x0 = gx * p.SX;
-#pragma unroll
-      for (int r = 0; r < BQ; ++r) {
-        const int bn = n0 + lq * 4 + 64 * r;
-        if ((p.Cs & 3) == 0 && bn + 3 < p.N) {
-          const int t = bn / p.Cs, c = bn - t * p.Cs;
-          const int sy = y0 + p.tap_dy[t], sx = x0 + p.tap_dx[t];
-          if (sy >= 0 && sy < p.H && sx >= 0 && sx < p.W) {
-            const float4 v = *reinterpret_cast<const float4*>(X + (((long)img * p.H + sy) * p.W + sx) * p.Cs + c);
-            vb[r][0] = v.x; vb[r][1] = v.y; vb[r][2] = v.z; vb[r][3] = v.w;
-          }
-        } else {
-#pragma unroll
-          for (int e = 0; e < 4; ++e) {
-            const int n = bn + e;
-            if (n >= p.N) continue;
-            const int t = n / p.Cs, c = n - t * p.Cs;
-            const int sy = y0 + p.tap_dy[t], sx = x0 + p.tap_dx[t];
-            if (sy >= 0 && sy < p.H && sx >= 0 && sx < p.W) vb[r][e] = X[(((long)img * p.H + sy) * p.W + sx) * p.Cs + c];
-          }
-        }
-      }
-    }
-    __syncthreads();  // previous tile fully consumed
-#pragma unroll
-    for (int r = 0; r < AQ; ++r)
-#pragma unroll
-      for (int e = 0; e < 4; ++e) As[(lq * 4 + 64 * r + e) * FPITCH + lk] = va[r][e];
-#pragma unroll
-    for (int r = 0; r < BQ; ++r)
-#pragma unroll
-      for (int e = 0; e < 4; ++e) Bs[(lq * 4 + 64 * r + e) * FPITCH + lk] = vb[r][e];
+    for (int r = 0; r < BQ; ++r) *reinterpret_cast<float4*>(&Bs[cur][lk * PB + lq * 4 + 64 * r]) = rb[r];
     __syncthreads();
+    if (it + 1 < nt) {
+      advance();
+      load(ra, rb);
+    }
     if (p.bias_slab && tn == 0 && tid < BM) {
 #pragma unroll
-      for (int k = 0; k < FBK; ++k) bias_acc += As[tid * FPITCH + k];
+      for (int k = 0; k < FBK; ++k) bias_acc += As[cur][k * PA + tid];
     }
-    float a[TM][8], b[TN][8];
+    const float* Ac = &As[cur][h * PA + wm * WM + l32];
+    const float* Bc = &Bs[cur][h * PB + wn * WN + l32];
 #pragma unroll
-    for (int i = 0; i < TM; ++i) {
-      const float* src = &As[(wm * WM + i * 32 + l32) * FPITCH + h * 8];
-      const float4 x0 = *reinterpret_cast<const float4*>(src), x1 = *reinterpret_cast<const float4*>(src + 4);
-      a[i][0] = x0.x; a[i][1] = x0.y; a[i][2] = x0.z; a[i][3] = x0.w;
-      a[i][4] = x1.x; a[i][5] = x1.y; a[i][6] = x1.z; a[i][7] = x1.w;
-    }
+    for (int s2 = 0; s2 < FBK / 2; ++s2) {
+      float a[TM], b[TN];
 #pragma unroll
-    for (int j = 0; j < TN; ++j) {
-      const float* src = &Bs[(wn * WN + j * 32 + l32) * FPITCH + h * 8];
-      const float4 x0 = *reinterpret_cast<const float4*>(src), x1 = *reinterpret_cast<const float4*>(src + 4);
-      b[j][0] = x0.x; b[j][1] = x0.y; b[j][2] = x0.z; b[j][3] = x0.w;
-      b[j][4] = x1.x; b[j][5] = x1.y; b[j][6] = x1.z; b[j][7] = x1.w;
-    }
+      for (int i = 0; i < TM; ++i) a[i] = Ac[2 * s2 * PA + i * 32];
 #pragma unroll
-    for (int s2 = 0; s2 < 8; ++s2)
+      for (int j = 0; j < TN; ++j) b[j] = Bc[2 * s2 * PB + j * 32];
 #pragma unroll
       for (int i = 0; i < TM; ++i)
 #pragma unroll
-        for (int j = 0; j < TN; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(a[i][s2], b[j][s2], acc[i][j], 0, 0, 0);
+        for (int j = 0; j < TN; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(a[i], b[j], acc[i][j], 0, 0, 0);
+    }
+    cur ^= 1;
   }
   float* out = p.slab + (long)split * p.M * p.N;
 #pragma unroll
