@@ -79,7 +79,7 @@ class Layer {
 
  protected:
   struct MbCache {
-    Tensor a, b, c;
+    Tensor a, b, c, d;
     std::vector<int64_t> shape;
     uint64_t u = 0;
     bool flag = false;
@@ -137,6 +137,9 @@ class BatchNorm : public Layer {
   void build(const std::vector<int64_t>& in, Device dev, uint64_t seed) override;
   Tensor forward(const Tensor& x, bool training) override;
   Tensor backward(const Tensor& dy) override;
+  // GPU: the following ReLU runs inside this layer's apply / backward kernels (fuse_bn_relu)
+  void set_fused_relu(bool b) { fused_relu_ = b; }
+  bool fused_relu() const { return fused_relu_; }
   Tensor running_mean, running_var;
 
  private:
@@ -144,6 +147,7 @@ class BatchNorm : public Layer {
   float eps_, momentum_;
   bool affine_;
   bool train_ = true;
+  bool fused_relu_ = false;
 };
 
 // activation kinds: relu, leaky_relu (0.01), elu (alpha 1), sigmoid, tanh, linear, softmax (over the
@@ -156,10 +160,14 @@ class Activation : public Layer {
   std::vector<int64_t> output_shape(const std::vector<int64_t>& in) const override { return in; }
   Tensor forward(const Tensor& x, bool training) override;
   Tensor backward(const Tensor& dy) override;
+  bool is_relu() const;
+  // GPU: the preceding BatchNorm applies this ReLU (fuse_bn_relu); forward / backward pass through
+  void set_passthrough(bool b) { passthrough_ = b; }
 
  private:
   std::string kind_;
   int code_;
+  bool passthrough_ = false;
 };
 
 // GroupNorm over G channel groups per image; gamma / beta per channel
@@ -252,6 +260,11 @@ class ResidualBlock : public Layer {
 
 // layer from its JSON record {"type", "name", "parameters"} (the LayerFactory of the formats)
 std::unique_ptr<Layer> create_layer(const json::Value& rec);
+
+// GPU fusion pass over a layer sequence: every BatchNorm directly followed by a ReLU applies the
+// ReLU itself (one pass instead of two forward and backward); the ReLU layer passes through.
+// `on` false undoes it (CPU placement). Sequential::initialize / ResidualBlock::build run it.
+void fuse_bn_relu(std::vector<std::unique_ptr<Layer>>& seq, bool on);
 
 class Sequential {
  public:

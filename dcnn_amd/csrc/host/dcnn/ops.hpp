@@ -76,10 +76,12 @@ void dense_fwd(const void* x, const void* w, const float* bias, void* y, int N, 
 void dense_dgrad(const void* dy, const void* w, void* dx, int N, int In, int Out);
 void dense_wgrad(const void* dy, const void* x, float* gw, float* gb, int N, int In, int Out);
 // training: batch statistics (saved mean / istd, running stats updated); eval: running stats
+// relu: y = max(bn(x), 0) in the same pass (a BatchNorm followed by a ReLU)
 void bn_fwd(const void* x, void* y, long R, int C, const float* g, const float* b, float eps, bool train,
-            float* rmean, float* rvar, float momentum, float* smean, float* sistd);
+            float* rmean, float* rvar, float momentum, float* smean, float* sistd, bool relu = false);
+// yout: the forward output of a BatchNorm + ReLU (dy is masked with yout > 0)
 void bn_bwd(const void* dy, const void* x, void* dx, long R, int C, const float* mean, const float* istd,
-            const float* g, float* dg, float* db, bool train);
+            const float* g, float* dg, float* db, bool train, const void* yout = nullptr);
 void maxpool_fwd(const void* x, void* y, uint8_t* idx, const PoolShape& p);
 void maxpool_bwd(const void* dy, const uint8_t* idx, void* dx, const PoolShape& p);
 void avgpool_fwd(const void* x, void* y, const PoolShape& p);

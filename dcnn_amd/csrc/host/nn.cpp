@@ -295,10 +295,11 @@ Tensor BatchNorm::forward(const Tensor& x, bool training) {
   Tensor y = act_empty(x.shape(), dev_);
   const float* g = affine_ ? params_[0].value.ptr<float>() : nullptr;
   const float* b = affine_ ? params_[1].value.ptr<float>() : nullptr;
-  if (dev_.is_gpu())
+  if (dev_.is_gpu()) {
     gpu_ops::bn_fwd(x.data(), y.data(), N * HW, c_, g, b, eps_, training, running_mean.ptr<float>(),
-                    running_var.ptr<float>(), momentum_, mean_.ptr<float>(), istd_.ptr<float>());
-  else
+                    running_var.ptr<float>(), momentum_, mean_.ptr<float>(), istd_.ptr<float>(), fused_relu_);
+    mc.d = fused_relu_ ? y : Tensor();  // (the ReLU mask of the backward)
+  } else
     cpu_ops::bn_fwd(x.ptr<float>(), y.ptr<float>(), N, c_, HW, g, b, eps_, training, running_mean.ptr<float>(),
                     running_var.ptr<float>(), momentum_, mean_.ptr<float>(), istd_.ptr<float>());
   x_ = x;
@@ -317,7 +318,7 @@ Tensor BatchNorm::backward(const Tensor& dy) {
   float* db = affine_ ? params_[1].grad.ptr<float>() : nullptr;
   if (dev_.is_gpu())
     gpu_ops::bn_bwd(dy.data(), x_.data(), dx.data(), N * HW, c_, mean_.ptr<float>(), istd_.ptr<float>(), g, dg, db,
-                    train_);
+                    train_, mc.d.defined() ? mc.d.data() : nullptr);
   else
     cpu_ops::bn_bwd(x_.ptr<float>(), dy.ptr<float>(), mean_.ptr<float>(), istd_.ptr<float>(), g, dx.ptr<float>(), dg,
                     db, N, c_, HW, train_);
@@ -336,8 +337,21 @@ json::Value Activation::parameters_config() const {
 
 static float act_alpha(int code) { return code == ACT_ELU ? 1.0f : 0.01f; }
 
+bool Activation::is_relu() const { return code_ == ACT_RELU; }
+
+void fuse_bn_relu(std::vector<std::unique_ptr<Layer>>& seq, bool on) {
+  for (size_t i = 0; i + 1 < seq.size(); ++i) {
+    auto* bn = dynamic_cast<BatchNorm*>(seq[i].get());
+    auto* act = dynamic_cast<Activation*>(seq[i + 1].get());
+    if (bn == nullptr || act == nullptr || !act->is_relu()) continue;
+    bn->set_fused_relu(on);
+    act->set_passthrough(on);
+  }
+}
+
 Tensor Activation::forward(const Tensor& x, bool training) {
   (void)training;
+  if (passthrough_ && dev_.is_gpu()) return x;  // (applied by the preceding BatchNorm)
   Tensor& x_ = mbc().a;
   Tensor& y_ = mbc().b;
   check_act(x, dev_, "activation");
@@ -360,6 +374,7 @@ Tensor Activation::forward(const Tensor& x, bool training) {
 }
 
 Tensor Activation::backward(const Tensor& dy) {
+  if (passthrough_ && dev_.is_gpu()) return dy;
   const Tensor& x_ = mbc().a;
   const Tensor& y_ = mbc().b;
   if (code_ == ACT_SOFTMAX) {
@@ -538,6 +553,8 @@ std::vector<int64_t> ResidualBlock::output_shape(const std::vector<int64_t>& in)
 
 void ResidualBlock::build(const std::vector<int64_t>& in, Device dev, uint64_t seed) {
   dev_ = dev;
+  fuse_bn_relu(main_, dev.is_gpu());
+  fuse_bn_relu(short_, dev.is_gpu());
   std::vector<int64_t> s = in;
   uint64_t k = 0;
   for (auto& l : main_) {
@@ -791,6 +808,7 @@ void Sequential::initialize(uint64_t seed) {
     input_chw_ = {0, 0, 0};
   }
   std::vector<int64_t> shape{1, input_chw_[0], input_chw_[1], input_chw_[2]};
+  fuse_bn_relu(layers_, dev_.is_gpu());
   uint64_t k = 0;
   for (auto& l : layers_) {
     l->build(shape, dev_, seed * 1000003ull + (k++) * 7919ull);
