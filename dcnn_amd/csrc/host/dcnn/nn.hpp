@@ -105,11 +105,15 @@ class Conv2D : public Layer {
   Tensor forward(const Tensor& x, bool training) override;
   Tensor backward(const Tensor& dy) override;
   bool takes_raw_input(const std::vector<int64_t>& in) const override;
+  // GPU: hand the output's BatchNorm statistics, computed in the conv epilogue, to `bn` (the
+  // BatchNorm that consumes this conv's output; fuse_bn_relu wires it)
+  void set_stats_consumer(class BatchNorm* bn) { stats_to_ = bn; }
 
  private:
   ConvShape shape_for(const std::vector<int64_t>& in) const;
   int ci_, co_, kh_, kw_, sh_, sw_, ph_, pw_;
   bool bias_;
+  class BatchNorm* stats_to_ = nullptr;
 };
 
 class Dense : public Layer {
@@ -140,6 +144,12 @@ class BatchNorm : public Layer {
   // GPU: the following ReLU runs inside this layer's apply / backward kernels (fuse_bn_relu)
   void set_fused_relu(bool b) { fused_relu_ = b; }
   bool fused_relu() const { return fused_relu_; }
+  // the next forward over the tensor at `x` takes its statistics from this producer slab
+  void offer_stats(const void* x, const float* slab, int rows) {
+    pending_x_ = x;
+    pending_slab_ = slab;
+    pending_rows_ = rows;
+  }
   Tensor running_mean, running_var;
 
  private:
@@ -148,6 +158,9 @@ class BatchNorm : public Layer {
   bool affine_;
   bool train_ = true;
   bool fused_relu_ = false;
+  const void* pending_x_ = nullptr;
+  const float* pending_slab_ = nullptr;
+  int pending_rows_ = 0;
 };
 
 // activation kinds: relu, leaky_relu (0.01), elu (alpha 1), sigmoid, tanh, linear, softmax (over the
@@ -262,8 +275,10 @@ class ResidualBlock : public Layer {
 std::unique_ptr<Layer> create_layer(const json::Value& rec);
 
 // GPU fusion pass over a layer sequence: every BatchNorm directly followed by a ReLU applies the
-// ReLU itself (one pass instead of two forward and backward); the ReLU layer passes through.
-// `on` false undoes it (CPU placement). Sequential::initialize / ResidualBlock::build run it.
+// ReLU itself (one pass instead of two forward and backward; the ReLU layer passes through), and
+// every conv directly followed by a BatchNorm hands it the statistics its epilogue computed (no
+// statistics pass over the conv output). `on` false undoes it (CPU placement).
+// Sequential::initialize / ResidualBlock::build run it.
 void fuse_bn_relu(std::vector<std::unique_ptr<Layer>>& seq, bool on);
 
 class Sequential {

@@ -62,14 +62,19 @@ void nchw_to_nhwc_bf16(const void* x, void* y, int N, int HW, int C);
 void cast_bf16(const float* x, void* y, long n);
 void zero(void* p, long nbytes);
 // w: bf16 [Co][KH][KW][C]; bias fp32 or null
-void conv_fwd(const void* x, const void* w, const float* bias, void* y, const ConvShape& s);
+// stat_rows != nullptr: also the BatchNorm statistics of y ([rows][3][Co] Welford triples, in a
+// workspace valid until the next conv_fwd / stem_fwd) from the conv's epilogue; returns the slab
+// and sets *stat_rows (0 and nullptr when the route has no statistics epilogue)
+const float* conv_fwd(const void* x, const void* w, const float* bias, void* y, const ConvShape& s,
+                      int* stat_rows = nullptr);
 void conv_dgrad(const void* dy, const void* w, void* dx, const ConvShape& s);
 // gw fp32 [Co][KH][KW][C] and gb fp32 [Co] accumulate (+=); gb may be null
 void conv_wgrad(const void* dy, const void* x, float* gw, float* gb, const ConvShape& s);
 // the network's first conv straight from the fp32 NCHW input (RGB stem kernel: <= 4 input
 // channels, 3x3 stride-1 'same', 16-multiple outputs up to 64); y bf16 NHWC
 bool stem_ok(const ConvShape& s);
-void stem_fwd(const float* x, const void* w, const float* bias, void* y, const ConvShape& s);
+const float* stem_fwd(const float* x, const void* w, const float* bias, void* y, const ConvShape& s,
+                      int* stat_rows = nullptr);
 void stem_wgrad(const void* dy, const float* x, float* gw, float* gb, const ConvShape& s);
 // w: bf16 [Out][In]
 void dense_fwd(const void* x, const void* w, const float* bias, void* y, int N, int In, int Out);
@@ -79,6 +84,9 @@ void dense_wgrad(const void* dy, const void* x, float* gw, float* gb, int N, int
 // relu: y = max(bn(x), 0) in the same pass (a BatchNorm followed by a ReLU)
 void bn_fwd(const void* x, void* y, long R, int C, const float* g, const float* b, float eps, bool train,
             float* rmean, float* rvar, float momentum, float* smean, float* sistd, bool relu = false);
+// training statistics from a producer's slab (conv_fwd stat_rows) instead of a pass over x
+void bn_fwd_slab(const void* x, void* y, long R, int C, const float* slab, int rows, const float* g, const float* b,
+                 float eps, float* rmean, float* rvar, float momentum, float* smean, float* sistd, bool relu);
 // yout: the forward output of a BatchNorm + ReLU (dy is masked with yout > 0)
 void bn_bwd(const void* dy, const void* x, void* dx, long R, int C, const float* mean, const float* istd,
             const float* g, float* dg, float* db, bool train, const void* yout = nullptr);

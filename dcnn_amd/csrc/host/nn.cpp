@@ -146,7 +146,6 @@ bool Conv2D::takes_raw_input(const std::vector<int64_t>& in) const {
 }
 
 Tensor Conv2D::forward(const Tensor& x, bool training) {
-  (void)training;
   Tensor& x_ = mbc().a;
   check_act(x, dev_, "conv2d");
   const ConvShape s = shape_for(x.shape());
@@ -155,13 +154,19 @@ Tensor Conv2D::forward(const Tensor& x, bool training) {
   if (dev_.is_gpu() && x.dtype() == DType::F32) {
     // the network input, fp32 NCHW, on the RGB stem kernel (Sequential::input_activation)
     if (x.layout() != Layout::NCHW || !gpu_ops::stem_ok(s)) throw std::runtime_error(name_ + ": fp32 input");
-    gpu_ops::stem_fwd(x.ptr<float>(), params_[0].shadow.data(), b, y.data(), s);
+    int rows = 0;
+    const float* st = gpu_ops::stem_fwd(x.ptr<float>(), params_[0].shadow.data(), b, y.data(), s,
+                                        stats_to_ && training ? &rows : nullptr);
+    if (stats_to_ && training) stats_to_->offer_stats(y.data(), st, rows);
     x_ = x;
     return y;
   }
-  if (dev_.is_gpu())
-    gpu_ops::conv_fwd(x.data(), params_[0].shadow.data(), b, y.data(), s);
-  else
+  if (dev_.is_gpu()) {
+    int rows = 0;
+    const float* st = gpu_ops::conv_fwd(x.data(), params_[0].shadow.data(), b, y.data(), s,
+                                        stats_to_ && training ? &rows : nullptr);
+    if (stats_to_ && training) stats_to_->offer_stats(y.data(), st, rows);
+  } else
     cpu_ops::conv_fwd(x.ptr<float>(), params_[0].value.ptr<float>(), b, y.ptr<float>(), s);
   x_ = x;
   return y;
@@ -295,13 +300,22 @@ Tensor BatchNorm::forward(const Tensor& x, bool training) {
   Tensor y = act_empty(x.shape(), dev_);
   const float* g = affine_ ? params_[0].value.ptr<float>() : nullptr;
   const float* b = affine_ ? params_[1].value.ptr<float>() : nullptr;
-  if (dev_.is_gpu()) {
+  const bool slab = dev_.is_gpu() && training && pending_x_ == x.data() && pending_slab_ && pending_rows_ > 0;
+  if (slab) {  // statistics from the producing conv's epilogue
+    gpu_ops::bn_fwd_slab(x.data(), y.data(), N * HW, c_, pending_slab_, pending_rows_, g, b, eps_,
+                         running_mean.ptr<float>(), running_var.ptr<float>(), momentum_, mean_.ptr<float>(),
+                         istd_.ptr<float>(), fused_relu_);
+    mc.d = fused_relu_ ? y : Tensor();
+  } else if (dev_.is_gpu()) {
     gpu_ops::bn_fwd(x.data(), y.data(), N * HW, c_, g, b, eps_, training, running_mean.ptr<float>(),
                     running_var.ptr<float>(), momentum_, mean_.ptr<float>(), istd_.ptr<float>(), fused_relu_);
     mc.d = fused_relu_ ? y : Tensor();  // (the ReLU mask of the backward)
   } else
     cpu_ops::bn_fwd(x.ptr<float>(), y.ptr<float>(), N, c_, HW, g, b, eps_, training, running_mean.ptr<float>(),
                     running_var.ptr<float>(), momentum_, mean_.ptr<float>(), istd_.ptr<float>());
+  pending_x_ = nullptr;
+  pending_slab_ = nullptr;
+  pending_rows_ = 0;
   x_ = x;
   return y;
 }
@@ -340,6 +354,9 @@ static float act_alpha(int code) { return code == ACT_ELU ? 1.0f : 0.01f; }
 bool Activation::is_relu() const { return code_ == ACT_RELU; }
 
 void fuse_bn_relu(std::vector<std::unique_ptr<Layer>>& seq, bool on) {
+  for (size_t i = 0; i + 1 < seq.size(); ++i)
+    if (auto* conv = dynamic_cast<Conv2D*>(seq[i].get()))
+      conv->set_stats_consumer(on ? dynamic_cast<BatchNorm*>(seq[i + 1].get()) : nullptr);
   for (size_t i = 0; i + 1 < seq.size(); ++i) {
     auto* bn = dynamic_cast<BatchNorm*>(seq[i].get());
     auto* act = dynamic_cast<Activation*>(seq[i + 1].get());

@@ -137,7 +137,7 @@ const hipStream_t S = nullptr;
 
 // grow-only workspace per purpose
 enum Slot { W_T = 0, SLAB, BSLAB, STAT_SLAB, STAT_SUMS, STAT_PART, LOSS_WS, LOSS_OUT, TICKETS, HPART, HTICKETS, GN_AFF,
-            NSLOTS };
+            FWD_STATS, NSLOTS };
 void* scratch(Slot s, size_t bytes) {
   static void* p[NSLOTS] = {};
   static size_t n[NSLOTS] = {};
@@ -260,10 +260,17 @@ void nchw_to_nhwc_bf16(const void* x, void* y, int N, int HW, int C) { transpose
 void cast_bf16(const float* x, void* y, long n) { cast_f32_bf16(x, static_cast<bf16*>(y), n, S); }
 void zero(void* p, long nbytes) { zero_bytes(p, nbytes, S); }
 
-void conv_fwd(const void* x, const void* w, const float* bias, void* y, const ConvShape& s) {
+const float* conv_fwd(const void* x, const void* w, const float* bias, void* y, const ConvShape& s, int* stat_rows) {
   const long xb = (long)s.N * s.H * s.W * s.C * 2, wb = (long)s.Co * s.KH * s.KW * s.C * 2;
+  const bool want = stat_rows != nullptr;
+  if (want) *stat_rows = 0;
+  auto slab_of = [&](int rows) {
+    *stat_rows = rows;
+    return static_cast<float*>(scratch(FWD_STATS, (size_t)rows * 3 * s.Co * 4));
+  };
+  const int M = s.N * s.OH * s.OW;
   // the shared routing table (conv_route.cpp): the same kernels as the Python front end
-  const int route = conv_fwd_route(route_geom(s, 0));
+  const int route = conv_fwd_route(route_geom(s, want ? 1 : 0));
   if (route == ROUTE_HALO && xb < (1l << 31)) {
     HConvArgs a{};
     a.A = static_cast<const bf16*>(x); a.B = static_cast<const bf16*>(w); a.C = static_cast<bf16*>(y);
@@ -273,23 +280,29 @@ void conv_fwd(const void* x, const void* w, const float* bias, void* y, const Co
       a.tap_dy[t] = t / s.KW - s.PH; a.tap_dx[t] = t % s.KW - s.PW; a.tap_b[t] = t * s.C;
     }
     a.bias = bias;
+    if (want) a.stats = slab_of(hconv_stat_rows(s.N, s.H, s.W, s.C, s.Co, a.ntaps, 0));
     hconv_workspace(a);
     hconv(a, S);
-    return;
+    return a.stats;
   }
   if (route == ROUTE_G1S) {
-    g1s(static_cast<const bf16*>(x), static_cast<const bf16*>(w), static_cast<bf16*>(y), s.N * s.OH * s.OW, s.Co, s.C,
-        s.H, s.W, s.OH, s.OW, s.SH, bias, nullptr, nullptr, 0, nullptr, 0, BnbArgs{}, 0, S);
-    return;
+    float* st = want ? slab_of(g1s_rows(M, s.Co, s.C, 1)) : nullptr;
+    g1s(static_cast<const bf16*>(x), static_cast<const bf16*>(w), static_cast<bf16*>(y), M, s.Co, s.C, s.H, s.W, s.OH,
+        s.OW, s.SH, bias, nullptr, st, 0, nullptr, 0, BnbArgs{}, want ? 1 : 0, S);
+    return st;
   }
   if (route != ROUTE_GENERIC && xb < (1l << 31) && wb < (1l << 31)) {
-    gemm_g2(g2_fwd_args(x, w, y, bias, s), S);
-    return;
+    G2Args a = g2_fwd_args(x, w, y, bias, s);
+    if (want) a.stats = slab_of(gemm_g2_stat_rows(M, s.Co));
+    gemm_g2(a, S);
+    return a.stats;
   }
   const int K = s.KH * s.KW * s.C;
-  NtArgs a{static_cast<const bf16*>(x), static_cast<const bf16*>(w), y, s.N * s.OH * s.OW, s.Co, K, 0, K, s.Co,
-           kConvFwd, s.N, s.H, s.W, s.C, s.OH, s.OW, s.KH, s.KW, s.SH, s.SW, s.PH, s.PW, bias, nullptr, nullptr, 0, 0};
+  float* st = want ? slab_of(gemm_nt_stat_rows(M, s.Co)) : nullptr;
+  NtArgs a{static_cast<const bf16*>(x), static_cast<const bf16*>(w), y, M, s.Co, K, 0, K, s.Co,
+           kConvFwd, s.N, s.H, s.W, s.C, s.OH, s.OW, s.KH, s.KW, s.SH, s.SW, s.PH, s.PW, bias, nullptr, st, 0, 0};
   gemm_nt(a, S);
+  return st;
 }
 
 void conv_dgrad(const void* dy, const void* w, void* dx, const ConvShape& s) {
@@ -419,13 +432,18 @@ bool stem_ok(const ConvShape& s) {
 }
 
 // weights / gradients: physical [Co][KH][KW][Ci] -> element strides of the logical (Co, Ci, ky, kx)
-void stem_fwd(const float* x, const void* w, const float* bias, void* y, const ConvShape& s) {
+const float* stem_fwd(const float* x, const void* w, const float* bias, void* y, const ConvShape& s, int* stat_rows) {
   StemArgs a{};
   a.x = x; a.w = w; a.w_bf16 = 1;
   a.ws[0] = 9l * s.C; a.ws[1] = 1; a.ws[2] = 3l * s.C; a.ws[3] = s.C;
   a.bias = bias; a.y = static_cast<bf16*>(y);
   a.N = s.N; a.Ci = s.C; a.H = s.H; a.W = s.W; a.Co = s.Co;
+  if (stat_rows) {
+    *stat_rows = stem_tiles_host(s.N, s.H, s.W);
+    a.slab = static_cast<float*>(scratch(FWD_STATS, (size_t)*stat_rows * 3 * s.Co * 4));
+  }
   dcnn::stem_fwd(a, S);
+  return a.slab;
 }
 
 void stem_wgrad(const void* dy, const float* x, float* gw, float* gb, const ConvShape& s) {
@@ -485,6 +503,13 @@ void bn_fwd(const void* x, void* y, long R, int C, const float* g, const float* 
   const int rows = bn_partial_rows(R, C);
   float* slab = static_cast<float*>(scratch(STAT_SLAB, (size_t)rows * 3 * C * 4));
   bn_partial(kBF16, x, nullptr, nullptr, nullptr, nullptr, nullptr, R, C, slab, 0, nullptr, S);
+  const auto st = reduce_stats(0, slab, rows, C);
+  bn_apply(kBF16, x, y, R, C, st.first, st.second, (float)R, g, b, eps, nullptr, relu ? 1 : 0, smean, sistd, rmean,
+           rvar, momentum, 0, S);
+}
+
+void bn_fwd_slab(const void* x, void* y, long R, int C, const float* slab, int rows, const float* g, const float* b,
+                 float eps, float* rmean, float* rvar, float momentum, float* smean, float* sistd, bool relu) {
   const auto st = reduce_stats(0, slab, rows, C);
   bn_apply(kBF16, x, y, R, C, st.first, st.second, (float)R, g, b, eps, nullptr, relu ? 1 : 0, smean, sistd, rmean,
            rvar, momentum, 0, S);
