@@ -144,6 +144,11 @@ class BatchNorm : public Layer {
   // GPU: the following ReLU runs inside this layer's apply / backward kernels (fuse_bn_relu)
   void set_fused_relu(bool b) { fused_relu_ = b; }
   bool fused_relu() const { return fused_relu_; }
+  // GPU: y = act(bn(x) + residual) in one pass (a residual block's tail BatchNorm, act = ReLU when
+  // `relu`), and its backward: the BatchNorm input gradient, *branch = the (masked) dy the
+  // shortcut branch receives
+  Tensor forward_residual(const Tensor& x, const Tensor& residual, bool relu, bool training);
+  Tensor backward_residual(const Tensor& dy, Tensor* branch);
   // the next forward over the tensor at `x` takes its statistics from this producer slab
   void offer_stats(const void* x, const float* slab, int rows) {
     pending_x_ = x;
@@ -158,6 +163,7 @@ class BatchNorm : public Layer {
   bool affine_;
   bool train_ = true;
   bool fused_relu_ = false;
+  Tensor forward_impl(const Tensor& x, bool training, const Tensor* residual, bool relu);
   const void* pending_x_ = nullptr;
   const float* pending_slab_ = nullptr;
   int pending_rows_ = 0;
@@ -267,6 +273,8 @@ class ResidualBlock : public Layer {
   const std::vector<std::unique_ptr<Layer>>& shortcut_path() const { return short_; }
 
  private:
+  // GPU: the main path's tail BatchNorm adds the shortcut and applies the block activation
+  class BatchNorm* fused_tail() const;
   std::vector<std::unique_ptr<Layer>> main_, short_;
   std::string act_;
 };

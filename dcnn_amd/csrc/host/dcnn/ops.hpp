@@ -81,15 +81,19 @@ void dense_fwd(const void* x, const void* w, const float* bias, void* y, int N, 
 void dense_dgrad(const void* dy, const void* w, void* dx, int N, int In, int Out);
 void dense_wgrad(const void* dy, const void* x, float* gw, float* gb, int N, int In, int Out);
 // training: batch statistics (saved mean / istd, running stats updated); eval: running stats
-// relu: y = max(bn(x), 0) in the same pass (a BatchNorm followed by a ReLU)
+// relu: y = max(bn(x) [+ residual], 0) in the same pass (a BatchNorm followed by a ReLU, or the
+// tail BatchNorm of a residual block with the shortcut added)
 void bn_fwd(const void* x, void* y, long R, int C, const float* g, const float* b, float eps, bool train,
-            float* rmean, float* rvar, float momentum, float* smean, float* sistd, bool relu = false);
+            float* rmean, float* rvar, float momentum, float* smean, float* sistd, bool relu = false,
+            const void* residual = nullptr);
 // training statistics from a producer's slab (conv_fwd stat_rows) instead of a pass over x
 void bn_fwd_slab(const void* x, void* y, long R, int C, const float* slab, int rows, const float* g, const float* b,
-                 float eps, float* rmean, float* rvar, float momentum, float* smean, float* sistd, bool relu);
-// yout: the forward output of a BatchNorm + ReLU (dy is masked with yout > 0)
+                 float eps, float* rmean, float* rvar, float momentum, float* smean, float* sistd, bool relu,
+                 const void* residual = nullptr);
+// yout: the forward output of a BatchNorm + ReLU (dy is masked with yout > 0); dy_out: the masked
+// dy is also stored there (the shortcut branch of a residual block)
 void bn_bwd(const void* dy, const void* x, void* dx, long R, int C, const float* mean, const float* istd,
-            const float* g, float* dg, float* db, bool train, const void* yout = nullptr);
+            const float* g, float* dg, float* db, bool train, const void* yout = nullptr, void* dy_out = nullptr);
 void maxpool_fwd(const void* x, void* y, uint8_t* idx, const PoolShape& p);
 void maxpool_bwd(const void* dy, const uint8_t* idx, void* dx, const PoolShape& p);
 void avgpool_fwd(const void* x, void* y, const PoolShape& p);

@@ -286,7 +286,15 @@ void BatchNorm::build(const std::vector<int64_t>& in, Device dev, uint64_t seed)
   caches_.clear();
 }
 
-Tensor BatchNorm::forward(const Tensor& x, bool training) {
+Tensor BatchNorm::forward(const Tensor& x, bool training) { return forward_impl(x, training, nullptr, fused_relu_); }
+
+Tensor BatchNorm::forward_residual(const Tensor& x, const Tensor& residual, bool relu, bool training) {
+  if (!dev_.is_gpu()) throw std::runtime_error(name_ + ": forward_residual is a GPU fusion");
+  if (residual.shape() != x.shape()) throw std::runtime_error(name_ + ": residual shape mismatch");
+  return forward_impl(x, training, &residual, relu);
+}
+
+Tensor BatchNorm::forward_impl(const Tensor& x, bool training, const Tensor* residual, bool relu) {
   check_act(x, dev_, "batchnorm");
   MbCache& mc = mbc();
   Tensor& x_ = mc.a;
@@ -300,24 +308,46 @@ Tensor BatchNorm::forward(const Tensor& x, bool training) {
   Tensor y = act_empty(x.shape(), dev_);
   const float* g = affine_ ? params_[0].value.ptr<float>() : nullptr;
   const float* b = affine_ ? params_[1].value.ptr<float>() : nullptr;
+  const void* res = residual ? residual->data() : nullptr;
   const bool slab = dev_.is_gpu() && training && pending_x_ == x.data() && pending_slab_ && pending_rows_ > 0;
   if (slab) {  // statistics from the producing conv's epilogue
     gpu_ops::bn_fwd_slab(x.data(), y.data(), N * HW, c_, pending_slab_, pending_rows_, g, b, eps_,
                          running_mean.ptr<float>(), running_var.ptr<float>(), momentum_, mean_.ptr<float>(),
-                         istd_.ptr<float>(), fused_relu_);
-    mc.d = fused_relu_ ? y : Tensor();
+                         istd_.ptr<float>(), relu, res);
+    mc.d = relu ? y : Tensor();  // (the ReLU mask of the backward)
   } else if (dev_.is_gpu()) {
     gpu_ops::bn_fwd(x.data(), y.data(), N * HW, c_, g, b, eps_, training, running_mean.ptr<float>(),
-                    running_var.ptr<float>(), momentum_, mean_.ptr<float>(), istd_.ptr<float>(), fused_relu_);
-    mc.d = fused_relu_ ? y : Tensor();  // (the ReLU mask of the backward)
-  } else
+                    running_var.ptr<float>(), momentum_, mean_.ptr<float>(), istd_.ptr<float>(), relu, res);
+    mc.d = relu ? y : Tensor();
+  } else {
     cpu_ops::bn_fwd(x.ptr<float>(), y.ptr<float>(), N, c_, HW, g, b, eps_, training, running_mean.ptr<float>(),
                     running_var.ptr<float>(), momentum_, mean_.ptr<float>(), istd_.ptr<float>());
+  }
   pending_x_ = nullptr;
   pending_slab_ = nullptr;
   pending_rows_ = 0;
   x_ = x;
   return y;
+}
+
+Tensor BatchNorm::backward_residual(const Tensor& dy, Tensor* branch) {
+  MbCache& mc = mbc();
+  const Tensor& x_ = mc.a;
+  const long N = x_.dim(0), HW = x_.dim(2) * x_.dim(3);
+  Tensor dx = act_empty(x_.shape(), dev_);
+  const float* g = affine_ ? params_[0].value.ptr<float>() : nullptr;
+  float* dg = affine_ ? params_[0].grad.ptr<float>() : nullptr;
+  float* db = affine_ ? params_[1].grad.ptr<float>() : nullptr;
+  if (mc.d.defined()) {
+    *branch = act_empty(dy.shape(), dev_);
+    gpu_ops::bn_bwd(dy.data(), x_.data(), dx.data(), N * HW, c_, mc.b.ptr<float>(), mc.c.ptr<float>(), g, dg, db,
+                    train_, mc.d.data(), branch->data());
+  } else {
+    *branch = dy;
+    gpu_ops::bn_bwd(dy.data(), x_.data(), dx.data(), N * HW, c_, mc.b.ptr<float>(), mc.c.ptr<float>(), g, dg, db,
+                    train_);
+  }
+  return dx;
 }
 
 Tensor BatchNorm::backward(const Tensor& dy) {
@@ -585,9 +615,24 @@ void ResidualBlock::build(const std::vector<int64_t>& in, Device dev, uint64_t s
   }
 }
 
+BatchNorm* ResidualBlock::fused_tail() const {
+  if (!dev_.is_gpu() || main_.size() < 2 || (act_ != "relu" && act_ != "linear")) return nullptr;
+  return dynamic_cast<BatchNorm*>(main_.back().get());
+}
+
 Tensor ResidualBlock::forward(const Tensor& x, bool training) {
   check_act(x, dev_, "residual_block");
   Tensor& y_ = mbc().a;
+  if (BatchNorm* tail = fused_tail()) {  // y = act(bn(main(x)) + shortcut(x)) in the BN's apply pass
+    Tensor sc = x;
+    for (auto& l : short_) sc = l->forward(sc, training);
+    Tensor m = x;
+    for (size_t i = 0; i + 1 < main_.size(); ++i) m = main_[i]->forward(m, training);
+    if (m.shape() != sc.shape())
+      throw std::runtime_error(name_ + ": main path " + shape_str(m.shape()) + " vs shortcut " + shape_str(sc.shape()));
+    y_ = tail->forward_residual(m, sc, act_ == "relu", training);
+    return y_;
+  }
   Tensor m = x;
   for (auto& l : main_) m = l->forward(m, training);
   Tensor sc = x;
@@ -606,6 +651,15 @@ Tensor ResidualBlock::forward(const Tensor& x, bool training) {
 
 Tensor ResidualBlock::backward(const Tensor& dy) {
   const Tensor& y_ = mbc().a;
+  if (BatchNorm* tail = fused_tail()) {
+    Tensor gs;  // the activation-masked dy, for the shortcut
+    Tensor gm = tail->backward_residual(dy, &gs);
+    for (size_t i = main_.size() - 1; i-- > 0;) gm = main_[i]->backward(gm);
+    for (size_t i = short_.size(); i-- > 0;) gs = short_[i]->backward(gs);
+    Tensor dx = act_empty(gm.shape(), dev_);
+    gpu_ops::add(gm.data(), gs.data(), dx.data(), dx.numel(), false);
+    return dx;
+  }
   Tensor g = dy;
   if (act_ == "relu") {
     g = act_empty(dy.shape(), dev_);

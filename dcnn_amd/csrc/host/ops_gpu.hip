@@ -494,9 +494,9 @@ static std::pair<const float*, int> reduce_stats(int mode, const float* slab, in
 }
 
 void bn_fwd(const void* x, void* y, long R, int C, const float* g, const float* b, float eps, bool train,
-            float* rmean, float* rvar, float momentum, float* smean, float* sistd, bool relu) {
+            float* rmean, float* rvar, float momentum, float* smean, float* sistd, bool relu, const void* residual) {
   if (!train) {
-    bn_apply(kBF16, x, y, R, C, nullptr, 1, (float)R, g, b, eps, nullptr, relu ? 1 : 0, smean, sistd, rmean, rvar,
+    bn_apply(kBF16, x, y, R, C, nullptr, 1, (float)R, g, b, eps, residual, relu ? 1 : 0, smean, sistd, rmean, rvar,
              momentum, 1, S);
     return;
   }
@@ -504,22 +504,23 @@ void bn_fwd(const void* x, void* y, long R, int C, const float* g, const float* 
   float* slab = static_cast<float*>(scratch(STAT_SLAB, (size_t)rows * 3 * C * 4));
   bn_partial(kBF16, x, nullptr, nullptr, nullptr, nullptr, nullptr, R, C, slab, 0, nullptr, S);
   const auto st = reduce_stats(0, slab, rows, C);
-  bn_apply(kBF16, x, y, R, C, st.first, st.second, (float)R, g, b, eps, nullptr, relu ? 1 : 0, smean, sistd, rmean,
+  bn_apply(kBF16, x, y, R, C, st.first, st.second, (float)R, g, b, eps, residual, relu ? 1 : 0, smean, sistd, rmean,
            rvar, momentum, 0, S);
 }
 
 void bn_fwd_slab(const void* x, void* y, long R, int C, const float* slab, int rows, const float* g, const float* b,
-                 float eps, float* rmean, float* rvar, float momentum, float* smean, float* sistd, bool relu) {
+                 float eps, float* rmean, float* rvar, float momentum, float* smean, float* sistd, bool relu,
+                 const void* residual) {
   const auto st = reduce_stats(0, slab, rows, C);
-  bn_apply(kBF16, x, y, R, C, st.first, st.second, (float)R, g, b, eps, nullptr, relu ? 1 : 0, smean, sistd, rmean,
+  bn_apply(kBF16, x, y, R, C, st.first, st.second, (float)R, g, b, eps, residual, relu ? 1 : 0, smean, sistd, rmean,
            rvar, momentum, 0, S);
 }
 
 void bn_bwd(const void* dy, const void* x, void* dx, long R, int C, const float* mean, const float* istd,
-            const float* g, float* dg, float* db, bool train, const void* yout) {
+            const float* g, float* dg, float* db, bool train, const void* yout, void* dy_out) {
   const int rows = bn_partial_rows(R, C);
   float* slab = static_cast<float*>(scratch(STAT_SLAB, (size_t)rows * 2 * C * 4));
-  bn_partial(kBF16, x, dy, yout, nullptr, mean, istd, R, C, slab, 1, nullptr, S);
+  bn_partial(kBF16, x, dy, yout, dy_out, mean, istd, R, C, slab, 1, nullptr, S);
   const auto st = reduce_stats(1, slab, rows, C);
   bn_bwd_apply(kBF16, dy, yout, x, dx, R, C, mean, istd, g, st.first, st.second, (float)R, dg, db, train ? 0 : 1, S);
 }
