@@ -108,6 +108,8 @@ class Conv2D : public Layer {
   // GPU: hand the output's BatchNorm statistics, computed in the conv epilogue, to `bn` (the
   // BatchNorm that consumes this conv's output; fuse_bn_relu wires it)
   void set_stats_consumer(class BatchNorm* bn) { stats_to_ = bn; }
+  // GPU: backward whose input gradient also adds `residual` in the data-gradient epilogue
+  Tensor backward_residual(const Tensor& dy, const Tensor& residual);
 
  private:
   ConvShape shape_for(const std::vector<int64_t>& in) const;

@@ -67,7 +67,8 @@ void zero(void* p, long nbytes);
 // and sets *stat_rows (0 and nullptr when the route has no statistics epilogue)
 const float* conv_fwd(const void* x, const void* w, const float* bias, void* y, const ConvShape& s,
                       int* stat_rows = nullptr);
-void conv_dgrad(const void* dy, const void* w, void* dx, const ConvShape& s);
+// residual: dx = dgrad + residual in the epilogue (a residual block's input gradient)
+void conv_dgrad(const void* dy, const void* w, void* dx, const ConvShape& s, const void* residual = nullptr);
 // gw fp32 [Co][KH][KW][C] and gb fp32 [Co] accumulate (+=); gb may be null
 void conv_wgrad(const void* dy, const void* x, float* gw, float* gb, const ConvShape& s);
 // the network's first conv straight from the fp32 NCHW input (RGB stem kernel: <= 4 input

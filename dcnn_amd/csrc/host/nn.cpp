@@ -195,6 +195,18 @@ Tensor Conv2D::backward(const Tensor& dy) {
   return dx;
 }
 
+Tensor Conv2D::backward_residual(const Tensor& dy, const Tensor& residual) {
+  const Tensor& x_ = mbc().a;
+  if (!dev_.is_gpu() || x_.dtype() == DType::F32 || residual.shape() != x_.shape())
+    throw std::runtime_error(name_ + ": backward_residual is a GPU fusion");
+  const ConvShape s = shape_for(x_.shape());
+  float* gb = bias_ ? params_[1].grad.ptr<float>() : nullptr;
+  gpu_ops::conv_wgrad(dy.data(), x_.data(), params_[0].grad.ptr<float>(), gb, s);
+  Tensor dx = act_empty(x_.shape(), dev_);
+  gpu_ops::conv_dgrad(dy.data(), params_[0].shadow.data(), dx.data(), s, residual.data());
+  return dx;
+}
+
 // ------------------------------------------------------------------ Dense
 Dense::Dense(int in_features, int out_features, bool bias, std::string name)
     : Layer(std::move(name)), in_(in_features), out_(out_features), bias_(bias) {}
@@ -654,8 +666,13 @@ Tensor ResidualBlock::backward(const Tensor& dy) {
   if (BatchNorm* tail = fused_tail()) {
     Tensor gs;  // the activation-masked dy, for the shortcut
     Tensor gm = tail->backward_residual(dy, &gs);
-    for (size_t i = main_.size() - 1; i-- > 0;) gm = main_[i]->backward(gm);
     for (size_t i = short_.size(); i-- > 0;) gs = short_[i]->backward(gs);
+    for (size_t i = main_.size() - 1; i-- > 1;) gm = main_[i]->backward(gm);
+    // the main path's first conv adds the shortcut gradient in its data-gradient epilogue
+    auto* head = dynamic_cast<Conv2D*>(main_[0].get());
+    if (head != nullptr && input_grad_ && gs.defined() && gs.dtype() == DType::BF16) return head->backward_residual(gm, gs);
+    gm = main_[0]->backward(gm);
+    if (!gm.defined() || !gs.defined()) return Tensor();
     Tensor dx = act_empty(gm.shape(), dev_);
     gpu_ops::add(gm.data(), gs.data(), dx.data(), dx.numel(), false);
     return dx;

@@ -305,7 +305,7 @@ const float* conv_fwd(const void* x, const void* w, const float* bias, void* y, 
   return st;
 }
 
-void conv_dgrad(const void* dy, const void* w, void* dx, const ConvShape& s) {
+void conv_dgrad(const void* dy, const void* w, void* dx, const ConvShape& s, const void* residual) {
   const int T = s.KH * s.KW, K = T * s.Co;
   bf16* wt = static_cast<bf16*>(scratch(W_T, (size_t)s.Co * T * s.C * 2));
   conv_weight_transpose(kBF16, w, wt, s.Co, T, s.C, S);  // [Co][T][C] -> [C][T][Co]
@@ -321,13 +321,14 @@ void conv_dgrad(const void* dy, const void* w, void* dx, const ConvShape& s) {
       const int ky = t / s.KW, kx = t % s.KW;
       a.tap_dy[t] = s.PH - ky; a.tap_dx[t] = s.PW - kx; a.tap_b[t] = t * s.Co;
     }
+    a.residual = static_cast<const bf16*>(residual);
     hconv_workspace(a);
     hconv(a, S);
     return;
   }
   if (route == ROUTE_G1S) {  // streaming 1x1 data gradient
     g1s(static_cast<const bf16*>(dy), wt, static_cast<bf16*>(dx), s.N * s.H * s.W, s.C, s.Co, s.H, s.W, s.H, s.W, 1,
-        nullptr, nullptr, nullptr, 0, nullptr, 0, BnbArgs{}, 0, S);
+        nullptr, static_cast<const bf16*>(residual), nullptr, 0, nullptr, 0, BnbArgs{}, 0, S);
     return;
   }
   if (route != ROUTE_GENERIC && dyb < (1l << 31) && wtb < (1l << 31)) {
@@ -367,6 +368,7 @@ void conv_dgrad(const void* dy, const void* w, void* dx, const ConvShape& s) {
       a.H = s.OH; a.W = s.OW; a.GH = cls[0].GH; a.GW = cls[0].GW; a.SY = 1; a.SX = 1;
       a.ntaps = nt; a.ldb = T * s.Co; a.ldc = s.C;
       a.OH = s.H; a.OW = s.W; a.OSY = s.SH; a.OSX = s.SW; a.ORY = cls[0].ry; a.ORX = cls[0].rx;
+      a.residual = static_cast<const bf16*>(residual);
       if (cls.size() > 1) {
         a.ncls = (int)cls.size();
         a.cls_rows = (int)rows;
@@ -379,7 +381,8 @@ void conv_dgrad(const void* dy, const void* w, void* dx, const ConvShape& s) {
     }
   }
   NtArgs a{static_cast<const bf16*>(dy), wt, dx, s.N * s.H * s.W, s.C, K, 0, K, s.C, kConvDgrad, s.N, s.OH, s.OW,
-           s.Co, s.H, s.W, s.KH, s.KW, s.SH, s.SW, s.PH, s.PW, nullptr, nullptr, nullptr, 0, 0};
+           s.Co, s.H, s.W, s.KH, s.KW, s.SH, s.SW, s.PH, s.PW, nullptr, static_cast<const bf16*>(residual), nullptr,
+           0, 0};
   gemm_nt(a, S);
 }
 
