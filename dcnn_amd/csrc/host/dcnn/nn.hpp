@@ -34,12 +34,22 @@ namespace dcnn {
 // One trainable tensor. `value` / `grad` are fp32 on the layer's device in `layout` (GPU conv
 // weights: physical [Co][KH][KW][Ci] = NHWC of the logical (Co, Ci, KH, KW)); `shadow` is the bf16
 // GEMM operand copy on the GPU. `shape` is the logical 4-D shape of the .bin record.
+struct ParamArena;
 struct Param {
   std::string name;
   std::vector<int64_t> shape;
   Layout layout = Layout::NCHW;
   Tensor value, grad, shadow;
   Tensor m, v;  // optimizer state (lazily created)
+  std::shared_ptr<ParamArena> arena;  // GPU: the flat buffers value / grad / m / v / shadow live in
+};
+
+// GPU parameter arena of a Sequential: every parameter's value, gradient, optimizer moments and
+// bf16 shadow as slices of five flat buffers (64-element aligned), so zero_grad is one memset and
+// an optimizer step one fused kernel over all `count` parameters (`n` elements, gaps stay zero)
+struct ParamArena {
+  Tensor value, grad, m, v, shadow;
+  size_t n = 0, count = 0;
 };
 
 class Layer {
@@ -338,6 +348,8 @@ class Sequential {
   Device dev_ = Device::cpu();
   bool training_ = true;
   bool initialized_ = false;
+  std::shared_ptr<ParamArena> arena_;
+  void pack_params();
 };
 
 class SequentialBuilder {

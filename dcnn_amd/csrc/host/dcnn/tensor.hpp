@@ -91,12 +91,14 @@ class Tensor {
   DType dtype() const { return dt_; }
   Device device() const { return st_ ? st_->device() : Device::cpu(); }
   Layout layout() const { return layout_; }
-  void* data() const { return st_ ? st_->data() : nullptr; }
+  void* data() const { return st_ ? static_cast<char*>(st_->data()) + off_ : nullptr; }
   template <typename T>
   T* ptr() const { return static_cast<T*>(data()); }
 
   // same storage, new logical shape / layout (element count must match)
   Tensor view(const std::vector<int64_t>& shape, Layout layout = Layout::NCHW) const;
+  // a tensor over this one's storage from byte offset `byte_off` (parameter arenas)
+  Tensor slice(size_t byte_off, const std::vector<int64_t>& shape, DType dt, Layout layout = Layout::NCHW) const;
   // grow-only: reallocate only when the new shape needs more bytes than the storage holds
   void ensure(const std::vector<int64_t>& shape, DType dt, Device dev, Layout layout = Layout::NCHW);
   Tensor clone() const;
@@ -113,6 +115,7 @@ class Tensor {
 
  private:
   std::shared_ptr<Storage> st_;
+  size_t off_ = 0;  // byte offset into st_
   std::vector<int64_t> shape_;
   DType dt_ = DType::F32;
   Layout layout_ = Layout::NCHW;

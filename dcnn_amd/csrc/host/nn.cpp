@@ -872,6 +872,53 @@ std::unique_ptr<Layer> create_layer(const json::Value& rec) {
 }
 
 // ------------------------------------------------------------------ Sequential
+namespace {
+// host fp32 values (logical order) into an existing parameter tensor's storage
+void assign_values(Tensor& dst, const std::vector<float>& v, const std::vector<int64_t>& shape, Layout layout) {
+  const Tensor h = Tensor::from_host(v, shape, Device::cpu(), DType::F32, layout);
+  if (h.nbytes() != dst.nbytes()) throw std::runtime_error("parameter size mismatch");
+  if (dst.device().is_gpu())
+    gpu::copy(dst.data(), h.data(), h.nbytes(), 0);
+  else
+    std::memcpy(dst.data(), h.data(), h.nbytes());
+}
+}  // namespace
+
+void Sequential::pack_params() {
+  arena_.reset();
+  std::vector<Param*> ps = parameters();
+  if (ps.empty() || !dev_.is_gpu()) return;
+  auto A = std::make_shared<ParamArena>();
+  std::vector<size_t> off;
+  for (Param* p : ps) {
+    off.push_back(A->n);
+    A->n += ((size_t)p->value.numel() + 63) / 64 * 64;
+  }
+  A->count = ps.size();
+  const int64_t n = (int64_t)A->n;
+  A->value = Tensor::zeros({n}, DType::F32, dev_);
+  A->grad = Tensor::zeros({n}, DType::F32, dev_);
+  A->m = Tensor::zeros({n}, DType::F32, dev_);
+  A->v = Tensor::zeros({n}, DType::F32, dev_);
+  A->shadow = Tensor::zeros({n}, DType::BF16, dev_);
+  for (size_t k = 0; k < ps.size(); ++k) {
+    Param* p = ps[k];
+    const auto& sh = p->value.shape();
+    const Layout lay = p->value.layout();
+    Tensor nv = A->value.slice(off[k] * 4, sh, DType::F32, lay);
+    gpu::copy(nv.data(), p->value.data(), p->value.nbytes(), 2);
+    p->value = nv;
+    p->grad = A->grad.slice(off[k] * 4, sh, DType::F32, lay);
+    p->m = A->m.slice(off[k] * 4, sh, DType::F32, lay);
+    p->v = A->v.slice(off[k] * 4, sh, DType::F32, lay);
+    Tensor ns = A->shadow.slice(off[k] * 2, sh, DType::BF16, lay);
+    if (p->shadow.defined()) gpu::copy(ns.data(), p->shadow.data(), p->shadow.nbytes(), 2);
+    p->shadow = ns;
+    p->arena = A;
+  }
+  arena_ = A;
+}
+
 void Sequential::set_device(Device d) {
   if (d.is_gpu() && gpu::device_count() <= d.index) throw std::runtime_error(d.str() + " not available");
   if (initialized_ && d != dev_) {
@@ -882,7 +929,7 @@ void Sequential::set_device(Device d) {
     initialized_ = false;
     initialize(0);
     size_t i = 0;
-    for (auto* p : parameters()) p->value = Tensor::from_host(vals[i++], p->shape, dev_, DType::F32, p->layout);
+    for (auto* p : parameters()) assign_values(p->value, vals[i++], p->shape, p->layout);
     for (auto& l : layers_) l->sync_shadow();
     return;
   }
@@ -902,6 +949,7 @@ void Sequential::initialize(uint64_t seed) {
     l->build(shape, dev_, seed * 1000003ull + (k++) * 7919ull);
     if (shape[1] > 0 && shape[2] > 0) shape = l->output_shape(shape);
   }
+  pack_params();
   initialized_ = true;
 }
 
@@ -927,6 +975,10 @@ size_t Sequential::num_parameters() {
 }
 
 void Sequential::zero_grad() {
+  if (arena_) {
+    gpu_ops::zero(arena_->grad.data(), (long)arena_->grad.nbytes());
+    return;
+  }
   for (auto* p : parameters()) {
     if (dev_.is_gpu())
       gpu_ops::zero(p->grad.data(), (long)p->grad.nbytes());
@@ -1055,7 +1107,7 @@ void Sequential::load_weights_file(const std::string& path) {
     if (t.numel() != p->value.numel())
       throw std::runtime_error("checkpoint tensor " + shape_str(t.shape()) + " does not match parameter " +
                                shape_str(p->shape));
-    p->value = Tensor::from_host(t.to_host_f32(), p->shape, dev_, DType::F32, p->layout);
+    assign_values(p->value, t.to_host_f32(), p->shape, p->layout);
   }
   for (auto& l : layers_) l->sync_shadow();
 }
@@ -1212,7 +1264,23 @@ LossResult softmax_cross_entropy(const Tensor& logits, const Tensor& labels_in) 
 }
 
 // ------------------------------------------------------------------ optimizers
+namespace {
+// every parameter of one arena, and nothing else: one fused update over the flat buffers
+ParamArena* whole_arena(const std::vector<Param*>& params) {
+  if (params.empty() || !params[0]->arena || params[0]->arena->count != params.size()) return nullptr;
+  ParamArena* a = params[0]->arena.get();
+  for (auto* p : params)
+    if (p->arena.get() != a) return nullptr;
+  return a;
+}
+}  // namespace
+
 void SGD::step(const std::vector<Param*>& params) {
+  if (ParamArena* a = whole_arena(params)) {
+    gpu_ops::sgd(a->value.ptr<float>(), a->grad.ptr<float>(), momentum_ != 0.f ? a->m.ptr<float>() : nullptr,
+                 a->shadow.data(), (long)a->n, lr_, momentum_);
+    return;
+  }
   for (auto* p : params) {
     if (momentum_ != 0.f && !p->m.defined()) p->m = Tensor::zeros(p->value.shape(), DType::F32, p->value.device());
     float* vel = momentum_ != 0.f ? p->m.ptr<float>() : nullptr;
@@ -1227,6 +1295,11 @@ void SGD::step(const std::vector<Param*>& params) {
 void Adam::step(const std::vector<Param*>& params) {
   ++t_;
   const float bc1 = 1.f - std::pow(b1_, (float)t_), bc2 = 1.f - std::pow(b2_, (float)t_);
+  if (ParamArena* a = whole_arena(params)) {
+    gpu_ops::adam(a->value.ptr<float>(), a->grad.ptr<float>(), a->m.ptr<float>(), a->v.ptr<float>(), a->shadow.data(),
+                  (long)a->n, lr_, b1_, b2_, eps_, bc1, bc2, wd_, decoupled_);
+    return;
+  }
   for (auto* p : params) {
     if (!p->m.defined()) {
       p->m = Tensor::zeros(p->value.shape(), DType::F32, p->value.device());

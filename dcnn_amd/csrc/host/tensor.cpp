@@ -156,11 +156,25 @@ Tensor Tensor::view(const std::vector<int64_t>& shape, Layout layout) const {
   return t;
 }
 
+Tensor Tensor::slice(size_t byte_off, const std::vector<int64_t>& shape, DType dt, Layout layout) const {
+  Tensor t;
+  t.st_ = st_;
+  t.off_ = off_ + byte_off;
+  t.shape_ = shape;
+  t.dt_ = dt;
+  t.layout_ = layout;
+  if (!st_ || t.off_ + t.nbytes() > st_->nbytes()) throw std::out_of_range("slice: outside the storage");
+  return t;
+}
+
 void Tensor::ensure(const std::vector<int64_t>& shape, DType dt, Device dev, Layout layout) {
   int64_t n = 1;
   for (auto s : shape) n *= s;
   const size_t need = (size_t)n * dtype_size(dt);
-  if (!st_ || st_->device() != dev || st_->nbytes() < need) st_ = std::make_shared<Storage>(dev, need);
+  if (!st_ || st_->device() != dev || st_->nbytes() - off_ < need) {
+    st_ = std::make_shared<Storage>(dev, need);
+    off_ = 0;
+  }
   shape_ = shape;
   dt_ = dt;
   layout_ = layout;
