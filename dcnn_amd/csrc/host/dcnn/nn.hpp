@@ -50,6 +50,13 @@ struct Param {
 struct ParamArena {
   Tensor value, grad, m, v, shadow;
   size_t n = 0, count = 0;
+  // every eligible conv's dgrad operand ([C][KH][KW][Co] bf16), regenerated from the shadows in
+  // one batched launch after each fused optimizer step (rows: src, dst, Co, T, C)
+  Tensor wt_table;
+  int n_wt = 0;
+  long wt_tiles = 0;
+  bool wt_valid = false;
+  void refresh_transposes();
 };
 
 class Layer {
@@ -120,12 +127,18 @@ class Conv2D : public Layer {
   void set_stats_consumer(class BatchNorm* bn) { stats_to_ = bn; }
   // GPU: backward whose input gradient also adds `residual` in the data-gradient epilogue
   Tensor backward_residual(const Tensor& dy, const Tensor& residual);
+  void sync_shadow() override;
+  // GPU parameter arena: allocate this conv's pre-transposed dgrad operand; the arena's batched
+  // transpose row and tile count (false: not eligible)
+  bool make_transposed_operand(std::vector<int64_t>& row, long& tiles);
 
  private:
   ConvShape shape_for(const std::vector<int64_t>& in) const;
   int ci_, co_, kh_, kw_, sh_, sw_, ph_, pw_;
   bool bias_;
   class BatchNorm* stats_to_ = nullptr;
+  Tensor wt_;  // pre-transposed dgrad operand (arena-managed)
+  const void* dgrad_operand(bool& transposed) const;
 };
 
 class Dense : public Layer {

@@ -67,8 +67,14 @@ void zero(void* p, long nbytes);
 // and sets *stat_rows (0 and nullptr when the route has no statistics epilogue)
 const float* conv_fwd(const void* x, const void* w, const float* bias, void* y, const ConvShape& s,
                       int* stat_rows = nullptr);
-// residual: dx = dgrad + residual in the epilogue (a residual block's input gradient)
-void conv_dgrad(const void* dy, const void* w, void* dx, const ConvShape& s, const void* residual = nullptr);
+// residual: dx = dgrad + residual in the epilogue (a residual block's input gradient);
+// w_transposed: w is already the [C][KH][KW][Co] dgrad operand (weight_transpose)
+void conv_dgrad(const void* dy, const void* w, void* dx, const ConvShape& s, const void* residual = nullptr,
+                bool w_transposed = false);
+// [Co][T][C] bf16 -> [C][T][Co]; the batched form takes a device table of rows
+// (src, dst, Co, T, C) and the largest 64x64-tile count per tap over the rows
+void weight_transpose(const void* w, void* wt, int Co, int T, int C);
+void multi_weight_transpose(const int64_t* table, int n, long max_tiles);
 // gw fp32 [Co][KH][KW][C] and gb fp32 [Co] accumulate (+=); gb may be null
 void conv_wgrad(const void* dy, const void* x, float* gw, float* gb, const ConvShape& s);
 // the network's first conv straight from the fp32 NCHW input (RGB stem kernel: <= 4 input

@@ -184,7 +184,9 @@ Tensor Conv2D::backward(const Tensor& dy) {
     gpu_ops::conv_wgrad(dy.data(), x_.data(), params_[0].grad.ptr<float>(), gb, s);
     if (!input_grad_) return Tensor();
     Tensor dx = act_empty(x_.shape(), dev_);
-    gpu_ops::conv_dgrad(dy.data(), params_[0].shadow.data(), dx.data(), s);
+    bool tr = false;
+    const void* w = dgrad_operand(tr);
+    gpu_ops::conv_dgrad(dy.data(), w, dx.data(), s, nullptr, tr);
     return dx;
   }
   Tensor dx = act_empty(x_.shape(), dev_);
@@ -203,8 +205,35 @@ Tensor Conv2D::backward_residual(const Tensor& dy, const Tensor& residual) {
   float* gb = bias_ ? params_[1].grad.ptr<float>() : nullptr;
   gpu_ops::conv_wgrad(dy.data(), x_.data(), params_[0].grad.ptr<float>(), gb, s);
   Tensor dx = act_empty(x_.shape(), dev_);
-  gpu_ops::conv_dgrad(dy.data(), params_[0].shadow.data(), dx.data(), s, residual.data());
+  bool tr = false;
+  const void* w = dgrad_operand(tr);
+  gpu_ops::conv_dgrad(dy.data(), w, dx.data(), s, residual.data(), tr);
   return dx;
+}
+
+bool Conv2D::make_transposed_operand(std::vector<int64_t>& row, long& tiles) {
+  if (!dev_.is_gpu() || ci_ % 8 || co_ % 8 || params_.empty()) return false;
+  wt_ = Tensor::empty({ci_, kh_, kw_, co_}, DType::BF16, dev_);
+  row = {(int64_t)(uintptr_t)params_[0].shadow.data(), (int64_t)(uintptr_t)wt_.data(), co_, kh_ * kw_, ci_};
+  tiles = (long)kh_ * kw_ * ((co_ + 63) / 64) * ((ci_ + 63) / 64);
+  return true;
+}
+
+void Conv2D::sync_shadow() {
+  Layer::sync_shadow();
+  if (wt_.defined()) gpu_ops::weight_transpose(params_[0].shadow.data(), wt_.data(), co_, kh_ * kw_, ci_);
+}
+
+const void* Conv2D::dgrad_operand(bool& transposed) const {
+  const ParamArena* a = params_[0].arena.get();
+  transposed = wt_.defined() && a != nullptr && a->wt_valid;
+  return transposed ? wt_.data() : params_[0].shadow.data();
+}
+
+void ParamArena::refresh_transposes() {
+  if (n_wt == 0) return;
+  gpu_ops::multi_weight_transpose(wt_table.ptr<int64_t>(), n_wt, wt_tiles);
+  wt_valid = true;
 }
 
 // ------------------------------------------------------------------ Dense
@@ -916,6 +945,24 @@ void Sequential::pack_params() {
     p->shadow = ns;
     p->arena = A;
   }
+  // the convs' pre-transposed dgrad operands (from the arena shadows)
+  std::vector<Layer*> all;
+  for (auto& l : layers_) l->collect_layers(all);
+  std::vector<int64_t> table;
+  for (Layer* l : all) {
+    auto* c = dynamic_cast<Conv2D*>(l);
+    std::vector<int64_t> row;
+    long tiles = 0;
+    if (c == nullptr || !c->make_transposed_operand(row, tiles)) continue;
+    table.insert(table.end(), row.begin(), row.end());
+    ++A->n_wt;
+    A->wt_tiles = std::max(A->wt_tiles, tiles);
+  }
+  if (A->n_wt) {
+    A->wt_table = Tensor::empty({(int64_t)table.size()}, DType::I64, dev_);
+    gpu::copy(A->wt_table.data(), table.data(), table.size() * 8, 0);
+    A->refresh_transposes();
+  }
   arena_ = A;
 }
 
@@ -1279,9 +1326,11 @@ void SGD::step(const std::vector<Param*>& params) {
   if (ParamArena* a = whole_arena(params)) {
     gpu_ops::sgd(a->value.ptr<float>(), a->grad.ptr<float>(), momentum_ != 0.f ? a->m.ptr<float>() : nullptr,
                  a->shadow.data(), (long)a->n, lr_, momentum_);
+    a->refresh_transposes();
     return;
   }
   for (auto* p : params) {
+    if (p->arena) p->arena->wt_valid = false;  // (the convs transpose their own operand)
     if (momentum_ != 0.f && !p->m.defined()) p->m = Tensor::zeros(p->value.shape(), DType::F32, p->value.device());
     float* vel = momentum_ != 0.f ? p->m.ptr<float>() : nullptr;
     if (p->value.device().is_gpu())
@@ -1298,9 +1347,11 @@ void Adam::step(const std::vector<Param*>& params) {
   if (ParamArena* a = whole_arena(params)) {
     gpu_ops::adam(a->value.ptr<float>(), a->grad.ptr<float>(), a->m.ptr<float>(), a->v.ptr<float>(), a->shadow.data(),
                   (long)a->n, lr_, b1_, b2_, eps_, bc1, bc2, wd_, decoupled_);
+    a->refresh_transposes();
     return;
   }
   for (auto* p : params) {
+    if (p->arena) p->arena->wt_valid = false;
     if (!p->m.defined()) {
       p->m = Tensor::zeros(p->value.shape(), DType::F32, p->value.device());
       p->v = Tensor::zeros(p->value.shape(), DType::F32, p->value.device());

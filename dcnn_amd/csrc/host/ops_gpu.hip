@@ -305,10 +305,22 @@ const float* conv_fwd(const void* x, const void* w, const float* bias, void* y, 
   return st;
 }
 
-void conv_dgrad(const void* dy, const void* w, void* dx, const ConvShape& s, const void* residual) {
+void weight_transpose(const void* w, void* wt, int Co, int T, int C) {
+  conv_weight_transpose(kBF16, w, static_cast<bf16*>(wt), Co, T, C, S);
+}
+void multi_weight_transpose(const int64_t* table, int n, long max_tiles) {
+  dcnn::multi_weight_transpose(table, n, max_tiles, S);
+}
+
+void conv_dgrad(const void* dy, const void* w, void* dx, const ConvShape& s, const void* residual,
+                bool w_transposed) {
   const int T = s.KH * s.KW, K = T * s.Co;
-  bf16* wt = static_cast<bf16*>(scratch(W_T, (size_t)s.Co * T * s.C * 2));
-  conv_weight_transpose(kBF16, w, wt, s.Co, T, s.C, S);  // [Co][T][C] -> [C][T][Co]
+  const bf16* wt = static_cast<const bf16*>(w);
+  if (!w_transposed) {
+    bf16* t = static_cast<bf16*>(scratch(W_T, (size_t)s.Co * T * s.C * 2));
+    conv_weight_transpose(kBF16, w, t, s.Co, T, s.C, S);  // [Co][T][C] -> [C][T][Co]
+    wt = t;
+  }
   const long dyb = (long)s.N * s.OH * s.OW * s.Co * 2, wtb = (long)s.C * T * s.Co * 2;
   const int route = conv_dgrad_route(route_geom(s, 0));  // shared routing table (conv_route.cpp)
   if (route == ROUTE_HALO && dyb < (1l << 31)) {
