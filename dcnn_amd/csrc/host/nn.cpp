@@ -1058,10 +1058,18 @@ Tensor Sequential::forward_activation(const Tensor& x_in, int mb) {
 
 Tensor Sequential::backward_activation(const Tensor& g_in, int mb) {
   Tensor g = g_in;
-  for (size_t i = layers_.size(); i-- > 0;) {
-    layers_[i]->set_micro_batch(mb);
-    g = layers_[i]->backward(g);
+  const bool defer = dev_.is_gpu();
+  if (defer) gpu_ops::begin_deferred_reduce();
+  try {
+    for (size_t i = layers_.size(); i-- > 0;) {
+      layers_[i]->set_micro_batch(mb);
+      g = layers_[i]->backward(g);
+    }
+  } catch (...) {
+    if (defer) gpu_ops::end_deferred_reduce();
+    throw;
   }
+  if (defer) gpu_ops::end_deferred_reduce();  // every weight gradient final before the optimizer
   return g;
 }
 

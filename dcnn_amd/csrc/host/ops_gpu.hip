@@ -11,6 +11,7 @@
 // the null stream in order; workspaces are grow-only device buffers reused across calls.
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
 #include <cstring>
 #include <map>
 #include <mutex>
@@ -246,13 +247,58 @@ ConvRouteGeom route_geom(const ConvShape& s, int g1s_mode) {
   return ConvRouteGeom{s.N, s.C, s.H, s.W, s.Co, s.KH, s.KW, s.SH, s.SW, s.PH, s.PW, s.OH, s.OW, g1s_mode};
 }
 
-void wgrad_reduce(const float* slab, float* gw, long n, const float* bslab, float* gb, long nb, int splits) {
+// Weight-gradient split-K partials: while a backward is open (begin/end_deferred_reduce) every
+// slab is a buffer of its own, queued, and summed into its gradient by ONE batched launch at the
+// end of the backward (multi_splitk_reduce, kMaxRed slabs per launch) instead of one reduce per
+// layer; outside it, the shared workspace and an immediate reduce.
+struct PendingRed {
+  Tensor slab;
+  float* out;
+  long n;
+  int splits;
+};
+std::vector<PendingRed> g_pending;
+bool g_defer = false;
+
+float* wgrad_slab(Slot slot, size_t bytes, Tensor& hold) {
+  if (!g_defer) return static_cast<float*>(scratch(slot, bytes));
+  int dev = 0;
+  HOST_HIP_CHECK(hipGetDevice(&dev));
+  hold = Tensor::empty({(int64_t)((bytes + 3) / 4)}, DType::F32, Device::gpu(dev));
+  return hold.ptr<float>();
+}
+
+void wgrad_reduce(const Tensor& hold, const Tensor& bhold, const float* slab, float* gw, long n, const float* bslab,
+                  float* gb, long nb, int splits) {
+  if (g_defer) {
+    g_pending.push_back({hold, gw, n, splits});
+    if (gb) g_pending.push_back({bhold, gb, nb, splits});
+    return;
+  }
   if (gb)
     splitk_reduce2(slab, gw, n, bslab, gb, nb, splits, 1, S);
   else
     splitk_reduce(slab, gw, n, splits, 1, S);
 }
 }  // namespace
+
+void begin_deferred_reduce() { g_defer = true; }
+void end_deferred_reduce() {
+  for (size_t b = 0; b < g_pending.size(); b += kMaxRed) {
+    MultiRed t{};
+    t.count = (int)std::min(g_pending.size() - b, (size_t)kMaxRed);
+    for (int k = 0; k < t.count; ++k) {
+      const PendingRed& e = g_pending[b + k];
+      t.e[k].slab = e.slab.ptr<float>();
+      t.e[k].out = e.out;
+      t.e[k].n = e.n;
+      t.e[k].splits = e.splits;
+    }
+    multi_splitk_reduce(t, S);
+  }
+  g_pending.clear();  // (the slabs return to the caching allocator, reused only by later work)
+  g_defer = false;
+}
 
 void input_to_nhwc(const float* x, void* y, int N, int C, int HW) { nchw_to_nhwc(kBF16, x, y, N, C, HW, S); }
 void nhwc_to_nchw(const void* x, void* y, int N, int HW, int C) { transpose16(x, y, N, HW, C); }
@@ -404,21 +450,23 @@ void conv_wgrad(const void* dy, const void* x, float* gw, float* gb, const ConvS
   const int route = conv_wgrad_route(route_geom(s, -1));  // shared routing table (conv_route.cpp)
   if (route == ROUTE_HALO) {
     const int splits = hwgrad_splits(s.N, s.H, s.W, s.C, s.Co);
-    float* slab = static_cast<float*>(scratch(SLAB, (size_t)splits * s.Co * Ng * 4));
-    float* bslab = gb ? static_cast<float*>(scratch(BSLAB, (size_t)splits * s.Co * 4)) : nullptr;
+    Tensor hold, bhold;
+    float* slab = wgrad_slab(SLAB, (size_t)splits * s.Co * Ng * 4, hold);
+    float* bslab = gb ? wgrad_slab(BSLAB, (size_t)splits * s.Co * 4, bhold) : nullptr;
     HWArgs a{};
     a.dY = static_cast<const bf16*>(dy); a.X = static_cast<const bf16*>(x); a.slab = slab; a.bias_slab = bslab;
     a.dy_bytes = (unsigned)dyb; a.x_bytes = (unsigned)xb;
     a.NB = s.N; a.H = s.H; a.W = s.W; a.Cs = s.C; a.Co = s.Co; a.ntaps = 9;
     for (int t = 0; t < 9; ++t) { a.tap_dy[t] = t / 3 - 1; a.tap_dx[t] = t % 3 - 1; }
     hwgrad(a, splits, S);
-    wgrad_reduce(slab, gw, (long)s.Co * Ng, bslab, gb, s.Co, splits);
+    wgrad_reduce(hold, bhold, slab, gw, (long)s.Co * Ng, bslab, gb, s.Co, splits);
     return;
   }
   if (route == ROUTE_GEMM_G2 && dyb < (1l << 31) && xb < (1l << 31) && P < (1 << 24)) {
     const int splits = gemm_t2_splits(s.Co, Ng, P);
-    float* slab = static_cast<float*>(scratch(SLAB, (size_t)splits * s.Co * Ng * 4));
-    float* bslab = gb ? static_cast<float*>(scratch(BSLAB, (size_t)splits * s.Co * 4)) : nullptr;
+    Tensor hold, bhold;
+    float* slab = wgrad_slab(SLAB, (size_t)splits * s.Co * Ng * 4, hold);
+    float* bslab = gb ? wgrad_slab(BSLAB, (size_t)splits * s.Co * 4, bhold) : nullptr;
     T2Args a{};
     a.dY = static_cast<const bf16*>(dy); a.X = static_cast<const bf16*>(x); a.slab = slab; a.bias_slab = bslab;
     a.a_bytes = (unsigned)dyb; a.b_bytes = (unsigned)xb;
@@ -429,16 +477,17 @@ void conv_wgrad(const void* dy, const void* x, float* gw, float* gb, const ConvS
       for (int kx = 0; kx < s.KW; ++kx, ++t) { a.tap_dy[t] = ky - s.PH; a.tap_dx[t] = kx - s.PW; }
     a.ntaps = t;
     gemm_t2(a, splits, S);
-    wgrad_reduce(slab, gw, (long)s.Co * Ng, bslab, gb, s.Co, splits);
+    wgrad_reduce(hold, bhold, slab, gw, (long)s.Co * Ng, bslab, gb, s.Co, splits);
     return;
   }
   const int splits = gemm_tn_splits(s.Co, Ng, P);
-  float* slab = static_cast<float*>(scratch(SLAB, (size_t)splits * s.Co * Ng * 4));
-  float* bslab = gb ? static_cast<float*>(scratch(BSLAB, (size_t)splits * s.Co * 4)) : nullptr;
+  Tensor hold, bhold;
+  float* slab = wgrad_slab(SLAB, (size_t)splits * s.Co * Ng * 4, hold);
+  float* bslab = gb ? wgrad_slab(BSLAB, (size_t)splits * s.Co * 4, bhold) : nullptr;
   TnArgs a{static_cast<const bf16*>(dy), static_cast<const bf16*>(x), slab, bslab, s.Co, Ng, P, kConvFwd, s.N, s.H,
            s.W, s.C, s.OH, s.OW, s.KH, s.KW, s.SH, s.SW, s.PH, s.PW, 0, 0};
   gemm_tn(a, splits, S);
-  wgrad_reduce(slab, gw, (long)s.Co * Ng, bslab, gb, s.Co, splits);
+  wgrad_reduce(hold, bhold, slab, gw, (long)s.Co * Ng, bslab, gb, s.Co, splits);
 }
 
 bool stem_ok(const ConvShape& s) {
@@ -464,15 +513,16 @@ const float* stem_fwd(const float* x, const void* w, const float* bias, void* y,
 void stem_wgrad(const void* dy, const float* x, float* gw, float* gb, const ConvShape& s) {
   const int blocks = stem_wgrad_blocks(s.N, s.H, s.W);
   const long n = 9l * s.C * s.Co;
-  float* slab = static_cast<float*>(scratch(SLAB, (size_t)blocks * n * 4));
-  float* bslab = gb ? static_cast<float*>(scratch(BSLAB, (size_t)blocks * s.Co * 4)) : nullptr;
+  Tensor hold, bhold;
+  float* slab = wgrad_slab(SLAB, (size_t)blocks * n * 4, hold);
+  float* bslab = gb ? wgrad_slab(BSLAB, (size_t)blocks * s.Co * 4, bhold) : nullptr;
   StemArgs a{};
   a.x = x; a.dy = static_cast<const bf16*>(dy); a.slab = slab; a.bias_slab = bslab;
   a.gs[0] = 9l * s.C; a.gs[1] = 1; a.gs[2] = 3l * s.C; a.gs[3] = s.C;
   a.n_slab = n;
   a.N = s.N; a.Ci = s.C; a.H = s.H; a.W = s.W; a.Co = s.Co;
   dcnn::stem_wgrad(a, blocks, S);
-  wgrad_reduce(slab, gw, n, bslab, gb, s.Co, blocks);
+  wgrad_reduce(hold, bhold, slab, gw, n, bslab, gb, s.Co, blocks);
 }
 
 void dense_fwd(const void* x, const void* w, const float* bias, void* y, int N, int In, int Out) {
@@ -491,12 +541,13 @@ void dense_dgrad(const void* dy, const void* w, void* dx, int N, int In, int Out
 
 void dense_wgrad(const void* dy, const void* x, float* gw, float* gb, int N, int In, int Out) {
   const int splits = gemm_tn_splits(Out, In, N);
-  float* slab = static_cast<float*>(scratch(SLAB, (size_t)splits * Out * In * 4));
-  float* bslab = gb ? static_cast<float*>(scratch(BSLAB, (size_t)splits * Out * 4)) : nullptr;
+  Tensor hold, bhold;
+  float* slab = wgrad_slab(SLAB, (size_t)splits * Out * In * 4, hold);
+  float* bslab = gb ? wgrad_slab(BSLAB, (size_t)splits * Out * 4, bhold) : nullptr;
   TnArgs a{static_cast<const bf16*>(dy), static_cast<const bf16*>(x), slab, bslab, Out, In, N, kPlain, 0, 0, 0, 0, 1,
            1, 1, 1, 1, 1, 0, 0, In, 0};
   gemm_tn(a, splits, S);
-  wgrad_reduce(slab, gw, (long)Out * In, bslab, gb, Out, splits);
+  wgrad_reduce(hold, bhold, slab, gw, (long)Out * In, bslab, gb, Out, splits);
 }
 
 // deterministic slab statistics: (pointer, parts) for bn_apply / bn_bwd_apply
