@@ -125,6 +125,9 @@ class Conv2D : public Layer {
   // GPU: hand the output's BatchNorm statistics, computed in the conv epilogue, to `bn` (the
   // BatchNorm that consumes this conv's output; fuse_bn_relu wires it)
   void set_stats_consumer(class BatchNorm* bn) { stats_to_ = bn; }
+  // GPU: the BatchNorm (+ ReLU) producing this conv's input; the data gradient's epilogue applies
+  // its ReLU mask and computes its backward statistics (fuse_bn_relu wires it)
+  void set_bnb_producer(class BatchNorm* bn) { bnb_from_ = bn; }
   // GPU: backward whose input gradient also adds `residual` in the data-gradient epilogue
   Tensor backward_residual(const Tensor& dy, const Tensor& residual);
   void sync_shadow() override;
@@ -137,6 +140,7 @@ class Conv2D : public Layer {
   int ci_, co_, kh_, kw_, sh_, sw_, ph_, pw_;
   bool bias_;
   class BatchNorm* stats_to_ = nullptr;
+  class BatchNorm* bnb_from_ = nullptr;
   Tensor wt_;  // pre-transposed dgrad operand (arena-managed)
   const void* dgrad_operand(bool& transposed) const;
 };
@@ -174,6 +178,15 @@ class BatchNorm : public Layer {
   // shortcut branch receives
   Tensor forward_residual(const Tensor& x, const Tensor& residual, bool relu, bool training);
   Tensor backward_residual(const Tensor& dy, Tensor* branch);
+  // backward-fusion operands of micro-batch `mb` (its forward's input, output mask, statistics)
+  gpu_ops::BnbOperands bnb_operands(int mb);
+  // the next backward over the gradient at `dy` takes its statistics from this consumer slab (the
+  // gradient is already masked)
+  void offer_bwd_stats(const void* dy, const float* slab, int rows) {
+    bwd_dy_ = dy;
+    bwd_slab_ = slab;
+    bwd_rows_ = rows;
+  }
   // the next forward over the tensor at `x` takes its statistics from this producer slab
   void offer_stats(const void* x, const float* slab, int rows) {
     pending_x_ = x;
@@ -189,6 +202,9 @@ class BatchNorm : public Layer {
   bool train_ = true;
   bool fused_relu_ = false;
   Tensor forward_impl(const Tensor& x, bool training, const Tensor* residual, bool relu);
+  const void* bwd_dy_ = nullptr;
+  const float* bwd_slab_ = nullptr;
+  int bwd_rows_ = 0;
   const void* pending_x_ = nullptr;
   const float* pending_slab_ = nullptr;
   int pending_rows_ = 0;

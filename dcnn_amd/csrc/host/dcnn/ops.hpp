@@ -70,10 +70,20 @@ void zero(void* p, long nbytes);
 // and sets *stat_rows (0 and nullptr when the route has no statistics epilogue)
 const float* conv_fwd(const void* x, const void* w, const float* bias, void* y, const ConvShape& s,
                       int* stat_rows = nullptr);
+// operands of the BatchNorm (+ ReLU) that produced a conv's input
+struct BnbOperands {
+  const void* y;  // the BN + ReLU output (ReLU mask; null: no ReLU)
+  const void* x;  // the BN input
+  const float* mean;
+  const float* istd;
+};
 // residual: dx = dgrad + residual in the epilogue (a residual block's input gradient);
-// w_transposed: w is already the [C][KH][KW][Co] dgrad operand (weight_transpose)
-void conv_dgrad(const void* dy, const void* w, void* dx, const ConvShape& s, const void* residual = nullptr,
-                bool w_transposed = false);
+// w_transposed: w is already the [C][KH][KW][Co] dgrad operand (weight_transpose);
+// bnb: the epilogue also masks dx with y > 0 and writes the producing BatchNorm's backward
+// statistics ([rows][2][C] sums of dx' and dx' * xhat) — returns that slab (valid until the next
+// conv_dgrad) and sets *bnb_rows; 0 / nullptr when the route has no such epilogue (dx is plain)
+const float* conv_dgrad(const void* dy, const void* w, void* dx, const ConvShape& s, const void* residual = nullptr,
+                        bool w_transposed = false, const BnbOperands* bnb = nullptr, int* bnb_rows = nullptr);
 // [Co][T][C] bf16 -> [C][T][Co]; the batched form takes a device table of rows
 // (src, dst, Co, T, C) and the largest 64x64-tile count per tap over the rows
 void weight_transpose(const void* w, void* wt, int Co, int T, int C);
@@ -100,6 +110,9 @@ void bn_fwd(const void* x, void* y, long R, int C, const float* g, const float* 
 void bn_fwd_slab(const void* x, void* y, long R, int C, const float* slab, int rows, const float* g, const float* b,
                  float eps, float* rmean, float* rvar, float momentum, float* smean, float* sistd, bool relu,
                  const void* residual = nullptr);
+// backward from a consumer's statistics slab (conv_dgrad bnb: dy already masked)
+void bn_bwd_slab(const void* dy, const void* x, void* dx, long R, int C, const float* mean, const float* istd,
+                 const float* g, float* dg, float* db, bool train, const float* slab, int rows);
 // yout: the forward output of a BatchNorm + ReLU (dy is masked with yout > 0); dy_out: the masked
 // dy is also stored there (the shortcut branch of a residual block)
 void bn_bwd(const void* dy, const void* x, void* dx, long R, int C, const float* mean, const float* istd,

@@ -186,6 +186,13 @@ Tensor Conv2D::backward(const Tensor& dy) {
     Tensor dx = act_empty(x_.shape(), dev_);
     bool tr = false;
     const void* w = dgrad_operand(tr);
+    if (bnb_from_ != nullptr) {
+      const gpu_ops::BnbOperands ops = bnb_from_->bnb_operands(mb_);
+      int rows = 0;
+      const float* st = gpu_ops::conv_dgrad(dy.data(), w, dx.data(), s, nullptr, tr, &ops, &rows);
+      if (rows > 0) bnb_from_->offer_bwd_stats(dx.data(), st, rows);
+      return dx;
+    }
     gpu_ops::conv_dgrad(dy.data(), w, dx.data(), s, nullptr, tr);
     return dx;
   }
@@ -209,6 +216,13 @@ Tensor Conv2D::backward_residual(const Tensor& dy, const Tensor& residual) {
   const void* w = dgrad_operand(tr);
   gpu_ops::conv_dgrad(dy.data(), w, dx.data(), s, residual.data(), tr);
   return dx;
+}
+
+gpu_ops::BnbOperands BatchNorm::bnb_operands(int mb) {
+  set_micro_batch(mb);
+  MbCache& mc = mbc();
+  return gpu_ops::BnbOperands{mc.d.defined() ? mc.d.data() : nullptr, mc.a.data(), mc.b.ptr<float>(),
+                              mc.c.ptr<float>()};
 }
 
 bool Conv2D::make_transposed_operand(std::vector<int64_t>& row, long& tiles) {
@@ -401,7 +415,14 @@ Tensor BatchNorm::backward(const Tensor& dy) {
   const float* g = affine_ ? params_[0].value.ptr<float>() : nullptr;
   float* dg = affine_ ? params_[0].grad.ptr<float>() : nullptr;
   float* db = affine_ ? params_[1].grad.ptr<float>() : nullptr;
-  if (dev_.is_gpu())
+  if (dev_.is_gpu() && bwd_dy_ == dy.data() && bwd_slab_ != nullptr && bwd_rows_ > 0) {
+    // statistics (and the ReLU mask) from the consuming conv's data-gradient epilogue
+    gpu_ops::bn_bwd_slab(dy.data(), x_.data(), dx.data(), N * HW, c_, mean_.ptr<float>(), istd_.ptr<float>(), g, dg,
+                         db, train_, bwd_slab_, bwd_rows_);
+    bwd_dy_ = nullptr;
+    bwd_slab_ = nullptr;
+    bwd_rows_ = 0;
+  } else if (dev_.is_gpu())
     gpu_ops::bn_bwd(dy.data(), x_.data(), dx.data(), N * HW, c_, mean_.ptr<float>(), istd_.ptr<float>(), g, dg, db,
                     train_, mc.d.defined() ? mc.d.data() : nullptr);
   else
@@ -428,6 +449,16 @@ void fuse_bn_relu(std::vector<std::unique_ptr<Layer>>& seq, bool on) {
   for (size_t i = 0; i + 1 < seq.size(); ++i)
     if (auto* conv = dynamic_cast<Conv2D*>(seq[i].get()))
       conv->set_stats_consumer(on ? dynamic_cast<BatchNorm*>(seq[i + 1].get()) : nullptr);
+  // BatchNorm [+ ReLU] -> Conv2D: the conv's data gradient carries the BN backward epilogue
+  for (size_t i = 0; i + 1 < seq.size(); ++i) {
+    auto* bn = dynamic_cast<BatchNorm*>(seq[i].get());
+    if (bn == nullptr) continue;
+    size_t j = i + 1;
+    auto* act = dynamic_cast<Activation*>(seq[j].get());
+    if (act != nullptr && act->is_relu() && j + 1 < seq.size()) ++j;
+    else if (act != nullptr) continue;
+    if (auto* conv = dynamic_cast<Conv2D*>(seq[j].get())) conv->set_bnb_producer(on ? bn : nullptr);
+  }
   for (size_t i = 0; i + 1 < seq.size(); ++i) {
     auto* bn = dynamic_cast<BatchNorm*>(seq[i].get());
     auto* act = dynamic_cast<Activation*>(seq[i + 1].get());

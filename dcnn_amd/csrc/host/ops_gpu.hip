@@ -138,7 +138,7 @@ const hipStream_t S = nullptr;
 
 // grow-only workspace per purpose
 enum Slot { W_T = 0, SLAB, BSLAB, STAT_SLAB, STAT_SUMS, STAT_PART, LOSS_WS, LOSS_OUT, TICKETS, HPART, HTICKETS, GN_AFF,
-            FWD_STATS, NSLOTS };
+            FWD_STATS, BWD_STATS, NSLOTS };
 void* scratch(Slot s, size_t bytes) {
   static void* p[NSLOTS] = {};
   static size_t n[NSLOTS] = {};
@@ -358,9 +358,21 @@ void multi_weight_transpose(const int64_t* table, int n, long max_tiles) {
   dcnn::multi_weight_transpose(table, n, max_tiles, S);
 }
 
-void conv_dgrad(const void* dy, const void* w, void* dx, const ConvShape& s, const void* residual,
-                bool w_transposed) {
+const float* conv_dgrad(const void* dy, const void* w, void* dx, const ConvShape& s, const void* residual,
+                        bool w_transposed, const BnbOperands* bnb, int* bnb_rows) {
   const int T = s.KH * s.KW, K = T * s.Co;
+  if (bnb_rows) *bnb_rows = 0;
+  BnbArgs ba{};
+  if (bnb) {
+    ba.y = static_cast<const bf16*>(bnb->y);
+    ba.x = static_cast<const bf16*>(bnb->x);
+    ba.mean = bnb->mean;
+    ba.istd = bnb->istd;
+  }
+  auto slab_of = [&](int rows) {
+    *bnb_rows = rows;
+    return static_cast<float*>(scratch(BWD_STATS, (size_t)rows * 2 * s.C * 4));
+  };
   const bf16* wt = static_cast<const bf16*>(w);
   if (!w_transposed) {
     bf16* t = static_cast<bf16*>(scratch(W_T, (size_t)s.Co * T * s.C * 2));
@@ -368,7 +380,8 @@ void conv_dgrad(const void* dy, const void* w, void* dx, const ConvShape& s, con
     wt = t;
   }
   const long dyb = (long)s.N * s.OH * s.OW * s.Co * 2, wtb = (long)s.C * T * s.Co * 2;
-  const int route = conv_dgrad_route(route_geom(s, 0));  // shared routing table (conv_route.cpp)
+  // shared routing table (conv_route.cpp); g1s mode 2: the streaming dgrad with the BN epilogue
+  const int route = conv_dgrad_route(route_geom(s, bnb ? 2 : 0));
   if (route == ROUTE_HALO && dyb < (1l << 31)) {
     // transposed conv of a stride-1 'same' conv: tap (ky, kx) reads dy at (PH - ky, PW - kx)
     HConvArgs a{};
@@ -380,14 +393,20 @@ void conv_dgrad(const void* dy, const void* w, void* dx, const ConvShape& s, con
       a.tap_dy[t] = s.PH - ky; a.tap_dx[t] = s.PW - kx; a.tap_b[t] = t * s.Co;
     }
     a.residual = static_cast<const bf16*>(residual);
+    if (bnb) {
+      a.bnb = ba;
+      a.stats = slab_of(hconv_stat_rows(s.N, s.OH, s.OW, s.Co, s.C, T, 0));
+    }
     hconv_workspace(a);
     hconv(a, S);
-    return;
+    return a.stats;
   }
   if (route == ROUTE_G1S) {  // streaming 1x1 data gradient
-    g1s(static_cast<const bf16*>(dy), wt, static_cast<bf16*>(dx), s.N * s.H * s.W, s.C, s.Co, s.H, s.W, s.H, s.W, 1,
-        nullptr, static_cast<const bf16*>(residual), nullptr, 0, nullptr, 0, BnbArgs{}, 0, S);
-    return;
+    const int M = s.N * s.H * s.W;
+    float* st = bnb ? slab_of(g1s_rows(M, s.C, s.Co, 2)) : nullptr;
+    g1s(static_cast<const bf16*>(dy), wt, static_cast<bf16*>(dx), M, s.C, s.Co, s.H, s.W, s.H, s.W, 1, nullptr,
+        static_cast<const bf16*>(residual), st, 0, nullptr, 0, bnb ? ba : BnbArgs{}, bnb ? 2 : 0, S);
+    return st;
   }
   if (route != ROUTE_GENERIC && dyb < (1l << 31) && wtb < (1l << 31)) {
     // stride-phase decomposition: output phase (ry, rx) is a dense GEMM over the taps reaching
@@ -435,13 +454,14 @@ void conv_dgrad(const void* dy, const void* w, void* dx, const ConvShape& s, con
         }
       }
       gemm_g2(a, S);
-      return;
+      return nullptr;
     }
   }
   NtArgs a{static_cast<const bf16*>(dy), wt, dx, s.N * s.H * s.W, s.C, K, 0, K, s.C, kConvDgrad, s.N, s.OH, s.OW,
            s.Co, s.H, s.W, s.KH, s.KW, s.SH, s.SW, s.PH, s.PW, nullptr, static_cast<const bf16*>(residual), nullptr,
            0, 0};
   gemm_nt(a, S);
+  return nullptr;
 }
 
 void conv_wgrad(const void* dy, const void* x, float* gw, float* gb, const ConvShape& s) {
@@ -580,6 +600,12 @@ void bn_fwd_slab(const void* x, void* y, long R, int C, const float* slab, int r
   const auto st = reduce_stats(0, slab, rows, C);
   bn_apply(kBF16, x, y, R, C, st.first, st.second, (float)R, g, b, eps, residual, relu ? 1 : 0, smean, sistd, rmean,
            rvar, momentum, 0, S);
+}
+
+void bn_bwd_slab(const void* dy, const void* x, void* dx, long R, int C, const float* mean, const float* istd,
+                 const float* g, float* dg, float* db, bool train, const float* slab, int rows) {
+  const auto st = reduce_stats(1, slab, rows, C);
+  bn_bwd_apply(kBF16, dy, nullptr, x, dx, R, C, mean, istd, g, st.first, st.second, (float)R, dg, db, train ? 0 : 1, S);
 }
 
 void bn_bwd(const void* dy, const void* x, void* dx, long R, int C, const float* mean, const float* istd,
