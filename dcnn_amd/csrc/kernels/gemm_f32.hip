@@ -1,15 +1,16 @@
-// fp32 implicit-GEMM convolution / dense kernels on CDNA4 MFMA (v_mfma_f32_16x16x4_f32).
+// fp32 implicit-GEMM convolution / dense kernels on CDNA4 MFMA.
 //
 // The fp32 compute path (the reference's only precision; BASELINE config "CIFAR-10 ResNet-9
 // fp32") uses the same gathered-GEMM formulation and host-side tap tables as the bf16 v2
-// kernels (gemm2.hip) — conv forward, phase-decomposed dgrad and dense share one NT kernel,
-// weight gradients one split-K TN kernel — with fp32 operands end to end:
+// kernels (gemm2.hip) — conv forward, phase-decomposed dgrad and dense share one NT kernel
+// family, weight gradients one split-K TN kernel family — with fp32 operands end to end:
 //
-// * 64x64 output tile, 256 threads (2x2 waves, 32x32 per wave = 2x2 MFMA 16x16 subtiles),
-//   BK = 16 reduction elements per stage; global float4 loads are register-staged one stage
-//   ahead (loads of tile k+1 overlap the MFMAs of tile k).
-// * Each lane reads one float4 of A and of B per 16-wide K block from LDS and issues four
-//   16x16x4 MFMAs (k permuted consistently between operands, so the sum is unchanged).
+// * Forward / dgrad: 128 x 128 or 128 x 64 tiles on v_mfma_f32_32x32x2_f32 where the grid still
+//   fills the chip with them, else 64 x 64 tiles on v_mfma_f32_16x16x4_f32 (2x2 waves, 32x32 per
+//   wave); BK = 16 reduction elements per stage, global float4 loads register-staged one stage
+//   ahead (loads of tile k+1 overlap the MFMAs of tile k), the tap of a 16-multiple channel block
+//   looked up wave-uniformly.
+// * Weight gradient: pixel-major LDS tiles (see gemm_t2f_wide_kernel), 64 / 128 per side.
 // * Padding / out-of-image taps are zero-filled from a per-row tap-validity mask.
 // * Epilogue: bias, residual add, ReLU and per-channel BatchNorm (sum, sum^2) partials, with
 //   the strided output-row scatter of a dgrad phase.
@@ -391,110 +392,9 @@ __global__ void __launch_bounds__(256, 2) gemm_g2f_wide_kernel(G2Args p) {
   }
 }
 
-// dW[m][n] (+ bias grad) = sum_p dY[p][m] * X[gather(p, tap(n))][c(n)] over this split's pixels
-__global__ void __launch_bounds__(256, 2) gemm_t2f_kernel(T2Args p) {
-  __shared__ __attribute__((aligned(16))) float As[FBM * FPITCH];  // [m][k]
-  __shared__ __attribute__((aligned(16))) float Bs[FBN * FPITCH];  // [n][k]
-  const float* dY = reinterpret_cast<const float*>(p.dY);
-  const float* X = reinterpret_cast<const float*>(p.X);
-  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
-  const int wm = wid >> 1, wn = wid & 1;
-  const int tiles_m = (p.M + FBM - 1) / FBM, tiles_n = (p.N + FBN - 1) / FBN;
-  const int tiles = tiles_m * tiles_n;
-  const int lt = xcd_remap_f(blockIdx.x, gridDim.x);
-  const int split = lt / tiles, tt = lt % tiles;
-  const int tm = tt / tiles_n, tn = tt % tiles_n;
-  const int m0 = tm * FBM, n0 = tn * FBN;
-  const long pbeg = (long)split * p.k_per_split;
-  const long pend = pbeg + p.k_per_split < p.P ? pbeg + p.k_per_split : p.P;
-
-  // loader: pixel row lk (0..15), 4 consecutive columns starting at 4*lq (0..15)
-  const int lk = tid >> 4, lq = tid & 15;
-  const int am = m0 + lq * 4;        // dY columns
-  const int bn = n0 + lq * 4;        // (tap, c) columns
-  const bool vecA = (p.ldy & 3) == 0 && am + 3 < p.M;
-  const bool vecB = (p.Cs & 3) == 0 && bn + 3 < p.N;
-  float bias_acc = 0.f;
-
-  f32x4 acc[2][2];
-#pragma unroll
-  for (int i = 0; i < 2; ++i)
-#pragma unroll
-    for (int j = 0; j < 2; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-
-  const int ghw = p.GH * p.GW;
-  for (long k0 = pbeg; k0 < pend; k0 += FBK) {
-    const long pix = k0 + lk;
-    float va[4] = {0.f, 0.f, 0.f, 0.f}, vb[4] = {0.f, 0.f, 0.f, 0.f};
-    if (pix < pend) {
-      if (vecA) {
-        const float4 v = *reinterpret_cast<const float4*>(dY + pix * p.ldy + am);
-        va[0] = v.x; va[1] = v.y; va[2] = v.z; va[3] = v.w;
-      } else {
-#pragma unroll
-        for (int e = 0; e < 4; ++e)
-          if (am + e < p.M) va[e] = dY[pix * p.ldy + am + e];
-      }
-      const int img = (int)(pix / ghw), rem = (int)(pix - (long)img * ghw);
-      const int gy = rem / p.GW, gx = rem - gy * p.GW;
-      const int y0 = gy * p.SY, x0 = gx * p.SX;
-      if (vecB) {
-        const int t = bn / p.Cs, c = bn - t * p.Cs;
-        const int sy = y0 + p.tap_dy[t], sx = x0 + p.tap_dx[t];
-        if (sy >= 0 && sy < p.H && sx >= 0 && sx < p.W) {
-          const float4 v = *reinterpret_cast<const float4*>(X + (((long)img * p.H + sy) * p.W + sx) * p.Cs + c);
-          vb[0] = v.x; vb[1] = v.y; vb[2] = v.z; vb[3] = v.w;
-        }
-      } else {
-#pragma unroll
-        for (int e = 0; e < 4; ++e) {
-          const int n = bn + e;
-          if (n >= p.N) continue;
-          const int t = n / p.Cs, c = n - t * p.Cs;
-          const int sy = y0 + p.tap_dy[t], sx = x0 + p.tap_dx[t];
-          if (sy >= 0 && sy < p.H && sx >= 0 && sx < p.W) vb[e] = X[(((long)img * p.H + sy) * p.W + sx) * p.Cs + c];
-        }
-      }
-    }
-    __syncthreads();  // previous tile fully consumed
-#pragma unroll
-    for (int e = 0; e < 4; ++e) {
-      As[(lq * 4 + e) * FPITCH + lk] = va[e];
-      Bs[(lq * 4 + e) * FPITCH + lk] = vb[e];
-    }
-    __syncthreads();
-    if (p.bias_slab && tn == 0 && tid < FBM) {
-#pragma unroll
-      for (int k = 0; k < FBK; ++k) bias_acc += As[tid * FPITCH + k];
-    }
-    const int g = lane >> 4;
-    float4 a[2], b[2];
-#pragma unroll
-    for (int i = 0; i < 2; ++i) a[i] = *reinterpret_cast<const float4*>(&As[(wm * 32 + i * 16 + (lane & 15)) * FPITCH + g * 4]);
-#pragma unroll
-    for (int j = 0; j < 2; ++j) b[j] = *reinterpret_cast<const float4*>(&Bs[(wn * 32 + j * 16 + (lane & 15)) * FPITCH + g * 4]);
-#pragma unroll
-    for (int i = 0; i < 2; ++i)
-#pragma unroll
-      for (int j = 0; j < 2; ++j) acc[i][j] = mfma4(a[i], b[j], acc[i][j]);
-  }
-  float* out = p.slab + (long)split * p.M * p.N;
-#pragma unroll
-  for (int i = 0; i < 2; ++i)
-#pragma unroll
-    for (int j = 0; j < 2; ++j) {
-      const int col = n0 + wn * 32 + j * 16 + (lane & 15);
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const int row = m0 + wm * 32 + i * 16 + (lane >> 4) * 4 + r;
-        if (row < p.M && col < p.N) out[(long)row * p.N + col] = acc[i][j][r];
-      }
-    }
-  if (p.bias_slab && tn == 0 && tid < FBM && m0 + tid < p.M) p.bias_slab[(long)split * p.M + m0 + tid] = bias_acc;
-}
-
-// Wide-tile variant of gemm_t2f_kernel: a 128 x 128 dW tile per split on v_mfma_f32_32x32x2_f32
-// (4 waves of 64 x 64). Both operands arrive pixel-major (a pixel's dY row, a pixel's gathered X
+// Exact-fp32 weight gradient, dW[m][n] (+ bias grad) = sum_p dY[p][m] * X[gather(p, tap(n))][c(n)]
+// over this split's pixels: a BM x BN (64 / 128) dW tile per split on v_mfma_f32_32x32x2_f32
+// (4 waves of BM/2 x BN/2). Both operands arrive pixel-major (a pixel's dY row, a pixel's gathered X
 // row), so the LDS tiles are kept pixel-major too — [k][m] / [k][n], float4 stores along m / n
 // (conflict-free) — and every MFMA operand is one ds_read_b32: lane half h reads pixel 2s + h of
 // the 16-pixel tile, lane l32 its column. The next tile's global loads are issued right after the
@@ -980,20 +880,29 @@ void set_f32_mode(int mode) { g_f32_mode = mode ? 1 : 0; }
 int get_f32_mode() { return f32_split() ? 1 : 0; }
 
 // exact-f32 forward / dgrad tile: 128 x 128 (32x32x2 MFMA) while that still gives >= 1.5
-// workgroups per CU, else the 64 x 64 16x16x4 kernel
-static int g2f_bm(int M, int N) {
-  const long wide = (long)((M + 127) / 128) * ((N + 127) / 128);
-  return (N >= 128 && wide >= 384) ? 128 : FBM;
+// workgroups per CU, else 128 x 64 (the same kernel, one 32-column MFMA tile per wave) while that
+// does, else the 64 x 64 16x16x4 kernel. (PMC, ResNet-9 b128: matrix-pipe busy 47.8% on the
+// 128-row tiles vs 37.9% on the 64 x 64 kernel, profiles/pmc_f32_r4.md)
+static int g2f_bn(int M, int N) {
+  const long rows = (M + 127) / 128;
+  if (N >= 128 && rows * ((N + 127) / 128) >= 384) return 128;
+  if (N >= 64 && rows * ((N + 63) / 64) >= 384) return 64;
+  return 0;  // the 64 x 64 kernel
 }
+static int g2f_bm(int M, int N) { return g2f_bn(M, N) ? 128 : FBM; }
 
 void gemm_g2f(const G2Args& a, hipStream_t s) {
   if (a.ntaps > 64) throw std::runtime_error("gemm_g2f: at most 64 taps");
+  const int bn = f32_split() ? 0 : g2f_bn(a.M, a.N);
   if (f32_split()) {
     const int tiles = ((a.M + FBM - 1) / FBM) * ((a.N + FBN - 1) / FBN);
     hipLaunchKernelGGL(gemm_g2x_kernel, dim3(tiles), dim3(256), 0, s, a);
-  } else if (g2f_bm(a.M, a.N) == 128) {
+  } else if (bn == 128) {
     const int tiles = ((a.M + 127) / 128) * ((a.N + 127) / 128);
     hipLaunchKernelGGL((gemm_g2f_wide_kernel<128, 128>), dim3(tiles), dim3(256), 0, s, a);
+  } else if (bn == 64) {
+    const int tiles = ((a.M + 127) / 128) * ((a.N + 63) / 64);
+    hipLaunchKernelGGL((gemm_g2f_wide_kernel<128, 64>), dim3(tiles), dim3(256), 0, s, a);
   } else {
     const int tiles = ((a.M + FBM - 1) / FBM) * ((a.N + FBN - 1) / FBN);
     hipLaunchKernelGGL(gemm_g2f_kernel, dim3(tiles), dim3(256), 0, s, a);
@@ -1006,14 +915,20 @@ int gemm_g2f_stat_rows(int M, int N) {
   return (M + bm - 1) / bm;
 }
 
-// exact-f32 weight-gradient tile: 128 x 128 when both sides hold at least 128 (fewer, larger
-// split-K slabs: every split still gets one workgroup per CU or more)
-static int t2f_bm(int M, int N) { return (M >= 128 && N >= 128) ? 128 : FBM; }
+// exact-f32 weight-gradient tile on the pixel-major 32x32x2 kernel: 128 rows / columns where the
+// side holds at least 128, else 64 (fewer, larger split-K slabs: every split still gets one
+// workgroup per CU or more). (PMC, ResNet-9 b128: matrix-pipe busy 43.1% on it vs 7.1% on the
+// 64 x 64 16x16x4 kernel)
+static void t2f_tile(int M, int N, int* bm, int* bn) {
+  *bm = M >= 128 ? 128 : 64;
+  *bn = N >= 128 ? 128 : 64;
+}
 
 int gemm_t2f_splits(int M, int N, int P) {
-  const int bm = f32_split() ? FBM : t2f_bm(M, N);
-  const int tiles = ((M + bm - 1) / bm) * ((N + bm - 1) / bm);
-  int splits = ((bm == 128 ? 512 : 1024) + tiles - 1) / tiles;
+  int bm = FBM, bn = FBN;
+  if (!f32_split()) t2f_tile(M, N, &bm, &bn);
+  const int tiles = ((M + bm - 1) / bm) * ((N + bn - 1) / bn);
+  int splits = ((bm * bn >= 128 * 128 ? 512 : 1024) + tiles - 1) / tiles;
   const long max_by_k = (P + 255) / 256;             // at least 256 pixels per split
   if (splits > max_by_k) splits = (int)max_by_k;
   const long slab_cap = (96l << 20) / (4l * M * N);  // <= 96 MB of fp32 partials
@@ -1030,12 +945,18 @@ void gemm_t2f(T2Args a, int splits, hipStream_t s) {
   if (f32_split()) {
     const int tiles = ((a.M + FBM - 1) / FBM) * ((a.N + FBN - 1) / FBN);
     hipLaunchKernelGGL(gemm_t2x_kernel, dim3(tiles * splits), dim3(256), 0, s, a);
-  } else if (t2f_bm(a.M, a.N) == 128) {
-    const int tiles = ((a.M + 127) / 128) * ((a.N + 127) / 128);
-    hipLaunchKernelGGL((gemm_t2f_wide_kernel<128, 128>), dim3(tiles * splits), dim3(256), 0, s, a);
   } else {
-    const int tiles = ((a.M + FBM - 1) / FBM) * ((a.N + FBN - 1) / FBN);
-    hipLaunchKernelGGL(gemm_t2f_kernel, dim3(tiles * splits), dim3(256), 0, s, a);
+    int bm, bn;
+    t2f_tile(a.M, a.N, &bm, &bn);
+    const int tiles = ((a.M + bm - 1) / bm) * ((a.N + bn - 1) / bn);
+    if (bm == 128 && bn == 128)
+      hipLaunchKernelGGL((gemm_t2f_wide_kernel<128, 128>), dim3(tiles * splits), dim3(256), 0, s, a);
+    else if (bm == 128)
+      hipLaunchKernelGGL((gemm_t2f_wide_kernel<128, 64>), dim3(tiles * splits), dim3(256), 0, s, a);
+    else if (bn == 128)
+      hipLaunchKernelGGL((gemm_t2f_wide_kernel<64, 128>), dim3(tiles * splits), dim3(256), 0, s, a);
+    else
+      hipLaunchKernelGGL((gemm_t2f_wide_kernel<64, 64>), dim3(tiles * splits), dim3(256), 0, s, a);
   }
   DCNN_LAUNCH_CHECK();
 }
