@@ -972,8 +972,9 @@ def _ticket(device, C, slot="stat"):
 
 class Stats:
     """Per-channel statistics for the BN apply kernels: ``parts == 1`` -> ``buf`` is the finished
-    [2][C] result; ``parts > 1`` -> ``buf`` holds [parts][3][C] level-1 partials that the
-    consuming kernel merges in its prologue (norm.hip read_stats). Used as a tensor (tests,
+    [2][C] result; ``parts > 1`` -> ``buf`` holds [parts][3][C] level-1 partials (or a producer's
+    raw Welford rows) that the consuming kernel merges in its prologue (norm.hip read_stats);
+    ``parts < -1`` (mode 1) -> ``buf`` holds a producer's -parts raw [2][C] sum rows. Used as a tensor (tests,
     inspection) it materialises the finished [2][C] statistics (``final()``, torch ops: off the
     training hot path)."""
     __slots__ = ("buf", "parts", "mode", "_final")
@@ -987,9 +988,10 @@ class Stats:
         if self._final is None:
             p = self.buf.double()
             C = p.shape[2]
+            parts = abs(self.parts)
             if self.mode == 0:  # Chan merges in part order (as read_stats)
                 n, mean, m2 = p[0, 0].clone(), p[0, 1].clone(), p[0, 2].clone()
-                for k in range(1, self.parts):
+                for k in range(1, parts):
                     nb, mb, m2b = p[k, 0], p[k, 1], p[k, 2]
                     tot = n + nb
                     d = mb - mean
@@ -1018,12 +1020,25 @@ def prewarm_tickets(device, slots=("loss",)):
         _ticket(torch.device(device), 0, slot=s)
 
 
+# producer statistics slabs of at most this many rows are handed to the consumers raw (they merge
+# the rows in their prologue, norm.hip read_stats) instead of paying a reduce launch
+_RAW_STAT_ROWS = 16
+
+
+def _raw_stats(mode, slab, rows):
+    return Stats(slab, rows if mode == 0 else -rows, mode) if 2 <= rows <= _RAW_STAT_ROWS else None
+
+
 def stat_reduce(mode, slab, rows, C, out):
     """Deterministic slab reduce (norm.hip bn_stat_reduce): mode 0 = Welford (count, mean, M2)
     tile triples -> (mean, biased var); mode 1 = (sum a, sum b) rows -> sums. Returns
-    :class:`Stats` (``out`` when one block covered all rows, else the partials buffer)."""
+    :class:`Stats` (``out`` when one block covered all rows, else the partials buffer; the slab
+    itself when it has at most ``_RAW_STAT_ROWS`` rows)."""
     if isinstance(slab, Stats):  # already folded inside the producing launch (statfold.h)
         return slab
+    raw = _raw_stats(mode, slab, rows)
+    if raw is not None:
+        return raw
     K = kernels()
     ny = K.bn_stat_parts(rows)
     part = _empty((ny, 3, C), F32, slab.device) if ny > 1 else None
@@ -1109,6 +1124,9 @@ def bn_bwd_apply_dual(dy, a, b):
 def stat_reduce_pair(mode, a, b, C):
     """Two independent forward/backward statistics reduces of the same C in ONE launch
     (norm.hip bn_stat_reduce2); ``a``/``b`` = (slab, rows, out). Returns two :class:`Stats`."""
+    raws = [_raw_stats(mode, slab, rows) for slab, rows, _ in (a, b)]
+    if raws[0] is not None or raws[1] is not None:
+        return tuple(r if r is not None else stat_reduce(mode, x[0], x[1], C, x[2]) for r, x in zip(raws, (a, b)))
     K = kernels()
     res, ptrs = [], []
     for slab, rows, out in (a, b):
