@@ -175,3 +175,19 @@ def test_cpp_tiny_imagenet_trainer_gpu_bench(bins, tmp_path):
     m = re.search(r"\"value\": (\S+),", out)
     assert m and float(m.group(1)) > 0, out
     print(out)
+
+
+@pytest.mark.gpu
+def test_cpp_resnet18_gpu_training_matches_cpu_backend(bins, tmp_path):
+    """The GPU backend's fused training path — conv-epilogue BatchNorm statistics, BN + ReLU,
+    residual-tail BN with the shortcut add and its masked branch gradient, the dgrad epilogue's
+    BN-backward statistics, head-conv shortcut add, deferred weight-gradient reduce, parameter
+    arena with the fused Adam step and batched weight transposes — against the CPU backend's
+    plain fp32 ops: the same initial weights and batches give the same losses over 3 Adam steps
+    to bf16 accuracy."""
+    args = ["train", "resnet18_tiny_imagenet", "3", "8"]
+    g = [float(v) for v in _lines(_run([bins["host_api_parity"], *args, "snap/g", "--device", "GPU"], tmp_path,
+                                       timeout=300))["losses"]]
+    c = [float(v) for v in _lines(_run([bins["host_api_parity"], *args, "snap/c"], tmp_path, timeout=600))["losses"]]
+    assert len(g) == len(c) == 3
+    np.testing.assert_allclose(g, c, rtol=5e-2)
