@@ -128,6 +128,9 @@ class Conv2D : public Layer {
   // GPU: the BatchNorm (+ ReLU) producing this conv's input; the data gradient's epilogue applies
   // its ReLU mask and computes its backward statistics (fuse_bn_relu wires it)
   void set_bnb_producer(class BatchNorm* bn) { bnb_from_ = bn; }
+  // the same across a residual-block boundary: the previous block's tail BatchNorm (its mask is
+  // the block output), applied only by backward_residual (after the shortcut gradient is added)
+  void set_block_bnb_producer(class BatchNorm* bn) { bnb_block_from_ = bn; }
   // GPU: backward whose input gradient also adds `residual` in the data-gradient epilogue
   Tensor backward_residual(const Tensor& dy, const Tensor& residual);
   void sync_shadow() override;
@@ -141,6 +144,7 @@ class Conv2D : public Layer {
   bool bias_;
   class BatchNorm* stats_to_ = nullptr;
   class BatchNorm* bnb_from_ = nullptr;
+  class BatchNorm* bnb_block_from_ = nullptr;
   Tensor wt_;  // pre-transposed dgrad operand (arena-managed)
   const void* dgrad_operand(bool& transposed) const;
 };
@@ -312,10 +316,12 @@ class ResidualBlock : public Layer {
   void set_micro_batch(int mb) override;
   const std::vector<std::unique_ptr<Layer>>& main_path() const { return main_; }
   const std::vector<std::unique_ptr<Layer>>& shortcut_path() const { return short_; }
-
- private:
   // GPU: the main path's tail BatchNorm adds the shortcut and applies the block activation
   class BatchNorm* fused_tail() const;
+  // the main path's first layer when it is a conv (its dgrad adds the shortcut gradient)
+  class Conv2D* head_conv() const;
+
+ private:
   std::vector<std::unique_ptr<Layer>> main_, short_;
   std::string act_;
 };
@@ -329,6 +335,10 @@ std::unique_ptr<Layer> create_layer(const json::Value& rec);
 // statistics pass over the conv output). `on` false undoes it (CPU placement).
 // Sequential::initialize / ResidualBlock::build run it.
 void fuse_bn_relu(std::vector<std::unique_ptr<Layer>>& seq, bool on);
+// after the layers are built: consecutive residual blocks with fused tails — the next block's
+// head-conv data gradient (shortcut gradient added) also masks with the previous block's output
+// and computes its tail BatchNorm's backward statistics
+void fuse_blocks(std::vector<std::unique_ptr<Layer>>& seq, bool on);
 
 class Sequential {
  public:

@@ -214,6 +214,13 @@ Tensor Conv2D::backward_residual(const Tensor& dy, const Tensor& residual) {
   Tensor dx = act_empty(x_.shape(), dev_);
   bool tr = false;
   const void* w = dgrad_operand(tr);
+  if (bnb_block_from_ != nullptr) {
+    const gpu_ops::BnbOperands ops = bnb_block_from_->bnb_operands(mb_);
+    int rows = 0;
+    const float* st = gpu_ops::conv_dgrad(dy.data(), w, dx.data(), s, residual.data(), tr, &ops, &rows);
+    if (rows > 0) bnb_block_from_->offer_bwd_stats(dx.data(), st, rows);
+    return dx;
+  }
   gpu_ops::conv_dgrad(dy.data(), w, dx.data(), s, residual.data(), tr);
   return dx;
 }
@@ -393,7 +400,15 @@ Tensor BatchNorm::backward_residual(const Tensor& dy, Tensor* branch) {
   const float* g = affine_ ? params_[0].value.ptr<float>() : nullptr;
   float* dg = affine_ ? params_[0].grad.ptr<float>() : nullptr;
   float* db = affine_ ? params_[1].grad.ptr<float>() : nullptr;
-  if (mc.d.defined()) {
+  if (bwd_dy_ == dy.data() && bwd_slab_ != nullptr && bwd_rows_ > 0) {
+    // dy already masked and its statistics computed by the next block's head-conv dgrad
+    *branch = dy;
+    gpu_ops::bn_bwd_slab(dy.data(), x_.data(), dx.data(), N * HW, c_, mc.b.ptr<float>(), mc.c.ptr<float>(), g, dg, db,
+                         train_, bwd_slab_, bwd_rows_);
+    bwd_dy_ = nullptr;
+    bwd_slab_ = nullptr;
+    bwd_rows_ = 0;
+  } else if (mc.d.defined()) {
     *branch = act_empty(dy.shape(), dev_);
     gpu_ops::bn_bwd(dy.data(), x_.data(), dx.data(), N * HW, c_, mc.b.ptr<float>(), mc.c.ptr<float>(), g, dg, db,
                     train_, mc.d.data(), branch->data());
@@ -684,6 +699,20 @@ void ResidualBlock::build(const std::vector<int64_t>& in, Device dev, uint64_t s
   for (auto& l : short_) {
     l->build(s, dev, seed * 31ull + (k++) * 104729ull);
     if (s[1] > 0) s = l->output_shape(s);
+  }
+}
+
+Conv2D* ResidualBlock::head_conv() const { return main_.empty() ? nullptr : dynamic_cast<Conv2D*>(main_[0].get()); }
+
+void fuse_blocks(std::vector<std::unique_ptr<Layer>>& seq, bool on) {
+  for (size_t i = 0; i + 1 < seq.size(); ++i) {
+    auto* prev = dynamic_cast<ResidualBlock*>(seq[i].get());
+    auto* next = dynamic_cast<ResidualBlock*>(seq[i + 1].get());
+    if (prev == nullptr || next == nullptr) continue;
+    BatchNorm* tail = prev->fused_tail();
+    Conv2D* head = next->head_conv();
+    if (head == nullptr) continue;
+    head->set_block_bnb_producer(on && tail != nullptr && next->fused_tail() != nullptr ? tail : nullptr);
   }
 }
 
@@ -1027,6 +1056,7 @@ void Sequential::initialize(uint64_t seed) {
     l->build(shape, dev_, seed * 1000003ull + (k++) * 7919ull);
     if (shape[1] > 0 && shape[2] > 0) shape = l->output_shape(shape);
   }
+  fuse_blocks(layers_, dev_.is_gpu());
   pack_params();
   initialized_ = true;
 }
