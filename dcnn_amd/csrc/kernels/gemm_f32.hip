@@ -209,13 +209,15 @@ __global__ void __launch_bounds__(256, 2) gemm_g2f_kernel(G2Args p) {
 // k = 8h .. 8h + 7 of the block); MFMA step s takes k = s from half 0 and k = 8 + s from half 1 for
 // BOTH operands, so every k is summed once (the order differs from the 16x16x4 kernel: exact f32
 // arithmetic, a different fma chain).
-template <int BM, int BN>
+template <int BM, int BN, int BK = FBK>
 __global__ void __launch_bounds__(256, 2) gemm_g2f_wide_kernel(G2Args p) {
   constexpr int WM = BM / 2, WN = BN / 2;     // per-wave tile
   constexpr int TM = WM / 32, TN = WN / 32;   // 32x32 MFMA tiles per wave
-  constexpr int AR = BM / 64, BR = BN / 64;   // loader rows per thread (64 rows per pass)
-  __shared__ __attribute__((aligned(16))) float As[2][BM * FPITCH];
-  __shared__ __attribute__((aligned(16))) float Bs[2][BN * FPITCH];
+  constexpr int PITCH = BK + 4;               // LDS row pitch (floats)
+  constexpr int CH = BK / 4, RP = 256 / CH;   // float4 chunks per row, rows per loader pass
+  constexpr int AR = BM / RP, BR = BN / RP;   // loader rows per thread
+  __shared__ __attribute__((aligned(16))) float As[2][BM * PITCH];
+  __shared__ __attribute__((aligned(16))) float Bs[2][BN * PITCH];
   __shared__ float red[2][4][BN];
   const float* A = reinterpret_cast<const float*>(p.A);
   const float* B = reinterpret_cast<const float*>(p.B);
@@ -230,14 +232,14 @@ __global__ void __launch_bounds__(256, 2) gemm_g2f_wide_kernel(G2Args p) {
   if (p.zero_ptr && blockIdx.x == 0)
     for (int i = tid; i < p.zero_n; i += 256) p.zero_ptr[i] = 0.f;
 
-  const int lr = tid >> 2, lc = tid & 3;  // loader: rows lr + 64 r, float4 chunk lc
+  const int lr = tid / CH, lc = tid % CH;  // loader: rows lr + RP r, float4 chunk lc
   long a_base[AR];
   uint64_t a_mask[AR];
 #pragma unroll
   for (int r = 0; r < AR; ++r) {
     a_base[r] = 0;
     a_mask[r] = 0;
-    const int m = m0 + lr + 64 * r;
+    const int m = m0 + lr + RP * r;
     if (m < p.M) {
       const int ghw = p.GH * p.GW;
       const int img = m / ghw, rem = m - img * ghw;
@@ -254,11 +256,11 @@ __global__ void __launch_bounds__(256, 2) gemm_g2f_wide_kernel(G2Args p) {
   long b_base[BR];
 #pragma unroll
   for (int r = 0; r < BR; ++r) {
-    const int n = n0 + lr + 64 * r;
+    const int n = n0 + lr + RP * r;
     b_ok[r] = n < p.N;
     b_base[r] = (long)n * p.ldb;
   }
-  const bool vec = (p.Cs & 3) == 0, uni = p.Cs % FBK == 0;
+  const bool vec = (p.Cs & 3) == 0, uni = p.Cs % BK == 0;
 
   auto load = [&](int k0, float4 (&ra)[AR], float4 (&rb)[BR]) {
     const int k = k0 + lc * 4;
@@ -266,7 +268,7 @@ __global__ void __launch_bounds__(256, 2) gemm_g2f_wide_kernel(G2Args p) {
     for (int r = 0; r < AR; ++r) ra[r] = make_float4(0.f, 0.f, 0.f, 0.f);
 #pragma unroll
     for (int r = 0; r < BR; ++r) rb[r] = make_float4(0.f, 0.f, 0.f, 0.f);
-    if (vec) {  // the 4 elements share one tap (16-multiple channels: wave-uniform, as above)
+    if (vec) {  // the 4 elements share one tap (BK-multiple channels: wave-uniform, as above)
       const int tu = k0 / p.Cs;
       const int t = uni ? tu : k / p.Cs, c = uni ? k0 - tu * p.Cs + lc * 4 : k - t * p.Cs;
       if (t < p.ntaps) {
@@ -303,39 +305,42 @@ __global__ void __launch_bounds__(256, 2) gemm_g2f_wide_kernel(G2Args p) {
       for (int e = 0; e < 16; ++e) acc[i][j][e] = 0.f;
 
   const int K = p.ntaps * p.Cs;
-  const int nk = (K + FBK - 1) / FBK;
+  const int nk = (K + BK - 1) / BK;
   float4 ra[AR], rb[BR];
   load(0, ra, rb);
   int cur = 0;
   const int h = lane >> 5, l32 = lane & 31;
   for (int kt = 0; kt < nk; ++kt) {
 #pragma unroll
-    for (int r = 0; r < AR; ++r) *reinterpret_cast<float4*>(&As[cur][(lr + 64 * r) * FPITCH + lc * 4]) = ra[r];
+    for (int r = 0; r < AR; ++r) *reinterpret_cast<float4*>(&As[cur][(lr + RP * r) * PITCH + lc * 4]) = ra[r];
 #pragma unroll
-    for (int r = 0; r < BR; ++r) *reinterpret_cast<float4*>(&Bs[cur][(lr + 64 * r) * FPITCH + lc * 4]) = rb[r];
+    for (int r = 0; r < BR; ++r) *reinterpret_cast<float4*>(&Bs[cur][(lr + RP * r) * PITCH + lc * 4]) = rb[r];
     __syncthreads();
-    if (kt + 1 < nk) load((kt + 1) * FBK, ra, rb);
-    float a[TM][8], b[TN][8];
+    if (kt + 1 < nk) load((kt + 1) * BK, ra, rb);
 #pragma unroll
-    for (int i = 0; i < TM; ++i) {
-      const float* src = &As[cur][(wm * WM + i * 32 + l32) * FPITCH + h * 8];
-      const float4 x0 = *reinterpret_cast<const float4*>(src), x1 = *reinterpret_cast<const float4*>(src + 4);
-      a[i][0] = x0.x; a[i][1] = x0.y; a[i][2] = x0.z; a[i][3] = x0.w;
-      a[i][4] = x1.x; a[i][5] = x1.y; a[i][6] = x1.z; a[i][7] = x1.w;
+    for (int kb = 0; kb < BK / 16; ++kb) {  // 16-wide k blocks, each in the two-half order above
+      float a[TM][8], b[TN][8];
+#pragma unroll
+      for (int i = 0; i < TM; ++i) {
+        const float* src = &As[cur][(wm * WM + i * 32 + l32) * PITCH + kb * 16 + h * 8];
+        const float4 x0 = *reinterpret_cast<const float4*>(src), x1 = *reinterpret_cast<const float4*>(src + 4);
+        a[i][0] = x0.x; a[i][1] = x0.y; a[i][2] = x0.z; a[i][3] = x0.w;
+        a[i][4] = x1.x; a[i][5] = x1.y; a[i][6] = x1.z; a[i][7] = x1.w;
+      }
+#pragma unroll
+      for (int j = 0; j < TN; ++j) {
+        const float* src = &Bs[cur][(wn * WN + j * 32 + l32) * PITCH + kb * 16 + h * 8];
+        const float4 x0 = *reinterpret_cast<const float4*>(src), x1 = *reinterpret_cast<const float4*>(src + 4);
+        b[j][0] = x0.x; b[j][1] = x0.y; b[j][2] = x0.z; b[j][3] = x0.w;
+        b[j][4] = x1.x; b[j][5] = x1.y; b[j][6] = x1.z; b[j][7] = x1.w;
+      }
+#pragma unroll
+      for (int s2 = 0; s2 < 8; ++s2)
+#pragma unroll
+        for (int i = 0; i < TM; ++i)
+#pragma unroll
+          for (int j = 0; j < TN; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(a[i][s2], b[j][s2], acc[i][j], 0, 0, 0);
     }
-#pragma unroll
-    for (int j = 0; j < TN; ++j) {
-      const float* src = &Bs[cur][(wn * WN + j * 32 + l32) * FPITCH + h * 8];
-      const float4 x0 = *reinterpret_cast<const float4*>(src), x1 = *reinterpret_cast<const float4*>(src + 4);
-      b[j][0] = x0.x; b[j][1] = x0.y; b[j][2] = x0.z; b[j][3] = x0.w;
-      b[j][4] = x1.x; b[j][5] = x1.y; b[j][6] = x1.z; b[j][7] = x1.w;
-    }
-#pragma unroll
-    for (int s2 = 0; s2 < 8; ++s2)
-#pragma unroll
-      for (int i = 0; i < TM; ++i)
-#pragma unroll
-        for (int j = 0; j < TN; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(a[i][s2], b[j][s2], acc[i][j], 0, 0, 0);
     cur ^= 1;
   }
 
@@ -891,6 +896,9 @@ static int g2f_bn(int M, int N) {
 }
 static int g2f_bm(int M, int N) { return g2f_bn(M, N) ? 128 : FBM; }
 
+static int g_f32_bk = 16;  // k-tile of the 128-row forward / dgrad kernels (test / tuning hook)
+void gemm_f32_set_bk(int bk) { g_f32_bk = bk == 32 ? 32 : 16; }
+
 void gemm_g2f(const G2Args& a, hipStream_t s) {
   if (a.ntaps > 64) throw std::runtime_error("gemm_g2f: at most 64 taps");
   const int bn = f32_split() ? 0 : g2f_bn(a.M, a.N);
@@ -899,10 +907,16 @@ void gemm_g2f(const G2Args& a, hipStream_t s) {
     hipLaunchKernelGGL(gemm_g2x_kernel, dim3(tiles), dim3(256), 0, s, a);
   } else if (bn == 128) {
     const int tiles = ((a.M + 127) / 128) * ((a.N + 127) / 128);
-    hipLaunchKernelGGL((gemm_g2f_wide_kernel<128, 128>), dim3(tiles), dim3(256), 0, s, a);
+    if (g_f32_bk == 32)
+      hipLaunchKernelGGL((gemm_g2f_wide_kernel<128, 128, 32>), dim3(tiles), dim3(256), 0, s, a);
+    else
+      hipLaunchKernelGGL((gemm_g2f_wide_kernel<128, 128>), dim3(tiles), dim3(256), 0, s, a);
   } else if (bn == 64) {
     const int tiles = ((a.M + 127) / 128) * ((a.N + 63) / 64);
-    hipLaunchKernelGGL((gemm_g2f_wide_kernel<128, 64>), dim3(tiles), dim3(256), 0, s, a);
+    if (g_f32_bk == 32)
+      hipLaunchKernelGGL((gemm_g2f_wide_kernel<128, 64, 32>), dim3(tiles), dim3(256), 0, s, a);
+    else
+      hipLaunchKernelGGL((gemm_g2f_wide_kernel<128, 64>), dim3(tiles), dim3(256), 0, s, a);
   } else {
     const int tiles = ((a.M + FBM - 1) / FBM) * ((a.N + FBN - 1) / FBN);
     hipLaunchKernelGGL(gemm_g2f_kernel, dim3(tiles), dim3(256), 0, s, a);
