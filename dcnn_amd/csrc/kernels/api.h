@@ -131,7 +131,6 @@ void pad_crop(const float* in, float* out, int NC, int H, int W, int OH, int OW,
 void gemm_g2f(const G2Args& a, hipStream_t s);
 int gemm_g2f_stat_rows(int M, int N);
 void gemm_t2f(T2Args a, int splits, hipStream_t s);
-void gemm_f32_set_bk(int bk);  // k-tile (16 / 32) of the 128-row fp32 forward / dgrad kernels
 int gemm_t2f_splits(int M, int N, int P);
 void set_f32_mode(int mode);  // 0 exact f32 MFMA (default), 1 split-bf16 (3 MFMAs)
 int get_f32_mode();

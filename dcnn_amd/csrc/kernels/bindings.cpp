@@ -423,7 +423,6 @@ PYBIND11_MODULE(_kernels, m) {
     }
   });
   m.def("multi_red_max", []() { return kMaxRed; });
-  m.def("gemm_f32_set_bk", &gemm_f32_set_bk);
   m.def("stem_supported", &stem_supported);
   m.def("stem_tiles", &stem_tiles_host);
   m.def("stem_wgrad_blocks", &stem_wgrad_blocks);

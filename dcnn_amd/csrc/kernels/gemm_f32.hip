@@ -209,6 +209,7 @@ __global__ void __launch_bounds__(256, 2) gemm_g2f_kernel(G2Args p) {
 // k = 8h .. 8h + 7 of the block); MFMA step s takes k = s from half 0 and k = 8 + s from half 1 for
 // BOTH operands, so every k is summed once (the order differs from the 16x16x4 kernel: exact f32
 // arithmetic, a different fma chain).
+// (BK = 32 measured slower: ResNet-9 fp32 15.3k -> 15.1k, ResNet-18 17.0k -> 16.5k img/s)
 template <int BM, int BN, int BK = FBK>
 __global__ void __launch_bounds__(256, 2) gemm_g2f_wide_kernel(G2Args p) {
   constexpr int WM = BM / 2, WN = BN / 2;     // per-wave tile
@@ -896,9 +897,6 @@ static int g2f_bn(int M, int N) {
 }
 static int g2f_bm(int M, int N) { return g2f_bn(M, N) ? 128 : FBM; }
 
-static int g_f32_bk = 16;  // k-tile of the 128-row forward / dgrad kernels (test / tuning hook)
-void gemm_f32_set_bk(int bk) { g_f32_bk = bk == 32 ? 32 : 16; }
-
 void gemm_g2f(const G2Args& a, hipStream_t s) {
   if (a.ntaps > 64) throw std::runtime_error("gemm_g2f: at most 64 taps");
   const int bn = f32_split() ? 0 : g2f_bn(a.M, a.N);
@@ -907,16 +905,10 @@ void gemm_g2f(const G2Args& a, hipStream_t s) {
     hipLaunchKernelGGL(gemm_g2x_kernel, dim3(tiles), dim3(256), 0, s, a);
   } else if (bn == 128) {
     const int tiles = ((a.M + 127) / 128) * ((a.N + 127) / 128);
-    if (g_f32_bk == 32)
-      hipLaunchKernelGGL((gemm_g2f_wide_kernel<128, 128, 32>), dim3(tiles), dim3(256), 0, s, a);
-    else
-      hipLaunchKernelGGL((gemm_g2f_wide_kernel<128, 128>), dim3(tiles), dim3(256), 0, s, a);
+    hipLaunchKernelGGL((gemm_g2f_wide_kernel<128, 128>), dim3(tiles), dim3(256), 0, s, a);
   } else if (bn == 64) {
     const int tiles = ((a.M + 127) / 128) * ((a.N + 63) / 64);
-    if (g_f32_bk == 32)
-      hipLaunchKernelGGL((gemm_g2f_wide_kernel<128, 64, 32>), dim3(tiles), dim3(256), 0, s, a);
-    else
-      hipLaunchKernelGGL((gemm_g2f_wide_kernel<128, 64>), dim3(tiles), dim3(256), 0, s, a);
+    hipLaunchKernelGGL((gemm_g2f_wide_kernel<128, 64>), dim3(tiles), dim3(256), 0, s, a);
   } else {
     const int tiles = ((a.M + FBM - 1) / FBM) * ((a.N + FBN - 1) / FBN);
     hipLaunchKernelGGL(gemm_g2f_kernel, dim3(tiles), dim3(256), 0, s, a);
