@@ -332,9 +332,14 @@ Tensor PipelineStage::decode(Message& m) const {
     case 1: dt = DType::BF16; break;
     default: throw std::runtime_error("activation payloads must be fp32 or bf16");
   }
-  Tensor t = Tensor::empty(shape, dt, Device::cpu(), layout);
+  // a GPU stage's own activation form (bf16 NHWC) goes straight from the payload to the device
+  const bool direct = dev_.is_gpu() && dt == DType::BF16 && layout == Layout::NHWC;
+  Tensor t = Tensor::empty(shape, dt, direct ? dev_ : Device::cpu(), layout);
   if (m.data.size() != t.nbytes()) throw std::runtime_error("tensor payload size does not match its shape");
-  std::memcpy(t.data(), m.data.data(), t.nbytes());
+  if (direct)
+    gpu::copy(t.data(), m.data.data(), t.nbytes(), 0);
+  else
+    std::memcpy(t.data(), m.data.data(), t.nbytes());
   if (t.rank() == 2) t = t.view({shape[0], shape[1], 1, 1}, Layout::NCHW);  // (N, F): 1x1 spatial
   return t;
 }
@@ -346,20 +351,23 @@ void PipelineStage::send_tensor(const std::string& to, uint16_t cmd, uint64_t mb
   m.payload_type = P_TYPED_JOB;
   m.mb_id = mb;
   if (t.defined()) {
-    const Tensor h = t.device().is_gpu() ? t.to(Device::cpu()) : t;
-    const auto& s = h.shape();
-    uint8_t code = h.dtype() == DType::F32 ? 0 : h.dtype() == DType::BF16 ? 1 : 0xff;
+    const auto& s = t.shape();
+    uint8_t code = t.dtype() == DType::F32 ? 0 : t.dtype() == DType::BF16 ? 1 : 0xff;
     if (code == 0xff) throw std::runtime_error("activation dtype must be fp32 or bf16");
     if (s.size() == 4 && s[2] == 1 && s[3] == 1 && as_logits) {
       m.shape = {(uint64_t)s[0], (uint64_t)s[1]};  // logits (N, classes)
-    } else if (s.size() == 4 && h.layout() == Layout::NHWC) {
+    } else if (s.size() == 4 && t.layout() == Layout::NHWC) {
       m.shape = {(uint64_t)s[0], (uint64_t)s[2], (uint64_t)s[3], (uint64_t)s[1]};
       code |= kChannelsLast;
     } else {
       for (auto d : s) m.shape.push_back((uint64_t)d);
     }
     m.dtype = code;
-    m.data.assign(static_cast<const char*>(h.data()), h.nbytes());
+    m.data.resize(t.nbytes());  // (device tensors copy straight into the payload)
+    if (t.device().is_gpu())
+      gpu::copy(m.data.data(), t.data(), t.nbytes(), 1);
+    else
+      std::memcpy(m.data.data(), t.data(), t.nbytes());
     if (cfg_.codec == "zlib" || cfg_.codec == "zstd") {
       const Codec c = cfg_.codec == "zlib" ? CODEC_ZLIB : CODEC_ZSTD;
       m.data = compress(m.data, c, 3);
