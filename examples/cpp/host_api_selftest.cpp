@@ -74,6 +74,20 @@ static void test_bf16_json_tensor() {
   CHECK(g.data() == p0 && g.numel() == 4);  // grow-only: no reallocation when smaller
   g.ensure({8, 8}, DType::F32, Device::cpu());
   CHECK(g.numel() == 64);
+  // slices share the storage at a byte offset (parameter arenas)
+  Tensor flat = Tensor::from_host(std::vector<float>{0, 1, 2, 3, 4, 5, 6, 7}, {8}, Device::cpu());
+  Tensor s1 = flat.slice(4 * 4, {2, 2}, DType::F32);
+  CHECK(s1.data() == static_cast<char*>(flat.data()) + 16);
+  CHECK((s1.to_host_f32() == std::vector<float>{4, 5, 6, 7}));
+  s1.ptr<float>()[0] = 40.f;
+  CHECK(flat.to_host_f32()[4] == 40.f);
+  bool threw = false;
+  try {
+    flat.slice(6 * 4, {4}, DType::F32);  // runs past the storage
+  } catch (const std::out_of_range&) {
+    threw = true;
+  }
+  CHECK(threw);
 }
 
 static Sequential small_model(bool with_bn) {
