@@ -1025,12 +1025,17 @@ def prewarm_tickets(device, slots=("loss",)):
 
 
 # producer statistics slabs of at most this many rows are handed to the consumers raw (they merge
-# the rows in their prologue, norm.hip read_stats) instead of paying a reduce launch
+# the rows in their prologue, norm.hip read_stats) instead of paying a reduce launch — while the
+# rows x channels every consumer workgroup merges stays small (a wide slab's merge would cost the
+# consumer more than the launch it saves)
 _RAW_STAT_ROWS = 16
+_RAW_STAT_ELEMS = 4096
 
 
 def _raw_stats(mode, slab, rows):
     if not 2 <= rows <= _RAW_STAT_ROWS or getattr(slab, "_stat_no_raw", False):
+        return None
+    if rows * slab.shape[-1] > _RAW_STAT_ELEMS:
         return None
     return Stats(slab, rows if mode == 0 else -rows, mode)
 
