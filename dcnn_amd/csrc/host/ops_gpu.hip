@@ -250,7 +250,9 @@ ConvRouteGeom route_geom(const ConvShape& s, int g1s_mode) {
 // Weight-gradient split-K partials: while a backward is open (begin/end_deferred_reduce) every
 // slab is a buffer of its own, queued, and summed into its gradient by ONE batched launch at the
 // end of the backward (multi_splitk_reduce, kMaxRed slabs per launch) instead of one reduce per
-// layer; outside it, the shared workspace and an immediate reduce.
+// layer; outside it, the shared workspace and an immediate reduce. (Like the scratch workspaces,
+// the queue is process state: one thread drives a process's GPU backend — the trainer, or a
+// pipeline stage's event loop.)
 struct PendingRed {
   Tensor slab;
   float* out;
