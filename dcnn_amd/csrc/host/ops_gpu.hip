@@ -574,9 +574,6 @@ void dense_wgrad(const void* dy, const void* x, float* gw, float* gb, int N, int
 
 // deterministic slab statistics: (pointer, parts) for bn_apply / bn_bwd_apply
 static std::pair<const float*, int> reduce_stats(int mode, const float* slab, int rows, int C) {
-  // a few raw producer rows go to the consumer as they are (norm.hip read_stats; ops/hip.py
-  // _RAW_STAT_ROWS / _RAW_STAT_ELEMS)
-  if (rows >= 2 && rows <= 16 && (long)rows * C <= 4096) return {slab, mode == 0 ? rows : -rows};
   const int parts = bn_stat_parts(rows);
   float* sums = static_cast<float*>(scratch(STAT_SUMS, (size_t)2 * C * 4));
   float* part = parts > 1 ? static_cast<float*>(scratch(STAT_PART, (size_t)parts * 3 * C * 4)) : nullptr;

@@ -257,24 +257,11 @@ __global__ void __launch_bounds__(64 * WAVES) bn_stat_reduce_kernel(const float*
 }
 
 // Statistics as the consumers see them: parts == 1 -> buf is the finished [2][C] result of
-// bn_stat_reduce; parts > 1 -> buf holds its [parts][3][C] level-1 partials (or, MODE 0, a
-// producer's raw Welford rows in the same format), merged here in part order (fixed:
-// deterministic); parts < -1 (MODE 1) -> a producer's -parts raw [2][C] sum rows, summed in row
-// order. A few raw rows are read directly instead of paying a reduce launch (ops/hip.py
-// stat_reduce). MODE 0 -> (mean, biased variance), MODE 1 -> (sum a, sum b).
+// bn_stat_reduce; parts > 1 -> buf holds its [parts][3][C] level-1 partials, merged here in part
+// order (fixed: deterministic). MODE 0 -> (mean, biased variance), MODE 1 -> (sum a, sum b).
 template <int MODE>
 __device__ __forceinline__ void read_stats(const float* __restrict__ buf, int parts, int C, int c, float& s0,
                                            float& s1) {
-  if (MODE == 1 && parts < -1) {
-    float a = 0.f, b = 0.f;
-    for (int p = 0; p < -parts; ++p) {
-      a += buf[(long)p * 2 * C + c];
-      b += buf[(long)p * 2 * C + C + c];
-    }
-    s0 = a;
-    s1 = b;
-    return;
-  }
   if (parts <= 1) {
     s0 = buf[c];
     s1 = buf[C + c];

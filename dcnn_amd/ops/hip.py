@@ -239,10 +239,6 @@ def conv2d_fwd(x, w, bias, stride, pad, *, stats=False, residual=None, relu=Fals
         if stats:
             rows = K.hconv_stat_rows(N, H, W, 3 * Ci, Co, KH * KW, 1)
             slab = _empty((rows, 3, Co), F32, x.device)
-            # (always reduced: read raw, these fp32-output rows moved the ResNet-9 input gradient
-            # from 1.5e-3 to 6.6e-3 relative to the CPU model, tools/dbg raw_ab; the reduced
-            # statistics keep the split-precision path within its 3e-3 budget)
-            slab._stat_no_raw = True
             sums = _empty((2 * Co,), F32, x.device)  # zeroed in-kernel
         K.hconv(xs.data_ptr(), ws.data_ptr(), 0, _nbytes(xs), _nbytes(ws), N, H, W, 3 * Ci, Co, KH * KW * 3 * Ci,
                 [(t[0], t[1], t[3]) for t in _fwd_taps(3 * Ci, W, KH, KW, ph, pw)], ptr(bias), 0, ptr(slab),
@@ -976,9 +972,8 @@ def _ticket(device, C, slot="stat"):
 
 class Stats:
     """Per-channel statistics for the BN apply kernels: ``parts == 1`` -> ``buf`` is the finished
-    [2][C] result; ``parts > 1`` -> ``buf`` holds [parts][3][C] level-1 partials (or a producer's
-    raw Welford rows) that the consuming kernel merges in its prologue (norm.hip read_stats);
-    ``parts < -1`` (mode 1) -> ``buf`` holds a producer's -parts raw [2][C] sum rows. Used as a tensor (tests,
+    [2][C] result; ``parts > 1`` -> ``buf`` holds [parts][3][C] level-1 partials that the
+    consuming kernel merges in its prologue (norm.hip read_stats). Used as a tensor (tests,
     inspection) it materialises the finished [2][C] statistics (``final()``, torch ops: off the
     training hot path)."""
     __slots__ = ("buf", "parts", "mode", "_final")
@@ -992,7 +987,7 @@ class Stats:
         if self._final is None:
             p = self.buf.double()
             C = p.shape[2]
-            parts = abs(self.parts)
+            parts = self.parts
             if self.mode == 0:  # Chan merges in part order (as read_stats)
                 n, mean, m2 = p[0, 0].clone(), p[0, 1].clone(), p[0, 2].clone()
                 for k in range(1, parts):
@@ -1024,32 +1019,14 @@ def prewarm_tickets(device, slots=("loss",)):
         _ticket(torch.device(device), 0, slot=s)
 
 
-# producer statistics slabs of at most this many rows are handed to the consumers raw (they merge
-# the rows in their prologue, norm.hip read_stats) instead of paying a reduce launch — while the
-# rows x channels every consumer workgroup merges stays small (a wide slab's merge would cost the
-# consumer more than the launch it saves)
-_RAW_STAT_ROWS = 16
-_RAW_STAT_ELEMS = 4096
-
-
-def _raw_stats(mode, slab, rows):
-    if not 2 <= rows <= _RAW_STAT_ROWS or getattr(slab, "_stat_no_raw", False):
-        return None
-    if rows * slab.shape[-1] > _RAW_STAT_ELEMS:
-        return None
-    return Stats(slab, rows if mode == 0 else -rows, mode)
-
-
 def stat_reduce(mode, slab, rows, C, out):
     """Deterministic slab reduce (norm.hip bn_stat_reduce): mode 0 = Welford (count, mean, M2)
     tile triples -> (mean, biased var); mode 1 = (sum a, sum b) rows -> sums. Returns
-    :class:`Stats` (``out`` when one block covered all rows, else the partials buffer; the slab
-    itself when it has at most ``_RAW_STAT_ROWS`` rows)."""
+    :class:`Stats` (``out`` when one block covered all rows, else the partials buffer).
+    (Handing small slabs to the consumers raw instead measured no faster: the consumer prologue's
+    merge costs what the launch saves, `profiles/experiment_raw_stats_r4.md`.)"""
     if isinstance(slab, Stats):  # already folded inside the producing launch (statfold.h)
         return slab
-    raw = _raw_stats(mode, slab, rows)
-    if raw is not None:
-        return raw
     K = kernels()
     ny = K.bn_stat_parts(rows)
     part = _empty((ny, 3, C), F32, slab.device) if ny > 1 else None
@@ -1135,9 +1112,6 @@ def bn_bwd_apply_dual(dy, a, b):
 def stat_reduce_pair(mode, a, b, C):
     """Two independent forward/backward statistics reduces of the same C in ONE launch
     (norm.hip bn_stat_reduce2); ``a``/``b`` = (slab, rows, out). Returns two :class:`Stats`."""
-    raws = [_raw_stats(mode, slab, rows) for slab, rows, _ in (a, b)]
-    if raws[0] is not None or raws[1] is not None:
-        return tuple(r if r is not None else stat_reduce(mode, x[0], x[1], C, x[2]) for r, x in zip(raws, (a, b)))
     K = kernels()
     res, ptrs = [], []
     for slab, rows, out in (a, b):
