@@ -180,7 +180,7 @@ json::Value PipelineCoordinator::stage_config(int i) const {
   c["prev_stage_endpoint"] = i > 0 ? endpoint_json(stages_[i - 1].host(), stages_[i - 1].port(), names_[i - 1]) : json::Value();
   c["coordinator_endpoint"] = endpoint_json(o_.host, port_, "coordinator");
   c["device"] = o_.stage_devices[i];
-  c["transport"] = "message";
+  c["transport"] = o_.transport;
   c["codec"] = o_.codec;
   c["compute_dtype"] = "auto";
   c["seed"] = o_.seed ? json::Value(*o_.seed + i) : json::Value();

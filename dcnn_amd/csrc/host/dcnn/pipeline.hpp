@@ -114,6 +114,20 @@ class PipelineStage {
     std::vector<int64_t> shape;
   };
   std::map<uint64_t, OutKind> out_kind_;
+  // transport "ipc" (same node, GPU stages): stage-to-stage tensors stay on the device. The sender
+  // copies into its exported buffer for (peer, micro-batch) and sends only the 64-byte handle; the
+  // receiver maps the buffer once and copies out on arrival. A (peer, micro-batch) buffer is
+  // rewritten only in a later step / batch, after the receiver has consumed it (the coordinator
+  // joins every micro-batch before the next one starts).
+  struct IpcSlot {
+    void* ptr = nullptr;
+    size_t bytes = 0;
+    std::string handle;
+  };
+  std::map<std::pair<std::string, uint64_t>, IpcSlot> ipc_out_;
+  std::vector<void*> ipc_retired_;                  // outgrown exports (a peer may still map them)
+  mutable std::map<std::string, void*> ipc_in_;     // handle -> this process's mapping
+  void release_ipc();
   long n_fwd_ = 0, n_bwd_ = 0, n_upd_ = 0;
   double fwd_ms_ = 0, bwd_ms_ = 0;
   std::thread beat_;
@@ -151,6 +165,7 @@ struct CoordinatorOptions {
   std::vector<std::string> stage_devices;  // per stage ("CPU", "GPU:0", ...); default CPU
   std::string loss = "softmax_crossentropy";
   std::string codec = "none";               // inline payload compression of the stages' sends
+  std::string transport = "message";        // "ipc": GPU stage-to-stage tensors via device IPC buffers
   bool grad_scale_mean = true;              // micro-batch gradients * 1 / num_microbatches
   double timeout_s = 120.0;
   double heartbeat_s = 0.0;                 // > 0: stages beat every heartbeat_s ...

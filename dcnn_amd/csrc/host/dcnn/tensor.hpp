@@ -54,6 +54,12 @@ void empty_cache();     // synchronise and return every cached block to the driv
 void copy(void* dst, const void* src, size_t nbytes, int kind);  // 0 h2d, 1 d2h, 2 d2d
 void zero(void* p, size_t nbytes);                                // stream-ordered memset
 void synchronize();
+// inter-process device buffers (same node): a dedicated allocation + its 64-byte IPC handle
+constexpr size_t kIpcHandleBytes = 64;
+void* ipc_alloc(size_t nbytes, void* handle_out);
+void ipc_free(void* p);
+void* ipc_open(const void* handle);  // map a peer process's buffer into this one
+void ipc_close(void* p);
 }  // namespace gpu
 
 class Storage {

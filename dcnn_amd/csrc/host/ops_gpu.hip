@@ -128,6 +128,35 @@ void copy(void* dst, const void* src, size_t nbytes, int kind) {
 }
 void zero(void* p, size_t nbytes) { HOST_HIP_CHECK(hipMemsetAsync(p, 0, nbytes, nullptr)); }
 void synchronize() { HOST_HIP_CHECK(hipDeviceSynchronize()); }
+
+// Inter-process buffers (pipeline transport "ipc"): a whole hipMalloc allocation (IPC exports the
+// base of an allocation, so these never come from the caching pool) and its 64-byte handle.
+void* ipc_alloc(size_t nbytes, void* handle_out) {
+  static_assert(sizeof(hipIpcMemHandle_t) == kIpcHandleBytes, "IPC handle size");
+  void* p = nullptr;
+  HOST_HIP_CHECK(hipMalloc(&p, nbytes));
+  hipIpcMemHandle_t h;
+  if (hipIpcGetMemHandle(&h, p) != hipSuccess) {
+    (void)hipGetLastError();
+    (void)hipFree(p);
+    throw std::runtime_error("hipIpcGetMemHandle failed (the host must allow dmabuf IPC)");
+  }
+  std::memcpy(handle_out, &h, sizeof h);
+  return p;
+}
+void ipc_free(void* p) {
+  if (p != nullptr) (void)hipFree(p);
+}
+void* ipc_open(const void* handle) {
+  hipIpcMemHandle_t h;
+  std::memcpy(&h, handle, sizeof h);
+  void* p = nullptr;
+  HOST_HIP_CHECK(hipIpcOpenMemHandle(&p, h, hipIpcMemLazyEnablePeerAccess));
+  return p;
+}
+void ipc_close(void* p) {
+  if (p != nullptr) (void)hipIpcCloseMemHandle(p);
+}
 }  // namespace gpu
 
 namespace gpu_ops {

@@ -18,6 +18,10 @@ namespace dcnn {
 
 namespace {
 constexpr uint8_t kChannelsLast = 0x10;  // dtype flag: NHWC physical buffer of an NCHW tensor
+// dtype flag: the payload is an IPC reference (64-byte handle + byte count), not the bytes
+// (transport "ipc", native stages only)
+constexpr uint8_t kIpcRef = 0x20;
+constexpr size_t kIpcRefBytes = gpu::kIpcHandleBytes + sizeof(uint64_t);
 constexpr uint64_t kFullState = 1;        // SEND_PARAMS "full" / LOAD_PARAMS micro-batch id
 
 std::optional<Endpoint> parse_endpoint(const json::Value* v) {
@@ -107,7 +111,22 @@ std::unique_ptr<Optimizer> create_optimizer(const json::Value& cfg) {
 
 PipelineStage::PipelineStage(Communicator* comm, bool verbose) : comm_(comm), verbose_(verbose), id_(comm->id()) {}
 
-PipelineStage::~PipelineStage() { stop_heartbeat(); }
+PipelineStage::~PipelineStage() {
+  stop_heartbeat();
+  try {
+    release_ipc();
+  } catch (...) {
+  }
+}
+
+void PipelineStage::release_ipc() {
+  for (auto& kv : ipc_in_) gpu::ipc_close(kv.second);
+  ipc_in_.clear();
+  for (auto& kv : ipc_out_) gpu::ipc_free(kv.second.ptr);
+  ipc_out_.clear();
+  for (void* p : ipc_retired_) gpu::ipc_free(p);
+  ipc_retired_.clear();
+}
 
 void PipelineStage::run(int poll_ms) {
   running_ = true;
@@ -265,10 +284,12 @@ void PipelineStage::process(Message& m) {
 
 void PipelineStage::configure(const std::string& text) {
   cfg_ = StageConfig::parse(text);
-  if (cfg_.transport != "message")
-    throw std::runtime_error("native stage: transport '" + cfg_.transport + "' not supported (inline tensors only)");
+  if (cfg_.transport != "message" && cfg_.transport != "ipc")
+    throw std::runtime_error("native stage: transport '" + cfg_.transport + "' not supported ('message' | 'ipc')");
   stop_heartbeat();
   dev_ = Device::parse(cfg_.device);
+  if (cfg_.transport == "ipc" && !dev_.is_gpu()) throw std::runtime_error("native stage: transport 'ipc' needs a GPU stage");
+  release_ipc();  // (a redeploy may change the neighbours)
   if (dev_.is_gpu()) gpu::set_device(dev_.index);
   model_ = std::make_unique<Sequential>(Sequential::load_from_config(cfg_.model_config));
   model_->set_device(dev_);
@@ -332,6 +353,22 @@ Tensor PipelineStage::decode(Message& m) const {
     case 1: dt = DType::BF16; break;
     default: throw std::runtime_error("activation payloads must be fp32 or bf16");
   }
+  if (code & kIpcRef) {
+    // a peer stage's device buffer: map it once, copy out now (the sender rewrites it only after
+    // this stage has answered for the micro-batch)
+    if (!dev_.is_gpu() || m.data.size() != kIpcRefBytes) throw std::runtime_error("malformed IPC tensor reference");
+    Tensor t = Tensor::empty(shape, dt, dev_, layout);
+    uint64_t nbytes = 0;
+    std::memcpy(&nbytes, m.data.data() + gpu::kIpcHandleBytes, sizeof nbytes);
+    if (nbytes != t.nbytes()) throw std::runtime_error("IPC tensor size does not match its shape");
+    const std::string key(m.data.data(), gpu::kIpcHandleBytes);
+    auto it = ipc_in_.find(key);
+    if (it == ipc_in_.end()) it = ipc_in_.emplace(key, gpu::ipc_open(key.data())).first;
+    gpu::copy(t.data(), it->second, t.nbytes(), 2);
+    gpu::synchronize();
+    if (t.rank() == 2) t = t.view({shape[0], shape[1], 1, 1}, Layout::NCHW);
+    return t;
+  }
   // a GPU stage's own activation form (bf16 NHWC) goes straight from the payload to the device
   const bool direct = dev_.is_gpu() && dt == DType::BF16 && layout == Layout::NHWC;
   Tensor t = Tensor::empty(shape, dt, direct ? dev_ : Device::cpu(), layout);
@@ -363,6 +400,23 @@ void PipelineStage::send_tensor(const std::string& to, uint16_t cmd, uint64_t mb
       for (auto d : s) m.shape.push_back((uint64_t)d);
     }
     m.dtype = code;
+    if (cfg_.transport == "ipc" && t.device().is_gpu() && (to == "next_stage" || to == "prev_stage")) {
+      IpcSlot& slot = ipc_out_[{to, mb}];
+      if (slot.bytes < t.nbytes()) {
+        if (slot.ptr != nullptr) ipc_retired_.push_back(slot.ptr);
+        slot.handle.assign(gpu::kIpcHandleBytes, '\0');
+        slot.ptr = gpu::ipc_alloc(t.nbytes(), slot.handle.data());
+        slot.bytes = t.nbytes();
+      }
+      gpu::copy(slot.ptr, t.data(), t.nbytes(), 2);
+      gpu::synchronize();  // complete before the peer, another process, reads it
+      const uint64_t nbytes = t.nbytes();
+      m.dtype = code | kIpcRef;
+      m.data.assign(slot.handle);
+      m.data.append(reinterpret_cast<const char*>(&nbytes), sizeof nbytes);
+      comm_->send(std::move(m));
+      return;
+    }
     m.data.resize(t.nbytes());  // (device tensors copy straight into the payload)
     if (t.device().is_gpu())
       gpu::copy(m.data.data(), t.data(), t.nbytes(), 1);

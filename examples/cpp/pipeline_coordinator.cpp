@@ -7,13 +7,15 @@
 //        [--microbatches 4] [--batch 64] [--steps 20] [--optimizer adam|sgd] [--lr 1e-3]
 //        [--momentum 0.9] [--devices CPU,CPU | --device GPU:0] [--loss softmax_crossentropy]
 //        [--data-x x.f32 --data-y y.i64] [--input C,H,W] [--classes K] [--save out]
-//        [--heartbeat S] [--json] [--bench W]
+//        [--heartbeat S] [--transport message|ipc] [--json] [--bench W]
 //
 // --spawn N starts N local native workers (this program never touches the GPU itself, so starting
 // them is safe). --init loads a saved model (path.json + path.bin [+ .bnstats]) whose weights are
 // pushed to the stages. --data-x / --data-y are raw fp32 NCHW images and int64 labels, batch after
 // batch; without them a learnable synthetic set of --input / --classes is used. --json prints one
 // JSON line per step; --bench W times the steps after W untimed warm-up steps (images/sec).
+// --transport ipc (GPU stages on one node): stage-to-stage activations and gradients stay on the
+// device (HIP IPC buffers); only their handles travel in the messages.
 // Reference parity: examples/semi_async_pipeline_coordinator.cpp, sync_pipeline_coordinator.cpp,
 // coordinator_tiny_imagenet.cpp; include/pipeline/distributed_coordinator.hpp.
 #include <signal.h>
@@ -99,6 +101,7 @@ std::vector<char> read_file(const std::string& path) {
 int main(int argc, char** argv) {
   std::string workers, model_name = "mnist_cnn", config_path, init, schedule = "semi_async", opt_name = "adam";
   std::string devices, loss_name = "softmax_crossentropy", data_x, data_y, save, input = "1,28,28";
+  std::string transport = "message";
   int spawn = 0, microbatches = 4, batch = 64, steps = 20, classes = 10, bench = -1;
   float lr = 1e-3f, momentum = 0.f;
   double heartbeat = 0;
@@ -132,6 +135,7 @@ int main(int argc, char** argv) {
     else if (k == "--save") save = v;
     else if (k == "--heartbeat") heartbeat = std::atof(v.c_str());
     else if (k == "--bench") bench = std::atoi(v.c_str());
+    else if (k == "--transport") transport = v;
     else {
       std::fprintf(stderr, "unknown option %s\n", k.c_str());
       return 2;
@@ -186,6 +190,7 @@ int main(int argc, char** argv) {
     o.num_microbatches = microbatches;
     o.loss = loss_name;
     o.heartbeat_s = heartbeat;
+    o.transport = transport;
     if (!devices.empty()) {
       o.stage_devices = split_list(devices);
       if (o.stage_devices.size() == 1) o.stage_devices.assign(eps.size(), o.stage_devices[0]);
@@ -268,9 +273,10 @@ int main(int argc, char** argv) {
       coord.barrier();
       const double sec = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
       std::printf("{\"metric\": \"images/sec pipeline training (native coordinator + %d stages, %s, %d micro-batches)\", "
-                  "\"value\": %.1f, \"ms_per_step\": %.3f, \"batch\": %d, \"steps\": %d, \"loss\": %.4f}\n",
+                  "\"value\": %.1f, \"ms_per_step\": %.3f, \"batch\": %d, \"steps\": %d, \"loss\": %.4f, "
+                  "\"transport\": \"%s\"}\n",
                   coord.num_stages(), schedule.c_str(), microbatches, (double)batch * steps / sec, 1e3 * sec / steps,
-                  batch, steps, last);
+                  batch, steps, last, transport.c_str());
     }
     for (const auto& line : coord.print_profiling()) std::fprintf(stderr, "%s", line.c_str());
     if (!save.empty()) {

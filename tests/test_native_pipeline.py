@@ -200,6 +200,29 @@ def test_native_coordinator_gpu_stages(worker_bin):
     assert np.mean([s["loss"] for s in steps[-3:]]) < np.mean([s["loss"] for s in steps[:3]])
 
 
+@pytest.mark.gpu
+def test_native_coordinator_ipc_transport_matches_messages(worker_bin):
+    """Transport "ipc": stage-to-stage tensors stay on the device (HIP IPC buffers, only handles in
+    the messages). The same bytes arrive as with inline payloads, so every step's loss is the same."""
+    import json
+    losses = {}
+    for transport in ("message", "ipc"):
+        out = subprocess.run([COORD, "--spawn", "3", "--model", "resnet9_cifar10", "--device", "GPU:0", "--input",
+                              "3,32,32", "--classes", "10", "--batch", "64", "--microbatches", "4", "--steps", "6",
+                              "--schedule", "1f1b", "--transport", transport, "--json"],
+                             capture_output=True, text=True, timeout=240)
+        assert out.returncode == 0, out.stderr[-2000:]
+        losses[transport] = [json.loads(l)["loss"] for l in out.stdout.splitlines() if l.startswith("{")]
+    assert len(losses["ipc"]) == 6 and all(np.isfinite(losses["ipc"]))
+    np.testing.assert_allclose(losses["ipc"], losses["message"], rtol=1e-6)
+
+
+def test_native_ipc_transport_needs_gpu_stages(worker_bin):
+    out = subprocess.run([COORD, "--spawn", "2", "--steps", "1", "--transport", "ipc"], capture_output=True, text=True,
+                         timeout=60)
+    assert out.returncode == 1 and "needs a GPU stage" in out.stderr
+
+
 def test_native_coordinator_rejects_bad_arguments(worker_bin):
     out = subprocess.run([COORD, "--workers", "", "--steps", "0"], capture_output=True, text=True, timeout=30)
     assert out.returncode == 1 and "no workers" in out.stderr
