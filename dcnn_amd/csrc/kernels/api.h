@@ -73,7 +73,9 @@ void hconv(HConvArgs a, hipStream_t s);
 int hconv_splits(int NB, int H, int W, int Cs, int N, int ntaps);
 int hconv_tiles(int NB, int H, int W, int Cs, int N, int ntaps);
 int hconv_tile_elems(int NB, int H, int W, int Cs, int N, int ntaps);
+int hconv_split_target();
 void hconv_set_split_target(int t);  // workgroups the split-K decision aims for (0: never split)
+void hconv_set_split_min_work(int w);  // least taps x 64-channel chunks per split (default 4)
 void bn_set_vectorised(int on);   // bf16 BatchNorm apply passes on the vectorised kernels (default on)
 bool hconv_supported(int NB, int H, int W, int Cs, int N, int ntaps);
 int hconv_stat_rows(int NB, int H, int W, int Cs, int N, int ntaps, int f32out);

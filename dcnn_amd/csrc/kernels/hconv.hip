@@ -495,9 +495,16 @@ bool hconv_supported(int NB, int H, int W, int Cs, int N, int ntaps) {
 }
 
 // target workgroup count of the split-K decision; 0 = never split (test hook)
-static int g_split_target = 512;
+// split-K target workgroups (hconv and the persistent hconv3): 256 = one per CU. 512 (two per CU)
+// split the 8x8 / 4x4 / 16x16 layers twice as often: more fp32 partials and last-arriver merges
+// for no extra overlap. bench.py img/s, 512 -> 256 (profiles/split_target_r4.md): ResNet-18 b64
+// 32.3k -> 35.0k, b128 54.2k -> 57.7k, b256 81.8k -> 83.5k; ResNet-50 b256 26.1k -> 26.2k, b32
+// 7.85k -> 7.82k.
+static int g_split_target = 256;
+static int g_split_min_work = 4;  // taps x 64-channel chunks a split keeps at least
 int hconv_split_target() { return g_split_target; }
 void hconv_set_split_target(int t) { g_split_target = t < 0 ? 0 : t; }
+void hconv_set_split_min_work(int w) { g_split_min_work = w < 1 ? 1 : w; }
 
 int hconv_tiles(int NB, int H, int W, int Cs, int N, int ntaps) {
   H3Plan pl;
@@ -528,7 +535,7 @@ int hconv_splits(int NB, int H, int W, int Cs, int N, int ntaps) {
   const long tiles = hconv_tiles(NB, H, W, Cs, N, ntaps);
   const int nchunk = Cs / 64, target = hconv_split_target();
   int s = 1;
-  while (target > 0 && tiles * s < target && nchunk % (2 * s) == 0 && (nchunk / (2 * s)) * ntaps >= 4) s *= 2;
+  while (target > 0 && tiles * s < target && nchunk % (2 * s) == 0 && (nchunk / (2 * s)) * ntaps >= g_split_min_work) s *= 2;
   return s;
 }
 

@@ -675,9 +675,9 @@ bool hconv3_plan(int NB, int H, int W, int Cs, int N, int ntaps, H3Plan* pl) {
   pl->tpi = GX > 1 ? 1 : (W / TW) * (H / TH);
   pl->tiles_m = NB * H * W / (TH * TW);
   pl->tiles_n = N / BN;
-  // split-K over 32-channel chunks until the grid holds the target workgroup count (two resident
-  // per CU); a split may hold a single chunk (then every workgroup runs one item), at most 8
-  // splits (the last arriver reads every partial back)
+  // split-K over 32-channel chunks until the work items reach the target count (hconv.hip
+  // g_split_target: one per CU); a split may hold a single chunk (then every workgroup runs one
+  // item), at most 8 splits (the last arriver reads every partial back)
   const long tiles = (long)pl->tiles_m * pl->tiles_n;
   const int nchunk = Cs / 32, target = hconv_split_target();
   int s = 1;

@@ -142,13 +142,14 @@ def test_hconv3_split_k_matches_unsplit(hip):
     w = (torch.randn(Co, C, 3, 3) / math.sqrt(9 * C)).cuda().bfloat16().contiguous(memory_format=CL)
     b = torch.randn(Co).cuda()
     outs = []
+    prev = K.hconv_split_target()
     try:
         for target in (512, 512, 0):
             K.hconv_set_split_target(target)
             y, part = hip.conv2d_fwd(x, w, b, (1, 1), (1, 1), stats=True, relu=True)
             outs.append((y.clone(), hip.bn_stats(y, part).clone()))
     finally:
-        K.hconv_set_split_target(512)
+        K.hconv_set_split_target(prev)
     (y1, s1), (y2, s2), (y0, s0) = outs
     assert torch.equal(y1, y2) and torch.equal(s1, s2)
     assert rel_err(y1, y0) < 5e-3 and rel_err(s1, s0) < 1e-3

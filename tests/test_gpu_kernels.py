@@ -708,6 +708,7 @@ def test_hconv_split_k_matches_unsplit(hip, case):
     dy = torch.randn(N, Co, H, W).cuda().to(torch.bfloat16).contiguous(memory_format=CL)
     wt = hip.conv_weight_t(w)
     outs = []
+    prev = K.hconv_split_target()
     try:
         for target in (512, 512, 0):
             K.hconv_set_split_target(target)
@@ -716,7 +717,7 @@ def test_hconv_split_k_matches_unsplit(hip, case):
             dx = hip.conv2d_dgrad(dy, wt, x.shape, (1, 1), (1, 1))
             outs.append((y.clone(), st.clone(), dx.clone()))
     finally:
-        K.hconv_set_split_target(512)
+        K.hconv_set_split_target(prev)
     (y1, s1, d1), (y2, s2, d2), (y0, s0, d0) = outs
     assert torch.equal(y1, y2) and torch.equal(s1, s2) and torch.equal(d1, d2)
     ref = F.relu(F.conv2d(x.float().cpu(), w.float().cpu(), b.cpu(), 1, 1))
@@ -744,6 +745,7 @@ def test_hconv_fp32_concat_accuracy(hip, case):
     dyg = dy.float().cuda().contiguous(memory_format=CL)
     wt = hip.conv_weight_t(wg, dtype=torch.float32)
     res = []
+    prev = K.hconv_split_target()
     try:
         for target in (512, 0):
             K.hconv_set_split_target(target)
@@ -751,7 +753,7 @@ def test_hconv_fp32_concat_accuracy(hip, case):
             dx = hip.conv2d_dgrad(dyg, wt, x.shape, (1, 1), (1, 1))
             res.append((y, dx))
     finally:
-        K.hconv_set_split_target(512)
+        K.hconv_set_split_target(prev)
     for y, dx in res:
         assert rel_err(y.double(), ref) < 2e-5, rel_err(y.double(), ref)
         assert rel_err(dx.double(), dref) < 2e-5, rel_err(dx.double(), dref)
