@@ -662,11 +662,14 @@ void t2_tile(int M, int N, int* bm, int* bn) {
   *bn = (N >= 128 && M < 128) ? 128 : 64;
 }
 
+static int g_t2_target = 512;  // split-K target workgroups of the gathered weight gradient
+void gemm_t2_set_split_target(int t) { g_t2_target = t < 1 ? 1 : t; }
+
 int gemm_t2_splits(int M, int N, int P) {
   int bm, bn;
   t2_tile(M, N, &bm, &bn);
   const long tiles = (long)((M + bm - 1) / bm) * ((N + bn - 1) / bn);
-  long splits = (512 + tiles - 1) / tiles;
+  long splits = (g_t2_target + tiles - 1) / tiles;
   // at least 256 reduction pixels per split (1024: ResNet-50 b32 7.9k -> 7.2k img/s,
   // profiles/wgrad_splits_r3.md)
   constexpr long min_k = 256;

@@ -525,7 +525,8 @@ bool hwgrad_supported(int NB, int H, int W, int Cs, int Co, int ntaps) {
   return (long)NB * H * W * (Cs > Co ? Cs : Co) * 2 < (1l << 31);
 }
 
-static constexpr int kHwTargetBlocks = 256;  // split-K target: one workgroup per CU
+static int kHwTargetBlocks = 256;  // split-K target: one workgroup per CU
+void hwgrad_set_split_target(int t) { kHwTargetBlocks = t < 1 ? 1 : t; }
 
 // number of split-K partial slabs (the caller sizes the slab [splits][Co][ntaps*Cs])
 int hwgrad_splits(int NB, int H, int W, int Cs, int Co) {
