@@ -120,6 +120,7 @@ PYBIND11_MODULE(_kernels, m) {
   m.def("hconv_split_target", &hconv_split_target);
   m.def("gemm_t2_set_split_target", &gemm_t2_set_split_target);
   m.def("hwgrad_set_split_target", &hwgrad_set_split_target);
+  m.def("hconv3_set_max_splits", &hconv3_set_max_splits);
   m.def("bn_set_vectorised", &bn_set_vectorised);
   m.def("hconv_tile_elems", &hconv_tile_elems);
   m.def("hconv3_set_grid_cap", &hconv3_set_grid_cap);

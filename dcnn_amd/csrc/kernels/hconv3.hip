@@ -649,6 +649,8 @@ static unsigned long long* g_h3_stamps = nullptr;
 void hconv3_set_stamps(uintptr_t p) { g_h3_stamps = reinterpret_cast<unsigned long long*>(p); }
 static int g_h3_grid_cap = 0;  // test hook: at most this many persistent workgroups (0: resident count)
 void hconv3_set_grid_cap(int n) { g_h3_grid_cap = n < 0 ? 0 : n; }
+static int g_h3_max_splits = 8;  // tuning hook: split-K slices per tile at most
+void hconv3_set_max_splits(int n) { g_h3_max_splits = n < 1 ? 1 : n; }
 
 // tile plan for a 3x3 stride-1 conv of NB x H x W pixels, Cs input / N output channels
 bool hconv3_plan(int NB, int H, int W, int Cs, int N, int ntaps, H3Plan* pl) {
@@ -681,7 +683,7 @@ bool hconv3_plan(int NB, int H, int W, int Cs, int N, int ntaps, H3Plan* pl) {
   const long tiles = (long)pl->tiles_m * pl->tiles_n;
   const int nchunk = Cs / 32, target = hconv_split_target();
   int s = 1;
-  while (tiles * s < target && nchunk % (2 * s) == 0 && s < 8) s *= 2;
+  while (tiles * s < target && nchunk % (2 * s) == 0 && s < g_h3_max_splits) s *= 2;
   pl->splits = s;
   return true;
 }
