@@ -212,6 +212,7 @@ PYBIND11_MODULE(_kernels, m) {
   m.attr("ROUTE_G1S") = (int)ROUTE_G1S;
   m.def("g1s_rows", &g1s_rows);
   m.def("g1s_enable", &g1s_enable);
+  m.def("g1s_set_waves_per_simd", &g1s_set_waves_per_simd);
   m.def("g1s_gen_rows", &g1s_gen_rows);
   m.def("g1s_gen", [](uintptr_t X, uintptr_t Wt, uintptr_t Y, int NB, int GH, int GW, int N, int Kc, int ldw,
                       std::vector<std::array<int, 3>> taps, int H, int W, int OHo, int OWo, int OS, int ORY, int ORX,

@@ -90,7 +90,9 @@ struct G1sArgs {
 // per-instance shape: TJ 16-pixel subtiles per tile, OCC waves per SIMD the registers allow
 // (K = 64: 32-pixel tiles keep the forward at ~150 VGPRs, three waves per SIMD to hide the
 // load latency behind each other's epilogues)
-static int g1s_occ_rt(int K, int mode) { (void)K; (void)mode; return 2; }  // waves per SIMD
+static int g_g1s_wps = 2;  // target waves per SIMD of the pixel-range split (tuning hook)
+void g1s_set_waves_per_simd(int w) { g_g1s_wps = w < 1 ? 1 : w; }
+static int g1s_occ_rt(int K, int mode) { (void)K; (void)mode; return g_g1s_wps; }  // waves per SIMD
 // (K = 32: one MFMA k step per subtile; weights 16 VGPRs)
 constexpr int kG1sTile = 32;  // pixels per tile (16 * TJ)
 // weights in LDS (shared by the workgroup's 4 waves) instead of VGPRs: K >= 256, and the K = 128
