@@ -90,7 +90,10 @@ struct G1sArgs {
 // per-instance shape: TJ 16-pixel subtiles per tile, OCC waves per SIMD the registers allow
 // (K = 64: 32-pixel tiles keep the forward at ~150 VGPRs, three waves per SIMD to hide the
 // load latency behind each other's epilogues)
-static int g_g1s_wps = 2;  // target waves per SIMD of the pixel-range split (tuning hook)
+// target waves per SIMD of the pixel-range split (tuning hook): 1 = longer pixel ranges, half
+// the statistics rows. bench.py img/s, 2 -> 1 (profiles/split_target_r4.md): ResNet-50 b256
+// 26.04k -> 26.35k, b32 7.80k -> 7.87k; ResNet-18 b64 / b256 unchanged.
+static int g_g1s_wps = 1;
 void g1s_set_waves_per_simd(int w) { g_g1s_wps = w < 1 ? 1 : w; }
 static int g1s_occ_rt(int K, int mode) { (void)K; (void)mode; return g_g1s_wps; }  // waves per SIMD
 // (K = 32: one MFMA k step per subtile; weights 16 VGPRs)
