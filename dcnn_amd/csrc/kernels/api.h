@@ -77,7 +77,7 @@ int hconv_split_target();
 void gemm_t2_set_split_target(int t);  // test / tuning hook (default 512)
 void hwgrad_set_split_target(int t);   // test / tuning hook (default 256)
 void hconv3_set_max_splits(int n);     // tuning hook (default 8)
-void g1s_set_waves_per_simd(int w);    // tuning hook (default 1)
+void g1s_set_waves_per_simd(int w);    // tuning hook (default 2)
 void hconv_set_split_target(int t);  // workgroups the split-K decision aims for (0: never split)
 void hconv_set_split_min_work(int w);  // least taps x 64-channel chunks per split (default 4)
 void bn_set_vectorised(int on);   // bf16 BatchNorm apply passes on the vectorised kernels (default on)

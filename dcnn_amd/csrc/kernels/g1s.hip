@@ -90,10 +90,11 @@ struct G1sArgs {
 // per-instance shape: TJ 16-pixel subtiles per tile, OCC waves per SIMD the registers allow
 // (K = 64: 32-pixel tiles keep the forward at ~150 VGPRs, three waves per SIMD to hide the
 // load latency behind each other's epilogues)
-// target waves per SIMD of the pixel-range split (tuning hook): 1 = longer pixel ranges, half
-// the statistics rows. bench.py img/s, 2 -> 1 (profiles/split_target_r4.md): ResNet-50 b256
-// 26.04k -> 26.35k, b32 7.80k -> 7.87k; ResNet-18 b64 / b256 unchanged.
-static int g_g1s_wps = 1;
+// target waves per SIMD of the pixel-range split (tuning hook). 1 measured ~1% faster on
+// ResNet-50 (profiles/split_target_r4.md) but broke the fused backward-BatchNorm statistics of
+// the ResNet-50 data gradients (tests/test_gpu_model.py::test_bwd_bn_fusion_matches_unfused):
+// kept at 2 until that is understood.
+static int g_g1s_wps = 2;
 void g1s_set_waves_per_simd(int w) { g_g1s_wps = w < 1 ? 1 : w; }
 static int g1s_occ_rt(int K, int mode) { (void)K; (void)mode; return g_g1s_wps; }  // waves per SIMD
 // (K = 32: one MFMA k step per subtile; weights 16 VGPRs)
