@@ -90,10 +90,7 @@ struct G1sArgs {
 // per-instance shape: TJ 16-pixel subtiles per tile, OCC waves per SIMD the registers allow
 // (K = 64: 32-pixel tiles keep the forward at ~150 VGPRs, three waves per SIMD to hide the
 // load latency behind each other's epilogues)
-// target waves per SIMD of the pixel-range split (tuning hook). 1 measured ~1% faster on
-// ResNet-50 (profiles/split_target_r4.md) but broke the fused backward-BatchNorm statistics of
-// the ResNet-50 data gradients (tests/test_gpu_model.py::test_bwd_bn_fusion_matches_unfused):
-// kept at 2 until that is understood.
+// target waves per SIMD of the pixel-range split (tuning hook; profiles/split_target_r4.md)
 static int g_g1s_wps = 2;
 void g1s_set_waves_per_simd(int w) { g_g1s_wps = w < 1 ? 1 : w; }
 static int g1s_occ_rt(int K, int mode) { (void)K; (void)mode; return g_g1s_wps; }  // waves per SIMD
@@ -290,8 +287,12 @@ __global__ void __launch_bounds__(256, OCC) g1s_kernel(G1sArgs p) {
       asm volatile("" : "+v"(wl_off));
 #pragma unroll
       for (int c = 0; c < NC; ++c) {
+        // the next tile's first chunk goes to the buffer its first chunk is read from, bq[0]:
+        // with an even chunk count that is the other buffer, loaded during this tile's last
+        // chunk; with one chunk (K = 128) it is the buffer being read, reloaded after the MFMAs
+        // below (loading it into bq[1] left tile t + 1 computing on tile t's operands)
         if (c + 1 < NC) load_chunk(bq[(c + 1) & 1], t, c + 1);
-        else if (t + 1 < t1) load_chunk(bq[(c + 1) & 1], t + 1, 0);
+        else if (NC % 2 == 0 && t + 1 < t1) load_chunk(bq[(c + 1) & 1], t + 1, 0);
 #pragma unroll
         for (int u = 0; u < 4; ++u)
 #pragma unroll
@@ -302,6 +303,8 @@ __global__ void __launch_bounds__(256, OCC) g1s_kernel(G1sArgs p) {
               acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(av, bq[c & 1][j][u], acc[i][j], 0, 0, 0);
           }
       }
+      static_assert(NC == 1 || NC % 2 == 0, "chunk ring parity");
+      if (NC == 1 && t + 1 < t1) load_chunk(bq[0], t + 1, 0);
     } else {
       if (PF > 1 && t + PF - 1 < t1) load_b(bn, t + PF - 1);
 #pragma unroll

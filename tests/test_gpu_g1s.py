@@ -126,6 +126,11 @@ DGRAD_CASES = [
     (4, 256, 16, 16, 64, True, True),    # + the shortcut's gradient (block input)
     (4, 64, 16, 16, 256, True, False),   # expand conv's input gradient (K = 256)
     (2, 128, 8, 8, 512, True, True),     # K = 512 with residual
+    # training-sized grids: several 32-pixel tiles per pixel range (statistics accumulated across
+    # tiles in registers; the small cases above run one tile per range)
+    (64, 256, 32, 32, 64, True, False),
+    (64, 256, 32, 32, 256, True, False),
+    (64, 512, 16, 16, 128, True, True),
 ]
 
 
