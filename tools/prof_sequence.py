@@ -5,6 +5,7 @@ sit in a captured step.
 
   python tools/prof_sequence.py gpurun_out/prof_r2a/run_results.db [max_rows]
 """
+import os
 import re
 import sqlite3
 import sys
@@ -16,6 +17,8 @@ def short(name):
 
 
 def main():
+    if len(sys.argv) < 2 or sys.argv[1].startswith("-") or not os.path.isfile(sys.argv[1]):
+        sys.exit(__doc__)  # (sqlite3.connect would create an empty database at a bad path)
     path = sys.argv[1]
     limit = int(sys.argv[2]) if len(sys.argv) > 2 else 400
     c = sqlite3.connect(path)
