@@ -8,6 +8,7 @@ training step), so eager warmup steps and graph replays are all counted.
   python tools/prof_summary.py gpurun_out/prof6/run_results.db > profiles/resnet18_b256.md
 """
 import csv
+import os
 import re
 import sqlite3
 import sys
@@ -38,6 +39,8 @@ def load(path):
 
 
 def main():
+    if len(sys.argv) < 2 or sys.argv[1].startswith("-") or not os.path.isfile(sys.argv[1]):
+        sys.exit(__doc__)  # (sqlite3.connect would create an empty database at a bad path)
     path = sys.argv[1]
     rows = load(path)
     steps = sum(v[0] for k, v in rows.items() if "adam_kernel" in k or "sgd_kernel" in k) or 1
