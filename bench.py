@@ -10,9 +10,9 @@ weights, Adam, softmax cross-entropy. Data parallel over RCCL, one process per G
       --master-port 29500 bench.py --gpus 8 --steps 50 --warmup 10
 
 Weak scaling: every rank trains --batch images per step (global batch = batch x gpus). The
-gradient all-reduce runs on the framework's own RCCL communicator (parallel/rccl.py; bucketed,
-on a comm stream overlapping the backward, captured in the step graph); --dp-backend torch uses
-torch.distributed's ProcessGroupNCCL instead.
+gradient all-reduce is bucketed, overlaps the backward and is captured in the step graph; it runs
+on torch.distributed's ProcessGroupNCCL (RCCL) by default, or on the framework's own RCCL
+communicator (parallel/rccl.py, no c10d) with --dp-backend rccl.
 Exactly K steps are timed between a barrier + device synchronisation on both sides; the
 slowest rank's time is reported. Every timed step runs the full forward, loss, backward,
 gradient all-reduce and optimizer update.
@@ -42,13 +42,14 @@ def main():
                     help="capture the per-step compute in a hipGraph (1) or run eagerly (0)")
     ap.add_argument("--bucket-mb", type=float, default=4.0)
     ap.add_argument("--grad-dtype", default="fp32", choices=["fp32", "bf16"],
-                    help="gradient all-reduce wire format (bf16: all_to_all shards + fp32 sum + all_gather)")
+                    help="gradient all-reduce wire format (bf16: packed shards reduce-scattered + all-gathered)")
     ap.add_argument("--pg", action="store_true",
                     help="create the RCCL process group even at world size 1 (torch data plane)")
-    ap.add_argument("--dp-backend", default=os.environ.get("DCNN_DP_BACKEND", "rccl"), choices=["rccl", "torch"],
-                    help="gradient data plane on GPUs: the framework's own RCCL communicator (rank/world from "
-                         "the launcher env, unique id over the native TCP plane, no torch.distributed) or "
-                         "torch.distributed's ProcessGroupNCCL (also the fallback if the in-tree plane fails)")
+    ap.add_argument("--dp-backend", default=os.environ.get("DCNN_DP_BACKEND", "torch"), choices=["rccl", "torch"],
+                    help="gradient data plane on GPUs: torch.distributed's ProcessGroupNCCL (RCCL; default) or "
+                         "the framework's own RCCL communicator (rank/world from the launcher env, unique id "
+                         "over the native TCP plane, no torch.distributed; opt-in, exits non-zero if it cannot "
+                         "be built)")
     ap.add_argument("--profile", action="store_true", help="print per-layer device times")
     ap.add_argument("--device", default="cuda")
     ap.add_argument("--dtype", default="bf16", choices=["bf16", "fp32"],
@@ -103,12 +104,12 @@ def main():
         try:
             dp = DataParallel(model, bucket_mb=a.bucket_mb, grad_dtype=a.grad_dtype, comm_backend="rccl")
             plane = "rccl" if dp.rccl is not None else "none"
-        except Exception as e:  # (symmetric failures, e.g. no librccl: every rank falls back)
-            print(f"[bench] in-tree RCCL plane unavailable ({e}); falling back to torch.distributed",
-                  file=sys.stderr)
-            in_tree = False
-            init_distributed("nccl")
-            dp = DataParallel(model, bucket_mb=a.bucket_mb, grad_dtype=a.grad_dtype, comm_backend="torch")
+        except Exception as e:
+            # no silent switch of planes: a rank failing alone (e.g. a bootstrap timeout) while the
+            # others are inside ncclCommInitRank would otherwise split the job across two planes
+            print(f"[bench] rank {rank}: in-tree RCCL plane failed ({e}); rerun with --dp-backend torch",
+                  file=sys.stderr, flush=True)
+            os._exit(3)
     else:
         dp = DataParallel(model, bucket_mb=a.bucket_mb, grad_dtype=a.grad_dtype, comm_backend="torch")
     if plane == "torch" and not dist.is_initialized():

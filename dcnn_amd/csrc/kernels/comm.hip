@@ -1,11 +1,11 @@
 // Gradient wire-format kernels for the data-parallel bf16 all-reduce (parallel/dp.py).
 //
-// A bf16 ring all-reduce would round the running sum to bf16 at every one of its world-1 hops.
-// Instead a bucket goes out as bf16 shards (all_to_all), each rank sums the world copies of its
-// shard in fp32 in a fixed rank order (deterministic), rounds once to bf16, and the reduced
-// shards are all-gathered and expanded back into the fp32 gradient arena. Same wire bytes as a
-// bf16 ring all-reduce (2 (w-1)/w * n * 2 B per rank), half of the fp32 one, one rounding.
-// All three passes are HBM-bound streams: 16-byte vector loads/stores, grid-stride.
+// On the GPU a bucket is packed to bf16 (grad_pack), reduce-scattered and all-gathered by RCCL
+// in bf16 (collectives only: they capture into the step's hipGraph), and expanded back into the
+// fp32 gradient arena (grad_unpack): half the wire bytes of the fp32 all-reduce. grad_sum_chunks
+// is the fixed rank-order fp32 sum of w bf16 shard copies (one rounding), the reduction of the
+// all_to_all form of the same wire format. All passes are HBM-bound streams: 16-byte vector
+// loads/stores, grid-stride.
 #include "api.h"
 #include "common.h"
 

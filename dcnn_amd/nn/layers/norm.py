@@ -102,7 +102,7 @@ class BatchNorm(ParameterizedLayer):
             args = dict(other=residual) if dual else dict(residual=residual)
             if self.training:
                 part = getattr(x, "_bn_partial", None)
-                if dual and isinstance(residual.sums, tuple) and not (part is not None and isinstance(part[0], hip.Stats)):
+                if dual and isinstance(residual.sums, tuple):
                     # this layer's and the deferred shortcut BatchNorm's reduces in one launch
                     sums, residual.sums = hip.stat_reduce_pair(0, hip.bn_stats_raw(xa, part), residual.sums, C)
                 else:
@@ -142,7 +142,7 @@ class BatchNorm(ParameterizedLayer):
         if self.training:
             part = getattr(x, "_bn_partial", None)
             # raw statistics rows: the consumer reduces them together with its own
-            sums = part[0] if (part is not None and isinstance(part[0], hip.Stats)) else hip.bn_stats_raw(xa, part)
+            sums = hip.bn_stats_raw(xa, part)
             mean = _arena_empty((C,), torch.float32, xa.device)
             istd = _arena_empty((C,), torch.float32, xa.device)
             d = hip.BnDeferred(xa, sums, xa.numel() // C, self._gamma(), self._beta(), self.epsilon, (mean, istd),

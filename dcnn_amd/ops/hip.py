@@ -157,7 +157,9 @@ def _f32_concat_ok(C, Co):
 
 
 
-_HCONV_1X1 = True  # K >= 1024 1x1 convs on small grids run on the split-K halo kernel
+# K >= 1024 1x1 convs on small grids run on the split-K halo kernel. Always on; tests flip it
+# (monkeypatch) to compare the halo route against the gathered-GEMM route on the same shapes.
+_HCONV_1X1 = True
 
 
 def _hconv_ok(N, OH, OW, H, W, sh, sw, Cs, Co, taps, wop, split3=False):
@@ -1025,8 +1027,6 @@ def stat_reduce(mode, slab, rows, C, out):
     :class:`Stats` (``out`` when one block covered all rows, else the partials buffer).
     (Handing small slabs to the consumers raw instead measured no faster: the consumer prologue's
     merge costs what the launch saves, `profiles/experiment_raw_stats_r4.md`.)"""
-    if isinstance(slab, Stats):  # already folded inside the producing launch (statfold.h)
-        return slab
     K = kernels()
     ny = K.bn_stat_parts(rows)
     part = _empty((ny, 3, C), F32, slab.device) if ny > 1 else None
@@ -1063,9 +1063,9 @@ def _trace_partial(kind, x):
 
 def bn_stats_raw(x, partial=None):
     """The (slab, rows, sums) statistics rows of x before the reduce (the producing conv's
-    epilogue slab, else a bn_partial pass), or an already reduced :class:`Stats` (folded)."""
+    epilogue slab, else a bn_partial pass)."""
     if partial is not None:
-        return partial[0] if isinstance(partial[0], Stats) else partial
+        return partial
     K = kernels()
     R, C = _rc(x)
     rows = K.bn_partial_rows(R, C)

@@ -13,12 +13,12 @@ The 1/world factor of the gradient average is folded into the loss gradient (eve
 linear in it) — the fused loss kernel multiplies it in (``grad_scale``) — so the all-reduce is a
 plain SUM and neither the gradient buffer nor the loss gradient needs an extra pass.
 
-``grad_dtype="bf16"`` halves the wire bytes: a bucket is packed to bf16, exchanged as shards
-(``all_to_all``), each rank sums the world copies of its shard in fp32 in rank order
-(``comm.hip``, deterministic, one rounding instead of one per ring hop), and the reduced shards
-are all-gathered and expanded back into the fp32 arena. On the GPU that pipeline runs on a side
-stream forked from the compute stream at the bucket's fire point, so backward compute keeps
-running while it waits on RCCL.
+``grad_dtype="bf16"`` halves the wire bytes: a bucket is packed to bf16 (``comm.hip``), its
+shards are reduce-scattered (RCCL sums bf16 shards hop by hop in a fixed ring order) and
+all-gathered, and the result is expanded back into the fp32 arena. On the GPU that pipeline
+runs on a side stream forked from the compute stream at the bucket's fire point, so backward
+compute keeps running while it waits on RCCL. Over gloo (CPU) the shards are exchanged with
+``all_to_all`` and each rank sums the world copies of its shard in fp32 in rank order.
 
 Every collective is issued from the stream it depends on, with no host synchronisation, so the
 whole step — forward, backward, bucket collectives and optimizer — can be captured as ONE
@@ -64,13 +64,16 @@ class DataParallel:
         # rank / world from the launcher's environment, the unique id over the native TCP control
         # plane (no torch.distributed at all), bucket all-reduces on a framework comm stream forked
         # from / joined to the compute stream with events (captured in the step graph); "torch" =
-        # torch.distributed (ProcessGroupNCCL = RCCL on ROCm, gloo on CPU). Default: "rccl" when
-        # torch.distributed is not initialised and the model is on a GPU, else "torch".
+        # torch.distributed (ProcessGroupNCCL = RCCL on ROCm, gloo on CPU). Default: "torch" for
+        # world size > 1 (the in-tree plane is opt-in there until a multi-GPU run of it is on
+        # record); "rccl" for a single GPU process without torch.distributed (forced world-1
+        # collectives, tests).
         import os
         from .rccl import env_rank_world
         want = comm_backend or os.environ.get("DCNN_DP_BACKEND")
         if want is None:
-            want = "rccl" if (not dist.is_initialized() and model.arena.grad.is_cuda) else "torch"
+            single = env_rank_world()[1] <= 1
+            want = "rccl" if (single and not dist.is_initialized() and model.arena.grad.is_cuda) else "torch"
         if want not in ("torch", "rccl"):
             raise ValueError("comm_backend must be 'torch' or 'rccl'")
         if want == "rccl" and not model.arena.grad.is_cuda:
@@ -204,8 +207,10 @@ class DataParallel:
         if self.world == 1 and not self.force_collectives:
             return
         flat = self.model.arena.grad
+        # (a forced world-1 run keeps the bf16 wire pipeline too, so one GPU exercises it)
+        plain = self.grad_dtype == "fp32" or (self.world == 1 and not self.force_collectives)
         if self.rccl is not None:
-            if self.grad_dtype == "fp32" or self.world == 1:
+            if plain:
                 # on the comm stream: forked after the bucket's last gradient kernel, joined in
                 # finish(); the remaining backward keeps the compute stream busy meanwhile
                 cs = self._cstream(flat.device)
@@ -214,7 +219,7 @@ class DataParallel:
                 return
             self._reduce_bf16_gpu(lo, hi)
             return
-        if self.grad_dtype == "fp32" or self.world == 1:
+        if plain:
             self._works.append(dist.all_reduce(flat[lo:hi], op=dist.ReduceOp.SUM, group=self.pg, async_op=True))
             return
         if flat.is_cuda:
@@ -234,25 +239,22 @@ class DataParallel:
         return b
 
     def _reduce_bf16_gpu(self, lo, hi):
+        """bf16 wire on the GPU: pack -> reduce-scatter (RCCL sums the bf16 shards, fp32 inside
+        each hop, a fixed ring order) -> all-gather -> unpack, on the comm stream. Collectives
+        only (no grouped point-to-point calls, whose rank-to-self form crashed hipGraph capture
+        in ncclGroupEnd at world size 1), so the whole pipeline is captured in the step graph."""
         from ..ops._ext import kernels, stream_ptr
         K = kernels()
         flat = self.model.arena.grad
-        n, shard, packed, recv, red, gathered = self._wire_bufs(lo, hi, flat.device)
+        n, shard, packed, _, red, gathered = self._wire_bufs(lo, hi, flat.device)
         with self._cstream(flat.device).fork():  # the bucket's gradients are complete on the compute stream
             st = stream_ptr(flat.device)
             K.grad_pack_bf16(flat[lo:hi].data_ptr(), packed.data_ptr(), n, 1.0, st)
-            if self.rccl is not None:  # all_to_all as grouped send/recv pairs on this stream
-                K.rccl.group_start()
-                for r in range(self.world):
-                    self.rccl.send(packed[r * shard:(r + 1) * shard], r)
-                    self.rccl.recv(recv[r * shard:(r + 1) * shard], r)
-                K.rccl.group_end()
-            else:
-                dist.all_to_all_single(recv, packed, group=self.pg, async_op=True).wait()
-            K.grad_sum_chunks_bf16(recv.data_ptr(), self.world, shard, shard, red.data_ptr(), st)
             if self.rccl is not None:
+                self.rccl.reduce_scatter(red, packed)
                 self.rccl.all_gather(gathered, red)
             else:
+                dist.reduce_scatter_tensor(red, packed, op=dist.ReduceOp.SUM, group=self.pg, async_op=True).wait()
                 dist.all_gather_into_tensor(gathered, red, group=self.pg, async_op=True).wait()
             K.grad_unpack_bf16(gathered.data_ptr(), flat[lo:hi].data_ptr(), n, st)
 

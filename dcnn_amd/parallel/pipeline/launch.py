@@ -9,10 +9,10 @@ the coordinator (loss, micro-batch schedule) on its main thread while its stage 
 worker thread.  The control plane is the native TCP communicator on 127.0.0.1
 (``--base-port`` + rank); activations and gradients move GPU-to-GPU over RCCL
 (``transport="p2p"``) or inline through TCP (``--transport message``).  On GPUs the P2P plane is
-the framework's own (``--p2p rccl``, default: parallel/rccl.py ``RcclP2P``, one communicator and
-one HIP stream per direction, bootstrapped over the native TCP plane — no torch.distributed);
-``--p2p torch`` uses torch.distributed isend/irecv on four process groups instead. On the CPU the
-same code runs over gloo. Schedules: ``sync`` (GPipe), ``semi_async``, ``1f1b``.
+torch.distributed isend/irecv on four process groups (``--p2p torch``, default) or the
+framework's own (``--p2p rccl``: parallel/rccl.py ``RcclP2P``, one communicator and one HIP
+stream per direction, bootstrapped over the native TCP plane — no torch.distributed; opt-in
+until a multi-GPU run of it is on record). On the CPU the same code runs over gloo. Schedules: ``sync`` (GPipe), ``semi_async``, ``1f1b``.
 """
 from __future__ import annotations
 
@@ -31,8 +31,8 @@ def run(argv=None) -> dict:
     ap.add_argument("--batch", type=int, default=256)
     ap.add_argument("--microbatches", type=int, default=8)
     ap.add_argument("--schedule", default="semi_async", choices=["semi_async", "sync", "1f1b"])
-    ap.add_argument("--p2p", default=os.environ.get("DCNN_P2P_BACKEND", "rccl"), choices=["rccl", "torch"],
-                    help="GPU data plane: the in-tree RCCL plane (no c10d) or torch.distributed groups")
+    ap.add_argument("--p2p", default=os.environ.get("DCNN_P2P_BACKEND", "torch"), choices=["rccl", "torch"],
+                    help="GPU data plane: torch.distributed groups (default) or the in-tree RCCL plane (no c10d)")
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=2)
     ap.add_argument("--transport", default="p2p", choices=["p2p", "message"])

@@ -146,9 +146,14 @@ class TrainStep:
         fused_opt = hasattr(self.opt, "fused") and self.opt.fused()
         if not fused_opt:
             raise RuntimeError("graph capture needs the fused flat-buffer optimizer on the GPU")
-        if self.dp.active and self.capture_collectives and (self.dp.rccl is not None
-                                                            or dist.get_backend(self.dp.pg) == "nccl"):
-            # (gloo moves CUDA tensors through the host: not capturable, keeps the segments)
+        torch_bf16 = self.dp.rccl is None and self.dp.grad_dtype == "bf16"
+        if self.dp.active and self.capture_collectives and not torch_bf16 and (
+                self.dp.rccl is not None or dist.get_backend(self.dp.pg) == "nccl"):
+            # (gloo moves CUDA tensors through the host: not capturable, keeps the segments; the
+            # bf16 wire on ProcessGroupNCCL keeps them too: its reduce-scatter / all-gather pair
+            # issued from the forked comm stream crashed hipGraph capture (SIGSEGV) at world size
+            # 1, while the same pair on the in-tree communicator captures and replays correctly,
+            # tests/test_gpu_dp.py::test_gpu_dp_bf16_wire_captured_world1)
             t0 = getattr(self.opt, "t", None)
             err = None
             try:

@@ -6,6 +6,9 @@
 //   host_api_parity forward <model> <x.bin> [--device GPU]
 //                                              logits of a saved model (path.json/.bin/.bnstats) in
 //                                              eval mode for an (N, C, H, W) .bin record
+//   host_api_parity grads <model_name> <batch> <out.bin> [--device GPU]
+//                                              one forward + backward; every parameter gradient
+//                                              (logical NCHW fp32 records) into out.bin
 //   host_api_parity train <model_name> <steps> <batch> <save> [--device GPU]
 //                                              Adam steps on a synthetic set, then save
 // Output is plain text: one "key v0 v1 ..." line per item.
@@ -90,6 +93,33 @@ int main(int argc, char** argv) {
       Tensor logits = m.forward(x);
       std::printf("params %zu\nlogits", m.num_parameters());
       for (float v : logits.to_host_f32()) std::printf(" %.9g", (double)v);
+      std::printf("\n");
+      return 0;
+    }
+    if (cmd == "grads" && argc >= 5) {
+      // one forward + backward on the first synthetic batch; every parameter's gradient is
+      // written (logical NCHW fp32 records, parameter order) to argv[4]
+      const Device dev = device_arg(argc, argv);
+      Sequential m = create_model(argv[2]);
+      m.set_device(dev);
+      m.initialize(11);
+      const int batch = std::atoi(argv[3]);
+      const bool cifar = std::string(argv[2]).find("cifar") != std::string::npos;
+      const int hw = cifar ? 32 : 64, classes = cifar ? 10 : 200;
+      SyntheticClassification data((size_t)batch, 3, hw, hw, classes, 5, 0.3f);
+      Loss loss = LossFactory::create("softmax_crossentropy");
+      data.reset(0);
+      Tensor x, y;
+      if (!data.next(batch, x, y)) throw std::runtime_error("no batch");
+      m.zero_grad();
+      LossResult r = loss(m.forward(x), y);
+      m.backward(r.grad);
+      std::ofstream f(argv[4], std::ios::binary);
+      std::printf("loss %.9g\nparams", r.loss);
+      for (Param* p : m.parameters()) {
+        p->grad.view(p->shape, p->layout).save(f);
+        std::printf(" %s", p->name.c_str());
+      }
       std::printf("\n");
       return 0;
     }

@@ -198,3 +198,55 @@ def test_gpu_bf16_grad_wire_kernels():
     out = torch.empty(n, device="cuda")
     K.grad_unpack_bf16(packed.data_ptr(), out.data_ptr(), n, stream_ptr())
     assert torch.equal(out, packed[:n].float())
+
+
+def _wire_worker(rank, port, out, backend, grad_dtype):
+    """World 1, forced collectives, whole-step graph capture: the bucket pipeline of
+    ``grad_dtype`` (fp32 all-reduce, or bf16 pack -> reduce-scatter -> all-gather -> unpack) runs
+    on the comm stream inside the captured step."""
+    import torch.distributed as dist
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), DCNN_DP_FORCE_COLLECTIVES="1",
+                      RANK="0", WORLD_SIZE="1", LOCAL_RANK="0")
+    torch.cuda.set_device(0)
+    if backend == "torch":
+        dist.init_process_group("nccl", rank=0, world_size=1, device_id=torch.device("cuda", 0))
+    from dcnn_amd.models import zoo
+    from dcnn_amd.nn import SGD, LossFactory
+    from dcnn_amd.parallel.dp import DataParallel
+    from dcnn_amd.runtime.step import TrainStep
+    m = zoo.create_model("resnet18_tiny_imagenet")
+    m.set_seed(5)
+    m.set_device("GPU:0")
+    m.initialize()
+    m.set_first_layer_input_grad(False)
+    dp = DataParallel(m, bucket_mb=4.0, grad_dtype=grad_dtype, comm_backend=backend)
+    assert dp.active and (dp.rccl is not None) == (backend == "rccl")
+    opt = SGD(0.0)  # lr 0: every step sees the same weights, so the gradients stay comparable
+    opt.attach(m)
+    st = TrainStep(dp, LossFactory.create("softmax_crossentropy"), opt, use_graph=True)
+    g = torch.Generator().manual_seed(11)
+    x = torch.randn(32, 3, 64, 64, generator=g).cuda()
+    y = torch.randint(0, 200, (32,), generator=g).cuda()
+    losses = [float(st(x, y)) for _ in range(3)]
+    torch.cuda.synchronize()
+    torch.save({"g": m.arena.grad.cpu(), "losses": losses, "whole": st._whole},
+               os.path.join(out, f"{backend}_{grad_dtype}.pt"))
+    if dp.rccl is not None:
+        dp.rccl.close()
+    if dist.is_initialized():
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("backend", ["rccl", "torch"])
+def test_gpu_dp_bf16_wire_captured_world1(tmp_path, backend):
+    """The bf16 gradient wire in the captured step (whole graph on the in-tree plane, segmented
+    on ProcessGroupNCCL): at world 1 the reduce-scatter / all-gather are identities, so the
+    step's gradient must be the fp32 step's rounded to bf16."""
+    for gd in ("fp32", "bf16"):
+        mp.spawn(_wire_worker, args=(_port(), str(tmp_path), backend, gd), nprocs=1, join=True)
+    a = torch.load(tmp_path / f"{backend}_fp32.pt", weights_only=True)
+    b = torch.load(tmp_path / f"{backend}_bf16.pt", weights_only=True)
+    # (ProcessGroupNCCL's bf16 pair runs between segment replays: runtime/step.py)
+    assert a["whole"] and b["whole"] == (backend == "rccl")
+    assert a["losses"] == b["losses"]
+    assert torch.equal(b["g"], a["g"].bfloat16().float())

@@ -216,3 +216,72 @@ def test_unknown_schedule_rejected():
             coord.train_step(torch.randn(2, 1, 28, 28), torch.randint(0, 10, (2,)), "zigzag")
     finally:
         coord.stop()
+
+
+class _FakeRcclPlane:
+    """Stands in for parallel.rccl.RcclP2P: per-(direction key, src, dst) FIFO queues shared by
+    the ranks of one test, recording every call (what P2PTransport's routing chose)."""
+
+    def __init__(self, rank, queues, log):
+        self.rank, self.q, self.log = rank, queues, log
+
+    def send(self, key, t, peer):
+        self.log.append(("send", key, self.rank, peer, tuple(t.shape), bool(t.is_contiguous())))
+        self.q.setdefault((key, self.rank, peer), []).append(t.clone())
+
+    def recv(self, key, t, src):
+        self.log.append(("recv", key, src, self.rank, tuple(t.shape)))
+        t.copy_(self.q[(key, src, self.rank)].pop(0))
+        return t
+
+
+class _Outbox:
+    def __init__(self, sender):
+        self.sender, self.sent = sender, []
+
+    def send(self, m):
+        m.sender = self.sender
+        self.sent.append(m)
+
+
+def test_p2p_transport_routes_through_rccl_plane():
+    """P2PTransport with the in-tree plane (rccl=...): forward jobs between stages ride the "fwd"
+    communicator, backward jobs "bwd", traffic to / from the coordinator the "cfwd" / "cbwd" ones;
+    channels-last activations travel as their physical NHWC buffer and come back as the same
+    logical NCHW tensor; receive slots are reused across steps; rank-local peers bypass RCCL."""
+    from dcnn_amd.parallel.pipeline import messages as M
+    from dcnn_amd.parallel.pipeline.transport import P2PTransport
+    C = M.CommandType
+    ranks = {"coordinator": 0, "stage_0": 0, "stage_1": 1}
+    q, log = {}, []
+    t0 = P2PTransport("stage_0", ranks, None, rccl=_FakeRcclPlane(0, q, log))
+    t1 = P2PTransport("stage_1", ranks, None, rccl=_FakeRcclPlane(1, q, log))
+    tc = P2PTransport("coordinator", ranks, None, rccl=_FakeRcclPlane(0, q, log))
+    g = torch.Generator().manual_seed(0)
+    for step in range(2):
+        act = torch.randn(4, 8, 5, 6, generator=g).to(memory_format=torch.channels_last)
+        o0 = _Outbox("stage_0")
+        t0.send(o0, "stage_1", C.FORWARD_JOB, 3, act)
+        got = t1.recv(o0.sent[-1], "cpu")
+        assert torch.equal(got, act) and got.shape == act.shape
+        grad = torch.randn(4, 8, 5, 6, generator=g)
+        o1 = _Outbox("stage_1")
+        t1.send(o1, "stage_0", C.BACKWARD_JOB, 3, grad)
+        assert torch.equal(t0.recv(o1.sent[-1], "cpu"), grad)
+        logits = torch.randn(4, 10, 1, 1, generator=g)
+        t1.send(o1, "coordinator", C.FORWARD_JOB, 3, logits)
+        assert torch.equal(tc.recv(o1.sent[-1], "cpu"), logits)
+        dlog = torch.randn(4, 10, 1, 1, generator=g)
+        oc = _Outbox("coordinator")
+        tc.send(oc, "stage_1", C.BACKWARD_JOB, 3, dlog)
+        assert torch.equal(t1.recv(oc.sent[-1], "cpu"), dlog)
+    keys = [(e[0], e[1]) for e in log]
+    assert keys[:8] == [("send", "fwd"), ("recv", "fwd"), ("send", "bwd"), ("recv", "bwd"),
+                        ("send", "cfwd"), ("recv", "cfwd"), ("send", "cbwd"), ("recv", "cbwd")]
+    assert log[0][4] == (4, 5, 6, 8) and log[0][5]  # NHWC physical buffer, contiguous
+    assert t1.slot_allocs == 2 and t0.slot_allocs == 1 and tc.slot_allocs == 1  # step 2 reused the slots
+    # rank-local peer (coordinator and stage_0 share rank 0): no RCCL call
+    n = len(log)
+    oc = _Outbox("coordinator")
+    tc.send(oc, "stage_0", C.FORWARD_JOB, 4, torch.ones(2, 3, 1, 1))
+    assert len(log) == n

@@ -1,0 +1,26 @@
+#!/bin/bash
+# Round-5 first GPU pass: the RCCL capture probe, the new GPU tests, per-shape conv timings (all
+# ResNet-18 shapes), the headline bench's per-layer profile, and four PMC passes that split the
+# conv kernels' wave cycles by cause (tools/pmc_table.py).
+# usage (via gpurun): bash tools/gpu_r5_a.sh TAG
+TAG=${1:-a}
+cd "$GRAFT_REPO_ROOT"; mkdir -p gpurun_out; export TMPDIR=/tmp
+R=$GRAFT_REPO_ROOT
+timeout -k 10 900 python -u tools/rccl_capture_probe.py > gpurun_out/probe_$TAG.log 2>&1 || exit $?
+timeout -k 10 600 python -u -m pytest -x -v --timeout 240 --timeout-method thread -p no:cacheprovider \
+  tests/test_gpu_dp.py::test_gpu_dp_bf16_wire_captured_world1 \
+  tests/test_cpp_host_blocks.py::test_cpp_resnet18_gpu_gradients_match_cpu_backend -s > gpurun_out/t_$TAG.log 2>&1 || exit $?
+timeout -k 10 300 python -u benchmarks/conv_bench.py --batch 256 --iters 20 > gpurun_out/conv_$TAG.log 2>&1 || exit $?
+timeout -k 10 240 python bench.py --steps 10 --warmup 3 --profile > gpurun_out/layers_$TAG.log 2>&1 || exit $?
+P1="GRBM_GUI_ACTIVE SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_VALU_MFMA_BUSY_CYCLES SQ_WAIT_INST_LDS"
+P2="SQ_WAVE_CYCLES SQ_ACTIVE_INST_LDS SQ_ACTIVE_INST_VMEM SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_SCA SQ_ACTIVE_INST_MISC SQ_INST_CYCLES_VMEM_RD SQ_INST_CYCLES_VMEM_WR"
+P3="SQ_LDS_IDX_ACTIVE SQ_LDS_BANK_CONFLICT SQ_LDS_UNALIGNED_STALL SQ_LDS_ADDR_CONFLICT SQ_INSTS_LDS SQ_INSTS_MFMA SQ_INSTS_VALU SQ_INSTS_SALU"
+P4="SQ_WAVE_CYCLES SQ_INST_LEVEL_VMEM SQ_INST_LEVEL_LDS SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_VALU_MFMA_COEXEC_CYCLES SQ_LDS_DATA_FIFO_FULL SQ_LDS_CMD_FIFO_FULL"
+n=0
+for P in "$P1" "$P2" "$P3" "$P4"; do
+  n=$((n+1))
+  (cd /tmp && timeout -s KILL 120 rocprofv3 --pmc $P --output-format csv -d $R/gpurun_out/pmc5_${TAG}_$n -o run -- python3 $R/benchmarks/conv_bench.py --batch 256 --iters 3 > $R/gpurun_out/pmc5_${TAG}_$n.log 2>&1) || exit $?
+done
+F=""
+for n in 1 2 3 4; do F="$F $(find gpurun_out/pmc5_${TAG}_$n -name '*counter_collection.csv' -print -quit)"; done
+python tools/pmc_table.py --match hconv3,hwgrad2,gemm_g2,gemm_t2,g1s $F > gpurun_out/pmc5_$TAG.md 2>&1
