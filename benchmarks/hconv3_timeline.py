@@ -1,7 +1,8 @@
 #!/usr/bin/env python3
 """Per-wave phase timeline of the hconv3 kernel (diagnostic s_memtime stamps, hconv3_set_stamps):
 prologue (halo + first weight stages landed), first chunk, remaining K loop, epilogue stores,
-statistics — medians over waves, in shader cycles, plus dispatch skew and the span of the grid.
+statistics — medians over waves, in shader cycles, and the K loop's share of each wave's life
+(s_memtime counts per XCD, so only same-wave stamp differences are used).
 
   python benchmarks/hconv3_timeline.py --batch 256 --shapes l1.c,l2.c
 """
@@ -49,24 +50,34 @@ def main():
         torch.cuda.synchronize()
         K.hconv3_set_stamps(0)
         t = buf.view(items, 4, 8).double().cpu()
-        t0 = t[:, :, 0][t[:, :, 0] > 0].min()
-        kloop = (t[:, :, 2] - t[:, :, 0]).sum()
-        epi = (t[:, :, 4] - t[:, :, 2]).sum()
+        # s_memtime is a per-XCD counter: only differences of stamps taken by the SAME wave are
+        # meaningful (cross-workgroup spans mix clocks). Split-K items that are not their tile's
+        # last arriver skip the epilogue stamps (3, 4): those phases use only the items that ran it.
+        ok = lambda *ks: torch.stack([t[:, :, k] > 0 for k in ks]).all(0)
+        per_item = {}
+        for name, a_, b_ in (("kloop", 0, 2), ("chunk0", 0, 1), ("epilogue", 2, 3), ("stats", 3, 4)):
+            m = ok(a_, b_)
+            per_item[name] = (t[:, :, b_] - t[:, :, a_])[m]
         first = t[:, :, 5] > 0
-        # a wave's life: from its workgroup's start to its last item's end; items of one workgroup
-        # are the ones whose start stamp falls inside it (grid-strided), summed over all waves
-        life_end = t[:, :, 4].max()
-        per_item = {"kloop": t[:, :, 2] - t[:, :, 0], "chunk0": t[:, :, 1] - t[:, :, 0],
-                    "epilogue": t[:, :, 3] - t[:, :, 2], "stats": t[:, :, 4] - t[:, :, 3]}
-        prologue = (t[:, :, 0] - t[:, :, 5])[first]
-        span = float(life_end - t0)
-        wg = int(first.sum()) // 4
-        print(f"{nm} {a.op} batch {N}: {items} items on {wg} workgroups, span {span:.0f} cyc; "
-              f"K loop share of item time {float(kloop / (kloop + epi)) * 100:.1f}%, "
-              f"of wave life {float(kloop / ((t[:, :, 4].max() - t0) * 4 * wg)) * 100:.1f}%")
-        print("   medians per item: " + "  ".join(f"{k} {float(v.median()):.0f}" for k, v in per_item.items())
-              + f"  prologue {float(prologue.median()):.0f}")
-
+        G = int(first[:, 0].sum())  # workgroups (each stamps 5 once, at its first item)
+        lives, kl, prol = [], [], []
+        for u0 in torch.nonzero(first[:, 0]).flatten().tolist():
+            us = list(range(u0, items, G))
+            for w in range(4):
+                start_ = t[u0, w, 5]
+                ends = [t[u, w, 4] if t[u, w, 4] > 0 else t[u, w, 2] for u in us]
+                lives.append(max(ends) - start_)
+                kl.append(sum(t[u, w, 2] - t[u, w, 0] for u in us))
+                prol.append(t[u0, w, 0] - start_)
+        lives, kl, prol = torch.tensor(lives), torch.tensor(kl), torch.tensor(prol)
+        kloop_sum = float(per_item["kloop"].sum())
+        epi_sum = float(per_item["epilogue"].sum() + per_item["stats"].sum())
+        print(f"{nm} {a.op} batch {N}: {items} items on {G} workgroups; median wave life {float(lives.median()):.0f} cyc; "
+              f"K loop share of wave life {100 * float(kl.sum() / lives.sum()):.1f}%, "
+              f"of item time (items with an epilogue) {100 * kloop_sum / max(kloop_sum + epi_sum, 1):.1f}%")
+        print("   medians per item: " + "  ".join(f"{k} {float(v.median()):.0f}" if v.numel() else f"{k} -"
+                                               for k, v in per_item.items())
+              + f"  prologue {float(prol.median()):.0f}")
 
 if __name__ == "__main__":
     main()

@@ -265,4 +265,29 @@ void split3_bf16(const float* in, bf16* out, long rows, int C, int pattern, hipS
 void im2col_nhwc(int dt, const void* x, void* col, const ConvGeom& g, hipStream_t s);
 void col2im_nhwc(int dt, const void* col, void* x, const void* residual, const ConvGeom& g, int chan_major,
                  hipStream_t s);
+// device-side batch assembly + augmentation chain (augment.hip, data/device_loader.py)
+enum { AUG_HFLIP = 0, AUG_VFLIP, AUG_ROTATION, AUG_BRIGHTNESS, AUG_CONTRAST, AUG_NOISE, AUG_CROP, AUG_CUTOUT,
+       AUG_NORMALIZE };
+constexpr int kAugMaxOps = 8;
+constexpr int kAugMaxFloats = 16384;  // C*H*W staged in LDS (two fp32 buffers: 128 KB)
+struct AugOpDev {
+  int kind;
+  float p;
+  float a[6];  // op parameters (normalize: mean[3], std[3])
+};
+struct AugBatchArgs {
+  const void* src;        // dataset [N][C][H][W], uint8 (x / 255) or fp32
+  int src_u8;
+  const int64_t* idx;     // [B] sample indices of this batch
+  const int64_t* labels;  // [N] (nullptr: no label gather)
+  int64_t* labels_out;    // [B]
+  float* out;             // [B][C][H][W] fp32
+  int B, C, H, W;
+  unsigned long long seed;
+  int nops;
+  AugOpDev ops[kAugMaxOps];
+};
+void gemm_t2_set_stages(int n);  // gathered weight gradient LDS ring depth (2 / 3; A/B hook)
+bool augment_batch_supported(int C, int H, int W);
+void augment_batch(const AugBatchArgs& a, hipStream_t s);
 }  // namespace dcnn

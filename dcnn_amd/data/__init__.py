@@ -5,3 +5,4 @@ from .datasets import (CIFAR10DataLoader, CIFAR100DataLoader, MNISTDataLoader, T
                        WiFiDataLoader, create_cifar10_loaders, create_cifar100_loaders, create_mnist_loaders,
                        create_tiny_image_loader)
 from .loader import ArrayDataLoader, BaseDataLoader, SyntheticDataLoader  # noqa: F401
+from .device_loader import DeviceDataLoader, to_device_loader  # noqa: F401

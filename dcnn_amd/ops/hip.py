@@ -49,6 +49,32 @@ def _check_act(x: torch.Tensor, what: str):
         raise ValueError(f"{what}: expected channels_last (NHWC) memory layout")
 
 
+# ---- conv call recorder (tests/test_gpu_geometry.py): every conv2d_fwd / dgrad / wgrad call's
+# shapes, epilogue options and routing-table decision, so a test can replay exactly the (kernel,
+# shape, epilogue) tuples a model's training step launches against an fp32 reference
+_RECORD = None
+
+
+class record_convs:
+    """``with record_convs() as calls:`` appends one dict per conv call made inside the block."""
+
+    def __enter__(self):
+        global _RECORD
+        self._prev, self.calls = _RECORD, []
+        _RECORD = self.calls
+        return self.calls
+
+    def __exit__(self, *exc):
+        global _RECORD
+        _RECORD = self._prev
+        return False
+
+
+def _rec(op, **kw):
+    if _RECORD is not None:
+        _RECORD.append(dict(op=op, **kw))
+
+
 def to_act(x: torch.Tensor, dtype: torch.dtype) -> torch.Tensor:
     """Bring a (N,C,H,W) tensor into the GPU activation format: NHWC memory, compute dtype."""
     if x.dim() == 4 and x.dtype == dtype and x.is_contiguous(memory_format=CL):
@@ -264,6 +290,9 @@ def conv2d_fwd(x, w, bias, stride, pad, *, stats=False, residual=None, relu=Fals
              if not out_fp32 else K.ROUTE_GENERIC)
     if route == K.ROUTE_HALO and KH * KW == 1 and not _HCONV_1X1:
         route = K.ROUTE_GEMM_G2
+    _rec("fwd", x=tuple(x.shape), w=(Co, Ci, KH, KW), padded_w=not (w.dim() == 4 and w.shape[1] == Ci), stride=(sh, sw),
+         pad=(ph, pw), stats=bool(stats), bias=bias is not None, residual=residual is not None, relu=bool(relu),
+         route=int(route), out_fp32=bool(out_fp32))
     if route == K.ROUTE_G1S:
         # streaming 1x1 conv (g1s.hip): weights in registers, one statistics row per pixel range
         rows = K.g1s_rows(M, Co, Ci, 1 if stats else 0)
@@ -331,6 +360,7 @@ def stem_conv_fwd(x, w, bias=None, stats=False):
     N, Ci, H, W = x.shape
     Co = w.shape[0]
     K = kernels()
+    _rec("stem_fwd", x=(N, Ci, H, W), w=(Co, Ci, 3, 3), stats=bool(stats), bias=bias is not None, route=-1)
     y = _empty((N, Co, H, W), BF16, x.device, True)
     slab = sums = None
     rows = 0
@@ -349,6 +379,7 @@ def stem_conv_wgrad(dy, x, grad_w, grad_b=None):
     N, Ci, H, W = x.shape
     Co = dy.shape[1]
     K = kernels()
+    _rec("stem_wgrad", x=(N, Ci, H, W), w=(Co, Ci, 3, 3), bias=grad_b is not None, route=-1)
     dy = dy.contiguous(memory_format=CL)
     assert dy.dtype == BF16 and tuple(dy.shape) == (N, Co, H, W)
     assert grad_w.is_contiguous() or grad_w.is_contiguous(memory_format=CL), "dense fp32 weight gradient"
@@ -606,6 +637,10 @@ def conv2d_dgrad(dy, wt, x_shape, stride, pad, *, residual=None, bnb=None):
         if not f32 else K.ROUTE_GEMM_G2
     if route == K.ROUTE_HALO and KH * KW == 1 and not _HCONV_1X1:
         route = K.ROUTE_GEMM_G2
+    if not f32:
+        _rec("dgrad", x=tuple(x_shape), w=(Co, Ci, KH, KW), stride=(sh, sw), pad=(ph, pw),
+             residual=residual is not None, bnb=bool(fuse_req), bnb_mask=bool(fuse_req and bnb.y is not None),
+             route=int(route))
     if not f32 and route == K.ROUTE_GENERIC:
         dx = _empty((N, Ci, H, W), BF16, dy.device, True)
         Kd = KH * KW * Co
@@ -842,6 +877,8 @@ def conv2d_wgrad(dy, x, w_shape, stride, pad, grad_w, grad_b=None):
     # the shared routing table (csrc/kernels/conv_route.cpp, also used by the C++ host API)
     route = (K.conv_wgrad_route(N, Ci, H, W, Co, KH, KW, stride[0], stride[1], pad[0], pad[1], OH, OW, -1)
              if Cx == Ci else K.ROUTE_GEMM_G2)
+    _rec("wgrad", x=(N, Ci, H, W), xpad=Cx, w=(Co, Ci, KH, KW), stride=tuple(stride), pad=tuple(pad),
+         bias=grad_b is not None, route=int(route))
     if route == K.ROUTE_HALO:
         # halo-tiled wgrad: X read ~1.4x instead of once per tap
         Ng = KH * KW * Ci

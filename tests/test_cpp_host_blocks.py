@@ -215,12 +215,24 @@ def test_cpp_resnet18_gpu_gradients_match_cpu_backend(bins, tmp_path):
     lc, names_c, gc = res["CPU"]
     assert names == names_c and len(gg) == len(gc) > 40
     assert abs(lg - lc) / abs(lc) < 2e-2
-    worst = []
-    for n, a, b in zip(names, gg, gc):
+    # A conv bias followed by BatchNorm has an exactly-zero true gradient (BN removes any
+    # per-channel constant): both backends hold rounding noise there, so such parameters (reference
+    # norm < 1e-4 of a typical gradient of their size) must only stay below 1e-2 of that size;
+    # every other parameter is held to a bf16-level relative error.
+    total = sum(float(b.double().norm()) ** 2 for b in gc) ** 0.5
+    numel = sum(b.numel() for b in gc)
+    worst, zeros = [], []
+    for k, (n, a, b) in enumerate(zip(names, gg, gc)):
         assert a.shape == b.shape, n
-        rel = float((a.double() - b.double()).norm() / b.double().norm().clamp_min(1e-30))
-        worst.append((rel, n))
+        typical = total * (b.numel() / numel) ** 0.5
+        rn = float(b.double().norm())
+        if rn < 1e-4 * typical:
+            zeros.append((float(a.double().norm()) / typical, f"{k}:{n}"))
+            continue
+        worst.append((float((a.double() - b.double()).norm()) / rn, f"{k}:{n}", rn))
     worst.sort(reverse=True)
-    print("worst per-parameter relative errors:", worst[:6])
-    bad = [(r, n) for r, n in worst if r > 3e-2]
+    print("worst per-parameter relative errors (rel, index:name, reference norm):", worst[:8])
+    print("analytically-zero gradients (GPU norm / typical):", sorted(zeros, reverse=True)[:4])
+    assert len(worst) > 40
+    bad = [w for w in worst if w[0] > 3e-2] + [z for z in zeros if z[0] > 1e-2]
     assert not bad, bad

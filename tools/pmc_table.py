@@ -37,6 +37,7 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("csv", nargs="+")
     ap.add_argument("--match", default="", help="comma-separated kernel-name substrings to keep")
+    ap.add_argument("--wide", default="", help="one row per kernel with these comma-separated columns")
     a = ap.parse_args()
     keep = [m for m in a.match.split(",") if m]
     rows = defaultdict(dict)
@@ -58,6 +59,13 @@ def main():
                     rows[name][k.replace("SQ_", "") + "/LDS_ACTIVE"] = f"{100 * v / lds:.1f}%"
                 else:
                     rows[name][k.replace("SQ_", "")] = f"{v:.4g}"
+    if a.wide:
+        cols_w = a.wide.split(",")
+        print("| kernel | " + " | ".join(cols_w) + " |")
+        print("|---|" + "---:|" * len(cols_w))
+        for name, cols in sorted(rows.items()):
+            print(f"| `{name}` | " + " | ".join(cols.get(c, "-") for c in cols_w) + " |")
+        return
     for name, cols in sorted(rows.items()):
         print(f"### `{name}`\n")
         print("| counter | value |\n|---|---:|")

@@ -3,9 +3,12 @@
 into a markdown table suitable for ``profiles/``.
 
 Per-step times are normalised by the number of optimizer-kernel dispatches (one per
-training step), so eager warmup steps and graph replays are all counted.
+training step). From a rocpd database only the LAST steps are counted (``--last N``, default: all
+but the first four steps): the window runs from the end of one optimizer dispatch to the end of
+the N-th after it, so it holds graph replays only, not the eager warm-up steps, the capture's
+warm-up or its allocator copies.
 
-  python tools/prof_summary.py gpurun_out/prof6/run_results.db > profiles/resnet18_b256.md
+  python tools/prof_summary.py gpurun_out/prof6/run_results.db [--last 10] > profiles/resnet18_b256.md
 """
 import csv
 import os
@@ -21,11 +24,20 @@ def _short(name: str) -> str:
     return name[:90]
 
 
-def load(path):
+def load(path, last=None):
     rows = defaultdict(lambda: [0, 0.0])
     if path.endswith(".db"):
         c = sqlite3.connect(path)
-        for name, dur in c.execute("select name, duration from kernels"):
+        ks = list(c.execute("select name, start, end, duration from kernels order by start"))
+        opt = [e for (n, _, e, _) in ks if "adam_kernel" in n or "sgd_kernel" in n]
+        lo, hi = None, None
+        if len(opt) >= 2:
+            m = last if last else max(1, len(opt) - 4)
+            m = min(m, len(opt) - 1)
+            lo, hi = opt[-m - 1], opt[-1]  # after the (m+1)-th last optimizer dispatch .. the last one
+        for name, st, en, dur in ks:
+            if lo is not None and not (st > lo and en <= hi):
+                continue
             r = rows[_short(name)]
             r[0] += 1
             r[1] += dur / 1e3  # ns -> us
@@ -42,12 +54,13 @@ def main():
     if len(sys.argv) < 2 or sys.argv[1].startswith("-") or not os.path.isfile(sys.argv[1]):
         sys.exit(__doc__)  # (sqlite3.connect would create an empty database at a bad path)
     path = sys.argv[1]
-    rows = load(path)
+    last = int(sys.argv[sys.argv.index("--last") + 1]) if "--last" in sys.argv else None
+    rows = load(path, last)
     steps = sum(v[0] for k, v in rows.items() if "adam_kernel" in k or "sgd_kernel" in k) or 1
     total = sum(v[1] for v in rows.values())
     print(f"# Kernel summary: `{path}`\n")
-    print(f"optimizer dispatches (= training steps traced): {steps}; total GPU kernel time {total / 1e3:.2f} ms; "
-          f"**{total / steps / 1e3:.3f} ms kernel time per step**\n")
+    print(f"optimizer dispatches (= training steps in the replay window): {steps}; total GPU kernel time "
+          f"{total / 1e3:.2f} ms; **{total / steps / 1e3:.3f} ms kernel time per step**\n")
     print("| kernel | calls | calls/step | total ms | us/step | % |")
     print("|---|---:|---:|---:|---:|---:|")
     for k, (n, us) in sorted(rows.items(), key=lambda kv: -kv[1][1]):

@@ -15,21 +15,21 @@ import subprocess
 import sys
 
 VARIANTS = {
-    # name: (communicators, side streams, captured, extra env)
+    # name: (communicators, side streams, captured, extra env); ordered from the expected-safe to
+    # the variants that hung / crashed (the run stops at the first timeout)
     "eager_1comm": (1, False, False, {}),
-    "cap_1comm_capstream": (1, False, True, {}),
-    "cap_1comm_side": (1, True, True, {}),
-    "cap_2comm_side": (2, True, True, {}),
-    "cap_2comm_side_nomix": (2, True, True, {"NCCL_GRAPH_MIXING_SUPPORT": "0"}),
-    "cap_1comm_capstream_nomix": (1, False, True, {"NCCL_GRAPH_MIXING_SUPPORT": "0"}),
-    "cap_2comm_capstream": (2, False, True, {}),
     "cap_allreduce_2comm_side": (2, True, True, {"_COLL": "1"}),
     # ProcessGroupNCCL (c10d) at world 1: reduce_scatter_tensor + all_gather_into_tensor, async +
     # wait, captured on the capture stream itself or on a forked side stream
     "c10d_rsag_eager": (1, False, False, {"_C10D": "1"}),
+    "c10d_allreduce_side": (1, True, True, {"_C10D": "1", "_COLL": "1"}),
     "c10d_rsag_capstream": (1, False, True, {"_C10D": "1"}),
     "c10d_rsag_side": (1, True, True, {"_C10D": "1"}),
-    "c10d_allreduce_side": (1, True, True, {"_C10D": "1", "_COLL": "1"}),
+    "cap_1comm_side": (1, True, True, {}),
+    "cap_2comm_side": (2, True, True, {}),
+    "cap_2comm_side_nomix": (2, True, True, {"NCCL_GRAPH_MIXING_SUPPORT": "0"}),
+    "cap_1comm_capstream_nomix": (1, False, True, {"NCCL_GRAPH_MIXING_SUPPORT": "0"}),
+    "cap_1comm_capstream": (1, False, True, {}),
 }
 
 
