@@ -59,11 +59,9 @@ def main():
     ap.add_argument("--set", default="r18", choices=["r18", "r50"], help="ResNet-18-tiny or ResNet-50-tiny shapes")
     ap.add_argument("--v3", type=int, default=1, help="third-generation 3x3 halo conv (hconv3.hip) on/off")
     ap.add_argument("--eager", action="store_true", help="time eager launches instead of one hipGraph replay")
-    ap.add_argument("--t2-stages", type=int, default=3, help="gathered weight-gradient LDS ring depth (2 / 3)")
     a = ap.parse_args()
     from dcnn_amd.ops import hip
     hip.kernels().hconv3_enable(a.v3)
-    hip.kernels().gemm_t2_set_stages(a.t2_stages)
     CL = torch.channels_last
     N = a.batch
     tot = {"fwd": 0.0, "dgrad": 0.0, "wgrad": 0.0}

@@ -268,7 +268,7 @@ void col2im_nhwc(int dt, const void* col, void* x, const void* residual, const C
 // device-side batch assembly + augmentation chain (augment.hip, data/device_loader.py)
 enum { AUG_HFLIP = 0, AUG_VFLIP, AUG_ROTATION, AUG_BRIGHTNESS, AUG_CONTRAST, AUG_NOISE, AUG_CROP, AUG_CUTOUT,
        AUG_NORMALIZE };
-constexpr int kAugMaxOps = 8;
+constexpr int kAugMaxOps = 12;
 constexpr int kAugMaxFloats = 16384;  // C*H*W staged in LDS (two fp32 buffers: 128 KB)
 struct AugOpDev {
   int kind;
@@ -287,7 +287,6 @@ struct AugBatchArgs {
   int nops;
   AugOpDev ops[kAugMaxOps];
 };
-void gemm_t2_set_stages(int n);  // gathered weight gradient LDS ring depth (2 / 3; A/B hook)
 bool augment_batch_supported(int C, int H, int W);
 void augment_batch(const AugBatchArgs& a, hipStream_t s);
 }  // namespace dcnn

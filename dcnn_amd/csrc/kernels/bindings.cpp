@@ -508,7 +508,6 @@ PYBIND11_MODULE(_kernels, m) {
   m.def("grad_unpack_bf16", [](uintptr_t in, uintptr_t g, long n, uintptr_t st) {
     grad_unpack_bf16(P<const bf16*>(in), P<float*>(g), n, S(st));
   });
-  m.def("gemm_t2_set_stages", &gemm_t2_set_stages);
   m.def("augment_batch_supported", &augment_batch_supported);
   // ops: (kind, probability, params[<= 6]) in chain order
   m.def("augment_batch", [](uintptr_t src, int src_u8, uintptr_t idx, uintptr_t labels, uintptr_t labels_out,
@@ -518,7 +517,7 @@ PYBIND11_MODULE(_kernels, m) {
     a.src = P<const void*>(src); a.src_u8 = src_u8; a.idx = P<const int64_t*>(idx);
     a.labels = P<const int64_t*>(labels); a.labels_out = P<int64_t*>(labels_out); a.out = P<float*>(out);
     a.B = B; a.C = C; a.H = H; a.W = W; a.seed = seed;
-    if (ops.size() > (size_t)kAugMaxOps) throw std::runtime_error("augment_batch: at most 8 ops");
+    if (ops.size() > (size_t)kAugMaxOps) throw std::runtime_error("augment_batch: at most 12 ops");
     a.nops = (int)ops.size();
     for (size_t k = 0; k < ops.size(); ++k) {
       a.ops[k].kind = std::get<0>(ops[k]);

@@ -360,15 +360,11 @@ __device__ __forceinline__ int tr_swz(int row) {
   else return 0;
 }
 
-// NST LDS stages: NST - 1 K-steps of (dY, X) tiles in flight while one is multiplied (3: counted
-// vmcnt waits and raw s_barrier, so the newest stage's LDS-DMA stays in flight across the barrier)
-template <int BM, int BN, bool FAST, int NST>
+template <int BM, int BN, bool FAST>
 __global__ void __launch_bounds__(256, 2) gemm_t2_kernel(T2Args p) {
   using T = T2<BM, BN>;
   constexpr int BK = T::BK;
-  constexpr int INS = T::A_INS + T::B_INS;  // LDS-DMA instructions per wave per stage
-  static_assert(NST == 2 || NST == 3, "2 or 3 stages");
-  __shared__ __attribute__((aligned(16))) char smem[NST * T::STAGE];
+  __shared__ __attribute__((aligned(16))) char smem[2 * T::STAGE];
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const int wm = wid >> 1, wn = wid & 1;
   const int tiles_m = (p.M + BM - 1) / BM, tiles_n = (p.N + BN - 1) / BN;
@@ -491,21 +487,11 @@ __global__ void __launch_bounds__(256, 2) gemm_t2_kernel(T2Args p) {
 
   const int nk = kend > kbeg ? (kend - kbeg + BK - 1) / BK : 0;
   if (nk > 0) stage(0, kbeg);
-  if (NST == 3 && nk > 1) {
-    stage(1, kbeg + BK);
-    asm volatile("s_waitcnt vmcnt(%0)" ::"n"(INS) : "memory");  // stage 0 landed, stage 1 may fly
-  } else {
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
   int cur = 0;
   for (int kt = 0; kt < nk; ++kt) {
-    if constexpr (NST == 2) {
-      if (kt + 1 < nk) stage(cur ^ 1, kbeg + (kt + 1) * BK);
-    } else {
-      // into the stage K-step kt - 1 read (every wave passed the barrier that closed it)
-      if (kt + 2 < nk) stage(cur == 0 ? 2 : cur - 1, kbeg + (kt + 2) * BK);
-    }
+    if (kt + 1 < nk) stage(cur ^ 1, kbeg + (kt + 1) * BK);
     const char* As = smem + cur * T::STAGE;
     const char* Bs = As + BK * BM * 2;
     if (do_bias) {
@@ -539,19 +525,9 @@ __global__ void __launch_bounds__(256, 2) gemm_t2_kernel(T2Args p) {
           acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[i], b[j], acc[i][j], 0, 0, 0);
       __builtin_amdgcn_s_setprio(0);
     }
-    if constexpr (NST == 2) {
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      __syncthreads();
-      cur ^= 1;
-    } else {
-      // K-step kt + 1 must have landed (this wave's loads, then the barrier for everyone's); the
-      // loads of kt + 2, issued after it, stay in flight
-      if (kt + 2 < nk)
-        asm volatile("s_waitcnt vmcnt(%0)\n\ts_waitcnt lgkmcnt(0)\n\ts_barrier" ::"n"(INS) : "memory");
-      else
-        asm volatile("s_waitcnt vmcnt(0)\n\ts_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
-      cur = cur == 2 ? 0 : cur + 1;
-    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    cur ^= 1;
   }
 
   float* out = p.slab + (long)split * p.M * p.N;
@@ -671,17 +647,10 @@ void gemm_g2(const G2Args& a_in, hipStream_t s) {
   throw std::runtime_error("gemm_g2: no variant");
 }
 
-static int g_t2_stages = 3;  // gemm_t2_set_stages(2): the 2-stage ring (A/B hook)
-void gemm_t2_set_stages(int n) { g_t2_stages = n == 2 ? 2 : 3; }
-
 template <int BM, int BN, bool FAST>
 static void launch_t2(T2Args a, int splits, hipStream_t s) {
   const int tiles = ((a.M + BM - 1) / BM) * ((a.N + BN - 1) / BN);
-  // 3 stages while two workgroups still fit a CU (every tile but 128 x 128)
-  if (g_t2_stages == 3 && 2 * 3 * T2<BM, BN>::STAGE <= 163840)
-    hipLaunchKernelGGL((gemm_t2_kernel<BM, BN, FAST, 3>), dim3(tiles * splits), dim3(256), 0, s, a);
-  else
-    hipLaunchKernelGGL((gemm_t2_kernel<BM, BN, FAST, 2>), dim3(tiles * splits), dim3(256), 0, s, a);
+  hipLaunchKernelGGL((gemm_t2_kernel<BM, BN, FAST>), dim3(tiles * splits), dim3(256), 0, s, a);
   DCNN_LAUNCH_CHECK();
 }
 

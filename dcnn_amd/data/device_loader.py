@@ -79,8 +79,8 @@ def device_ops(strategy: Optional[AugmentationStrategy], C: int):
                 m, s = args[0], args[len(args) // 2]
                 args = [m, m, m, s, s, s]
         out.append((_KINDS.index(name), float(p), [float(v) for v in args]))
-    if len(out) > 8:
-        raise ValueError("device augmentation: at most 8 ops per chain")
+    if len(out) > 12:
+        raise ValueError("device augmentation: at most 12 ops per chain")
     return out
 
 

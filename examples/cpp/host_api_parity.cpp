@@ -6,9 +6,11 @@
 //   host_api_parity forward <model> <x.bin> [--device GPU]
 //                                              logits of a saved model (path.json/.bin/.bnstats) in
 //                                              eval mode for an (N, C, H, W) .bin record
-//   host_api_parity grads <model_name> <batch> <out.bin> [--device GPU]
+//   host_api_parity grads <model_name> <batch> <out.bin> [<prefix>] [--device GPU]
 //                                              one forward + backward; every parameter gradient
-//                                              (logical NCHW fp32 records) into out.bin
+//                                              (logical NCHW fp32 records) into out.bin; with a
+//                                              prefix also the initial model (prefix.json/.bin)
+//                                              and the batch (prefix.x.bin, prefix.y.bin)
 //   host_api_parity train <model_name> <steps> <batch> <save> [--device GPU]
 //                                              Adam steps on a synthetic set, then save
 // Output is plain text: one "key v0 v1 ..." line per item.
@@ -111,6 +113,17 @@ int main(int argc, char** argv) {
       data.reset(0);
       Tensor x, y;
       if (!data.next(batch, x, y)) throw std::runtime_error("no batch");
+      if (argc >= 6 && argv[5][0] != '-') {
+        // the initial weights and the batch, for another front end to run the same step
+        const std::string pre = argv[5];
+        m.save_to_file(pre);
+        std::ofstream fx(pre + ".x.bin", std::ios::binary);
+        x.to(Device::cpu()).save(fx);
+        std::vector<float> yl;
+        for (int64_t v : y.to(Device::cpu()).to_host_i64()) yl.push_back((float)v);
+        std::ofstream fy(pre + ".y.bin", std::ios::binary);
+        Tensor::from_host(yl, {(int64_t)yl.size(), 1, 1, 1}, Device::cpu()).save(fy);
+      }
       m.zero_grad();
       LossResult r = loss(m.forward(x), y);
       m.backward(r.grad);

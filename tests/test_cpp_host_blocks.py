@@ -198,41 +198,120 @@ def test_cpp_resnet18_gpu_training_matches_cpu_backend(bins, tmp_path):
 
 @pytest.mark.gpu
 def test_cpp_resnet18_gpu_gradients_match_cpu_backend(bins, tmp_path):
-    """Every parameter gradient of one ResNet-18 step on the GPU backend's fused path (conv
+    """Every parameter gradient of one ResNet-18 step on the C++ GPU backend's fused path (conv
     epilogue statistics, BN + ReLU, residual tails with the shortcut add and masked branch
     gradient, dgrad-epilogue BN-backward statistics, head-conv shortcut add, deferred split-K
-    weight-gradient reduce) against the CPU backend's plain fp32 ops on the same weights and
-    batch: per-parameter relative L2 error at bf16 level. A wrong ReLU mask, a swapped
-    statistics slab or a wrong block's shortcut gradient moves one layer's error to O(1)."""
-    from dcnn_amd.nn.sequential import load_tensor
+    weight-gradient reduce) against the C++ CPU backend's plain fp32 ops on the same weights and
+    batch, per parameter (relative L2 error and cosine).
+
+    bf16 activations and gradients compound through 17 BatchNorm backwards of a random-init
+    network, so the stem's gradient legitimately drifts from fp32 (cosine ~0.92 at batch 16). The
+    yardstick is the Python front end's GPU path — validated layer by layer against fp32 by
+    tests/test_gpu_model.py::test_gpu_vs_cpu_model_teacher_forced — run on the same weights and
+    batch; the same fused GPU path in exact fp32 must match the CPU to 1e-2 (measured 4e-3: this
+    random-init backward amplifies relative rounding ~1000x from the classifier to the stem, which
+    is also why bf16 drifts by ~0.4 there — precision, not a fusion error). Per parameter the C++ GPU error may exceed the Python GPU error
+    by at most 25% + 0.02,
+    the norm ratios to the fp32 gradient within 0.05 of the Python path's, and the classifier's
+    gradient (no compounding) to 2e-2. A wrong
+    ReLU mask, a swapped statistics slab or a wrong block's shortcut gradient moves the affected
+    layers' errors to O(1)."""
+    from dcnn_amd.nn import LossFactory
+    from dcnn_amd.nn.sequential import Sequential, load_tensor
+    from dcnn_amd.parallel.dp import DataParallel
     res = {}
     for dev in ("GPU", "CPU"):
-        args = [bins["host_api_parity"], "grads", "resnet18_tiny_imagenet", "16", f"g_{dev}.bin"]
-        out = _lines(_run(args + (["--device", "GPU"] if dev == "GPU" else []), tmp_path, timeout=600))
+        args = [bins["host_api_parity"], "grads", "resnet18_tiny_imagenet", os.environ.get("DCNN_GRAD_BATCH", "16"),
+                f"g_{dev}.bin"]
+        if dev == "GPU":
+            args += ["snap/init", "--device", "GPU"]
+        (tmp_path / "snap").mkdir(exist_ok=True)
+        out = _lines(_run(args, tmp_path, timeout=600))
         with open(tmp_path / f"g_{dev}.bin", "rb") as f:
-            res[dev] = (float(out["loss"][0]), out["params"], [load_tensor(f) for _ in out["params"]])
+            res[dev] = (float(out["loss"][0]), out["params"], [load_tensor(f).double() for _ in out["params"]])
     lg, names, gg = res["GPU"]
     lc, names_c, gc = res["CPU"]
     assert names == names_c and len(gg) == len(gc) > 40
     assert abs(lg - lc) / abs(lc) < 2e-2
-    # A conv bias followed by BatchNorm has an exactly-zero true gradient (BN removes any
-    # per-channel constant): both backends hold rounding noise there, so such parameters (reference
-    # norm < 1e-4 of a typical gradient of their size) must only stay below 1e-2 of that size;
-    # every other parameter is held to a bf16-level relative error.
-    total = sum(float(b.double().norm()) ** 2 for b in gc) ** 0.5
+    # the Python front end's GPU step on the same initial weights and batch: bf16 (the yardstick)
+    # and exact fp32 (the same fused kernels and fusion plan with IEEE fp32 operands)
+    from dcnn_amd.ops import hip
+    with open(tmp_path / "snap" / "init.x.bin", "rb") as f:
+        x = load_tensor(f).cuda()
+    with open(tmp_path / "snap" / "init.y.bin", "rb") as f:
+        y = load_tensor(f).reshape(-1).long().cuda()
+
+    def py_grads(dtype):
+        m = Sequential.from_file(str(tmp_path / "snap" / "init"), device="GPU:0")
+        if dtype == torch.float32:
+            m.set_compute_dtype(torch.float32)
+        m.set_training(True)
+        dp = DataParallel(m, broadcast=False)
+        m.clear_gradients()
+        out = dp.forward(x)
+        _, grad, _ = LossFactory.create("softmax_crossentropy").loss_and_grad(out, y)
+        dp.backward(grad, prescaled=True)
+        torch.cuda.synchronize()
+        g = [t.detach().double().cpu().reshape(c.shape) for t, c in zip(m.gradients(), gc)]
+        assert len(g) == len(gc)
+        return g
+
+    gp = py_grads(torch.bfloat16)
+    concat = hip.get_f32_concat()
+    hip.set_f32_concat(False)
+    hip.kernels().set_f32_mode(0)
+    try:
+        g32 = py_grads(torch.float32)
+    finally:
+        hip.set_f32_concat(concat)
+
+    def err(a, b):
+        return float((a - b).norm() / b.norm().clamp_min(1e-30))
+
+    total = sum(float(b.norm()) ** 2 for b in gc) ** 0.5
     numel = sum(b.numel() for b in gc)
-    worst, zeros = [], []
-    for k, (n, a, b) in enumerate(zip(names, gg, gc)):
-        assert a.shape == b.shape, n
+    rows, bad = [], []
+    for k, (n, a, p, q, b) in enumerate(zip(names, gg, gp, g32, gc)):
         typical = total * (b.numel() / numel) ** 0.5
-        rn = float(b.double().norm())
-        if rn < 1e-4 * typical:
-            zeros.append((float(a.double().norm()) / typical, f"{k}:{n}"))
+        if float(b.norm()) < 1e-4 * typical:  # conv bias before BatchNorm: exactly-zero true gradient
+            if float(a.norm()) > 0.1 * typical or float(q.norm()) > 1e-2 * typical:
+                bad.append((k, n, "zero-gradient parameter", float(a.norm()) / typical, float(q.norm()) / typical))
             continue
-        worst.append((float((a.double() - b.double()).norm()) / rn, f"{k}:{n}", rn))
-    worst.sort(reverse=True)
-    print("worst per-parameter relative errors (rel, index:name, reference norm):", worst[:8])
-    print("analytically-zero gradients (GPU norm / typical):", sorted(zeros, reverse=True)[:4])
-    assert len(worst) > 40
-    bad = [w for w in worst if w[0] > 3e-2] + [z for z in zeros if z[0] > 1e-2]
+        e_cpp, e_py, e32 = err(a, b), err(p, b), err(q, b)
+        ratio, ratio_py = float(a.norm() / b.norm()), float(p.norm() / b.norm())
+        rows.append((k, n, round(e_cpp, 4), round(e_py, 4), round(ratio, 4), round(ratio_py, 4), round(e32, 6)))
+        if e_cpp > 1.25 * e_py + 0.02 or abs(ratio - ratio_py) > 0.05 or e32 > 1e-2:
+            bad.append(rows[-1])
+    print("per parameter (index, name, C++ GPU bf16 error, Python GPU bf16 error, C++ GPU / CPU norm, "
+          "Python GPU / CPU norm, Python GPU exact-fp32 error):", rows)
+    assert rows[-1][2] < 2e-2 and rows[-2][2] < 2e-2, rows[-2:]  # classifier weights / bias
     assert not bad, bad
+
+def test_cpp_and_python_cpu_gradients_identical(bins, tmp_path):
+    """The C++ host API and the Python front end on the CPU backend: the same initial ResNet-18
+    weights and batch give bit-identical parameter gradients (both run the native fp32 kernels;
+    the check covers the layer order, the gradient layouts and the snapshot / batch hand-off the
+    GPU test above relies on)."""
+    from dcnn_amd.nn import LossFactory
+    from dcnn_amd.nn.sequential import Sequential, load_tensor
+    from dcnn_amd.parallel.dp import DataParallel
+    (tmp_path / "snap").mkdir()
+    out = _lines(_run([bins["host_api_parity"], "grads", "resnet18_tiny_imagenet", "4", "g.bin", "snap/init"],
+                      tmp_path, timeout=300))
+    with open(tmp_path / "g.bin", "rb") as f:
+        gc = [load_tensor(f) for _ in out["params"]]
+    m = Sequential.from_file(str(tmp_path / "snap" / "init"))
+    m.set_training(True)
+    with open(tmp_path / "snap" / "init.x.bin", "rb") as f:
+        x = load_tensor(f)
+    with open(tmp_path / "snap" / "init.y.bin", "rb") as f:
+        y = load_tensor(f).reshape(-1).long()
+    dp = DataParallel(m, broadcast=False)
+    m.clear_gradients()
+    loss, grad, _ = LossFactory.create("softmax_crossentropy").loss_and_grad(dp.forward(x), y)
+    assert abs(float(loss) - float(out["loss"][0])) < 1e-5
+    dp.backward(grad, prescaled=True)
+    gp = m.gradients()
+    assert len(gp) == len(gc) > 40
+    for k, (a, b) in enumerate(zip(gp, gc)):
+        assert torch.equal(a.detach().reshape(b.shape), b), k

@@ -24,9 +24,11 @@ def test_device_ops_translation():
     assert ops[2][2] == pytest.approx([0.485, 0.456, 0.406, 0.229, 0.224, 0.225])
     one = device_ops(AugmentationBuilder().normalize((0.5,), (0.25,)).build(), 1)
     assert one[0][2] == [0.5, 0.5, 0.5, 0.25, 0.25, 0.25]
+    b = AugmentationBuilder()
+    for _ in range(13):
+        b.horizontal_flip()
     with pytest.raises(ValueError):
-        device_ops(AugmentationBuilder().horizontal_flip().vertical_flip().rotation().brightness().contrast()
-                   .gaussian_noise().random_crop().cutout().normalize().build(), 3)
+        device_ops(b.build(), 3)
 
 
 def test_reference_chain_semantics():
