@@ -464,12 +464,22 @@ class Adam : public Optimizer {
   void step(const std::vector<Param*>& params) override;
   long step_count() const { return t_; }
   void set_step_count(long t) { t_ = t; }
+  // a replayed graph ran one step on the device: mirror it on the host (t) and upload a changed
+  // learning rate before the replay
+  void before_replay();
+  // host step state (lr, t) -> the device step scalars (outside a capture)
+  void upload_hyper();
 
  private:
   float b1_, b2_, eps_, wd_;
   bool decoupled_;
   long t_ = 0;
+  // GPU arena path: step scalars in device memory {lr, bc1, bc2, t}, updated on the device
+  Tensor hyper_;
+  float hyper_lr_ = -1.f;
+  long hyper_t_ = -1;
 };
+
 
 // ---- data
 class DataSource {

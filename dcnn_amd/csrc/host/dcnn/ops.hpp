@@ -141,6 +141,13 @@ void relu_mask(const void* dy, const void* y, void* dx, long n);
 void adam(float* p, const float* g, float* m, float* v, void* shadow, long n, float lr, float b1, float b2, float eps,
           float bc1, float bc2, float wd, bool decoupled);
 void sgd(float* p, const float* g, float* vel, void* shadow, long n, float lr, float momentum);
+// device-resident Adam step scalars hyper = {lr, bc1, bc2, t} (a captured step replays with the
+// current values): t += 1 and the bias corrections on the device, then the fused update reading them
+void adam_hyper_step(float* hyper, float b1, float b2);
+void adam_dev(float* p, const float* g, float* m, float* v, void* shadow, long n, float b1, float b2, float eps,
+              float wd, bool decoupled, const float* hyper);
+// {loss (fp32), -, correct (int32)} of the last fused loss launch (read after a graph replay)
+const void* loss_device();
 }  // namespace gpu_ops
 
 }  // namespace dcnn

@@ -45,15 +45,59 @@ float bf16_to_f32(uint16_t b);
 namespace gpu {
 int device_count();
 void set_device(int dev);
-// caching allocator: freed blocks are reused by later allocations of the same size class (all
-// host API work runs on the null stream in order, so reuse is ordered after the last reader)
+// caching allocator: freed blocks are reused by later allocations of the same size class (the
+// host API enqueues a thread's work on one flow in order, so reuse is ordered after the last
+// reader); blocks allocated while a Graph captures belong to that graph (below)
 void* alloc(size_t nbytes);
 void free(void* p);
 size_t cached_bytes();  // bytes held in the free lists
 void empty_cache();     // synchronise and return every cached block to the driver
-void copy(void* dst, const void* src, size_t nbytes, int kind);  // 0 h2d, 1 d2h, 2 d2d
+void copy(void* dst, const void* src, size_t nbytes, int kind);  // 0 h2d, 1 d2h (host waits), 2 d2d (async)
 void zero(void* p, size_t nbytes);                                // stream-ordered memset
 void synchronize();
+
+// Flows (reference include/device/flow.hpp:11-64): the HIP stream the calling thread's host API
+// work is enqueued on. Default: the thread's own blocking stream on the current device (created on
+// first use); set_flow() redirects the thread's work (nullptr: back to the default). Events order
+// work across flows without a host wait.
+using Flow = void*;   // hipStream_t
+using Event = void*;  // hipEvent_t
+Flow flow();
+void set_flow(Flow f);
+Flow flow_create();
+void flow_destroy(Flow f);
+void flow_synchronize(Flow f = nullptr);  // nullptr: the current flow
+Event event_create();
+void event_destroy(Event e);
+void event_record(Event e, Flow f = nullptr);
+void flow_wait(Flow f, Event e);  // f waits for e (device side)
+void event_synchronize(Event e);
+
+// Graph: captures the host API work the calling thread enqueues on its current flow between
+// begin() and end() into one hipGraph and replays it with one launch (the reference runs every
+// op eagerly; the Python front end captures its steps the same way, runtime/step.py). Every
+// device block allocated during the capture belongs to the graph — freed blocks return to the
+// graph's private free list, never to other users — so a replay finds the same addresses; the
+// blocks return to the shared cache when the graph is destroyed. Inside a capture no host copy or
+// host wait may run (the host API's loss readback is deferred: see gpu_ops::loss_device()).
+class Graph {
+ public:
+  Graph() = default;
+  ~Graph();
+  Graph(const Graph&) = delete;
+  Graph& operator=(const Graph&) = delete;
+  void begin();
+  void end();
+  void replay();  // on the current flow
+  bool ready() const { return exec_ != nullptr; }
+  static bool capturing();  // the calling thread is inside begin() / end()
+
+ private:
+  void* graph_ = nullptr;  // hipGraph_t
+  void* exec_ = nullptr;   // hipGraphExec_t
+  void* pool_ = nullptr;   // the graph's private blocks
+  Flow flow_ = nullptr;
+};
 // inter-process device buffers (same node): a dedicated allocation + its 64-byte IPC handle
 constexpr size_t kIpcHandleBytes = 64;
 void* ipc_alloc(size_t nbytes, void* handle_out);

@@ -39,6 +39,28 @@ class Loss {
   std::string type_;
 };
 
+// One training step (zero_grad, forward, loss, backward, optimizer) captured into a gpu::Graph
+// and replayed with one launch (the C++ counterpart of the Python front end's runtime/step.py).
+// The batch is copied into static device tensors before each replay; the loss stays on the
+// device until loss() reads it. capture() runs two eager warm-up steps first (workspaces, kernel
+// instances, allocator size classes) and restores the parameters and optimizer moments they
+// changed, so the first replay is the first update.
+class TrainGraph {
+ public:
+  TrainGraph(Sequential& model, Adam& opt, const Loss& loss) : model_(model), opt_(opt), loss_(loss) {}
+  double step(const Tensor& x, const Tensor& labels);  // eager on the first call: captures, then replays
+  double last_loss();                                  // host read of the last replay's loss
+
+ private:
+  void capture(const Tensor& x, const Tensor& labels);
+  Sequential& model_;
+  Adam& opt_;
+  const Loss& loss_;
+  gpu::Graph graph_;
+  Tensor sx_, sy_;
+  bool captured_ = false;
+};
+
 struct LossFactory {
   // "crossentropy"|"ce", "softmax_crossentropy"|"softmax_ce", "logsoftmax_crossentropy"|
   // "logsoftmax_ce", "mse", "mae", "huber" (param: delta)

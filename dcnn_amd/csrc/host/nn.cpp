@@ -1410,15 +1410,41 @@ void SGD::step(const std::vector<Param*>& params) {
   }
 }
 
-void Adam::step(const std::vector<Param*>& params) {
+void Adam::upload_hyper() {
+  if (!hyper_.defined()) return;
+  const float h[4] = {lr_, 0.f, 0.f, (float)t_};  // bc1 / bc2 are recomputed by the next step
+  gpu::copy(hyper_.data(), h, sizeof h, 0);
+  hyper_lr_ = lr_;
+  hyper_t_ = t_;
+}
+
+void Adam::before_replay() {
+  if (hyper_.defined() && hyper_lr_ != lr_) {
+    gpu::copy(hyper_.data(), &lr_, sizeof lr_, 0);
+    hyper_lr_ = lr_;
+  }
   ++t_;
-  const float bc1 = 1.f - std::pow(b1_, (float)t_), bc2 = 1.f - std::pow(b2_, (float)t_);
+  ++hyper_t_;
+}
+
+void Adam::step(const std::vector<Param*>& params) {
   if (ParamArena* a = whole_arena(params)) {
-    gpu_ops::adam(a->value.ptr<float>(), a->grad.ptr<float>(), a->m.ptr<float>(), a->v.ptr<float>(), a->shadow.data(),
-                  (long)a->n, lr_, b1_, b2_, eps_, bc1, bc2, wd_, decoupled_);
+    // step scalars on the device (a captured step replays with the current lr and t)
+    if (!hyper_.defined()) hyper_ = Tensor::zeros({4}, DType::F32, a->value.device());
+    if (hyper_lr_ != lr_ || hyper_t_ != t_) {
+      if (gpu::Graph::capturing()) throw std::runtime_error("Adam: step scalars changed inside a graph capture");
+      upload_hyper();
+    }
+    ++t_;
+    ++hyper_t_;
+    gpu_ops::adam_hyper_step(hyper_.ptr<float>(), b1_, b2_);
+    gpu_ops::adam_dev(a->value.ptr<float>(), a->grad.ptr<float>(), a->m.ptr<float>(), a->v.ptr<float>(),
+                      a->shadow.data(), (long)a->n, b1_, b2_, eps_, wd_, decoupled_, hyper_.ptr<float>());
     a->refresh_transposes();
     return;
   }
+  ++t_;
+  const float bc1 = 1.f - std::pow(b1_, (float)t_), bc2 = 1.f - std::pow(b2_, (float)t_);
   for (auto* p : params) {
     if (p->arena) p->arena->wt_valid = false;
     if (!p->m.defined()) {

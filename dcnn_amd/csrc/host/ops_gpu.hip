@@ -12,6 +12,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <cmath>
 #include <cstring>
 #include <map>
 #include <mutex>
@@ -41,16 +42,23 @@ namespace {
 // kernel still reads it is only reused by work queued after that kernel. Size classes are
 // quarter-power-of-two steps (at most 25% slack); on an out-of-memory the cached blocks are
 // released and the allocation retried.
+// A graph's private blocks: everything allocated while it captured (gpu::Graph).
+struct CapturePool {
+  std::map<std::pair<int, size_t>, std::vector<void*>> free_blocks;
+  std::vector<void*> owned;
+};
 struct BlockPool {
   std::mutex mu;
   std::map<std::pair<int, size_t>, std::vector<void*>> free_blocks;
   std::unordered_map<void*, std::pair<int, size_t>> owner;  // block -> (device, class bytes)
+  std::unordered_map<void*, CapturePool*> graph_owned;      // block -> the graph it belongs to
   size_t cached = 0;
 };
 BlockPool& pool() {
   static BlockPool* p = new BlockPool;  // never destroyed: tensors may outlive static teardown
   return *p;
 }
+thread_local CapturePool* t_capture = nullptr;  // the pool of the graph this thread is capturing
 size_t size_class(size_t n) {
   if (n <= 512) return 512;
   int lg = 63 - __builtin_clzll((unsigned long long)(n - 1));  // 2^lg < n <= 2^(lg + 1)
@@ -81,20 +89,34 @@ void* alloc(size_t nbytes) {
   const size_t cls = size_class(nbytes);
   BlockPool& bp = pool();
   std::lock_guard<std::mutex> g(bp.mu);
-  auto it = bp.free_blocks.find({dev, cls});
-  if (it != bp.free_blocks.end() && !it->second.empty()) {
-    void* p = it->second.back();
-    it->second.pop_back();
-    bp.cached -= cls;
-    return p;
+  CapturePool* cp = t_capture;
+  if (cp) {  // a capturing graph first reuses its own freed blocks
+    auto it = cp->free_blocks.find({dev, cls});
+    if (it != cp->free_blocks.end() && !it->second.empty()) {
+      void* p = it->second.back();
+      it->second.pop_back();
+      return p;
+    }
   }
   void* p = nullptr;
-  if (hipMalloc(&p, cls) != hipSuccess) {
-    (void)hipGetLastError();
-    release_cached(bp);
-    HOST_HIP_CHECK(hipMalloc(&p, cls));
+  auto it = bp.free_blocks.find({dev, cls});
+  if (it != bp.free_blocks.end() && !it->second.empty()) {
+    p = it->second.back();
+    it->second.pop_back();
+    bp.cached -= cls;
+  } else {
+    if (hipMalloc(&p, cls) != hipSuccess) {
+      (void)hipGetLastError();
+      if (cp) throw std::runtime_error("gpu::alloc: out of memory while capturing a graph");
+      release_cached(bp);
+      HOST_HIP_CHECK(hipMalloc(&p, cls));
+    }
+    bp.owner[p] = {dev, cls};
   }
-  bp.owner[p] = {dev, cls};
+  if (cp) {
+    bp.graph_owned[p] = cp;
+    cp->owned.push_back(p);
+  }
   return p;
 }
 void free(void* p) {
@@ -104,6 +126,11 @@ void free(void* p) {
   auto it = bp.owner.find(p);
   if (it == bp.owner.end()) {
     (void)hipFree(p);
+    return;
+  }
+  auto gi = bp.graph_owned.find(p);
+  if (gi != bp.graph_owned.end()) {  // a graph's block stays the graph's
+    gi->second->free_blocks[it->second].push_back(p);
     return;
   }
   bp.free_blocks[it->second].push_back(p);
@@ -119,15 +146,114 @@ void empty_cache() {
   std::lock_guard<std::mutex> g(bp.mu);
   release_cached(bp);
 }
+// ---- flows (streams) and events
+namespace {
+thread_local hipStream_t t_flow = nullptr;      // set_flow() override
+thread_local hipStream_t t_default[64] = {};    // the thread's default flow per device
+}  // namespace
+Flow flow() {
+  if (t_flow) return t_flow;
+  int dev = 0;
+  HOST_HIP_CHECK(hipGetDevice(&dev));
+  if (!t_default[dev]) HOST_HIP_CHECK(hipStreamCreate(&t_default[dev]));  // (blocking: ordered with the null stream)
+  return t_default[dev];
+}
+void set_flow(Flow f) { t_flow = static_cast<hipStream_t>(f); }
+Flow flow_create() {
+  hipStream_t s = nullptr;
+  HOST_HIP_CHECK(hipStreamCreate(&s));
+  return s;
+}
+void flow_destroy(Flow f) {
+  if (f) (void)hipStreamDestroy(static_cast<hipStream_t>(f));
+}
+void flow_synchronize(Flow f) { HOST_HIP_CHECK(hipStreamSynchronize(static_cast<hipStream_t>(f ? f : flow()))); }
+Event event_create() {
+  hipEvent_t e = nullptr;
+  HOST_HIP_CHECK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+  return e;
+}
+void event_destroy(Event e) {
+  if (e) (void)hipEventDestroy(static_cast<hipEvent_t>(e));
+}
+void event_record(Event e, Flow f) {
+  HOST_HIP_CHECK(hipEventRecord(static_cast<hipEvent_t>(e), static_cast<hipStream_t>(f ? f : flow())));
+}
+void flow_wait(Flow f, Event e) {
+  HOST_HIP_CHECK(hipStreamWaitEvent(static_cast<hipStream_t>(f ? f : flow()), static_cast<hipEvent_t>(e), 0));
+}
+void event_synchronize(Event e) { HOST_HIP_CHECK(hipEventSynchronize(static_cast<hipEvent_t>(e))); }
+
 void copy(void* dst, const void* src, size_t nbytes, int kind) {
   static const hipMemcpyKind k[] = {hipMemcpyHostToDevice, hipMemcpyDeviceToHost, hipMemcpyDeviceToDevice};
-  if (kind == 2)  // device to device: stream-ordered, the host does not wait
-    HOST_HIP_CHECK(hipMemcpyAsync(dst, src, nbytes, k[kind], nullptr));
-  else
-    HOST_HIP_CHECK(hipMemcpy(dst, src, nbytes, k[kind]));
+  hipStream_t s = static_cast<hipStream_t>(flow());
+  HOST_HIP_CHECK(hipMemcpyAsync(dst, src, nbytes, k[kind], s));
+  // host <-> device: the host buffer is usable when this returns (and a D2H sees the flow's work)
+  if (kind != 2) {
+    if (Graph::capturing()) throw std::runtime_error("gpu::copy: a host copy inside a graph capture");
+    HOST_HIP_CHECK(hipStreamSynchronize(s));
+  }
 }
-void zero(void* p, size_t nbytes) { HOST_HIP_CHECK(hipMemsetAsync(p, 0, nbytes, nullptr)); }
+void zero(void* p, size_t nbytes) { HOST_HIP_CHECK(hipMemsetAsync(p, 0, nbytes, static_cast<hipStream_t>(flow()))); }
 void synchronize() { HOST_HIP_CHECK(hipDeviceSynchronize()); }
+
+// ---- graphs
+bool Graph::capturing() { return t_capture != nullptr; }
+void Graph::begin() {
+  if (t_capture) throw std::runtime_error("gpu::Graph: nested capture");
+  if (exec_) throw std::runtime_error("gpu::Graph: already captured");
+  flow_ = flow();
+  auto* cp = new CapturePool;
+  pool_ = cp;
+  // a previous eager step's work must not be captured into (or race with) the graph
+  HOST_HIP_CHECK(hipStreamSynchronize(static_cast<hipStream_t>(flow_)));
+  HOST_HIP_CHECK(hipStreamBeginCapture(static_cast<hipStream_t>(flow_), hipStreamCaptureModeThreadLocal));
+  t_capture = cp;
+}
+void Graph::end() {
+  if (t_capture != pool_) throw std::runtime_error("gpu::Graph: end() without begin()");
+  t_capture = nullptr;
+  hipGraph_t g = nullptr;
+  HOST_HIP_CHECK(hipStreamEndCapture(static_cast<hipStream_t>(flow_), &g));
+  graph_ = g;
+  hipGraphExec_t ex = nullptr;
+  HOST_HIP_CHECK(hipGraphInstantiate(&ex, g, nullptr, nullptr, 0));
+  exec_ = ex;
+}
+void Graph::replay() {
+  if (!exec_) throw std::runtime_error("gpu::Graph: replay before capture");
+  HOST_HIP_CHECK(hipGraphLaunch(static_cast<hipGraphExec_t>(exec_), static_cast<hipStream_t>(flow())));
+}
+Graph::~Graph() {
+  if (t_capture == pool_ && pool_) {  // destroyed mid-capture (an exception): end the capture
+    t_capture = nullptr;
+    hipGraph_t g = nullptr;
+    (void)hipStreamEndCapture(static_cast<hipStream_t>(flow_), &g);
+    if (g) (void)hipGraphDestroy(g);
+    (void)hipGetLastError();
+  }
+  if (exec_ || graph_) (void)hipDeviceSynchronize();  // no replay in flight uses the blocks below
+  if (exec_) (void)hipGraphExecDestroy(static_cast<hipGraphExec_t>(exec_));
+  if (graph_) (void)hipGraphDestroy(static_cast<hipGraph_t>(graph_));
+  if (auto* cp = static_cast<CapturePool*>(pool_)) {
+    BlockPool& bp = pool();
+    std::lock_guard<std::mutex> g(bp.mu);
+    // the graph's blocks return to the shared cache (blocks still held by live tensors come back
+    // there when those are freed)
+    std::unordered_map<void*, bool> is_free;
+    for (auto& kv : cp->free_blocks)
+      for (void* p : kv.second) is_free[p] = true;
+    for (void* p : cp->owned) {
+      bp.graph_owned.erase(p);
+      if (is_free.count(p)) {
+        auto o = bp.owner.find(p);
+        bp.free_blocks[o->second].push_back(p);
+        bp.cached += o->second.second;
+      }
+    }
+    delete cp;
+  }
+}
 
 // Inter-process buffers (pipeline transport "ipc"): a whole hipMalloc allocation (IPC exports the
 // base of an allocation, so these never come from the caching pool) and its 64-byte handle.
@@ -163,7 +289,8 @@ namespace gpu_ops {
 namespace {
 constexpr int kPlain = 0, kConvFwd = 1, kConvDgrad = 2;
 constexpr int kBF16 = 1;
-const hipStream_t S = nullptr;
+// the calling thread's current flow (gpu::flow()): every launch of the host API goes there
+inline hipStream_t cur() { return static_cast<hipStream_t>(gpu::flow()); }
 
 // grow-only workspace per purpose
 enum Slot { W_T = 0, SLAB, BSLAB, STAT_SLAB, STAT_SUMS, STAT_PART, LOSS_WS, LOSS_OUT, TICKETS, HPART, HTICKETS, GN_AFF,
@@ -199,7 +326,7 @@ __global__ void transpose16_kernel(const uint16_t* __restrict__ in, uint16_t* __
 
 void transpose16(const void* in, void* out, int batch, int rows, int cols) {
   dim3 grid((cols + 31) / 32, (rows + 31) / 32, batch);
-  hipLaunchKernelGGL(transpose16_kernel, grid, dim3(32, 8), 0, S, static_cast<const uint16_t*>(in),
+  hipLaunchKernelGGL(transpose16_kernel, grid, dim3(32, 8), 0, cur(), static_cast<const uint16_t*>(in),
                      static_cast<uint16_t*>(out), rows, cols);
   HOST_HIP_CHECK(hipGetLastError());
 }
@@ -241,7 +368,7 @@ void hconv_workspace(HConvArgs& a) {
   const size_t need = (size_t)tiles * 64 * 4;
   a.tickets = static_cast<unsigned*>(scratch(HTICKETS, need));
   if (zeroed < need) {
-    HOST_HIP_CHECK(hipMemset(a.tickets, 0, need));
+    HOST_HIP_CHECK(hipMemsetAsync(a.tickets, 0, need, cur()));
     zeroed = need;
   }
 }
@@ -307,9 +434,9 @@ void wgrad_reduce(const Tensor& hold, const Tensor& bhold, const float* slab, fl
     return;
   }
   if (gb)
-    splitk_reduce2(slab, gw, n, bslab, gb, nb, splits, 1, S);
+    splitk_reduce2(slab, gw, n, bslab, gb, nb, splits, 1, cur());
   else
-    splitk_reduce(slab, gw, n, splits, 1, S);
+    splitk_reduce(slab, gw, n, splits, 1, cur());
 }
 }  // namespace
 
@@ -325,17 +452,17 @@ void end_deferred_reduce() {
       t.e[k].n = e.n;
       t.e[k].splits = e.splits;
     }
-    multi_splitk_reduce(t, S);
+    multi_splitk_reduce(t, cur());
   }
   g_pending.clear();  // (the slabs return to the caching allocator, reused only by later work)
   g_defer = false;
 }
 
-void input_to_nhwc(const float* x, void* y, int N, int C, int HW) { nchw_to_nhwc(kBF16, x, y, N, C, HW, S); }
+void input_to_nhwc(const float* x, void* y, int N, int C, int HW) { nchw_to_nhwc(kBF16, x, y, N, C, HW, cur()); }
 void nhwc_to_nchw(const void* x, void* y, int N, int HW, int C) { transpose16(x, y, N, HW, C); }
 void nchw_to_nhwc_bf16(const void* x, void* y, int N, int HW, int C) { transpose16(x, y, N, C, HW); }
-void cast_bf16(const float* x, void* y, long n) { cast_f32_bf16(x, static_cast<bf16*>(y), n, S); }
-void zero(void* p, long nbytes) { zero_bytes(p, nbytes, S); }
+void cast_bf16(const float* x, void* y, long n) { cast_f32_bf16(x, static_cast<bf16*>(y), n, cur()); }
+void zero(void* p, long nbytes) { zero_bytes(p, nbytes, cur()); }
 
 const float* conv_fwd(const void* x, const void* w, const float* bias, void* y, const ConvShape& s, int* stat_rows) {
   const long xb = (long)s.N * s.H * s.W * s.C * 2, wb = (long)s.Co * s.KH * s.KW * s.C * 2;
@@ -359,34 +486,34 @@ const float* conv_fwd(const void* x, const void* w, const float* bias, void* y, 
     a.bias = bias;
     if (want) a.stats = slab_of(hconv_stat_rows(s.N, s.H, s.W, s.C, s.Co, a.ntaps, 0));
     hconv_workspace(a);
-    hconv(a, S);
+    hconv(a, cur());
     return a.stats;
   }
   if (route == ROUTE_G1S) {
     float* st = want ? slab_of(g1s_rows(M, s.Co, s.C, 1)) : nullptr;
     g1s(static_cast<const bf16*>(x), static_cast<const bf16*>(w), static_cast<bf16*>(y), M, s.Co, s.C, s.H, s.W, s.OH,
-        s.OW, s.SH, bias, nullptr, st, 0, nullptr, 0, BnbArgs{}, want ? 1 : 0, S);
+        s.OW, s.SH, bias, nullptr, st, 0, nullptr, 0, BnbArgs{}, want ? 1 : 0, cur());
     return st;
   }
   if (route != ROUTE_GENERIC && xb < (1l << 31) && wb < (1l << 31)) {
     G2Args a = g2_fwd_args(x, w, y, bias, s);
     if (want) a.stats = slab_of(gemm_g2_stat_rows(M, s.Co));
-    gemm_g2(a, S);
+    gemm_g2(a, cur());
     return a.stats;
   }
   const int K = s.KH * s.KW * s.C;
   float* st = want ? slab_of(gemm_nt_stat_rows(M, s.Co)) : nullptr;
   NtArgs a{static_cast<const bf16*>(x), static_cast<const bf16*>(w), y, M, s.Co, K, 0, K, s.Co,
            kConvFwd, s.N, s.H, s.W, s.C, s.OH, s.OW, s.KH, s.KW, s.SH, s.SW, s.PH, s.PW, bias, nullptr, st, 0, 0};
-  gemm_nt(a, S);
+  gemm_nt(a, cur());
   return st;
 }
 
 void weight_transpose(const void* w, void* wt, int Co, int T, int C) {
-  conv_weight_transpose(kBF16, w, static_cast<bf16*>(wt), Co, T, C, S);
+  conv_weight_transpose(kBF16, w, static_cast<bf16*>(wt), Co, T, C, cur());
 }
 void multi_weight_transpose(const int64_t* table, int n, long max_tiles) {
-  dcnn::multi_weight_transpose(table, n, max_tiles, S);
+  dcnn::multi_weight_transpose(table, n, max_tiles, cur());
 }
 
 const float* conv_dgrad(const void* dy, const void* w, void* dx, const ConvShape& s, const void* residual,
@@ -407,7 +534,7 @@ const float* conv_dgrad(const void* dy, const void* w, void* dx, const ConvShape
   const bf16* wt = static_cast<const bf16*>(w);
   if (!w_transposed) {
     bf16* t = static_cast<bf16*>(scratch(W_T, (size_t)s.Co * T * s.C * 2));
-    conv_weight_transpose(kBF16, w, t, s.Co, T, s.C, S);  // [Co][T][C] -> [C][T][Co]
+    conv_weight_transpose(kBF16, w, t, s.Co, T, s.C, cur());  // [Co][T][C] -> [C][T][Co]
     wt = t;
   }
   const long dyb = (long)s.N * s.OH * s.OW * s.Co * 2, wtb = (long)s.C * T * s.Co * 2;
@@ -429,14 +556,14 @@ const float* conv_dgrad(const void* dy, const void* w, void* dx, const ConvShape
       a.stats = slab_of(hconv_stat_rows(s.N, s.OH, s.OW, s.Co, s.C, T, 0));
     }
     hconv_workspace(a);
-    hconv(a, S);
+    hconv(a, cur());
     return a.stats;
   }
   if (route == ROUTE_G1S) {  // streaming 1x1 data gradient
     const int M = s.N * s.H * s.W;
     float* st = bnb ? slab_of(g1s_rows(M, s.C, s.Co, 2)) : nullptr;
     g1s(static_cast<const bf16*>(dy), wt, static_cast<bf16*>(dx), M, s.C, s.Co, s.H, s.W, s.H, s.W, 1, nullptr,
-        static_cast<const bf16*>(residual), st, 0, nullptr, 0, bnb ? ba : BnbArgs{}, bnb ? 2 : 0, S);
+        static_cast<const bf16*>(residual), st, 0, nullptr, 0, bnb ? ba : BnbArgs{}, bnb ? 2 : 0, cur());
     return st;
   }
   if (route != ROUTE_GENERIC && dyb < (1l << 31) && wtb < (1l << 31)) {
@@ -484,14 +611,14 @@ const float* conv_dgrad(const void* dy, const void* w, void* dx, const ConvShape
           a.cls_t0[k] = cls[k].t0; a.cls_nt[k] = cls[k].nt; a.cls_ory[k] = cls[k].ry; a.cls_orx[k] = cls[k].rx;
         }
       }
-      gemm_g2(a, S);
+      gemm_g2(a, cur());
       return nullptr;
     }
   }
   NtArgs a{static_cast<const bf16*>(dy), wt, dx, s.N * s.H * s.W, s.C, K, 0, K, s.C, kConvDgrad, s.N, s.OH, s.OW,
            s.Co, s.H, s.W, s.KH, s.KW, s.SH, s.SW, s.PH, s.PW, nullptr, static_cast<const bf16*>(residual), nullptr,
            0, 0};
-  gemm_nt(a, S);
+  gemm_nt(a, cur());
   return nullptr;
 }
 
@@ -509,7 +636,7 @@ void conv_wgrad(const void* dy, const void* x, float* gw, float* gb, const ConvS
     a.dy_bytes = (unsigned)dyb; a.x_bytes = (unsigned)xb;
     a.NB = s.N; a.H = s.H; a.W = s.W; a.Cs = s.C; a.Co = s.Co; a.ntaps = 9;
     for (int t = 0; t < 9; ++t) { a.tap_dy[t] = t / 3 - 1; a.tap_dx[t] = t % 3 - 1; }
-    hwgrad(a, splits, S);
+    hwgrad(a, splits, cur());
     wgrad_reduce(hold, bhold, slab, gw, (long)s.Co * Ng, bslab, gb, s.Co, splits);
     return;
   }
@@ -527,7 +654,7 @@ void conv_wgrad(const void* dy, const void* x, float* gw, float* gb, const ConvS
     for (int ky = 0; ky < s.KH; ++ky)
       for (int kx = 0; kx < s.KW; ++kx, ++t) { a.tap_dy[t] = ky - s.PH; a.tap_dx[t] = kx - s.PW; }
     a.ntaps = t;
-    gemm_t2(a, splits, S);
+    gemm_t2(a, splits, cur());
     wgrad_reduce(hold, bhold, slab, gw, (long)s.Co * Ng, bslab, gb, s.Co, splits);
     return;
   }
@@ -537,7 +664,7 @@ void conv_wgrad(const void* dy, const void* x, float* gw, float* gb, const ConvS
   float* bslab = gb ? wgrad_slab(BSLAB, (size_t)splits * s.Co * 4, bhold) : nullptr;
   TnArgs a{static_cast<const bf16*>(dy), static_cast<const bf16*>(x), slab, bslab, s.Co, Ng, P, kConvFwd, s.N, s.H,
            s.W, s.C, s.OH, s.OW, s.KH, s.KW, s.SH, s.SW, s.PH, s.PW, 0, 0};
-  gemm_tn(a, splits, S);
+  gemm_tn(a, splits, cur());
   wgrad_reduce(hold, bhold, slab, gw, (long)s.Co * Ng, bslab, gb, s.Co, splits);
 }
 
@@ -557,7 +684,7 @@ const float* stem_fwd(const float* x, const void* w, const float* bias, void* y,
     *stat_rows = stem_tiles_host(s.N, s.H, s.W);
     a.slab = static_cast<float*>(scratch(FWD_STATS, (size_t)*stat_rows * 3 * s.Co * 4));
   }
-  dcnn::stem_fwd(a, S);
+  dcnn::stem_fwd(a, cur());
   return a.slab;
 }
 
@@ -572,22 +699,22 @@ void stem_wgrad(const void* dy, const float* x, float* gw, float* gb, const Conv
   a.gs[0] = 9l * s.C; a.gs[1] = 1; a.gs[2] = 3l * s.C; a.gs[3] = s.C;
   a.n_slab = n;
   a.N = s.N; a.Ci = s.C; a.H = s.H; a.W = s.W; a.Co = s.Co;
-  dcnn::stem_wgrad(a, blocks, S);
+  dcnn::stem_wgrad(a, blocks, cur());
   wgrad_reduce(hold, bhold, slab, gw, n, bslab, gb, s.Co, blocks);
 }
 
 void dense_fwd(const void* x, const void* w, const float* bias, void* y, int N, int In, int Out) {
   NtArgs a{static_cast<const bf16*>(x), static_cast<const bf16*>(w), y, N, Out, In, In, In, Out, kPlain, 0, 0, 0, 0,
            1, 1, 1, 1, 1, 1, 0, 0, bias, nullptr, nullptr, 0, 0};
-  gemm_nt(a, S);
+  gemm_nt(a, cur());
 }
 
 void dense_dgrad(const void* dy, const void* w, void* dx, int N, int In, int Out) {
   bf16* wt = static_cast<bf16*>(scratch(W_T, (size_t)In * Out * 2));
-  conv_weight_transpose(kBF16, w, wt, Out, 1, In, S);  // [Out][In] -> [In][Out]
+  conv_weight_transpose(kBF16, w, wt, Out, 1, In, cur());  // [Out][In] -> [In][Out]
   NtArgs a{static_cast<const bf16*>(dy), wt, dx, N, In, Out, Out, Out, In, kPlain, 0, 0, 0, 0, 1, 1, 1, 1, 1, 1, 0, 0,
            nullptr, nullptr, nullptr, 0, 0};
-  gemm_nt(a, S);
+  gemm_nt(a, cur());
 }
 
 void dense_wgrad(const void* dy, const void* x, float* gw, float* gb, int N, int In, int Out) {
@@ -597,7 +724,7 @@ void dense_wgrad(const void* dy, const void* x, float* gw, float* gb, int N, int
   float* bslab = gb ? wgrad_slab(BSLAB, (size_t)splits * Out * 4, bhold) : nullptr;
   TnArgs a{static_cast<const bf16*>(dy), static_cast<const bf16*>(x), slab, bslab, Out, In, N, kPlain, 0, 0, 0, 0, 1,
            1, 1, 1, 1, 1, 0, 0, In, 0};
-  gemm_tn(a, splits, S);
+  gemm_tn(a, splits, cur());
   wgrad_reduce(hold, bhold, slab, gw, (long)Out * In, bslab, gb, Out, splits);
 }
 
@@ -606,7 +733,7 @@ static std::pair<const float*, int> reduce_stats(int mode, const float* slab, in
   const int parts = bn_stat_parts(rows);
   float* sums = static_cast<float*>(scratch(STAT_SUMS, (size_t)2 * C * 4));
   float* part = parts > 1 ? static_cast<float*>(scratch(STAT_PART, (size_t)parts * 3 * C * 4)) : nullptr;
-  bn_stat_reduce(mode, slab, rows, C, sums, part, nullptr, S);
+  bn_stat_reduce(mode, slab, rows, C, sums, part, nullptr, cur());
   return {parts > 1 ? part : sums, parts};
 }
 
@@ -614,15 +741,15 @@ void bn_fwd(const void* x, void* y, long R, int C, const float* g, const float* 
             float* rmean, float* rvar, float momentum, float* smean, float* sistd, bool relu, const void* residual) {
   if (!train) {
     bn_apply(kBF16, x, y, R, C, nullptr, 1, (float)R, g, b, eps, residual, relu ? 1 : 0, smean, sistd, rmean, rvar,
-             momentum, 1, S);
+             momentum, 1, cur());
     return;
   }
   const int rows = bn_partial_rows(R, C);
   float* slab = static_cast<float*>(scratch(STAT_SLAB, (size_t)rows * 3 * C * 4));
-  bn_partial(kBF16, x, nullptr, nullptr, nullptr, nullptr, nullptr, R, C, slab, 0, nullptr, S);
+  bn_partial(kBF16, x, nullptr, nullptr, nullptr, nullptr, nullptr, R, C, slab, 0, nullptr, cur());
   const auto st = reduce_stats(0, slab, rows, C);
   bn_apply(kBF16, x, y, R, C, st.first, st.second, (float)R, g, b, eps, residual, relu ? 1 : 0, smean, sistd, rmean,
-           rvar, momentum, 0, S);
+           rvar, momentum, 0, cur());
 }
 
 void bn_fwd_slab(const void* x, void* y, long R, int C, const float* slab, int rows, const float* g, const float* b,
@@ -630,37 +757,56 @@ void bn_fwd_slab(const void* x, void* y, long R, int C, const float* slab, int r
                  const void* residual) {
   const auto st = reduce_stats(0, slab, rows, C);
   bn_apply(kBF16, x, y, R, C, st.first, st.second, (float)R, g, b, eps, residual, relu ? 1 : 0, smean, sistd, rmean,
-           rvar, momentum, 0, S);
+           rvar, momentum, 0, cur());
 }
 
 void bn_bwd_slab(const void* dy, const void* x, void* dx, long R, int C, const float* mean, const float* istd,
                  const float* g, float* dg, float* db, bool train, const float* slab, int rows) {
   const auto st = reduce_stats(1, slab, rows, C);
-  bn_bwd_apply(kBF16, dy, nullptr, x, dx, R, C, mean, istd, g, st.first, st.second, (float)R, dg, db, train ? 0 : 1, S);
+  bn_bwd_apply(kBF16, dy, nullptr, x, dx, R, C, mean, istd, g, st.first, st.second, (float)R, dg, db, train ? 0 : 1, cur());
 }
 
 void bn_bwd(const void* dy, const void* x, void* dx, long R, int C, const float* mean, const float* istd,
             const float* g, float* dg, float* db, bool train, const void* yout, void* dy_out) {
   const int rows = bn_partial_rows(R, C);
   float* slab = static_cast<float*>(scratch(STAT_SLAB, (size_t)rows * 2 * C * 4));
-  bn_partial(kBF16, x, dy, yout, dy_out, mean, istd, R, C, slab, 1, nullptr, S);
+  bn_partial(kBF16, x, dy, yout, dy_out, mean, istd, R, C, slab, 1, nullptr, cur());
   const auto st = reduce_stats(1, slab, rows, C);
-  bn_bwd_apply(kBF16, dy, yout, x, dx, R, C, mean, istd, g, st.first, st.second, (float)R, dg, db, train ? 0 : 1, S);
+  bn_bwd_apply(kBF16, dy, yout, x, dx, R, C, mean, istd, g, st.first, st.second, (float)R, dg, db, train ? 0 : 1, cur());
 }
 
 void maxpool_fwd(const void* x, void* y, uint8_t* idx, const PoolShape& p) {
   if (p.KH * p.KW > 256) throw std::invalid_argument("maxpool: window larger than 256 taps");
-  dcnn::maxpool_fwd(kBF16, x, y, idx, geom(p), S);
+  dcnn::maxpool_fwd(kBF16, x, y, idx, geom(p), cur());
 }
 void maxpool_bwd(const void* dy, const uint8_t* idx, void* dx, const PoolShape& p) {
-  dcnn::maxpool_bwd(kBF16, dy, idx, dx, geom(p), S);
+  dcnn::maxpool_bwd(kBF16, dy, idx, dx, geom(p), cur());
 }
-void avgpool_fwd(const void* x, void* y, const PoolShape& p) { dcnn::avgpool_fwd(kBF16, x, y, geom(p), S); }
-void avgpool_bwd(const void* dy, void* dx, const PoolShape& p) { dcnn::avgpool_bwd(kBF16, dy, dx, geom(p), S); }
+void avgpool_fwd(const void* x, void* y, const PoolShape& p) { dcnn::avgpool_fwd(kBF16, x, y, geom(p), cur()); }
+void avgpool_bwd(const void* dy, void* dx, const PoolShape& p) { dcnn::avgpool_bwd(kBF16, dy, dx, geom(p), cur()); }
 
-void act_fwd(int kind, const void* x, void* y, long n, float alpha) { dcnn::act_fwd(kBF16, x, y, n, kind, alpha, S); }
+void act_fwd(int kind, const void* x, void* y, long n, float alpha) { dcnn::act_fwd(kBF16, x, y, n, kind, alpha, cur()); }
 void act_bwd(int kind, const void* x, const void* dy, void* dx, long n, float alpha) {
-  dcnn::act_bwd(kBF16, x, dy, dx, n, kind, alpha, S);
+  dcnn::act_bwd(kBF16, x, dy, dx, n, kind, alpha, cur());
+}
+
+// the fused loss kernels leave {loss (fp32), -, correct (int32)} in the LOSS_OUT slot; eager calls
+// read it back, inside a graph capture the value stays on the device (loss_device())
+double read_loss(const char* out, long* correct) {
+  if (gpu::Graph::capturing()) {
+    if (correct) *correct = -1;
+    return std::nan("");
+  }
+  char host[16];
+  hipStream_t s = cur();
+  HOST_HIP_CHECK(hipMemcpyAsync(host, out, 16, hipMemcpyDeviceToHost, s));
+  HOST_HIP_CHECK(hipStreamSynchronize(s));
+  float l;
+  int c;
+  std::memcpy(&l, host, 4);
+  std::memcpy(&c, host + 8, 4);
+  if (correct) *correct = c;
+  return l;
 }
 
 double softmax_ce(const void* pred, const int64_t* labels, void* grad, int N, int C, long* correct) {
@@ -668,21 +814,14 @@ double softmax_ce(const void* pred, const int64_t* labels, void* grad, int N, in
   static unsigned* tickets = nullptr;  // zeroed once; every launch leaves them zeroed
   if (N > 4 && !tickets) {
     tickets = static_cast<unsigned*>(scratch(TICKETS, 64 * 4));
-    HOST_HIP_CHECK(hipMemset(tickets, 0, 64 * 4));
+    HOST_HIP_CHECK(hipMemsetAsync(tickets, 0, 64 * 4, cur()));
   }
   char* out = static_cast<char*>(scratch(LOSS_OUT, 16));
   float* loss = reinterpret_cast<float*>(out);
   int* corr = reinterpret_cast<int*>(out + 8);
   loss_fused(kBF16, pred, nullptr, labels, grad, loss, corr, N, C, 1, 1e-15f, 1.0f, ws, N > 4 ? tickets : nullptr,
-             S);
-  char host[16];
-  HOST_HIP_CHECK(hipMemcpy(host, out, 16, hipMemcpyDeviceToHost));
-  float l;
-  int c;
-  std::memcpy(&l, host, 4);
-  std::memcpy(&c, host + 8, 4);
-  if (correct) *correct = c;
-  return l;
+             cur());
+  return read_loss(out, correct);
 }
 
 double loss(int kind, const void* pred, const float* target, const int64_t* labels, void* grad, int N, int C,
@@ -691,57 +830,58 @@ double loss(int kind, const void* pred, const float* target, const int64_t* labe
   static unsigned* tickets = nullptr;
   if (N > 4 && !tickets) {
     tickets = static_cast<unsigned*>(scratch(TICKETS, 64 * 4));
-    HOST_HIP_CHECK(hipMemset(tickets, 0, 64 * 4));
+    HOST_HIP_CHECK(hipMemsetAsync(tickets, 0, 64 * 4, cur()));
   }
   char* out = static_cast<char*>(scratch(LOSS_OUT, 16));
   loss_fused(kBF16, pred, target, labels, grad, reinterpret_cast<float*>(out), reinterpret_cast<int*>(out + 8), N, C,
-             kind, param, 1.0f, ws, N > 4 ? tickets : nullptr, S);
-  char host[16];
-  HOST_HIP_CHECK(hipMemcpy(host, out, 16, hipMemcpyDeviceToHost));
-  float l;
-  int c;
-  std::memcpy(&l, host, 4);
-  std::memcpy(&c, host + 8, 4);
-  if (correct) *correct = c;
-  return l;
+             kind, param, 1.0f, ws, N > 4 ? tickets : nullptr, cur());
+  return read_loss(out, correct);
 }
 
 void groupnorm_fwd(const void* x, void* y, int N, int HW, int C, int G, const float* g, const float* b, float eps,
                    float* smean, float* sistd) {
-  gn_fwd(kBF16, x, y, N, HW, C, G, g, b, eps, smean, sistd, S);
+  gn_fwd(kBF16, x, y, N, HW, C, G, g, b, eps, smean, sistd, cur());
 }
 
 void groupnorm_bwd(const void* dy, const void* x, void* dx, int N, int HW, int C, int G, const float* g,
                    const float* mean, const float* istd, float* dg, float* db) {
   float* aff = static_cast<float*>(scratch(GN_AFF, (size_t)N * 2 * C * 4));  // per-image affine partials
-  gn_bwd(kBF16, dy, x, dx, N, HW, C, G, g, mean, istd, dg, db, aff, S);
+  gn_bwd(kBF16, dy, x, dx, N, HW, C, G, g, mean, istd, dg, db, aff, cur());
 }
 
-void softmax_fwd(const void* x, void* y, long rows, int C) { softmax_rows(kBF16, x, y, rows, C, S); }
+void softmax_fwd(const void* x, void* y, long rows, int C) { softmax_rows(kBF16, x, y, rows, C, cur()); }
 void softmax_bwd(const void* y, const void* dy, void* dx, long rows, int C) {
-  softmax_rows_bwd(kBF16, y, dy, dx, rows, C, S);
+  softmax_rows_bwd(kBF16, y, dy, dx, rows, C, cur());
 }
-void dropout(const void* x, void* y, long n, float p, uint64_t seed) { dcnn::dropout(kBF16, x, y, n, p, seed, nullptr, S); }
+void dropout(const void* x, void* y, long n, float p, uint64_t seed) { dcnn::dropout(kBF16, x, y, n, p, seed, nullptr, cur()); }
 
 void add(const void* a, const void* b, void* y, long n, bool relu) {
-  hipLaunchKernelGGL(add_bf16_kernel, dim3(grid_of(n)), dim3(256), 0, S, static_cast<const bf16*>(a),
+  hipLaunchKernelGGL(add_bf16_kernel, dim3(grid_of(n)), dim3(256), 0, cur(), static_cast<const bf16*>(a),
                      static_cast<const bf16*>(b), static_cast<bf16*>(y), n, relu ? 1 : 0);
   HOST_HIP_CHECK(hipGetLastError());
 }
 
 void relu_mask(const void* dy, const void* y, void* dx, long n) {
-  hipLaunchKernelGGL(relu_mask_bf16_kernel, dim3(grid_of(n)), dim3(256), 0, S, static_cast<const bf16*>(dy),
+  hipLaunchKernelGGL(relu_mask_bf16_kernel, dim3(grid_of(n)), dim3(256), 0, cur(), static_cast<const bf16*>(dy),
                      static_cast<const bf16*>(y), static_cast<bf16*>(dx), n);
   HOST_HIP_CHECK(hipGetLastError());
 }
 
 void adam(float* p, const float* g, float* m, float* v, void* shadow, long n, float lr, float b1, float b2, float eps,
           float bc1, float bc2, float wd, bool decoupled) {
-  adam_step(p, g, m, v, static_cast<bf16*>(shadow), n, lr, b1, b2, eps, bc1, bc2, wd, decoupled ? 1 : 0, nullptr, S);
+  adam_step(p, g, m, v, static_cast<bf16*>(shadow), n, lr, b1, b2, eps, bc1, bc2, wd, decoupled ? 1 : 0, nullptr, cur());
+}
+
+const void* loss_device() { return scratch(LOSS_OUT, 16); }
+
+void adam_hyper_step(float* hyper, float b1, float b2) { adam_scalars(hyper, b1, b2, cur()); }
+void adam_dev(float* p, const float* g, float* m, float* v, void* shadow, long n, float b1, float b2, float eps,
+              float wd, bool decoupled, const float* hyper) {
+  adam_step(p, g, m, v, static_cast<bf16*>(shadow), n, 0.f, b1, b2, eps, 1.f, 1.f, wd, decoupled ? 1 : 0, hyper, cur());
 }
 
 void sgd(float* p, const float* g, float* vel, void* shadow, long n, float lr, float momentum) {
-  sgd_step(p, g, vel, static_cast<bf16*>(shadow), n, lr, momentum, nullptr, S);
+  sgd_step(p, g, vel, static_cast<bf16*>(shadow), n, lr, momentum, nullptr, cur());
 }
 
 }  // namespace gpu_ops

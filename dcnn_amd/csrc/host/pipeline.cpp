@@ -365,7 +365,7 @@ Tensor PipelineStage::decode(Message& m) const {
     auto it = ipc_in_.find(key);
     if (it == ipc_in_.end()) it = ipc_in_.emplace(key, gpu::ipc_open(key.data())).first;
     gpu::copy(t.data(), it->second, t.nbytes(), 2);
-    gpu::synchronize();
+    gpu::flow_synchronize();  // (this stage's flow: the copy is done before any reply goes out)
     if (t.rank() == 2) t = t.view({shape[0], shape[1], 1, 1}, Layout::NCHW);
     return t;
   }
@@ -409,7 +409,7 @@ void PipelineStage::send_tensor(const std::string& to, uint16_t cmd, uint64_t mb
         slot.bytes = t.nbytes();
       }
       gpu::copy(slot.ptr, t.data(), t.nbytes(), 2);
-      gpu::synchronize();  // complete before the peer, another process, reads it
+      gpu::flow_synchronize();  // the slot is complete (this stage's flow) before the peer process reads it
       const uint64_t nbytes = t.nbytes();
       m.dtype = code | kIpcRef;
       m.data.assign(slot.handle);

@@ -45,6 +45,74 @@ LossResult Loss::compute(const Tensor& pred, const Tensor* labels_in, const Tens
   return r;
 }
 
+// ================================================================= captured training step
+void TrainGraph::capture(const Tensor& x, const Tensor& labels) {
+  const Device dev = model_.device();
+  sx_ = x.to(dev).clone();
+  sy_ = labels.to(dev).clone();
+  std::vector<Param*> params = model_.parameters();
+  ParamArena* a = params.empty() ? nullptr : params[0]->arena.get();
+  if (!a) throw std::runtime_error("TrainGraph: the model's parameters are not in a GPU arena");
+  // the warm-up steps must not train: snapshot what they change (parameters, moments, shadow)
+  const Tensor v0 = a->value.clone(), m0 = a->m.clone(), w0 = a->v.clone(), s0 = a->shadow.clone();
+  const long t0 = opt_.step_count();
+  auto eager = [&] {
+    model_.zero_grad();
+    LossResult r = loss_(model_.forward(sx_), sy_);
+    model_.backward(r.grad);
+    opt_.step(params);
+  };
+  for (int i = 0; i < 2; ++i) eager();
+  gpu::copy(a->value.data(), v0.data(), v0.nbytes(), 2);
+  gpu::copy(a->m.data(), m0.data(), m0.nbytes(), 2);
+  gpu::copy(a->v.data(), w0.data(), w0.nbytes(), 2);
+  gpu::copy(a->shadow.data(), s0.data(), s0.nbytes(), 2);
+  a->refresh_transposes();
+  opt_.set_step_count(t0);
+  opt_.upload_hyper();
+  gpu::flow_synchronize();
+  graph_.begin();
+  try {
+    eager();
+  } catch (...) {
+    graph_.end();
+    throw;
+  }
+  graph_.end();
+  opt_.set_step_count(t0);  // the captured step has not run yet: each replay advances it
+  opt_.upload_hyper();
+  captured_ = true;
+}
+
+double TrainGraph::step(const Tensor& x, const Tensor& labels) {
+  const Device dev = model_.device();
+  if (!dev.is_gpu()) {  // the CPU backend runs the same step eagerly
+    model_.zero_grad();
+    LossResult r = loss_(model_.forward(x), labels);
+    model_.backward(r.grad);
+    opt_.step(model_.parameters());
+    return r.loss;
+  }
+  if (!captured_) capture(x, labels);
+  if (x.numel() != sx_.numel() || labels.numel() != sy_.numel())
+    throw std::runtime_error("TrainGraph: the batch shape changed after capture");
+  // the batch into the static slots (device-resident batches: stream-ordered D2D copies)
+  if (x.device() == dev) gpu::copy(sx_.data(), x.data(), sx_.nbytes(), 2);
+  else gpu::copy(sx_.data(), x.to(dev).data(), sx_.nbytes(), 2);
+  if (labels.device() == dev) gpu::copy(sy_.data(), labels.data(), sy_.nbytes(), 2);
+  else gpu::copy(sy_.data(), labels.to(dev).data(), sy_.nbytes(), 2);
+  opt_.before_replay();
+  graph_.replay();
+  return std::nan("");
+}
+
+double TrainGraph::last_loss() {
+  if (!model_.device().is_gpu() || !captured_) return std::nan("");
+  float l = 0.f;
+  gpu::copy(&l, gpu_ops::loss_device(), sizeof l, 1);
+  return l;
+}
+
 Loss LossFactory::create(const std::string& name, float param) {
   std::string n = name;
   std::transform(n.begin(), n.end(), n.begin(), ::tolower);

@@ -11,7 +11,7 @@
 //                                              (logical NCHW fp32 records) into out.bin; with a
 //                                              prefix also the initial model (prefix.json/.bin)
 //                                              and the batch (prefix.x.bin, prefix.y.bin)
-//   host_api_parity train <model_name> <steps> <batch> <save> [--device GPU]
+//   host_api_parity train <model_name> <steps> <batch> <save> [--device GPU] [--graph]
 //                                              Adam steps on a synthetic set, then save
 // Output is plain text: one "key v0 v1 ..." line per item.
 #include <cstdio>
@@ -149,8 +149,16 @@ int main(int argc, char** argv) {
       Loss loss = LossFactory::create("softmax_crossentropy");
       data.reset(0);
       Tensor x, y;
+      bool graph = false;  // --graph: the GPU step captured once (TrainGraph) and replayed
+      for (int i = 1; i < argc; ++i) graph = graph || std::string(argv[i]) == "--graph";
+      TrainGraph tg(m, opt, loss);
       std::printf("losses");
       for (int i = 0; i < steps && data.next(batch, x, y); ++i) {
+        if (graph && dev.is_gpu()) {
+          tg.step(x, y);
+          std::printf(" %.6g", tg.last_loss());
+          continue;
+        }
         m.zero_grad();
         LossResult r = loss(m.forward(x), y);
         m.backward(r.grad);

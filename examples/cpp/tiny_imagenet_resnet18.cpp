@@ -4,11 +4,12 @@
 //   dcnn_amd/bin/tiny_imagenet_resnet18 [--device CPU|GPU] [--model resnet18_tiny_imagenet]
 //        [--data data/tiny-imagenet-200] [--epochs E] [--steps S] [--batch B] [--lr 1e-3]
 //        [--loss logsoftmax_ce] [--scheduler cosine_annealing_lr] [--max-per-class K]
-//        [--save model_snapshots/resnet18] [--bench]
+//        [--save model_snapshots/resnet18] [--bench [--eager]]
 //
 // Without --data it trains on a learnable synthetic 3x64x64 200-class set. --bench times
 // --steps training steps after 3 warm-up steps on two device-resident synthetic batches and
-// prints one JSON line (images/sec). The saved
+// prints one JSON line (images/sec); on the GPU the step is captured into a hipGraph
+// (dcnn::TrainGraph) and replayed, --eager launches every kernel from the host instead. The saved
 // model (path.json + path.bin + path.bnstats) loads in Python with Sequential.from_file.
 // Honours the reference's .env keys DEVICE_TYPE / EPOCHS / BATCH_SIZE / LR_INITIAL.
 // Reference parity: examples/tiny_imagenet_resnet18.cpp:23-107 (Adam, logsoftmax-CE, profiling),
@@ -38,10 +39,11 @@ int main(int argc, char** argv) {
   int epochs = std::atoi(env_or("EPOCHS", "1").c_str()), steps = -1, max_per_class = 0;
   int batch = std::atoi(env_or("BATCH_SIZE", "64").c_str());
   float lr = std::atof(env_or("LR_INITIAL", "0.001").c_str());
-  bool bench = false;
+  bool bench = false, eager = false;
   for (int i = 1; i < argc; ++i) {
     const std::string k = argv[i];
     if (k == "--bench") { bench = true; continue; }
+    if (k == "--eager") { eager = true; continue; }
     if (i + 1 >= argc) break;
     const std::string v = argv[++i];
     if (k == "--device") device = v;
@@ -93,8 +95,13 @@ int main(int argc, char** argv) {
       }
       const int timed = steps > 0 ? steps : 20;
       int k = 0;
+      // GPU: the step captured into a hipGraph (TrainGraph: gpu::Graph on the thread's flow) and
+      // replayed with one launch per step; --eager launches every kernel from the host
+      const bool graph = dev.is_gpu() && !eager;
+      TrainGraph tg(model, opt, loss);
       auto one = [&] {
         const auto& [x, y] = staged[(size_t)(k++) % staged.size()];
+        if (graph) return tg.step(x, y);
         model.zero_grad();
         Tensor logits = model.forward(x);
         LossResult r = loss(logits, y);
@@ -109,10 +116,11 @@ int main(int argc, char** argv) {
       for (int i = 0; i < timed; ++i) last = one();
       if (dev.is_gpu()) gpu::synchronize();
       const double s = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+      if (graph) last = tg.last_loss();
       std::printf("{\"metric\": \"images/sec %s training (C++ host API)\", \"value\": %.1f, \"ms_per_step\": %.3f, "
-                  "\"batch\": %d, \"steps\": %d, \"device\": \"%s\", \"loss\": %.4f}\n",
+                  "\"batch\": %d, \"steps\": %d, \"device\": \"%s\", \"hipgraph\": %s, \"loss\": %.4f}\n",
                   model_name.c_str(), (double)batch * timed / s, 1e3 * s / timed, batch, timed, dev.str().c_str(),
-                  last);
+                  graph ? "true" : "false", last);
       return 0;
     }
     std::unique_ptr<Scheduler> sched;

@@ -315,3 +315,24 @@ def test_cpp_and_python_cpu_gradients_identical(bins, tmp_path):
     assert len(gp) == len(gc) > 40
     for k, (a, b) in enumerate(zip(gp, gc)):
         assert torch.equal(a.detach().reshape(b.shape), b), k
+
+
+@pytest.mark.gpu
+def test_cpp_train_graph_replay_matches_eager(bins, tmp_path):
+    """dcnn::TrainGraph (gpu::Graph capture of the whole C++ training step on the thread's flow,
+    graph-owned allocations, device-resident Adam scalars, deferred loss readback): the replayed
+    steps give bit-identical losses and trained weights to the eager steps (deterministic kernels),
+    and the warm-up steps of the capture do not train."""
+    args = ["train", "resnet18_tiny_imagenet", "4", "8"]
+    e = _lines(_run([bins["host_api_parity"], *args, "snap/e", "--device", "GPU"], tmp_path, timeout=300))
+    g = _lines(_run([bins["host_api_parity"], *args, "snap/g", "--device", "GPU", "--graph"], tmp_path, timeout=300))
+    assert e["losses"] == g["losses"], (e["losses"], g["losses"])
+    assert (tmp_path / "snap" / "e.bin").read_bytes() == (tmp_path / "snap" / "g.bin").read_bytes()
+
+
+@pytest.mark.gpu
+def test_cpp_tiny_imagenet_trainer_graph_bench(bins, tmp_path):
+    out = _run([bins["tiny_imagenet_resnet18"], "--device", "GPU", "--batch", "64", "--steps", "10", "--bench"],
+               tmp_path, timeout=300)
+    assert '"hipgraph": true' in out and re.search(r"\"value\": (\S+),", out), out
+    print(out)
