@@ -182,6 +182,16 @@ class BatchNorm : public Layer {
   // shortcut branch receives
   Tensor forward_residual(const Tensor& x, const Tensor& residual, bool relu, bool training);
   Tensor backward_residual(const Tensor& dy, Tensor* branch);
+  // GPU pairing with a projection shortcut's BatchNorm (`deferred`): forward_deferred takes that
+  // layer's statistics rows now; the tail's forward_dual applies both BatchNorms, the residual add
+  // and the activation in one pass. backward_dual: both data gradients from one pass over the
+  // tail's masked gradient (false: not applicable, the caller runs the two backwards)
+  void forward_deferred(const Tensor& x, bool training);
+  Tensor forward_dual(const Tensor& x, BatchNorm& deferred, bool relu, bool training);
+  bool backward_dual(const Tensor& dy, BatchNorm& deferred, Tensor& dx, Tensor& dx_deferred);
+  // GPU: the following ReLU + max-pool run inside this layer's training apply (fuse_bn_relu; the
+  // stem's BatchNorm -> ReLU -> max-pool)
+  void set_fused_pool(class Pool2D* p) { fused_pool_ = p; }
   // backward-fusion operands of micro-batch `mb` (its forward's input, output mask, statistics)
   gpu_ops::BnbOperands bnb_operands(int mb);
   // the next backward over the gradient at `dy` takes its statistics from this consumer slab (the
@@ -206,6 +216,9 @@ class BatchNorm : public Layer {
   bool train_ = true;
   bool fused_relu_ = false;
   Tensor forward_impl(const Tensor& x, bool training, const Tensor* residual, bool relu);
+  Tensor apply_deferred(bool training);
+  class Pool2D* fused_pool_ = nullptr;
+  gpu_ops::BnRaw deferred_raw_{nullptr, 0};
   const void* bwd_dy_ = nullptr;
   const float* bwd_slab_ = nullptr;
   int bwd_rows_ = 0;
@@ -279,9 +292,18 @@ class Pool2D : public Layer {
   std::vector<int64_t> output_shape(const std::vector<int64_t>& in) const override;
   Tensor forward(const Tensor& x, bool training) override;
   Tensor backward(const Tensor& dy) override;
+  bool is_max() const { return max_; }
+  PoolShape shape_for(const std::vector<int64_t>& in) const;
+  // GPU: the preceding BatchNorm + ReLU computes this pool's output in its training apply
+  // (BatchNorm::set_fused_pool); forward then passes it through and backward is the max-pool
+  // backward fused with that BatchNorm's backward statistics
+  void set_fused_producer(class BatchNorm* bn) { bn_ = bn; }
+  // the index buffer for a pre-pooled output `ypool` of an input of shape `in`
+  uint8_t* accept_prepooled(const Tensor& ypool, const std::vector<int64_t>& in);
+  void clear_prepooled() { mbc().flag = false; }
 
  private:
-  PoolShape shape_for(const std::vector<int64_t>& in) const;
+  class BatchNorm* bn_ = nullptr;
   bool max_;
   int kh_, kw_, sh_, sw_, ph_, pw_;
 };
@@ -320,6 +342,9 @@ class ResidualBlock : public Layer {
   class BatchNorm* fused_tail() const;
   // the main path's first layer when it is a conv (its dgrad adds the shortcut gradient)
   class Conv2D* head_conv() const;
+  // GPU: the projection shortcut's closing BatchNorm, paired with the fused tail
+  // (BatchNorm::forward_dual / backward_dual); null without one
+  class BatchNorm* dual_shortcut() const;
 
  private:
   std::vector<std::unique_ptr<Layer>> main_, short_;

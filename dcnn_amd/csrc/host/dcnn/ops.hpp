@@ -117,6 +117,61 @@ void bn_bwd_slab(const void* dy, const void* x, void* dx, long R, int C, const f
 // dy is also stored there (the shortcut branch of a residual block)
 void bn_bwd(const void* dy, const void* x, void* dx, long R, int C, const float* mean, const float* istd,
             const float* g, float* dg, float* db, bool train, const void* yout = nullptr, void* dy_out = nullptr);
+// ---- paired BatchNorms: a residual block's tail BatchNorm and its projection shortcut's
+// BatchNorm share one apply pass forward (the shortcut's normalised output is never written) and
+// one pass over the shared gradient backward; both statistics reduces run in one launch.
+// While a SecondaryStats scope is alive on this thread, conv_fwd / stem_fwd write their statistics
+// slab to a second workspace, so the shortcut conv's slab survives the main path's convs.
+struct SecondaryStats {
+  SecondaryStats();
+  ~SecondaryStats();
+};
+// raw training statistics rows of x ([rows][3][C] Welford triples): the producer's slab when
+// given, else a statistics pass over x into the secondary workspace
+struct BnRaw {
+  const float* slab;
+  int rows;
+};
+BnRaw bn_stats_raw(const void* x, long R, int C, const float* slab, int rows);
+struct BnFwdSide {
+  const void* x;
+  BnRaw raw;  // training only
+  const float* g;
+  const float* b;
+  float eps;
+  float* rmean;
+  float* rvar;
+  float momentum;
+  float* smean;
+  float* sistd;
+};
+bool bn_dual_ok(long R, int C);
+// y = act(bn_a(a.x) + bn_b(b.x)): train = batch statistics of both sides (saved, running stats
+// updated), else running statistics
+void bn_fwd_dual(const BnFwdSide& a, const BnFwdSide& b, void* y, long R, int C, bool relu, bool train);
+struct BnBwdSides {
+  const void* x;
+  void* dx;
+  const float* mean;
+  const float* istd;
+  const float* g;
+  float* dg;
+  float* db;
+};
+// dx_a and dx_b of two training BatchNorms fed the same (already masked) gradient dy in one pass:
+// a's backward statistics from a consumer slab (conv_dgrad bnb), b's from a statistics pass here
+void bn_bwd_dual(const void* dy, const BnBwdSides& a, const float* slab_a, int rows_a, const BnBwdSides& b, long R,
+                 int C);
+// ---- training BatchNorm + ReLU + non-overlapping max-pool in one pass (the stem): the
+// full-resolution output is never stored; statistics from the producer slab (or a pass over x)
+bool bn_relu_maxpool_ok(const PoolShape& p);
+void bn_relu_maxpool(const void* x, void* y, uint8_t* idx, const PoolShape& p, const float* slab, int rows,
+                     const float* g, const float* b, float eps, float* rmean, float* rvar, float momentum,
+                     float* smean, float* sistd);
+// its backward: max-pool backward masked with ypool > 0, plus the BatchNorm's backward statistics
+// slab (returned, *rows set) for bn_bwd_slab
+const float* maxpool_bwd_bnb(const void* dy, const uint8_t* idx, const void* ypool, const void* x, const float* mean,
+                             const float* istd, void* dx, const PoolShape& p, int* rows);
 void maxpool_fwd(const void* x, void* y, uint8_t* idx, const PoolShape& p);
 void maxpool_bwd(const void* dy, const uint8_t* idx, void* dx, const PoolShape& p);
 void avgpool_fwd(const void* x, void* y, const PoolShape& p);

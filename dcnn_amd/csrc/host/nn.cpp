@@ -372,6 +372,25 @@ Tensor BatchNorm::forward_impl(const Tensor& x, bool training, const Tensor* res
   const float* b = affine_ ? params_[1].value.ptr<float>() : nullptr;
   const void* res = residual ? residual->data() : nullptr;
   const bool slab = dev_.is_gpu() && training && pending_x_ == x.data() && pending_slab_ && pending_rows_ > 0;
+  if (fused_pool_ != nullptr) {
+    const PoolShape p = fused_pool_->shape_for(x.shape());
+    if (dev_.is_gpu() && training && relu && residual == nullptr && gpu_ops::bn_relu_maxpool_ok(p)) {
+      // BatchNorm + ReLU + max-pool in one pass: the full-resolution output is never stored, the
+      // pool layer passes this result through (its backward masks with the pooled value)
+      Tensor yp = act_empty({p.N, p.C, p.OH, p.OW}, dev_);
+      uint8_t* idx = fused_pool_->accept_prepooled(yp, x.shape());
+      gpu_ops::bn_relu_maxpool(x.data(), yp.data(), idx, p, slab ? pending_slab_ : nullptr, slab ? pending_rows_ : 0,
+                               g, b, eps_, running_mean.ptr<float>(), running_var.ptr<float>(), momentum_,
+                               mean_.ptr<float>(), istd_.ptr<float>());
+      mc.d = Tensor();
+      pending_x_ = nullptr;
+      pending_slab_ = nullptr;
+      pending_rows_ = 0;
+      x_ = x;
+      return yp;
+    }
+    fused_pool_->clear_prepooled();
+  }
   if (slab) {  // statistics from the producing conv's epilogue
     gpu_ops::bn_fwd_slab(x.data(), y.data(), N * HW, c_, pending_slab_, pending_rows_, g, b, eps_,
                          running_mean.ptr<float>(), running_var.ptr<float>(), momentum_, mean_.ptr<float>(),
@@ -390,6 +409,113 @@ Tensor BatchNorm::forward_impl(const Tensor& x, bool training, const Tensor* res
   pending_rows_ = 0;
   x_ = x;
   return y;
+}
+
+void BatchNorm::forward_deferred(const Tensor& x, bool training) {
+  check_act(x, dev_, "batchnorm");
+  if (!dev_.is_gpu()) throw std::runtime_error(name_ + ": forward_deferred is a GPU fusion");
+  if (x.dim(1) != c_) throw std::runtime_error(name_ + ": channel count mismatch");
+  MbCache& mc = mbc();
+  mc.a = x;
+  mc.b.ensure({c_}, DType::F32, dev_);
+  mc.c.ensure({c_}, DType::F32, dev_);
+  mc.d = Tensor();
+  train_ = training;
+  deferred_raw_ = gpu_ops::BnRaw{nullptr, 0};
+  if (training) {
+    const bool slab = pending_x_ == x.data() && pending_slab_ && pending_rows_ > 0;
+    deferred_raw_ = gpu_ops::bn_stats_raw(x.data(), x.dim(0) * x.dim(2) * x.dim(3), c_, slab ? pending_slab_ : nullptr,
+                                          slab ? pending_rows_ : 0);
+  }
+  pending_x_ = nullptr;
+  pending_slab_ = nullptr;
+  pending_rows_ = 0;
+}
+
+// the deferred BatchNorm's own output (when the consumer cannot pair it)
+Tensor BatchNorm::apply_deferred(bool training) {
+  MbCache& mc = mbc();
+  const Tensor& x = mc.a;
+  const long R = x.dim(0) * x.dim(2) * x.dim(3);
+  Tensor y = act_empty(x.shape(), dev_);
+  const float* g = affine_ ? params_[0].value.ptr<float>() : nullptr;
+  const float* b = affine_ ? params_[1].value.ptr<float>() : nullptr;
+  if (training)
+    gpu_ops::bn_fwd_slab(x.data(), y.data(), R, c_, deferred_raw_.slab, deferred_raw_.rows, g, b, eps_,
+                         running_mean.ptr<float>(), running_var.ptr<float>(), momentum_, mc.b.ptr<float>(),
+                         mc.c.ptr<float>(), false);
+  else
+    gpu_ops::bn_fwd(x.data(), y.data(), R, c_, g, b, eps_, false, running_mean.ptr<float>(), running_var.ptr<float>(),
+                    momentum_, mc.b.ptr<float>(), mc.c.ptr<float>());
+  return y;
+}
+
+Tensor BatchNorm::forward_dual(const Tensor& x, BatchNorm& o, bool relu, bool training) {
+  check_act(x, dev_, "batchnorm");
+  if (x.dim(1) != c_) throw std::runtime_error(name_ + ": channel count mismatch");
+  MbCache& oc = o.mbc();
+  const long R = x.dim(0) * x.dim(2) * x.dim(3);
+  if (oc.a.shape() != x.shape() || o.c_ != c_ || !gpu_ops::bn_dual_ok(R, c_)) {
+    const Tensor ys = o.apply_deferred(training);
+    return forward_impl(x, training, &ys, relu);
+  }
+  MbCache& mc = mbc();
+  mc.b.ensure({c_}, DType::F32, dev_);
+  mc.c.ensure({c_}, DType::F32, dev_);
+  train_ = training;
+  gpu_ops::BnRaw raw{nullptr, 0};
+  if (training) {
+    const bool slab = pending_x_ == x.data() && pending_slab_ && pending_rows_ > 0;
+    raw = gpu_ops::bn_stats_raw(x.data(), R, c_, slab ? pending_slab_ : nullptr, slab ? pending_rows_ : 0);
+  }
+  auto side = [](BatchNorm& l, MbCache& c, const gpu_ops::BnRaw& r) {
+    return gpu_ops::BnFwdSide{c.a.data(),
+                              r,
+                              l.affine_ ? l.params_[0].value.ptr<float>() : nullptr,
+                              l.affine_ ? l.params_[1].value.ptr<float>() : nullptr,
+                              l.eps_,
+                              l.running_mean.ptr<float>(),
+                              l.running_var.ptr<float>(),
+                              l.momentum_,
+                              c.b.ptr<float>(),
+                              c.c.ptr<float>()};
+  };
+  mc.a = x;
+  Tensor y = act_empty(x.shape(), dev_);
+  gpu_ops::bn_fwd_dual(side(*this, mc, raw), side(o, oc, o.deferred_raw_), y.data(), R, c_, relu, training);
+  mc.d = relu ? y : Tensor();
+  pending_x_ = nullptr;
+  pending_slab_ = nullptr;
+  pending_rows_ = 0;
+  o.deferred_raw_ = gpu_ops::BnRaw{nullptr, 0};
+  return y;
+}
+
+bool BatchNorm::backward_dual(const Tensor& dy, BatchNorm& o, Tensor& dx, Tensor& dx_o) {
+  MbCache& mc = mbc();
+  MbCache& oc = o.mbc();
+  const Tensor& x_ = mc.a;
+  if (!dev_.is_gpu() || bwd_dy_ != dy.data() || bwd_slab_ == nullptr || bwd_rows_ <= 0 || !train_ || !o.train_ ||
+      oc.a.shape() != x_.shape() || o.c_ != c_)
+    return false;
+  const long R = x_.dim(0) * x_.dim(2) * x_.dim(3);
+  if (!gpu_ops::bn_dual_ok(R, c_)) return false;
+  dx = act_empty(x_.shape(), dev_);
+  dx_o = act_empty(oc.a.shape(), dev_);
+  auto side = [](BatchNorm& l, MbCache& c, Tensor& d) {
+    return gpu_ops::BnBwdSides{c.a.data(),
+                               d.data(),
+                               c.b.ptr<float>(),
+                               c.c.ptr<float>(),
+                               l.affine_ ? l.params_[0].value.ptr<float>() : nullptr,
+                               l.affine_ ? l.params_[0].grad.ptr<float>() : nullptr,
+                               l.affine_ ? l.params_[1].grad.ptr<float>() : nullptr};
+  };
+  gpu_ops::bn_bwd_dual(dy.data(), side(*this, mc, dx), bwd_slab_, bwd_rows_, side(o, oc, dx_o), R, c_);
+  bwd_dy_ = nullptr;
+  bwd_slab_ = nullptr;
+  bwd_rows_ = 0;
+  return true;
 }
 
 Tensor BatchNorm::backward_residual(const Tensor& dy, Tensor* branch) {
@@ -480,6 +606,15 @@ void fuse_bn_relu(std::vector<std::unique_ptr<Layer>>& seq, bool on) {
     if (bn == nullptr || act == nullptr || !act->is_relu()) continue;
     bn->set_fused_relu(on);
     act->set_passthrough(on);
+  }
+  // BatchNorm -> ReLU -> max-pool: the pool runs inside the BatchNorm's training apply
+  for (size_t i = 0; i + 2 < seq.size(); ++i) {
+    auto* bn = dynamic_cast<BatchNorm*>(seq[i].get());
+    auto* act = dynamic_cast<Activation*>(seq[i + 1].get());
+    auto* pool = dynamic_cast<Pool2D*>(seq[i + 2].get());
+    if (bn == nullptr || act == nullptr || !act->is_relu() || pool == nullptr || !pool->is_max()) continue;
+    bn->set_fused_pool(on ? pool : nullptr);
+    pool->set_fused_producer(on ? bn : nullptr);
   }
 }
 
@@ -716,6 +851,11 @@ void fuse_blocks(std::vector<std::unique_ptr<Layer>>& seq, bool on) {
   }
 }
 
+BatchNorm* ResidualBlock::dual_shortcut() const {
+  if (short_.empty() || fused_tail() == nullptr) return nullptr;
+  return dynamic_cast<BatchNorm*>(short_.back().get());
+}
+
 BatchNorm* ResidualBlock::fused_tail() const {
   if (!dev_.is_gpu() || main_.size() < 2 || (act_ != "relu" && act_ != "linear")) return nullptr;
   return dynamic_cast<BatchNorm*>(main_.back().get());
@@ -725,13 +865,22 @@ Tensor ResidualBlock::forward(const Tensor& x, bool training) {
   check_act(x, dev_, "residual_block");
   Tensor& y_ = mbc().a;
   if (BatchNorm* tail = fused_tail()) {  // y = act(bn(main(x)) + shortcut(x)) in the BN's apply pass
+    // a projection shortcut's closing BatchNorm is applied inside the same pass (forward_dual):
+    // its statistics rows are taken now (the shortcut conv's slab in the secondary workspace, so
+    // the main path's convs leave it intact), its normalised output is never written
+    BatchNorm* sbn = dual_shortcut();
     Tensor sc = x;
-    for (auto& l : short_) sc = l->forward(sc, training);
+    {
+      std::unique_ptr<gpu_ops::SecondaryStats> alt(sbn ? new gpu_ops::SecondaryStats() : nullptr);
+      for (size_t i = 0; i + (sbn ? 1 : 0) < short_.size(); ++i) sc = short_[i]->forward(sc, training);
+    }
+    if (sbn) sbn->forward_deferred(sc, training);
     Tensor m = x;
     for (size_t i = 0; i + 1 < main_.size(); ++i) m = main_[i]->forward(m, training);
     if (m.shape() != sc.shape())
       throw std::runtime_error(name_ + ": main path " + shape_str(m.shape()) + " vs shortcut " + shape_str(sc.shape()));
-    y_ = tail->forward_residual(m, sc, act_ == "relu", training);
+    y_ = sbn ? tail->forward_dual(m, *sbn, act_ == "relu", training)
+             : tail->forward_residual(m, sc, act_ == "relu", training);
     return y_;
   }
   Tensor m = x;
@@ -753,9 +902,15 @@ Tensor ResidualBlock::forward(const Tensor& x, bool training) {
 Tensor ResidualBlock::backward(const Tensor& dy) {
   const Tensor& y_ = mbc().a;
   if (BatchNorm* tail = fused_tail()) {
-    Tensor gs;  // the activation-masked dy, for the shortcut
-    Tensor gm = tail->backward_residual(dy, &gs);
-    for (size_t i = short_.size(); i-- > 0;) gs = short_[i]->backward(gs);
+    Tensor gs, gm;  // gs: the activation-masked dy, for the shortcut
+    BatchNorm* sbn = dual_shortcut();
+    if (sbn != nullptr && tail->backward_dual(dy, *sbn, gm, gs)) {
+      // both BatchNorms' data gradients from one pass; gs is already below the shortcut BatchNorm
+      for (size_t i = short_.size() - 1; i-- > 0;) gs = short_[i]->backward(gs);
+    } else {
+      gm = tail->backward_residual(dy, &gs);
+      for (size_t i = short_.size(); i-- > 0;) gs = short_[i]->backward(gs);
+    }
     for (size_t i = main_.size() - 1; i-- > 1;) gm = main_[i]->backward(gm);
     // the main path's first conv adds the shortcut gradient in its data-gradient epilogue
     auto* head = dynamic_cast<Conv2D*>(main_[0].get());
@@ -846,8 +1001,21 @@ std::vector<int64_t> Pool2D::output_shape(const std::vector<int64_t>& in) const 
   return {in[0], in[1], p.OH, p.OW};
 }
 
+uint8_t* Pool2D::accept_prepooled(const Tensor& ypool, const std::vector<int64_t>& in) {
+  MbCache& mc = mbc();
+  const PoolShape p = shape_for(in);
+  mc.a.ensure({(int64_t)p.N * p.C * p.OH * p.OW}, DType::U8, dev_);
+  mc.b = ypool;
+  mc.shape = in;
+  mc.flag = true;
+  return mc.a.ptr<uint8_t>();
+}
+
 Tensor Pool2D::forward(const Tensor& x, bool training) {
   (void)training;
+  if (bn_ != nullptr && mbc().flag && mbc().b.defined() && mbc().b.data() == x.data())
+    return x;  // computed by the fused BatchNorm + ReLU (accept_prepooled)
+  mbc().flag = false;
   Tensor& idx_ = mbc().a;
   std::vector<int64_t>& in_shape_ = mbc().shape;
   check_act(x, dev_, "pool2d");
@@ -876,6 +1044,16 @@ Tensor Pool2D::backward(const Tensor& dy) {
   const std::vector<int64_t>& in_shape_ = mbc().shape;
   const PoolShape p = shape_for(in_shape_);
   Tensor dx = act_empty(in_shape_, dev_);
+  if (mbc().flag && bn_ != nullptr) {
+    // masked with the pooled value (y > 0) and the BatchNorm's backward statistics in the same
+    // pass; the BatchNorm's backward picks them up (offer_bwd_stats)
+    const gpu_ops::BnbOperands ops = bn_->bnb_operands(mb_);
+    int rows = 0;
+    const float* slab = gpu_ops::maxpool_bwd_bnb(dy.data(), idx_.ptr<uint8_t>(), mbc().b.data(), ops.x, ops.mean,
+                                                 ops.istd, dx.data(), p, &rows);
+    bn_->offer_bwd_stats(dx.data(), slab, rows);
+    return dx;
+  }
   if (max_) {
     if (dev_.is_gpu())
       gpu_ops::maxpool_bwd(dy.data(), idx_.ptr<uint8_t>(), dx.data(), p);

@@ -294,7 +294,7 @@ inline hipStream_t cur() { return static_cast<hipStream_t>(gpu::flow()); }
 
 // grow-only workspace per purpose
 enum Slot { W_T = 0, SLAB, BSLAB, STAT_SLAB, STAT_SUMS, STAT_PART, LOSS_WS, LOSS_OUT, TICKETS, HPART, HTICKETS, GN_AFF,
-            FWD_STATS, BWD_STATS, NSLOTS };
+            FWD_STATS, BWD_STATS, FWD_STATS2, STAT_SLAB2, STAT_SUMS2, STAT_PART2, NSLOTS };
 void* scratch(Slot s, size_t bytes) {
   static void* p[NSLOTS] = {};
   static size_t n[NSLOTS] = {};
@@ -399,6 +399,10 @@ G2Args g2_fwd_args(const void* x, const void* w, void* y, const float* bias, con
   return a;
 }
 
+// SecondaryStats scope: forward conv statistics go to the second slab workspace
+thread_local bool t_secondary = false;
+inline Slot fwd_stats_slot() { return t_secondary ? FWD_STATS2 : FWD_STATS; }
+
 ConvRouteGeom route_geom(const ConvShape& s, int g1s_mode) {
   return ConvRouteGeom{s.N, s.C, s.H, s.W, s.Co, s.KH, s.KW, s.SH, s.SW, s.PH, s.PW, s.OH, s.OW, g1s_mode};
 }
@@ -470,7 +474,7 @@ const float* conv_fwd(const void* x, const void* w, const float* bias, void* y, 
   if (want) *stat_rows = 0;
   auto slab_of = [&](int rows) {
     *stat_rows = rows;
-    return static_cast<float*>(scratch(FWD_STATS, (size_t)rows * 3 * s.Co * 4));
+    return static_cast<float*>(scratch(fwd_stats_slot(), (size_t)rows * 3 * s.Co * 4));
   };
   const int M = s.N * s.OH * s.OW;
   // the shared routing table (conv_route.cpp): the same kernels as the Python front end
@@ -611,8 +615,16 @@ const float* conv_dgrad(const void* dy, const void* w, void* dx, const ConvShape
           a.cls_t0[k] = cls[k].t0; a.cls_nt[k] = cls[k].nt; a.cls_ory[k] = cls[k].ry; a.cls_orx[k] = cls[k].rx;
         }
       }
+      // the producing BatchNorm's mask + backward statistics in the epilogue when every stride
+      // phase has taps (a zero-tap phase's rows are written by the fill path, not the MMA epilogue)
+      bool all_taps = true;
+      for (const Cls& c : cls) all_taps = all_taps && c.nt > 0;
+      if (bnb && all_taps) {
+        a.bnb = ba;
+        a.stats = slab_of(gemm_g2_stat_rows(a.M, s.C));
+      }
       gemm_g2(a, cur());
-      return nullptr;
+      return a.stats;
     }
   }
   NtArgs a{static_cast<const bf16*>(dy), wt, dx, s.N * s.H * s.W, s.C, K, 0, K, s.C, kConvDgrad, s.N, s.OH, s.OW,
@@ -682,7 +694,7 @@ const float* stem_fwd(const float* x, const void* w, const float* bias, void* y,
   a.N = s.N; a.Ci = s.C; a.H = s.H; a.W = s.W; a.Co = s.Co;
   if (stat_rows) {
     *stat_rows = stem_tiles_host(s.N, s.H, s.W);
-    a.slab = static_cast<float*>(scratch(FWD_STATS, (size_t)*stat_rows * 3 * s.Co * 4));
+    a.slab = static_cast<float*>(scratch(fwd_stats_slot(), (size_t)*stat_rows * 3 * s.Co * 4));
   }
   dcnn::stem_fwd(a, cur());
   return a.slab;
@@ -773,6 +785,87 @@ void bn_bwd(const void* dy, const void* x, void* dx, long R, int C, const float*
   bn_partial(kBF16, x, dy, yout, dy_out, mean, istd, R, C, slab, 1, nullptr, cur());
   const auto st = reduce_stats(1, slab, rows, C);
   bn_bwd_apply(kBF16, dy, yout, x, dx, R, C, mean, istd, g, st.first, st.second, (float)R, dg, db, train ? 0 : 1, cur());
+}
+
+SecondaryStats::SecondaryStats() { t_secondary = true; }
+SecondaryStats::~SecondaryStats() { t_secondary = false; }
+
+BnRaw bn_stats_raw(const void* x, long R, int C, const float* slab, int rows) {
+  if (slab != nullptr && rows > 0) return BnRaw{slab, rows};
+  const int n = bn_partial_rows(R, C);
+  float* s = static_cast<float*>(scratch(STAT_SLAB2, (size_t)n * 3 * C * 4));
+  bn_partial(kBF16, x, nullptr, nullptr, nullptr, nullptr, nullptr, R, C, s, 0, nullptr, cur());
+  return BnRaw{s, n};
+}
+
+bool bn_dual_ok(long R, int C) { return bn_apply_dual_supported(R, C); }
+
+// both statistics reduces of a pair in one launch: (pointer, parts) per side
+static void reduce_pair(int mode, const float* slab_a, int rows_a, const float* slab_b, int rows_b, int C,
+                        std::pair<const float*, int>& a, std::pair<const float*, int>& b) {
+  const int pa = bn_stat_parts(rows_a), pb = bn_stat_parts(rows_b);
+  float* sa = static_cast<float*>(scratch(STAT_SUMS, (size_t)2 * C * 4));
+  float* sb = static_cast<float*>(scratch(STAT_SUMS2, (size_t)2 * C * 4));
+  float* qa = pa > 1 ? static_cast<float*>(scratch(STAT_PART, (size_t)pa * 3 * C * 4)) : nullptr;
+  float* qb = pb > 1 ? static_cast<float*>(scratch(STAT_PART2, (size_t)pb * 3 * C * 4)) : nullptr;
+  bn_stat_reduce2(mode, slab_a, rows_a, sa, qa, slab_b, rows_b, sb, qb, C, cur());
+  a = {pa > 1 ? qa : sa, pa};
+  b = {pb > 1 ? qb : sb, pb};
+}
+
+void bn_fwd_dual(const BnFwdSide& a, const BnFwdSide& b, void* y, long R, int C, bool relu, bool train) {
+  std::pair<const float*, int> sa{nullptr, 1}, sb{nullptr, 1};
+  if (train) reduce_pair(0, a.raw.slab, a.raw.rows, b.raw.slab, b.raw.rows, C, sa, sb);
+  auto side = [&](const BnFwdSide& s, const std::pair<const float*, int>& st) {
+    return BnSide{s.x,     st.first, st.second, (float)R, s.g,        s.b,    s.eps,
+                  s.smean, s.sistd,  s.rmean,   s.rvar,   s.momentum, train ? 0 : 1};
+  };
+  if (!bn_apply_dual(side(a, sa), side(b, sb), y, R, C, relu ? 1 : 0, cur()))
+    throw std::runtime_error("bn_fwd_dual: unsupported shape");
+}
+
+void bn_bwd_dual(const void* dy, const BnBwdSides& a, const float* slab_a, int rows_a, const BnBwdSides& b, long R,
+                 int C) {
+  const int rows_b = bn_partial_rows(R, C);
+  float* slab_b = static_cast<float*>(scratch(STAT_SLAB, (size_t)rows_b * 2 * C * 4));
+  bn_partial(kBF16, b.x, dy, nullptr, nullptr, b.mean, b.istd, R, C, slab_b, 1, nullptr, cur());
+  std::pair<const float*, int> sa, sb;
+  reduce_pair(1, slab_a, rows_a, slab_b, rows_b, C, sa, sb);
+  auto side = [&](const BnBwdSides& s, const std::pair<const float*, int>& st) {
+    return BnBwdSide{s.x, s.dx, s.mean, s.istd, s.g, st.first, st.second, (float)R, s.dg, s.db};
+  };
+  if (!bn_bwd_apply_dual(dy, side(a, sa), side(b, sb), R, C, cur()))
+    throw std::runtime_error("bn_bwd_dual: unsupported shape");
+}
+
+bool bn_relu_maxpool_ok(const PoolShape& p) {
+  const PoolGeom g = geom(p);
+  return dcnn::bn_relu_maxpool_supported(g) && dcnn::maxpool_bwd_bnb_supported(g);
+}
+
+void bn_relu_maxpool(const void* x, void* y, uint8_t* idx, const PoolShape& p, const float* slab, int rows,
+                     const float* g, const float* b, float eps, float* rmean, float* rvar, float momentum,
+                     float* smean, float* sistd) {
+  const long R = (long)p.N * p.H * p.W;
+  if (slab == nullptr || rows <= 0) {
+    rows = bn_partial_rows(R, p.C);
+    float* s = static_cast<float*>(scratch(STAT_SLAB, (size_t)rows * 3 * p.C * 4));
+    bn_partial(kBF16, x, nullptr, nullptr, nullptr, nullptr, nullptr, R, p.C, s, 0, nullptr, cur());
+    slab = s;
+  }
+  const auto st = reduce_stats(0, slab, rows, p.C);
+  dcnn::bn_relu_maxpool(static_cast<const bf16*>(x), static_cast<bf16*>(y), idx, geom(p), st.first, st.second,
+                        (float)R, g, b, eps, smean, sistd, rmean, rvar, momentum, cur());
+}
+
+const float* maxpool_bwd_bnb(const void* dy, const uint8_t* idx, const void* ypool, const void* x, const float* mean,
+                             const float* istd, void* dx, const PoolShape& p, int* rows) {
+  const PoolGeom g = geom(p);
+  *rows = maxpool_bwd_bnb_rows(g);
+  float* slab = static_cast<float*>(scratch(BWD_STATS, (size_t)*rows * 2 * p.C * 4));
+  dcnn::maxpool_bwd_bnb(static_cast<const bf16*>(dy), idx, static_cast<const bf16*>(ypool),
+                        static_cast<const bf16*>(x), mean, istd, static_cast<bf16*>(dx), g, slab, nullptr, cur());
+  return slab;
 }
 
 void maxpool_fwd(const void* x, void* y, uint8_t* idx, const PoolShape& p) {
