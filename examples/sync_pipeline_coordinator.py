@@ -3,7 +3,7 @@
 examples/sync_pipeline_coordinator.cpp): MNIST CNN split across WORKER1/WORKER2, per-phase
 timings printed per batch.  Start the workers first:
 
-    python examples/network_worker.py 8001 &  python examples/network_worker.py 8002 &
+    python -m dcnn_amd.parallel.pipeline.worker 8001 &  python -m dcnn_amd.parallel.pipeline.worker 8002 &
     python examples/sync_pipeline_coordinator.py
 
 ``--local`` runs both stages in-process instead (no workers needed).
