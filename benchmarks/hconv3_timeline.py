@@ -41,7 +41,7 @@ def main():
             items = K.hconv_tiles(N, H, W, Co, C, 9) * K.hconv_splits(N, H, W, Co, C, 9)
         # per item u and wave: [0] item start, [1] first chunk done, [2] K loop done, [3] epilogue
         # computed + stored, [4] item end (statistics merged); [5] workgroup start (first item)
-        buf = torch.zeros(items * 4 * 8, dtype=torch.int64, device="cuda")
+        buf = torch.zeros(items * 4 * 16, dtype=torch.int64, device="cuda")
         for _ in range(3):
             fn()
         torch.cuda.synchronize()
@@ -49,7 +49,7 @@ def main():
         fn()
         torch.cuda.synchronize()
         K.hconv3_set_stamps(0)
-        t = buf.view(items, 4, 8).double().cpu()
+        t = buf.view(items, 4, 16).double().cpu()
         # s_memtime is a per-XCD counter: only differences of stamps taken by the SAME wave are
         # meaningful (cross-workgroup spans mix clocks). Split-K items that are not their tile's
         # last arriver skip the epilogue stamps (3, 4): those phases use only the items that ran it.
@@ -60,6 +60,11 @@ def main():
             per_item[name] = (t[:, :, b_] - t[:, :, a_])[m]
         first = t[:, :, 5] > 0
         G = int(first[:, 0].sum())  # workgroups (each stamps 5 once, at its first item)
+        # prologue split: [5] -> [6] address setup, [6] -> [7] first DMA issue + landing (vmcnt),
+        # [7] -> [0] first barrier (the workgroup's other waves)
+        pro = {nm_: (t[:, :, b_] - t[:, :, a_])[first & ok(a_, b_)] for nm_, a_, b_ in
+               (("args", 5, 8), ("halo_tab", 8, 9), ("w_tab", 9, 10), ("frag", 10, 11), ("addrs", 11, 6),
+                ("dma", 6, 7), ("barrier", 7, 0))}
         lives, kl, prol = [], [], []
         for u0 in torch.nonzero(first[:, 0]).flatten().tolist():
             us = list(range(u0, items, G))
@@ -77,7 +82,8 @@ def main():
               f"of item time (items with an epilogue) {100 * kloop_sum / max(kloop_sum + epi_sum, 1):.1f}%")
         print("   medians per item: " + "  ".join(f"{k} {float(v.median()):.0f}" if v.numel() else f"{k} -"
                                                for k, v in per_item.items())
-              + f"  prologue {float(prol.median()):.0f}")
+              + f"  prologue {float(prol.median()):.0f} (" + "  ".join(
+                  f"{k} {float(v.median()):.0f}" for k, v in pro.items() if v.numel()) + ")")
 
 if __name__ == "__main__":
     main()

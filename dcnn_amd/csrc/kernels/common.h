@@ -155,6 +155,21 @@ struct Philox {
   }
 };
 
+// Division by a run-time invariant divisor d >= 1 (Granlund-Montgomery): q = (umulhi(n, mul) + n)
+// >> shr, exact for n < 2^31. The launcher builds it once; in the kernel it is a multiply-high, an
+// add and a shift (scalar or vector) instead of the ~40-instruction reciprocal sequence of a
+// plain run-time division.
+struct FastDiv {
+  unsigned mul, shr, d;
+};
+inline FastDiv make_fastdiv(unsigned d) {
+  unsigned l = 0;
+  while ((1ull << l) < d) ++l;
+  const unsigned long long m = ((1ull << 32) * ((1ull << l) - d)) / d + 1;
+  return FastDiv{(unsigned)m, l, d};
+}
+__device__ __forceinline__ unsigned fdiv(unsigned n, const FastDiv& f) { return (__umulhi(n, f.mul) + n) >> f.shr; }
+
 inline int ceil_div(long a, long b) { return (int)((a + b - 1) / b); }
 inline int grid_for(long n, int block, int cap = 2048 * 4) {
   long g = (n + block - 1) / block;

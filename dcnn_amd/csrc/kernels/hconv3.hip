@@ -145,8 +145,11 @@ struct H3Geo {
   int nchunk;              // 32-channel chunks per split
   int nitems;              // tiles_m * tiles_n * splits
   int tb[9];               // weight column offset (elements) of tap (dy + 1) * 3 + (dx + 1)
+  // the run-time divisors of the halo table and the item decode as multiply-shift reciprocals
+  // (a plain run-time division is a ~40-instruction sequence; the prologue did ~30 per lane)
+  FastDiv fd_pitch, fd_ih1, fd_iw1, fd_spl, fd_tn, fd_tpi, fd_txt;
   unsigned c_bytes;        // output bytes (32-bit store offsets)
-  unsigned long long* stamps;  // diagnostic timeline [nitems][NW][8] (STAMP instance only)
+  unsigned long long* stamps;  // diagnostic timeline [nitems][NW][16] (STAMP instance only)
 };
 
 // NW waves per workgroup, WC of them along the output channels (64 each), NW / WC along the
@@ -184,7 +187,7 @@ __global__ void __launch_bounds__(NW * 64, 8 / NW) hconv3_kernel(HConvArgs p, H3
   const int lr = lane & 15, lh = lane >> 4;
   auto stamp = [&](int u, int k) H3L {
     if constexpr (STAMP) {
-      if (lane == 0) g.stamps[((size_t)u * NW + wid) * 8 + k] = __builtin_amdgcn_s_memtime();
+      if (lane == 0) g.stamps[((size_t)u * NW + wid) * 16 + k] = __builtin_amdgcn_s_memtime();
     }
   };
   const int SPL = p.splits;
@@ -202,6 +205,7 @@ __global__ void __launch_bounds__(NW * 64, 8 / NW) hconv3_kernel(HConvArgs p, H3
   const int HW2 = g.TW + g.GX + 1;                       // halo columns
   const int HPX = (g.TH + g.GY + 1) * pitch;             // halo pixels per tile (pitch-padded)
   const int nch = g.nchunk;                              // chunks per item (even, or 1: a 32-channel input)
+  stamp(u, 8);
 
   // ---- halo loader, item-invariant part: instruction k of this wave fills halo pixels
   // [16(wid*HN + k), +16); lane -> (image, row + 1, column + 1 within the image window, chunk
@@ -212,11 +216,11 @@ __global__ void __launch_bounds__(NW * 64, 8 / NW) hconv3_kernel(HConvArgs p, H3
     const int P = (wid * HN + k) * 16 + (lane >> 2);
     unsigned v = 0xffffffffu;
     if (P < HPX) {
-      const int hy = P / pitch, hx = P - hy * pitch;
+      const int hy = (int)fdiv((unsigned)P, g.fd_pitch), hx = P - hy * pitch;
       int cy = hy, cx = hx, im = 0;
       bool ok = hx < HW2;
       if (gut) {
-        const int iy = hy / (g.IH + 1), ix = hx / (g.IW + 1);
+        const int iy = (int)fdiv((unsigned)hy, g.fd_ih1), ix = (int)fdiv((unsigned)hx, g.fd_iw1);
         cy = hy - iy * (g.IH + 1);
         cx = hx - ix * (g.IW + 1);
         im = iy * g.GX + ix;
@@ -226,6 +230,7 @@ __global__ void __launch_bounds__(NW * 64, 8 / NW) hconv3_kernel(HConvArgs p, H3
     }
     hpk[k] = v;
   }
+  stamp(u, 9);
   // ---- weight loader, item-invariant part: stage row R = dx * BN + n (3 taps x BN rows, 64 B)
   unsigned wrc[NWI];  // (stage row's output channel + 1) | chunk slot byte offset << 16
   int wtb[NWI][3];  // byte offset of the instruction's tap column for kernel rows dy = 0..2 (SGPRs)
@@ -234,10 +239,14 @@ __global__ void __launch_bounds__(NW * 64, 8 / NW) hconv3_kernel(HConvArgs p, H3
     const int R0 = (wid * NWI + k) * 16;  // first stage row of the instruction (wave-uniform)
     const int R = R0 + (lane >> 2);
     const int dx = R0 / BN, n = R - dx * BN;
+    // (a select over the three taps of the row, not a run-time index into the kernel arguments)
 #pragma unroll
-    for (int dy = 0; dy < 3; ++dy) wtb[k][dy] = __builtin_amdgcn_readfirstlane(dx < 3 ? g.tb[dy * 3 + dx] * 2 : 0);
+    for (int dy = 0; dy < 3; ++dy)
+      wtb[k][dy] = __builtin_amdgcn_readfirstlane(
+          dx == 0 ? g.tb[dy * 3] * 2 : dx == 1 ? g.tb[dy * 3 + 1] * 2 : dx == 2 ? g.tb[dy * 3 + 2] * 2 : 0);
     wrc[k] = (unsigned)(dx < 3 ? h3_rowch(n) + 1 : 0) | ((unsigned)(((lane & 3) ^ h3_wswz(n)) * 16) << 16);
   }
+  stamp(u, 10);
 
   // ---- per-item geometry and source addresses
   struct Item {
@@ -245,13 +254,14 @@ __global__ void __launch_bounds__(NW * 64, 8 / NW) hconv3_kernel(HConvArgs p, H3
   };
   auto decode = [&](int v) H3L {
     Item t;
-    t.zs = v % SPL;
-    t.lt = v / SPL;
-    t.tm = t.lt / g.tiles_n;
+    t.lt = (int)fdiv((unsigned)v, g.fd_spl);
+    t.zs = v - t.lt * SPL;
+    t.tm = (int)fdiv((unsigned)t.lt, g.fd_tn);
     t.n0 = (t.lt - t.tm * g.tiles_n) * BN;
-    const int ig = t.tm / tpi, trem = t.tm - ig * tpi;
-    t.y0 = (trem / tx_tiles) * 16;
-    t.x0 = (trem % tx_tiles) * 16;
+    const int ig = (int)fdiv((unsigned)t.tm, g.fd_tpi), trem = t.tm - ig * tpi;
+    const int ty = (int)fdiv((unsigned)trem, g.fd_txt);
+    t.y0 = ty * 16;
+    t.x0 = (trem - ty * tx_tiles) * 16;
     t.img0 = ig * (g.GY * g.GX);
     t.cbase = t.zs * nch * 32;  // first input channel of this split
     return t;
@@ -327,6 +337,7 @@ __global__ void __launch_bounds__(NW * 64, 8 / NW) hconv3_kernel(HConvArgs p, H3
     }
   };
   set_baddr(0);
+  stamp(u, 11);
   auto baddr_of = [&](int j, int dy, int dx) H3L {
     if constexpr (PITCH > 0) return baddr[j][dx] + dy * PITCH * 64;
     else return baddr[j][dy * 3 + dx];
@@ -384,10 +395,12 @@ __global__ void __launch_bounds__(NW * 64, 8 / NW) hconv3_kernel(HConvArgs p, H3
   // ---- first item's prologue: halo chunk 0, W(0, 0) landed; W(0, 1) in flight
   unsigned hs[HN], ws[NWI];
   addrs(decode(u), hs, ws);
+  stamp(u, 6);
   load_halo(I0{}, 0, hs);
   load_w(I0{}, 0, 0, ws);
   load_w(I1{}, 0, 1, ws);
   vmwait<NWI>();
+  stamp(u, 7);
   h3_barrier();
   int nst = 0;  // output stores issued after the item's W(0, 1) (the previous item's epilogue)
 
@@ -763,6 +776,9 @@ bool hconv3_try(const HConvArgs& a0, hipStream_t s) {
   g.lGX = __builtin_ctz(pl.GX); g.lIH = __builtin_ctz(pl.IH); g.lIW = __builtin_ctz(pl.IW);
   g.tx_tiles = pl.tx_tiles; g.tpi = pl.tpi;
   g.tiles_n = pl.tiles_n; g.tiles_m = pl.tiles_m;
+  g.fd_pitch = make_fastdiv(pl.pitch); g.fd_ih1 = make_fastdiv(pl.IH + 1); g.fd_iw1 = make_fastdiv(pl.IW + 1);
+  g.fd_spl = make_fastdiv(pl.splits); g.fd_tn = make_fastdiv(pl.tiles_n); g.fd_tpi = make_fastdiv(pl.tpi);
+  g.fd_txt = make_fastdiv(pl.tx_tiles);
   g.nchunk = a.Cs / 32 / pl.splits;
   g.nitems = pl.tiles_m * pl.tiles_n * pl.splits;
   g.c_bytes = (unsigned)c_bytes;
