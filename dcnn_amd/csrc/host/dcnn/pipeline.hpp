@@ -17,6 +17,7 @@
 #pragma once
 #include <atomic>
 #include <chrono>
+#include <functional>
 #include <map>
 #include <memory>
 #include <optional>
@@ -114,6 +115,28 @@ class PipelineStage {
     std::vector<int64_t> shape;
   };
   std::map<uint64_t, OutKind> out_kind_;
+  // GPU stages: one hipGraph per (phase, micro-batch), captured from the second step on (the
+  // first step runs eagerly, so every workspace already has its final size) and replayed after
+  // that: a micro-batch's forward / backward on this stage is one graph launch instead of hundreds
+  // of eager kernel launches. A micro-batch's backward graph reads the activations its forward
+  // graph leaves in that graph's buffers, so both phases of a micro-batch run captured or both
+  // eagerly; an eager forward (first step, DCNN_STAGE_GRAPHS=0, or a new input shape / train-eval
+  // mode) drops that micro-batch's graphs, and the next step captures them again.
+  struct MbGraph {
+    std::unique_ptr<gpu::Graph> g;
+    Tensor in, out;  // the graph's static input buffer and output
+    std::vector<int64_t> shape;
+    DType dt = DType::F32;
+    Layout layout = Layout::NCHW;
+    bool training = true;
+  };
+  std::map<uint64_t, MbGraph> fwd_graph_, bwd_graph_;
+  std::map<uint64_t, bool> fwd_graphed_;  // the micro-batch's last forward ran its graph
+  bool graphs_ = false;
+  Tensor run_graph(std::map<uint64_t, MbGraph>& tab, uint64_t mb, const Tensor& in, bool training,
+                   const std::function<Tensor(const Tensor&)>& body);
+  void drop_graphs(uint64_t mb);
+  void drop_all_graphs();
   // transport "ipc" (same node, GPU stages): stage-to-stage tensors stay on the device. The sender
   // copies into its exported buffer for (peer, micro-batch) and sends only the 64-byte handle; the
   // receiver maps the buffer once and copies out on arrival. A (peer, micro-batch) buffer is

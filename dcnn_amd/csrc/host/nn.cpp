@@ -373,6 +373,7 @@ Tensor BatchNorm::forward_impl(const Tensor& x, bool training, const Tensor* res
   const void* res = residual ? residual->data() : nullptr;
   const bool slab = dev_.is_gpu() && training && pending_x_ == x.data() && pending_slab_ && pending_rows_ > 0;
   if (fused_pool_ != nullptr) {
+    fused_pool_->set_micro_batch(mb_);  // (its own forward sets it only after this one)
     const PoolShape p = fused_pool_->shape_for(x.shape());
     if (dev_.is_gpu() && training && relu && residual == nullptr && gpu_ops::bn_relu_maxpool_ok(p)) {
       // BatchNorm + ReLU + max-pool in one pass: the full-resolution output is never stored, the

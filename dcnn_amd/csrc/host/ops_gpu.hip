@@ -105,9 +105,11 @@ void* alloc(size_t nbytes) {
     it->second.pop_back();
     bp.cached -= cls;
   } else {
-    if (hipMalloc(&p, cls) != hipSuccess) {
+    const hipError_t e = hipMalloc(&p, cls);
+    if (e != hipSuccess) {
       (void)hipGetLastError();
-      if (cp) throw std::runtime_error("gpu::alloc: out of memory while capturing a graph");
+      if (cp) throw std::runtime_error(std::string("gpu::alloc: hipMalloc failed while capturing a graph: ") +
+                                       hipGetErrorString(e));
       release_cached(bp);
       HOST_HIP_CHECK(hipMalloc(&p, cls));
     }
@@ -207,7 +209,9 @@ void Graph::begin() {
   pool_ = cp;
   // a previous eager step's work must not be captured into (or race with) the graph
   HOST_HIP_CHECK(hipStreamSynchronize(static_cast<hipStream_t>(flow_)));
-  HOST_HIP_CHECK(hipStreamBeginCapture(static_cast<hipStream_t>(flow_), hipStreamCaptureModeThreadLocal));
+  // relaxed: a block the capture needs beyond the cached ones comes from hipMalloc, which the
+  // stricter modes refuse while a capture is open (the allocation is not stream work)
+  HOST_HIP_CHECK(hipStreamBeginCapture(static_cast<hipStream_t>(flow_), hipStreamCaptureModeRelaxed));
   t_capture = cp;
 }
 void Graph::end() {

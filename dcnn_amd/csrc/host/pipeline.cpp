@@ -4,6 +4,7 @@
 #include <unistd.h>
 
 #include <cmath>
+#include <cstdlib>
 #include <cstdio>
 #include <cstring>
 #include <fstream>
@@ -290,7 +291,10 @@ void PipelineStage::configure(const std::string& text) {
   dev_ = Device::parse(cfg_.device);
   if (cfg_.transport == "ipc" && !dev_.is_gpu()) throw std::runtime_error("native stage: transport 'ipc' needs a GPU stage");
   release_ipc();  // (a redeploy may change the neighbours)
+  drop_all_graphs();  // (they hold the previous model's buffers)
   if (dev_.is_gpu()) gpu::set_device(dev_.index);
+  const char* ge = std::getenv("DCNN_STAGE_GRAPHS");
+  graphs_ = dev_.is_gpu() && !(ge != nullptr && std::string(ge) == "0");
   model_ = std::make_unique<Sequential>(Sequential::load_from_config(cfg_.model_config));
   model_->set_device(dev_);
   model_->initialize((uint64_t)cfg_.seed.value_or(0));
@@ -443,7 +447,16 @@ void PipelineStage::forward(Message& m) {
   } else {
     a = convert(x, DType::F32, Layout::NCHW, dev_);
   }
-  const Tensor out = model_->forward_activation(a, (int)mb);
+  Tensor out;
+  if (graphs_ && n_upd_ >= 1) {
+    out = run_graph(fwd_graph_, mb, a, model_->is_training(),
+                    [&](const Tensor& in) { return model_->forward_activation(in, (int)mb); });
+    fwd_graphed_[mb] = true;
+  } else {
+    drop_graphs(mb);
+    out = model_->forward_activation(a, (int)mb);
+    fwd_graphed_[mb] = false;
+  }
   out_kind_[mb] = OutKind{out.dtype(), out.layout(), out.shape()};
   const bool last = cfg_.stage_index == cfg_.num_stages - 1;
   send_tensor(last ? "coordinator" : "next_stage", FORWARD_JOB, mb, out, last);
@@ -464,12 +477,60 @@ void PipelineStage::backward(Message& m) {
     g = g.view(k.shape, k.layout);
   }
   g = convert(g, k.dt, k.layout, dev_);
-  Tensor gin = model_->backward_activation(g, (int)mb);
+  Tensor gin;
+  auto fg = fwd_graphed_.find(mb);
+  if (graphs_ && fg != fwd_graphed_.end() && fg->second)
+    gin = run_graph(bwd_graph_, mb, g, true, [&](const Tensor& in) { return model_->backward_activation(in, (int)mb); });
+  else
+    gin = model_->backward_activation(g, (int)mb);
   const bool first = cfg_.stage_index == 0;
   if (first && !cfg_.first_layer_input_grad) gin = Tensor();
   send_tensor(first ? "coordinator" : "prev_stage", BACKWARD_JOB, mb, gin, false);
   ++n_bwd_;
   bwd_ms_ += std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+}
+
+Tensor PipelineStage::run_graph(std::map<uint64_t, MbGraph>& tab, uint64_t mb, const Tensor& in, bool training,
+                                const std::function<Tensor(const Tensor&)>& body) {
+  MbGraph& G = tab[mb];
+  if (G.g && (G.shape != in.shape() || G.dt != in.dtype() || G.layout != in.layout() || G.training != training)) {
+    drop_graphs(mb);  // (both phases: the backward graph reads the forward graph's buffers)
+    return run_graph(tab, mb, in, training, body);
+  }
+  if (!G.g) {
+    G.in = Tensor::empty(in.shape(), in.dtype(), dev_, in.layout());
+    copy_into(G.in, in);
+    G.g = std::make_unique<gpu::Graph>();
+    G.g->begin();
+    try {
+      G.out = body(G.in);
+    } catch (...) {
+      G.g.reset();  // (ends the capture)
+      tab.erase(mb);
+      throw;
+    }
+    G.g->end();
+    G.shape = in.shape();
+    G.dt = in.dtype();
+    G.layout = in.layout();
+    G.training = training;
+  } else {
+    copy_into(G.in, in);
+  }
+  G.g->replay();
+  return G.out;
+}
+
+void PipelineStage::drop_graphs(uint64_t mb) {
+  fwd_graph_.erase(mb);
+  bwd_graph_.erase(mb);
+  fwd_graphed_.erase(mb);
+}
+
+void PipelineStage::drop_all_graphs() {
+  fwd_graph_.clear();
+  bwd_graph_.clear();
+  fwd_graphed_.clear();
 }
 
 namespace {

@@ -217,6 +217,26 @@ def test_native_coordinator_ipc_transport_matches_messages(worker_bin):
     np.testing.assert_allclose(losses["ipc"], losses["message"], rtol=1e-6)
 
 
+@pytest.mark.gpu
+def test_native_stage_graphs_match_eager(worker_bin):
+    """GPU stages capture one hipGraph per (phase, micro-batch) from the second step on and replay
+    it after; the replays run the same kernels on the same data as the eager path, so every step's
+    loss is the same with the graphs off (DCNN_STAGE_GRAPHS=0)."""
+    import json
+    import os
+    losses = {}
+    for graphs in ("0", "1"):
+        env = dict(os.environ, DCNN_STAGE_GRAPHS=graphs)
+        out = subprocess.run([COORD, "--spawn", "3", "--model", "resnet9_cifar10", "--device", "GPU:0", "--input",
+                              "3,32,32", "--classes", "10", "--batch", "64", "--microbatches", "4", "--steps", "6",
+                              "--schedule", "1f1b", "--transport", "ipc", "--json"],
+                             capture_output=True, text=True, timeout=240, env=env)
+        assert out.returncode == 0, out.stderr[-2000:]
+        losses[graphs] = [json.loads(l)["loss"] for l in out.stdout.splitlines() if l.startswith("{")]
+    assert len(losses["1"]) == 6 and all(np.isfinite(losses["1"]))
+    np.testing.assert_allclose(losses["1"], losses["0"], rtol=1e-6)
+
+
 def test_native_ipc_transport_needs_gpu_stages(worker_bin):
     out = subprocess.run([COORD, "--spawn", "2", "--steps", "1", "--transport", "ipc"], capture_output=True, text=True,
                          timeout=60)

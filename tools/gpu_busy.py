@@ -4,20 +4,27 @@ N optimizer steps, the wall span, the union of kernel-busy intervals (any kernel
 stream), the idle time and its largest gaps, and how many kernels ran concurrently. Used to tell
 a host/scheduling-bound run (idle gaps between kernels) from a device-bound one.
 
-  python tools/gpu_busy.py gpurun_out/prof_x/run_results.db [--steps 5] [--opt-per-step S]
+  python tools/gpu_busy.py gpurun_out/prof_x/run_results.db [more.db ...] [--steps 5] [--opt-per-step S]
 
-(--opt-per-step: optimizer dispatches per training step, e.g. the stage count of a pipeline.)
+(--opt-per-step: optimizer dispatches per training step, e.g. the stage count of a pipeline.
+Several databases — one per process of a multi-process run on the same GPU, e.g. native pipeline
+stage workers — are merged into one timeline: the device timestamps share one clock.)
 """
 import sqlite3
 import sys
 
 
 def main():
-    path = sys.argv[1]
+    args, paths = sys.argv[1:], []
+    while args and not args[0].startswith("--"):
+        paths.append(args.pop(0))
     nsteps = int(sys.argv[sys.argv.index("--steps") + 1]) if "--steps" in sys.argv else 5
     per = int(sys.argv[sys.argv.index("--opt-per-step") + 1]) if "--opt-per-step" in sys.argv else 1
-    c = sqlite3.connect(path)
-    ks = sorted((int(s), int(e), n) for s, e, n in c.execute("select start, end, name from kernels"))
+    ks = []
+    for path in paths:
+        c = sqlite3.connect(path)
+        ks += [(int(s), int(e), n) for s, e, n in c.execute("select start, end, name from kernels")]
+    ks.sort()
     opt = [i for i, k in enumerate(ks) if "adam_kernel" in k[2] or "sgd_kernel" in k[2]][per - 1::per]
     if len(opt) < nsteps + 1:
         nsteps = max(1, len(opt) - 1)
