@@ -220,6 +220,37 @@ void PipelineCoordinator::deploy_stages() {
   const auto now = Clock::now();
   for (const auto& s : names_) last_beat_[s] = now;
   sent_lr_ = lr_.learning_rate();
+  enable_stage_loss();
+}
+
+void PipelineCoordinator::send_f64(const std::string& to, uint16_t cmd, uint64_t mb, const std::vector<double>& v) {
+  Message m;
+  m.recipient = to;
+  m.command = cmd;
+  m.payload_type = P_TYPED_JOB;
+  m.mb_id = mb;
+  m.dtype = 5;  // f64
+  m.shape = {(uint64_t)v.size()};
+  m.data.assign(reinterpret_cast<const char*>(v.data()), v.size() * sizeof(double));
+  comm_->send(std::move(m));
+}
+
+void PipelineCoordinator::enable_stage_loss() {
+  stage_loss_on_ = false;
+  if (o_.stage_loss == 0 || names_.empty()) return;
+  bool native = false, gpu = false;
+  for (const json::Value& st : status())
+    if (st.get_string("id", "") == names_.back()) {
+      native = st.get_bool("native", false);
+      gpu = st.get_string("device", "").rfind("GPU", 0) == 0;
+    }
+  if (o_.stage_loss == 1 && !native) throw PipelineError("stage loss: the last stage is not a native stage");
+  if (!native || (o_.stage_loss < 0 && !gpu)) return;
+  const int M = o_.num_microbatches;
+  const double scale = o_.grad_scale_mean && M > 1 ? 1.0 / M : 1.0;
+  send_f64(names_.back(), LABELS_TRANSFER, kLossConfigMb, {(double)loss_.kind(), (double)loss_.param(), scale});
+  join(LABELS_TRANSFER, 1);
+  stage_loss_on_ = true;
 }
 
 void PipelineCoordinator::broadcast(uint16_t cmd, const std::string& text) {
@@ -357,7 +388,30 @@ std::vector<PipelineCoordinator::Pending> PipelineCoordinator::split(const Tenso
   return out;
 }
 
-void PipelineCoordinator::forward_mb(const Pending& p) { send_job(names_.front(), FORWARD_JOB, p.mb, p.x.data(), p.shape); }
+void PipelineCoordinator::forward_mb(const Pending& p) {
+  // (the labels first: the last stage needs them when the micro-batch's activations arrive)
+  if (stage_loss_on_) send_f64(names_.back(), LABELS_TRANSFER, p.mb, std::vector<double>(p.y.begin(), p.y.end()));
+  send_job(names_.front(), FORWARD_JOB, p.mb, p.x.data(), p.shape);
+}
+
+// (a P_STRING payload carries no micro-batch id field: the last stage's loss report names it)
+static Message& with_mb(Message& m) {
+  if (m.payload_type == P_STRING) m.mb_id = (uint64_t)json::Value::parse(m.text).get_int("mb", 0);
+  return m;
+}
+
+// a micro-batch's output: the last stage's loss report (its backward already started there), or
+// its logits (the loss here, the gradient back to the last stage)
+void PipelineCoordinator::take_output(Message& out, Pending& p, StepResult& r) {
+  if (out.payload_type == P_STRING) {
+    const json::Value v = json::Value::parse(out.text);
+    r.loss += v.get_number("loss", 0.0);
+    r.correct += (long)v.get_int("correct", 0);
+    r.samples += v.get_int("samples", 0);
+    return;
+  }
+  loss_and_backward(out, p, r);
+}
 
 void PipelineCoordinator::loss_and_backward(Message& out, Pending& p, StepResult& r) {
   const std::vector<double> v = payload_values(out);
@@ -383,8 +437,8 @@ StepResult PipelineCoordinator::run_sync(std::vector<Pending>& mbs) {
   StepResult r;
   for (auto& p : mbs) forward_mb(p);
   std::map<uint64_t, Message> outs;
-  for (auto& m : join(FORWARD_JOB, mbs.size())) outs[m.mb_id] = std::move(m);
-  for (auto& p : mbs) loss_and_backward(outs.at(p.mb), p, r);
+  for (auto& m : join(FORWARD_JOB, mbs.size())) outs[with_mb(m).mb_id] = std::move(m);
+  for (auto& p : mbs) take_output(outs.at(p.mb), p, r);
   join(BACKWARD_JOB, mbs.size());
   return r;
 }
@@ -400,7 +454,7 @@ StepResult PipelineCoordinator::run_semi_async(std::vector<Pending>& mbs) {
       if (seconds_since(t0) > o_.timeout_s) throw PipelineError("timeout waiting for pipeline outputs");
       continue;
     }
-    loss_and_backward(m, mbs.at(m.mb_id), r);
+    take_output(m, mbs.at(with_mb(m).mb_id), r);
     ++done;
   }
   join(BACKWARD_JOB, mbs.size());
@@ -424,7 +478,7 @@ StepResult PipelineCoordinator::run_1f1b(std::vector<Pending>& mbs) {
       continue;
     }
     if (msg.command == FORWARD_JOB) {
-      loss_and_backward(msg, mbs.at(msg.mb_id), r);
+      take_output(msg, mbs.at(with_mb(msg).mb_id), r);
     } else {
       ++done;
       if (sent < m) forward_mb(mbs[sent++]);
@@ -448,7 +502,11 @@ StepResult PipelineCoordinator::evaluate_batch(const Tensor& x, const Tensor& la
   for (auto& p : mbs) forward_mb(p);
   StepResult r;
   for (auto& m : join(FORWARD_JOB, mbs.size())) {
-    Pending& p = mbs.at(m.mb_id);
+    Pending& p = mbs.at(with_mb(m).mb_id);
+    if (m.payload_type == P_STRING) {  // (the last stage's loss; no backward in eval mode)
+      take_output(m, p, r);
+      continue;
+    }
     const std::vector<double> v = payload_values(m);
     const int64_t N = (int64_t)p.y.size(), C = (int64_t)v.size() / N;
     const Tensor pred = Tensor::from_host(std::vector<float>(v.begin(), v.end()), {N, C}, Device::cpu());

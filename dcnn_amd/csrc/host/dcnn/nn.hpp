@@ -93,6 +93,9 @@ class Layer {
   bool input_grad() const { return input_grad_; }
   // the network input (fp32 NCHW, logical input shape `in`) is consumed as is (GPU RGB stem conv)
   virtual bool takes_raw_input(const std::vector<int64_t>& in) const { (void)in; return false; }
+  // forward + backward FLOPs for a logical input shape (the pipeline's FLOP-balanced partition;
+  // the Python layers' forward_flops + backward_flops)
+  virtual double flops(const std::vector<int64_t>& in) const { (void)in; return 0; }
 
  protected:
   struct MbCache {
@@ -122,6 +125,7 @@ class Conv2D : public Layer {
   Tensor forward(const Tensor& x, bool training) override;
   Tensor backward(const Tensor& dy) override;
   bool takes_raw_input(const std::vector<int64_t>& in) const override;
+  double flops(const std::vector<int64_t>& in) const override;
   // GPU: hand the output's BatchNorm statistics, computed in the conv epilogue, to `bn` (the
   // BatchNorm that consumes this conv's output; fuse_bn_relu wires it)
   void set_stats_consumer(class BatchNorm* bn) { stats_to_ = bn; }
@@ -158,6 +162,7 @@ class Dense : public Layer {
   void build(const std::vector<int64_t>& in, Device dev, uint64_t seed) override;
   Tensor forward(const Tensor& x, bool training) override;
   Tensor backward(const Tensor& dy) override;
+  double flops(const std::vector<int64_t>& in) const override { return 6.0 * in[0] * in_ * out_; }
 
  private:
   int in_, out_;
@@ -171,6 +176,9 @@ class BatchNorm : public Layer {
   std::string type() const override { return "batchnorm"; }
   json::Value parameters_config() const override;
   std::vector<int64_t> output_shape(const std::vector<int64_t>& in) const override { return in; }
+  double flops(const std::vector<int64_t>& in) const override {
+    return 15.0 * (double)in[0] * (double)in[1] * (double)in[2] * (double)in[3];  // 6 forward + 9 backward
+  }
   void build(const std::vector<int64_t>& in, Device dev, uint64_t seed) override;
   Tensor forward(const Tensor& x, bool training) override;
   Tensor backward(const Tensor& dy) override;
@@ -329,6 +337,7 @@ class ResidualBlock : public Layer {
   std::string type() const override { return "residual_block"; }
   json::Value parameters_config() const override;
   std::vector<int64_t> output_shape(const std::vector<int64_t>& in) const override;
+  double flops(const std::vector<int64_t>& in) const override;
   void build(const std::vector<int64_t>& in, Device dev, uint64_t seed) override;
   Tensor forward(const Tensor& x, bool training) override;
   Tensor backward(const Tensor& dy) override;
@@ -387,6 +396,8 @@ class Sequential {
   // the network input (fp32 NCHW, any device) as the first layer's activation
   Tensor input_activation(const Tensor& x) const;
   std::vector<Param*> parameters();
+  // forward + backward FLOPs of every top-level layer for an (N, C, H, W) input
+  std::vector<double> layer_flops(const std::vector<int64_t>& in) const;
   // every BatchNorm, depth-first through residual blocks (the .bnstats record order)
   std::vector<BatchNorm*> batchnorms();
   void zero_grad();

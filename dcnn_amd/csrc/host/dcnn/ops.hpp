@@ -181,7 +181,12 @@ void act_bwd(int kind, const void* x, const void* dy, void* dx, long n, float al
 // pred / grad bf16 [N][C]; returns the mean loss, correct count in *correct
 double softmax_ce(const void* pred, const int64_t* labels, void* grad, int N, int C, long* correct);
 double loss(int kind, const void* pred, const float* target, const int64_t* labels, void* grad, int N, int C,
-            float param, long* correct);
+            float param, long* correct, float grad_scale = 1.f);
+// the same without reading the value back: read_last_loss() after later work on the flow (a
+// pipeline's last stage launches its backward first, then reads the loss once)
+void loss_launch(int kind, const void* pred, const float* target, const int64_t* labels, void* grad, int N, int C,
+                 float param, float grad_scale = 1.f);
+double read_last_loss(long* correct);
 // GroupNorm over bf16 NHWC rows [N][HW][C]
 void groupnorm_fwd(const void* x, void* y, int N, int HW, int C, int G, const float* g, const float* b, float eps,
                    float* smean, float* sistd);

@@ -69,6 +69,8 @@ std::unique_ptr<Optimizer> create_optimizer(const json::Value& cfg);
 // flat state of a run of layers: every parameter in checkpoint order, then every BatchNorm's
 // running mean / variance (depth-first through residual blocks), fp32 values in logical order
 std::vector<double> pack_state(const std::vector<Layer*>& layers);
+// LABELS_TRANSFER micro-batch id of the stage-loss configuration message
+constexpr uint64_t kLossConfigMb = ~0ull;
 void unpack_state(const std::vector<Layer*>& layers, const double* v, size_t n);
 
 class PipelineStage {
@@ -88,6 +90,9 @@ class PipelineStage {
   void connect_peers();
   void forward(dcnn_native::Message& m);
   void backward(dcnn_native::Message& m);
+  void run_backward(uint64_t mb, Tensor g, const std::chrono::steady_clock::time_point& t0);
+  void take_labels(dcnn_native::Message& m);
+  Tensor labels_for(uint64_t mb);
   void reply(uint16_t cmd, const std::string& text = std::string());
   void send_tensor(const std::string& to, uint16_t cmd, uint64_t mb, const Tensor& t, bool as_logits);
   Tensor decode(dcnn_native::Message& m) const;
@@ -130,6 +135,12 @@ class PipelineStage {
     Layout layout = Layout::NCHW;
     bool training = true;
   };
+  // the loss on this (last) stage's device (LABELS_TRANSFER; native coordinator): every forward
+  // output's loss + gradient (scaled by grad_scale_) right here, the backward starts at once and
+  // only the loss value goes to the coordinator — no logits / gradient round trip over the host
+  std::unique_ptr<Loss> stage_loss_;
+  float grad_scale_ = 1.f;
+  std::map<uint64_t, Tensor> labels_;  // device int64 labels per micro-batch (until its forward)
   std::map<uint64_t, MbGraph> fwd_graph_, bwd_graph_;
   std::map<uint64_t, bool> fwd_graphed_;  // the micro-batch's last forward ran its graph
   bool graphs_ = false;
@@ -194,6 +205,9 @@ struct CoordinatorOptions {
   double heartbeat_s = 0.0;                 // > 0: stages beat every heartbeat_s ...
   int heartbeat_misses = 3;                 // ... and are declared failed after this many misses
   std::optional<int64_t> seed;              // stage i initialises with seed + i
+  // the loss on the last stage's device (LABELS_TRANSFER): -1 when the last stage is a native GPU
+  // stage, 0 never (logits to this coordinator, the loss on its CPU), 1 whenever it is native
+  int stage_loss = -1;
   std::string host = "127.0.0.1";           // the address stages reach the coordinator at
   int port = 0;                             // 0: any free port
 };
@@ -205,8 +219,9 @@ struct StepResult {
 };
 
 // Coordinator of separate stage processes (native `network_worker`s or Python workers: the same
-// commands, StageConfig JSON and payloads) over the TCP control plane. The loss runs here on the
-// CPU; activations and gradients travel inline in the job messages.
+// commands, StageConfig JSON and payloads) over the TCP control plane. The loss runs on the last
+// stage's GPU when that stage is native (CoordinatorOptions::stage_loss), else here on the CPU;
+// activations and gradients travel inline in the job messages or as device IPC references.
 class PipelineCoordinator {
  public:
   PipelineCoordinator(json::Value model_config, json::Value optimizer_config, std::vector<Endpoint> stages,
@@ -271,6 +286,9 @@ class PipelineCoordinator {
   void send_job(const std::string& to, uint16_t cmd, uint64_t mb, const float* data, const std::vector<int64_t>& shape);
   void forward_mb(const Pending& p);
   void loss_and_backward(dcnn_native::Message& out, Pending& p, StepResult& r);
+  void take_output(dcnn_native::Message& out, Pending& p, StepResult& r);
+  void enable_stage_loss();
+  void send_f64(const std::string& to, uint16_t cmd, uint64_t mb, const std::vector<double>& v);
   StepResult run_sync(std::vector<Pending>& mbs);
   StepResult run_semi_async(std::vector<Pending>& mbs);
   StepResult run_1f1b(std::vector<Pending>& mbs);
@@ -287,6 +305,7 @@ class PipelineCoordinator {
   LrControl lr_;
   float sent_lr_;
   bool deployed_ = false;
+  bool stage_loss_on_ = false;  // the last stage computes the loss (enable_stage_loss)
   long steps_ = 0;
   std::map<std::string, std::chrono::steady_clock::time_point> last_beat_;
   struct Stash;  // messages taken off the queue while waiting for another kind

@@ -27,7 +27,9 @@ class Loss {
  public:
   Loss(int kind, float param, std::string type) : kind_(kind), param_(param), type_(std::move(type)) {}
   // logits / predictions [N, C] (device), labels int64 [N] or target fp32 [N, C] (any device)
-  LossResult compute(const Tensor& pred, const Tensor* labels, const Tensor* target = nullptr) const;
+  // grad_scale multiplies the gradient (e.g. 1 / micro-batches), not the loss value
+  LossResult compute(const Tensor& pred, const Tensor* labels, const Tensor* target = nullptr,
+                     float grad_scale = 1.f) const;
   LossResult operator()(const Tensor& pred, const Tensor& labels) const { return compute(pred, &labels); }
   const std::string& type() const { return type_; }
   int kind() const { return kind_; }

@@ -141,6 +141,12 @@ void Conv2D::build(const std::vector<int64_t>& in, Device dev, uint64_t seed) {
   if (bias_) add_param("bias", {co_, 1, 1, 1}, Layout::NCHW, uniform_init((size_t)co_, bound, seed + 1));
 }
 
+double Conv2D::flops(const std::vector<int64_t>& in) const {
+  const ConvShape s = shape_for(in);
+  const double out = (double)s.N * s.OH * s.OW, k = (double)ci_ * kh_ * kw_;
+  return 6.0 * co_ * k * out + (bias_ ? 2.0 * co_ * out : 0.0);  // forward 2, backward 4 per MAC
+}
+
 bool Conv2D::takes_raw_input(const std::vector<int64_t>& in) const {
   return dev_.is_gpu() && in.size() == 4 && in[1] == ci_ && gpu_ops::stem_ok(shape_for(in));
 }
@@ -838,6 +844,21 @@ void ResidualBlock::build(const std::vector<int64_t>& in, Device dev, uint64_t s
   }
 }
 
+double ResidualBlock::flops(const std::vector<int64_t>& in) const {
+  double f = 0;
+  std::vector<int64_t> s = in;
+  for (auto& l : main_) {
+    f += l->flops(s);
+    s = l->output_shape(s);
+  }
+  std::vector<int64_t> t = in;
+  for (auto& l : short_) {
+    f += l->flops(t);
+    t = l->output_shape(t);
+  }
+  return f + 2.0 * (double)s[0] * (double)s[1] * (double)s[2] * (double)s[3];  // the join
+}
+
 Conv2D* ResidualBlock::head_conv() const { return main_.empty() ? nullptr : dynamic_cast<Conv2D*>(main_[0].get()); }
 
 void fuse_blocks(std::vector<std::unique_ptr<Layer>>& seq, bool on) {
@@ -1272,6 +1293,16 @@ void Sequential::zero_grad() {
     else
       p->grad.zero_();
   }
+}
+
+std::vector<double> Sequential::layer_flops(const std::vector<int64_t>& in) const {
+  std::vector<double> out;
+  std::vector<int64_t> s = in;
+  for (auto& l : layers_) {
+    out.push_back(l->flops(s));
+    s = l->output_shape(s);
+  }
+  return out;
 }
 
 Tensor Sequential::input_activation(const Tensor& x_in) const {

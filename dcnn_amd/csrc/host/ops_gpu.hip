@@ -922,7 +922,15 @@ double softmax_ce(const void* pred, const int64_t* labels, void* grad, int N, in
 }
 
 double loss(int kind, const void* pred, const float* target, const int64_t* labels, void* grad, int N, int C,
-            float param, long* correct) {
+            float param, long* correct, float grad_scale) {
+  loss_launch(kind, pred, target, labels, grad, N, C, param, grad_scale);
+  return read_last_loss(correct);
+}
+
+double read_last_loss(long* correct) { return read_loss(static_cast<const char*>(scratch(LOSS_OUT, 16)), correct); }
+
+void loss_launch(int kind, const void* pred, const float* target, const int64_t* labels, void* grad, int N, int C,
+                 float param, float grad_scale) {
   float* ws = N > 4 ? static_cast<float*>(scratch(LOSS_WS, (size_t)loss_workspace_floats(N) * 4)) : nullptr;
   static unsigned* tickets = nullptr;
   if (N > 4 && !tickets) {
@@ -931,8 +939,7 @@ double loss(int kind, const void* pred, const float* target, const int64_t* labe
   }
   char* out = static_cast<char*>(scratch(LOSS_OUT, 16));
   loss_fused(kBF16, pred, target, labels, grad, reinterpret_cast<float*>(out), reinterpret_cast<int*>(out + 8), N, C,
-             kind, param, 1.0f, ws, N > 4 ? tickets : nullptr, cur());
-  return read_loss(out, correct);
+             kind, param, grad_scale, ws, N > 4 ? tickets : nullptr, cur());
 }
 
 void groupnorm_fwd(const void* x, void* y, int N, int HW, int C, int G, const float* g, const float* b, float eps,

@@ -1,5 +1,6 @@
 // Native pipeline stage (dcnn/pipeline.hpp): configuration, tensor payloads, the command handlers.
 #include "dcnn/pipeline.hpp"
+#include "dcnn/ops.hpp"
 
 #include <unistd.h>
 
@@ -160,6 +161,7 @@ void PipelineStage::process(Message& m) {
     switch (cmd) {
       case FORWARD_JOB: forward(m); break;
       case BACKWARD_JOB: backward(m); break;
+      case LABELS_TRANSFER: take_labels(m); break;
       case UPDATE_PARAMETERS: {
         if (m.payload_type == P_STRING && !m.text.empty()) {
           const json::Value hp = json::Value::parse(m.text);
@@ -459,9 +461,78 @@ void PipelineStage::forward(Message& m) {
   }
   out_kind_[mb] = OutKind{out.dtype(), out.layout(), out.shape()};
   const bool last = cfg_.stage_index == cfg_.num_stages - 1;
+  if (last && stage_loss_) {
+    // loss + d loss / d logits on this device; the coordinator gets the value, the backward starts
+    const Tensor labels = labels_for(mb);
+    const int64_t N = out.dim(0), C = out.numel() / N;
+    LossResult lr;
+    const bool train = model_->is_training();
+    if (dev_.is_gpu()) {
+      // the loss kernel and the backward go out first; one read of the value after them
+      lr.grad = Tensor::empty({N, C}, DType::BF16, dev_, Layout::NHWC);
+      gpu_ops::loss_launch(stage_loss_->kind(), out.data(), nullptr, labels.ptr<int64_t>(), lr.grad.data(), (int)N,
+                           (int)C, stage_loss_->param(), grad_scale_);
+      ++n_fwd_;
+      fwd_ms_ += std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+      if (train) run_backward(mb, lr.grad, std::chrono::steady_clock::now());
+      lr.loss = gpu_ops::read_last_loss(&lr.correct);
+    } else {
+      lr = stage_loss_->compute(out.view({N, C}, out.layout()), &labels, nullptr, grad_scale_);
+      ++n_fwd_;
+      fwd_ms_ += std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+    }
+    Message r;
+    r.recipient = "coordinator";
+    r.command = FORWARD_JOB;
+    r.payload_type = P_STRING;
+    json::Value v = json::Value::object();
+    v["mb"] = (int64_t)mb;
+    v["loss"] = lr.loss;
+    v["correct"] = (int64_t)lr.correct;
+    v["samples"] = N;
+    r.text = v.dump(-1);
+    comm_->send(std::move(r));
+    if (train && !dev_.is_gpu()) run_backward(mb, lr.grad, std::chrono::steady_clock::now());
+    return;
+  }
   send_tensor(last ? "coordinator" : "next_stage", FORWARD_JOB, mb, out, last);
   ++n_fwd_;
   fwd_ms_ += std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+}
+
+void PipelineStage::take_labels(Message& m) {
+  if (m.payload_type != P_TYPED_JOB || (m.dtype & 0x0F) != 5) throw std::runtime_error("LABELS_TRANSFER: f64 payload expected");
+  std::vector<double> v(m.data.size() / sizeof(double));
+  std::memcpy(v.data(), m.data.data(), v.size() * sizeof(double));
+  if (m.mb_id == kLossConfigMb) {
+    if (v.size() != 3) throw std::runtime_error("LABELS_TRANSFER: loss configuration is [kind, param, scale]");
+    if (cfg_.stage_index != cfg_.num_stages - 1) throw std::runtime_error("the stage loss runs on the last stage");
+    stage_loss_ = std::make_unique<Loss>((int)v[0], (float)v[1], "stage_loss");
+    grad_scale_ = (float)v[2];
+    labels_.clear();
+    reply(LABELS_TRANSFER, "ok");
+    return;
+  }
+  std::vector<int64_t> y(v.size());
+  for (size_t i = 0; i < v.size(); ++i) y[i] = (int64_t)v[i];
+  labels_[m.mb_id] = Tensor::from_host_i64(y, dev_);
+}
+
+// the micro-batch's labels: sent by the coordinator before its input, but the queue serves
+// LABELS_TRANSFER after FORWARD_JOB, so they may still be queued when the forward gets here
+Tensor PipelineStage::labels_for(uint64_t mb) {
+  const auto t0 = std::chrono::steady_clock::now();
+  while (labels_.find(mb) == labels_.end()) {
+    Message m;
+    if (comm_->queue().pop_command(LABELS_TRANSFER, m, 50)) {
+      take_labels(m);
+    } else if (std::chrono::steady_clock::now() - t0 > std::chrono::seconds(60)) {
+      throw std::runtime_error("no labels for micro-batch " + std::to_string(mb));
+    }
+  }
+  Tensor y = labels_.at(mb);
+  labels_.erase(mb);
+  return y;
 }
 
 void PipelineStage::backward(Message& m) {
@@ -477,6 +548,12 @@ void PipelineStage::backward(Message& m) {
     g = g.view(k.shape, k.layout);
   }
   g = convert(g, k.dt, k.layout, dev_);
+  run_backward(mb, g, t0);
+}
+
+void PipelineStage::run_backward(uint64_t mb, Tensor g, const std::chrono::steady_clock::time_point& t0) {
+  const OutKind& k = out_kind_.at(mb);
+  if (g.shape() != k.shape) g = g.view(k.shape, k.layout);  // ((N, C) logits gradient of an (N, C, 1, 1) output)
   Tensor gin;
   auto fg = fwd_graphed_.find(mb);
   if (graphs_ && fg != fwd_graphed_.end() && fg->second)

@@ -21,7 +21,7 @@ bool decode_jpeg(const unsigned char* data, size_t n, std::vector<unsigned char>
 namespace dcnn {
 
 // ================================================================= losses
-LossResult Loss::compute(const Tensor& pred, const Tensor* labels_in, const Tensor* target_in) const {
+LossResult Loss::compute(const Tensor& pred, const Tensor* labels_in, const Tensor* target_in, float grad_scale) const {
   if (pred.rank() != 2) throw std::runtime_error("loss: expected [N, C] predictions");
   const int N = (int)pred.dim(0), C = (int)pred.dim(1);
   const Device dev = pred.device();
@@ -37,10 +37,14 @@ LossResult Loss::compute(const Tensor& pred, const Tensor* labels_in, const Tens
   LossResult r;
   if (dev.is_gpu()) {
     r.grad = Tensor::empty({N, C}, DType::BF16, dev, Layout::NHWC);
-    r.loss = gpu_ops::loss(kind_, pred.data(), tp, lp, r.grad.data(), N, C, param_, &r.correct);
+    r.loss = gpu_ops::loss(kind_, pred.data(), tp, lp, r.grad.data(), N, C, param_, &r.correct, grad_scale);
   } else {
     r.grad = Tensor::empty({N, C}, DType::F32, dev);
     r.loss = cpu_ops::loss(kind_, pred.ptr<float>(), tp, lp, r.grad.ptr<float>(), N, C, param_, &r.correct);
+    if (grad_scale != 1.f) {
+      float* g = r.grad.ptr<float>();
+      for (int64_t i = 0; i < (int64_t)N * C; ++i) g[i] *= grad_scale;
+    }
   }
   return r;
 }

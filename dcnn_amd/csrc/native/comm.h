@@ -36,6 +36,10 @@ enum Command : uint16_t {
   BARRIER_SYNC, CHECKPOINT_REQUEST, CHECKPOINT_COMPLETE,
   UPDATE_LOAD, REPORT_LOAD, LOAD_REPORT,
   PRINT_PROFILING, PROFILING_PRINTED, CLEAR_PROFILING, PROFILING_CLEARED,
+  // native extension (the loss on the last stage's GPU, dcnn/pipeline.hpp): coordinator -> last
+  // stage, f64 payload [kind, param, gradient scale] with micro-batch id kLossConfig = enable (the
+  // stage answers with this command), else [label...] of that micro-batch
+  LABELS_TRANSFER,
   CMD_COUNT
 };
 const char* command_name(uint16_t c);

@@ -7,7 +7,8 @@
 //        [--microbatches 4] [--batch 64] [--steps 20] [--optimizer adam|sgd] [--lr 1e-3]
 //        [--momentum 0.9] [--devices CPU,CPU | --device GPU:0] [--loss softmax_crossentropy]
 //        [--data-x x.f32 --data-y y.i64] [--input C,H,W] [--classes K] [--save out]
-//        [--heartbeat S] [--transport message|ipc] [--json] [--bench W]
+//        [--heartbeat S] [--transport message|ipc] [--stage-loss auto|0|1] [--partitioner naive|flops]
+//        [--json] [--bench W]
 //
 // --spawn N starts N local native workers (this program never touches the GPU itself, so starting
 // them is safe). --init loads a saved model (path.json + path.bin [+ .bnstats]) whose weights are
@@ -15,7 +16,9 @@
 // batch; without them a learnable synthetic set of --input / --classes is used. --json prints one
 // JSON line per step; --bench W times the steps after W untimed warm-up steps (images/sec).
 // --transport ipc (GPU stages on one node): stage-to-stage activations and gradients stay on the
-// device (HIP IPC buffers); only their handles travel in the messages.
+// device (HIP IPC buffers); only their handles travel in the messages. --stage-loss: the loss on
+// the last stage's GPU (auto: when that stage is a native GPU stage) — the labels go there, only
+// the loss value comes back, and the backward starts without a round trip through this process.
 // Reference parity: examples/semi_async_pipeline_coordinator.cpp, sync_pipeline_coordinator.cpp,
 // coordinator_tiny_imagenet.cpp; include/pipeline/distributed_coordinator.hpp.
 #include <signal.h>
@@ -101,8 +104,8 @@ std::vector<char> read_file(const std::string& path) {
 int main(int argc, char** argv) {
   std::string workers, model_name = "mnist_cnn", config_path, init, schedule = "semi_async", opt_name = "adam";
   std::string devices, loss_name = "softmax_crossentropy", data_x, data_y, save, input = "1,28,28";
-  std::string transport = "message";
-  int spawn = 0, microbatches = 4, batch = 64, steps = 20, classes = 10, bench = -1;
+  std::string transport = "message", partitioner = "naive";
+  int spawn = 0, microbatches = 4, batch = 64, steps = 20, classes = 10, bench = -1, stage_loss = -1;
   float lr = 1e-3f, momentum = 0.f;
   double heartbeat = 0;
   bool json_out = false;
@@ -136,6 +139,8 @@ int main(int argc, char** argv) {
     else if (k == "--heartbeat") heartbeat = std::atof(v.c_str());
     else if (k == "--bench") bench = std::atoi(v.c_str());
     else if (k == "--transport") transport = v;
+    else if (k == "--stage-loss") stage_loss = v == "auto" ? -1 : std::atoi(v.c_str());
+    else if (k == "--partitioner") partitioner = v;
     else {
       std::fprintf(stderr, "unknown option %s\n", k.c_str());
       return 2;
@@ -191,12 +196,22 @@ int main(int argc, char** argv) {
     o.loss = loss_name;
     o.heartbeat_s = heartbeat;
     o.transport = transport;
+    o.stage_loss = stage_loss;
     if (!devices.empty()) {
       o.stage_devices = split_list(devices);
       if (o.stage_devices.size() == 1) o.stage_devices.assign(eps.size(), o.stage_devices[0]);
     }
     PipelineCoordinator coord(model.get_config(), oc, eps, o);
-    coord.initialize();
+    std::vector<Partition> parts;
+    if (partitioner == "flops") {
+      // FLOP-balanced stages (forward + backward of each top-level layer at the micro-batch shape)
+      std::vector<int64_t> shape{std::max(1, batch / std::max(1, microbatches))};
+      for (const auto& d : split_list(input)) shape.push_back(std::atoll(d.c_str()));
+      parts = balanced_partitions(model.layer_flops(shape), (int)eps.size());
+    } else if (partitioner != "naive") {
+      throw std::invalid_argument("unknown partitioner " + partitioner + " (naive, flops)");
+    }
+    coord.initialize(parts);
     coord.deploy_stages();
     coord.start();
     coord.send_parameters(model);

@@ -135,11 +135,14 @@ def test_native_stages_train_like_python_stages(worker_bin, schedule, opt_name):
 COORD = os.path.join(ROOT, "dcnn_amd", "bin", "pipeline_coordinator")
 
 
+@pytest.mark.parametrize("stage_loss", ["0", "1"])
 @pytest.mark.parametrize("schedule", ["sync", "semi_async", "1f1b"])
-def test_native_coordinator_trains_like_python_coordinator(worker_bin, tmp_path, schedule):
+def test_native_coordinator_trains_like_python_coordinator(worker_bin, tmp_path, schedule, stage_loss):
     """The C++ coordinator (csrc/host/coordinator.cpp, bin/pipeline_coordinator) driving native
     workers: the same per-step losses and the same trained model (gathered from the stages and
-    saved by the C++ program, loaded in Python) as the Python coordinator on the same batches."""
+    saved by the C++ program, loaded in Python) as the Python coordinator on the same batches —
+    with the loss on the coordinator (stage_loss 0) or on the last stage (1: labels to that stage,
+    its backward starts there, only the loss value comes back)."""
     import json
     from dcnn_amd.nn import Adam, Sequential
     from dcnn_amd.parallel.pipeline import InProcessCoordinator
@@ -170,7 +173,8 @@ def test_native_coordinator_trains_like_python_coordinator(worker_bin, tmp_path,
             [COORD, "--workers", ",".join(f"127.0.0.1:{p}" for p in w.ports), "--init", init, "--schedule", schedule,
              "--microbatches", "2", "--batch", "8", "--steps", "3", "--optimizer", "adam", "--lr", "2e-3",
              "--data-x", str(tmp_path / "x.f32"), "--data-y", str(tmp_path / "y.i64"), "--input", "3,12,12",
-             "--json", "--save", str(tmp_path / "out")], capture_output=True, text=True, timeout=120)
+             "--json", "--save", str(tmp_path / "out"), "--stage-loss", stage_loss],
+            capture_output=True, text=True, timeout=120)
     finally:
         w.close()
     assert out.returncode == 0, out.stderr
