@@ -119,7 +119,8 @@ struct PipelineCoordinator::Stash {
 
 struct PipelineCoordinator::Pending {
   uint64_t mb = 0;
-  std::vector<float> x;
+  const float* x = nullptr;  // the micro-batch's rows of the step's input (alive for the step)
+  std::shared_ptr<std::vector<float>> hold;  // (a converted copy when the input is not host fp32)
   std::vector<int64_t> shape;
   std::vector<int64_t> y;
 };
@@ -366,7 +367,16 @@ void PipelineCoordinator::send_job(const std::string& to, uint16_t cmd, uint64_t
 
 std::vector<PipelineCoordinator::Pending> PipelineCoordinator::split(const Tensor& x_in, const Tensor& labels) const {
   if (x_in.rank() < 2) throw std::invalid_argument("train_step: x must be (N, ...)");
-  const std::vector<float> x = x_in.to_host_f32();
+  // host fp32 input: the micro-batches point into it (the caller keeps x alive for the step);
+  // anything else is converted once
+  std::shared_ptr<std::vector<float>> hold;
+  const float* x = nullptr;
+  if (!x_in.device().is_gpu() && x_in.dtype() == DType::F32 && x_in.layout() == Layout::NCHW) {
+    x = x_in.ptr<float>();
+  } else {
+    hold = std::make_shared<std::vector<float>>(x_in.to_host_f32());
+    x = hold->data();
+  }
   const std::vector<int64_t> y = labels.to_host_i64();
   const int64_t N = x_in.dim(0), per = x_in.numel() / N;
   if ((int64_t)y.size() != N) throw std::invalid_argument("train_step: one label per sample required");
@@ -379,7 +389,8 @@ std::vector<PipelineCoordinator::Pending> PipelineCoordinator::split(const Tenso
     const int64_t e = i == M - 1 ? N : s + base;
     Pending& p = out[i];
     p.mb = (uint64_t)i;
-    p.x.assign(x.begin() + s * per, x.begin() + e * per);
+    p.x = x + s * per;
+    p.hold = hold;
     p.shape = x_in.shape();
     p.shape[0] = e - s;
     p.y.assign(y.begin() + s, y.begin() + e);
@@ -391,7 +402,7 @@ std::vector<PipelineCoordinator::Pending> PipelineCoordinator::split(const Tenso
 void PipelineCoordinator::forward_mb(const Pending& p) {
   // (the labels first: the last stage needs them when the micro-batch's activations arrive)
   if (stage_loss_on_) send_f64(names_.back(), LABELS_TRANSFER, p.mb, std::vector<double>(p.y.begin(), p.y.end()));
-  send_job(names_.front(), FORWARD_JOB, p.mb, p.x.data(), p.shape);
+  send_job(names_.front(), FORWARD_JOB, p.mb, p.x, p.shape);
 }
 
 // (a P_STRING payload carries no micro-batch id field: the last stage's loss report names it)

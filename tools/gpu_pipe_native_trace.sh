@@ -15,7 +15,7 @@ for i in 0 1 2 3; do
   PIDS+=($!)
 done
 sleep 20
-timeout -k 10 240 dcnn_amd/bin/pipeline_coordinator --workers 127.0.0.1:29400,127.0.0.1:29401,127.0.0.1:29402,127.0.0.1:29403 --model resnet50_tiny_imagenet --input 3,64,64 --classes 200 --device GPU:0 --batch 256 --microbatches 8 --schedule 1f1b --steps 8 --bench 2 --transport ipc >> $L 2>&1; rc=$?
+timeout -k 10 240 dcnn_amd/bin/pipeline_coordinator --workers 127.0.0.1:29400,127.0.0.1:29401,127.0.0.1:29402,127.0.0.1:29403 --model resnet50_tiny_imagenet --input 3,64,64 --classes 200 --device GPU:0 --batch 256 --microbatches 8 --schedule 1f1b --steps 8 --bench 2 --transport ipc --partitioner flops >> $L 2>&1; rc=$?
 for p in "${PIDS[@]}"; do wait $p; done
 [ $rc -eq 0 ] || exit $rc
 DBS=$(find gpurun_out/pnt_$TAG -name 'run_results.db' | sort)
