@@ -87,9 +87,6 @@ bool hconv_v3(int NB, int H, int W, int Cs, int N, int ntaps);  // shape runs on
 void hconv3_enable(int on);
 void hconv3_set_grid_cap(int n);      // test hook: cap the persistent grid (0: resident workgroups)
 void hconv3_set_stamps(uintptr_t p);  // diagnostic per-item timeline buffer (u64 [items][4][16]) or 0
-// BatchNorm-fold experiment hook: the next statistics forwards read relu(scale * x + shift) of their
-// input (fp32 scale [Cs] then shift [Cs] at p), applied to the halo in LDS; 0 = off
-void hconv3_set_input_affine(uintptr_t p);
 // halo-tiled stride-1 weight gradient (hwgrad.hip): slab[split][Co][t*Cs + c] = partial dW
 struct HWArgs {
   const bf16* dY; const bf16* X; float* slab; float* bias_slab;  // bias_slab[split][Co] (optional)

@@ -127,7 +127,6 @@ PYBIND11_MODULE(_kernels, m) {
   m.def("hconv3_enable", &hconv3_enable);
   m.def("hconv_v3", &hconv_v3);
   m.def("hconv3_set_stamps", &hconv3_set_stamps);
-  m.def("hconv3_set_input_affine", &hconv3_set_input_affine);
   m.def("hwgrad",
         [](uintptr_t dY, uintptr_t X, uintptr_t slab, uintptr_t bias_slab, unsigned dy_bytes, unsigned x_bytes, int NB,
            int H, int W, int Cs, int Co, std::vector<std::array<int, 2>> taps, int splits, int ldy, int ldx,

@@ -150,9 +150,6 @@ struct H3Geo {
   FastDiv fd_pitch, fd_ih1, fd_iw1;
   unsigned c_bytes;        // output bytes (32-bit store offsets)
   unsigned long long* stamps;  // diagnostic timeline [nitems][NW][16] (STAMP instance only)
-  // AIN instance (BatchNorm-fold experiment): the input is relu(scale[c] * x + shift[c]) of the
-  // stored x, applied to the halo in LDS; ain = scale [Cs] then shift [Cs]
-  const float* ain;
 };
 
 // NW waves per workgroup, WC of them along the output channels (64 each), NW / WC along the
@@ -164,8 +161,6 @@ struct H3 {
   static constexpr int HALO = NW * HN * 1024;   // one halo buffer
   static constexpr int WST = NW * NWI * 1024;   // one weight stage (3 taps x BN rows x 64 B, padded)
   static constexpr int LDS = 2 * HALO + 2 * WST;
-  static constexpr int AIN_MAXC = 512;          // AIN table: scale + shift of up to 512 input channels
-  static constexpr int LDS_AIN = LDS + 2 * AIN_MAXC * 4;
   static_assert(3 * BN * 64 <= WST, "weight stage");
   static_assert(WP * BN * 3 * 4 + 16 <= HALO, "epilogue scratch lives in the last chunk's halo buffer");
   static_assert(LDS <= 163840, "LDS budget");
@@ -177,7 +172,7 @@ struct H3 {
 // backward-BatchNorm fusion (optional residual); 3 = forward statistics with bias / residual /
 // ReLU at run time.
 // STAMP: diagnostic instance with s_memtime stamps (benchmarks/hconv3_timeline.py).
-template <int NW, int WC, int TWC, int HN, int NWI, int PITCH, int EPI, bool STAMP, bool AIN = false>
+template <int NW, int WC, int TWC, int HN, int NWI, int PITCH, int EPI, bool STAMP>
 __global__ void __launch_bounds__(NW * 64, 8 / NW) hconv3_kernel(HConvArgs p, H3Geo g) {
   using T = H3<NW, WC, TWC, HN, NWI, PITCH>;
   constexpr int BN = T::BN, WP = T::WP;
@@ -202,13 +197,6 @@ __global__ void __launch_bounds__(NW * 64, 8 / NW) hconv3_kernel(HConvArgs p, H3
   stamp(u, 5);
   if (p.zero_ptr && blockIdx.x == 0)
     for (int i = tid; i < p.zero_n; i += NT) p.zero_ptr[i] = 0.f;
-  float* ain_lds = reinterpret_cast<float*>(smem + T::LDS);  // AIN: scale [Cs], shift at + AIN_MAXC
-  if constexpr (AIN) {
-    for (int i = tid; i < p.Cs; i += NT) {
-      ain_lds[i] = g.ain[i];
-      ain_lds[T::AIN_MAXC + i] = g.ain[p.Cs + i];
-    }
-  }
   const i32x4 rsA = raw_rsrc(p.A, p.a_bytes);
   const i32x4 rsB = raw_rsrc(p.B, p.b_bytes);
   const int tx_tiles = g.tx_tiles, tpi = g.tpi;
@@ -316,33 +304,6 @@ __global__ void __launch_bounds__(NW * 64, 8 / NW) hconv3_kernel(HConvArgs p, H3
       glds16_at<BUF * T::HALO + K * 1024>(rsA, hbase, hs[K] + co);
     });
   };
-  // AIN: this lane's own DMA'd halo pieces of buffer BUF (64 lanes x 16 B per instruction, lane
-  // order) -> relu(scale * x + shift) in place; out-of-image pieces (never loaded, zero) stay zero.
-  // Runs after the lane's vmcnt wait and before the barrier that publishes the buffer.
-  auto ain_halo = [&](auto buf_c, int cbase_chunk, const unsigned* hsv) H3L {
-    if constexpr (AIN) {
-      constexpr int BUF = decltype(buf_c)::value;
-#pragma unroll
-      for (int k = 0; k < HN; ++k) {
-        if (hsv[k] == kOOB3) continue;
-        const int slot = (int)((hpk[k] >> 24) & 3);
-        const int c0 = cbase_chunk + slot * 8;
-        char* q = smem + BUF * T::HALO + (wid * HN + k) * 1024 + lane * 16;
-        float f[8];
-        unpack8(*reinterpret_cast<const uint4*>(q), f);
-#pragma unroll
-        for (int h = 0; h < 2; ++h) {  // (4 channels at a time: the kernel has no registers to spare)
-          const float4 sc = *reinterpret_cast<const float4*>(ain_lds + c0 + 4 * h);
-          const float4 sh = *reinterpret_cast<const float4*>(ain_lds + T::AIN_MAXC + c0 + 4 * h);
-          f[4 * h + 0] = fmaxf(fmaf(sc.x, f[4 * h + 0], sh.x), 0.f);
-          f[4 * h + 1] = fmaxf(fmaf(sc.y, f[4 * h + 1], sh.y), 0.f);
-          f[4 * h + 2] = fmaxf(fmaf(sc.z, f[4 * h + 2], sh.z), 0.f);
-          f[4 * h + 3] = fmaxf(fmaf(sc.w, f[4 * h + 3], sh.w), 0.f);
-        }
-        *reinterpret_cast<uint4*>(q) = pack8(f);
-      }
-    }
-  };
   auto load_w = [&](auto stage_c, int c, int dy, const unsigned* ws) H3L {
     constexpr int ST = decltype(stage_c)::value;
     h3_static_for<0, NWI>([&](auto kc) H3L {
@@ -432,7 +393,6 @@ __global__ void __launch_bounds__(NW * 64, 8 / NW) hconv3_kernel(HConvArgs p, H3
 
   // ---- first item's prologue: halo chunk 0, W(0, 0) landed; W(0, 1) in flight
   unsigned hs[HN], ws[NWI];
-  int nxt_cbase = 0;  // (AIN) first input channel of the item whose chunk 0 the last chunk prefetches
   addrs(decode(u), hs, ws);
   stamp(u, 6);
   load_halo(I0{}, 0, hs);
@@ -440,10 +400,6 @@ __global__ void __launch_bounds__(NW * 64, 8 / NW) hconv3_kernel(HConvArgs p, H3
   load_w(I1{}, 0, 1, ws);
   vmwait<NWI>();
   stamp(u, 7);
-  if constexpr (AIN) {
-    __syncthreads();  // (the AIN table is complete)
-    ain_halo(I0{}, decode(u).cbase, hs);
-  }
   h3_barrier();
   int nst = 0;  // output stores issued after the item's W(0, 1) (the previous item's epilogue)
 
@@ -480,13 +436,7 @@ __global__ void __launch_bounds__(NW * 64, 8 / NW) hconv3_kernel(HConvArgs p, H3
         if (!last) {
           load_halo(S1{}, c + 1, hs);
         } else if (has_next) {
-          if constexpr (AIN) {
-            const Item nt = decode(un);
-            addrs_h(nt, hs);
-            nxt_cbase = nt.cbase;
-          } else {
-            addrs_h(decode(un), hs);
-          }
+          addrs_h(decode(un), hs);
           load_halo(S1{}, 0, hs);
         }
       };
@@ -504,11 +454,6 @@ __global__ void __launch_bounds__(NW * 64, 8 / NW) hconv3_kernel(HConvArgs p, H3
       h3_barrier();
       step(hb_c, I1{}, S1{}, nothing, [&]() H3L { load_w(S0{}, c, 2, ws); });
       vmwait<0>();
-      if constexpr (AIN) {
-        // the next halo chunk (this item's c + 1, or the next item's chunk 0) has landed
-        if (!last) ain_halo(S1{}, (u % SPL) * nch * 32 + (c + 1) * 32, hs);
-        else if (has_next) ain_halo(S1{}, nxt_cbase, hs);
-      }
       h3_barrier();
       step(hb_c, I2{}, S0{}, nothing, [&]() H3L {
         if (!last) {
@@ -714,8 +659,6 @@ static int g_h3 = 1;  // hconv3_enable(0): the previous kernel (test hook)
 void hconv3_enable(int on) { g_h3 = on; }
 static unsigned long long* g_h3_stamps = nullptr;
 void hconv3_set_stamps(uintptr_t p) { g_h3_stamps = reinterpret_cast<unsigned long long*>(p); }
-static const float* g_h3_ain = nullptr;
-void hconv3_set_input_affine(uintptr_t p) { g_h3_ain = reinterpret_cast<const float*>(p); }
 static int g_h3_grid_cap = 0;  // test hook: at most this many persistent workgroups (0: resident count)
 void hconv3_set_grid_cap(int n) { g_h3_grid_cap = n < 0 ? 0 : n; }
 static int g_h3_max_splits = 8;  // tuning hook: split-K slices per tile at most
@@ -757,11 +700,11 @@ bool hconv3_plan(int NB, int H, int W, int Cs, int N, int ntaps, H3Plan* pl) {
   return true;
 }
 
-template <int NW, int WC, int TWC, int HN, int NWI, int PITCH, int EPI, bool STAMP, bool AIN = false>
+template <int NW, int WC, int TWC, int HN, int NWI, int PITCH, int EPI, bool STAMP>
 static void launch_h3e(const HConvArgs& a, const H3Geo& g, hipStream_t s) {
   using T = H3<NW, WC, TWC, HN, NWI, PITCH>;
-  auto k = hconv3_kernel<NW, WC, TWC, HN, NWI, PITCH, EPI, STAMP, AIN>;
-  constexpr int lds = AIN ? T::LDS_AIN : T::LDS;
+  auto k = hconv3_kernel<NW, WC, TWC, HN, NWI, PITCH, EPI, STAMP>;
+  constexpr int lds = T::LDS;
   static int resident = 0;  // workgroups of this instance the device holds at once
   if (!resident) {
     DCNN_HIP_CHECK(hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, lds));
@@ -794,13 +737,6 @@ static int h3_epi(const HConvArgs& a) {
 template <int NW, int WC, int TWC, int HN, int NWI, int PITCH>
 static void launch_h3(const HConvArgs& a, const H3Geo& g, hipStream_t s) {
   const int epi = h3_epi(a);
-  if (g.ain) {  // (BatchNorm-fold experiment: the statistics forward on 16x16+ maps only)
-    if constexpr (HN == 6) {
-      if (epi == 1 && a.Cs <= H3<NW, WC, TWC, HN, NWI, PITCH>::AIN_MAXC)
-        return launch_h3e<NW, WC, TWC, HN, NWI, PITCH, 1, false, true>(a, g, s);
-    }
-    throw std::runtime_error("hconv3: input affine only on the statistics forward of 16x16+ maps");
-  }
   // (timeline instances: the statistics forward and the plain dgrad)
   if (g.stamps && epi == 1) return launch_h3e<NW, WC, TWC, HN, NWI, PITCH, 1, true>(a, g, s);
   if (g.stamps && epi == 0) return launch_h3e<NW, WC, TWC, HN, NWI, PITCH, 0, true>(a, g, s);
@@ -845,7 +781,6 @@ bool hconv3_try(const HConvArgs& a0, hipStream_t s) {
   g.nitems = pl.tiles_m * pl.tiles_n * pl.splits;
   g.c_bytes = (unsigned)c_bytes;
   g.stamps = g_h3_stamps;
-  g.ain = g_h3_ain;
   launch_h3_plan(pl, a, g, s);
   return true;
 }
