@@ -9,6 +9,7 @@
 // include/data_loading/{mnist,cifar10,cifar100,tiny_imagenet}_data_loader.hpp,
 // include/nn/example_models.hpp:13-437 (model zoo).
 #pragma once
+#include <functional>
 #include <memory>
 #include <string>
 #include <vector>
@@ -52,6 +53,9 @@ class TrainGraph {
   TrainGraph(Sequential& model, Adam& opt, const Loss& loss) : model_(model), opt_(opt), loss_(loss) {}
   double step(const Tensor& x, const Tensor& labels);  // eager on the first call: captures, then replays
   double last_loss();                                  // host read of the last replay's loss
+  // runs between the backward and the optimizer of every step, inside the capture (e.g. the
+  // data-parallel gradient all-reduce, dist::DataParallel::all_reduce_mean on the arena gradient)
+  void set_gradient_hook(std::function<void()> f) { grad_hook_ = std::move(f); }
 
  private:
   void capture(const Tensor& x, const Tensor& labels);
@@ -61,6 +65,7 @@ class TrainGraph {
   gpu::Graph graph_;
   Tensor sx_, sy_;
   bool captured_ = false;
+  std::function<void()> grad_hook_;
 };
 
 struct LossFactory {

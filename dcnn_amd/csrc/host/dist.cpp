@@ -1,0 +1,137 @@
+// Data parallelism of the C++ host API (dcnn/dist.hpp).
+#include "dcnn/dist.hpp"
+
+#include <arpa/inet.h>
+#include <netdb.h>
+#include <netinet/in.h>
+#include <sys/socket.h>
+#include <unistd.h>
+
+#include <chrono>
+#include <cstdlib>
+#include <cstring>
+#include <stdexcept>
+#include <thread>
+
+#include "../kernels/collective.h"
+#include "dcnn/ops.hpp"
+
+namespace dcnn {
+namespace dist {
+
+namespace {
+int env_int(const char* k, int d) {
+  const char* v = std::getenv(k);
+  return v && *v ? std::atoi(v) : d;
+}
+void send_all(int fd, const char* p, size_t n) {
+  while (n) {
+    const ssize_t k = ::send(fd, p, n, MSG_NOSIGNAL);
+    if (k <= 0) throw std::runtime_error("dist: send failed");
+    p += k;
+    n -= (size_t)k;
+  }
+}
+void recv_all(int fd, char* p, size_t n) {
+  while (n) {
+    const ssize_t k = ::recv(fd, p, n, 0);
+    if (k <= 0) throw std::runtime_error("dist: recv failed");
+    p += k;
+    n -= (size_t)k;
+  }
+}
+}  // namespace
+
+Env Env::from_env() {
+  Env e;
+  e.rank = env_int("RANK", 0);
+  e.world = env_int("WORLD_SIZE", 1);
+  e.local_rank = env_int("LOCAL_RANK", e.rank);
+  if (const char* a = std::getenv("MASTER_ADDR")) e.addr = a;
+  e.port = env_int("MASTER_PORT", 29500);
+  if (e.world < 1 || e.rank < 0 || e.rank >= e.world) throw std::invalid_argument("dist: bad RANK / WORLD_SIZE");
+  return e;
+}
+
+std::string exchange_unique_id(const Env& e, int port_offset, double timeout_s) {
+  if (e.world == 1) return coll::unique_id();
+  const int port = e.port + port_offset;
+  const auto t0 = std::chrono::steady_clock::now();
+  auto expired = [&] {
+    return std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count() > timeout_s;
+  };
+  if (e.rank == 0) {
+    const std::string id = coll::unique_id();
+    const int fd = ::socket(AF_INET, SOCK_STREAM, 0);
+    if (fd < 0) throw std::runtime_error("dist: socket failed");
+    const int one = 1;
+    ::setsockopt(fd, SOL_SOCKET, SO_REUSEADDR, &one, sizeof one);
+    sockaddr_in a{};
+    a.sin_family = AF_INET;
+    a.sin_addr.s_addr = htonl(INADDR_ANY);
+    a.sin_port = htons((uint16_t)port);
+    if (::bind(fd, reinterpret_cast<sockaddr*>(&a), sizeof a) != 0 || ::listen(fd, e.world) != 0) {
+      ::close(fd);
+      throw std::runtime_error("dist: rank 0 cannot listen on port " + std::to_string(port));
+    }
+    for (int served = 1; served < e.world; ++served) {
+      const int c = ::accept(fd, nullptr, nullptr);
+      if (c < 0) {
+        ::close(fd);
+        throw std::runtime_error("dist: accept failed");
+      }
+      send_all(c, id.data(), id.size());
+      ::close(c);
+    }
+    ::close(fd);
+    return id;
+  }
+  addrinfo hints{}, *res = nullptr;
+  hints.ai_family = AF_INET;
+  hints.ai_socktype = SOCK_STREAM;
+  if (::getaddrinfo(e.addr.c_str(), std::to_string(port).c_str(), &hints, &res) != 0 || !res)
+    throw std::runtime_error("dist: cannot resolve " + e.addr);
+  std::string id(128, '\0');
+  while (true) {
+    const int fd = ::socket(AF_INET, SOCK_STREAM, 0);
+    if (fd >= 0 && ::connect(fd, res->ai_addr, res->ai_addrlen) == 0) {
+      recv_all(fd, &id[0], id.size());
+      ::close(fd);
+      break;
+    }
+    if (fd >= 0) ::close(fd);
+    if (expired()) {
+      ::freeaddrinfo(res);
+      throw std::runtime_error("dist: no rank 0 at " + e.addr + ":" + std::to_string(port));
+    }
+    std::this_thread::sleep_for(std::chrono::milliseconds(50));
+  }
+  ::freeaddrinfo(res);
+  return id;
+}
+
+DataParallel::DataParallel(const Env& e, int port_offset) : env_(e) {
+  if (!coll::available()) throw std::runtime_error("dist: RCCL unavailable: " + coll::load_error());
+  gpu::set_device(e.local_rank);
+  const std::string id = exchange_unique_id(e, port_offset);
+  comm_ = std::make_unique<coll::Comm>(id, e.world, e.rank, e.local_rank);
+  scratch_ = Tensor::zeros({1}, DType::F32, Device::gpu(e.local_rank));
+}
+
+DataParallel::~DataParallel() = default;
+
+void DataParallel::all_reduce_mean(float* data, size_t n) {
+  if (n == 0) return;
+  comm_->all_reduce(data, data, n, 0, 4, gpu::flow());  // fp32, average (world 1 too: one code path)
+}
+
+double DataParallel::max(double v) {
+  float f = (float)v;
+  gpu::copy(scratch_.data(), &f, sizeof f, 0);
+  comm_->all_reduce(scratch_.data(), scratch_.data(), 1, 0, 2, gpu::flow());
+  gpu::copy(&f, scratch_.data(), sizeof f, 1);
+  return f;
+}
+
+}  // namespace dist
+}  // namespace dcnn

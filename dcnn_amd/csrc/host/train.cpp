@@ -64,6 +64,7 @@ void TrainGraph::capture(const Tensor& x, const Tensor& labels) {
     model_.zero_grad();
     LossResult r = loss_(model_.forward(sx_), sy_);
     model_.backward(r.grad);
+    if (grad_hook_) grad_hook_();
     opt_.step(params);
   };
   for (int i = 0; i < 2; ++i) eager();
@@ -94,6 +95,7 @@ double TrainGraph::step(const Tensor& x, const Tensor& labels) {
     model_.zero_grad();
     LossResult r = loss_(model_.forward(x), labels);
     model_.backward(r.grad);
+    if (grad_hook_) grad_hook_();
     opt_.step(model_.parameters());
     return r.loss;
   }

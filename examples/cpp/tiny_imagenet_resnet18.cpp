@@ -4,23 +4,29 @@
 //   dcnn_amd/bin/tiny_imagenet_resnet18 [--device CPU|GPU] [--model resnet18_tiny_imagenet]
 //        [--data data/tiny-imagenet-200] [--epochs E] [--steps S] [--batch B] [--lr 1e-3]
 //        [--loss logsoftmax_ce] [--scheduler cosine_annealing_lr] [--max-per-class K]
-//        [--save model_snapshots/resnet18] [--bench [--eager]]
+//        [--save model_snapshots/resnet18] [--bench [--eager]] [--dp]
 //
 // Without --data it trains on a learnable synthetic 3x64x64 200-class set. --bench times
 // --steps training steps after 3 warm-up steps on two device-resident synthetic batches and
 // prints one JSON line (images/sec); on the GPU the step is captured into a hipGraph
 // (dcnn::TrainGraph) and replayed, --eager launches every kernel from the host instead. The saved
 // model (path.json + path.bin + path.bnstats) loads in Python with Sequential.from_file.
+// --dp (GPU, --bench): data parallel over RCCL, one process per GPU under the torch.distributed
+// launcher's variables (RANK / WORLD_SIZE / LOCAL_RANK / MASTER_ADDR / MASTER_PORT; dcnn/dist.hpp):
+// each rank trains --batch samples per step, the gradient all-reduce (mean) runs inside the captured
+// step, rank 0 prints the whole job's images/sec with the slowest rank's time.
 // Honours the reference's .env keys DEVICE_TYPE / EPOCHS / BATCH_SIZE / LR_INITIAL.
 // Reference parity: examples/tiny_imagenet_resnet18.cpp:23-107 (Adam, logsoftmax-CE, profiling),
 // include/nn/example_models.hpp:306-331 (the model).
 #include <chrono>
+#include <functional>
 #include <cstdio>
 #include <cstdlib>
 #include <iostream>
 #include <memory>
 #include <string>
 
+#include "dcnn/dist.hpp"
 #include "dcnn/nn.hpp"
 #include "dcnn/train.hpp"
 
@@ -39,11 +45,12 @@ int main(int argc, char** argv) {
   int epochs = std::atoi(env_or("EPOCHS", "1").c_str()), steps = -1, max_per_class = 0;
   int batch = std::atoi(env_or("BATCH_SIZE", "64").c_str());
   float lr = std::atof(env_or("LR_INITIAL", "0.001").c_str());
-  bool bench = false, eager = false;
+  bool bench = false, eager = false, dp_on = false;
   for (int i = 1; i < argc; ++i) {
     const std::string k = argv[i];
     if (k == "--bench") { bench = true; continue; }
     if (k == "--eager") { eager = true; continue; }
+    if (k == "--dp") { dp_on = true; continue; }
     if (i + 1 >= argc) break;
     const std::string v = argv[++i];
     if (k == "--device") device = v;
@@ -60,7 +67,14 @@ int main(int argc, char** argv) {
   }
   try {
     Sequential model = create_model(model_name);
-    const Device dev = Device::parse(device);
+    std::unique_ptr<dist::DataParallel> dp;
+    Device dev = Device::parse(device);
+    if (dp_on) {
+      if (!dev.is_gpu() || !bench) throw std::invalid_argument("--dp: GPU --bench runs only");
+      const dist::Env env = dist::Env::from_env();
+      dp = std::make_unique<dist::DataParallel>(env);  // (selects GPU LOCAL_RANK)
+      dev = Device::gpu(env.local_rank);
+    }
     model.set_device(dev);
     model.initialize(42);
     std::printf("%s on %s: %zu parameters\n", model.name().c_str(), dev.str().c_str(), model.num_parameters());
@@ -99,6 +113,15 @@ int main(int argc, char** argv) {
       // replayed with one launch per step; --eager launches every kernel from the host
       const bool graph = dev.is_gpu() && !eager;
       TrainGraph tg(model, opt, loss);
+      // data parallel: the mean of the flat arena gradient over the ranks, between the backward
+      // and the optimizer (inside the captured step)
+      std::function<void()> allreduce;
+      if (dp) {
+        ParamArena* arena = model.parameters().at(0)->arena.get();
+        if (!arena) throw std::runtime_error("--dp: the parameters are not in a GPU arena");
+        allreduce = [&dp, arena] { dp->all_reduce_mean(arena->grad.ptr<float>(), (size_t)arena->grad.numel()); };
+        tg.set_gradient_hook(allreduce);
+      }
       auto one = [&] {
         const auto& [x, y] = staged[(size_t)(k++) % staged.size()];
         if (graph) return tg.step(x, y);
@@ -106,6 +129,7 @@ int main(int argc, char** argv) {
         Tensor logits = model.forward(x);
         LossResult r = loss(logits, y);
         model.backward(r.grad);
+        if (allreduce) allreduce();
         opt.step(model.parameters());
         return r.loss;
       };
@@ -115,12 +139,16 @@ int main(int argc, char** argv) {
       double last = 0;
       for (int i = 0; i < timed; ++i) last = one();
       if (dev.is_gpu()) gpu::synchronize();
-      const double s = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+      double s = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
       if (graph) last = tg.last_loss();
-      std::printf("{\"metric\": \"images/sec %s training (C++ host API)\", \"value\": %.1f, \"ms_per_step\": %.3f, "
-                  "\"batch\": %d, \"steps\": %d, \"device\": \"%s\", \"hipgraph\": %s, \"loss\": %.4f}\n",
-                  model_name.c_str(), (double)batch * timed / s, 1e3 * s / timed, batch, timed, dev.str().c_str(),
-                  graph ? "true" : "false", last);
+      const int world = dp ? dp->world() : 1;
+      if (dp) s = dp->max(s);  // the slowest rank
+      if (!dp || dp->rank() == 0)
+        std::printf("{\"metric\": \"images/sec %s training (C++ host API)\", \"value\": %.1f, \"ms_per_step\": %.3f, "
+                    "\"batch\": %d, \"steps\": %d, \"device\": \"%s\", \"hipgraph\": %s, \"loss\": %.6f, "
+                    "\"world\": %d, \"data_parallel\": %s}\n",
+                    model_name.c_str(), (double)batch * world * timed / s, 1e3 * s / timed, batch, timed,
+                    dev.str().c_str(), graph ? "true" : "false", last, world, dp ? "\"rccl\"" : "null");
       return 0;
     }
     std::unique_ptr<Scheduler> sched;

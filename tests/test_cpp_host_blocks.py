@@ -336,3 +336,25 @@ def test_cpp_tiny_imagenet_trainer_graph_bench(bins, tmp_path):
                tmp_path, timeout=300)
     assert '"hipgraph": true' in out and re.search(r"\"value\": (\S+),", out), out
     print(out)
+
+
+@pytest.mark.gpu
+def test_cpp_data_parallel_world1_matches_single(bins, tmp_path):
+    """C++ data parallelism (dcnn/dist.hpp: rendezvous, in-tree RCCL communicator, the gradient
+    all-reduce inside the captured step) at world size 1: the RCCL mean over one rank is the
+    gradient itself, so the captured step trains exactly like the single-process one."""
+    import json
+    import socket
+    with socket.socket() as s_:
+        s_.bind(("127.0.0.1", 0))
+        port = s_.getsockname()[1]
+    cmd = [bins["tiny_imagenet_resnet18"], "--device", "GPU", "--batch", "64", "--steps", "6", "--bench"]
+    plain = json.loads([l for l in _run(cmd, tmp_path, timeout=300).splitlines() if l.startswith("{")][-1])
+    env = dict(os.environ, RANK="0", WORLD_SIZE="1", LOCAL_RANK="0", MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    r = subprocess.run(cmd + ["--dp"], cwd=tmp_path, stdout=subprocess.PIPE, stderr=subprocess.STDOUT, text=True,
+                       timeout=300, env=env)
+    assert r.returncode == 0, r.stdout[-3000:]
+    dp = json.loads([l for l in r.stdout.splitlines() if l.startswith("{")][-1])
+    assert dp["world"] == 1 and dp["data_parallel"] == "rccl" and dp["hipgraph"] is True
+    assert dp["loss"] == plain["loss"], (dp, plain)
+    print(plain, dp)
