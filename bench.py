@@ -16,6 +16,11 @@ communicator (parallel/rccl.py, no c10d) with --dp-backend rccl.
 Exactly K steps are timed between a barrier + device synchronisation on both sides; the
 slowest rank's time is reported. Every timed step runs the full forward, loss, backward,
 gradient all-reduce and optimizer update.
+
+--engine native runs the same step on the C++ host API instead (bin/tiny_imagenet_resnet18: the
+framework's own Tensor, flows and gpu::Graph capture, the gradient mean over the in-tree RCCL
+communicator inside the captured step; no torch in the timed process), one child process per rank
+under the same launcher variables.
 """
 import argparse
 import json
@@ -29,6 +34,45 @@ import torch.distributed as dist
 sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
 
 METRIC = "images/sec (whole node) ResNet-18 Tiny-ImageNet training at 1/2/4/8 MI355X"
+ROOT = os.path.dirname(os.path.abspath(__file__))
+
+
+def native_main(a):
+    """--engine native: the timed steps run in the C++ trainer (one child process per rank, the
+    launcher's RANK / WORLD_SIZE / LOCAL_RANK / MASTER_* passed through); its JSON line becomes this
+    contract's line on rank 0."""
+    import subprocess
+    world, rank = int(os.environ.get("WORLD_SIZE", "1")), int(os.environ.get("RANK", "0"))
+    if a.gpus != world and world > 1:
+        raise SystemExit(f"--gpus {a.gpus} but WORLD_SIZE={world}")
+    if a.device != "cuda" or a.dtype != "bf16":
+        raise SystemExit("--engine native: bf16 on GPUs only")
+    cmd = [os.path.join(ROOT, "dcnn_amd", "bin", "tiny_imagenet_resnet18"), "--device", "GPU", "--model", a.model,
+           "--batch", str(a.batch), "--steps", str(a.steps), "--warmup", str(a.warmup), "--loss", "softmax_ce",
+           "--bench"] + (["--dp"] if world > 1 else [])
+    env = dict(os.environ)
+    env.setdefault("MASTER_ADDR", "127.0.0.1")
+    env.setdefault("MASTER_PORT", "29533")
+    r = subprocess.run(cmd, env=env, stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True)
+    if r.returncode != 0:
+        print(r.stdout[-2000:] + r.stderr[-4000:], file=sys.stderr, flush=True)
+        raise SystemExit(r.returncode)
+    if rank != 0:
+        return
+    d = json.loads([l for l in r.stdout.splitlines() if l.startswith("{")][-1])
+    from dcnn_amd.models import INPUT_SHAPES
+    C, H, W = INPUT_SHAPES[a.model]
+    print(json.dumps({
+        "metric": METRIC if a.model == "resnet18_tiny_imagenet" else f"images/sec (whole node) {a.model} training",
+        "value": round(d["value"], 2), "unit": "images/sec", "n_gpus": world, "steps": a.steps, "warmup": a.warmup,
+        "ms_per_step": round(d["ms_per_step"], 4), "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
+        "dtype": "bf16", "data": f"synthetic (random {H}x{W}x{C} inputs + random labels, random init)",
+        "config": {"model": a.model, "global_batch": a.batch * world, "per_gpu_batch": a.batch, "seq_len": None,
+                   "image_size": [C, H, W], "parallelism": f"dp{world}", "optimizer": "adam",
+                   "grad_allreduce": "fp32" if world > 1 else None, "data_plane": d.get("data_parallel"),
+                   "hipgraph": d.get("hipgraph"), "final_loss": round(d.get("loss", float("nan")), 4),
+                   "f32_mode": None, "engine": "native (C++ host API)"},
+    }), flush=True)
 
 
 def main():
@@ -50,6 +94,8 @@ def main():
                          "the framework's own RCCL communicator (rank/world from the launcher env, unique id "
                          "over the native TCP plane, no torch.distributed; opt-in, exits non-zero if it cannot "
                          "be built)")
+    ap.add_argument("--engine", default=os.environ.get("DCNN_BENCH_ENGINE", "python"), choices=["python", "native"],
+                    help="python: the Python front end's captured step (default); native: the C++ host API trainer")
     ap.add_argument("--profile", action="store_true", help="print per-layer device times")
     ap.add_argument("--device", default="cuda")
     ap.add_argument("--dtype", default="bf16", choices=["bf16", "fp32"],
@@ -61,6 +107,8 @@ def main():
                          "halo convs ([hi|lo|hi] channels, ~2^-16 relative per product) + exact elsewhere; "
                          "split = 3xbf16 on the gathered GEMMs too")
     a = ap.parse_args()
+    if a.engine == "native":
+        return native_main(a)
 
     from dcnn_amd.parallel.dp import DataParallel, init_distributed
     from dcnn_amd.parallel.rccl import env_rank_world

@@ -4,10 +4,10 @@
 //   dcnn_amd/bin/tiny_imagenet_resnet18 [--device CPU|GPU] [--model resnet18_tiny_imagenet]
 //        [--data data/tiny-imagenet-200] [--epochs E] [--steps S] [--batch B] [--lr 1e-3]
 //        [--loss logsoftmax_ce] [--scheduler cosine_annealing_lr] [--max-per-class K]
-//        [--save model_snapshots/resnet18] [--bench [--eager]] [--dp]
+//        [--save model_snapshots/resnet18] [--bench [--eager] [--warmup W]] [--dp]
 //
 // Without --data it trains on a learnable synthetic 3x64x64 200-class set. --bench times
-// --steps training steps after 3 warm-up steps on two device-resident synthetic batches and
+// --steps training steps after --warmup (3) warm-up steps on two device-resident synthetic batches and
 // prints one JSON line (images/sec); on the GPU the step is captured into a hipGraph
 // (dcnn::TrainGraph) and replayed, --eager launches every kernel from the host instead. The saved
 // model (path.json + path.bin + path.bnstats) loads in Python with Sequential.from_file.
@@ -18,6 +18,7 @@
 // Honours the reference's .env keys DEVICE_TYPE / EPOCHS / BATCH_SIZE / LR_INITIAL.
 // Reference parity: examples/tiny_imagenet_resnet18.cpp:23-107 (Adam, logsoftmax-CE, profiling),
 // include/nn/example_models.hpp:306-331 (the model).
+#include <algorithm>
 #include <chrono>
 #include <functional>
 #include <cstdio>
@@ -42,7 +43,7 @@ std::string env_or(const char* k, const std::string& d) {
 int main(int argc, char** argv) {
   std::string device = env_or("DEVICE_TYPE", "CPU"), data, save, model_name = "resnet18_tiny_imagenet";
   std::string loss_name = "logsoftmax_ce", sched_name;
-  int epochs = std::atoi(env_or("EPOCHS", "1").c_str()), steps = -1, max_per_class = 0;
+  int epochs = std::atoi(env_or("EPOCHS", "1").c_str()), steps = -1, max_per_class = 0, warmup = 3;
   int batch = std::atoi(env_or("BATCH_SIZE", "64").c_str());
   float lr = std::atof(env_or("LR_INITIAL", "0.001").c_str());
   bool bench = false, eager = false, dp_on = false;
@@ -64,6 +65,7 @@ int main(int argc, char** argv) {
     else if (k == "--scheduler") sched_name = v;
     else if (k == "--max-per-class") max_per_class = std::atoi(v.c_str());
     else if (k == "--save") save = v;
+    else if (k == "--warmup") warmup = std::atoi(v.c_str());
   }
   try {
     Sequential model = create_model(model_name);
@@ -133,7 +135,7 @@ int main(int argc, char** argv) {
         opt.step(model.parameters());
         return r.loss;
       };
-      for (int i = 0; i < 3; ++i) one();
+      for (int i = 0; i < std::max(1, warmup); ++i) one();
       if (dev.is_gpu()) gpu::synchronize();
       const auto t0 = std::chrono::steady_clock::now();
       double last = 0;
