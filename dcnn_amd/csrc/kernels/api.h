@@ -83,6 +83,12 @@ void hconv_set_split_min_work(int w);  // least taps x 64-channel chunks per spl
 void bn_set_vectorised(int on);   // bf16 BatchNorm apply passes on the vectorised kernels (default on)
 bool hconv_supported(int NB, int H, int W, int Cs, int N, int ntaps);
 int hconv_stat_rows(int NB, int H, int W, int Cs, int N, int ntaps, int f32out);
+// exact fp32 on the persistent halo conv (hconv3.hip F32 instances): A / B fp32 through the pointer
+// fields, Cs fp32 input channels, ldb / tap_b in fp32 elements, output Cf (+ residual_f), statistics
+// / bias / ReLU as hconv; false = not covered (nothing launched). Split-K workspace as hconv with
+// hconv3_f32_splits (0: not covered); statistics rows = the tile count (hconv3_f32_tiles).
+bool hconv3_f32_try(const HConvArgs& a, hipStream_t s);
+int hconv3_f32_splits(int NB, int H, int W, int Cs, int N, int ntaps);
 bool hconv_v3(int NB, int H, int W, int Cs, int N, int ntaps);  // shape runs on hconv3
 void hconv3_enable(int on);
 void hconv3_set_grid_cap(int n);      // test hook: cap the persistent grid (0: resident workgroups)

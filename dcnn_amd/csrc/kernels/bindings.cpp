@@ -111,6 +111,25 @@ PYBIND11_MODULE(_kernels, m) {
           a.bias = P<const float*>(bias); a.residual = P<const bf16*>(residual); a.stats = P<float*>(stats); a.relu = relu;
           hconv(a, S(stream));
         });
+  m.def("hconv3_f32",
+        [](uintptr_t A, uintptr_t B, unsigned a_bytes, unsigned b_bytes, int NB, int H, int W, int Cs, int N, int ldb,
+           std::vector<std::array<int, 3>> taps, uintptr_t bias, uintptr_t stats, int relu, uintptr_t zero_ptr,
+           int zero_n, uintptr_t Cf, uintptr_t residual_f, int splits, uintptr_t part, uintptr_t tickets,
+           uintptr_t stream) {
+          HConvArgs a{};
+          a.splits = splits; a.part = P<float*>(part); a.tickets = P<unsigned*>(tickets);
+          a.Cf = P<float*>(Cf); a.residual_f = P<const float*>(residual_f);
+          a.zero_ptr = P<float*>(zero_ptr); a.zero_n = zero_n;
+          a.A = P<const bf16*>(A); a.B = P<const bf16*>(B);
+          a.a_bytes = a_bytes; a.b_bytes = b_bytes;
+          a.NB = NB; a.H = H; a.W = W; a.Cs = Cs; a.N = N; a.ldb = ldb;
+          if (taps.size() != 9) return false;
+          a.ntaps = 9;
+          for (size_t i = 0; i < taps.size(); ++i) { a.tap_dy[i] = taps[i][0]; a.tap_dx[i] = taps[i][1]; a.tap_b[i] = taps[i][2]; }
+          a.bias = P<const float*>(bias); a.stats = P<float*>(stats); a.relu = relu;
+          return hconv3_f32_try(a, S(stream));
+        });
+  m.def("hconv3_f32_splits", &hconv3_f32_splits);
   m.def("hconv_supported", &hconv_supported);
   m.def("hconv_stat_rows", &hconv_stat_rows);
   m.def("hconv_splits", &hconv_splits);

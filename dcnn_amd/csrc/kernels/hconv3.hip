@@ -34,6 +34,12 @@
 //    perm(l) and the chunk is XOR-swizzled by bit 2 of the halo pixel index, so every 16-lane
 //    ds_read_b128 group covers 16 distinct slots for any tap shift.
 //
+// fp32 instances (F32): IEEE fp32 operands on v_mfma_f32_16x16x4_f32 with the same LDS layout.
+// A 16-channel fp32 chunk is 64 bytes per pixel, exactly a 32-channel bf16 chunk, so the launcher
+// presents an fp32 tensor of C channels as a bf16 one of 2C (rows, taps, DMA pieces, swizzles and
+// the tile plan unchanged); each 16-byte fragment is then 4 fp32 channels feeding 4 MFMAs (k = 4),
+// the output and the residual are fp32 (HConvArgs::Cf / residual_f).
+//
 // Reference parity: the reference runs this GEMM as im2col + cuBLAS SGEMM or cuDNN
 // (src/nn/layers_impl/cuda/conv2d_ops.cu:18-128, cudnn_conv2d_ops.cu:187-244).
 #include <cstdio>
@@ -172,7 +178,7 @@ struct H3 {
 // backward-BatchNorm fusion (optional residual); 3 = forward statistics with bias / residual /
 // ReLU at run time.
 // STAMP: diagnostic instance with s_memtime stamps (benchmarks/hconv3_timeline.py).
-template <int NW, int WC, int TWC, int HN, int NWI, int PITCH, int EPI, bool STAMP>
+template <int NW, int WC, int TWC, int HN, int NWI, int PITCH, int EPI, bool STAMP, bool F32 = false>
 __global__ void __launch_bounds__(NW * 64, 8 / NW) hconv3_kernel(HConvArgs p, H3Geo g) {
   using T = H3<NW, WC, TWC, HN, NWI, PITCH>;
   constexpr int BN = T::BN, WP = T::WP;
@@ -350,7 +356,7 @@ __global__ void __launch_bounds__(NW * 64, 8 / NW) hconv3_kernel(HConvArgs p, H3
       const int iy = ty >> g.lIH, ix = tx >> g.lIW;  // (0, 0) unless gutter layout
       const unsigned pix = ((unsigned)(t.img0 + (iy << g.lGX) + ix) * p.H + t.y0 + ty - (iy << g.lIH)) * p.W + t.x0 +
                            tx - (ix << g.lIW);
-      oo[j] = (pix * (unsigned)p.N + t.n0 + wc * 64 + 8 * lh) * 2u;
+      oo[j] = (pix * (unsigned)p.N + t.n0 + wc * 64 + 8 * lh) * (F32 ? 4u : 2u);
     }
   };
 
@@ -370,10 +376,26 @@ __global__ void __launch_bounds__(NW * 64, 8 / NW) hconv3_kernel(HConvArgs p, H3
     };
     auto mm = [&](int dx, int i0, int i1) H3L {
       __builtin_amdgcn_s_setprio(1);
+      if constexpr (F32) {
+        // 4 fp32 channels per fragment lane: lane group lh holds channels 4 lh .. 4 lh + 3 of the
+        // chunk, MFMA m takes channel 4 lh + m as its k = lh (A and B alike), the 4 MFMAs of a tile
+        // are 16 independent MFMAs apart
 #pragma unroll
-      for (int i = i0; i < i1; ++i)
+        for (int m = 0; m < 4; ++m)
 #pragma unroll
-        for (int j = 0; j < 4; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[dx][i], b[dx][j], acc[i][j], 0, 0, 0);
+          for (int i = i0; i < i1; ++i)
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+              const f32x4 av = __builtin_bit_cast(f32x4, a[dx][i]), bv = __builtin_bit_cast(f32x4, b[dx][j]);
+              acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(av[m], bv[m], acc[i][j], 0, 0, 0);
+            }
+      } else {
+#pragma unroll
+        for (int i = i0; i < i1; ++i)
+#pragma unroll
+          for (int j = 0; j < 4; ++j)
+            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[dx][i], b[dx][j], acc[i][j], 0, 0, 0);
+      }
       __builtin_amdgcn_s_setprio(0);
     };
     pre();
@@ -562,6 +584,33 @@ __global__ void __launch_bounds__(NW * 64, 8 / NW) hconv3_kernel(HConvArgs p, H3
           mu[e] = has_x ? p.bnb.mean[cb + 32 * h + e] : 0.f;
           is[e] = has_x ? p.bnb.istd[cb + 32 * h + e] : 0.f;
         }
+        float gv[4][8], xh[4][8];  // [j][e]: stored value, and (bnb) stored value * xhat
+        if constexpr (F32) {
+          // fp32 output (+ fp32 residual): 32 bytes per lane and channel half
+          const char* rfb = reinterpret_cast<const char*>(p.residual_f);
+          char* cfb = reinterpret_cast<char*>(p.Cf);
+          const bool has_rf = p.residual_f != nullptr;
+#pragma unroll
+          for (int j = 0; j < 4; ++j) {
+            const unsigned o = oo[j] + h * 128;
+            float4 r0 = make_float4(0.f, 0.f, 0.f, 0.f), r1 = r0;
+            if (has_rf) {
+              r0 = *reinterpret_cast<const float4*>(rfb + o);
+              r1 = *reinterpret_cast<const float4*>(rfb + o + 16);
+            }
+            const float rf[8] = {r0.x, r0.y, r0.z, r0.w, r1.x, r1.y, r1.z, r1.w};
+#pragma unroll
+            for (int e = 0; e < 8; ++e) {
+              float f = acc[2 * h + (e >> 2)][j][e & 3] + bv[e];
+              if (has_rf) f += rf[e];
+              if (relu) f = fmaxf(f, 0.f);
+              gv[j][e] = f;
+              xh[j][e] = 0.f;
+            }
+            *reinterpret_cast<float4*>(cfb + o) = make_float4(gv[j][0], gv[j][1], gv[j][2], gv[j][3]);
+            *reinterpret_cast<float4*>(cfb + o + 16) = make_float4(gv[j][4], gv[j][5], gv[j][6], gv[j][7]);
+          }
+        } else {
         uint4 rr[4], yy[4], xx[4];
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
@@ -570,7 +619,6 @@ __global__ void __launch_bounds__(NW * 64, 8 / NW) hconv3_kernel(HConvArgs p, H3
           yy[j] = has_y ? *reinterpret_cast<const uint4*>(ybytes + o) : make_uint4(0u, 0u, 0u, 0u);
           xx[j] = has_x ? *reinterpret_cast<const uint4*>(xbytes + o) : make_uint4(0u, 0u, 0u, 0u);
         }
-        float gv[4][8], xh[4][8];  // [j][e]: stored value, and (bnb) stored value * xhat
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
           float f[8], rf[8], yf[8], xf[8];
@@ -589,6 +637,7 @@ __global__ void __launch_bounds__(NW * 64, 8 / NW) hconv3_kernel(HConvArgs p, H3
           unpack8(ov, gv[j]);  // statistics of the values actually stored
 #pragma unroll
           for (int e = 0; e < 8; ++e) xh[j][e] = has_x ? gv[j][e] * ((xf[e] - mu[e]) * is[e]) : 0.f;
+        }
         }
         if (stats) {
 #pragma unroll
@@ -700,10 +749,10 @@ bool hconv3_plan(int NB, int H, int W, int Cs, int N, int ntaps, H3Plan* pl) {
   return true;
 }
 
-template <int NW, int WC, int TWC, int HN, int NWI, int PITCH, int EPI, bool STAMP>
+template <int NW, int WC, int TWC, int HN, int NWI, int PITCH, int EPI, bool STAMP, bool F32 = false>
 static void launch_h3e(const HConvArgs& a, const H3Geo& g, hipStream_t s) {
   using T = H3<NW, WC, TWC, HN, NWI, PITCH>;
-  auto k = hconv3_kernel<NW, WC, TWC, HN, NWI, PITCH, EPI, STAMP>;
+  auto k = hconv3_kernel<NW, WC, TWC, HN, NWI, PITCH, EPI, STAMP, F32>;
   constexpr int lds = T::LDS;
   static int resident = 0;  // workgroups of this instance the device holds at once
   if (!resident) {
@@ -731,12 +780,18 @@ static void launch_h3e(const HConvArgs& a, const H3Geo& g, hipStream_t s) {
 static int h3_epi(const HConvArgs& a) {
   if (a.bnb.x) return (a.stats && !a.relu && !a.bias) ? 2 : -1;
   if (!a.stats) return 0;
-  return (a.residual || a.relu || a.bias) ? 3 : 1;
+  return (a.residual || a.residual_f || a.relu || a.bias) ? 3 : 1;
 }
 
 template <int NW, int WC, int TWC, int HN, int NWI, int PITCH>
 static void launch_h3(const HConvArgs& a, const H3Geo& g, hipStream_t s) {
   const int epi = h3_epi(a);
+  if (a.Cf) {  // fp32 operands (hconv3_f32_try): no backward-BN epilogue
+    if (epi == 1) return launch_h3e<NW, WC, TWC, HN, NWI, PITCH, 1, false, true>(a, g, s);
+    if (epi == 3) return launch_h3e<NW, WC, TWC, HN, NWI, PITCH, 3, false, true>(a, g, s);
+    if (epi == 0) return launch_h3e<NW, WC, TWC, HN, NWI, PITCH, 0, false, true>(a, g, s);
+    throw std::runtime_error("hconv3 fp32: no backward-BatchNorm epilogue");
+  }
   // (timeline instances: the statistics forward and the plain dgrad)
   if (g.stamps && epi == 1) return launch_h3e<NW, WC, TWC, HN, NWI, PITCH, 1, true>(a, g, s);
   if (g.stamps && epi == 0) return launch_h3e<NW, WC, TWC, HN, NWI, PITCH, 0, true>(a, g, s);
@@ -752,11 +807,35 @@ static void launch_h3_plan(const H3Plan& pl, const HConvArgs& a, const H3Geo& g,
   throw std::runtime_error("hconv3: no kernel instance for this plan");
 }
 
+static bool hconv3_run(const HConvArgs& a0, hipStream_t s);
+
 // returns false when the shape / taps / epilogue options are not covered (caller falls back)
 bool hconv3_try(const HConvArgs& a0, hipStream_t s) {
+  if (a0.Cf) return false;
+  return hconv3_run(a0, s);
+}
+
+// fp32 operands: A / B fp32 (passed through the bf16 pointer fields), Cs fp32 input channels,
+// ldb / tap_b in fp32 elements, output Cf (+ residual_f), no backward-BN fusion. Presented to the
+// plan as bf16 with 2 Cs channels (see the header comment).
+bool hconv3_f32_try(const HConvArgs& a0, hipStream_t s) {
+  if (!a0.Cf || a0.bnb.x || a0.residual) return false;
+  HConvArgs a = a0;
+  a.Cs = 2 * a0.Cs;
+  a.ldb = 2 * a0.ldb;
+  for (int t = 0; t < a.ntaps; ++t) a.tap_b[t] = 2 * a0.tap_b[t];
+  if ((long)a.NB * a.H * a.W * a.N * 4 >= 0x80000000l) return false;
+  return hconv3_run(a, s);
+}
+
+int hconv3_f32_splits(int NB, int H, int W, int Cs, int N, int ntaps) {
   H3Plan pl;
-  if (a0.Cf || h3_epi(a0) < 0 || !hconv3_plan(a0.NB, a0.H, a0.W, a0.Cs, a0.N, a0.ntaps, &pl))
-    return false;
+  return hconv3_plan(NB, H, W, 2 * Cs, N, ntaps, &pl) ? pl.splits : 0;
+}
+
+static bool hconv3_run(const HConvArgs& a0, hipStream_t s) {
+  H3Plan pl;
+  if (h3_epi(a0) < 0 || !hconv3_plan(a0.NB, a0.H, a0.W, a0.Cs, a0.N, a0.ntaps, &pl)) return false;
   H3Geo g{};
   for (int t = 0; t < 9; ++t) g.tb[t] = -1;
   for (int t = 0; t < a0.ntaps; ++t) {
@@ -766,7 +845,7 @@ bool hconv3_try(const HConvArgs& a0, hipStream_t s) {
   }
   for (int t = 0; t < 9; ++t)
     if (g.tb[t] < 0) return false;
-  const long c_bytes = (long)a0.NB * a0.H * a0.W * a0.N * 2;
+  const long c_bytes = (long)a0.NB * a0.H * a0.W * a0.N * (a0.Cf ? 4 : 2);
   if (a0.a_bytes >= 0x80000000u || a0.b_bytes >= 0x80000000u || c_bytes >= 0x80000000l) return false;
   HConvArgs a = a0;
   if (a.splits != pl.splits) throw std::runtime_error("hconv3: split count mismatch (use hconv_splits)");

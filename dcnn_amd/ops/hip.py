@@ -214,6 +214,10 @@ class _SplitWs:
 # the unsplit accumulation order, and an ill-conditioned batch-8 BatchNorm backward chain
 # (tests/test_gpu_model.py::test_fp32_gpu_model_matches_cpu) amplifies any order change ~300x
 _NOSPLIT = (1, 0, 0)
+# exact fp32 3x3 stride-1 convs and data gradients on the persistent halo conv's fp32 instances
+# (DCNN_H3_F32=0: the gathered f32 GEMM); launches counted for the tests
+_H3_F32 = os.environ.get("DCNN_H3_F32", "1") == "1"
+_H3_F32_STATS = {"fwd": 0, "dgrad": 0}
 
 
 def _hconv_split(K, NB, H, W, Cs, N, ntaps, device):
@@ -273,6 +277,20 @@ def conv2d_fwd(x, w, bias, stride, pad, *, stats=False, residual=None, relu=Fals
                 int(relu), ptr(sums), 2 * Co if stats else 0, _NOBNB, y.data_ptr(), ptr(residual),
                 *_NOSPLIT, stream_ptr())
         return y, ((slab, rows, sums) if stats else None)
+    if (x.dtype == F32 and _H3_F32 and (KH, KW, sh, sw, ph, pw) == (3, 3, 1, 1, 1, 1) and w.dim() == 4
+            and w.shape[1] == Ci):
+        # exact fp32 3x3 on the persistent halo conv (hconv3 F32 instances: v_mfma_f32_16x16x4_f32)
+        taps = [(t[0], t[1], t[3]) for t in _fwd_taps(Ci, W, KH, KW, ph, pw)]
+        if len(taps) == 9 and K.hconv3_f32_splits(N, H, W, Ci, Co, 9):
+            y = _empty((N, Co, OH, OW), F32, x.device, True)
+            rows = K.hconv_stat_rows(N, H, W, 2 * Ci, Co, 9, 0) if stats else 0
+            slab = _empty((rows, 3, Co), F32, x.device) if stats else None
+            sums = _empty((2 * Co,), F32, x.device) if stats else None  # zeroed in-kernel
+            if K.hconv3_f32(x.data_ptr(), w.data_ptr(), _nbytes(x), _nbytes(w), N, H, W, Ci, Co, KH * KW * Ci, taps,
+                            ptr(bias), ptr(slab), int(relu), ptr(sums), 2 * Co if stats else 0, y.data_ptr(),
+                            ptr(residual), *_hconv_split(K, N, H, W, 2 * Ci, Co, 9, x.device), stream_ptr()):
+                _H3_F32_STATS["fwd"] += 1
+                return y, ((slab, rows, sums) if stats else None)
     if x.dtype == F32:  # fp32 compute path: MFMA f32 16x16x4 gathered GEMM
         y = _empty((N, Co, OH, OW), F32, x.device, True)
         slab, rows, sums = None, 0, None
@@ -687,6 +705,14 @@ def conv2d_dgrad(dy, wt, x_shape, stride, pad, *, residual=None, bnb=None):
                 KH * KW * 3 * Co, [(t[0], t[1], 3 * t[3]) for t in classes[0][4]], 0, 0, 0, 0, 0, 0, _NOBNB,
                 dx.data_ptr(), ptr(residual), *_NOSPLIT, st)
         return dx
+    if (f32 and _H3_F32 and len(classes) == 1 and not empty_class and (KH, KW, sh, sw, ph, pw) == (3, 3, 1, 1, 1, 1)
+            and len(classes[0][4]) == 9 and K.hconv3_f32_splits(N, OH, OW, Co, Ci, 9)):
+        # exact fp32 data gradient on the persistent halo conv (transposed weights, reversed taps)
+        if K.hconv3_f32(dy.data_ptr(), wt.data_ptr(), _nbytes(dy), _nbytes(wt), N, OH, OW, Co, Ci, KH * KW * Co,
+                        [(t[0], t[1], t[3]) for t in classes[0][4]], 0, 0, 0, 0, 0, dx.data_ptr(), ptr(residual),
+                        *_hconv_split(K, N, OH, OW, 2 * Co, Ci, 9, dy.device), st):
+            _H3_F32_STATS["dgrad"] += 1
+            return dx
     g2 = K.gemm_g2f if f32 else K.gemm_g2
     fuse = (bnb is not None and _BNB and not bnb.pooled and not f32 and not empty_class and bnb.x.dtype == BF16
             and tuple(bnb.x.shape) == (N, Ci, H, W))

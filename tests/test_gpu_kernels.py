@@ -523,7 +523,10 @@ def test_dropout_regenerates_mask(hip):
 # ------------------------------------------------------------------ fp32 compute path (MFMA f32)
 F32_CASES = CONV_CASES + [(2, 3, 32, 32, 64, 3, 1, 1), (2, 6, 9, 9, 10, 3, 2, 1), (1, 5, 7, 7, 7, 1, 1, 0),
                           (4, 64, 16, 16, 64, 3, 1, 1), (2, 128, 8, 8, 64, 3, 1, 1), (8, 64, 4, 4, 128, 3, 1, 1),
-                          (2, 64, 32, 32, 128, 3, 1, 1)]
+                          (2, 64, 32, 32, 128, 3, 1, 1),
+                          # exact-fp32 halo conv: gutter layouts, split-K, a 16-channel input
+                          (16, 64, 8, 8, 128, 3, 1, 1), (16, 128, 4, 4, 64, 3, 1, 1), (4, 16, 16, 16, 64, 3, 1, 1),
+                          (64, 256, 8, 8, 256, 3, 1, 1)]
 
 
 @pytest.fixture(params=["exact", "split", "concat"], ids=["f32exact", "f32split", "f32concat"])
@@ -552,6 +555,7 @@ def test_conv_fp32_fwd_dgrad_wgrad(hip, case, f32mode):
     xg = x.cuda().contiguous(memory_format=CL)
     wg = w.cuda().contiguous(memory_format=CL)
     r = torch.randn(F.conv2d(x, w, None, s, p).shape)
+    h3 = dict(hip._H3_F32_STATS)
     y, partial = hip.conv2d_fwd(xg, wg, b.cuda(), (s, s), (p, p), stats=True,
                                 residual=r.cuda().contiguous(memory_format=CL), relu=True)
     y_ref = torch.relu(F.conv2d(x, w, b, s, p) + r)
@@ -559,6 +563,8 @@ def test_conv_fp32_fwd_dgrad_wgrad(hip, case, f32mode):
     concat = (f32mode == "concat" and Ci % 64 == 0 and Co % 64 == 0 and k == 3 and s == 1 and p == 1
               and hip.kernels().hconv_supported(N, H, W, 3 * Ci, Co, 9))
     assert hasattr(xg, "_s3") == concat  # the split-precision halo path ran exactly when eligible
+    h3_ok = (not concat and k == 3 and s == 1 and p == 1 and hip.kernels().hconv3_f32_splits(N, H, W, Ci, Co, 9) > 0)
+    assert (hip._H3_F32_STATS["fwd"] > h3["fwd"]) == h3_ok  # the exact fp32 halo conv ran exactly when eligible
     assert rel_err(y, y_ref) < 1e-5, rel_err(y, y_ref)
     stats = hip.bn_stats(y, partial)  # (mean, biased variance)
     assert rel_err(stats[:Co], y_ref.double().mean((0, 2, 3))) < 1e-5
