@@ -110,6 +110,11 @@ struct HWArgs {
 void hwgrad(HWArgs a, int splits, hipStream_t s);
 bool hwgrad_supported(int NB, int H, int W, int Cs, int Co, int ntaps);
 int hwgrad_splits(int NB, int H, int W, int Cs, int Co);
+// exact fp32 halo weight gradient (3x3 pad-1 stride-1): dY / X fp32 through HWArgs' pointer fields,
+// Cs / Co fp32 channels (multiples of 32), slab [splits][Co][9 Cs]
+bool hwgrad_f32_supported(int NB, int H, int W, int Cs, int Co);
+int hwgrad_f32_splits(int NB, int H, int W, int Cs, int Co);
+void hwgrad_f32(HWArgs a, int splits, hipStream_t s);
 void hwgrad_set_version(int v);  // 2: tap-shift-invariant kernel where it applies, 1: first kernel
 
 void gemm_nt(const NtArgs& a, hipStream_t s);

@@ -166,6 +166,20 @@ PYBIND11_MODULE(_kernels, m) {
           hwgrad(a, splits, S(stream));
         });
   m.def("hwgrad_supported", &hwgrad_supported);
+  m.def("hwgrad_f32",
+        [](uintptr_t dY, uintptr_t X, uintptr_t slab, uintptr_t bias_slab, unsigned dy_bytes, unsigned x_bytes, int NB,
+           int H, int W, int Cs, int Co, int splits, uintptr_t stream) {
+          HWArgs a{};
+          a.dY = P<const bf16*>(dY); a.X = P<const bf16*>(X); a.slab = P<float*>(slab);
+          a.bias_slab = P<float*>(bias_slab);
+          a.dy_bytes = dy_bytes; a.x_bytes = x_bytes;
+          a.NB = NB; a.H = H; a.W = W; a.Cs = Cs; a.Co = Co;
+          a.ntaps = 9;
+          for (int t = 0; t < 9; ++t) { a.tap_dy[t] = t / 3 - 1; a.tap_dx[t] = t % 3 - 1; }
+          hwgrad_f32(a, splits, S(stream));
+        });
+  m.def("hwgrad_f32_supported", &hwgrad_f32_supported);
+  m.def("hwgrad_f32_splits", &hwgrad_f32_splits);
   m.def("split3_bf16", [](uintptr_t in, uintptr_t out, long rows, int C, int pattern, uintptr_t st) {
     split3_bf16(P<const float*>(in), P<bf16*>(out), rows, C, pattern, S(st));
   });

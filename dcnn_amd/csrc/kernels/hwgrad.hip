@@ -285,6 +285,14 @@ struct HWGeo2 {
   // on those reads, accepted — the addressing savings are the same)
 };
 
+template <int K, int N, class F>
+__device__ __forceinline__ void h3w_static_for(F&& f) {
+  if constexpr (K < N) {
+    f(std::integral_constant<int, K>{});
+    h3w_static_for<K + 1, N>(f);
+  }
+}
+
 __device__ __forceinline__ bf16x4 tr4_at(const char* addr) {
   return __builtin_amdgcn_ds_read_tr16_b64_v4bf16((__attribute__((address_space(3))) bf16x4*)(const_cast<char*>(addr)));
 }
@@ -295,7 +303,14 @@ __device__ __forceinline__ bf16x4 tr4_at(const char* addr) {
 // wave per SIMD: every wait is exposed). TSP = 3: 12 waves, taps in thirds. The first four waves
 // issue the tile loads. Measured (batch 256): TSP 2 wgrad l1..l4 42.5/35.3/37.4/40.0 ->
 // 40.8/33.7/35.5/38.1 us, whole step 78.3k -> 80.0k img/s.
-template <int TW, int TH, int IMG, int NS, int TSP = 1>
+// F32: exact fp32 operands (hwgrad_f32). As in hconv3's fp32 instances, an fp32 row of C channels
+// is a bf16 row of 2C byte for byte, so the launcher passes 2 Co / 2 Cs / 2 ldy / 2 ldx and the
+// staging (DMA pieces, swizzle, halo rows) is the bf16 one; a workgroup then owns 32 (co) x 9 x
+// 32 (ci) fp32 outputs. The fragments are single fp32 values (ds_read_b32, no transposing read) for
+// v_mfma_f32_16x16x4_f32: wave w takes co half w >> 1 and ci half w & 1 (one 16x16 tile per tap),
+// MFMA k0 (of 4 per 16-pixel block) takes pixels k0 + 4 lh — 4 rows apart, so the two pixels of a
+// 32-lane read group sit in chunk-swizzle classes 4 apart and hit disjoint banks.
+template <int TW, int TH, int IMG, int NS, int TSP = 1, bool F32 = false>
 __global__ void __launch_bounds__(256 * TSP, 1) hwgrad2_kernel(HWArgs p) {
   using G = HWGeo2<TW, TH, IMG>;
   constexpr int HNI = G::HNI, HW2P = G::HW2P, HPIP = G::HPIP, HPP = G::HPP, TPX = G::TPX, STAGE = G::STAGE;
@@ -386,8 +401,129 @@ __global__ void __launch_bounds__(256 * TSP, 1) hwgrad2_kernel(HWArgs p) {
     }
   }
 
+  // F32 fragment bases: pixel (block b, MFMA k0, lane group lh) = 16 b + k0 + 4 lh; the block's
+  // rows are a compile-time offset (a multiple of 8 LDS rows: the swizzle is unchanged)
+  int fa[4], fb[4][3];
+  const int fco = 16 * (wid >> 1) + (lane & 15), fci = 16 * (wid & 1) + (lane & 15);  // fp32 columns
+  if constexpr (F32) {
+#pragma unroll
+    for (int k0 = 0; k0 < 4; ++k0) {
+      const int px = k0 + 4 * (lane >> 4);  // pixel within the 16-pixel block
+      fa[k0] = px * 128 + (((fco >> 2) ^ wswz2(px)) << 4) + (fco & 3) * 4;
+      // halo row of the block-0 pixel px at tap (dy, dx) = (-1, d - 1)
+      int hr0;
+      if constexpr (TW == 16) hr0 = HW2P + px + 1;                             // row 0 of the tile
+      else if constexpr (TW == 8) hr0 = ((px >> 3) + 1) * HW2P + (px & 7) + 1;  // rows 0-1
+      else hr0 = ((px >> 2) + 1) * HW2P + (px & 3) + 1;                         // TW 4: image 0, rows 0-3
+#pragma unroll
+      for (int d = 0; d < 3; ++d) {
+        const int row = hr0 + (d - 1) - HW2P;
+        fb[k0][d] = PT * 128 + row * 128 + (((fci >> 2) ^ wswz2(row)) << 4) + (fci & 3) * 4;
+      }
+    }
+  }
+  // halo-row offset of 16-pixel block b relative to block 0 (compile time)
+  auto blk_rows = [](int b) constexpr {
+    if (TW == 16) return b * HW2P;                                    // one image row per block
+    if (TW == 8) return (b / 4) * HPIP + (b % 4) * 2 * HW2P;         // 2 rows per block, 4 per image
+    return b * HPIP;                                                   // TW 4: one image per block
+  };
+
   // the tile loop and epilogue for taps TB .. TB + NTW - 1 (compile-time: register arrays indexed
   // by tap stay static)
+  auto run_f32 = [&](auto tb_c, auto ntw_c) {
+    constexpr int TB = decltype(tb_c)::value, NTW = decltype(ntw_c)::value;
+    f32x4 acc[NTW];
+#pragma unroll
+    for (int t = 0; t < NTW; ++t) acc[t] = f32x4{0.f, 0.f, 0.f, 0.f};
+    const bool do_bias = p.bias_slab != nullptr && c0 == 0 && th == 0;
+    float bias_acc = 0.f;
+    const int nt = tend - tbeg;
+    if (nt > 0) load_tile(0, tbeg);
+    if (NS == 3 && nt > 1) load_tile(1, tbeg + 1);
+    if (NS == 3 && nt > 1)
+      asm volatile("s_waitcnt vmcnt(%0)" ::"n"(INS) : "memory");
+    else
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    int cur = 0;
+    for (int it = 0; it < nt; ++it) {
+      if (it + NS - 1 < nt) load_tile(cur == 0 ? NS - 1 : cur - 1, tbeg + it + NS - 1);
+      const char* S0 = smem + cur * STAGE;
+      auto lds_f = [&](int off) { return *reinterpret_cast<const float*>(S0 + off); };
+      float a[2], b[2][NTW];
+      auto rd = [&](auto blk_c, int k0, int c) {
+        constexpr int B = decltype(blk_c)::value;
+        a[c] = lds_f(fa[k0] + B * 16 * 128);
+#pragma unroll
+        for (int t = 0; t < NTW; ++t) {
+          const int tt = TB + t, dy = tt / 3, dx = tt % 3;
+          b[c][t] = lds_f(fb[k0][dx] + (blk_rows(B) + dy * HW2P) * 128);
+        }
+      };
+      h3w_static_for<0, 8>([&](auto blk_c) {
+        constexpr int B = decltype(blk_c)::value;
+        rd(blk_c, 0, 0);
+#pragma unroll
+        for (int k0 = 0; k0 < 4; ++k0) {
+          const int c = k0 & 1;
+          if (k0 + 1 < 4) rd(blk_c, k0 + 1, c ^ 1);
+#pragma unroll
+          for (int t = 0; t < NTW; ++t) acc[t] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[c], b[c][t], acc[t], 0, 0, 0);
+        }
+        (void)B;
+      });
+      if (do_bias) {  // dY column sums: thread -> fp32 column tid & 31, rows (tid >> 5) + 8 r
+        const int col = tid & 31;
+        for (int r = tid >> 5; r < PT; r += 8)
+          bias_acc += *reinterpret_cast<const float*>(S0 + r * 128 + (((col >> 2) ^ wswz2(r)) << 4) + (col & 3) * 4);
+      }
+      if (NS == 3 && it + 2 < nt)
+        asm volatile("s_waitcnt vmcnt(%0)\n\ts_waitcnt lgkmcnt(0)\n\ts_barrier" ::"n"(INS) : "memory");
+      else
+        asm volatile("s_waitcnt vmcnt(0)\n\ts_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+      cur = cur == NS - 1 ? 0 : cur + 1;
+    }
+    // ---- slab[split][co][t * Cs + ci] in fp32 units (Co / Cs of the launcher are doubled)
+    const int Cs = p.Cs / 2, Co = p.Co / 2, cof = co0 / 2, cif = c0 / 2;
+    const long Ng = 9l * Cs;
+    const long slab_idx = (long)pair * nsplits + split;
+    float* out = p.slab + slab_idx * Co * Ng;
+    float* stg = reinterpret_cast<float*>(smem);
+    constexpr int ET = G::EPI_TAPS;
+#pragma unroll
+    for (int t0 = 0; t0 < 9; t0 += ET) {
+      __syncthreads();
+#pragma unroll
+      for (int u = 0; u < ET; ++u) {
+        const int tl = t0 + u - TB;
+        if (t0 + u < 9 && tl >= 0 && tl < NTW) {
+#pragma unroll
+          for (int r = 0; r < 4; ++r)
+            stg[(u * 32 + 16 * (wid >> 1) + (lane >> 4) * 4 + r) * 36 + 16 * (wid & 1) + (lane & 15)] = acc[tl][r];
+        }
+      }
+      __syncthreads();
+      const int nrows = (9 - t0 < ET ? 9 - t0 : ET) * 32;
+      for (int q = tid; q < nrows * 8; q += NT) {
+        const int row = q >> 3, c4 = (q & 7) * 4;
+        const int u = row >> 5, co = cof + (row & 31);
+        const float4 v = *reinterpret_cast<const float4*>(stg + row * 36 + c4);
+        *reinterpret_cast<float4*>(out + (long)co * Ng + (t0 + u) * Cs + cif + c4) = v;
+      }
+    }
+    if (p.bias_slab != nullptr && c0 == 0) {
+      __syncthreads();
+      if (tid < 256) stg[tid] = bias_acc;
+      __syncthreads();
+      if (tid < 32) {
+        float sum = 0.f;
+#pragma unroll
+        for (int gi = 0; gi < 8; ++gi) sum += stg[gi * 32 + tid];
+        p.bias_slab[slab_idx * Co + cof + tid] = p.pair_bias[pair] ? sum : 0.f;
+      }
+    }
+  };
   auto run = [&](auto tb_c, auto ntw_c) {
     constexpr int TB = decltype(tb_c)::value, NTW = decltype(ntw_c)::value;
     f32x4 acc[4][NTW];
@@ -494,7 +630,11 @@ __global__ void __launch_bounds__(256 * TSP, 1) hwgrad2_kernel(HWArgs p) {
     }
 
   };
-  if constexpr (TSP == 1) {
+  if constexpr (F32) {
+    static_assert(TSP == 2, "fp32: 8 waves");
+    if (th == 0) run_f32(std::integral_constant<int, 0>{}, std::integral_constant<int, 5>{});
+    else run_f32(std::integral_constant<int, 5>{}, std::integral_constant<int, 4>{});
+  } else if constexpr (TSP == 1) {
     run(std::integral_constant<int, 0>{}, std::integral_constant<int, 9>{});
   } else if constexpr (TSP == 2) {
     if (th == 0) run(std::integral_constant<int, 0>{}, std::integral_constant<int, 5>{});
@@ -617,6 +757,47 @@ void hwgrad(HWArgs a, int splits, hipStream_t s) {
   DCNN_HW(4, 4, 8, 2)
 #undef DCNN_HW
   throw std::runtime_error("hwgrad: no kernel for this geometry");
+}
+
+bool hwgrad_f32_supported(int NB, int H, int W, int Cs, int Co) {
+  int th, tw, img;
+  if (Cs % 32 || Co % 32) return false;
+  if (!hw_geometry(H, W, &th, &tw, &img) || NB % img) return false;
+  return (long)NB * H * W * (Cs > Co ? Cs : Co) * 4 < (1l << 31);
+}
+
+int hwgrad_f32_splits(int NB, int H, int W, int Cs, int Co) { return hwgrad_splits(NB, H, W, 2 * Cs, 2 * Co); }
+
+// exact fp32 weight gradient of a 3x3 / pad-1 stride-1 conv: dY / X fp32 through the bf16 pointer
+// fields, Cs / Co in fp32 channels, standard taps; slab [splits][Co][9 Cs] fp32 as hwgrad
+void hwgrad_f32(HWArgs a, int splits, hipStream_t s) {
+  if (!hwgrad_f32_supported(a.NB, a.H, a.W, a.Cs, a.Co) || a.ntaps != 9)
+    throw std::runtime_error("hwgrad_f32: unsupported shape");
+  for (int t = 0; t < 9; ++t)
+    if (a.tap_dy[t] != t / 3 - 1 || a.tap_dx[t] != t % 3 - 1) throw std::runtime_error("hwgrad_f32: 3x3 pad-1 taps only");
+  if (splits != hwgrad_f32_splits(a.NB, a.H, a.W, a.Cs, a.Co)) throw std::runtime_error("hwgrad_f32: split count mismatch");
+  // the bf16 view of the fp32 rows (see hwgrad2_kernel's F32 note)
+  a.Cs *= 2; a.Co *= 2;
+  a.npairs = 1; a.ldy = a.Co; a.ldx = a.Cs;
+  a.pair_yoff[0] = a.pair_xoff[0] = 0; a.pair_bias[0] = 1;
+  hw_geometry(a.H, a.W, &a.TH, &a.TW, &a.IMG);
+  const int total = (a.NB / a.IMG) * (a.H / a.TH) * (a.W / a.TW);
+  a.tiles_per_split = (total + splits - 1) / splits;
+  const int grid = splits * (a.Co / 64) * (a.Cs / 64);
+#define DCNN_HWF(TW_, TH_, IMG_, NS_)                                                                   \
+  if (a.TW == TW_ && a.TH == TH_ && a.IMG == IMG_) {                                                    \
+    auto k = hwgrad2_kernel<TW_, TH_, IMG_, NS_, 2, true>;                                              \
+    const int lds = NS_ * HWGeo2<TW_, TH_, IMG_>::STAGE;                                                \
+    DCNN_HIP_CHECK(hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, lds)); \
+    hipLaunchKernelGGL(k, dim3(grid, 1), dim3(512), lds, s, a);                                         \
+    DCNN_LAUNCH_CHECK();                                                                                \
+    return;                                                                                             \
+  }
+  DCNN_HWF(16, 8, 1, 3)
+  DCNN_HWF(8, 8, 2, 2)
+  DCNN_HWF(4, 4, 8, 2)
+#undef DCNN_HWF
+  throw std::runtime_error("hwgrad_f32: no kernel for this geometry");
 }
 
 }  // namespace dcnn

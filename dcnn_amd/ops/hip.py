@@ -217,7 +217,9 @@ _NOSPLIT = (1, 0, 0)
 # exact fp32 3x3 stride-1 convs and data gradients on the persistent halo conv's fp32 instances
 # (DCNN_H3_F32=0: the gathered f32 GEMM); launches counted for the tests
 _H3_F32 = os.environ.get("DCNN_H3_F32", "1") == "1"
-_H3_F32_STATS = {"fwd": 0, "dgrad": 0}
+# and their weight gradients on the halo wgrad's fp32 instances (DCNN_HW_F32=0: gemm_t2f)
+_HW_F32 = os.environ.get("DCNN_HW_F32", "1") == "1"
+_H3_F32_STATS = {"fwd": 0, "dgrad": 0, "wgrad": 0}
 
 
 def _hconv_split(K, NB, H, W, Cs, N, ntaps, device):
@@ -887,6 +889,17 @@ def conv2d_wgrad(dy, x, w_shape, stride, pad, grad_w, grad_b=None):
         K.hwgrad(dys.data_ptr(), xs.data_ptr(), slab.data_ptr(), ptr(bslab), _nbytes(dys), _nbytes(xs), N, H, W, Ci,
                  Co, taps, splits, 3 * Co, 3 * Ci, [(0, 0, 1), (0, Ci, 0), (Co, 0, 1)], st)
         _reduce_wb(K, slab, grad_w, Co * Ng, bslab, grad_b, Co, 3 * splits, st)
+        return
+    if (dy.dtype == F32 and _HW_F32 and Cx == Ci and (KH, KW, *stride, *pad) == (3, 3, 1, 1, 1, 1)
+            and (OH, OW) == (H, W) and K.hwgrad_f32_supported(N, H, W, Ci, Co)):
+        Ng = 9 * Ci
+        splits = K.hwgrad_f32_splits(N, H, W, Ci, Co)
+        slab = _empty((splits, Co, Ng), F32, x.device)
+        bslab = _empty((splits, Co), F32, x.device) if grad_b is not None else None
+        K.hwgrad_f32(dy.data_ptr(), x.data_ptr(), slab.data_ptr(), ptr(bslab), _nbytes(dy), _nbytes(x), N, H, W,
+                     Ci, Co, splits, st)
+        _H3_F32_STATS["wgrad"] += 1
+        _reduce_wb(K, slab, grad_w, Co * Ng, bslab, grad_b, Co, splits, st)
         return
     if dy.dtype == F32:
         assert x.dtype == F32 and Cx == Ci

@@ -526,7 +526,9 @@ F32_CASES = CONV_CASES + [(2, 3, 32, 32, 64, 3, 1, 1), (2, 6, 9, 9, 10, 3, 2, 1)
                           (2, 64, 32, 32, 128, 3, 1, 1),
                           # exact-fp32 halo conv: gutter layouts, split-K, a 16-channel input
                           (16, 64, 8, 8, 128, 3, 1, 1), (16, 128, 4, 4, 64, 3, 1, 1), (4, 16, 16, 16, 64, 3, 1, 1),
-                          (64, 256, 8, 8, 256, 3, 1, 1)]
+                          (64, 256, 8, 8, 256, 3, 1, 1),
+                          # exact-fp32 halo wgrad: 32-channel blocks (not 64-multiples)
+                          (4, 32, 16, 16, 96, 3, 1, 1), (8, 96, 4, 4, 32, 3, 1, 1)]
 
 
 @pytest.fixture(params=["exact", "split", "concat"], ids=["f32exact", "f32split", "f32concat"])
@@ -577,7 +579,10 @@ def test_conv_fp32_fwd_dgrad_wgrad(hip, case, f32mode):
     assert dx.dtype == torch.float32 and rel_err(dx, dx_ref) < 1e-5, rel_err(dx, dx_ref)
     gw = torch.ones(Co, Ci, k, k, device="cuda").contiguous(memory_format=CL)
     gb = torch.ones(Co, device="cuda")
+    h3 = dict(hip._H3_F32_STATS)
     hip.conv2d_wgrad(dyg, xg, w.shape, (s, s), (p, p), gw, gb)
+    hw_ok = not concat and k == 3 and s == 1 and p == 1 and hip.kernels().hwgrad_f32_supported(N, H, W, Ci, Co)
+    assert (hip._H3_F32_STATS["wgrad"] > h3["wgrad"]) == hw_ok  # the exact fp32 halo wgrad ran when eligible
     gw_ref = torch.nn.grad.conv2d_weight(x, w.shape, dy, s, p) + 1
     assert rel_err(gw, gw_ref) < 1e-5, rel_err(gw, gw_ref)
     assert rel_err(gb, dy.sum((0, 2, 3)) + 1) < 1e-5

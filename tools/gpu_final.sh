@@ -5,7 +5,7 @@
 TAG=${1:-final}
 cd "$GRAFT_REPO_ROOT"; mkdir -p gpurun_out; export TMPDIR=/tmp
 ok() { case $1 in 0|1) return 0;; *) return 1;; esac; }
-timeout -k 10 600 python -u -m pytest tests -m gpu -q -rf --timeout 300 --timeout-method thread -p no:cacheprovider > gpurun_out/t_$TAG.log 2>&1; rc=$?
+timeout -k 10 1000 python -u -m pytest tests -m gpu -q -rf --timeout 300 --timeout-method thread -p no:cacheprovider > gpurun_out/t_$TAG.log 2>&1; rc=$?
 echo "pytest rc=$rc" >> gpurun_out/t_$TAG.log; ok $rc || exit $rc
 timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/smoke_$TAG.log 2>&1 || exit $?
 timeout -k 10 300 python bench.py > gpurun_out/bench_$TAG.log 2>&1 || exit $?
