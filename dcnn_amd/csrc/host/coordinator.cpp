@@ -141,6 +141,11 @@ PipelineCoordinator::PipelineCoordinator(json::Value model_config, json::Value o
   if (o_.num_microbatches <= 0) throw std::invalid_argument("PipelineCoordinator: num_microbatches must be > 0");
   if (o_.stage_devices.empty()) o_.stage_devices.assign(stages_.size(), "CPU");
   if (o_.stage_devices.size() != stages_.size()) throw std::invalid_argument("one device per stage required");
+  if (o_.transport == "rccl")  // (RCCL refuses two ranks of one communicator on one device)
+    for (size_t i = 0; i + 1 < stages_.size(); ++i)
+      if (o_.stage_devices[i].rfind("GPU", 0) != 0 || o_.stage_devices[i] == o_.stage_devices[i + 1])
+        throw std::invalid_argument("transport 'rccl': adjacent stages need distinct GPUs (" + o_.stage_devices[i] +
+                                    ", " + o_.stage_devices[i + 1] + ")");
 }
 
 PipelineCoordinator::~PipelineCoordinator() {
@@ -222,6 +227,11 @@ void PipelineCoordinator::deploy_stages() {
   for (const auto& s : names_) last_beat_[s] = now;
   sent_lr_ = lr_.learning_rate();
   enable_stage_loss();
+  if (o_.transport == "rccl" && num_stages() > 1) {
+    // every stage is configured: open the stage-pair RCCL links (the stages chain their joins)
+    broadcast(P2P_CONNECT);
+    join(P2P_CONNECT, (size_t)num_stages());
+  }
 }
 
 void PipelineCoordinator::send_f64(const std::string& to, uint16_t cmd, uint64_t mb, const std::vector<double>& v) {

@@ -10,8 +10,11 @@
 // Reference parity: the reference has no data parallelism (SURVEY §2.13 maps DP over RCCL to
 // MI355X as an addition); the Python front end's counterpart is parallel/dp.py.
 #pragma once
+#include <cstdint>
+#include <map>
 #include <memory>
 #include <string>
+#include <vector>
 
 #include "tensor.hpp"
 
@@ -48,6 +51,51 @@ class DataParallel {
   Env env_;
   std::unique_ptr<coll::Comm> comm_;
   Tensor scratch_;
+};
+
+// One direction of a stage-to-stage device data plane (the native pipeline's transport "rccl",
+// dcnn/pipeline.hpp): a two-rank RCCL communicator (rank 0 = the lower stage) that carries one
+// kind of tensor one way — activations down or gradients up — on a flow of its own, so a send
+// waiting for its receiver never sits in front of the opposite direction's traffic or of compute.
+// Hand-offs are event-ordered on the device: a send starts after the work the calling thread's
+// flow holds so far; the flow that asks for a receive waits for it. No host synchronisation per
+// tensor (the IPC transport copies and waits on the host).
+//
+// Reference parity: the reference moves activations as host fp32 over TCP
+// (include/pipeline/tcp_communicator.hpp:190,455); the Python front end's counterpart of this
+// plane is parallel/rccl.py's RcclP2P (one communicator and one stream per direction).
+class P2PLink {
+ public:
+  // blocks until the peer has joined with the same id (rank 0 / 1 of the pair)
+  P2PLink(const std::string& unique_id, int rank, bool sender, int device);
+  ~P2PLink();
+  P2PLink(const P2PLink&) = delete;
+  P2PLink& operator=(const P2PLink&) = delete;
+  bool sender() const { return sender_; }
+  // t's bytes to the peer after the current flow's work so far; t stays referenced (slot `key`,
+  // e.g. the micro-batch) until that send has completed
+  void send(const Tensor& t, uint64_t key);
+  // a fresh device tensor filled by the peer's next send; the current flow waits for it
+  Tensor recv(const std::vector<int64_t>& shape, DType dt, Layout layout, Device dev);
+  // host: every send so far has completed (its peer posted the receive); slots released
+  void drain();
+  // world-1 self loop of the same code path (tests): t's bytes through a one-rank communicator's
+  // send + receive pair (one group) into a fresh tensor, ordered like send() / recv()
+  static Tensor loopback(const Tensor& t);
+
+ private:
+  P2PLink() = default;
+  void* flow_ = nullptr;   // gpu::Flow
+  void* ready_ = nullptr;  // gpu::Event: the caller's flow reached the hand-off
+  void* done_ = nullptr;   // gpu::Event: the last transfer on the link flow
+  std::unique_ptr<coll::Comm> comm_;
+  bool sender_ = false;
+  int peer_ = 0;
+  struct Held {
+    Tensor t;
+    void* ev = nullptr;  // gpu::Event recorded after its send
+  };
+  std::map<uint64_t, Held> held_;
 };
 
 }  // namespace dist

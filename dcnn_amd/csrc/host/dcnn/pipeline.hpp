@@ -37,6 +37,9 @@ class Communicator;
 }  // namespace dcnn_native
 
 namespace dcnn {
+namespace dist {
+class P2PLink;
+}
 
 struct Endpoint {
   std::string communication_type = "tcp";  // "tcp" | "in_process"
@@ -162,6 +165,14 @@ class PipelineStage {
   std::vector<void*> ipc_retired_;                  // outgrown exports (a peer may still map them)
   mutable std::map<std::string, void*> ipc_in_;     // handle -> this process's mapping
   void release_ipc();
+  // transport "rccl" (GPU stages on distinct devices, any node): stage-to-stage tensors as RCCL
+  // sends on per-direction two-rank links (dist::P2PLink); the job message carries only the shape.
+  // Opened on the coordinator's P2P_CONNECT (after every stage is configured): a stage sends its
+  // next stage the pair's two unique ids, joins its previous stage's links, then its next stage's.
+  std::unique_ptr<dist::P2PLink> act_out_, act_in_, grad_out_, grad_in_;
+  std::string prev_ids_;  // the previous stage's ids, when they arrive before the coordinator's request
+  void connect_links(dcnn_native::Message& m);
+  void release_links();
   long n_fwd_ = 0, n_bwd_ = 0, n_upd_ = 0;
   double fwd_ms_ = 0, bwd_ms_ = 0;
   std::thread beat_;
@@ -199,7 +210,9 @@ struct CoordinatorOptions {
   std::vector<std::string> stage_devices;  // per stage ("CPU", "GPU:0", ...); default CPU
   std::string loss = "softmax_crossentropy";
   std::string codec = "none";               // inline payload compression of the stages' sends
-  std::string transport = "message";        // "ipc": GPU stage-to-stage tensors via device IPC buffers
+  // "ipc": GPU stage-to-stage tensors via device IPC buffers (one node); "rccl": as RCCL sends over
+  // per-direction stage-pair links (native GPU stages on distinct devices)
+  std::string transport = "message";
   bool grad_scale_mean = true;              // micro-batch gradients * 1 / num_microbatches
   double timeout_s = 120.0;
   double heartbeat_s = 0.0;                 // > 0: stages beat every heartbeat_s ...

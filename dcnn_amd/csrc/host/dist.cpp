@@ -133,5 +133,83 @@ double DataParallel::max(double v) {
   return f;
 }
 
+P2PLink::P2PLink(const std::string& unique_id, int rank, bool sender, int device) : sender_(sender) {
+  if (!coll::available()) throw std::runtime_error("dist: RCCL unavailable: " + coll::load_error());
+  if (rank != 0 && rank != 1) throw std::invalid_argument("P2PLink: rank 0 or 1");
+  gpu::set_device(device);
+  peer_ = 1 - rank;
+  comm_ = std::make_unique<coll::Comm>(unique_id, 2, rank, device);
+  flow_ = gpu::flow_create();
+  ready_ = gpu::event_create();
+  done_ = gpu::event_create();
+}
+
+P2PLink::~P2PLink() {
+  try {
+    drain();
+  } catch (...) {
+  }
+  for (auto& kv : held_)
+    if (kv.second.ev) gpu::event_destroy(kv.second.ev);
+  if (ready_) gpu::event_destroy(ready_);
+  if (done_) gpu::event_destroy(done_);
+  comm_.reset();
+  if (flow_) gpu::flow_destroy(flow_);
+}
+
+void P2PLink::send(const Tensor& t, uint64_t key) {
+  if (!sender_) throw std::logic_error("P2PLink: receive-only link");
+  if (!t.device().is_gpu()) throw std::invalid_argument("P2PLink: device tensors only");
+  Held& h = held_[key];
+  if (h.ev) gpu::event_synchronize(h.ev);  // the slot's previous send has completed
+  else h.ev = gpu::event_create();
+  gpu::event_record(ready_);  // (current flow)
+  gpu::flow_wait(flow_, ready_);
+  comm_->send(t.data(), t.nbytes(), 4, peer_, flow_);  // bytes (uint8)
+  gpu::event_record(h.ev, flow_);
+  h.t = t;
+}
+
+Tensor P2PLink::recv(const std::vector<int64_t>& shape, DType dt, Layout layout, Device dev) {
+  if (sender_) throw std::logic_error("P2PLink: send-only link");
+  // the buffer comes from the current flow's cache: the link flow starts after that flow's work
+  // so far (a recycled block's last reader), and the current flow continues after the receive
+  Tensor t = Tensor::empty(shape, dt, dev, layout);
+  gpu::event_record(ready_);
+  gpu::flow_wait(flow_, ready_);
+  comm_->recv(t.data(), t.nbytes(), 4, peer_, flow_);
+  gpu::event_record(done_, flow_);
+  gpu::flow_wait(gpu::flow(), done_);
+  return t;
+}
+
+void P2PLink::drain() {
+  for (auto& kv : held_) {
+    if (kv.second.ev) gpu::event_synchronize(kv.second.ev);
+    kv.second.t = Tensor();
+  }
+}
+
+Tensor P2PLink::loopback(const Tensor& t) {
+  if (!coll::available()) throw std::runtime_error("dist: RCCL unavailable: " + coll::load_error());
+  if (!t.device().is_gpu()) throw std::invalid_argument("P2PLink: device tensors only");
+  P2PLink l;
+  l.comm_ = std::make_unique<coll::Comm>(coll::unique_id(), 1, 0, t.device().index);
+  l.flow_ = gpu::flow_create();
+  l.ready_ = gpu::event_create();
+  l.done_ = gpu::event_create();
+  Tensor out = Tensor::empty(t.shape(), t.dtype(), t.device(), t.layout());
+  gpu::event_record(l.ready_);
+  gpu::flow_wait(l.flow_, l.ready_);
+  coll::group_start();  // (a rank's send to itself and its receive must be one group)
+  l.comm_->send(t.data(), t.nbytes(), 4, 0, l.flow_);
+  l.comm_->recv(out.data(), out.nbytes(), 4, 0, l.flow_);
+  coll::group_end();
+  gpu::event_record(l.done_, l.flow_);
+  gpu::flow_wait(gpu::flow(), l.done_);
+  gpu::flow_synchronize(l.flow_);  // (the link and its flow go away here)
+  return out;
+}
+
 }  // namespace dist
 }  // namespace dcnn

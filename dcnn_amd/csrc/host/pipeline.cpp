@@ -1,5 +1,6 @@
 // Native pipeline stage (dcnn/pipeline.hpp): configuration, tensor payloads, the command handlers.
 #include "dcnn/pipeline.hpp"
+#include "dcnn/dist.hpp"
 #include "dcnn/ops.hpp"
 
 #include <unistd.h>
@@ -12,6 +13,7 @@
 #include <sstream>
 #include <stdexcept>
 
+#include "../kernels/collective.h"
 #include "../native/comm.h"
 
 using namespace dcnn_native;
@@ -24,6 +26,10 @@ constexpr uint8_t kChannelsLast = 0x10;  // dtype flag: NHWC physical buffer of 
 // (transport "ipc", native stages only)
 constexpr uint8_t kIpcRef = 0x20;
 constexpr size_t kIpcRefBytes = gpu::kIpcHandleBytes + sizeof(uint64_t);
+// dtype flag: the tensor travels on the stage pair's RCCL link; the payload is empty (transport
+// "rccl", native stages only)
+constexpr uint8_t kRcclRef = 0x40;
+constexpr size_t kIdBytes = 128;  // ncclUniqueId
 constexpr uint64_t kFullState = 1;        // SEND_PARAMS "full" / LOAD_PARAMS micro-batch id
 
 std::optional<Endpoint> parse_endpoint(const json::Value* v) {
@@ -116,9 +122,63 @@ PipelineStage::PipelineStage(Communicator* comm, bool verbose) : comm_(comm), ve
 PipelineStage::~PipelineStage() {
   stop_heartbeat();
   try {
+    release_links();
     release_ipc();
   } catch (...) {
   }
+}
+
+void PipelineStage::release_links() {
+  act_out_.reset();
+  act_in_.reset();
+  grad_out_.reset();
+  grad_in_.reset();
+}
+
+void PipelineStage::connect_links(Message& m) {
+  if (m.payload_type == P_TYPED_JOB) {  // the previous stage's ids, ahead of the coordinator's request
+    if (m.data.size() != 2 * kIdBytes) throw std::runtime_error("P2P_CONNECT: malformed unique ids");
+    prev_ids_ = m.data;
+    return;
+  }
+  if (cfg_.transport != "rccl") throw std::runtime_error("P2P_CONNECT: the stage transport is '" + cfg_.transport + "'");
+  release_links();
+  const int dev = dev_.index;
+  const bool has_prev = cfg_.stage_index > 0, has_next = cfg_.stage_index < cfg_.num_stages - 1;
+  std::string next_ids;
+  if (has_next) {
+    next_ids = coll::unique_id() + coll::unique_id();  // activations down, gradients up
+    Message u;
+    u.recipient = "next_stage";
+    u.command = P2P_CONNECT;
+    u.payload_type = P_TYPED_JOB;
+    u.dtype = 4;  // u8
+    u.shape = {(uint64_t)next_ids.size()};
+    u.data = next_ids;
+    comm_->send(std::move(u));
+  }
+  // the previous pair first, then the next: stage i's next pair is stage i + 1's previous pair,
+  // so the blocking joins chain from the first stage down without a cycle
+  if (has_prev) {
+    const auto t0 = std::chrono::steady_clock::now();
+    while (prev_ids_.empty()) {
+      Message q;
+      if (comm_->queue().pop_command(P2P_CONNECT, q, 50)) {
+        if (q.payload_type != P_TYPED_JOB) throw std::runtime_error("P2P_CONNECT: second request before the links opened");
+        connect_links(q);
+      } else if (std::chrono::steady_clock::now() - t0 > std::chrono::seconds(120)) {
+        throw std::runtime_error("P2P_CONNECT: no unique ids from the previous stage");
+      }
+    }
+    act_in_ = std::make_unique<dist::P2PLink>(prev_ids_.substr(0, kIdBytes), 1, false, dev);
+    grad_out_ = std::make_unique<dist::P2PLink>(prev_ids_.substr(kIdBytes), 1, true, dev);
+    prev_ids_.clear();
+  }
+  if (has_next) {
+    act_out_ = std::make_unique<dist::P2PLink>(next_ids.substr(0, kIdBytes), 0, true, dev);
+    grad_in_ = std::make_unique<dist::P2PLink>(next_ids.substr(kIdBytes), 0, false, dev);
+  }
+  reply(P2P_CONNECT, "ok");
 }
 
 void PipelineStage::release_ipc() {
@@ -162,11 +222,15 @@ void PipelineStage::process(Message& m) {
       case FORWARD_JOB: forward(m); break;
       case BACKWARD_JOB: backward(m); break;
       case LABELS_TRANSFER: take_labels(m); break;
+      case P2P_CONNECT: connect_links(m); break;
       case UPDATE_PARAMETERS: {
         if (m.payload_type == P_STRING && !m.text.empty()) {
           const json::Value hp = json::Value::parse(m.text);
           if (hp.has("learning_rate")) opt_->set_learning_rate((float)hp.at("learning_rate").as_number());
         }
+        // every micro-batch's sends have their receives posted by now: release their slots
+        if (act_out_) act_out_->drain();
+        if (grad_out_) grad_out_->drain();
         opt_->step(model_->parameters());
         model_->zero_grad();
         ++n_upd_;
@@ -287,11 +351,14 @@ void PipelineStage::process(Message& m) {
 
 void PipelineStage::configure(const std::string& text) {
   cfg_ = StageConfig::parse(text);
-  if (cfg_.transport != "message" && cfg_.transport != "ipc")
-    throw std::runtime_error("native stage: transport '" + cfg_.transport + "' not supported ('message' | 'ipc')");
+  if (cfg_.transport != "message" && cfg_.transport != "ipc" && cfg_.transport != "rccl")
+    throw std::runtime_error("native stage: transport '" + cfg_.transport + "' not supported ('message' | 'ipc' | 'rccl')");
   stop_heartbeat();
   dev_ = Device::parse(cfg_.device);
-  if (cfg_.transport == "ipc" && !dev_.is_gpu()) throw std::runtime_error("native stage: transport 'ipc' needs a GPU stage");
+  if (cfg_.transport != "message" && !dev_.is_gpu())
+    throw std::runtime_error("native stage: transport '" + cfg_.transport + "' needs a GPU stage");
+  release_links();
+  prev_ids_.clear();
   release_ipc();  // (a redeploy may change the neighbours)
   drop_all_graphs();  // (they hold the previous model's buffers)
   if (dev_.is_gpu()) gpu::set_device(dev_.index);
@@ -359,6 +426,14 @@ Tensor PipelineStage::decode(Message& m) const {
     case 1: dt = DType::BF16; break;
     default: throw std::runtime_error("activation payloads must be fp32 or bf16");
   }
+  if (code & kRcclRef) {
+    // the peer's send on this pair's link (sent before the message; RCCL matches in order)
+    dist::P2PLink* l = m.command == FORWARD_JOB ? act_in_.get() : m.command == BACKWARD_JOB ? grad_in_.get() : nullptr;
+    if (l == nullptr || !dev_.is_gpu()) throw std::runtime_error("RCCL tensor reference without an open link");
+    Tensor t = l->recv(shape, dt, layout, dev_);
+    if (t.rank() == 2) t = t.view({shape[0], shape[1], 1, 1}, Layout::NCHW);
+    return t;
+  }
   if (code & kIpcRef) {
     // a peer stage's device buffer: map it once, copy out now (the sender rewrites it only after
     // this stage has answered for the micro-batch)
@@ -406,6 +481,14 @@ void PipelineStage::send_tensor(const std::string& to, uint16_t cmd, uint64_t mb
       for (auto d : s) m.shape.push_back((uint64_t)d);
     }
     m.dtype = code;
+    if (cfg_.transport == "rccl" && t.device().is_gpu() && (to == "next_stage" || to == "prev_stage")) {
+      dist::P2PLink* l = to == "next_stage" ? act_out_.get() : grad_out_.get();
+      if (l == nullptr) throw std::runtime_error("transport 'rccl': the stage links are not open (P2P_CONNECT)");
+      l->send(t, mb);
+      m.dtype = code | kRcclRef;
+      comm_->send(std::move(m));
+      return;
+    }
     if (cfg_.transport == "ipc" && t.device().is_gpu() && (to == "next_stage" || to == "prev_stage")) {
       IpcSlot& slot = ipc_out_[{to, mb}];
       if (slot.bytes < t.nbytes()) {

@@ -27,7 +27,8 @@ static const char* kNames[] = {
     "CONFIG_TRANSFER", "CONFIG_RECEIVED", "LOAD_PARAMS", "PARAMS_LOADED", "SEND_PARAMS", "PARAMS_TRANSFER",
     "STATUS_REQUEST", "STATUS_RESPONSE", "PARAMETERS_UPDATED", "HEALTH_CHECK", "ERROR_REPORT", "JOB_FAILURE",
     "BARRIER_SYNC", "CHECKPOINT_REQUEST", "CHECKPOINT_COMPLETE", "UPDATE_LOAD", "REPORT_LOAD", "LOAD_REPORT",
-    "PRINT_PROFILING", "PROFILING_PRINTED", "CLEAR_PROFILING", "PROFILING_CLEARED", "LABELS_TRANSFER"};
+    "PRINT_PROFILING", "PROFILING_PRINTED", "CLEAR_PROFILING", "PROFILING_CLEARED", "LABELS_TRANSFER",
+    "P2P_CONNECT"};
 static_assert(sizeof(kNames) / sizeof(kNames[0]) == CMD_COUNT, "command table");
 
 const char* command_name(uint16_t c) { return c < CMD_COUNT ? kNames[c] : "UNKNOWN"; }

@@ -40,6 +40,10 @@ enum Command : uint16_t {
   // stage, f64 payload [kind, param, gradient scale] with micro-batch id kLossConfig = enable (the
   // stage answers with this command), else [label...] of that micro-batch
   LABELS_TRANSFER,
+  // native extension (transport "rccl"): coordinator -> every stage = open the stage-to-stage RCCL
+  // links (each stage answers with this command when its links are up); stage -> next stage = the
+  // two 128-byte unique ids of that pair's links (u8 payload: activations down, gradients up)
+  P2P_CONNECT,
   CMD_COUNT
 };
 const char* command_name(uint16_t c);

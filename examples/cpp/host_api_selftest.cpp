@@ -8,6 +8,7 @@
 #include <sstream>
 #include <string>
 
+#include "dcnn/dist.hpp"
 #include "dcnn/nn.hpp"
 
 using namespace dcnn;
@@ -201,6 +202,32 @@ static void test_gpu_vs_cpu() {
   }
 }
 
+// the native pipeline's RCCL stage link (transport "rccl") at world size 1: a GPU-produced bf16
+// NHWC activation through a one-rank communicator's send / receive on the link's own flow, read
+// back on the caller's flow (event ordering both ways), then a second round trip of another size
+static void test_p2p_loopback() {
+  Sequential g = smooth_model();
+  g.set_device(Device::gpu(0));
+  g.initialize(3);
+  SyntheticClassification src(16, 8, 8, 8, 10, 3, 1.0f);
+  src.reset(0);
+  Tensor x, y;
+  src.next(16, x, y);
+  const Tensor a = g.forward(x);  // produced on the caller's flow just before the hand-off
+  const Tensor b = dist::P2PLink::loopback(a);
+  CHECK(b.shape() == a.shape() && b.dtype() == a.dtype() && b.layout() == a.layout());
+  const auto ha = a.to_host_f32(), hb = b.to_host_f32();
+  size_t diff = 0;
+  for (size_t i = 0; i < ha.size(); ++i) diff += ha[i] != hb[i];
+  CHECK(diff == 0);
+  std::vector<float> v(3 * 5 * 7 * 11);
+  for (size_t i = 0; i < v.size(); ++i) v[i] = (float)i * 0.25f - 100.f;
+  const Tensor c = Tensor::from_host(v, {3, 5, 7, 11}, Device::gpu(0), DType::F32);
+  const auto hc = dist::P2PLink::loopback(c).to_host_f32();
+  CHECK(hc == v);
+  std::printf("p2p loopback ok (%zu + %zu values, %zu differ)\n", ha.size(), v.size(), diff);
+}
+
 int main(int argc, char** argv) {
   const bool gpu = argc > 2 && std::string(argv[1]) == "--device" && std::string(argv[2]) == "GPU";
   try {
@@ -210,6 +237,7 @@ int main(int argc, char** argv) {
     test_gradcheck(false);
     test_gradcheck(true);
     if (gpu) test_gpu_vs_cpu();
+    if (gpu) test_p2p_loopback();
   } catch (const std::exception& e) {
     std::fprintf(stderr, "exception: %s\n", e.what());
     return 1;

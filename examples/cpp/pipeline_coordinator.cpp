@@ -7,7 +7,7 @@
 //        [--microbatches 4] [--batch 64] [--steps 20] [--optimizer adam|sgd] [--lr 1e-3]
 //        [--momentum 0.9] [--devices CPU,CPU | --device GPU:0] [--loss softmax_crossentropy]
 //        [--data-x x.f32 --data-y y.i64] [--input C,H,W] [--classes K] [--save out]
-//        [--heartbeat S] [--transport message|ipc] [--stage-loss auto|0|1] [--partitioner naive|flops]
+//        [--heartbeat S] [--transport message|ipc|rccl] [--stage-loss auto|0|1] [--partitioner naive|flops]
 //        [--json] [--bench W]
 //
 // --spawn N starts N local native workers (this program never touches the GPU itself, so starting
@@ -16,7 +16,9 @@
 // batch; without them a learnable synthetic set of --input / --classes is used. --json prints one
 // JSON line per step; --bench W times the steps after W untimed warm-up steps (images/sec).
 // --transport ipc (GPU stages on one node): stage-to-stage activations and gradients stay on the
-// device (HIP IPC buffers); only their handles travel in the messages. --stage-loss: the loss on
+// device (HIP IPC buffers); only their handles travel in the messages. --transport rccl (GPU stages
+// on distinct devices, one node or several): they travel as RCCL sends on per-direction stage-pair
+// links, the messages carry only their shapes. --stage-loss: the loss on
 // the last stage's GPU (auto: when that stage is a native GPU stage) — the labels go there, only
 // the loss value comes back, and the backward starts without a round trip through this process.
 // Reference parity: examples/semi_async_pipeline_coordinator.cpp, sync_pipeline_coordinator.cpp,

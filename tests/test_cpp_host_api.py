@@ -102,6 +102,7 @@ def test_selftest_gpu_matches_cpu_backend(host_bins, tmp_path):
     rc, out = _run([host_bins["host_api_selftest"], "--device", "GPU"], tmp_path, timeout=300)
     assert rc == 0, out
     assert "gpu vs cpu loss" in out
+    assert "p2p loopback ok" in out  # the native pipeline's RCCL stage link, world size 1
 
 
 @pytest.mark.gpu

@@ -247,6 +247,15 @@ def test_native_ipc_transport_needs_gpu_stages(worker_bin):
     assert out.returncode == 1 and "needs a GPU stage" in out.stderr
 
 
+def test_native_rccl_transport_needs_distinct_gpus(worker_bin):
+    """transport "rccl" pairs adjacent stages in two-rank RCCL communicators: CPU stages, or two
+    stages on one GPU (RCCL refuses both ranks on one device), are rejected before any stage runs."""
+    for devices in ("CPU,CPU", "GPU:0,GPU:0"):
+        out = subprocess.run([COORD, "--spawn", "2", "--steps", "1", "--transport", "rccl", "--devices", devices],
+                             capture_output=True, text=True, timeout=60)
+        assert out.returncode == 1 and "adjacent stages need distinct GPUs" in out.stderr, out.stderr
+
+
 def test_native_coordinator_rejects_bad_arguments(worker_bin):
     out = subprocess.run([COORD, "--workers", "", "--steps", "0"], capture_output=True, text=True, timeout=30)
     assert out.returncode == 1 and "no workers" in out.stderr
