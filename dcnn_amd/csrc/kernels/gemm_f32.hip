@@ -575,7 +575,7 @@ __global__ void __launch_bounds__(256, 2) gemm_t2f_wide_kernel(T2Args p) {
 // 3 bf16 MFMAs = 3/16 of the cycles of the exact 16x16x4 f32 MFMA chain for the same K: the fp32
 // path's GEMMs become ~4-5x cheaper in matrix-pipe time. Same tiling, tap gathers, epilogue
 // (bias / residual / ReLU / BN statistics) and split-K slabs as the exact kernels above.
-// Opt-in (set_f32_mode(1), DCNN_F32_SPLIT=1): on ResNet-18/ResNet-9 fp32 these gathered-GEMM
+// Opt-in (set_f32_mode(1), `bench.py --f32-mode split`): on ResNet-18/ResNet-9 fp32 these gathered-GEMM
 // kernels are bound by their tap-gather loads, not the matrix pipe, so the split forward/dgrad
 // kernel was 18% faster and the split wgrad 26% slower than exact (profiles/fp32_split_r2.md) —
 // the exact f32 MFMA path stays the default. tests/test_gpu_kernels.py bounds the split error

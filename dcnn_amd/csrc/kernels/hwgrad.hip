@@ -84,8 +84,6 @@ __global__ void __launch_bounds__(256, 1) hwgrad_kernel(HWArgs p) {
   const int tbeg = split * p.tiles_per_split;
   const int tend = min(total_tiles, tbeg + p.tiles_per_split);
 
-  // DCNN_HWGRAD_DBG (timing experiments only, results are wrong when set): bit 1 = no slab
-  // stores, bit 2 = no global loads (zero-record descriptors), bit 16 = no pixel tiles
   const i32x4 rsY = raw_rsrc(p.dY, p.dy_bytes);
   const i32x4 rsX = raw_rsrc(p.X, p.x_bytes);
 
