@@ -203,11 +203,11 @@ class ResidualBlock(Layer):
         receive), reduce the shortcut BatchNorm's statistics in the same launch as the tail's
         (hip.stat_reduce_pair). Returns the shortcut's incoming gradient carrying its reduced
         statistics, or None (unpaired path)."""
-        from ...ops import hip
+        from ...ops import fusion, hip
         sp = self.shortcut_path
         pre = getattr(grad, "_bnb", None)
         bns = sp[-1] if sp and isinstance(sp[-1], BatchNorm) else None
-        if (bns is None or pre is None or pre[0] is not self.main_path[-1] or not hip._BN_DUAL
+        if (bns is None or pre is None or pre[0] is not self.main_path[-1] or not fusion.BN_DUAL
                 or isinstance(pre[1], hip.Stats) or grad.dtype != torch.bfloat16
                 or not grad.is_contiguous(memory_format=torch.channels_last)):
             return None

@@ -3,7 +3,7 @@ library's shape query stubbed: which convs go to the halo kernel (hconv / hconv3
 gathered GEMM or the streaming 1x1 kernel."""
 import pytest
 
-from dcnn_amd.ops import hip
+from dcnn_amd.ops import fusion, hip
 
 
 class _Stub:
@@ -14,7 +14,7 @@ class _Stub:
 @pytest.fixture
 def stub(monkeypatch):
     monkeypatch.setattr(hip, "kernels", lambda: _Stub())
-    monkeypatch.setattr(hip, "_HCONV_1X1", True)
+    monkeypatch.setattr(fusion, "HCONV_1X1", True)
 
 
 TAP1 = [(0, 0, 0, 0)]
@@ -40,7 +40,7 @@ def test_1x1_only_k1024_small_grid(stub):
 
 
 def test_1x1_switch_off(stub, monkeypatch):
-    monkeypatch.setattr(hip, "_HCONV_1X1", False)
+    monkeypatch.setattr(fusion, "HCONV_1X1", False)
     assert not hip._hconv_ok(32, 8, 8, 8, 8, 1, 1, 1024, 256, TAP1, None)
 
 

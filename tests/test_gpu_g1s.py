@@ -11,6 +11,8 @@ import pytest
 import torch
 import torch.nn.functional as F
 
+from dcnn_amd.ops import fusion
+
 pytestmark = pytest.mark.gpu
 
 CL = torch.channels_last
@@ -189,7 +191,7 @@ def test_hconv_1x1_k1024(hip, case, monkeypatch):
     wt = hip.conv_weight_t(wg)
     outs = {}
     for on in (False, True):
-        monkeypatch.setattr(hip, "_HCONV_1X1", on)
+        monkeypatch.setattr(fusion, "HCONV_1X1", on)
         y, partial = hip.conv2d_fwd(xg, wg, None, (1, 1), (0, 0), stats=True)
         st = hip.bn_stats(y, partial).clone()
         dx = hip.conv2d_dgrad(dy, wt, (N, Ci, H, W), (1, 1), (0, 0))

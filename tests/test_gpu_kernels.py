@@ -7,6 +7,8 @@ import pytest
 import torch
 import torch.nn.functional as F
 
+from dcnn_amd.ops import fusion
+
 pytestmark = pytest.mark.gpu
 
 CL = torch.channels_last
@@ -228,13 +230,14 @@ def test_deferred_reduce_in_model_backward(hip):
     assert not hip.grad_reducer.pending and not hip.grad_reducer.active
     deferred = [t.float().cpu().clone() for t in m.gradients()]
     m.clear_gradients()
-    prev = hip._DEFER_REDUCE
-    hip._DEFER_REDUCE = False
+    from dcnn_amd.ops import fusion
+    prev = fusion.DEFER_REDUCE
+    fusion.DEFER_REDUCE = False
     try:
         m.forward(x, return_on_input_device=False)
         m.backward(g)
     finally:
-        hip._DEFER_REDUCE = prev
+        fusion.DEFER_REDUCE = prev
     for a, b in zip(deferred, m.gradients()):
         assert rel_err(b, a) < 2e-2, rel_err(b, a)
 
@@ -789,7 +792,7 @@ def test_strided_dgrad_grouped_launch(hip, case, monkeypatch):
     wt = hip.conv_weight_t(w)
     outs = []
     for grouped in (True, False):
-        monkeypatch.setattr(hip, "_G2_GROUP", grouped)
+        monkeypatch.setattr(fusion, "G2_GROUP", grouped)
         outs.append(hip.conv2d_dgrad(dy, wt, (N, Ci, H, W), (s, s), (p, p), residual=res))
     assert torch.equal(outs[0], outs[1])
     ref = torch.nn.grad.conv2d_input((N, Ci, H, W), w.float().cpu(), dy.float().cpu(), s, p) + res.float().cpu()

@@ -224,10 +224,12 @@ def test_bwd_bn_fusion_matches_unfused(name, monkeypatch):
             calls["n"] += 1
             return real(*a)
 
+    from dcnn_amd.ops import fusion, hip_norm
     monkeypatch.setattr(hip, "kernels", lambda: Spy())
+    monkeypatch.setattr(hip_norm, "kernels", lambda: Spy())  # (the BatchNorm passes' module)
     res = {}
     for fuse in (False, "again", True, "fused again"):
-        monkeypatch.setattr(hip, "_BNB", fuse is True or fuse == "fused again")
+        monkeypatch.setattr(fusion, "BNB", fuse is True or fuse == "fused again")
         m = create_model(name)
         m.set_seed(11)
         m.set_device("GPU:0")
@@ -342,10 +344,11 @@ def test_projection_shortcut_bn_dual_apply_matches_separate():
     x = torch.randn(8, 3, 64, 64, device="cuda")
     y = torch.randint(0, 200, (8,), device="cuda")
     res = []
-    saved = hip._BN_DUAL
+    from dcnn_amd.ops import fusion
+    saved = fusion.BN_DUAL
     try:
         for dual in (True, False):
-            hip._BN_DUAL = dual
+            fusion.BN_DUAL = dual
             m = create_model("resnet18_tiny_imagenet")
             m.set_seed(3)
             m.set_device("GPU:0")
@@ -360,7 +363,7 @@ def test_projection_shortcut_bn_dual_apply_matches_separate():
             ev = m.forward(x).clone()
             res.append((out.clone(), loss.clone(), m.arena.grad.clone(), bufs, ev))
     finally:
-        hip._BN_DUAL = saved
+        fusion.BN_DUAL = saved
     (o1, l1, g1, b1, e1), (o0, l0, g0, b0, e0) = res
     assert torch.equal(o1, o0) and torch.equal(l1, l0)
     assert torch.equal(g1, g0)
