@@ -47,6 +47,21 @@ __device__ __forceinline__ float wave_max(float v) {
   return v;
 }
 
+// ---- kernel-argument prefetch ---------------------------------------------------------------
+// Kernels with more arguments than their SGPR budget holds get their argument loads sunk to the
+// first uses, one scalar-load round trip to memory per group (hconv3: five serialised groups in
+// the prologue). One batch of loads touching every 64-byte line of the argument segment, issued
+// first and waited for once, turns those later loads into scalar-cache hits.
+template <int BYTES>
+__device__ __forceinline__ void prefetch_kernargs() {
+  typedef const __attribute__((address_space(4))) unsigned karg_u32;
+  karg_u32* k = (karg_u32*)__builtin_amdgcn_kernarg_segment_ptr();
+  unsigned d = 0;
+#pragma unroll
+  for (int o = 0; o < BYTES; o += 64) d ^= __builtin_nontemporal_load(k + o / 4);
+  asm volatile("" ::"s"(d));
+}
+
 // ---- opaque 16-byte direct-to-LDS loads ------------------------------------------------------
 // The compiler's wait-count pass cannot tell which LDS bytes a builtin LDS-DMA load writes, so it
 // puts `s_waitcnt vmcnt(0)` in front of every later ds_read_b64_tr_b16 — which serialises a

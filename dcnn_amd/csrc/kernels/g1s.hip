@@ -102,6 +102,7 @@ constexpr bool g1s_wl(int K, int mode) { return K >= 256 || (K == 128 && mode ==
 
 template <int K, int MODE, int OCC, int PF, bool EP, bool GEN = false>
 __global__ void __launch_bounds__(256, OCC) g1s_kernel(G1sArgs p) {
+  prefetch_kernargs<sizeof(G1sArgs)>();
   constexpr int KK = K / 32, TJ = 2, TP = 16 * TJ;
   // K >= 256: the 64 x K weight slice lives in LDS, shared by the workgroup's 4 waves (same
   // channel slice, 4 pixel ranges), instead of K / 2 VGPRs per lane

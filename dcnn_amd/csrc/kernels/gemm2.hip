@@ -61,6 +61,7 @@ struct G2 {
 
 template <int BM, int BN, int BK, bool UNI, int NST>
 __global__ void __launch_bounds__(256, 2) gemm_g2_kernel(G2Args p) {
+  prefetch_kernargs<sizeof(G2Args)>();
   using T = G2<BM, BN, BK, UNI, NST>;
   __shared__ __attribute__((aligned(16))) char smem[T::LDS];
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
@@ -362,6 +363,7 @@ __device__ __forceinline__ int tr_swz(int row) {
 
 template <int BM, int BN, bool FAST>
 __global__ void __launch_bounds__(256, 2) gemm_t2_kernel(T2Args p) {
+  prefetch_kernargs<sizeof(T2Args)>();
   using T = T2<BM, BN>;
   constexpr int BK = T::BK;
   __shared__ __attribute__((aligned(16))) char smem[2 * T::STAGE];

@@ -41,6 +41,7 @@ __device__ __forceinline__ f32x4 mfma4(const float4& a, const float4& b, f32x4 c
 
 // C[m][n] = sum_{t, c} Src[pix(m) + tap t][c] * B[n][tap_b[t] + c]   (G2Args semantics, fp32)
 __global__ void __launch_bounds__(256, 2) gemm_g2f_kernel(G2Args p) {
+  prefetch_kernargs<sizeof(G2Args)>();
   __shared__ __attribute__((aligned(16))) float As[2][FBM * FPITCH];
   __shared__ __attribute__((aligned(16))) float Bs[2][FBN * FPITCH];
   __shared__ float red[2][4][FBN];  // per M-wave: shifted (sum, sum^2), pivot, count
@@ -409,6 +410,7 @@ __global__ void __launch_bounds__(256, 2) gemm_g2f_wide_kernel(G2Args p) {
 // coordinates advance incrementally (no divisions in the loop).
 template <int BM, int BN>
 __global__ void __launch_bounds__(256, 2) gemm_t2f_wide_kernel(T2Args p) {
+  prefetch_kernargs<sizeof(T2Args)>();
   constexpr int WM = BM / 2, WN = BN / 2, TM = WM / 32, TN = WN / 32;
   constexpr int AQ = BM / 64, BQ = BN / 64;  // float4 column groups per thread (16 threads x 4 cols per pass)
   constexpr int PA = BM + 4, PB = BN + 4;    // LDS row pitch (floats)

@@ -234,6 +234,7 @@ __device__ __forceinline__ void hc_epilogue(const HConvArgs& p,
 
 template <int BM, int BN, int TPS, int NHB, int NBS, bool F32O>
 __global__ void __launch_bounds__(256, 1) hconv_kernel(HConvArgs p) {
+  prefetch_kernargs<sizeof(HConvArgs)>();
   using T = HC<BM, BN, TPS, NHB, NBS, F32O>;
   static_assert(NBS >= 2 && NBS <= 4 && (NBS == 2 || TPS == 1), "deep weight ring needs 1 tap per step");
   extern __shared__ __attribute__((aligned(16))) char smem[];

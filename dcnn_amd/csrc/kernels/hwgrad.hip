@@ -310,6 +310,7 @@ __device__ __forceinline__ bf16x4 tr4_at(const char* addr) {
 // 32-lane read group sit in chunk-swizzle classes 4 apart and hit disjoint banks.
 template <int TW, int TH, int IMG, int NS, int TSP = 1, bool F32 = false>
 __global__ void __launch_bounds__(256 * TSP, 1) hwgrad2_kernel(HWArgs p) {
+  prefetch_kernargs<sizeof(HWArgs)>();
   using G = HWGeo2<TW, TH, IMG>;
   constexpr int HNI = G::HNI, HW2P = G::HW2P, HPIP = G::HPIP, HPP = G::HPP, TPX = G::TPX, STAGE = G::STAGE;
   constexpr int INS = 4 + HNI;
