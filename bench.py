@@ -17,10 +17,15 @@ Exactly K steps are timed between a barrier + device synchronisation on both sid
 slowest rank's time is reported. Every timed step runs the full forward, loss, backward,
 gradient all-reduce and optimizer update.
 
---engine native runs the same step on the C++ host API instead (bin/tiny_imagenet_resnet18: the
-framework's own Tensor, flows and gpu::Graph capture, the gradient mean over the in-tree RCCL
-communicator inside the captured step; no torch in the timed process), one child process per rank
-under the same launcher variables.
+Engines: the same step on the C++ host API (bin/tiny_imagenet_resnet18: the framework's own
+Tensor, flows and gpu::Graph capture; no torch in the timed process; one child process per rank
+under the same launcher variables, the gradient mean over the in-tree RCCL communicator inside the
+captured step) or on the Python front end (torch tensors, torch.cuda graphs). --engine auto (the
+default) picks the C++ engine for ResNet-18 on a single GPU at batch <= 256 (same-box A/B,
+profiles/engine_ab_r5.md: b256 85.1k vs 85.1k, b64 36.2k vs 35.8k img/s) and the Python one for
+N > 1, whose bucketed gradient all-reduces overlap the backward (the C++ engine reduces once after
+the backward), and for ResNet-50 and larger batches (Python 1-2% faster there); a single-GPU C++
+run that fails falls back to the Python engine.
 """
 import argparse
 import json
@@ -75,6 +80,18 @@ def native_main(a):
     }), flush=True)
 
 
+def auto_native(a):
+    """--engine auto: the C++ engine covers this run (one GPU process, bf16, the default step
+    options, a model of the C++ factory, the trainer binary built)."""
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    default_step = (a.graph == 1 and not a.pg and not a.profile and a.grad_dtype == "fp32"
+                    and a.dp_backend == "torch" and a.bucket_mb == 4.0)
+    return (world == 1 and a.gpus == 1 and a.device == "cuda" and a.dtype == "bf16" and default_step
+            and a.model in ("resnet18_tiny_imagenet", "resnet34_tiny_imagenet") and a.batch <= 256
+            and os.access(os.path.join(ROOT, "dcnn_amd", "bin", "tiny_imagenet_resnet18"), os.X_OK)
+            and torch.cuda.device_count() > 0)
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -94,8 +111,9 @@ def main():
                          "the framework's own RCCL communicator (rank/world from the launcher env, unique id "
                          "over the native TCP plane, no torch.distributed; opt-in, exits non-zero if it cannot "
                          "be built)")
-    ap.add_argument("--engine", default=os.environ.get("DCNN_BENCH_ENGINE", "python"), choices=["python", "native"],
-                    help="python: the Python front end's captured step (default); native: the C++ host API trainer")
+    ap.add_argument("--engine", default=os.environ.get("DCNN_BENCH_ENGINE", "auto"), choices=["auto", "python", "native"],
+                    help="native: the C++ host API trainer; python: the Python front end's captured step; auto "
+                         "(default): native on one GPU (falls back to python if it fails), python for N > 1")
     ap.add_argument("--profile", action="store_true", help="print per-layer device times")
     ap.add_argument("--device", default="cuda")
     ap.add_argument("--dtype", default="bf16", choices=["bf16", "fp32"],
@@ -109,6 +127,11 @@ def main():
     a = ap.parse_args()
     if a.engine == "native":
         return native_main(a)
+    if a.engine == "auto" and auto_native(a):
+        try:
+            return native_main(a)
+        except SystemExit as e:  # (one process: nothing else depends on this rank's plane)
+            print(f"[bench] C++ engine failed ({e.code}); running the Python engine", file=sys.stderr, flush=True)
 
     from dcnn_amd.parallel.dp import DataParallel, init_distributed
     from dcnn_amd.parallel.rccl import env_rank_world

@@ -6,6 +6,7 @@ the GPU against the C++ CPU backend."""
 import os
 import re
 import subprocess
+import sys
 
 import numpy as np
 import pytest
@@ -358,3 +359,23 @@ def test_cpp_data_parallel_world1_matches_single(bins, tmp_path):
     assert dp["world"] == 1 and dp["data_parallel"] == "rccl" and dp["hipgraph"] is True
     assert dp["loss"] == plain["loss"], (dp, plain)
     print(plain, dp)
+
+
+@pytest.mark.gpu
+def test_bench_default_engine_contract_line(bins, tmp_path):
+    """`python bench.py` on one GPU runs the C++ engine (--engine auto) and prints the contract's
+    single JSON line with the whole-job value, the timed step count and the engine named."""
+    import json
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    r = subprocess.run([sys.executable, os.path.join(root, "bench.py"), "--batch", "64", "--steps", "4", "--warmup", "2"],
+                       cwd=tmp_path, stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True, timeout=300)
+    assert r.returncode == 0, r.stderr[-3000:]
+    lines = [l for l in r.stdout.splitlines() if l.startswith("{")]
+    assert len(lines) == 1, r.stdout
+    d = json.loads(lines[0])
+    for k in ("metric", "value", "unit", "n_gpus", "steps", "warmup", "ms_per_step", "higher_is_better", "scaling",
+              "vs_baseline", "dtype", "data", "config"):
+        assert k in d, k
+    assert d["n_gpus"] == 1 and d["steps"] == 4 and d["warmup"] == 2 and d["dtype"] == "bf16"
+    assert d["config"]["engine"] == "native (C++ host API)" and d["config"]["global_batch"] == 64
+    assert abs(d["value"] - 64 * 1000.0 / d["ms_per_step"]) < 0.02 * d["value"]
