@@ -23,9 +23,10 @@ under the same launcher variables, the gradient mean over the in-tree RCCL commu
 captured step) or on the Python front end (torch tensors, torch.cuda graphs). --engine auto (the
 default) picks the C++ engine for ResNet-18 on a single GPU at batch <= 256 (same-box A/B,
 profiles/engine_ab_r5.md: b256 85.1k vs 85.1k, b64 36.2k vs 35.8k img/s) and the Python one for
-N > 1, whose bucketed gradient all-reduces overlap the backward (the C++ engine reduces once after
-the backward), and for ResNet-50 and larger batches (Python 1-2% faster there); a single-GPU C++
-run that fails falls back to the Python engine.
+N > 1 (its torch.distributed ProcessGroupNCCL path is the one exercised at world > 1 so far; the C++
+engine's bucketed, overlapped RCCL mean has run at world 1 only), and for ResNet-50 and larger
+batches (Python 1-2% faster there); a single-GPU C++ run that fails falls back to the Python
+engine.
 """
 import argparse
 import json

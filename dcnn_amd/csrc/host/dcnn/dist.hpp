@@ -22,6 +22,7 @@ namespace dcnn {
 namespace coll {
 class Comm;
 }
+class Sequential;
 
 namespace dist {
 
@@ -47,10 +48,31 @@ class DataParallel {
   // host scalar maximum over ranks (e.g. the slowest rank's step time)
   double max(double v);
 
+  // Overlapped bucketed gradient mean over `model`'s GPU parameter arena (the Python plane's
+  // scheme, parallel/dp.py): the flat gradient is cut at top-level layer boundaries into buckets
+  // of >= bucket_mb; each bucket's mean starts on this communicator's own flow as soon as the
+  // backward has produced it (the layer hook, after the weight-gradient reduces queued so far are
+  // flushed), while the earlier layers' backward continues on the compute flow; finish() reduces
+  // the rest and makes the current flow wait for every bucket. Fork / join are events, so the
+  // whole pattern is captured into a training step graph.
+  void attach(Sequential& model, double bucket_mb = 4.0);
+  void on_layer_done(size_t layer);  // Sequential::set_backward_hook
+  void finish();                     // between the backward and the optimizer
+  int buckets_last_step() const { return nb_last_; }
+
  private:
   Env env_;
   std::unique_ptr<coll::Comm> comm_;
   Tensor scratch_;
+  // overlap state: gradient base, per top-level layer the first arena element of its parameters
+  // (SIZE_MAX: none), the reduced suffix [reduced_lo, n)
+  float* g_ = nullptr;
+  size_t n_ = 0, reduced_lo_ = 0, bucket_elems_ = 0;
+  std::vector<size_t> lo_;
+  void* flow_ = nullptr;  // gpu::Flow
+  void* ev_ = nullptr;    // gpu::Event
+  int nb_ = 0, nb_last_ = 0;
+  void fork_bucket(size_t lo, size_t hi);
 };
 
 // One direction of a stage-to-stage device data plane (the native pipeline's transport "rccl",

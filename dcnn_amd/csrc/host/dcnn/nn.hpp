@@ -404,6 +404,9 @@ class Sequential {
   size_t num_parameters();
   const std::vector<std::unique_ptr<Layer>>& layers() const { return layers_; }
   const std::string& name() const { return name_; }
+  // called with the top-level layer index after each layer's backward (in backward order), inside
+  // a capture too (the data-parallel bucket all-reduces start from here: dist::DataParallel)
+  void set_backward_hook(std::function<void(size_t)> f) { bwd_hook_ = std::move(f); }
 
   json::Value get_config() const;
   void print_config() const;
@@ -424,6 +427,7 @@ class Sequential {
   bool training_ = true;
   bool initialized_ = false;
   std::shared_ptr<ParamArena> arena_;
+  std::function<void(size_t)> bwd_hook_;
   void pack_params();
 };
 

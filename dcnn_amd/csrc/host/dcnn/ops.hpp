@@ -57,6 +57,9 @@ namespace gpu_ops {
 // weight-gradient partial reduces of a backward batched into one launch at its end
 void begin_deferred_reduce();
 void end_deferred_reduce();
+// launch the weight-gradient reduces queued so far now and keep queueing (a gradient consumer
+// inside the backward: the data-parallel bucket all-reduce)
+void flush_deferred_reduce();
 // fp32 NCHW network input -> bf16 NHWC activation
 void input_to_nhwc(const float* x, void* y, int N, int C, int HW);
 // bf16 [N][HW][C] <-> [N][C][HW] (Flatten keeps the NCHW feature order of the reference)

@@ -13,7 +13,11 @@
 #include <stdexcept>
 #include <thread>
 
+#include <algorithm>
+#include <cstdint>
+
 #include "../kernels/collective.h"
+#include "dcnn/nn.hpp"
 #include "dcnn/ops.hpp"
 
 namespace dcnn {
@@ -123,6 +127,71 @@ DataParallel::~DataParallel() = default;
 void DataParallel::all_reduce_mean(float* data, size_t n) {
   if (n == 0) return;
   comm_->all_reduce(data, data, n, 0, 4, gpu::flow());  // fp32, average (world 1 too: one code path)
+}
+
+void DataParallel::attach(Sequential& model, double bucket_mb) {
+  const auto params = model.parameters();
+  if (params.empty() || !params[0]->arena) throw std::runtime_error("DataParallel::attach: no GPU parameter arena");
+  ParamArena* a = params[0]->arena.get();
+  g_ = a->grad.ptr<float>();
+  n_ = (size_t)a->grad.numel();
+  bucket_elems_ = (size_t)(bucket_mb * (1 << 20) / sizeof(float));
+  if (bucket_elems_ < 1) bucket_elems_ = 1;
+  lo_.clear();
+  for (const auto& l : model.layers()) {
+    size_t lo = SIZE_MAX;
+    std::vector<Param*> ps;
+    l->collect_params(ps);
+    for (Param* p : ps) {
+      if (p->arena.get() != a) throw std::runtime_error("DataParallel::attach: parameters outside the arena");
+      lo = std::min(lo, (size_t)(p->grad.ptr<float>() - g_));
+    }
+    lo_.push_back(lo);
+  }
+  // the backward completes layers last to first: the suffix from a layer's first element is final
+  // only if the arena holds the layers in order
+  size_t prev = 0;
+  for (size_t lo : lo_) {
+    if (lo == SIZE_MAX) continue;
+    if (lo < prev) throw std::runtime_error("DataParallel::attach: arena not in layer order");
+    prev = lo;
+  }
+  if (!flow_) flow_ = gpu::flow_create();
+  if (!ev_) ev_ = gpu::event_create();
+  reduced_lo_ = n_;
+  nb_ = 0;
+  model.set_backward_hook([this](size_t i) { on_layer_done(i); });
+}
+
+void DataParallel::fork_bucket(size_t lo, size_t hi) {
+  gpu_ops::flush_deferred_reduce();  // the bucket's weight gradients are summed first
+  gpu::event_record(ev_);            // (the compute flow up to here)
+  gpu::flow_wait(flow_, ev_);
+  comm_->all_reduce(g_ + lo, g_ + lo, hi - lo, 0, 4, flow_);
+  ++nb_;
+}
+
+void DataParallel::on_layer_done(size_t layer) {
+  if (!g_ || layer >= lo_.size()) return;
+  // the final suffix: from the first element of the lowest layer done so far that has parameters
+  size_t lo = SIZE_MAX;
+  for (size_t j = layer; j < lo_.size(); ++j) lo = std::min(lo, lo_[j]);
+  if (lo == SIZE_MAX || lo >= reduced_lo_) return;
+  if (reduced_lo_ - lo < bucket_elems_) return;
+  fork_bucket(lo, reduced_lo_);
+  reduced_lo_ = lo;
+}
+
+void DataParallel::finish() {
+  if (!g_) {
+    throw std::runtime_error("DataParallel::finish: attach() first");
+  }
+  if (reduced_lo_ > 0) fork_bucket(0, reduced_lo_);
+  gpu::event_record(ev_, flow_);  // join: the optimizer reads every bucket's mean
+  gpu::flow_wait(gpu::flow(), ev_);
+  nb_last_ = nb_;
+  nb_ = 0;
+  reduced_lo_ = n_;
 }
 
 double DataParallel::max(double v) {

@@ -1335,6 +1335,7 @@ Tensor Sequential::backward_activation(const Tensor& g_in, int mb) {
     for (size_t i = layers_.size(); i-- > 0;) {
       layers_[i]->set_micro_batch(mb);
       g = layers_[i]->backward(g);
+      if (bwd_hook_) bwd_hook_(i);
     }
   } catch (...) {
     if (defer) gpu_ops::end_deferred_reduce();

@@ -449,6 +449,11 @@ void wgrad_reduce(const Tensor& hold, const Tensor& bhold, const float* slab, fl
 }  // namespace
 
 void begin_deferred_reduce() { g_defer = true; }
+void flush_deferred_reduce() {
+  const bool on = g_defer;
+  end_deferred_reduce();
+  g_defer = on;
+}
 void end_deferred_reduce() {
   for (size_t b = 0; b < g_pending.size(); b += kMaxRed) {
     MultiRed t{};

@@ -115,13 +115,22 @@ int main(int argc, char** argv) {
       // replayed with one launch per step; --eager launches every kernel from the host
       const bool graph = dev.is_gpu() && !eager;
       TrainGraph tg(model, opt, loss);
-      // data parallel: the mean of the flat arena gradient over the ranks, between the backward
-      // and the optimizer (inside the captured step)
+      // data parallel: the mean of the flat arena gradient over the ranks, inside the captured
+      // step: bucketed and started from the backward's layer hook on the communicator's own flow
+      // (overlapping the earlier layers' backward), joined before the optimizer; DCNN_DP_OVERLAP=0:
+      // one all-reduce of the whole arena after the backward
       std::function<void()> allreduce;
       if (dp) {
         ParamArena* arena = model.parameters().at(0)->arena.get();
         if (!arena) throw std::runtime_error("--dp: the parameters are not in a GPU arena");
-        allreduce = [&dp, arena] { dp->all_reduce_mean(arena->grad.ptr<float>(), (size_t)arena->grad.numel()); };
+        const char* ov = std::getenv("DCNN_DP_OVERLAP");
+        if (!(ov && std::string(ov) == "0")) {
+          const char* mb = std::getenv("DCNN_DP_BUCKET_MB");
+          dp->attach(model, mb && *mb ? std::atof(mb) : 4.0);
+          allreduce = [&dp] { dp->finish(); };
+        } else {
+          allreduce = [&dp, arena] { dp->all_reduce_mean(arena->grad.ptr<float>(), (size_t)arena->grad.numel()); };
+        }
         tg.set_gradient_hook(allreduce);
       }
       auto one = [&] {
@@ -148,9 +157,10 @@ int main(int argc, char** argv) {
       if (!dp || dp->rank() == 0)
         std::printf("{\"metric\": \"images/sec %s training (C++ host API)\", \"value\": %.1f, \"ms_per_step\": %.3f, "
                     "\"batch\": %d, \"steps\": %d, \"device\": \"%s\", \"hipgraph\": %s, \"loss\": %.6f, "
-                    "\"world\": %d, \"data_parallel\": %s}\n",
+                    "\"world\": %d, \"data_parallel\": %s, \"dp_buckets\": %d}\n",
                     model_name.c_str(), (double)batch * world * timed / s, 1e3 * s / timed, batch, timed,
-                    dev.str().c_str(), graph ? "true" : "false", last, world, dp ? "\"rccl\"" : "null");
+                    dev.str().c_str(), graph ? "true" : "false", last, world, dp ? "\"rccl\"" : "null",
+                    dp ? dp->buckets_last_step() : 0);
       return 0;
     }
     std::unique_ptr<Scheduler> sched;

@@ -358,6 +358,15 @@ def test_cpp_data_parallel_world1_matches_single(bins, tmp_path):
     dp = json.loads([l for l in r.stdout.splitlines() if l.startswith("{")][-1])
     assert dp["world"] == 1 and dp["data_parallel"] == "rccl" and dp["hipgraph"] is True
     assert dp["loss"] == plain["loss"], (dp, plain)
+    # the overlapped bucketed mean (buckets forked from the backward's layer hook onto the
+    # communicator's flow inside the capture; 1 MB buckets: several) and the one-shot mean
+    for extra, check in (({"DCNN_DP_BUCKET_MB": "1"}, lambda d: d["dp_buckets"] > 3),
+                         ({"DCNN_DP_OVERLAP": "0"}, lambda d: d["dp_buckets"] == 0)):
+        r = subprocess.run(cmd + ["--dp"], cwd=tmp_path, stdout=subprocess.PIPE, stderr=subprocess.STDOUT, text=True,
+                           timeout=300, env=dict(env, **extra))
+        assert r.returncode == 0, r.stdout[-3000:]
+        d = json.loads([l for l in r.stdout.splitlines() if l.startswith("{")][-1])
+        assert check(d) and d["loss"] == plain["loss"], (extra, d, plain)
     print(plain, dp)
 
 
