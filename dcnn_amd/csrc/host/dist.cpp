@@ -122,7 +122,14 @@ DataParallel::DataParallel(const Env& e, int port_offset) : env_(e) {
   scratch_ = Tensor::zeros({1}, DType::F32, Device::gpu(e.local_rank));
 }
 
-DataParallel::~DataParallel() = default;
+DataParallel::~DataParallel() {
+  try {
+    if (flow_) gpu::flow_synchronize(flow_);
+    if (ev_) gpu::event_destroy(ev_);
+    if (flow_) gpu::flow_destroy(flow_);
+  } catch (...) {
+  }
+}
 
 void DataParallel::all_reduce_mean(float* data, size_t n) {
   if (n == 0) return;

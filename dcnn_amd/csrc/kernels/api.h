@@ -249,7 +249,8 @@ int stem_tiles_host(int N, int H, int W);
 int stem_wgrad_blocks(int N, int H, int W);
 void stem_fwd(StemArgs a, hipStream_t s);
 void stem_wgrad(StemArgs a, int blocks, hipStream_t s);
-void multi_weight_transpose(const int64_t* table, int n, long max_tiles, hipStream_t s);
+// f32: fp32 operands (the exact fp32 path), else bf16
+void multi_weight_transpose(const int64_t* table, int n, long max_tiles, hipStream_t s, int f32 = 0);
 void im2col(const float* x, float* col, int N, int C, int H, int W, int KH, int KW, int SH, int SW, int PH, int PW,
             int OH, int OW, hipStream_t s);
 void col2im(const float* col, float* x, int N, int C, int H, int W, int KH, int KW, int SH, int SW, int PH, int PW,

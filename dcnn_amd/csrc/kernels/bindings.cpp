@@ -486,8 +486,8 @@ PYBIND11_MODULE(_kernels, m) {
     a.N = N; a.Ci = Ci; a.H = H; a.W = W; a.Co = Co;
     stem_wgrad(a, blocks, S(st));
   });
-  m.def("multi_weight_transpose", [](uintptr_t table, int n, long max_tiles, uintptr_t st) {
-    multi_weight_transpose(P<const int64_t*>(table), n, max_tiles, S(st));
+  m.def("multi_weight_transpose", [](uintptr_t table, int n, long max_tiles, uintptr_t st, int f32) {
+    multi_weight_transpose(P<const int64_t*>(table), n, max_tiles, S(st), f32);
   });
   m.def("cast_f32_bf16",[](uintptr_t x, uintptr_t y, long n, uintptr_t st) {
     cast_f32_bf16(P<const float*>(x), P<bf16*>(y), n, S(st));

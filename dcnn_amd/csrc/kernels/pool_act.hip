@@ -504,10 +504,14 @@ __global__ void conv_weight_transpose_kernel(const S* __restrict__ w, bf16* __re
 // [Co][T][Ci] -> [Ci][T][Co] for every conv of a model in one launch (blockIdx.y = conv). Each
 // workgroup moves one 64(co) x 64(ci) tile of one tap through LDS: 16-byte coalesced loads along
 // ci, 16-byte coalesced stores along co (Ci, Co multiples of 8, 256-byte aligned arena views).
+// T = bf16 (the bf16 compute path's operands) or float (the exact fp32 path's): 16-byte vectors of
+// V = 16 / sizeof(T) elements; Ci, Co multiples of V.
+template <typename T>
 __global__ void __launch_bounds__(256) multi_weight_transpose_kernel(const int64_t* __restrict__ table) {
+  constexpr int V = 16 / (int)sizeof(T), RV = 64 / V;  // elements per vector, vectors per 64-row
   const int64_t* e = table + blockIdx.y * 5;
-  const bf16* w = reinterpret_cast<const bf16*>(e[0]);
-  bf16* wt = reinterpret_cast<bf16*>(e[1]);
+  const T* w = reinterpret_cast<const T*>(e[0]);
+  T* wt = reinterpret_cast<T*>(e[1]);
   const int Co = (int)e[2], T_ = (int)e[3], Ci = (int)e[4];
   const int tco = (Co + 63) / 64, tci = (Ci + 63) / 64;
   int b = blockIdx.x;
@@ -515,31 +519,34 @@ __global__ void __launch_bounds__(256) multi_weight_transpose_kernel(const int64
   const int t = b % T_;
   b /= T_;
   const int ic = b % tci, oc = b / tci;
-  __shared__ bf16 tile[64][72];  // row pitch 144 B keeps the 16-byte row chunks aligned
-  for (int k = threadIdx.x; k < 64 * 8; k += 256) {
-    const int r = k >> 3, c8 = (k & 7) * 8;
-    const int co = oc * 64 + r, ci = ic * 64 + c8;
+  __shared__ T tile[64][64 + V];  // row pitch keeps the 16-byte row chunks aligned
+  for (int k = threadIdx.x; k < 64 * RV; k += 256) {
+    const int r = k / RV, cv = (k % RV) * V;
+    const int co = oc * 64 + r, ci = ic * 64 + cv;
     uint4 v = make_uint4(0, 0, 0, 0);
     if (co < Co && ci < Ci) v = *reinterpret_cast<const uint4*>(w + ((long)co * T_ + t) * Ci + ci);
-    *reinterpret_cast<uint4*>(&tile[r][c8]) = v;
+    *reinterpret_cast<uint4*>(&tile[r][cv]) = v;
   }
   __syncthreads();
-  for (int k = threadIdx.x; k < 64 * 8; k += 256) {
-    const int r = k >> 3, c8 = (k & 7) * 8;  // r: ci within the tile, c8: first of 8 co
-    const int ci = ic * 64 + r, co = oc * 64 + c8;
+  for (int k = threadIdx.x; k < 64 * RV; k += 256) {
+    const int r = k / RV, cv = (k % RV) * V;  // r: ci within the tile, cv: first of V co
+    const int ci = ic * 64 + r, co = oc * 64 + cv;
     if (ci < Ci && co < Co) {
       uint4 v;
-      bf16* o = reinterpret_cast<bf16*>(&v);
+      T* o = reinterpret_cast<T*>(&v);
 #pragma unroll
-      for (int j = 0; j < 8; ++j) o[j] = tile[c8 + j][r];
+      for (int j = 0; j < V; ++j) o[j] = tile[cv + j][r];
       *reinterpret_cast<uint4*>(wt + ((long)ci * T_ + t) * Co + co) = v;
     }
   }
 }
 
-void multi_weight_transpose(const int64_t* table, int n, long max_tiles, hipStream_t s) {
+void multi_weight_transpose(const int64_t* table, int n, long max_tiles, hipStream_t s, int f32) {
   if (n <= 0) return;
-  hipLaunchKernelGGL(multi_weight_transpose_kernel, dim3((unsigned)max_tiles, n), dim3(256), 0, s, table);
+  if (f32)
+    hipLaunchKernelGGL(multi_weight_transpose_kernel<float>, dim3((unsigned)max_tiles, n), dim3(256), 0, s, table);
+  else
+    hipLaunchKernelGGL(multi_weight_transpose_kernel<bf16>, dim3((unsigned)max_tiles, n), dim3(256), 0, s, table);
   DCNN_LAUNCH_CHECK();
 }
 

@@ -216,11 +216,11 @@ class Sequential:
             if isinstance(self.layers[0], ResidualBlock):
                 self.layers[0]._plan()
         self._transposer = None
-        if on_gpu and self.initialized and self.compute_dtype == torch.bfloat16:
+        if on_gpu and self.initialized and self.compute_dtype in (torch.bfloat16, torch.float32):
             from ..ops.hip import WeightTransposer
             convs = [l for l in _all_layers(self.layers) if isinstance(l, Conv2D)]
             if convs:
-                self._transposer = WeightTransposer(convs)
+                self._transposer = WeightTransposer(convs, self.compute_dtype)
 
     def prepare_backward(self) -> None:
         """Per-step setup of the backward pass: all dgrad weight operands in one launch, and the

@@ -238,17 +238,20 @@ def cast_bf16(src, dst):
 
 
 class WeightTransposer:
-    """Regenerates every conv's dgrad operand ([Ci][KH][KW][Co] bf16) from the bf16 shadow
-    weights in ONE kernel launch per step (instead of one launch per conv)."""
+    """Regenerates every conv's dgrad operand ([Ci][KH][KW][Co]) from the bf16 shadow weights (or,
+    on the fp32 compute path, the fp32 channels_last masters) in ONE kernel launch per step
+    (instead of one launch per conv)."""
 
-    def __init__(self, convs):
+    def __init__(self, convs, dtype=BF16):
+        self.dtype = dtype
         self.convs = [c for c in convs if c.in_channels % 8 == 0 and c.out_channels % 8 == 0]
         rows = []
         self.max_tiles = 0  # 64x64 (co, ci) tiles per tap: the launch's x extent
         for c in self.convs:
             w = c.weight_operand(0)
             Co, Ci, KH, KW = w.shape
-            c._wt_buf = _arena.persistent((Ci, KH, KW, Co), BF16, w.device)
+            assert w.dtype == dtype and (w.is_contiguous(memory_format=CL) or KH * KW == 1)
+            c._wt_buf = _arena.persistent((Ci, KH, KW, Co), dtype, w.device)
             rows.append([w.data_ptr(), c._wt_buf.data_ptr(), Co, KH * KW, Ci])
             self.max_tiles = max(self.max_tiles, KH * KW * ((Co + 63) // 64) * ((Ci + 63) // 64))
         self.table = torch.tensor(rows, dtype=torch.int64).to(self.convs[0]._wt_buf.device) if rows else None
@@ -256,7 +259,8 @@ class WeightTransposer:
     def run(self):
         if self.table is None:
             return
-        kernels().multi_weight_transpose(self.table.data_ptr(), len(self.convs), self.max_tiles, stream_ptr())
+        kernels().multi_weight_transpose(self.table.data_ptr(), len(self.convs), self.max_tiles, stream_ptr(),
+                                         int(self.dtype == F32))
         for c in self.convs:
             c._wt_valid = True
 
