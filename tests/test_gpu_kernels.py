@@ -897,3 +897,23 @@ def test_maxpool_vectorised_vs_torch(hip, geom):
     dx = hip.maxpool_bwd(dy.cuda().bfloat16().contiguous(memory_format=CL), idx, (N, C, H, W), ph, pw, sh, sw, pad_h,
                          pad_w)
     assert rel_err(dx, xr.grad) < 1e-2  # bf16 rounding of summed window gradients only
+
+
+@pytest.mark.parametrize("geom", [(2, 2, 2, 2, 0, 0), (3, 3, 3, 3, 0, 0), (3, 3, 2, 2, 1, 1)])
+@pytest.mark.parametrize("C", [12, 64])
+def test_maxpool_fp32_vs_torch(hip, geom, C):
+    """fp32 max-pool forward / backward (the 4-channel vector kernels on non-overlapping windows,
+    the generic kernel otherwise) against torch.nn.functional.max_pool2d: distinct values, so the
+    argmax is unique and both directions match exactly."""
+    ph, pw, sh, sw, pad_h, pad_w = geom
+    N, H, W = 2, 18, 18
+    torch.manual_seed(22)
+    x = (torch.randperm(N * C * H * W).float() - 1000.0).view(N, C, H, W) / 7.0
+    xr = x.clone().requires_grad_(True)
+    yr = F.max_pool2d(xr, (ph, pw), (sh, sw), (pad_h, pad_w))
+    dy = torch.randn_like(yr)
+    yr.backward(dy)
+    y, idx = hip.maxpool_fwd(x.cuda().contiguous(memory_format=CL), ph, pw, sh, sw, pad_h, pad_w)
+    assert y.dtype == torch.float32 and torch.equal(y.cpu(), yr.detach())
+    dx = hip.maxpool_bwd(dy.cuda().contiguous(memory_format=CL), idx, (N, C, H, W), ph, pw, sh, sw, pad_h, pad_w)
+    assert torch.equal(dx.cpu(), xr.grad)
