@@ -487,13 +487,42 @@ __global__ void __launch_bounds__(256) bn_bwd_apply_kernel(const T* __restrict__
 // ---------------------------------------------------------------------------------------
 __device__ __forceinline__ uint4 ldg16(const bf16* p) { return *reinterpret_cast<const uint4*>(p); }
 
+// 8-element vectors of the apply passes: one 16-byte bf16 vector, or two 16-byte fp32 halves
+// (the fp32 compute path; same trips / prologue scheme, twice the bytes per vector)
+template <typename T>
+struct Vec8;
+template <>
+struct Vec8<bf16> {
+  using type = uint4;
+  __device__ __forceinline__ static type load(const bf16* p) { return ldg16(p); }
+  __device__ __forceinline__ static void unpack(const type& v, float* f) { unpack8(v, f); }
+  __device__ __forceinline__ static void store(bf16* p, const float* f) { *reinterpret_cast<uint4*>(p) = pack8(f); }
+};
+template <>
+struct Vec8<float> {
+  struct type {
+    float4 a, b;
+  };
+  __device__ __forceinline__ static type load(const float* p) {
+    return type{*reinterpret_cast<const float4*>(p), *reinterpret_cast<const float4*>(p + 4)};
+  }
+  __device__ __forceinline__ static void unpack(const type& v, float* f) {
+    f[0] = v.a.x; f[1] = v.a.y; f[2] = v.a.z; f[3] = v.a.w;
+    f[4] = v.b.x; f[5] = v.b.y; f[6] = v.b.z; f[7] = v.b.w;
+  }
+  __device__ __forceinline__ static void store(float* p, const float* f) {
+    *reinterpret_cast<float4*>(p) = make_float4(f[0], f[1], f[2], f[3]);
+    *reinterpret_cast<float4*>(p + 4) = make_float4(f[4], f[5], f[6], f[7]);
+  }
+};
+
 // y = x*scale + shift (+ residual) (ReLU)
-template <int U, bool RES>
-__global__ void __launch_bounds__(256) bn_apply_v_kernel(const bf16* __restrict__ x, bf16* __restrict__ y,
+template <typename T, int U, bool RES>
+__global__ void __launch_bounds__(256) bn_apply_v_kernel(const T* __restrict__ x, T* __restrict__ y,
                                                          unsigned nv, int C, const float* __restrict__ sums,
                                                          int parts, float count, const float* __restrict__ gamma,
                                                          const float* __restrict__ beta, float eps,
-                                                         const bf16* __restrict__ residual, int relu,
+                                                         const T* __restrict__ residual, int relu,
                                                          float* __restrict__ save_mean,
                                                          float* __restrict__ save_istd,
                                                          float* __restrict__ run_mean, float* __restrict__ run_var,
@@ -501,15 +530,16 @@ __global__ void __launch_bounds__(256) bn_apply_v_kernel(const bf16* __restrict_
   extern __shared__ __attribute__((aligned(16))) float sh[];
   float* scale = sh;
   float* shift = sh + C;
+  using VT = Vec8<T>;
   const unsigned stride = gridDim.x * 256u, cv = (unsigned)C / 8;
   unsigned i = blockIdx.x * 256u + threadIdx.x;
-  uint4 xv[U], rv[U];
+  typename VT::type xv[U], rv[U];
 #pragma unroll
   for (int u = 0; u < U; ++u) {
     const unsigned k = i + u * stride;
     if (k < nv) {
-      xv[u] = ldg16(x + (size_t)k * 8);
-      if (RES) rv[u] = ldg16(residual + (size_t)k * 8);
+      xv[u] = VT::load(x + (size_t)k * 8);
+      if (RES) rv[u] = VT::load(residual + (size_t)k * 8);
     }
   }
   for (int c = threadIdx.x; c < C; c += 256) {
@@ -538,13 +568,13 @@ __global__ void __launch_bounds__(256) bn_apply_v_kernel(const bf16* __restrict_
   while (true) {
     // the next trip's loads go out before this trip's stores (loads and stores overlap)
     const unsigned inx = i + U * stride;
-    uint4 xn[U], rn[U];
+    typename VT::type xn[U], rn[U];
 #pragma unroll
     for (int u = 0; u < U; ++u) {
       const unsigned k = inx + u * stride;
       if (inx < nv && k < nv) {
-        xn[u] = ldg16(x + (size_t)k * 8);
-        if (RES) rn[u] = ldg16(residual + (size_t)k * 8);
+        xn[u] = VT::load(x + (size_t)k * 8);
+        if (RES) rn[u] = VT::load(residual + (size_t)k * 8);
       }
     }
 #pragma unroll
@@ -557,8 +587,8 @@ __global__ void __launch_bounds__(256) bn_apply_v_kernel(const bf16* __restrict_
         const float sc[8] = {s0.x, s0.y, s0.z, s0.w, s1.x, s1.y, s1.z, s1.w};
         const float sf[8] = {h0.x, h0.y, h0.z, h0.w, h1.x, h1.y, h1.z, h1.w};
         float f[8], r[8];
-        unpack8(xv[u], f);
-        if (RES) unpack8(rv[u], r);
+        VT::unpack(xv[u], f);
+        if (RES) VT::unpack(rv[u], r);
 #pragma unroll
         for (int v = 0; v < 8; ++v) {
           float t = f[v] * sc[v] + sf[v];
@@ -566,7 +596,7 @@ __global__ void __launch_bounds__(256) bn_apply_v_kernel(const bf16* __restrict_
           if (relu) t = fmaxf(t, 0.f);
           f[v] = t;
         }
-        *reinterpret_cast<uint4*>(y + (size_t)k * 8) = pack8(f);
+        VT::store(y + (size_t)k * 8, f);
       }
     }
     if (inx >= nv) break;
@@ -581,10 +611,10 @@ __global__ void __launch_bounds__(256) bn_apply_v_kernel(const bf16* __restrict_
 
 // dx = A*dy' + B*(x - mean) + D per channel, with A = gamma*istd, B = -A*istd*mean(dy' xhat),
 // D = -A*mean(dy') (the same algebra as bn_bwd_apply_kernel, three coefficients instead of five)
-template <int U, bool MASK>
-__global__ void __launch_bounds__(256) bn_bwd_apply_v_kernel(const bf16* __restrict__ dy,
-                                                             const bf16* __restrict__ yout,
-                                                             const bf16* __restrict__ x, bf16* __restrict__ dx,
+template <typename T, int U, bool MASK>
+__global__ void __launch_bounds__(256) bn_bwd_apply_v_kernel(const T* __restrict__ dy,
+                                                             const T* __restrict__ yout,
+                                                             const T* __restrict__ x, T* __restrict__ dx,
                                                              unsigned nv, int C, const float* __restrict__ mean,
                                                              const float* __restrict__ istd,
                                                              const float* __restrict__ gamma,
@@ -596,16 +626,17 @@ __global__ void __launch_bounds__(256) bn_bwd_apply_v_kernel(const bf16* __restr
   float* cbm = sh + C;     // B
   float* cm = sh + 2 * C;  // mean
   float* cd = sh + 3 * C;  // D
+  using VT = Vec8<T>;
   const unsigned stride = gridDim.x * 256u, cv = (unsigned)C / 8;
   unsigned i = blockIdx.x * 256u + threadIdx.x;
-  uint4 dv[U], xv[U], yv[U];
+  typename VT::type dv[U], xv[U], yv[U];
 #pragma unroll
   for (int u = 0; u < U; ++u) {
     const unsigned k = i + u * stride;
     if (k < nv) {
-      dv[u] = ldg16(dy + (size_t)k * 8);
-      xv[u] = ldg16(x + (size_t)k * 8);
-      if (MASK) yv[u] = ldg16(yout + (size_t)k * 8);
+      dv[u] = VT::load(dy + (size_t)k * 8);
+      xv[u] = VT::load(x + (size_t)k * 8);
+      if (MASK) yv[u] = VT::load(yout + (size_t)k * 8);
     }
   }
   for (int c = threadIdx.x; c < C; c += 256) {
@@ -629,14 +660,14 @@ __global__ void __launch_bounds__(256) bn_bwd_apply_v_kernel(const bf16* __restr
   };
   while (true) {
     const unsigned inx = i + U * stride;  // next trip's loads before this trip's stores
-    uint4 dn[U], xn[U], yn[U];
+    typename VT::type dn[U], xn[U], yn[U];
 #pragma unroll
     for (int u = 0; u < U; ++u) {
       const unsigned k = inx + u * stride;
       if (inx < nv && k < nv) {
-        dn[u] = ldg16(dy + (size_t)k * 8);
-        xn[u] = ldg16(x + (size_t)k * 8);
-        if (MASK) yn[u] = ldg16(yout + (size_t)k * 8);
+        dn[u] = VT::load(dy + (size_t)k * 8);
+        xn[u] = VT::load(x + (size_t)k * 8);
+        if (MASK) yn[u] = VT::load(yout + (size_t)k * 8);
       }
     }
 #pragma unroll
@@ -649,17 +680,17 @@ __global__ void __launch_bounds__(256) bn_bwd_apply_v_kernel(const bf16* __restr
         ld8(cbm + c0, B);
         ld8(cm + c0, M);
         ld8(cd + c0, D);
-        unpack8(dv[u], d);
-        unpack8(xv[u], xf);
+        VT::unpack(dv[u], d);
+        VT::unpack(xv[u], xf);
         if (MASK) {
           float yo[8];
-          unpack8(yv[u], yo);
+          VT::unpack(yv[u], yo);
 #pragma unroll
           for (int v = 0; v < 8; ++v) d[v] = yo[v] > 0.f ? d[v] : 0.f;
         }
 #pragma unroll
         for (int v = 0; v < 8; ++v) d[v] = A[v] * d[v] + B[v] * (xf[v] - M[v]) + D[v];
-        *reinterpret_cast<uint4*>(dx + (size_t)k * 8) = pack8(d);
+        VT::store(dx + (size_t)k * 8, d);
       }
     }
     if (inx >= nv) break;
@@ -1072,20 +1103,18 @@ static void bn_apply_t(const T* x, T* y, long R, int C, const float* sums, int p
                        float* save_istd, float* run_mean, float* run_var, float momentum, int use_running,
                        hipStream_t s) {
   const size_t shm = 2 * C * sizeof(float);
-  if constexpr (std::is_same<T, bf16>::value) {
-    if (bn_v_ok(R, C)) {
-      int U, g;
-      const unsigned nv = (unsigned)(R * C / 8);
-      bn_v_launch_shape(nv, &U, &g);
-#define DCNN_BNV(U_, RES_)                                                                                    \
-  if (U == U_ && (residual != nullptr) == RES_)                                                               \
-    hipLaunchKernelGGL((bn_apply_v_kernel<U_, RES_>), dim3(g), dim3(256), shm, s, x, y, nv, C, sums, parts, count, \
+  if (bn_v_ok(R, C)) {
+    int U, g;
+    const unsigned nv = (unsigned)(R * C / 8);
+    bn_v_launch_shape(nv, &U, &g);
+#define DCNN_BNV(U_, RES_)                                                                                       \
+  if (U == U_ && (residual != nullptr) == RES_)                                                                  \
+    hipLaunchKernelGGL((bn_apply_v_kernel<T, U_, RES_>), dim3(g), dim3(256), shm, s, x, y, nv, C, sums, parts, count, \
                        gamma, beta, eps, residual, relu, save_mean, save_istd, run_mean, run_var, momentum, use_running);
-      DCNN_BNV(1, false) DCNN_BNV(2, false) DCNN_BNV(4, false) DCNN_BNV(1, true) DCNN_BNV(2, true) DCNN_BNV(4, true)
+    DCNN_BNV(1, false) DCNN_BNV(2, false) DCNN_BNV(4, false) DCNN_BNV(1, true) DCNN_BNV(2, true) DCNN_BNV(4, true)
 #undef DCNN_BNV
-      DCNN_LAUNCH_CHECK();
-      return;
-    }
+    DCNN_LAUNCH_CHECK();
+    return;
   }
   if (C % 8 == 0) {
     const int g = grid_for(R * C / 8, 256, 2048);
@@ -1114,21 +1143,19 @@ template <typename T>
 static void bn_bwd_apply_t(const T* dy, const T* yout, const T* x, T* dx, long R, int C, const float* mean,
                            const float* istd, const float* gamma, const float* sums, int parts, float count,
                            float* dgamma, float* dbeta, int eval_mode, hipStream_t s) {
-  if constexpr (std::is_same<T, bf16>::value) {
-    if (bn_v_ok(R, C)) {
-      int U, g;
-      const unsigned nv = (unsigned)(R * C / 8);
-      bn_v_launch_shape(nv, &U, &g);
-      const size_t shm4 = 4 * C * sizeof(float);
-#define DCNN_BNBV(U_, MASK_)                                                                                   \
-  if (U == U_ && (yout != nullptr) == MASK_)                                                                   \
-    hipLaunchKernelGGL((bn_bwd_apply_v_kernel<U_, MASK_>), dim3(g), dim3(256), shm4, s, dy, yout, x, dx, nv, C, mean, \
+  if (bn_v_ok(R, C)) {
+    int U, g;
+    const unsigned nv = (unsigned)(R * C / 8);
+    bn_v_launch_shape(nv, &U, &g);
+    const size_t shm4 = 4 * C * sizeof(float);
+#define DCNN_BNBV(U_, MASK_)                                                                                      \
+  if (U == U_ && (yout != nullptr) == MASK_)                                                                      \
+    hipLaunchKernelGGL((bn_bwd_apply_v_kernel<T, U_, MASK_>), dim3(g), dim3(256), shm4, s, dy, yout, x, dx, nv, C, mean, \
                        istd, gamma, sums, parts, count, dgamma, dbeta, eval_mode);
-      DCNN_BNBV(1, false) DCNN_BNBV(2, false) DCNN_BNBV(4, false) DCNN_BNBV(1, true) DCNN_BNBV(2, true) DCNN_BNBV(4, true)
+    DCNN_BNBV(1, false) DCNN_BNBV(2, false) DCNN_BNBV(4, false) DCNN_BNBV(1, true) DCNN_BNBV(2, true) DCNN_BNBV(4, true)
 #undef DCNN_BNBV
-      DCNN_LAUNCH_CHECK();
-      return;
-    }
+    DCNN_LAUNCH_CHECK();
+    return;
   }
   const size_t shm = 5 * C * sizeof(float);
   if (C % 8 == 0) {
