@@ -1,6 +1,8 @@
 // Layers, Sequential, loss, optimizers and the training loop of the C++ host API (dcnn/nn.hpp).
 #include "dcnn/nn.hpp"
 
+#include "../kernels/fusion_plan.h"
+
 #include <algorithm>
 #include <chrono>
 #include <cmath>
@@ -593,35 +595,46 @@ static float act_alpha(int code) { return code == ACT_ELU ? 1.0f : 0.01f; }
 
 bool Activation::is_relu() const { return code_ == ACT_RELU; }
 
+// a layer's kind for the shared fusion planner (csrc/kernels/fusion_plan.h)
+static int fuse_kind(const Layer* l) {
+  if (dynamic_cast<const Conv2D*>(l)) return FK_CONV;
+  if (dynamic_cast<const BatchNorm*>(l)) return FK_BN;
+  if (auto* a = dynamic_cast<const Activation*>(l)) return a->is_relu() ? FK_RELU : FK_ACT;
+  if (auto* p = dynamic_cast<const Pool2D*>(l)) return p->is_max() ? FK_MAXPOOL : FK_OTHER;
+  return FK_OTHER;
+}
+
+static std::vector<int> fuse_kinds(const std::vector<std::unique_ptr<Layer>>& seq) {
+  std::vector<int> k;
+  for (const auto& l : seq) k.push_back(fuse_kind(l.get()));
+  return k;
+}
+
+// the shared planner's decisions (plan_sequence_fusions: the rules the Python layers apply too)
+// wired into this sequence's layers; on = false clears every link
 void fuse_bn_relu(std::vector<std::unique_ptr<Layer>>& seq, bool on) {
-  for (size_t i = 0; i + 1 < seq.size(); ++i)
-    if (auto* conv = dynamic_cast<Conv2D*>(seq[i].get()))
-      conv->set_stats_consumer(on ? dynamic_cast<BatchNorm*>(seq[i + 1].get()) : nullptr);
-  // BatchNorm [+ ReLU] -> Conv2D: the conv's data gradient carries the BN backward epilogue
-  for (size_t i = 0; i + 1 < seq.size(); ++i) {
-    auto* bn = dynamic_cast<BatchNorm*>(seq[i].get());
-    if (bn == nullptr) continue;
-    size_t j = i + 1;
-    auto* act = dynamic_cast<Activation*>(seq[j].get());
-    if (act != nullptr && act->is_relu() && j + 1 < seq.size()) ++j;
-    else if (act != nullptr) continue;
-    if (auto* conv = dynamic_cast<Conv2D*>(seq[j].get())) conv->set_bnb_producer(on ? bn : nullptr);
-  }
-  for (size_t i = 0; i + 1 < seq.size(); ++i) {
-    auto* bn = dynamic_cast<BatchNorm*>(seq[i].get());
-    auto* act = dynamic_cast<Activation*>(seq[i + 1].get());
-    if (bn == nullptr || act == nullptr || !act->is_relu()) continue;
-    bn->set_fused_relu(on);
-    act->set_passthrough(on);
-  }
-  // BatchNorm -> ReLU -> max-pool: the pool runs inside the BatchNorm's training apply
-  for (size_t i = 0; i + 2 < seq.size(); ++i) {
-    auto* bn = dynamic_cast<BatchNorm*>(seq[i].get());
-    auto* act = dynamic_cast<Activation*>(seq[i + 1].get());
-    auto* pool = dynamic_cast<Pool2D*>(seq[i + 2].get());
-    if (bn == nullptr || act == nullptr || !act->is_relu() || pool == nullptr || !pool->is_max()) continue;
-    bn->set_fused_pool(on ? pool : nullptr);
-    pool->set_fused_producer(on ? bn : nullptr);
+  const std::vector<int> f = plan_sequence_fusions(fuse_kinds(seq));
+  for (size_t i = 0; i < seq.size(); ++i) {
+    Layer* l = seq[i].get();
+    if (auto* conv = dynamic_cast<Conv2D*>(l)) {
+      // conv -> BatchNorm: the conv's epilogue emits the BatchNorm's statistics rows
+      conv->set_stats_consumer(on && (f[i] & FF_EMIT_BN_STATS) ? static_cast<BatchNorm*>(seq[i + 1].get()) : nullptr);
+      // BatchNorm [+ ReLU] -> conv: the conv's data gradient carries the BatchNorm backward
+      BatchNorm* prod = nullptr;
+      if (on && (f[i] & FF_BNB_CONSUMER))
+        prod = static_cast<BatchNorm*>(seq[fuse_kind(seq[i - 1].get()) == FK_BN ? i - 1 : i - 2].get());
+      conv->set_bnb_producer(prod);
+    } else if (auto* bn = dynamic_cast<BatchNorm*>(l)) {
+      bn->set_fused_relu(on && (f[i] & FF_FUSE_RELU));
+      // BatchNorm -> ReLU -> max-pool: the pool runs inside the BatchNorm's training apply
+      Pool2D* pool = on && (f[i] & FF_FUSE_POOL) ? static_cast<Pool2D*>(seq[i + 2].get()) : nullptr;
+      bn->set_fused_pool(pool);
+      if (pool) pool->set_fused_producer(bn);
+    } else if (auto* act = dynamic_cast<Activation*>(l)) {
+      act->set_passthrough(on && (f[i] & FF_PASSTHROUGH));
+    } else if (auto* pool = dynamic_cast<Pool2D*>(l)) {
+      if (!on || i < 2 || !(f[i - 2] & FF_FUSE_POOL)) pool->set_fused_producer(nullptr);
+    }
   }
 }
 
@@ -873,14 +886,21 @@ void fuse_blocks(std::vector<std::unique_ptr<Layer>>& seq, bool on) {
   }
 }
 
+// the shared planner's residual rules (plan_residual_fusions; the Python ResidualBlock too)
 BatchNorm* ResidualBlock::dual_shortcut() const {
-  if (short_.empty() || fused_tail() == nullptr) return nullptr;
-  return dynamic_cast<BatchNorm*>(short_.back().get());
+  if (!dev_.is_gpu() ||
+      !(plan_residual_fusions(fuse_kinds(main_), fuse_kinds(short_), act_ == "relu" || act_ == "linear") &
+        RF_DUAL_SHORTCUT))
+    return nullptr;
+  return static_cast<BatchNorm*>(short_.back().get());
 }
 
 BatchNorm* ResidualBlock::fused_tail() const {
-  if (!dev_.is_gpu() || main_.size() < 2 || (act_ != "relu" && act_ != "linear")) return nullptr;
-  return dynamic_cast<BatchNorm*>(main_.back().get());
+  if (!dev_.is_gpu() ||
+      !(plan_residual_fusions(fuse_kinds(main_), fuse_kinds(short_), act_ == "relu" || act_ == "linear") &
+        RF_FUSED_TAIL))
+    return nullptr;
+  return static_cast<BatchNorm*>(main_.back().get());
 }
 
 Tensor ResidualBlock::forward(const Tensor& x, bool training) {

@@ -2,6 +2,8 @@
 #pragma once
 #include <hip/hip_runtime.h>
 #include <stdint.h>
+
+#include "fusion_plan.h"  // the shared fusion planner (both front ends)
 typedef __bf16 bf16;
 
 namespace dcnn {
@@ -165,6 +167,7 @@ enum ConvRoute : int { ROUTE_GENERIC = 0, ROUTE_GEMM_G2 = 1, ROUTE_HALO = 2, ROU
 int conv_fwd_route(ConvRouteGeom g);
 int conv_dgrad_route(ConvRouteGeom g);
 int conv_wgrad_route(ConvRouteGeom g);
+// (the shared fusion planner: fusion_plan.h, included above)
 void splitk_reduce(const float* slab, float* out, long n, int splits, int accumulate, hipStream_t s);
 // weight + bias slabs in one launch (nb = 0: bias segment absent)
 void splitk_reduce2(const float* slab, float* out, long n, const float* bslab, float* bout, long nb, int splits,

@@ -243,6 +243,16 @@ PYBIND11_MODULE(_kernels, m) {
   m.attr("ROUTE_GEMM_G2") = (int)ROUTE_GEMM_G2;
   m.attr("ROUTE_HALO") = (int)ROUTE_HALO;
   m.attr("ROUTE_G1S") = (int)ROUTE_G1S;
+  // the shared fusion planner (fusion_plan.cpp)
+  m.def("plan_sequence_fusions", &plan_sequence_fusions);
+  m.def("plan_residual_fusions", &plan_residual_fusions);
+  for (auto [name, v] : {std::pair<const char*, int>{"FK_OTHER", FK_OTHER}, {"FK_CONV", FK_CONV}, {"FK_BN", FK_BN},
+                         {"FK_RELU", FK_RELU}, {"FK_ACT", FK_ACT}, {"FK_MAXPOOL", FK_MAXPOOL},
+                         {"FF_EMIT_BN_STATS", FF_EMIT_BN_STATS}, {"FF_FUSE_RELU", FF_FUSE_RELU},
+                         {"FF_PASSTHROUGH", FF_PASSTHROUGH}, {"FF_FUSE_POOL", FF_FUSE_POOL},
+                         {"FF_BNB_CONSUMER", FF_BNB_CONSUMER}, {"RF_FUSED_TAIL", RF_FUSED_TAIL},
+                         {"RF_DUAL_SHORTCUT", RF_DUAL_SHORTCUT}})
+    m.attr(name) = v;
   m.def("g1s_rows", &g1s_rows);
   m.def("g1s_enable", &g1s_enable);
   m.def("g1s_set_waves_per_simd", &g1s_set_waves_per_simd);

@@ -19,8 +19,32 @@ from .misc import Activation, MaxPool2D
 from .norm import BatchNorm
 
 
+def fuse_kinds(layers: List[Layer]) -> List[int]:
+    """Layer kinds for the shared fusion planner (csrc/kernels/fusion_plan.h)."""
+    from ...ops._ext import kernels
+    K = kernels()
+    out = []
+    for l in layers:
+        if isinstance(l, Conv2D):
+            out.append(K.FK_CONV)
+        elif isinstance(l, BatchNorm):
+            out.append(K.FK_BN)
+        elif isinstance(l, Activation):
+            out.append(K.FK_RELU if l.activation_name == "relu" else K.FK_ACT)
+        elif isinstance(l, MaxPool2D):
+            out.append(K.FK_MAXPOOL)
+        else:
+            out.append(K.FK_OTHER)
+    return out
+
+
 def plan_fusion(layers: List[Layer], on_gpu: bool) -> None:
-    """Mark cross-layer fusions for the GPU path (no-op on CPU: pure reference semantics)."""
+    """Mark cross-layer fusions for the GPU path (no-op on CPU: pure reference semantics). The
+    rules are the shared planner's (csrc/kernels/fusion_plan.cpp, plan_sequence_fusions) — the
+    C++ host API's nn.cpp applies the same ones: conv -> BatchNorm statistics rows from the conv
+    epilogue, BatchNorm -> ReLU in one apply pass, BatchNorm + ReLU + max-pool (the pool computed by
+    the BatchNorm's forward when the shapes allow it at run time). The backward-BatchNorm requests
+    of BatchNorm [+ ReLU] -> conv are made at run time here (BatchNorm.bwd_bn_spec)."""
     for l in layers:
         if isinstance(l, Conv2D):
             l.emit_bn_stats = False
@@ -32,17 +56,18 @@ def plan_fusion(layers: List[Layer], on_gpu: bool) -> None:
             l.passthrough = False
     if not on_gpu:
         return
-    for a, b in zip(layers[:-1], layers[1:]):
-        if isinstance(a, Conv2D) and isinstance(b, BatchNorm):
-            a.emit_bn_stats = True
-        if isinstance(a, BatchNorm) and isinstance(b, Activation) and b.activation_name == "relu":
-            a.fuse_relu = True
-            b.passthrough = True
-    for a, b, c in zip(layers[:-2], layers[1:-1], layers[2:]):
-        # BatchNorm + ReLU + max-pool (ResNet stem): the pool is computed by the BatchNorm's
-        # forward when the shapes allow it at run time (BatchNorm.forward / MaxPool2D.forward)
-        if isinstance(a, BatchNorm) and a.fuse_relu and b.passthrough and isinstance(c, MaxPool2D):
-            a.fuse_pool = c
+    from ...ops._ext import kernels
+    K = kernels()
+    flags = K.plan_sequence_fusions(fuse_kinds(layers))
+    for i, (l, f) in enumerate(zip(layers, flags)):
+        if isinstance(l, Conv2D) and f & K.FF_EMIT_BN_STATS:
+            l.emit_bn_stats = True
+        if isinstance(l, BatchNorm) and f & K.FF_FUSE_RELU:
+            l.fuse_relu = True
+        if isinstance(l, Activation) and f & K.FF_PASSTHROUGH:
+            l.passthrough = True
+        if isinstance(l, BatchNorm) and f & K.FF_FUSE_POOL:
+            l.fuse_pool = layers[i + 2]
 
 
 class ResidualBlock(Layer):
@@ -55,7 +80,7 @@ class ResidualBlock(Layer):
         self.shortcut_path = list(shortcut_path or [])
         self.activation_type = activation
         self.act = ActivationFactory.create(activation)
-        self._fused = False
+        self._fused = self._dual = False
 
     # structure -------------------------------------------------------------------------
     def sublayers(self) -> List[Layer]:
@@ -108,7 +133,13 @@ class ResidualBlock(Layer):
         plan_fusion(self.main_path, on_gpu)
         plan_fusion(self.shortcut_path, on_gpu)
         act_ok = self.activation_type in ("relu", "none", "linear")
-        self._fused = on_gpu and bool(self.main_path) and isinstance(self.main_path[-1], BatchNorm) and act_ok
+        self._fused = self._dual = False
+        if on_gpu:  # the shared planner's residual rules (fusion_plan.cpp, plan_residual_fusions)
+            from ...ops._ext import kernels
+            K = kernels()
+            rf = K.plan_residual_fusions(fuse_kinds(self.main_path), fuse_kinds(self.shortcut_path), act_ok)
+            self._fused = bool(rf & K.RF_FUSED_TAIL)
+            self._dual = bool(rf & K.RF_DUAL_SHORTCUT)
         if self._fused:
             self.main_path[-1].emit_masked_grad = True
         for l in self.sublayers():
@@ -133,7 +164,7 @@ class ResidualBlock(Layer):
             sp = self.shortcut_path
             # a projection shortcut ending in BatchNorm is applied inside the tail BatchNorm's
             # pass (hip.bn_apply_dual): its normalised output is never written
-            defer = bool(sp) and isinstance(sp[-1], BatchNorm) and self.compute_dtype == torch.bfloat16
+            defer = self._dual and self.compute_dtype == torch.bfloat16
             for l in (sp[:-1] if defer else sp):
                 s = l.forward(s, mb_id)
             if defer:
@@ -206,7 +237,7 @@ class ResidualBlock(Layer):
         from ...ops import fusion, hip
         sp = self.shortcut_path
         pre = getattr(grad, "_bnb", None)
-        bns = sp[-1] if sp and isinstance(sp[-1], BatchNorm) else None
+        bns = sp[-1] if self._dual else None
         if (bns is None or pre is None or pre[0] is not self.main_path[-1] or not fusion.BN_DUAL
                 or isinstance(pre[1], hip.Stats) or grad.dtype != torch.bfloat16
                 or not grad.is_contiguous(memory_format=torch.channels_last)):
