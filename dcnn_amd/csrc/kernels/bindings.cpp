@@ -115,8 +115,11 @@ PYBIND11_MODULE(_kernels, m) {
         [](uintptr_t A, uintptr_t B, unsigned a_bytes, unsigned b_bytes, int NB, int H, int W, int Cs, int N, int ldb,
            std::vector<std::array<int, 3>> taps, uintptr_t bias, uintptr_t stats, int relu, uintptr_t zero_ptr,
            int zero_n, uintptr_t Cf, uintptr_t residual_f, int splits, uintptr_t part, uintptr_t tickets,
-           uintptr_t stream) {
+           uintptr_t stream, std::array<uintptr_t, 4> bnb) {
           HConvArgs a{};
+          // backward-BatchNorm fusion: (y, x, mean, istd), y / x the BatchNorm's fp32 tensors
+          a.bnb.y = P<const bf16*>(bnb[0]); a.bnb.x = P<const bf16*>(bnb[1]);
+          a.bnb.mean = P<const float*>(bnb[2]); a.bnb.istd = P<const float*>(bnb[3]);
           a.splits = splits; a.part = P<float*>(part); a.tickets = P<unsigned*>(tickets);
           a.Cf = P<float*>(Cf); a.residual_f = P<const float*>(residual_f);
           a.zero_ptr = P<float*>(zero_ptr); a.zero_n = zero_n;
@@ -128,7 +131,12 @@ PYBIND11_MODULE(_kernels, m) {
           for (size_t i = 0; i < taps.size(); ++i) { a.tap_dy[i] = taps[i][0]; a.tap_dx[i] = taps[i][1]; a.tap_b[i] = taps[i][2]; }
           a.bias = P<const float*>(bias); a.stats = P<float*>(stats); a.relu = relu;
           return hconv3_f32_try(a, S(stream));
-        });
+        },
+        py::arg("A"), py::arg("B"), py::arg("a_bytes"), py::arg("b_bytes"), py::arg("NB"), py::arg("H"), py::arg("W"),
+        py::arg("Cs"), py::arg("N"), py::arg("ldb"), py::arg("taps"), py::arg("bias"), py::arg("stats"),
+        py::arg("relu"), py::arg("zero_ptr"), py::arg("zero_n"), py::arg("Cf"), py::arg("residual_f"),
+        py::arg("splits"), py::arg("part"), py::arg("tickets"), py::arg("stream"),
+        py::arg("bnb") = std::array<uintptr_t, 4>{0, 0, 0, 0});
   m.def("hconv3_f32_splits", &hconv3_f32_splits);
   m.def("hconv_supported", &hconv_supported);
   m.def("hconv_stat_rows", &hconv_stat_rows);

@@ -587,7 +587,9 @@ __global__ void __launch_bounds__(NW * 64, 8 / NW) hconv3_kernel(HConvArgs p, H3
         }
         float gv[4][8], xh[4][8];  // [j][e]: stored value, and (bnb) stored value * xhat
         if constexpr (F32) {
-          // fp32 output (+ fp32 residual): 32 bytes per lane and channel half
+          // fp32 output (+ fp32 residual): 32 bytes per lane and channel half; with the
+          // backward-BatchNorm fusion (EPI 2) the consuming BatchNorm's fp32 ReLU output (mask) and
+          // input (xhat) come in the same 32-byte rows
           const char* rfb = reinterpret_cast<const char*>(p.residual_f);
           char* cfb = reinterpret_cast<char*>(p.Cf);
           const bool has_rf = p.residual_f != nullptr;
@@ -600,13 +602,33 @@ __global__ void __launch_bounds__(NW * 64, 8 / NW) hconv3_kernel(HConvArgs p, H3
               r1 = *reinterpret_cast<const float4*>(rfb + o + 16);
             }
             const float rf[8] = {r0.x, r0.y, r0.z, r0.w, r1.x, r1.y, r1.z, r1.w};
+            if constexpr (bnb) {
+              float4 y0 = make_float4(1.f, 1.f, 1.f, 1.f), y1 = y0;
+              if (has_y) {
+                y0 = *reinterpret_cast<const float4*>(ybytes + o);
+                y1 = *reinterpret_cast<const float4*>(ybytes + o + 16);
+              }
+              const float4 x0 = *reinterpret_cast<const float4*>(xbytes + o);
+              const float4 x1 = *reinterpret_cast<const float4*>(xbytes + o + 16);
+              const float yf[8] = {y0.x, y0.y, y0.z, y0.w, y1.x, y1.y, y1.z, y1.w};
+              const float xf[8] = {x0.x, x0.y, x0.z, x0.w, x1.x, x1.y, x1.z, x1.w};
 #pragma unroll
-            for (int e = 0; e < 8; ++e) {
-              float f = acc[2 * h + (e >> 2)][j][e & 3] + bv[e];
-              if (has_rf) f += rf[e];
-              if (relu) f = fmaxf(f, 0.f);
-              gv[j][e] = f;
-              xh[j][e] = 0.f;
+              for (int e = 0; e < 8; ++e) {
+                float f = acc[2 * h + (e >> 2)][j][e & 3];
+                if (has_rf) f += rf[e];
+                f = yf[e] > 0.f ? f : 0.f;
+                gv[j][e] = f;
+                xh[j][e] = f * ((xf[e] - mu[e]) * is[e]);
+              }
+            } else {
+#pragma unroll
+              for (int e = 0; e < 8; ++e) {
+                float f = acc[2 * h + (e >> 2)][j][e & 3] + bv[e];
+                if (has_rf) f += rf[e];
+                if (relu) f = fmaxf(f, 0.f);
+                gv[j][e] = f;
+                xh[j][e] = 0.f;
+              }
             }
             *reinterpret_cast<float4*>(cfb + o) = make_float4(gv[j][0], gv[j][1], gv[j][2], gv[j][3]);
             *reinterpret_cast<float4*>(cfb + o + 16) = make_float4(gv[j][4], gv[j][5], gv[j][6], gv[j][7]);
@@ -787,11 +809,11 @@ static int h3_epi(const HConvArgs& a) {
 template <int NW, int WC, int TWC, int HN, int NWI, int PITCH>
 static void launch_h3(const HConvArgs& a, const H3Geo& g, hipStream_t s) {
   const int epi = h3_epi(a);
-  if (a.Cf) {  // fp32 operands (hconv3_f32_try): no backward-BN epilogue
+  if (a.Cf) {  // fp32 operands (hconv3_f32_try)
     if (epi == 1) return launch_h3e<NW, WC, TWC, HN, NWI, PITCH, 1, false, true>(a, g, s);
+    if (epi == 2) return launch_h3e<NW, WC, TWC, HN, NWI, PITCH, 2, false, true>(a, g, s);
     if (epi == 3) return launch_h3e<NW, WC, TWC, HN, NWI, PITCH, 3, false, true>(a, g, s);
-    if (epi == 0) return launch_h3e<NW, WC, TWC, HN, NWI, PITCH, 0, false, true>(a, g, s);
-    throw std::runtime_error("hconv3 fp32: no backward-BatchNorm epilogue");
+    return launch_h3e<NW, WC, TWC, HN, NWI, PITCH, 0, false, true>(a, g, s);
   }
   // (timeline instances: the statistics forward and the plain dgrad)
   if (g.stamps && epi == 1) return launch_h3e<NW, WC, TWC, HN, NWI, PITCH, 1, true>(a, g, s);
@@ -820,7 +842,7 @@ bool hconv3_try(const HConvArgs& a0, hipStream_t s) {
 // ldb / tap_b in fp32 elements, output Cf (+ residual_f), no backward-BN fusion. Presented to the
 // plan as bf16 with 2 Cs channels (see the header comment).
 bool hconv3_f32_try(const HConvArgs& a0, hipStream_t s) {
-  if (!a0.Cf || a0.bnb.x || a0.residual) return false;
+  if (!a0.Cf || a0.residual) return false;  // (bnb.y / bnb.x: fp32 tensors through the bf16 fields)
   HConvArgs a = a0;
   a.Cs = 2 * a0.Cs;
   a.ldb = 2 * a0.ldb;

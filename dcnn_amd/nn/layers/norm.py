@@ -197,7 +197,10 @@ class BatchNorm(ParameterizedLayer):
         if ent is None:
             return None
         x, yout, mean, istd, was_training = ent
-        if not (was_training and x.is_cuda and x.dtype == torch.bfloat16 and x.is_contiguous(memory_format=torch.channels_last)):
+        # (fp32: only the exact-fp32 halo data gradient honours the request; every other producer
+        # ignores it and the BatchNorm runs its own statistics pass)
+        if not (was_training and x.is_cuda and x.dtype in (torch.bfloat16, torch.float32)
+                and x.is_contiguous(memory_format=torch.channels_last)):
             return None
         from ...ops.hip import BnbRequest
         if yout is _POOLED:  # only the max-pool's fused backward can honour this request

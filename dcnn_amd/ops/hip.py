@@ -125,7 +125,7 @@ _NOSPLIT = (1, 0, 0)
 _H3_F32 = os.environ.get("DCNN_H3_F32", "1") == "1"
 # and their weight gradients on the halo wgrad's fp32 instances (DCNN_HW_F32=0: gemm_t2f)
 _HW_F32 = os.environ.get("DCNN_HW_F32", "1") == "1"
-_H3_F32_STATS = {"fwd": 0, "dgrad": 0, "wgrad": 0}
+_H3_F32_STATS = {"fwd": 0, "dgrad": 0, "dgrad_bnb": 0, "wgrad": 0}
 
 
 def _hconv_split(K, NB, H, W, Cs, N, ntaps, device):
@@ -396,11 +396,22 @@ def conv2d_dgrad(dy, wt, x_shape, stride, pad, *, residual=None, bnb=None):
         return dx
     if (f32 and _H3_F32 and len(classes) == 1 and not empty_class and (KH, KW, sh, sw, ph, pw) == (3, 3, 1, 1, 1, 1)
             and len(classes[0][4]) == 9 and K.hconv3_f32_splits(N, OH, OW, Co, Ci, 9)):
-        # exact fp32 data gradient on the persistent halo conv (transposed weights, reversed taps)
+        # exact fp32 data gradient on the persistent halo conv (transposed weights, reversed taps),
+        # with the consuming BatchNorm's ReLU mask + backward statistics in the epilogue when asked
+        fuse32 = (bnb is not None and fusion.BNB and not bnb.pooled and bnb.x.dtype == F32
+                  and tuple(bnb.x.shape) == (N, Ci, H, W) and (bnb.y is None or bnb.y.dtype == F32))
+        rows = K.hconv_stat_rows(N, H, W, 2 * Co, Ci, 9, 0) if fuse32 else 0
+        slab = _empty((rows, 2, Ci), F32, dy.device) if fuse32 else None
+        sums = _empty((2 * Ci,), F32, dy.device) if fuse32 else None  # zeroed in-kernel
         if K.hconv3_f32(dy.data_ptr(), wt.data_ptr(), _nbytes(dy), _nbytes(wt), N, OH, OW, Co, Ci, KH * KW * Co,
-                        [(t[0], t[1], t[3]) for t in classes[0][4]], 0, 0, 0, 0, 0, dx.data_ptr(), ptr(residual),
-                        *_hconv_split(K, N, OH, OW, 2 * Co, Ci, 9, dy.device), st):
+                        [(t[0], t[1], t[3]) for t in classes[0][4]], 0, ptr(slab), 0, ptr(sums),
+                        2 * Ci if fuse32 else 0, dx.data_ptr(), ptr(residual),
+                        *_hconv_split(K, N, OH, OW, 2 * Co, Ci, 9, dy.device), st,
+                        bnb.args() if fuse32 else _NOBNB):
             _H3_F32_STATS["dgrad"] += 1
+            if fuse32:
+                _H3_F32_STATS["dgrad_bnb"] += 1
+                dx._bnb = (bnb.bn, slab, rows, sums)
             return dx
     g2 = K.gemm_g2f if f32 else K.gemm_g2
     fuse = (bnb is not None and fusion.BNB and not bnb.pooled and not f32 and not empty_class and bnb.x.dtype == BF16

@@ -422,3 +422,42 @@ def test_fp32_modes_vs_fp64_cpu_resnet9():
         assert fe < bf and de < bd and ge < bg, (mode, errs)
     # split precision drops the lo*lo product: its forward error sits above the exact mode's
     assert errs["exact"][0] < errs["concat"][0], errs
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("name", ["resnet9_cifar10", "resnet18_tiny_imagenet"])
+def test_fp32_bwd_bn_fusion_matches_unfused(name, monkeypatch):
+    """Exact fp32: the consuming BatchNorm's ReLU mask + backward statistics in the epilogue of the
+    fp32 halo data gradient (hconv3 F32 EPI 2) == the separate statistics pass; the fusion fires.
+    Only summation order differs (fp32), so the gradients agree to fp32-reduction level."""
+    from dcnn_amd.models import INPUT_SHAPES, NUM_CLASSES, create_model
+    from dcnn_amd.nn import LossFactory
+    from dcnn_amd.ops import fusion, hip
+    prev_concat = hip.get_f32_concat()
+    hip.set_f32_concat(False)  # (exact fp32 everywhere: the halo conv's fp32 instances)
+    try:
+        torch.manual_seed(6)
+        C, H, W = INPUT_SHAPES[name]
+        x = torch.randn(16, C, H, W, device="cuda")
+        y = torch.randint(0, NUM_CLASSES[name], (16,), device="cuda")
+        lf = LossFactory.create("softmax_crossentropy")
+        res = {}
+        for fuse in (False, True):
+            monkeypatch.setattr(fusion, "BNB", fuse)
+            m = create_model(name)
+            m.set_seed(12)
+            m.set_device("GPU:0")
+            m.set_compute_dtype(torch.float32)
+            m.initialize()
+            n0 = hip._H3_F32_STATS["dgrad_bnb"]
+            out = m.forward(x, return_on_input_device=False)
+            _, g, _ = lf.loss_and_grad(out, y)
+            m.backward(g)
+            torch.cuda.synchronize()
+            res[fuse] = ([t.float().cpu().clone() for t in m.gradients()], hip._H3_F32_STATS["dgrad_bnb"] - n0)
+    finally:
+        hip.set_f32_concat(prev_concat)
+    (g0, n_off), (g1, n_on) = res[False], res[True]
+    assert n_off == 0 and n_on > 0, (n_off, n_on)
+    whole = torch.cat([(a - b).reshape(-1) for a, b in zip(g0, g1)]).norm() / torch.cat([a.reshape(-1) for a in g0]).norm()
+    assert whole < 1e-4, whole
