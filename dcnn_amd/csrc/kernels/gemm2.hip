@@ -257,21 +257,24 @@ __global__ void __launch_bounds__(256, 2) gemm_g2_kernel(G2Args p) {
     const int gy = rem / p.GW, gx = rem - gy * p.GW;
     return ((long)img * p.OH + gy * p.OSY + ory) * p.OW + gx * p.OSX + orx;
   };
-  // the operands of row + RSTEP are loaded before row's store: a load's wait also waits for every
-  // older store, so loading after the previous row's store would serialise each row on a store
+  // every row's operands are loaded before the first store: a load's wait also waits for every
+  // older store, and one latency per tile instead of one per row matters at 2 waves per SIMD
   const bool has_res = p.residual != nullptr, has_y = bnb && p.bnb.y != nullptr, has_x = bnb && p.stats;
-  uint4 c_res{}, c_y{}, c_x{};
-  auto fetch = [&](int row, uint4& r_, uint4& y_, uint4& x_) {
-    if (row >= BM || m0 + row >= p.M || !col_ok) return;
+  constexpr int NR = BM / RSTEP;       // rows per thread
+  uint4 c_res[NR], c_y[NR], c_x[NR];
+#pragma unroll
+  for (int i = 0; i < NR; ++i) {
+    c_res[i] = c_y[i] = c_x[i] = uint4{0u, 0u, 0u, 0u};
+    const int row = r0 + i * RSTEP;
+    if (m0 + row >= p.M || !col_ok) continue;
     const long o = orow_of(row) * p.ldc + ncol;
-    if (has_res) r_ = *reinterpret_cast<const uint4*>(p.residual + o);
-    if (has_y) y_ = *reinterpret_cast<const uint4*>(p.bnb.y + o);
-    if (has_x) x_ = *reinterpret_cast<const uint4*>(p.bnb.x + o);
-  };
-  fetch(r0, c_res, c_y, c_x);
-  for (int row = r0; row < BM; row += RSTEP) {
-    uint4 n_res{}, n_y{}, n_x{};
-    fetch(row + RSTEP, n_res, n_y, n_x);
+    if (has_res) c_res[i] = *reinterpret_cast<const uint4*>(p.residual + o);
+    if (has_y) c_y[i] = *reinterpret_cast<const uint4*>(p.bnb.y + o);
+    if (has_x) c_x[i] = *reinterpret_cast<const uint4*>(p.bnb.x + o);
+  }
+#pragma unroll
+  for (int i = 0; i < NR; ++i) {
+    const int row = r0 + i * RSTEP;
     const int m = m0 + row;
     if (m < p.M && col_ok) {
       const long orow = orow_of(row);
@@ -279,7 +282,7 @@ __global__ void __launch_bounds__(256, 2) gemm_g2_kernel(G2Args p) {
       unpack8(*reinterpret_cast<const uint4*>(smem + row * T::EPI_PITCH + cg * 16), f);
       if (has_res) {
         float rr[8];
-        unpack8(c_res, rr);
+        unpack8(c_res[i], rr);
 #pragma unroll
         for (int v = 0; v < 8; ++v) f[v] += rr[v];
       }
@@ -289,7 +292,7 @@ __global__ void __launch_bounds__(256, 2) gemm_g2_kernel(G2Args p) {
       }
       if (has_y) {
         float yo[8];
-        unpack8(c_y, yo);
+        unpack8(c_y[i], yo);
 #pragma unroll
         for (int v = 0; v < 8; ++v) f[v] = yo[v] > 0.f ? f[v] : 0.f;
       }
@@ -300,7 +303,7 @@ __global__ void __launch_bounds__(256, 2) gemm_g2_kernel(G2Args p) {
         unpack8(o, g);
         if (bnb) {
           float xv[8];
-          unpack8(c_x, xv);
+          unpack8(c_x[i], xv);
 #pragma unroll
           for (int v = 0; v < 8; ++v) { s[v] += g[v]; q[v] += g[v] * (xv[v] - mu[v]) * is[v]; }
         } else {
@@ -309,9 +312,6 @@ __global__ void __launch_bounds__(256, 2) gemm_g2_kernel(G2Args p) {
         }
       }
     }
-    c_res = n_res;
-    c_y = n_y;
-    c_x = n_x;
   }
   if (p.stats) {
     __syncthreads();
