@@ -59,9 +59,19 @@ def main():
     ap.add_argument("--set", default="r18", choices=["r18", "r50"], help="ResNet-18-tiny or ResNet-50-tiny shapes")
     ap.add_argument("--v3", type=int, default=1, help="third-generation 3x3 halo conv (hconv3.hip) on/off")
     ap.add_argument("--eager", action="store_true", help="time eager launches instead of one hipGraph replay")
+    ap.add_argument("--halo-1x1", type=int, default=1, help="K >= 1024 1x1 convs on the halo kernel (ops/fusion.py)")
+    ap.add_argument("--torch-mm", action="store_true",
+                    help="also time the 1x1 shapes' plain GEMMs on torch.mm (hipBLASLt; no fused statistics)")
+    ap.add_argument("--split-target", type=int, default=None, help="hconv split-K workgroup target (tuning hook)")
+    ap.add_argument("--split-min-work", type=int, default=None, help="hconv least taps x chunks per split")
     a = ap.parse_args()
-    from dcnn_amd.ops import hip
+    from dcnn_amd.ops import hip, fusion
+    if a.split_target is not None:
+        hip.kernels().hconv_set_split_target(a.split_target)
+    if a.split_min_work is not None:
+        hip.kernels().hconv_set_split_min_work(a.split_min_work)
     hip.kernels().hconv3_enable(a.v3)
+    fusion.HCONV_1X1 = bool(a.halo_1x1)
     CL = torch.channels_last
     N = a.batch
     tot = {"fwd": 0.0, "dgrad": 0.0, "wgrad": 0.0}
@@ -90,8 +100,17 @@ def main():
             "dgrad": lambda: hip.conv2d_dgrad(dy, wt, x.shape, (s, s), (p, p)),
             "wgrad": lambda: hip.conv2d_wgrad(dy, x, w.shape, (s, s), (p, p), gw, None),
         }
+        if a.torch_mm and k == 1 and s == 1:
+            xm, dym = x.permute(0, 2, 3, 1).reshape(-1, Ci), dy.permute(0, 2, 3, 1).reshape(-1, Co)  # NHWC rows (views)
+            w2 = w.reshape(Co, Ci)
+            ops["mm_fwd"] = lambda: torch.mm(xm, w2.t())
+            ops["mm_dgrad"] = lambda: torch.mm(dym, w2)
+            ops["mm_wgrad"] = lambda: torch.mm(dym.t(), xm)
+            for o in ("mm_fwd", "mm_dgrad", "mm_wgrad"):
+                hbm[o] = hbm[o[3:]]
+                tot.setdefault(o, 0.0)
         for op, fn in ops.items():
-            if a.only and op != a.only:
+            if a.only and op.replace("mm_", "") != a.only:
                 continue
             if op == "dgrad" and nm == "stem":
                 continue

@@ -69,9 +69,12 @@ __global__ void __launch_bounds__(256, 2) gemm_g2_kernel(G2Args p) {
   const int tiles_n = (p.N + BN - 1) / BN;
   const int lt = xcd_remap2(blockIdx.x, gridDim.x);
   const int tm = lt / tiles_n, tn = lt % tiles_n;
-  const int m0 = tm * BM, n0 = tn * BN;
-  // row class of this tile (grouped strided-dgrad phases; one class otherwise)
-  const int cls = p.ncls > 1 ? m0 / p.cls_rows : 0;
+  // row class of this tile (grouped strided-dgrad phases; one class otherwise). The classes are
+  // interleaved tile row by tile row: each XCD's contiguous share of the remapped grid holds every
+  // phase of the same pixels (the dY rows they share stay in that XCD's L2, and the 4-tap class
+  // is not one XCD's tail)
+  const int cls = p.ncls > 1 ? tm % p.ncls : 0;
+  const int m0 = p.ncls > 1 ? cls * p.cls_rows + (tm / p.ncls) * BM : tm * BM, n0 = tn * BN;
   const int mcls = cls * p.cls_rows;                 // first row of the class
   const int ct0 = p.cls_t0[cls], ntp = p.cls_nt[cls];
   const int ory = p.cls_ory[cls], orx = p.cls_orx[cls];

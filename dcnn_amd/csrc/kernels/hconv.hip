@@ -337,9 +337,8 @@ __global__ void __launch_bounds__(256, 1) hconv_kernel(HConvArgs p) {
   const int nsteps = nchunk * spc;
   // step j's weights live in stage j % NBS; step k + NBS - 1 is issued at the top of step k into
   // the stage step k - 1 consumed. The halo of chunk c + 1 is issued at the first step of chunk
-  // c, >= NBS steps before it is read (host: spc >= NBS), so it is always older than the weight
-  // stage being waited for and the per-step wait counts only weight loads (a halo issued later
-  // in the window only makes the wait conservative).
+  // c ahead of that step's weights, so it is always older than the weight stages a wait leaves
+  // in flight and the per-step wait counts only weight loads.
   constexpr int BU = TPS * T::B_INS;  // weight loads per lane per step
   auto step_ct = [&](int j, int* cj, int* tj) { *cj = j / spc; *tj = (j - *cj * spc) * TPS; };
   load_halo(0, cbase);
@@ -356,12 +355,15 @@ __global__ void __launch_bounds__(256, 1) hconv_kernel(HConvArgs p) {
   int bcur = 0;
   for (int k = 0; k < nsteps; ++k) {
     const int c = k / spc, t0 = (k - c * spc) * TPS;
+    // the next chunk's halo goes out BEFORE this step's weight stage: the end-of-step wait leaves
+    // only the newest (NBS - 2) weight stages in flight, so the halo has landed by the next step
+    // whatever the steps per chunk
+    if (NHB == 2 && t0 == 0 && c + 1 < nchunk) load_halo((c + 1) & 1, cbase + (c + 1) * 64);
     if (k + NBS - 1 < nsteps) {
       int cj, tj;
       step_ct(k + NBS - 1, &cj, &tj);
       load_b(bcur == 0 ? NBS - 1 : bcur - 1, cbase + cj * 64, tj);
     }
-    if (NHB == 2 && t0 == 0 && c + 1 < nchunk) load_halo((c + 1) & 1, cbase + (c + 1) * 64);
     const char* Hs = smem + (NHB == 2 ? (c & 1) : 0) * T_rt.HALO;
 #pragma unroll
     for (int u = 0; u < TPS; ++u) {
