@@ -62,6 +62,7 @@ def main():
     ap.add_argument("--halo-1x1", type=int, default=1, help="K >= 1024 1x1 convs on the halo kernel (ops/fusion.py)")
     ap.add_argument("--torch-mm", action="store_true",
                     help="also time the 1x1 shapes' plain GEMMs on torch.mm (hipBLASLt; no fused statistics)")
+    ap.add_argument("--hwgrad-s2", type=int, default=None, help="3x3 stride-2 wgrad on the stride-2 halo kernel (ops/fusion.py)")
     ap.add_argument("--split-target", type=int, default=None, help="hconv split-K workgroup target (tuning hook)")
     ap.add_argument("--split-min-work", type=int, default=None, help="hconv least taps x chunks per split")
     a = ap.parse_args()
@@ -72,6 +73,8 @@ def main():
         hip.kernels().hconv_set_split_min_work(a.split_min_work)
     hip.kernels().hconv3_enable(a.v3)
     fusion.HCONV_1X1 = bool(a.halo_1x1)
+    if a.hwgrad_s2 is not None:
+        fusion.HWGRAD_S2 = bool(a.hwgrad_s2)
     CL = torch.channels_last
     N = a.batch
     tot = {"fwd": 0.0, "dgrad": 0.0, "wgrad": 0.0}

@@ -661,7 +661,20 @@ void conv_wgrad(const void* dy, const void* x, float* gw, float* gb, const ConvS
     wgrad_reduce(hold, bhold, slab, gw, (long)s.Co * Ng, bslab, gb, s.Co, splits);
     return;
   }
-  if (route == ROUTE_GEMM_G2 && dyb < (1l << 31) && xb < (1l << 31) && P < (1 << 24)) {
+  if (route == ROUTE_HALO_S2) {  // 3x3 stride 2: the stride-2 halo kernel (dY grid OH x OW)
+    const int splits = hwgrad_s2_splits(s.N, s.OH, s.OW, s.C, s.Co);
+    Tensor hold, bhold;
+    float* slab = wgrad_slab(SLAB, (size_t)splits * s.Co * Ng * 4, hold);
+    float* bslab = gb ? wgrad_slab(BSLAB, (size_t)splits * s.Co * 4, bhold) : nullptr;
+    HWArgs a{};
+    a.dY = static_cast<const bf16*>(dy); a.X = static_cast<const bf16*>(x); a.slab = slab; a.bias_slab = bslab;
+    a.dy_bytes = (unsigned)dyb; a.x_bytes = (unsigned)xb;
+    a.NB = s.N; a.H = s.OH; a.W = s.OW; a.Cs = s.C; a.Co = s.Co; a.ntaps = 9;
+    hwgrad_s2(a, splits, cur());
+    wgrad_reduce(hold, bhold, slab, gw, (long)s.Co * Ng, bslab, gb, s.Co, splits);
+    return;
+  }
+  if ((route == ROUTE_GEMM_G2 || route == ROUTE_HALO_S2) && dyb < (1l << 31) && xb < (1l << 31) && P < (1 << 24)) {
     const int splits = gemm_t2_splits(s.Co, Ng, P);
     Tensor hold, bhold;
     float* slab = wgrad_slab(SLAB, (size_t)splits * s.Co * Ng * 4, hold);

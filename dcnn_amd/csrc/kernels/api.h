@@ -118,6 +118,11 @@ bool hwgrad_f32_supported(int NB, int H, int W, int Cs, int Co);
 int hwgrad_f32_splits(int NB, int H, int W, int Cs, int Co);
 void hwgrad_f32(HWArgs a, int splits, hipStream_t s);
 void hwgrad_set_version(int v);  // 2: tap-shift-invariant kernel where it applies, 1: first kernel
+// halo weight gradient of a 3x3 / stride-2 / pad-1 conv (hwgrad.hip): dY H x W (the output grid), X
+// 2H x 2W, plain operands (ldy = Co, ldx = Cs), slab [splits][Co][9 Cs] (+ bias_slab [splits][Co])
+bool hwgrad_s2_supported(int NB, int H, int W, int Cs, int Co);
+int hwgrad_s2_splits(int NB, int H, int W, int Cs, int Co);
+void hwgrad_s2(HWArgs a, int splits, hipStream_t s);
 
 void gemm_nt(const NtArgs& a, hipStream_t s);
 void gemm_g2(const G2Args& a, hipStream_t s);
@@ -163,7 +168,7 @@ int gemm_tn_splits(int M, int N, int P);
 struct ConvRouteGeom {
   int N, C, H, W, Co, KH, KW, SH, SW, PH, PW, OH, OW, g1s_mode;
 };
-enum ConvRoute : int { ROUTE_GENERIC = 0, ROUTE_GEMM_G2 = 1, ROUTE_HALO = 2, ROUTE_G1S = 3 };
+enum ConvRoute : int { ROUTE_GENERIC = 0, ROUTE_GEMM_G2 = 1, ROUTE_HALO = 2, ROUTE_G1S = 3, ROUTE_HALO_S2 = 4 };
 int conv_fwd_route(ConvRouteGeom g);
 int conv_dgrad_route(ConvRouteGeom g);
 int conv_wgrad_route(ConvRouteGeom g);

@@ -174,6 +174,18 @@ PYBIND11_MODULE(_kernels, m) {
           hwgrad(a, splits, S(stream));
         });
   m.def("hwgrad_supported", &hwgrad_supported);
+  m.def("hwgrad_s2_supported", &hwgrad_s2_supported);
+  m.def("hwgrad_s2_splits", &hwgrad_s2_splits);
+  m.def("hwgrad_s2",
+        [](uintptr_t dY, uintptr_t X, uintptr_t slab, uintptr_t bias_slab, unsigned dy_bytes, unsigned x_bytes, int NB,
+           int H, int W, int Cs, int Co, int splits, uintptr_t stream) {
+          HWArgs a{};
+          a.dY = P<const bf16*>(dY); a.X = P<const bf16*>(X); a.slab = P<float*>(slab);
+          a.bias_slab = P<float*>(bias_slab);
+          a.dy_bytes = dy_bytes; a.x_bytes = x_bytes;
+          a.NB = NB; a.H = H; a.W = W; a.Cs = Cs; a.Co = Co; a.ntaps = 9;
+          hwgrad_s2(a, splits, S(stream));
+        });
   m.def("hwgrad_f32",
         [](uintptr_t dY, uintptr_t X, uintptr_t slab, uintptr_t bias_slab, unsigned dy_bytes, unsigned x_bytes, int NB,
            int H, int W, int Cs, int Co, int splits, uintptr_t stream) {
@@ -251,6 +263,7 @@ PYBIND11_MODULE(_kernels, m) {
   m.attr("ROUTE_GEMM_G2") = (int)ROUTE_GEMM_G2;
   m.attr("ROUTE_HALO") = (int)ROUTE_HALO;
   m.attr("ROUTE_G1S") = (int)ROUTE_G1S;
+  m.attr("ROUTE_HALO_S2") = (int)ROUTE_HALO_S2;
   // the shared fusion planner (fusion_plan.cpp)
   m.def("plan_sequence_fusions", &plan_sequence_fusions);
   m.def("plan_residual_fusions", &plan_residual_fusions);

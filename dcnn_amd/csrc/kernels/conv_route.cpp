@@ -45,6 +45,11 @@ int conv_dgrad_route(ConvRouteGeom g) {
 
 int conv_wgrad_route(ConvRouteGeom g) {
   if (same_reach1(g) && g.KH == 3 && g.KW == 3 && hwgrad_supported(g.N, g.H, g.W, g.C, g.Co, 9)) return ROUTE_HALO;
+  // 3x3 stride-2 pad-1 downsampling convs: the stride-2 halo kernel (hwgrad_s2; ResNet-18 b256
+  // 85.0k -> 86.4k img/s over gemm_t2, profiles/experiment_hwgrad_s2_r5.md)
+  if (g.KH == 3 && g.KW == 3 && g.SH == 2 && g.SW == 2 && g.PH == 1 && g.PW == 1 && g.H == 2 * g.OH &&
+      g.W == 2 * g.OW && hwgrad_s2_supported(g.N, g.OH, g.OW, g.C, g.Co))
+    return ROUTE_HALO_S2;
   if (g.C % 8 == 0 && g.Co % 8 == 0 && g.KH * g.KW <= 64) return ROUTE_GEMM_G2;  // gemm_t2
   return ROUTE_GENERIC;
 }

@@ -799,4 +799,249 @@ void hwgrad_f32(HWArgs a, int splits, hipStream_t s) {
   throw std::runtime_error("hwgrad_f32: no kernel for this geometry");
 }
 
+
+// ---------------------------------------------------------------------------------------------
+// Stride-2 halo weight gradient (3x3, pad 1, the downsampling convs of a ResNet stage):
+//
+//   dW[co][t][ci] = sum_p dY[p][co] * X[2 p + off_t][ci]
+//
+// A 64-pixel output tile (TW x TH x IMG) reaches a (2 TH + 1) x (2 TW + 1) input halo per image:
+// staged once in LDS (natural row-major layout, zero-filled borders) and read by all 9 taps at a
+// per-tap row offset dy * (2 TW + 1) + dx from the lane's pixel row 2 y + 1, 2 x + 1 — each lane
+// of a transposing read supplies its own row address, so the stride needs no special layout. The
+// gathered TN GEMM (gemm_t2) instead re-reads dY once per tap column block and gathers X per tap.
+// 64-pixel tiles keep three (dY, halo) stages in LDS (48-52 KB each); the workgroup owns 64 (co)
+// x 9 x 64 (ci) of dW as the stride-1 hwgrad_kernel, split-K slabs reduced by the caller.
+// ---------------------------------------------------------------------------------------------
+template <int TW, int TH, int IMG>
+struct HWGeoS2 {
+  static constexpr int TPX = TH * TW, PX = TPX * IMG;   // output pixels per tile (GEMM K)
+  static constexpr int HW2 = 2 * TW + 1, HPI = (2 * TH + 1) * HW2, HP = IMG * HPI;
+  static constexpr int HNI = (HP + 31) / 32;            // halo glds per wave per tile
+  static constexpr int HPR = HNI * 32;
+  static constexpr int YI = PX / 32;                    // dY glds per lane per tile
+  static constexpr int KS = PX / 32;                    // 32-pixel k-steps per tile
+  static constexpr int STAGE = PX * 128 + HPR * 128;
+  static_assert(PX == 64, "64-pixel tiles");
+};
+
+template <int TW, int TH, int IMG, int NS>
+__global__ void __launch_bounds__(256, 1) hwgrad_s2_kernel(HWArgs p) {
+  prefetch_kernargs<sizeof(HWArgs)>();
+  using G = HWGeoS2<TW, TH, IMG>;
+  constexpr int HNI = G::HNI, HW2 = G::HW2, HPI = G::HPI, HP = G::HP, TPX = G::TPX, PX = G::PX;
+  constexpr int YI = G::YI, KS = G::KS, STAGE = G::STAGE;
+  constexpr int INS = YI + HNI;  // direct-to-LDS loads per lane per tile (the vmcnt unit)
+  constexpr int ET = (NS * STAGE) / (64 * 68 * 4) < 9 ? (NS * STAGE) / (64 * 68 * 4) : 9;  // taps per epilogue pass
+  static_assert(NS == 2 || NS == 3, "2 or 3 stages");
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int co_tiles = p.Co / 64, ci_chunks = p.Cs / 64;
+  const int per_split = co_tiles * ci_chunks;
+  const int lt = xcd_remap_w(blockIdx.x, gridDim.x);
+  const int split = lt / per_split, rem = lt - split * per_split;
+  const int nsplits = gridDim.x / per_split;
+  const int co0 = (rem / ci_chunks) * 64, c0 = (rem % ci_chunks) * 64;
+  const int IH = 2 * p.H, IW = 2 * p.W;  // input grid (p.H x p.W is the output / dY grid)
+
+  const int tx_tiles = p.W / TW, ty_tiles = p.H / TH, tpi = tx_tiles * ty_tiles;
+  const int total_tiles = (p.NB / IMG) * tpi;
+  const int tbeg = split * p.tiles_per_split;
+  const int tend = min(total_tiles, tbeg + p.tiles_per_split);
+  const i32x4 rsY = raw_rsrc(p.dY, p.dy_bytes);
+  const i32x4 rsX = raw_rsrc(p.X, p.x_bytes);
+
+  // ---- dY loader: YI glds per lane, rows (pixels) fixed relative to the tile origin ----
+  const int slot = lane & 7;
+  unsigned y_rel[YI], y_col[YI];
+#pragma unroll
+  for (int i = 0; i < YI; ++i) {
+    const int row = (wid * YI + i) * 8 + (lane >> 3);
+    const int im = row / TPX, r2 = row - im * TPX;
+    y_rel[i] = (unsigned)((im * p.H + r2 / TW) * p.W + r2 % TW);
+    y_col[i] = (unsigned)((co0 + ((slot ^ wswz(row)) * 8)) * 2);
+  }
+  // ---- halo loader: row (im, hy, hx) -> input pixel (2 y0 + hy, 2 x0 + hx), hy / hx from -1 ----
+  int h_rel[HNI], h_hy[HNI], h_hx[HNI];
+#pragma unroll
+  for (int j = 0; j < HNI; ++j) {
+    const int row = (wid * HNI + j) * 8 + (lane >> 3);
+    const int im = row / HPI, r2 = row - im * HPI;
+    const int hy = r2 / HW2 - 1, hx = r2 % HW2 - 1;
+    const bool real = row < HP;
+    h_hy[j] = real ? hy : -(1 << 20);  // padding rows of the buffer: never valid
+    h_hx[j] = hx;
+    h_rel[j] = ((im * IH + hy) * IW + hx) * p.Cs * 2 + (c0 + ((slot ^ wswz(row)) * 8)) * 2;
+  }
+  auto load_tile = [&](int buf, int tile) {
+    char* Ys = smem + buf * STAGE;
+    char* Hs = Ys + PX * 128;
+    const int ig = tile / tpi, tr = tile - ig * tpi;
+    const int y0 = (tr / tx_tiles) * TH, x0 = (tr % tx_tiles) * TW;
+    const int g0 = (ig * IMG * p.H + y0) * p.W + x0;  // tile origin pixel (dY grid)
+#pragma unroll
+    for (int i = 0; i < YI; ++i)
+      glds16w(rsY, Ys + (wid * YI + i) * 1024, (unsigned)(g0 + y_rel[i]) * (unsigned)(p.Co * 2) + y_col[i]);
+    const int gx = ((ig * IMG * IH + 2 * y0) * IW + 2 * x0) * p.Cs * 2;  // halo origin (input grid)
+#pragma unroll
+    for (int j = 0; j < HNI; ++j) {
+      const bool ok = (unsigned)(2 * y0 + h_hy[j]) < (unsigned)IH && (unsigned)(2 * x0 + h_hx[j]) < (unsigned)IW;
+      glds16w(rsX, Hs + (wid * HNI + j) * 1024, ok ? (unsigned)(gx + h_rel[j]) : kOOBw);
+    }
+  };
+
+  // ---- per-lane halo row of the tap (0, 0) for each (k-step, half) pixel quad: input pixel
+  //      (2 y + 1, 2 x + 1) of the halo for output pixel (y, x) ----
+  int hrow[2 * KS];
+#pragma unroll
+  for (int s = 0; s < 2 * KS; ++s) {
+    const int px = (s >> 1) * 32 + 8 * (lane >> 4) + (s & 1) * 4 + ((lane & 15) >> 2);
+    const int im = px / TPX, r2 = px - im * TPX;
+    hrow[s] = im * HPI + (2 * (r2 / TW) + 1) * HW2 + 2 * (r2 % TW) + 1;
+  }
+
+  f32x4 acc[4][9];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int t = 0; t < 9; ++t) acc[i][t] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  const int bcol = wid * 16 + 4 * (lane & 3);  // B column (input channel) this lane reads
+  const bool do_bias = p.bias_slab != nullptr && c0 == 0;
+  float bias_acc = 0.f;
+  const int nt = tend - tbeg;
+  if (nt > 0) load_tile(0, tbeg);
+  if (NS == 3 && nt > 1) load_tile(1, tbeg + 1);
+  if (NS == 3 && nt > 1)
+    asm volatile("s_waitcnt vmcnt(%0)" ::"n"(INS) : "memory");  // tile 0 landed, tile 1 may fly
+  else
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  int cur = 0;
+  for (int it = 0; it < nt; ++it) {
+    if (it + NS - 1 < nt) load_tile(cur == 0 ? NS - 1 : cur - 1, tbeg + it + NS - 1);
+    const char* Ys = smem + cur * STAGE;
+    const char* Hs = Ys + PX * 128;
+    bf16x8 a[2][4], b[2][9];
+    auto read_step = [&](int kk, bf16x8* av, bf16x8* bv) {
+      const int krow = kk * 32 + 8 * (lane >> 4) + ((lane & 15) >> 2);
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int col = i * 16 + 4 * (lane & 3);
+        const bf16x4 lo = tr4(Ys, krow, col), hi = tr4(Ys, krow + 4, col);
+        av[i] = bf16x8{lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+      }
+#pragma unroll
+      for (int t = 0; t < 9; ++t) {
+        const int toff = (t / 3 - 1) * HW2 + (t % 3 - 1);
+        const bf16x4 lo = tr4(Hs, hrow[kk * 2] + toff, bcol), hi = tr4(Hs, hrow[kk * 2 + 1] + toff, bcol);
+        bv[t] = bf16x8{lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+      }
+    };
+    read_step(0, a[0], b[0]);
+#pragma unroll
+    for (int kk = 0; kk < KS; ++kk) {
+      const int c = kk & 1;
+      __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0): step kk's fragments have landed
+      if (kk + 1 < KS) read_step(kk + 1, a[c ^ 1], b[c ^ 1]);
+#pragma unroll
+      for (int t = 0; t < 9; ++t)
+#pragma unroll
+        for (int i = 0; i < 4; ++i) acc[i][t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[c][i], b[c][t], acc[i][t], 0, 0, 0);
+    }
+    if (do_bias) {  // bias gradient: column sums of the staged dY tile (first ci chunk only)
+      const int col = tid & 63, chn = col >> 3, w = (col & 7) * 2;
+      for (int r = tid >> 6; r < PX; r += 4)
+        bias_acc += (float)*reinterpret_cast<const bf16*>(Ys + r * 128 + ((chn ^ wswz(r)) << 4) + w);
+    }
+    if (NS == 3 && it + 2 < nt)
+      asm volatile("s_waitcnt vmcnt(%0)\n\ts_waitcnt lgkmcnt(0)\n\ts_barrier" ::"n"(INS) : "memory");
+    else
+      asm volatile("s_waitcnt vmcnt(0)\n\ts_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+    cur = cur == NS - 1 ? 0 : cur + 1;
+  }
+
+  // ---- slab[split][co][t*Cs + ci] (as hwgrad_kernel) ----
+  const long Ng = 9l * p.Cs;
+  float* out = p.slab + (long)split * p.Co * Ng;
+  float* stg = reinterpret_cast<float*>(smem);
+#pragma unroll
+  for (int t0 = 0; t0 < 9; t0 += ET) {
+    __syncthreads();
+#pragma unroll
+    for (int u = 0; u < ET; ++u) {
+      if (t0 + u < 9) {
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+#pragma unroll
+          for (int r = 0; r < 4; ++r)
+            stg[(u * 64 + i * 16 + (lane >> 4) * 4 + r) * 68 + wid * 16 + (lane & 15)] = acc[i][t0 + u][r];
+      }
+    }
+    __syncthreads();
+    const int nrows = (9 - t0 < ET ? 9 - t0 : ET) * 64;
+    for (int q = tid; q < nrows * 16; q += 256) {
+      const int row = q >> 4, c4 = (q & 15) * 4;
+      const int u = row >> 6, co = co0 + (row & 63);
+      const float4 v = *reinterpret_cast<const float4*>(stg + row * 68 + c4);
+      *reinterpret_cast<float4*>(out + (long)co * Ng + (t0 + u) * p.Cs + c0 + c4) = v;
+    }
+  }
+  if (do_bias) {
+    __syncthreads();
+    stg[tid] = bias_acc;
+    __syncthreads();
+    if (tid < 64) p.bias_slab[(long)split * p.Co + co0 + tid] = stg[tid] + stg[tid + 64] + stg[tid + 128] + stg[tid + 192];
+  }
+  (void)nsplits;
+}
+
+// output-grid tile geometry of the stride-2 kernel: 8 x 8 tiles, or 4 x 4 maps four images a tile
+static bool hw_s2_geometry(int H, int W, int* TH, int* TW, int* IMG) {
+  if (H % 8 == 0 && W % 8 == 0) { *TW = 8; *TH = 8; *IMG = 1; return true; }
+  if (H == 4 && W == 4) { *TW = 4; *TH = 4; *IMG = 4; return true; }
+  return false;
+}
+
+bool hwgrad_s2_supported(int NB, int H, int W, int Cs, int Co) {
+  int th, tw, img;
+  if (Cs % 64 || Co % 64 || !hw_s2_geometry(H, W, &th, &tw, &img) || NB % img) return false;
+  return (long)NB * 4 * H * W * Cs * 2 < (1l << 31) && (long)NB * H * W * Co * 2 < (1l << 31);
+}
+
+int hwgrad_s2_splits(int NB, int H, int W, int Cs, int Co) {
+  int th, tw, img;
+  if (!hw_s2_geometry(H, W, &th, &tw, &img)) return 1;
+  const int total = (NB / img) * (H / th) * (W / tw);
+  const int per_split = (Co / 64) * (Cs / 64);
+  int want = (kHwTargetBlocks + per_split - 1) / per_split;
+  if (want < 1) want = 1;
+  constexpr int min_tps = 4;  // >= 256 pixels per split (64-pixel tiles)
+  if (want > total / min_tps) want = total / min_tps > 1 ? total / min_tps : 1;
+  const int tps = (total + want - 1) / want;
+  return (total + tps - 1) / tps;
+}
+
+void hwgrad_s2(HWArgs a, int splits, hipStream_t s) {
+  if (!hwgrad_s2_supported(a.NB, a.H, a.W, a.Cs, a.Co)) throw std::runtime_error("hwgrad_s2: unsupported shape");
+  if (splits != hwgrad_s2_splits(a.NB, a.H, a.W, a.Cs, a.Co)) throw std::runtime_error("hwgrad_s2: split count mismatch");
+  hw_s2_geometry(a.H, a.W, &a.TH, &a.TW, &a.IMG);
+  const int total = (a.NB / a.IMG) * (a.H / a.TH) * (a.W / a.TW);
+  a.tiles_per_split = (total + splits - 1) / splits;
+  const int grid = splits * (a.Co / 64) * (a.Cs / 64);
+#define DCNN_HWS2(TW_, TH_, IMG_)                                                                      \
+  if (a.TW == TW_ && a.TH == TH_ && a.IMG == IMG_) {                                                   \
+    auto k = hwgrad_s2_kernel<TW_, TH_, IMG_, 3>;                                                      \
+    const int lds = 3 * HWGeoS2<TW_, TH_, IMG_>::STAGE;                                                \
+    DCNN_HIP_CHECK(hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, lds)); \
+    hipLaunchKernelGGL(k, dim3(grid), dim3(256), lds, s, a);                                           \
+    DCNN_LAUNCH_CHECK();                                                                               \
+    return;                                                                                            \
+  }
+  DCNN_HWS2(8, 8, 1)  // 3 x 48 KB
+  DCNN_HWS2(4, 4, 4)  // 3 x 52 KB
+#undef DCNN_HWS2
+  throw std::runtime_error("hwgrad_s2: no variant");
+}
+
 }  // namespace dcnn

@@ -7,4 +7,5 @@ BNB = True           # backward-BatchNorm fusion (ReLU mask + statistics) into t
                      # max-pool backward epilogue, and BatchNorm + ReLU + max-pool in one forward pass
 BN_DUAL = True       # projection-shortcut BatchNorm pairs in one pass (forward apply, backward)
 DEFER_REDUCE = True  # one batched split-K weight-gradient reduce per backward
+HWGRAD_S2 = True     # 3x3 stride-2 weight gradients on the stride-2 halo kernel (else gemm_t2)
 HCONV_1X1 = True     # 1x1 convs on the halo kernel (else the routing table's GEMM choice; test hook)

@@ -535,6 +535,16 @@ def conv2d_wgrad(dy, x, w_shape, stride, pad, grad_w, grad_b=None):
              if Cx == Ci else K.ROUTE_GEMM_G2)
     _rec("wgrad", x=(N, Ci, H, W), xpad=Cx, w=(Co, Ci, KH, KW), stride=tuple(stride), pad=tuple(pad),
          bias=grad_b is not None, route=int(route))
+    if route == K.ROUTE_HALO_S2 and fusion.HWGRAD_S2:
+        # stride-2 halo wgrad: the 64-pixel tile's (2 TH + 1) x (2 TW + 1) input halo staged once for 9 taps
+        Ng = 9 * Ci
+        splits = K.hwgrad_s2_splits(N, OH, OW, Ci, Co)
+        slab = _empty((splits, Co, Ng), F32, x.device)
+        bslab = _empty((splits, Co), F32, x.device) if grad_b is not None else None
+        K.hwgrad_s2(dy.data_ptr(), x.data_ptr(), slab.data_ptr(), ptr(bslab), _nbytes(dy), _nbytes(x), N, OH, OW, Ci,
+                    Co, splits, st)
+        _reduce_wb(K, slab, grad_w, Co * Ng, bslab, grad_b, Co, splits, st)
+        return
     if route == K.ROUTE_HALO:
         # halo-tiled wgrad: X read ~1.4x instead of once per tap
         Ng = KH * KW * Ci

@@ -75,4 +75,5 @@ def test_shared_route_table():
     assert K.conv_dgrad_route(256, 64, 32, 32, 64, 3, 3, 1, 1, 1, 1, 32, 32, 2) == K.ROUTE_HALO
     assert K.conv_dgrad_route(256, 64, 32, 32, 256, 1, 1, 1, 1, 0, 0, 32, 32, 0) == K.ROUTE_G1S
     assert K.conv_wgrad_route(256, 64, 32, 32, 64, 3, 3, 1, 1, 1, 1, 32, 32, -1) == K.ROUTE_HALO
-    assert K.conv_wgrad_route(256, 64, 32, 32, 128, 3, 3, 2, 2, 1, 1, 16, 16, -1) == K.ROUTE_GEMM_G2
+    assert K.conv_wgrad_route(256, 64, 32, 32, 128, 3, 3, 2, 2, 1, 1, 16, 16, -1) == K.ROUTE_HALO_S2  # stride-2 halo
+    assert K.conv_wgrad_route(256, 64, 32, 32, 128, 1, 1, 2, 2, 0, 0, 16, 16, -1) == K.ROUTE_GEMM_G2  # strided 1x1

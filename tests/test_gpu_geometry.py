@@ -197,7 +197,8 @@ def test_recorded_conv_tuples_cover_the_routes():
     assert {"fwd", "dgrad", "wgrad", "stem_fwd", "stem_wgrad"} <= ops, ops
     routes = {(c["op"], c["route"]) for c, _ in tups}
     for r in (("fwd", K.ROUTE_HALO), ("fwd", K.ROUTE_G1S), ("fwd", K.ROUTE_GEMM_G2), ("dgrad", K.ROUTE_HALO),
-              ("dgrad", K.ROUTE_G1S), ("dgrad", K.ROUTE_GEMM_G2), ("wgrad", K.ROUTE_HALO), ("wgrad", K.ROUTE_GEMM_G2)):
+              ("dgrad", K.ROUTE_G1S), ("dgrad", K.ROUTE_GEMM_G2), ("wgrad", K.ROUTE_HALO), ("wgrad", K.ROUTE_GEMM_G2),
+              ("wgrad", K.ROUTE_HALO_S2)):
         assert r in routes, (r, sorted(routes))
     assert any(c["op"] == "dgrad" and c["bnb"] for c, _ in tups)
     assert any(c["op"] == "fwd" and c["stats"] for c, _ in tups)

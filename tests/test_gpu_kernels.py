@@ -778,6 +778,35 @@ def test_hconv_fp32_concat_accuracy(hip, case):
         assert ea < 4 * eb + 1e-7, (ea, eb)
 
 
+@pytest.mark.parametrize("case", [(8, 64, 32, 32, 128), (16, 128, 16, 16, 256), (16, 256, 8, 8, 512), (4, 64, 64, 64, 64),
+                                  (32, 128, 32, 32, 128)])
+@pytest.mark.parametrize("bias", [False, True])
+def test_wgrad_stride2_halo(hip, case, bias, monkeypatch):
+    """3x3 stride-2 weight gradient on the stride-2 halo kernel (hwgrad_s2: 64-pixel tiles, the
+    input halo staged once for all taps) == the gathered gemm_t2 path and the fp32 reference
+    (weights and bias accumulate into the existing gradient: beta = 1)."""
+    from dcnn_amd.ops._ext import kernels
+    N, Ci, H, W, Co = case
+    assert kernels().hwgrad_s2_supported(N, H // 2, W // 2, Ci, Co)
+    torch.manual_seed(10)
+    x = torch.randn(N, Ci, H, W).cuda().to(torch.bfloat16).contiguous(memory_format=CL)
+    dy = torch.randn(N, Co, H // 2, W // 2).cuda().to(torch.bfloat16).contiguous(memory_format=CL)
+    g0 = torch.randn(Co, Ci, 3, 3).cuda().contiguous(memory_format=CL)
+    outs = []
+    for s2 in (True, False):
+        monkeypatch.setattr(fusion, "HWGRAD_S2", s2)
+        gw = g0.clone()
+        gb = torch.ones(Co, device="cuda") if bias else None
+        hip.conv2d_wgrad(dy, x, (Co, Ci, 3, 3), (2, 2), (1, 1), gw, gb)
+        outs.append((gw, gb))
+    ref = torch.nn.grad.conv2d_weight(x.float().cpu(), (Co, Ci, 3, 3), dy.float().cpu(), 2, 1) + g0.cpu()
+    for gw, gb in outs:
+        assert rel_err(gw, ref) < 1e-4, rel_err(gw, ref)
+        if bias:
+            assert rel_err(gb, dy.float().sum((0, 2, 3)) + 1) < 1e-4
+    assert rel_err(outs[0][0], outs[1][0]) < 1e-4
+
+
 @pytest.mark.parametrize("case", [(8, 64, 32, 32, 128, 3, 2, 1), (16, 256, 8, 8, 512, 3, 2, 1), (4, 32, 16, 16, 64, 5, 2, 2),
                                   (8, 64, 16, 16, 128, 1, 2, 0), (16, 256, 8, 8, 512, 1, 2, 0)])
 def test_strided_dgrad_grouped_launch(hip, case, monkeypatch):
