@@ -38,6 +38,8 @@ import torch
 import torch.distributed as dist
 
 sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+# ProcessGroupNCCL's event cache vs collectives recorded under hipGraph capture (dcnn_amd/__init__.py)
+os.environ.setdefault("TORCH_NCCL_CUDA_EVENT_CACHE", "0")
 
 METRIC = "images/sec (whole node) ResNet-18 Tiny-ImageNet training at 1/2/4/8 MI355X"
 ROOT = os.path.dirname(os.path.abspath(__file__))

@@ -67,6 +67,7 @@ def _rccl_worker(rank, port, out, with_pg, use_graph, whole=True):
                       DCNN_DP_FORCE_COLLECTIVES="1")  # world 1 skips the identity all-reduce otherwise
     torch.cuda.set_device(0)
     if with_pg:
+        os.environ.setdefault("TORCH_NCCL_CUDA_EVENT_CACHE", "0")  # (as dcnn_amd/__init__.py)
         dist.init_process_group("nccl", rank=0, world_size=1, device_id=torch.device("cuda", 0))
     from dcnn_amd.models import zoo
     from dcnn_amd.nn import Adam, LossFactory
@@ -209,6 +210,7 @@ def _wire_worker(rank, port, out, backend, grad_dtype):
                       RANK="0", WORLD_SIZE="1", LOCAL_RANK="0")
     torch.cuda.set_device(0)
     if backend == "torch":
+        os.environ.setdefault("TORCH_NCCL_CUDA_EVENT_CACHE", "0")  # (as dcnn_amd/__init__.py)
         dist.init_process_group("nccl", rank=0, world_size=1, device_id=torch.device("cuda", 0))
     from dcnn_amd.models import zoo
     from dcnn_amd.nn import SGD, LossFactory

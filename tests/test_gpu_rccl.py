@@ -57,6 +57,7 @@ def _worker(rank, port, out, backend):
     import torch.distributed as dist
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), DCNN_DP_FORCE_COLLECTIVES="1")
     torch.cuda.set_device(0)
+    os.environ.setdefault("TORCH_NCCL_CUDA_EVENT_CACHE", "0")  # (as dcnn_amd/__init__.py)
     dist.init_process_group("nccl", rank=0, world_size=1, device_id=torch.device("cuda", 0))
     from dcnn_amd.models import zoo
     from dcnn_amd.nn import Adam, LossFactory
