@@ -825,8 +825,10 @@ struct HWGeoS2 {
   static_assert(PX == 64, "64-pixel tiles");
 };
 
-template <int TW, int TH, int IMG, int NS>
-__global__ void __launch_bounds__(256, 1) hwgrad_s2_kernel(HWArgs p) {
+// TSP = 2: 8 waves, two per SIMD — wave w + 4 shares wave w's 16 input channels and takes taps 5..8
+// while wave w takes 0..4 (as hwgrad2_kernel); the first four waves issue the tile loads.
+template <int TW, int TH, int IMG, int NS, int TSP = 1>
+__global__ void __launch_bounds__(256 * TSP, 1) hwgrad_s2_kernel(HWArgs p) {
   prefetch_kernargs<sizeof(HWArgs)>();
   using G = HWGeoS2<TW, TH, IMG>;
   constexpr int HNI = G::HNI, HW2 = G::HW2, HPI = G::HPI, HP = G::HP, TPX = G::TPX, PX = G::PX;
@@ -835,7 +837,8 @@ __global__ void __launch_bounds__(256, 1) hwgrad_s2_kernel(HWArgs p) {
   constexpr int ET = (NS * STAGE) / (64 * 68 * 4) < 9 ? (NS * STAGE) / (64 * 68 * 4) : 9;  // taps per epilogue pass
   static_assert(NS == 2 || NS == 3, "2 or 3 stages");
   extern __shared__ __attribute__((aligned(16))) char smem[];
-  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int tid = threadIdx.x, lane = tid & 63, wid = (tid >> 6) & 3, th = tid >> 8;
+  constexpr int NT = 256 * TSP;
   const int co_tiles = p.Co / 64, ci_chunks = p.Cs / 64;
   const int per_split = co_tiles * ci_chunks;
   const int lt = xcd_remap_w(blockIdx.x, gridDim.x);
@@ -874,6 +877,7 @@ __global__ void __launch_bounds__(256, 1) hwgrad_s2_kernel(HWArgs p) {
     h_rel[j] = ((im * IH + hy) * IW + hx) * p.Cs * 2 + (c0 + ((slot ^ wswz(row)) * 8)) * 2;
   }
   auto load_tile = [&](int buf, int tile) {
+    if (TSP > 1 && th != 0) return;
     char* Ys = smem + buf * STAGE;
     char* Hs = Ys + PX * 128;
     const int ig = tile / tpi, tr = tile - ig * tpi;
@@ -900,14 +904,16 @@ __global__ void __launch_bounds__(256, 1) hwgrad_s2_kernel(HWArgs p) {
     hrow[s] = im * HPI + (2 * (r2 / TW) + 1) * HW2 + 2 * (r2 % TW) + 1;
   }
 
-  f32x4 acc[4][9];
+  auto run = [&](auto tb_c, auto ntw_c) {
+  constexpr int TB = decltype(tb_c)::value, NTW = decltype(ntw_c)::value;
+  f32x4 acc[4][NTW];
 #pragma unroll
   for (int i = 0; i < 4; ++i)
 #pragma unroll
-    for (int t = 0; t < 9; ++t) acc[i][t] = f32x4{0.f, 0.f, 0.f, 0.f};
+    for (int t = 0; t < NTW; ++t) acc[i][t] = f32x4{0.f, 0.f, 0.f, 0.f};
 
   const int bcol = wid * 16 + 4 * (lane & 3);  // B column (input channel) this lane reads
-  const bool do_bias = p.bias_slab != nullptr && c0 == 0;
+  const bool do_bias = p.bias_slab != nullptr && c0 == 0 && th == 0;
   float bias_acc = 0.f;
   const int nt = tend - tbeg;
   if (nt > 0) load_tile(0, tbeg);
@@ -922,7 +928,7 @@ __global__ void __launch_bounds__(256, 1) hwgrad_s2_kernel(HWArgs p) {
     if (it + NS - 1 < nt) load_tile(cur == 0 ? NS - 1 : cur - 1, tbeg + it + NS - 1);
     const char* Ys = smem + cur * STAGE;
     const char* Hs = Ys + PX * 128;
-    bf16x8 a[2][4], b[2][9];
+    bf16x8 a[2][4], b[2][NTW];
     auto read_step = [&](int kk, bf16x8* av, bf16x8* bv) {
       const int krow = kk * 32 + 8 * (lane >> 4) + ((lane & 15) >> 2);
 #pragma unroll
@@ -932,10 +938,10 @@ __global__ void __launch_bounds__(256, 1) hwgrad_s2_kernel(HWArgs p) {
         av[i] = bf16x8{lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
       }
 #pragma unroll
-      for (int t = 0; t < 9; ++t) {
-        const int toff = (t / 3 - 1) * HW2 + (t % 3 - 1);
+      for (int tl = 0; tl < NTW; ++tl) {
+        const int t = TB + tl, toff = (t / 3 - 1) * HW2 + (t % 3 - 1);
         const bf16x4 lo = tr4(Hs, hrow[kk * 2] + toff, bcol), hi = tr4(Hs, hrow[kk * 2 + 1] + toff, bcol);
-        bv[t] = bf16x8{lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+        bv[tl] = bf16x8{lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
       }
     };
     read_step(0, a[0], b[0]);
@@ -945,7 +951,7 @@ __global__ void __launch_bounds__(256, 1) hwgrad_s2_kernel(HWArgs p) {
       __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0): step kk's fragments have landed
       if (kk + 1 < KS) read_step(kk + 1, a[c ^ 1], b[c ^ 1]);
 #pragma unroll
-      for (int t = 0; t < 9; ++t)
+      for (int t = 0; t < NTW; ++t)
 #pragma unroll
         for (int i = 0; i < 4; ++i) acc[i][t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[c][i], b[c][t], acc[i][t], 0, 0, 0);
     }
@@ -970,28 +976,36 @@ __global__ void __launch_bounds__(256, 1) hwgrad_s2_kernel(HWArgs p) {
     __syncthreads();
 #pragma unroll
     for (int u = 0; u < ET; ++u) {
-      if (t0 + u < 9) {
+      const int tl = t0 + u - TB;  // this wave's accumulator slot of tap t0 + u
+      if (t0 + u < 9 && tl >= 0 && tl < NTW) {
 #pragma unroll
         for (int i = 0; i < 4; ++i)
 #pragma unroll
           for (int r = 0; r < 4; ++r)
-            stg[(u * 64 + i * 16 + (lane >> 4) * 4 + r) * 68 + wid * 16 + (lane & 15)] = acc[i][t0 + u][r];
+            stg[(u * 64 + i * 16 + (lane >> 4) * 4 + r) * 68 + wid * 16 + (lane & 15)] = acc[i][tl][r];
       }
     }
     __syncthreads();
     const int nrows = (9 - t0 < ET ? 9 - t0 : ET) * 64;
-    for (int q = tid; q < nrows * 16; q += 256) {
+    for (int q = tid; q < nrows * 16; q += NT) {
       const int row = q >> 4, c4 = (q & 15) * 4;
       const int u = row >> 6, co = co0 + (row & 63);
       const float4 v = *reinterpret_cast<const float4*>(stg + row * 68 + c4);
       *reinterpret_cast<float4*>(out + (long)co * Ng + (t0 + u) * p.Cs + c0 + c4) = v;
     }
   }
-  if (do_bias) {
+  if (p.bias_slab != nullptr && c0 == 0) {  // (every wave passes the same barriers)
     __syncthreads();
-    stg[tid] = bias_acc;
+    if (tid < 256) stg[tid] = bias_acc;
     __syncthreads();
     if (tid < 64) p.bias_slab[(long)split * p.Co + co0 + tid] = stg[tid] + stg[tid + 64] + stg[tid + 128] + stg[tid + 192];
+  }
+  };
+  if constexpr (TSP == 1) {
+    run(std::integral_constant<int, 0>{}, std::integral_constant<int, 9>{});
+  } else {
+    if (th == 0) run(std::integral_constant<int, 0>{}, std::integral_constant<int, 5>{});
+    else run(std::integral_constant<int, 5>{}, std::integral_constant<int, 4>{});
   }
   (void)nsplits;
 }
@@ -1031,10 +1045,10 @@ void hwgrad_s2(HWArgs a, int splits, hipStream_t s) {
   const int grid = splits * (a.Co / 64) * (a.Cs / 64);
 #define DCNN_HWS2(TW_, TH_, IMG_)                                                                      \
   if (a.TW == TW_ && a.TH == TH_ && a.IMG == IMG_) {                                                   \
-    auto k = hwgrad_s2_kernel<TW_, TH_, IMG_, 3>;                                                      \
+    auto k = hwgrad_s2_kernel<TW_, TH_, IMG_, 3, 2>;                                                   \
     const int lds = 3 * HWGeoS2<TW_, TH_, IMG_>::STAGE;                                                \
     DCNN_HIP_CHECK(hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, lds)); \
-    hipLaunchKernelGGL(k, dim3(grid), dim3(256), lds, s, a);                                           \
+    hipLaunchKernelGGL(k, dim3(grid), dim3(512), lds, s, a);                                           \
     DCNN_LAUNCH_CHECK();                                                                               \
     return;                                                                                            \
   }
