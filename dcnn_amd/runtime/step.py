@@ -186,6 +186,9 @@ class TrainStep:
             torch.cuda.synchronize()
         segs, fires = self._segments()
         self._segs, self._fires = segs, fires
+        # thread_local capture (as the whole-step graph): ProcessGroupNCCL's watchdog thread queries
+        # eager collectives' events while a segment is being captured; in the global mode that
+        # query invalidates the capture ("operation not permitted when stream is capturing")
         self.graphs = []
         pool = None
         self.opt.prepare_step()  # upload scalars used during capture (replays re-upload)
@@ -197,7 +200,8 @@ class TrainStep:
         try:
             for k, (hi, lo) in enumerate(segs):
                 g = torch.cuda.CUDAGraph()
-                with capture_guard(), torch.cuda.graph(g, pool=pool, stream=self._capture_stream()):
+                with capture_guard(), torch.cuda.graph(g, pool=pool, stream=self._capture_stream(),
+                                                       capture_error_mode="thread_local"):
                     if k == 0:
                         self.opt.clear_gradients()
                         out = self.dp.forward(self._static_x)
@@ -218,7 +222,8 @@ class TrainStep:
                 self.graphs.append(g)
             if active:
                 g = torch.cuda.CUDAGraph()
-                with capture_guard(), torch.cuda.graph(g, pool=pool, stream=self._capture_stream()):
+                with capture_guard(), torch.cuda.graph(g, pool=pool, stream=self._capture_stream(),
+                                                       capture_error_mode="thread_local"):
                     self.opt.launch_step()
                 self.graphs.append(g)
         finally:
