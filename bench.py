@@ -10,8 +10,9 @@ weights, Adam, softmax cross-entropy. Data parallel over RCCL, one process per G
       --master-port 29500 bench.py --gpus 8 --steps 50 --warmup 10
 
 Weak scaling: every rank trains --batch images per step (global batch = batch x gpus). The
-gradient all-reduce is bucketed, overlaps the backward and is captured in the step graph; it runs
-on torch.distributed's ProcessGroupNCCL (RCCL) by default, or on the framework's own RCCL
+gradient all-reduce is bucketed, overlaps the backward and is captured in the step graph. On the
+C++ engine (the default) it runs on the in-tree RCCL communicator; on the Python engine on
+torch.distributed's ProcessGroupNCCL (RCCL) by default, or on the framework's own RCCL
 communicator (parallel/rccl.py, no c10d) with --dp-backend rccl.
 Exactly K steps are timed between a barrier + device synchronisation on both sides; the
 slowest rank's time is reported. Every timed step runs the full forward, loss, backward,
@@ -19,14 +20,14 @@ gradient all-reduce and optimizer update.
 
 Engines: the same step on the C++ host API (bin/tiny_imagenet_resnet18: the framework's own
 Tensor, flows and gpu::Graph capture; no torch in the timed process; one child process per rank
-under the same launcher variables, the gradient mean over the in-tree RCCL communicator inside the
-captured step) or on the Python front end (torch tensors, torch.cuda graphs). --engine auto (the
-default) picks the C++ engine for ResNet-18 on a single GPU at batch <= 256 (same-box A/B,
-profiles/engine_ab_r5.md: b256 85.1k vs 85.1k, b64 36.2k vs 35.8k img/s) and the Python one for
-N > 1 (its torch.distributed ProcessGroupNCCL path is the one exercised at world > 1 so far; the C++
-engine's bucketed, overlapped RCCL mean has run at world 1 only), and for ResNet-50 and larger
-batches (Python 1-2% faster there); a single-GPU C++ run that fails falls back to the Python
-engine.
+under the same launcher variables; at N > 1 rank 0's weights are broadcast and the bucketed,
+overlapped gradient mean runs over the in-tree RCCL communicator (dcnn/dist.hpp) inside the captured
+step) or on the Python front end (torch tensors, torch.cuda graphs). --engine auto (the default)
+picks the C++ engine for ResNet-18/34 at batch <= 256 at EVERY N, so the 1- and N-GPU points of the
+scaling curve come from the same code (same-box A/B at N = 1: profiles/engine_ab_r5.md), and the
+Python one for ResNet-50 and larger batches (1-2% faster there). A C++ run that fails on any rank
+(the ranks agree over a CPU-only gloo group of this launcher process; no GPU work in it) falls back
+to the Python engine on every rank.
 """
 import argparse
 import json
@@ -51,54 +52,95 @@ METRIC = "images/sec (whole node) ResNet-18 Tiny-ImageNet training at 1/2/4/8 MI
 ROOT = os.path.dirname(os.path.abspath(__file__))
 
 
+class NativeFailed(Exception):
+    pass
+
+
+def _agree_group(timeout_s):
+    """A CPU-only gloo group of the launcher processes (no GPU): the ranks' agreement on whether
+    every C++ child succeeded."""
+    import datetime
+    os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+    os.environ.setdefault("MASTER_PORT", "29533")
+    dist.init_process_group("gloo", timeout=datetime.timedelta(seconds=timeout_s))
+
+
 def native_main(a):
-    """--engine native: the timed steps run in the C++ trainer (one child process per rank, the
-    launcher's RANK / WORLD_SIZE / LOCAL_RANK / MASTER_* passed through); its JSON line becomes this
-    contract's line on rank 0."""
+    """The timed steps run in the C++ trainer (one child process per rank, the launcher's RANK /
+    WORLD_SIZE / LOCAL_RANK / MASTER_* passed through; the child's own rendezvous at MASTER_PORT +
+    17); its JSON line becomes this contract's line on rank 0. Raises NativeFailed (on every rank)
+    when any rank's child failed."""
     import subprocess
     world, rank = int(os.environ.get("WORLD_SIZE", "1")), int(os.environ.get("RANK", "0"))
     if a.gpus != world and world > 1:
         raise SystemExit(f"--gpus {a.gpus} but WORLD_SIZE={world}")
-    if a.device != "cuda" or a.dtype != "bf16":
-        raise SystemExit("--engine native: bf16 on GPUs only")
-    cmd = [os.path.join(ROOT, "dcnn_amd", "bin", "tiny_imagenet_resnet18"), "--device", "GPU", "--model", a.model,
+    if (a.device, a.dtype) not in (("cuda", "bf16"), ("cpu", "fp32")):
+        raise SystemExit("--engine native: bf16 on GPUs (or the fp32 CPU backend)")
+    model = a.model
+    if os.environ.get("DCNN_BENCH_FAULT_RANK") == str(rank):  # (tests: this rank's child fails)
+        model = "no_such_model"
+    cmd = [os.path.join(ROOT, "dcnn_amd", "bin", "tiny_imagenet_resnet18"), "--device",
+           "GPU" if a.device == "cuda" else "CPU", "--model", model,
            "--batch", str(a.batch), "--steps", str(a.steps), "--warmup", str(a.warmup), "--loss", "softmax_ce",
            "--bench"] + (["--dp"] if world > 1 else [])
     env = dict(os.environ)
     env.setdefault("MASTER_ADDR", "127.0.0.1")
     env.setdefault("MASTER_PORT", "29533")
-    r = subprocess.run(cmd, env=env, stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True)
-    if r.returncode != 0:
-        print(r.stdout[-2000:] + r.stderr[-4000:], file=sys.stderr, flush=True)
-        raise SystemExit(r.returncode)
+    env.setdefault("DCNN_DP_BUCKET_MB", str(a.bucket_mb))
+    env.setdefault("DCNN_DIST_TIMEOUT", "180")
+    if world > 1:
+        _agree_group(a.native_timeout + 300)
+    ok, out, err = False, "", ""
+    try:
+        r = subprocess.run(cmd, env=env, stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True,
+                           timeout=a.native_timeout)
+        ok, out, err = r.returncode == 0, r.stdout, r.stderr
+        if not ok:
+            err += f"\n[bench] rank {rank}: C++ engine exited {r.returncode}"
+    except subprocess.TimeoutExpired as e:
+        out = e.stdout.decode() if isinstance(e.stdout, bytes) else (e.stdout or "")
+        err = (e.stderr.decode() if isinstance(e.stderr, bytes) else (e.stderr or "")) + \
+            f"\n[bench] rank {rank}: C++ engine timed out after {a.native_timeout} s"
+    lines = [l for l in out.splitlines() if l.startswith("{")]
+    ok = ok and (rank != 0 or bool(lines))
+    if world > 1:
+        flag = torch.tensor([1 if ok else 0], dtype=torch.int32)
+        dist.all_reduce(flag, op=dist.ReduceOp.MIN)
+        all_ok = bool(flag.item())
+        dist.destroy_process_group()
+    else:
+        all_ok = ok
+    if not all_ok:
+        print(out[-2000:] + err[-4000:], file=sys.stderr, flush=True)
+        raise NativeFailed(f"rank {rank}: {'ok' if ok else 'failed'}; another rank failed" if ok else f"rank {rank} failed")
     if rank != 0:
         return
-    d = json.loads([l for l in r.stdout.splitlines() if l.startswith("{")][-1])
+    d = json.loads(lines[-1])
     from dcnn_amd.models import INPUT_SHAPES
     C, H, W = INPUT_SHAPES[a.model]
     print(json.dumps({
         "metric": METRIC if a.model == "resnet18_tiny_imagenet" else f"images/sec (whole node) {a.model} training",
         "value": round(d["value"], 2), "unit": "images/sec", "n_gpus": world, "steps": a.steps, "warmup": a.warmup,
         "ms_per_step": round(d["ms_per_step"], 4), "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
-        "dtype": "bf16", "data": f"synthetic (random {H}x{W}x{C} inputs + random labels, random init)",
+        "dtype": a.dtype, "data": d.get("data", f"synthetic {H}x{W}x{C}"),
         "config": {"model": a.model, "global_batch": a.batch * world, "per_gpu_batch": a.batch, "seq_len": None,
                    "image_size": [C, H, W], "parallelism": f"dp{world}", "optimizer": "adam",
                    "grad_allreduce": "fp32" if world > 1 else None, "data_plane": d.get("data_parallel"),
+                   "dp_buckets": d.get("dp_buckets") if world > 1 else None,
                    "hipgraph": d.get("hipgraph"), "final_loss": round(d.get("loss", float("nan")), 4),
                    "f32_mode": None, "engine": "native (C++ host API)"},
     }), flush=True)
 
 
 def auto_native(a):
-    """--engine auto: the C++ engine covers this run (one GPU process, bf16, the default step
-    options, a model of the C++ factory, the trainer binary built)."""
+    """--engine auto: the C++ engine covers this run (bf16 on GPUs, the default step options, a
+    model of the C++ factory at batch <= 256, the trainer binary built), at any N."""
     world = int(os.environ.get("WORLD_SIZE", "1"))
-    default_step = (a.graph == 1 and not a.pg and not a.profile and a.grad_dtype == "fp32"
-                    and a.dp_backend == "torch" and a.bucket_mb == 4.0)
-    return (world == 1 and a.gpus == 1 and a.device == "cuda" and a.dtype == "bf16" and default_step
+    default_step = (a.graph == 1 and not a.pg and not a.profile and a.grad_dtype == "fp32")
+    return (a.gpus == world and a.device == "cuda" and a.dtype == "bf16" and default_step
             and a.model in ("resnet18_tiny_imagenet", "resnet34_tiny_imagenet") and a.batch <= 256
             and os.access(os.path.join(ROOT, "dcnn_amd", "bin", "tiny_imagenet_resnet18"), os.X_OK)
-            and torch.cuda.device_count() > 0)
+            and torch.cuda.device_count() >= world)
 
 
 def main():
@@ -122,7 +164,10 @@ def main():
                          "be built)")
     ap.add_argument("--engine", default=os.environ.get("DCNN_BENCH_ENGINE", "auto"), choices=["auto", "python", "native"],
                     help="native: the C++ host API trainer; python: the Python front end's captured step; auto "
-                         "(default): native on one GPU (falls back to python if it fails), python for N > 1")
+                         "(default): native for ResNet-18/34 at any N (python if it fails on any rank), python "
+                         "otherwise")
+    ap.add_argument("--native-timeout", type=int, default=int(os.environ.get("DCNN_BENCH_NATIVE_TIMEOUT", "420")),
+                    help="seconds the C++ engine's run may take before it counts as failed")
     ap.add_argument("--profile", action="store_true", help="print per-layer device times")
     ap.add_argument("--device", default="cuda")
     ap.add_argument("--dtype", default="bf16", choices=["bf16", "fp32"],
@@ -135,12 +180,15 @@ def main():
                          "split = 3xbf16 on the gathered GEMMs too")
     a = ap.parse_args()
     if a.engine == "native":
-        return native_main(a)
+        try:
+            return native_main(a)
+        except NativeFailed as e:
+            raise SystemExit(f"[bench] C++ engine failed: {e}")
     if a.engine == "auto" and auto_native(a):
         try:
             return native_main(a)
-        except SystemExit as e:  # (one process: nothing else depends on this rank's plane)
-            print(f"[bench] C++ engine failed ({e.code}); running the Python engine", file=sys.stderr, flush=True)
+        except NativeFailed as e:  # (every rank raises: the agreement above)
+            print(f"[bench] C++ engine failed ({e}); running the Python engine", file=sys.stderr, flush=True)
 
     from dcnn_amd.parallel.dp import DataParallel, init_distributed
     from dcnn_amd.parallel.rccl import env_rank_world

@@ -1,6 +1,7 @@
 // Data parallelism of the C++ host API: one process per GPU, gradients all-reduced over the
 // in-tree RCCL communicator (csrc/kernels/collective.h) on the calling thread's flow, so the
-// collective is part of a captured training step (TrainGraph::set_gradient_hook).
+// collective is part of a captured training step (TrainGraph::set_gradient_hook); on the CPU
+// device the same schedule runs over a TCP ring of the processes (HostRing).
 //
 // Launch: the torch.distributed launcher's variables (RANK, WORLD_SIZE, LOCAL_RANK, MASTER_ADDR,
 // MASTER_PORT) — `python -m torch.distributed.run --nproc-per-node N ... <program>` or any script
@@ -30,31 +31,73 @@ struct Env {
   int rank = 0, world = 1, local_rank = 0;
   std::string addr = "127.0.0.1";
   int port = 29500;
-  static Env from_env();  // defaults: a single process
+  double timeout_s = 120.0;  // rendezvous / host-plane wait limit (DCNN_DIST_TIMEOUT)
+  static Env from_env();     // defaults: a single process
 };
 
-// the 128-byte RCCL unique id of rank 0 on every rank (TCP at e.addr : e.port + port_offset)
-std::string exchange_unique_id(const Env& e, int port_offset = 17, double timeout_s = 120.0);
+// the 128-byte RCCL unique id of rank 0 on every rank (TCP at e.addr : e.port + port_offset);
+// every wait — rank 0 for the other ranks, a rank for rank 0 — ends after e.timeout_s with an error
+std::string exchange_unique_id(const Env& e, int port_offset = 17);
 
+// Host data plane of the CPU device: a TCP ring of the ranks' processes (rank r sends to r + 1 and
+// receives from r - 1). Rendezvous at e.addr : e.port + port_offset: rank 0 collects every rank's
+// listening address and hands out the table, then each rank connects to its successor. All
+// reductions run in a fixed order (ring reduce-scatter + all-gather over W chunks), so every rank
+// ends with bitwise the same result and reruns are deterministic.
+class HostRing {
+ public:
+  HostRing(const Env& e, int port_offset);
+  ~HostRing();
+  HostRing(const HostRing&) = delete;
+  HostRing& operator=(const HostRing&) = delete;
+  int rank() const { return rank_; }
+  int world() const { return world_; }
+  enum Op { kSum, kMax };
+  void all_reduce(float* x, size_t n, Op op = kSum);
+  void broadcast(void* x, size_t nbytes, int root = 0);  // down the ring from `root`
+  void barrier();
+
+ private:
+  int rank_ = 0, world_ = 1;
+  int next_ = -1, prev_ = -1;  // sockets: to rank + 1, from rank - 1
+  double timeout_s_ = 120.0;
+  // send `sn` bytes to the successor while receiving `rn` from the predecessor (poll-driven, so a
+  // ring of blocking senders cannot deadlock)
+  void exchange(const char* s, size_t sn, char* r, size_t rn);
+};
+
+// Data parallelism over the processes of one job: the mean of the model's gradients over the
+// ranks between the backward and the optimizer. GPU: the in-tree RCCL communicator on GPU
+// local_rank, inside the captured step. CPU: the HostRing above (same bucket schedule, host
+// reduction), so the schedule and the rendezvous run multi-process in CPU CI.
 class DataParallel {
  public:
-  // selects GPU local_rank, rendezvous, creates the communicator (every rank must construct it)
-  explicit DataParallel(const Env& e, int port_offset = 17);
+  // selects GPU local_rank (GPU), rendezvous, creates the plane (every rank must construct it)
+  DataParallel(const Env& e, Device dev, int port_offset = 17);
+  explicit DataParallel(const Env& e, int port_offset = 17) : DataParallel(e, Device::gpu(e.local_rank), port_offset) {}
   ~DataParallel();
   int rank() const { return env_.rank; }
   int world() const { return env_.world; }
-  // in place: data <- mean over ranks (fp32), on the current flow (capturable)
+  Device device() const { return dev_; }
+  const char* plane() const { return dev_.is_gpu() ? "rccl" : "tcp"; }
+  // in place: data <- mean over ranks (fp32); GPU: device memory, on the current flow (capturable)
   void all_reduce_mean(float* data, size_t n);
   // host scalar maximum over ranks (e.g. the slowest rank's step time)
   double max(double v);
+  // every rank has reached this point (GPU: and the current flow's work so far has completed)
+  void barrier();
+  // rank 0's parameter values (and bf16 shadows, BatchNorm running statistics) on every rank, so
+  // replicas start identical whatever each rank's seed or checkpoint was
+  void broadcast_parameters(Sequential& model);
 
-  // Overlapped bucketed gradient mean over `model`'s GPU parameter arena (the Python plane's
-  // scheme, parallel/dp.py): the flat gradient is cut at top-level layer boundaries into buckets
-  // of >= bucket_mb; each bucket's mean starts on this communicator's own flow as soon as the
-  // backward has produced it (the layer hook, after the weight-gradient reduces queued so far are
-  // flushed), while the earlier layers' backward continues on the compute flow; finish() reduces
-  // the rest and makes the current flow wait for every bucket. Fork / join are events, so the
-  // whole pattern is captured into a training step graph.
+  // Overlapped bucketed gradient mean over `model`'s parameters (the Python plane's scheme,
+  // parallel/dp.py): the gradients are cut at top-level layer boundaries into buckets of
+  // >= bucket_mb; a bucket's mean starts as soon as the backward has produced it (the layer hook).
+  // GPU: the parameters live in one arena, a bucket is a contiguous range whose mean runs on this
+  // communicator's own flow (after the weight-gradient reduces queued so far are flushed) while
+  // the earlier layers' backward continues; finish() reduces the rest and makes the current flow
+  // wait for every bucket. Fork / join are events, so the pattern is captured into a step graph.
+  // CPU: a bucket's gradients are packed, ring-reduced and unpacked at the hook (synchronously).
   void attach(Sequential& model, double bucket_mb = 4.0);
   void on_layer_done(size_t layer);  // Sequential::set_backward_hook
   void finish();                     // between the backward and the optimizer
@@ -62,17 +105,22 @@ class DataParallel {
 
  private:
   Env env_;
+  Device dev_;
   std::unique_ptr<coll::Comm> comm_;
+  std::unique_ptr<HostRing> ring_;
   Tensor scratch_;
-  // overlap state: gradient base, per top-level layer the first arena element of its parameters
-  // (SIZE_MAX: none), the reduced suffix [reduced_lo, n)
+  // bucket state: per top-level layer its gradient segments (GPU: the first arena element of its
+  // parameters, SIZE_MAX = none), layers [next_, L) already reduced this step
   float* g_ = nullptr;
-  size_t n_ = 0, reduced_lo_ = 0, bucket_elems_ = 0;
+  size_t n_ = 0, reduced_lo_ = 0, bucket_elems_ = 0, next_ = 0;
   std::vector<size_t> lo_;
+  std::vector<std::vector<std::pair<float*, size_t>>> segs_;
+  std::vector<size_t> layer_elems_;
+  std::vector<float> pack_;
   void* flow_ = nullptr;  // gpu::Flow
   void* ev_ = nullptr;    // gpu::Event
   int nb_ = 0, nb_last_ = 0;
-  void fork_bucket(size_t lo, size_t hi);
+  void reduce_layers(size_t lo_layer, size_t hi_layer);
 };
 
 // One direction of a stage-to-stage device data plane (the native pipeline's transport "rccl",

@@ -57,8 +57,13 @@ void TrainGraph::capture(const Tensor& x, const Tensor& labels) {
   std::vector<Param*> params = model_.parameters();
   ParamArena* a = params.empty() ? nullptr : params[0]->arena.get();
   if (!a) throw std::runtime_error("TrainGraph: the model's parameters are not in a GPU arena");
-  // the warm-up steps must not train: snapshot what they change (parameters, moments, shadow)
+  // the warm-up steps must not train: snapshot what they change (parameters, moments, shadow,
+  // BatchNorm running statistics)
   const Tensor v0 = a->value.clone(), m0 = a->m.clone(), w0 = a->v.clone(), s0 = a->shadow.clone();
+  std::vector<std::pair<Tensor, Tensor>> bn0;  // (live buffer, its snapshot)
+  for (BatchNorm* bn : model_.batchnorms())
+    for (Tensor* t : {&bn->running_mean, &bn->running_var})
+      if (t->defined()) bn0.emplace_back(*t, t->clone());
   const long t0 = opt_.step_count();
   auto eager = [&] {
     model_.zero_grad();
@@ -72,6 +77,7 @@ void TrainGraph::capture(const Tensor& x, const Tensor& labels) {
   gpu::copy(a->m.data(), m0.data(), m0.nbytes(), 2);
   gpu::copy(a->v.data(), w0.data(), w0.nbytes(), 2);
   gpu::copy(a->shadow.data(), s0.data(), s0.nbytes(), 2);
+  for (auto& [live, snap] : bn0) gpu::copy(live.data(), snap.data(), snap.nbytes(), 2);
   a->refresh_transposes();
   opt_.set_step_count(t0);
   opt_.upload_hyper();

@@ -225,8 +225,13 @@ class DeviceDataLoader(BaseDataLoader):
     def load_data(self, *a, **kw) -> bool:
         return True
 
+    def shuffle(self) -> None:
+        super().shuffle()  # (in place: the cached device copy of the order is stale)
+        self._order_dev = None
+
     def reset(self) -> None:
         super().reset()
+        self._order_dev = None
         self.epoch += 1
 
     def _device_order(self) -> torch.Tensor:

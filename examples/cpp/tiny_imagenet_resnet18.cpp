@@ -11,10 +11,11 @@
 // prints one JSON line (images/sec); on the GPU the step is captured into a hipGraph
 // (dcnn::TrainGraph) and replayed, --eager launches every kernel from the host instead. The saved
 // model (path.json + path.bin + path.bnstats) loads in Python with Sequential.from_file.
-// --dp (GPU, --bench): data parallel over RCCL, one process per GPU under the torch.distributed
-// launcher's variables (RANK / WORLD_SIZE / LOCAL_RANK / MASTER_ADDR / MASTER_PORT; dcnn/dist.hpp):
-// each rank trains --batch samples per step, the gradient all-reduce (mean) runs inside the captured
-// step, rank 0 prints the whole job's images/sec with the slowest rank's time.
+// --dp (--bench): data parallel, one process per GPU under the torch.distributed launcher's
+// variables (RANK / WORLD_SIZE / LOCAL_RANK / MASTER_ADDR / MASTER_PORT; dcnn/dist.hpp): rank 0's
+// weights are broadcast, each rank trains --batch samples per step, the bucketed gradient mean runs
+// inside the captured step over RCCL (--device CPU: over the host TCP ring), the timed steps are
+// fenced by barriers and rank 0 prints the whole job's images/sec with the slowest rank's time.
 // Honours the reference's .env keys DEVICE_TYPE / EPOCHS / BATCH_SIZE / LR_INITIAL.
 // Reference parity: examples/tiny_imagenet_resnet18.cpp:23-107 (Adam, logsoftmax-CE, profiling),
 // include/nn/example_models.hpp:306-331 (the model).
@@ -72,13 +73,14 @@ int main(int argc, char** argv) {
     std::unique_ptr<dist::DataParallel> dp;
     Device dev = Device::parse(device);
     if (dp_on) {
-      if (!dev.is_gpu() || !bench) throw std::invalid_argument("--dp: GPU --bench runs only");
+      if (!bench) throw std::invalid_argument("--dp: --bench runs only");
       const dist::Env env = dist::Env::from_env();
-      dp = std::make_unique<dist::DataParallel>(env);  // (selects GPU LOCAL_RANK)
-      dev = Device::gpu(env.local_rank);
+      dp = std::make_unique<dist::DataParallel>(env, dev);  // (GPU: selects GPU LOCAL_RANK)
+      dev = dp->device();
     }
     model.set_device(dev);
     model.initialize(42);
+    if (dp) dp->broadcast_parameters(model);  // identical replicas whatever each rank's seed
     std::printf("%s on %s: %zu parameters\n", model.name().c_str(), dev.str().c_str(), model.num_parameters());
     Adam opt(lr);
     Loss loss = LossFactory::create(loss_name);
@@ -91,8 +93,9 @@ int main(int argc, char** argv) {
       train = std::move(tr);
       val = std::make_unique<ImageDataset>(load_tiny_imagenet(data, "val", 0, 2));
     } else {
+      // (data parallel: each rank draws its own samples)
       train = std::make_unique<SyntheticClassification>(bench ? (size_t)batch * (steps + 4) : (size_t)4 * batch, C, HW,
-                                                        HW, classes, 7, 0.5f);
+                                                        HW, classes, 7 + (dp ? (uint64_t)dp->rank() : 0), 0.5f);
       val = std::make_unique<SyntheticClassification>((size_t)batch, C, HW, HW, classes, 7, 0.5f);
     }
     if (bench) {
@@ -122,9 +125,8 @@ int main(int argc, char** argv) {
       std::function<void()> allreduce;
       if (dp) {
         ParamArena* arena = model.parameters().at(0)->arena.get();
-        if (!arena) throw std::runtime_error("--dp: the parameters are not in a GPU arena");
         const char* ov = std::getenv("DCNN_DP_OVERLAP");
-        if (!(ov && std::string(ov) == "0")) {
+        if (!(ov && std::string(ov) == "0") || !arena) {
           const char* mb = std::getenv("DCNN_DP_BUCKET_MB");
           dp->attach(model, mb && *mb ? std::atof(mb) : 4.0);
           allreduce = [&dp] { dp->finish(); };
@@ -145,11 +147,17 @@ int main(int argc, char** argv) {
         return r.loss;
       };
       for (int i = 0; i < std::max(1, warmup); ++i) one();
-      if (dev.is_gpu()) gpu::synchronize();
+      // the timed region is bracketed by a device synchronisation + a barrier over the ranks on
+      // both sides; the slowest rank's time is reported
+      auto fence = [&] {
+        if (dev.is_gpu()) gpu::synchronize();
+        if (dp) dp->barrier();
+      };
+      fence();
       const auto t0 = std::chrono::steady_clock::now();
       double last = 0;
       for (int i = 0; i < timed; ++i) last = one();
-      if (dev.is_gpu()) gpu::synchronize();
+      fence();
       double s = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
       if (graph) last = tg.last_loss();
       const int world = dp ? dp->world() : 1;
@@ -157,10 +165,12 @@ int main(int argc, char** argv) {
       if (!dp || dp->rank() == 0)
         std::printf("{\"metric\": \"images/sec %s training (C++ host API)\", \"value\": %.1f, \"ms_per_step\": %.3f, "
                     "\"batch\": %d, \"steps\": %d, \"device\": \"%s\", \"hipgraph\": %s, \"loss\": %.6f, "
-                    "\"world\": %d, \"data_parallel\": %s, \"dp_buckets\": %d}\n",
+                    "\"world\": %d, \"data_parallel\": %s%s%s, \"dp_buckets\": %d, \"data\": \"synthetic: %s, "
+                    "2 device-resident batches per rank, random init\"}\n",
                     model_name.c_str(), (double)batch * world * timed / s, 1e3 * s / timed, batch, timed,
-                    dev.str().c_str(), graph ? "true" : "false", last, world, dp ? "\"rccl\"" : "null",
-                    dp ? dp->buckets_last_step() : 0);
+                    dev.str().c_str(), graph ? "true" : "false", last, world, dp ? "\"" : "", dp ? dp->plane() : "null",
+                    dp ? "\"" : "", dp ? dp->buckets_last_step() : 0,
+                    data.empty() ? "a learnable class-template set (SyntheticClassification)" : "staged from --data");
       return 0;
     }
     std::unique_ptr<Scheduler> sched;

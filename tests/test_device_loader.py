@@ -95,3 +95,21 @@ def test_device_loader_plain_gather_and_f32_storage():
     x, y = batches[1]
     assert torch.equal(x.cpu(), torch.from_numpy(data[8:16]))
     assert y.shape == (8, 10, 1, 1) and torch.equal(y.view(8, 10).argmax(1).cpu(), torch.from_numpy(labels[8:16]))
+
+
+@pytest.mark.gpu
+def test_device_loader_reshuffles_every_epoch():
+    """The epoch order is reshuffled in place on the host; the device copy must follow it."""
+    from dcnn_amd.data import DeviceDataLoader
+    n = 24
+    data = np.arange(n, dtype=np.float32).reshape(n, 1, 1, 1) * np.ones((1, 1, 2, 2), np.float32) + 0.5
+    labels = np.arange(n) % 10
+    ld = DeviceDataLoader(data=data, labels=labels, num_classes=10, batch_size=8, shuffle=True, seed=7)
+    seen = []
+    for _ in range(3):
+        xs = [x[:, 0, 0, 0].cpu().numpy() for x, _ in ld]
+        got = np.concatenate(xs) - 0.5
+        assert sorted(got.tolist()) == list(range(n))  # every sample once
+        assert np.array_equal(got, ld.order.astype(np.float32))  # in this epoch's host order
+        seen.append(got)
+    assert not np.array_equal(seen[0], seen[1]) and not np.array_equal(seen[1], seen[2])
