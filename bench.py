@@ -41,12 +41,6 @@ import torch.distributed as dist
 sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
 # ProcessGroupNCCL's event cache vs collectives recorded under hipGraph capture (dcnn_amd/__init__.py)
 os.environ.setdefault("TORCH_NCCL_CUDA_EVENT_CACHE", "0")
-# N > 1: segmented step capture — compute segments replayed as graphs, each bucket's all-reduce
-# issued asynchronously between two replays — so no process-group collective is recorded inside a
-# capture (its watchdog thread intermittently aborted world-1 ranks that captured collectives,
-# README "Known gaps"); DCNN_DP_CAPTURE=1 keeps the whole-step graph
-if int(os.environ.get("WORLD_SIZE", "1")) > 1:
-    os.environ.setdefault("DCNN_DP_CAPTURE", "0")
 
 METRIC = "images/sec (whole node) ResNet-18 Tiny-ImageNet training at 1/2/4/8 MI355X"
 ROOT = os.path.dirname(os.path.abspath(__file__))

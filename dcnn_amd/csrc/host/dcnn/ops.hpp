@@ -60,6 +60,8 @@ void end_deferred_reduce();
 // launch the weight-gradient reduces queued so far now and keep queueing (a gradient consumer
 // inside the backward: the data-parallel bucket all-reduce)
 void flush_deferred_reduce();
+// test-only fault injection (capi.cpp): bit 0 = conv_dgrad drops the fused BatchNorm ReLU mask
+void set_fault(int f);
 // fp32 NCHW network input -> bf16 NHWC activation
 void input_to_nhwc(const float* x, void* y, int N, int C, int HW);
 // bf16 [N][HW][C] <-> [N][C][HW] (Flatten keeps the NCHW feature order of the reference)

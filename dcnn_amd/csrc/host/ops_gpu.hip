@@ -13,6 +13,8 @@
 
 #include <algorithm>
 #include <cmath>
+#include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <map>
 #include <mutex>
@@ -356,6 +358,29 @@ int grid_of(long n) {
   return (int)(g > 8192 ? 8192 : (g < 1 ? 1 : g));
 }
 
+// ---- op recording (DCNN_RECORD_OPS=<file>): one JSON line per conv call with its geometry, the
+// epilogue options and the routing decision, so tests/test_gpu_cpp_geometry.py replays exactly the
+// calls a production step makes (through the C ABI, capi.cpp) against fp32 PyTorch
+FILE* rec_file() {
+  static FILE* f = [] {
+    const char* p = std::getenv("DCNN_RECORD_OPS");
+    return p && *p ? std::fopen(p, "a") : nullptr;
+  }();
+  return f;
+}
+void rec(const char* op, const ConvShape& s, int route, std::initializer_list<std::pair<const char*, int>> flags) {
+  FILE* f = rec_file();
+  if (!f) return;
+  std::fprintf(f, "{\"op\": \"%s\", \"shape\": [%d, %d, %d, %d, %d, %d, %d, %d, %d, %d, %d, %d, %d], \"route\": %d", op,
+               s.N, s.C, s.H, s.W, s.Co, s.KH, s.KW, s.SH, s.SW, s.PH, s.PW, s.OH, s.OW, route);
+  for (const auto& kv : flags) std::fprintf(f, ", \"%s\": %d", kv.first, kv.second);
+  std::fprintf(f, "}\n");
+  std::fflush(f);
+}
+// test-only fault injection (capi.cpp dcnn_c_set_fault): bit 0 drops the fused BatchNorm
+// backward's ReLU mask operand in conv_dgrad (the geometry test must then fail)
+int g_fault = 0;
+
 // split-K workspace of a halo conv: (partials, zeroed ticket words) — the kernel leaves them zeroed
 void hconv_workspace(HConvArgs& a) {
   a.splits = hconv_splits(a.NB, a.H, a.W, a.Cs, a.N, a.ntaps);
@@ -449,6 +474,7 @@ void wgrad_reduce(const Tensor& hold, const Tensor& bhold, const float* slab, fl
 }  // namespace
 
 void begin_deferred_reduce() { g_defer = true; }
+void set_fault(int f) { g_fault = f; }
 void flush_deferred_reduce() {
   const bool on = g_defer;
   end_deferred_reduce();
@@ -488,6 +514,7 @@ const float* conv_fwd(const void* x, const void* w, const float* bias, void* y, 
   const int M = s.N * s.OH * s.OW;
   // the shared routing table (conv_route.cpp): the same kernels as the Python front end
   const int route = conv_fwd_route(route_geom(s, want ? 1 : 0));
+  rec("fwd", s, route, {{"bias", bias != nullptr}, {"stats", want}});
   if (route == ROUTE_HALO && xb < (1l << 31)) {
     HConvArgs a{};
     a.A = static_cast<const bf16*>(x); a.B = static_cast<const bf16*>(w); a.C = static_cast<bf16*>(y);
@@ -535,7 +562,7 @@ const float* conv_dgrad(const void* dy, const void* w, void* dx, const ConvShape
   if (bnb_rows) *bnb_rows = 0;
   BnbArgs ba{};
   if (bnb) {
-    ba.y = static_cast<const bf16*>(bnb->y);
+    ba.y = (g_fault & 1) ? nullptr : static_cast<const bf16*>(bnb->y);
     ba.x = static_cast<const bf16*>(bnb->x);
     ba.mean = bnb->mean;
     ba.istd = bnb->istd;
@@ -553,6 +580,8 @@ const float* conv_dgrad(const void* dy, const void* w, void* dx, const ConvShape
   const long dyb = (long)s.N * s.OH * s.OW * s.Co * 2, wtb = (long)s.C * T * s.Co * 2;
   // shared routing table (conv_route.cpp); g1s mode 2: the streaming dgrad with the BN epilogue
   const int route = conv_dgrad_route(route_geom(s, bnb ? 2 : 0));
+  rec("dgrad", s, route, {{"residual", residual != nullptr}, {"w_t", w_transposed}, {"bnb", bnb != nullptr},
+                         {"bnb_mask", bnb != nullptr && bnb->y != nullptr}});
   if (route == ROUTE_HALO && dyb < (1l << 31)) {
     // transposed conv of a stride-1 'same' conv: tap (ky, kx) reads dy at (PH - ky, PW - kx)
     HConvArgs a{};
@@ -647,6 +676,7 @@ void conv_wgrad(const void* dy, const void* x, float* gw, float* gb, const ConvS
   const int Ng = s.KH * s.KW * s.C, P = s.N * s.OH * s.OW;
   const long dyb = (long)P * s.Co * 2, xb = (long)s.N * s.H * s.W * s.C * 2;
   const int route = conv_wgrad_route(route_geom(s, -1));  // shared routing table (conv_route.cpp)
+  rec("wgrad", s, route, {{"bias", gb != nullptr}, {"deferred", g_defer}});
   if (route == ROUTE_HALO) {
     const int splits = hwgrad_splits(s.N, s.H, s.W, s.C, s.Co);
     Tensor hold, bhold;
@@ -709,6 +739,7 @@ bool stem_ok(const ConvShape& s) {
 
 // weights / gradients: physical [Co][KH][KW][Ci] -> element strides of the logical (Co, Ci, ky, kx)
 const float* stem_fwd(const float* x, const void* w, const float* bias, void* y, const ConvShape& s, int* stat_rows) {
+  rec("stem_fwd", s, -1, {{"bias", bias != nullptr}, {"stats", stat_rows != nullptr}});
   StemArgs a{};
   a.x = x; a.w = w; a.w_bf16 = 1;
   a.ws[0] = 9l * s.C; a.ws[1] = 1; a.ws[2] = 3l * s.C; a.ws[3] = s.C;
@@ -723,6 +754,7 @@ const float* stem_fwd(const float* x, const void* w, const float* bias, void* y,
 }
 
 void stem_wgrad(const void* dy, const float* x, float* gw, float* gb, const ConvShape& s) {
+  rec("stem_wgrad", s, -1, {{"bias", gb != nullptr}, {"deferred", g_defer}});
   const int blocks = stem_wgrad_blocks(s.N, s.H, s.W);
   const long n = 9l * s.C * s.Co;
   Tensor hold, bhold;

@@ -220,7 +220,17 @@ class DataParallel:
             self._reduce_bf16_gpu(lo, hi)
             return
         if plain:
-            self._works.append(dist.all_reduce(flat[lo:hi], op=dist.ReduceOp.SUM, group=self.pg, async_op=True))
+            if flat.is_cuda:
+                # blocking-form collective on the comm stream (forked after the bucket's gradients,
+                # joined in finish()): it overlaps the rest of the backward like an async work, but
+                # no Work handle is queued for ProcessGroupNCCL's watchdog. An async_op=True work
+                # issued under hipGraph capture is queued although its end event was recorded in
+                # the capture; the watchdog's query of that event fails (hipErrorCapturedEvent) and
+                # aborts the rank (tools/pg_capture_probe.py --mode async, profiles/pg_capture_probe_r6.md)
+                with self._cstream(flat.device).fork():
+                    dist.all_reduce(flat[lo:hi], op=dist.ReduceOp.SUM, group=self.pg)
+            else:
+                self._works.append(dist.all_reduce(flat[lo:hi], op=dist.ReduceOp.SUM, group=self.pg, async_op=True))
             return
         if flat.is_cuda:
             self._reduce_bf16_gpu(lo, hi)
@@ -254,8 +264,9 @@ class DataParallel:
                 self.rccl.reduce_scatter(red, packed)
                 self.rccl.all_gather(gathered, red)
             else:
-                dist.reduce_scatter_tensor(red, packed, op=dist.ReduceOp.SUM, group=self.pg, async_op=True).wait()
-                dist.all_gather_into_tensor(gathered, red, group=self.pg, async_op=True).wait()
+                # (blocking forms: no async Work for the watchdog, see reduce_bucket)
+                dist.reduce_scatter_tensor(red, packed, op=dist.ReduceOp.SUM, group=self.pg)
+                dist.all_gather_into_tensor(gathered, red, group=self.pg)
             K.grad_unpack_bf16(gathered.data_ptr(), flat[lo:hi].data_ptr(), n, st)
 
     def _reduce_bf16_cpu(self, lo, hi):
