@@ -10,6 +10,7 @@
 // include/nn/example_models.hpp:13-437 (model zoo).
 #pragma once
 #include <functional>
+#include <initializer_list>
 #include <memory>
 #include <string>
 #include <vector>
@@ -261,6 +262,8 @@ class ImageDataset : public DataSource {
   void normalize(const std::vector<float>& mean, const std::vector<float>& stdev);
   // horizontal flip with probability p per sample (applied at batch time)
   void set_random_flip(float p) { flip_ = p; }
+  const std::vector<float>& images() const { return img_; }
+  const std::vector<int64_t>& labels() const { return labels_; }
 
  private:
   std::vector<float> img_;
@@ -271,6 +274,56 @@ class ImageDataset : public DataSource {
   float flip_ = 0.f;
   std::vector<size_t> order_;
   size_t pos_ = 0;
+};
+
+// HBM-resident image classification set (the GPU data path): the whole set lives in device memory
+// (uint8 when every value is an exact k / 255, as decoded images are: 1.2 GB for Tiny-ImageNet's
+// 100k training images, else fp32) and every batch is assembled by ONE kernel launch on the current
+// flow (augment.hip: gather by the epoch order + the augmentation chain + labels), so training never
+// waits on host decoding, augmentation or host-to-device copies. The chain's draws are a counter
+// hash of (epoch seed, sample, op, draw) — the Python DeviceDataLoader's kernel and semantics
+// (data/device_loader.py): a rerun reproduces every batch.
+// Reference parity: include/data_loading/tiny_imagenet_data_loader.hpp:481 (batches of the epoch
+// order), include/data_augmentation/augmentation.hpp:114 (the op chain: crop, flips, rotation,
+// brightness, contrast, noise, cutout, normalisation).
+class DeviceImageDataset : public DataSource {
+ public:
+  DeviceImageDataset(const ImageDataset& host, Device dev, uint64_t seed = 0, bool shuffle = true,
+                     bool drop_last = true);
+  // the augmentation chain, applied in the order added (at most 12 ops; p = probability per sample)
+  DeviceImageDataset& horizontal_flip(float p = 0.5f);
+  DeviceImageDataset& vertical_flip(float p = 0.5f);
+  DeviceImageDataset& rotation(float p, float max_degrees);
+  DeviceImageDataset& brightness(float p, float delta);
+  DeviceImageDataset& contrast(float p, float delta);
+  DeviceImageDataset& gaussian_noise(float p, float sigma);
+  DeviceImageDataset& random_crop(float p, int pad);  // shift by up to +-pad pixels, zero fill
+  DeviceImageDataset& cutout(float p, int size);
+  DeviceImageDataset& normalize(const std::vector<float>& mean = {0.485f, 0.456f, 0.406f},
+                                const std::vector<float>& stdev = {0.229f, 0.224f, 0.225f});
+  void reset(uint64_t epoch) override;
+  // x: fp32 [B, C, H, W] and labels int64 [B], both on the device
+  bool next(int batch, Tensor& x, Tensor& labels) override;
+  size_t size() const override { return n_; }
+  bool stored_u8() const { return u8_; }
+  size_t device_bytes() const { return data_.nbytes(); }
+  uint64_t epoch_seed() const;
+
+ private:
+  struct Op {
+    int kind;
+    float p;
+    float a[6];
+  };
+  DeviceImageDataset& add(int kind, float p, std::initializer_list<float> a);
+  Device dev_;
+  Tensor data_, labels_, order_dev_;
+  std::vector<int64_t> order_;
+  std::vector<Op> ops_;
+  size_t n_ = 0, pos_ = 0;
+  int c_, h_, w_;
+  uint64_t seed_, epoch_ = 0;
+  bool shuffle_, drop_last_, u8_ = false;
 };
 
 // MNIST CSV (label, 784 pixels per row; header row auto-detected) -> [N, 1, 28, 28] / 255

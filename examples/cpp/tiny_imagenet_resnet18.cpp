@@ -4,9 +4,12 @@
 //   dcnn_amd/bin/tiny_imagenet_resnet18 [--device CPU|GPU] [--model resnet18_tiny_imagenet]
 //        [--data data/tiny-imagenet-200] [--epochs E] [--steps S] [--batch B] [--lr 1e-3]
 //        [--loss logsoftmax_ce] [--scheduler cosine_annealing_lr] [--max-per-class K]
-//        [--save model_snapshots/resnet18] [--bench [--eager] [--warmup W]] [--dp]
+//        [--save model_snapshots/resnet18] [--bench [--eager] [--warmup W]] [--dp] [--device-data]
 //
-// Without --data it trains on a learnable synthetic 3x64x64 200-class set. --bench times
+// Without --data it trains on a learnable synthetic 3x64x64 200-class set. --device-data (GPU, with
+// --data): the GPU data path (DeviceImageDataset): the decoded set lives in HBM as uint8 and every
+// batch is one augment_batch launch (random crop +-4, horizontal flip, ImageNet normalisation) on
+// the training flow — with --bench that launch is inside every timed step. --bench times
 // --steps training steps after --warmup (3) warm-up steps on two device-resident synthetic batches and
 // prints one JSON line (images/sec); on the GPU the step is captured into a hipGraph
 // (dcnn::TrainGraph) and replayed, --eager launches every kernel from the host instead. The saved
@@ -47,12 +50,13 @@ int main(int argc, char** argv) {
   int epochs = std::atoi(env_or("EPOCHS", "1").c_str()), steps = -1, max_per_class = 0, warmup = 3;
   int batch = std::atoi(env_or("BATCH_SIZE", "64").c_str());
   float lr = std::atof(env_or("LR_INITIAL", "0.001").c_str());
-  bool bench = false, eager = false, dp_on = false;
+  bool bench = false, eager = false, dp_on = false, device_data = false;
   for (int i = 1; i < argc; ++i) {
     const std::string k = argv[i];
     if (k == "--bench") { bench = true; continue; }
     if (k == "--eager") { eager = true; continue; }
     if (k == "--dp") { dp_on = true; continue; }
+    if (k == "--device-data") { device_data = true; continue; }
     if (i + 1 >= argc) break;
     const std::string v = argv[++i];
     if (k == "--device") device = v;
@@ -87,7 +91,20 @@ int main(int argc, char** argv) {
     const bool cifar = model_name.find("cifar") != std::string::npos;
     const int C = 3, HW = cifar ? 32 : 64, classes = cifar ? 10 : 200;
     std::unique_ptr<DataSource> train, val;
-    if (!data.empty()) {
+    if (!data.empty() && device_data) {
+      // the GPU data path: decoded once into HBM (uint8), every batch one augment_batch launch
+      if (!dev.is_gpu()) throw std::invalid_argument("--device-data: GPU runs only");
+      const uint64_t rs = dp ? (uint64_t)dp->rank() : 0;
+      auto tr = std::make_unique<DeviceImageDataset>(load_tiny_imagenet(data, "train", max_per_class, 1), dev,
+                                                     1 + rs);
+      tr->random_crop(1.f, 4).horizontal_flip(0.5f).normalize();
+      std::printf("device dataset: %zu images, %.1f MB of HBM (%s)\n", tr->size(), tr->device_bytes() / 1e6,
+                  tr->stored_u8() ? "uint8" : "fp32");
+      train = std::move(tr);
+      auto va = std::make_unique<DeviceImageDataset>(load_tiny_imagenet(data, "val", 0, 2), dev, 2, false, false);
+      va->normalize();
+      val = std::move(va);
+    } else if (!data.empty()) {
       auto tr = std::make_unique<ImageDataset>(load_tiny_imagenet(data, "train", max_per_class, 1));
       tr->set_random_flip(0.5f);
       train = std::move(tr);
@@ -104,7 +121,15 @@ int main(int argc, char** argv) {
       // not host-side data synthesis)
       train->reset(0);
       std::vector<std::pair<Tensor, Tensor>> staged;
-      for (int i = 0; i < 2; ++i) {
+      // the device dataset assembles a fresh augmented batch inside every timed step instead
+      uint64_t epoch = 0;
+      auto fresh = [&](Tensor& xb, Tensor& yb) {
+        if (!train->next(batch, xb, yb)) {
+          train->reset(++epoch);
+          if (!train->next(batch, xb, yb)) throw std::runtime_error("--bench: fewer samples than one batch");
+        }
+      };
+      for (int i = 0; i < (device_data ? 0 : 2); ++i) {
         Tensor xh, yh;
         if (!train->next(batch, xh, yh)) {
           train->reset(1);
@@ -136,7 +161,9 @@ int main(int argc, char** argv) {
         tg.set_gradient_hook(allreduce);
       }
       auto one = [&] {
-        const auto& [x, y] = staged[(size_t)(k++) % staged.size()];
+        Tensor dx, dy;
+        if (device_data) fresh(dx, dy);
+        const auto& [x, y] = device_data ? std::pair<Tensor, Tensor>{dx, dy} : staged[(size_t)(k++) % staged.size()];
         if (graph) return tg.step(x, y);
         model.zero_grad();
         Tensor logits = model.forward(x);
@@ -165,12 +192,14 @@ int main(int argc, char** argv) {
       if (!dp || dp->rank() == 0)
         std::printf("{\"metric\": \"images/sec %s training (C++ host API)\", \"value\": %.1f, \"ms_per_step\": %.3f, "
                     "\"batch\": %d, \"steps\": %d, \"device\": \"%s\", \"hipgraph\": %s, \"loss\": %.6f, "
-                    "\"world\": %d, \"data_parallel\": %s%s%s, \"dp_buckets\": %d, \"data\": \"synthetic: %s, "
-                    "2 device-resident batches per rank, random init\"}\n",
+                    "\"world\": %d, \"data_parallel\": %s%s%s, \"dp_buckets\": %d, \"data\": \"%s, random init\"}\n",
                     model_name.c_str(), (double)batch * world * timed / s, 1e3 * s / timed, batch, timed,
                     dev.str().c_str(), graph ? "true" : "false", last, world, dp ? "\"" : "", dp ? dp->plane() : "null",
                     dp ? "\"" : "", dp ? dp->buckets_last_step() : 0,
-                    data.empty() ? "a learnable class-template set (SyntheticClassification)" : "staged from --data");
+                    data.empty() ? "synthetic: 2 device-resident batches per rank of a learnable class-template set "
+                                   "(SyntheticClassification)"
+                    : device_data ? "--data decoded into HBM, one augment_batch launch per step (crop, flip, normalise)"
+                                  : "2 device-resident batches per rank staged from --data");
       return 0;
     }
     std::unique_ptr<Scheduler> sched;
