@@ -7,6 +7,7 @@
 #include <chrono>
 #include <cmath>
 #include <cstdio>
+#include <cstdlib>
 #include <filesystem>
 #include <fstream>
 #include <iostream>
@@ -1349,7 +1350,12 @@ Tensor Sequential::forward_activation(const Tensor& x_in, int mb) {
 
 Tensor Sequential::backward_activation(const Tensor& g_in, int mb) {
   Tensor g = g_in;
-  const bool defer = dev_.is_gpu();
+  // (DCNN_DEFER_REDUCE=0: each weight gradient's split-K reduce right after its kernel — experiment)
+  static const bool defer_env = [] {
+    const char* v = std::getenv("DCNN_DEFER_REDUCE");
+    return !(v && std::string(v) == "0");
+  }();
+  const bool defer = dev_.is_gpu() && defer_env;
   if (defer) gpu_ops::begin_deferred_reduce();
   try {
     for (size_t i = layers_.size(); i-- > 0;) {

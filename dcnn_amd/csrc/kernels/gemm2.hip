@@ -125,26 +125,54 @@ __global__ void __launch_bounds__(256, 2) gemm_g2_kernel(G2Args p) {
     b_base[i] = (unsigned)((long)n * p.ldb * 2);
   }
 
+  // this class's tap table in VGPR lanes (ntaps <= 64 = one wave): lane t holds tap t's source
+  // offset and weight column, so a K-step's uniform tap reads its entries with v_readlane — no
+  // scalar-memory round trip (and s_waitcnt lgkmcnt(0), which also drains the MFMA operands' LDS
+  // reads) per glds instruction in the K loop
+  const int tab_src = lane < ntp ? p.tap_srcoff[ct0 + lane] : 0;
+  const int tab_b = lane < ntp ? p.tap_b[ct0 + lane] : 0;
+  // UNI: the K-steps are staged in order, BK apart, so the (tap, channel) of the next stage is a
+  // uniform counter pair (no per-stage integer division)
+  int st_t = 0, st_c = 0;
+
   auto stage = [&](int buf, int k0) {
     char* As = smem + buf * T::STAGE;
     char* Bs = As + BM * BK * 2;
-    // tap / channel of this K-step (uniform when Cs % BK == 0)
-    int tU = 0, cU = 0;
-    if constexpr (UNI) { tU = k0 / p.Cs; cU = k0 - tU * p.Cs; }
+    if constexpr (UNI) {
+      const int t = st_t, c0 = st_c;
+      st_c += BK;
+      if (st_c >= p.Cs) { st_c -= p.Cs; ++st_t; }
+      const bool tok = t < ntp;
+      const int tl = tok ? t : 0;
+      const int src = __builtin_amdgcn_readlane(tab_src, tl), tb = __builtin_amdgcn_readlane(tab_b, tl);
+#pragma unroll
+      for (int i = 0; i < T::A_INS; ++i) {
+        const int c = c0 + a_lch[i] * 8;
+        const bool ok = tok && c < p.Cs && ((a_mask[i] >> tl) & 1ull);
+        const unsigned voff = ok ? a_base[i] + (unsigned)(src * 2 + c * 2) : kOOB;
+        glds16(rsA, As + (wid * T::A_INS + i) * 1024, voff);
+      }
+#pragma unroll
+      for (int i = 0; i < T::B_INS; ++i) {
+        const int c = c0 + b_lch[i] * 8;
+        const bool ok = b_ok[i] && tok && c < p.Cs;
+        const unsigned voff = ok ? b_base[i] + (unsigned)((tb + c) * 2) : kOOB;
+        glds16(rsB, Bs + (wid * T::B_INS + i) * 1024, voff);
+      }
+      return;
+    }
 #pragma unroll
     for (int i = 0; i < T::A_INS; ++i) {
-      int t, c;
-      if constexpr (UNI) { t = tU; c = cU + a_lch[i] * 8; }
-      else { const int k = k0 + a_lch[i] * 8; t = k / p.Cs; c = k - t * p.Cs; }
+      const int k = k0 + a_lch[i] * 8;
+      const int t = k / p.Cs, c = k - t * p.Cs;
       const bool ok = t < ntp && c < p.Cs && ((a_mask[i] >> t) & 1ull);
       const unsigned voff = ok ? a_base[i] + (unsigned)(p.tap_srcoff[ct0 + t] * 2 + c * 2) : kOOB;
       glds16(rsA, As + (wid * T::A_INS + i) * 1024, voff);
     }
 #pragma unroll
     for (int i = 0; i < T::B_INS; ++i) {
-      int t, c;
-      if constexpr (UNI) { t = tU; c = cU + b_lch[i] * 8; }
-      else { const int k = k0 + b_lch[i] * 8; t = k / p.Cs; c = k - t * p.Cs; }
+      const int k = k0 + b_lch[i] * 8;
+      const int t = k / p.Cs, c = k - t * p.Cs;
       const bool ok = b_ok[i] && t < ntp && c < p.Cs;
       const unsigned voff = ok ? b_base[i] + (unsigned)((p.tap_b[ct0 + t] + c) * 2) : kOOB;
       glds16(rsB, Bs + (wid * T::B_INS + i) * 1024, voff);
@@ -162,22 +190,28 @@ __global__ void __launch_bounds__(256, 2) gemm_g2_kernel(G2Args p) {
   auto compute = [&](int buf) {
     const char* As = smem + buf * T::STAGE;
     const char* Bs = As + BM * BK * 2;
+    // every fragment of the K-step is read up front (one LDS latency per stage, not one per 32-wide
+    // slice: the second slice's reads are in flight while the first slice's MFMAs issue)
+    constexpr int KK = BK / 32;
+    bf16x8 a[KK][T::TM], b[KK][T::TN];
 #pragma unroll
-    for (int kk = 0; kk < BK / 32; ++kk) {
+    for (int kk = 0; kk < KK; ++kk) {
       const int c = kk * 4 + (lane >> 4);
-      bf16x8 a[T::TM], b[T::TN];
 #pragma unroll
       for (int i = 0; i < T::TM; ++i)
-        a[i] = *reinterpret_cast<const bf16x8*>(As + T::off(wm * (BM / 2) + i * 16 + (lane & 15), c));
+        a[kk][i] = *reinterpret_cast<const bf16x8*>(As + T::off(wm * (BM / 2) + i * 16 + (lane & 15), c));
 #pragma unroll
       for (int j = 0; j < T::TN; ++j)
-        b[j] = *reinterpret_cast<const bf16x8*>(Bs + T::off(wn * (BN / 2) + j * 16 + (lane & 15), c));
+        b[kk][j] = *reinterpret_cast<const bf16x8*>(Bs + T::off(wn * (BN / 2) + j * 16 + (lane & 15), c));
+    }
+#pragma unroll
+    for (int kk = 0; kk < KK; ++kk) {
       __builtin_amdgcn_s_setprio(1);
 #pragma unroll
       for (int i = 0; i < T::TM; ++i)
 #pragma unroll
         for (int j = 0; j < T::TN; ++j)
-          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[i], b[j], acc[i][j], 0, 0, 0);
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[kk][i], b[kk][j], acc[i][j], 0, 0, 0);
       __builtin_amdgcn_s_setprio(0);
     }
   };

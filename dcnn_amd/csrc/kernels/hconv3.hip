@@ -578,6 +578,7 @@ __global__ void __launch_bounds__(NW * 64, 8 / NW) hconv3_kernel(HConvArgs p, H3
       // one channel half at a time (keeps the epilogue's operand registers to a half)
 #pragma unroll
       for (int h = 0; h < 2; ++h) {
+        if (it.n0 + wc * 64 + 32 * h >= p.N) continue;  // (wave-uniform: the N = 32 tile's upper half)
         float bv[8], mu[8], is[8];
 #pragma unroll
         for (int e = 0; e < 8; ++e) {
@@ -695,7 +696,7 @@ __global__ void __launch_bounds__(NW * 64, 8 / NW) hconv3_kernel(HConvArgs p, H3
       stamp(u, 3);
       if (stats) {
         __syncthreads();
-        if (tid < BN) {
+        if (tid < BN && it.n0 + tid < p.N) {
           if (bnb) {
             float a = 0.f, b = 0.f;
 #pragma unroll
@@ -740,7 +741,9 @@ void hconv3_set_max_splits(int n) { g_h3_max_splits = n < 1 ? 1 : n; }
 bool hconv3_plan(int NB, int H, int W, int Cs, int N, int ntaps, H3Plan* pl) {
   // an even 32-channel chunk count (split-K pairs), or one chunk (32 input channels: ResNet-18's
   // first residual conv)
-  if (!g_h3 || ntaps != 9 || (Cs % 64 && Cs != 32) || N % 64) return false;
+  // N = 32 (the 32-channel data gradient of ResNet-18's first residual conv): one 64-channel tile
+  // whose upper half reads zero weights (buffer range) and is neither stored nor counted
+  if (!g_h3 || ntaps != 9 || (Cs % 64 && Cs != 32) || (N % 64 && N != 32)) return false;
   // 4-wave workgroups of 64 output channels x one 16 x 16 pixel tile, two per CU. Maps of 16 x 16
   // and larger (multiples of 16): image windows, halo 18 x 18 (pitch 18, 6 DMA instructions per
   // wave and chunk, LDS 72 KB). 8 x 8 maps: 2 x 2 images per tile, halo 19 x 19 (6 instructions);
@@ -760,7 +763,7 @@ bool hconv3_plan(int NB, int H, int W, int Cs, int N, int ntaps, H3Plan* pl) {
   pl->tx_tiles = GX > 1 ? 1 : W / TW;
   pl->tpi = GX > 1 ? 1 : (W / TW) * (H / TH);
   pl->tiles_m = NB * H * W / (TH * TW);
-  pl->tiles_n = N / BN;
+  pl->tiles_n = (N + BN - 1) / BN;
   // split-K over 32-channel chunks until the work items reach the target count (hconv.hip
   // g_split_target: one per CU); a split may hold a single chunk (then every workgroup runs one
   // item), at most 8 splits (the last arriver reads every partial back)

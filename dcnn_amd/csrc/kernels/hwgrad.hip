@@ -1001,6 +1001,12 @@ __global__ void __launch_bounds__(256 * TSP, 1) hwgrad_s2_kernel(HWArgs p) {
     if (tid < 64) p.bias_slab[(long)split * p.Co + co0 + tid] = stg[tid] + stg[tid + 64] + stg[tid + 128] + stg[tid + 192];
   }
   };
+  // TSP == 2: the two wave groups run different instantiations of `run`, and both contain
+  // workgroup barriers. They stay matched because every barrier in `run` sits in a loop or branch
+  // whose bounds are workgroup-uniform and independent of the tap range (TB, NTW): the K loop over
+  // this split's nt tiles, the epilogue's 9 / ET tap blocks, and the bias block (c0 == 0). Any
+  // barrier added under a TB- or NTW-dependent condition would deadlock the workgroup; keep
+  // tap-range dependence inside the barrier-free MFMA / staging code only.
   if constexpr (TSP == 1) {
     run(std::integral_constant<int, 0>{}, std::integral_constant<int, 9>{});
   } else {
