@@ -23,6 +23,7 @@
 
 #include "common.h"
 #include "api.h"
+#include "stat_fold.h"
 
 namespace dcnn {
 
@@ -359,13 +360,18 @@ __global__ void __launch_bounds__(256, 2) gemm_g2_kernel(G2Args p) {
       red[(r0 * 2 + 1) * BN + cg * 8 + v] = q[v];
     }
     __syncthreads();
+    // (folded statistics: agent-coherent row stores, read back by the group's last arriver)
+    const bool fold = p.fold.tickets != nullptr;
+    const __amdgpu_buffer_rsrc_t rsS = stat_rsrc(p.stats);
     if (bnb) {  // backward: plain sums [tiles][2][N]
       for (int c = tid; c < 2 * BN; c += 256) {
         const int which = c / BN, cc = c % BN;
         if (n0 + cc < p.N) {
           float a = 0.f;
           for (int k = 0; k < RSTEP; ++k) a += red[(k * 2 + which) * BN + cc];
-          *&p.stats[((long)tm * 2 + which) * p.N + n0 + cc] = a;
+          const long o = ((long)tm * 2 + which) * p.N + n0 + cc;
+          if (fold) stat_store_sc1(rsS, o, a);
+          else p.stats[o] = a;
         }
       }
     } else if (tid < BN && n0 + tid < p.N) {  // forward: Welford triple [tiles][3][N]
@@ -373,7 +379,21 @@ __global__ void __launch_bounds__(256, 2) gemm_g2_kernel(G2Args p) {
       for (int k = 0; k < RSTEP; ++k) { a += red[(k * 2 + 0) * BN + tid]; b += red[(k * 2 + 1) * BN + tid]; }
       const float cnt = (float)min(BM, p.M - m0);
       const Welford w = welford_from_shifted(cnt, piv_col, a, b);
-      store_welford(p.stats, tm, p.N, n0 + tid, w);
+      if (fold) {
+        const long o = ((long)tm * 3) * p.N + n0 + tid;
+        stat_store_sc1(rsS, o, w.n);
+        stat_store_sc1(rsS, o + p.N, w.mean);
+        stat_store_sc1(rsS, o + 2l * p.N, w.m2);
+      } else {
+        store_welford(p.stats, tm, p.N, n0 + tid, w);
+      }
+    }
+    if (fold) {  // this tile's slice of statistics row tm arrives (stat_fold.h)
+      __syncthreads();  // (the reduction scratch is the fold's LDS)
+      const int rows = (p.M + BM - 1) / BM;
+      int* flags = reinterpret_cast<int*>(smem + kStatFoldLds);
+      if (bnb) stat_fold_arrive<1>(p.stats, rows, p.N, 1, [&](int) { return tm; }, p.fold, flags, smem);
+      else stat_fold_arrive<0>(p.stats, rows, p.N, 1, [&](int) { return tm; }, p.fold, flags, smem);
     }
   }
 }
@@ -653,6 +673,7 @@ int gemm_g2_row_tile(int M, int N) {
 
 void gemm_g2(const G2Args& a_in, hipStream_t s) {
   G2Args a = a_in;
+  if (a.fold.tickets && !a.stats) throw std::runtime_error("gemm_g2: statistics fold without statistics rows");
   if (a.N % 8 != 0 || a.Cs % 8 != 0 || a.ldb % 8 != 0 || a.ldc % 8 != 0 || a.ntaps > 64 || a.ntaps < 1)
     throw std::runtime_error("gemm_g2: unsupported shape (needs N, Cs, ldb, ldc multiples of 8, 1..64 taps)");
   int bm, bn;
@@ -669,6 +690,7 @@ void gemm_g2(const G2Args& a_in, hipStream_t s) {
   }
   const int bk = (a.Cs % 64 == 0) ? 64 : 32;
   const bool uni = a.Cs % bk == 0;
+  a.fold.arrivals = (a.N + bn - 1) / bn;  // (every column tile writes its slice of a statistics row)
 #define DCNN_G2(BM, BN, BK, U) if (bm == BM && bn == BN && bk == BK && uni == U) return launch_g2<BM, BN, BK, U>(a, s)
   DCNN_G2(128, 128, 64, true);
   DCNN_G2(128, 64, 64, true);
