@@ -4,7 +4,8 @@
 // averaged gradient / updated parameters are written for comparison against a world-1 run on the
 // whole batch.
 //
-//   dcnn_amd/bin/dp_selftest --device CPU|GPU --out DIR [--batch 16] [--bucket-mb 0.004]
+//   dcnn_amd/bin/dp_selftest --device CPU|GPU|UID --out DIR [--batch 16] [--bucket-mb 0.004]
+//   (UID: only the RCCL unique-id rendezvous of the GPU plane, exchange_unique_id)
 //                            [--graph]   (GPU: Adam + the captured TrainGraph step)
 //                            [--no-dp]   (the same step without the gradient mean: world-1 baseline)
 //
@@ -74,6 +75,15 @@ int main(int argc, char** argv) {
   }
   try {
     const dist::Env env = dist::Env::from_env();
+    if (device == "UID") {  // the RCCL unique-id rendezvous alone (no device work): every rank
+                            // prints a hash of the id it holds
+      const std::string id = dist::exchange_unique_id(env);
+      uint64_t h = 1469598103934665603ull;
+      for (unsigned char ch : id) h = (h ^ ch) * 1099511628211ull;
+      std::printf("{\"rank\": %d, \"uid_hash\": \"%016llx\", \"uid_bytes\": %zu}\n", env.rank,
+                  (unsigned long long)h, id.size());
+      return 0;
+    }
     Device dev = Device::parse(device);
     dist::DataParallel dp(env, dev);
     dev = dp.device();

@@ -127,3 +127,18 @@ def test_gpu_cpp_dp_rccl_world1(exe, tmp_path, graph):
         assert rc == 0, o
     for x, y in zip(_load(a / "w1r0.bin"), _load(b / "w1r0.bin")):
         assert np.array_equal(x, y)
+
+
+@pytest.mark.gpu
+def test_gpu_cpp_dp_unique_id_rendezvous_world3(exe, tmp_path):
+    """The GPU plane's rendezvous at world 3: rank 0's RCCL unique id reaches every rank over TCP
+    (exchange_unique_id; the communicator itself needs one GPU per rank, which one box lacks)."""
+    outs = _launch(exe, 3, tmp_path, device="UID", timeout=120)
+    hashes = set()
+    for rc, o in outs:
+        assert rc == 0, o
+        line = [l for l in o.splitlines() if l.startswith("{")][-1]
+        d = __import__("json").loads(line)
+        assert d["uid_bytes"] == 128
+        hashes.add(d["uid_hash"])
+    assert len(hashes) == 1, hashes
