@@ -54,6 +54,8 @@ struct G2Args {
   int cls_t0[4], cls_nt[4], cls_ory[4], cls_orx[4];
   // statistics fold (stat_fold.h; `stats` rows reduced in the kernel, no bn_stat_reduce)
   StatFold fold;
+  // split-K (set by gemm_g2() for long-K 1x1 GEMMs on small grids): K slices, fp32 partials
+  int ksplit; float* kpart;
 };
 struct T2Args {
   const bf16* dY; const bf16* X; float* slab; float* bias_slab;
@@ -139,6 +141,10 @@ void hwgrad_s2(HWArgs a, int splits, hipStream_t s);
 
 void gemm_nt(const NtArgs& a, hipStream_t s);
 void gemm_g2(const G2Args& a, hipStream_t s);
+// split-K for long-K (>= 1024) 1x1 GEMMs on small grids: K slices to fp32 partials + an epilogue
+// launch (default on; 0: the routing table keeps those convs on the halo kernel)
+void gemm_g2_set_splitk(int on);
+int gemm_g2_splitk_enabled();
 int gemm_g2_stat_rows(int M, int N);
 int gemm_g2_row_tile(int M, int N);  // BM the launcher picks for an M x N output
 void gemm_t2(T2Args a, int splits, hipStream_t s);

@@ -20,11 +20,18 @@ bool same_reach1(const ConvRouteGeom& g) {
 bool halo_1x1(int M, int K, int N) { return K >= 1024 && (long)(M / 64) * (N / 64) < 256; }
 }  // namespace
 
+// the halo_1x1 shapes on the gathered GEMM's split-K path instead (gemm2.hip g2_ksplit: K slices
+// over ~512 workgroups + one epilogue launch; ResNet-50 b32 K >= 1024 1x1 convs)
+static bool splitk_1x1(int M, int K, int N) {
+  return gemm_g2_splitk_enabled() && halo_1x1(M, K, N) && K % 8 == 0 && N % 8 == 0;
+}
+
 int conv_fwd_route(ConvRouteGeom g) {
   const int M = g.N * g.OH * g.OW, T = g.KH * g.KW;
   if (g.KH == 1 && g.KW == 1 && g.PH == 0 && g.PW == 0 && g.SH == g.SW && g.g1s_mode >= 0 &&
       g1s_rows(M, g.Co, g.C, g.g1s_mode) > 0)
     return ROUTE_G1S;
+  if (T == 1 && g.SH == 1 && g.SW == 1 && g.PH == 0 && g.PW == 0 && splitk_1x1(M, g.C, g.Co)) return ROUTE_GEMM_G2;
   if (same_reach1(g) && (T > 1 || halo_1x1(M, g.C, g.Co)) && hconv_supported(g.N, g.H, g.W, g.C, g.Co, T))
     return ROUTE_HALO;
   if (g.C % 8 == 0 && g.Co % 8 == 0 && T <= 64) return ROUTE_GEMM_G2;
@@ -33,6 +40,7 @@ int conv_fwd_route(ConvRouteGeom g) {
 
 int conv_dgrad_route(ConvRouteGeom g) {
   const int M = g.N * g.H * g.W, T = g.KH * g.KW;
+  if (T == 1 && g.SH == 1 && g.SW == 1 && g.PH == 0 && g.PW == 0 && splitk_1x1(M, g.Co, g.C)) return ROUTE_GEMM_G2;
   // the data gradient of a 'same' stride-1 conv is a 'same' conv of dY with the flipped taps
   if (same_reach1(g) && (T > 1 || halo_1x1(M, g.Co, g.C)) && hconv_supported(g.N, g.H, g.W, g.Co, g.C, T))
     return ROUTE_HALO;

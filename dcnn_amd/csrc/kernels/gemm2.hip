@@ -20,6 +20,9 @@
 // The weight-gradient kernel (tn2) uses the same loader on both operands (pixels = K) and
 // ds_read_b64_tr_b16 transposed fragment reads; split-K partials go to an fp32 slab.
 #include <cstdio>
+#include <cstdlib>
+#include <map>
+#include <mutex>
 
 #include "common.h"
 #include "api.h"
@@ -60,6 +63,143 @@ struct G2 {
   __device__ static __forceinline__ int off(int row, int ch) { return row * (BK * 2) + ((ch ^ swz(row)) << 4); }
 };
 
+// ---- epilogue 2 (shared by the GEMM and its split-K epilogue kernel): the bf16 tile staged in
+// LDS ([BM][EPI_PITCH]) -> 16-byte rows to global (+residual, ReLU, backward-BN mask) and the
+// BatchNorm statistics rows of the stored values. All 256 threads; holds barriers.
+template <int BM, int BN, int EPI_PITCH>
+__device__ __forceinline__ void g2_epilogue2(const G2Args& p, char* smem, int m0, int n0, int tm, int mcls, int ory,
+                                             int orx) {
+  const int tid = threadIdx.x;
+  // ---- epilogue 2: 16-byte rows -> global (+residual, ReLU, BN partial stats) ----
+  constexpr int CG = BN / 8;           // column groups of 8
+  constexpr int RSTEP = 256 / CG;      // rows handled concurrently
+  const int cg = tid % CG, r0 = tid / CG;
+  const int ncol = n0 + cg * 8;
+  const bool col_ok = ncol < p.N;      // N % 8 == 0 for this kernel
+  float s[8], q[8], mu[8], is[8], pv[8];
+#pragma unroll
+  for (int v = 0; v < 8; ++v) s[v] = q[v] = mu[v] = is[v] = pv[v] = 0.f;
+  const bool bnb = p.bnb.x != nullptr;  // backward-BN fusion (api.h BnbArgs)
+  if (bnb && col_ok) {
+#pragma unroll
+    for (int v = 0; v < 8; ++v) { mu[v] = p.bnb.mean[ncol + v]; is[v] = p.bnb.istd[ncol + v]; }
+  }
+  // forward statistics about a pivot (tile row 0, always a valid row): (count, mean, M2) triples
+  float piv_col = 0.f;
+  if (p.stats && !bnb) {
+    unpack8(*reinterpret_cast<const uint4*>(smem + cg * 16), pv);
+    if (tid < BN) piv_col = (float)*reinterpret_cast<const bf16*>(smem + tid * 2);
+  }
+  const int ghw = p.GH * p.GW;
+  auto orow_of = [&](int row) {
+    const int ml = m0 + row - mcls;
+    const int img = ml / ghw, rem = ml - img * ghw;
+    const int gy = rem / p.GW, gx = rem - gy * p.GW;
+    return ((long)img * p.OH + gy * p.OSY + ory) * p.OW + gx * p.OSX + orx;
+  };
+  // every row's operands are loaded before the first store: a load's wait also waits for every
+  // older store, and one latency per tile instead of one per row matters at 2 waves per SIMD
+  const bool has_res = p.residual != nullptr, has_y = bnb && p.bnb.y != nullptr, has_x = bnb && p.stats;
+  constexpr int NR = BM / RSTEP;       // rows per thread
+  uint4 c_res[NR], c_y[NR], c_x[NR];
+#pragma unroll
+  for (int i = 0; i < NR; ++i) {
+    c_res[i] = c_y[i] = c_x[i] = uint4{0u, 0u, 0u, 0u};
+    const int row = r0 + i * RSTEP;
+    if (m0 + row >= p.M || !col_ok) continue;
+    const long o = orow_of(row) * p.ldc + ncol;
+    if (has_res) c_res[i] = *reinterpret_cast<const uint4*>(p.residual + o);
+    if (has_y) c_y[i] = *reinterpret_cast<const uint4*>(p.bnb.y + o);
+    if (has_x) c_x[i] = *reinterpret_cast<const uint4*>(p.bnb.x + o);
+  }
+#pragma unroll
+  for (int i = 0; i < NR; ++i) {
+    const int row = r0 + i * RSTEP;
+    const int m = m0 + row;
+    if (m < p.M && col_ok) {
+      const long orow = orow_of(row);
+      float f[8];
+      unpack8(*reinterpret_cast<const uint4*>(smem + row * EPI_PITCH + cg * 16), f);
+      if (has_res) {
+        float rr[8];
+        unpack8(c_res[i], rr);
+#pragma unroll
+        for (int v = 0; v < 8; ++v) f[v] += rr[v];
+      }
+      if (p.relu) {
+#pragma unroll
+        for (int v = 0; v < 8; ++v) f[v] = fmaxf(f[v], 0.f);
+      }
+      if (has_y) {
+        float yo[8];
+        unpack8(c_y[i], yo);
+#pragma unroll
+        for (int v = 0; v < 8; ++v) f[v] = yo[v] > 0.f ? f[v] : 0.f;
+      }
+      const uint4 o = pack8(f);
+      *reinterpret_cast<uint4*>(reinterpret_cast<bf16*>(p.C) + orow * p.ldc + ncol) = o;
+      if (p.stats) {
+        float g[8];
+        unpack8(o, g);
+        if (bnb) {
+          float xv[8];
+          unpack8(c_x[i], xv);
+#pragma unroll
+          for (int v = 0; v < 8; ++v) { s[v] += g[v]; q[v] += g[v] * (xv[v] - mu[v]) * is[v]; }
+        } else {
+#pragma unroll
+          for (int v = 0; v < 8; ++v) { const float d = g[v] - pv[v]; s[v] += d; q[v] += d * d; }
+        }
+      }
+    }
+  }
+  if (p.stats) {
+    __syncthreads();
+    float* red = reinterpret_cast<float*>(smem);  // [RSTEP][2][BN]
+#pragma unroll
+    for (int v = 0; v < 8; ++v) {
+      red[(r0 * 2 + 0) * BN + cg * 8 + v] = s[v];
+      red[(r0 * 2 + 1) * BN + cg * 8 + v] = q[v];
+    }
+    __syncthreads();
+    // (folded statistics: agent-coherent row stores, read back by the group's last arriver)
+    const bool fold = p.fold.tickets != nullptr;
+    const __amdgpu_buffer_rsrc_t rsS = stat_rsrc(p.stats);
+    if (bnb) {  // backward: plain sums [tiles][2][N]
+      for (int c = tid; c < 2 * BN; c += 256) {
+        const int which = c / BN, cc = c % BN;
+        if (n0 + cc < p.N) {
+          float a = 0.f;
+          for (int k = 0; k < RSTEP; ++k) a += red[(k * 2 + which) * BN + cc];
+          const long o = ((long)tm * 2 + which) * p.N + n0 + cc;
+          if (fold) stat_store_sc1(rsS, o, a);
+          else p.stats[o] = a;
+        }
+      }
+    } else if (tid < BN && n0 + tid < p.N) {  // forward: Welford triple [tiles][3][N]
+      float a = 0.f, b = 0.f;
+      for (int k = 0; k < RSTEP; ++k) { a += red[(k * 2 + 0) * BN + tid]; b += red[(k * 2 + 1) * BN + tid]; }
+      const float cnt = (float)min(BM, p.M - m0);
+      const Welford w = welford_from_shifted(cnt, piv_col, a, b);
+      if (fold) {
+        const long o = ((long)tm * 3) * p.N + n0 + tid;
+        stat_store_sc1(rsS, o, w.n);
+        stat_store_sc1(rsS, o + p.N, w.mean);
+        stat_store_sc1(rsS, o + 2l * p.N, w.m2);
+      } else {
+        store_welford(p.stats, tm, p.N, n0 + tid, w);
+      }
+    }
+    if (fold) {  // this tile's slice of statistics row tm arrives (stat_fold.h)
+      __syncthreads();  // (the reduction scratch is the fold's LDS)
+      const int rows = (p.M + BM - 1) / BM;
+      int* flags = reinterpret_cast<int*>(smem + kStatFoldLds);
+      if (bnb) stat_fold_arrive<1>(p.stats, rows, p.N, 1, [&](int) { return tm; }, p.fold, flags, smem);
+      else stat_fold_arrive<0>(p.stats, rows, p.N, 1, [&](int) { return tm; }, p.fold, flags, smem);
+    }
+  }
+}
+
 template <int BM, int BN, int BK, bool UNI, int NST>
 __global__ void __launch_bounds__(256, 2) gemm_g2_kernel(G2Args p) {
   prefetch_kernargs<sizeof(G2Args)>();
@@ -68,7 +208,11 @@ __global__ void __launch_bounds__(256, 2) gemm_g2_kernel(G2Args p) {
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const int wm = wid >> 1, wn = wid & 1;
   const int tiles_n = (p.N + BN - 1) / BN;
-  const int lt = xcd_remap2(blockIdx.x, gridDim.x);
+  const int lt_all = xcd_remap2(blockIdx.x, gridDim.x);
+  // split-K (plain 1x1 GEMMs with long K on small grids, gemm_g2()): workgroup = (tile, K slice);
+  // the slices of a tile are neighbours in the remapped order (one XCD's L2 holds the tile's B)
+  const int ks = p.ksplit > 1 ? p.ksplit : 1;
+  const int lt = lt_all / ks, kslice = lt_all - lt * ks;
   const int tm = lt / tiles_n, tn = lt % tiles_n;
   // row class of this tile (grouped strided-dgrad phases; one class otherwise). The classes are
   // interleaved tile row by tile row: each XCD's contiguous share of the remapped grid holds every
@@ -187,7 +331,15 @@ __global__ void __launch_bounds__(256, 2) gemm_g2_kernel(G2Args p) {
     for (int j = 0; j < T::TN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
   const int K = ntp * p.Cs;
-  const int nk = (K + BK - 1) / BK;
+  const int nk_all = (K + BK - 1) / BK;
+  // this workgroup's K-steps [kb, kb + nk) (all of them without split-K)
+  const int kb = (int)((long)nk_all * kslice / ks);
+  const int nk = (int)((long)nk_all * (kslice + 1) / ks) - kb;
+  if constexpr (UNI) {  // (the stage counters start at the slice's first K-step)
+    const int k0 = kb * BK;
+    st_t = k0 / p.Cs;
+    st_c = k0 - st_t * p.Cs;
+  }
   auto compute = [&](int buf) {
     const char* As = smem + buf * T::STAGE;
     const char* Bs = As + BM * BK * 2;
@@ -216,13 +368,14 @@ __global__ void __launch_bounds__(256, 2) gemm_g2_kernel(G2Args p) {
       __builtin_amdgcn_s_setprio(0);
     }
   };
+  const int kofs = kb * BK;
   if constexpr (NST == 2) {
-    stage(0, 0);
+    stage(0, kofs);
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
     int cur = 0;
     for (int kt = 0; kt < nk; ++kt) {
-      if (kt + 1 < nk) stage(cur ^ 1, (kt + 1) * BK);
+      if (kt + 1 < nk) stage(cur ^ 1, kofs + (kt + 1) * BK);
       compute(cur);
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       __syncthreads();
@@ -233,9 +386,9 @@ __global__ void __launch_bounds__(256, 2) gemm_g2_kernel(G2Args p) {
     // MFMA phases to land. Only counted vmcnt waits (the newest stage stays in flight across
     // the barrier) and raw s_barrier, which unlike __syncthreads() does not drain the
     // outstanding LDS-DMA.
-    stage(0, 0);
+    stage(0, kofs);
     if (nk > 1) {
-      stage(1, BK);
+      stage(1, kofs + BK);
       asm volatile("s_waitcnt vmcnt(%0)" ::"n"(T::INS) : "memory");
     } else {
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -244,7 +397,7 @@ __global__ void __launch_bounds__(256, 2) gemm_g2_kernel(G2Args p) {
     int cur = 0;
     for (int kt = 0; kt < nk; ++kt) {
       const bool more = kt + 2 < nk;
-      if (more) stage(cur == 0 ? 2 : cur - 1, (kt + 2) * BK);
+      if (more) stage(cur == 0 ? 2 : cur - 1, kofs + (kt + 2) * BK);
       compute(cur);
       if (more) asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)" ::"n"(T::INS) : "memory");
       else asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
@@ -254,6 +407,23 @@ __global__ void __launch_bounds__(256, 2) gemm_g2_kernel(G2Args p) {
     }
   }
 
+  if (ks > 1) {
+    // fp32 partial tile of this K slice -> kpart[slice][M][N] (the epilogue kernel sums the
+    // slices in order and runs the epilogue, g2_splitk_epi_kernel)
+    float* out = p.kpart + (long)kslice * p.M * p.N;
+#pragma unroll
+    for (int i = 0; i < T::TM; ++i)
+#pragma unroll
+      for (int j = 0; j < T::TN; ++j) {
+        const int n = n0 + wn * (BN / 2) + j * 16 + (lane & 15);
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int m = m0 + wm * (BM / 2) + i * 16 + (lane >> 4) * 4 + r;
+          if (m < p.M && n < p.N) out[(long)m * p.N + n] = acc[i][j][r];
+        }
+      }
+    return;
+  }
   // ---- epilogue 1: acc (+bias) -> bf16 LDS tile [BM][BN] ----
 #pragma unroll
   for (int j = 0; j < T::TN; ++j) {
@@ -268,134 +438,69 @@ __global__ void __launch_bounds__(256, 2) gemm_g2_kernel(G2Args p) {
       }
   }
   __syncthreads();
-  // ---- epilogue 2: 16-byte rows -> global (+residual, ReLU, BN partial stats) ----
-  constexpr int CG = BN / 8;           // column groups of 8
-  constexpr int RSTEP = 256 / CG;      // rows handled concurrently
-  const int cg = tid % CG, r0 = tid / CG;
-  const int ncol = n0 + cg * 8;
-  const bool col_ok = ncol < p.N;      // N % 8 == 0 for this kernel
-  float s[8], q[8], mu[8], is[8], pv[8];
+  g2_epilogue2<BM, BN, T::EPI_PITCH>(p, smem, m0, n0, tm, mcls, ory, orx);
+}
+
+constexpr int kG2MaxSplit = 8;  // K slices of the split-K path at most
+
+// split-K epilogue (gemm_g2 with ksplit > 1): output tile (tm, tn) = the fixed-order sum of the
+// K slices' fp32 partials (+bias), staged as the bf16 tile epilogue 1 would have staged, then the
+// GEMM's own epilogue 2 (residual, ReLU, backward-BN mask, statistics rows) — the same statistics
+// row per BM-row tile as the unsplit kernel, so the consumers see the same layout
+template <int BM, int BN>
+__global__ void __launch_bounds__(256, 2) g2_splitk_epi_kernel(G2Args p) {
+  prefetch_kernargs<sizeof(G2Args)>();
+  constexpr int EPI_PITCH = BN * 2 + 16;
+  constexpr int RSTEP = 256 / (BN / 8);
+  constexpr int L1 = BM * EPI_PITCH, L2 = RSTEP * 2 * BN * 4, L3 = kStatFoldLds + 64 * 4;
+  constexpr int LDS = L1 > L2 ? (L1 > L3 ? L1 : L3) : (L2 > L3 ? L2 : L3);
+  __shared__ __attribute__((aligned(16))) char smem[LDS];
+  const int tid = threadIdx.x;
+  const int tiles_n = (p.N + BN - 1) / BN;
+  const int lt = xcd_remap2(blockIdx.x, gridDim.x);
+  const int tm = lt / tiles_n, tn = lt % tiles_n;
+  const int m0 = tm * BM, n0 = tn * BN;
+  constexpr int C4 = BN / 4, RS = 256 / C4;  // 4 columns per thread, RS rows at a time
+  const int c4 = tid % C4, rr = tid / C4;
+  const int n = n0 + c4 * 4;
+  float bv[4] = {0.f, 0.f, 0.f, 0.f};
+  if (p.bias && n < p.N) {
 #pragma unroll
-  for (int v = 0; v < 8; ++v) s[v] = q[v] = mu[v] = is[v] = pv[v] = 0.f;
-  const bool bnb = p.bnb.x != nullptr;  // backward-BN fusion (api.h BnbArgs)
-  if (bnb && col_ok) {
-#pragma unroll
-    for (int v = 0; v < 8; ++v) { mu[v] = p.bnb.mean[ncol + v]; is[v] = p.bnb.istd[ncol + v]; }
+    for (int v = 0; v < 4; ++v) bv[v] = p.bias[n + v];
   }
-  // forward statistics about a pivot (tile row 0, always a valid row): (count, mean, M2) triples
-  float piv_col = 0.f;
-  if (p.stats && !bnb) {
-    unpack8(*reinterpret_cast<const uint4*>(smem + cg * 16), pv);
-    if (tid < BN) piv_col = (float)*reinterpret_cast<const bf16*>(smem + tid * 2);
-  }
-  const int ghw = p.GH * p.GW;
-  auto orow_of = [&](int row) {
-    const int ml = m0 + row - mcls;
-    const int img = ml / ghw, rem = ml - img * ghw;
-    const int gy = rem / p.GW, gx = rem - gy * p.GW;
-    return ((long)img * p.OH + gy * p.OSY + ory) * p.OW + gx * p.OSX + orx;
-  };
-  // every row's operands are loaded before the first store: a load's wait also waits for every
-  // older store, and one latency per tile instead of one per row matters at 2 waves per SIMD
-  const bool has_res = p.residual != nullptr, has_y = bnb && p.bnb.y != nullptr, has_x = bnb && p.stats;
-  constexpr int NR = BM / RSTEP;       // rows per thread
-  uint4 c_res[NR], c_y[NR], c_x[NR];
+  const long slice = (long)p.M * p.N;
+  const int ks = p.ksplit;  // (<= kG2MaxSplit)
+  // every slice's partial of two rows is loaded before the first add (one memory latency per
+  // row pair, not one per slice), then summed in slice order (deterministic)
+  static_assert((BM / RS) % 2 == 0, "row pairs");
+#pragma unroll 1
+  for (int row = rr; row < BM; row += 2 * RS) {
+    float4 v[2][kG2MaxSplit];
 #pragma unroll
-  for (int i = 0; i < NR; ++i) {
-    c_res[i] = c_y[i] = c_x[i] = uint4{0u, 0u, 0u, 0u};
-    const int row = r0 + i * RSTEP;
-    if (m0 + row >= p.M || !col_ok) continue;
-    const long o = orow_of(row) * p.ldc + ncol;
-    if (has_res) c_res[i] = *reinterpret_cast<const uint4*>(p.residual + o);
-    if (has_y) c_y[i] = *reinterpret_cast<const uint4*>(p.bnb.y + o);
-    if (has_x) c_x[i] = *reinterpret_cast<const uint4*>(p.bnb.x + o);
-  }
+    for (int h = 0; h < 2; ++h) {
+      const int m = m0 + row + h * RS;
+      const bool ok = m < p.M && n < p.N;
+      const float* src = p.kpart + (long)(ok ? m : 0) * p.N + (ok ? n : 0);
 #pragma unroll
-  for (int i = 0; i < NR; ++i) {
-    const int row = r0 + i * RSTEP;
-    const int m = m0 + row;
-    if (m < p.M && col_ok) {
-      const long orow = orow_of(row);
-      float f[8];
-      unpack8(*reinterpret_cast<const uint4*>(smem + row * T::EPI_PITCH + cg * 16), f);
-      if (has_res) {
-        float rr[8];
-        unpack8(c_res[i], rr);
+      for (int k = 0; k < kG2MaxSplit; ++k)
+        v[h][k] = (ok && k < ks) ? *reinterpret_cast<const float4*>(src + k * slice) : make_float4(0.f, 0.f, 0.f, 0.f);
+    }
 #pragma unroll
-        for (int v = 0; v < 8; ++v) f[v] += rr[v];
+    for (int h = 0; h < 2; ++h) {
+      float4 acc = v[h][0];
+#pragma unroll
+      for (int k = 1; k < kG2MaxSplit; ++k) {
+        acc.x += v[h][k].x; acc.y += v[h][k].y; acc.z += v[h][k].z; acc.w += v[h][k].w;
       }
-      if (p.relu) {
-#pragma unroll
-        for (int v = 0; v < 8; ++v) f[v] = fmaxf(f[v], 0.f);
-      }
-      if (has_y) {
-        float yo[8];
-        unpack8(c_y[i], yo);
-#pragma unroll
-        for (int v = 0; v < 8; ++v) f[v] = yo[v] > 0.f ? f[v] : 0.f;
-      }
-      const uint4 o = pack8(f);
-      *reinterpret_cast<uint4*>(reinterpret_cast<bf16*>(p.C) + orow * p.ldc + ncol) = o;
-      if (p.stats) {
-        float g[8];
-        unpack8(o, g);
-        if (bnb) {
-          float xv[8];
-          unpack8(c_x[i], xv);
-#pragma unroll
-          for (int v = 0; v < 8; ++v) { s[v] += g[v]; q[v] += g[v] * (xv[v] - mu[v]) * is[v]; }
-        } else {
-#pragma unroll
-          for (int v = 0; v < 8; ++v) { const float d = g[v] - pv[v]; s[v] += d; q[v] += d * d; }
-        }
-      }
+      bf16* d = reinterpret_cast<bf16*>(smem + (row + h * RS) * EPI_PITCH + c4 * 8);
+      d[0] = (bf16)(acc.x + bv[0]);
+      d[1] = (bf16)(acc.y + bv[1]);
+      d[2] = (bf16)(acc.z + bv[2]);
+      d[3] = (bf16)(acc.w + bv[3]);
     }
   }
-  if (p.stats) {
-    __syncthreads();
-    float* red = reinterpret_cast<float*>(smem);  // [RSTEP][2][BN]
-#pragma unroll
-    for (int v = 0; v < 8; ++v) {
-      red[(r0 * 2 + 0) * BN + cg * 8 + v] = s[v];
-      red[(r0 * 2 + 1) * BN + cg * 8 + v] = q[v];
-    }
-    __syncthreads();
-    // (folded statistics: agent-coherent row stores, read back by the group's last arriver)
-    const bool fold = p.fold.tickets != nullptr;
-    const __amdgpu_buffer_rsrc_t rsS = stat_rsrc(p.stats);
-    if (bnb) {  // backward: plain sums [tiles][2][N]
-      for (int c = tid; c < 2 * BN; c += 256) {
-        const int which = c / BN, cc = c % BN;
-        if (n0 + cc < p.N) {
-          float a = 0.f;
-          for (int k = 0; k < RSTEP; ++k) a += red[(k * 2 + which) * BN + cc];
-          const long o = ((long)tm * 2 + which) * p.N + n0 + cc;
-          if (fold) stat_store_sc1(rsS, o, a);
-          else p.stats[o] = a;
-        }
-      }
-    } else if (tid < BN && n0 + tid < p.N) {  // forward: Welford triple [tiles][3][N]
-      float a = 0.f, b = 0.f;
-      for (int k = 0; k < RSTEP; ++k) { a += red[(k * 2 + 0) * BN + tid]; b += red[(k * 2 + 1) * BN + tid]; }
-      const float cnt = (float)min(BM, p.M - m0);
-      const Welford w = welford_from_shifted(cnt, piv_col, a, b);
-      if (fold) {
-        const long o = ((long)tm * 3) * p.N + n0 + tid;
-        stat_store_sc1(rsS, o, w.n);
-        stat_store_sc1(rsS, o + p.N, w.mean);
-        stat_store_sc1(rsS, o + 2l * p.N, w.m2);
-      } else {
-        store_welford(p.stats, tm, p.N, n0 + tid, w);
-      }
-    }
-    if (fold) {  // this tile's slice of statistics row tm arrives (stat_fold.h)
-      __syncthreads();  // (the reduction scratch is the fold's LDS)
-      const int rows = (p.M + BM - 1) / BM;
-      int* flags = reinterpret_cast<int*>(smem + kStatFoldLds);
-      if (bnb) stat_fold_arrive<1>(p.stats, rows, p.N, 1, [&](int) { return tm; }, p.fold, flags, smem);
-      else stat_fold_arrive<0>(p.stats, rows, p.N, 1, [&](int) { return tm; }, p.fold, flags, smem);
-    }
-  }
+  __syncthreads();
+  g2_epilogue2<BM, BN, EPI_PITCH>(p, smem, m0, n0, tm, 0, p.cls_ory[0], p.cls_orx[0]);
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -622,9 +727,64 @@ __global__ void __launch_bounds__(256, 2) gemm_t2_kernel(T2Args p) {
 // tile but 128x128), else 2 (g2_stages() == 0: that rule)
 static int g2_stages() { return 0; }
 
+// split-K partial workspace per (device, stream): grow-only, allocated in the eager warm-up
+// before a graph captures the step (a capture that would need a larger one throws)
+static float* g2_kpart(size_t bytes, hipStream_t s) {
+  static std::mutex mu;
+  static std::map<std::pair<int, hipStream_t>, std::pair<float*, size_t>> ws;
+  int dev = 0;
+  DCNN_HIP_CHECK(hipGetDevice(&dev));
+  std::lock_guard<std::mutex> g(mu);
+  auto& e = ws[{dev, s}];
+  if (e.second < bytes) {
+    hipStreamCaptureStatus st = hipStreamCaptureStatusNone;
+    DCNN_HIP_CHECK(hipStreamIsCapturing(s, &st));
+    if (st != hipStreamCaptureStatusNone)
+      throw std::runtime_error("gemm_g2: split-K workspace must grow outside graph capture (run a step eagerly first)");
+    if (e.first) DCNN_HIP_CHECK(hipFree(e.first));
+    const size_t n = bytes > (size_t)(32 << 20) ? bytes : (size_t)(32 << 20);
+    DCNN_HIP_CHECK(hipMalloc(&e.first, n));
+    e.second = n;
+  }
+  return e.first;
+}
+
+// tuning / test hook: split-K for long-K 1x1 GEMMs on small grids (DCNN_G2_SPLITK=0: off)
+static int g_g2_splitk = [] {
+  const char* v = std::getenv("DCNN_G2_SPLITK");
+  return (v && v[0] == '0') ? 0 : 1;
+}();
+void gemm_g2_set_splitk(int on) { g_g2_splitk = on; }
+int gemm_g2_splitk_enabled() { return g_g2_splitk; }
+
+// K slices of a plain 1x1 GEMM (one tap, unit strides, no row classes) with K >= 1024 whose tile
+// grid cannot fill the chip: enough slices for ~512 workgroups, each keeping >= 4 K-steps
+static int g2_ksplit(const G2Args& a, int tiles, int bk) {
+  if (g_g2_splitk != 1 || a.ntaps != 1 || a.ncls > 1 || a.Cs < 1024 || tiles >= 256) return 1;
+  if (a.tap_dy[0] != 0 || a.tap_dx[0] != 0 || a.SY != 1 || a.SX != 1 || a.OSY != 1 || a.OSX != 1 ||
+      a.GH != a.H || a.GW != a.W || a.OH != a.GH || a.OW != a.GW || a.ldc != a.N || a.fold.tickets)
+    return 1;
+  const int nk = (a.Cs + bk - 1) / bk;
+  int ks = (512 + tiles - 1) / tiles;
+  if (ks > nk / 4) ks = nk / 4;
+  if (ks > kG2MaxSplit) ks = kG2MaxSplit;
+  return ks < 2 ? 1 : ks;
+}
+
 template <int BM, int BN, int BK, bool UNI>
-static void launch_g2(const G2Args& a, hipStream_t s) {
-  const int tiles = ((a.M + BM - 1) / BM) * ((a.N + BN - 1) / BN);
+static void launch_g2(const G2Args& a0, hipStream_t s) {
+  const int tiles = ((a0.M + BM - 1) / BM) * ((a0.N + BN - 1) / BN);
+  G2Args a = a0;
+  a.ksplit = g2_ksplit(a0, tiles, BK);
+  if (a.ksplit > 1) {
+    a.kpart = g2_kpart((size_t)a.ksplit * a.M * a.N * 4, s);
+    hipLaunchKernelGGL((gemm_g2_kernel<BM, BN, BK, UNI, 2>), dim3(tiles * a.ksplit), dim3(256), 0, s, a);
+    DCNN_LAUNCH_CHECK();
+    a.zero_ptr = nullptr;  // (zeroed by the GEMM launch)
+    hipLaunchKernelGGL((g2_splitk_epi_kernel<BM, BN>), dim3(tiles), dim3(256), 0, s, a);
+    DCNN_LAUNCH_CHECK();
+    return;
+  }
   // single-step K loops (1x1 convs on 32-64 channels and their data gradients) never use a third
   // ring stage: 2 stages there free LDS for one more resident workgroup per CU (layer-1 1x1 dgrad
   // 27.0 -> 22.3 us; two-step loops keep 3 stages: both steps in flight from the prologue)
@@ -645,6 +805,8 @@ static void launch_g2(const G2Args& a, hipStream_t s) {
 // Tile choice: the largest tile that still gives >= ~2 workgroups per CU.
 void g2_tile(int M, int N, int* bm, int* bn) {
   auto tiles = [&](int m, int n) { return (long)((M + m - 1) / m) * ((N + n - 1) / n); };
+  // (DCNN_G2_SPLITK=2 experiment: grids below 192 tiles of 64 x 64 on 32 x 64 tiles instead)
+  if (g_g2_splitk == 2 && N <= 256 && tiles(64, 64) < 192) { *bm = 32; *bn = 64; return; }
   if (N >= 128 && tiles(128, 128) >= 480) { *bm = 128; *bn = 128; return; }
   // wide-N, mid-M (8x8-map convs of 256 channels, M = 16384): 64 x 128 beats 128 x 64 at the
   // same tile count (layer-3 strided forward 32.7 -> 29.5 us, layer-4 strided dgrad 42.7 -> 40.0)
@@ -696,6 +858,7 @@ void gemm_g2(const G2Args& a_in, hipStream_t s) {
   DCNN_G2(128, 64, 64, true);
   DCNN_G2(64, 128, 64, true);
   DCNN_G2(64, 64, 64, true);
+  DCNN_G2(32, 64, 64, true);
   DCNN_G2(128, 128, 32, true);
   DCNN_G2(128, 64, 32, true);
   DCNN_G2(64, 128, 32, true);
