@@ -200,6 +200,7 @@ class BatchNorm : public Layer {
   // GPU: the following ReLU + max-pool run inside this layer's training apply (fuse_bn_relu; the
   // stem's BatchNorm -> ReLU -> max-pool)
   void set_fused_pool(class Pool2D* p) { fused_pool_ = p; }
+  bool fused_pool() const { return fused_pool_ != nullptr; }
   // backward-fusion operands of micro-batch `mb` (its forward's input, output mask, statistics)
   gpu_ops::BnbOperands bnb_operands(int mb);
   // the next backward over the gradient at `dy` takes its statistics from this consumer slab (the

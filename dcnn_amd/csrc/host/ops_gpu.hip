@@ -380,7 +380,10 @@ void rec(const char* op, const ConvShape& s, int route, std::initializer_list<st
 }
 // test-only fault injection (capi.cpp dcnn_c_set_fault): bit 0 drops the fused BatchNorm
 // backward's ReLU mask operand in conv_dgrad (the geometry test must then fail)
-int g_fault = 0;
+int g_fault = [] {  // (DCNN_TEST_FAULT=<bits>: the same faults for a whole test process)
+  const char* v = std::getenv("DCNN_TEST_FAULT");
+  return v && *v ? std::atoi(v) : 0;
+}();
 
 // split-K workspace of a halo conv: (partials, zeroed ticket words) — the kernel leaves them zeroed
 void hconv_workspace(HConvArgs& a) {

@@ -288,6 +288,54 @@ def test_cpp_resnet18_gpu_gradients_match_cpu_backend(bins, tmp_path):
     assert rows[-1][2] < 2e-2 and rows[-2][2] < 2e-2, rows[-2:]  # classifier weights / bias
     assert not bad, bad
 
+def _segments(out):
+    rows = []
+    for line in out.splitlines():
+        if line.startswith("segment "):
+            f = line.split()
+            rows.append((f[3], float(f[5]), float(f[7]), float(f[9]), f[10], float(f[12]), float(f[14])))
+    return rows
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("model,batch", [("resnet18_tiny_imagenet", 64), ("resnet50_tiny_imagenet", 32)])
+def test_cpp_gpu_layers_teacher_forced_absolute(bins, tmp_path, model, batch):
+    """Every segment of the C++ GPU backend (a top-level layer — residual blocks with all their
+    internal fusions — or a BatchNorm with the ReLU / max-pool fused into it) against the CPU
+    backend's fp32 step, fed the CPU input and output gradient (teacher forcing: no error
+    compounding through the network), with absolute bounds per segment: output, input gradient
+    and every parameter gradient to bf16 accuracy. A deliberately dropped BatchNorm ReLU mask in
+    the dgrad epilogue (DCNN_TEST_FAULT=1) must fail it.
+    Reference parity: unit_tests/layer_device_agnosticity_test.cpp:60-103."""
+    out = _run([bins["host_api_parity"], "blocks", model, str(batch), "--device", "GPU"], tmp_path, timeout=600)
+    rows = _segments(out)
+    assert len(rows) >= 10, out[-2000:]
+    print("segments (name, fwd rel, bwd rel, param rel, worst param, bwd cosine, param cosine):")
+    for row in rows:
+        print(row)
+    env = dict(os.environ, DCNN_TEST_FAULT="1")
+    r = subprocess.run([bins["host_api_parity"], "blocks", model, str(batch), "--device", "GPU"], cwd=tmp_path,
+                       env=env, stdout=subprocess.PIPE, stderr=subprocess.STDOUT, text=True, timeout=600)
+    faulty = _segments(r.stdout)
+    print("with the fault:")
+    for row in faulty:
+        print(row)
+    # measured on MI355X (ResNet-18 b64 / ResNet-50 b32): fwd <= 0.009, bwd <= 0.104 (cosine >=
+    # 0.9946), param <= 0.114 (cosine >= 0.9935); with the fault: bwd >= 0.74, param >= 0.99
+    # (the input gradient is compared with the CPU gradient masked by the producing ReLU where the
+    # GPU conv masks it in its dgrad epilogue: host_api_parity.cpp blocks mode)
+    bad = [r for r in rows if r[1] > 2e-2 or r[2] > 0.2 or r[3] > 0.2 or r[5] < 0.99 or r[6] < 0.99]
+    assert not bad, bad
+    assert len(faulty) == len(rows), r.stdout[-2000:]
+    blocks = [(g, f) for g, f in zip(rows, faulty) if "block" in g[0]]
+    assert blocks
+    for good, bad_row in blocks:
+        assert bad_row[0] == good[0]
+        # the fault drops the mask in every block's first dgrad: input and parameter gradients
+        # fall far outside the bounds above
+        assert bad_row[2] > 0.4 and bad_row[3] > 0.5 and bad_row[6] < 0.9, (good, bad_row)
+
+
 def test_cpp_and_python_cpu_gradients_identical(bins, tmp_path):
     """The C++ host API and the Python front end on the CPU backend: the same initial ResNet-18
     weights and batch give bit-identical parameter gradients (both run the native fp32 kernels;
