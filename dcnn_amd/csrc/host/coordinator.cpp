@@ -485,21 +485,26 @@ StepResult PipelineCoordinator::run_semi_async(std::vector<Pending>& mbs) {
 StepResult PipelineCoordinator::run_1f1b(std::vector<Pending>& mbs) {
   StepResult r;
   const size_t m = mbs.size(), cap = (size_t)std::max(1, num_stages());
-  size_t sent = 0, done = 0;
+  size_t sent = 0, done = 0, outs = 0;
   while (sent < std::min(m, cap)) forward_mb(mbs[sent++]);
   const auto t0 = Clock::now();
-  while (done < m) {
+  // every output AND every backward: with the loss on the last stage, that stage starts a
+  // micro-batch's backward before it reports the loss, so on a transport that does not block its
+  // host (device-ordered IPC, RCCL) the first stage's backward can finish first
+  while (done < m || outs < m) {
     check_errors();
     Message msg;
     // either completion: an output (loss, then its backward) or a finished backward (admit the
     // next forward)
     if (!recv_any({FORWARD_JOB, BACKWARD_JOB}, msg, 20)) {
       if (seconds_since(t0) > o_.timeout_s)
-        throw PipelineError("1F1B: timeout (" + std::to_string(done) + "/" + std::to_string(m) + " backwards done)");
+        throw PipelineError("1F1B: timeout (" + std::to_string(done) + "/" + std::to_string(m) + " backwards, " +
+                            std::to_string(outs) + "/" + std::to_string(m) + " outputs)");
       continue;
     }
     if (msg.command == FORWARD_JOB) {
       take_output(msg, mbs.at(with_mb(msg).mb_id), r);
+      ++outs;
     } else {
       ++done;
       if (sent < m) forward_mb(mbs[sent++]);

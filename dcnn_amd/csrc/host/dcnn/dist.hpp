@@ -152,13 +152,17 @@ class P2PLink {
   // world-1 self loop of the same code path (tests): t's bytes through a one-rank communicator's
   // send + receive pair (one group) into a fresh tensor, ordered like send() / recv()
   static Tensor loopback(const Tensor& t);
+  // a sender / receiver pair on one one-rank communicator (tests of send() / recv() themselves,
+  // each on its own link flow): a send and its receive must be posted inside one
+  // coll::group_start() / group_end() (a rank's send to itself is matched within its group)
+  static std::pair<std::unique_ptr<P2PLink>, std::unique_ptr<P2PLink>> self_pair(int device);
 
  private:
   P2PLink() = default;
   void* flow_ = nullptr;   // gpu::Flow
   void* ready_ = nullptr;  // gpu::Event: the caller's flow reached the hand-off
   void* done_ = nullptr;   // gpu::Event: the last transfer on the link flow
-  std::unique_ptr<coll::Comm> comm_;
+  std::shared_ptr<coll::Comm> comm_;  // (shared by a self_pair)
   bool sender_ = false;
   int peer_ = 0;
   struct Held {

@@ -156,14 +156,26 @@ class PipelineStage {
   // receiver maps the buffer once and copies out on arrival. A (peer, micro-batch) buffer is
   // rewritten only in a later step / batch, after the receiver has consumed it (the coordinator
   // joins every micro-batch before the next one starts).
+  // The hand-off (DCNN_IPC_HANDOFF): "host" (default) — the sender's host waits for its copy
+  // before the message goes out, the receiver's host for its copy out; "event" — an interprocess
+  // event the sender records after its copy, the receiver's flow waits on it; "flag" — each buffer
+  // starts with a 32-bit flag the sender's flow sets to the hand-off's sequence number after its
+  // copy (stream write-value), the receiver's flow waits for it (stream wait-value). In the device-
+  // ordered modes a receiver's copies are complete before it answers UPDATE_PARAMETERS; within a
+  // step every later hand-off on its flow follows them. (Measured: profiles/pipeline_ipc_handoff_r6.md.)
   struct IpcSlot {
-    void* ptr = nullptr;
-    size_t bytes = 0;
+    void* ptr = nullptr;  // flag header (kIpcHeader bytes), then the tensor bytes
+    size_t bytes = 0;     // tensor capacity
     std::string handle;
+    uint32_t seq = 0;     // "flag": the last hand-off's sequence number
+    void* ev = nullptr;   // "event": gpu::Event (interprocess), recorded after each copy
+    std::string ev_handle;
   };
   std::map<std::pair<std::string, uint64_t>, IpcSlot> ipc_out_;
   std::vector<void*> ipc_retired_;                  // outgrown exports (a peer may still map them)
   mutable std::map<std::string, void*> ipc_in_;     // handle -> this process's mapping
+  mutable std::map<std::string, void*> ipc_ev_in_;  // event handle -> this process's event
+  mutable bool ipc_device_ordered_ = false;         // a device-ordered receive since the last update
   void release_ipc();
   // transport "rccl" (GPU stages on distinct devices, any node): stage-to-stage tensors as RCCL
   // sends on per-direction two-rank links (dist::P2PLink); the job message carries only the shape.
@@ -178,6 +190,16 @@ class PipelineStage {
   std::thread beat_;
   std::atomic<bool> beat_stop_{false};
 };
+
+// The RCCL transport's tensor hand-off (PipelineStage's sends / receives on transport "rccl",
+// exposed for the GPU test that drives it through a one-rank link pair, dist::P2PLink::self_pair):
+// send_rccl fills m's typed-job header (shape / dtype code with the RCCL flag; no payload bytes)
+// and sends t's bytes on l; recv_rccl reads that header and receives the bytes from l into a fresh
+// tensor on dev (the current flow waits for it).
+namespace wire {
+void send_rccl(dist::P2PLink& l, const Tensor& t, uint64_t mb, bool as_logits, dcnn_native::Message& m);
+Tensor recv_rccl(dist::P2PLink& l, const dcnn_native::Message& m, Device dev);
+}  // namespace wire
 
 // ---------------------------------------------------------------- coordinator
 class PipelineError : public std::runtime_error {

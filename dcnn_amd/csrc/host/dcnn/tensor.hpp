@@ -104,6 +104,16 @@ void* ipc_alloc(size_t nbytes, void* handle_out);
 void ipc_free(void* p);
 void* ipc_open(const void* handle);  // map a peer process's buffer into this one
 void ipc_close(void* p);
+// stream-ordered 32-bit flag operations on device memory (also a peer's IPC mapping): the IPC
+// transport's hand-off without a host wait. write: *p = v after the current flow's work so far;
+// wait: the current flow's later work starts once *p >= v. false: the device lacks them.
+bool stream_values_supported();
+// inter-process events: an event another process can wait on (its 64-byte handle; nullptr when the
+// runtime cannot export one), and a peer's event opened here
+Event ipc_event_create(void* handle_out);
+Event ipc_event_open(const void* handle);
+void flow_write_u32(void* p, uint32_t v);
+void flow_wait_u32_geq(void* p, uint32_t v);
 }  // namespace gpu
 
 class Storage {

@@ -522,7 +522,7 @@ P2PLink::P2PLink(const std::string& unique_id, int rank, bool sender, int device
   if (rank != 0 && rank != 1) throw std::invalid_argument("P2PLink: rank 0 or 1");
   gpu::set_device(device);
   peer_ = 1 - rank;
-  comm_ = std::make_unique<coll::Comm>(unique_id, 2, rank, device);
+  comm_ = std::make_shared<coll::Comm>(unique_id, 2, rank, device);
   flow_ = gpu::flow_create();
   ready_ = gpu::event_create();
   done_ = gpu::event_create();
@@ -550,7 +550,8 @@ void P2PLink::send(const Tensor& t, uint64_t key) {
   gpu::event_record(ready_);  // (current flow)
   gpu::flow_wait(flow_, ready_);
   comm_->send(t.data(), t.nbytes(), 4, peer_, flow_);  // bytes (uint8)
-  gpu::event_record(h.ev, flow_);
+  // (inside a group the send is enqueued at the group's end: the record follows it there)
+  coll::after_group([ev = h.ev, fl = flow_] { gpu::event_record(ev, fl); });
   h.t = t;
 }
 
@@ -562,8 +563,10 @@ Tensor P2PLink::recv(const std::vector<int64_t>& shape, DType dt, Layout layout,
   gpu::event_record(ready_);
   gpu::flow_wait(flow_, ready_);
   comm_->recv(t.data(), t.nbytes(), 4, peer_, flow_);
-  gpu::event_record(done_, flow_);
-  gpu::flow_wait(gpu::flow(), done_);
+  coll::after_group([this] {
+    gpu::event_record(done_, flow_);
+    gpu::flow_wait(gpu::flow(), done_);
+  });
   return t;
 }
 
@@ -574,11 +577,27 @@ void P2PLink::drain() {
   }
 }
 
+std::pair<std::unique_ptr<P2PLink>, std::unique_ptr<P2PLink>> P2PLink::self_pair(int device) {
+  if (!coll::available()) throw std::runtime_error("dist: RCCL unavailable: " + coll::load_error());
+  gpu::set_device(device);
+  auto comm = std::make_shared<coll::Comm>(coll::unique_id(), 1, 0, device);
+  std::unique_ptr<P2PLink> tx(new P2PLink()), rx(new P2PLink());
+  for (P2PLink* l : {tx.get(), rx.get()}) {
+    l->comm_ = comm;
+    l->peer_ = 0;
+    l->flow_ = gpu::flow_create();
+    l->ready_ = gpu::event_create();
+    l->done_ = gpu::event_create();
+  }
+  tx->sender_ = true;
+  return {std::move(tx), std::move(rx)};
+}
+
 Tensor P2PLink::loopback(const Tensor& t) {
   if (!coll::available()) throw std::runtime_error("dist: RCCL unavailable: " + coll::load_error());
   if (!t.device().is_gpu()) throw std::invalid_argument("P2PLink: device tensors only");
   P2PLink l;
-  l.comm_ = std::make_unique<coll::Comm>(coll::unique_id(), 1, 0, t.device().index);
+  l.comm_ = std::make_shared<coll::Comm>(coll::unique_id(), 1, 0, t.device().index);
   l.flow_ = gpu::flow_create();
   l.ready_ = gpu::event_create();
   l.done_ = gpu::event_create();

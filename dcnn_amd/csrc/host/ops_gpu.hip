@@ -289,6 +289,47 @@ void* ipc_open(const void* handle) {
 void ipc_close(void* p) {
   if (p != nullptr) (void)hipIpcCloseMemHandle(p);
 }
+Event ipc_event_create(void* handle_out) {
+  static_assert(sizeof(hipIpcEventHandle_t) == kIpcHandleBytes, "IPC event handle size");
+  hipEvent_t e = nullptr;
+  if (hipEventCreateWithFlags(&e, hipEventDisableTiming | hipEventInterprocess) != hipSuccess) {
+    (void)hipGetLastError();
+    return nullptr;
+  }
+  hipIpcEventHandle_t h;
+  if (hipIpcGetEventHandle(&h, e) != hipSuccess) {
+    (void)hipGetLastError();
+    (void)hipEventDestroy(e);
+    return nullptr;
+  }
+  std::memcpy(handle_out, &h, sizeof h);
+  return e;
+}
+Event ipc_event_open(const void* handle) {
+  hipIpcEventHandle_t h;
+  std::memcpy(&h, handle, sizeof h);
+  hipEvent_t e = nullptr;
+  HOST_HIP_CHECK(hipIpcOpenEventHandle(&e, h));
+  return e;
+}
+bool stream_values_supported() {
+  static const bool ok = [] {
+    int dev = 0, v = 0;
+    if (hipGetDevice(&dev) != hipSuccess) return false;
+    if (hipDeviceGetAttribute(&v, hipDeviceAttributeCanUseStreamWaitValue, dev) != hipSuccess) {
+      (void)hipGetLastError();
+      return false;
+    }
+    return v != 0;
+  }();
+  return ok;
+}
+void flow_write_u32(void* p, uint32_t v) {
+  HOST_HIP_CHECK(hipStreamWriteValue32(static_cast<hipStream_t>(flow()), p, v, 0));
+}
+void flow_wait_u32_geq(void* p, uint32_t v) {
+  HOST_HIP_CHECK(hipStreamWaitValue32(static_cast<hipStream_t>(flow()), p, v, hipStreamWaitValueGte, 0xffffffffu));
+}
 }  // namespace gpu
 
 namespace gpu_ops {

@@ -26,11 +26,75 @@ constexpr uint8_t kChannelsLast = 0x10;  // dtype flag: NHWC physical buffer of 
 // (transport "ipc", native stages only)
 constexpr uint8_t kIpcRef = 0x20;
 constexpr size_t kIpcRefBytes = gpu::kIpcHandleBytes + sizeof(uint64_t);
+// ... + the hand-off's sequence number ("flag" mode; 0: no flag to wait for) [+ the sender's
+// interprocess event handle ("event" mode)]
+constexpr size_t kIpcRefSeqBytes = kIpcRefBytes + sizeof(uint64_t);
+constexpr size_t kIpcRefEvBytes = kIpcRefSeqBytes + gpu::kIpcHandleBytes;
+constexpr size_t kIpcHeader = 256;  // flag word, padded (the tensor bytes stay 256-byte aligned)
 // dtype flag: the tensor travels on the stage pair's RCCL link; the payload is empty (transport
 // "rccl", native stages only)
 constexpr uint8_t kRcclRef = 0x40;
 constexpr size_t kIdBytes = 128;  // ncclUniqueId
 constexpr uint64_t kFullState = 1;        // SEND_PARAMS "full" / LOAD_PARAMS micro-batch id
+
+enum class Handoff { Host, Event, Flag };
+Handoff ipc_handoff() {
+  static const Handoff h = [] {
+    const char* e = std::getenv("DCNN_IPC_HANDOFF");
+    const std::string v = e ? e : "host";
+    if (v == "event") return Handoff::Event;
+    if (v == "flag") return gpu::stream_values_supported() ? Handoff::Flag : Handoff::Host;
+    if (v != "host") throw std::runtime_error("DCNN_IPC_HANDOFF: host | event | flag");
+    return Handoff::Host;
+  }();
+  return h;
+}
+
+// t's typed-job header: m.shape (logical NCHW dims; NHWC buffers as N, H, W, C with the channels-
+// last flag; logits as (N, classes)), returns the dtype code
+uint8_t encode_header(const Tensor& t, bool as_logits, Message& m) {
+  const auto& s = t.shape();
+  uint8_t code = t.dtype() == DType::F32 ? 0 : t.dtype() == DType::BF16 ? 1 : 0xff;
+  if (code == 0xff) throw std::runtime_error("activation dtype must be fp32 or bf16");
+  m.shape.clear();
+  if (s.size() == 4 && s[2] == 1 && s[3] == 1 && as_logits) {
+    m.shape = {(uint64_t)s[0], (uint64_t)s[1]};  // logits (N, classes)
+  } else if (s.size() == 4 && t.layout() == Layout::NHWC) {
+    m.shape = {(uint64_t)s[0], (uint64_t)s[2], (uint64_t)s[3], (uint64_t)s[1]};
+    code |= kChannelsLast;
+  } else {
+    for (auto d : s) m.shape.push_back((uint64_t)d);
+  }
+  return code;
+}
+
+struct Header {
+  std::vector<int64_t> shape;
+  DType dt = DType::F32;
+  Layout layout = Layout::NCHW;
+  int code = 0;
+};
+Header decode_header(const Message& m) {
+  Header h;
+  h.code = m.payload_type == P_TYPED_JOB ? m.dtype : 0;
+  h.shape.assign(m.shape.begin(), m.shape.end());
+  if ((h.code & kChannelsLast) && h.shape.size() == 4) {
+    h.shape = {h.shape[0], h.shape[3], h.shape[1], h.shape[2]};
+    h.layout = Layout::NHWC;
+  }
+  switch (h.code & 0x0F) {
+    case 0: h.dt = DType::F32; break;
+    case 1: h.dt = DType::BF16; break;
+    default: throw std::runtime_error("activation payloads must be fp32 or bf16");
+  }
+  return h;
+}
+
+// (N, F) tensors travel as rank 2: 1x1 spatial again on arrival
+Tensor as_4d(Tensor t, const std::vector<int64_t>& shape) {
+  if (t.rank() == 2) t = t.view({shape[0], shape[1], 1, 1}, Layout::NCHW);
+  return t;
+}
 
 std::optional<Endpoint> parse_endpoint(const json::Value* v) {
   if (v == nullptr || v->is_null()) return std::nullopt;
@@ -182,9 +246,15 @@ void PipelineStage::connect_links(Message& m) {
 }
 
 void PipelineStage::release_ipc() {
+  if ((!ipc_out_.empty() || !ipc_in_.empty()) && dev_.is_gpu()) gpu::synchronize();  // (no hand-off in flight)
   for (auto& kv : ipc_in_) gpu::ipc_close(kv.second);
   ipc_in_.clear();
-  for (auto& kv : ipc_out_) gpu::ipc_free(kv.second.ptr);
+  for (auto& kv : ipc_ev_in_) gpu::event_destroy(kv.second);
+  ipc_ev_in_.clear();
+  for (auto& kv : ipc_out_) {
+    gpu::ipc_free(kv.second.ptr);
+    if (kv.second.ev) gpu::event_destroy(kv.second.ev);
+  }
   ipc_out_.clear();
   for (void* p : ipc_retired_) gpu::ipc_free(p);
   ipc_retired_.clear();
@@ -233,6 +303,10 @@ void PipelineStage::process(Message& m) {
         if (grad_out_) grad_out_->drain();
         opt_->step(model_->parameters());
         model_->zero_grad();
+        // the step's IPC copies out of the peers' buffers are complete before this answer (the
+        // peers rewrite them in the next step)
+        if (ipc_device_ordered_) gpu::flow_synchronize();
+        ipc_device_ordered_ = false;
         ++n_upd_;
         reply(PARAMETERS_UPDATED);
         break;
@@ -413,42 +487,47 @@ Tensor PipelineStage::decode(Message& m) const {
     m.data = decompress(m.data, (Codec)m.codec, 0);
     m.codec = CODEC_NONE;
   }
-  const int code = m.payload_type == P_TYPED_JOB ? m.dtype : 0;
-  std::vector<int64_t> shape(m.shape.begin(), m.shape.end());
-  Layout layout = Layout::NCHW;
-  if ((code & kChannelsLast) && shape.size() == 4) {
-    shape = {shape[0], shape[3], shape[1], shape[2]};
-    layout = Layout::NHWC;
-  }
-  DType dt;
-  switch (code & 0x0F) {
-    case 0: dt = DType::F32; break;
-    case 1: dt = DType::BF16; break;
-    default: throw std::runtime_error("activation payloads must be fp32 or bf16");
-  }
-  if (code & kRcclRef) {
+  const Header hd = decode_header(m);
+  const std::vector<int64_t>& shape = hd.shape;
+  const DType dt = hd.dt;
+  const Layout layout = hd.layout;
+  if (hd.code & kRcclRef) {
     // the peer's send on this pair's link (sent before the message; RCCL matches in order)
     dist::P2PLink* l = m.command == FORWARD_JOB ? act_in_.get() : m.command == BACKWARD_JOB ? grad_in_.get() : nullptr;
     if (l == nullptr || !dev_.is_gpu()) throw std::runtime_error("RCCL tensor reference without an open link");
-    Tensor t = l->recv(shape, dt, layout, dev_);
-    if (t.rank() == 2) t = t.view({shape[0], shape[1], 1, 1}, Layout::NCHW);
-    return t;
+    return wire::recv_rccl(*l, m, dev_);
   }
-  if (code & kIpcRef) {
-    // a peer stage's device buffer: map it once, copy out now (the sender rewrites it only after
-    // this stage has answered for the micro-batch)
-    if (!dev_.is_gpu() || m.data.size() != kIpcRefBytes) throw std::runtime_error("malformed IPC tensor reference");
+  if (hd.code & kIpcRef) {
+    // a peer stage's device buffer: map it once, copy out on this stage's flow once the sender's
+    // copy into it has completed (its flag; the sender rewrites the buffer only in a later step)
+    if (!dev_.is_gpu() || (m.data.size() != kIpcRefSeqBytes && m.data.size() != kIpcRefEvBytes))
+      throw std::runtime_error("malformed IPC tensor reference");
     Tensor t = Tensor::empty(shape, dt, dev_, layout);
-    uint64_t nbytes = 0;
+    uint64_t nbytes = 0, seq = 0;
     std::memcpy(&nbytes, m.data.data() + gpu::kIpcHandleBytes, sizeof nbytes);
+    std::memcpy(&seq, m.data.data() + kIpcRefBytes, sizeof seq);
     if (nbytes != t.nbytes()) throw std::runtime_error("IPC tensor size does not match its shape");
     const std::string key(m.data.data(), gpu::kIpcHandleBytes);
     auto it = ipc_in_.find(key);
     if (it == ipc_in_.end()) it = ipc_in_.emplace(key, gpu::ipc_open(key.data())).first;
-    gpu::copy(t.data(), it->second, t.nbytes(), 2);
-    gpu::flow_synchronize();  // (this stage's flow: the copy is done before any reply goes out)
-    if (t.rank() == 2) t = t.view({shape[0], shape[1], 1, 1}, Layout::NCHW);
-    return t;
+    char* base = static_cast<char*>(it->second);
+    bool device_ordered = false;
+    if (m.data.size() == kIpcRefEvBytes) {
+      const std::string ek(m.data.data() + kIpcRefSeqBytes, gpu::kIpcHandleBytes);
+      auto e = ipc_ev_in_.find(ek);
+      if (e == ipc_ev_in_.end()) e = ipc_ev_in_.emplace(ek, gpu::ipc_event_open(ek.data())).first;
+      gpu::flow_wait(nullptr, e->second);
+      device_ordered = true;
+    } else if (seq != 0) {
+      gpu::flow_wait_u32_geq(base, (uint32_t)seq);
+      device_ordered = true;
+    }
+    gpu::copy(t.data(), base + kIpcHeader, t.nbytes(), 2);
+    if (device_ordered)
+      ipc_device_ordered_ = true;
+    else
+      gpu::flow_synchronize();  // (host-waited hand-off: the copy is done before any reply goes out)
+    return as_4d(t, shape);
   }
   // a GPU stage's own activation form (bf16 NHWC) goes straight from the payload to the device
   const bool direct = dev_.is_gpu() && dt == DType::BF16 && layout == Layout::NHWC;
@@ -469,40 +548,49 @@ void PipelineStage::send_tensor(const std::string& to, uint16_t cmd, uint64_t mb
   m.payload_type = P_TYPED_JOB;
   m.mb_id = mb;
   if (t.defined()) {
-    const auto& s = t.shape();
-    uint8_t code = t.dtype() == DType::F32 ? 0 : t.dtype() == DType::BF16 ? 1 : 0xff;
-    if (code == 0xff) throw std::runtime_error("activation dtype must be fp32 or bf16");
-    if (s.size() == 4 && s[2] == 1 && s[3] == 1 && as_logits) {
-      m.shape = {(uint64_t)s[0], (uint64_t)s[1]};  // logits (N, classes)
-    } else if (s.size() == 4 && t.layout() == Layout::NHWC) {
-      m.shape = {(uint64_t)s[0], (uint64_t)s[2], (uint64_t)s[3], (uint64_t)s[1]};
-      code |= kChannelsLast;
-    } else {
-      for (auto d : s) m.shape.push_back((uint64_t)d);
-    }
-    m.dtype = code;
     if (cfg_.transport == "rccl" && t.device().is_gpu() && (to == "next_stage" || to == "prev_stage")) {
       dist::P2PLink* l = to == "next_stage" ? act_out_.get() : grad_out_.get();
       if (l == nullptr) throw std::runtime_error("transport 'rccl': the stage links are not open (P2P_CONNECT)");
-      l->send(t, mb);
-      m.dtype = code | kRcclRef;
+      wire::send_rccl(*l, t, mb, as_logits, m);
       comm_->send(std::move(m));
       return;
     }
+    const uint8_t code = encode_header(t, as_logits, m);
+    m.dtype = code;
     if (cfg_.transport == "ipc" && t.device().is_gpu() && (to == "next_stage" || to == "prev_stage")) {
       IpcSlot& slot = ipc_out_[{to, mb}];
       if (slot.bytes < t.nbytes()) {
         if (slot.ptr != nullptr) ipc_retired_.push_back(slot.ptr);
         slot.handle.assign(gpu::kIpcHandleBytes, '\0');
-        slot.ptr = gpu::ipc_alloc(t.nbytes(), slot.handle.data());
+        slot.ptr = gpu::ipc_alloc(kIpcHeader + t.nbytes(), slot.handle.data());
         slot.bytes = t.nbytes();
+        gpu::zero(slot.ptr, kIpcHeader);
+        slot.seq = 0;
       }
-      gpu::copy(slot.ptr, t.data(), t.nbytes(), 2);
-      gpu::flow_synchronize();  // the slot is complete (this stage's flow) before the peer process reads it
+      gpu::copy(static_cast<char*>(slot.ptr) + kIpcHeader, t.data(), t.nbytes(), 2);
+      uint64_t seq = 0;
+      Handoff mode = ipc_handoff();
+      if (mode == Handoff::Event && slot.ev == nullptr) {
+        std::string h(gpu::kIpcHandleBytes, '\0');
+        slot.ev = gpu::ipc_event_create(h.data());
+        if (slot.ev) slot.ev_handle = h;
+      }
+      if (mode == Handoff::Event && slot.ev == nullptr) mode = Handoff::Host;  // (no exportable events)
+      if (mode == Handoff::Flag) {
+        seq = ++slot.seq;
+        if (seq == 0xffffffffull) throw std::runtime_error("IPC hand-off sequence exhausted");
+        gpu::flow_write_u32(slot.ptr, (uint32_t)seq);  // (after the copy: the receiver's flow waits for it)
+      } else if (mode == Handoff::Event) {
+        gpu::event_record(slot.ev);  // (after the copy: the receiver's flow waits for it)
+      } else {
+        gpu::flow_synchronize();  // the slot is complete (this stage's flow) before the peer process reads it
+      }
       const uint64_t nbytes = t.nbytes();
       m.dtype = code | kIpcRef;
       m.data.assign(slot.handle);
       m.data.append(reinterpret_cast<const char*>(&nbytes), sizeof nbytes);
+      m.data.append(reinterpret_cast<const char*>(&seq), sizeof seq);
+      if (mode == Handoff::Event) m.data.append(slot.ev_handle);
       comm_->send(std::move(m));
       return;
     }
@@ -858,5 +946,23 @@ void PipelineStage::stop_heartbeat() {
   beat_stop_ = true;
   if (beat_.joinable()) beat_.join();
 }
+
+namespace wire {
+void send_rccl(dist::P2PLink& l, const Tensor& t, uint64_t mb, bool as_logits, Message& m) {
+  const uint8_t code = encode_header(t, as_logits, m);
+  m.payload_type = P_TYPED_JOB;
+  m.mb_id = mb;
+  m.data.clear();
+  l.send(t, mb);  // (before the message: the receiver posts its receive when the message arrives)
+  m.dtype = code | kRcclRef;
+}
+
+Tensor recv_rccl(dist::P2PLink& l, const Message& m, Device dev) {
+  const Header hd = decode_header(m);
+  if (!(hd.code & kRcclRef)) throw std::runtime_error("not an RCCL tensor reference");
+  if (!dev.is_gpu()) throw std::runtime_error("RCCL tensor reference on a CPU stage");
+  return as_4d(l.recv(hd.shape, hd.dt, hd.layout, dev), hd.shape);
+}
+}  // namespace wire
 
 }  // namespace dcnn

@@ -7,6 +7,7 @@
 #include <mutex>
 #include <stdexcept>
 #include <string>
+#include <vector>
 
 #include <hip/hip_runtime.h>
 #include <rccl/rccl.h>
@@ -118,8 +119,31 @@ std::string unique_id() {
   check(need().get_unique_id(&id), "ncclGetUniqueId");
   return std::string(reinterpret_cast<const char*>(&id), sizeof(id));
 }
-void group_start() { check(need().group_start(), "ncclGroupStart"); }
-void group_end() { check(need().group_end(), "ncclGroupEnd"); }
+namespace {
+thread_local int t_group_depth = 0;
+thread_local std::vector<std::function<void()>> t_after_group;
+}  // namespace
+
+void group_start() {
+  check(need().group_start(), "ncclGroupStart");
+  ++t_group_depth;
+}
+void group_end() {
+  if (t_group_depth > 0) --t_group_depth;
+  check(need().group_end(), "ncclGroupEnd");
+  if (t_group_depth == 0 && !t_after_group.empty()) {
+    std::vector<std::function<void()>> fs;
+    fs.swap(t_after_group);
+    for (auto& f : fs) f();
+  }
+}
+bool in_group() { return t_group_depth > 0; }
+void after_group(std::function<void()> f) {
+  if (t_group_depth > 0)
+    t_after_group.push_back(std::move(f));
+  else
+    f();
+}
 
 Comm::Comm(const std::string& uid, int world, int rank, int device) : world_(world), rank_(rank) {
   if (uid.size() != sizeof(ncclUniqueId)) throw std::runtime_error("rccl: unique id must be 128 bytes");

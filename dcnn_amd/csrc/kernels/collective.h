@@ -12,6 +12,7 @@
 // RCCL send/recv + all-reduce on MI355X.
 #pragma once
 #include <cstddef>
+#include <functional>
 #include <string>
 
 namespace dcnn {
@@ -21,8 +22,13 @@ bool available();
 std::string load_error();
 int version();
 std::string unique_id();  // a fresh 128-byte ncclUniqueId (rank 0 creates it, every rank joins with it)
+// (nestable; the calling thread's group) RCCL enqueues a group's operations at its outermost end
 void group_start();
 void group_end();
+bool in_group();  // the calling thread is inside group_start() / group_end()
+// f after the calling thread's outermost group_end() (at once outside a group): work that must
+// follow a grouped operation on its stream, e.g. an event record
+void after_group(std::function<void()> f);
 
 // dtype codes (shared with parallel/rccl.py): 0 float32, 1 bfloat16, 2 float16, 3 int32, 4 uint8;
 // reduction ops: 0 sum, 1 prod, 2 max, 3 min, 4 avg

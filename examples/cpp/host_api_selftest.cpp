@@ -8,8 +8,11 @@
 #include <sstream>
 #include <string>
 
+#include "../../dcnn_amd/csrc/kernels/collective.h"
+#include "../../dcnn_amd/csrc/native/comm.h"  // (Message: the stage's job messages)
 #include "dcnn/dist.hpp"
 #include "dcnn/nn.hpp"
+#include "dcnn/pipeline.hpp"
 
 using namespace dcnn;
 
@@ -228,6 +231,70 @@ static void test_p2p_loopback() {
   std::printf("p2p loopback ok (%zu + %zu values, %zu differ)\n", ha.size(), v.size(), diff);
 }
 
+// the RCCL stage transport's own send / receive (dist::P2PLink::send / recv, each link on its own
+// flow, and the stage's job-message header: wire::send_rccl / recv_rccl, the functions
+// PipelineStage's transport "rccl" calls) through a one-rank sender / receiver pair — a send to
+// itself is matched within one RCCL group, so each hand-off is one group here, where two stage
+// processes post theirs independently. Activations (bf16 NHWC, produced on the caller's flow just
+// before the send), logits (fp32 (N, classes): rank 2 on the wire) and gradients, interleaved over
+// two micro-batch slots and read back on the caller's flow.
+static void test_p2p_pair() {
+  auto pair = dist::P2PLink::self_pair(0);
+  dist::P2PLink& tx = *pair.first;
+  dist::P2PLink& rx = *pair.second;
+  SequentialBuilder b("p2p_pair");
+  b.input({8, 8, 8}).conv2d(16, 3, 3, 1, 1, 1, 1).batchnorm().activation("relu");
+  Sequential g = b.build();
+  g.set_device(Device::gpu(0));
+  g.initialize(7);
+  size_t checked = 0, differ = 0;
+  for (int k = 0; k < 6; ++k) {
+    SyntheticClassification src(8, 8, 8, 8, 10, 11 + k, 1.0f);
+    src.reset(0);
+    Tensor x, y;
+    src.next(8, x, y);
+    std::vector<float> lv(8 * 10), gv(8 * 16 * 8 * 8);
+    for (size_t i = 0; i < lv.size(); ++i) lv[i] = std::sin(0.37f * (float)(i + 13 * k));
+    for (size_t i = 0; i < gv.size(); ++i) gv[i] = std::cos(0.11f * (float)(i + 7 * k)) * 1e-3f;
+    struct Case {
+      Tensor t;
+      bool logits;
+    } cases[] = {{g.forward(x), false},
+                 {Tensor::from_host(lv, {8, 10, 1, 1}, Device::gpu(0), DType::F32), true},
+                 {Tensor::from_host(gv, {8, 16, 8, 8}, Device::gpu(0), DType::BF16, Layout::NHWC), false}};
+    for (const Case& c : cases) {
+      dcnn_native::Message m;
+      m.command = dcnn_native::FORWARD_JOB;
+      coll::group_start();
+      wire::send_rccl(tx, c.t, (uint64_t)(k % 2), c.logits, m);
+      Tensor r = wire::recv_rccl(rx, m, Device::gpu(0));
+      coll::group_end();
+      CHECK((m.dtype & 0x40) != 0 && m.data.empty() && m.mb_id == (uint64_t)(k % 2));
+      // ((N, F) tensors — the GPU forward's flattened output — arrive as (N, F, 1, 1) NCHW: the same
+      // bytes, features in logical order)
+      const bool flat = c.t.rank() == 2;
+      const std::vector<int64_t> want = flat ? std::vector<int64_t>{c.t.dim(0), c.t.dim(1), 1, 1} : c.t.shape();
+      const Layout want_layout = flat ? Layout::NCHW : c.t.layout();
+      if (!(r.shape() == want && r.dtype() == c.t.dtype() && r.layout() == want_layout)) {
+        auto str = [](const Tensor& t) {
+          std::string o = "[";
+          for (auto d : t.shape()) o += std::to_string(d) + ",";
+          return o + "] dt " + std::to_string((int)t.dtype()) + " layout " + std::to_string((int)t.layout());
+        };
+        std::printf("p2p pair: sent %s, received %s\n", str(c.t).c_str(), str(r).c_str());
+      }
+      CHECK(r.shape() == want && r.dtype() == c.t.dtype() && r.layout() == want_layout);
+      const auto ht = c.t.to_host_f32(), hr = r.to_host_f32();
+      CHECK(ht.size() == hr.size());
+      for (size_t i = 0; i < std::min(ht.size(), hr.size()); ++i) differ += ht[i] != hr[i];
+      checked += ht.size();
+    }
+  }
+  tx.drain();
+  CHECK(differ == 0);
+  std::printf("p2p pair ok (%zu values over 18 hand-offs, %zu differ)\n", checked, differ);
+}
+
 int main(int argc, char** argv) {
   const bool gpu = argc > 2 && std::string(argv[1]) == "--device" && std::string(argv[2]) == "GPU";
   try {
@@ -238,6 +305,7 @@ int main(int argc, char** argv) {
     test_gradcheck(true);
     if (gpu) test_gpu_vs_cpu();
     if (gpu) test_p2p_loopback();
+    if (gpu) test_p2p_pair();
   } catch (const std::exception& e) {
     std::fprintf(stderr, "exception: %s\n", e.what());
     return 1;

@@ -103,6 +103,8 @@ def test_selftest_gpu_matches_cpu_backend(host_bins, tmp_path):
     assert rc == 0, out
     assert "gpu vs cpu loss" in out
     assert "p2p loopback ok" in out  # the native pipeline's RCCL stage link, world size 1
+    # P2PLink::send / recv on their own flows + the stage's RCCL job-message header, bit-exact
+    assert "p2p pair ok" in out and ", 0 differ)" in out.split("p2p pair ok")[1].splitlines()[0], out
 
 
 @pytest.mark.gpu

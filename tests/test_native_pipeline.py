@@ -207,18 +207,28 @@ def test_native_coordinator_gpu_stages(worker_bin):
 @pytest.mark.gpu
 def test_native_coordinator_ipc_transport_matches_messages(worker_bin):
     """Transport "ipc": stage-to-stage tensors stay on the device (HIP IPC buffers, only handles in
-    the messages). The same bytes arrive as with inline payloads, so every step's loss is the same."""
+    the messages). The same bytes arrive as with inline payloads, so every step's loss is the same —
+    with the host-waited hand-off (default) and with the device-ordered ones (DCNN_IPC_HANDOFF=event:
+    an interprocess event; =flag: a flag the sender's stream writes and the receiver's stream waits
+    on) — no host wait on either side, which also lets the first stage's backward finish before the
+    last stage's loss report."""
     import json
-    losses = {}
-    for transport in ("message", "ipc"):
+    losses, samples = {}, {}
+    modes = ("host", "event", "flag")
+    for transport, wait in [("message", "host")] + [("ipc", w) for w in modes]:
+        env = dict(os.environ, DCNN_IPC_HANDOFF=wait)
         out = subprocess.run([COORD, "--spawn", "3", "--model", "resnet9_cifar10", "--device", "GPU:0", "--input",
                               "3,32,32", "--classes", "10", "--batch", "64", "--microbatches", "4", "--steps", "6",
                               "--schedule", "1f1b", "--transport", transport, "--json"],
-                             capture_output=True, text=True, timeout=240)
+                             capture_output=True, text=True, timeout=240, env=env)
         assert out.returncode == 0, out.stderr[-2000:]
-        losses[transport] = [json.loads(l)["loss"] for l in out.stdout.splitlines() if l.startswith("{")]
-    assert len(losses["ipc"]) == 6 and all(np.isfinite(losses["ipc"]))
-    np.testing.assert_allclose(losses["ipc"], losses["message"], rtol=1e-6)
+        rows = [json.loads(l) for l in out.stdout.splitlines() if l.startswith("{")]
+        losses[transport, wait] = [r["loss"] for r in rows]
+        samples[transport, wait] = [r["samples"] for r in rows]
+    for k in [("ipc", w) for w in modes]:
+        assert len(losses[k]) == 6 and all(np.isfinite(losses[k]))
+        assert samples[k] == [64] * 6, samples  # every micro-batch's report inside its own step
+        np.testing.assert_allclose(losses[k], losses["message", "host"], rtol=1e-6)
 
 
 @pytest.mark.gpu
