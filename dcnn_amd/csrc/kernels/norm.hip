@@ -10,6 +10,8 @@
 //     dgamma/dbeta (intended semantics; reference defect G4 overwrote on GPU).
 // Semantics kept: biased variance for normalisation, unbiased for the running variance,
 // running = (1-m)*running + m*batch (batchnorm_ops.cu:141-153).
+#include <cstdlib>
+
 #include "common.h"
 #include "api.h"
 
@@ -542,16 +544,31 @@ __global__ void __launch_bounds__(256) bn_apply_v_kernel(const T* __restrict__ x
       if (RES) rv[u] = VT::load(residual + (size_t)k * 8);
     }
   }
-  for (int c = threadIdx.x; c < C; c += 256) {
-    float mean, istd;
-    if (use_running) {
-      mean = run_mean[c];
-      istd = rsqrtf(run_var[c] + eps);
-    } else {
-      float var;
-      read_stats<0>(sums, parts, C, c, mean, var);
-      istd = rsqrtf(var + eps);
-      if (blockIdx.x == 0) {
+  // the coefficient table, four channels per lane per round with all their loads issued together
+  // (channel indices clamped so the loads need no guard; C = 2048 is 8 channels per lane)
+  for (int cb = threadIdx.x; cb < C; cb += 1024) {
+    float m4[4], v4[4], g4[4], b4[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int c = min(cb + 256 * j, C - 1);
+      if (use_running) {
+        m4[j] = run_mean[c];
+        v4[j] = run_var[c];
+      } else if (parts <= 1) {
+        m4[j] = sums[c];
+        v4[j] = sums[C + c];
+      } else {
+        read_stats<0>(sums, parts, C, c, m4[j], v4[j]);
+      }
+      g4[j] = gamma ? gamma[c] : 1.f;
+      b4[j] = beta ? beta[c] : 0.f;
+    }
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int c = cb + 256 * j;
+      if (c >= C) break;
+      const float mean = m4[j], var = v4[j], istd = rsqrtf(var + eps);
+      if (!use_running && blockIdx.x == 0) {
         if (save_mean) { save_mean[c] = mean; save_istd[c] = istd; }
         if (run_mean) {
           const float unbiased = count > 1.f ? var * count / (count - 1.f) : var;
@@ -559,10 +576,9 @@ __global__ void __launch_bounds__(256) bn_apply_v_kernel(const T* __restrict__ x
           run_var[c] = (1.f - momentum) * run_var[c] + momentum * unbiased;
         }
       }
+      scale[c] = g4[j] * istd;
+      shift[c] = b4[j] - mean * g4[j] * istd;
     }
-    const float g = gamma ? gamma[c] : 1.f, b = beta ? beta[c] : 0.f;
-    scale[c] = g * istd;
-    shift[c] = b - mean * g * istd;
   }
   __syncthreads();
   while (true) {
@@ -639,18 +655,40 @@ __global__ void __launch_bounds__(256) bn_bwd_apply_v_kernel(const T* __restrict
       if (MASK) yv[u] = VT::load(yout + (size_t)k * 8);
     }
   }
-  for (int c = threadIdx.x; c < C; c += 256) {
-    const float g = gamma ? gamma[c] : 1.f, is = istd[c];
-    float sdy = 0.f, sdyx = 0.f;
-    if (sums) read_stats<1>(sums, parts, C, c, sdy, sdyx);
-    const float a = g * is;
-    ca[c] = a;
-    cbm[c] = eval_mode ? 0.f : -a * is * (sdyx / count);
-    cm[c] = mean[c];
-    cd[c] = eval_mode ? 0.f : -a * (sdy / count);
-    if (blockIdx.x == 0 && sums) {
-      if (dgamma) dgamma[c] += sdyx;
-      if (dbeta) dbeta[c] += sdy;
+  // (four channels per lane per round, loads together: as bn_apply_v_kernel)
+  for (int cb = threadIdx.x; cb < C; cb += 1024) {
+    float g4[4], is4[4], m4[4], s4[4], sx4[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int c = min(cb + 256 * j, C - 1);
+      g4[j] = gamma ? gamma[c] : 1.f;
+      is4[j] = istd[c];
+      m4[j] = mean[c];
+      s4[j] = 0.f;
+      sx4[j] = 0.f;
+      if (sums) {
+        if (parts <= 1) {
+          s4[j] = sums[c];
+          sx4[j] = sums[C + c];
+        } else {
+          read_stats<1>(sums, parts, C, c, s4[j], sx4[j]);
+        }
+      }
+    }
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int c = cb + 256 * j;
+      if (c >= C) break;
+      const float is = is4[j], sdy = s4[j], sdyx = sx4[j];
+      const float a = g4[j] * is;
+      ca[c] = a;
+      cbm[c] = eval_mode ? 0.f : -a * is * (sdyx / count);
+      cm[c] = m4[j];
+      cd[c] = eval_mode ? 0.f : -a * (sdy / count);
+      if (blockIdx.x == 0 && sums) {
+        if (dgamma) dgamma[c] += sdyx;
+        if (dbeta) dbeta[c] += sdy;
+      }
     }
   }
   __syncthreads();
@@ -709,16 +747,30 @@ __global__ void __launch_bounds__(256) bn_bwd_apply_v_kernel(const T* __restrict
 // written or re-read). Same trips / prologue scheme as bn_apply_v_kernel; workgroup 0 saves both
 // layers' (mean, istd) and updates both running statistics.
 __device__ __forceinline__ void bn_side_coeffs(const BnSide& b, int C, float* scale, float* shift, bool first) {
-  for (int c = threadIdx.x; c < C; c += 256) {
-    float mean, istd;
-    if (b.use_running) {
-      mean = b.run_mean[c];
-      istd = rsqrtf(b.run_var[c] + b.eps);
-    } else {
-      float var;
-      read_stats<0>(b.sums, b.parts, C, c, mean, var);
-      istd = rsqrtf(var + b.eps);
-      if (first) {
+  // (four channels per lane per round, loads together: as bn_apply_v_kernel)
+  for (int cb = threadIdx.x; cb < C; cb += 1024) {
+    float m4[4], v4[4], g4[4], b4[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int c = min(cb + 256 * j, C - 1);
+      if (b.use_running) {
+        m4[j] = b.run_mean[c];
+        v4[j] = b.run_var[c];
+      } else if (b.parts <= 1) {
+        m4[j] = b.sums[c];
+        v4[j] = b.sums[C + c];
+      } else {
+        read_stats<0>(b.sums, b.parts, C, c, m4[j], v4[j]);
+      }
+      g4[j] = b.gamma ? b.gamma[c] : 1.f;
+      b4[j] = b.beta ? b.beta[c] : 0.f;
+    }
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int c = cb + 256 * j;
+      if (c >= C) break;
+      const float mean = m4[j], var = v4[j], istd = rsqrtf(var + b.eps);
+      if (!b.use_running && first) {
         if (b.save_mean) { b.save_mean[c] = mean; b.save_istd[c] = istd; }
         if (b.run_mean) {
           const float unbiased = b.count > 1.f ? var * b.count / (b.count - 1.f) : var;
@@ -726,10 +778,9 @@ __device__ __forceinline__ void bn_side_coeffs(const BnSide& b, int C, float* sc
           b.run_var[c] = (1.f - b.momentum) * b.run_var[c] + b.momentum * unbiased;
         }
       }
+      scale[c] = g4[j] * istd;
+      shift[c] = b4[j] - mean * g4[j] * istd;
     }
-    const float g = b.gamma ? b.gamma[c] : 1.f, be = b.beta ? b.beta[c] : 0.f;
-    scale[c] = g * istd;
-    shift[c] = be - mean * g * istd;
   }
 }
 
@@ -799,18 +850,40 @@ bool bn_apply_dual_supported(long R, int C) {
 // / dbeta.
 __device__ __forceinline__ void bn_bwd_side_coeffs(const BnBwdSide& b, int C, float* ca, float* cbm, float* cm,
                                                    float* cd, bool first) {
-  for (int c = threadIdx.x; c < C; c += 256) {
-    const float g = b.gamma ? b.gamma[c] : 1.f, is = b.istd[c];
-    float sdy = 0.f, sdyx = 0.f;
-    if (b.sums) read_stats<1>(b.sums, b.parts, C, c, sdy, sdyx);
-    const float a = g * is;
-    ca[c] = a;
-    cbm[c] = -a * is * (sdyx / b.count);
-    cm[c] = b.mean[c];
-    cd[c] = -a * (sdy / b.count);
-    if (first && b.sums) {
-      if (b.dgamma) b.dgamma[c] += sdyx;
-      if (b.dbeta) b.dbeta[c] += sdy;
+  // (four channels per lane per round, loads together: as bn_apply_v_kernel)
+  for (int cb = threadIdx.x; cb < C; cb += 1024) {
+    float g4[4], is4[4], m4[4], s4[4], sx4[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int c = min(cb + 256 * j, C - 1);
+      g4[j] = b.gamma ? b.gamma[c] : 1.f;
+      is4[j] = b.istd[c];
+      m4[j] = b.mean[c];
+      s4[j] = 0.f;
+      sx4[j] = 0.f;
+      if (b.sums) {
+        if (b.parts <= 1) {
+          s4[j] = b.sums[c];
+          sx4[j] = b.sums[C + c];
+        } else {
+          read_stats<1>(b.sums, b.parts, C, c, s4[j], sx4[j]);
+        }
+      }
+    }
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int c = cb + 256 * j;
+      if (c >= C) break;
+      const float is = is4[j], sdy = s4[j], sdyx = sx4[j];
+      const float a = g4[j] * is;
+      ca[c] = a;
+      cbm[c] = -a * is * (sdyx / b.count);
+      cm[c] = m4[j];
+      cd[c] = -a * (sdy / b.count);
+      if (first && b.sums) {
+        if (b.dgamma) b.dgamma[c] += sdyx;
+        if (b.dbeta) b.dbeta[c] += sdy;
+      }
     }
   }
 }
@@ -896,7 +969,7 @@ bool bn_apply_dual(const BnSide& a, const BnSide& b, void* y, long R, int C, int
 }
 
 // vectors per thread per trip and grid of the bf16 apply passes
-static void bn_v_launch_shape(long nv, int* U, int* grid) {
+static void bn_v_launch_shape(long nv, int C, int* U, int* grid) {
   // default: 1 vector per lane per trip, at most 1024 workgroups, so the large passes make
   // several software-pipelined trips (next trip's loads in flight under this trip's stores).
   // Measured on the ResNet-18 shapes (benchmarks/bn_bench.py, tools/gpu_bnsweep.sh): one pass
@@ -904,8 +977,10 @@ static void bn_v_launch_shape(long nv, int* U, int* grid) {
   // 107.7 us (2 vectors: 107.0 us, but 0.5% slower end to end at batch 64 / 128)
   constexpr long g_cap = 1024;
   *U = 1;
+  (void)C;  // (fewer, wider workgroups for C >= 1024 measured slower: profiles/bn_bandwidth_r6.md)
+  const long cap = g_cap;
   long g = (nv + 256l * *U - 1) / (256l * *U);
-  if (g > g_cap) g = g_cap;
+  if (g > cap) g = cap;
   if (g < 1) g = 1;
   *grid = (int)g;
 }
@@ -1106,7 +1181,7 @@ static void bn_apply_t(const T* x, T* y, long R, int C, const float* sums, int p
   if (bn_v_ok(R, C)) {
     int U, g;
     const unsigned nv = (unsigned)(R * C / 8);
-    bn_v_launch_shape(nv, &U, &g);
+    bn_v_launch_shape(nv, C, &U, &g);
 #define DCNN_BNV(U_, RES_)                                                                                       \
   if (U == U_ && (residual != nullptr) == RES_)                                                                  \
     hipLaunchKernelGGL((bn_apply_v_kernel<T, U_, RES_>), dim3(g), dim3(256), shm, s, x, y, nv, C, sums, parts, count, \
@@ -1146,7 +1221,7 @@ static void bn_bwd_apply_t(const T* dy, const T* yout, const T* x, T* dx, long R
   if (bn_v_ok(R, C)) {
     int U, g;
     const unsigned nv = (unsigned)(R * C / 8);
-    bn_v_launch_shape(nv, &U, &g);
+    bn_v_launch_shape(nv, C, &U, &g);
     const size_t shm4 = 4 * C * sizeof(float);
 #define DCNN_BNBV(U_, MASK_)                                                                                      \
   if (U == U_ && (yout != nullptr) == MASK_)                                                                      \
