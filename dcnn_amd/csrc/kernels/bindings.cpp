@@ -226,6 +226,8 @@ PYBIND11_MODULE(_kernels, m) {
           gemm_g2f(a, S(stream));
         });
   m.def("gemm_g2f_stat_rows", &gemm_g2f_stat_rows);
+  m.def("gemm_g2_set_splitk", &gemm_g2_set_splitk);  // (DCNN_G2_SPLITK at run time: tests / A/B)
+  m.def("gemm_g2_splitk_enabled", &gemm_g2_splitk_enabled);
   m.def("set_f32_mode", &set_f32_mode);
   m.def("get_f32_mode", &get_f32_mode);
   m.def("gemm_t2f",

@@ -23,6 +23,7 @@
 #include <cstdlib>
 #include <map>
 #include <mutex>
+#include <vector>
 
 #include "common.h"
 #include "api.h"
@@ -728,10 +729,14 @@ __global__ void __launch_bounds__(256, 2) gemm_t2_kernel(T2Args p) {
 static int g2_stages() { return 0; }
 
 // split-K partial workspace per (device, stream): grow-only, allocated in the eager warm-up
-// before a graph captures the step (a capture that would need a larger one throws)
+// before a graph captures the step. An outgrown buffer is kept (a graph captured earlier still
+// reads it). A capture whose stream has no large-enough workspace yet (warm-up ran on another
+// stream, e.g. torch.cuda.graph's side stream) borrows the largest one of the device: its owner is
+// the warm-up stream, which the graph's replays are ordered with; with none large enough it throws.
 static float* g2_kpart(size_t bytes, hipStream_t s) {
   static std::mutex mu;
   static std::map<std::pair<int, hipStream_t>, std::pair<float*, size_t>> ws;
+  static std::vector<float*> retired;  // (never freed: captured graphs may hold them)
   int dev = 0;
   DCNN_HIP_CHECK(hipGetDevice(&dev));
   std::lock_guard<std::mutex> g(mu);
@@ -739,9 +744,15 @@ static float* g2_kpart(size_t bytes, hipStream_t s) {
   if (e.second < bytes) {
     hipStreamCaptureStatus st = hipStreamCaptureStatusNone;
     DCNN_HIP_CHECK(hipStreamIsCapturing(s, &st));
-    if (st != hipStreamCaptureStatusNone)
+    if (st != hipStreamCaptureStatusNone) {
+      const std::pair<float*, size_t>* best = nullptr;
+      for (const auto& kv : ws)
+        if (kv.first.first == dev && kv.second.second >= bytes && (!best || kv.second.second > best->second))
+          best = &kv.second;
+      if (best) return best->first;
       throw std::runtime_error("gemm_g2: split-K workspace must grow outside graph capture (run a step eagerly first)");
-    if (e.first) DCNN_HIP_CHECK(hipFree(e.first));
+    }
+    if (e.first) retired.push_back(e.first);
     const size_t n = bytes > (size_t)(32 << 20) ? bytes : (size_t)(32 << 20);
     DCNN_HIP_CHECK(hipMalloc(&e.first, n));
     e.second = n;

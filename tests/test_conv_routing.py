@@ -68,7 +68,16 @@ def test_shared_route_table():
     assert fwd(256, 256, 8, 8, 256, 3, 1, 1) == K.ROUTE_HALO          # 8x8 maps (gutter layout)
     assert fwd(256, 128, 16, 16, 256, 3, 2, 1) == K.ROUTE_GEMM_G2     # strided 3x3
     assert fwd(256, 64, 32, 32, 128, 1, 2, 0) == K.ROUTE_G1S          # strided 1x1 projection
-    assert fwd(32, 1024, 8, 8, 256, 1, 1, 0) == K.ROUTE_HALO          # K >= 1024 1x1, small grid
+    # K >= 1024 1x1, small grid: gemm_g2 split-K (default), the halo kernel's split-K without it
+    prev = K.gemm_g2_splitk_enabled()
+    try:
+        K.gemm_g2_set_splitk(1)
+        assert fwd(32, 1024, 8, 8, 256, 1, 1, 0) == K.ROUTE_GEMM_G2
+        assert K.conv_dgrad_route(32, 256, 8, 8, 1024, 1, 1, 1, 1, 0, 0, 8, 8, 0) == K.ROUTE_GEMM_G2
+        K.gemm_g2_set_splitk(0)
+        assert fwd(32, 1024, 8, 8, 256, 1, 1, 0) == K.ROUTE_HALO
+    finally:
+        K.gemm_g2_set_splitk(prev)
     assert fwd(256, 1024, 8, 8, 256, 1, 1, 0) == K.ROUTE_GEMM_G2      # ... large grid
     assert fwd(8, 3, 32, 32, 16, 3, 1, 1) == K.ROUTE_GENERIC          # odd channel count
     assert fwd(256, 64, 32, 32, 256, 1, 1, 0, -1) != K.ROUTE_G1S      # epilogue not on g1s
