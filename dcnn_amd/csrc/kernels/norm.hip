@@ -11,6 +11,7 @@
 // Semantics kept: biased variance for normalisation, unbiased for the running variance,
 // running = (1-m)*running + m*batch (batchnorm_ops.cu:141-153).
 #include <cstdlib>
+#include <type_traits>
 
 #include "common.h"
 #include "api.h"
@@ -546,40 +547,48 @@ __global__ void __launch_bounds__(256) bn_apply_v_kernel(const T* __restrict__ x
   }
   // the coefficient table, four channels per lane per round with all their loads issued together
   // (channel indices clamped so the loads need no guard; C = 2048 is 8 channels per lane)
-  for (int cb = threadIdx.x; cb < C; cb += 1024) {
-    float m4[4], v4[4], g4[4], b4[4];
+  auto table = [&](auto j_c) {
+    constexpr int J = decltype(j_c)::value;
+    for (int cb = threadIdx.x; cb < C; cb += 256 * J) {
+      float m4[J], v4[J], g4[J], b4[J];
 #pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      const int c = min(cb + 256 * j, C - 1);
-      if (use_running) {
-        m4[j] = run_mean[c];
-        v4[j] = run_var[c];
-      } else if (parts <= 1) {
-        m4[j] = sums[c];
-        v4[j] = sums[C + c];
-      } else {
-        read_stats<0>(sums, parts, C, c, m4[j], v4[j]);
-      }
-      g4[j] = gamma ? gamma[c] : 1.f;
-      b4[j] = beta ? beta[c] : 0.f;
-    }
-#pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      const int c = cb + 256 * j;
-      if (c >= C) break;
-      const float mean = m4[j], var = v4[j], istd = rsqrtf(var + eps);
-      if (!use_running && blockIdx.x == 0) {
-        if (save_mean) { save_mean[c] = mean; save_istd[c] = istd; }
-        if (run_mean) {
-          const float unbiased = count > 1.f ? var * count / (count - 1.f) : var;
-          run_mean[c] = (1.f - momentum) * run_mean[c] + momentum * mean;
-          run_var[c] = (1.f - momentum) * run_var[c] + momentum * unbiased;
+      for (int j = 0; j < J; ++j) {
+        const int c = min(cb + 256 * j, C - 1);
+        if (use_running) {
+          m4[j] = run_mean[c];
+          v4[j] = run_var[c];
+        } else if (parts <= 1) {
+          m4[j] = sums[c];
+          v4[j] = sums[C + c];
+        } else {
+          read_stats<0>(sums, parts, C, c, m4[j], v4[j]);
         }
+        g4[j] = gamma ? gamma[c] : 1.f;
+        b4[j] = beta ? beta[c] : 0.f;
       }
-      scale[c] = g4[j] * istd;
-      shift[c] = b4[j] - mean * g4[j] * istd;
+#pragma unroll
+      for (int j = 0; j < J; ++j) {
+        const int c = cb + 256 * j;
+        if (c >= C) break;
+        const float mean = m4[j], var = v4[j], istd = rsqrtf(var + eps);
+        if (!use_running && blockIdx.x == 0) {
+          if (save_mean) { save_mean[c] = mean; save_istd[c] = istd; }
+          if (run_mean) {
+            const float unbiased = count > 1.f ? var * count / (count - 1.f) : var;
+            run_mean[c] = (1.f - momentum) * run_mean[c] + momentum * mean;
+            run_var[c] = (1.f - momentum) * run_var[c] + momentum * unbiased;
+          }
+        }
+        scale[c] = g4[j] * istd;
+        shift[c] = b4[j] - mean * g4[j] * istd;
+      }
     }
-  }
+  };
+  // (one channel per lane per round up to C = 256: the clamped extra loads cost the short passes)
+  if (C > 256)
+    table(std::integral_constant<int, 4>{});
+  else
+    table(std::integral_constant<int, 1>{});
   __syncthreads();
   while (true) {
     // the next trip's loads go out before this trip's stores (loads and stores overlap)
@@ -656,41 +665,49 @@ __global__ void __launch_bounds__(256) bn_bwd_apply_v_kernel(const T* __restrict
     }
   }
   // (four channels per lane per round, loads together: as bn_apply_v_kernel)
-  for (int cb = threadIdx.x; cb < C; cb += 1024) {
-    float g4[4], is4[4], m4[4], s4[4], sx4[4];
+  auto table = [&](auto j_c) {
+    constexpr int J = decltype(j_c)::value;
+    for (int cb = threadIdx.x; cb < C; cb += 256 * J) {
+      float g4[J], is4[J], m4[J], s4[J], sx4[J];
 #pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      const int c = min(cb + 256 * j, C - 1);
-      g4[j] = gamma ? gamma[c] : 1.f;
-      is4[j] = istd[c];
-      m4[j] = mean[c];
-      s4[j] = 0.f;
-      sx4[j] = 0.f;
-      if (sums) {
-        if (parts <= 1) {
-          s4[j] = sums[c];
-          sx4[j] = sums[C + c];
-        } else {
-          read_stats<1>(sums, parts, C, c, s4[j], sx4[j]);
+      for (int j = 0; j < J; ++j) {
+        const int c = min(cb + 256 * j, C - 1);
+        g4[j] = gamma ? gamma[c] : 1.f;
+        is4[j] = istd[c];
+        m4[j] = mean[c];
+        s4[j] = 0.f;
+        sx4[j] = 0.f;
+        if (sums) {
+          if (parts <= 1) {
+            s4[j] = sums[c];
+            sx4[j] = sums[C + c];
+          } else {
+            read_stats<1>(sums, parts, C, c, s4[j], sx4[j]);
+          }
+        }
+      }
+#pragma unroll
+      for (int j = 0; j < J; ++j) {
+        const int c = cb + 256 * j;
+        if (c >= C) break;
+        const float is = is4[j], sdy = s4[j], sdyx = sx4[j];
+        const float a = g4[j] * is;
+        ca[c] = a;
+        cbm[c] = eval_mode ? 0.f : -a * is * (sdyx / count);
+        cm[c] = m4[j];
+        cd[c] = eval_mode ? 0.f : -a * (sdy / count);
+        if (blockIdx.x == 0 && sums) {
+          if (dgamma) dgamma[c] += sdyx;
+          if (dbeta) dbeta[c] += sdy;
         }
       }
     }
-#pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      const int c = cb + 256 * j;
-      if (c >= C) break;
-      const float is = is4[j], sdy = s4[j], sdyx = sx4[j];
-      const float a = g4[j] * is;
-      ca[c] = a;
-      cbm[c] = eval_mode ? 0.f : -a * is * (sdyx / count);
-      cm[c] = m4[j];
-      cd[c] = eval_mode ? 0.f : -a * (sdy / count);
-      if (blockIdx.x == 0 && sums) {
-        if (dgamma) dgamma[c] += sdyx;
-        if (dbeta) dbeta[c] += sdy;
-      }
-    }
-  }
+  };
+  // (one channel per lane per round up to C = 256: the clamped extra loads cost the short passes)
+  if (C > 256)
+    table(std::integral_constant<int, 4>{});
+  else
+    table(std::integral_constant<int, 1>{});
   __syncthreads();
   auto ld8 = [](const float* p, float* o) {
     const float4 a = *reinterpret_cast<const float4*>(p), b = *reinterpret_cast<const float4*>(p + 4);
@@ -748,40 +765,48 @@ __global__ void __launch_bounds__(256) bn_bwd_apply_v_kernel(const T* __restrict
 // layers' (mean, istd) and updates both running statistics.
 __device__ __forceinline__ void bn_side_coeffs(const BnSide& b, int C, float* scale, float* shift, bool first) {
   // (four channels per lane per round, loads together: as bn_apply_v_kernel)
-  for (int cb = threadIdx.x; cb < C; cb += 1024) {
-    float m4[4], v4[4], g4[4], b4[4];
+  auto table = [&](auto j_c) {
+    constexpr int J = decltype(j_c)::value;
+    for (int cb = threadIdx.x; cb < C; cb += 256 * J) {
+      float m4[J], v4[J], g4[J], b4[J];
 #pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      const int c = min(cb + 256 * j, C - 1);
-      if (b.use_running) {
-        m4[j] = b.run_mean[c];
-        v4[j] = b.run_var[c];
-      } else if (b.parts <= 1) {
-        m4[j] = b.sums[c];
-        v4[j] = b.sums[C + c];
-      } else {
-        read_stats<0>(b.sums, b.parts, C, c, m4[j], v4[j]);
-      }
-      g4[j] = b.gamma ? b.gamma[c] : 1.f;
-      b4[j] = b.beta ? b.beta[c] : 0.f;
-    }
-#pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      const int c = cb + 256 * j;
-      if (c >= C) break;
-      const float mean = m4[j], var = v4[j], istd = rsqrtf(var + b.eps);
-      if (!b.use_running && first) {
-        if (b.save_mean) { b.save_mean[c] = mean; b.save_istd[c] = istd; }
-        if (b.run_mean) {
-          const float unbiased = b.count > 1.f ? var * b.count / (b.count - 1.f) : var;
-          b.run_mean[c] = (1.f - b.momentum) * b.run_mean[c] + b.momentum * mean;
-          b.run_var[c] = (1.f - b.momentum) * b.run_var[c] + b.momentum * unbiased;
+      for (int j = 0; j < J; ++j) {
+        const int c = min(cb + 256 * j, C - 1);
+        if (b.use_running) {
+          m4[j] = b.run_mean[c];
+          v4[j] = b.run_var[c];
+        } else if (b.parts <= 1) {
+          m4[j] = b.sums[c];
+          v4[j] = b.sums[C + c];
+        } else {
+          read_stats<0>(b.sums, b.parts, C, c, m4[j], v4[j]);
         }
+        g4[j] = b.gamma ? b.gamma[c] : 1.f;
+        b4[j] = b.beta ? b.beta[c] : 0.f;
       }
-      scale[c] = g4[j] * istd;
-      shift[c] = b4[j] - mean * g4[j] * istd;
+#pragma unroll
+      for (int j = 0; j < J; ++j) {
+        const int c = cb + 256 * j;
+        if (c >= C) break;
+        const float mean = m4[j], var = v4[j], istd = rsqrtf(var + b.eps);
+        if (!b.use_running && first) {
+          if (b.save_mean) { b.save_mean[c] = mean; b.save_istd[c] = istd; }
+          if (b.run_mean) {
+            const float unbiased = b.count > 1.f ? var * b.count / (b.count - 1.f) : var;
+            b.run_mean[c] = (1.f - b.momentum) * b.run_mean[c] + b.momentum * mean;
+            b.run_var[c] = (1.f - b.momentum) * b.run_var[c] + b.momentum * unbiased;
+          }
+        }
+        scale[c] = g4[j] * istd;
+        shift[c] = b4[j] - mean * g4[j] * istd;
+      }
     }
-  }
+  };
+  // (one channel per lane per round up to C = 256: the clamped extra loads cost the short passes)
+  if (C > 256)
+    table(std::integral_constant<int, 4>{});
+  else
+    table(std::integral_constant<int, 1>{});
 }
 
 __global__ void __launch_bounds__(256) bn_apply_dual_kernel(BnSide a, BnSide b, bf16* __restrict__ y, unsigned nv,
@@ -851,41 +876,49 @@ bool bn_apply_dual_supported(long R, int C) {
 __device__ __forceinline__ void bn_bwd_side_coeffs(const BnBwdSide& b, int C, float* ca, float* cbm, float* cm,
                                                    float* cd, bool first) {
   // (four channels per lane per round, loads together: as bn_apply_v_kernel)
-  for (int cb = threadIdx.x; cb < C; cb += 1024) {
-    float g4[4], is4[4], m4[4], s4[4], sx4[4];
+  auto table = [&](auto j_c) {
+    constexpr int J = decltype(j_c)::value;
+    for (int cb = threadIdx.x; cb < C; cb += 256 * J) {
+      float g4[J], is4[J], m4[J], s4[J], sx4[J];
 #pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      const int c = min(cb + 256 * j, C - 1);
-      g4[j] = b.gamma ? b.gamma[c] : 1.f;
-      is4[j] = b.istd[c];
-      m4[j] = b.mean[c];
-      s4[j] = 0.f;
-      sx4[j] = 0.f;
-      if (b.sums) {
-        if (b.parts <= 1) {
-          s4[j] = b.sums[c];
-          sx4[j] = b.sums[C + c];
-        } else {
-          read_stats<1>(b.sums, b.parts, C, c, s4[j], sx4[j]);
+      for (int j = 0; j < J; ++j) {
+        const int c = min(cb + 256 * j, C - 1);
+        g4[j] = b.gamma ? b.gamma[c] : 1.f;
+        is4[j] = b.istd[c];
+        m4[j] = b.mean[c];
+        s4[j] = 0.f;
+        sx4[j] = 0.f;
+        if (b.sums) {
+          if (b.parts <= 1) {
+            s4[j] = b.sums[c];
+            sx4[j] = b.sums[C + c];
+          } else {
+            read_stats<1>(b.sums, b.parts, C, c, s4[j], sx4[j]);
+          }
+        }
+      }
+#pragma unroll
+      for (int j = 0; j < J; ++j) {
+        const int c = cb + 256 * j;
+        if (c >= C) break;
+        const float is = is4[j], sdy = s4[j], sdyx = sx4[j];
+        const float a = g4[j] * is;
+        ca[c] = a;
+        cbm[c] = -a * is * (sdyx / b.count);
+        cm[c] = m4[j];
+        cd[c] = -a * (sdy / b.count);
+        if (first && b.sums) {
+          if (b.dgamma) b.dgamma[c] += sdyx;
+          if (b.dbeta) b.dbeta[c] += sdy;
         }
       }
     }
-#pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      const int c = cb + 256 * j;
-      if (c >= C) break;
-      const float is = is4[j], sdy = s4[j], sdyx = sx4[j];
-      const float a = g4[j] * is;
-      ca[c] = a;
-      cbm[c] = -a * is * (sdyx / b.count);
-      cm[c] = m4[j];
-      cd[c] = -a * (sdy / b.count);
-      if (first && b.sums) {
-        if (b.dgamma) b.dgamma[c] += sdyx;
-        if (b.dbeta) b.dbeta[c] += sdy;
-      }
-    }
-  }
+  };
+  // (one channel per lane per round up to C = 256: the clamped extra loads cost the short passes)
+  if (C > 256)
+    table(std::integral_constant<int, 4>{});
+  else
+    table(std::integral_constant<int, 1>{});
 }
 
 __global__ void __launch_bounds__(256) bn_bwd_apply_dual_kernel(const bf16* __restrict__ dy, BnBwdSide a,
