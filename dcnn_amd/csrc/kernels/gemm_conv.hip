@@ -571,8 +571,18 @@ __global__ void splitk_reduce_kernel(SplitkSeg a, SplitkSeg b, int gxa, int spli
 // blocks are not the launch's tail. Fixed summation order throughout: bit-reproducible, no atomics.
 template <int G>
 __global__ void __launch_bounds__(256) multi_splitk_reduce_kernel(MultiRed t) {
+  // this workgroup's entry: the last one whose unit0 <= blockIdx.x (binary search: ~6 dependent
+  // kernel-argument loads instead of up to 48 on a linear scan, before the first slab load)
   int k = 0;
-  while (k + 1 < t.count && (int)blockIdx.x >= t.e[k + 1].unit0) ++k;
+  for (int lo = 0, hi = t.count - 1; lo <= hi;) {
+    const int mid = (lo + hi) >> 1;
+    if (t.e[mid].unit0 <= (int)blockIdx.x) {
+      k = mid;
+      lo = mid + 1;
+    } else {
+      hi = mid - 1;
+    }
+  }
   const float* slab = t.e[k].slab;
   float* out = t.e[k].out;
   const long n = t.e[k].n;
