@@ -60,11 +60,16 @@ def main():
             per_item[name] = (t[:, :, b_] - t[:, :, a_])[m]
         first = t[:, :, 5] > 0
         G = int(first[:, 0].sum())  # workgroups (each stamps 5 once, at its first item)
-        # prologue split: [5] -> [6] address setup, [6] -> [7] first DMA issue + landing (vmcnt),
-        # [7] -> [0] first barrier (the workgroup's other waves)
-        pro = {nm_: (t[:, :, b_] - t[:, :, a_])[first & ok(a_, b_)] for nm_, a_, b_ in
+        # prologue split. 16 x 16+ maps (l1-l3): [5] -> [8] arguments, [8] -> [10] weight table,
+        # [10] -> [9] weight addresses + W(0, 0) DMA issue + halo table, [9] -> [6] halo addresses,
+        # [6] -> [11] halo / W(0, 1) issue + fragment addresses, [11] -> [7] first DMA landing
+        # (vmcnt), [7] -> [0] first barrier. The 4 x 4-map gutter layout (l4) keeps the older order
+        # [5] args [8] halo table [9] weight table [10] fragment addresses [11] addresses [6] DMA [7].
+        seq = ((("args", 5, 8), ("w_tab", 8, 10), ("w_dma+halo_tab", 10, 9), ("addrs_h", 9, 6),
+                ("issue+frag", 6, 11), ("dma", 11, 7), ("barrier", 7, 0)) if H > 4 else
                (("args", 5, 8), ("halo_tab", 8, 9), ("w_tab", 9, 10), ("frag", 10, 11), ("addrs", 11, 6),
-                ("dma", 6, 7), ("barrier", 7, 0))}
+                ("dma", 6, 7), ("barrier", 7, 0)))
+        pro = {nm_: (t[:, :, b_] - t[:, :, a_])[first & ok(a_, b_)] for nm_, a_, b_ in seq}
         lives, kl, prol = [], [], []
         for u0 in torch.nonzero(first[:, 0]).flatten().tolist():
             us = list(range(u0, items, G))

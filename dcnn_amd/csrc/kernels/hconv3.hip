@@ -214,30 +214,9 @@ __global__ void __launch_bounds__(NW * 64, 8 / NW) hconv3_kernel(HConvArgs p, H3
   const int nch = g.nchunk;                              // chunks per item (even, or 1: a 32-channel input)
   stamp(u, 8);
 
-  // ---- halo loader, item-invariant part: instruction k of this wave fills halo pixels
-  // [16(wid*HN + k), +16); lane -> (image, row + 1, column + 1 within the image window, chunk
-  // slot), packed; gutters and row padding are never loaded (zero-filled by the buffer range)
+  // ---- halo loader, item-invariant part (filled in the first item's prologue, after the first
+  // weight DMA is issued: its latency hides the table's integer work)
   unsigned hpk[HN];
-#pragma unroll
-  for (int k = 0; k < HN; ++k) {
-    const int P = (wid * HN + k) * 16 + (lane >> 2);
-    unsigned v = 0xffffffffu;
-    if (P < HPX) {
-      const int hy = (int)fdiv((unsigned)P, g.fd_pitch), hx = P - hy * pitch;
-      int cy = hy, cx = hx, im = 0;
-      bool ok = hx < HW2;
-      if (gut) {
-        const int iy = (int)fdiv((unsigned)hy, g.fd_ih1), ix = (int)fdiv((unsigned)hx, g.fd_iw1);
-        cy = hy - iy * (g.IH + 1);
-        cx = hx - ix * (g.IW + 1);
-        im = iy * g.GX + ix;
-        ok = ok && cy != 0 && cx != 0;
-      }
-      if (ok) v = (unsigned)cx | ((unsigned)cy << 8) | ((unsigned)im << 16) | ((unsigned)((lane & 3) ^ h3_swz<TWC>(P)) << 24);
-    }
-    hpk[k] = v;
-  }
-  stamp(u, 9);
   // ---- weight loader, item-invariant part: stage row R = dx * BN + n (3 taps x BN rows, 64 B)
   unsigned wrc[NWI];  // (stage row's output channel + 1) | chunk slot byte offset << 16
   int wtb[NWI][3];  // byte offset of the instruction's tap column for kernel rows dy = 0..2 (SGPRs)
@@ -342,8 +321,7 @@ __global__ void __launch_bounds__(NW * 64, 8 / NW) hconv3_kernel(HConvArgs p, H3
       }
     }
   };
-  set_baddr(0);
-  stamp(u, 11);
+
   auto baddr_of = [&](int j, int dy, int dx) H3L {
     if constexpr (PITCH > 0) return baddr[j][dx] + dy * PITCH * 64;
     else return baddr[j][dy * 3 + dx];
@@ -415,12 +393,58 @@ __global__ void __launch_bounds__(NW * 64, 8 / NW) hconv3_kernel(HConvArgs p, H3
   auto nothing = []() H3L {};
 
   // ---- first item's prologue: halo chunk 0, W(0, 0) landed; W(0, 1) in flight
+  auto fill_hpk = [&]() H3L {
+    // ---- halo loader, item-invariant part: instruction k of this wave fills halo pixels
+    // [16(wid*HN + k), +16); lane -> (image, row + 1, column + 1 within the image window, chunk
+    // slot), packed; gutters and row padding are never loaded (zero-filled by the buffer range)
+#pragma unroll
+    for (int k = 0; k < HN; ++k) {
+      const int P = (wid * HN + k) * 16 + (lane >> 2);
+      unsigned v = 0xffffffffu;
+      if (P < HPX) {
+        const int hy = (int)fdiv((unsigned)P, g.fd_pitch), hx = P - hy * pitch;
+        int cy = hy, cx = hx, im = 0;
+        bool ok = hx < HW2;
+        if (gut) {
+          const int iy = (int)fdiv((unsigned)hy, g.fd_ih1), ix = (int)fdiv((unsigned)hx, g.fd_iw1);
+          cy = hy - iy * (g.IH + 1);
+          cx = hx - ix * (g.IW + 1);
+          im = iy * g.GX + ix;
+          ok = ok && cy != 0 && cx != 0;
+        }
+        if (ok) v = (unsigned)cx | ((unsigned)cy << 8) | ((unsigned)im << 16) | ((unsigned)((lane & 3) ^ h3_swz<TWC>(P)) << 24);
+      }
+      hpk[k] = v;
+    }
+  };
   unsigned hs[HN], ws[NWI];
-  addrs(decode(u), hs, ws);
-  stamp(u, 6);
-  load_halo(I0{}, 0, hs);
-  load_w(I0{}, 0, 0, ws);
-  load_w(I1{}, 0, 1, ws);
+  const Item t0 = decode(u);
+  if constexpr (HN != 7) {
+    // (issue order W(0, 0), halo chunk 0, W(0, 1): the weight DMA goes out before the halo table
+    // is built and the fragment addresses are derived while both are in flight; vmcnt(NWI) below
+    // still means "W(0, 0) and the halo landed, W(0, 1) in flight")
+    addrs_w(t0, ws);
+    load_w(I0{}, 0, 0, ws);
+    fill_hpk();
+    stamp(u, 9);
+    addrs_h(t0, hs);
+    stamp(u, 6);
+    load_halo(I0{}, 0, hs);
+    load_w(I1{}, 0, 1, ws);
+    set_baddr(0);
+    stamp(u, 11);
+  } else {
+    // (the 4 x 4-map gutter instances keep the plain order: the one above spills VGPRs there)
+    fill_hpk();
+    stamp(u, 9);
+    set_baddr(0);
+    stamp(u, 11);
+    addrs(t0, hs, ws);
+    stamp(u, 6);
+    load_halo(I0{}, 0, hs);
+    load_w(I0{}, 0, 0, ws);
+    load_w(I1{}, 0, 1, ws);
+  }
   vmwait<NWI>();
   stamp(u, 7);
   h3_barrier();
