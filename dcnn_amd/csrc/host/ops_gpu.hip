@@ -341,8 +341,7 @@ inline hipStream_t cur() { return static_cast<hipStream_t>(gpu::flow()); }
 
 // grow-only workspace per purpose
 enum Slot { W_T = 0, SLAB, BSLAB, STAT_SLAB, STAT_SUMS, STAT_PART, LOSS_WS, LOSS_OUT, TICKETS, HPART, HTICKETS, GN_AFF,
-            FWD_STATS, BWD_STATS, FWD_STATS2, STAT_SLAB2, STAT_SUMS2, STAT_PART2, FWD_FOLD, BWD_FOLD, FWD_FOLD2,
-            FOLD_TICKETS, NSLOTS };
+            FWD_STATS, BWD_STATS, FWD_STATS2, STAT_SLAB2, STAT_SUMS2, STAT_PART2, NSLOTS };
 void* scratch(Slot s, size_t bytes) {
   static void* p[NSLOTS] = {};
   static size_t n[NSLOTS] = {};
@@ -477,33 +476,6 @@ G2Args g2_fwd_args(const void* x, const void* w, void* y, const float* bias, con
 thread_local bool t_secondary = false;
 inline Slot fwd_stats_slot() { return t_secondary ? FWD_STATS2 : FWD_STATS; }
 
-// Statistics folded by the producing kernel (stat_fold.h, opt-in DCNN_STAT_FOLD=1): the producer
-// returns its reduced statistics (the finished [2][C] or [groups][3][C] partials) in place of its
-// raw rows, with rows = kFolded + groups; the BatchNorm entry points then skip their
-// bn_stat_reduce launch. Off by default: on gemm_g2 the per-workgroup store drain + ticket round
-// trip costs more than the launch it saves (profiles/experiment_stat_fold_r6.md).
-constexpr int kFolded = 1 << 24;
-bool fold_enabled() {
-  static const bool on = [] {
-    const char* v = std::getenv("DCNN_STAT_FOLD");
-    return v && std::string(v) == "1";
-  }();
-  return on;
-}
-StatFold make_fold(Slot out, int rows, int C) {
-  constexpr size_t kTicketWords = 4096;  // zeroed once, left zeroed by every folding launch
-  static bool zeroed = false;
-  unsigned* tk = static_cast<unsigned*>(scratch(FOLD_TICKETS, kTicketWords * 4));
-  if (!zeroed) {
-    HOST_HIP_CHECK(hipMemsetAsync(tk, 0, kTicketWords * 4, cur()));
-    zeroed = true;
-  }
-  const int groups = stat_fold_groups(rows);
-  if ((size_t)groups > kTicketWords) throw std::runtime_error("statistics fold: too many row groups");
-  float* buf = static_cast<float*>(scratch(out, (size_t)(groups == 1 ? 2 : 3 * groups) * C * 4));
-  return StatFold{buf, buf, tk, 0};
-}
-
 ConvRouteGeom route_geom(const ConvShape& s, int g1s_mode) {
   return ConvRouteGeom{s.N, s.C, s.H, s.W, s.Co, s.KH, s.KW, s.SH, s.SW, s.PH, s.PW, s.OH, s.OW, g1s_mode};
 }
@@ -597,8 +569,6 @@ const float* conv_fwd(const void* x, const void* w, const float* bias, void* y, 
     }
     a.bias = bias;
     if (want) a.stats = slab_of(hconv_stat_rows(s.N, s.H, s.W, s.C, s.Co, a.ntaps, 0));
-    // (the halo conv keeps its rows for bn_stat_reduce: a fold would break hconv3's register
-    // budget, profiles/experiment_stat_fold_r6.md)
     hconv_workspace(a);
     hconv(a, cur());
     return a.stats;
@@ -612,13 +582,6 @@ const float* conv_fwd(const void* x, const void* w, const float* bias, void* y, 
   if (route != ROUTE_GENERIC && xb < (1l << 31) && wb < (1l << 31)) {
     G2Args a = g2_fwd_args(x, w, y, bias, s);
     if (want) a.stats = slab_of(gemm_g2_stat_rows(M, s.Co));
-    if (want && fold_enabled()) {
-      const int rows = *stat_rows;
-      a.fold = make_fold(t_secondary ? FWD_FOLD2 : FWD_FOLD, rows, s.Co);
-      gemm_g2(a, cur());
-      *stat_rows = kFolded + stat_fold_groups(rows);
-      return a.fold.out;
-    }
     gemm_g2(a, cur());
     return a.stats;
   }
@@ -741,13 +704,6 @@ const float* conv_dgrad(const void* dy, const void* w, void* dx, const ConvShape
       if (bnb && all_taps) {
         a.bnb = ba;
         a.stats = slab_of(gemm_g2_stat_rows(a.M, s.C));
-        if (fold_enabled()) {
-          const int rows = *bnb_rows;
-          a.fold = make_fold(BWD_FOLD, rows, s.C);
-          gemm_g2(a, cur());
-          *bnb_rows = kFolded + stat_fold_groups(rows);
-          return a.fold.out;
-        }
       }
       gemm_g2(a, cur());
       return a.stats;
@@ -884,7 +840,6 @@ void dense_wgrad(const void* dy, const void* x, float* gw, float* gb, int N, int
 
 // deterministic slab statistics: (pointer, parts) for bn_apply / bn_bwd_apply
 static std::pair<const float*, int> reduce_stats(int mode, const float* slab, int rows, int C) {
-  if (rows >= kFolded) return {slab, rows - kFolded};  // (reduced by its producer)
   const int parts = bn_stat_parts(rows);
   float* sums = static_cast<float*>(scratch(STAT_SUMS, (size_t)2 * C * 4));
   float* part = parts > 1 ? static_cast<float*>(scratch(STAT_PART, (size_t)parts * 3 * C * 4)) : nullptr;
@@ -946,20 +901,6 @@ bool bn_dual_ok(long R, int C) { return bn_apply_dual_supported(R, C); }
 // both statistics reduces of a pair in one launch: (pointer, parts) per side
 static void reduce_pair(int mode, const float* slab_a, int rows_a, const float* slab_b, int rows_b, int C,
                         std::pair<const float*, int>& a, std::pair<const float*, int>& b) {
-  if (rows_a >= kFolded || rows_b >= kFolded) {  // a producer reduced its side: one launch at most
-    if (rows_a >= kFolded) a = {slab_a, rows_a - kFolded};
-    else a = reduce_stats(mode, slab_a, rows_a, C);
-    if (rows_b >= kFolded) {
-      b = {slab_b, rows_b - kFolded};
-    } else {  // (the second side's own workspaces: side a's may hold its result)
-      const int pb = bn_stat_parts(rows_b);
-      float* sb = static_cast<float*>(scratch(STAT_SUMS2, (size_t)2 * C * 4));
-      float* qb = pb > 1 ? static_cast<float*>(scratch(STAT_PART2, (size_t)pb * 3 * C * 4)) : nullptr;
-      bn_stat_reduce(mode, slab_b, rows_b, C, sb, qb, nullptr, cur());
-      b = {pb > 1 ? qb : sb, pb};
-    }
-    return;
-  }
   const int pa = bn_stat_parts(rows_a), pb = bn_stat_parts(rows_b);
   float* sa = static_cast<float*>(scratch(STAT_SUMS, (size_t)2 * C * 4));
   float* sb = static_cast<float*>(scratch(STAT_SUMS2, (size_t)2 * C * 4));

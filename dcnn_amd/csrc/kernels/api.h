@@ -25,17 +25,6 @@ struct TnArgs {
   const bf16* dY; const bf16* X; float* slab; float* bias_slab;
   int M, N, P; int mode; int nb, sh, sw, cs, gh, gw; int kh, kw, strh, strw, padh, padw; int ldx; int k_per_split;
 };
-// In-kernel fold of a producer's BatchNorm statistics rows (stat_fold.h): tickets == nullptr = no
-// fold (the host launches bn_stat_reduce). Rows are merged in groups of kStatGroupRows.
-constexpr int kStatGroupRows = 128;  // = bn_stat_reduce's rows per level-1 block
-__host__ __device__ inline int stat_fold_groups(int rows) { return (rows + kStatGroupRows - 1) / kStatGroupRows; }
-struct StatFold {
-  float* out;          // one group: the finished [2][C] statistics
-  float* part;         // several groups: [groups][3][C] level-1 partials (read_stats' layout)
-  unsigned* tickets;   // >= groups zeroed words, left zeroed
-  int arrivals;        // arrivals per row (column tiles writing a slice of each row; set by the launcher)
-};
-
 struct G2Args {
   const bf16* A; const bf16* B; bf16* C;
   unsigned a_bytes, b_bytes;
@@ -52,8 +41,6 @@ struct G2Args {
   // ncls <= 1: the single class (taps 0..ntaps-1, ORY/ORX), filled in by gemm_g2().
   int ncls, cls_rows;
   int cls_t0[4], cls_nt[4], cls_ory[4], cls_orx[4];
-  // statistics fold (stat_fold.h; `stats` rows reduced in the kernel, no bn_stat_reduce)
-  StatFold fold;
   // split-K (set by gemm_g2() for long-K 1x1 GEMMs on small grids): K slices, fp32 partials
   int ksplit; float* kpart;
 };

@@ -27,7 +27,6 @@
 
 #include "common.h"
 #include "api.h"
-#include "stat_fold.h"
 
 namespace dcnn {
 
@@ -163,45 +162,28 @@ __device__ __forceinline__ void g2_epilogue2(const G2Args& p, char* smem, int m0
       red[(r0 * 2 + 1) * BN + cg * 8 + v] = q[v];
     }
     __syncthreads();
-    // (folded statistics: agent-coherent row stores, read back by the group's last arriver)
-    const bool fold = p.fold.tickets != nullptr;
-    const __amdgpu_buffer_rsrc_t rsS = stat_rsrc(p.stats);
     if (bnb) {  // backward: plain sums [tiles][2][N]
       for (int c = tid; c < 2 * BN; c += 256) {
         const int which = c / BN, cc = c % BN;
         if (n0 + cc < p.N) {
           float a = 0.f;
           for (int k = 0; k < RSTEP; ++k) a += red[(k * 2 + which) * BN + cc];
-          const long o = ((long)tm * 2 + which) * p.N + n0 + cc;
-          if (fold) stat_store_sc1(rsS, o, a);
-          else p.stats[o] = a;
+          p.stats[((long)tm * 2 + which) * p.N + n0 + cc] = a;
         }
       }
     } else if (tid < BN && n0 + tid < p.N) {  // forward: Welford triple [tiles][3][N]
       float a = 0.f, b = 0.f;
       for (int k = 0; k < RSTEP; ++k) { a += red[(k * 2 + 0) * BN + tid]; b += red[(k * 2 + 1) * BN + tid]; }
       const float cnt = (float)min(BM, p.M - m0);
-      const Welford w = welford_from_shifted(cnt, piv_col, a, b);
-      if (fold) {
-        const long o = ((long)tm * 3) * p.N + n0 + tid;
-        stat_store_sc1(rsS, o, w.n);
-        stat_store_sc1(rsS, o + p.N, w.mean);
-        stat_store_sc1(rsS, o + 2l * p.N, w.m2);
-      } else {
-        store_welford(p.stats, tm, p.N, n0 + tid, w);
-      }
-    }
-    if (fold) {  // this tile's slice of statistics row tm arrives (stat_fold.h)
-      __syncthreads();  // (the reduction scratch is the fold's LDS)
-      const int rows = (p.M + BM - 1) / BM;
-      int* flags = reinterpret_cast<int*>(smem + kStatFoldLds);
-      if (bnb) stat_fold_arrive<1>(p.stats, rows, p.N, 1, [&](int) { return tm; }, p.fold, flags, smem);
-      else stat_fold_arrive<0>(p.stats, rows, p.N, 1, [&](int) { return tm; }, p.fold, flags, smem);
+      store_welford(p.stats, tm, p.N, n0 + tid, welford_from_shifted(cnt, piv_col, a, b));
     }
   }
 }
 
-template <int BM, int BN, int BK, bool UNI, int NST>
+// SPLIT: the split-K instance (gemm_g2() on long-K 1x1 GEMMs: workgroup = (tile, K slice), fp32
+// partial tiles out, g2_splitk_epi_kernel runs the epilogue). A separate instance: the slice decode
+// and the partial store cost the plain instances ~50 VGPRs and an occupancy step.
+template <int BM, int BN, int BK, bool UNI, int NST, bool SPLIT = false>
 __global__ void __launch_bounds__(256, 2) gemm_g2_kernel(G2Args p) {
   prefetch_kernargs<sizeof(G2Args)>();
   using T = G2<BM, BN, BK, UNI, NST>;
@@ -212,8 +194,8 @@ __global__ void __launch_bounds__(256, 2) gemm_g2_kernel(G2Args p) {
   const int lt_all = xcd_remap2(blockIdx.x, gridDim.x);
   // split-K (plain 1x1 GEMMs with long K on small grids, gemm_g2()): workgroup = (tile, K slice);
   // the slices of a tile are neighbours in the remapped order (one XCD's L2 holds the tile's B)
-  const int ks = p.ksplit > 1 ? p.ksplit : 1;
-  const int lt = lt_all / ks, kslice = lt_all - lt * ks;
+  const int ks = SPLIT ? p.ksplit : 1;
+  const int lt = SPLIT ? lt_all / ks : lt_all, kslice = SPLIT ? lt_all - lt * ks : 0;
   const int tm = lt / tiles_n, tn = lt % tiles_n;
   // row class of this tile (grouped strided-dgrad phases; one class otherwise). The classes are
   // interleaved tile row by tile row: each XCD's contiguous share of the remapped grid holds every
@@ -334,9 +316,9 @@ __global__ void __launch_bounds__(256, 2) gemm_g2_kernel(G2Args p) {
   const int K = ntp * p.Cs;
   const int nk_all = (K + BK - 1) / BK;
   // this workgroup's K-steps [kb, kb + nk) (all of them without split-K)
-  const int kb = (int)((long)nk_all * kslice / ks);
-  const int nk = (int)((long)nk_all * (kslice + 1) / ks) - kb;
-  if constexpr (UNI) {  // (the stage counters start at the slice's first K-step)
+  const int kb = SPLIT ? (int)((long)nk_all * kslice / ks) : 0;
+  const int nk = SPLIT ? (int)((long)nk_all * (kslice + 1) / ks) - kb : nk_all;
+  if constexpr (UNI && SPLIT) {  // (the stage counters start at the slice's first K-step)
     const int k0 = kb * BK;
     st_t = k0 / p.Cs;
     st_c = k0 - st_t * p.Cs;
@@ -408,7 +390,7 @@ __global__ void __launch_bounds__(256, 2) gemm_g2_kernel(G2Args p) {
     }
   }
 
-  if (ks > 1) {
+  if constexpr (SPLIT) {
     // fp32 partial tile of this K slice -> kpart[slice][M][N] (the epilogue kernel sums the
     // slices in order and runs the epilogue, g2_splitk_epi_kernel)
     float* out = p.kpart + (long)kslice * p.M * p.N;
@@ -453,8 +435,8 @@ __global__ void __launch_bounds__(256, 2) g2_splitk_epi_kernel(G2Args p) {
   prefetch_kernargs<sizeof(G2Args)>();
   constexpr int EPI_PITCH = BN * 2 + 16;
   constexpr int RSTEP = 256 / (BN / 8);
-  constexpr int L1 = BM * EPI_PITCH, L2 = RSTEP * 2 * BN * 4, L3 = kStatFoldLds + 64 * 4;
-  constexpr int LDS = L1 > L2 ? (L1 > L3 ? L1 : L3) : (L2 > L3 ? L2 : L3);
+  constexpr int L1 = BM * EPI_PITCH, L2 = RSTEP * 2 * BN * 4;
+  constexpr int LDS = L1 > L2 ? L1 : L2;
   __shared__ __attribute__((aligned(16))) char smem[LDS];
   const int tid = threadIdx.x;
   const int tiles_n = (p.N + BN - 1) / BN;
@@ -773,7 +755,7 @@ int gemm_g2_splitk_enabled() { return g_g2_splitk; }
 static int g2_ksplit(const G2Args& a, int tiles, int bk) {
   if (g_g2_splitk != 1 || a.ntaps != 1 || a.ncls > 1 || a.Cs < 1024 || tiles >= 256) return 1;
   if (a.tap_dy[0] != 0 || a.tap_dx[0] != 0 || a.SY != 1 || a.SX != 1 || a.OSY != 1 || a.OSX != 1 ||
-      a.GH != a.H || a.GW != a.W || a.OH != a.GH || a.OW != a.GW || a.ldc != a.N || a.fold.tickets)
+      a.GH != a.H || a.GW != a.W || a.OH != a.GH || a.OW != a.GW || a.ldc != a.N)
     return 1;
   const int nk = (a.Cs + bk - 1) / bk;
   int ks = (512 + tiles - 1) / tiles;
@@ -786,15 +768,18 @@ template <int BM, int BN, int BK, bool UNI>
 static void launch_g2(const G2Args& a0, hipStream_t s) {
   const int tiles = ((a0.M + BM - 1) / BM) * ((a0.N + BN - 1) / BN);
   G2Args a = a0;
-  a.ksplit = g2_ksplit(a0, tiles, BK);
-  if (a.ksplit > 1) {
-    a.kpart = g2_kpart((size_t)a.ksplit * a.M * a.N * 4, s);
-    hipLaunchKernelGGL((gemm_g2_kernel<BM, BN, BK, UNI, 2>), dim3(tiles * a.ksplit), dim3(256), 0, s, a);
-    DCNN_LAUNCH_CHECK();
-    a.zero_ptr = nullptr;  // (zeroed by the GEMM launch)
-    hipLaunchKernelGGL((g2_splitk_epi_kernel<BM, BN>), dim3(tiles), dim3(256), 0, s, a);
-    DCNN_LAUNCH_CHECK();
-    return;
+  a.ksplit = 1;
+  if constexpr (BK == 64 && UNI) {  // (split-K shapes: K >= 1024, so always 64-wide uniform K-steps)
+    a.ksplit = g2_ksplit(a0, tiles, BK);
+    if (a.ksplit > 1) {
+      a.kpart = g2_kpart((size_t)a.ksplit * a.M * a.N * 4, s);
+      hipLaunchKernelGGL((gemm_g2_kernel<BM, BN, BK, UNI, 2, true>), dim3(tiles * a.ksplit), dim3(256), 0, s, a);
+      DCNN_LAUNCH_CHECK();
+      a.zero_ptr = nullptr;  // (zeroed by the GEMM launch)
+      hipLaunchKernelGGL((g2_splitk_epi_kernel<BM, BN>), dim3(tiles), dim3(256), 0, s, a);
+      DCNN_LAUNCH_CHECK();
+      return;
+    }
   }
   // single-step K loops (1x1 convs on 32-64 channels and their data gradients) never use a third
   // ring stage: 2 stages there free LDS for one more resident workgroup per CU (layer-1 1x1 dgrad
@@ -846,7 +831,6 @@ int gemm_g2_row_tile(int M, int N) {
 
 void gemm_g2(const G2Args& a_in, hipStream_t s) {
   G2Args a = a_in;
-  if (a.fold.tickets && !a.stats) throw std::runtime_error("gemm_g2: statistics fold without statistics rows");
   if (a.N % 8 != 0 || a.Cs % 8 != 0 || a.ldb % 8 != 0 || a.ldc % 8 != 0 || a.ntaps > 64 || a.ntaps < 1)
     throw std::runtime_error("gemm_g2: unsupported shape (needs N, Cs, ldb, ldc multiples of 8, 1..64 taps)");
   int bm, bn;
@@ -863,7 +847,6 @@ void gemm_g2(const G2Args& a_in, hipStream_t s) {
   }
   const int bk = (a.Cs % 64 == 0) ? 64 : 32;
   const bool uni = a.Cs % bk == 0;
-  a.fold.arrivals = (a.N + bn - 1) / bn;  // (every column tile writes its slice of a statistics row)
 #define DCNN_G2(BM, BN, BK, U) if (bm == BM && bn == BN && bk == BK && uni == U) return launch_g2<BM, BN, BK, U>(a, s)
   DCNN_G2(128, 128, 64, true);
   DCNN_G2(128, 64, 64, true);

@@ -99,25 +99,16 @@ def _slab(L, ptr, rows, width, C):
     return t.double()
 
 
-FOLDED = 1 << 24  # ops_gpu.hip kFolded: rows >= this = the producer reduced its rows in-kernel
-
-
 def _check_stats(L, y, ptr, rows):
-    """Forward epilogue rows (count, mean, M2) merged in float64 == the stored output's moments;
-    folded statistics (stat_fold.h): the finished (mean, var) of one group, or the groups' level-1
-    Welford partials."""
+    """Forward epilogue rows (count, mean, M2) merged in float64 == the stored output's moments."""
     C = y.shape[1]
     yd = y.double()
-    if rows >= FOLDED and rows - FOLDED == 1:
-        s = _slab(L, ptr, 1, 2, C)[0]
-        mean, var = s[0], s[1]
-    else:
-        s = _slab(L, ptr, rows - FOLDED if rows >= FOLDED else rows, 3, C)
-        n, mu, m2 = s[:, 0], s[:, 1], s[:, 2]
-        tot = n.sum(0)
-        mean = (n * mu).sum(0) / tot
-        var = (m2.sum(0) + (n * (mu - mean) ** 2).sum(0)) / tot
-        assert float(tot[0]) == y.numel() // C, "statistics rows: pixel count"
+    s = _slab(L, ptr, rows, 3, C)
+    n, mu, m2 = s[:, 0], s[:, 1], s[:, 2]
+    tot = n.sum(0)
+    mean = (n * mu).sum(0) / tot
+    var = (m2.sum(0) + (n * (mu - mean) ** 2).sum(0)) / tot
+    assert float(tot[0]) == y.numel() // C, "statistics rows: pixel count"
     rm, rv = yd.mean((0, 2, 3)), yd.var((0, 2, 3), unbiased=False)
     assert (mean - rm).abs().max() < 1e-4 * (1 + rm.abs().max()), "forward statistics: mean"
     assert ((var - rv).abs() / rv.clamp_min(1e-12)).max() < 1e-3, "forward statistics: variance"
@@ -187,10 +178,7 @@ def _replay(L, c, g):
         _close(dx.float(), ref, "data gradient")
         if c["bnb"] and rows.value > 0:
             r = rows.value
-            if r >= FOLDED:  # reduced in the kernel: [2][C] sums, or [groups][3][C] partial sums
-                s = _slab(L, slab.value, 1, 2, Ci)[0] if r - FOLDED == 1 else _slab(L, slab.value, r - FOLDED, 3, Ci)[:, :2].sum(0)
-            else:
-                s = _slab(L, slab.value, r, 2, Ci).sum(0)
+            s = _slab(L, slab.value, r, 2, Ci).sum(0)
             d = dx.double()
             xhat = (xb.double() - mean.double()[None, :, None, None]) * istd.double()[None, :, None, None]
             ref_s = torch.stack([d.sum((0, 2, 3)), (d * xhat).sum((0, 2, 3))])
