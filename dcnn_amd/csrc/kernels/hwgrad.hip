@@ -373,6 +373,12 @@ __global__ void __launch_bounds__(256 * TSP, 1) hwgrad2_kernel(HWArgs p) {
     }
   };
 
+  // the first tile(s) go out before the fragment-address arithmetic below (both run variants start
+  // with them; only ALU work sits between here and their counted waits)
+  const int nt = tend - tbeg;
+  if (nt > 0) load_tile(0, tbeg);
+  if (NS == 3 && nt > 1) load_tile(1, tbeg + 1);
+
   // ---- fragment base addresses (stage-relative bytes) ----
   // pixel of (k-step kk, half h) for this lane: kk*32 + h*16 + 4*(lane>>4) + ((lane&15)>>2)
   const int lpx = 4 * (lane >> 4) + ((lane & 15) >> 2);
@@ -437,9 +443,6 @@ __global__ void __launch_bounds__(256 * TSP, 1) hwgrad2_kernel(HWArgs p) {
     for (int t = 0; t < NTW; ++t) acc[t] = f32x4{0.f, 0.f, 0.f, 0.f};
     const bool do_bias = p.bias_slab != nullptr && c0 == 0 && th == 0;
     float bias_acc = 0.f;
-    const int nt = tend - tbeg;
-    if (nt > 0) load_tile(0, tbeg);
-    if (NS == 3 && nt > 1) load_tile(1, tbeg + 1);
     if (NS == 3 && nt > 1)
       asm volatile("s_waitcnt vmcnt(%0)" ::"n"(INS) : "memory");
     else
@@ -533,9 +536,6 @@ __global__ void __launch_bounds__(256 * TSP, 1) hwgrad2_kernel(HWArgs p) {
 
     const bool do_bias = p.bias_slab != nullptr && c0 == 0 && th == 0;
     float bias_acc = 0.f;
-    const int nt = tend - tbeg;
-    if (nt > 0) load_tile(0, tbeg);
-    if (NS == 3 && nt > 1) load_tile(1, tbeg + 1);
     if (NS == 3 && nt > 1)
       asm volatile("s_waitcnt vmcnt(%0)" ::"n"(INS) : "memory");
     else
