@@ -894,6 +894,11 @@ __global__ void __launch_bounds__(256 * TSP, 1) hwgrad_s2_kernel(HWArgs p) {
     }
   };
 
+  // the first tile(s) go out before the halo-row table below (only ALU work until their waits)
+  const int nt = tend - tbeg;
+  if (nt > 0) load_tile(0, tbeg);
+  if (NS == 3 && nt > 1) load_tile(1, tbeg + 1);
+
   // ---- per-lane halo row of the tap (0, 0) for each (k-step, half) pixel quad: input pixel
   //      (2 y + 1, 2 x + 1) of the halo for output pixel (y, x) ----
   int hrow[2 * KS];
@@ -915,9 +920,6 @@ __global__ void __launch_bounds__(256 * TSP, 1) hwgrad_s2_kernel(HWArgs p) {
   const int bcol = wid * 16 + 4 * (lane & 3);  // B column (input channel) this lane reads
   const bool do_bias = p.bias_slab != nullptr && c0 == 0 && th == 0;
   float bias_acc = 0.f;
-  const int nt = tend - tbeg;
-  if (nt > 0) load_tile(0, tbeg);
-  if (NS == 3 && nt > 1) load_tile(1, tbeg + 1);
   if (NS == 3 && nt > 1)
     asm volatile("s_waitcnt vmcnt(%0)" ::"n"(INS) : "memory");  // tile 0 landed, tile 1 may fly
   else

@@ -1,5 +1,5 @@
 #!/bin/bash
-# hwgrad2: first tile loads before the fragment-address setup — tests + same-box A/B vs HEAD (tools/ab_old)
+# hwgrad kernels: first tile loads before the address setup — tests + same-box A/B vs HEAD (tools/ab_old)
 cd $GRAFT_REPO_ROOT; mkdir -p gpurun_out; export TMPDIR=/tmp
 L=gpurun_out/it20.log; : > $L
 timeout -k 10 900 python -u -m pytest -x -q --timeout 300 --timeout-method thread -p no:cacheprovider tests/test_gpu_kernels.py tests/test_gpu_hconv3.py tests/test_gpu_cpp_geometry.py -m gpu >> $L 2>&1 || { tail -30 $L; exit 1; }
