@@ -68,8 +68,11 @@ __device__ __forceinline__ int h3_perm(int l) {
   if constexpr (TWC == 4) return l;
   return l < 4 ? l : (l >= 12 ? l - 8 : l + 4);
 }
-template <int TWC>
+// (GUT: the 4 x 4-map gutter layout, runtime pitch 21: a 2-bit swizzle of pixel bits 2-3; the
+// 1-bit one left 33% of its ds_read_b128 cycles bank-conflicted, profiles/pmc_stalls_r5.md)
+template <int TWC, bool GUT = false>
 __device__ __forceinline__ int h3_swz(int P) {
+  if constexpr (GUT) return (P >> 2) & 3;
   if constexpr (TWC == 4) return ((P >> 3) & 1) << 1;
   return ((P >> 2) & 1) << 1;
 }
@@ -317,7 +320,7 @@ __global__ void __launch_bounds__(NW * 64, 8 / NW) hconv3_kernel(HConvArgs p, H3
 #pragma unroll
       for (int t = 0; t < NBA; ++t) {
         const int P = P0 + (NBA == 3 ? t : (t / 3) * pitch + (t % 3));
-        baddr[j][t] = P * 64 + ((lh ^ h3_swz<TWC>(P)) << 4);
+        baddr[j][t] = P * 64 + ((lh ^ h3_swz<TWC, HN == 7>(P)) << 4);
       }
     }
   };
@@ -412,7 +415,7 @@ __global__ void __launch_bounds__(NW * 64, 8 / NW) hconv3_kernel(HConvArgs p, H3
           im = iy * g.GX + ix;
           ok = ok && cy != 0 && cx != 0;
         }
-        if (ok) v = (unsigned)cx | ((unsigned)cy << 8) | ((unsigned)im << 16) | ((unsigned)((lane & 3) ^ h3_swz<TWC>(P)) << 24);
+        if (ok) v = (unsigned)cx | ((unsigned)cy << 8) | ((unsigned)im << 16) | ((unsigned)((lane & 3) ^ h3_swz<TWC, HN == 7>(P)) << 24);
       }
       hpk[k] = v;
     }
