@@ -43,6 +43,9 @@ struct G2Args {
   int cls_t0[4], cls_nt[4], cls_ory[4], cls_orx[4];
   // split-K (set by gemm_g2() for long-K 1x1 GEMMs on small grids): K slices, fp32 partials
   int ksplit; float* kpart;
+  // multiply-shift reciprocals of GH * GW and GW (set by gemm_g2(): the per-row pixel decode of
+  // the A loader and the epilogue without run-time integer divisions; common.h FastDiv layout)
+  unsigned fd_ghw[3], fd_gw[3];
 };
 struct T2Args {
   const bf16* dY; const bf16* X; float* slab; float* bias_slab;

@@ -44,6 +44,11 @@ __device__ __forceinline__ void glds16(__amdgpu_buffer_rsrc_t rsrc, char* lds, u
 
 constexpr unsigned kOOB = 0x80000000u;  // any offset >= num_records reads zeros
 
+// n / d for n < 2^31 with G2Args' multiply-shift reciprocal {mul, shr, d} (common.h FastDiv)
+__device__ __forceinline__ unsigned g2_div(int n, const unsigned* f) {
+  return fdiv((unsigned)n, FastDiv{f[0], f[1], f[2]});
+}
+
 // ---------------------------------------------------------------------------------------------
 // gathered NT GEMM
 // ---------------------------------------------------------------------------------------------
@@ -93,8 +98,8 @@ __device__ __forceinline__ void g2_epilogue2(const G2Args& p, char* smem, int m0
   const int ghw = p.GH * p.GW;
   auto orow_of = [&](int row) {
     const int ml = m0 + row - mcls;
-    const int img = ml / ghw, rem = ml - img * ghw;
-    const int gy = rem / p.GW, gx = rem - gy * p.GW;
+    const int img = (int)g2_div(ml, p.fd_ghw), rem = ml - img * ghw;
+    const int gy = (int)g2_div(rem, p.fd_gw), gx = rem - gy * p.GW;
     return ((long)img * p.OH + gy * p.OSY + ory) * p.OW + gx * p.OSX + orx;
   };
   // every row's operands are loaded before the first store: a load's wait also waits for every
@@ -227,10 +232,9 @@ __global__ void __launch_bounds__(256, 2) gemm_g2_kernel(G2Args p) {
     uint64_t mask = 0;
     unsigned base = 0;
     if (m < p.M) {
-      const int ghw = p.GH * p.GW;
       const int ml = m - mcls;
-      const int img = ml / ghw, rem = ml - img * ghw;
-      const int gy = rem / p.GW, gx = rem - gy * p.GW;
+      const int img = (int)g2_div(ml, p.fd_ghw), rem = ml - img * p.GH * p.GW;
+      const int gy = (int)g2_div(rem, p.fd_gw), gx = rem - gy * p.GW;
       const int y0 = gy * p.SY, x0 = gx * p.SX;
       base = (unsigned)((((long)img * p.H + y0) * p.W + x0) * p.Cs * 2);
       for (int t = 0; t < ntp; ++t) {
@@ -844,6 +848,12 @@ void gemm_g2(const G2Args& a_in, hipStream_t s) {
     for (int c = 0; c < a.ncls; ++c)
       if (a.cls_nt[c] < 0 || a.cls_t0[c] < 0 || a.cls_t0[c] + a.cls_nt[c] > a.ntaps)
         throw std::runtime_error("gemm_g2: class tap range out of bounds");
+  }
+  {
+    const FastDiv f1 = make_fastdiv((unsigned)(a.GH * a.GW)), f2 = make_fastdiv((unsigned)a.GW);
+    a.fd_ghw[0] = f1.mul; a.fd_ghw[1] = f1.shr; a.fd_ghw[2] = f1.d;
+    a.fd_gw[0] = f2.mul; a.fd_gw[1] = f2.shr; a.fd_gw[2] = f2.d;
+    if ((long)a.M >= (1l << 31)) throw std::runtime_error("gemm_g2: M >= 2^31");
   }
   const int bk = (a.Cs % 64 == 0) ? 64 : 32;
   const bool uni = a.Cs % bk == 0;
