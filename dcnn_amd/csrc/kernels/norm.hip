@@ -606,7 +606,7 @@ __global__ void __launch_bounds__(256) bn_apply_v_kernel(const T* __restrict__ x
     for (int u = 0; u < U; ++u) {
       const unsigned k = i + u * stride;
       if (k < nv) {
-        const int c0 = (int)(k % cv) * 8;
+        const int c0 = (int)((cv & (cv - 1)) == 0 ? (k & (cv - 1)) : k % cv) * 8;  // (C / 8 a power of two: a mask)
         const float4 s0 = *reinterpret_cast<const float4*>(scale + c0), s1 = *reinterpret_cast<const float4*>(scale + c0 + 4);
         const float4 h0 = *reinterpret_cast<const float4*>(shift + c0), h1 = *reinterpret_cast<const float4*>(shift + c0 + 4);
         const float sc[8] = {s0.x, s0.y, s0.z, s0.w, s1.x, s1.y, s1.z, s1.w};
@@ -729,7 +729,7 @@ __global__ void __launch_bounds__(256) bn_bwd_apply_v_kernel(const T* __restrict
     for (int u = 0; u < U; ++u) {
       const unsigned k = i + u * stride;
       if (k < nv) {
-        const int c0 = (int)(k % cv) * 8;
+        const int c0 = (int)((cv & (cv - 1)) == 0 ? (k & (cv - 1)) : k % cv) * 8;  // (C / 8 a power of two: a mask)
         float A[8], B[8], M[8], D[8], d[8], xf[8];
         ld8(ca + c0, A);
         ld8(cbm + c0, B);
@@ -839,7 +839,7 @@ __global__ void __launch_bounds__(256) bn_apply_dual_kernel(BnSide a, BnSide b, 
       na = ldg16(xa + (size_t)inx * 8);
       nb = ldg16(xb + (size_t)inx * 8);
     }
-    const int c0 = (int)(i % cv) * 8;
+    const int c0 = (int)((cv & (cv - 1)) == 0 ? (i & (cv - 1)) : i % cv) * 8;  // (C / 8 a power of two: a mask)
     float A[8], HA[8], B[8], HB[8], fa[8], fb[8];
     ld8(sa + c0, A);
     ld8(ha + c0, HA);
@@ -952,7 +952,7 @@ __global__ void __launch_bounds__(256) bn_bwd_apply_dual_kernel(const bf16* __re
       na = ldg16(xa + (size_t)inx * 8);
       nb = ldg16(xb + (size_t)inx * 8);
     }
-    const int c0 = (int)(i % cv) * 8;
+    const int c0 = (int)((cv & (cv - 1)) == 0 ? (i & (cv - 1)) : i % cv) * 8;  // (C / 8 a power of two: a mask)
     float d[8];
     unpack8(vd, d);
 #pragma unroll
