@@ -65,6 +65,10 @@ def main():
     ap.add_argument("--hwgrad-s2", type=int, default=None, help="3x3 stride-2 wgrad on the stride-2 halo kernel (ops/fusion.py)")
     ap.add_argument("--split-target", type=int, default=None, help="hconv split-K workgroup target (tuning hook)")
     ap.add_argument("--split-min-work", type=int, default=None, help="hconv least taps x chunks per split")
+    ap.add_argument("--bnb", action="store_true",
+                    help="dgrad with the production epilogue: the consuming BatchNorm's ReLU mask (y) and "
+                         "backward statistics (x, mean, istd) fused in (BnbRequest)")
+    ap.add_argument("--no-group", action="store_true", help="strided dgrad phases as separate launches")
     a = ap.parse_args()
     from dcnn_amd.ops import hip, fusion
     if a.split_target is not None:
@@ -73,6 +77,8 @@ def main():
         hip.kernels().hconv_set_split_min_work(a.split_min_work)
     hip.kernels().hconv3_enable(a.v3)
     fusion.HCONV_1X1 = bool(a.halo_1x1)
+    if a.no_group:
+        fusion.G2_GROUP = False
     if a.hwgrad_s2 is not None:
         fusion.HWGRAD_S2 = bool(a.hwgrad_s2)
     CL = torch.channels_last
@@ -98,9 +104,17 @@ def main():
         hbm = {"fwd": 2.0 * (N * H * W * Ci + N * OH * OW * Co + Co * Ci * k * k),
                "dgrad": 2.0 * (N * H * W * Ci + N * OH * OW * Co + Co * Ci * k * k),
                "wgrad": 2.0 * (N * H * W * Ci + N * OH * OW * Co) + 4.0 * Co * Ci * k * k}
+        bnb = None
+        if a.bnb and Ci >= 8:
+            # the BatchNorm that produced x: ReLU output y (mask), input xb, saved statistics
+            from dcnn_amd.ops.hip_base import BnbRequest
+            xb = torch.randn_like(x)
+            bnb = BnbRequest(None, torch.relu(xb), xb, torch.zeros(Ci, device="cuda"),
+                             torch.ones(Ci, device="cuda"))
+            hbm["dgrad"] += 4.0 * N * H * W * Ci  # y and x read in the epilogue
         ops = {
             "fwd": lambda: hip.conv2d_fwd(x, wf, None, (s, s), (p, p), stats=True),
-            "dgrad": lambda: hip.conv2d_dgrad(dy, wt, x.shape, (s, s), (p, p)),
+            "dgrad": lambda: hip.conv2d_dgrad(dy, wt, x.shape, (s, s), (p, p), bnb=bnb),
             "wgrad": lambda: hip.conv2d_wgrad(dy, x, w.shape, (s, s), (p, p), gw, None),
         }
         if a.torch_mm and k == 1 and s == 1:

@@ -712,7 +712,13 @@ __global__ void __launch_bounds__(256, 2) gemm_t2_kernel(T2Args p) {
 // ---------------------------------------------------------------------------------------------
 // LDS ring depth: 3 stages wherever the deeper ring still leaves two workgroups per CU (every
 // tile but 128x128), else 2 (g2_stages() == 0: that rule)
-static int g2_stages() { return 0; }
+static int g2_stages() {
+  static const int v = [] {
+    const char* e = std::getenv("DCNN_G2_STAGES");  // experiment hook: force 2 or 3 ring stages
+    return e ? std::atoi(e) : 0;
+  }();
+  return v == 2 || v == 3 ? v : 0;
+}
 
 // split-K partial workspace per (device, stream): grow-only, allocated in the eager warm-up
 // before a graph captures the step. An outgrown buffer is kept (a graph captured earlier still
@@ -804,6 +810,12 @@ static void launch_g2(const G2Args& a0, hipStream_t s) {
 
 // Tile choice: the largest tile that still gives >= ~2 workgroups per CU.
 void g2_tile(int M, int N, int* bm, int* bn) {
+  static const int force = [] {  // experiment hook: DCNN_G2_TILE=BMxBN forces one tile shape
+    const char* e = std::getenv("DCNN_G2_TILE");
+    int m = 0, n = 0;
+    return (e && std::sscanf(e, "%dx%d", &m, &n) == 2) ? m * 1000 + n : 0;
+  }();
+  if (force) { *bm = force / 1000; *bn = force % 1000; return; }
   auto tiles = [&](int m, int n) { return (long)((M + m - 1) / m) * ((N + n - 1) / n); };
   // (DCNN_G2_SPLITK=2 experiment: grids below 192 tiles of 64 x 64 on 32 x 64 tiles instead)
   if (g_g2_splitk == 2 && N <= 256 && tiles(64, 64) < 192) { *bm = 32; *bn = 64; return; }
