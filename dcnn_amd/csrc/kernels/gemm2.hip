@@ -799,8 +799,14 @@ static void launch_g2(const G2Args& a0, hipStream_t s) {
     const int k = a.cls_nt[c] * ((a.Cs + BK - 1) / BK);
     ksteps = k > ksteps ? k : ksteps;
   }
+  // The 128 x 64 tile also stays at 2 stages: there the third stage costs an occupancy step (3 -> 2
+  // workgroups per CU: 131 VGPRs, 49 vs 74 KB of LDS) that the deeper ring does not buy back.
+  // ResNet-18 b256 step, per-kernel trace (tools/gpu/g2stages_prof.sh): the l2.b1c1 data gradient
+  // 75.6 -> 67.1 us and the l2.proj one 29.3 -> 24.8 us at 2 stages, while the 64 x 128 / 64 x 64
+  // tiles (2 -> 3 and 3 -> 5 per CU at 2 stages) got slower there (26.8 -> 30.0, 28.8 -> 37.6 us).
+  constexpr bool deep = !(BM == 128 && BN == 64);
   const int stages = g2_stages() ? g2_stages()
-                                 : ((2 * G2<BM, BN, BK, UNI, 3>::LDS <= 163840 && ksteps > 1) ? 3 : 2);
+                                 : ((deep && 2 * G2<BM, BN, BK, UNI, 3>::LDS <= 163840 && ksteps > 1) ? 3 : 2);
   if (stages == 3)
     hipLaunchKernelGGL((gemm_g2_kernel<BM, BN, BK, UNI, 3>), dim3(tiles), dim3(256), 0, s, a);
   else
