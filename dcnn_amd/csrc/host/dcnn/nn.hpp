@@ -137,6 +137,12 @@ class Conv2D : public Layer {
   void set_block_bnb_producer(class BatchNorm* bn) { bnb_block_from_ = bn; }
   // GPU: backward whose input gradient also adds `residual` in the data-gradient epilogue
   Tensor backward_residual(const Tensor& dy, const Tensor& residual);
+  // GPU RGB stem (the network input, fp32, on the stem kernel): true when this micro-batch's
+  // forward ran it, so backward_stem_bn applies
+  bool ran_stem() const;
+  // the stem's weight gradient with its BatchNorm's backward applied to `dy` on the fly
+  // (Sequential::backward_activation; gpu_ops::stem_wgrad_bn)
+  void backward_stem_bn(const Tensor& dy, const gpu_ops::StemBn& bn);
   void sync_shadow() override;
   // GPU parameter arena: allocate this conv's pre-transposed dgrad operand; the arena's batched
   // transpose row and tile count (false: not eligible)
@@ -216,6 +222,10 @@ class BatchNorm : public Layer {
     pending_slab_ = slab;
     pending_rows_ = rows;
   }
+  // GPU: this layer's backward over `dy` folded into the stem conv's weight gradient (its input
+  // gradient has no other consumer): false when not applicable (no consumer statistics slab for
+  // dy, or eval mode), the caller then runs the two backwards
+  bool backward_into_stem(const Tensor& dy, Conv2D& stem);
   Tensor running_mean, running_var;
 
  private:

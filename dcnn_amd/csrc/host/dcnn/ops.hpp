@@ -101,6 +101,23 @@ bool stem_ok(const ConvShape& s);
 const float* stem_fwd(const float* x, const void* w, const float* bias, void* y, const ConvShape& s,
                       int* stat_rows = nullptr);
 void stem_wgrad(const void* dy, const float* x, float* gw, float* gb, const ConvShape& s);
+// the stem's own BatchNorm backward folded into its weight gradient (that BatchNorm's input
+// gradient is never materialised: the stem conv is its only consumer). dy is the BatchNorm's
+// masked output gradient with its statistics rows in `slab` (bn_bwd_slab's operands); the
+// BatchNorm's parameter gradients dg / db accumulate as bn_bwd_slab's do. Same result as
+// bn_bwd_slab followed by stem_wgrad, bit for bit.
+struct StemBn {
+  const void* x;             // BatchNorm input (the stem conv's output), bf16 NHWC
+  const float* mean;         // saved batch statistics
+  const float* istd;
+  const float* gamma;        // null: no affine
+  float* dgamma;
+  float* dbeta;
+  const float* slab;         // backward statistics rows (sum dy, sum dy * xhat)
+  int rows;
+  bool train;
+};
+void stem_wgrad_bn(const void* dy, const float* x, float* gw, float* gb, const ConvShape& s, const StemBn& bn);
 // w: bf16 [Out][In]
 void dense_fwd(const void* x, const void* w, const float* bias, void* y, int N, int In, int Out);
 void dense_dgrad(const void* dy, const void* w, void* dx, int N, int In, int Out);

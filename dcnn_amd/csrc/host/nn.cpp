@@ -181,6 +181,18 @@ Tensor Conv2D::forward(const Tensor& x, bool training) {
   return y;
 }
 
+bool Conv2D::ran_stem() const {
+  const Tensor& x_ = const_cast<Conv2D*>(this)->mbc().a;
+  return dev_.is_gpu() && x_.defined() && x_.dtype() == DType::F32;
+}
+
+void Conv2D::backward_stem_bn(const Tensor& dy, const gpu_ops::StemBn& bn) {
+  const Tensor& x_ = mbc().a;
+  const ConvShape s = shape_for(x_.shape());
+  gpu_ops::stem_wgrad_bn(dy.data(), x_.ptr<float>(), params_[0].grad.ptr<float>(),
+                         bias_ ? params_[1].grad.ptr<float>() : nullptr, s, bn);
+}
+
 Tensor Conv2D::backward(const Tensor& dy) {
   const Tensor& x_ = mbc().a;
   const ConvShape s = shape_for(x_.shape());
@@ -554,6 +566,27 @@ Tensor BatchNorm::backward_residual(const Tensor& dy, Tensor* branch) {
                     train_);
   }
   return dx;
+}
+
+bool BatchNorm::backward_into_stem(const Tensor& dy, Conv2D& stem) {
+  MbCache& mc = mbc();
+  if (!dev_.is_gpu() || !train_ || bwd_dy_ != dy.data() || bwd_slab_ == nullptr || bwd_rows_ <= 0 ||
+      !stem.ran_stem() || mc.a.dtype() != DType::BF16)
+    return false;
+  gpu_ops::StemBn bn{mc.a.data(),
+                     mc.b.ptr<float>(),
+                     mc.c.ptr<float>(),
+                     affine_ ? params_[0].value.ptr<float>() : nullptr,
+                     affine_ ? params_[0].grad.ptr<float>() : nullptr,
+                     affine_ ? params_[1].grad.ptr<float>() : nullptr,
+                     bwd_slab_,
+                     bwd_rows_,
+                     train_};
+  stem.backward_stem_bn(dy, bn);
+  bwd_dy_ = nullptr;
+  bwd_slab_ = nullptr;
+  bwd_rows_ = 0;
+  return true;
 }
 
 Tensor BatchNorm::backward(const Tensor& dy) {
@@ -1356,10 +1389,31 @@ Tensor Sequential::backward_activation(const Tensor& g_in, int mb) {
     return !(v && std::string(v) == "0");
   }();
   const bool defer = dev_.is_gpu() && defer_env;
+  // (DCNN_STEM_BN_FOLD=0: the stem BatchNorm's backward as its own pass — test / A-B hook)
+  static const bool stem_bn_env = [] {
+    const char* v = std::getenv("DCNN_STEM_BN_FOLD");
+    return !(v && std::string(v) == "0");
+  }();
+  const bool stem_bn_fold = dev_.is_gpu() && stem_bn_env && layers_.size() > 1;
   if (defer) gpu_ops::begin_deferred_reduce();
   try {
     for (size_t i = layers_.size(); i-- > 0;) {
       layers_[i]->set_micro_batch(mb);
+      if (i == 1 && stem_bn_fold) {
+        // the RGB stem's BatchNorm backward inside the stem's weight-gradient kernel (its input
+        // gradient, a full-resolution pass written and read once, is never materialised)
+        auto* bn = dynamic_cast<BatchNorm*>(layers_[1].get());
+        auto* conv = dynamic_cast<Conv2D*>(layers_[0].get());
+        if (bn && conv) {
+          conv->set_micro_batch(mb);
+          if (bn->backward_into_stem(g, *conv)) {
+            if (bwd_hook_) bwd_hook_(1);
+            if (bwd_hook_) bwd_hook_(0);
+            g = Tensor();
+            break;
+          }
+        }
+      }
       g = layers_[i]->backward(g);
       if (bwd_hook_) bwd_hook_(i);
     }

@@ -797,9 +797,25 @@ const float* stem_fwd(const float* x, const void* w, const float* bias, void* y,
   return a.slab;
 }
 
+static void stem_wgrad_impl(const void* dy, const float* x, float* gw, float* gb, const ConvShape& s,
+                            const StemBn* bn);
+
 void stem_wgrad(const void* dy, const float* x, float* gw, float* gb, const ConvShape& s) {
-  rec("stem_wgrad", s, -1, {{"bias", gb != nullptr}, {"deferred", g_defer}});
-  const int blocks = stem_wgrad_blocks(s.N, s.H, s.W);
+  stem_wgrad_impl(dy, x, gw, gb, s, nullptr);
+}
+
+static std::pair<const float*, int> reduce_stats(int mode, const float* slab, int rows, int C);
+
+void stem_wgrad_bn(const void* dy, const float* x, float* gw, float* gb, const ConvShape& s, const StemBn& bn) {
+  stem_wgrad_impl(dy, x, gw, gb, s, &bn);
+}
+
+static void stem_wgrad_impl(const void* dy, const float* x, float* gw, float* gb, const ConvShape& s,
+                            const StemBn* bn) {
+  rec("stem_wgrad", s, -1, {{"bias", gb != nullptr}, {"deferred", g_defer}, {"bn", bn != nullptr}});
+  std::pair<const float*, int> st{nullptr, 0};
+  if (bn) st = reduce_stats(1, bn->slab, bn->rows, s.Co);  // (before the slab scratch below is taken)
+  const int blocks = bn ? stem_wgrad_blocks_bnt(s.N, s.H, s.W) : stem_wgrad_blocks(s.N, s.H, s.W);
   const long n = 9l * s.C * s.Co;
   Tensor hold, bhold;
   float* slab = wgrad_slab(SLAB, (size_t)blocks * n * 4, hold);
@@ -809,6 +825,11 @@ void stem_wgrad(const void* dy, const float* x, float* gw, float* gb, const Conv
   a.gs[0] = 9l * s.C; a.gs[1] = 1; a.gs[2] = 3l * s.C; a.gs[3] = s.C;
   a.n_slab = n;
   a.N = s.N; a.Ci = s.C; a.H = s.H; a.W = s.W; a.Co = s.Co;
+  if (bn) {
+    a.bn_x = static_cast<const bf16*>(bn->x); a.bn_mean = bn->mean; a.bn_istd = bn->istd; a.bn_gamma = bn->gamma;
+    a.bn_sums = st.first; a.bn_parts = st.second; a.bn_count = (float)((long)s.N * s.H * s.W);
+    a.bn_dgamma = bn->dgamma; a.bn_dbeta = bn->dbeta; a.bn_eval = bn->train ? 0 : 1;
+  }
   dcnn::stem_wgrad(a, blocks, cur());
   wgrad_reduce(hold, bhold, slab, gw, n, bslab, gb, s.Co, blocks);
 }

@@ -260,10 +260,17 @@ struct StemArgs {
   const float* bias; bf16* y; float* slab; float* zero_ptr; int zero_n;  // fwd
   const bf16* dy; float* bias_slab; long gs[4]; long n_slab;             // wgrad (gs: grad strides)
   int halo_bytes; int N, Ci, H, W, Co, TH;
+  // wgrad with the stem BatchNorm's backward applied to dy on the fly (bn_x != nullptr: dy is that
+  // BatchNorm's masked output gradient, bn_x its input): dy' = A dy + B (x - mean) + D per channel,
+  // bn_bwd_apply_v_kernel's coefficients from the reduced sums (bn_sums / bn_parts, as
+  // bn_stat_reduce leaves them); workgroup 0 adds the BatchNorm's parameter gradients
+  const bf16* bn_x; const float* bn_mean; const float* bn_istd; const float* bn_gamma; const float* bn_sums;
+  int bn_parts; float bn_count; float* bn_dgamma; float* bn_dbeta; int bn_eval;
 };
 bool stem_supported(int N, int Ci, int H, int W, int Co);
 int stem_tiles_host(int N, int H, int W);
 int stem_wgrad_blocks(int N, int H, int W);
+int stem_wgrad_blocks_bnt(int N, int H, int W);  // (StemArgs::bn_x set)
 void stem_fwd(StemArgs a, hipStream_t s);
 void stem_wgrad(StemArgs a, int blocks, hipStream_t s);
 // f32: fp32 operands (the exact fp32 path), else bf16

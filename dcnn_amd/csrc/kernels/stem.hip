@@ -176,8 +176,12 @@ __global__ void __launch_bounds__(256, NCB <= 2 ? 8 : 4) stem_fwd_kernel(StemArg
 // weight gradient: workgroup b accumulates tiles b, b + grid, ...; each tile's 16 k-steps of 32
 // pixels are split over the 4 waves. D[co][k] with k = tap*4 + ch (k < 36), k = 36: ones.
 // ---------------------------------------------------------------------------------------------
-template <int NCB>
-__global__ void __launch_bounds__(256, NCB <= 2 ? 4 : 2) stem_wgrad_kernel(StemArgs p) {
+// BNT: the BatchNorm-backward transform of dy (StemArgs::bn_x; the stem BatchNorm's data gradient
+// is never written: this kernel is its only consumer). The 16-byte vectors of each staged dY tile
+// are rewritten in LDS as bf16(A dy + B (x - mean) + D), the exact arithmetic and rounding of
+// bn_bwd_apply_v_kernel, so the weight gradient is bit-identical to the unfused pair of passes.
+template <int NCB, bool BNT>
+__global__ void __launch_bounds__(256, NCB <= 2 ? (BNT ? 3 : 4) : 2) stem_wgrad_kernel(StemArgs p) {
   constexpr int CO = NCB * 16;
   extern __shared__ __attribute__((aligned(16))) char smem[];
   bf16* halo = reinterpret_cast<bf16*>(smem);                     // [(TH+2)(W+2)][4]
@@ -186,6 +190,35 @@ __global__ void __launch_bounds__(256, NCB <= 2 ? 4 : 2) stem_wgrad_kernel(StemA
   const int HW2 = p.W + 2;
   const int ntile = stem_tiles(p);
   const i32x4 rs_dy = raw_rsrc(p.dy, (unsigned)((long)p.N * p.H * p.W * CO * 2));
+  // [4][CO] after the dY tile: A, B, mean, D (BNT)
+  float* coef = reinterpret_cast<float*>(smem + p.halo_bytes + SPX * CO * 2);
+  if constexpr (BNT) {
+    for (int c = threadIdx.x; c < CO; c += 256) {
+      // the reduced sums as bn_bwd_apply_v_kernel reads them (read_stats<1>: parts merged in order)
+      float sdy, sdyx;
+      if (p.bn_parts <= 1) {
+        sdy = p.bn_sums[c];
+        sdyx = p.bn_sums[CO + c];
+      } else {
+        sdy = p.bn_sums[c];
+        sdyx = p.bn_sums[CO + c];
+        for (int q = 1; q < p.bn_parts; ++q) {
+          sdy += p.bn_sums[(long)q * 3 * CO + c];
+          sdyx += p.bn_sums[(long)q * 3 * CO + CO + c];
+        }
+      }
+      const float is = p.bn_istd[c], a = (p.bn_gamma ? p.bn_gamma[c] : 1.f) * is;
+      coef[c] = a;
+      coef[CO + c] = p.bn_eval ? 0.f : -a * is * (sdyx / p.bn_count);
+      coef[2 * CO + c] = p.bn_mean[c];
+      coef[3 * CO + c] = p.bn_eval ? 0.f : -a * (sdy / p.bn_count);
+      if (blockIdx.x == 0) {
+        if (p.bn_dgamma) p.bn_dgamma[c] += sdyx;
+        if (p.bn_dbeta) p.bn_dbeta[c] += sdy;
+      }
+    }
+  }
+  constexpr int NVT = SPX * CO / 8 / 256;  // 16-byte vectors of a dY tile per thread
   f32x4 acc[NCB][3];
 #pragma unroll
   for (int cb = 0; cb < NCB; ++cb)
@@ -212,8 +245,39 @@ __global__ void __launch_bounds__(256, NCB <= 2 ? 4 : 2) stem_wgrad_kernel(StemA
       glds16_opaque(rs_dy, reinterpret_cast<char*>(dys) + blk * 1024, src + blk * 1024 + lane * 16);
     }
     stage_halo(p, tile, halo);
+    // the BatchNorm input rows of the tile (same NHWC offsets as dY), issued before the wait for
+    // the dY tile so their latency overlaps it (BNT instances run 3 workgroups per CU: the 4-per-CU
+    // register budget spills with these in flight)
+    uint4 xv[BNT ? NVT : 1];
+    if constexpr (BNT) {
+      const char* xb = reinterpret_cast<const char*>(p.bn_x) + src;
+#pragma unroll
+      for (int j = 0; j < NVT; ++j) xv[j] = *reinterpret_cast<const uint4*>(xb + (threadIdx.x + j * 256) * 16);
+    }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
+    if constexpr (BNT) {
+      {
+        constexpr int j0 = 0, RV = NVT;
+#pragma unroll
+        for (int j = 0; j < RV; ++j) {
+          const int v = threadIdx.x + (j0 + j) * 256;
+          int c0 = (v % (CO / 8)) * 8;
+          // (opaque per round: keeps the coefficient reads here instead of hoisted out of the tile
+          // loop, where 32 more live registers would spill across the MFMA loop)
+          asm volatile("" : "+v"(c0));
+          uint4* q = reinterpret_cast<uint4*>(dys) + v;
+          float d[8], xf[8];
+          unpack8(*q, d);
+          unpack8(xv[j], xf);
+#pragma unroll
+          for (int e = 0; e < 8; ++e)
+            d[e] = coef[c0 + e] * d[e] + coef[CO + c0 + e] * (xf[e] - coef[2 * CO + c0 + e]) + coef[3 * CO + c0 + e];
+          *q = pack8(d);
+        }
+      }
+      __syncthreads();
+    }
     for (int ks = wid; ks < SPX / 32; ks += 4) {
       // this lane's 8 pixels (GEMM k) of the step: ks*32 + kg*8 .. +7, all in one image row
       const int p0 = ks * 32 + kg * 8, py = p0 / p.W, px0 = p0 - py * p.W;
@@ -274,6 +338,19 @@ int stem_wgrad_blocks(int N, int H, int W) {
   return t < 1024 ? t : 1024;
 }
 
+// the BatchNorm-folding instance holds 3 workgroups per CU (its register budget): one resident
+// wave of workgroups instead of 1024 (DCNN_STEM_BNT_BLOCKS: experiment override)
+int stem_wgrad_blocks_bnt(int N, int H, int W) {
+  static const int forced = [] {
+    const char* e = std::getenv("DCNN_STEM_BNT_BLOCKS");
+    return e ? std::atoi(e) : 0;
+  }();
+  int dev = 0, cus = 256;
+  if (hipGetDevice(&dev) == hipSuccess) hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+  const int t = stem_tiles_host(N, H, W), want = forced > 0 ? forced : 3 * cus;
+  return t < want ? t : want;
+}
+
 void stem_fwd(StemArgs a, hipStream_t s) {
   if (!stem_supported(a.N, a.Ci, a.H, a.W, a.Co)) throw std::runtime_error("stem_fwd: unsupported shape");
   a.TH = SPX / a.W;
@@ -289,14 +366,17 @@ void stem_fwd(StemArgs a, hipStream_t s) {
 
 void stem_wgrad(StemArgs a, int blocks, hipStream_t s) {
   if (!stem_supported(a.N, a.Ci, a.H, a.W, a.Co)) throw std::runtime_error("stem_wgrad: unsupported shape");
-  if (blocks != stem_wgrad_blocks(a.N, a.H, a.W)) throw std::runtime_error("stem_wgrad: block count mismatch");
+  if (blocks < 1 || blocks > stem_tiles_host(a.N, a.H, a.W)) throw std::runtime_error("stem_wgrad: bad block count");
   a.TH = SPX / a.W;
   a.halo_bytes = (((a.TH + 2) * (a.W + 2) * 8) + 15) / 16 * 16;
-  const int main = a.halo_bytes + SPX * a.Co * 2, epi = 4 * a.Co * 48 * 4;
+  const bool bnt = a.bn_x != nullptr;
+  if (bnt && (!a.bn_mean || !a.bn_istd || !a.bn_sums || a.bn_parts < 1 || a.bn_count <= 0.f))
+    throw std::runtime_error("stem_wgrad: incomplete BatchNorm-backward operands");
+  const int main = a.halo_bytes + SPX * a.Co * 2 + (bnt ? 4 * a.Co * 4 : 0), epi = 4 * a.Co * 48 * 4;
   const int lds = main > epi ? main : epi;
 #define DCNN_SW(C)                                                                                        \
   {                                                                                                       \
-    auto k = stem_wgrad_kernel<C>;                                                                        \
+    auto k = bnt ? stem_wgrad_kernel<C, true> : stem_wgrad_kernel<C, false>;                              \
     DCNN_HIP_CHECK(hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, lds)); \
     hipLaunchKernelGGL(k, dim3(blocks), dim3(256), lds, s, a);                                            \
   }

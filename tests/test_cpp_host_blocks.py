@@ -288,6 +288,33 @@ def test_cpp_resnet18_gpu_gradients_match_cpu_backend(bins, tmp_path):
     assert rows[-1][2] < 2e-2 and rows[-2][2] < 2e-2, rows[-2:]  # classifier weights / bias
     assert not bad, bad
 
+@pytest.mark.gpu
+def test_cpp_stem_bn_fold_matches_unfused(bins, tmp_path):
+    """The stem BatchNorm's backward folded into the stem's weight-gradient kernel
+    (gpu_ops::stem_wgrad_bn: dy' = A dy + B (x - mean) + D per channel on the staged dY tile, the
+    BatchNorm's parameter gradients from the same reduced sums) against the unfused pair of passes
+    (bn_bwd_slab + stem_wgrad, DCNN_STEM_BN_FOLD=0) on the same weights and batch: every parameter
+    gradient bit-identical (same arithmetic and bf16 rounding of dy')."""
+    from dcnn_amd.nn.sequential import load_tensor
+    res = {}
+    for fold in ("1", "0"):
+        env = dict(os.environ, DCNN_STEM_BN_FOLD=fold)
+        r = subprocess.run([bins["host_api_parity"], "grads", "resnet18_tiny_imagenet", "64", f"g{fold}.bin",
+                            "--device", "GPU"], cwd=tmp_path, env=env, stdout=subprocess.PIPE,
+                           stderr=subprocess.STDOUT, text=True, timeout=600)
+        assert r.returncode == 0, r.stdout[-3000:]
+        out = _lines(r.stdout)
+        with open(tmp_path / f"g{fold}.bin", "rb") as f:
+            res[fold] = (out["params"], [load_tensor(f) for _ in out["params"]])
+    names, g1 = res["1"]
+    names0, g0 = res["0"]
+    assert names == names0 and len(g1) > 40
+    for n, a, b in zip(names, g1, g0):
+        assert torch.equal(a, b), (n, float((a - b).abs().max()), float(b.abs().max()))
+    # the fold touches the stem conv and its BatchNorm: their gradients are non-trivial
+    assert float(g1[0].abs().max()) > 0 and float(g1[2].abs().max()) > 0
+
+
 def _segments(out):
     rows = []
     for line in out.splitlines():
