@@ -356,6 +356,9 @@ __global__ void __launch_bounds__(256) bn_apply_kernel(const T* __restrict__ x, 
 // comparison exactly as bn_apply + maxpool_fwd would, idx = window position of the max. The
 // full-resolution BN output is never written: the backward (maxpool_bwd_bnb) masks with the
 // pooled value and recomputes xhat from x.
+// P > 0: a compile-time P x P window (the ResNet stems' 2 x 2): the window's loads are issued
+// together instead of one dependent load per window pixel (the run-time loop serialised them)
+template <int P>
 __global__ void __launch_bounds__(256) bn_relu_maxpool_kernel(const bf16* __restrict__ x, bf16* __restrict__ y,
                                                               uint8_t* __restrict__ idx, PoolGeom g,
                                                               const float* __restrict__ sums, int parts,
@@ -410,16 +413,31 @@ __global__ void __launch_bounds__(256) bn_relu_maxpool_kernel(const bf16* __rest
     uint8_t bi[8];
 #pragma unroll
     for (int e = 0; e < 8; ++e) { sc[e] = scale[cv * 8 + e]; sf[e] = shift[cv * 8 + e]; best[e] = -INFINITY; bi[e] = 0; }
-    for (int ky = 0; ky < g.ph; ++ky)
-      for (int kx = 0; kx < g.pw; ++kx) {
-        const int iy = oy * g.ph + ky, ix = ox * g.pw + kx;
-        unpack8(*reinterpret_cast<const uint4*>(x + (((long)n * g.H + iy) * g.W + ix) * g.C + cv * 8), v);
+    auto take = [&](const uint4& raw, int local) {
+      unpack8(raw, v);
 #pragma unroll
-        for (int e = 0; e < 8; ++e) {
-          const float r = (float)(bf16)fmaxf(v[e] * sc[e] + sf[e], 0.f);
-          if (r > best[e]) { best[e] = r; bi[e] = (uint8_t)(ky * g.pw + kx); }
-        }
+      for (int e = 0; e < 8; ++e) {
+        const float r = (float)(bf16)fmaxf(v[e] * sc[e] + sf[e], 0.f);
+        if (r > best[e]) { best[e] = r; bi[e] = (uint8_t)local; }
       }
+    };
+    if constexpr (P > 0) {
+      uint4 w[P * P];
+#pragma unroll
+      for (int ky = 0; ky < P; ++ky)
+#pragma unroll
+        for (int kx = 0; kx < P; ++kx)
+          w[ky * P + kx] = *reinterpret_cast<const uint4*>(
+              x + (((long)n * g.H + oy * P + ky) * g.W + ox * P + kx) * g.C + cv * 8);
+#pragma unroll
+      for (int k = 0; k < P * P; ++k) take(w[k], k);
+    } else {
+      for (int ky = 0; ky < g.ph; ++ky)
+        for (int kx = 0; kx < g.pw; ++kx) {
+          const int iy = oy * g.ph + ky, ix = ox * g.pw + kx;
+          take(*reinterpret_cast<const uint4*>(x + (((long)n * g.H + iy) * g.W + ix) * g.C + cv * 8), ky * g.pw + kx);
+        }
+    }
     *reinterpret_cast<uint4*>(y + i * 8) = pack8(best);
     *reinterpret_cast<uint2*>(idx + i * 8) = *reinterpret_cast<uint2*>(bi);
   }
@@ -1199,7 +1217,8 @@ void bn_relu_maxpool(const bf16* x, bf16* y, uint8_t* idx, PoolGeom g, const flo
                      float* run_mean, float* run_var, float momentum, hipStream_t s) {
   if (!bn_relu_maxpool_supported(g)) throw std::runtime_error("bn_relu_maxpool: unsupported geometry");
   const long total = (long)g.N * g.OH * g.OW * g.C / 8;
-  hipLaunchKernelGGL(bn_relu_maxpool_kernel, dim3(grid_for(total, 256, 2048)), dim3(256), 2 * g.C * sizeof(float), s,
+  auto k = (g.ph == 2 && g.pw == 2) ? bn_relu_maxpool_kernel<2> : bn_relu_maxpool_kernel<0>;
+  hipLaunchKernelGGL(k, dim3(grid_for(total, 256, 2048)), dim3(256), 2 * g.C * sizeof(float), s,
                      x, y, idx, g, sums, parts, count, gamma, beta, eps, save_mean, save_istd, run_mean, run_var,
                      momentum);
   DCNN_LAUNCH_CHECK();

@@ -763,6 +763,8 @@ static void avgpool_bwd_t(const void* dy, void* dx, PoolGeom g, hipStream_t s) {
 // gradient / pooled output / argmax are read once instead of once per window pixel and the
 // index arithmetic is 32-bit and per window (the per-pixel 64-bit div/mod chains of the generic
 // kernel made it ALU bound). Statistics partials per block in the same [blocks][2][C] layout.
+// (P > 0: a compile-time P x P window, its x loads issued together)
+template <int P>
 __global__ void __launch_bounds__(256) maxpool_bwd_bnb_w_kernel(const bf16* __restrict__ dy,
                                                                 const uint8_t* __restrict__ idx,
                                                                 const bf16* __restrict__ ypool,
@@ -796,20 +798,36 @@ __global__ void __launch_bounds__(256) maxpool_bwd_bnb_w_kernel(const bf16* __re
     unpack8(*reinterpret_cast<const uint4*>(ypool + (size_t)i * 8), yp);
     const uint2 ib = *reinterpret_cast<const uint2*>(idx + (size_t)i * 8);
     const uint8_t* b = reinterpret_cast<const uint8_t*>(&ib);
-    for (int ky = 0; ky < g.ph; ++ky)
-      for (int kx = 0; kx < g.pw; ++kx) {
-        const int local = ky * g.pw + kx;
-        const size_t xi = (((size_t)n * g.H + oy * g.ph + ky) * g.W + ox * g.pw + kx) * g.C + cv * 8;
-        float xv[8], out[8];
-        unpack8(*reinterpret_cast<const uint4*>(x + xi), xv);
+    auto put = [&](const uint4& raw, int local, size_t xi) {
+      float xv[8], out[8];
+      unpack8(raw, xv);
 #pragma unroll
-        for (int e = 0; e < 8; ++e) {
-          out[e] = (b[e] == local && yp[e] > 0.f) ? d[e] : 0.f;
-          s[e] += out[e];
-          q[e] += out[e] * (xv[e] - mu[e]) * is[e];
-        }
-        *reinterpret_cast<uint4*>(dx + xi) = pack8(out);
+      for (int e = 0; e < 8; ++e) {
+        out[e] = (b[e] == local && yp[e] > 0.f) ? d[e] : 0.f;
+        s[e] += out[e];
+        q[e] += out[e] * (xv[e] - mu[e]) * is[e];
       }
+      *reinterpret_cast<uint4*>(dx + xi) = pack8(out);
+    };
+    if constexpr (P > 0) {
+      size_t xi[P * P];
+      uint4 w[P * P];
+#pragma unroll
+      for (int ky = 0; ky < P; ++ky)
+#pragma unroll
+        for (int kx = 0; kx < P; ++kx) {
+          xi[ky * P + kx] = (((size_t)n * g.H + oy * P + ky) * g.W + ox * P + kx) * g.C + cv * 8;
+          w[ky * P + kx] = *reinterpret_cast<const uint4*>(x + xi[ky * P + kx]);
+        }
+#pragma unroll
+      for (int k = 0; k < P * P; ++k) put(w[k], k, xi[k]);
+    } else {
+      for (int ky = 0; ky < g.ph; ++ky)
+        for (int kx = 0; kx < g.pw; ++kx) {
+          const size_t xi = (((size_t)n * g.H + oy * g.ph + ky) * g.W + ox * g.pw + kx) * g.C + cv * 8;
+          put(*reinterpret_cast<const uint4*>(x + xi), ky * g.pw + kx, xi);
+        }
+    }
   }
 #pragma unroll
   for (int e = 0; e < 8; ++e) {
@@ -839,7 +857,8 @@ void maxpool_bwd_bnb(const bf16* dy, const uint8_t* idx, const bf16* ypool, cons
   if (!maxpool_bwd_bnb_supported(g)) throw std::runtime_error("maxpool_bwd_bnb: unsupported geometry");
   if (g.H % g.ph == 0 && g.W % g.pw == 0 && g.OH == g.H / g.ph && g.OW == g.W / g.pw &&
       (long)g.N * g.H * g.W * g.C < (1l << 31)) {
-    hipLaunchKernelGGL(maxpool_bwd_bnb_w_kernel, dim3(bnb_pool_blocks(g)), dim3(256), 0, s, dy, idx, ypool, x, mean,
+    hipLaunchKernelGGL((g.ph == 2 && g.pw == 2) ? maxpool_bwd_bnb_w_kernel<2> : maxpool_bwd_bnb_w_kernel<0>,
+                       dim3(bnb_pool_blocks(g)), dim3(256), 0, s, dy, idx, ypool, x, mean,
                        istd, dx, g, slab, zero_sums);
     DCNN_LAUNCH_CHECK();
     return;
