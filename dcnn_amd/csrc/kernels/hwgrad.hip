@@ -308,7 +308,9 @@ __device__ __forceinline__ bf16x4 tr4_at(const char* addr) {
 // v_mfma_f32_16x16x4_f32: wave w takes co half w >> 1 and ci half w & 1 (one 16x16 tile per tap),
 // MFMA k0 (of 4 per 16-pixel block) takes pixels k0 + 4 lh — 4 rows apart, so the two pixels of a
 // 32-lane read group sit in chunk-swizzle classes 4 apart and hit disjoint banks.
-template <int TW, int TH, int IMG, int NS, int TSP = 1, bool F32 = false>
+// C32: Cs = 32 (one 64-channel chunk, the upper half read as zeros and not stored); its own
+// instances, so the compare stays out of the others (ResNet-50 b32 measured -0.3% with it inline)
+template <int TW, int TH, int IMG, int NS, int TSP = 1, bool F32 = false, bool C32 = false>
 __global__ void __launch_bounds__(256 * TSP, 1) hwgrad2_kernel(HWArgs p) {
   prefetch_kernargs<sizeof(HWArgs)>();
   using G = HWGeo2<TW, TH, IMG>;
@@ -318,7 +320,9 @@ __global__ void __launch_bounds__(256 * TSP, 1) hwgrad2_kernel(HWArgs p) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int tid = threadIdx.x, lane = tid & 63, wid = (tid >> 6) & 3, th = tid >> 8;
   constexpr int NT = 256 * TSP;
-  const int co_tiles = p.Co / 64, ci_chunks = p.Cs / 64;
+  // (Cs = 32: one 64-channel chunk whose upper half reads zeros and is not stored — ResNet-18's
+  // first residual conv, 32 input channels)
+  const int co_tiles = p.Co / 64, ci_chunks = (p.Cs + 63) / 64;
   const int per_split = co_tiles * ci_chunks;
   const int lt = xcd_remap_w(blockIdx.x, gridDim.x);
   const int split = lt / per_split, rem = lt - split * per_split;
@@ -350,7 +354,7 @@ __global__ void __launch_bounds__(256 * TSP, 1) hwgrad2_kernel(HWArgs p) {
     const int row = (wid * HNI + j) * 8 + (lane >> 3);
     const int im = row / HPIP, r2 = row - im * HPIP;
     const int hy = r2 / HW2P - 1, hx = r2 % HW2P - 1;
-    const bool real = row < HPP && hx <= TW;
+    const bool real = row < HPP && hx <= TW && (!C32 || c0 + ((slot ^ wswz2(row)) * 8) < p.Cs);
     h_hy[j] = real ? hy : -(1 << 20);
     h_hx[j] = hx;
     h_rel[j] = ((im * p.H + hy) * p.W + hx) * p.ldx * 2 + (xoff + c0 + ((slot ^ wswz2(row)) * 8)) * 2;
@@ -616,7 +620,7 @@ __global__ void __launch_bounds__(256 * TSP, 1) hwgrad2_kernel(HWArgs p) {
         const int row = q >> 4, c4 = (q & 15) * 4;
         const int u = row >> 6, co = co0 + (row & 63);
         const float4 v = *reinterpret_cast<const float4*>(stg + row * 68 + c4);
-        *reinterpret_cast<float4*>(out + (long)co * Ng + (t0 + u) * p.Cs + c0 + c4) = v;
+        if (!C32 || c0 + c4 < p.Cs) *reinterpret_cast<float4*>(out + (long)co * Ng + (t0 + u) * p.Cs + c0 + c4) = v;
       }
     }
     if (p.bias_slab != nullptr && c0 == 0) {  // (every wave passes the same barriers)
@@ -656,9 +660,13 @@ static bool hw_geometry(int H, int W, int* TH, int* TW, int* IMG) {
   return false;
 }
 
+static int g_hwgrad_version = 2;  // (hwgrad_set_version below)
+
 bool hwgrad_supported(int NB, int H, int W, int Cs, int Co, int ntaps) {
   int th, tw, img;
-  if (Cs % 64 || Co % 64 || ntaps != 9) return false;  // 3x3 (all 9 taps unrolled)
+  // 3x3 (all 9 taps unrolled); Cs = 32 on the tap-shift-invariant kernel only (a half-empty
+  // 64-channel chunk: ResNet-18 layer 1's first conv, 52.8 us on the gathered GEMM)
+  if ((Cs % 64 && !(Cs == 32 && g_hwgrad_version == 2)) || Co % 64 || ntaps != 9) return false;
   if (!hw_geometry(H, W, &th, &tw, &img) || NB % img) return false;
   // 32-bit buffer offsets
   return (long)NB * H * W * (Cs > Co ? Cs : Co) * 2 < (1l << 31);
@@ -672,7 +680,7 @@ int hwgrad_splits(int NB, int H, int W, int Cs, int Co) {
   int th, tw, img;
   if (!hw_geometry(H, W, &th, &tw, &img)) return 1;
   const int total = (NB / img) * (H / th) * (W / tw);
-  const int per_split = (Co / 64) * (Cs / 64);
+  const int per_split = (Co / 64) * ((Cs + 63) / 64);
   int want = (kHwTargetBlocks + per_split - 1) / per_split;
   if (want < 1) want = 1;
   if (want > total) want = total;
@@ -687,7 +695,6 @@ int hwgrad_splits(int NB, int H, int W, int Cs, int Co) {
 
 // kernel generation: 2 = tap-shift-invariant addressing where it applies (8 waves, taps split
 // 0-4 / 5-8 over two waves per SIMD), 1 = first kernel only (test hook)
-static int g_hwgrad_version = 2;
 void hwgrad_set_version(int v) { g_hwgrad_version = v; }
 
 void hwgrad(HWArgs a, int splits, hipStream_t s) {
@@ -710,17 +717,19 @@ void hwgrad(HWArgs a, int splits, hipStream_t s) {
   hw_geometry(a.H, a.W, &a.TH, &a.TW, &a.IMG);
   const int total = (a.NB / a.IMG) * (a.H / a.TH) * (a.W / a.TW);
   a.tiles_per_split = (total + splits - 1) / splits;
-  const int grid = splits * (a.Co / 64) * (a.Cs / 64);
+  const int grid = splits * (a.Co / 64) * ((a.Cs + 63) / 64);
   constexpr int stages = 3;
   // tap-shift-invariant variant (hwgrad2_kernel) for the standard 3x3 / pad-1 taps on 16- and
   // 8-wide maps (hwgrad_set_version(1) keeps the first kernel)
   const int ver = g_hwgrad_version;
   bool std_taps = a.ntaps == 9;
   for (int t = 0; t < a.ntaps && std_taps; ++t) std_taps = a.tap_dy[t] == t / 3 - 1 && a.tap_dx[t] == t % 3 - 1;
+  const bool c32 = a.Cs % 64 != 0;
+  if (c32 && !(ver == 2 && std_taps)) throw std::runtime_error("hwgrad: Cs = 32 needs the standard 3x3 taps");
   if (ver == 2 && std_taps) {
 #define DCNN_HW2(TW_, TH_, IMG_, NS_)                                                                   \
     if (a.TW == TW_ && a.TH == TH_ && a.IMG == IMG_) {                                                  \
-      auto k = hwgrad2_kernel<TW_, TH_, IMG_, NS_, 2>;                                                  \
+      auto k = c32 ? hwgrad2_kernel<TW_, TH_, IMG_, NS_, 2, false, true> : hwgrad2_kernel<TW_, TH_, IMG_, NS_, 2>; \
       const int lds = NS_ * HWGeo2<TW_, TH_, IMG_>::STAGE;                                              \
       DCNN_HIP_CHECK(hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, lds)); \
       hipLaunchKernelGGL(k, dim3(grid, a.npairs), dim3(512), lds, s, a);                                \
@@ -730,7 +739,7 @@ void hwgrad(HWArgs a, int splits, hipStream_t s) {
     DCNN_HW2(16, 8, 1, 3)  // 3 x 48 KB
     DCNN_HW2(8, 8, 2, 2)   // 2 x 56 KB (three stages would need 168 KB)
     if (g_hwgrad_version == 2 && a.TW == 4 && a.TH == 4 && a.IMG == 8) {
-      auto k = hwgrad2_kernel<4, 4, 8, 2, 2>;  // 2 x 64 KB
+      auto k = c32 ? hwgrad2_kernel<4, 4, 8, 2, 2, false, true> : hwgrad2_kernel<4, 4, 8, 2, 2>;  // 2 x 64 KB
       const int lds = 2 * HWGeo2<4, 4, 8>::STAGE;
       DCNN_HIP_CHECK(hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, lds));
       hipLaunchKernelGGL(k, dim3(grid, a.npairs), dim3(512), lds, s, a);

@@ -121,6 +121,22 @@ def test_halo_wgrad(hip, case, version):
         kernels().hwgrad_set_version(2)
 
 
+@pytest.mark.parametrize("case", [(4, 32, 32, 32, 64), (6, 32, 16, 16, 128), (8, 32, 8, 8, 64), (16, 32, 4, 4, 64)])
+def test_halo_wgrad_32_input_channels(hip, case):
+    """Cs = 32 on the tap-shift-invariant halo wgrad (ResNet-18's first residual conv): one
+    64-channel chunk whose upper half is read as zeros (buffer range) and never stored; every
+    geometry against the fp32 reference, accumulating into the existing gradient. The first
+    kernel generation does not take it."""
+    from dcnn_amd.ops._ext import kernels
+    N, Ci, H, W, Co = case
+    kernels().hwgrad_set_version(1)
+    try:
+        assert not kernels().hwgrad_supported(N, H, W, Ci, Co, 9)
+    finally:
+        kernels().hwgrad_set_version(2)
+    _halo_wgrad_case(hip, case)
+
+
 def _halo_wgrad_case(hip, case):
     from dcnn_amd.ops._ext import kernels
     N, Ci, H, W, Co = case
