@@ -81,6 +81,11 @@ struct BnbOperands {
   const void* x;  // the BN input
   const float* mean;
   const float* istd;
+  // a plain BatchNorm + ReLU (no residual): the halo dgrad recomputes the mask from x, gamma,
+  // beta instead of reading y (one full-resolution read fewer)
+  const float* gamma = nullptr;
+  const float* beta = nullptr;
+  bool mask_from_x = false;
 };
 // residual: dx = dgrad + residual in the epilogue (a residual block's input gradient);
 // w_transposed: w is already the [C][KH][KW][Co] dgrad operand (weight_transpose);

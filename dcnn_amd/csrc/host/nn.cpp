@@ -249,8 +249,13 @@ Tensor Conv2D::backward_residual(const Tensor& dy, const Tensor& residual) {
 gpu_ops::BnbOperands BatchNorm::bnb_operands(int mb) {
   set_micro_batch(mb);
   MbCache& mc = mbc();
-  return gpu_ops::BnbOperands{mc.d.defined() ? mc.d.data() : nullptr, mc.a.data(), mc.b.ptr<float>(),
-                              mc.c.ptr<float>()};
+  gpu_ops::BnbOperands o{mc.d.defined() ? mc.d.data() : nullptr, mc.a.data(), mc.b.ptr<float>(), mc.c.ptr<float>()};
+  if (mc.d.defined() && mc.flag) {  // (mc.flag: mc.d is a plain BN + ReLU output, forward_impl)
+    o.gamma = affine_ ? params_[0].value.ptr<float>() : nullptr;
+    o.beta = affine_ ? params_[1].value.ptr<float>() : nullptr;
+    o.mask_from_x = true;
+  }
+  return o;
 }
 
 bool Conv2D::make_transposed_operand(std::vector<int64_t>& row, long& tiles) {
@@ -405,6 +410,7 @@ Tensor BatchNorm::forward_impl(const Tensor& x, bool training, const Tensor* res
                                g, b, eps_, running_mean.ptr<float>(), running_var.ptr<float>(), momentum_,
                                mean_.ptr<float>(), istd_.ptr<float>());
       mc.d = Tensor();
+      mc.flag = false;
       pending_x_ = nullptr;
       pending_slab_ = nullptr;
       pending_rows_ = 0;
@@ -418,10 +424,12 @@ Tensor BatchNorm::forward_impl(const Tensor& x, bool training, const Tensor* res
                          running_mean.ptr<float>(), running_var.ptr<float>(), momentum_, mean_.ptr<float>(),
                          istd_.ptr<float>(), relu, res);
     mc.d = relu ? y : Tensor();  // (the ReLU mask of the backward)
+    mc.flag = relu && res == nullptr && training;  // (the mask is a function of x: bnb_operands)
   } else if (dev_.is_gpu()) {
     gpu_ops::bn_fwd(x.data(), y.data(), N * HW, c_, g, b, eps_, training, running_mean.ptr<float>(),
                     running_var.ptr<float>(), momentum_, mean_.ptr<float>(), istd_.ptr<float>(), relu, res);
     mc.d = relu ? y : Tensor();
+    mc.flag = relu && res == nullptr && training;
   } else {
     cpu_ops::bn_fwd(x.ptr<float>(), y.ptr<float>(), N, c_, HW, g, b, eps_, training, running_mean.ptr<float>(),
                     running_var.ptr<float>(), momentum_, mean_.ptr<float>(), istd_.ptr<float>());
@@ -442,6 +450,7 @@ void BatchNorm::forward_deferred(const Tensor& x, bool training) {
   mc.b.ensure({c_}, DType::F32, dev_);
   mc.c.ensure({c_}, DType::F32, dev_);
   mc.d = Tensor();
+  mc.flag = false;
   train_ = training;
   deferred_raw_ = gpu_ops::BnRaw{nullptr, 0};
   if (training) {
@@ -506,6 +515,7 @@ Tensor BatchNorm::forward_dual(const Tensor& x, BatchNorm& o, bool relu, bool tr
   Tensor y = act_empty(x.shape(), dev_);
   gpu_ops::bn_fwd_dual(side(*this, mc, raw), side(o, oc, o.deferred_raw_), y.data(), R, c_, relu, training);
   mc.d = relu ? y : Tensor();
+  mc.flag = false;
   pending_x_ = nullptr;
   pending_slab_ = nullptr;
   pending_rows_ = 0;

@@ -634,6 +634,16 @@ const float* conv_dgrad(const void* dy, const void* w, void* dx, const ConvShape
     ba.x = static_cast<const bf16*>(bnb->x);
     ba.mean = bnb->mean;
     ba.istd = bnb->istd;
+    // (the fault drops the mask either way)
+    static const bool mask_x_env = [] {
+      const char* v = std::getenv("DCNN_BNB_MASK_X");
+      return !(v && v[0] == '0');
+    }();
+    if (bnb->mask_from_x && bnb->y && mask_x_env && !(g_fault & 1)) {
+      ba.mask_x = 1;
+      ba.gamma = bnb->gamma;
+      ba.beta = bnb->beta;
+    }
   }
   auto slab_of = [&](int rows) {
     *bnb_rows = rows;

@@ -14,6 +14,10 @@ namespace dcnn {
 // separate pass over dy, x and y. Inactive when x == nullptr.
 struct BnbArgs {
   const bf16* y; const bf16* x; const float* mean; const float* istd;
+  // mask_x (hconv3's data-gradient epilogue only; the other kernels use y): the ReLU mask
+  // recomputed from x as the forward apply computed it, x * (gamma istd) + (beta - mean gamma
+  // istd) > 0, instead of read from y (a plain BatchNorm + ReLU; gamma / beta null: no affine)
+  const float* gamma; const float* beta; int mask_x;
 };
 struct NtArgs {
   const bf16* A; const bf16* B; void* C;

@@ -179,7 +179,8 @@ struct H3 {
 // kind, is never a run-time branch): 0 = no statistics (bias / residual / ReLU at run time);
 // 1 = forward BatchNorm statistics, no bias / residual / ReLU; 2 = data gradient with the
 // backward-BatchNorm fusion (optional residual); 3 = forward statistics with bias / residual /
-// ReLU at run time.
+// ReLU at run time; 4 = EPI 2 with the ReLU mask recomputed from the BatchNorm input
+// (BnbArgs::mask_x) instead of read from its output.
 // STAMP: diagnostic instance with s_memtime stamps (benchmarks/hconv3_timeline.py).
 template <int NW, int WC, int TWC, int HN, int NWI, int PITCH, int EPI, bool STAMP, bool F32 = false>
 __global__ void __launch_bounds__(NW * 64, 8 / NW) hconv3_kernel(HConvArgs p, H3Geo g) {
@@ -593,8 +594,9 @@ __global__ void __launch_bounds__(NW * 64, 8 / NW) hconv3_kernel(HConvArgs p, H3
       // channels cb + 32 h + e (e = 0..7) = acc[2h + (e >> 2)][j][e & 3], cb = n0 + wc*64 + 8*lh.
       // Per channel half: operand loads (bias, BN mean / istd, residual, ReLU output, BN input),
       // arithmetic, 4 x 16-byte stores, statistics rows.
-      constexpr bool bnb = EPI == 2, stats = EPI != 0, opts = EPI == 0 || EPI == 3;
-      const bool has_res = EPI != 1 && p.residual != nullptr, has_y = bnb && p.bnb.y != nullptr;
+      constexpr bool bnb = EPI == 2 || EPI == 4, stats = EPI != 0, opts = EPI == 0 || EPI == 3;
+      constexpr bool mask_x = EPI == 4;  // (the ReLU mask recomputed from x: BnbArgs::mask_x)
+      const bool has_res = EPI != 1 && p.residual != nullptr, has_y = EPI == 2 && p.bnb.y != nullptr;
       constexpr bool has_x = bnb;
       const bool has_bias = opts && p.bias != nullptr, relu = opts && p.relu;
       const int cb = it.n0 + wc * 64 + 8 * lh;
@@ -606,12 +608,21 @@ __global__ void __launch_bounds__(NW * 64, 8 / NW) hconv3_kernel(HConvArgs p, H3
 #pragma unroll
       for (int h = 0; h < 2; ++h) {
         if (it.n0 + wc * 64 + 32 * h >= p.N) continue;  // (wave-uniform: the N = 32 tile's upper half)
-        float bv[8], mu[8], is[8];
+        float bv[8], mu[8], is[8], msc[8], msf[8];
 #pragma unroll
         for (int e = 0; e < 8; ++e) {
           bv[e] = has_bias ? p.bias[cb + 32 * h + e] : 0.f;
           mu[e] = has_x ? p.bnb.mean[cb + 32 * h + e] : 0.f;
           is[e] = has_x ? p.bnb.istd[cb + 32 * h + e] : 0.f;
+        }
+        if constexpr (!F32 && mask_x) {  // the forward apply's scale / shift, same expressions
+#pragma unroll
+          for (int e = 0; e < 8; ++e) {
+            const float gm = p.bnb.gamma ? p.bnb.gamma[cb + 32 * h + e] : 1.f;
+            const float bt = p.bnb.beta ? p.bnb.beta[cb + 32 * h + e] : 0.f;
+            msc[e] = gm * is[e];
+            msf[e] = bt - mu[e] * gm * is[e];
+          }
         }
         float gv[4][8], xh[4][8];  // [j][e]: stored value, and (bnb) stored value * xhat
         if constexpr (F32) {
@@ -682,6 +693,7 @@ __global__ void __launch_bounds__(NW * 64, 8 / NW) hconv3_kernel(HConvArgs p, H3
             if (has_res) f[e] += rf[e];
             if (relu) f[e] = fmaxf(f[e], 0.f);
             if (has_y) f[e] = yf[e] > 0.f ? f[e] : 0.f;
+            if constexpr (mask_x) f[e] = xf[e] * msc[e] + msf[e] > 0.f ? f[e] : 0.f;
           }
           const uint4 ov = pack8(f);
           *reinterpret_cast<uint4*>(cbytes + oo[j] + h * 64) = ov;
@@ -831,7 +843,7 @@ static void launch_h3e(const HConvArgs& a, const H3Geo& g, hipStream_t s) {
 
 // the epilogue instance for these options (-1: not covered)
 static int h3_epi(const HConvArgs& a) {
-  if (a.bnb.x) return (a.stats && !a.relu && !a.bias) ? 2 : -1;
+  if (a.bnb.x) return (a.stats && !a.relu && !a.bias) ? (a.bnb.mask_x && !a.Cf ? 4 : 2) : -1;
   if (!a.stats) return 0;
   return (a.residual || a.residual_f || a.relu || a.bias) ? 3 : 1;
 }
@@ -851,6 +863,7 @@ static void launch_h3(const HConvArgs& a, const H3Geo& g, hipStream_t s) {
   if (epi == 1) return launch_h3e<NW, WC, TWC, HN, NWI, PITCH, 1, false>(a, g, s);
   if (epi == 2) return launch_h3e<NW, WC, TWC, HN, NWI, PITCH, 2, false>(a, g, s);
   if (epi == 3) return launch_h3e<NW, WC, TWC, HN, NWI, PITCH, 3, false>(a, g, s);
+  if (epi == 4) return launch_h3e<NW, WC, TWC, HN, NWI, PITCH, 4, false>(a, g, s);
   launch_h3e<NW, WC, TWC, HN, NWI, PITCH, 0, false>(a, g, s);
 }
 

@@ -289,16 +289,21 @@ def test_cpp_resnet18_gpu_gradients_match_cpu_backend(bins, tmp_path):
     assert not bad, bad
 
 @pytest.mark.gpu
-def test_cpp_stem_bn_fold_matches_unfused(bins, tmp_path):
-    """The stem BatchNorm's backward folded into the stem's weight-gradient kernel
-    (gpu_ops::stem_wgrad_bn: dy' = A dy + B (x - mean) + D per channel on the staged dY tile, the
-    BatchNorm's parameter gradients from the same reduced sums) against the unfused pair of passes
-    (bn_bwd_slab + stem_wgrad, DCNN_STEM_BN_FOLD=0) on the same weights and batch: every parameter
-    gradient bit-identical (same arithmetic and bf16 rounding of dy')."""
+@pytest.mark.parametrize("switch", ["DCNN_STEM_BN_FOLD", "DCNN_BNB_MASK_X"])
+def test_cpp_fusion_switch_matches_unfused(bins, tmp_path, switch):
+    """Two C++ engine fusions against their switched-off form on the same weights and batch, every
+    parameter gradient bit-identical:
+    * DCNN_STEM_BN_FOLD: the stem BatchNorm's backward folded into the stem's weight-gradient
+      kernel (gpu_ops::stem_wgrad_bn: dy' = A dy + B (x - mean) + D per channel on the staged dY
+      tile, the BatchNorm's parameter gradients from the same reduced sums) vs bn_bwd_slab +
+      stem_wgrad (same arithmetic and bf16 rounding of dy');
+    * DCNN_BNB_MASK_X: the halo dgrad's backward-BatchNorm epilogue recomputing the ReLU mask from
+      the BatchNorm input (x * gamma istd + (beta - mean gamma istd) > 0, the forward apply's own
+      expressions) vs reading it from the BatchNorm output."""
     from dcnn_amd.nn.sequential import load_tensor
     res = {}
     for fold in ("1", "0"):
-        env = dict(os.environ, DCNN_STEM_BN_FOLD=fold)
+        env = dict(os.environ, **{switch: fold})
         r = subprocess.run([bins["host_api_parity"], "grads", "resnet18_tiny_imagenet", "64", f"g{fold}.bin",
                             "--device", "GPU"], cwd=tmp_path, env=env, stdout=subprocess.PIPE,
                            stderr=subprocess.STDOUT, text=True, timeout=600)
