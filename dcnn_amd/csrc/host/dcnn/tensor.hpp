@@ -53,6 +53,8 @@ void free(void* p);
 size_t cached_bytes();  // bytes held in the free lists
 void empty_cache();     // synchronise and return every cached block to the driver
 void copy(void* dst, const void* src, size_t nbytes, int kind);  // 0 h2d, 1 d2h (host waits), 2 d2d (async)
+// two device-to-device copies in one kernel launch (stream-ordered, capturable)
+void copy2_d2d(void* d0, const void* s0, size_t n0, void* d1, const void* s1, size_t n1);
 void zero(void* p, size_t nbytes);                                // stream-ordered memset
 void synchronize();
 

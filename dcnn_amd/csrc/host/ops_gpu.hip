@@ -198,6 +198,9 @@ void copy(void* dst, const void* src, size_t nbytes, int kind) {
     HOST_HIP_CHECK(hipStreamSynchronize(s));
   }
 }
+void copy2_d2d(void* d0, const void* s0, size_t n0, void* d1, const void* s1, size_t n1) {
+  copy_pair(d0, s0, (long)n0, d1, s1, (long)n1, static_cast<hipStream_t>(flow()));
+}
 void zero(void* p, size_t nbytes) { HOST_HIP_CHECK(hipMemsetAsync(p, 0, nbytes, static_cast<hipStream_t>(flow()))); }
 void synchronize() { HOST_HIP_CHECK(hipDeviceSynchronize()); }
 

@@ -108,11 +108,16 @@ double TrainGraph::step(const Tensor& x, const Tensor& labels) {
   if (!captured_) capture(x, labels);
   if (x.numel() != sx_.numel() || labels.numel() != sy_.numel())
     throw std::runtime_error("TrainGraph: the batch shape changed after capture");
-  // the batch into the static slots (device-resident batches: stream-ordered D2D copies)
-  if (x.device() == dev) gpu::copy(sx_.data(), x.data(), sx_.nbytes(), 2);
-  else gpu::copy(sx_.data(), x.to(dev).data(), sx_.nbytes(), 2);
-  if (labels.device() == dev) gpu::copy(sy_.data(), labels.data(), sy_.nbytes(), 2);
-  else gpu::copy(sy_.data(), labels.to(dev).data(), sy_.nbytes(), 2);
+  // the batch into the static slots (device-resident batches: stream-ordered D2D copies, both in
+  // one kernel launch)
+  if (x.device() == dev && labels.device() == dev) {
+    gpu::copy2_d2d(sx_.data(), x.data(), sx_.nbytes(), sy_.data(), labels.data(), sy_.nbytes());
+  } else {
+    if (x.device() == dev) gpu::copy(sx_.data(), x.data(), sx_.nbytes(), 2);
+    else gpu::copy(sx_.data(), x.to(dev).data(), sx_.nbytes(), 2);
+    if (labels.device() == dev) gpu::copy(sy_.data(), labels.data(), sy_.nbytes(), 2);
+    else gpu::copy(sy_.data(), labels.to(dev).data(), sy_.nbytes(), 2);
+  }
   opt_.before_replay();
   graph_.replay();
   return std::nan("");

@@ -297,6 +297,7 @@ void grad_pack_bf16(const float* g, bf16* out, long n, float scale, hipStream_t 
 void grad_sum_chunks_bf16(const bf16* src, int w, long ld, long n, bf16* dst, hipStream_t s);
 void grad_unpack_bf16(const bf16* in, float* g, long n, hipStream_t s);
 void zero_bytes(void* p, long nbytes, hipStream_t s);
+void copy_pair(void* d0, const void* s0, long n0, void* d1, const void* s1, long n1, hipStream_t s);
 // fp32 rows [rows][C] -> bf16 [rows][3C]: pattern 0 = [hi | lo | hi], 1 = [hi | hi | lo]
 // (hi = bf16(x), lo = bf16(x - hi)); a conv over the concatenations sums hi*hi + lo*hi + hi*lo
 void split3_bf16(const float* in, bf16* out, long rows, int C, int pattern, hipStream_t s);
