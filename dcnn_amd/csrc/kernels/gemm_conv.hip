@@ -724,7 +724,11 @@ int gemm_tn_splits(int M, int N, int P) {
   const int bm = M >= 128 ? 128 : 64, bn = N >= 128 ? 128 : 64;
   const long tiles = (long)((M + bm - 1) / bm) * ((N + bn - 1) / bn);
   long splits = (512 + tiles - 1) / tiles;
-  const long max_by_k = P / (64 * 4) > 0 ? P / (64 * 4) : 1;
+  // at least 4 K-steps (256 reduction rows) per split; a grid of few tiles (a classifier's weight
+  // gradient: 200 x 512 over the batch, 8 tiles) may go down to one K-step per split instead of
+  // running 8 workgroups through the whole batch (ResNet-18 fc: 17.7 us at one split)
+  const long min_k = tiles < 32 ? 64 : 64 * 4;
+  const long max_by_k = P / min_k > 0 ? P / min_k : 1;
   if (splits > max_by_k) splits = max_by_k;
   const long max_by_mem = (64l << 20) / (4l * M * N) > 0 ? (64l << 20) / (4l * M * N) : 1;
   if (splits > max_by_mem) splits = max_by_mem;
