@@ -172,7 +172,11 @@ constexpr int kStatRW = 16;
 // waves per reduce block (rows per block = 16 x waves): fewer rows per block = more blocks in the
 // (latency-bound) reduce and more partials for the consumers to merge (8: 0.1-0.6% faster end
 // to end than 16 at batch 64 and 256)
-static constexpr int g_stat_waves = 8;
+static const int g_stat_waves = [] {  // (DCNN_STAT_WAVES=4|8|16: experiment override)
+  const char* e = std::getenv("DCNN_STAT_WAVES");
+  const int v = e ? std::atoi(e) : 8;
+  return v == 4 || v == 16 ? v : 8;
+}();
 
 // Merge up to kStatRW rows [r0, r1) of channel c: every load in flight at once, then a pairwise
 // tree (log2 16 = 4 dependent merge levels instead of a 16-long chain). Fixed order.
