@@ -172,6 +172,9 @@ constexpr int kStatRW = 16;
 // waves per reduce block (rows per block = 16 x waves): fewer rows per block = more blocks in the
 // (latency-bound) reduce and more partials for the consumers to merge (8: 0.1-0.6% faster end
 // to end than 16 at batch 64 and 256)
+// (round 6, tools/gpu/statwaves.sh, same box, 3 alternating reps, ResNet-18 b256 / ResNet-50 b32
+// img/s: 8 waves 91.76k-91.98k / 8145-8150, 4 waves 90.92k-91.10k / 8084-8091, 16 waves
+// 91.78k-91.98k / 8130-8131)
 static const int g_stat_waves = [] {  // (DCNN_STAT_WAVES=4|8|16: experiment override)
   const char* e = std::getenv("DCNN_STAT_WAVES");
   const int v = e ? std::atoi(e) : 8;
